@@ -1,0 +1,554 @@
+"""CPU ORACLE (test infrastructure only - see oracle/__init__.py).
+
+Restatement of the six reference scripts over columnar ``Tables``.  Each function cites
+the reference lines it follows (paths relative to the reference's ``program/``).
+Python-level per-project loops are kept where the reference has them; they run in
+seconds on the golden cases and on bounded samples of config 2.
+"""
+from __future__ import annotations
+
+import statistics
+import warnings
+from collections import defaultdict
+
+import numpy as np
+import pandas as pd
+from scipy import stats
+
+import tse_amd  # noqa: F401  (registers the package)
+from tse_amd.schema import (BT_COVERAGE, BT_FUZZING, LIMIT_US, R_FINISH, R_HALFWAY_LOWER,
+                            R_HALFWAY_UPPER, RQ3_LIMIT_US, TS_NULL, US_PER_DAY, Tables)
+from tse_amd.rq.results import (Describe, RQ1Result, RQ2AddResult, RQ2CountResult, RQ3Result,
+                                RQ4aResult, RQ4bResult)
+from tse_amd.rq import common
+
+FIXED_CODES = (0, 1)           # 'Fixed', 'Fixed (Verified)'
+
+
+class _Seg:
+    """Rows of a table selected by ``mask``, sorted by (project, key, row) with per-project
+    [start, end) offsets - the ``WHERE project = ... ORDER BY key`` of every per-project query."""
+
+    def __init__(self, project, key, mask, n_projects):
+        idx = np.nonzero(mask)[0]
+        order = np.lexsort((idx, key[idx], project[idx]))
+        self.idx = idx[order]
+        self.key = key[self.idx]
+        pr = project[self.idx].astype(np.int64)
+        self.start = np.searchsorted(pr, np.arange(n_projects), "left")
+        self.end = np.searchsorted(pr, np.arange(n_projects), "right")
+
+    def rows(self, p):
+        return self.idx[self.start[p]:self.end[p]]
+
+    def keys(self, p):
+        return self.key[self.start[p]:self.end[p]]
+
+
+def eligible_projects(t: Tables) -> np.ndarray:
+    """rq1_detection_rate.py:144-152 (and the 5 copies): GROUP BY project HAVING COUNT(*) >= 365
+    over coverage IS NOT NULL AND coverage > 0 AND date < '2025-01-08'.  SQLite returns
+    the groups in project order."""
+    m = t.c_coverage_valid & (t.c_coverage > 0) & (t.c_date < LIMIT_US)
+    cnt = np.bincount(t.c_project[m].astype(np.int64), minlength=len(t.projects))
+    return np.nonzero(cnt >= 365)[0]
+
+
+def _describe(x) -> Describe:
+    """rq3_diff_coverage_at_detection.py:25-66 numbers."""
+    a = np.asarray(x, dtype=np.float64)
+    n = len(a)
+    return Describe(count=n, n_pos=int(np.sum(a > 0)), n_zero=int(np.sum(a == 0)), n_neg=int(np.sum(a < 0)),
+                    mean=float(np.mean(a)), median=float(np.median(a)), std=float(np.std(a)),
+                    min=float(np.min(a)), max=float(np.max(a)),
+                    q1=float(np.percentile(a, 25)), q3=float(np.percentile(a, 75)))
+
+
+# --------------------------------------------------------------------------------------- RQ1
+def rq1(t: Tables, threshold: int = 100) -> RQ1Result:
+    """rq1_detection_rate.py:101-269 with queries1.py:15-58 (SAME_DATE_BUILD_ISSUE),
+    :267-278 (ALL_FUZZING_BUILD), :280-314 (GET_ISSUES_WITHOUT_MATCHING_BUILD)."""
+    P = len(t.projects)
+    lim = t.i_rts < LIMIT_US                                   # :121-127
+    fixed = np.isin(t.i_status, FIXED_CODES)
+    elig = eligible_projects(t)
+    is_elig = np.zeros(P, bool)
+    is_elig[elig] = True
+    # valid join partner: Fuzzing, result IN ('Finish','Halfway'), DATE(t) < LIMIT
+    vb = (t.b_type == BT_FUZZING) & np.isin(t.b_result, (R_FINISH, R_HALFWAY_LOWER)) & (t.b_time < LIMIT_US)
+    minv = np.full(P, TS_NULL, dtype=np.int64)
+    np.minimum.at(minv, t.b_project[vb].astype(np.int64), t.b_time[vb])
+    cand = fixed & is_elig[t.i_project]
+    has = (t.i_rts != TS_NULL) & (t.i_rts > minv[t.i_project])
+    picnt = np.bincount(t.pi_project.astype(np.int64), minlength=P)
+    n_without = int(picnt[t.i_project[cand & ~has]].sum())     # queries1.py:280-314 (inner JOIN project_info)
+    tgt = fixed & is_elig[t.i_project] & lim                    # :172-185
+    # phase 1: ALL Fuzzing builds, any result, no date limit  (:189-203)
+    fz = t.b_type == BT_FUZZING
+    nF = np.bincount(t.b_project[fz].astype(np.int64), minlength=P)
+    nfe = nF[elig]
+    max_iter = int(nfe.max()) if len(nfe) else 0
+    iter_total = np.array([int(np.sum(nfe >= i)) for i in range(1, max_iter + 1)], dtype=np.int64)
+    # SAME_DATE_BUILD_ISSUE: latest valid build strictly before rts; ROW_NUMBER per number
+    vseg = _Seg(t.b_project, t.b_time, vb, P)
+    ci = np.nonzero(cand & (t.i_rts != TS_NULL))[0]
+    mb = np.full(len(ci), -1, dtype=np.int64)
+    for k, i in enumerate(ci.tolist()):
+        p = int(t.i_project[i])
+        keys = vseg.keys(p)
+        j = int(np.searchsorted(keys, t.i_rts[i], "left")) - 1
+        if j >= 0:
+            mb[k] = vseg.rows(p)[j]
+    ok = mb >= 0
+    ci, mb = ci[ok], mb[ok]
+    # dedup by issue number: keep the row with the latest build time (ties: first in output order)
+    order = np.lexsort((ci, t.i_rts[ci], t.i_project[ci]))
+    ci, mb = ci[order], mb[order]
+    best = {}
+    for k, (i, b) in enumerate(zip(ci.tolist(), mb.tolist())):
+        num = int(t.i_number[i])
+        tb = int(t.b_time[b])
+        if num not in best or tb > best[num][0]:
+            best[num] = (tb, k)
+    keep = np.zeros(len(ci), bool)
+    for _, k in best.values():
+        keep[k] = True
+    ci, mb = ci[keep], mb[keep]
+    # phase 2: iteration = #ALL Fuzzing builds with timecreated < rts  (:213-230)
+    fseg = _Seg(t.b_project, t.b_time, fz, P)
+    pairs = set()
+    for i in ci.tolist():
+        p = int(t.i_project[i])
+        it = int(np.searchsorted(fseg.keys(p), t.i_rts[i], "left"))
+        if it > 0:
+            pairs.add((it, p))
+    iter_det = np.zeros(max_iter, dtype=np.int64)
+    for it, _ in pairs:
+        iter_det[it - 1] += 1
+    res = RQ1Result(
+        n_issues_lim=int(lim.sum()), n_issues_lim_projects=len(np.unique(t.i_project[lim])),
+        n_fixed_lim=int((lim & fixed).sum()), n_fixed_lim_projects=len(np.unique(t.i_project[lim & fixed])),
+        eligible=elig, n_without_matching=n_without,
+        n_target=int(tgt.sum()), n_target_projects=len(np.unique(t.i_project[tgt])),
+        total_fuzz_builds=int(nfe.sum()), matched_issue=ci, matched_build=mb,
+        n_matched_projects=len(np.unique(t.i_project[ci])),
+        iter_total=iter_total, iter_detected=iter_det, min_project_threshold=threshold)
+    _, _, _, late = common.rq1_rates(iter_total, iter_det, threshold)
+    if late:
+        a = np.array(late)
+        nz = [r for r in late if r != 0]
+        res.late = Describe(count=len(late), n_zero=int(np.sum(a == 0)), min=min(late), max=max(late),
+                            q1=float(np.percentile(late, 25)), q3=float(np.percentile(late, 75)),
+                            median=float(np.median(late)), mean=float(np.mean(late)),
+                            min_nonzero=min(nz) if nz else None)
+    return res
+
+
+# ---------------------------------------------------------------------------------- RQ2 count
+def rq2_count(t: Tables) -> RQ2CountResult:
+    """rq2_coverage_count.py:244-483 with queries1.py:120-129 (GET_TOTAL_COVERAGE_EACH_PROJECT)."""
+    P = len(t.projects)
+    elig = eligible_projects(t)
+    m = t.c_coverage_valid & (t.c_coverage != 0) & (t.c_date < LIMIT_US)
+    seg = _Seg(t.c_project, t.c_date, m, P)
+    raw_n, n_tr, sw_w, sw_p, corr = [], [], [], [], []
+    sessions = [[]]
+    for p in elig.tolist():
+        rows = seg.rows(p)
+        raw_n.append(len(rows))
+        if len(rows) == 0:
+            n_tr.append(0)
+            sw_w.append(np.nan)
+            sw_p.append(np.nan)
+            continue
+        cv = t.c_covered[rows].astype(np.float64)
+        tt = t.c_total[rows].astype(np.float64)
+        keep = t.c_total[rows] != 0
+        trend = list(cv[keep] / tt[keep] * 100)                 # :300-303
+        n_tr.append(len(trend))
+        if len(trend) >= 3:                                     # :305-314
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                w, pv = stats.shapiro(trend)
+            sw_w.append(float(w))
+            sw_p.append(float(pv))
+        else:
+            sw_w.append(np.nan)
+            sw_p.append(np.nan)
+        if len(trend) < 2:                                      # :316-322
+            c = np.nan
+        else:
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                c, _ = stats.spearmanr(range(len(trend)), trend)
+        corr.append(float(c))
+        for i, v in enumerate(trend):                           # :330-333
+            if len(sessions) <= i:
+                sessions.append([])
+            sessions[i].append(v)
+    offs = np.zeros(len(sessions) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(s) for s in sessions])
+    vals = np.array([v for s in sessions for v in s], dtype=np.float64)
+    ca = np.array(corr, dtype=np.float64)
+    valid = ca[~np.isnan(ca)]
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        cmean = float(np.mean(valid))
+        cmed = float(np.median(valid))
+    ge = [i for i, s in enumerate(sessions) if len(s) >= 100]  # :390
+    avg = [statistics.mean(sessions[i]) for i in ge]          # :439-440
+    med = [statistics.median(sessions[i]) for i in ge]
+    sp = None
+    if len(med) > 1:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            r = stats.spearmanr(list(range(len(med))), med)
+        sp = (float(r.statistic), float(r.pvalue))
+    shp = None
+    if len(med) >= 3:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            shp = float(stats.shapiro(med)[1])
+    pct = np.array([[np.percentile(sessions[i], q) for i in ge] for q in (5, 25, 50, 75, 95)],
+                   dtype=np.float64).reshape(5, len(ge))
+    dmean = np.array([np.mean(sessions[i]) for i in ge], dtype=np.float64)
+    return RQ2CountResult(eligible=elig, raw_n=np.array(raw_n, np.int64), n_trend=np.array(n_tr, np.int64),
+                          sw_w=np.array(sw_w), sw_p=np.array(sw_p), corr=ca,
+                          session_offsets=offs, session_values=vals, corr_mean=cmean, corr_median=cmed,
+                          ge100=np.array(ge, np.int64), average_trend=np.array(avg), median_trend=np.array(med),
+                          spearman_median=sp, shapiro_median_p=shp, dist_percentiles=pct, dist_mean=dmean)
+
+
+# ------------------------------------------------------------------------------------ RQ2 add
+def rq2_add(t: Tables) -> RQ2AddResult:
+    """rq2_coverage_and_added.py:73-238: change points of (modules, revisions) over Coverage
+    builds and the coverage rows of the two surrounding days."""
+    P = len(t.projects)
+    elig = eligible_projects(t)                                  # QUERY_PROJECTS, ORDER BY project
+    bm = (t.b_type == BT_COVERAGE) & np.isin(t.b_result, (R_HALFWAY_UPPER, R_FINISH)) & (t.b_time < LIMIT_US)
+    bseg = _Seg(t.b_project, t.b_time, bm, P)
+    cseg = _Seg(t.c_project, t.c_date, t.c_date < LIMIT_US, P)
+    gkey = t.group_key()
+    out = {k: [] for k in ("p", "f", "e", "s", "ci", "ci1", "dt", "dc")}
+    cov_f = np.zeros(P, bool)
+    tot_f = np.zeros(P, bool)
+    for p in elig.tolist():
+        br = bseg.rows(p)
+        if len(br) == 0:
+            continue
+        cr = cseg.rows(p)
+        if len(cr) == 0:
+            continue
+        cov_f[p] = not t.c_covered_valid[cr].all()
+        tot_f[p] = not t.c_total_valid[cr].all()
+        cday = t.c_date[cr] // US_PER_DAY
+        k = gkey[br]
+        starts = np.nonzero(np.r_[True, k[1:] != k[:-1]])[0]
+        ends = np.r_[starts[1:] - 1, len(br) - 1]
+        for i in range(len(starts) - 1):
+            e = br[ends[i]]
+            s = br[starts[i + 1]]
+            row = []
+            for b in (e, s):
+                d = t.b_time[b] // US_PER_DAY
+                j = int(np.searchsorted(cday, d, "left"))
+                row.append(int(cr[j]) if j < len(cday) and cday[j] == d else -1)
+            c0, c1 = row
+
+            def val(c):
+                if c < 0:
+                    return np.nan, np.nan
+                cv = float(t.c_covered[c]) if t.c_covered_valid[c] else np.nan
+                tv = float(t.c_total[c]) if t.c_total_valid[c] else np.nan
+                return cv, tv
+            cv0, tv0 = val(c0)
+            cv1, tv1 = val(c1)
+            v0 = not np.isnan(tv0) and tv0 != 0                  # :189-200
+            v1 = not np.isnan(tv1) and tv1 != 0
+            if v0 and v1:
+                dt_ = tv1 - tv0
+                dc_ = (cv1 / tv1) * 100 - (cv0 / tv0) * 100
+            else:
+                dt_ = dc_ = np.nan
+            for key, v in zip(("p", "f", "e", "s", "ci", "ci1", "dt", "dc"),
+                              (p, br[starts[i]], e, s, c0, c1, dt_, dc_)):
+                out[key].append(v)
+    return RQ2AddResult(projects=elig, row_project=np.array(out["p"], np.int64),
+                        row_first_build=np.array(out["f"], np.int64),
+                        row_end_build=np.array(out["e"], np.int64), row_start_build=np.array(out["s"], np.int64),
+                        row_cov_i=np.array(out["ci"], np.int64), row_cov_i1=np.array(out["ci1"], np.int64),
+                        diff_total=np.array(out["dt"], np.float64), diff_coverage=np.array(out["dc"], np.float64),
+                        covered_is_float=cov_f, total_is_float=tot_f)
+
+
+# ---------------------------------------------------------------------------------------- RQ3
+def rq3(t: Tables) -> RQ3Result:
+    """rq3_diff_coverage_at_detection.py:202-360."""
+    P = len(t.projects)
+    elig = eligible_projects(t)
+    is_elig = np.zeros(P, bool)
+    is_elig[elig] = True
+    im = np.isin(t.i_status, FIXED_CODES) & is_elig[t.i_project] & (t.i_rts < LIMIT_US)
+    iss = np.nonzero(im)[0]
+    iss = iss[np.lexsort((iss, t.i_rts[iss], t.i_project[iss]))]   # ORDER BY project, rts
+    fz = _Seg(t.b_project, t.b_time, (t.b_type == BT_FUZZING) & np.isin(t.b_result, (R_HALFWAY_UPPER, R_FINISH))
+              & (t.b_time < LIMIT_US), P)
+    cb = _Seg(t.b_project, t.b_time, (t.b_type == BT_COVERAGE) & (t.b_time < RQ3_LIMIT_US), P)
+    tc = _Seg(t.c_project, t.c_date, t.c_covered_valid & (t.c_date < RQ3_LIMIT_US), P)
+    canon = t.rev_canon()
+    det = []
+    non = []
+    cur = -1
+    for i in iss.tolist():
+        p = int(t.i_project[i])
+        rts = int(t.i_rts[i])
+        if p != cur:
+            if cur >= 0:                                          # flush previous project (:245-257)
+                rows = tc.rows(cur)
+                if len(rows):
+                    dd = {d[4] // US_PER_DAY for d in det if d[3] == cur}
+                    for k in range(1, len(rows)):
+                        a, b = rows[k - 1], rows[k]
+                        if t.c_date[b] // US_PER_DAY not in dd and t.c_total[a] > 0 and t.c_total[b] > 0:
+                            non.append(((t.c_covered[b] / t.c_total[b] - t.c_covered[a] / t.c_total[a]) * 100,
+                                        int(t.c_covered[b] - t.c_covered[a]), int(t.c_total[b] - t.c_total[a])))
+            cur = p
+        fr, cr, tr = fz.rows(p), cb.rows(p), tc.rows(p)
+        if len(fr) == 0 or len(cr) == 0 or len(tr) == 0:
+            continue
+        j = int(np.searchsorted(fz.keys(p), rts, "left")) - 1       # :269
+        if j < 0:
+            continue
+        lf = fr[j]
+        j2 = int(np.searchsorted(cb.keys(p), rts, "right"))         # :273 first t > rts
+        if j2 >= len(cr):
+            continue
+        fc = cr[j2]
+        if t.b_result[fc] not in (R_HALFWAY_UPPER, R_FINISH):
+            continue
+        if t.b_time[fc] - t.b_time[lf] > 24 * 3600 * 1_000_000:      # :277
+            continue
+        if canon[lf] < 0 or canon[lf] != canon[fc]:                  # :280
+            continue
+        target = rts // US_PER_DAY + 1
+        days = tc.keys(p) // US_PER_DAY
+        pair = None
+        for k in range(1, len(tr)):                                  # :286-292
+            if days[k] == target:
+                if t.c_covered[tr[k]] == 0:
+                    break
+                pair = (tr[k - 1], tr[k])
+                break
+        if pair is None:
+            continue
+        a, b = pair
+        if t.c_total[a] > 0 and t.c_total[b] > 0:
+            det.append(((t.c_covered[b] / t.c_total[b] - t.c_covered[a] / t.c_total[a]) * 100,
+                        int(t.c_covered[b] - t.c_covered[a]), int(t.c_total[b] - t.c_total[a]), p, rts, i))
+    dpct = np.array([d[0] for d in det], np.float64)
+    npct = np.array([d[0] for d in non], np.float64)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        dd_ = _describe(dpct) if len(det) else None
+        nd_ = _describe(npct) if len(non) else None
+        dt_ = _describe([d[2] for d in det]) if len(det) else None
+        ad = an = lv = bm = None
+        if len(det) and len(non):
+            r = stats.anderson(list(dpct), dist="norm")
+            ad = (float(r.statistic), np.asarray(r.critical_values))
+            r = stats.anderson(list(npct), dist="norm")
+            an = (float(r.statistic), np.asarray(r.critical_values))
+            s_, p_ = stats.levene(list(dpct), list(npct))
+            lv = (float(s_), float(p_))
+            s_, p_ = stats.brunnermunzel(list(dpct), list(npct))
+            bm = (float(s_), float(p_))
+    return RQ3Result(n_all_issues=len(iss), det_pct=dpct, det_cov=np.array([d[1] for d in det], np.int64),
+                     det_tot=np.array([d[2] for d in det], np.int64), det_project=np.array([d[3] for d in det], np.int64),
+                     det_issue=np.array([d[5] for d in det], np.int64), non_pct=npct,
+                     non_cov=np.array([d[1] for d in non], np.int64), non_tot=np.array([d[2] for d in non], np.int64),
+                     desc_detected=dd_, desc_non=nd_, desc_det_total=dt_, anderson_det=ad, anderson_non=an,
+                     levene=lv, brunnermunzel=bm)
+
+
+# --------------------------------------------------------------------------------------- RQ4a
+def rq4a(t: Tables) -> RQ4aResult:
+    """rq4a_bug.py:653-804 (+ :82-153, :156-207, :246-414, :806-841)."""
+    P = len(t.projects)
+    elig = eligible_projects(t)
+    groups, corpus_us = common.corpus_groups(t, elig, add_missing_to_g1=True)
+    fb = _Seg(t.b_project, t.b_time, (t.b_type == BT_FUZZING) & (t.b_time < LIMIT_US), P)
+    fi = _Seg(t.i_project, t.i_rts, np.isin(t.i_status, FIXED_CODES) & (t.i_rts < LIMIT_US), P)
+    stats_ = {}
+    for g in ("group1", "group2"):                                   # :324-346
+        tot = defaultdict(int)
+        det = defaultdict(set)
+        for p in groups[g]:
+            bt = fb.keys(p)
+            if len(bt) == 0:
+                continue
+            for i in range(1, len(bt) + 1):
+                tot[i] += 1
+            for it in fi.keys(p).tolist():
+                k = int(np.searchsorted(bt, it, "left"))
+                if k > 0:
+                    det[k].add(p)
+        stats_[g] = (tot, det)
+    mx = max([max(stats_[g][0].keys(), default=0) for g in stats_] +
+             [max(stats_[g][1].keys(), default=0) for g in stats_])
+    arr = {}
+    for g in stats_:
+        tot, det = stats_[g]
+        arr[g] = (np.array([tot.get(i, 0) for i in range(1, mx + 1)], np.int64),
+                  np.array([len(det.get(i, ())) for i in range(1, mx + 1)], np.int64))
+    rows = common.rq4a_rows(arr["group1"][0], arr["group1"][1], arr["group2"][0], arr["group2"][1])
+    after = {}
+    for key, col in (("g1", 3), ("g2", 6)):
+        rates = [r[col] for r in rows]
+        fb5 = next((i for i, r in enumerate(rates) if r < 5), len(rates))
+        ra = rates[fb5:]
+        after[key] = ((float(np.median(ra)), float(np.subtract(*np.percentile(ra, [75, 25]))))
+                      if ra else None)
+    # G4: introduction iteration (:246-299) and pre/post windows (:350-412)
+    intro = []
+    N = 7
+    steps = {s: [0, 0] for s in list(range(-N, 0)) + list(range(1, N + 1))}
+    trans = [0, 0, 0, 0]
+    any_window = False
+    for p in groups["group4"]:
+        ct = corpus_us.get(p)
+        if ct is None:
+            continue
+        bt = fb.keys(p)
+        intro.append((p, 0 if len(bt) == 0 else int(np.searchsorted(bt, ct, "left"))))
+        it = fi.keys(p)
+        npre = int(np.searchsorted(bt, ct, "left"))
+        if npre == 0:
+            continue
+        idx = npre - 1
+        if idx - (N - 1) < 0 or idx + N >= len(bt) - 1:
+            continue
+        any_window = True
+        pre_any = post_any = False
+        for k in range(1, N + 1):
+            a, b = bt[idx - (k - 1)], bt[idx - (k - 1) + 1]
+            d = bool(np.any((it >= a) & (it < b)))
+            steps[-k][0] += 1
+            steps[-k][1] += d
+            pre_any |= d
+            a, b = bt[idx + k], bt[idx + k + 1]
+            d = bool(np.any((it >= a) & (it < b)))
+            steps[k][0] += 1
+            steps[k][1] += d
+            post_any |= d
+        trans[0 if (pre_any and post_any) else 1 if pre_any else 2 if post_any else 3] += 1
+    pos = [k for _, k in intro if k > 0]
+    istats = None
+    if pos:
+        s = pd.Series(pos)
+        istats = (float(s.mean()), float(s.median()), int(s.min()), int(s.max()))
+    pre_n = sum(steps[s][0] for s in range(-N, 0))
+    pre_d = sum(steps[s][1] for s in range(-N, 0))
+    post_n = sum(steps[s][0] for s in range(1, N + 1))
+    post_d = sum(steps[s][1] for s in range(1, N + 1))
+    overall = ((pre_d / pre_n * 100) if pre_n else 0, (post_d / post_n * 100) if post_n else 0)
+    return RQ4aResult(groups=groups, g1_total=arr["group1"][0], g1_det=arr["group1"][1],
+                      g2_total=arr["group2"][0], g2_det=arr["group2"][1], after=after, intro=intro,
+                      intro_stats=istats, g4_steps={s: tuple(v) for s, v in steps.items()},
+                      g4_transition=tuple(trans), g4_overall=overall, n_g4_analyzed=steps[-1][0],
+                      has_g4_transition=any_window)
+
+
+# --------------------------------------------------------------------------------------- RQ4b
+def rq4b(t: Tables) -> RQ4bResult:
+    """rq4b_coverage.py:1209-1261 (+ :183-313, :725-1015, :1061-1085)."""
+    P = len(t.projects)
+    elig = eligible_projects(t)
+    groups, corpus_us = common.corpus_groups(t, elig, add_missing_to_g1=False)
+    full = _Seg(t.c_project, t.c_date, t.c_coverage_valid & (t.c_coverage > 0) & (t.c_date < LIMIT_US), P)
+    sess = {}
+    for g in ("group2", "group1"):                                   # :914-936
+        ss = [[]]
+        for p in groups[g]:
+            v = t.c_coverage[full.rows(p)]
+            for i, x in enumerate(v.tolist()):
+                while len(ss) <= i:
+                    ss.append([])
+                ss[i].append(x)
+        sess[g] = ss
+    ms = max([int(full.end[p] - full.start[p]) for g in ("group2", "group1") for p in groups[g]] + [0])
+    for g in sess:
+        if len(sess[g]) < ms:
+            sess[g].extend([[] for _ in range(ms - len(sess[g]))])
+    c2 = np.array([len(sess["group2"][i]) for i in range(ms)], np.int64)
+    c1 = np.array([len(sess["group1"][i]) for i in range(ms)], np.int64)
+    q2 = np.full((ms, 3), np.nan)
+    q1 = np.full((ms, 3), np.nan)
+    pb = np.full(ms, np.nan)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for i in range(ms):
+            a, b = sess["group2"][i], sess["group1"][i]
+            if a:
+                q2[i] = np.percentile(a, [25, 50, 75])
+            if b:
+                q1[i] = np.percentile(b, [25, 50, 75])
+            if len(a) >= 5 and len(b) >= 5:
+                try:
+                    pb[i] = stats.brunnermunzel(a, b, alternative="two-sided")[1]
+                except Exception:
+                    pass
+    last = -1
+    for i in range(ms):
+        if c2[i] >= 100 and c1[i] >= 100:
+            last = i
+    sp6 = common.rq4b_spearman6(q2[:last + 1], q1[:last + 1], lambda x, y: stats.spearmanr(x, y)) \
+        if last >= 0 else None
+    # deltas (:725-797)
+    pos_all = _Seg(t.c_project, t.c_date, t.c_coverage_valid & (t.c_coverage > 0), P)
+    pre = [[] for _ in range(7)]
+    post = [[] for _ in range(7)]
+    nproj = 0
+    g34 = set(groups["group3"]) | set(groups["group4"])
+    for p in common.corpus_order(t, elig):
+        if p not in g34 or p not in corpus_us:
+            continue
+        cd = (corpus_us[p] // US_PER_DAY) * US_PER_DAY
+        k = pos_all.keys(p)
+        r = pos_all.rows(p)
+        j = int(np.searchsorted(k, cd, "left"))
+        pre_v = t.c_coverage[r[max(0, j - 7):j]][::-1]
+        post_v = t.c_coverage[r[j:j + 7]]
+        if len(pre_v) < 7 or len(post_v) < 7:
+            continue
+        nproj += 1
+        for i in range(7):
+            pre[i].append(float(pre_v[i]))
+            post[i].append(float(post_v[i]))
+    pre = [np.array(x) for x in pre]
+    post = [np.array(x) for x in post]
+    pre_med = [float(np.median(x)) if len(x) else np.nan for x in pre]
+    post_med = [float(np.median(x)) if len(x) else np.nan for x in post]
+    # initial coverage (:221-313)
+    init = {}
+    for g in ("group2", "group1"):
+        init[g] = np.array([t.c_coverage[full.rows(p)[0]] for p in sorted(groups[g]) if len(full.rows(p))],
+                           np.float64)
+    a, b = init["group2"], init["group1"]
+    mwu_p = cliff = bm = lv = None
+    if len(a) and len(b):
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            _, mwu_p = stats.mannwhitneyu(list(a), list(b), alternative="two-sided")
+            u1, _ = stats.mannwhitneyu(list(a), list(b), alternative="greater")
+            cliff = float((2 * u1) / (len(a) * len(b)) - 1)
+            s_, p_ = stats.brunnermunzel(list(a), list(b), alternative="two-sided")
+            bm = (float(s_), float(p_))
+            s_, p_ = stats.levene(list(a), list(b))
+            lv = (float(s_), float(p_))
+        mwu_p = float(mwu_p)
+    gc = tuple(len(groups[g]) for g in ("group1", "group2", "group3", "group4"))
+    return RQ4bResult(group_counts=gc, n_sessions=ms, c2=c2, c1=c1, g2_q=q2, g1_q=q1, p_bm=pb,
+                      last_valid_idx=last, spearman6=sp6, n_delta_projects=nproj, pre_cov=pre, post_cov=post,
+                      pre_median=pre_med, post_median=post_med, n_g2=len(groups["group2"]),
+                      n_g1=len(groups["group1"]), init_g2=a, init_g1=b, mwu_p=mwu_p, cliff=cliff, bm=bm,
+                      levene=lv)
