@@ -1,0 +1,168 @@
+/*
+ * fz.h - C ABI of libfz, the MI355X (gfx950) analytics engine for the RQ1-RQ4 computations of
+ * the "1 million fuzzing sessions" replication package.
+ *
+ * What this boundary replaces (reference paths relative to /root/reference):
+ *   program/__module/dbFile.py:5-38        DB(...).connect() / executeQuery("select", sql) -> rows.
+ *                                          Every RQ script fetches session rows through it; the
+ *                                          columnar store (fz_store_build) is its replacement.
+ *   program/__module/queries1.py:15-314    the SQL the scripts send (GROUP BY/HAVING eligibility,
+ *                                          as-of joins with ROW_NUMBER, per-project ordered scans).
+ *   program/research_questions/rq*.py      the Python loops + numpy/scipy statistics over those rows
+ *                                          (one fz_rq* entry point per script, see each declaration).
+ *
+ * Conventions
+ *   - Every pointer in fz_tables and in the *_out structs is a DEVICE pointer (HBM), owned by the
+ *     caller; the library never frees or retains them past the call (fz_tables must stay alive
+ *     until the fz_rq* calls that use the store built from it have returned).
+ *   - The library allocates only scratch and the sorted store, owned by the opaque fz_ctx.
+ *   - Every call returns 0 on success or a negative FZ_E* code; fz_last_error() returns a
+ *     thread-local message for the last failure.  No C++ exception crosses this boundary.
+ *   - Calls on one fz_ctx are serialised by the caller; contexts on different GPUs may be used
+ *     concurrently (one host thread / process per GPU).  All work is enqueued on the stream
+ *     given to fz_ctx_create; a call returns after its device results are complete.
+ *   - Timestamps are int64 microseconds since 1970-01-01 of the naive DB value; FZ_TS_NULL marks
+ *     SQL NULL.  Codes: build_type 0 Fuzzing / 1 Coverage; result 0 'Finish', 1 'Halfway',
+ *     2 'HalfWay', 3 'Error', 255 NULL; status 0 'Fixed', 1 'Fixed (Verified)', others not fixed.
+ */
+#ifndef FZ_H
+#define FZ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FZ_ABI_VERSION 1
+#define FZ_TS_NULL INT64_MAX
+
+#define FZ_OK 0
+#define FZ_E_INVALID (-1)   /* bad argument / shape */
+#define FZ_E_DEVICE (-2)    /* HIP runtime error */
+#define FZ_E_STATE (-3)     /* call order (e.g. fz_rq* before fz_store_build) */
+#define FZ_E_NOMEM (-4)
+
+/* validity bits of fz_tables.c_valid */
+#define FZ_VALID_COVERAGE 1u
+#define FZ_VALID_COVERED 2u
+#define FZ_VALID_TOTAL 4u
+
+typedef struct fz_ctx fz_ctx;
+
+/* The four session tables in columnar form (schema: SURVEY.md 8(c)).  Row order is arbitrary
+ * (heap order); the store sorts.  All arrays are device pointers. */
+typedef struct fz_tables {
+    int64_t n_projects;          /* project ids are 0..n_projects-1, id order == byte order of names */
+    /* buildlog_data (queries1.py:18-55) */
+    int64_t n_builds;
+    const uint32_t *b_project;
+    const uint8_t *b_type;
+    const uint8_t *b_result;
+    const int64_t *b_time;       /* timecreated */
+    const int32_t *b_group;      /* id of str(modules)+'_'+str(revisions)  (rq2_coverage_and_added.py:129) */
+    const int32_t *b_rev_canon;  /* id of sorted(revisions[1:-2].split(',')), -1 NULL (rq3:280) */
+    /* total_coverage (3_get_coverage_data.py:132) */
+    int64_t n_cov;
+    const uint32_t *c_project;
+    const int64_t *c_date;
+    const double *c_coverage;
+    const int64_t *c_covered;
+    const int64_t *c_total;
+    const uint8_t *c_valid;      /* FZ_VALID_* bits */
+    /* issues (queries1.py:20-43) */
+    int64_t n_issues;
+    const int64_t *i_number;
+    const uint32_t *i_project;
+    const int64_t *i_rts;
+    const uint8_t *i_status;
+    /* project_info: number of rows per project id (queries1.py:292-295 inner join) */
+    const int32_t *pi_count;
+} fz_tables;
+
+/* Returned by fz_store_build: sizes the caller needs to allocate fz_rq* outputs. */
+typedef struct fz_store_stats {
+    int64_t n_projects;
+    int64_t n_fuzz;                 /* Fuzzing builds (any result, any time) */
+    int64_t n_coverage_builds;
+    int64_t max_fuzz_per_project;   /* RQ1 iteration axis length upper bound */
+    int64_t max_cov_per_project;    /* coverage rows of one project */
+    int64_t sort_passes;            /* radix passes run (builds + coverage + issues) */
+} fz_store_stats;
+
+/* Numbers of rq3's print_summary_statistics (rq3_diff_coverage_at_detection.py:25-66) and the RQ1
+ * late-stage block (rq1_detection_rate.py:256-268): numpy mean (pairwise), median, std(ddof=0),
+ * percentile(linear) 25/75, min, max, counts. */
+typedef struct fz_describe {
+    int64_t count, n_pos, n_zero, n_neg;
+    double mean, median, std, min, max, q1, q3;
+    double min_nonzero;             /* NaN if none */
+    int64_t has_nonzero;
+} fz_describe;
+
+/* ---- context ---------------------------------------------------------------------------- */
+int fz_abi_version(void);
+const char *fz_last_error(void);
+/* stream: a hipStream_t (NULL = the device's null stream). */
+int fz_ctx_create(int device, void *stream, fz_ctx **out);
+int fz_ctx_destroy(fz_ctx *ctx);
+/* Re-target the context to another stream (e.g. torch's current stream). */
+int fz_ctx_set_stream(fz_ctx *ctx, void *stream);
+
+/* ---- store: replaces the PostgreSQL tables + indexes behind dbFile.DB ------------------ */
+/* Sorts buildlog_data by (build_type, project, timecreated), total_coverage by (project, date),
+ * issues by (project, rts) (stable: ties keep row order), builds per-project segment offsets. */
+int fz_store_build(fz_ctx *ctx, const fz_tables *t, fz_store_stats *stats);
+
+/* ---- RQ1: rq1_detection_rate.py:101-269 ------------------------------------------------- */
+enum {
+    FZ_RQ1_ISSUES_LIM = 0,        /* issues with rts < LIMIT                         :121-127 */
+    FZ_RQ1_ISSUES_LIM_PROJECTS,
+    FZ_RQ1_FIXED_LIM,             /* fixed issues with rts < LIMIT                   :129-136 */
+    FZ_RQ1_FIXED_LIM_PROJECTS,
+    FZ_RQ1_ELIGIBLE,              /* projects with >= 365 coverage rows              :144-152 */
+    FZ_RQ1_WITHOUT_MATCHING,      /* queries1.py:280-314                                      */
+    FZ_RQ1_TARGET,                /* :172-185                                                 */
+    FZ_RQ1_TARGET_PROJECTS,
+    FZ_RQ1_TOTAL_FUZZ,            /* sum of Fuzzing builds of eligible projects       :189-203 */
+    FZ_RQ1_MATCHED,               /* SAME_DATE_BUILD_ISSUE rows after ROW_NUMBER dedup        */
+    FZ_RQ1_MATCHED_PROJECTS,
+    FZ_RQ1_MAX_ITER,              /* length of iter_total / iter_detected                     */
+    FZ_RQ1_KEPT_ITERS,            /* iterations with total >= threshold                :233-239 */
+    FZ_RQ1_FIRST_DOWN,            /* first kept iteration key with rate < 5, -1 if none :247-253 */
+    FZ_RQ1_LATE,                  /* late-stage rates described in late (0 = none)            */
+    FZ_RQ1_NCOUNTS = 16
+};
+
+typedef struct fz_rq1_out {
+    int64_t *counts;              /* [FZ_RQ1_NCOUNTS] */
+    uint8_t *eligible;            /* [n_projects] 1 = eligible */
+    int64_t *iter_total;          /* [max_fuzz_per_project] projects with >= i Fuzzing builds */
+    int64_t *iter_detected;       /* [max_fuzz_per_project] distinct projects detecting at i */
+    int64_t *matched_issue;       /* [n_issues] issue rows, ORDER BY project, rts */
+    int64_t *matched_build;       /* [n_issues] joined build row */
+    fz_describe *late;            /* [1] late-stage detection-rate summary */
+} fz_rq1_out;
+
+int fz_rq1(fz_ctx *ctx, int64_t min_project_threshold, const fz_rq1_out *out);
+
+/* ---- per-kernel probe (bench.py roofline) ------------------------------------------------ */
+/* Start timing every launch of the named kernel (e.g. "radix_scatter", "elig_hist") with HIP
+ * events on the context stream; fz_probe_end synchronises the stream and returns the number of
+ * launches, their summed device milliseconds and their summed algorithmic bytes. */
+int fz_probe_begin(fz_ctx *ctx, const char *kernel_name);
+int fz_probe_end(fz_ctx *ctx, int64_t *launches, double *total_ms, double *algo_bytes);
+
+/* ---- primitives (exported for kernel-level tests and the roofline bench) ----------------- */
+/* Stable LSD radix sort of (key, value) pairs over key bits [0, bits).  keys/vals in place. */
+int fz_radix_sort_u64(fz_ctx *ctx, uint64_t *keys, uint32_t *vals, int64_t n, int bits);
+/* numpy-compatible describe of a device fp64 vector (sorts a scratch copy). */
+int fz_describe_f64(fz_ctx *ctx, const double *x, int64_t n, fz_describe *host_out);
+/* Per-project count of total_coverage rows with coverage valid, > 0 and date < limit
+ * (the GROUP BY/HAVING of rq1_detection_rate.py:144-152), on the unsorted table. */
+int fz_eligibility_count(fz_ctx *ctx, const fz_tables *t, int64_t date_limit, int32_t *counts);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FZ_H */

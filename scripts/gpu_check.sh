@@ -1,0 +1,23 @@
+#!/bin/bash
+# GPU session: parity tests, smoke, bench, rocprof kernel stats.  Each GPU step has its own time
+# limit; a fault / abort / timeout (exit >= 124) ends the script, an ordinary test failure does not.
+cd "$(dirname "$0")/.." || exit 1
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+TAG=${TAG:-r01}
+run() {  # run <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name exit $rc"; tail -5 "$OUT/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "fatal step $name ($rc): stopping"; exit $rc; fi
+  return $rc
+}
+STEPS=${STEPS:-tests,smoke,bench,prof}
+[[ $STEPS == *tests* ]] && run pytest_gpu 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+[[ $STEPS == *smoke* ]] && run smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()"
+[[ $STEPS == *bench* ]] && run bench 400 python -u bench.py
+[[ $STEPS == *prof* ]] && run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline
+echo done

@@ -21,3 +21,27 @@ import tse_amd  # noqa: E402,F401
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels through libfz.so)")
     config.addinivalue_line("markers", "slow: longer CPU test")
+
+
+@pytest.fixture(scope="session")
+def engine():
+    """One libfz context on cuda:0 for the whole GPU test session (fails loudly without a GPU)."""
+    from tse_amd import engine as E
+    eng = E.Engine(0)
+    yield eng
+    eng.close()
+
+
+@pytest.fixture(scope="session")
+def engine_for(engine):
+    """engine_for(case): the engine with that golden case's tables uploaded and the store built."""
+    import goldens
+    state = {"case": None}
+
+    def get(case):
+        if state["case"] != case:
+            engine.upload(goldens.tables(case))
+            engine.build_store()
+            state["case"] = case
+        return engine
+    return get

@@ -1,0 +1,146 @@
+// Public C ABI (include/fz.h): error capture, context lifetime, and thin wrappers that reset the
+// scratch arena and forward to the implementation.
+#include <cstring>
+#include <string>
+
+#include "fz_internal.h"
+#include "fz_views.h"
+
+namespace fz {
+void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats);
+void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_out *o);
+void eligibility_counts(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *counts);
+}  // namespace fz
+
+namespace {
+thread_local std::string g_err;
+
+template <typename F>
+int guarded(fz_ctx *c, F &&f) {
+    try {
+        if (!c) throw fz::Error(FZ_E_INVALID, "null fz_ctx");
+        FZ_HIP(hipSetDevice(c->device));
+        c->arena.reset();
+        f();
+        return FZ_OK;
+    } catch (const fz::Error &e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        g_err = "host allocation failed";
+        return FZ_E_NOMEM;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return FZ_E_INVALID;
+    }
+}
+}  // namespace
+
+extern "C" {
+
+int fz_abi_version(void) { return FZ_ABI_VERSION; }
+
+const char *fz_last_error(void) { return g_err.c_str(); }
+
+int fz_ctx_create(int device, void *stream, fz_ctx **out) {
+    try {
+        if (!out) throw fz::Error(FZ_E_INVALID, "fz_ctx_create: out is null");
+        *out = nullptr;
+        int n = 0;
+        FZ_HIP(hipGetDeviceCount(&n));
+        if (device < 0 || device >= n) throw fz::Error(FZ_E_INVALID, "fz_ctx_create: no such device");
+        FZ_HIP(hipSetDevice(device));
+        fz_ctx *c = new fz_ctx();
+        c->device = device;
+        c->stream = static_cast<hipStream_t>(stream);
+        void *h = nullptr;
+        if (hipHostMalloc(&h, 4096, hipHostMallocDefault) != hipSuccess) {
+            delete c;
+            throw fz::Error(FZ_E_DEVICE, "fz_ctx_create: hipHostMalloc failed");
+        }
+        c->h_pinned = static_cast<int64_t *>(h);
+        *out = c;
+        return FZ_OK;
+    } catch (const fz::Error &e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return FZ_E_INVALID;
+    }
+}
+
+int fz_ctx_destroy(fz_ctx *ctx) {
+    if (!ctx) return FZ_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+    delete ctx;
+    return FZ_OK;
+}
+
+int fz_ctx_set_stream(fz_ctx *ctx, void *stream) {
+    return guarded(ctx, [&] { ctx->stream = static_cast<hipStream_t>(stream); });
+}
+
+int fz_store_build(fz_ctx *ctx, const fz_tables *t, fz_store_stats *stats) {
+    return guarded(ctx, [&] { fz::store_build(ctx, t, stats); });
+}
+
+int fz_rq1(fz_ctx *ctx, int64_t min_project_threshold, const fz_rq1_out *out) {
+    return guarded(ctx, [&] { fz::rq1(ctx, min_project_threshold, out); });
+}
+
+int fz_probe_begin(fz_ctx *ctx, const char *kernel_name) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(kernel_name != nullptr, "fz_probe_begin: null name");
+        ctx->probe.name = kernel_name;
+        ctx->probe.used = 0;
+        ctx->probe.launches = 0;
+        ctx->probe.bytes = 0.0;
+    });
+}
+
+int fz_probe_end(fz_ctx *ctx, int64_t *launches, double *total_ms, double *algo_bytes) {
+    return guarded(ctx, [&] {
+        fz::Probe &p = ctx->probe;
+        fz::sync(ctx);
+        double ms = 0.0;
+        for (size_t i = 0; i + 1 < p.used; i += 2) {
+            float e = 0.f;
+            FZ_HIP(hipEventElapsedTime(&e, p.pool[i], p.pool[i + 1]));
+            ms += e;
+        }
+        if (launches) *launches = p.launches;
+        if (total_ms) *total_ms = ms;
+        if (algo_bytes) *algo_bytes = p.bytes;
+        p.name.clear();
+        p.used = 0;
+    });
+}
+
+int fz_radix_sort_u64(fz_ctx *ctx, uint64_t *keys, uint32_t *vals, int64_t n, int bits) {
+    return guarded(ctx, [&] {
+        FZ_CHECK((keys != nullptr || n == 0) && n >= 0 && bits >= 0 && bits <= 64, "fz_radix_sort_u64: bad arguments");
+        fz::radix_sort_pairs(ctx, keys, vals, n, bits);
+    });
+}
+
+int fz_describe_f64(fz_ctx *ctx, const double *x, int64_t n, fz_describe *host_out) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(host_out != nullptr && n >= 0 && (x != nullptr || n == 0), "fz_describe_f64: bad arguments");
+        fz_describe *d = ctx->arena.get<fz_describe>(1);
+        fz::describe_f64(ctx, x, n, d);
+        FZ_HIP(hipMemcpyAsync(host_out, d, sizeof(fz_describe), hipMemcpyDeviceToHost, ctx->stream));
+        fz::sync(ctx);
+    });
+}
+
+int fz_eligibility_count(fz_ctx *ctx, const fz_tables *t, int64_t date_limit, int32_t *counts) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(t != nullptr && counts != nullptr, "fz_eligibility_count: bad arguments");
+        fz::eligibility_counts(ctx, t, date_limit, counts);
+    });
+}
+
+}  // extern "C"

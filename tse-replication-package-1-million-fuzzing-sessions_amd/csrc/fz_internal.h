@@ -1,0 +1,234 @@
+// Internal declarations shared by the libfz translation units.
+//
+// Design: one fz_ctx per GPU.  It owns
+//   * a scratch arena (grow-only device blocks, bump-allocated, reset at the start of every
+//     public call) so steady-state calls never hipMalloc;
+//   * the sorted store (fz_store.hip) - the replacement for PostgreSQL's tables + indexes.
+// Kernels are plain HIP for gfx950: 256-thread workgroups (4 waves of 64), wave-level
+// ballot/popcount for ranking and counting, LDS for block-level staging.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "fz.h"
+
+namespace fz {
+
+constexpr int kBlock = 256;   // threads per workgroup (4 wave64)
+constexpr int kWave = 64;
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define FZ_HIP(expr)                                                                           \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess)                                                                  \
+            throw ::fz::Error(FZ_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+#define FZ_CHECK(cond, msg)                                              \
+    do {                                                                 \
+        if (!(cond)) throw ::fz::Error(FZ_E_INVALID, std::string(msg)); \
+    } while (0)
+
+#define FZ_LAUNCH_CHECK() FZ_HIP(hipGetLastError())
+
+// Grow-only bump allocator over device blocks.
+class Arena {
+   public:
+    ~Arena() { release(); }
+    void *alloc(size_t bytes) {
+        bytes = (bytes + 255) & ~size_t(255);
+        if (bytes == 0) bytes = 256;
+        for (; cur_ < blocks_.size(); ++cur_) {
+            Block &b = blocks_[cur_];
+            if (b.used + bytes <= b.size) {
+                void *p = static_cast<char *>(b.ptr) + b.used;
+                b.used += bytes;
+                return p;
+            }
+        }
+        size_t sz = bytes < (size_t(64) << 20) ? (size_t(64) << 20) : bytes;
+        void *p = nullptr;
+        FZ_HIP(hipMalloc(&p, sz));
+        blocks_.push_back({p, sz, bytes});
+        cur_ = blocks_.size() - 1;
+        return p;
+    }
+    template <typename T>
+    T *get(int64_t n) {
+        return static_cast<T *>(alloc(size_t(n < 1 ? 1 : n) * sizeof(T)));
+    }
+    void reset() {
+        for (auto &b : blocks_) b.used = 0;
+        cur_ = 0;
+    }
+    void release() {
+        for (auto &b : blocks_) (void)hipFree(b.ptr);
+        blocks_.clear();
+        cur_ = 0;
+    }
+
+   private:
+    struct Block {
+        void *ptr;
+        size_t size;
+        size_t used;
+    };
+    std::vector<Block> blocks_;
+    size_t cur_ = 0;
+};
+
+// Persistent device buffer (re-allocated only when it must grow).
+struct DevBuf {
+    void *ptr = nullptr;
+    size_t cap = 0;
+    ~DevBuf() {
+        if (ptr) (void)hipFree(ptr);
+    }
+    template <typename T>
+    T *ensure(int64_t n) {
+        size_t bytes = size_t(n < 1 ? 1 : n) * sizeof(T);
+        if (bytes > cap) {
+            if (ptr) FZ_HIP(hipFree(ptr));
+            ptr = nullptr;
+            FZ_HIP(hipMalloc(&ptr, bytes));
+            cap = bytes;
+        }
+        return static_cast<T *>(ptr);
+    }
+    template <typename T>
+    T *as() const {
+        return static_cast<T *>(ptr);
+    }
+};
+
+// A sorted view of one table (non-owning): rows in (project, time) order, their original row ids,
+// sort times, projects, and per-project [offs[p], offs[p+1]) segments (n_projects + 1 entries).
+struct View {
+    int64_t n = 0;
+    int64_t max_seg = 0;
+    const int32_t *row = nullptr;
+    const int64_t *time = nullptr;
+    const uint32_t *proj = nullptr;
+    const int64_t *offs = nullptr;
+};
+
+// The replacement for the PostgreSQL tables + indexes: every table sorted once per load.
+struct Store {
+    bool built = false;
+    fz_tables t{};
+    int64_t P = 0;
+    DevBuf b_row, b_time, b_proj, c_row, c_time, c_proj, i_row, i_time, i_proj;
+    DevBuf off_fuzz, off_covb, off_cov, off_iss;
+    View fuzz;    // buildlog_data, build_type = Fuzzing, by (project, timecreated)   queries1.py:267-278
+    View covb;    // buildlog_data, build_type = Coverage, by (project, timecreated)
+    View cov;     // total_coverage by (project, date)                              queries1.py:120-129
+    View issues;  // issues by (project, rts), ties in row order                    rq3:219-232
+    int64_t passes = 0;
+    int64_t tmin[3] = {0, 0, 0}, tmax[3] = {0, 0, 0};  // builds, coverage, issues (non-NULL)
+};
+
+// Per-kernel timing probe (fz_probe_begin/end): brackets every launch of ONE named kernel with
+// HIP events on the context stream and accumulates its algorithmic bytes, so bench.py can
+// report achieved GB/s for that kernel over the timed region.
+struct Probe {
+    std::string name;
+    std::vector<hipEvent_t> pool;  // pairs (start, stop)
+    size_t used = 0;
+    int64_t launches = 0;
+    double bytes = 0.0;
+    bool active() const { return !name.empty(); }
+};
+
+}  // namespace fz
+
+struct fz_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    fz::Arena arena;
+    fz::Store store;
+    fz::Probe probe;
+    int64_t *h_pinned = nullptr;   // small pinned host staging area (4 KiB)
+};
+
+namespace fz {
+// RAII bracket around one launch of kernel `name` moving `bytes` algorithmic bytes.
+struct ProbeScope {
+    fz_ctx *c;
+    bool on;
+    ProbeScope(fz_ctx *ctx, const char *name, double bytes) : c(ctx), on(false) {
+        Probe &p = c->probe;
+        if (!p.active() || p.name != name) return;
+        if (p.used + 2 > p.pool.size()) {
+            for (int i = 0; i < 64; ++i) {
+                hipEvent_t e;
+                FZ_HIP(hipEventCreate(&e));
+                p.pool.push_back(e);
+            }
+        }
+        FZ_HIP(hipEventRecord(p.pool[p.used], c->stream));
+        p.bytes += bytes;
+        p.launches += 1;
+        on = true;
+    }
+    ~ProbeScope() {
+        if (on) {
+            (void)hipEventRecord(c->probe.pool[c->probe.used + 1], c->stream);
+            c->probe.used += 2;
+        }
+    }
+};
+}  // namespace fz
+
+namespace fz {
+
+// ---- primitives (fz_prims.hip) --------------------------------------------------------------
+// Device-wide exclusive scan of int64 (in != out allowed). Returns nothing; total written to
+// out_total (device) if non-null.
+void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, int64_t *out_total);
+// Stable LSD radix sort of (uint64 key, uint32 value) over bits [0, bits).  Uses arena scratch;
+// the result is written back to keys/vals.
+void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int bits);
+// min/max over int64 values skipping FZ_TS_NULL: writes {min, max} to host array.
+void minmax_i64_to_host(fz_ctx *c, const int64_t *const *cols, const int64_t *ns, int ncols,
+                        int64_t *host_minmax);
+// Per-project [start,end) offsets of a project-sorted uint32 array.
+void segment_offsets(fz_ctx *c, const uint32_t *sorted_proj, int64_t n, int64_t P, int64_t *offsets);
+// numpy-compatible describe of a device double vector (n may be 0).
+void describe_f64(fz_ctx *c, const double *x, int64_t n, fz_describe *dev_out);
+// Order-preserving uint64 image of a double (for radix sorting doubles; NaN sorts last).
+__host__ __device__ inline uint64_t f64_key(double d) {
+    uint64_t u = __builtin_bit_cast(uint64_t, d);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__host__ __device__ inline double f64_from_key(uint64_t k) {
+    uint64_t u = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    return __builtin_bit_cast(double, u);
+}
+
+inline int bits_for(uint64_t maxval) {
+    int b = 0;
+    while (b < 64 && (maxval >> b) != 0) ++b;
+    return b;
+}
+
+inline unsigned grid_for(int64_t n, int per_block = kBlock, unsigned cap = 8192) {
+    int64_t g = (n + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return unsigned(g);
+}
+
+void sync(fz_ctx *c);
+
+}  // namespace fz

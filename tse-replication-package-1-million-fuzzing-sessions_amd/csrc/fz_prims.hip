@@ -1,0 +1,461 @@
+// Device-wide primitives: exclusive scan, stable LSD radix sort, min/max, segment offsets,
+// numpy-compatible describe.  All launches go to the context stream; scratch comes from the arena.
+#include <cmath>
+
+#include "fz_device.h"
+#include "fz_internal.h"
+#include "fz_views.h"
+
+namespace fz {
+
+void sync(fz_ctx *c) { FZ_HIP(hipStreamSynchronize(c->stream)); }
+
+// ------------------------------------------------------------------------------ scan (int64)
+constexpr int kScanItems = 8;
+constexpr int kScanChunk = kBlock * kScanItems;  // 2048 elements per workgroup
+
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(const int64_t *__restrict__ in, int64_t n,
+                                                        int64_t *__restrict__ sums) {
+    __shared__ int64_t s_tmp[4];
+    const int64_t base = int64_t(blockIdx.x) * kScanChunk;
+    int64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        int64_t idx = base + i * kBlock + threadIdx.x;
+        if (idx < n) acc += in[idx];
+    }
+    int64_t tot = block_sum(acc, s_tmp);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// Exclusive scan of one chunk per workgroup, plus a per-chunk carry (may be null).
+__global__ __launch_bounds__(kBlock) void k_scan_chunk(const int64_t *__restrict__ in, int64_t *__restrict__ out,
+                                                       int64_t n, const int64_t *__restrict__ carry,
+                                                       int64_t *__restrict__ total) {
+    __shared__ int64_t s_val[kScanChunk];
+    __shared__ int64_t s_tmp[4];
+    const int64_t base = int64_t(blockIdx.x) * kScanChunk;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        int64_t idx = base + i * kBlock + threadIdx.x;
+        s_val[i * kBlock + threadIdx.x] = idx < n ? in[idx] : 0;
+    }
+    __syncthreads();
+    int64_t loc[kScanItems];
+    int64_t run = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        loc[i] = run;
+        run += s_val[threadIdx.x * kScanItems + i];
+    }
+    int64_t btot;
+    int64_t off = block_excl_scan(run, s_tmp, &btot);
+    off += carry ? carry[blockIdx.x] : 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) s_val[threadIdx.x * kScanItems + i] = loc[i] + off;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        int64_t idx = base + i * kBlock + threadIdx.x;
+        if (idx < n) out[idx] = s_val[i * kBlock + threadIdx.x];
+    }
+    if (total && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *total = off + btot;
+}
+
+void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, int64_t *out_total) {
+    if (n <= 0) {
+        if (out_total) FZ_HIP(hipMemsetAsync(out_total, 0, sizeof(int64_t), c->stream));
+        return;
+    }
+    const int64_t nb = (n + kScanChunk - 1) / kScanChunk;
+    if (nb == 1) {
+        k_scan_chunk<<<1, kBlock, 0, c->stream>>>(in, out, n, nullptr, out_total);
+        FZ_LAUNCH_CHECK();
+        return;
+    }
+    int64_t *sums = c->arena.get<int64_t>(nb);
+    k_scan_reduce<<<unsigned(nb), kBlock, 0, c->stream>>>(in, n, sums);
+    FZ_LAUNCH_CHECK();
+    scan_exclusive_i64(c, sums, sums, nb, nullptr);  // recursion depth log_2048(n)
+    k_scan_chunk<<<unsigned(nb), kBlock, 0, c->stream>>>(in, out, n, sums, out_total);
+    FZ_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------- LSD radix sort
+constexpr int kRadixBits = 8;
+constexpr int kRadix = 1 << kRadixBits;
+constexpr int kSortItems = 16;
+constexpr int kSortTile = kBlock * kSortItems;  // 4096 keys per workgroup
+
+// Per-tile digit histogram, digit-major: counts[d * nb + tile].
+__global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t *__restrict__ keys, int64_t n, int shift,
+                                                       int64_t *__restrict__ counts, int64_t nb) {
+    __shared__ uint32_t s_hist[kRadix];
+    s_hist[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t base = int64_t(blockIdx.x) * kSortTile;
+    for (int r = 0; r < kSortItems; ++r) {
+        const int64_t idx = base + r * kBlock + threadIdx.x;
+        const bool valid = idx < n;
+        const uint32_t d = valid ? uint32_t(keys[idx] >> shift) & (kRadix - 1) : 0u;
+        const uint64_t peers = match_digit<kRadixBits>(d, valid);
+        if (valid && (__ffsll((long long)peers) - 1) == lane_id()) atomicAdd(&s_hist[d], uint32_t(__popcll(peers)));
+    }
+    __syncthreads();
+    counts[int64_t(threadIdx.x) * nb + blockIdx.x] = s_hist[threadIdx.x];
+}
+
+// Stable scatter: ranks inside the tile follow row order (round, wave, lane); the tile is staged
+// digit-sorted in LDS and written out in runs (coalesced per digit).
+template <bool HAS_VALS>
+__global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t *__restrict__ keys_in,
+                                                          const uint32_t *__restrict__ vals_in,
+                                                          uint64_t *__restrict__ keys_out,
+                                                          uint32_t *__restrict__ vals_out, int64_t n, int shift,
+                                                          const int64_t *__restrict__ counts,
+                                                          const int64_t *__restrict__ offsets, int64_t nb) {
+    __shared__ uint64_t s_keys[kSortTile];
+    __shared__ uint32_t s_vals[HAS_VALS ? kSortTile : 1];
+    __shared__ uint32_t s_start[kRadix];
+    __shared__ uint32_t s_run[kRadix];
+    __shared__ uint32_t s_wcnt[4][kRadix];
+    __shared__ int64_t s_goff[kRadix];
+    __shared__ uint32_t s_tmp[4];
+
+    const int tid = threadIdx.x;
+    const int w = wave_id();
+    const int64_t base = int64_t(blockIdx.x) * kSortTile;
+    {
+        uint32_t cnt = uint32_t(counts[int64_t(tid) * nb + blockIdx.x]);
+        uint32_t st = block_excl_scan(cnt, s_tmp, (uint32_t *)nullptr);
+        s_start[tid] = st;
+        s_run[tid] = 0;
+        s_goff[tid] = offsets[int64_t(tid) * nb + blockIdx.x];
+    }
+    for (int r = 0; r < kSortItems; ++r) {
+        const int64_t idx = base + r * kBlock + tid;
+        const bool valid = idx < n;
+        uint64_t k = valid ? keys_in[idx] : 0ull;
+        uint32_t v = 0;
+        if (HAS_VALS && valid) v = vals_in[idx];
+        const uint32_t d = uint32_t(k >> shift) & (kRadix - 1);
+        for (int i = 0; i < 4; ++i) s_wcnt[i][tid] = 0;
+        __syncthreads();
+        const uint64_t peers = match_digit<kRadixBits>(d, valid);
+        const uint32_t rank = uint32_t(__popcll(peers & lanemask_lt()));
+        if (valid && (__ffsll((long long)peers) - 1) == lane_id()) s_wcnt[w][d] = uint32_t(__popcll(peers));
+        __syncthreads();
+        if (valid) {
+            uint32_t wpre = 0;
+            for (int i = 0; i < w; ++i) wpre += s_wcnt[i][d];
+            const uint32_t pos = s_start[d] + s_run[d] + wpre + rank;
+            s_keys[pos] = k;
+            if (HAS_VALS) s_vals[pos] = v;
+        }
+        __syncthreads();
+        s_run[tid] += s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
+    }
+    __syncthreads();
+    const int64_t valid_n = (n - base) < kSortTile ? (n - base) : kSortTile;
+    for (int i = tid; i < valid_n; i += kBlock) {
+        const uint64_t k = s_keys[i];
+        const uint32_t d = uint32_t(k >> shift) & (kRadix - 1);
+        const int64_t gpos = s_goff[d] + (i - int64_t(s_start[d]));
+        keys_out[gpos] = k;
+        if (HAS_VALS) vals_out[gpos] = s_vals[i];
+    }
+}
+
+void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int bits) {
+    if (n <= 1 || bits <= 0) return;
+    const int64_t nb = (n + kSortTile - 1) / kSortTile;
+    uint64_t *k2 = c->arena.get<uint64_t>(n);
+    uint32_t *v2 = vals ? c->arena.get<uint32_t>(n) : nullptr;
+    int64_t *counts = c->arena.get<int64_t>(nb * kRadix);
+    int64_t *offs = c->arena.get<int64_t>(nb * kRadix);
+    uint64_t *ka = keys, *kb = k2;
+    uint32_t *va = vals, *vb = v2;
+    int passes = 0;
+    for (int shift = 0; shift < bits; shift += kRadixBits) {
+        {
+            ProbeScope ps(c, "radix_hist", 8.0 * double(n));
+            k_radix_hist<<<unsigned(nb), kBlock, 0, c->stream>>>(ka, n, shift, counts, nb);
+            FZ_LAUNCH_CHECK();
+        }
+        scan_exclusive_i64(c, counts, offs, nb * kRadix, nullptr);
+        {
+            // algorithmic traffic of one pass: read + write every key (8 B) and value (4 B)
+            ProbeScope ps(c, "radix_scatter", (vals ? 24.0 : 16.0) * double(n));
+            if (vals)
+                k_radix_scatter<true><<<unsigned(nb), kBlock, 0, c->stream>>>(ka, va, kb, vb, n, shift, counts, offs,
+                                                                              nb);
+            else
+                k_radix_scatter<false><<<unsigned(nb), kBlock, 0, c->stream>>>(ka, va, kb, vb, n, shift, counts, offs,
+                                                                               nb);
+            FZ_LAUNCH_CHECK();
+        }
+        std::swap(ka, kb);
+        std::swap(va, vb);
+        ++passes;
+    }
+    if (ka != keys) {
+        FZ_HIP(hipMemcpyAsync(keys, ka, size_t(n) * sizeof(uint64_t), hipMemcpyDeviceToDevice, c->stream));
+        if (vals) FZ_HIP(hipMemcpyAsync(vals, va, size_t(n) * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+    }
+    c->store.passes += passes;
+}
+
+// ------------------------------------------------------------------------------- min / max
+__global__ __launch_bounds__(kBlock) void k_minmax(const int64_t *__restrict__ x, int64_t n,
+                                                   unsigned long long *__restrict__ mm) {
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const int64_t v = x[i];
+        if (v == FZ_TS_NULL) continue;
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
+    lo = wave_min(lo);
+    hi = wave_max(hi);
+    if (lane_id() == 0) {
+        // order-preserving unsigned images so one unsigned atomic min/max covers negatives too
+        atomicMin(&mm[0], (unsigned long long)(lo) ^ 0x8000000000000000ull);
+        atomicMax(&mm[1], (unsigned long long)(hi) ^ 0x8000000000000000ull);
+    }
+}
+
+void minmax_i64_to_host(fz_ctx *c, const int64_t *const *cols, const int64_t *ns, int ncols, int64_t *host_minmax) {
+    unsigned long long *mm = c->arena.get<unsigned long long>(2 * ncols);
+    std::vector<unsigned long long> init(2 * ncols);
+    for (int i = 0; i < ncols; ++i) {
+        init[2 * i] = ~0ull;
+        init[2 * i + 1] = 0ull;
+    }
+    FZ_HIP(hipMemcpyAsync(mm, init.data(), init.size() * 8, hipMemcpyHostToDevice, c->stream));
+    for (int i = 0; i < ncols; ++i) {
+        if (ns[i] <= 0) continue;
+        k_minmax<<<grid_for(ns[i], kBlock, 1024), kBlock, 0, c->stream>>>(cols[i], ns[i], mm + 2 * i);
+        FZ_LAUNCH_CHECK();
+    }
+    FZ_HIP(hipMemcpyAsync(c->h_pinned, mm, 2 * ncols * 8, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    for (int i = 0; i < 2 * ncols; ++i)
+        host_minmax[i] = int64_t(uint64_t(c->h_pinned[i]) ^ 0x8000000000000000ull);
+}
+
+// ------------------------------------------------------------------------ segment offsets
+__global__ __launch_bounds__(kBlock) void k_segment_offsets(const uint32_t *__restrict__ proj, int64_t n, int64_t P,
+                                                            int64_t *__restrict__ offsets) {
+    const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (p > P) return;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (int64_t(proj[mid]) < p) lo = mid + 1;
+        else hi = mid;
+    }
+    offsets[p] = lo;
+}
+
+void segment_offsets(fz_ctx *c, const uint32_t *sorted_proj, int64_t n, int64_t P, int64_t *offsets) {
+    k_segment_offsets<<<grid_for(P + 1, kBlock, 1u << 30), kBlock, 0, c->stream>>>(sorted_proj, n, P, offsets);
+    FZ_LAUNCH_CHECK();
+}
+
+// -------------------------------------------------------------------------------- describe
+__global__ void k_set_i64(int64_t *p, int64_t v) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *p = v;
+}
+
+// keys of x[0..n) as order-preserving images; entries past n sort last.
+__global__ __launch_bounds__(kBlock) void k_f64_keys(const double *__restrict__ x, int64_t nmax,
+                                                     const int64_t *__restrict__ d_n, uint64_t *__restrict__ k) {
+    const int64_t n = *d_n;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nmax; i += int64_t(gridDim.x) * kBlock)
+        k[i] = i < n ? f64_key(x[i]) : ~0ull;
+}
+
+// Double-double partial sums of x (pass 1) or of (x - mean)^2 (pass 2, mean read from device).
+__global__ __launch_bounds__(kBlock) void k_dd_partial(const double *__restrict__ x, const int64_t *__restrict__ d_n,
+                                                       const double *__restrict__ mean, double *__restrict__ part) {
+    __shared__ double s_hi[4], s_lo[4];
+    const int64_t n = *d_n;
+    DD acc{0.0, 0.0};
+    const double m = mean ? *mean : 0.0;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        double v = x[i];
+        if (mean) {
+            v = v - m;
+            v = v * v;
+        }
+        acc = dd_add_d(acc, v);
+    }
+    acc = wave_dd_sum(acc);
+    if (lane_id() == 0) {
+        s_hi[wave_id()] = acc.hi;
+        s_lo[wave_id()] = acc.lo;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        DD t{s_hi[0], s_lo[0]};
+        for (int i = 1; i < 4; ++i) t = dd_add(t, DD{s_hi[i], s_lo[i]});
+        part[2 * blockIdx.x] = t.hi;
+        part[2 * blockIdx.x + 1] = t.lo;
+    }
+}
+
+// Reduce the partials; writes sum/n to *out (mode 0: mean; mode 1: sqrt(sum/n) = std, ddof 0).
+__global__ __launch_bounds__(kBlock) void k_dd_final(const double *__restrict__ part, int nparts,
+                                                     const int64_t *__restrict__ d_n, int mode,
+                                                     double *__restrict__ out) {
+    __shared__ double s_hi[4], s_lo[4];
+    const int64_t n = *d_n;
+    DD acc{0.0, 0.0};
+    for (int i = threadIdx.x; i < nparts; i += kBlock) acc = dd_add(acc, DD{part[2 * i], part[2 * i + 1]});
+    acc = wave_dd_sum(acc);
+    if (lane_id() == 0) {
+        s_hi[wave_id()] = acc.hi;
+        s_lo[wave_id()] = acc.lo;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        DD t{s_hi[0], s_lo[0]};
+        for (int i = 1; i < 4; ++i) t = dd_add(t, DD{s_hi[i], s_lo[i]});
+        const double s = t.hi + t.lo;
+        const double q = n > 0 ? s / double(n) : NAN;
+        *out = mode == 0 ? q : sqrt(q);
+    }
+}
+
+__device__ inline int64_t lower_bound_u64(const uint64_t *a, int64_t n, uint64_t v) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ inline int64_t upper_bound_u64(const uint64_t *a, int64_t n, uint64_t v) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (a[mid] <= v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_describe_finish(const uint64_t *__restrict__ sk, const int64_t *__restrict__ d_n,
+                                  const double *__restrict__ ms, fz_describe *__restrict__ out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int64_t n = *d_n;
+    fz_describe d;
+    d.count = n;
+    if (n <= 0) {
+        d.n_pos = d.n_zero = d.n_neg = 0;
+        d.mean = d.median = d.std = d.min = d.max = d.q1 = d.q3 = d.min_nonzero = NAN;
+        d.has_nonzero = 0;
+        *out = d;
+        return;
+    }
+    d.mean = ms[0];
+    d.std = ms[1];
+    const uint64_t kneg0 = f64_key(-0.0), kpos0 = f64_key(0.0), kinf = f64_key(INFINITY);
+    const int64_t lt0 = lower_bound_u64(sk, n, kneg0);
+    const int64_t le0 = upper_bound_u64(sk, n, kpos0);
+    const int64_t leinf = upper_bound_u64(sk, n, kinf);
+    d.n_neg = lt0;
+    d.n_zero = le0 - lt0;
+    d.n_pos = leinf - le0;
+    auto get = [&](int64_t i) { return f64_from_key(sk[i]); };
+    d.min = get(0);
+    d.max = get(n - 1);
+    // np.median: middle element, or mean of the two middle ones ((a + b) / 2)
+    d.median = (n & 1) ? get(n / 2) : (get(n / 2 - 1) + get(n / 2)) / 2.0;
+    d.q1 = np_percentile_sorted(get, n, 25.0);
+    d.q3 = np_percentile_sorted(get, n, 75.0);
+    // min over values != 0 (rq1_detection_rate.py:264)
+    if (lt0 > 0) {
+        d.min_nonzero = get(0);
+        d.has_nonzero = 1;
+    } else if (le0 < n) {
+        d.min_nonzero = get(le0);
+        d.has_nonzero = 1;
+    } else {
+        d.min_nonzero = NAN;
+        d.has_nonzero = 0;
+    }
+    *out = d;
+}
+
+void describe_f64_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n, fz_describe *dev_out) {
+    const int64_t nn = nmax < 1 ? 1 : nmax;
+    uint64_t *k = c->arena.get<uint64_t>(nn);
+    const unsigned g = grid_for(nn, kBlock, 1024);
+    k_f64_keys<<<g, kBlock, 0, c->stream>>>(x, nmax, d_n, k);
+    FZ_LAUNCH_CHECK();
+    radix_sort_pairs(c, k, nullptr, nmax, 64);
+    double *part = c->arena.get<double>(2 * g);
+    double *ms = c->arena.get<double>(2);
+    k_dd_partial<<<g, kBlock, 0, c->stream>>>(x, d_n, nullptr, part);
+    k_dd_final<<<1, kBlock, 0, c->stream>>>(part, int(g), d_n, 0, ms);
+    k_dd_partial<<<g, kBlock, 0, c->stream>>>(x, d_n, ms, part);
+    k_dd_final<<<1, kBlock, 0, c->stream>>>(part, int(g), d_n, 1, ms + 1);
+    k_describe_finish<<<1, 64, 0, c->stream>>>(k, d_n, ms, dev_out);
+    FZ_LAUNCH_CHECK();
+}
+
+void describe_f64(fz_ctx *c, const double *x, int64_t n, fz_describe *dev_out) {
+    int64_t *d_n = c->arena.get<int64_t>(1);
+    k_set_i64<<<1, 64, 0, c->stream>>>(d_n, n < 0 ? 0 : n);
+    FZ_LAUNCH_CHECK();
+    describe_f64_dn(c, x, n < 0 ? 0 : n, d_n, dev_out);
+}
+
+// ----------------------------------------------------------------------- views / compaction
+__global__ __launch_bounds__(kBlock) void k_compact_view(const int32_t *__restrict__ rows,
+                                                         const int64_t *__restrict__ times,
+                                                         const uint32_t *__restrict__ proj, int64_t n,
+                                                         const int64_t *__restrict__ flags,
+                                                         const int64_t *__restrict__ pos, int32_t *__restrict__ orow,
+                                                         int64_t *__restrict__ otime, uint32_t *__restrict__ oproj) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        if (flags[i]) {
+            const int64_t p = pos[i];
+            orow[p] = rows[i];
+            otime[p] = times[i];
+            oproj[p] = proj[i];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_segment_offsets_dn(const uint32_t *__restrict__ proj,
+                                                               const int64_t *__restrict__ d_n, int64_t P,
+                                                               int64_t *__restrict__ offsets) {
+    const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (p > P) return;
+    int64_t lo = 0, hi = *d_n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (int64_t(proj[mid]) < p) lo = mid + 1;
+        else hi = mid;
+    }
+    offsets[p] = lo;
+}
+
+__global__ __launch_bounds__(kBlock) void k_count_flags(const uint8_t *__restrict__ f, int64_t n, int64_t *out) {
+    __shared__ int64_t s_tmp[4];
+    int64_t acc = 0;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+        acc += f[i] != 0;
+    acc = block_sum(acc, s_tmp);
+    if (threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long *>(out), (unsigned long long)acc);
+}
+
+void count_flags(fz_ctx *c, const uint8_t *flags, int64_t P, int64_t *out) {
+    k_count_flags<<<grid_for(P, kBlock, 256), kBlock, 0, c->stream>>>(flags, P, out);
+    FZ_LAUNCH_CHECK();
+}
+
+}  // namespace fz

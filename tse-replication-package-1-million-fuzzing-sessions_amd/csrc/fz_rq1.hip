@@ -1,0 +1,369 @@
+// RQ1 - bug-detection rate per fuzzing iteration (rq1_detection_rate.py:101-269).
+//
+// Reference flow and its replacement here:
+//   eligibility GROUP BY/HAVING (:144-152)            -> k_elig_hist (LDS-privatised histogram)
+//   878 x ALL_FUZZING_BUILD (:189-203)                -> segment lengths of store.fuzz, histogram,
+//                                                        reverse scan (projects alive at iteration i)
+//   SAME_DATE_BUILD_ISSUE as-of join (queries1.py:15-58) -> per-issue lower_bound in the filtered
+//                                                        (Finish|Halfway, < LIMIT) Fuzzing view
+//   ROW_NUMBER() OVER (PARTITION BY number ...)        -> two stable radix sorts (build time desc,
+//                                                        then number); segment heads survive
+//   43k x O(B) iteration scans (:213-230)             -> per-issue lower_bound in store.fuzz;
+//                                                        distinct (iteration, project) by adjacency
+//   finalize + late-stage stats (:233-268)            -> rate kernel + describe_f64_dn
+#include "fz_device.h"
+#include "fz_internal.h"
+#include "fz_views.h"
+
+namespace fz {
+
+constexpr int64_t kLimitUs = 1736294400000000LL;  // '2025-01-08 00:00:00' (queries1.py:3)
+constexpr int64_t kEligMin = 365;                 // HAVING COUNT(*) >= 365
+
+// total_coverage rows: coverage IS NOT NULL AND coverage > 0 AND date < LIMIT, per project.
+__global__ __launch_bounds__(kBlock) void k_elig_hist(const uint32_t *__restrict__ proj,
+                                                      const int64_t *__restrict__ date,
+                                                      const double *__restrict__ cov,
+                                                      const uint8_t *__restrict__ valid, int64_t n, int64_t P,
+                                                      int64_t limit, int32_t *__restrict__ counts, int use_lds) {
+    extern __shared__ int32_t s_hist[];
+    if (use_lds) {
+        for (int64_t p = threadIdx.x; p < P; p += kBlock) s_hist[p] = 0;
+        __syncthreads();
+    }
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const bool ok = (valid[i] & FZ_VALID_COVERAGE) && cov[i] > 0.0 && date[i] < limit;
+        if (ok) {
+            if (use_lds) atomicAdd(&s_hist[proj[i]], 1);
+            else atomicAdd(&counts[proj[i]], 1);
+        }
+    }
+    if (use_lds) {
+        __syncthreads();
+        for (int64_t p = threadIdx.x; p < P; p += kBlock)
+            if (s_hist[p]) atomicAdd(&counts[p], s_hist[p]);
+    }
+}
+
+void eligibility_counts(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *counts) {
+    const int64_t P = t->n_projects;
+    FZ_HIP(hipMemsetAsync(counts, 0, size_t(P > 0 ? P : 1) * 4, c->stream));
+    if (t->n_cov <= 0 || P <= 0) return;
+    const int use_lds = P <= 16384;
+    const size_t lds = use_lds ? size_t(P) * 4 : 0;
+    // algorithmic bytes: project 4 + date 8 + coverage 8 + validity 1 per row
+    ProbeScope ps(c, "elig_hist", 21.0 * double(t->n_cov));
+    k_elig_hist<<<grid_for(t->n_cov, kBlock, 1024), kBlock, lds, c->stream>>>(
+        t->c_project, t->c_date, t->c_coverage, t->c_valid, t->n_cov, P, limit, counts, use_lds);
+    FZ_LAUNCH_CHECK();
+}
+
+__global__ __launch_bounds__(kBlock) void k_elig_flags(const int32_t *__restrict__ counts, int64_t P,
+                                                       uint8_t *__restrict__ elig, int64_t *__restrict__ n_elig) {
+    for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < P; p += int64_t(gridDim.x) * kBlock) {
+        const bool e = counts[p] >= kEligMin;
+        elig[p] = e;
+        if (e) atomic_add_i64(n_elig, 1);
+    }
+}
+
+// Histogram of Fuzzing-build counts over eligible projects; total and max.
+__global__ __launch_bounds__(kBlock) void k_iter_hist(const int64_t *__restrict__ offs, const uint8_t *__restrict__ elig,
+                                                      int64_t P, int64_t *__restrict__ hist,
+                                                      int64_t *__restrict__ counts) {
+    for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < P; p += int64_t(gridDim.x) * kBlock) {
+        if (!elig[p]) continue;
+        const int64_t nf = offs[p + 1] - offs[p];
+        atomic_add_i64(&hist[nf], 1);
+        atomic_add_i64(&counts[FZ_RQ1_TOTAL_FUZZ], nf);
+        atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ1_MAX_ITER]), (unsigned long long)nf);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_reverse_tail(const int64_t *__restrict__ hist, int64_t M,
+                                                         int64_t *__restrict__ rev) {
+    for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < M; j += int64_t(gridDim.x) * kBlock)
+        rev[j] = hist[M - j];
+}
+
+// iter_total[i-1] = sum_{k >= i} hist[k]
+__global__ __launch_bounds__(kBlock) void k_iter_total(const int64_t *__restrict__ rev_excl,
+                                                       const int64_t *__restrict__ rev, int64_t M,
+                                                       int64_t *__restrict__ iter_total) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x + 1; i <= M; i += int64_t(gridDim.x) * kBlock) {
+        const int64_t j = M - i;
+        iter_total[i - 1] = rev_excl[j] + rev[j];
+    }
+}
+
+struct ValidFuzzRq1 {  // result IN ('Finish', 'Halfway') AND DATE(timecreated) < LIMIT  (queries1.py:39-43)
+    const uint8_t *result;
+    const int64_t *time;
+    __device__ bool operator()(int32_t r) const {
+        const uint8_t x = result[r];
+        return (x == 0 || x == 1) && time[r] < kLimitUs;
+    }
+};
+
+// One pass over the (project, rts)-sorted issues: counts, per-project flags, as-of join.
+__global__ __launch_bounds__(kBlock) void k_issue_pass(View iss, const uint8_t *__restrict__ status,
+                                                       const uint8_t *__restrict__ elig,
+                                                       const int32_t *__restrict__ pi_count,
+                                                       const int32_t *__restrict__ vrow,
+                                                       const int64_t *__restrict__ vtime,
+                                                       const int64_t *__restrict__ voffs, int64_t *__restrict__ counts,
+                                                       uint8_t *__restrict__ f_lim, uint8_t *__restrict__ f_fixlim,
+                                                       uint8_t *__restrict__ f_tgt, int64_t *__restrict__ mbuild,
+                                                       int64_t *__restrict__ mbtime) {
+    for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < iss.n; j += int64_t(gridDim.x) * kBlock) {
+        const int32_t r = iss.row[j];
+        const uint32_t p = iss.proj[j];
+        const int64_t rts = iss.time[j];
+        const bool lim = rts < kLimitUs;
+        const bool fixed = status[r] <= 1;
+        const bool el = elig[p];
+        if (lim) {
+            atomic_add_i64(&counts[FZ_RQ1_ISSUES_LIM], 1);
+            f_lim[p] = 1;
+            if (fixed) {
+                atomic_add_i64(&counts[FZ_RQ1_FIXED_LIM], 1);
+                f_fixlim[p] = 1;
+                if (el) {
+                    atomic_add_i64(&counts[FZ_RQ1_TARGET], 1);
+                    f_tgt[p] = 1;
+                }
+            }
+        }
+        int64_t mb = -1, bt = 0;
+        if (fixed && el) {
+            if (rts != FZ_TS_NULL) {
+                const int64_t lo = voffs[p], hi = voffs[p + 1];
+                const int64_t k = lower_bound_i64(vtime, lo, hi, rts);
+                if (k > lo) {
+                    mb = vrow[k - 1];
+                    bt = vtime[k - 1];
+                }
+            }
+            if (mb < 0 && pi_count) atomic_add_i64(&counts[FZ_RQ1_WITHOUT_MATCHING], pi_count[p]);
+        }
+        mbuild[j] = mb;
+        mbtime[j] = bt;
+    }
+}
+
+// ROW_NUMBER() OVER (PARTITION BY number ORDER BY timecreated DESC) = 1: stage keys.
+__global__ __launch_bounds__(kBlock) void k_dedup_keys1(const int64_t *__restrict__ mbuild,
+                                                        const int64_t *__restrict__ mbtime, int64_t n, int64_t btmax,
+                                                        uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < n; j += int64_t(gridDim.x) * kBlock) {
+        keys[j] = mbuild[j] >= 0 ? uint64_t(btmax - mbtime[j]) : 0ull;
+        vals[j] = uint32_t(j);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_dedup_keys2(const uint32_t *__restrict__ vals,
+                                                        const int64_t *__restrict__ mbuild, View iss,
+                                                        const int64_t *__restrict__ number, int64_t n,
+                                                        uint64_t *__restrict__ keys) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const uint32_t j = vals[i];
+        keys[i] = mbuild[j] >= 0 ? (uint64_t(number[iss.row[j]]) ^ 0x8000000000000000ull) : ~0ull;
+    }
+}
+
+// Sorted by (number, build time desc, output order): the head of each number segment survives.
+__global__ __launch_bounds__(kBlock) void k_dedup_heads(const uint32_t *__restrict__ vals,
+                                                        const uint64_t *__restrict__ keys,
+                                                        const int64_t *__restrict__ mbuild, int64_t n,
+                                                        int64_t *__restrict__ keep) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const uint32_t j = vals[i];
+        bool head = mbuild[j] >= 0;
+        if (head && i > 0) {
+            const uint32_t pj = vals[i - 1];
+            head = !(mbuild[pj] >= 0 && keys[i - 1] == keys[i]);
+        }
+        keep[j] = head ? 1 : 0;
+    }
+}
+
+// Compact kept matches in (project, rts) order; iteration = #Fuzzing builds with time < rts.
+__global__ __launch_bounds__(kBlock) void k_matched_out(View iss, const int64_t *__restrict__ keep,
+                                                        const int64_t *__restrict__ pos,
+                                                        const int64_t *__restrict__ mbuild, View fuzz,
+                                                        int64_t *__restrict__ out_issue,
+                                                        int64_t *__restrict__ out_build, int64_t *__restrict__ it_arr,
+                                                        uint32_t *__restrict__ p_arr, uint8_t *__restrict__ f_match) {
+    for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < iss.n; j += int64_t(gridDim.x) * kBlock) {
+        if (!keep[j]) continue;
+        const int64_t q = pos[j];
+        const uint32_t p = iss.proj[j];
+        out_issue[q] = iss.row[j];
+        out_build[q] = mbuild[j];
+        const int64_t lo = fuzz.offs[p], hi = fuzz.offs[p + 1];
+        it_arr[q] = lower_bound_i64(fuzz.time, lo, hi, iss.time[j]) - lo;
+        p_arr[q] = p;
+        f_match[p] = 1;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_distinct_iter(const int64_t *__restrict__ it_arr,
+                                                          const uint32_t *__restrict__ p_arr,
+                                                          const int64_t *__restrict__ d_n,
+                                                          int64_t *__restrict__ iter_det) {
+    const int64_t n = *d_n;
+    for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < n; q += int64_t(gridDim.x) * kBlock) {
+        const int64_t it = it_arr[q];
+        if (it <= 0) continue;
+        if (q > 0 && p_arr[q - 1] == p_arr[q] && it_arr[q - 1] == it) continue;
+        atomic_add_i64(&iter_det[it - 1], 1);
+    }
+}
+
+// Kept iterations are the prefix 1..K (iter_total is non-increasing); first key with rate < 5.
+__global__ __launch_bounds__(kBlock) void k_rates(const int64_t *__restrict__ iter_total,
+                                                  const int64_t *__restrict__ iter_det, int64_t M, int64_t threshold,
+                                                  int64_t *__restrict__ counts, double *__restrict__ rates) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < M; i += int64_t(gridDim.x) * kBlock) {
+        const int64_t tot = iter_total[i];
+        if (tot < threshold || tot <= 0) continue;
+        atomic_add_i64(&counts[FZ_RQ1_KEPT_ITERS], 1);
+        const double r = double(iter_det[i]) / double(tot) * 100.0;  // :245 (Python float ops)
+        rates[i] = r;
+        if (r < 5.0) atomicMin(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ1_FIRST_DOWN]),
+                                (unsigned long long)(i + 1));
+    }
+}
+
+// late = rates[first_down:] (first_down is a KEY used as a list index; -1 -> the last rate).
+__global__ void k_late_bounds(int64_t *__restrict__ counts, int64_t *__restrict__ late_lo) {
+    if (threadIdx.x || blockIdx.x) return;
+    const int64_t K = counts[FZ_RQ1_KEPT_ITERS];
+    int64_t fd = counts[FZ_RQ1_FIRST_DOWN];
+    if (uint64_t(fd) == ~0ull) fd = -1;
+    counts[FZ_RQ1_FIRST_DOWN] = fd;
+    int64_t lo = fd >= 0 ? fd : K - 1;
+    if (lo < 0) lo = 0;
+    const int64_t n = K > lo ? K - lo : 0;
+    counts[FZ_RQ1_LATE] = n;
+    late_lo[0] = lo;
+    late_lo[1] = n;
+}
+
+__global__ __launch_bounds__(kBlock) void k_late_copy(const double *__restrict__ rates,
+                                                      const int64_t *__restrict__ late_lo, double *__restrict__ late) {
+    const int64_t lo = late_lo[0], n = late_lo[1];
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+        late[i] = rates[lo + i];
+}
+
+void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_out *o) {
+    Store &s = c->store;
+    FZ_CHECK(s.built, "fz_rq1: call fz_store_build first");
+    FZ_CHECK(o && o->counts && o->eligible && o->iter_total && o->iter_detected && o->matched_issue &&
+                 o->matched_build && o->late,
+             "fz_rq1: null output buffer");
+    const fz_tables &t = s.t;
+    const int64_t P = s.P;
+    const int64_t M = s.fuzz.max_seg;
+    hipStream_t st = c->stream;
+    FZ_HIP(hipMemsetAsync(o->counts, 0, FZ_RQ1_NCOUNTS * sizeof(int64_t), st));
+    FZ_HIP(hipMemsetAsync(o->counts + FZ_RQ1_FIRST_DOWN, 0xff, sizeof(int64_t), st));
+    FZ_HIP(hipMemsetAsync(o->iter_total, 0, size_t(M > 0 ? M : 1) * 8, st));
+    FZ_HIP(hipMemsetAsync(o->iter_detected, 0, size_t(M > 0 ? M : 1) * 8, st));
+
+    // eligibility (:144-152)
+    int32_t *ecount = c->arena.get<int32_t>(P);
+    eligibility_counts(c, &t, kLimitUs, ecount);
+    if (P > 0) {
+        k_elig_flags<<<grid_for(P), kBlock, 0, st>>>(ecount, P, o->eligible, o->counts + FZ_RQ1_ELIGIBLE);
+        FZ_LAUNCH_CHECK();
+    }
+
+    // phase 1: projects alive at each iteration (:189-203)
+    int64_t *hist = c->arena.get<int64_t>(M + 1);
+    FZ_HIP(hipMemsetAsync(hist, 0, size_t(M + 1) * 8, st));
+    if (P > 0) {
+        k_iter_hist<<<grid_for(P), kBlock, 0, st>>>(s.fuzz.offs, o->eligible, P, hist, o->counts);
+        FZ_LAUNCH_CHECK();
+    }
+    if (M > 0) {
+        int64_t *rev = c->arena.get<int64_t>(M);
+        int64_t *rex = c->arena.get<int64_t>(M);
+        k_reverse_tail<<<grid_for(M), kBlock, 0, st>>>(hist, M, rev);
+        scan_exclusive_i64(c, rev, rex, M, nullptr);
+        k_iter_total<<<grid_for(M), kBlock, 0, st>>>(rex, rev, M, o->iter_total);
+        FZ_LAUNCH_CHECK();
+    }
+
+    // SAME_DATE_BUILD_ISSUE partner view
+    TmpView v1;
+    filter_view(c, s.fuzz.row, s.fuzz.time, s.fuzz.proj, s.fuzz.n, P, ValidFuzzRq1{t.b_result, t.b_time}, v1);
+
+    // issues pass
+    const int64_t NI = s.issues.n;
+    uint8_t *flags = c->arena.get<uint8_t>(4 * P);
+    FZ_HIP(hipMemsetAsync(flags, 0, size_t(4 * (P > 0 ? P : 1)), st));
+    uint8_t *f_lim = flags, *f_fixlim = flags + P, *f_tgt = flags + 2 * P, *f_match = flags + 3 * P;
+    int64_t *mbuild = c->arena.get<int64_t>(NI);
+    int64_t *mbtime = c->arena.get<int64_t>(NI);
+    if (NI > 0) {
+        k_issue_pass<<<grid_for(NI, kBlock, 2048), kBlock, 0, st>>>(s.issues, t.i_status, o->eligible, t.pi_count,
+                                                                    v1.row, v1.time, v1.offs, o->counts, f_lim,
+                                                                    f_fixlim, f_tgt, mbuild, mbtime);
+        FZ_LAUNCH_CHECK();
+    }
+
+    // ROW_NUMBER dedup by issue number
+    int64_t *keep = c->arena.get<int64_t>(NI);
+    int64_t *pos = c->arena.get<int64_t>(NI);
+    int64_t *d_nm = o->counts + FZ_RQ1_MATCHED;
+    if (NI > 0) {
+        uint64_t *keys = c->arena.get<uint64_t>(NI);
+        uint32_t *vals = c->arena.get<uint32_t>(NI);
+        const unsigned g = grid_for(NI, kBlock, 2048);
+        const int64_t btmax = s.tmax[0];
+        const int tb = bits_for(uint64_t(s.tmax[0] >= s.tmin[0] ? s.tmax[0] - s.tmin[0] : 0));
+        k_dedup_keys1<<<g, kBlock, 0, st>>>(mbuild, mbtime, NI, btmax, keys, vals);
+        FZ_LAUNCH_CHECK();
+        radix_sort_pairs(c, keys, vals, NI, tb);
+        k_dedup_keys2<<<g, kBlock, 0, st>>>(vals, mbuild, s.issues, t.i_number, NI, keys);
+        FZ_LAUNCH_CHECK();
+        radix_sort_pairs(c, keys, vals, NI, 64);
+        k_dedup_heads<<<g, kBlock, 0, st>>>(vals, keys, mbuild, NI, keep);
+        FZ_LAUNCH_CHECK();
+    }
+    scan_exclusive_i64(c, keep, pos, NI, d_nm);
+
+    // phase 2: iteration of each kept match; distinct (iteration, project) (:213-230)
+    int64_t *it_arr = c->arena.get<int64_t>(NI);
+    uint32_t *p_arr = c->arena.get<uint32_t>(NI);
+    if (NI > 0) {
+        const unsigned g = grid_for(NI, kBlock, 2048);
+        k_matched_out<<<g, kBlock, 0, st>>>(s.issues, keep, pos, mbuild, s.fuzz, o->matched_issue, o->matched_build,
+                                            it_arr, p_arr, f_match);
+        k_distinct_iter<<<g, kBlock, 0, st>>>(it_arr, p_arr, d_nm, o->iter_detected);
+        FZ_LAUNCH_CHECK();
+    }
+    if (P > 0) {
+        count_flags(c, f_lim, P, o->counts + FZ_RQ1_ISSUES_LIM_PROJECTS);
+        count_flags(c, f_fixlim, P, o->counts + FZ_RQ1_FIXED_LIM_PROJECTS);
+        count_flags(c, f_tgt, P, o->counts + FZ_RQ1_TARGET_PROJECTS);
+        count_flags(c, f_match, P, o->counts + FZ_RQ1_MATCHED_PROJECTS);
+    }
+
+    // finalize (:233-268)
+    double *rates = c->arena.get<double>(M);
+    double *late = c->arena.get<double>(M);
+    int64_t *late_lo = c->arena.get<int64_t>(2);
+    if (M > 0) {
+        k_rates<<<grid_for(M), kBlock, 0, st>>>(o->iter_total, o->iter_detected, M, threshold, o->counts, rates);
+        FZ_LAUNCH_CHECK();
+    }
+    k_late_bounds<<<1, 64, 0, st>>>(o->counts, late_lo);
+    k_late_copy<<<grid_for(M > 0 ? M : 1), kBlock, 0, st>>>(rates, late_lo, late);
+    FZ_LAUNCH_CHECK();
+    describe_f64_dn(c, late, M, late_lo + 1, o->late);
+}
+
+}  // namespace fz

@@ -1,0 +1,220 @@
+// The columnar store: replaces the PostgreSQL tables + (project, time) indexes every RQ query
+// scans through dbFile.DB.executeQuery (program/__module/dbFile.py:16-24).
+//
+// fz_store_build sorts each table once with the stable LSD radix sort (fz_prims.hip) on a packed
+// key (build_type | project | time - tmin), NULL timestamps mapped past the maximum so they sort
+// last within their project (PostgreSQL's ASC NULLS LAST).  When the packed key would exceed
+// 64 bits the sort runs in two stable stages (time, then prefix) - LSD order makes that exact.
+#include "fz_device.h"
+#include "fz_internal.h"
+#include "fz_views.h"
+
+namespace fz {
+
+struct Prefix {
+    const uint32_t *proj;
+    const uint8_t *type;  // null: prefix = project only
+    int pbits;
+    __device__ uint64_t operator()(int64_t r) const {
+        uint64_t p = proj[r];
+        if (type) {
+            uint64_t t = type[r] > 1 ? 2u : type[r];  // Fuzzing, Coverage, any other type last
+            p |= t << pbits;
+        }
+        return p;
+    }
+};
+
+__global__ __launch_bounds__(kBlock) void k_keys_full(Prefix pre, const int64_t *__restrict__ time, int64_t n,
+                                                      int64_t tmin, uint64_t tnull, int tbits,
+                                                      uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const int64_t t = time[i];
+        const uint64_t tn = t == FZ_TS_NULL ? tnull : uint64_t(t - tmin);
+        keys[i] = (tbits < 64 ? (pre(i) << tbits) : 0ull) | tn;
+        vals[i] = uint32_t(i);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_keys_time(const int64_t *__restrict__ time, int64_t n, int64_t tmin,
+                                                      uint64_t tnull, uint64_t *__restrict__ keys,
+                                                      uint32_t *__restrict__ vals) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const int64_t t = time[i];
+        keys[i] = t == FZ_TS_NULL ? tnull : uint64_t(t - tmin);
+        vals[i] = uint32_t(i);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_keys_prefix(Prefix pre, const uint32_t *__restrict__ vals, int64_t n,
+                                                        uint64_t *__restrict__ keys) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+        keys[i] = pre(vals[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_gather_sorted(const uint32_t *__restrict__ vals,
+                                                          const int64_t *__restrict__ time,
+                                                          const uint32_t *__restrict__ proj, int64_t n,
+                                                          int32_t *__restrict__ orow, int64_t *__restrict__ otime,
+                                                          uint32_t *__restrict__ oproj) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const uint32_t r = vals[i];
+        orow[i] = int32_t(r);
+        otime[i] = time[r];
+        oproj[i] = proj[r];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_count_types(const uint8_t *__restrict__ type, int64_t n,
+                                                        unsigned long long *__restrict__ cnt) {
+    __shared__ int64_t s_tmp[4];
+    int64_t a = 0, b = 0;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        a += type[i] == 0;
+        b += type[i] == 1;
+    }
+    a = block_sum(a, s_tmp);
+    b = block_sum(b, s_tmp);
+    if (threadIdx.x == 0) {
+        atomicAdd(&cnt[0], (unsigned long long)a);
+        atomicAdd(&cnt[1], (unsigned long long)b);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_max_seg(const int64_t *__restrict__ offs, int64_t P,
+                                                    unsigned long long *__restrict__ out) {
+    int64_t m = 0;
+    for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < P; p += int64_t(gridDim.x) * kBlock) {
+        const int64_t l = offs[p + 1] - offs[p];
+        m = l > m ? l : m;
+    }
+    m = wave_max(m);
+    if (lane_id() == 0) atomicMax(out, (unsigned long long)m);
+}
+
+// Sort one table into (row, time, proj) buffers.
+static void sort_table(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time, int64_t tmin,
+                       int64_t tmax, int32_t *orow, int64_t *otime, uint32_t *oproj) {
+    if (n <= 0) return;
+    const uint64_t range = tmax >= tmin ? uint64_t(tmax - tmin) : 0ull;
+    const uint64_t tnull = range + 1;  // NULLs after every real time
+    const int tbits = bits_for(tnull);
+    uint64_t *keys = c->arena.get<uint64_t>(n);
+    uint32_t *vals = c->arena.get<uint32_t>(n);
+    const unsigned g = grid_for(n, kBlock, 4096);
+    if (prefix_bits + tbits <= 64) {
+        k_keys_full<<<g, kBlock, 0, c->stream>>>(pre, time, n, tmin, tnull, tbits, keys, vals);
+        FZ_LAUNCH_CHECK();
+        radix_sort_pairs(c, keys, vals, n, prefix_bits + tbits);
+    } else {
+        k_keys_time<<<g, kBlock, 0, c->stream>>>(time, n, tmin, tnull, keys, vals);
+        FZ_LAUNCH_CHECK();
+        radix_sort_pairs(c, keys, vals, n, tbits);
+        k_keys_prefix<<<g, kBlock, 0, c->stream>>>(pre, vals, n, keys);
+        FZ_LAUNCH_CHECK();
+        radix_sort_pairs(c, keys, vals, n, prefix_bits);
+    }
+    k_gather_sorted<<<g, kBlock, 0, c->stream>>>(vals, time, pre.proj, n, orow, otime, oproj);
+    FZ_LAUNCH_CHECK();
+}
+
+static View make_view(fz_ctx *c, const int32_t *row, const int64_t *time, const uint32_t *proj, int64_t n, int64_t P,
+                      DevBuf &offbuf) {
+    View v;
+    v.n = n;
+    v.row = row;
+    v.time = time;
+    v.proj = proj;
+    int64_t *offs = offbuf.ensure<int64_t>(P + 1);
+    segment_offsets(c, proj, n, P, offs);
+    v.offs = offs;
+    return v;
+}
+
+void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
+    FZ_CHECK(t != nullptr, "fz_store_build: tables is null");
+    FZ_CHECK(t->n_projects >= 0 && t->n_builds >= 0 && t->n_cov >= 0 && t->n_issues >= 0, "negative table size");
+    FZ_CHECK(t->n_builds < (int64_t(1) << 31) && t->n_cov < (int64_t(1) << 31) && t->n_issues < (int64_t(1) << 31),
+             "tables are limited to 2^31 rows per shard");
+    Store &s = c->store;
+    s.built = false;
+    s.t = *t;
+    s.P = t->n_projects;
+    s.passes = 0;
+    const int64_t P = s.P;
+    const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
+
+    // one host round trip: time ranges of the three tables + build-type counts
+    int64_t mm[6];
+    const int64_t *cols[3] = {t->b_time, t->c_date, t->i_rts};
+    const int64_t ns[3] = {t->n_builds, t->n_cov, t->n_issues};
+    unsigned long long *tcnt = c->arena.get<unsigned long long>(2);
+    FZ_HIP(hipMemsetAsync(tcnt, 0, 16, c->stream));
+    if (t->n_builds > 0) {
+        k_count_types<<<grid_for(t->n_builds, kBlock, 1024), kBlock, 0, c->stream>>>(t->b_type, t->n_builds, tcnt);
+        FZ_LAUNCH_CHECK();
+    }
+    minmax_i64_to_host(c, cols, ns, 3, mm);  // syncs the stream
+    unsigned long long hcnt[2];
+    FZ_HIP(hipMemcpy(hcnt, tcnt, 16, hipMemcpyDeviceToHost));
+    const int64_t n_fuzz = int64_t(hcnt[0]), n_covb = int64_t(hcnt[1]);
+    for (int i = 0; i < 3; ++i) {
+        s.tmin[i] = mm[2 * i];
+        s.tmax[i] = mm[2 * i + 1];
+    }
+
+    // buildlog_data by (type, project, time)
+    {
+        const int64_t n = t->n_builds;
+        int32_t *row = s.b_row.ensure<int32_t>(n);
+        int64_t *tm = s.b_time.ensure<int64_t>(n);
+        uint32_t *pr = s.b_proj.ensure<uint32_t>(n);
+        sort_table(c, n, Prefix{t->b_project, t->b_type, pbits}, pbits + 2, t->b_time, mm[0], mm[1], row, tm, pr);
+        s.fuzz = make_view(c, row, tm, pr, n_fuzz, P, s.off_fuzz);
+        s.covb = make_view(c, row + n_fuzz, tm + n_fuzz, pr + n_fuzz, n_covb, P, s.off_covb);
+    }
+    // total_coverage by (project, date)
+    {
+        const int64_t n = t->n_cov;
+        int32_t *row = s.c_row.ensure<int32_t>(n);
+        int64_t *tm = s.c_time.ensure<int64_t>(n);
+        uint32_t *pr = s.c_proj.ensure<uint32_t>(n);
+        sort_table(c, n, Prefix{t->c_project, nullptr, pbits}, pbits, t->c_date, mm[2], mm[3], row, tm, pr);
+        s.cov = make_view(c, row, tm, pr, n, P, s.off_cov);
+    }
+    // issues by (project, rts)
+    {
+        const int64_t n = t->n_issues;
+        int32_t *row = s.i_row.ensure<int32_t>(n);
+        int64_t *tm = s.i_time.ensure<int64_t>(n);
+        uint32_t *pr = s.i_proj.ensure<uint32_t>(n);
+        sort_table(c, n, Prefix{t->i_project, nullptr, pbits}, pbits, t->i_rts, mm[4], mm[5], row, tm, pr);
+        s.issues = make_view(c, row, tm, pr, n, P, s.off_iss);
+    }
+    // longest segments (sizes the per-iteration outputs)
+    unsigned long long *mx = c->arena.get<unsigned long long>(4);
+    FZ_HIP(hipMemsetAsync(mx, 0, 32, c->stream));
+    const View *vs[4] = {&s.fuzz, &s.covb, &s.cov, &s.issues};
+    for (int i = 0; i < 4; ++i) {
+        if (P <= 0) break;
+        k_max_seg<<<grid_for(P, kBlock, 64), kBlock, 0, c->stream>>>(vs[i]->offs, P, mx + i);
+        FZ_LAUNCH_CHECK();
+    }
+    FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 32, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    s.fuzz.max_seg = c->h_pinned[0];
+    s.covb.max_seg = c->h_pinned[1];
+    s.cov.max_seg = c->h_pinned[2];
+    s.issues.max_seg = c->h_pinned[3];
+    s.built = true;
+    if (stats) {
+        stats->n_projects = P;
+        stats->n_fuzz = n_fuzz;
+        stats->n_coverage_builds = n_covb;
+        stats->max_fuzz_per_project = s.fuzz.max_seg;
+        stats->max_cov_per_project = s.cov.max_seg;
+        stats->sort_passes = s.passes;
+    }
+}
+
+}  // namespace fz

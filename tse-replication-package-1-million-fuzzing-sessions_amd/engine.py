@@ -1,0 +1,242 @@
+"""ctypes binding of ``libfz.so`` (C ABI: ``include/fz.h``) and the device-resident tables.
+
+This is the drop-in for ``program/__module/dbFile.py:5-38`` (``DB.connect`` /
+``DB.executeQuery``): instead of one SQL round trip per project, the columnar tables are
+uploaded to HBM once (``DeviceTables``), sorted once into the store (``Engine.build_store``,
+the replacement for PostgreSQL's tables + indexes) and every RQ computation runs as HIP
+kernels over it.  PyTorch-ROCm is used only to allocate device buffers and to provide the
+stream; all compute goes through ``libfz``.  There is no CPU fallback: without the built
+library or without a GPU every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import LIB_PATH
+from .schema import Tables
+
+FZ_RQ1_NCOUNTS = 16
+(RQ1_ISSUES_LIM, RQ1_ISSUES_LIM_PROJECTS, RQ1_FIXED_LIM, RQ1_FIXED_LIM_PROJECTS, RQ1_ELIGIBLE,
+ RQ1_WITHOUT_MATCHING, RQ1_TARGET, RQ1_TARGET_PROJECTS, RQ1_TOTAL_FUZZ, RQ1_MATCHED,
+ RQ1_MATCHED_PROJECTS, RQ1_MAX_ITER, RQ1_KEPT_ITERS, RQ1_FIRST_DOWN, RQ1_LATE) = range(15)
+
+VALID_COVERAGE, VALID_COVERED, VALID_TOTAL = 1, 2, 4
+
+_P = C.c_void_p
+_I64 = C.c_int64
+
+
+class FzTables(C.Structure):
+    _fields_ = [("n_projects", _I64),
+                ("n_builds", _I64), ("b_project", _P), ("b_type", _P), ("b_result", _P), ("b_time", _P),
+                ("b_group", _P), ("b_rev_canon", _P),
+                ("n_cov", _I64), ("c_project", _P), ("c_date", _P), ("c_coverage", _P), ("c_covered", _P),
+                ("c_total", _P), ("c_valid", _P),
+                ("n_issues", _I64), ("i_number", _P), ("i_project", _P), ("i_rts", _P), ("i_status", _P),
+                ("pi_count", _P)]
+
+
+class FzStoreStats(C.Structure):
+    _fields_ = [("n_projects", _I64), ("n_fuzz", _I64), ("n_coverage_builds", _I64),
+                ("max_fuzz_per_project", _I64), ("max_cov_per_project", _I64), ("sort_passes", _I64)]
+
+
+class FzDescribe(C.Structure):
+    _fields_ = [("count", _I64), ("n_pos", _I64), ("n_zero", _I64), ("n_neg", _I64),
+                ("mean", C.c_double), ("median", C.c_double), ("std", C.c_double), ("min", C.c_double),
+                ("max", C.c_double), ("q1", C.c_double), ("q3", C.c_double), ("min_nonzero", C.c_double),
+                ("has_nonzero", _I64)]
+
+
+DESCRIBE_DOUBLES = 13  # sizeof(fz_describe) / 8
+
+
+class FzRq1Out(C.Structure):
+    _fields_ = [("counts", _P), ("eligible", _P), ("iter_total", _P), ("iter_detected", _P),
+                ("matched_issue", _P), ("matched_build", _P), ("late", _P)]
+
+
+# every symbol include/fz.h declares, with its ctypes signature
+SIGNATURES = {
+    "fz_abi_version": (C.c_int, []),
+    "fz_last_error": (C.c_char_p, []),
+    "fz_ctx_create": (C.c_int, [C.c_int, _P, C.POINTER(_P)]),
+    "fz_ctx_destroy": (C.c_int, [_P]),
+    "fz_ctx_set_stream": (C.c_int, [_P, _P]),
+    "fz_store_build": (C.c_int, [_P, C.POINTER(FzTables), C.POINTER(FzStoreStats)]),
+    "fz_rq1": (C.c_int, [_P, _I64, C.POINTER(FzRq1Out)]),
+    "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),
+    "fz_probe_end": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "fz_radix_sort_u64": (C.c_int, [_P, _P, _P, _I64, C.c_int]),
+    "fz_describe_f64": (C.c_int, [_P, _P, _I64, C.POINTER(FzDescribe)]),
+    "fz_eligibility_count": (C.c_int, [_P, C.POINTER(FzTables), _I64, _P]),
+}
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """dlopen libfz and bind every exported symbol (works without a GPU: no HIP call is made)."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libfz not built: {path} is missing (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.fz_abi_version() != 1:
+        raise RuntimeError("libfz ABI version mismatch")
+    if path == LIB_PATH:
+        _lib = lib
+    return lib
+
+
+class FzError(RuntimeError):
+    pass
+
+
+def _check(lib, rc):
+    if rc != 0:
+        raise FzError(f"libfz error {rc}: {lib.fz_last_error().decode(errors='replace')}")
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("the fz engine needs a ROCm GPU (torch.cuda.is_available() is False); "
+                           "there is no CPU fallback - use oracle/ only as a test checker")
+    return torch
+
+
+@dataclass
+class DeviceTables:
+    """The four session tables as device columns (HBM), plus the host ``Tables`` they came from
+    (text pools stay on the host: the renderer needs them, the kernels never do)."""
+    host: Tables
+    cols: dict
+    fz: FzTables
+
+    @property
+    def n_rows(self):
+        return self.host.n_rows
+
+
+def _pin(t):
+    return t.pin_memory() if t.numel() > 0 else t
+
+
+class Engine:
+    """One engine per GPU: a ``fz_ctx`` bound to torch's current stream on ``device``."""
+
+    def __init__(self, device: int = 0, lib_path: str = LIB_PATH):
+        self.torch = _torch()
+        self.lib = load_library(lib_path)
+        self.device = device
+        self.dev = self.torch.device("cuda", device)
+        self.stream = self.torch.cuda.current_stream(self.dev)
+        ctx = _P()
+        _check(self.lib, self.lib.fz_ctx_create(device, _P(self.stream.cuda_stream), C.byref(ctx)))
+        self.ctx = ctx
+        self.tables: Optional[DeviceTables] = None
+        self.stats: Optional[FzStoreStats] = None
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.fz_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- columnar loader: host columns -> HBM -------------------------------------------------
+    def upload(self, t: Tables) -> DeviceTables:
+        """Stream the typed columns to HBM (pinned host staging, async copies on our stream)."""
+        torch = self.torch
+        P = len(t.projects)
+        c_valid = (t.c_coverage_valid.astype(np.uint8) * VALID_COVERAGE
+                   | t.c_covered_valid.astype(np.uint8) * VALID_COVERED
+                   | t.c_total_valid.astype(np.uint8) * VALID_TOTAL)
+        pi_count = np.bincount(t.pi_project.astype(np.int64), minlength=P).astype(np.int32)
+        host = {
+            "b_project": t.b_project.view(np.int32), "b_type": t.b_type, "b_result": t.b_result,
+            "b_time": t.b_time, "b_group": t.group_key().astype(np.int32),
+            "b_rev_canon": t.rev_canon().astype(np.int32),
+            "c_project": t.c_project.view(np.int32), "c_date": t.c_date, "c_coverage": t.c_coverage,
+            "c_covered": t.c_covered, "c_total": t.c_total, "c_valid": c_valid,
+            "i_number": t.i_number, "i_project": t.i_project.view(np.int32), "i_rts": t.i_rts,
+            "i_status": t.i_status, "pi_count": pi_count,
+        }
+        cols = {}
+        with torch.cuda.stream(self.stream):
+            for k, a in host.items():
+                h = _pin(torch.from_numpy(np.ascontiguousarray(a)))
+                cols[k] = h.to(self.dev, non_blocking=True)
+        ptr = {k: _P(v.data_ptr()) for k, v in cols.items()}
+        fz = FzTables(n_projects=P, n_builds=len(t.b_project), n_cov=len(t.c_project), n_issues=len(t.i_project),
+                      **ptr)
+        self.tables = DeviceTables(host=t, cols=cols, fz=fz)
+        return self.tables
+
+    # ---- store ---------------------------------------------------------------------------------
+    def build_store(self, dt: Optional[DeviceTables] = None) -> FzStoreStats:
+        dt = dt or self.tables
+        if dt is None:
+            raise FzError("no tables uploaded")
+        st = FzStoreStats()
+        _check(self.lib, self.lib.fz_store_build(self.ctx, C.byref(dt.fz), C.byref(st)))
+        self.tables = dt
+        self.stats = st
+        return st
+
+    # ---- helpers ------------------------------------------------------------------------------
+    def empty(self, n, dtype):
+        return self.torch.empty(max(int(n), 1), dtype=dtype, device=self.dev)
+
+    def zeros(self, n, dtype):
+        return self.torch.zeros(max(int(n), 1), dtype=dtype, device=self.dev)
+
+    def synchronize(self):
+        self.stream.synchronize()
+
+    def radix_sort(self, keys, vals=None, bits=64):
+        n = keys.numel()
+        _check(self.lib, self.lib.fz_radix_sort_u64(self.ctx, _P(keys.data_ptr()),
+                                                   _P(vals.data_ptr()) if vals is not None else None, n, bits))
+
+    def probe_begin(self, kernel: str):
+        _check(self.lib, self.lib.fz_probe_begin(self.ctx, kernel.encode()))
+
+    def probe_end(self):
+        """-> (launches, total device ms, algorithmic bytes) of the probed kernel."""
+        n, ms, b = _I64(), C.c_double(), C.c_double()
+        _check(self.lib, self.lib.fz_probe_end(self.ctx, C.byref(n), C.byref(ms), C.byref(b)))
+        return int(n.value), float(ms.value), float(b.value)
+
+    def describe(self, x):
+        d = FzDescribe()
+        _check(self.lib, self.lib.fz_describe_f64(self.ctx, _P(x.data_ptr()), x.numel(), C.byref(d)))
+        return d
+
+    def eligibility_counts(self, limit_us):
+        out = self.zeros(self.tables.fz.n_projects, self.torch.int32)
+        _check(self.lib, self.lib.fz_eligibility_count(self.ctx, C.byref(self.tables.fz), limit_us,
+                                                      _P(out.data_ptr())))
+        return out
+
+
+def describe_from_doubles(a: np.ndarray):
+    """fz_describe laid out as 13 x 8 bytes -> field dict."""
+    b = np.asarray(a).view(np.uint8).tobytes()
+    d = FzDescribe.from_buffer_copy(b[:C.sizeof(FzDescribe)])
+    return d
