@@ -215,9 +215,21 @@ __global__ __launch_bounds__(kBlock) void k_minmax(const int64_t *__restrict__ x
         lo = v < lo ? v : lo;
         hi = v > hi ? v : hi;
     }
+    __shared__ int64_t s_lo[4], s_hi[4];
     lo = wave_min(lo);
     hi = wave_max(hi);
     if (lane_id() == 0) {
+        s_lo[wave_id()] = lo;
+        s_hi[wave_id()] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < 4; ++i) {
+            lo = s_lo[i] < lo ? s_lo[i] : lo;
+            hi = s_hi[i] > hi ? s_hi[i] : hi;
+        }
+        lo = s_lo[0] < lo ? s_lo[0] : lo;
+        hi = s_hi[0] > hi ? s_hi[0] : hi;
         // order-preserving unsigned images so one unsigned atomic min/max covers negatives too
         atomicMin(&mm[0], (unsigned long long)(lo) ^ 0x8000000000000000ull);
         atomicMax(&mm[1], (unsigned long long)(hi) ^ 0x8000000000000000ull);
@@ -234,7 +246,7 @@ void minmax_i64_to_host(fz_ctx *c, const int64_t *const *cols, const int64_t *ns
     FZ_HIP(hipMemcpyAsync(mm, init.data(), init.size() * 8, hipMemcpyHostToDevice, c->stream));
     for (int i = 0; i < ncols; ++i) {
         if (ns[i] <= 0) continue;
-        k_minmax<<<grid_for(ns[i], kBlock, 1024), kBlock, 0, c->stream>>>(cols[i], ns[i], mm + 2 * i);
+        k_minmax<<<grid_for(ns[i], kBlock * 8, 512), kBlock, 0, c->stream>>>(cols[i], ns[i], mm + 2 * i);
         FZ_LAUNCH_CHECK();
     }
     FZ_HIP(hipMemcpyAsync(c->h_pinned, mm, 2 * ncols * 8, hipMemcpyDeviceToHost, c->stream));

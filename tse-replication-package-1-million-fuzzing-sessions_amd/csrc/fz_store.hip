@@ -65,6 +65,22 @@ __global__ __launch_bounds__(kBlock) void k_gather_sorted(const uint32_t *__rest
     }
 }
 
+// Single-stage sorts carry (project, time) in the key: unpack instead of gathering by row id.
+__global__ __launch_bounds__(kBlock) void k_unpack_sorted(const uint64_t *__restrict__ keys,
+                                                          const uint32_t *__restrict__ vals, int64_t n, int tbits,
+                                                          int64_t tmin, uint64_t tnull, uint64_t pmask,
+                                                          int32_t *__restrict__ orow, int64_t *__restrict__ otime,
+                                                          uint32_t *__restrict__ oproj) {
+    const uint64_t tmask = tbits >= 64 ? ~0ull : ((1ull << tbits) - 1ull);
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const uint64_t k = keys[i];
+        const uint64_t tn = k & tmask;
+        orow[i] = int32_t(vals[i]);
+        otime[i] = tn == tnull ? FZ_TS_NULL : int64_t(tn) + tmin;
+        oproj[i] = tbits >= 64 ? 0u : uint32_t((k >> tbits) & pmask);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_count_types(const uint8_t *__restrict__ type, int64_t n,
                                                         unsigned long long *__restrict__ cnt) {
     __shared__ int64_t s_tmp[4];
@@ -106,6 +122,10 @@ static void sort_table(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const 
         k_keys_full<<<g, kBlock, 0, c->stream>>>(pre, time, n, tmin, tnull, tbits, keys, vals);
         FZ_LAUNCH_CHECK();
         radix_sort_pairs(c, keys, vals, n, prefix_bits + tbits);
+        const uint64_t pmask = pre.pbits >= 32 ? 0xffffffffull : ((1ull << pre.pbits) - 1ull);
+        k_unpack_sorted<<<g, kBlock, 0, c->stream>>>(keys, vals, n, tbits, tmin, tnull, pmask, orow, otime, oproj);
+        FZ_LAUNCH_CHECK();
+        return;
     } else {
         k_keys_time<<<g, kBlock, 0, c->stream>>>(time, n, tmin, tnull, keys, vals);
         FZ_LAUNCH_CHECK();
@@ -151,7 +171,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     unsigned long long *tcnt = c->arena.get<unsigned long long>(2);
     FZ_HIP(hipMemsetAsync(tcnt, 0, 16, c->stream));
     if (t->n_builds > 0) {
-        k_count_types<<<grid_for(t->n_builds, kBlock, 1024), kBlock, 0, c->stream>>>(t->b_type, t->n_builds, tcnt);
+        k_count_types<<<grid_for(t->n_builds, kBlock * 8, 512), kBlock, 0, c->stream>>>(t->b_type, t->n_builds, tcnt);
         FZ_LAUNCH_CHECK();
     }
     minmax_i64_to_host(c, cols, ns, 3, mm);  // syncs the stream

@@ -51,7 +51,10 @@ def rq1_collect(eng: E.Engine, bufs: RQ1Buffers, threshold: int = 100) -> RQ1Res
     M = int(cnt[E.RQ1_MAX_ITER])
     late = None
     if cnt[E.RQ1_LATE] > 0:
-        late = _describe(E.describe_from_doubles(bufs.late.cpu().numpy()), with_min_nonzero=True)
+        d = _describe(E.describe_from_doubles(bufs.late.cpu().numpy()), with_min_nonzero=True)
+        # rq1_detection_rate.py:256-268 reports only these numbers (no sign split, no std)
+        late = Describe(count=d.count, n_zero=d.n_zero, min=d.min, max=d.max, q1=d.q1, q3=d.q3,
+                        median=d.median, mean=d.mean, min_nonzero=d.min_nonzero)
     elig = np.nonzero(bufs.eligible.cpu().numpy()[:eng.tables.fz.n_projects])[0]
     return RQ1Result(
         n_issues_lim=int(cnt[E.RQ1_ISSUES_LIM]), n_issues_lim_projects=int(cnt[E.RQ1_ISSUES_LIM_PROJECTS]),
