@@ -146,6 +146,61 @@ typedef struct fz_rq1_out {
 
 int fz_rq1(fz_ctx *ctx, int64_t min_project_threshold, const fz_rq1_out *out);
 
+/* ---- RQ2 (count): rq2_coverage_count.py:244-483 ------------------------------------------ */
+enum {
+    FZ_RQ2C_ELIGIBLE = 0,   /* eligible projects                                     :272-280 */
+    FZ_RQ2C_SESSIONS,       /* len(coverage_by_session_index) = max(1, longest trend)  :285,330 */
+    FZ_RQ2C_GE100,          /* sessions with >= 100 values (a prefix)                  :390 */
+    FZ_RQ2C_VALUES,         /* trend values over all projects                          :300-303 */
+    FZ_RQ2C_NCOUNTS = 8
+};
+enum {
+    FZ_RQ2C_CORR_MEAN = 0,  /* np.mean / np.median of the valid per-project Spearman rho :356-361 */
+    FZ_RQ2C_CORR_MEDIAN,
+    FZ_RQ2C_SP_RHO,         /* spearmanr(range(K), median_trend)                       :443-445 */
+    FZ_RQ2C_SP_P,
+    FZ_RQ2C_SW_MEDIAN_P,    /* shapiro(median_trend).pvalue                            :449-458 */
+    FZ_RQ2C_NSCALARS = 8
+};
+typedef struct fz_rq2_count_out {
+    int64_t *counts;            /* [FZ_RQ2C_NCOUNTS] */
+    double *scalars;            /* [FZ_RQ2C_NSCALARS] */
+    uint8_t *eligible;          /* [n_projects] */
+    int64_t *raw_n;             /* [n_projects] rows fetched per project (queries1.py:120-129) */
+    int64_t *n_trend;           /* [n_projects] values after `total_line != 0` */
+    double *sw_w, *sw_p;        /* [n_projects] Shapiro-Wilk (NaN when n < 3)              :305-314 */
+    double *corr;               /* [n_projects] Spearman vs index (NaN when undefined)     :316-322 */
+    int64_t *session_offsets;   /* [max_cov_per_project + 2] CSR of coverage_by_session_index */
+    double *session_values;     /* [n_cov] */
+    double *average_trend;      /* [max_cov_per_project] statistics.mean per session       :439 */
+    double *median_trend;       /* [max_cov_per_project] statistics.median per session     :440 */
+    double *dist_percentiles;   /* [max_cov_per_project * 5] np.percentile 5/25/50/75/95   :139-152 */
+    double *dist_mean;          /* [max_cov_per_project] np.mean per session */
+} fz_rq2_count_out;
+
+int fz_rq2_count(fz_ctx *ctx, const fz_rq2_count_out *out);
+
+/* ---- RQ2/RQ3 support (add): rq2_coverage_and_added.py:73-238 ------------------------------- */
+enum { FZ_RQ2A_ELIGIBLE = 0, FZ_RQ2A_ROWS, FZ_RQ2A_RUNS, FZ_RQ2A_NCOUNTS = 4 };
+typedef struct fz_rq2_add_out {
+    int64_t *counts;            /* [FZ_RQ2A_NCOUNTS] */
+    uint8_t *eligible;          /* [n_projects] */
+    /* one row per pair of consecutive (modules, revisions) runs, ORDER BY project, time; capacity
+     * n_coverage_builds */
+    int64_t *row_project;
+    int64_t *row_first_build;   /* first build of run i (modules_i / revisions_i)            :135-149 */
+    int64_t *row_end_build;     /* last build of run i (timecreated_i)                               */
+    int64_t *row_start_build;   /* first build of run i+1                                            */
+    int64_t *row_cov_i;         /* coverage row on date(end of run i), -1 none               :170-184 */
+    int64_t *row_cov_i1;        /* coverage row on date(start of run i+1)                            */
+    double *diff_total;         /* t1 - t0 (NaN unless both totals valid and != 0)           :189-200 */
+    double *diff_coverage;      /* c1/t1*100 - c0/t0*100                                             */
+    uint8_t *covered_is_float;  /* [n_projects] pandas upcast: a NULL covered_line in the project    */
+    uint8_t *total_is_float;    /* [n_projects]                                                      */
+} fz_rq2_add_out;
+
+int fz_rq2_add(fz_ctx *ctx, const fz_rq2_add_out *out);
+
 /* ---- per-kernel probe (bench.py roofline) ------------------------------------------------ */
 /* Start timing every launch of the named kernel (e.g. "radix_scatter", "elig_hist") with HIP
  * events on the context stream; fz_probe_end synchronises the stream and returns the number of

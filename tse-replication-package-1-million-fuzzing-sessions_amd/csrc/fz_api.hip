@@ -10,6 +10,8 @@ namespace fz {
 void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats);
 void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_out *o);
 void eligibility_counts(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *counts);
+void rq2_count(fz_ctx *c, const fz_rq2_count_out *o);
+void rq2_add(fz_ctx *c, const fz_rq2_add_out *o);
 }  // namespace fz
 
 namespace {
@@ -89,6 +91,14 @@ int fz_store_build(fz_ctx *ctx, const fz_tables *t, fz_store_stats *stats) {
 
 int fz_rq1(fz_ctx *ctx, int64_t min_project_threshold, const fz_rq1_out *out) {
     return guarded(ctx, [&] { fz::rq1(ctx, min_project_threshold, out); });
+}
+
+int fz_rq2_count(fz_ctx *ctx, const fz_rq2_count_out *out) {
+    return guarded(ctx, [&] { fz::rq2_count(ctx, out); });
+}
+
+int fz_rq2_add(fz_ctx *ctx, const fz_rq2_add_out *out) {
+    return guarded(ctx, [&] { fz::rq2_add(ctx, out); });
 }
 
 int fz_probe_begin(fz_ctx *ctx, const char *kernel_name) {

@@ -67,6 +67,20 @@ __global__ __launch_bounds__(kBlock) void k_elig_flags(const int32_t *__restrict
     }
 }
 
+// elig[p] = project has >= 365 qualifying coverage rows; *d_count += number eligible.
+// Every RQ script starts from this set (rq1:144-152, rq2_count:272-280, rq2_add:20-27, rq3:222-226,
+// rq4a:68-80, rq4b:164-181 - the same GROUP BY/HAVING).
+void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count) {
+    const fz_tables &t = c->store.t;
+    const int64_t P = t.n_projects;
+    int32_t *ecount = c->arena.get<int32_t>(P);
+    eligibility_counts(c, &t, kLimitUs, ecount);
+    if (P > 0) {
+        k_elig_flags<<<grid_for(P), kBlock, 0, c->stream>>>(ecount, P, elig, d_count);
+        FZ_LAUNCH_CHECK();
+    }
+}
+
 // Histogram of Fuzzing-build counts over eligible projects; total and max.
 __global__ __launch_bounds__(kBlock) void k_iter_hist(const int64_t *__restrict__ offs, const uint8_t *__restrict__ elig,
                                                       int64_t P, int64_t *__restrict__ hist,
@@ -273,12 +287,7 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_out *o) {
     FZ_HIP(hipMemsetAsync(o->iter_detected, 0, size_t(M > 0 ? M : 1) * 8, st));
 
     // eligibility (:144-152)
-    int32_t *ecount = c->arena.get<int32_t>(P);
-    eligibility_counts(c, &t, kLimitUs, ecount);
-    if (P > 0) {
-        k_elig_flags<<<grid_for(P), kBlock, 0, st>>>(ecount, P, o->eligible, o->counts + FZ_RQ1_ELIGIBLE);
-        FZ_LAUNCH_CHECK();
-    }
+    eligible_projects(c, o->eligible, o->counts + FZ_RQ1_ELIGIBLE);
 
     // phase 1: projects alive at each iteration (:189-203)
     int64_t *hist = c->arena.get<int64_t>(M + 1);

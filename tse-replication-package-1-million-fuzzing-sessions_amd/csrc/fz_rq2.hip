@@ -1,0 +1,309 @@
+// RQ2 - coverage trends per project and per session index (rq2_coverage_count.py:244-483).
+//
+//   878 x GET_TOTAL_COVERAGE_EACH_PROJECT (queries1.py:120-129) -> one filtered view of the
+//        (project, date)-sorted coverage store
+//   trend = covered/total*100 (:300-303)                         -> elementwise fp64
+//   shapiro / spearmanr per project (:305-322)                   -> segmented sort + tie ranks +
+//        chunked segmented reductions (fz_series.hip)
+//   coverage_by_session_index transpose (:330-333)               -> radix sort on (index, project)
+//   per-session mean/median/percentiles (:139-152, :439-440)     -> segmented sort per session
+//   spearman/shapiro of the median trend (:443-458)              -> the same kernels, one segment
+#include "fz_seg.h"
+#include "fz_stats.h"
+
+namespace fz {
+
+constexpr int64_t kLimitUs2 = 1736294400000000LL;  // '2025-01-08'
+
+void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count);
+
+struct CovTrendRows {  // coverage IS NOT NULL AND coverage != 0 AND DATE(date) < LIMIT, eligible only
+    const uint32_t *proj;
+    const double *cov;
+    const uint8_t *valid;
+    const int64_t *date;
+    const uint8_t *elig;
+    __device__ bool operator()(int32_t r) const {
+        return (valid[r] & FZ_VALID_COVERAGE) && cov[r] != 0.0 && date[r] < kLimitUs2 && elig[proj[r]];
+    }
+};
+struct NonZeroTotal {  // `if total != 0` (:300-303)
+    const int64_t *total;
+    __device__ bool operator()(int32_t r) const { return total[r] != 0; }
+};
+
+void rq2_count(fz_ctx *c, const fz_rq2_count_out *o) {
+    Store &s = c->store;
+    FZ_CHECK(s.built, "fz_rq2_count: call fz_store_build first");
+    FZ_CHECK(o && o->counts && o->scalars && o->eligible && o->raw_n && o->n_trend && o->sw_w && o->sw_p && o->corr &&
+                 o->session_offsets && o->session_values && o->average_trend && o->median_trend &&
+                 o->dist_percentiles && o->dist_mean,
+             "fz_rq2_count: null output buffer");
+    const fz_tables &t = s.t;
+    const int64_t P = s.P;
+    const int64_t M = s.cov.max_seg;  // longest possible trend
+    const int64_t NC = s.cov.n;
+    hipStream_t st = c->stream;
+    FZ_HIP(hipMemsetAsync(o->counts, 0, FZ_RQ2C_NCOUNTS * 8, st));
+
+    eligible_projects(c, o->eligible, o->counts + FZ_RQ2C_ELIGIBLE);
+    TmpView V, T;
+    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P,
+                CovTrendRows{t.c_project, t.c_coverage, t.c_valid, t.c_date, o->eligible}, V);
+    filter_view(c, V.row, V.time, V.proj, NC, P, NonZeroTotal{t.c_total}, T);
+
+    int64_t *counts = o->counts;
+    int64_t *raw_n = o->raw_n, *n_trend = o->n_trend;
+    const int64_t *voffs = V.offs, *toffs = T.offs;
+    per_seg(c, P, [=] __device__(int64_t p) {
+        raw_n[p] = voffs[p + 1] - voffs[p];
+        const int64_t nt = toffs[p + 1] - toffs[p];
+        n_trend[p] = nt;
+        atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ2C_SESSIONS]), (unsigned long long)nt);
+    });
+    // trend values in (project, date) order
+    double *tv = c->arena.get<double>(NC);
+    const int32_t *trow = T.row;
+    const int64_t *cov_c = t.c_covered, *cov_t = t.c_total;
+    int64_t *d_nt = T.d_n;
+    map_n(c, NC, d_nt, [=] __device__(int64_t j) {
+        const int32_t r = trow[j];
+        tv[j] = double(cov_c[r]) / double(cov_t[r]) * 100.0;
+    });
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        counts[FZ_RQ2C_VALUES] = *d_nt;
+        if (counts[FZ_RQ2C_SESSIONS] < 1) counts[FZ_RQ2C_SESSIONS] = 1;  // starts as [[]] (:285)
+    });
+
+    // per-project Spearman (vs index) and Shapiro-Wilk
+    Segs sp{P, T.offs, NC};
+    ChunkedSegs cs = chunked(c, sp);
+    const int32_t *segid = reinterpret_cast<const int32_t *>(T.proj);
+    SortedSegs ss = seg_sort_f64(c, tv, sp, segid);
+    TieRanks tr = seg_tie_ranks(c, cs, segid, ss.val);
+    seg_spearman_index(c, cs, ss, tr, o->corr, nullptr);
+    seg_shapiro(c, cs, tv, ss, o->sw_w, o->sw_p);
+
+    // coverage_by_session_index: order by (index within project, project)
+    const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
+    const int ibits = bits_for(uint64_t(M));
+    uint64_t *key = c->arena.get<uint64_t>(NC);
+    uint32_t *idx = c->arena.get<uint32_t>(NC);
+    const uint32_t *tproj = T.proj;
+    map_n(c, NC, nullptr, [=] __device__(int64_t j) {
+        const int64_t live = *d_nt;
+        if (j < live) {
+            const uint32_t p = tproj[j];
+            key[j] = (uint64_t(j - toffs[p]) << pbits) | p;
+        } else {
+            key[j] = uint64_t(M) << pbits;  // past every real index
+        }
+        idx[j] = uint32_t(j);
+    });
+    radix_sort_pairs(c, key, idx, NC, ibits + pbits);
+    double *sv = o->session_values;
+    uint32_t *sid = c->arena.get<uint32_t>(NC);
+    map_n(c, NC, nullptr, [=] __device__(int64_t k) {
+        const int64_t live = *d_nt;
+        sid[k] = uint32_t(key[k] >> pbits);
+        if (k < live) sv[k] = tv[idx[k]];
+    });
+    k_segment_offsets_dn<<<grid_for(M + 1, kBlock, 1u << 30), kBlock, 0, st>>>(sid, d_nt, M, o->session_offsets);
+    FZ_LAUNCH_CHECK();
+
+    // per-session statistics (sessions are non-increasing in size: >= 100 is a prefix)
+    Segs ses{M, o->session_offsets, NC};
+    ChunkedSegs cs2 = chunked(c, ses);
+    const int32_t *sseg = reinterpret_cast<const int32_t *>(sid);
+    SortedSegs ss2 = seg_sort_f64(c, sv, ses, sseg);
+    const int64_t *soffs = o->session_offsets;
+    per_seg(c, M, [=] __device__(int64_t i) {
+        if (soffs[i + 1] - soffs[i] >= 100) atomic_add_i64(&counts[FZ_RQ2C_GE100], 1);
+    });
+    seg_mean(c, cs2, sv, o->average_trend);
+    seg_median(c, ses, ss2.val, o->median_trend);
+    const double q5[5] = {5.0, 25.0, 50.0, 75.0, 95.0};
+    seg_percentiles(c, ses, ss2.val, q5, 5, o->dist_percentiles);
+    FZ_HIP(hipMemcpyAsync(o->dist_mean, o->average_trend, size_t(M > 0 ? M : 1) * 8, hipMemcpyDeviceToDevice, st));
+
+    // tests on the median trend (one segment of K values)
+    double *sc = o->scalars;
+    {
+        const int64_t *d_k = counts + FZ_RQ2C_GE100;
+        Segs one{1, single_segment(c, d_k), M};
+        ChunkedSegs cs3 = chunked(c, one);
+        int32_t *sg3 = segment_ids(c, one);
+        SortedSegs ss3 = seg_sort_f64(c, o->median_trend, one, sg3);
+        TieRanks tr3 = seg_tie_ranks(c, cs3, sg3, ss3.val);
+        seg_spearman_index(c, cs3, ss3, tr3, sc + FZ_RQ2C_SP_RHO, sc + FZ_RQ2C_SP_P);
+        double *w3 = c->arena.get<double>(1);
+        seg_shapiro(c, cs3, o->median_trend, ss3, w3, sc + FZ_RQ2C_SW_MEDIAN_P);
+    }
+    // mean / median of the valid (non-NaN) per-project correlations
+    {
+        int64_t *flag = c->arena.get<int64_t>(P);
+        int64_t *pos = c->arena.get<int64_t>(P);
+        int64_t *d_nv = c->arena.get<int64_t>(1);
+        const double *corr = o->corr;
+        map_n(c, P, nullptr, [=] __device__(int64_t p) { flag[p] = (raw_n[p] > 0 && !isnan(corr[p])) ? 1 : 0; });
+        scan_exclusive_i64(c, flag, pos, P, d_nv);
+        double *vals = c->arena.get<double>(P);
+        map_n(c, P, nullptr, [=] __device__(int64_t p) {
+            if (flag[p]) vals[pos[p]] = corr[p];
+        });
+        fz_describe *d = c->arena.get<fz_describe>(1);
+        describe_f64_dn(c, vals, P, d_nv, d);
+        map_n(c, 1, nullptr, [=] __device__(int64_t) {
+            sc[FZ_RQ2C_CORR_MEAN] = d->mean;
+            sc[FZ_RQ2C_CORR_MEDIAN] = d->median;
+        });
+    }
+}
+
+// ------------------------------------------------------------------------------ RQ2 (add)
+// rq2_coverage_and_added.py:73-238: change points of (modules, revisions) over Coverage builds.
+constexpr int64_t kDayUs = 86400000000LL;
+
+struct CovBuildRows {  // result IN ('HalfWay', 'Finish') AND timecreated < LIMIT (:50-69), eligible
+    const uint32_t *proj;
+    const uint8_t *result;
+    const int64_t *time;
+    const uint8_t *elig;
+    __device__ bool operator()(int32_t r) const {
+        const uint8_t x = result[r];
+        return (x == 2 || x == 0) && time[r] < kLimitUs2 && elig[proj[r]];
+    }
+};
+struct CovRowsBeforeLimit {  // GET_COVERAGE_DATA: date < LIMIT, no NULL filter (:30-47), eligible
+    const uint32_t *proj;
+    const int64_t *date;
+    const uint8_t *elig;
+    __device__ bool operator()(int32_t r) const { return date[r] < kLimitUs2 && elig[proj[r]]; }
+};
+
+__device__ inline int64_t floor_div(int64_t a, int64_t b) {
+    const int64_t q = a / b;
+    return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
+}
+
+// first coverage row of [lo, hi) whose calendar day equals `day` (the reference's first match), or -1
+__device__ inline int64_t first_row_on_day(const int64_t *ctime, const int32_t *crow, int64_t lo, int64_t hi,
+                                           int64_t day) {
+    const int64_t k = lower_bound_i64(ctime, lo, hi, day * kDayUs);
+    if (k < hi && floor_div(ctime[k], kDayUs) == day) return crow[k];
+    return -1;
+}
+
+void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
+    Store &s = c->store;
+    FZ_CHECK(s.built, "fz_rq2_add: call fz_store_build first");
+    FZ_CHECK(o && o->counts && o->eligible && o->row_project && o->row_first_build && o->row_end_build &&
+                 o->row_start_build && o->row_cov_i && o->row_cov_i1 && o->diff_total && o->diff_coverage &&
+                 o->covered_is_float && o->total_is_float,
+             "fz_rq2_add: null output buffer");
+    const fz_tables &t = s.t;
+    const int64_t P = s.P;
+    hipStream_t st = c->stream;
+    FZ_HIP(hipMemsetAsync(o->counts, 0, FZ_RQ2A_NCOUNTS * 8, st));
+    FZ_HIP(hipMemsetAsync(o->covered_is_float, 0, size_t(P > 0 ? P : 1), st));
+    FZ_HIP(hipMemsetAsync(o->total_is_float, 0, size_t(P > 0 ? P : 1), st));
+    eligible_projects(c, o->eligible, o->counts + FZ_RQ2A_ELIGIBLE);
+
+    TmpView B, CV;
+    filter_view(c, s.covb.row, s.covb.time, s.covb.proj, s.covb.n, P,
+                CovBuildRows{t.b_project, t.b_result, t.b_time, o->eligible}, B);
+    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, s.cov.n, P, CovRowsBeforeLimit{t.c_project, t.c_date, o->eligible},
+                CV);
+    const int64_t NB = s.covb.n;
+    const int64_t *boffs = B.offs, *coffs = CV.offs;
+    // pandas upcast flags: a NULL covered/total among the project's fetched coverage rows
+    {
+        uint8_t *anyc = c->arena.get<uint8_t>(P), *anyt = c->arena.get<uint8_t>(P);
+        FZ_HIP(hipMemsetAsync(anyc, 0, size_t(P > 0 ? P : 1), st));
+        FZ_HIP(hipMemsetAsync(anyt, 0, size_t(P > 0 ? P : 1), st));
+        const int32_t *crow = CV.row;
+        const uint32_t *cproj = CV.proj;
+        const uint8_t *valid = t.c_valid;
+        map_n(c, s.cov.n, CV.d_n, [=] __device__(int64_t j) {
+            const uint8_t v = valid[crow[j]];
+            if (!(v & FZ_VALID_COVERED)) anyc[cproj[j]] = 1;
+            if (!(v & FZ_VALID_TOTAL)) anyt[cproj[j]] = 1;
+        });
+        uint8_t *cf = o->covered_is_float, *tf = o->total_is_float;
+        per_seg(c, P, [=] __device__(int64_t p) {
+            const bool used = boffs[p + 1] > boffs[p] && coffs[p + 1] > coffs[p];
+            cf[p] = used && anyc[p];
+            tf[p] = used && anyt[p];
+        });
+    }
+    // run starts: group = cumsum(key != key.shift()) within the project (:129-131)
+    int64_t *start = c->arena.get<int64_t>(NB);
+    int64_t *rid = c->arena.get<int64_t>(NB);
+    int64_t *runpos = c->arena.get<int64_t>(NB + 1);
+    int64_t *d_runs = o->counts + FZ_RQ2A_RUNS;
+    const int32_t *brow = B.row;
+    const uint32_t *bproj = B.proj;
+    const int32_t *grp = t.b_group;
+    const int64_t *d_nb = B.d_n;
+    map_n(c, NB, nullptr, [=] __device__(int64_t j) {
+        if (j >= *d_nb) {
+            start[j] = 0;
+            return;
+        }
+        const uint32_t p = bproj[j];
+        start[j] = (coffs[p + 1] > coffs[p]) && (j == boffs[p] || grp[brow[j]] != grp[brow[j - 1]]) ? 1 : 0;
+    });
+    scan_exclusive_i64(c, start, rid, NB, d_runs);
+    map_n(c, NB, nullptr, [=] __device__(int64_t j) {
+        if (start[j]) runpos[rid[j]] = j;
+        if (j == 0) runpos[*d_runs] = *d_nb;
+    });
+    // a pair for run r when run r + 1 belongs to the same project
+    int64_t *pflag = c->arena.get<int64_t>(NB);
+    int64_t *ppos = c->arena.get<int64_t>(NB);
+    map_n(c, NB, nullptr, [=] __device__(int64_t r) {
+        const int64_t R = *d_runs;
+        pflag[r] = (r + 1 < R && bproj[runpos[r]] == bproj[runpos[r + 1]]) ? 1 : 0;
+    });
+    scan_exclusive_i64(c, pflag, ppos, NB, o->counts + FZ_RQ2A_ROWS);
+    const int64_t *btime = t.b_time;
+    const int64_t *ctime = CV.time;
+    const int32_t *crow = CV.row;
+    const int64_t *cov_c = t.c_covered, *cov_t = t.c_total;
+    const uint8_t *valid = t.c_valid;
+    const fz_rq2_add_out out = *o;
+    map_n(c, NB, nullptr, [=] __device__(int64_t r) {
+        if (!pflag[r]) return;
+        const int64_t q = ppos[r];
+        const int64_t j0 = runpos[r], j1 = runpos[r + 1];
+        const uint32_t p = bproj[j0];
+        const int32_t f = brow[j0], e = brow[j1 - 1], sb = brow[j1];
+        const int64_t c0 = first_row_on_day(ctime, crow, coffs[p], coffs[p + 1], floor_div(btime[e], kDayUs));
+        const int64_t c1 = first_row_on_day(ctime, crow, coffs[p], coffs[p + 1], floor_div(btime[sb], kDayUs));
+        auto cell = [&](int64_t cr, double &cv, double &tv) {
+            cv = tv = NAN;
+            if (cr < 0) return;
+            const uint8_t v = valid[cr];
+            if (v & FZ_VALID_COVERED) cv = double(cov_c[cr]);
+            if (v & FZ_VALID_TOTAL) tv = double(cov_t[cr]);
+        };
+        double cv0, tv0, cv1, tv1;
+        cell(c0, cv0, tv0);
+        cell(c1, cv1, tv1);
+        double dt = NAN, dc = NAN;
+        if (!isnan(tv0) && tv0 != 0.0 && !isnan(tv1) && tv1 != 0.0) {
+            dt = tv1 - tv0;
+            dc = (cv1 / tv1) * 100.0 - (cv0 / tv0) * 100.0;
+        }
+        out.row_project[q] = p;
+        out.row_first_build[q] = f;
+        out.row_end_build[q] = e;
+        out.row_start_build[q] = sb;
+        out.row_cov_i[q] = c0;
+        out.row_cov_i1[q] = c1;
+        out.diff_total[q] = dt;
+        out.diff_coverage[q] = dc;
+    });
+}
+
+}  // namespace fz

@@ -1,0 +1,164 @@
+// Segmented series toolkit: many independent series (one per project, per session index, or a
+// single series) laid out contiguously with offsets[S + 1].
+//
+// Load balance (Zipf projects, 1e6-point series - SURVEY.md 8(d) configs 4/5): reductions never
+// map one segment to one workgroup.  Segments are cut into chunks of at most kChunk elements
+// (ChunkMap); one workgroup reduces one chunk into double-double partials, then one wave per
+// segment adds its chunks in order.  Results are deterministic (fixed order, no float atomics).
+#pragma once
+
+#include "fz_device.h"
+#include "fz_internal.h"
+#include "fz_views.h"
+
+namespace fz {
+
+constexpr int kChunk = 2048;
+
+struct Segs {
+    int64_t S = 0;                 // number of segments
+    const int64_t *offs = nullptr; // [S + 1] device
+    int64_t n_cap = 0;             // host upper bound of offs[S]
+};
+
+struct ChunkMap {
+    int64_t cap = 0;
+    int64_t *d_n = nullptr;
+    int32_t *seg = nullptr;
+    int64_t *begin = nullptr;
+    int64_t *end = nullptr;
+};
+
+ChunkMap make_chunks(fz_ctx *c, const Segs &sg);
+// seg id of every element (binary search over offsets); elements past offs[S] get S.
+int32_t *segment_ids(fz_ctx *c, const Segs &sg);
+
+template <int NV, typename F>
+__global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, F f, double *__restrict__ part) {
+    __shared__ double s_hi[4][NV], s_lo[4][NV];
+    const int64_t k = blockIdx.x;
+    if (k >= *cm.d_n) return;
+    const int32_t seg = cm.seg[k];
+    DD acc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = DD{0.0, 0.0};
+    for (int64_t i = cm.begin[k] + threadIdx.x; i < cm.end[k]; i += kBlock) {
+        double x[NV];
+        f(i, seg, x);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] = dd_add_d(acc[v], x[v]);
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        DD r = wave_dd_sum(acc[v]);
+        if (lane_id() == 0) {
+            s_hi[wave_id()][v] = r.hi;
+            s_lo[wave_id()][v] = r.lo;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        const int v = threadIdx.x;
+        DD t{s_hi[0][v], s_lo[0][v]};
+        for (int w = 1; w < 4; ++w) t = dd_add(t, DD{s_hi[w][v], s_lo[w][v]});
+        part[(k * NV + v) * 2] = t.hi;
+        part[(k * NV + v) * 2 + 1] = t.lo;
+    }
+}
+
+// out[s * NV + v] = sum over segment s's chunks (one wave per segment, chunks in order).
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_seg_sum(ChunkMap cm, int64_t S, const int64_t *__restrict__ chunk_off,
+                                                    const double *__restrict__ part, double *__restrict__ out) {
+    const int64_t s = int64_t(blockIdx.x) * 4 + wave_id();
+    if (s >= S) return;
+    const int64_t c0 = chunk_off[s], c1 = chunk_off[s + 1];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        DD acc{0.0, 0.0};
+        for (int64_t k = c0 + lane_id(); k < c1; k += 64) acc = dd_add(acc, DD{part[(k * NV + v) * 2], part[(k * NV + v) * 2 + 1]});
+        acc = wave_dd_sum(acc);
+        if (lane_id() == 0) out[s * NV + v] = acc.hi + acc.lo;
+    }
+}
+
+// Chunk offsets per segment (kept beside the map so k_seg_sum can find a segment's chunks).
+struct ChunkedSegs {
+    Segs sg;
+    ChunkMap cm;
+    int64_t *chunk_off = nullptr;  // [S + 1]
+};
+ChunkedSegs chunked(fz_ctx *c, const Segs &sg);
+
+// Segmented sum of NV per-element values f(i, seg, x[NV]) -> out[S][NV] (device).
+template <int NV, typename F>
+void seg_reduce(fz_ctx *c, const ChunkedSegs &cs, F f, double *out) {
+    double *part = c->arena.get<double>(cs.cm.cap * NV * 2);
+    if (cs.cm.cap > 0) {
+        k_chunk_reduce<NV, F><<<unsigned(cs.cm.cap), kBlock, 0, c->stream>>>(cs.cm, f, part);
+        FZ_LAUNCH_CHECK();
+    }
+    if (cs.sg.S > 0) {
+        k_seg_sum<NV><<<unsigned((cs.sg.S + 3) / 4), kBlock, 0, c->stream>>>(cs.cm, cs.sg.S, cs.chunk_off, part, out);
+        FZ_LAUNCH_CHECK();
+    }
+}
+
+// Per-segment finishing: f(s) for s in [0, S).
+template <typename F>
+__global__ __launch_bounds__(kBlock) void k_per_seg(int64_t S, F f) {
+    for (int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x; s < S; s += int64_t(gridDim.x) * kBlock) f(s);
+}
+template <typename F>
+void per_seg(fz_ctx *c, int64_t S, F f) {
+    if (S <= 0) return;
+    k_per_seg<F><<<grid_for(S, kBlock, 4096), kBlock, 0, c->stream>>>(S, f);
+    FZ_LAUNCH_CHECK();
+}
+// Per-element map over [0, n_cap) with the device count d_n (elements >= *d_n skipped).
+template <typename F>
+__global__ __launch_bounds__(kBlock) void k_map(int64_t n_cap, const int64_t *__restrict__ d_n, F f) {
+    const int64_t n = d_n ? *d_n : n_cap;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) f(i);
+}
+template <typename F>
+void map_n(fz_ctx *c, int64_t n_cap, const int64_t *d_n, F f) {
+    if (n_cap <= 0) return;
+    k_map<F><<<grid_for(n_cap, kBlock, 8192), kBlock, 0, c->stream>>>(n_cap, d_n, f);
+    FZ_LAUNCH_CHECK();
+}
+
+// ---- series operations (fz_series.hip) ----------------------------------------------------
+// Values of each segment sorted ascending (stable: ties keep source order).  pos[i] = source
+// index of sorted element i.  Elements past offs[S] are left at the end.
+struct SortedSegs {
+    double *val = nullptr;
+    int32_t *pos = nullptr;
+};
+SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int32_t *segid);
+
+// Average (tie-aware) 1-based rank of every sorted element within its segment, and the number of
+// distinct values per segment (ngroups[S], as double).
+struct TieRanks {
+    double *rank = nullptr;
+    double *ngroups = nullptr;
+};
+TieRanks seg_tie_ranks(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const double *sorted);
+
+// scipy.stats.spearmanr(range(n), series) per segment -> rho[S], p[S] (NaN: n < 2 or constant).
+void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, const TieRanks &tr, double *rho,
+                        double *pval);
+// scipy.stats.shapiro per segment (src in original order, ss its sorted image) -> W[S], p[S]
+// (NaN where n < 3).
+void seg_shapiro(fz_ctx *c, const ChunkedSegs &cs, const double *src, const SortedSegs &ss, double *w, double *p);
+// numpy.percentile(seg, q[j]) for sorted segments -> out[s * nq + j] (NaN for empty segments).
+void seg_percentiles(fz_ctx *c, const Segs &sg, const double *sorted, const double *q_host, int nq, double *out);
+// sum / n per segment in double-double (statistics.mean / np.mean within 1 ulp) -> out[S].
+void seg_mean(fz_ctx *c, const ChunkedSegs &cs, const double *vals, double *out);
+// statistics.median / np.median of sorted segments: middle value or (a + b) / 2 -> out[S].
+void seg_median(fz_ctx *c, const Segs &sg, const double *sorted, double *out);
+
+// A device offsets array [0, *d_n] for one segment whose length is known only on the device.
+const int64_t *single_segment(fz_ctx *c, const int64_t *d_n);
+
+}  // namespace fz

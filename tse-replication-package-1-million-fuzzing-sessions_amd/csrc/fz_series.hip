@@ -1,0 +1,307 @@
+// Segmented series operations (fz_seg.h): chunk maps, segmented sort, tie ranks, Spearman vs
+// index, Shapiro-Wilk, percentiles, means, medians.
+#include "fz_seg.h"
+#include "fz_stats.h"
+
+namespace fz {
+
+// ------------------------------------------------------------------------------ chunk maps
+__global__ __launch_bounds__(kBlock) void k_chunk_count(const int64_t *__restrict__ offs, int64_t S,
+                                                        int64_t *__restrict__ cnt) {
+    for (int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x; s < S; s += int64_t(gridDim.x) * kBlock) {
+        const int64_t len = offs[s + 1] - offs[s];
+        cnt[s] = (len + kChunk - 1) / kChunk;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_chunk_fill(const int64_t *__restrict__ offs, int64_t S,
+                                                       const int64_t *__restrict__ coff, ChunkMap cm) {
+    const int64_t n = *cm.d_n;
+    for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < n; k += int64_t(gridDim.x) * kBlock) {
+        const int64_t s = upper_bound_i64(coff, 0, S + 1, k) - 1;
+        const int64_t b = offs[s] + (k - coff[s]) * kChunk;
+        const int64_t e = b + kChunk < offs[s + 1] ? b + kChunk : offs[s + 1];
+        cm.seg[k] = int32_t(s);
+        cm.begin[k] = b;
+        cm.end[k] = e;
+    }
+}
+
+ChunkedSegs chunked(fz_ctx *c, const Segs &sg) {
+    ChunkedSegs cs;
+    cs.sg = sg;
+    ChunkMap &cm = cs.cm;
+    cm.cap = sg.S + sg.n_cap / kChunk + 1;
+    cm.d_n = c->arena.get<int64_t>(1);
+    cm.seg = c->arena.get<int32_t>(cm.cap);
+    cm.begin = c->arena.get<int64_t>(cm.cap);
+    cm.end = c->arena.get<int64_t>(cm.cap);
+    cs.chunk_off = c->arena.get<int64_t>(sg.S + 1);
+    int64_t *cnt = c->arena.get<int64_t>(sg.S + 1);
+    FZ_HIP(hipMemsetAsync(cnt, 0, size_t(sg.S + 1) * 8, c->stream));
+    if (sg.S > 0) {
+        k_chunk_count<<<grid_for(sg.S), kBlock, 0, c->stream>>>(sg.offs, sg.S, cnt);
+        FZ_LAUNCH_CHECK();
+    }
+    scan_exclusive_i64(c, cnt, cs.chunk_off, sg.S + 1, cm.d_n);
+    k_chunk_fill<<<grid_for(cm.cap, kBlock, 4096), kBlock, 0, c->stream>>>(sg.offs, sg.S, cs.chunk_off, cm);
+    FZ_LAUNCH_CHECK();
+    return cs;
+}
+
+ChunkMap make_chunks(fz_ctx *c, const Segs &sg) { return chunked(c, sg).cm; }
+
+int32_t *segment_ids(fz_ctx *c, const Segs &sg) {
+    int32_t *id = c->arena.get<int32_t>(sg.n_cap);
+    const int64_t *offs = sg.offs;
+    const int64_t S = sg.S;
+    map_n(c, sg.n_cap, nullptr, [=] __device__(int64_t i) {
+        const int64_t s = upper_bound_i64(offs, 0, S + 1, i) - 1;
+        id[i] = int32_t(s > S ? S : (s < 0 ? 0 : s));
+    });
+    return id;
+}
+
+const int64_t *single_segment(fz_ctx *c, const int64_t *d_n) {
+    int64_t *o = c->arena.get<int64_t>(2);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        o[0] = 0;
+        o[1] = *d_n;
+    });
+    return o;
+}
+
+// -------------------------------------------------------------------------- segmented sort
+SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int32_t *segid) {
+    const int64_t n = sg.n_cap;
+    SortedSegs out;
+    out.val = c->arena.get<double>(n);
+    out.pos = c->arena.get<int32_t>(n);
+    if (n <= 0) return out;
+    uint64_t *keys = c->arena.get<uint64_t>(n);
+    uint32_t *vals = reinterpret_cast<uint32_t *>(out.pos);
+    const int64_t *offs = sg.offs;
+    const int64_t S = sg.S;
+    // stage 1: by value (elements past the live count sort last)
+    map_n(c, n, nullptr, [=] __device__(int64_t i) {
+        const int64_t live = offs[S];
+        keys[i] = i < live ? f64_key(src[i]) : ~0ull;
+        vals[i] = uint32_t(i);
+    });
+    radix_sort_pairs(c, keys, vals, n, 64);
+    // stage 2: by segment, stable
+    map_n(c, n, nullptr, [=] __device__(int64_t i) {
+        const int64_t live = offs[S];
+        const uint32_t j = vals[i];
+        keys[i] = int64_t(j) < live ? uint64_t(segid[j]) : uint64_t(S);
+    });
+    radix_sort_pairs(c, keys, vals, n, bits_for(uint64_t(S)));
+    double *ov = out.val;
+    map_n(c, n, nullptr, [=] __device__(int64_t i) {
+        const int64_t live = offs[S];
+        ov[i] = i < live ? src[vals[i]] : 0.0;
+    });
+    return out;
+}
+
+// ------------------------------------------------------------------------------ tie ranks
+TieRanks seg_tie_ranks(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const double *sorted) {
+    const Segs &sg = cs.sg;
+    const int64_t n = sg.n_cap;
+    const int64_t *offs = sg.offs;
+    const int64_t S = sg.S;
+    TieRanks tr;
+    tr.rank = c->arena.get<double>(n);
+    tr.ngroups = c->arena.get<double>(S);
+    int64_t *flag = c->arena.get<int64_t>(n);
+    int64_t *gid = c->arena.get<int64_t>(n);
+    int64_t *gstart = c->arena.get<int64_t>(n + 1);
+    map_n(c, n, nullptr, [=] __device__(int64_t i) {
+        const int64_t live = offs[S];
+        if (i >= live) {
+            flag[i] = 0;
+            return;
+        }
+        const int64_t s = segid[i];
+        flag[i] = (i == offs[s] || sorted[i] != sorted[i - 1]) ? 1 : 0;
+    });
+    int64_t *d_g = c->arena.get<int64_t>(1);
+    scan_exclusive_i64(c, flag, gid, n, d_g);
+    map_n(c, n, nullptr, [=] __device__(int64_t i) {
+        if (flag[i]) gstart[gid[i]] = i;
+        if (i == 0) gstart[*d_g] = offs[S];
+    });
+    double *rank = tr.rank;
+    map_n(c, n, nullptr, [=] __device__(int64_t i) {
+        const int64_t live = offs[S];
+        if (i >= live) return;
+        const int64_t g = gid[i] + (flag[i] ? 0 : -1);  // exclusive scan: group index of element i
+        const int64_t s = segid[i];
+        const int64_t a = gstart[g], b = gstart[g + 1];
+        rank[i] = double(a + b + 1) / 2.0 - double(offs[s]);
+    });
+    seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t, double *x) { x[0] = double(flag[i]); }, tr.ngroups);
+    return tr;
+}
+
+// --------------------------------------------------------------------- Spearman vs index
+void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, const TieRanks &tr, double *rho,
+                        double *pval) {
+    const int64_t *offs = cs.sg.offs;
+    const int64_t S = cs.sg.S;
+    const int32_t *pos = ss.pos;
+    const double *rank = tr.rank;
+    double *sums = c->arena.get<double>(S * 3);
+    // deviations from the common mean rank (n+1)/2 are half-integers: the products are exact
+    seg_reduce<3>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
+        const int64_t b = offs[s];
+        const double m = double(offs[s + 1] - b + 1) / 2.0;
+        const double rx = double(pos[i] - b + 1) - m;
+        const double ry = rank[i] - m;
+        x[0] = rx * ry;
+        x[1] = rx * rx;
+        x[2] = ry * ry;
+    }, sums);
+    const double *ng = tr.ngroups;
+    per_seg(c, S, [=] __device__(int64_t s) {
+        const int64_t n = offs[s + 1] - offs[s];
+        double r = NAN, p = NAN;
+        if (n >= 2 && ng[s] > 1.0) {
+            // np.corrcoef: c01 / std0 / std1 with c = dot(dev, dev.T) / (n - 1)
+            const double d = double(n - 1);
+            const double cxy = sums[3 * s] / d, cxx = sums[3 * s + 1] / d, cyy = sums[3 * s + 2] / d;
+            r = cxy / sqrt(cxx) / sqrt(cyy);
+            if (r > 1.0) r = 1.0;
+            if (r < -1.0) r = -1.0;
+            const double dof = double(n - 2);
+            double q = dof / ((r + 1.0) * (1.0 - r));
+            if (q < 0.0) q = 0.0;  // numpy clip(0); NaN stays NaN
+            const double t = r * sqrt(q);
+            p = 2.0 * stats::t_sf(fabs(t), dof);
+        }
+        rho[s] = r;
+        if (pval) pval[s] = p;
+    });
+}
+
+// ------------------------------------------------------------------------- Shapiro-Wilk
+void seg_shapiro(fz_ctx *c, const ChunkedSegs &cs, const double *src, const SortedSegs &ss, double *w, double *p) {
+    const int64_t *offs = cs.sg.offs;
+    const int64_t S = cs.sg.S;
+    const double *v = ss.val;
+    double *summ2 = c->arena.get<double>(S);
+    double *coef = c->arena.get<double>(S * 4);   // a1, a2, fac, i1
+    double *shift = c->arena.get<double>(S * 2);  // x0 (= x[n//2]), range
+    double *s1 = c->arena.get<double>(S * 2);     // sx, sa
+    double *s2 = c->arena.get<double>(S * 3);     // ssa, ssx, sax
+    // pass A: summ2 = 2 * sum_{i <= n/2} m_i^2
+    seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
+        const int64_t b = offs[s], n = offs[s + 1] - b, k = i - b + 1;
+        double m = 0.0;
+        if (n >= 3 && k <= n / 2) m = stats::sw_m(k, n);
+        x[0] = m * m;
+    }, summ2);
+    per_seg(c, S, [=] __device__(int64_t s) {
+        const int64_t b = offs[s], n = offs[s + 1] - b;
+        if (n < 3) return;
+        const stats::SwCoef cf = stats::sw_coef(n, 2.0 * summ2[s]);
+        coef[4 * s] = cf.a1;
+        coef[4 * s + 1] = cf.a2;
+        coef[4 * s + 2] = cf.fac;
+        coef[4 * s + 3] = double(cf.i1);
+        const double x0 = src[b + n / 2];  // scipy: y = sort(x); y -= x[N//2]
+        shift[2 * s] = x0;
+        shift[2 * s + 1] = (v[b + n - 1] - x0) - (v[b] - x0);
+    });
+    auto coef_of = [=] __device__(int32_t s, int64_t n) {
+        stats::SwCoef cf;
+        cf.n = n;
+        cf.a1 = coef[4 * s];
+        cf.a2 = coef[4 * s + 1];
+        cf.fac = coef[4 * s + 2];
+        cf.i1 = int(coef[4 * s + 3]);
+        return cf;
+    };
+    // pass B: sx = sum y/range, sa = sum of signed coefficients
+    seg_reduce<2>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
+        const int64_t b = offs[s], n = offs[s + 1] - b;
+        x[0] = x[1] = 0.0;
+        if (n < 3) return;
+        const double range = shift[2 * s + 1];
+        x[0] = (v[i] - shift[2 * s]) / range;
+        x[1] = stats::sw_coef_at(coef_of(s, n), i - b + 1);
+    }, s1);
+    // pass C: ssa, ssx, sax
+    seg_reduce<3>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
+        const int64_t b = offs[s], n = offs[s + 1] - b;
+        x[0] = x[1] = x[2] = 0.0;
+        if (n < 3) return;
+        const double range = shift[2 * s + 1];
+        const double sa = s1[2 * s + 1] / double(n), sx = s1[2 * s] / double(n);
+        const double asa = stats::sw_coef_at(coef_of(s, n), i - b + 1) - sa;
+        const double xsx = (v[i] - shift[2 * s]) / range - sx;
+        x[0] = asa * asa;
+        x[1] = xsx * xsx;
+        x[2] = asa * xsx;
+    }, s2);
+    per_seg(c, S, [=] __device__(int64_t s) {
+        const int64_t n = offs[s + 1] - offs[s];
+        if (n < 3) {
+            w[s] = NAN;
+            p[s] = NAN;
+            return;
+        }
+        if (shift[2 * s + 1] < stats::kSwSmall) {  // zero range: scipy returns (1.0, 1.0)
+            w[s] = 1.0;
+            p[s] = 1.0;
+            return;
+        }
+        const double ssa = s2[3 * s], ssx = s2[3 * s + 1], sax = s2[3 * s + 2];
+        const double ssassx = sqrt(ssa * ssx);
+        const double w1 = (ssassx - sax) * (ssassx + sax) / (ssa * ssx);
+        const double ww = 1.0 - w1;
+        w[s] = ww;
+        p[s] = stats::sw_pvalue(n, ww, w1);
+    });
+}
+
+// ------------------------------------------------------------- percentiles, means, medians
+void seg_percentiles(fz_ctx *c, const Segs &sg, const double *sorted, const double *q_host, int nq, double *out) {
+    double q[8];
+    for (int j = 0; j < nq && j < 8; ++j) q[j] = q_host[j];
+    const int64_t *offs = sg.offs;
+    per_seg(c, sg.S, [=] __device__(int64_t s) {
+        const int64_t b = offs[s], n = offs[s + 1] - b;
+        for (int j = 0; j < nq; ++j) {
+            if (n <= 0) {
+                out[s * nq + j] = NAN;
+                continue;
+            }
+            out[s * nq + j] = np_percentile_sorted([&](int64_t k) { return sorted[b + k]; }, n, q[j]);
+        }
+    });
+}
+
+void seg_mean(fz_ctx *c, const ChunkedSegs &cs, const double *vals, double *out) {
+    double *sum = c->arena.get<double>(cs.sg.S);
+    seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t, double *x) { x[0] = vals[i]; }, sum);
+    const int64_t *offs = cs.sg.offs;
+    per_seg(c, cs.sg.S, [=] __device__(int64_t s) {
+        const int64_t n = offs[s + 1] - offs[s];
+        out[s] = n > 0 ? sum[s] / double(n) : NAN;
+    });
+}
+
+void seg_median(fz_ctx *c, const Segs &sg, const double *sorted, double *out) {
+    const int64_t *offs = sg.offs;
+    per_seg(c, sg.S, [=] __device__(int64_t s) {
+        const int64_t b = offs[s], n = offs[s + 1] - b;
+        if (n <= 0) {
+            out[s] = NAN;
+            return;
+        }
+        out[s] = (n & 1) ? sorted[b + n / 2] : (sorted[b + n / 2 - 1] + sorted[b + n / 2]) / 2.0;
+    });
+}
+
+}  // namespace fz

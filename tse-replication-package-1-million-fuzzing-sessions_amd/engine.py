@@ -61,6 +61,27 @@ class FzRq1Out(C.Structure):
                 ("matched_issue", _P), ("matched_build", _P), ("late", _P)]
 
 
+FZ_RQ2C_NCOUNTS, FZ_RQ2C_NSCALARS = 8, 8
+RQ2C_ELIGIBLE, RQ2C_SESSIONS, RQ2C_GE100, RQ2C_VALUES = range(4)
+RQ2C_CORR_MEAN, RQ2C_CORR_MEDIAN, RQ2C_SP_RHO, RQ2C_SP_P, RQ2C_SW_MEDIAN_P = range(5)
+
+
+class FzRq2CountOut(C.Structure):
+    _fields_ = [(n, _P) for n in ("counts", "scalars", "eligible", "raw_n", "n_trend", "sw_w", "sw_p", "corr",
+                                  "session_offsets", "session_values", "average_trend", "median_trend",
+                                  "dist_percentiles", "dist_mean")]
+
+
+FZ_RQ2A_NCOUNTS = 4
+RQ2A_ELIGIBLE, RQ2A_ROWS, RQ2A_RUNS = range(3)
+
+
+class FzRq2AddOut(C.Structure):
+    _fields_ = [(n, _P) for n in ("counts", "eligible", "row_project", "row_first_build", "row_end_build",
+                                  "row_start_build", "row_cov_i", "row_cov_i1", "diff_total", "diff_coverage",
+                                  "covered_is_float", "total_is_float")]
+
+
 # every symbol include/fz.h declares, with its ctypes signature
 SIGNATURES = {
     "fz_abi_version": (C.c_int, []),
@@ -70,6 +91,8 @@ SIGNATURES = {
     "fz_ctx_set_stream": (C.c_int, [_P, _P]),
     "fz_store_build": (C.c_int, [_P, C.POINTER(FzTables), C.POINTER(FzStoreStats)]),
     "fz_rq1": (C.c_int, [_P, _I64, C.POINTER(FzRq1Out)]),
+    "fz_rq2_count": (C.c_int, [_P, C.POINTER(FzRq2CountOut)]),
+    "fz_rq2_add": (C.c_int, [_P, C.POINTER(FzRq2AddOut)]),
     "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),
     "fz_probe_end": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "fz_radix_sort_u64": (C.c_int, [_P, _P, _P, _I64, C.c_int]),

@@ -11,7 +11,7 @@ import ctypes as C
 import numpy as np
 
 from .. import engine as E
-from .results import Describe, RQ1Result
+from .results import Describe, RQ1Result, RQ2AddResult, RQ2CountResult
 
 
 def _describe(d: E.FzDescribe, with_min_nonzero=False) -> Describe:
@@ -74,3 +74,97 @@ def rq1(eng: E.Engine, threshold: int = 100) -> RQ1Result:
     bufs = RQ1Buffers(eng)
     rq1_launch(eng, bufs, threshold)
     return rq1_collect(eng, bufs, threshold)
+
+
+class OutBuffers:
+    """Device buffers for one fz_* output struct: spec = [(field, n, torch dtype)] in struct order."""
+
+    def __init__(self, eng: E.Engine, struct_cls, spec):
+        self.names = [n for n, _, _ in spec]
+        for name, n, dt in spec:
+            setattr(self, name, eng.zeros(n, dt))
+        self.out = struct_cls(*[C.c_void_p(getattr(self, n).data_ptr()) for n in self.names])
+
+    def host(self, name, n=None):
+        a = getattr(self, name)
+        return (a if n is None else a[:n]).cpu().numpy()
+
+
+# ------------------------------------------------------------------------------------ RQ2 count
+def rq2_count_buffers(eng: E.Engine) -> OutBuffers:
+    torch = eng.torch
+    fz, st = eng.tables.fz, eng.stats
+    P, M, NC = fz.n_projects, max(int(st.max_cov_per_project), 1), fz.n_cov
+    f64, i64, u8 = torch.float64, torch.int64, torch.uint8
+    return OutBuffers(eng, E.FzRq2CountOut, [
+        ("counts", E.FZ_RQ2C_NCOUNTS, i64), ("scalars", E.FZ_RQ2C_NSCALARS, f64), ("eligible", P, u8),
+        ("raw_n", P, i64), ("n_trend", P, i64), ("sw_w", P, f64), ("sw_p", P, f64), ("corr", P, f64),
+        ("session_offsets", M + 2, i64), ("session_values", NC, f64), ("average_trend", M, f64),
+        ("median_trend", M, f64), ("dist_percentiles", 5 * M, f64), ("dist_mean", M, f64)])
+
+
+def rq2_count_launch(eng: E.Engine, b: OutBuffers):
+    E._check(eng.lib, eng.lib.fz_rq2_count(eng.ctx, C.byref(b.out)))
+
+
+def rq2_count_collect(eng: E.Engine, b: OutBuffers) -> RQ2CountResult:
+    P = eng.tables.fz.n_projects
+    cnt = b.host("counts")
+    sc = b.host("scalars")
+    elig = np.nonzero(b.host("eligible", P))[0]
+    raw_n = b.host("raw_n", P)[elig]
+    ns, K, nv = int(cnt[E.RQ2C_SESSIONS]), int(cnt[E.RQ2C_GE100]), int(cnt[E.RQ2C_VALUES])
+    corr = b.host("corr", P)[elig][raw_n > 0]
+    pct = b.host("dist_percentiles", 5 * K).reshape(K, 5).T.copy() if K else np.zeros((5, 0))
+    return RQ2CountResult(
+        eligible=elig, raw_n=raw_n, n_trend=b.host("n_trend", P)[elig], sw_w=b.host("sw_w", P)[elig],
+        sw_p=b.host("sw_p", P)[elig], corr=corr, session_offsets=b.host("session_offsets", ns + 1),
+        session_values=b.host("session_values", nv), corr_mean=float(sc[E.RQ2C_CORR_MEAN]),
+        corr_median=float(sc[E.RQ2C_CORR_MEDIAN]), ge100=np.arange(K, dtype=np.int64),
+        average_trend=b.host("average_trend", K), median_trend=b.host("median_trend", K),
+        spearman_median=(float(sc[E.RQ2C_SP_RHO]), float(sc[E.RQ2C_SP_P])) if K > 1 else None,
+        shapiro_median_p=float(sc[E.RQ2C_SW_MEDIAN_P]) if K >= 3 else None,
+        dist_percentiles=pct, dist_mean=b.host("dist_mean", K))
+
+
+def rq2_count(eng: E.Engine) -> RQ2CountResult:
+    """rq2_coverage_count.main's analysis (rq2_coverage_count.py:244-483) on the GPU."""
+    b = rq2_count_buffers(eng)
+    rq2_count_launch(eng, b)
+    return rq2_count_collect(eng, b)
+
+
+# -------------------------------------------------------------------------------------- RQ2 add
+def rq2_add_buffers(eng: E.Engine) -> OutBuffers:
+    torch = eng.torch
+    fz, st = eng.tables.fz, eng.stats
+    P, NB = fz.n_projects, max(int(st.n_coverage_builds), 1)
+    f64, i64, u8 = torch.float64, torch.int64, torch.uint8
+    return OutBuffers(eng, E.FzRq2AddOut, [
+        ("counts", E.FZ_RQ2A_NCOUNTS, i64), ("eligible", P, u8), ("row_project", NB, i64),
+        ("row_first_build", NB, i64), ("row_end_build", NB, i64), ("row_start_build", NB, i64),
+        ("row_cov_i", NB, i64), ("row_cov_i1", NB, i64), ("diff_total", NB, f64), ("diff_coverage", NB, f64),
+        ("covered_is_float", P, u8), ("total_is_float", P, u8)])
+
+
+def rq2_add_launch(eng: E.Engine, b: OutBuffers):
+    E._check(eng.lib, eng.lib.fz_rq2_add(eng.ctx, C.byref(b.out)))
+
+
+def rq2_add_collect(eng: E.Engine, b: OutBuffers) -> RQ2AddResult:
+    P = eng.tables.fz.n_projects
+    n = int(b.host("counts")[E.RQ2A_ROWS])
+    return RQ2AddResult(
+        projects=np.nonzero(b.host("eligible", P))[0], row_project=b.host("row_project", n),
+        row_first_build=b.host("row_first_build", n), row_end_build=b.host("row_end_build", n),
+        row_start_build=b.host("row_start_build", n), row_cov_i=b.host("row_cov_i", n),
+        row_cov_i1=b.host("row_cov_i1", n), diff_total=b.host("diff_total", n),
+        diff_coverage=b.host("diff_coverage", n), covered_is_float=b.host("covered_is_float", P).astype(bool),
+        total_is_float=b.host("total_is_float", P).astype(bool))
+
+
+def rq2_add(eng: E.Engine) -> RQ2AddResult:
+    """rq2_coverage_and_added.analyze_coverage_change (rq2_coverage_and_added.py:73-238) on the GPU."""
+    b = rq2_add_buffers(eng)
+    rq2_add_launch(eng, b)
+    return rq2_add_collect(eng, b)
