@@ -50,7 +50,7 @@ void rq2_count(fz_ctx *c, const fz_rq2_count_out *o) {
     TmpView V, T;
     filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P,
                 CovTrendRows{t.c_project, t.c_coverage, t.c_valid, t.c_date, o->eligible}, V);
-    filter_view(c, V.row, V.time, V.proj, NC, P, NonZeroTotal{t.c_total}, T);
+    filter_view(c, V.row, V.time, V.proj, NC, P, NonZeroTotal{t.c_total}, T, V.d_n);
 
     int64_t *counts = o->counts;
     int64_t *raw_n = o->raw_n, *n_trend = o->n_trend;

@@ -22,10 +22,12 @@ struct TmpView {
 };
 
 template <typename Pred>
-__global__ __launch_bounds__(kBlock) void k_flag_rows(const int32_t *__restrict__ rows, int64_t n, Pred pred,
+__global__ __launch_bounds__(kBlock) void k_flag_rows(const int32_t *__restrict__ rows, int64_t n,
+                                                      const int64_t *__restrict__ d_live, Pred pred,
                                                       int64_t *__restrict__ flags) {
+    const int64_t live = d_live ? *d_live : n;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
-        flags[i] = pred(rows[i]) ? 1 : 0;
+        flags[i] = (i < live && pred(rows[i])) ? 1 : 0;
 }
 
 __global__ __launch_bounds__(kBlock) void k_compact_view(const int32_t *__restrict__ rows,
@@ -40,10 +42,11 @@ __global__ __launch_bounds__(kBlock) void k_segment_offsets_dn(const uint32_t *_
                                                                const int64_t *__restrict__ d_n, int64_t P,
                                                                int64_t *__restrict__ offsets);
 
-// Rows of src (n rows, in view order) satisfying pred(row) -> dst (same order).
+// Rows of src (n rows, in view order; only the first *src_live when given) satisfying pred(row)
+// -> dst (same order).
 template <typename Pred>
 void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uint32_t *proj, int64_t n, int64_t P,
-                 Pred pred, TmpView &dst) {
+                 Pred pred, TmpView &dst, const int64_t *src_live = nullptr) {
     dst.cap = n;
     dst.d_n = c->arena.get<int64_t>(1);
     dst.row = c->arena.get<int32_t>(n);
@@ -53,7 +56,7 @@ void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uin
     int64_t *flags = c->arena.get<int64_t>(n);
     int64_t *pos = c->arena.get<int64_t>(n);
     if (n > 0) {
-        k_flag_rows<<<grid_for(n, kBlock, 4096), kBlock, 0, c->stream>>>(rows, n, pred, flags);
+        k_flag_rows<<<grid_for(n, kBlock, 4096), kBlock, 0, c->stream>>>(rows, n, src_live, pred, flags);
         FZ_LAUNCH_CHECK();
     }
     scan_exclusive_i64(c, flags, pos, n, dst.d_n);
