@@ -201,6 +201,31 @@ typedef struct fz_rq2_add_out {
 
 int fz_rq2_add(fz_ctx *ctx, const fz_rq2_add_out *out);
 
+/* ---- RQ3: rq3_diff_coverage_at_detection.py:202-360 -------------------------------------- */
+enum { FZ_RQ3_ISSUES = 0, FZ_RQ3_DETECTED, FZ_RQ3_NON_DETECTED, FZ_RQ3_ELIGIBLE, FZ_RQ3_NCOUNTS = 4 };
+enum {
+    FZ_RQ3_AD_DET = 0,            /* anderson(detected).statistic, then 5 critical values   :329 */
+    FZ_RQ3_AD_NON = 6,            /* anderson(non-detected)                                 :335 */
+    FZ_RQ3_LEVENE_W = 12,         /* levene(det, non) (center='median')                     :344 */
+    FZ_RQ3_LEVENE_P,
+    FZ_RQ3_BM_STAT,               /* brunnermunzel(det, non)                                :349 */
+    FZ_RQ3_BM_P,
+    FZ_RQ3_NTESTS = 16
+};
+typedef struct fz_rq3_out {
+    int64_t *counts;              /* [FZ_RQ3_NCOUNTS] */
+    uint8_t *eligible;            /* [n_projects] */
+    double *det_pct;              /* [n_issues] detected: (c1/t1 - c0/t0) * 100            :296-302 */
+    int64_t *det_cov, *det_tot;   /* covered / total line deltas                                   */
+    int64_t *det_project, *det_issue;
+    double *non_pct;              /* [n_cov] non-detected day-to-day changes               :245-257 */
+    int64_t *non_cov, *non_tot;
+    fz_describe *describe;        /* [3] detected pct, non-detected pct, detected total    :25-66 */
+    double *tests;                /* [FZ_RQ3_NTESTS] */
+} fz_rq3_out;
+
+int fz_rq3(fz_ctx *ctx, const fz_rq3_out *out);
+
 /* ---- per-kernel probe (bench.py roofline) ------------------------------------------------ */
 /* Start timing every launch of the named kernel (e.g. "radix_scatter", "elig_hist") with HIP
  * events on the context stream; fz_probe_end synchronises the stream and returns the number of

@@ -32,8 +32,9 @@ def assert_same(ours, ref, path="result", rtol=RTOL):
         for k in ref:
             assert_same(ours[k], ref[k], f"{path}[{k!r}]", rtol)
         return
-    if isinstance(ref, (list, tuple)) and not (len(ref) and isinstance(ref[0], (int, float, np.number))
-                                               and not isinstance(ref[0], bool)):
+    scalar = (int, float, np.number)
+    if isinstance(ref, (list, tuple)) and not (len(ref) and all(isinstance(x, scalar) and not isinstance(x, bool)
+                                                                for x in ref)):
         assert len(ours) == len(ref), f"{path}: len {len(ours)} != {len(ref)}"
         for i, (a, b) in enumerate(zip(ours, ref)):
             assert_same(a, b, f"{path}[{i}]", rtol)

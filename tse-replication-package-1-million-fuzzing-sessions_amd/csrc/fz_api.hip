@@ -12,6 +12,7 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_out *o);
 void eligibility_counts(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *counts);
 void rq2_count(fz_ctx *c, const fz_rq2_count_out *o);
 void rq2_add(fz_ctx *c, const fz_rq2_add_out *o);
+void rq3(fz_ctx *c, const fz_rq3_out *o);
 }  // namespace fz
 
 namespace {
@@ -99,6 +100,10 @@ int fz_rq2_count(fz_ctx *ctx, const fz_rq2_count_out *out) {
 
 int fz_rq2_add(fz_ctx *ctx, const fz_rq2_add_out *out) {
     return guarded(ctx, [&] { fz::rq2_add(ctx, out); });
+}
+
+int fz_rq3(fz_ctx *ctx, const fz_rq3_out *out) {
+    return guarded(ctx, [&] { fz::rq3(ctx, out); });
 }
 
 int fz_probe_begin(fz_ctx *ctx, const char *kernel_name) {

@@ -401,13 +401,23 @@ __global__ void k_describe_finish(const uint64_t *__restrict__ sk, const int64_t
     *out = d;
 }
 
-void describe_f64_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n, fz_describe *dev_out) {
+uint64_t *sorted_keys_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n) {
     const int64_t nn = nmax < 1 ? 1 : nmax;
     uint64_t *k = c->arena.get<uint64_t>(nn);
-    const unsigned g = grid_for(nn, kBlock, 1024);
-    k_f64_keys<<<g, kBlock, 0, c->stream>>>(x, nmax, d_n, k);
+    k_f64_keys<<<grid_for(nn, kBlock, 1024), kBlock, 0, c->stream>>>(x, nmax, d_n, k);
     FZ_LAUNCH_CHECK();
     radix_sort_pairs(c, k, nullptr, nmax, 64);
+    return k;
+}
+
+void describe_f64_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n, fz_describe *dev_out) {
+    describe_sorted_dn(c, sorted_keys_dn(c, x, nmax, d_n), x, nmax, d_n, dev_out);
+}
+
+void describe_sorted_dn(fz_ctx *c, const uint64_t *k, const double *x, int64_t nmax, const int64_t *d_n,
+                        fz_describe *dev_out) {
+    const int64_t nn = nmax < 1 ? 1 : nmax;
+    const unsigned g = grid_for(nn, kBlock, 1024);
     double *part = c->arena.get<double>(2 * g);
     double *ms = c->arena.get<double>(2);
     k_dd_partial<<<g, kBlock, 0, c->stream>>>(x, d_n, nullptr, part);

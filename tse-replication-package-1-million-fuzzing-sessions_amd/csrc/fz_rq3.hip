@@ -1,0 +1,280 @@
+// RQ3 - coverage change on the day after a bug is fixed vs ordinary day-to-day changes
+// (rq3_diff_coverage_at_detection.py:202-360).
+//
+//   per-issue loop with 3 queries per project (:241-302)  -> one thread per issue over three
+//        filtered views: last Fuzzing build before rts (lower_bound), first Coverage build after
+//        rts (upper_bound), coverage pair on day rts+1 (lower_bound on the day)
+//   non-detected flush on project change (:245-257)      -> one thread per coverage row of the
+//        flushed projects, excluded days found by binary search in that project's detections
+//   summary / anderson / levene / brunnermunzel (:25-66, :321-352) -> sorted keys + chunked
+//        double-double reductions + the segmented rank tests (fz_series.hip)
+#include "fz_seg.h"
+#include "fz_stats.h"
+
+namespace fz {
+
+constexpr int64_t kLim3 = 1736294400000000LL;    // '2025-01-08'
+constexpr int64_t kLim3b = 1736380800000000LL;   // '2025-01-09' (rq3:262-263)
+constexpr int64_t kDay3 = 86400000000LL;
+constexpr int64_t kGapUs = 24LL * 3600LL * 1000000LL;
+
+void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count);
+
+__device__ inline int64_t fdiv_day(int64_t a) {
+    const int64_t q = a / kDay3;
+    return (a % kDay3 != 0 && a < 0) ? q - 1 : q;
+}
+
+struct FixedIssuesRq3 {  // status fixed, eligible project, rts < LIMIT (:219-232)
+    const uint32_t *proj;
+    const uint8_t *status;
+    const int64_t *rts;
+    const uint8_t *elig;
+    __device__ bool operator()(int32_t r) const { return status[r] <= 1 && rts[r] < kLim3 && elig[proj[r]]; }
+};
+struct FuzzRq3 {  // Fuzzing, result IN ('HalfWay', 'Finish'), DATE(timecreated) < '2025-01-08' (:260-261)
+    const uint8_t *result;
+    const int64_t *time;
+    __device__ bool operator()(int32_t r) const { return (result[r] == 2 || result[r] == 0) && time[r] < kLim3; }
+};
+struct CovBuildRq3 {  // Coverage, any result, DATE(timecreated) < '2025-01-09' (:262)
+    const int64_t *time;
+    __device__ bool operator()(int32_t r) const { return time[r] < kLim3b; }
+};
+struct CovRowsRq3 {  // covered_line IS NOT NULL AND DATE(date) < '2025-01-09' (:263)
+    const uint8_t *valid;
+    const int64_t *date;
+    __device__ bool operator()(int32_t r) const { return (valid[r] & FZ_VALID_COVERED) && date[r] < kLim3b; }
+};
+
+// anderson(x, dist='norm') from ascending keys: A2 and the 5 rounded critical values.
+static void anderson_sorted(fz_ctx *c, const uint64_t *sk, const double *x, int64_t nmax, const int64_t *d_n,
+                            double *out) {
+    Segs one{1, single_segment(c, d_n), nmax};
+    ChunkedSegs cs = chunked(c, one);
+    double *ms = c->arena.get<double>(4);
+    seg_mean(c, cs, x, ms);  // xbar
+    seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t, double *v) {
+        const double d = x[i] - ms[0];
+        v[0] = d * d;
+    }, ms + 1);
+    seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t, double *v) {
+        const double N = double(*d_n);
+        const double s = sqrt(ms[1] / (N - 1.0));  // np.std(ddof=1)
+        const int64_t n = *d_n;
+        const double wi = (f64_from_key(sk[i]) - ms[0]) / s;
+        const double wj = (f64_from_key(sk[n - 1 - i]) - ms[0]) / s;
+        v[0] = (2.0 * double(i + 1) - 1.0) / N * (stats::log_ndtr(wi) + stats::log_ndtr(-wj));
+    }, ms + 2);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        const double N = double(*d_n);
+        out[0] = -N - ms[2];
+        const double av[5] = {0.576, 0.656, 0.787, 0.918, 1.092};
+        for (int k = 0; k < 5; ++k) out[1 + k] = rint(av[k] / (1.0 + 4.0 / N - 25.0 / N / N) * 1000.0) / 1000.0;
+    });
+}
+
+// levene([x, y], center='median') (scipy _morestats.py levene).
+static void levene_two(fz_ctx *c, const uint64_t *skx, const double *x, int64_t nxm, const int64_t *d_nx,
+                       const uint64_t *sky, const double *y, int64_t nym, const int64_t *d_ny, double *out) {
+    double *med = c->arena.get<double>(2);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        for (int g = 0; g < 2; ++g) {
+            const uint64_t *k = g ? sky : skx;
+            const int64_t n = g ? *d_ny : *d_nx;
+            med[g] = n <= 0 ? NAN
+                            : ((n & 1) ? f64_from_key(k[n / 2])
+                                       : (f64_from_key(k[n / 2 - 1]) + f64_from_key(k[n / 2])) / 2.0);
+        }
+    });
+    double *zb = c->arena.get<double>(2), *dv = c->arena.get<double>(2);
+    Segs sx{1, single_segment(c, d_nx), nxm}, sy{1, single_segment(c, d_ny), nym};
+    ChunkedSegs cx = chunked(c, sx), cy = chunked(c, sy);
+    seg_reduce<1>(c, cx, [=] __device__(int64_t i, int32_t, double *v) { v[0] = fabs(x[i] - med[0]); }, zb);
+    seg_reduce<1>(c, cy, [=] __device__(int64_t i, int32_t, double *v) { v[0] = fabs(y[i] - med[1]); }, zb + 1);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        zb[0] /= double(*d_nx);
+        zb[1] /= double(*d_ny);
+    });
+    seg_reduce<1>(c, cx, [=] __device__(int64_t i, int32_t, double *v) {
+        const double d = fabs(x[i] - med[0]) - zb[0];
+        v[0] = d * d;
+    }, dv);
+    seg_reduce<1>(c, cy, [=] __device__(int64_t i, int32_t, double *v) {
+        const double d = fabs(y[i] - med[1]) - zb[1];
+        v[0] = d * d;
+    }, dv + 1);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        const double nx = double(*d_nx), ny = double(*d_ny), N = nx + ny;
+        double zbar = 0.0;
+        zbar += zb[0] * nx;
+        zbar += zb[1] * ny;
+        zbar /= N;
+        const double numer = (N - 2.0) * (nx * (zb[0] - zbar) * (zb[0] - zbar) + ny * (zb[1] - zbar) * (zb[1] - zbar));
+        double dvar = 0.0;
+        dvar += dv[0];
+        dvar += dv[1];
+        const double W = numer / (1.0 * dvar);
+        out[0] = W;
+        out[1] = stats::f1_sf(W, N - 2.0);
+    });
+}
+
+void rq3(fz_ctx *c, const fz_rq3_out *o) {
+    Store &s = c->store;
+    FZ_CHECK(s.built, "fz_rq3: call fz_store_build first");
+    FZ_CHECK(o && o->counts && o->eligible && o->det_pct && o->det_cov && o->det_tot && o->det_project &&
+                 o->det_issue && o->non_pct && o->non_cov && o->non_tot && o->describe && o->tests,
+             "fz_rq3: null output buffer");
+    const fz_tables &t = s.t;
+    const int64_t P = s.P, NI = s.issues.n, NC = s.cov.n;
+    hipStream_t st = c->stream;
+    int64_t *counts = o->counts;
+    FZ_HIP(hipMemsetAsync(counts, 0, FZ_RQ3_NCOUNTS * 8, st));
+    eligible_projects(c, o->eligible, counts + FZ_RQ3_ELIGIBLE);
+
+    TmpView I, F, CB, TC;
+    filter_view(c, s.issues.row, s.issues.time, s.issues.proj, NI, P,
+                FixedIssuesRq3{t.i_project, t.i_status, t.i_rts, o->eligible}, I);
+    filter_view(c, s.fuzz.row, s.fuzz.time, s.fuzz.proj, s.fuzz.n, P, FuzzRq3{t.b_result, t.b_time}, F);
+    filter_view(c, s.covb.row, s.covb.time, s.covb.proj, s.covb.n, P, CovBuildRq3{t.b_time}, CB);
+    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P, CovRowsRq3{t.c_valid, t.c_date}, TC);
+
+    // ---- detected: one thread per issue (:241-302)
+    int64_t *dflag = c->arena.get<int64_t>(NI);
+    int64_t *dpos = c->arena.get<int64_t>(NI);
+    int64_t *pa = c->arena.get<int64_t>(NI);  // coverage pair (row a, row b)
+    int64_t *pb = c->arena.get<int64_t>(NI);
+    const int32_t *irow = I.row;
+    const uint32_t *iproj = I.proj;
+    const int64_t *irts = I.time;
+    const int64_t *d_ni = I.d_n;
+    const TmpView Fv = F, CBv = CB, TCv = TC;
+    const uint8_t *result = t.b_result;
+    const int64_t *btime = t.b_time;
+    const int32_t *canon = t.b_rev_canon;
+    const int64_t *cvd = t.c_covered, *ctot = t.c_total;
+    map_n(c, NI, nullptr, [=] __device__(int64_t j) {
+        dflag[j] = 0;
+        if (j >= *d_ni) return;
+        const uint32_t p = iproj[j];
+        const int64_t rts = irts[j];
+        const int64_t f0 = Fv.offs[p], f1 = Fv.offs[p + 1];
+        const int64_t b0 = CBv.offs[p], b1 = CBv.offs[p + 1];
+        const int64_t c0 = TCv.offs[p], c1 = TCv.offs[p + 1];
+        if (f0 == f1 || b0 == b1 || c0 == c1) return;
+        const int64_t k = lower_bound_i64(Fv.time, f0, f1, rts) - 1;  // last fuzz build before rts
+        if (k < f0) return;
+        const int64_t k2 = upper_bound_i64(CBv.time, b0, b1, rts);   // first coverage build after rts
+        if (k2 >= b1) return;
+        const int32_t lf = Fv.row[k], fc = CBv.row[k2];
+        if (!(result[fc] == 2 || result[fc] == 0)) return;
+        if (btime[fc] - btime[lf] > kGapUs) return;  // total_seconds()/3600 > 24 (:277)
+        if (canon[lf] < 0 || canon[lf] != canon[fc]) return;
+        const int64_t target = fdiv_day(rts) + 1;
+        int64_t kk = lower_bound_i64(TCv.time, c0, c1, target * kDay3);
+        if (kk < c0 + 1) kk = c0 + 1;  // the reference scans rows i >= 1
+        if (kk >= c1 || fdiv_day(TCv.time[kk]) != target) return;
+        const int32_t ra = TCv.row[kk - 1], rb = TCv.row[kk];
+        if (cvd[rb] == 0) return;      // break without a pair (:291)
+        if (!(ctot[ra] > 0 && ctot[rb] > 0)) return;
+        dflag[j] = 1;
+        pa[j] = ra;
+        pb[j] = rb;
+    });
+    scan_exclusive_i64(c, dflag, dpos, NI, counts + FZ_RQ3_DETECTED);
+    uint32_t *dproj = c->arena.get<uint32_t>(NI);
+    int64_t *dday = c->arena.get<int64_t>(NI);
+    const fz_rq3_out out = *o;
+    map_n(c, NI, nullptr, [=] __device__(int64_t j) {
+        if (!dflag[j]) return;
+        const int64_t q = dpos[j];
+        const int64_t ra = pa[j], rb = pb[j];
+        out.det_pct[q] = (double(cvd[rb]) / double(ctot[rb]) - double(cvd[ra]) / double(ctot[ra])) * 100.0;
+        out.det_cov[q] = cvd[rb] - cvd[ra];
+        out.det_tot[q] = ctot[rb] - ctot[ra];
+        out.det_project[q] = iproj[j];
+        out.det_issue[q] = irow[j];
+        dproj[q] = iproj[j];
+        dday[q] = fdiv_day(irts[j]);
+    });
+    int64_t *doffs = c->arena.get<int64_t>(P + 1);
+    k_segment_offsets_dn<<<grid_for(P + 1, kBlock, 1u << 30), kBlock, 0, st>>>(dproj, counts + FZ_RQ3_DETECTED, P,
+                                                                              doffs);
+    FZ_LAUNCH_CHECK();
+
+    // ---- non-detected: projects with issues, except the last one (never flushed, :245-257)
+    uint8_t *hasiss = c->arena.get<uint8_t>(P);
+    const int64_t *ioffs = I.offs;
+    per_seg(c, P, [=] __device__(int64_t p) {
+        const int64_t n = *d_ni;
+        const uint32_t last = n > 0 ? iproj[n - 1] : 0xffffffffu;
+        hasiss[p] = (ioffs[p + 1] > ioffs[p]) && uint32_t(p) != last;
+    });
+    int64_t *nflag = c->arena.get<int64_t>(NC);
+    int64_t *npos = c->arena.get<int64_t>(NC);
+    map_n(c, NC, nullptr, [=] __device__(int64_t k) {
+        nflag[k] = 0;
+        if (k >= *TCv.d_n) return;
+        const uint32_t p = TCv.proj[k];
+        if (!hasiss[p] || k == TCv.offs[p]) return;
+        const int32_t ra = TCv.row[k - 1], rb = TCv.row[k];
+        const int64_t day = fdiv_day(TCv.time[k]);
+        const int64_t lo = doffs[p], hi = doffs[p + 1];
+        const int64_t q = lower_bound_i64(dday, lo, hi, day);
+        if (q < hi && dday[q] == day) return;  // a detection day of this project
+        if (!(ctot[ra] > 0 && ctot[rb] > 0)) return;
+        nflag[k] = 1;
+    });
+    scan_exclusive_i64(c, nflag, npos, NC, counts + FZ_RQ3_NON_DETECTED);
+    map_n(c, NC, nullptr, [=] __device__(int64_t k) {
+        if (!nflag[k]) return;
+        const int64_t q = npos[k];
+        const int32_t ra = TCv.row[k - 1], rb = TCv.row[k];
+        out.non_pct[q] = (double(cvd[rb]) / double(ctot[rb]) - double(cvd[ra]) / double(ctot[ra])) * 100.0;
+        out.non_cov[q] = cvd[rb] - cvd[ra];
+        out.non_tot[q] = ctot[rb] - ctot[ra];
+    });
+    map_n(c, 1, nullptr, [=] __device__(int64_t) { counts[FZ_RQ3_ISSUES] = *d_ni; });
+
+    // ---- statistics (:321-352)
+    const int64_t *d_nd = counts + FZ_RQ3_DETECTED, *d_nn = counts + FZ_RQ3_NON_DETECTED;
+    double *dtot_f = c->arena.get<double>(NI);
+    const int64_t *dt = o->det_tot;
+    map_n(c, NI, d_nd, [=] __device__(int64_t q) { dtot_f[q] = double(dt[q]); });
+    uint64_t *skd = sorted_keys_dn(c, o->det_pct, NI, d_nd);
+    uint64_t *skn = sorted_keys_dn(c, o->non_pct, NC, d_nn);
+    describe_sorted_dn(c, skd, o->det_pct, NI, d_nd, o->describe);
+    describe_sorted_dn(c, skn, o->non_pct, NC, d_nn, o->describe + 1);
+    describe_f64_dn(c, dtot_f, NI, d_nd, o->describe + 2);
+    anderson_sorted(c, skd, o->det_pct, NI, d_nd, o->tests + FZ_RQ3_AD_DET);
+    anderson_sorted(c, skn, o->non_pct, NC, d_nn, o->tests + FZ_RQ3_AD_NON);
+    levene_two(c, skd, o->det_pct, NI, d_nd, skn, o->non_pct, NC, d_nn, o->tests + FZ_RQ3_LEVENE_W);
+    // brunnermunzel(det, non): one segment holding both samples
+    {
+        const int64_t cap = NI + NC;
+        double *v = c->arena.get<double>(cap);
+        uint8_t *g = c->arena.get<uint8_t>(cap);
+        const double *dp = o->det_pct, *np_ = o->non_pct;
+        map_n(c, cap, nullptr, [=] __device__(int64_t i) {
+            const int64_t nd = *d_nd, nn = *d_nn;
+            if (i < nd) {
+                v[i] = dp[i];
+                g[i] = 0;
+            } else if (i < nd + nn) {
+                v[i] = np_[i - nd];
+                g[i] = 1;
+            }
+        });
+        int64_t *d_all = c->arena.get<int64_t>(1);
+        map_n(c, 1, nullptr, [=] __device__(int64_t) { *d_all = *d_nd + *d_nn; });
+        Segs one{1, single_segment(c, d_all), cap};
+        int32_t *sid = segment_ids(c, one);
+        RankTestOut rt;
+        rt.bm_stat = o->tests + FZ_RQ3_BM_STAT;
+        rt.bm_p = o->tests + FZ_RQ3_BM_P;
+        seg_rank_tests(c, v, g, one, sid, rt);
+    }
+}
+
+}  // namespace fz

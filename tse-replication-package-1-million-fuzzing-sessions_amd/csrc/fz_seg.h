@@ -142,6 +142,9 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
 struct TieRanks {
     double *rank = nullptr;
     double *ngroups = nullptr;
+    int64_t *flag = nullptr;    // 1 at the first element of each tie group
+    int64_t *gid = nullptr;     // exclusive scan of flag (group of element i = gid[i] - 1 + flag[i])
+    int64_t *gstart = nullptr;  // [groups + 1] first element of each group, sentinel offs[S]
 };
 TieRanks seg_tie_ranks(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const double *sorted);
 
@@ -157,6 +160,16 @@ void seg_percentiles(fz_ctx *c, const Segs &sg, const double *sorted, const doub
 void seg_mean(fz_ctx *c, const ChunkedSegs &cs, const double *vals, double *out);
 // statistics.median / np.median of sorted segments: middle value or (a + b) / 2 -> out[S].
 void seg_median(fz_ctx *c, const Segs &sg, const double *sorted, double *out);
+
+// Two-sample rank tests per segment (x = grp 0, y = grp 1): Brunner-Munzel and Mann-Whitney U
+// (asymptotic).  Any output pointer may be null.  All outputs are [S] doubles.
+struct RankTestOut {
+    double *bm_stat = nullptr, *bm_p = nullptr;
+    double *u1 = nullptr, *mwu_p_two = nullptr, *mwu_p_greater = nullptr, *ties = nullptr;
+    double *nx = nullptr, *ny = nullptr;
+};
+void seg_rank_tests(fz_ctx *c, const double *vals, const uint8_t *grp, const Segs &sg, const int32_t *segid,
+                    const RankTestOut &o);
 
 // A device offsets array [0, *d_n] for one segment whose length is known only on the device.
 const int64_t *single_segment(fz_ctx *c, const int64_t *d_n);

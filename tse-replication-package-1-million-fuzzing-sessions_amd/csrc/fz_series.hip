@@ -141,7 +141,100 @@ TieRanks seg_tie_ranks(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, c
         rank[i] = double(a + b + 1) / 2.0 - double(offs[s]);
     });
     seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t, double *x) { x[0] = double(flag[i]); }, tr.ngroups);
+    tr.flag = flag;
+    tr.gid = gid;
+    tr.gstart = gstart;
     return tr;
+}
+
+// ------------------------------------------------------------ two-sample rank tests per segment
+// Each segment holds the x sample (grp 0) and the y sample (grp 1) in any order.
+//   Brunner-Munzel (scipy _stats_py.py brunnermunzel, t distribution, two-sided)
+//   Mann-Whitney U asymptotic (scipy _mannwhitneyu.py: tie term, continuity) two-sided + greater
+void seg_rank_tests(fz_ctx *c, const double *vals, const uint8_t *grp, const Segs &sg, const int32_t *segid,
+                    const RankTestOut &o) {
+    const int64_t n = sg.n_cap, S = sg.S;
+    const int64_t *offs = sg.offs;
+    ChunkedSegs cs = chunked(c, sg);
+    SortedSegs ss = seg_sort_f64(c, vals, sg, segid);
+    TieRanks tr = seg_tie_ranks(c, cs, segid, ss.val);
+    // cx[i] = number of x elements before sorted position i (cx[n] = total)
+    int64_t *isx = c->arena.get<int64_t>(n);
+    int64_t *cx = c->arena.get<int64_t>(n + 1);
+    const int32_t *pos = ss.pos;
+    map_n(c, n, nullptr, [=] __device__(int64_t i) { isx[i] = (i < offs[S] && grp[pos[i]] == 0) ? 1 : 0; });
+    scan_exclusive_i64(c, isx, cx, n, cx + n);
+    // within-sample average rank of every element
+    double *rw = c->arena.get<double>(n);
+    const int64_t *flag = tr.flag, *gid = tr.gid, *gstart = tr.gstart;
+    map_n(c, n, nullptr, [=] __device__(int64_t i) {
+        if (i >= offs[S]) return;
+        const int64_t s = segid[i], s0 = offs[s];
+        const int64_t g = gid[i] - 1 + flag[i];
+        const int64_t a = gstart[g], b = gstart[g + 1];
+        const int64_t xb = cx[a] - cx[s0], xg = cx[b] - cx[a];
+        const int64_t yb = (a - s0) - xb, yg = (b - a) - xg;
+        rw[i] = isx[i] ? double(xb) + double(xg + 1) / 2.0 : double(yb) + double(yg + 1) / 2.0;
+    });
+    const double *rc = tr.rank;
+    double *s1 = c->arena.get<double>(S * 6);
+    seg_reduce<6>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
+        const bool xs = isx[i];
+        x[0] = xs ? rc[i] : 0.0;
+        x[1] = xs ? 0.0 : rc[i];
+        x[2] = xs ? 1.0 : 0.0;
+        x[3] = xs ? 0.0 : 1.0;
+        // tie term t^3 - t (int64-exact), split into two exactly representable halves
+        int64_t tt = 0;
+        if (flag[i]) {
+            const int64_t g = gid[i];
+            const int64_t t = gstart[g + 1] - gstart[g];
+            tt = t * t * t - t;
+        }
+        x[4] = double(tt & ~int64_t((1 << 26) - 1));
+        x[5] = double(tt & int64_t((1 << 26) - 1));
+    }, s1);
+    double *s2 = c->arena.get<double>(S * 2);
+    seg_reduce<2>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
+        const double nx = s1[6 * s + 2], ny = s1[6 * s + 3];
+        const bool xs = isx[i];
+        const double cm = xs ? s1[6 * s] / nx : s1[6 * s + 1] / ny;  // np.mean(rankcx) / (rankcy)
+        const double wm = xs ? (nx + 1.0) / 2.0 : (ny + 1.0) / 2.0;  // np.mean(rankx) (exact)
+        const double d = ((rc[i] - rw[i]) - cm) + wm;
+        x[0] = xs ? d * d : 0.0;
+        x[1] = xs ? 0.0 : d * d;
+    }, s2);
+    per_seg(c, S, [=] __device__(int64_t s) {
+        const double nx = s1[6 * s + 2], ny = s1[6 * s + 3];
+        const double rcx = s1[6 * s] / nx, rcy = s1[6 * s + 1] / ny;
+        const double Sx = s2[2 * s] / (nx - 1.0), Sy = s2[2 * s + 1] / (ny - 1.0);
+        double w = nx * ny * (rcy - rcx);
+        w /= (nx + ny) * sqrt(nx * Sx + ny * Sy);
+        const double num = (nx * Sx + ny * Sy) * (nx * Sx + ny * Sy);
+        const double den = (nx * Sx) * (nx * Sx) / (nx - 1.0) + (ny * Sy) * (ny * Sy) / (ny - 1.0);
+        const double df = num / den;
+        if (o.bm_stat) o.bm_stat[s] = w;
+        if (o.bm_p) o.bm_p[s] = 2.0 * stats::t_sf(fabs(w), df);
+        if (o.nx) o.nx[s] = nx;
+        if (o.ny) o.ny[s] = ny;
+        // Mann-Whitney U (x vs y)
+        const double R1 = s1[6 * s];
+        const double U1 = R1 - nx * (nx + 1.0) / 2.0;
+        const double U2 = nx * ny - U1;
+        const double nn = nx + ny;
+        const double tie = s1[6 * s + 4] + s1[6 * s + 5];
+        const double mu = nx * ny / 2.0;
+        const double sd = sqrt(nx * ny / 12.0 * ((nn + 1.0) - tie / (nn * (nn - 1.0))));
+        if (o.u1) o.u1[s] = U1;
+        auto pv = [&](double U, double f) {
+            const double z = (U - mu - 0.5) / sd;
+            double p = stats::norm_sf(z) * f;
+            return p < 0.0 ? 0.0 : (p > 1.0 ? 1.0 : p);
+        };
+        if (o.mwu_p_two) o.mwu_p_two[s] = pv(U1 > U2 ? U1 : U2, 2.0);
+        if (o.mwu_p_greater) o.mwu_p_greater[s] = pv(U1, 1.0);
+        if (o.ties) o.ties[s] = tie;
+    });
 }
 
 // --------------------------------------------------------------------- Spearman vs index

@@ -82,6 +82,16 @@ class FzRq2AddOut(C.Structure):
                                   "covered_is_float", "total_is_float")]
 
 
+FZ_RQ3_NCOUNTS, FZ_RQ3_NTESTS = 4, 16
+RQ3_ISSUES, RQ3_DETECTED, RQ3_NON_DETECTED, RQ3_ELIGIBLE = range(4)
+RQ3_AD_DET, RQ3_AD_NON, RQ3_LEVENE_W, RQ3_LEVENE_P, RQ3_BM_STAT, RQ3_BM_P = 0, 6, 12, 13, 14, 15
+
+
+class FzRq3Out(C.Structure):
+    _fields_ = [(n, _P) for n in ("counts", "eligible", "det_pct", "det_cov", "det_tot", "det_project", "det_issue",
+                                  "non_pct", "non_cov", "non_tot", "describe", "tests")]
+
+
 # every symbol include/fz.h declares, with its ctypes signature
 SIGNATURES = {
     "fz_abi_version": (C.c_int, []),
@@ -93,6 +103,7 @@ SIGNATURES = {
     "fz_rq1": (C.c_int, [_P, _I64, C.POINTER(FzRq1Out)]),
     "fz_rq2_count": (C.c_int, [_P, C.POINTER(FzRq2CountOut)]),
     "fz_rq2_add": (C.c_int, [_P, C.POINTER(FzRq2AddOut)]),
+    "fz_rq3": (C.c_int, [_P, C.POINTER(FzRq3Out)]),
     "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),
     "fz_probe_end": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "fz_radix_sort_u64": (C.c_int, [_P, _P, _P, _I64, C.c_int]),

@@ -11,7 +11,7 @@ import ctypes as C
 import numpy as np
 
 from .. import engine as E
-from .results import Describe, RQ1Result, RQ2AddResult, RQ2CountResult
+from .results import Describe, RQ1Result, RQ2AddResult, RQ2CountResult, RQ3Result
 
 
 def _describe(d: E.FzDescribe, with_min_nonzero=False) -> Describe:
@@ -168,3 +168,46 @@ def rq2_add(eng: E.Engine) -> RQ2AddResult:
     b = rq2_add_buffers(eng)
     rq2_add_launch(eng, b)
     return rq2_add_collect(eng, b)
+
+
+# ------------------------------------------------------------------------------------------ RQ3
+def rq3_buffers(eng: E.Engine) -> OutBuffers:
+    torch = eng.torch
+    fz = eng.tables.fz
+    P, NI, NC = fz.n_projects, fz.n_issues, fz.n_cov
+    f64, i64, u8 = torch.float64, torch.int64, torch.uint8
+    return OutBuffers(eng, E.FzRq3Out, [
+        ("counts", E.FZ_RQ3_NCOUNTS, i64), ("eligible", P, u8), ("det_pct", NI, f64), ("det_cov", NI, i64),
+        ("det_tot", NI, i64), ("det_project", NI, i64), ("det_issue", NI, i64), ("non_pct", NC, f64),
+        ("non_cov", NC, i64), ("non_tot", NC, i64), ("describe", 3 * E.DESCRIBE_DOUBLES, f64),
+        ("tests", E.FZ_RQ3_NTESTS, f64)])
+
+
+def rq3_launch(eng: E.Engine, b: OutBuffers):
+    E._check(eng.lib, eng.lib.fz_rq3(eng.ctx, C.byref(b.out)))
+
+
+def rq3_collect(eng: E.Engine, b: OutBuffers) -> RQ3Result:
+    cnt = b.host("counts")
+    nd, nn = int(cnt[E.RQ3_DETECTED]), int(cnt[E.RQ3_NON_DETECTED])
+    desc = b.host("describe").reshape(3, E.DESCRIBE_DOUBLES)
+    ts = b.host("tests")
+    both = nd > 0 and nn > 0
+    return RQ3Result(
+        n_all_issues=int(cnt[E.RQ3_ISSUES]), det_pct=b.host("det_pct", nd), det_cov=b.host("det_cov", nd),
+        det_tot=b.host("det_tot", nd), det_project=b.host("det_project", nd), det_issue=b.host("det_issue", nd),
+        non_pct=b.host("non_pct", nn), non_cov=b.host("non_cov", nn), non_tot=b.host("non_tot", nn),
+        desc_detected=_describe(E.describe_from_doubles(desc[0])) if nd else None,
+        desc_non=_describe(E.describe_from_doubles(desc[1])) if nn else None,
+        desc_det_total=_describe(E.describe_from_doubles(desc[2])) if nd else None,
+        anderson_det=(float(ts[E.RQ3_AD_DET]), ts[E.RQ3_AD_DET + 1:E.RQ3_AD_DET + 6].copy()) if both else None,
+        anderson_non=(float(ts[E.RQ3_AD_NON]), ts[E.RQ3_AD_NON + 1:E.RQ3_AD_NON + 6].copy()) if both else None,
+        levene=(float(ts[E.RQ3_LEVENE_W]), float(ts[E.RQ3_LEVENE_P])) if both else None,
+        brunnermunzel=(float(ts[E.RQ3_BM_STAT]), float(ts[E.RQ3_BM_P])) if both else None)
+
+
+def rq3(eng: E.Engine) -> RQ3Result:
+    """rq3_diff_coverage_at_detection.main's analysis (rq3_diff_coverage_at_detection.py:202-360)."""
+    b = rq3_buffers(eng)
+    rq3_launch(eng, b)
+    return rq3_collect(eng, b)
