@@ -226,6 +226,75 @@ typedef struct fz_rq3_out {
 
 int fz_rq3(fz_ctx *ctx, const fz_rq3_out *out);
 
+/* ---- RQ4 inputs: data/processed_data/csv/project_corpus_analysis.csv (user_corpus.py:225-233) ---
+ * Parsed on the host (it is a ~1k-row CSV) into per-project columns, independent of eligibility:
+ *   member[p]   bit g (g = 0..3) set when some CSV row puts p in G(g+1) (rq4a_bug.py:94-108:
+ *               time_elapsed_seconds NaN -> G1, == 0 -> G2, (0, 7 d) -> G3, >= 7 d -> G4);
+ *               bit 4 when p has no CSV row at all (rq4a adds eligible ones to G1, :110-113)
+ *   corpus_us[p]  corpus_commit_time as UTC microseconds (pd.to_datetime(utc=True)), FZ_TS_NULL if none
+ *   order[k]    project of the k-th CSV row with a non-NaN time_elapsed_seconds (rq4b :216, :744) */
+typedef struct fz_rq4_groups {
+    const uint8_t *member;
+    const int64_t *corpus_us;
+    const int32_t *order;
+    int64_t n_order;
+} fz_rq4_groups;
+
+/* ---- RQ4a: rq4a_bug.py:653-884 ----------------------------------------------------------- */
+enum {
+    FZ_RQ4A_MAX_ITER = 0,        /* length of the G1/G2 iteration tables                          */
+    FZ_RQ4A_ROWS,                /* iterations where both totals >= 100 (a prefix)         :164-193 */
+    FZ_RQ4A_G1, FZ_RQ4A_G2, FZ_RQ4A_G3, FZ_RQ4A_G4,   /* group sizes (eligible)                    */
+    FZ_RQ4A_HAS_WINDOW,          /* some G4 project had a full pre/post window             :374-401 */
+    FZ_RQ4A_AFTER_G1, FZ_RQ4A_AFTER_G2, /* rates after the first < 5 %                     :698-747 */
+    FZ_RQ4A_INTRO_POS,           /* G4 projects with introduction iteration > 0             :277-285 */
+    FZ_RQ4A_NCOUNTS = 12
+};
+enum {
+    FZ_RQ4A_AFTER_G1_MEDIAN = 0, FZ_RQ4A_AFTER_G1_IQR, FZ_RQ4A_AFTER_G2_MEDIAN, FZ_RQ4A_AFTER_G2_IQR,
+    FZ_RQ4A_INTRO_MEAN, FZ_RQ4A_INTRO_MEDIAN, FZ_RQ4A_INTRO_MIN, FZ_RQ4A_INTRO_MAX,
+    FZ_RQ4A_PRE_RATE, FZ_RQ4A_POST_RATE, FZ_RQ4A_NSCALARS = 12
+};
+typedef struct fz_rq4a_out {
+    int64_t *counts;             /* [FZ_RQ4A_NCOUNTS] */
+    double *scalars;             /* [FZ_RQ4A_NSCALARS] */
+    uint8_t *eligible;           /* [n_projects] */
+    uint8_t *member;             /* [n_projects] bit g: project in G(g+1) (eligible, rq4a rules) */
+    int64_t *g1_total, *g1_det, *g2_total, *g2_det;  /* [max_fuzz_per_project]       :302-346 */
+    int64_t *intro;              /* [n_projects] G4 introduction iteration, -1 n/a       :246-299 */
+    int64_t *g4_steps;           /* [15 * 2] (projects, detected) at step s = -7..7 -> (s + 7) */
+    int64_t *g4_transition;      /* [4] pre&post, pre only, post only, neither            :806-841 */
+} fz_rq4a_out;
+
+int fz_rq4a(fz_ctx *ctx, const fz_rq4_groups *groups, const fz_rq4a_out *out);
+
+/* ---- RQ4b: rq4b_coverage.py:1209-1261 ---------------------------------------------------- */
+enum {
+    FZ_RQ4B_SESSIONS = 0,        /* longest G1/G2 coverage series                          :917-936 */
+    FZ_RQ4B_LAST,                /* last session with both groups >= 100 values, -1 none   :849-860 */
+    FZ_RQ4B_DELTA_PROJECTS,      /* G3/G4 projects with 7 + 7 coverage points              :725-797 */
+    FZ_RQ4B_INIT_G2, FZ_RQ4B_INIT_G1,  /* initial-coverage sample sizes                    :221-246 */
+    FZ_RQ4B_G1, FZ_RQ4B_G2, FZ_RQ4B_G3, FZ_RQ4B_G4,
+    FZ_RQ4B_NCOUNTS = 12
+};
+enum { FZ_RQ4B_MWU_P = 0, FZ_RQ4B_CLIFF, FZ_RQ4B_BM_STAT, FZ_RQ4B_BM_P, FZ_RQ4B_LEVENE_W, FZ_RQ4B_LEVENE_P,
+       FZ_RQ4B_NTESTS = 8 };
+typedef struct fz_rq4b_out {
+    int64_t *counts;             /* [FZ_RQ4B_NCOUNTS] */
+    uint8_t *eligible;           /* [n_projects] */
+    uint8_t *member;             /* [n_projects] bit g: project in G(g+1) (eligible, rq4b rules) */
+    int64_t *c2, *c1;            /* [max_cov_per_project] values per session index, G2 / G1 */
+    double *g2_q, *g1_q;         /* [max_cov_per_project * 3] np.percentile 25/50/75        :966-972 */
+    double *p_bm;                /* [max_cov_per_project] brunnermunzel p, NaN if a side < 5 :978-985 */
+    double *spearman6;           /* [12] (rho, p): G1 Q1, Med, Q3, G2 Q1, Med, Q3            :879-899 */
+    double *pre_cov, *post_cov;  /* [7 * n_projects] step-major: step i occupies [i*n, i*n+n)  */
+    double *pre_median, *post_median; /* [7]                                              :1061-1085 */
+    double *init_g2, *init_g1;   /* [n_projects] first coverage per project (sorted ids)   :221-246 */
+    double *tests;               /* [FZ_RQ4B_NTESTS] MWU p, Cliff delta, BM, Levene        :248-313 */
+} fz_rq4b_out;
+
+int fz_rq4b(fz_ctx *ctx, const fz_rq4_groups *groups, const fz_rq4b_out *out);
+
 /* ---- per-kernel probe (bench.py roofline) ------------------------------------------------ */
 /* Start timing every launch of the named kernel (e.g. "radix_scatter", "elig_hist") with HIP
  * events on the context stream; fz_probe_end synchronises the stream and returns the number of

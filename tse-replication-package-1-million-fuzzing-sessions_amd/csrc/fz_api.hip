@@ -13,6 +13,8 @@ void eligibility_counts(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *c
 void rq2_count(fz_ctx *c, const fz_rq2_count_out *o);
 void rq2_add(fz_ctx *c, const fz_rq2_add_out *o);
 void rq3(fz_ctx *c, const fz_rq3_out *o);
+void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o);
+void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o);
 }  // namespace fz
 
 namespace {
@@ -104,6 +106,14 @@ int fz_rq2_add(fz_ctx *ctx, const fz_rq2_add_out *out) {
 
 int fz_rq3(fz_ctx *ctx, const fz_rq3_out *out) {
     return guarded(ctx, [&] { fz::rq3(ctx, out); });
+}
+
+int fz_rq4a(fz_ctx *ctx, const fz_rq4_groups *groups, const fz_rq4a_out *out) {
+    return guarded(ctx, [&] { fz::rq4a(ctx, groups, out); });
+}
+
+int fz_rq4b(fz_ctx *ctx, const fz_rq4_groups *groups, const fz_rq4b_out *out) {
+    return guarded(ctx, [&] { fz::rq4b(ctx, groups, out); });
 }
 
 int fz_probe_begin(fz_ctx *ctx, const char *kernel_name) {

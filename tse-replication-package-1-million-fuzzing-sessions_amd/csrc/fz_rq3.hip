@@ -74,52 +74,6 @@ static void anderson_sorted(fz_ctx *c, const uint64_t *sk, const double *x, int6
     });
 }
 
-// levene([x, y], center='median') (scipy _morestats.py levene).
-static void levene_two(fz_ctx *c, const uint64_t *skx, const double *x, int64_t nxm, const int64_t *d_nx,
-                       const uint64_t *sky, const double *y, int64_t nym, const int64_t *d_ny, double *out) {
-    double *med = c->arena.get<double>(2);
-    map_n(c, 1, nullptr, [=] __device__(int64_t) {
-        for (int g = 0; g < 2; ++g) {
-            const uint64_t *k = g ? sky : skx;
-            const int64_t n = g ? *d_ny : *d_nx;
-            med[g] = n <= 0 ? NAN
-                            : ((n & 1) ? f64_from_key(k[n / 2])
-                                       : (f64_from_key(k[n / 2 - 1]) + f64_from_key(k[n / 2])) / 2.0);
-        }
-    });
-    double *zb = c->arena.get<double>(2), *dv = c->arena.get<double>(2);
-    Segs sx{1, single_segment(c, d_nx), nxm}, sy{1, single_segment(c, d_ny), nym};
-    ChunkedSegs cx = chunked(c, sx), cy = chunked(c, sy);
-    seg_reduce<1>(c, cx, [=] __device__(int64_t i, int32_t, double *v) { v[0] = fabs(x[i] - med[0]); }, zb);
-    seg_reduce<1>(c, cy, [=] __device__(int64_t i, int32_t, double *v) { v[0] = fabs(y[i] - med[1]); }, zb + 1);
-    map_n(c, 1, nullptr, [=] __device__(int64_t) {
-        zb[0] /= double(*d_nx);
-        zb[1] /= double(*d_ny);
-    });
-    seg_reduce<1>(c, cx, [=] __device__(int64_t i, int32_t, double *v) {
-        const double d = fabs(x[i] - med[0]) - zb[0];
-        v[0] = d * d;
-    }, dv);
-    seg_reduce<1>(c, cy, [=] __device__(int64_t i, int32_t, double *v) {
-        const double d = fabs(y[i] - med[1]) - zb[1];
-        v[0] = d * d;
-    }, dv + 1);
-    map_n(c, 1, nullptr, [=] __device__(int64_t) {
-        const double nx = double(*d_nx), ny = double(*d_ny), N = nx + ny;
-        double zbar = 0.0;
-        zbar += zb[0] * nx;
-        zbar += zb[1] * ny;
-        zbar /= N;
-        const double numer = (N - 2.0) * (nx * (zb[0] - zbar) * (zb[0] - zbar) + ny * (zb[1] - zbar) * (zb[1] - zbar));
-        double dvar = 0.0;
-        dvar += dv[0];
-        dvar += dv[1];
-        const double W = numer / (1.0 * dvar);
-        out[0] = W;
-        out[1] = stats::f1_sf(W, N - 2.0);
-    });
-}
-
 void rq3(fz_ctx *c, const fz_rq3_out *o) {
     Store &s = c->store;
     FZ_CHECK(s.built, "fz_rq3: call fz_store_build first");

@@ -1,0 +1,465 @@
+// RQ4 - seed-corpus groups (rq4a_bug.py: bug detection; rq4b_coverage.py: coverage).
+//
+// Groups come from project_corpus_analysis.csv, parsed on the host into per-project columns
+// (fz_rq4_groups, see fz.h); everything per build / issue / coverage row runs here:
+//   rq4a  G1/G2 per-iteration tables (:302-346)        -> histogram + reverse scan; distinct
+//         (iteration, project) by adjacency in (project, rts) order
+//         G4 pre/post windows + introduction (:246-412) -> one thread per G4 project, issue counts
+//         in [t_k, t_k+1) by two lower_bounds
+//   rq4b  per-session quartiles + Brunner-Munzel (:910-1015) -> radix transpose to
+//         (session, group, project) order, segmented sorts, segmented rank tests
+//         coverage deltas around the corpus date (:725-797), initial-coverage MWU / Cliff /
+//         BM / Levene (:221-313)                        -> per-project binary searches + rank tests
+#include "fz_seg.h"
+#include "fz_stats.h"
+
+namespace fz {
+
+constexpr int64_t kLim4 = 1736294400000000LL;  // '2025-01-08'
+constexpr int64_t kDay4 = 86400000000LL;
+constexpr int kWin = 7;                         // ANALYSIS_ITERATIONS / DAYS_THRESHOLD (rq4a:43-46)
+
+void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count);
+
+__device__ inline int64_t fdiv4(int64_t a, int64_t b) {
+    const int64_t q = a / b;
+    return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
+}
+
+struct BuildsBeforeLimit {  // get_project_fuzzing_builds: Fuzzing, any result, timecreated < LIMIT (rq4a:124-137)
+    const int64_t *time;
+    __device__ bool operator()(int32_t r) const { return time[r] < kLim4; }
+};
+struct FixedBeforeLimit {  // get_project_fixed_issues: Fixed*, rts < LIMIT (rq4a:140-153)
+    const uint8_t *status;
+    const int64_t *rts;
+    __device__ bool operator()(int32_t r) const { return status[r] <= 1 && rts[r] < kLim4; }
+};
+
+// eligible group membership; rq4a (missing_to_g1) also puts CSV-missing eligible projects in G1
+static void group_members(fz_ctx *c, const fz_rq4_groups *g, const uint8_t *elig, uint8_t *member,
+                          int64_t *counts4, bool missing_to_g1) {
+    const uint8_t *m = g->member;
+    const int64_t P = c->store.P;
+    per_seg(c, P, [=] __device__(int64_t p) {
+        uint8_t b = 0;
+        if (elig[p]) {
+            b = m[p] & 0xF;
+            if (missing_to_g1 && (m[p] & 0x10)) b |= 1;
+        }
+        member[p] = b;
+        for (int k = 0; k < 4; ++k)
+            if (b & (1 << k)) atomic_add_i64(&counts4[k], 1);
+    });
+}
+
+// ------------------------------------------------------------------------------------ RQ4a
+void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
+    Store &s = c->store;
+    FZ_CHECK(s.built, "fz_rq4a: call fz_store_build first");
+    FZ_CHECK(g && g->member && g->corpus_us, "fz_rq4a: null groups");
+    FZ_CHECK(o && o->counts && o->scalars && o->eligible && o->member && o->g1_total && o->g1_det && o->g2_total &&
+                 o->g2_det && o->intro && o->g4_steps && o->g4_transition,
+             "fz_rq4a: null output buffer");
+    const fz_tables &t = s.t;
+    const int64_t P = s.P, M = s.fuzz.max_seg, NI = s.issues.n;
+    const int64_t MM = M > 0 ? M : 1;
+    hipStream_t st = c->stream;
+    int64_t *counts = o->counts;
+    double *sc = o->scalars;
+    FZ_HIP(hipMemsetAsync(counts, 0, FZ_RQ4A_NCOUNTS * 8, st));
+    for (int64_t *a : {o->g1_total, o->g1_det, o->g2_total, o->g2_det}) FZ_HIP(hipMemsetAsync(a, 0, MM * 8, st));
+    FZ_HIP(hipMemsetAsync(o->intro, 0xff, size_t(P > 0 ? P : 1) * 8, st));
+    FZ_HIP(hipMemsetAsync(o->g4_steps, 0, 30 * 8, st));
+    FZ_HIP(hipMemsetAsync(o->g4_transition, 0, 4 * 8, st));
+    int64_t *scratch = c->arena.get<int64_t>(4);
+    eligible_projects(c, o->eligible, scratch);
+    group_members(c, g, o->eligible, o->member, counts + FZ_RQ4A_G1, true);
+    const uint8_t *member = o->member;
+
+    TmpView FB, FI;
+    filter_view(c, s.fuzz.row, s.fuzz.time, s.fuzz.proj, s.fuzz.n, P, BuildsBeforeLimit{t.b_time}, FB);
+    filter_view(c, s.issues.row, s.issues.time, s.issues.proj, NI, P, FixedBeforeLimit{t.i_status, t.i_rts}, FI);
+    const int64_t *fboffs = FB.offs, *fbtime = FB.time, *fioffs = FI.offs, *fitime = FI.time;
+
+    // totals[i] += 1 for i = 1..#builds, per group (:339-340)
+    int64_t *hist = c->arena.get<int64_t>(2 * (M + 1));
+    FZ_HIP(hipMemsetAsync(hist, 0, size_t(2 * (M + 1)) * 8, st));
+    per_seg(c, P, [=] __device__(int64_t p) {
+        const int64_t nb = fboffs[p + 1] - fboffs[p];
+        const uint8_t b = member[p];
+        if (nb <= 0) return;
+        for (int k = 0; k < 2; ++k)
+            if (b & (1 << k)) {
+                atomic_add_i64(&hist[k * (M + 1) + nb], 1);
+                atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ4A_MAX_ITER]), (unsigned long long)nb);
+            }
+    });
+    int64_t *rev = c->arena.get<int64_t>(MM), *rex = c->arena.get<int64_t>(MM);
+    for (int k = 0; k < 2; ++k) {
+        const int64_t *h = hist + k * (M + 1);
+        int64_t *tot = k == 0 ? o->g1_total : o->g2_total;
+        if (M <= 0) break;
+        map_n(c, M, nullptr, [=] __device__(int64_t j) { rev[j] = h[M - j]; });
+        scan_exclusive_i64(c, rev, rex, M, nullptr);
+        map_n(c, M, nullptr, [=] __device__(int64_t i0) { tot[i0] = rex[M - (i0 + 1)] + rev[M - (i0 + 1)]; });
+    }
+    // detected[k] |= {p}: k = #builds < issue time (:341-346), distinct per (k, p)
+    int64_t *kk = c->arena.get<int64_t>(NI);
+    const uint32_t *fiproj = FI.proj;
+    const int64_t *d_nfi = FI.d_n;
+    map_n(c, NI, d_nfi, [=] __device__(int64_t j) {
+        const uint32_t p = fiproj[j];
+        const int64_t lo = fboffs[p], hi = fboffs[p + 1];
+        kk[j] = (member[p] & 3) ? lower_bound_i64(fbtime, lo, hi, fitime[j]) - lo : 0;
+    });
+    int64_t *g1d = o->g1_det, *g2d = o->g2_det;
+    map_n(c, NI, d_nfi, [=] __device__(int64_t j) {
+        const int64_t k = kk[j];
+        if (k <= 0) return;
+        const uint32_t p = fiproj[j];
+        if (j > 0 && fiproj[j - 1] == p && kk[j - 1] == k) return;
+        if (member[p] & 1) atomic_add_i64(&g1d[k - 1], 1);
+        if (member[p] & 2) atomic_add_i64(&g2d[k - 1], 1);
+    });
+
+    // rows with both totals >= 100 (a prefix), rates, first rate < 5, after-slices (:156-207, :698-747)
+    const int64_t *g1t = o->g1_total, *g2t = o->g2_total;
+    double *rates = c->arena.get<double>(2 * MM);
+    int64_t *first = c->arena.get<int64_t>(2);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) { first[0] = first[1] = INT64_MAX; });
+    map_n(c, M, nullptr, [=] __device__(int64_t i) {
+        const int64_t a = g1t[i], b = g2t[i];
+        if (a < 100 || b < 100) return;
+        atomic_add_i64(&counts[FZ_RQ4A_ROWS], 1);
+        const double r1 = a > 0 ? double(g1d[i]) / double(a) * 100.0 : 0.0;
+        const double r2 = b > 0 ? double(g2d[i]) / double(b) * 100.0 : 0.0;
+        rates[i] = r1;
+        rates[MM + i] = r2;
+        if (r1 < 5.0) atomicMin(reinterpret_cast<unsigned long long *>(&first[0]), (unsigned long long)i);
+        if (r2 < 5.0) atomicMin(reinterpret_cast<unsigned long long *>(&first[1]), (unsigned long long)i);
+    });
+    int64_t *nafter = counts + FZ_RQ4A_AFTER_G1;
+    double *after = c->arena.get<double>(2 * MM);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        const int64_t K = counts[FZ_RQ4A_ROWS];
+        for (int k = 0; k < 2; ++k) {
+            const int64_t f = first[k] == INT64_MAX ? K : first[k];
+            nafter[k] = K - f;
+            first[k] = f;
+        }
+    });
+    map_n(c, 2 * MM, nullptr, [=] __device__(int64_t i) {
+        const int k = i >= MM;
+        const int64_t j = i - k * MM;
+        if (j < nafter[k]) after[k * MM + j] = rates[k * MM + first[k] + j];
+    });
+    fz_describe *dsc = c->arena.get<fz_describe>(3);
+    describe_f64_dn(c, after, MM, nafter, dsc);
+    describe_f64_dn(c, after + MM, MM, nafter + 1, dsc + 1);
+
+    // G4: introduction iteration and pre/post windows (:246-299, :350-412)
+    const int64_t *cus = g->corpus_us;
+    int64_t *intro = o->intro, *steps = o->g4_steps, *trans = o->g4_transition;
+    per_seg(c, P, [=] __device__(int64_t p) {
+        if (!(member[p] & 8) || cus[p] == FZ_TS_NULL) return;
+        const int64_t ct = cus[p];
+        const int64_t lo = fboffs[p], hi = fboffs[p + 1], nb = hi - lo;
+        const int64_t npre = lower_bound_i64(fbtime, lo, hi, ct) - lo;
+        intro[p] = npre;
+        if (npre > 0) atomic_add_i64(&counts[FZ_RQ4A_INTRO_POS], 1);
+        if (npre == 0) return;
+        const int64_t idx = npre - 1;
+        if (idx - (kWin - 1) < 0 || idx + kWin >= nb - 1) return;
+        counts[FZ_RQ4A_HAS_WINDOW] = 1;
+        const int64_t i0 = fioffs[p], i1 = fioffs[p + 1];
+        auto any = [&](int64_t a, int64_t b) {  // some issue T with a <= T < b
+            return lower_bound_i64(fitime, i0, i1, b) > lower_bound_i64(fitime, i0, i1, a);
+        };
+        bool pre = false, post = false;
+        for (int k = 1; k <= kWin; ++k) {
+            const bool d1 = any(fbtime[lo + idx - (k - 1)], fbtime[lo + idx - (k - 1) + 1]);
+            atomic_add_i64(&steps[2 * (kWin - k)], 1);
+            if (d1) atomic_add_i64(&steps[2 * (kWin - k) + 1], 1);
+            pre |= d1;
+            const bool d2 = any(fbtime[lo + idx + k], fbtime[lo + idx + k + 1]);
+            atomic_add_i64(&steps[2 * (kWin + k)], 1);
+            if (d2) atomic_add_i64(&steps[2 * (kWin + k) + 1], 1);
+            post |= d2;
+        }
+        atomic_add_i64(&trans[(pre && post) ? 0 : pre ? 1 : post ? 2 : 3], 1);
+    });
+    // introduction-iteration stats over the positive ones (pandas Series mean/median/min/max)
+    int64_t *pf = c->arena.get<int64_t>(P), *pp = c->arena.get<int64_t>(P), *d_np = c->arena.get<int64_t>(1);
+    double *iv = c->arena.get<double>(P);
+    map_n(c, P, nullptr, [=] __device__(int64_t p) { pf[p] = intro[p] > 0 ? 1 : 0; });
+    scan_exclusive_i64(c, pf, pp, P, d_np);
+    map_n(c, P, nullptr, [=] __device__(int64_t p) {
+        if (pf[p]) iv[pp[p]] = double(intro[p]);
+    });
+    describe_f64_dn(c, iv, P, d_np, dsc + 2);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        sc[FZ_RQ4A_AFTER_G1_MEDIAN] = dsc[0].median;
+        sc[FZ_RQ4A_AFTER_G1_IQR] = dsc[0].q3 - dsc[0].q1;
+        sc[FZ_RQ4A_AFTER_G2_MEDIAN] = dsc[1].median;
+        sc[FZ_RQ4A_AFTER_G2_IQR] = dsc[1].q3 - dsc[1].q1;
+        sc[FZ_RQ4A_INTRO_MEAN] = dsc[2].mean;
+        sc[FZ_RQ4A_INTRO_MEDIAN] = dsc[2].median;
+        sc[FZ_RQ4A_INTRO_MIN] = dsc[2].min;
+        sc[FZ_RQ4A_INTRO_MAX] = dsc[2].max;
+        int64_t pn = 0, pd = 0, qn = 0, qd = 0;
+        for (int k = 1; k <= kWin; ++k) {
+            pn += steps[2 * (kWin - k)];
+            pd += steps[2 * (kWin - k) + 1];
+            qn += steps[2 * (kWin + k)];
+            qd += steps[2 * (kWin + k) + 1];
+        }
+        sc[FZ_RQ4A_PRE_RATE] = pn ? double(pd) / double(pn) * 100.0 : 0.0;
+        sc[FZ_RQ4A_POST_RATE] = qn ? double(qd) / double(qn) * 100.0 : 0.0;
+    });
+}
+
+// ------------------------------------------------------------------------------------ RQ4b
+struct FullTrendRows {  // get_full_coverage_trend: coverage > 0, date < LIMIT (rq4b:315-326), G1/G2 only
+    const uint32_t *proj;
+    const double *cov;
+    const uint8_t *valid;
+    const int64_t *date;
+    const uint8_t *member;
+    __device__ bool operator()(int32_t r) const {
+        return (valid[r] & FZ_VALID_COVERAGE) && cov[r] > 0.0 && date[r] < kLim4 && (member[proj[r]] & 3);
+    }
+};
+struct PositiveCoverage34 {  // get_coverage_deltas: coverage > 0, any date (rq4b:745-772), G3/G4 only
+    const uint32_t *proj;
+    const double *cov;
+    const uint8_t *valid;
+    const uint8_t *member;
+    __device__ bool operator()(int32_t r) const {
+        return (valid[r] & FZ_VALID_COVERAGE) && cov[r] > 0.0 && (member[proj[r]] & 12);
+    }
+};
+
+void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o) {
+    Store &s = c->store;
+    FZ_CHECK(s.built, "fz_rq4b: call fz_store_build first");
+    FZ_CHECK(g && g->member && g->corpus_us && (g->order || g->n_order == 0), "fz_rq4b: null groups");
+    FZ_CHECK(o && o->counts && o->eligible && o->member && o->c2 && o->c1 && o->g2_q && o->g1_q && o->p_bm &&
+                 o->spearman6 && o->pre_cov && o->post_cov && o->pre_median && o->post_median && o->init_g2 &&
+                 o->init_g1 && o->tests,
+             "fz_rq4b: null output buffer");
+    const fz_tables &t = s.t;
+    const int64_t P = s.P, M = s.cov.max_seg, NC = s.cov.n;
+    const int64_t MM = M > 0 ? M : 1;
+    hipStream_t st = c->stream;
+    int64_t *counts = o->counts;
+    FZ_HIP(hipMemsetAsync(counts, 0, FZ_RQ4B_NCOUNTS * 8, st));
+    int64_t *scratch = c->arena.get<int64_t>(4);
+    eligible_projects(c, o->eligible, scratch);
+    group_members(c, g, o->eligible, o->member, counts + FZ_RQ4B_G1, false);
+    const uint8_t *member = o->member;
+    const double *cov = t.c_coverage;
+
+    // ---- per-session quartiles and Brunner-Munzel, G2 (x) vs G1 (y) (:910-1015)
+    TmpView F;
+    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P,
+                FullTrendRows{t.c_project, t.c_coverage, t.c_valid, t.c_date, member}, F);
+    const int64_t *foffs = F.offs;
+    const int32_t *frow = F.row;
+    const uint32_t *fproj = F.proj;
+    const int64_t *d_nf = F.d_n;
+    per_seg(c, P, [=] __device__(int64_t p) {
+        atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ4B_SESSIONS]),
+                  (unsigned long long)(foffs[p + 1] - foffs[p]));
+    });
+    const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
+    const int64_t S2 = 2 * MM;                   // (session, group) segments
+    const int sbits = bits_for(uint64_t(S2 + 1));
+    uint64_t *key = c->arena.get<uint64_t>(NC);
+    uint32_t *idx = c->arena.get<uint32_t>(NC);
+    map_n(c, NC, nullptr, [=] __device__(int64_t j) {
+        if (j < *d_nf) {
+            const uint32_t p = fproj[j];
+            const uint64_t grp = (member[p] & 2) ? 0u : 1u;  // G2 -> x, G1 -> y
+            key[j] = ((uint64_t(j - foffs[p]) * 2u + grp) << pbits) | p;
+        } else {
+            key[j] = uint64_t(S2) << pbits;
+        }
+        idx[j] = uint32_t(j);
+    });
+    radix_sort_pairs(c, key, idx, NC, sbits + pbits);
+    double *v2 = c->arena.get<double>(NC);
+    uint32_t *sid2 = c->arena.get<uint32_t>(NC);
+    int32_t *sess = c->arena.get<int32_t>(NC);
+    uint8_t *grp2 = c->arena.get<uint8_t>(NC);
+    map_n(c, NC, nullptr, [=] __device__(int64_t k) {
+        const uint32_t sg = uint32_t(key[k] >> pbits);
+        sid2[k] = sg;
+        sess[k] = int32_t(sg >> 1);
+        grp2[k] = uint8_t(sg & 1u);
+        if (k < *d_nf) v2[k] = cov[frow[idx[k]]];
+    });
+    int64_t *offs2 = c->arena.get<int64_t>(S2 + 1);
+    k_segment_offsets_dn<<<grid_for(S2 + 1, kBlock, 1u << 30), kBlock, 0, st>>>(sid2, d_nf, S2, offs2);
+    FZ_LAUNCH_CHECK();
+    int64_t *soffs = c->arena.get<int64_t>(MM + 1);
+    int64_t *c2 = o->c2, *c1 = o->c1;
+    map_n(c, MM + 1, nullptr, [=] __device__(int64_t i) {
+        soffs[i] = offs2[2 * i];
+        if (i < MM) {
+            c2[i] = offs2[2 * i + 1] - offs2[2 * i];
+            c1[i] = offs2[2 * i + 2] - offs2[2 * i + 1];
+        }
+    });
+    Segs sg2{S2, offs2, NC};
+    SortedSegs ss2 = seg_sort_f64(c, v2, sg2, reinterpret_cast<const int32_t *>(sid2));
+    double *qq = c->arena.get<double>(S2 * 3);
+    const double q3[3] = {25.0, 50.0, 75.0};
+    seg_percentiles(c, sg2, ss2.val, q3, 3, qq);
+    double *g2q = o->g2_q, *g1q = o->g1_q;
+    map_n(c, MM * 3, nullptr, [=] __device__(int64_t k) {
+        const int64_t i = k / 3, j = k % 3;
+        g2q[k] = qq[(2 * i) * 3 + j];
+        g1q[k] = qq[(2 * i + 1) * 3 + j];
+    });
+    {
+        double *pbm = o->p_bm;
+        RankTestOut rt;
+        rt.bm_p = pbm;
+        seg_rank_tests(c, v2, grp2, Segs{MM, soffs, NC}, sess, rt);
+        map_n(c, MM, nullptr, [=] __device__(int64_t i) {
+            if (!(c2[i] >= 5 && c1[i] >= 5)) pbm[i] = NAN;
+        });
+    }
+    // last session with both groups >= 100 (:849-860); Spearman of the quartile sequences (:879-899)
+    int64_t *lastp1 = c->arena.get<int64_t>(1);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) { *lastp1 = 0; });
+    map_n(c, MM, nullptr, [=] __device__(int64_t i) {
+        if (c2[i] >= 100 && c1[i] >= 100)
+            atomicMax(reinterpret_cast<unsigned long long *>(lastp1), (unsigned long long)(i + 1));
+    });
+    map_n(c, 1, nullptr, [=] __device__(int64_t) { counts[FZ_RQ4B_LAST] = *lastp1 - 1; });
+    {
+        double *seq = c->arena.get<double>(6 * MM);
+        int64_t *offs6 = c->arena.get<int64_t>(7);
+        map_n(c, 7, nullptr, [=] __device__(int64_t k) { offs6[k] = k * (*lastp1); });
+        map_n(c, 6 * MM, nullptr, [=] __device__(int64_t k) {
+            const int64_t n = *lastp1;
+            if (n <= 0 || k >= 6 * n) return;
+            const int64_t sgi = k / n, i = k % n;  // G1 Q1, Med, Q3, then G2 Q1, Med, Q3
+            seq[k] = sgi < 3 ? g1q[i * 3 + sgi] : g2q[i * 3 + sgi - 3];
+        });
+        Segs s6{6, offs6, 6 * MM};
+        ChunkedSegs cs6 = chunked(c, s6);
+        int32_t *id6 = segment_ids(c, s6);
+        SortedSegs ss6 = seg_sort_f64(c, seq, s6, id6);
+        TieRanks tr6 = seg_tie_ranks(c, cs6, id6, ss6.val);
+        double *rho = c->arena.get<double>(6), *pv = c->arena.get<double>(6);
+        seg_spearman_index(c, cs6, ss6, tr6, rho, pv);
+        double *sp = o->spearman6;
+        map_n(c, 6, nullptr, [=] __device__(int64_t k) {
+            sp[2 * k] = rho[k];
+            sp[2 * k + 1] = pv[k];
+        });
+    }
+
+    // ---- coverage deltas around the corpus date for G3 u G4, CSV order (:725-797)
+    {
+        TmpView PC;
+        filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P,
+                    PositiveCoverage34{t.c_project, t.c_coverage, t.c_valid, member}, PC);
+        const int64_t NO = g->n_order;
+        const int64_t NOC = NO > 0 ? NO : 1;
+        int64_t *df = c->arena.get<int64_t>(NOC), *dp = c->arena.get<int64_t>(NOC), *dj = c->arena.get<int64_t>(NOC);
+        const int32_t *order = g->order;
+        const int64_t *cus = g->corpus_us;
+        const int64_t *pcoffs = PC.offs, *pctime = PC.time;
+        const int32_t *pcrow = PC.row;
+        map_n(c, NOC, nullptr, [=] __device__(int64_t k) {
+            df[k] = 0;
+            if (k >= NO) return;
+            const int32_t p = order[k];
+            if (!(member[p] & 12) || cus[p] == FZ_TS_NULL) return;
+            const int64_t cd = fdiv4(cus[p], kDay4) * kDay4;  // corpus_time.date() (UTC)
+            const int64_t lo = pcoffs[p], hi = pcoffs[p + 1];
+            const int64_t j = lower_bound_i64(pctime, lo, hi, cd);
+            if (j - lo >= kWin && hi - j >= kWin) {
+                df[k] = 1;
+                dj[k] = j;
+            }
+        });
+        int64_t *d_nd = counts + FZ_RQ4B_DELTA_PROJECTS;
+        scan_exclusive_i64(c, df, dp, NOC, d_nd);
+        double *pre = o->pre_cov, *post = o->post_cov;
+        map_n(c, NOC, nullptr, [=] __device__(int64_t k) {
+            if (!df[k]) return;
+            const int64_t n = *d_nd, q = dp[k], j = dj[k];
+            for (int i = 0; i < kWin; ++i) {
+                pre[i * n + q] = cov[pcrow[j - 1 - i]];  // DESC LIMIT 7 before the date
+                post[i * n + q] = cov[pcrow[j + i]];     // first 7 from the date
+            }
+        });
+        int64_t *offs7 = c->arena.get<int64_t>(kWin + 1);
+        map_n(c, kWin + 1, nullptr, [=] __device__(int64_t i) { offs7[i] = i * (*d_nd); });
+        Segs s7{kWin, offs7, int64_t(kWin) * (P > 0 ? P : 1)};
+        int32_t *id7 = segment_ids(c, s7);
+        SortedSegs sp = seg_sort_f64(c, pre, s7, id7);
+        seg_median(c, s7, sp.val, o->pre_median);
+        SortedSegs so = seg_sort_f64(c, post, s7, id7);
+        seg_median(c, s7, so.val, o->post_median);
+    }
+
+    // ---- initial coverage of G2 vs G1 (:221-313)
+    {
+        int64_t *f2 = c->arena.get<int64_t>(P), *f1 = c->arena.get<int64_t>(P);
+        int64_t *q2 = c->arena.get<int64_t>(P), *q1 = c->arena.get<int64_t>(P);
+        map_n(c, P, nullptr, [=] __device__(int64_t p) {
+            const bool has = foffs[p + 1] > foffs[p];
+            f2[p] = has && (member[p] & 2);
+            f1[p] = has && (member[p] & 1);
+        });
+        int64_t *n2 = counts + FZ_RQ4B_INIT_G2, *n1 = counts + FZ_RQ4B_INIT_G1;
+        scan_exclusive_i64(c, f2, q2, P, n2);
+        scan_exclusive_i64(c, f1, q1, P, n1);
+        double *a = o->init_g2, *b = o->init_g1;
+        const int32_t *fr = frow;
+        map_n(c, P, nullptr, [=] __device__(int64_t p) {
+            if (f2[p]) a[q2[p]] = cov[fr[foffs[p]]];
+            if (f1[p]) b[q1[p]] = cov[fr[foffs[p]]];
+        });
+        const int64_t cap = 2 * (P > 0 ? P : 1);
+        double *v = c->arena.get<double>(cap);
+        uint8_t *gr = c->arena.get<uint8_t>(cap);
+        map_n(c, cap, nullptr, [=] __device__(int64_t i) {
+            const int64_t na = *n2, nb = *n1;
+            if (i < na) {
+                v[i] = a[i];
+                gr[i] = 0;
+            } else if (i < na + nb) {
+                v[i] = b[i - na];
+                gr[i] = 1;
+            }
+        });
+        int64_t *d_all = c->arena.get<int64_t>(1);
+        map_n(c, 1, nullptr, [=] __device__(int64_t) { *d_all = *n2 + *n1; });
+        Segs one{1, single_segment(c, d_all), cap};
+        int32_t *sid = segment_ids(c, one);
+        double *ts = o->tests;
+        double *u1 = c->arena.get<double>(1);
+        RankTestOut rt;
+        rt.mwu_p_two = ts + FZ_RQ4B_MWU_P;
+        rt.u1 = u1;
+        rt.bm_stat = ts + FZ_RQ4B_BM_STAT;
+        rt.bm_p = ts + FZ_RQ4B_BM_P;
+        rt.exact_scratch = c->arena.get<double>(8 * cap + 1);
+        seg_rank_tests(c, v, gr, one, sid, rt);
+        map_n(c, 1, nullptr, [=] __device__(int64_t) {
+            ts[FZ_RQ4B_CLIFF] = (2.0 * u1[0]) / (double(*n2) * double(*n1)) - 1.0;
+        });
+        uint64_t *ska = sorted_keys_dn(c, a, P, n2);
+        uint64_t *skb = sorted_keys_dn(c, b, P, n1);
+        levene_two(c, ska, a, P, n2, skb, b, P, n1, ts + FZ_RQ4B_LEVENE_W);
+    }
+}
+
+}  // namespace fz

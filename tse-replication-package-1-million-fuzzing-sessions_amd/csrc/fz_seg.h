@@ -167,9 +167,18 @@ struct RankTestOut {
     double *bm_stat = nullptr, *bm_p = nullptr;
     double *u1 = nullptr, *mwu_p_two = nullptr, *mwu_p_greater = nullptr, *ties = nullptr;
     double *nx = nullptr, *ny = nullptr;
+    // scipy's method='auto' picks the EXACT null distribution when min(nx, ny) <= 8 and there are
+    // no ties; that path needs a polynomial of (8 * n_cap + 1) doubles per segment (single-segment
+    // calls only).  Null: always asymptotic.
+    double *exact_scratch = nullptr;
 };
 void seg_rank_tests(fz_ctx *c, const double *vals, const uint8_t *grp, const Segs &sg, const int32_t *segid,
                     const RankTestOut &o);
+
+// scipy.stats.levene([x, y]) (center='median') from the samples and their ascending keys
+// -> out[0] = W, out[1] = p (F(1, N-2) survival, cephes fdtrc rounding).
+void levene_two(fz_ctx *c, const uint64_t *skx, const double *x, int64_t nxm, const int64_t *d_nx,
+                const uint64_t *sky, const double *y, int64_t nym, const int64_t *d_ny, double *out);
 
 // A device offsets array [0, *d_n] for one segment whose length is known only on the device.
 const int64_t *single_segment(fz_ctx *c, const int64_t *d_n);

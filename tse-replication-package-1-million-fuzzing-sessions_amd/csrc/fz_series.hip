@@ -226,9 +226,37 @@ void seg_rank_tests(fz_ctx *c, const double *vals, const uint8_t *grp, const Seg
         const double mu = nx * ny / 2.0;
         const double sd = sqrt(nx * ny / 12.0 * ((nn + 1.0) - tie / (nn * (nn - 1.0))));
         if (o.u1) o.u1[s] = U1;
+        // exact null distribution (scipy _mannwhitneyu._MWU): counts of U = coefficients of the
+        // Gaussian binomial [n1+n2 choose n1]_q, built as prod_k (1 - q^(n2+k)) / (1 - q^k)
+        const bool exact = o.exact_scratch && S == 1 && !(nx > 8.0 && ny > 8.0) && !(tie > 0.0);
+        double *conf = o.exact_scratch;
+        int64_t n1 = int64_t(nx < ny ? nx : ny), n2 = int64_t(nx < ny ? ny : nx);
+        double total = 1.0;
+        if (exact) {
+            const int64_t deg = n1 * n2;
+            for (int64_t u = 0; u <= deg; ++u) conf[u] = u == 0 ? 1.0 : 0.0;
+            for (int64_t k = 1; k <= n1; ++k) {
+                const int64_t m = n2 + k;
+                for (int64_t u = deg; u >= m; --u) conf[u] -= conf[u - m];
+                for (int64_t u = k; u <= deg; ++u) conf[u] += conf[u - k];
+            }
+            total = 0.0;
+            for (int64_t u = 0; u <= deg; ++u) total += conf[u];
+        }
         auto pv = [&](double U, double f) {
-            const double z = (U - mu - 0.5) / sd;
-            double p = stats::norm_sf(z) * f;
+            double p;
+            if (exact) {  // _MWU.sf(U): 1 - cdf(U) + pmf(U) when U < n1*n2 - U, else cdf(n1*n2 - U)
+                const int64_t k = int64_t(U);
+                const int64_t kc = n1 * n2 - k;
+                const int64_t lim = k < kc ? k : kc;
+                double cdf = 0.0;
+                for (int64_t u = 0; u <= lim; ++u) cdf += conf[u] / total;
+                p = k < kc ? 1.0 - cdf + conf[k] / total : cdf;
+            } else {
+                const double z = (U - mu - 0.5) / sd;
+                p = stats::norm_sf(z);
+            }
+            p *= f;
             return p < 0.0 ? 0.0 : (p > 1.0 ? 1.0 : p);
         };
         if (o.mwu_p_two) o.mwu_p_two[s] = pv(U1 > U2 ? U1 : U2, 2.0);
@@ -394,6 +422,52 @@ void seg_median(fz_ctx *c, const Segs &sg, const double *sorted, double *out) {
             return;
         }
         out[s] = (n & 1) ? sorted[b + n / 2] : (sorted[b + n / 2 - 1] + sorted[b + n / 2]) / 2.0;
+    });
+}
+
+// levene([x, y], center='median') (scipy _morestats.py levene).
+void levene_two(fz_ctx *c, const uint64_t *skx, const double *x, int64_t nxm, const int64_t *d_nx,
+                       const uint64_t *sky, const double *y, int64_t nym, const int64_t *d_ny, double *out) {
+    double *med = c->arena.get<double>(2);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        for (int g = 0; g < 2; ++g) {
+            const uint64_t *k = g ? sky : skx;
+            const int64_t n = g ? *d_ny : *d_nx;
+            med[g] = n <= 0 ? NAN
+                            : ((n & 1) ? f64_from_key(k[n / 2])
+                                       : (f64_from_key(k[n / 2 - 1]) + f64_from_key(k[n / 2])) / 2.0);
+        }
+    });
+    double *zb = c->arena.get<double>(2), *dv = c->arena.get<double>(2);
+    Segs sx{1, single_segment(c, d_nx), nxm}, sy{1, single_segment(c, d_ny), nym};
+    ChunkedSegs cx = chunked(c, sx), cy = chunked(c, sy);
+    seg_reduce<1>(c, cx, [=] __device__(int64_t i, int32_t, double *v) { v[0] = fabs(x[i] - med[0]); }, zb);
+    seg_reduce<1>(c, cy, [=] __device__(int64_t i, int32_t, double *v) { v[0] = fabs(y[i] - med[1]); }, zb + 1);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        zb[0] /= double(*d_nx);
+        zb[1] /= double(*d_ny);
+    });
+    seg_reduce<1>(c, cx, [=] __device__(int64_t i, int32_t, double *v) {
+        const double d = fabs(x[i] - med[0]) - zb[0];
+        v[0] = d * d;
+    }, dv);
+    seg_reduce<1>(c, cy, [=] __device__(int64_t i, int32_t, double *v) {
+        const double d = fabs(y[i] - med[1]) - zb[1];
+        v[0] = d * d;
+    }, dv + 1);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        const double nx = double(*d_nx), ny = double(*d_ny), N = nx + ny;
+        double zbar = 0.0;
+        zbar += zb[0] * nx;
+        zbar += zb[1] * ny;
+        zbar /= N;
+        const double numer = (N - 2.0) * (nx * (zb[0] - zbar) * (zb[0] - zbar) + ny * (zb[1] - zbar) * (zb[1] - zbar));
+        double dvar = 0.0;
+        dvar += dv[0];
+        dvar += dv[1];
+        const double W = numer / (1.0 * dvar);
+        out[0] = W;
+        out[1] = stats::f1_sf(W, N - 2.0);
     });
 }
 

@@ -92,6 +92,34 @@ class FzRq3Out(C.Structure):
                                   "non_pct", "non_cov", "non_tot", "describe", "tests")]
 
 
+class FzRq4Groups(C.Structure):
+    _fields_ = [("member", _P), ("corpus_us", _P), ("order", _P), ("n_order", _I64)]
+
+
+FZ_RQ4A_NCOUNTS, FZ_RQ4A_NSCALARS = 12, 12
+(RQ4A_MAX_ITER, RQ4A_ROWS, RQ4A_G1, RQ4A_G2, RQ4A_G3, RQ4A_G4, RQ4A_HAS_WINDOW, RQ4A_AFTER_G1, RQ4A_AFTER_G2,
+ RQ4A_INTRO_POS) = range(10)
+(RQ4A_AFTER_G1_MEDIAN, RQ4A_AFTER_G1_IQR, RQ4A_AFTER_G2_MEDIAN, RQ4A_AFTER_G2_IQR, RQ4A_INTRO_MEAN,
+ RQ4A_INTRO_MEDIAN, RQ4A_INTRO_MIN, RQ4A_INTRO_MAX, RQ4A_PRE_RATE, RQ4A_POST_RATE) = range(10)
+
+
+class FzRq4aOut(C.Structure):
+    _fields_ = [(n, _P) for n in ("counts", "scalars", "eligible", "member", "g1_total", "g1_det", "g2_total",
+                                  "g2_det", "intro", "g4_steps", "g4_transition")]
+
+
+FZ_RQ4B_NCOUNTS, FZ_RQ4B_NTESTS = 12, 8
+(RQ4B_SESSIONS, RQ4B_LAST, RQ4B_DELTA_PROJECTS, RQ4B_INIT_G2, RQ4B_INIT_G1, RQ4B_G1, RQ4B_G2, RQ4B_G3,
+ RQ4B_G4) = range(9)
+RQ4B_MWU_P, RQ4B_CLIFF, RQ4B_BM_STAT, RQ4B_BM_P, RQ4B_LEVENE_W, RQ4B_LEVENE_P = range(6)
+
+
+class FzRq4bOut(C.Structure):
+    _fields_ = [(n, _P) for n in ("counts", "eligible", "member", "c2", "c1", "g2_q", "g1_q", "p_bm", "spearman6",
+                                  "pre_cov", "post_cov", "pre_median", "post_median", "init_g2", "init_g1",
+                                  "tests")]
+
+
 # every symbol include/fz.h declares, with its ctypes signature
 SIGNATURES = {
     "fz_abi_version": (C.c_int, []),
@@ -104,6 +132,8 @@ SIGNATURES = {
     "fz_rq2_count": (C.c_int, [_P, C.POINTER(FzRq2CountOut)]),
     "fz_rq2_add": (C.c_int, [_P, C.POINTER(FzRq2AddOut)]),
     "fz_rq3": (C.c_int, [_P, C.POINTER(FzRq3Out)]),
+    "fz_rq4a": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.POINTER(FzRq4aOut)]),
+    "fz_rq4b": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.POINTER(FzRq4bOut)]),
     "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),
     "fz_probe_end": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "fz_radix_sort_u64": (C.c_int, [_P, _P, _P, _I64, C.c_int]),
@@ -211,15 +241,21 @@ class Engine:
             "i_number": t.i_number, "i_project": t.i_project.view(np.int32), "i_rts": t.i_rts,
             "i_status": t.i_status, "pi_count": pi_count,
         }
+        from .rq.common import corpus_columns
+        member, corpus_us, order = corpus_columns(t)
+        host.update({"g_member": member, "g_corpus_us": corpus_us, "g_order": order})
         cols = {}
         with torch.cuda.stream(self.stream):
             for k, a in host.items():
                 h = _pin(torch.from_numpy(np.ascontiguousarray(a)))
                 cols[k] = h.to(self.dev, non_blocking=True)
-        ptr = {k: _P(v.data_ptr()) for k, v in cols.items()}
+        ptr = {k: _P(v.data_ptr()) for k, v in cols.items() if not k.startswith("g_")}
         fz = FzTables(n_projects=P, n_builds=len(t.b_project), n_cov=len(t.c_project), n_issues=len(t.i_project),
                       **ptr)
         self.tables = DeviceTables(host=t, cols=cols, fz=fz)
+        self.groups = FzRq4Groups(member=_P(cols["g_member"].data_ptr()),
+                                  corpus_us=_P(cols["g_corpus_us"].data_ptr()),
+                                  order=_P(cols["g_order"].data_ptr()), n_order=len(order))
         return self.tables
 
     # ---- store ---------------------------------------------------------------------------------

@@ -69,6 +69,42 @@ def corpus_groups(t: Tables, eligible, add_missing_to_g1: bool):
     return out, corpus_us
 
 
+def corpus_columns(t: Tables):
+    """Loader of project_corpus_analysis.csv for the GPU path (fz_rq4_groups in include/fz.h).
+
+    Eligibility-independent per-project columns, so the device can apply the eligible set itself:
+    member bit g = some CSV row puts the project in G(g+1) (rq4a_bug.py:94-108), bit 4 = project
+    absent from the CSV (rq4a_bug.py:110-113); corpus_us = corpus_commit_time parsed with
+    ``utc=True`` (last qualifying row wins, as the reference's dict does); order = projects of the
+    CSV rows with a time_elapsed_seconds value, in file order (rq4b_coverage.py:216, :744).
+    """
+    from ..schema import TS_NULL
+    df = read_corpus(t)
+    pid = {n: i for i, n in enumerate(t.projects)}
+    P = len(t.projects)
+    member = np.zeros(P, dtype=np.uint8)
+    corpus_us = np.full(P, TS_NULL, dtype=np.int64)
+    te = df["time_elapsed_seconds"]
+    null = te.isna()
+    masks = [null, (te == 0) & (~null), (te > 0) & (te < DAYS_THRESHOLD * 86400) & (~null),
+             (te >= DAYS_THRESHOLD * 86400) & (~null)]
+    names = df["project_name"]
+    for g, m in enumerate(masks):
+        for n in names[m]:
+            if n in pid:
+                member[pid[n]] |= np.uint8(1 << g)
+    seen = np.zeros(P, dtype=bool)
+    for n in names:
+        if n in pid:
+            seen[pid[n]] = True
+    member[~seen] |= np.uint8(16)
+    for n, ts in zip(names[~null], df["corpus_commit_time"][~null]):
+        if n in pid and not pd.isna(ts):
+            corpus_us[pid[n]] = int(ts.value // 1000)
+    order = np.array([pid[n] for n in names[~null] if n in pid], dtype=np.int32)
+    return member, corpus_us, order
+
+
 def corpus_order(t: Tables, eligible) -> List[int]:
     """Row order of ``group_2_3_4_df.iterrows()`` (rq4b_coverage.py:216, :744)."""
     f = _filtered(t, eligible)

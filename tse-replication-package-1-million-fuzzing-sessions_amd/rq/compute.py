@@ -11,7 +11,7 @@ import ctypes as C
 import numpy as np
 
 from .. import engine as E
-from .results import Describe, RQ1Result, RQ2AddResult, RQ2CountResult, RQ3Result
+from .results import Describe, RQ1Result, RQ2AddResult, RQ2CountResult, RQ3Result, RQ4aResult, RQ4bResult
 
 
 def _describe(d: E.FzDescribe, with_min_nonzero=False) -> Describe:
@@ -211,3 +211,101 @@ def rq3(eng: E.Engine) -> RQ3Result:
     b = rq3_buffers(eng)
     rq3_launch(eng, b)
     return rq3_collect(eng, b)
+
+
+def _groups(member, P):
+    return {f"group{k + 1}": np.nonzero(member[:P] & (1 << k))[0].tolist() for k in range(4)}
+
+
+# ----------------------------------------------------------------------------------------- RQ4a
+def rq4a_buffers(eng: E.Engine) -> OutBuffers:
+    torch = eng.torch
+    fz, st = eng.tables.fz, eng.stats
+    P, M = fz.n_projects, max(int(st.max_fuzz_per_project), 1)
+    f64, i64, u8 = torch.float64, torch.int64, torch.uint8
+    return OutBuffers(eng, E.FzRq4aOut, [
+        ("counts", E.FZ_RQ4A_NCOUNTS, i64), ("scalars", E.FZ_RQ4A_NSCALARS, f64), ("eligible", P, u8),
+        ("member", P, u8), ("g1_total", M, i64), ("g1_det", M, i64), ("g2_total", M, i64), ("g2_det", M, i64),
+        ("intro", P, i64), ("g4_steps", 30, i64), ("g4_transition", 4, i64)])
+
+
+def rq4a_launch(eng: E.Engine, b: OutBuffers):
+    E._check(eng.lib, eng.lib.fz_rq4a(eng.ctx, C.byref(eng.groups), C.byref(b.out)))
+
+
+def rq4a_collect(eng: E.Engine, b: OutBuffers) -> RQ4aResult:
+    P = eng.tables.fz.n_projects
+    cnt, sc = b.host("counts"), b.host("scalars")
+    mx = int(cnt[E.RQ4A_MAX_ITER])
+    groups = _groups(b.host("member"), P)
+    intro_a = b.host("intro", P)
+    steps = b.host("g4_steps").reshape(15, 2)
+    after = {}
+    for key, n, med, iqr in (("g1", E.RQ4A_AFTER_G1, E.RQ4A_AFTER_G1_MEDIAN, E.RQ4A_AFTER_G1_IQR),
+                             ("g2", E.RQ4A_AFTER_G2, E.RQ4A_AFTER_G2_MEDIAN, E.RQ4A_AFTER_G2_IQR)):
+        after[key] = (float(sc[med]), float(sc[iqr])) if cnt[n] > 0 else None
+    return RQ4aResult(
+        groups=groups, g1_total=b.host("g1_total", mx), g1_det=b.host("g1_det", mx),
+        g2_total=b.host("g2_total", mx), g2_det=b.host("g2_det", mx), after=after,
+        intro=[(p, int(intro_a[p])) for p in groups["group4"] if intro_a[p] >= 0],
+        intro_stats=((float(sc[E.RQ4A_INTRO_MEAN]), float(sc[E.RQ4A_INTRO_MEDIAN]), int(sc[E.RQ4A_INTRO_MIN]),
+                      int(sc[E.RQ4A_INTRO_MAX])) if cnt[E.RQ4A_INTRO_POS] > 0 else None),
+        g4_steps={s: (int(steps[s + 7, 0]), int(steps[s + 7, 1])) for s in list(range(-7, 0)) + list(range(1, 8))},
+        g4_transition=tuple(int(x) for x in b.host("g4_transition")),
+        g4_overall=(float(sc[E.RQ4A_PRE_RATE]), float(sc[E.RQ4A_POST_RATE])), n_g4_analyzed=int(steps[6, 0]),
+        has_g4_transition=bool(cnt[E.RQ4A_HAS_WINDOW]))
+
+
+def rq4a(eng: E.Engine) -> RQ4aResult:
+    """rq4a_bug.main's analysis (rq4a_bug.py:653-884) on the GPU."""
+    b = rq4a_buffers(eng)
+    rq4a_launch(eng, b)
+    return rq4a_collect(eng, b)
+
+
+# ----------------------------------------------------------------------------------------- RQ4b
+def rq4b_buffers(eng: E.Engine) -> OutBuffers:
+    torch = eng.torch
+    fz, st = eng.tables.fz, eng.stats
+    P, M = fz.n_projects, max(int(st.max_cov_per_project), 1)
+    PP = max(P, 1)
+    f64, i64, u8 = torch.float64, torch.int64, torch.uint8
+    return OutBuffers(eng, E.FzRq4bOut, [
+        ("counts", E.FZ_RQ4B_NCOUNTS, i64), ("eligible", P, u8), ("member", P, u8), ("c2", M, i64), ("c1", M, i64),
+        ("g2_q", 3 * M, f64), ("g1_q", 3 * M, f64), ("p_bm", M, f64), ("spearman6", 12, f64),
+        ("pre_cov", 7 * PP, f64), ("post_cov", 7 * PP, f64), ("pre_median", 7, f64), ("post_median", 7, f64),
+        ("init_g2", P, f64), ("init_g1", P, f64), ("tests", E.FZ_RQ4B_NTESTS, f64)])
+
+
+def rq4b_launch(eng: E.Engine, b: OutBuffers):
+    E._check(eng.lib, eng.lib.fz_rq4b(eng.ctx, C.byref(eng.groups), C.byref(b.out)))
+
+
+def rq4b_collect(eng: E.Engine, b: OutBuffers) -> RQ4bResult:
+    P = eng.tables.fz.n_projects
+    cnt, ts = b.host("counts"), b.host("tests")
+    ms, last, nd = int(cnt[E.RQ4B_SESSIONS]), int(cnt[E.RQ4B_LAST]), int(cnt[E.RQ4B_DELTA_PROJECTS])
+    n2, n1 = int(cnt[E.RQ4B_INIT_G2]), int(cnt[E.RQ4B_INIT_G1])
+    sp = b.host("spearman6")
+    pre, post = b.host("pre_cov"), b.host("post_cov")
+    both = n2 > 0 and n1 > 0
+    return RQ4bResult(
+        group_counts=tuple(int(cnt[k]) for k in (E.RQ4B_G1, E.RQ4B_G2, E.RQ4B_G3, E.RQ4B_G4)), n_sessions=ms,
+        c2=b.host("c2", ms), c1=b.host("c1", ms), g2_q=b.host("g2_q", 3 * ms).reshape(ms, 3),
+        g1_q=b.host("g1_q", 3 * ms).reshape(ms, 3), p_bm=b.host("p_bm", ms), last_valid_idx=last,
+        spearman6=[(float(sp[2 * k]), float(sp[2 * k + 1])) for k in range(6)] if last >= 0 else None,
+        n_delta_projects=nd, pre_cov=[pre[i * nd:(i + 1) * nd].copy() for i in range(7)],
+        post_cov=[post[i * nd:(i + 1) * nd].copy() for i in range(7)],
+        pre_median=[float(x) for x in b.host("pre_median")], post_median=[float(x) for x in b.host("post_median")],
+        n_g2=int(cnt[E.RQ4B_G2]), n_g1=int(cnt[E.RQ4B_G1]), init_g2=b.host("init_g2", n2),
+        init_g1=b.host("init_g1", n1), mwu_p=float(ts[E.RQ4B_MWU_P]) if both else None,
+        cliff=float(ts[E.RQ4B_CLIFF]) if both else None,
+        bm=(float(ts[E.RQ4B_BM_STAT]), float(ts[E.RQ4B_BM_P])) if both else None,
+        levene=(float(ts[E.RQ4B_LEVENE_W]), float(ts[E.RQ4B_LEVENE_P])) if both else None)
+
+
+def rq4b(eng: E.Engine) -> RQ4bResult:
+    """rq4b_coverage.main's analysis (rq4b_coverage.py:1209-1261) on the GPU."""
+    b = rq4b_buffers(eng)
+    rq4b_launch(eng, b)
+    return rq4b_collect(eng, b)
