@@ -30,7 +30,7 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PROBE_KERNEL = "radix_scatter"   # dominant kernel of the step (profiles/r01_*_stats.csv)
-STAGES = ["store", "rq1"]
+STAGES = ["store", "rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"]
 
 
 def parse():
@@ -67,11 +67,18 @@ def main():
     eng.upload(t)
     eng.build_store()
     rq1_bufs = compute.RQ1Buffers(eng)
+    bufs = {"rq2_count": compute.rq2_count_buffers(eng), "rq2_add": compute.rq2_add_buffers(eng),
+            "rq3": compute.rq3_buffers(eng), "rq4a": compute.rq4a_buffers(eng), "rq4b": compute.rq4b_buffers(eng)}
+    launch = {"rq2_count": compute.rq2_count_launch, "rq2_add": compute.rq2_add_launch, "rq3": compute.rq3_launch,
+              "rq4a": compute.rq4a_launch, "rq4b": compute.rq4b_launch}
 
     def step():
         eng.build_store()
         compute.rq1_launch(eng, rq1_bufs)
+        for name in ("rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"):
+            launch[name](eng, bufs[name])
         if world > 1:
+            # projects are disjoint across ranks: per-iteration project counts add
             dist.all_reduce(rq1_bufs.iter_total)
             dist.all_reduce(rq1_bufs.iter_detected)
 
