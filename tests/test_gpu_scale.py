@@ -1,0 +1,39 @@
+"""GPU parity beyond the golden cases: the bench table itself (config 2, ~2.9M session rows) and a
+Zipf-skewed table whose giant projects exceed the one-workgroup (LDS) sort limit, exercising the
+device-wide fallback paths.  The CPU oracle (itself pinned to the reference's golden outputs) is
+the checker; all six analyses are compared field by field."""
+import numpy as np
+import pytest
+
+import tse_amd.synth as synth
+from gpu_common import assert_same
+from oracle import rq_oracle as orc
+from tse_amd.rq import compute
+
+pytestmark = pytest.mark.gpu
+
+STAGES = [("rq1", compute.rq1, orc.rq1), ("rq2_count", compute.rq2_count, orc.rq2_count),
+          ("rq2_add", compute.rq2_add, orc.rq2_add), ("rq3", compute.rq3, orc.rq3),
+          ("rq4a", compute.rq4a, orc.rq4a), ("rq4b", compute.rq4b, orc.rq4b)]
+
+
+def _check_all(engine, t):
+    engine.upload(t)
+    st = engine.build_store()
+    for name, gpu, cpu in STAGES:
+        assert_same(gpu(engine), cpu(t), path=name)
+    return st
+
+
+def test_zipf_giant_projects(engine):
+    cfg = synth.SynthConfig(n_projects=24, seed=21, zipf_s=1.2, len_mean_days=900, issues_mean=120,
+                            dup_numbers=3, hex_len=12)
+    t = synth.generate(cfg)
+    st = _check_all(engine, t)
+    assert st.max_fuzz_per_project > 4096 and st.max_cov_per_project > 4096  # fallback paths ran
+
+
+def test_config2_bench_table(engine):
+    t = synth.generate(synth.config("c2"))
+    st = _check_all(engine, t)
+    assert st.n_fuzz == int(np.sum(t.b_type == 0))

@@ -402,6 +402,7 @@ __global__ void k_describe_finish(const uint64_t *__restrict__ sk, const int64_t
 }
 
 uint64_t *sorted_keys_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n) {
+    if (nmax <= 4096) return sort_small_keys(c, x, nmax < 1 ? 1 : nmax, d_n);  // one workgroup, LDS
     const int64_t nn = nmax < 1 ? 1 : nmax;
     uint64_t *k = c->arena.get<uint64_t>(nn);
     k_f64_keys<<<grid_for(nn, kBlock, 1024), kBlock, 0, c->stream>>>(x, nmax, d_n, k);

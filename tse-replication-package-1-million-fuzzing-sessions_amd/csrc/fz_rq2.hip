@@ -76,7 +76,7 @@ void rq2_count(fz_ctx *c, const fz_rq2_count_out *o) {
     });
 
     // per-project Spearman (vs index) and Shapiro-Wilk
-    Segs sp{P, T.offs, NC};
+    Segs sp{P, T.offs, NC, M};
     ChunkedSegs cs = chunked(c, sp);
     const int32_t *segid = reinterpret_cast<const int32_t *>(T.proj);
     SortedSegs ss = seg_sort_f64(c, tv, sp, segid);
@@ -112,7 +112,7 @@ void rq2_count(fz_ctx *c, const fz_rq2_count_out *o) {
     FZ_LAUNCH_CHECK();
 
     // per-session statistics (sessions are non-increasing in size: >= 100 is a prefix)
-    Segs ses{M, o->session_offsets, NC};
+    Segs ses{M, o->session_offsets, NC, P};  // a session holds at most one value per project
     ChunkedSegs cs2 = chunked(c, ses);
     const int32_t *sseg = reinterpret_cast<const int32_t *>(sid);
     SortedSegs ss2 = seg_sort_f64(c, sv, ses, sseg);

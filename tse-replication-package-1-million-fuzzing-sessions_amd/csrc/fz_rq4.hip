@@ -311,7 +311,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o) {
             c1[i] = offs2[2 * i + 2] - offs2[2 * i + 1];
         }
     });
-    Segs sg2{S2, offs2, NC};
+    Segs sg2{S2, offs2, NC, P};
     SortedSegs ss2 = seg_sort_f64(c, v2, sg2, reinterpret_cast<const int32_t *>(sid2));
     double *qq = c->arena.get<double>(S2 * 3);
     const double q3[3] = {25.0, 50.0, 75.0};
@@ -326,7 +326,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o) {
         double *pbm = o->p_bm;
         RankTestOut rt;
         rt.bm_p = pbm;
-        seg_rank_tests(c, v2, grp2, Segs{MM, soffs, NC}, sess, rt);
+        seg_rank_tests(c, v2, grp2, Segs{MM, soffs, NC, P}, sess, rt);
         map_n(c, MM, nullptr, [=] __device__(int64_t i) {
             if (!(c2[i] >= 5 && c1[i] >= 5)) pbm[i] = NAN;
         });
@@ -349,7 +349,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o) {
             const int64_t sgi = k / n, i = k % n;  // G1 Q1, Med, Q3, then G2 Q1, Med, Q3
             seq[k] = sgi < 3 ? g1q[i * 3 + sgi] : g2q[i * 3 + sgi - 3];
         });
-        Segs s6{6, offs6, 6 * MM};
+        Segs s6{6, offs6, 6 * MM, MM};
         ChunkedSegs cs6 = chunked(c, s6);
         int32_t *id6 = segment_ids(c, s6);
         SortedSegs ss6 = seg_sort_f64(c, seq, s6, id6);
@@ -401,7 +401,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o) {
         });
         int64_t *offs7 = c->arena.get<int64_t>(kWin + 1);
         map_n(c, kWin + 1, nullptr, [=] __device__(int64_t i) { offs7[i] = i * (*d_nd); });
-        Segs s7{kWin, offs7, int64_t(kWin) * (P > 0 ? P : 1)};
+        Segs s7{kWin, offs7, int64_t(kWin) * (P > 0 ? P : 1), P};
         int32_t *id7 = segment_ids(c, s7);
         SortedSegs sp = seg_sort_f64(c, pre, s7, id7);
         seg_median(c, s7, sp.val, o->pre_median);

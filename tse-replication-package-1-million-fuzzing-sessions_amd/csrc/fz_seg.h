@@ -19,7 +19,13 @@ struct Segs {
     int64_t S = 0;                 // number of segments
     const int64_t *offs = nullptr; // [S + 1] device
     int64_t n_cap = 0;             // host upper bound of offs[S]
+    int64_t max_len = 0;           // host upper bound of one segment's length (0: n_cap)
+    int64_t len_bound() const { return max_len > 0 && max_len < n_cap ? max_len : n_cap; }
 };
+
+// Segments no longer than this are sorted inside one workgroup (LDS bitonic network); longer
+// ones take the device-wide LSD radix path.
+constexpr int64_t kLdsSortMax = 4096;
 
 struct ChunkMap {
     int64_t cap = 0;

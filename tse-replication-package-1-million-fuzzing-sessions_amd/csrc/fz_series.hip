@@ -72,12 +72,76 @@ const int64_t *single_segment(fz_ctx *c, const int64_t *d_n) {
 }
 
 // -------------------------------------------------------------------------- segmented sort
+// One workgroup per segment of <= kLdsSortMax values: bitonic network over (key, position) pairs
+// in LDS (48 KiB), padded to a power of two with +inf keys.  Ties may come out in any order -
+// every consumer (ranks, percentiles, rank tests) is invariant to the order inside a tie group.
+__global__ __launch_bounds__(kBlock) void k_seg_sort_lds(const double *__restrict__ src,
+                                                         const int64_t *__restrict__ offs, int64_t S,
+                                                         double *__restrict__ out_val, int32_t *__restrict__ out_pos,
+                                                         uint64_t *__restrict__ out_key) {
+    __shared__ uint64_t sk[kLdsSortMax];
+    __shared__ int32_t sp[kLdsSortMax];
+    const int tid = threadIdx.x;
+    for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
+        const int64_t b = offs[s];
+        const int n = int(offs[s + 1] - b);
+        if (n <= 0) continue;
+        int np2 = 1;
+        while (np2 < n) np2 <<= 1;
+        for (int i = tid; i < np2; i += kBlock) {
+            sk[i] = i < n ? f64_key(src[b + i]) : ~0ull;
+            sp[i] = i;
+        }
+        __syncthreads();
+        for (int k = 2; k <= np2; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = tid; i < np2; i += kBlock) {
+                    const int ixj = i ^ j;
+                    if (ixj > i) {
+                        const uint64_t a = sk[i], d = sk[ixj];
+                        const bool up = (i & k) == 0;
+                        if ((a > d) == up) {
+                            sk[i] = d;
+                            sk[ixj] = a;
+                            const int32_t t = sp[i];
+                            sp[i] = sp[ixj];
+                            sp[ixj] = t;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (int i = tid; i < n; i += kBlock) {
+            if (out_val) out_val[b + i] = f64_from_key(sk[i]);
+            if (out_pos) out_pos[b + i] = int32_t(b + sp[i]);
+            if (out_key) out_key[b + i] = sk[i];
+        }
+        __syncthreads();
+    }
+}
+
+uint64_t *sort_small_keys(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n) {
+    uint64_t *k = c->arena.get<uint64_t>(nmax);
+    const int64_t *offs = single_segment(c, d_n);
+    map_n(c, nmax, nullptr, [=] __device__(int64_t i) { k[i] = ~0ull; });  // entries past *d_n
+    k_seg_sort_lds<<<1, kBlock, 0, c->stream>>>(x, offs, 1, nullptr, nullptr, k);
+    FZ_LAUNCH_CHECK();
+    return k;
+}
+
 SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int32_t *segid) {
     const int64_t n = sg.n_cap;
     SortedSegs out;
     out.val = c->arena.get<double>(n);
     out.pos = c->arena.get<int32_t>(n);
     if (n <= 0) return out;
+    if (sg.len_bound() <= kLdsSortMax) {
+        const unsigned g = unsigned(sg.S < 8192 ? (sg.S > 0 ? sg.S : 1) : 8192);
+        k_seg_sort_lds<<<g, kBlock, 0, c->stream>>>(src, sg.offs, sg.S, out.val, out.pos, nullptr);
+        FZ_LAUNCH_CHECK();
+        return out;
+    }
     uint64_t *keys = c->arena.get<uint64_t>(n);
     uint32_t *vals = reinterpret_cast<uint32_t *>(out.pos);
     const int64_t *offs = sg.offs;

@@ -108,6 +108,113 @@ __global__ __launch_bounds__(kBlock) void k_max_seg(const int64_t *__restrict__ 
     if (lane_id() == 0) atomicMax(out, (unsigned long long)m);
 }
 
+// ---- fast path: prefix LSD (2 passes) + per-segment LDS sort by (time, row) -----------------
+constexpr int kSegSortMax = 4096;
+
+__global__ __launch_bounds__(kBlock) void k_keys_prefix_rows(Prefix pre, int64_t n, uint64_t *__restrict__ keys,
+                                                             uint32_t *__restrict__ vals) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        keys[i] = pre(i);
+        vals[i] = uint32_t(i);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_prefix_offsets(const uint64_t *__restrict__ keys, int64_t n, int64_t S,
+                                                           int64_t *__restrict__ offs) {
+    const int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (s > S) return;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (keys[mid] < uint64_t(s)) lo = mid + 1;
+        else hi = mid;
+    }
+    offs[s] = lo;
+}
+
+// One workgroup per prefix segment (<= kSegSortMax rows, already in row order): bitonic sort of
+// (time, position) pairs in LDS - the position tie-break keeps equal times in row order (stable).
+__global__ __launch_bounds__(kBlock) void k_seg_time_sort(const uint32_t *__restrict__ rows,
+                                                          const int64_t *__restrict__ time,
+                                                          const int64_t *__restrict__ offs, int64_t S, uint32_t pmask,
+                                                          int32_t *__restrict__ orow, int64_t *__restrict__ otime,
+                                                          uint32_t *__restrict__ oproj,
+                                                          unsigned long long *__restrict__ big) {
+    __shared__ int64_t st[kSegSortMax];
+    __shared__ int32_t si[kSegSortMax];
+    const int tid = threadIdx.x;
+    for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
+        const int64_t b = offs[s];
+        const int64_t len = offs[s + 1] - b;
+        if (len <= 0) continue;
+        if (len > kSegSortMax) {  // the host re-sorts the table on the full-key path
+            if (tid == 0) atomicAdd(big, (unsigned long long)len);
+            continue;
+        }
+        const int n = int(len);
+        int np2 = 1;
+        while (np2 < n) np2 <<= 1;
+        for (int i = tid; i < np2; i += kBlock) {
+            st[i] = i < n ? time[rows[b + i]] : INT64_MAX;  // NULL = INT64_MAX sorts last; pads after
+            si[i] = i;
+        }
+        __syncthreads();
+        for (int k = 2; k <= np2; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = tid; i < np2; i += kBlock) {
+                    const int ixj = i ^ j;
+                    if (ixj > i) {
+                        const int64_t ta = st[i], tb = st[ixj];
+                        const int32_t ia = si[i], ib = si[ixj];
+                        const bool gt = ta > tb || (ta == tb && ia > ib);
+                        if (gt == ((i & k) == 0)) {
+                            st[i] = tb;
+                            st[ixj] = ta;
+                            si[i] = ib;
+                            si[ixj] = ia;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        const uint32_t p = uint32_t(s) & pmask;
+        for (int i = tid; i < n; i += kBlock) {
+            orow[b + i] = int32_t(rows[b + si[i]]);
+            otime[b + i] = st[i];
+            oproj[b + i] = p;
+        }
+        __syncthreads();
+    }
+}
+
+// Sorts by (prefix, time, row); returns the device counter of rows in segments too long for LDS
+// (non-zero -> the caller re-sorts with sort_table()).
+static unsigned long long *sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time,
+                                           int32_t *orow, int64_t *otime, uint32_t *oproj) {
+    unsigned long long *big = c->arena.get<unsigned long long>(1);
+    FZ_HIP(hipMemsetAsync(big, 0, 8, c->stream));
+    if (n <= 0) return big;
+    uint64_t *keys = c->arena.get<uint64_t>(n);
+    uint32_t *vals = c->arena.get<uint32_t>(n);
+    const unsigned g = grid_for(n, kBlock, 4096);
+    k_keys_prefix_rows<<<g, kBlock, 0, c->stream>>>(pre, n, keys, vals);
+    FZ_LAUNCH_CHECK();
+    radix_sort_pairs(c, keys, vals, n, prefix_bits);
+    const int64_t S = int64_t(1) << prefix_bits;
+    int64_t *offs = c->arena.get<int64_t>(S + 1);
+    k_prefix_offsets<<<grid_for(S + 1, kBlock, 1u << 30), kBlock, 0, c->stream>>>(keys, n, S, offs);
+    FZ_LAUNCH_CHECK();
+    const uint32_t pmask = pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << pre.pbits) - 1ull);
+    {
+        ProbeScope ps(c, "seg_time_sort", 28.0 * double(n));  // row 4 + gathered time 8 + out 16 B
+        k_seg_time_sort<<<unsigned(S < 16384 ? S : 16384), kBlock, 0, c->stream>>>(vals, time, offs, S, pmask, orow,
+                                                                                  otime, oproj, big);
+        FZ_LAUNCH_CHECK();
+    }
+    return big;
+}
+
 // Sort one table into (row, time, proj) buffers.
 static void sort_table(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time, int64_t tmin,
                        int64_t tmax, int32_t *orow, int64_t *otime, uint32_t *oproj) {
@@ -183,45 +290,69 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         s.tmax[i] = mm[2 * i + 1];
     }
 
-    // buildlog_data by (type, project, time)
-    {
-        const int64_t n = t->n_builds;
-        int32_t *row = s.b_row.ensure<int32_t>(n);
-        int64_t *tm = s.b_time.ensure<int64_t>(n);
-        uint32_t *pr = s.b_proj.ensure<uint32_t>(n);
-        sort_table(c, n, Prefix{t->b_project, t->b_type, pbits}, pbits + 2, t->b_time, mm[0], mm[1], row, tm, pr);
+    // the three tables: (prefix = [type|]project) LSD passes, then each segment sorted by time in LDS
+    struct Tab {
+        int64_t n;
+        Prefix pre;
+        int pbits_total;
+        const int64_t *time;
+        int64_t tmin, tmax;
+        DevBuf *row, *tm, *pr;
+    };
+    Tab tabs[3] = {
+        {t->n_builds, Prefix{t->b_project, t->b_type, pbits}, pbits + 2, t->b_time, mm[0], mm[1], &s.b_row, &s.b_time,
+         &s.b_proj},
+        {t->n_cov, Prefix{t->c_project, nullptr, pbits}, pbits, t->c_date, mm[2], mm[3], &s.c_row, &s.c_time, &s.c_proj},
+        {t->n_issues, Prefix{t->i_project, nullptr, pbits}, pbits, t->i_rts, mm[4], mm[5], &s.i_row, &s.i_time,
+         &s.i_proj},
+    };
+    unsigned long long *big[3];
+    for (int k = 0; k < 3; ++k) {
+        Tab &b = tabs[k];
+        big[k] = sort_table_fast(c, b.n, b.pre, b.pbits_total, b.time, b.row->ensure<int32_t>(b.n),
+                                 b.tm->ensure<int64_t>(b.n), b.pr->ensure<uint32_t>(b.n));
+    }
+    auto make_views = [&]() {
+        int32_t *row = s.b_row.as<int32_t>();
+        int64_t *tm = s.b_time.as<int64_t>();
+        uint32_t *pr = s.b_proj.as<uint32_t>();
         s.fuzz = make_view(c, row, tm, pr, n_fuzz, P, s.off_fuzz);
         s.covb = make_view(c, row + n_fuzz, tm + n_fuzz, pr + n_fuzz, n_covb, P, s.off_covb);
-    }
-    // total_coverage by (project, date)
-    {
-        const int64_t n = t->n_cov;
-        int32_t *row = s.c_row.ensure<int32_t>(n);
-        int64_t *tm = s.c_time.ensure<int64_t>(n);
-        uint32_t *pr = s.c_proj.ensure<uint32_t>(n);
-        sort_table(c, n, Prefix{t->c_project, nullptr, pbits}, pbits, t->c_date, mm[2], mm[3], row, tm, pr);
-        s.cov = make_view(c, row, tm, pr, n, P, s.off_cov);
-    }
-    // issues by (project, rts)
-    {
-        const int64_t n = t->n_issues;
-        int32_t *row = s.i_row.ensure<int32_t>(n);
-        int64_t *tm = s.i_time.ensure<int64_t>(n);
-        uint32_t *pr = s.i_proj.ensure<uint32_t>(n);
-        sort_table(c, n, Prefix{t->i_project, nullptr, pbits}, pbits, t->i_rts, mm[4], mm[5], row, tm, pr);
-        s.issues = make_view(c, row, tm, pr, n, P, s.off_iss);
-    }
-    // longest segments (sizes the per-iteration outputs)
+        s.cov = make_view(c, s.c_row.as<int32_t>(), s.c_time.as<int64_t>(), s.c_proj.as<uint32_t>(), t->n_cov, P,
+                          s.off_cov);
+        s.issues = make_view(c, s.i_row.as<int32_t>(), s.i_time.as<int64_t>(), s.i_proj.as<uint32_t>(), t->n_issues,
+                             P, s.off_iss);
+    };
+    make_views();
+    // longest segments (sizes the per-iteration outputs) + rows left for the full-key path
     unsigned long long *mx = c->arena.get<unsigned long long>(4);
-    FZ_HIP(hipMemsetAsync(mx, 0, 32, c->stream));
-    const View *vs[4] = {&s.fuzz, &s.covb, &s.cov, &s.issues};
-    for (int i = 0; i < 4; ++i) {
-        if (P <= 0) break;
-        k_max_seg<<<grid_for(P, kBlock, 64), kBlock, 0, c->stream>>>(vs[i]->offs, P, mx + i);
-        FZ_LAUNCH_CHECK();
+    auto read_stats = [&]() {
+        FZ_HIP(hipMemsetAsync(mx, 0, 32, c->stream));
+        const View *vs[4] = {&s.fuzz, &s.covb, &s.cov, &s.issues};
+        for (int i = 0; i < 4; ++i) {
+            if (P <= 0) break;
+            k_max_seg<<<grid_for(P, kBlock, 64), kBlock, 0, c->stream>>>(vs[i]->offs, P, mx + i);
+            FZ_LAUNCH_CHECK();
+        }
+        FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 32, hipMemcpyDeviceToHost, c->stream));
+        for (int k = 0; k < 3; ++k)
+            FZ_HIP(hipMemcpyAsync(c->h_pinned + 4 + k, big[k], 8, hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+    };
+    read_stats();
+    bool redo = false;
+    for (int k = 0; k < 3; ++k) {
+        if (c->h_pinned[4 + k] == 0) continue;  // every segment fit in LDS
+        Tab &b = tabs[k];
+        sort_table(c, b.n, b.pre, b.pbits_total, b.time, b.tmin, b.tmax, b.row->as<int32_t>(), b.tm->as<int64_t>(),
+                   b.pr->as<uint32_t>());
+        FZ_HIP(hipMemsetAsync(big[k], 0, 8, c->stream));
+        redo = true;
     }
-    FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 32, hipMemcpyDeviceToHost, c->stream));
-    sync(c);
+    if (redo) {
+        make_views();
+        read_stats();
+    }
     s.fuzz.max_seg = c->h_pinned[0];
     s.covb.max_seg = c->h_pinned[1];
     s.cov.max_seg = c->h_pinned[2];

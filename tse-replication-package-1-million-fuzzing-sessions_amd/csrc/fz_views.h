@@ -97,6 +97,8 @@ void count_flags(fz_ctx *c, const uint8_t *flags, int64_t P, int64_t *out);
 void describe_f64_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n, fz_describe *dev_out);
 // ascending order-preserving keys (f64_key) of x[0..*d_n); entries past *d_n are ~0.
 uint64_t *sorted_keys_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n);
+// the same for nmax <= 4096 in one workgroup (LDS bitonic network, fz_series.hip)
+uint64_t *sort_small_keys(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n);
 void describe_sorted_dn(fz_ctx *c, const uint64_t *sorted_keys, const double *x, int64_t nmax, const int64_t *d_n,
                         fz_describe *dev_out);
 
