@@ -22,6 +22,7 @@ namespace fz {
 
 constexpr int kBlock = 256;   // threads per workgroup (4 wave64)
 constexpr int kWave = 64;
+constexpr int kSortBlock = 1024;  // LDS bitonic sorts: 16 waves share one 4096-entry network
 
 struct Error : std::runtime_error {
     int code;
@@ -136,6 +137,10 @@ struct Store {
     View issues;  // issues by (project, rts), ties in row order                    rq3:219-232
     int64_t passes = 0;
     int64_t tmin[3] = {0, 0, 0}, tmax[3] = {0, 0, 0};  // builds, coverage, issues (non-NULL)
+    int64_t num_min = 0, num_max = 0;                   // issues.number range
+    // eligible projects (the GROUP BY/HAVING every script starts from), computed once per load
+    DevBuf elig;     // uint8 [P]
+    DevBuf n_elig;   // int64 [1]
 };
 
 // Per-kernel timing probe (fz_probe_begin/end): brackets every launch of ONE named kernel with

@@ -62,9 +62,56 @@ __global__ __launch_bounds__(kBlock) void k_scan_chunk(const int64_t *__restrict
     if (total && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *total = off + btot;
 }
 
+// One 1024-thread workgroup scans up to 8192 elements (64 KiB of LDS): a single launch for the
+// mid-sized scans (radix digit counts of <= 32 tiles, per-project offsets, compactions).
+constexpr int kScan1Threads = 1024;
+constexpr int kScan1Items = 8;
+constexpr int kScan1Max = kScan1Threads * kScan1Items;
+
+__global__ __launch_bounds__(kScan1Threads) void k_scan_single(const int64_t *__restrict__ in,
+                                                               int64_t *__restrict__ out, int64_t n,
+                                                               int64_t *__restrict__ total) {
+    __shared__ int64_t s_val[kScan1Max];
+    __shared__ int64_t s_w[kScan1Threads / 64];
+    const int tid = threadIdx.x;
+    for (int i = 0; i < kScan1Items; ++i) {
+        const int idx = i * kScan1Threads + tid;
+        s_val[idx] = idx < n ? in[idx] : 0;
+    }
+    __syncthreads();
+    int64_t loc[kScan1Items];
+    int64_t run = 0;
+    for (int i = 0; i < kScan1Items; ++i) {
+        loc[i] = run;
+        run += s_val[tid * kScan1Items + i];
+    }
+    const int64_t inc = wave_incl_scan(run);
+    if (lane_id() == 63) s_w[wave_id()] = inc;
+    __syncthreads();
+    int64_t woff = 0, tot = 0;
+    for (int w = 0; w < kScan1Threads / 64; ++w) {
+        const int64_t v = s_w[w];
+        if (w < wave_id()) woff += v;
+        tot += v;
+    }
+    const int64_t off = woff + inc - run;
+    for (int i = 0; i < kScan1Items; ++i) s_val[tid * kScan1Items + i] = loc[i] + off;
+    __syncthreads();
+    for (int i = 0; i < kScan1Items; ++i) {
+        const int idx = i * kScan1Threads + tid;
+        if (idx < n) out[idx] = s_val[idx];
+    }
+    if (total && tid == 0) *total = tot;
+}
+
 void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, int64_t *out_total) {
     if (n <= 0) {
         if (out_total) FZ_HIP(hipMemsetAsync(out_total, 0, sizeof(int64_t), c->stream));
+        return;
+    }
+    if (n > kScanChunk && n <= kScan1Max) {
+        k_scan_single<<<1, kScan1Threads, 0, c->stream>>>(in, out, n, out_total);
+        FZ_LAUNCH_CHECK();
         return;
     }
     const int64_t nb = (n + kScanChunk - 1) / kScanChunk;

@@ -20,65 +20,113 @@ namespace fz {
 constexpr int64_t kLimitUs = 1736294400000000LL;  // '2025-01-08 00:00:00' (queries1.py:3)
 constexpr int64_t kEligMin = 365;                 // HAVING COUNT(*) >= 365
 
+__global__ __launch_bounds__(kBlock) void k_copy_elig(const uint8_t *__restrict__ src, const int64_t *__restrict__ n,
+                                                      int64_t P, uint8_t *__restrict__ dst, int64_t *__restrict__ d_count) {
+    for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < P; p += int64_t(gridDim.x) * kBlock)
+        dst[p] = src[p];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && d_count) *d_count = *n;
+}
+
 // total_coverage rows: coverage IS NOT NULL AND coverage > 0 AND date < LIMIT, per project.
+// One workgroup per CU streams a contiguous slice into an LDS histogram and writes it as one row
+// of a [blocks][P] partial table (no global atomics, deterministic); k_elig_sum adds the columns.
+constexpr int kEligBlocks = 256;
+constexpr int64_t kEligLdsMax = 16384;  // 64 KiB of int32 bins
+
 __global__ __launch_bounds__(kBlock) void k_elig_hist(const uint32_t *__restrict__ proj,
                                                       const int64_t *__restrict__ date,
                                                       const double *__restrict__ cov,
                                                       const uint8_t *__restrict__ valid, int64_t n, int64_t P,
-                                                      int64_t limit, int32_t *__restrict__ counts, int use_lds) {
+                                                      int64_t limit, int32_t *__restrict__ part) {
     extern __shared__ int32_t s_hist[];
-    if (use_lds) {
-        for (int64_t p = threadIdx.x; p < P; p += kBlock) s_hist[p] = 0;
-        __syncthreads();
-    }
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    for (int64_t p = threadIdx.x; p < P; p += kBlock) s_hist[p] = 0;
+    __syncthreads();
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = int64_t(blockIdx.x) * per, hi = lo + per < n ? lo + per : n;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
         const bool ok = (valid[i] & FZ_VALID_COVERAGE) && cov[i] > 0.0 && date[i] < limit;
-        if (ok) {
-            if (use_lds) atomicAdd(&s_hist[proj[i]], 1);
-            else atomicAdd(&counts[proj[i]], 1);
-        }
+        if (ok) atomicAdd(&s_hist[proj[i]], 1);
     }
-    if (use_lds) {
-        __syncthreads();
-        for (int64_t p = threadIdx.x; p < P; p += kBlock)
-            if (s_hist[p]) atomicAdd(&counts[p], s_hist[p]);
+    __syncthreads();
+    for (int64_t p = threadIdx.x; p < P; p += kBlock) part[int64_t(blockIdx.x) * P + p] = s_hist[p];
+}
+
+// fallback for very many projects: global atomics straight into counts
+__global__ __launch_bounds__(kBlock) void k_elig_atomic(const uint32_t *__restrict__ proj,
+                                                        const int64_t *__restrict__ date,
+                                                        const double *__restrict__ cov,
+                                                        const uint8_t *__restrict__ valid, int64_t n, int64_t limit,
+                                                        int32_t *__restrict__ counts) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+        if ((valid[i] & FZ_VALID_COVERAGE) && cov[i] > 0.0 && date[i] < limit) atomicAdd(&counts[proj[i]], 1);
+}
+
+__global__ __launch_bounds__(kBlock) void k_elig_sum(const int32_t *__restrict__ part, int nb, int64_t P,
+                                                     int32_t *__restrict__ counts, uint8_t *__restrict__ elig,
+                                                     int64_t *__restrict__ n_elig) {
+    for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < P; p += int64_t(gridDim.x) * kBlock) {
+        int32_t s = 0;
+        if (part) {
+            for (int b = 0; b < nb; ++b) s += part[int64_t(b) * P + p];
+            if (counts) counts[p] = s;
+        } else {
+            s = counts[p];
+        }
+        if (elig) {
+            const bool e = s >= kEligMin;
+            elig[p] = e;
+            if (e) atomic_add_i64(n_elig, 1);
+        }
     }
 }
 
-void eligibility_counts(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *counts) {
+// counts[p] (and, if elig != null, elig[p] = counts >= 365 with *n_elig += #eligible)
+static void eligibility(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *counts, uint8_t *elig,
+                        int64_t *n_elig) {
     const int64_t P = t->n_projects;
-    FZ_HIP(hipMemsetAsync(counts, 0, size_t(P > 0 ? P : 1) * 4, c->stream));
-    if (t->n_cov <= 0 || P <= 0) return;
-    const int use_lds = P <= 16384;
-    const size_t lds = use_lds ? size_t(P) * 4 : 0;
+    if (P <= 0) return;
     // algorithmic bytes: project 4 + date 8 + coverage 8 + validity 1 per row
     ProbeScope ps(c, "elig_hist", 21.0 * double(t->n_cov));
-    k_elig_hist<<<grid_for(t->n_cov, kBlock, 1024), kBlock, lds, c->stream>>>(
-        t->c_project, t->c_date, t->c_coverage, t->c_valid, t->n_cov, P, limit, counts, use_lds);
+    if (P <= kEligLdsMax) {
+        const int nb = t->n_cov > 0 ? kEligBlocks : 1;
+        int32_t *part = c->arena.get<int32_t>(int64_t(nb) * P);
+        k_elig_hist<<<nb, kBlock, size_t(P) * 4, c->stream>>>(t->c_project, t->c_date, t->c_coverage, t->c_valid,
+                                                               t->n_cov, P, limit, part);
+        k_elig_sum<<<grid_for(P), kBlock, 0, c->stream>>>(part, nb, P, counts, elig, n_elig);
+    } else {
+        if (!counts) counts = c->arena.get<int32_t>(P);
+        FZ_HIP(hipMemsetAsync(counts, 0, size_t(P) * 4, c->stream));
+        k_elig_atomic<<<grid_for(t->n_cov, kBlock, 2048), kBlock, 0, c->stream>>>(
+            t->c_project, t->c_date, t->c_coverage, t->c_valid, t->n_cov, limit, counts);
+        k_elig_sum<<<grid_for(P), kBlock, 0, c->stream>>>(nullptr, 0, P, counts, elig, n_elig);
+    }
     FZ_LAUNCH_CHECK();
 }
 
-__global__ __launch_bounds__(kBlock) void k_elig_flags(const int32_t *__restrict__ counts, int64_t P,
-                                                       uint8_t *__restrict__ elig, int64_t *__restrict__ n_elig) {
-    for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < P; p += int64_t(gridDim.x) * kBlock) {
-        const bool e = counts[p] >= kEligMin;
-        elig[p] = e;
-        if (e) atomic_add_i64(n_elig, 1);
-    }
+void eligibility_counts(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *counts) {
+    eligibility(c, t, limit, counts, nullptr, nullptr);
 }
 
-// elig[p] = project has >= 365 qualifying coverage rows; *d_count += number eligible.
+// Computed once per fz_store_build (store.elig / store.n_elig).
+void store_eligibility(fz_ctx *c) {
+    Store &s = c->store;
+    const int64_t P = s.P;
+    uint8_t *elig = s.elig.ensure<uint8_t>(P);
+    int64_t *n = s.n_elig.ensure<int64_t>(1);
+    FZ_HIP(hipMemsetAsync(n, 0, 8, c->stream));
+    eligibility(c, &s.t, kLimitUs, nullptr, elig, n);
+}
+
+// elig[p] = project has >= 365 qualifying coverage rows; *d_count = number eligible.
 // Every RQ script starts from this set (rq1:144-152, rq2_count:272-280, rq2_add:20-27, rq3:222-226,
-// rq4a:68-80, rq4b:164-181 - the same GROUP BY/HAVING).
+// rq4a:68-80, rq4b:164-181 - the same GROUP BY/HAVING), so the store computes it once per load.
 void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count) {
-    const fz_tables &t = c->store.t;
-    const int64_t P = t.n_projects;
-    int32_t *ecount = c->arena.get<int32_t>(P);
-    eligibility_counts(c, &t, kLimitUs, ecount);
-    if (P > 0) {
-        k_elig_flags<<<grid_for(P), kBlock, 0, c->stream>>>(ecount, P, elig, d_count);
-        FZ_LAUNCH_CHECK();
-    }
+    const Store &s = c->store;
+    const int64_t P = s.P;
+    const uint8_t *src = s.elig.as<uint8_t>();
+    const int64_t *n = s.n_elig.as<int64_t>();
+    k_copy_elig<<<grid_for(P > 0 ? P : 1), kBlock, 0, c->stream>>>(src, n, P, elig, d_count);
+    FZ_LAUNCH_CHECK();
 }
 
 // Histogram of Fuzzing-build counts over eligible projects; total and max.
@@ -165,39 +213,40 @@ __global__ __launch_bounds__(kBlock) void k_issue_pass(View iss, const uint8_t *
     }
 }
 
-// ROW_NUMBER() OVER (PARTITION BY number ORDER BY timecreated DESC) = 1: stage keys.
-__global__ __launch_bounds__(kBlock) void k_dedup_keys1(const int64_t *__restrict__ mbuild,
-                                                        const int64_t *__restrict__ mbtime, int64_t n, int64_t btmax,
-                                                        uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+// ROW_NUMBER() OVER (PARTITION BY number ORDER BY timecreated DESC) = 1 (queries1.py:29-32):
+// sort the matched rows by issue number (range-compressed key, stable in output order); in each
+// number group the row with the latest build time survives, the earliest in output order on ties.
+__global__ __launch_bounds__(kBlock) void k_dedup_keys(const int64_t *__restrict__ mbuild, View iss,
+                                                       const int64_t *__restrict__ number, int64_t n, int64_t nmin,
+                                                       uint64_t pad, uint64_t *__restrict__ keys,
+                                                       uint32_t *__restrict__ vals) {
     for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < n; j += int64_t(gridDim.x) * kBlock) {
-        keys[j] = mbuild[j] >= 0 ? uint64_t(btmax - mbtime[j]) : 0ull;
+        keys[j] = mbuild[j] >= 0 ? uint64_t(number[iss.row[j]] - nmin) : pad;
         vals[j] = uint32_t(j);
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_dedup_keys2(const uint32_t *__restrict__ vals,
-                                                        const int64_t *__restrict__ mbuild, View iss,
-                                                        const int64_t *__restrict__ number, int64_t n,
-                                                        uint64_t *__restrict__ keys) {
+__global__ __launch_bounds__(kBlock) void k_dedup_pick(const uint32_t *__restrict__ vals,
+                                                       const uint64_t *__restrict__ keys,
+                                                       const int64_t *__restrict__ mbuild,
+                                                       const int64_t *__restrict__ mbtime, int64_t n,
+                                                       int64_t *__restrict__ keep) {
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
         const uint32_t j = vals[i];
-        keys[i] = mbuild[j] >= 0 ? (uint64_t(number[iss.row[j]]) ^ 0x8000000000000000ull) : ~0ull;
-    }
-}
-
-// Sorted by (number, build time desc, output order): the head of each number segment survives.
-__global__ __launch_bounds__(kBlock) void k_dedup_heads(const uint32_t *__restrict__ vals,
-                                                        const uint64_t *__restrict__ keys,
-                                                        const int64_t *__restrict__ mbuild, int64_t n,
-                                                        int64_t *__restrict__ keep) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        const uint32_t j = vals[i];
-        bool head = mbuild[j] >= 0;
-        if (head && i > 0) {
-            const uint32_t pj = vals[i - 1];
-            head = !(mbuild[pj] >= 0 && keys[i - 1] == keys[i]);
+        if (mbuild[j] < 0) {
+            keep[j] = 0;
+            continue;
         }
-        keep[j] = head ? 1 : 0;
+        const uint64_t k = keys[i];
+        int64_t a = i, b = i + 1;  // the number group [a, b) (tiny: duplicates are rare)
+        while (a > 0 && keys[a - 1] == k) --a;
+        while (b < n && keys[b] == k) ++b;
+        uint32_t best = vals[a];
+        for (int64_t q = a + 1; q < b; ++q) {
+            const uint32_t v = vals[q];
+            if (mbtime[v] > mbtime[best] || (mbtime[v] == mbtime[best] && v < best)) best = v;
+        }
+        keep[j] = best == j ? 1 : 0;
     }
 }
 
@@ -331,15 +380,11 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_out *o) {
         uint64_t *keys = c->arena.get<uint64_t>(NI);
         uint32_t *vals = c->arena.get<uint32_t>(NI);
         const unsigned g = grid_for(NI, kBlock, 2048);
-        const int64_t btmax = s.tmax[0];
-        const int tb = bits_for(uint64_t(s.tmax[0] >= s.tmin[0] ? s.tmax[0] - s.tmin[0] : 0));
-        k_dedup_keys1<<<g, kBlock, 0, st>>>(mbuild, mbtime, NI, btmax, keys, vals);
+        const uint64_t pad = uint64_t(s.num_max >= s.num_min ? s.num_max - s.num_min : 0) + 1;
+        k_dedup_keys<<<g, kBlock, 0, st>>>(mbuild, s.issues, t.i_number, NI, s.num_min, pad, keys, vals);
         FZ_LAUNCH_CHECK();
-        radix_sort_pairs(c, keys, vals, NI, tb);
-        k_dedup_keys2<<<g, kBlock, 0, st>>>(vals, mbuild, s.issues, t.i_number, NI, keys);
-        FZ_LAUNCH_CHECK();
-        radix_sort_pairs(c, keys, vals, NI, 64);
-        k_dedup_heads<<<g, kBlock, 0, st>>>(vals, keys, mbuild, NI, keep);
+        radix_sort_pairs(c, keys, vals, NI, bits_for(pad));
+        k_dedup_pick<<<g, kBlock, 0, st>>>(vals, keys, mbuild, mbtime, NI, keep);
         FZ_LAUNCH_CHECK();
     }
     scan_exclusive_i64(c, keep, pos, NI, d_nm);

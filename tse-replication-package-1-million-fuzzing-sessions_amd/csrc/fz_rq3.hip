@@ -196,17 +196,13 @@ void rq3(fz_ctx *c, const fz_rq3_out *o) {
     double *dtot_f = c->arena.get<double>(NI);
     const int64_t *dt = o->det_tot;
     map_n(c, NI, d_nd, [=] __device__(int64_t q) { dtot_f[q] = double(dt[q]); });
-    uint64_t *skd = sorted_keys_dn(c, o->det_pct, NI, d_nd);
-    uint64_t *skn = sorted_keys_dn(c, o->non_pct, NC, d_nn);
-    describe_sorted_dn(c, skd, o->det_pct, NI, d_nd, o->describe);
-    describe_sorted_dn(c, skn, o->non_pct, NC, d_nn, o->describe + 1);
-    describe_f64_dn(c, dtot_f, NI, d_nd, o->describe + 2);
-    anderson_sorted(c, skd, o->det_pct, NI, d_nd, o->tests + FZ_RQ3_AD_DET);
-    anderson_sorted(c, skn, o->non_pct, NC, d_nn, o->tests + FZ_RQ3_AD_NON);
-    levene_two(c, skd, o->det_pct, NI, d_nd, skn, o->non_pct, NC, d_nn, o->tests + FZ_RQ3_LEVENE_W);
-    // brunnermunzel(det, non): one segment holding both samples
+    // One sort of det u non serves everything: Brunner-Munzel ranks the union, and a stable
+    // partition of the sorted union by sample gives each sample's sorted keys (describe,
+    // anderson, levene) - instead of three separate device-wide sorts.
+    const int64_t cap = NI + NC;
+    uint64_t *skd = c->arena.get<uint64_t>(cap);
+    uint64_t *skn = c->arena.get<uint64_t>(cap);
     {
-        const int64_t cap = NI + NC;
         double *v = c->arena.get<double>(cap);
         uint8_t *g = c->arena.get<uint8_t>(cap);
         const double *dp = o->det_pct, *np_ = o->non_pct;
@@ -224,11 +220,30 @@ void rq3(fz_ctx *c, const fz_rq3_out *o) {
         map_n(c, 1, nullptr, [=] __device__(int64_t) { *d_all = *d_nd + *d_nn; });
         Segs one{1, single_segment(c, d_all), cap};
         int32_t *sid = segment_ids(c, one);
+        ChunkedSegs cs = chunked(c, one);
+        SortedSegs ss = seg_sort_f64(c, v, one, sid);
         RankTestOut rt;
         rt.bm_stat = o->tests + FZ_RQ3_BM_STAT;
         rt.bm_p = o->tests + FZ_RQ3_BM_P;
-        seg_rank_tests(c, v, g, one, sid, rt);
+        seg_rank_tests_sorted(c, ss, g, cs, sid, rt);
+        // stable partition of the sorted union into the two samples
+        int64_t *isdet = c->arena.get<int64_t>(cap), *before = c->arena.get<int64_t>(cap);
+        const int32_t *pos = ss.pos;
+        const double *sv = ss.val;
+        map_n(c, cap, nullptr, [=] __device__(int64_t i) { isdet[i] = (i < *d_all && g[pos[i]] == 0) ? 1 : 0; });
+        scan_exclusive_i64(c, isdet, before, cap, nullptr);
+        map_n(c, cap, d_all, [=] __device__(int64_t i) {
+            const uint64_t k = f64_key(sv[i]);
+            if (isdet[i]) skd[before[i]] = k;
+            else skn[i - before[i]] = k;
+        });
     }
+    describe_sorted_dn(c, skd, o->det_pct, NI, d_nd, o->describe);
+    describe_sorted_dn(c, skn, o->non_pct, NC, d_nn, o->describe + 1);
+    describe_f64_dn(c, dtot_f, NI, d_nd, o->describe + 2);
+    anderson_sorted(c, skd, o->det_pct, NI, d_nd, o->tests + FZ_RQ3_AD_DET);
+    anderson_sorted(c, skn, o->non_pct, NC, d_nn, o->tests + FZ_RQ3_AD_NON);
+    levene_two(c, skd, o->det_pct, NI, d_nd, skn, o->non_pct, NC, d_nn, o->tests + FZ_RQ3_LEVENE_W);
 }
 
 }  // namespace fz

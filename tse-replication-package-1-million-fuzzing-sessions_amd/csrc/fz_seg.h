@@ -180,6 +180,9 @@ struct RankTestOut {
 };
 void seg_rank_tests(fz_ctx *c, const double *vals, const uint8_t *grp, const Segs &sg, const int32_t *segid,
                     const RankTestOut &o);
+// the same on already sorted segments (grp indexed by source position ss.pos)
+void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, const ChunkedSegs &cs,
+                           const int32_t *segid, const RankTestOut &o);
 
 // scipy.stats.levene([x, y]) (center='median') from the samples and their ascending keys
 // -> out[0] = W, out[1] = p (F(1, N-2) survival, cephes fdtrc rounding).

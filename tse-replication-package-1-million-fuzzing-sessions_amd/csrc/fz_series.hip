@@ -75,7 +75,7 @@ const int64_t *single_segment(fz_ctx *c, const int64_t *d_n) {
 // One workgroup per segment of <= kLdsSortMax values: bitonic network over (key, position) pairs
 // in LDS (48 KiB), padded to a power of two with +inf keys.  Ties may come out in any order -
 // every consumer (ranks, percentiles, rank tests) is invariant to the order inside a tie group.
-__global__ __launch_bounds__(kBlock) void k_seg_sort_lds(const double *__restrict__ src,
+__global__ __launch_bounds__(kSortBlock) void k_seg_sort_lds(const double *__restrict__ src,
                                                          const int64_t *__restrict__ offs, int64_t S,
                                                          double *__restrict__ out_val, int32_t *__restrict__ out_pos,
                                                          uint64_t *__restrict__ out_key) {
@@ -88,14 +88,14 @@ __global__ __launch_bounds__(kBlock) void k_seg_sort_lds(const double *__restric
         if (n <= 0) continue;
         int np2 = 1;
         while (np2 < n) np2 <<= 1;
-        for (int i = tid; i < np2; i += kBlock) {
+        for (int i = tid; i < np2; i += kSortBlock) {
             sk[i] = i < n ? f64_key(src[b + i]) : ~0ull;
             sp[i] = i;
         }
         __syncthreads();
         for (int k = 2; k <= np2; k <<= 1) {
             for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = tid; i < np2; i += kBlock) {
+                for (int i = tid; i < np2; i += kSortBlock) {
                     const int ixj = i ^ j;
                     if (ixj > i) {
                         const uint64_t a = sk[i], d = sk[ixj];
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_sort_lds(const double *__restric
                 __syncthreads();
             }
         }
-        for (int i = tid; i < n; i += kBlock) {
+        for (int i = tid; i < n; i += kSortBlock) {
             if (out_val) out_val[b + i] = f64_from_key(sk[i]);
             if (out_pos) out_pos[b + i] = int32_t(b + sp[i]);
             if (out_key) out_key[b + i] = sk[i];
@@ -125,7 +125,7 @@ uint64_t *sort_small_keys(fz_ctx *c, const double *x, int64_t nmax, const int64_
     uint64_t *k = c->arena.get<uint64_t>(nmax);
     const int64_t *offs = single_segment(c, d_n);
     map_n(c, nmax, nullptr, [=] __device__(int64_t i) { k[i] = ~0ull; });  // entries past *d_n
-    k_seg_sort_lds<<<1, kBlock, 0, c->stream>>>(x, offs, 1, nullptr, nullptr, k);
+    k_seg_sort_lds<<<1, kSortBlock, 0, c->stream>>>(x, offs, 1, nullptr, nullptr, k);
     FZ_LAUNCH_CHECK();
     return k;
 }
@@ -138,7 +138,7 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
     if (n <= 0) return out;
     if (sg.len_bound() <= kLdsSortMax) {
         const unsigned g = unsigned(sg.S < 8192 ? (sg.S > 0 ? sg.S : 1) : 8192);
-        k_seg_sort_lds<<<g, kBlock, 0, c->stream>>>(src, sg.offs, sg.S, out.val, out.pos, nullptr);
+        k_seg_sort_lds<<<g, kSortBlock, 0, c->stream>>>(src, sg.offs, sg.S, out.val, out.pos, nullptr);
         FZ_LAUNCH_CHECK();
         return out;
     }
@@ -153,13 +153,15 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
         vals[i] = uint32_t(i);
     });
     radix_sort_pairs(c, keys, vals, n, 64);
-    // stage 2: by segment, stable
-    map_n(c, n, nullptr, [=] __device__(int64_t i) {
-        const int64_t live = offs[S];
-        const uint32_t j = vals[i];
-        keys[i] = int64_t(j) < live ? uint64_t(segid[j]) : uint64_t(S);
-    });
-    radix_sort_pairs(c, keys, vals, n, bits_for(uint64_t(S)));
+    // stage 2: by segment, stable (one segment: already in place)
+    if (S > 1) {
+        map_n(c, n, nullptr, [=] __device__(int64_t i) {
+            const int64_t live = offs[S];
+            const uint32_t j = vals[i];
+            keys[i] = int64_t(j) < live ? uint64_t(segid[j]) : uint64_t(S);
+        });
+        radix_sort_pairs(c, keys, vals, n, bits_for(uint64_t(S)));
+    }
     double *ov = out.val;
     map_n(c, n, nullptr, [=] __device__(int64_t i) {
         const int64_t live = offs[S];
@@ -217,10 +219,16 @@ TieRanks seg_tie_ranks(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, c
 //   Mann-Whitney U asymptotic (scipy _mannwhitneyu.py: tie term, continuity) two-sided + greater
 void seg_rank_tests(fz_ctx *c, const double *vals, const uint8_t *grp, const Segs &sg, const int32_t *segid,
                     const RankTestOut &o) {
-    const int64_t n = sg.n_cap, S = sg.S;
-    const int64_t *offs = sg.offs;
     ChunkedSegs cs = chunked(c, sg);
     SortedSegs ss = seg_sort_f64(c, vals, sg, segid);
+    seg_rank_tests_sorted(c, ss, grp, cs, segid, o);
+}
+
+void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, const ChunkedSegs &cs,
+                           const int32_t *segid, const RankTestOut &o) {
+    const Segs &sg = cs.sg;
+    const int64_t n = sg.n_cap, S = sg.S;
+    const int64_t *offs = sg.offs;
     TieRanks tr = seg_tie_ranks(c, cs, segid, ss.val);
     // cx[i] = number of x elements before sorted position i (cx[n] = total)
     int64_t *isx = c->arena.get<int64_t>(n);

@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kBlock) void k_prefix_offsets(const uint64_t *__res
 
 // One workgroup per prefix segment (<= kSegSortMax rows, already in row order): bitonic sort of
 // (time, position) pairs in LDS - the position tie-break keeps equal times in row order (stable).
-__global__ __launch_bounds__(kBlock) void k_seg_time_sort(const uint32_t *__restrict__ rows,
+__global__ __launch_bounds__(kSortBlock) void k_seg_time_sort(const uint32_t *__restrict__ rows,
                                                           const int64_t *__restrict__ time,
                                                           const int64_t *__restrict__ offs, int64_t S, uint32_t pmask,
                                                           int32_t *__restrict__ orow, int64_t *__restrict__ otime,
@@ -154,14 +154,14 @@ __global__ __launch_bounds__(kBlock) void k_seg_time_sort(const uint32_t *__rest
         const int n = int(len);
         int np2 = 1;
         while (np2 < n) np2 <<= 1;
-        for (int i = tid; i < np2; i += kBlock) {
+        for (int i = tid; i < np2; i += kSortBlock) {
             st[i] = i < n ? time[rows[b + i]] : INT64_MAX;  // NULL = INT64_MAX sorts last; pads after
             si[i] = i;
         }
         __syncthreads();
         for (int k = 2; k <= np2; k <<= 1) {
             for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = tid; i < np2; i += kBlock) {
+                for (int i = tid; i < np2; i += kSortBlock) {
                     const int ixj = i ^ j;
                     if (ixj > i) {
                         const int64_t ta = st[i], tb = st[ixj];
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_time_sort(const uint32_t *__rest
             }
         }
         const uint32_t p = uint32_t(s) & pmask;
-        for (int i = tid; i < n; i += kBlock) {
+        for (int i = tid; i < n; i += kSortBlock) {
             orow[b + i] = int32_t(rows[b + si[i]]);
             otime[b + i] = st[i];
             oproj[b + i] = p;
@@ -208,7 +208,7 @@ static unsigned long long *sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int
     const uint32_t pmask = pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << pre.pbits) - 1ull);
     {
         ProbeScope ps(c, "seg_time_sort", 28.0 * double(n));  // row 4 + gathered time 8 + out 16 B
-        k_seg_time_sort<<<unsigned(S < 16384 ? S : 16384), kBlock, 0, c->stream>>>(vals, time, offs, S, pmask, orow,
+        k_seg_time_sort<<<unsigned(S < 16384 ? S : 16384), kSortBlock, 0, c->stream>>>(vals, time, offs, S, pmask, orow,
                                                                                   otime, oproj, big);
         FZ_LAUNCH_CHECK();
     }
@@ -258,6 +258,8 @@ static View make_view(fz_ctx *c, const int32_t *row, const int64_t *time, const 
     return v;
 }
 
+void store_eligibility(fz_ctx *c);  // fz_rq1.hip
+
 void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     FZ_CHECK(t != nullptr, "fz_store_build: tables is null");
     FZ_CHECK(t->n_projects >= 0 && t->n_builds >= 0 && t->n_cov >= 0 && t->n_issues >= 0, "negative table size");
@@ -272,16 +274,19 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
 
     // one host round trip: time ranges of the three tables + build-type counts
-    int64_t mm[6];
-    const int64_t *cols[3] = {t->b_time, t->c_date, t->i_rts};
-    const int64_t ns[3] = {t->n_builds, t->n_cov, t->n_issues};
+    int64_t mm[8];
+    const int64_t *cols[4] = {t->b_time, t->c_date, t->i_rts, t->i_number};
+    const int64_t ns[4] = {t->n_builds, t->n_cov, t->n_issues, t->n_issues};
+    store_eligibility(c);
     unsigned long long *tcnt = c->arena.get<unsigned long long>(2);
     FZ_HIP(hipMemsetAsync(tcnt, 0, 16, c->stream));
     if (t->n_builds > 0) {
         k_count_types<<<grid_for(t->n_builds, kBlock * 8, 512), kBlock, 0, c->stream>>>(t->b_type, t->n_builds, tcnt);
         FZ_LAUNCH_CHECK();
     }
-    minmax_i64_to_host(c, cols, ns, 3, mm);  // syncs the stream
+    minmax_i64_to_host(c, cols, ns, 4, mm);  // syncs the stream
+    s.num_min = mm[6];
+    s.num_max = mm[7];
     unsigned long long hcnt[2];
     FZ_HIP(hipMemcpy(hcnt, tcnt, 16, hipMemcpyDeviceToHost));
     const int64_t n_fuzz = int64_t(hcnt[0]), n_covb = int64_t(hcnt[1]);
