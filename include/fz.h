@@ -146,6 +146,27 @@ typedef struct fz_rq1_out {
 
 int fz_rq1(fz_ctx *ctx, int64_t min_project_threshold, const fz_rq1_out *out);
 
+/* Project-sharded RQ1.  SAME_DATE_BUILD_ISSUE dedups with ROW_NUMBER() OVER
+ * (PARTITION BY i.number ORDER BY timecreated DESC) (queries1.py:29-32) - across projects, so across
+ * shards.  fz_rq1_ex runs fz_rq1 with the other shards' matches as extra competitors: a local
+ * match survives only if it beats every competitor with its number (later build time; on a tie the
+ * earlier row in ORDER BY project, rts - i.e. a competitor with before = 1 wins ties).  Device
+ * arrays of n entries; n = 0 is fz_rq1. */
+typedef struct fz_rq1_ext {
+    int64_t n;
+    const int64_t *number;        /* issue number */
+    const int64_t *build_time;    /* matched build timecreated */
+    const uint8_t *before;        /* 1: the competitor's shard precedes this one in project order */
+} fz_rq1_ext;
+
+int fz_rq1_ex(fz_ctx *ctx, int64_t min_project_threshold, const fz_rq1_ext *ext, const fz_rq1_out *out);
+
+/* Finishing of RQ1 (rq1_detection_rate.py:233-268) on shard-summed iteration tables: recomputes
+ * counts[FZ_RQ1_KEPT_ITERS], counts[FZ_RQ1_FIRST_DOWN], counts[FZ_RQ1_LATE] and *late from
+ * iter_total / iter_detected[max_iter] (device).  Other counts are left untouched. */
+int fz_rq1_finish(fz_ctx *ctx, int64_t min_project_threshold, const int64_t *iter_total,
+                  const int64_t *iter_detected, int64_t max_iter, int64_t *counts, fz_describe *late);
+
 /* ---- RQ2 (count): rq2_coverage_count.py:244-483 ------------------------------------------ */
 enum {
     FZ_RQ2C_ELIGIBLE = 0,   /* eligible projects                                     :272-280 */
@@ -202,7 +223,15 @@ typedef struct fz_rq2_add_out {
 int fz_rq2_add(fz_ctx *ctx, const fz_rq2_add_out *out);
 
 /* ---- RQ3: rq3_diff_coverage_at_detection.py:202-360 -------------------------------------- */
-enum { FZ_RQ3_ISSUES = 0, FZ_RQ3_DETECTED, FZ_RQ3_NON_DETECTED, FZ_RQ3_ELIGIBLE, FZ_RQ3_NCOUNTS = 4 };
+enum {
+    FZ_RQ3_ISSUES = 0,
+    FZ_RQ3_DETECTED,
+    FZ_RQ3_NON_DETECTED,
+    FZ_RQ3_ELIGIBLE,
+    FZ_RQ3_NON_LAST,              /* non-detected rows of the last issue-bearing project (0 unless
+                                     FZ_RQ3_FLUSH_LAST; they are the tail of non_*) */
+    FZ_RQ3_NCOUNTS = 8
+};
 enum {
     FZ_RQ3_AD_DET = 0,            /* anderson(detected).statistic, then 5 critical values   :329 */
     FZ_RQ3_AD_NON = 6,            /* anderson(non-detected)                                 :335 */
@@ -225,6 +254,20 @@ typedef struct fz_rq3_out {
 } fz_rq3_out;
 
 int fz_rq3(fz_ctx *ctx, const fz_rq3_out *out);
+
+/* Project-sharded RQ3.  The reference flushes a project's non-detected changes when the issue loop
+ * moves to the next project, so the globally last issue-bearing project is never flushed
+ * (rq3:245-257).  With FZ_RQ3_FLUSH_LAST a shard flushes its last project too and reports that
+ * project's row count in counts[FZ_RQ3_NON_LAST]; the caller drops those rows on the last shard
+ * that has issues and runs the statistics once over the gathered samples (fz_rq3_stats). */
+#define FZ_RQ3_FLUSH_LAST 1u
+int fz_rq3_ex(fz_ctx *ctx, uint32_t flags, const fz_rq3_out *out);
+
+/* RQ3 statistics (rq3:321-352) over two device samples: describe[3] (detected pct, non-detected
+ * pct, detected total-line delta) and tests[FZ_RQ3_NTESTS] (Anderson x2, Levene, Brunner-Munzel;
+ * left unset unless both samples are non-empty). */
+int fz_rq3_stats(fz_ctx *ctx, const double *det_pct, const int64_t *det_tot, int64_t n_det, const double *non_pct,
+                 int64_t n_non, fz_describe *describe, double *tests);
 
 /* ---- RQ4 inputs: data/processed_data/csv/project_corpus_analysis.csv (user_corpus.py:225-233) ---
  * Parsed on the host (it is a ~1k-row CSV) into per-project columns, independent of eligibility:

@@ -8,11 +8,15 @@
 
 namespace fz {
 void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats);
-void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_out *o);
+void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_ext *ext, const fz_rq1_out *o);
+void rq1_finish(fz_ctx *c, int64_t threshold, const int64_t *iter_total, const int64_t *iter_det, int64_t M,
+                int64_t *counts, fz_describe *late);
 void eligibility_counts(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *counts);
 void rq2_count(fz_ctx *c, const fz_rq2_count_out *o);
 void rq2_add(fz_ctx *c, const fz_rq2_add_out *o);
-void rq3(fz_ctx *c, const fz_rq3_out *o);
+void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o);
+void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t NI, const int64_t *d_nd,
+               const double *non_pct, int64_t NC, const int64_t *d_nn, fz_describe *describe, double *tests);
 void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o);
 void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o);
 }  // namespace fz
@@ -93,7 +97,20 @@ int fz_store_build(fz_ctx *ctx, const fz_tables *t, fz_store_stats *stats) {
 }
 
 int fz_rq1(fz_ctx *ctx, int64_t min_project_threshold, const fz_rq1_out *out) {
-    return guarded(ctx, [&] { fz::rq1(ctx, min_project_threshold, out); });
+    return guarded(ctx, [&] { fz::rq1(ctx, min_project_threshold, nullptr, out); });
+}
+
+int fz_rq1_ex(fz_ctx *ctx, int64_t min_project_threshold, const fz_rq1_ext *ext, const fz_rq1_out *out) {
+    return guarded(ctx, [&] { fz::rq1(ctx, min_project_threshold, ext, out); });
+}
+
+int fz_rq1_finish(fz_ctx *ctx, int64_t min_project_threshold, const int64_t *iter_total,
+                  const int64_t *iter_detected, int64_t max_iter, int64_t *counts, fz_describe *late) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(counts && late && max_iter >= 0 && (max_iter == 0 || (iter_total && iter_detected)),
+                 "fz_rq1_finish: bad arguments");
+        fz::rq1_finish(ctx, min_project_threshold, iter_total, iter_detected, max_iter, counts, late);
+    });
 }
 
 int fz_rq2_count(fz_ctx *ctx, const fz_rq2_count_out *out) {
@@ -105,7 +122,25 @@ int fz_rq2_add(fz_ctx *ctx, const fz_rq2_add_out *out) {
 }
 
 int fz_rq3(fz_ctx *ctx, const fz_rq3_out *out) {
-    return guarded(ctx, [&] { fz::rq3(ctx, out); });
+    return guarded(ctx, [&] { fz::rq3(ctx, 0u, out); });
+}
+
+int fz_rq3_ex(fz_ctx *ctx, uint32_t flags, const fz_rq3_out *out) {
+    return guarded(ctx, [&] { fz::rq3(ctx, flags, out); });
+}
+
+int fz_rq3_stats(fz_ctx *ctx, const double *det_pct, const int64_t *det_tot, int64_t n_det, const double *non_pct,
+                 int64_t n_non, fz_describe *describe, double *tests) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(describe && tests && n_det >= 0 && n_non >= 0 && (n_det == 0 || (det_pct && det_tot)) &&
+                     (n_non == 0 || non_pct),
+                 "fz_rq3_stats: bad arguments");
+        int64_t *d_n = ctx->arena.get<int64_t>(2);
+        const int64_t h[2] = {n_det, n_non};
+        FZ_HIP(hipMemcpyAsync(d_n, h, sizeof(h), hipMemcpyHostToDevice, ctx->stream));
+        fz::rq3_stats(ctx, det_pct, det_tot, n_det, d_n, non_pct, n_non, d_n + 1, describe, tests);
+        fz::sync(ctx);  // h lives on this stack frame
+    });
 }
 
 int fz_rq4a(fz_ctx *ctx, const fz_rq4_groups *groups, const fz_rq4a_out *out) {

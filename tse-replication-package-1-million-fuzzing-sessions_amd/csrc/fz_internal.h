@@ -164,6 +164,10 @@ struct fz_ctx {
     fz::Store store;
     fz::Probe probe;
     int64_t *h_pinned = nullptr;   // small pinned host staging area (4 KiB)
+    // single-pass scan state (fz_prims.hip): tile tickets + per-tile status words; both are left
+    // zeroed by the last workgroup of every scan, so the next scan (or a graph replay) starts clean
+    fz::DevBuf scan_status;        // uint64 [tiles]
+    fz::DevBuf scan_counters;      // uint32 [2]: ticket, done
 };
 
 namespace fz {

@@ -226,13 +226,18 @@ __global__ __launch_bounds__(kBlock) void k_dedup_keys(const int64_t *__restrict
     }
 }
 
+// Entries [0, n_loc) are this shard's matches; entries from n_loc on are other shards' (ext):
+// they compete for their number but are never kept.  Tie order = ORDER BY project, rts across
+// shards: an ext entry from a preceding shard sorts before every local row, one from a following
+// shard after.
 __global__ __launch_bounds__(kBlock) void k_dedup_pick(const uint32_t *__restrict__ vals,
                                                        const uint64_t *__restrict__ keys,
                                                        const int64_t *__restrict__ mbuild,
-                                                       const int64_t *__restrict__ mbtime, int64_t n,
-                                                       int64_t *__restrict__ keep) {
+                                                       const int64_t *__restrict__ mbtime, int64_t n_loc,
+                                                       fz_rq1_ext ext, int64_t n, int64_t *__restrict__ keep) {
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
         const uint32_t j = vals[i];
+        if (j >= n_loc) continue;
         if (mbuild[j] < 0) {
             keep[j] = 0;
             continue;
@@ -241,12 +246,29 @@ __global__ __launch_bounds__(kBlock) void k_dedup_pick(const uint32_t *__restric
         int64_t a = i, b = i + 1;  // the number group [a, b) (tiny: duplicates are rare)
         while (a > 0 && keys[a - 1] == k) --a;
         while (b < n && keys[b] == k) ++b;
-        uint32_t best = vals[a];
-        for (int64_t q = a + 1; q < b; ++q) {
+        const int64_t tj = mbtime[j];
+        bool win = true;
+        for (int64_t q = a; q < b && win; ++q) {
             const uint32_t v = vals[q];
-            if (mbtime[v] > mbtime[best] || (mbtime[v] == mbtime[best] && v < best)) best = v;
+            if (v == j) continue;
+            if (v < n_loc) {
+                if (mbuild[v] < 0) continue;
+                win = tj > mbtime[v] || (tj == mbtime[v] && j < v);
+            } else {
+                const int64_t e = v - n_loc, te = ext.build_time[e];
+                win = tj > te || (tj == te && !ext.before[e]);
+            }
         }
-        keep[j] = best == j ? 1 : 0;
+        keep[j] = win ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_dedup_ext_keys(fz_rq1_ext ext, int64_t nmin, uint64_t pad, int64_t n_loc,
+                                                           uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    for (int64_t e = int64_t(blockIdx.x) * kBlock + threadIdx.x; e < ext.n; e += int64_t(gridDim.x) * kBlock) {
+        const int64_t d = ext.number[e] - nmin;
+        keys[n_loc + e] = d >= 0 && uint64_t(d) < pad ? uint64_t(d) : pad;
+        vals[n_loc + e] = uint32_t(n_loc + e);
     }
 }
 
@@ -320,12 +342,34 @@ __global__ __launch_bounds__(kBlock) void k_late_copy(const double *__restrict__
         late[i] = rates[lo + i];
 }
 
-void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_out *o) {
+void rq1_finish(fz_ctx *c, int64_t threshold, const int64_t *iter_total, const int64_t *iter_det, int64_t M,
+                int64_t *counts, fz_describe *late_out) {
+    hipStream_t st = c->stream;
+    FZ_HIP(hipMemsetAsync(counts + FZ_RQ1_KEPT_ITERS, 0, sizeof(int64_t), st));
+    FZ_HIP(hipMemsetAsync(counts + FZ_RQ1_FIRST_DOWN, 0xff, sizeof(int64_t), st));
+    double *rates = c->arena.get<double>(M);
+    double *late = c->arena.get<double>(M);
+    int64_t *late_lo = c->arena.get<int64_t>(2);
+    if (M > 0) {
+        k_rates<<<grid_for(M), kBlock, 0, st>>>(iter_total, iter_det, M, threshold, counts, rates);
+        FZ_LAUNCH_CHECK();
+    }
+    k_late_bounds<<<1, 64, 0, st>>>(counts, late_lo);
+    k_late_copy<<<grid_for(M > 0 ? M : 1), kBlock, 0, st>>>(rates, late_lo, late);
+    FZ_LAUNCH_CHECK();
+    describe_f64_dn(c, late, M, late_lo + 1, late_out);
+}
+
+void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_ext *ext_in, const fz_rq1_out *o) {
     Store &s = c->store;
     FZ_CHECK(s.built, "fz_rq1: call fz_store_build first");
     FZ_CHECK(o && o->counts && o->eligible && o->iter_total && o->iter_detected && o->matched_issue &&
                  o->matched_build && o->late,
              "fz_rq1: null output buffer");
+    const fz_rq1_ext ext = ext_in ? *ext_in : fz_rq1_ext{0, nullptr, nullptr, nullptr};
+    FZ_CHECK(ext.n >= 0 && (ext.n == 0 || (ext.number && ext.build_time && ext.before)),
+             "fz_rq1_ex: bad competitor arrays");
+    FZ_CHECK(s.issues.n + ext.n < (int64_t(1) << 32), "fz_rq1_ex: too many competitors");
     const fz_tables &t = s.t;
     const int64_t P = s.P;
     const int64_t M = s.fuzz.max_seg;
@@ -377,14 +421,20 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_out *o) {
     int64_t *pos = c->arena.get<int64_t>(NI);
     int64_t *d_nm = o->counts + FZ_RQ1_MATCHED;
     if (NI > 0) {
-        uint64_t *keys = c->arena.get<uint64_t>(NI);
-        uint32_t *vals = c->arena.get<uint32_t>(NI);
-        const unsigned g = grid_for(NI, kBlock, 2048);
+        const int64_t NA = NI + ext.n;
+        uint64_t *keys = c->arena.get<uint64_t>(NA);
+        uint32_t *vals = c->arena.get<uint32_t>(NA);
+        const unsigned g = grid_for(NA, kBlock, 2048);
         const uint64_t pad = uint64_t(s.num_max >= s.num_min ? s.num_max - s.num_min : 0) + 1;
-        k_dedup_keys<<<g, kBlock, 0, st>>>(mbuild, s.issues, t.i_number, NI, s.num_min, pad, keys, vals);
+        k_dedup_keys<<<grid_for(NI, kBlock, 2048), kBlock, 0, st>>>(mbuild, s.issues, t.i_number, NI, s.num_min, pad,
+                                                                    keys, vals);
         FZ_LAUNCH_CHECK();
-        radix_sort_pairs(c, keys, vals, NI, bits_for(pad));
-        k_dedup_pick<<<g, kBlock, 0, st>>>(vals, keys, mbuild, mbtime, NI, keep);
+        if (ext.n > 0) {
+            k_dedup_ext_keys<<<grid_for(ext.n, kBlock, 2048), kBlock, 0, st>>>(ext, s.num_min, pad, NI, keys, vals);
+            FZ_LAUNCH_CHECK();
+        }
+        radix_sort_pairs(c, keys, vals, NA, bits_for(pad));
+        k_dedup_pick<<<g, kBlock, 0, st>>>(vals, keys, mbuild, mbtime, NI, ext, NA, keep);
         FZ_LAUNCH_CHECK();
     }
     scan_exclusive_i64(c, keep, pos, NI, d_nm);
@@ -407,17 +457,7 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_out *o) {
     }
 
     // finalize (:233-268)
-    double *rates = c->arena.get<double>(M);
-    double *late = c->arena.get<double>(M);
-    int64_t *late_lo = c->arena.get<int64_t>(2);
-    if (M > 0) {
-        k_rates<<<grid_for(M), kBlock, 0, st>>>(o->iter_total, o->iter_detected, M, threshold, o->counts, rates);
-        FZ_LAUNCH_CHECK();
-    }
-    k_late_bounds<<<1, 64, 0, st>>>(o->counts, late_lo);
-    k_late_copy<<<grid_for(M > 0 ? M : 1), kBlock, 0, st>>>(rates, late_lo, late);
-    FZ_LAUNCH_CHECK();
-    describe_f64_dn(c, late, M, late_lo + 1, o->late);
+    rq1_finish(c, threshold, o->iter_total, o->iter_detected, M, o->counts, o->late);
 }
 
 }  // namespace fz

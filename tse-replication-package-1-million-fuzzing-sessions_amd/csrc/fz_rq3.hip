@@ -74,7 +74,10 @@ static void anderson_sorted(fz_ctx *c, const uint64_t *sk, const double *x, int6
     });
 }
 
-void rq3(fz_ctx *c, const fz_rq3_out *o) {
+void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t NI, const int64_t *d_nd,
+               const double *non_pct, int64_t NC, const int64_t *d_nn, fz_describe *describe, double *tests);
+
+void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     Store &s = c->store;
     FZ_CHECK(s.built, "fz_rq3: call fz_store_build first");
     FZ_CHECK(o && o->counts && o->eligible && o->det_pct && o->det_cov && o->det_tot && o->det_project &&
@@ -157,13 +160,15 @@ void rq3(fz_ctx *c, const fz_rq3_out *o) {
                                                                               doffs);
     FZ_LAUNCH_CHECK();
 
-    // ---- non-detected: projects with issues, except the last one (never flushed, :245-257)
+    // ---- non-detected: projects with issues, except the last one (never flushed, :245-257) -
+    // unless this is a shard that is not the last one (FZ_RQ3_FLUSH_LAST; the caller decides)
     uint8_t *hasiss = c->arena.get<uint8_t>(P);
     const int64_t *ioffs = I.offs;
+    const bool flush_last = flags & FZ_RQ3_FLUSH_LAST;
     per_seg(c, P, [=] __device__(int64_t p) {
         const int64_t n = *d_ni;
         const uint32_t last = n > 0 ? iproj[n - 1] : 0xffffffffu;
-        hasiss[p] = (ioffs[p + 1] > ioffs[p]) && uint32_t(p) != last;
+        hasiss[p] = (ioffs[p + 1] > ioffs[p]) && (flush_last || uint32_t(p) != last);
     });
     int64_t *nflag = c->arena.get<int64_t>(NC);
     int64_t *npos = c->arena.get<int64_t>(NC);
@@ -179,6 +184,7 @@ void rq3(fz_ctx *c, const fz_rq3_out *o) {
         if (q < hi && dday[q] == day) return;  // a detection day of this project
         if (!(ctot[ra] > 0 && ctot[rb] > 0)) return;
         nflag[k] = 1;
+        if (p == iproj[*d_ni - 1]) atomic_add_i64(&counts[FZ_RQ3_NON_LAST], 1);
     });
     scan_exclusive_i64(c, nflag, npos, NC, counts + FZ_RQ3_NON_DETECTED);
     map_n(c, NC, nullptr, [=] __device__(int64_t k) {
@@ -191,10 +197,15 @@ void rq3(fz_ctx *c, const fz_rq3_out *o) {
     });
     map_n(c, 1, nullptr, [=] __device__(int64_t) { counts[FZ_RQ3_ISSUES] = *d_ni; });
 
-    // ---- statistics (:321-352)
-    const int64_t *d_nd = counts + FZ_RQ3_DETECTED, *d_nn = counts + FZ_RQ3_NON_DETECTED;
+    rq3_stats(c, o->det_pct, o->det_tot, NI, counts + FZ_RQ3_DETECTED, o->non_pct, NC, counts + FZ_RQ3_NON_DETECTED,
+              o->describe, o->tests);
+}
+
+// ---- statistics (:321-352) over samples of device lengths *d_nd <= NI and *d_nn <= NC
+void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t NI, const int64_t *d_nd,
+               const double *non_pct, int64_t NC, const int64_t *d_nn, fz_describe *describe, double *tests) {
     double *dtot_f = c->arena.get<double>(NI);
-    const int64_t *dt = o->det_tot;
+    const int64_t *dt = det_tot;
     map_n(c, NI, d_nd, [=] __device__(int64_t q) { dtot_f[q] = double(dt[q]); });
     // One sort of det u non serves everything: Brunner-Munzel ranks the union, and a stable
     // partition of the sorted union by sample gives each sample's sorted keys (describe,
@@ -205,7 +216,7 @@ void rq3(fz_ctx *c, const fz_rq3_out *o) {
     {
         double *v = c->arena.get<double>(cap);
         uint8_t *g = c->arena.get<uint8_t>(cap);
-        const double *dp = o->det_pct, *np_ = o->non_pct;
+        const double *dp = det_pct, *np_ = non_pct;
         map_n(c, cap, nullptr, [=] __device__(int64_t i) {
             const int64_t nd = *d_nd, nn = *d_nn;
             if (i < nd) {
@@ -223,8 +234,8 @@ void rq3(fz_ctx *c, const fz_rq3_out *o) {
         ChunkedSegs cs = chunked(c, one);
         SortedSegs ss = seg_sort_f64(c, v, one, sid);
         RankTestOut rt;
-        rt.bm_stat = o->tests + FZ_RQ3_BM_STAT;
-        rt.bm_p = o->tests + FZ_RQ3_BM_P;
+        rt.bm_stat = tests + FZ_RQ3_BM_STAT;
+        rt.bm_p = tests + FZ_RQ3_BM_P;
         seg_rank_tests_sorted(c, ss, g, cs, sid, rt);
         // stable partition of the sorted union into the two samples
         int64_t *isdet = c->arena.get<int64_t>(cap), *before = c->arena.get<int64_t>(cap);
@@ -238,12 +249,12 @@ void rq3(fz_ctx *c, const fz_rq3_out *o) {
             else skn[i - before[i]] = k;
         });
     }
-    describe_sorted_dn(c, skd, o->det_pct, NI, d_nd, o->describe);
-    describe_sorted_dn(c, skn, o->non_pct, NC, d_nn, o->describe + 1);
-    describe_f64_dn(c, dtot_f, NI, d_nd, o->describe + 2);
-    anderson_sorted(c, skd, o->det_pct, NI, d_nd, o->tests + FZ_RQ3_AD_DET);
-    anderson_sorted(c, skn, o->non_pct, NC, d_nn, o->tests + FZ_RQ3_AD_NON);
-    levene_two(c, skd, o->det_pct, NI, d_nd, skn, o->non_pct, NC, d_nn, o->tests + FZ_RQ3_LEVENE_W);
+    describe_sorted_dn(c, skd, det_pct, NI, d_nd, describe);
+    describe_sorted_dn(c, skn, non_pct, NC, d_nn, describe + 1);
+    describe_f64_dn(c, dtot_f, NI, d_nd, describe + 2);
+    anderson_sorted(c, skd, det_pct, NI, d_nd, tests + FZ_RQ3_AD_DET);
+    anderson_sorted(c, skn, non_pct, NC, d_nn, tests + FZ_RQ3_AD_NON);
+    levene_two(c, skd, det_pct, NI, d_nd, skn, non_pct, NC, d_nn, tests + FZ_RQ3_LEVENE_W);
 }
 
 }  // namespace fz

@@ -39,16 +39,31 @@ ChunkMap make_chunks(fz_ctx *c, const Segs &sg);
 // seg id of every element (binary search over offsets); elements past offs[S] get S.
 int32_t *segment_ids(fz_ctx *c, const Segs &sg);
 
+// Chunk k of a segmented reduction.  Explicit maps (cm.d_n != null) list the chunks; implicit
+// ones (cps chunks per segment, chosen on the host when every segment is short) derive chunk k
+// from the offsets - segment k / cps, piece k % cps - so no map kernels run.  With out != null
+// (cps == 1) the chunk sum is the segment result and is written straight to out.
 template <int NV, typename F>
-__global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, F f, double *__restrict__ part) {
+__global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, const int64_t *__restrict__ offs, int64_t cps,
+                                                         F f, double *__restrict__ part, double *__restrict__ out) {
     __shared__ double s_hi[4][NV], s_lo[4][NV];
     const int64_t k = blockIdx.x;
-    if (k >= *cm.d_n) return;
-    const int32_t seg = cm.seg[k];
+    int32_t seg;
+    int64_t b, e;
+    if (cm.d_n) {
+        if (k >= *cm.d_n) return;
+        seg = cm.seg[k];
+        b = cm.begin[k];
+        e = cm.end[k];
+    } else {
+        seg = int32_t(k / cps);
+        b = offs[seg] + (k % cps) * kChunk;
+        e = b + kChunk < offs[seg + 1] ? b + kChunk : offs[seg + 1];
+    }
     DD acc[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) acc[v] = DD{0.0, 0.0};
-    for (int64_t i = cm.begin[k] + threadIdx.x; i < cm.end[k]; i += kBlock) {
+    for (int64_t i = b + threadIdx.x; i < e; i += kBlock) {
         double x[NV];
         f(i, seg, x);
 #pragma unroll
@@ -67,18 +82,23 @@ __global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, F f, doubl
         const int v = threadIdx.x;
         DD t{s_hi[0][v], s_lo[0][v]};
         for (int w = 1; w < 4; ++w) t = dd_add(t, DD{s_hi[w][v], s_lo[w][v]});
-        part[(k * NV + v) * 2] = t.hi;
-        part[(k * NV + v) * 2 + 1] = t.lo;
+        if (out) {
+            out[int64_t(seg) * NV + v] = t.hi + t.lo;
+        } else {
+            part[(k * NV + v) * 2] = t.hi;
+            part[(k * NV + v) * 2 + 1] = t.lo;
+        }
     }
 }
 
-// out[s * NV + v] = sum over segment s's chunks (one wave per segment, chunks in order).
+// out[s * NV + v] = sum over segment s's chunks (one wave per segment, chunks in order; implicit
+// maps: chunk_off == null, segment s owns chunks [s * cps, (s + 1) * cps)).
 template <int NV>
-__global__ __launch_bounds__(kBlock) void k_seg_sum(ChunkMap cm, int64_t S, const int64_t *__restrict__ chunk_off,
+__global__ __launch_bounds__(kBlock) void k_seg_sum(int64_t S, const int64_t *__restrict__ chunk_off, int64_t cps,
                                                     const double *__restrict__ part, double *__restrict__ out) {
     const int64_t s = int64_t(blockIdx.x) * 4 + wave_id();
     if (s >= S) return;
-    const int64_t c0 = chunk_off[s], c1 = chunk_off[s + 1];
+    const int64_t c0 = chunk_off ? chunk_off[s] : s * cps, c1 = chunk_off ? chunk_off[s + 1] : (s + 1) * cps;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         DD acc{0.0, 0.0};
@@ -89,25 +109,31 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum(ChunkMap cm, int64_t S, cons
 }
 
 // Chunk offsets per segment (kept beside the map so k_seg_sum can find a segment's chunks).
+// Implicit when cps > 0 (then cm is empty and chunk_off null).
 struct ChunkedSegs {
     Segs sg;
     ChunkMap cm;
     int64_t *chunk_off = nullptr;  // [S + 1]
+    int64_t cps = 0;               // implicit: chunks per segment
 };
 ChunkedSegs chunked(fz_ctx *c, const Segs &sg);
 
 // Segmented sum of NV per-element values f(i, seg, x[NV]) -> out[S][NV] (device).
 template <int NV, typename F>
 void seg_reduce(fz_ctx *c, const ChunkedSegs &cs, F f, double *out) {
-    double *part = c->arena.get<double>(cs.cm.cap * NV * 2);
-    if (cs.cm.cap > 0) {
-        k_chunk_reduce<NV, F><<<unsigned(cs.cm.cap), kBlock, 0, c->stream>>>(cs.cm, f, part);
+    const int64_t S = cs.sg.S;
+    if (S <= 0) return;
+    if (cs.cps == 1) {
+        k_chunk_reduce<NV, F><<<unsigned(S), kBlock, 0, c->stream>>>(cs.cm, cs.sg.offs, 1, f, nullptr, out);
         FZ_LAUNCH_CHECK();
+        return;
     }
-    if (cs.sg.S > 0) {
-        k_seg_sum<NV><<<unsigned((cs.sg.S + 3) / 4), kBlock, 0, c->stream>>>(cs.cm, cs.sg.S, cs.chunk_off, part, out);
-        FZ_LAUNCH_CHECK();
-    }
+    const int64_t blocks = cs.cps > 0 ? S * cs.cps : cs.cm.cap;
+    double *part = c->arena.get<double>(blocks * NV * 2);
+    k_chunk_reduce<NV, F><<<unsigned(blocks), kBlock, 0, c->stream>>>(cs.cm, cs.sg.offs, cs.cps, f, part, nullptr);
+    FZ_LAUNCH_CHECK();
+    k_seg_sum<NV><<<unsigned((S + 3) / 4), kBlock, 0, c->stream>>>(S, cs.chunk_off, cs.cps, part, out);
+    FZ_LAUNCH_CHECK();
 }
 
 // Per-segment finishing: f(s) for s in [0, S).

@@ -30,6 +30,14 @@ __global__ __launch_bounds__(kBlock) void k_chunk_fill(const int64_t *__restrict
 ChunkedSegs chunked(fz_ctx *c, const Segs &sg) {
     ChunkedSegs cs;
     cs.sg = sg;
+    // Short segments: implicit chunks (no map kernels) while the grid stays near the explicit
+    // one - an empty chunk's workgroup exits after two offset loads.
+    const int64_t cps = sg.len_bound() > kChunk ? (sg.len_bound() + kChunk - 1) / kChunk : 1;
+    const int64_t explicit_cap = sg.S + sg.n_cap / kChunk + 1;
+    if (sg.S > 0 && (cps == 1 || sg.S * cps <= 2 * explicit_cap + 4096) && sg.S * cps < (int64_t(1) << 31)) {
+        cs.cps = cps;
+        return cs;
+    }
     ChunkMap &cm = cs.cm;
     cm.cap = sg.S + sg.n_cap / kChunk + 1;
     cm.d_n = c->arena.get<int64_t>(1);
@@ -95,9 +103,9 @@ __global__ __launch_bounds__(kSortBlock) void k_seg_sort_lds(const double *__res
         __syncthreads();
         for (int k = 2; k <= np2; k <<= 1) {
             for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = tid; i < np2; i += kSortBlock) {
-                    const int ixj = i ^ j;
-                    if (ixj > i) {
+                for (int t = tid; t < (np2 >> 1); t += kSortBlock) {  // every thread owns a pair
+                    const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;  // j = 2^m
+                    {
                         const uint64_t a = sk[i], d = sk[ixj];
                         const bool up = (i & k) == 0;
                         if ((a > d) == up) {

@@ -161,9 +161,9 @@ __global__ __launch_bounds__(kSortBlock) void k_seg_time_sort(const uint32_t *__
         __syncthreads();
         for (int k = 2; k <= np2; k <<= 1) {
             for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = tid; i < np2; i += kSortBlock) {
-                    const int ixj = i ^ j;
-                    if (ixj > i) {
+                for (int t = tid; t < (np2 >> 1); t += kSortBlock) {  // every thread owns a pair
+                    const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;  // j = 2^m
+                    {
                         const int64_t ta = st[i], tb = st[ixj];
                         const int32_t ia = si[i], ib = si[ixj];
                         const bool gt = ta > tb || (ta == tb && ia > ib);

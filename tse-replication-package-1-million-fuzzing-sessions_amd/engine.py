@@ -61,6 +61,10 @@ class FzRq1Out(C.Structure):
                 ("matched_issue", _P), ("matched_build", _P), ("late", _P)]
 
 
+class FzRq1Ext(C.Structure):
+    _fields_ = [("n", _I64), ("number", _P), ("build_time", _P), ("before", _P)]
+
+
 FZ_RQ2C_NCOUNTS, FZ_RQ2C_NSCALARS = 8, 8
 RQ2C_ELIGIBLE, RQ2C_SESSIONS, RQ2C_GE100, RQ2C_VALUES = range(4)
 RQ2C_CORR_MEAN, RQ2C_CORR_MEDIAN, RQ2C_SP_RHO, RQ2C_SP_P, RQ2C_SW_MEDIAN_P = range(5)
@@ -82,8 +86,9 @@ class FzRq2AddOut(C.Structure):
                                   "covered_is_float", "total_is_float")]
 
 
-FZ_RQ3_NCOUNTS, FZ_RQ3_NTESTS = 4, 16
-RQ3_ISSUES, RQ3_DETECTED, RQ3_NON_DETECTED, RQ3_ELIGIBLE = range(4)
+FZ_RQ3_NCOUNTS, FZ_RQ3_NTESTS = 8, 16
+RQ3_ISSUES, RQ3_DETECTED, RQ3_NON_DETECTED, RQ3_ELIGIBLE, RQ3_NON_LAST = range(5)
+FZ_RQ3_FLUSH_LAST = 1
 RQ3_AD_DET, RQ3_AD_NON, RQ3_LEVENE_W, RQ3_LEVENE_P, RQ3_BM_STAT, RQ3_BM_P = 0, 6, 12, 13, 14, 15
 
 
@@ -129,9 +134,13 @@ SIGNATURES = {
     "fz_ctx_set_stream": (C.c_int, [_P, _P]),
     "fz_store_build": (C.c_int, [_P, C.POINTER(FzTables), C.POINTER(FzStoreStats)]),
     "fz_rq1": (C.c_int, [_P, _I64, C.POINTER(FzRq1Out)]),
+    "fz_rq1_ex": (C.c_int, [_P, _I64, C.POINTER(FzRq1Ext), C.POINTER(FzRq1Out)]),
+    "fz_rq1_finish": (C.c_int, [_P, _I64, _P, _P, _I64, _P, _P]),
     "fz_rq2_count": (C.c_int, [_P, C.POINTER(FzRq2CountOut)]),
     "fz_rq2_add": (C.c_int, [_P, C.POINTER(FzRq2AddOut)]),
     "fz_rq3": (C.c_int, [_P, C.POINTER(FzRq3Out)]),
+    "fz_rq3_ex": (C.c_int, [_P, C.c_uint32, C.POINTER(FzRq3Out)]),
+    "fz_rq3_stats": (C.c_int, [_P, _P, _P, _I64, _P, _I64, _P, _P]),
     "fz_rq4a": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.POINTER(FzRq4aOut)]),
     "fz_rq4b": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.POINTER(FzRq4bOut)]),
     "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),

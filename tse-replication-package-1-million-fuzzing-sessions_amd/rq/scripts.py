@@ -60,8 +60,9 @@ def analyse(name: str, eng: E.Engine, t: Tables, cwd: str) -> render.Rendered:
     raise ValueError(f"unknown script {name!r}")
 
 
-def emit(r: render.Rendered, cwd: str, out=sys.stdout) -> None:
+def emit(r: render.Rendered, cwd: str, out=None) -> None:
     """Write files (relative keys under cwd), stdout lines and log records like the reference."""
+    out = out or sys.stdout
     for path, data in r.files.items():
         full = path if os.path.isabs(path) else os.path.join(cwd, path)
         os.makedirs(os.path.dirname(full), exist_ok=True)
