@@ -7,9 +7,11 @@ issues - resident in HBM.  One step = one pass of the hot path over it: the colu
 results left in HBM.  `value` = session rows (builds + coverage + issues) per second, whole job.
 
 Multi-GPU (torchrun): weak scaling, one process per GPU.  Each rank owns its own project shard (a
-config-2-sized table of disjoint projects); the per-iteration RQ1 histograms are summed across
-ranks with one RCCL all-reduce per step (the only exchange the path has: projects are disjoint,
-so distinct-project counts add).
+config-2-sized table of disjoint projects; global project ids rank * P + p).  A step runs the
+local stages and the exchange steps of tse_amd/parallel.py over RCCL: RQ1 (all-gather of match
+numbers for the cross-shard ROW_NUMBER dedup, all-reduce of counters and per-iteration tables,
+finishing on the summed tables), RQ3 (all-gather of the detected / non-detected samples, last
+project rule, statistics over the union) and the RQ1 / RQ2 row gathers.
 
 Also reported: `roofline` for the dominant kernel (probe = HIP events around every launch of that
 kernel inside the timed region; algorithmic bytes per launch as in DESIGN.md) and `cpu_baseline`
@@ -31,6 +33,9 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PROBE_KERNEL = "radix_scatter"   # dominant kernel of the step (profiles/r01_*_stats.csv)
 STAGES = ["store", "rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"]
+WORKLOADS = {"c2": "config2: ~1M-session synthetic table",
+             "c3": "config3: 100M-row coverage-only table, 10k projects x 10k days",
+             "c5": "config5: Zipf(1.2) rows per project, coverage-only, 10k projects"}
 
 
 def parse():
@@ -40,7 +45,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # e.g. --config c3 --stages store,rq2_count,rq4b: the coverage-only 100M-row table (SURVEY 8(d)
+    # config 3) through the stages that read total_coverage
+    ap.add_argument("--stages", default=",".join(STAGES))
     ap.add_argument("--probe", default=PROBE_KERNEL)
+    # rehearsal on a one-GPU box: several ranks on cuda:0 exchanging over gloo (the driver's
+    # multi-GPU runs use the default, RCCL)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     return ap.parse_args()
 
 
@@ -56,31 +67,59 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
 
     cfg = synth.config(args.config, seed=synth.config(args.config).seed + 1000 * rank)
     t = synth.generate(cfg)
+    if world > 1:
+        t = weak_shard(t, rank, world)
     eng = E.Engine(local)
     eng.upload(t)
-    eng.build_store()
+    st = eng.build_store()
+    if world > 1:
+        from tse_amd import parallel as par
+        M = par.agree_max(int(st.max_fuzz_per_project), dev)
+        rq1_shard = par.GpuRQ1Shard(eng, M)
+        rq3_shard = par.GpuRQ3Shard(eng)
     rq1_bufs = compute.RQ1Buffers(eng)
     bufs = {"rq2_count": compute.rq2_count_buffers(eng), "rq2_add": compute.rq2_add_buffers(eng),
             "rq3": compute.rq3_buffers(eng), "rq4a": compute.rq4a_buffers(eng), "rq4b": compute.rq4b_buffers(eng)}
     launch = {"rq2_count": compute.rq2_count_launch, "rq2_add": compute.rq2_add_launch, "rq3": compute.rq3_launch,
               "rq4a": compute.rq4a_launch, "rq4b": compute.rq4b_launch}
 
+    stages = [s for s in STAGES if s in args.stages.split(",")]
+
     def step():
         eng.build_store()
-        compute.rq1_launch(eng, rq1_bufs)
-        for name in ("rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"):
-            launch[name](eng, bufs[name])
-        if world > 1:
-            # projects are disjoint across ranks: per-iteration project counts add
-            dist.all_reduce(rq1_bufs.iter_total)
-            dist.all_reduce(rq1_bufs.iter_detected)
+        if world == 1:
+            if "rq1" in stages:
+                compute.rq1_launch(eng, rq1_bufs)
+            for name in ("rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"):
+                if name in stages:
+                    launch[name](eng, bufs[name])
+            return
+        # sharded: exact RQ1 / RQ3 recombination + row gathers (tse_amd/parallel.py)
+        if "rq1" in stages:
+            part = par.rq1_sharded(rq1_shard, rank, world)[0]
+            par.gather_rows({"issue": part["matched_issue"], "build": part["matched_build"]}, world)
+        for name in ("rq2_count", "rq2_add", "rq4a", "rq4b"):
+            if name in stages:
+                launch[name](eng, bufs[name])
+        if "rq2_add" in stages:
+            b = bufs["rq2_add"]
+            n_add = int(b.counts[E.RQ2A_ROWS].item())
+            par.gather_rows({"project": b.row_project[:n_add], "diff_total": b.diff_total[:n_add],
+                             "diff_coverage": b.diff_coverage[:n_add]}, world)
+        if "rq3" in stages:
+            par.rq3_sharded(rq3_shard, rank, world)
 
     for _ in range(args.warmup):
         step()
@@ -108,9 +147,9 @@ def main():
     if world > 1:
         v = torch.tensor([elapsed, rows], dtype=torch.float64, device=dev)
         tmax = v[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        par.all_reduce(tmax, dist.ReduceOp.MAX)
         rsum = v[1:].clone()
-        dist.all_reduce(rsum, op=dist.ReduceOp.SUM)
+        par.all_reduce(rsum)
         elapsed, rows = float(tmax.item()), float(rsum.item())
 
     out = None
@@ -127,16 +166,16 @@ def main():
                     "launches_per_step": launches / args.steps}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(t)
+            cpu = cpu_baseline(t, stages)
         out = {
             "metric": "session-rows/sec through RQ1-RQ4 aggregates+stats",
             "value": round(value, 1), "unit": "session-rows/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int64/fp64", "data": "synthetic",
-            "config": {"workload": f"config2: ~1M-session synthetic table ({args.config}), "
+            "config": {"workload": f"{WORKLOADS.get(args.config, args.config)} ({args.config}), "
                                    f"{len(t.projects)} projects/rank",
                        "rows_per_rank": t.n_rows, "builds": int(len(t.b_project)), "coverage": int(len(t.c_project)),
-                       "issues": int(len(t.i_project)), "stages": STAGES, "parallelism": f"project-shard x{world}",
+                       "issues": int(len(t.i_project)), "stages": stages, "parallelism": f"project-shard x{world}",
                        "device_ms_per_step": round(dev_ms / args.steps, 4)},
             "roofline": roof, "cpu_baseline": cpu,
         }
@@ -147,12 +186,27 @@ def main():
     return out
 
 
-def cpu_baseline(t):
+def weak_shard(t, rank, world):
+    """Rank `rank`'s table as one shard of a world-times-larger job: project ids rank * P + p in a
+    global id space of world * P projects, issue numbers made unique per rank (OSS-Fuzz numbers
+    are unique per tracker; the cross-shard dedup check still runs every step)."""
+    import dataclasses
+    P = len(t.projects)
+    off = np.uint32(rank * P)
+    # this rank's projects keep their names (the corpus CSV refers to them); the other ranks'
+    # ids get placeholder names
+    names = [n if r == rank else f"~{r}-{n}" for r in range(world) for n in t.projects]
+    return dataclasses.replace(
+        t, projects=names, b_project=t.b_project + off, c_project=t.c_project + off, i_project=t.i_project + off,
+        pi_project=t.pi_project + off, i_number=t.i_number + np.int64(rank) * 100_000_000)
+
+
+def cpu_baseline(t, stages):
     """The oracle port (numpy/scipy, single thread) over the same stages on the same table."""
     from oracle import rq_oracle as orc
     fns = {"rq1": orc.rq1, "rq2_count": orc.rq2_count, "rq2_add": orc.rq2_add, "rq3": orc.rq3,
            "rq4a": orc.rq4a, "rq4b": orc.rq4b}
-    stages = [s for s in STAGES if s in fns]
+    stages = [s for s in stages if s in fns]
     t0 = time.perf_counter()
     reps = 0
     while True:

@@ -261,6 +261,7 @@ int fz_rq3(fz_ctx *ctx, const fz_rq3_out *out);
  * project's row count in counts[FZ_RQ3_NON_LAST]; the caller drops those rows on the last shard
  * that has issues and runs the statistics once over the gathered samples (fz_rq3_stats). */
 #define FZ_RQ3_FLUSH_LAST 1u
+#define FZ_RQ3_SKIP_STATS 2u    /* leave describe / tests untouched (a shard: fz_rq3_stats runs once) */
 int fz_rq3_ex(fz_ctx *ctx, uint32_t flags, const fz_rq3_out *out);
 
 /* RQ3 statistics (rq3:321-352) over two device samples: describe[3] (detected pct, non-detected

@@ -65,9 +65,13 @@ def _describe(x) -> Describe:
 
 
 # --------------------------------------------------------------------------------------- RQ1
-def rq1(t: Tables, threshold: int = 100) -> RQ1Result:
+def rq1(t: Tables, threshold: int = 100, ext=None) -> RQ1Result:
     """rq1_detection_rate.py:101-269 with queries1.py:15-58 (SAME_DATE_BUILD_ISSUE),
-    :267-278 (ALL_FUZZING_BUILD), :280-314 (GET_ISSUES_WITHOUT_MATCHING_BUILD)."""
+    :267-278 (ALL_FUZZING_BUILD), :280-314 (GET_ISSUES_WITHOUT_MATCHING_BUILD).
+
+    ``ext`` = (numbers, build_times, before) of other shards' matches (fz_rq1_ex): they compete
+    in the ROW_NUMBER dedup (a preceding shard's entry wins ties, a following one loses them)
+    but are never output."""
     P = len(t.projects)
     lim = t.i_rts < LIMIT_US                                   # :121-127
     fixed = np.isin(t.i_status, FIXED_CODES)
@@ -104,15 +108,23 @@ def rq1(t: Tables, threshold: int = 100) -> RQ1Result:
     # dedup by issue number: keep the row with the latest build time (ties: first in output order)
     order = np.lexsort((ci, t.i_rts[ci], t.i_project[ci]))
     ci, mb = ci[order], mb[order]
-    best = {}
+    best, after = {}, {}
+    if ext is not None:
+        for num, tb, bf in zip(*(np.asarray(a).tolist() for a in ext)):
+            if bf:
+                if num not in best or tb > best[num][0]:
+                    best[num] = (tb, -1)
+            else:
+                after[num] = max(after.get(num, tb), tb)
     for k, (i, b) in enumerate(zip(ci.tolist(), mb.tolist())):
         num = int(t.i_number[i])
         tb = int(t.b_time[b])
         if num not in best or tb > best[num][0]:
             best[num] = (tb, k)
     keep = np.zeros(len(ci), bool)
-    for _, k in best.values():
-        keep[k] = True
+    for num, (tb, k) in best.items():
+        if k >= 0 and not (num in after and after[num] > tb):
+            keep[k] = True
     ci, mb = ci[keep], mb[keep]
     # phase 2: iteration = #ALL Fuzzing builds with timecreated < rts  (:213-230)
     fseg = _Seg(t.b_project, t.b_time, fz, P)
@@ -282,8 +294,33 @@ def rq2_add(t: Tables) -> RQ2AddResult:
 
 
 # ---------------------------------------------------------------------------------------- RQ3
-def rq3(t: Tables) -> RQ3Result:
-    """rq3_diff_coverage_at_detection.py:202-360."""
+def rq3_stats(dpct, dtot, npct):
+    """rq3_diff_coverage_at_detection.py:25-66, :321-352 over the two samples."""
+    dpct = np.asarray(dpct, np.float64)
+    npct = np.asarray(npct, np.float64)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        dd_ = _describe(dpct) if len(dpct) else None
+        nd_ = _describe(npct) if len(npct) else None
+        dt_ = _describe(list(dtot)) if len(dpct) else None
+        ad = an = lv = bm = None
+        if len(dpct) and len(npct):
+            r = stats.anderson(list(dpct), dist="norm")
+            ad = (float(r.statistic), np.asarray(r.critical_values))
+            r = stats.anderson(list(npct), dist="norm")
+            an = (float(r.statistic), np.asarray(r.critical_values))
+            s_, p_ = stats.levene(list(dpct), list(npct))
+            lv = (float(s_), float(p_))
+            s_, p_ = stats.brunnermunzel(list(dpct), list(npct))
+            bm = (float(s_), float(p_))
+    return dict(desc_detected=dd_, desc_non=nd_, desc_det_total=dt_, anderson_det=ad, anderson_non=an, levene=lv,
+                brunnermunzel=bm)
+
+
+def rq3(t: Tables, flush_last: bool = False) -> RQ3Result:
+    """rq3_diff_coverage_at_detection.py:202-360.  ``flush_last`` (fz_rq3_ex FZ_RQ3_FLUSH_LAST, a
+    shard that is not the last one): flush the last issue-bearing project too and report its row
+    count in ``n_non_last``."""
     P = len(t.projects)
     elig = eligible_projects(t)
     is_elig = np.zeros(P, bool)
@@ -298,20 +335,26 @@ def rq3(t: Tables) -> RQ3Result:
     canon = t.rev_canon()
     det = []
     non = []
+
+    def flush(proj):                                              # :245-257
+        rows = tc.rows(proj)
+        n0 = len(non)
+        if len(rows):
+            dd = {d[4] // US_PER_DAY for d in det if d[3] == proj}
+            for k in range(1, len(rows)):
+                a, b = rows[k - 1], rows[k]
+                if t.c_date[b] // US_PER_DAY not in dd and t.c_total[a] > 0 and t.c_total[b] > 0:
+                    non.append(((t.c_covered[b] / t.c_total[b] - t.c_covered[a] / t.c_total[a]) * 100,
+                                int(t.c_covered[b] - t.c_covered[a]), int(t.c_total[b] - t.c_total[a])))
+        return len(non) - n0
+
     cur = -1
     for i in iss.tolist():
         p = int(t.i_project[i])
         rts = int(t.i_rts[i])
         if p != cur:
-            if cur >= 0:                                          # flush previous project (:245-257)
-                rows = tc.rows(cur)
-                if len(rows):
-                    dd = {d[4] // US_PER_DAY for d in det if d[3] == cur}
-                    for k in range(1, len(rows)):
-                        a, b = rows[k - 1], rows[k]
-                        if t.c_date[b] // US_PER_DAY not in dd and t.c_total[a] > 0 and t.c_total[b] > 0:
-                            non.append(((t.c_covered[b] / t.c_total[b] - t.c_covered[a] / t.c_total[a]) * 100,
-                                        int(t.c_covered[b] - t.c_covered[a]), int(t.c_total[b] - t.c_total[a])))
+            if cur >= 0:                                          # flush previous project
+                flush(cur)
             cur = p
         fr, cr, tr = fz.rows(p), cb.rows(p), tc.rows(p)
         if len(fr) == 0 or len(cr) == 0 or len(tr) == 0:
@@ -345,29 +388,15 @@ def rq3(t: Tables) -> RQ3Result:
         if t.c_total[a] > 0 and t.c_total[b] > 0:
             det.append(((t.c_covered[b] / t.c_total[b] - t.c_covered[a] / t.c_total[a]) * 100,
                         int(t.c_covered[b] - t.c_covered[a]), int(t.c_total[b] - t.c_total[a]), p, rts, i))
+    n_last = flush(cur) if (flush_last and cur >= 0) else 0
     dpct = np.array([d[0] for d in det], np.float64)
     npct = np.array([d[0] for d in non], np.float64)
-    with warnings.catch_warnings():
-        warnings.simplefilter("ignore")
-        dd_ = _describe(dpct) if len(det) else None
-        nd_ = _describe(npct) if len(non) else None
-        dt_ = _describe([d[2] for d in det]) if len(det) else None
-        ad = an = lv = bm = None
-        if len(det) and len(non):
-            r = stats.anderson(list(dpct), dist="norm")
-            ad = (float(r.statistic), np.asarray(r.critical_values))
-            r = stats.anderson(list(npct), dist="norm")
-            an = (float(r.statistic), np.asarray(r.critical_values))
-            s_, p_ = stats.levene(list(dpct), list(npct))
-            lv = (float(s_), float(p_))
-            s_, p_ = stats.brunnermunzel(list(dpct), list(npct))
-            bm = (float(s_), float(p_))
+    dtot = np.array([d[2] for d in det], np.int64)
     return RQ3Result(n_all_issues=len(iss), det_pct=dpct, det_cov=np.array([d[1] for d in det], np.int64),
-                     det_tot=np.array([d[2] for d in det], np.int64), det_project=np.array([d[3] for d in det], np.int64),
+                     det_tot=dtot, det_project=np.array([d[3] for d in det], np.int64),
                      det_issue=np.array([d[5] for d in det], np.int64), non_pct=npct,
                      non_cov=np.array([d[1] for d in non], np.int64), non_tot=np.array([d[2] for d in non], np.int64),
-                     desc_detected=dd_, desc_non=nd_, desc_det_total=dt_, anderson_det=ad, anderson_non=an,
-                     levene=lv, brunnermunzel=bm)
+                     n_non_last=n_last, **rq3_stats(dpct, dtot, npct))
 
 
 # --------------------------------------------------------------------------------------- RQ4a

@@ -1,0 +1,104 @@
+"""Project-sharded RQ1 / RQ3 on the GPU: 2 ranks (both on cuda:0 - the box has one GPU), each
+with its own libfz context holding only its projects' rows, exchanging over gloo (RCCL needs
+one GPU per rank).  The exchange is the same code bench.py runs over RCCL; rank 0 checks the
+recombined results against the oracle on the whole table."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from test_parallel import _free_port, make_table
+
+pytestmark = pytest.mark.gpu
+
+
+class _HostView:
+    """Wraps a GPU shard so the gloo collectives see CPU tensors."""
+
+    def __init__(self, shard, dev):
+        self.s, self.dev = shard, dev
+
+    def run(self, *a):
+        a = tuple(None if x is None else tuple(v.to(self.dev) for v in x) for x in a)
+        return {k: v.cpu() for k, v in self.s.run(*a).items()}
+
+    def finish(self, counts, it, idt):
+        c, i, d = (x.to(self.dev) for x in (counts, it, idt))
+        self.s.finish(c, i, d)
+        counts.copy_(c.cpu())
+
+    def stats(self, *a):
+        return {k: v.cpu() for k, v in self.s.stats(*(x.to(self.dev) for x in a)).items()}
+
+
+class _RQ3View(_HostView):
+    """... and maps the shard's detected issue rows to global row ids before they are gathered."""
+
+    def __init__(self, shard, dev, issue_rows):
+        super().__init__(shard, dev)
+        self.issue_rows = issue_rows
+
+    def run(self):
+        out = super().run()
+        out["det_issue"] = torch.from_numpy(self.issue_rows[out["det_issue"].numpy()].astype(np.int64))
+        return out
+
+
+def _worker(rank, world, port, case, errfile):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _check(rank, world, case)
+    except BaseException:
+        import traceback
+        with open(f"{errfile}.{rank}", "w") as f:
+            f.write(traceback.format_exc())
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _check(rank, world, case):
+    from gpu_common import assert_same
+    from oracle import rq_oracle as orc
+    from tse_amd import engine as E
+    from tse_amd import parallel as par
+    from tse_amd.rq import compute
+    t = make_table(case, world)
+    lo, hi = par.shard_bounds(t, world)[rank]
+    ts, rows = par.take_shard(t, lo, hi)
+    eng = E.Engine(0)
+    eng.upload(ts)
+    st = eng.build_store()
+    M = par.agree_max(int(st.max_fuzz_per_project))
+    g1 = _HostView(par.GpuRQ1Shard(eng, M), eng.dev)
+    part, counts, it, idt, reran = par.rq1_sharded(g1, rank, world)
+    mi = torch.from_numpy(rows.issues[part["matched_issue"].numpy()].astype(np.int64))
+    mb = torch.from_numpy(rows.builds[part["matched_build"].numpy()].astype(np.int64))
+    rows1 = par.gather_rows({"matched_issue": mi, "matched_build": mb}, world)
+    elig = g1.s.bufs.eligible.cpu().to(torch.int64)
+    torch.distributed.all_reduce(elig)
+    late = g1.s.bufs.late.cpu().numpy()
+    total3, cols3, st3 = par.rq3_sharded(_RQ3View(par.GpuRQ3Shard(eng), eng.dev, rows.issues), rank, world)
+    if rank == 0:
+        ours3 = compute.rq3_result(total3, {k: v.numpy() for k, v in cols3.items()}, st3["describe"].numpy(),
+                                   st3["tests"].numpy())
+        assert_same(ours3, orc.rq3(t), "rq3")
+        ours1 = compute.rq1_result(counts.numpy(), it.numpy()[:int(counts[E.RQ1_MAX_ITER])],
+                                   idt.numpy()[:int(counts[E.RQ1_MAX_ITER])], late, rows1["matched_issue"].numpy(),
+                                   rows1["matched_build"].numpy(), np.nonzero(elig.numpy())[0])
+        assert_same(ours1, orc.rq1(t), "rq1")
+    eng.close()
+
+
+@pytest.mark.parametrize("case", ["collide", "last_shard_no_issues"])
+def test_gpu_sharded_rq1_rq3(case, tmp_path):
+    errfile = str(tmp_path / "err")
+    try:
+        mp.spawn(_worker, args=(2, _free_port(), case, errfile), nprocs=2, join=True)
+    except Exception:
+        msgs = [open(f"{errfile}.{r}").read() for r in range(2) if os.path.exists(f"{errfile}.{r}")]
+        raise AssertionError("\n".join(msgs) or "worker failed")

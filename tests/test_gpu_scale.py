@@ -37,3 +37,15 @@ def test_config2_bench_table(engine):
     t = synth.generate(synth.config("c2"))
     st = _check_all(engine, t)
     assert st.n_fuzz == int(np.sum(t.b_type == 0))
+
+
+@pytest.mark.parametrize("cfg", [
+    # config 3 shape: coverage only, contiguous daily series longer than one LDS sort (> 4096)
+    synth.config("c3", n_projects=40, rows_per_project=5000),
+    # config 5 shape: coverage only, Zipf rows per project
+    synth.config("c5", n_projects=60, len_mean_days=3000),
+], ids=["c3_shape", "c5_shape"])
+def test_coverage_only_tables(engine, cfg):
+    t = synth.generate(cfg)
+    assert len(t.b_project) == 0 and len(t.i_project) == 0
+    _check_all(engine, t)

@@ -1,0 +1,206 @@
+"""Project-sharded multi-GPU layer (tse_amd/parallel.py) on CPU: world_size 2 and 3 over gloo.
+
+Each rank runs the exchange drivers over ORACLE shards (the CPU restatement of one rank's local
+analysis); rank 0 checks the recombined result against the oracle on the whole table.  The
+tables are built so that the exchange steps matter: issue numbers collide across shards (the
+ROW_NUMBER dedup spans projects), a "twin" project in the last shard duplicates the first
+eligible project (equal build times -> tie broken by project order, i.e. by rank), and one case
+leaves the last shard without issues (the never-flushed RQ3 project then sits on another rank).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from tse_amd import parallel as par
+from tse_amd import synth
+from tse_amd.rq import common
+from tse_amd.schema import Tables
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def make_table(case: str, world: int) -> Tables:
+    from oracle import rq_oracle as orc
+    t = synth.generate(synth.config("tiny"))
+    P = len(t.projects)
+    elig = orc.eligible_projects(t)
+    src, dst = int(elig[0]), P - 1
+    # twin: project dst := a copy of project src (builds, coverage, issues with the same numbers)
+    def twin(proj, cols):
+        keep = proj != dst
+        take = np.nonzero(proj == src)[0]
+        out = [np.concatenate([c[keep], c[take]]) for c in cols]
+        return out, int(keep.sum())
+    (bp, bt, br, bti, bm, brv, bn), nb = twin(t.b_project, (t.b_project, t.b_type, t.b_result, t.b_time, t.b_modules,
+                                                             t.b_revisions, t.b_name))
+    bp[nb:] = dst
+    (cp, cd, cc, ccv, cv, cvv, ct, ctv), nc = twin(t.c_project, (t.c_project, t.c_date, t.c_coverage,
+                                                                 t.c_coverage_valid, t.c_covered, t.c_covered_valid,
+                                                                 t.c_total, t.c_total_valid))
+    cp[nc:] = dst
+    (ip, inum, irts, ist, inew), ni = twin(t.i_project, (t.i_project, t.i_number, t.i_rts, t.i_status, t.i_new_id))
+    ip[ni:] = dst
+    inum = inum.copy()
+    inum[:ni] = 1_000_000 + (inum[:ni] % 97)          # collisions across projects (and shards)
+    inum[ni:] = inum[np.nonzero(ip[:ni] == src)[0]]   # the twin's issues reuse the source's numbers
+    t = Tables(projects=t.projects, b_project=bp, b_type=bt, b_result=br, b_time=bti, b_modules=bm, b_revisions=brv,
+               b_name=bn, modules_pool=t.modules_pool, revisions_pool=t.revisions_pool, c_project=cp, c_date=cd,
+               c_coverage=cc, c_coverage_valid=ccv, c_covered=cv, c_covered_valid=cvv, c_total=ct, c_total_valid=ctv,
+               i_number=inum, i_project=ip, i_rts=irts, i_status=ist, i_new_id=inew, pi_project=t.pi_project,
+               pi_first_commit=t.pi_first_commit, build_types=t.build_types, results=t.results,
+               statuses=t.statuses, corpus_csv=t.corpus_csv)
+    if case == "last_shard_no_issues":
+        lo, _ = par.shard_bounds(t, world)[-1]
+        keep = t.i_project.astype(np.int64) < lo
+        import dataclasses
+        t = dataclasses.replace(t, i_number=t.i_number[keep], i_project=t.i_project[keep], i_rts=t.i_rts[keep],
+                                i_status=t.i_status[keep], i_new_id=t.i_new_id[keep])
+    return t
+
+
+class OracleRQ1Shard:
+    def __init__(self, t, rows, max_iter, threshold=100):
+        self.t, self.rows, self.M, self.threshold = t, rows, max_iter, threshold
+
+    def run(self, ext):
+        from oracle import rq_oracle as orc
+        r = orc.rq1(self.t, self.threshold, ext=None if ext is None else tuple(x.numpy() for x in ext))
+        self.result = r
+        c = np.zeros(par.RQ1_NCOUNTS, np.int64)
+        c[par.RQ1_ISSUES_LIM], c[par.RQ1_ISSUES_LIM_PROJECTS] = r.n_issues_lim, r.n_issues_lim_projects
+        c[par.RQ1_FIXED_LIM], c[par.RQ1_FIXED_LIM_PROJECTS] = r.n_fixed_lim, r.n_fixed_lim_projects
+        c[par.RQ1_ELIGIBLE], c[par.RQ1_WITHOUT_MATCHING] = len(r.eligible), r.n_without_matching
+        c[par.RQ1_TARGET], c[par.RQ1_TARGET_PROJECTS] = r.n_target, r.n_target_projects
+        c[par.RQ1_TOTAL_FUZZ], c[par.RQ1_MATCHED] = r.total_fuzz_builds, len(r.matched_issue)
+        c[par.RQ1_MATCHED_PROJECTS], c[par.RQ1_MAX_ITER] = r.n_matched_projects, len(r.iter_total)
+        it = np.zeros(self.M, np.int64)
+        idt = np.zeros(self.M, np.int64)
+        it[:len(r.iter_total)] = r.iter_total
+        idt[:len(r.iter_detected)] = r.iter_detected
+        return {"counts": torch.from_numpy(c), "iter_total": torch.from_numpy(it),
+                "iter_detected": torch.from_numpy(idt),
+                "number": torch.from_numpy(self.t.i_number[r.matched_issue].astype(np.int64)),
+                "build_time": torch.from_numpy(self.t.b_time[r.matched_build].astype(np.int64)),
+                "matched_issue": torch.from_numpy(self.rows.issues[r.matched_issue].astype(np.int64)),
+                "matched_build": torch.from_numpy(self.rows.builds[r.matched_build].astype(np.int64))}
+
+    def finish(self, counts, it, idt):
+        M = int(counts[par.RQ1_MAX_ITER])
+        keys, rates, first_down, late = common.rq1_rates(it.numpy()[:M], idt.numpy()[:M], self.threshold)
+        counts[par.RQ1_KEPT_ITERS] = len(keys)
+        counts[par.RQ1_FIRST_DOWN] = first_down
+        counts[par.RQ1_LATE] = len(late)
+        self.late = late
+
+
+class OracleRQ3Shard:
+    def __init__(self, t, rows):
+        self.t, self.rows = t, rows
+
+    def run(self):
+        from oracle import rq_oracle as orc
+        r = orc.rq3(self.t, flush_last=True)
+        c = np.zeros(par.RQ3_NCOUNTS, np.int64)
+        c[par.RQ3_ISSUES], c[par.RQ3_DETECTED], c[par.RQ3_NON_DETECTED] = r.n_all_issues, len(r.det_pct), len(r.non_pct)
+        c[par.RQ3_ELIGIBLE], c[par.RQ3_NON_LAST] = len(orc.eligible_projects(self.t)), r.n_non_last
+        T = lambda a, dt=np.int64: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))  # noqa: E731
+        return {"counts": T(c), "det_pct": T(r.det_pct, np.float64), "det_cov": T(r.det_cov), "det_tot": T(r.det_tot),
+                "det_project": T(r.det_project), "det_issue": T(self.rows.issues[r.det_issue]),
+                "non_pct": T(r.non_pct, np.float64), "non_cov": T(r.non_cov), "non_tot": T(r.non_tot)}
+
+    def stats(self, det_pct, det_tot, non_pct):
+        from oracle import rq_oracle as orc
+        return orc.rq3_stats(det_pct.numpy(), det_tot.numpy(), non_pct.numpy())
+
+
+def _worker(rank, world, port, case, errfile):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _check(rank, world, case)
+    except BaseException as e:  # report to the parent (mp.spawn only sees the exit code)
+        with open(f"{errfile}.{rank}", "w") as f:
+            import traceback
+            f.write(traceback.format_exc())
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _check(rank, world, case):
+    from oracle import rq_oracle as orc
+    from gpu_common import assert_same
+    t = make_table(case, world)
+    lo, hi = par.shard_bounds(t, world)[rank]
+    ts, rows = par.take_shard(t, lo, hi)
+    # RQ1
+    nF = np.bincount(ts.b_project[ts.b_type == 0].astype(np.int64), minlength=len(t.projects))
+    M = par.agree_max(int(nF.max()) if len(nF) else 0)
+    sh = OracleRQ1Shard(ts, rows, max(M, 1))
+    part, counts, it, idt, reran = par.rq1_sharded(sh, rank, world)
+    rows1 = par.gather_rows({"matched_issue": part["matched_issue"], "matched_build": part["matched_build"]}, world)
+    any_rerun = torch.tensor([int(reran)])
+    torch.distributed.all_reduce(any_rerun)
+    # RQ3
+    total3, cols3, st3 = par.rq3_sharded(OracleRQ3Shard(ts, rows), rank, world)
+    if rank != 0:
+        return
+    g = orc.rq1(t)
+    assert int(any_rerun) > 0, "the table was built to need the cross-shard dedup"
+    c = counts.numpy()
+    assert c[par.RQ1_ISSUES_LIM] == g.n_issues_lim and c[par.RQ1_ISSUES_LIM_PROJECTS] == g.n_issues_lim_projects
+    assert c[par.RQ1_FIXED_LIM] == g.n_fixed_lim and c[par.RQ1_FIXED_LIM_PROJECTS] == g.n_fixed_lim_projects
+    assert c[par.RQ1_ELIGIBLE] == len(g.eligible) and c[par.RQ1_WITHOUT_MATCHING] == g.n_without_matching
+    assert c[par.RQ1_TARGET] == g.n_target and c[par.RQ1_TARGET_PROJECTS] == g.n_target_projects
+    assert c[par.RQ1_TOTAL_FUZZ] == g.total_fuzz_builds
+    assert c[par.RQ1_MATCHED] == len(g.matched_issue) and c[par.RQ1_MATCHED_PROJECTS] == g.n_matched_projects
+    Mg = int(c[par.RQ1_MAX_ITER])
+    assert Mg == len(g.iter_total)
+    np.testing.assert_array_equal(it.numpy()[:Mg], g.iter_total)
+    np.testing.assert_array_equal(idt.numpy()[:Mg], g.iter_detected)
+    np.testing.assert_array_equal(rows1["matched_issue"].numpy(), g.matched_issue)
+    np.testing.assert_array_equal(rows1["matched_build"].numpy(), g.matched_build)
+    _, _, first_down, late = common.rq1_rates(g.iter_total, g.iter_detected, 100)
+    assert c[par.RQ1_FIRST_DOWN] == first_down and c[par.RQ1_LATE] == len(late)
+    g3 = orc.rq3(t)
+    assert total3[par.RQ3_ISSUES] == g3.n_all_issues
+    for k in ("det_pct", "det_cov", "det_tot", "det_project", "det_issue", "non_pct", "non_cov", "non_tot"):
+        np.testing.assert_array_equal(cols3[k].numpy(), getattr(g3, k), err_msg=k)
+    for k, v in st3.items():
+        assert_same(v, getattr(g3, k), k)
+
+
+def _spawn(world, case, tmp_path):
+    errfile = str(tmp_path / "err")
+    try:
+        mp.spawn(_worker, args=(world, _free_port(), case, errfile), nprocs=world, join=True)
+    except Exception:
+        msgs = [open(f"{errfile}.{r}").read() for r in range(world) if os.path.exists(f"{errfile}.{r}")]
+        raise AssertionError("\n".join(msgs) or "worker failed")
+
+
+def test_shard_bounds_cover_and_balance():
+    t = synth.generate(synth.config("tiny"))
+    for world in (1, 2, 3, 8):
+        b = par.shard_bounds(t, world)
+        assert b[0][0] == 0 and b[-1][1] == len(t.projects)
+        assert all(b[r][1] == b[r + 1][0] for r in range(world - 1))
+        parts = [par.take_shard(t, lo, hi)[0] for lo, hi in b]
+        assert sum(p.n_rows for p in parts) == t.n_rows
+        if world > 1:
+            sizes = np.array([p.n_rows for p in parts], float)
+            assert sizes.max() <= 2.5 * t.n_rows / world
+
+
+@pytest.mark.parametrize("world,case", [(2, "collide"), (3, "collide"), (3, "last_shard_no_issues")])
+def test_sharded_rq1_rq3_match_whole_table(world, case, tmp_path):
+    _spawn(world, case, tmp_path)

@@ -197,8 +197,9 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     });
     map_n(c, 1, nullptr, [=] __device__(int64_t) { counts[FZ_RQ3_ISSUES] = *d_ni; });
 
-    rq3_stats(c, o->det_pct, o->det_tot, NI, counts + FZ_RQ3_DETECTED, o->non_pct, NC, counts + FZ_RQ3_NON_DETECTED,
-              o->describe, o->tests);
+    if (!(flags & FZ_RQ3_SKIP_STATS))
+        rq3_stats(c, o->det_pct, o->det_tot, NI, counts + FZ_RQ3_DETECTED, o->non_pct, NC,
+                  counts + FZ_RQ3_NON_DETECTED, o->describe, o->tests);
 }
 
 // ---- statistics (:321-352) over samples of device lengths *d_nd <= NI and *d_nn <= NC

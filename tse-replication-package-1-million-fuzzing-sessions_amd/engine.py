@@ -88,7 +88,7 @@ class FzRq2AddOut(C.Structure):
 
 FZ_RQ3_NCOUNTS, FZ_RQ3_NTESTS = 8, 16
 RQ3_ISSUES, RQ3_DETECTED, RQ3_NON_DETECTED, RQ3_ELIGIBLE, RQ3_NON_LAST = range(5)
-FZ_RQ3_FLUSH_LAST = 1
+FZ_RQ3_FLUSH_LAST, FZ_RQ3_SKIP_STATS = 1, 2
 RQ3_AD_DET, RQ3_AD_NON, RQ3_LEVENE_W, RQ3_LEVENE_P, RQ3_BM_STAT, RQ3_BM_P = 0, 6, 12, 13, 14, 15
 
 

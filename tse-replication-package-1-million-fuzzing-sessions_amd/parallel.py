@@ -1,0 +1,314 @@
+"""Project-sharded multi-GPU layer (BASELINE.json north_star "Multi-GPU layer").
+
+One process per GPU (torchrun), ``torch.distributed`` over RCCL on the GPU box (gloo in the CPU
+tests).  Every per-project computation of the RQ scripts is independent, so the session tables are
+cut into contiguous project-id ranges with about equal row counts (``shard_bounds``); each rank
+uploads only its own projects' rows (``take_shard``; project ids stay global) and runs the
+per-project kernels locally.  The exchange steps are the places where the reference's arithmetic
+spans projects:
+
+RQ1 (``rq1_sharded``)
+    * per-iteration tables (``total_projects[i]``, distinct detecting projects) and the scalar
+      counters are summed - projects are disjoint across ranks, so distinct-project counts add -
+      and the iteration axis length is a MAX (all_reduce);
+    * the SAME_DATE_BUILD_ISSUE dedup ``ROW_NUMBER() OVER (PARTITION BY i.number ORDER BY
+      timecreated DESC)`` (queries1.py:29-32) partitions by issue number ACROSS projects: every
+      rank all-gathers the (number, build time) of the other ranks' matches; a rank whose matches
+      share a number with another rank's re-runs its match with those as competitors
+      (``fz_rq1_ex``).  A rank's first-pass winners contain the global winner, so one re-run is
+      exact;
+    * finishing (kept iterations, first_down, late-stage summary, rq1:233-268) runs on the summed
+      tables (``fz_rq1_finish``).
+RQ3 (``rq3_sharded``)
+    * detected / non-detected samples are all-gathered in rank (= project) order;
+    * the reference flushes a project's non-detected changes when its issue loop reaches the next
+      project, so only the globally last issue-bearing project is never flushed (rq3:245-257):
+      every rank runs with ``FZ_RQ3_FLUSH_LAST`` and the tail of the last rank with issues is
+      dropped;
+    * the statistics run once over the gathered samples (``fz_rq3_stats``).
+RQ2 coverage-and-added (``gather_rows``): per-project change rows, concatenated in rank order.
+
+The drivers take a *shard* object (``run`` / ``finish`` / ``stats``) so the same exchange code runs
+over the GPU engine (``GpuRQ1Shard``, ``GpuRQ3Shard``) and, in the CPU tests, over the oracle.
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass
+from typing import List, Tuple
+
+import numpy as np
+
+from .schema import Tables
+
+# fz.h RQ1 counter layout (FZ_RQ1_*)
+(RQ1_ISSUES_LIM, RQ1_ISSUES_LIM_PROJECTS, RQ1_FIXED_LIM, RQ1_FIXED_LIM_PROJECTS, RQ1_ELIGIBLE,
+ RQ1_WITHOUT_MATCHING, RQ1_TARGET, RQ1_TARGET_PROJECTS, RQ1_TOTAL_FUZZ, RQ1_MATCHED, RQ1_MATCHED_PROJECTS,
+ RQ1_MAX_ITER, RQ1_KEPT_ITERS, RQ1_FIRST_DOWN, RQ1_LATE) = range(15)
+RQ1_NCOUNTS = 16
+# fz.h RQ3 counter layout (FZ_RQ3_*)
+RQ3_ISSUES, RQ3_DETECTED, RQ3_NON_DETECTED, RQ3_ELIGIBLE, RQ3_NON_LAST = range(5)
+RQ3_NCOUNTS = 8
+
+
+# ------------------------------------------------------------------------------------- sharding
+def shard_bounds(t: Tables, world: int) -> List[Tuple[int, int]]:
+    """Contiguous project-id ranges [lo, hi), one per rank, with about equal session-row counts
+    (prefix sum of per-project rows; a giant project stays whole on one rank and is split across
+    workgroups there)."""
+    P = len(t.projects)
+    rows = (np.bincount(t.b_project.astype(np.int64), minlength=P)
+            + np.bincount(t.c_project.astype(np.int64), minlength=P)
+            + np.bincount(t.i_project.astype(np.int64), minlength=P)).astype(np.int64)
+    cum = np.concatenate([[0], np.cumsum(rows)])
+    total = int(cum[-1])
+    cuts = [0]
+    for r in range(1, world):
+        target = total * r / world
+        k = int(np.searchsorted(cum, target, "left"))
+        if k > 0 and abs(cum[k - 1] - target) <= abs(cum[min(k, P)] - target):
+            k -= 1
+        cuts.append(min(max(k, cuts[-1]), P))
+    cuts.append(P)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+@dataclass
+class ShardRows:
+    """Global row ids of a shard's rows (shard row i == global row ids[i])."""
+    lo: int
+    hi: int
+    builds: np.ndarray
+    coverage: np.ndarray
+    issues: np.ndarray
+
+
+def take_shard(t: Tables, lo: int, hi: int) -> Tuple[Tables, ShardRows]:
+    """The rows of projects [lo, hi) in their original (heap) order; project ids, vocabularies,
+    string pools and the corpus CSV stay global."""
+    def sel(p):
+        p = p.astype(np.int64)
+        return np.nonzero((p >= lo) & (p < hi))[0]
+    b, c, i = sel(t.b_project), sel(t.c_project), sel(t.i_project)
+    pi = sel(t.pi_project)
+    s = dataclasses.replace(
+        t, b_project=t.b_project[b], b_type=t.b_type[b], b_result=t.b_result[b], b_time=t.b_time[b],
+        b_modules=t.b_modules[b], b_revisions=t.b_revisions[b], b_name=t.b_name[b],
+        c_project=t.c_project[c], c_date=t.c_date[c], c_coverage=t.c_coverage[c],
+        c_coverage_valid=t.c_coverage_valid[c], c_covered=t.c_covered[c], c_covered_valid=t.c_covered_valid[c],
+        c_total=t.c_total[c], c_total_valid=t.c_total_valid[c],
+        i_number=t.i_number[i], i_project=t.i_project[i], i_rts=t.i_rts[i], i_status=t.i_status[i],
+        i_new_id=t.i_new_id[i], pi_project=t.pi_project[pi], pi_first_commit=t.pi_first_commit[pi])
+    return s, ShardRows(lo, hi, b, c, i)
+
+
+# ---------------------------------------------------------------------------------- collectives
+def _dist():
+    import torch.distributed as dist
+    return dist
+
+
+def _staged(x) -> bool:
+    # RCCL ("nccl") takes device tensors directly; gloo (CPU tests, one-GPU rehearsals with several
+    # ranks on one device) only host tensors for all_gather - stage device tensors through the host
+    return x.is_cuda and _dist().get_backend() == "gloo"
+
+
+def all_reduce(x, op=None):
+    """In-place all-reduce (default SUM)."""
+    dist = _dist()
+    op = dist.ReduceOp.SUM if op is None else op
+    if _staged(x):
+        h = x.cpu()
+        dist.all_reduce(h, op=op)
+        x.copy_(h)
+    else:
+        dist.all_reduce(x, op=op)
+
+
+def all_gather(x):
+    """All-gather of equal-shape tensors -> list in rank order (on x's device)."""
+    import torch
+    dist = _dist()
+    world = dist.get_world_size()
+    if _staged(x):
+        h = x.cpu()
+        outs = [torch.empty_like(h) for _ in range(world)]
+        dist.all_gather(outs, h)
+        return [o.to(x.device) for o in outs]
+    outs = [torch.empty_like(x) for _ in range(world)]
+    dist.all_gather(outs, x)
+    return outs
+
+
+def all_gather_v(x):
+    """All-gather of a 1-D tensor whose length differs per rank -> list (rank order) of tensors."""
+    import torch
+    n = torch.tensor([x.numel()], dtype=torch.int64, device=x.device)
+    sizes = [int(v) for v in torch.cat(all_gather(n)).tolist()]
+    m = max(max(sizes), 1)
+    buf = torch.zeros(m, dtype=x.dtype, device=x.device)
+    buf[:x.numel()] = x.reshape(-1)
+    return [o[:k] for o, k in zip(all_gather(buf), sizes)]
+
+
+def agree_max(v: int, device=None) -> int:
+    """MAX over ranks of a host integer (e.g. the RQ1 iteration-axis length, agreed once per load
+    so every rank's per-iteration buffers have the same shape)."""
+    import torch
+    x = torch.tensor([int(v)], dtype=torch.int64, device=device)
+    all_reduce(x, _dist().ReduceOp.MAX)
+    return int(x.item())
+
+
+# ----------------------------------------------------------------------------------------- RQ1
+def rq1_sharded(shard, rank: int, world: int):
+    """Exact RQ1 over project shards.  ``shard.run(ext)`` returns a dict of tensors (one device):
+    counts[RQ1_NCOUNTS] int64, iter_total / iter_detected [M] int64 (M agreed across ranks),
+    number / build_time int64 of this rank's matches (ORDER BY project, rts); ext is None or
+    (number, build_time, before) tensors of competing matches from other ranks.
+    ``shard.finish(counts, iter_total, iter_detected)`` recomputes the finishing counters in place.
+    Returns (part, counts, iter_total, iter_detected, reran) - part = the final local run."""
+    import torch
+    dist = _dist()
+    part = shard.run(None)
+    reran = False
+    if world > 1:
+        nums = all_gather_v(part["number"])
+        bts = all_gather_v(part["build_time"])
+        mine = part["number"]
+        en, eb, ef = [], [], []
+        for r in range(world):
+            if r == rank or nums[r].numel() == 0 or mine.numel() == 0:
+                continue
+            hit = torch.isin(nums[r], mine)
+            if bool(hit.any()):
+                en.append(nums[r][hit])
+                eb.append(bts[r][hit])
+                ef.append(torch.full((int(hit.sum()),), 1 if r < rank else 0, dtype=torch.uint8, device=mine.device))
+        if en:
+            part = shard.run((torch.cat(en), torch.cat(eb), torch.cat(ef)))
+            reran = True
+    counts = part["counts"].clone()
+    it, idt = part["iter_total"].clone(), part["iter_detected"].clone()
+    if world > 1:
+        mx = counts[RQ1_MAX_ITER:RQ1_MAX_ITER + 1].clone()
+        all_reduce(counts)
+        all_reduce(mx, dist.ReduceOp.MAX)
+        counts[RQ1_MAX_ITER] = mx[0]
+        all_reduce(it)
+        all_reduce(idt)
+    shard.finish(counts, it, idt)
+    return part, counts, it, idt, reran
+
+
+# ----------------------------------------------------------------------------------------- RQ3
+RQ3_DET_F = ("det_pct",)
+RQ3_DET_I = ("det_cov", "det_tot", "det_project", "det_issue")
+RQ3_NON_F = ("non_pct",)
+RQ3_NON_I = ("non_cov", "non_tot")
+
+
+def rq3_sharded(shard, rank: int, world: int):
+    """Exact RQ3 over project shards.  ``shard.run()`` runs with FZ_RQ3_FLUSH_LAST and returns
+    counts[RQ3_NCOUNTS] int64 plus the det_* / non_* columns (sliced to their lengths);
+    ``shard.stats(det_pct, det_tot, non_pct)`` runs the statistics over the gathered samples.
+    Returns (counts, columns dict, stats) - columns in global project order."""
+    import torch
+    part = shard.run()
+    counts = part["counts"]
+    if world > 1:
+        cl = [c.cpu().numpy() for c in all_gather(counts)]
+        cols = {k: all_gather_v(part[k]) for k in RQ3_DET_F + RQ3_DET_I + RQ3_NON_F + RQ3_NON_I}
+    else:
+        cl = [counts.cpu().numpy()]
+        cols = {k: [part[k]] for k in RQ3_DET_F + RQ3_DET_I + RQ3_NON_F + RQ3_NON_I}
+    with_issues = [r for r in range(world) if cl[r][RQ3_ISSUES] > 0]
+    last = with_issues[-1] if with_issues else -1
+    if last >= 0:  # the globally last issue-bearing project is never flushed (rq3:245-257)
+        drop = int(cl[last][RQ3_NON_LAST])
+        for k in RQ3_NON_F + RQ3_NON_I:
+            v = cols[k][last]
+            cols[k][last] = v[:v.numel() - drop]
+    out = {k: torch.cat(v) for k, v in cols.items()}
+    total = np.sum(np.stack(cl), axis=0)
+    total[RQ3_DETECTED] = out["det_pct"].numel()
+    total[RQ3_NON_DETECTED] = out["non_pct"].numel()
+    total[RQ3_NON_LAST] = 0
+    st = shard.stats(out["det_pct"], out["det_tot"], out["non_pct"])
+    return total, out, st
+
+
+# ------------------------------------------------------------------------------------ row gathers
+def gather_rows(cols: dict, world: int) -> dict:
+    """Concatenate per-rank row columns in rank (= project) order (RQ2 change rows, RQ1 raw rows)."""
+    import torch
+    if world == 1:
+        return dict(cols)
+    return {k: torch.cat(all_gather_v(v)) for k, v in cols.items()}
+
+
+# --------------------------------------------------------------------------------- GPU shards
+class GpuRQ1Shard:
+    """RQ1 of one rank on its engine (libfz fz_rq1_ex / fz_rq1_finish)."""
+
+    def __init__(self, eng, max_iter: int, threshold: int = 100):
+        import ctypes as C
+        from . import engine as E
+        from .rq import compute
+        self.E, self.C, self.eng, self.threshold = E, C, eng, threshold
+        self.bufs = compute.RQ1Buffers(eng, max_iter=max_iter)
+        self.b_time = eng.tables.cols["b_time"]
+        self.i_number = eng.tables.cols["i_number"]
+
+    def run(self, ext):
+        E, C, eng, b = self.E, self.C, self.eng, self.bufs
+        keep = None
+        if ext is None:
+            x = E.FzRq1Ext(0, None, None, None)
+        else:
+            keep = tuple(v.contiguous() for v in ext)
+            x = E.FzRq1Ext(keep[0].numel(), C.c_void_p(keep[0].data_ptr()), C.c_void_p(keep[1].data_ptr()),
+                           C.c_void_p(keep[2].data_ptr()))
+        E._check(eng.lib, eng.lib.fz_rq1_ex(eng.ctx, self.threshold, C.byref(x), C.byref(b.out)))
+        n = int(b.counts[RQ1_MATCHED].item())
+        mi, mb = b.matched_issue[:n], b.matched_build[:n]
+        return {"counts": b.counts, "iter_total": b.iter_total, "iter_detected": b.iter_detected,
+                "number": self.i_number[mi], "build_time": self.b_time[mb], "matched_issue": mi, "matched_build": mb}
+
+    def finish(self, counts, it, idt):
+        E, C, eng = self.E, self.C, self.eng
+        E._check(eng.lib, eng.lib.fz_rq1_finish(eng.ctx, self.threshold, C.c_void_p(it.data_ptr()),
+                                                C.c_void_p(idt.data_ptr()), it.numel(),
+                                                C.c_void_p(counts.data_ptr()), C.c_void_p(self.bufs.late.data_ptr())))
+
+
+class GpuRQ3Shard:
+    """RQ3 of one rank on its engine (libfz fz_rq3_ex with FZ_RQ3_FLUSH_LAST / fz_rq3_stats)."""
+
+    def __init__(self, eng):
+        import ctypes as C
+        from . import engine as E
+        from .rq import compute
+        self.E, self.C, self.eng = E, C, eng
+        self.bufs = compute.rq3_buffers(eng)
+
+    def run(self):
+        E, C, eng, b = self.E, self.C, self.eng, self.bufs
+        E._check(eng.lib, eng.lib.fz_rq3_ex(eng.ctx, E.FZ_RQ3_FLUSH_LAST | E.FZ_RQ3_SKIP_STATS, C.byref(b.out)))
+        cnt = b.counts.cpu()
+        nd, nn = int(cnt[RQ3_DETECTED]), int(cnt[RQ3_NON_DETECTED])
+        out = {"counts": b.counts}
+        for k in RQ3_DET_F + RQ3_DET_I:
+            out[k] = getattr(b, k)[:nd]
+        for k in RQ3_NON_F + RQ3_NON_I:
+            out[k] = getattr(b, k)[:nn]
+        return out
+
+    def stats(self, det_pct, det_tot, non_pct):
+        E, C, eng, b = self.E, self.C, self.eng, self.bufs
+        P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+        E._check(eng.lib, eng.lib.fz_rq3_stats(eng.ctx, P(det_pct), P(det_tot), det_pct.numel(), P(non_pct),
+                                               non_pct.numel(), C.c_void_p(b.describe.data_ptr()),
+                                               C.c_void_p(b.tests.data_ptr())))
+        return {"describe": b.describe, "tests": b.tests}

@@ -24,10 +24,11 @@ def _describe(d: E.FzDescribe, with_min_nonzero=False) -> Describe:
 class RQ1Buffers:
     """Device outputs of fz_rq1, allocated once per store (re-used across bench steps)."""
 
-    def __init__(self, eng: E.Engine):
+    def __init__(self, eng: E.Engine, max_iter: int = 0):
         torch = eng.torch
         fz = eng.tables.fz
-        M = max(int(eng.stats.max_fuzz_per_project), 1)
+        # max_iter: the iteration axis agreed across shards (parallel.agree_max), >= the local one
+        M = max(int(eng.stats.max_fuzz_per_project), int(max_iter), 1)
         self.counts = eng.zeros(E.FZ_RQ1_NCOUNTS, torch.int64)
         self.eligible = eng.zeros(fz.n_projects, torch.uint8)
         self.iter_total = eng.zeros(M, torch.int64)
@@ -49,23 +50,31 @@ def rq1_collect(eng: E.Engine, bufs: RQ1Buffers, threshold: int = 100) -> RQ1Res
     cnt = bufs.counts.cpu().numpy()
     n_match = int(cnt[E.RQ1_MATCHED])
     M = int(cnt[E.RQ1_MAX_ITER])
+    return rq1_result(cnt, bufs.iter_total[:M].cpu().numpy(), bufs.iter_detected[:M].cpu().numpy(),
+                      bufs.late.cpu().numpy(), bufs.matched_issue[:n_match].cpu().numpy(),
+                      bufs.matched_build[:n_match].cpu().numpy(),
+                      np.nonzero(bufs.eligible.cpu().numpy()[:eng.tables.fz.n_projects])[0], threshold)
+
+
+def rq1_result(cnt, iter_total, iter_detected, late_doubles, matched_issue, matched_build, eligible,
+               threshold: int = 100) -> RQ1Result:
+    """RQ1Result from fz_rq1's counters and arrays (host copies; also the sharded recombination)."""
     late = None
     if cnt[E.RQ1_LATE] > 0:
-        d = _describe(E.describe_from_doubles(bufs.late.cpu().numpy()), with_min_nonzero=True)
+        d = _describe(E.describe_from_doubles(late_doubles), with_min_nonzero=True)
         # rq1_detection_rate.py:256-268 reports only these numbers (no sign split, no std)
         late = Describe(count=d.count, n_zero=d.n_zero, min=d.min, max=d.max, q1=d.q1, q3=d.q3,
                         median=d.median, mean=d.mean, min_nonzero=d.min_nonzero)
-    elig = np.nonzero(bufs.eligible.cpu().numpy()[:eng.tables.fz.n_projects])[0]
+    elig = np.asarray(eligible)
     return RQ1Result(
         n_issues_lim=int(cnt[E.RQ1_ISSUES_LIM]), n_issues_lim_projects=int(cnt[E.RQ1_ISSUES_LIM_PROJECTS]),
         n_fixed_lim=int(cnt[E.RQ1_FIXED_LIM]), n_fixed_lim_projects=int(cnt[E.RQ1_FIXED_LIM_PROJECTS]),
         eligible=elig, n_without_matching=int(cnt[E.RQ1_WITHOUT_MATCHING]),
         n_target=int(cnt[E.RQ1_TARGET]), n_target_projects=int(cnt[E.RQ1_TARGET_PROJECTS]),
         total_fuzz_builds=int(cnt[E.RQ1_TOTAL_FUZZ]),
-        matched_issue=bufs.matched_issue[:n_match].cpu().numpy(),
-        matched_build=bufs.matched_build[:n_match].cpu().numpy(),
+        matched_issue=np.asarray(matched_issue), matched_build=np.asarray(matched_build),
         n_matched_projects=int(cnt[E.RQ1_MATCHED_PROJECTS]),
-        iter_total=bufs.iter_total[:M].cpu().numpy(), iter_detected=bufs.iter_detected[:M].cpu().numpy(),
+        iter_total=np.asarray(iter_total), iter_detected=np.asarray(iter_detected),
         min_project_threshold=threshold, late=late)
 
 
@@ -187,23 +196,32 @@ def rq3_launch(eng: E.Engine, b: OutBuffers):
     E._check(eng.lib, eng.lib.fz_rq3(eng.ctx, C.byref(b.out)))
 
 
+RQ3_COLUMNS = ("det_pct", "det_cov", "det_tot", "det_project", "det_issue", "non_pct", "non_cov", "non_tot")
+
+
 def rq3_collect(eng: E.Engine, b: OutBuffers) -> RQ3Result:
     cnt = b.host("counts")
     nd, nn = int(cnt[E.RQ3_DETECTED]), int(cnt[E.RQ3_NON_DETECTED])
-    desc = b.host("describe").reshape(3, E.DESCRIBE_DOUBLES)
-    ts = b.host("tests")
+    cols = {k: b.host(k, nd if k.startswith("det") else nn) for k in RQ3_COLUMNS}
+    return rq3_result(cnt, cols, b.host("describe"), b.host("tests"))
+
+
+def rq3_result(cnt, cols, describe_doubles, tests) -> RQ3Result:
+    """RQ3Result from fz_rq3's counters, columns and statistics (also the sharded recombination)."""
+    nd, nn = len(cols["det_pct"]), len(cols["non_pct"])
+    desc = np.asarray(describe_doubles).reshape(3, E.DESCRIBE_DOUBLES)
+    ts = np.asarray(tests)
     both = nd > 0 and nn > 0
     return RQ3Result(
-        n_all_issues=int(cnt[E.RQ3_ISSUES]), det_pct=b.host("det_pct", nd), det_cov=b.host("det_cov", nd),
-        det_tot=b.host("det_tot", nd), det_project=b.host("det_project", nd), det_issue=b.host("det_issue", nd),
-        non_pct=b.host("non_pct", nn), non_cov=b.host("non_cov", nn), non_tot=b.host("non_tot", nn),
+        n_all_issues=int(cnt[E.RQ3_ISSUES]), **{k: np.asarray(cols[k]) for k in RQ3_COLUMNS},
         desc_detected=_describe(E.describe_from_doubles(desc[0])) if nd else None,
         desc_non=_describe(E.describe_from_doubles(desc[1])) if nn else None,
         desc_det_total=_describe(E.describe_from_doubles(desc[2])) if nd else None,
         anderson_det=(float(ts[E.RQ3_AD_DET]), ts[E.RQ3_AD_DET + 1:E.RQ3_AD_DET + 6].copy()) if both else None,
         anderson_non=(float(ts[E.RQ3_AD_NON]), ts[E.RQ3_AD_NON + 1:E.RQ3_AD_NON + 6].copy()) if both else None,
         levene=(float(ts[E.RQ3_LEVENE_W]), float(ts[E.RQ3_LEVENE_P])) if both else None,
-        brunnermunzel=(float(ts[E.RQ3_BM_STAT]), float(ts[E.RQ3_BM_P])) if both else None)
+        brunnermunzel=(float(ts[E.RQ3_BM_STAT]), float(ts[E.RQ3_BM_P])) if both else None,
+        n_non_last=int(cnt[E.RQ3_NON_LAST]))
 
 
 def rq3(eng: E.Engine) -> RQ3Result:

@@ -106,6 +106,7 @@ class RQ3Result:
     anderson_non: Optional[Tuple[float, np.ndarray]]
     levene: Optional[Tuple[float, float]]
     brunnermunzel: Optional[Tuple[float, float]]
+    n_non_last: int = 0                # sharded runs: non-detected rows of the last project (tail)
 
 
 @dataclass
