@@ -161,7 +161,8 @@ def main():
             avg_ms = probe_ms / launches
             ach = probe_bytes / launches / (avg_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": args.probe,
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.probe, args.config),
+                    "kernel": args.probe,
                     "avg_launch_us": round(avg_ms * 1e3, 3), "bytes_per_launch": probe_bytes / launches,
                     "launches_per_step": launches / args.steps}
         cpu = None
@@ -184,6 +185,22 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     return out
+
+
+def pmc_traffic(probe, config):
+    """HBM bytes per launch of the probed kernel from the committed PMC passes (profiles/
+    *_pmc_traffic.json, written by scripts/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE
+    runs of this bench with the gfx950 FETCH_SIZE correction), or None."""
+    import glob
+    kern = {"radix_scatter": "k_radix_scatter"}.get(probe, probe)
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel_match") == kern and d.get("config") == config:
+            return round(float(d["traffic_bytes_per_launch"]))
+    return None
 
 
 def weak_shard(t, rank, world):

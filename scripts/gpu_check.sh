@@ -20,6 +20,9 @@ STEPS=${STEPS:-tests,smoke,bench,prof}
 [[ $STEPS == *smoke* ]] && run smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* ]] && run bench 400 python -u bench.py
 [[ $STEPS == *rehearse2* ]] && run bench_rehearse2 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo --no-cpu-baseline
+# PMC passes: one counter group per run (FETCH_SIZE uses 3 TCC slots, WRITE_SIZE 2), SIGKILL limit
+[[ $STEPS == *pmcF* ]] && run pmc_fetch 150 timeout -s KILL 140 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_$TAG -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline
+[[ $STEPS == *pmcW* ]] && run pmc_write 150 timeout -s KILL 140 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline
 [[ $STEPS == *c3* ]] && run bench_c3 600 python -u bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline
 [[ $STEPS == *pc3* ]] && run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c3_$TAG -o run -- python -u bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline
 [[ $STEPS == *prof* ]] && run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline
