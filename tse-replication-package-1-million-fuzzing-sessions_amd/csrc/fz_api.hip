@@ -63,7 +63,7 @@ int fz_ctx_create(int device, void *stream, fz_ctx **out) {
         c->device = device;
         c->stream = static_cast<hipStream_t>(stream);
         void *h = nullptr;
-        if (hipHostMalloc(&h, 4096, hipHostMallocDefault) != hipSuccess) {
+        if (hipHostMalloc(&h, 32768, hipHostMallocDefault) != hipSuccess) {
             delete c;
             throw fz::Error(FZ_E_DEVICE, "fz_ctx_create: hipHostMalloc failed");
         }

@@ -323,34 +323,212 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t *__rest
     }
 }
 
+// ---- single-sweep LSD passes (one launch per digit pass) -----------------------------------
+// One histogram kernel counts every pass's digits up front (passes whose digit is the same for
+// all keys are skipped: they are identity permutations).  Each pass is then ONE kernel: a tile
+// ranks its 4096 keys (stable: round, wave, lane order), publishes its per-digit counts, and gets
+// its global base per digit by decoupled look-back over the preceding tiles' status words
+// {flag:2, epoch:14, count:48} (tiles in ticket order; 8 predecessors per poll) - no per-tile
+// histogram pass, no device-wide scan of the tile x digit counts.  Epoch tags make stale words
+// from earlier passes invisible, so the status array is never cleared between passes.
+constexpr int kOsMaxPasses = 8;
+constexpr uint64_t kOsAgg = 1ull << 62, kOsInc = 2ull << 62, kOsFlags = 3ull << 62;
+constexpr uint64_t kOsValMask = (1ull << 48) - 1ull, kOsEpochMask = ((1ull << 14) - 1ull) << 48;
+constexpr int kOsWindow = 8;
+
+__global__ __launch_bounds__(kBlock) void k_onesweep_hist(const uint64_t *__restrict__ keys, int64_t n, int npass,
+                                                          unsigned long long *__restrict__ ghist) {
+    __shared__ uint32_t s_h[kOsMaxPasses][kRadix];
+    for (int i = threadIdx.x; i < kOsMaxPasses * kRadix; i += kBlock) (&s_h[0][0])[i] = 0u;
+    __syncthreads();
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i - threadIdx.x < n;
+         i += int64_t(gridDim.x) * kBlock) {
+        const bool valid = i < n;
+        const uint64_t k = valid ? keys[i] : 0ull;
+        for (int p = 0; p < npass; ++p) {
+            const uint32_t d = uint32_t(k >> (p * kRadixBits)) & (kRadix - 1);
+            // wave-uniform digit (typical for the high digits): one add instead of 64 conflicting
+            const uint32_t d0 = __shfl(d, 0, 64);
+            const uint64_t act = __ballot(valid);
+            if (__ballot(valid && d == d0) == act) {
+                if (lane_id() == 0 && act) atomicAdd(&s_h[p][d0], uint32_t(__popcll(act)));
+            } else if (valid) {
+                atomicAdd(&s_h[p][d], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < npass * kRadix; i += kBlock) {
+        const uint32_t v = (&s_h[0][0])[i];
+        if (v) atomicAdd(&ghist[i], (unsigned long long)v);
+    }
+}
+
+template <bool HAS_VALS>
+__global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict__ keys_in,
+                                                     const uint32_t *__restrict__ vals_in,
+                                                     uint64_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
+                                                     int64_t n, int shift, const unsigned long long *__restrict__ ghist,
+                                                     uint64_t *__restrict__ status, unsigned int *__restrict__ ticket,
+                                                     unsigned int ticket_base, uint64_t epoch) {
+    __shared__ uint64_t s_keys[kSortTile];
+    __shared__ uint32_t s_vals[HAS_VALS ? kSortTile : 1];
+    __shared__ uint32_t s_run[kRadix];
+    __shared__ uint32_t s_wcnt[4][kRadix];
+    __shared__ uint32_t s_start[kRadix];
+    __shared__ int64_t s_goff[kRadix];
+    __shared__ uint32_t s_tmp[4];
+    __shared__ int64_t s_tmp64[4];
+    __shared__ unsigned int s_tile;
+
+    const int tid = threadIdx.x;
+    const int w = wave_id();
+    if (tid == 0) s_tile = atomicAdd(ticket, 1u) - ticket_base;
+    s_run[tid] = 0;
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int64_t base = tile * kSortTile;
+
+    uint64_t k[kSortItems];
+    uint32_t v[kSortItems];
+    uint32_t rank[kSortItems];
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        const int64_t idx = base + r * kBlock + tid;
+        const bool valid = idx < n;
+        k[r] = valid ? keys_in[idx] : 0ull;
+        v[r] = (HAS_VALS && valid) ? vals_in[idx] : 0u;
+    }
+    // stable in-tile ranks: (round, wave, lane) order
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        const bool valid = base + r * kBlock + tid < n;
+        const uint32_t d = uint32_t(k[r] >> shift) & (kRadix - 1);
+        for (int i = 0; i < 4; ++i) s_wcnt[i][tid] = 0;
+        __syncthreads();
+        const uint64_t peers = match_digit<kRadixBits>(d, valid);
+        const uint32_t lrank = uint32_t(__popcll(peers & lanemask_lt()));
+        if (valid && (__ffsll((long long)peers) - 1) == lane_id()) s_wcnt[w][d] = uint32_t(__popcll(peers));
+        __syncthreads();
+        uint32_t wpre = 0;
+        for (int i = 0; i < w; ++i) wpre += s_wcnt[i][d];
+        rank[r] = s_run[d] + wpre + lrank;
+        __syncthreads();
+        s_run[tid] += s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
+    }
+    __syncthreads();
+    const uint32_t cnt = s_run[tid];
+    // publish this tile's count of digit tid, then look back for the counts of all earlier tiles
+    uint64_t *my = &status[tile * kRadix + tid];
+    __hip_atomic_store(my, (tile == 0 ? kOsInc : kOsAgg) | epoch | uint64_t(cnt), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    s_start[tid] = block_excl_scan(cnt, s_tmp, (uint32_t *)nullptr);
+    const int64_t gstart = block_excl_scan(int64_t(ghist[tid]), s_tmp64, (int64_t *)nullptr);
+    int64_t prefix = 0;
+    for (int64_t q = tile - 1; q >= 0;) {
+        uint64_t sw[kOsWindow];
+#pragma unroll
+        for (int j = 0; j < kOsWindow; ++j)
+            sw[j] = q - j >= 0 ? __hip_atomic_load(&status[(q - j) * kRadix + tid], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : (kOsInc | epoch);
+        int j = 0;
+        bool done = false;
+        for (; j < kOsWindow; ++j) {
+            const uint64_t x = sw[j];
+            if ((x & kOsEpochMask) != epoch || !(x & kOsFlags)) break;  // not published yet
+            prefix += int64_t(x & kOsValMask);
+            if ((x & kOsFlags) == kOsInc) {
+                done = true;
+                break;
+            }
+        }
+        if (done) break;
+        q -= j;
+        if (j < kOsWindow) __builtin_amdgcn_s_sleep(1);
+    }
+    if (tile > 0)
+        __hip_atomic_store(my, kOsInc | epoch | uint64_t(prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_goff[tid] = gstart + prefix - int64_t(s_start[tid]);
+    // stage the tile digit-sorted in LDS, then write it out in per-digit runs
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        if (base + r * kBlock + tid < n) {
+            const uint32_t d = uint32_t(k[r] >> shift) & (kRadix - 1);
+            const uint32_t pos = s_start[d] + rank[r];
+            s_keys[pos] = k[r];
+            if (HAS_VALS) s_vals[pos] = v[r];
+        }
+    }
+    __syncthreads();
+    const int64_t valid_n = (n - base) < kSortTile ? (n - base) : kSortTile;
+    for (int i = tid; i < valid_n; i += kBlock) {
+        const uint64_t kk = s_keys[i];
+        const uint32_t d = uint32_t(kk >> shift) & (kRadix - 1);
+        const int64_t gpos = s_goff[d] + i;
+        keys_out[gpos] = kk;
+        if (HAS_VALS) vals_out[gpos] = s_vals[i];
+    }
+}
+
 void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int bits) {
     if (n <= 1 || bits <= 0) return;
+    const int npass = (bits + kRadixBits - 1) / kRadixBits;
     const int64_t nb = (n + kSortTile - 1) / kSortTile;
+    FZ_CHECK(n < (int64_t(1) << 47), "radix_sort_pairs: too many keys");
+    // digit totals of every pass (one read of the keys)
+    unsigned long long *ghist = c->arena.get<unsigned long long>(kOsMaxPasses * kRadix);
+    FZ_HIP(hipMemsetAsync(ghist, 0, sizeof(unsigned long long) * kOsMaxPasses * kRadix, c->stream));
+    {
+        ProbeScope ps(c, "radix_hist", 8.0 * double(n));
+        k_onesweep_hist<<<grid_for(n, kBlock * 8, 2048), kBlock, 0, c->stream>>>(keys, n, npass, ghist);
+        FZ_LAUNCH_CHECK();
+    }
+    unsigned long long *hh = reinterpret_cast<unsigned long long *>(c->h_pinned);
+    FZ_HIP(hipMemcpyAsync(hh, ghist, sizeof(unsigned long long) * npass * kRadix, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    bool need[kOsMaxPasses];
+    for (int p = 0; p < npass; ++p) {
+        int nz = 0;
+        for (int d = 0; d < kRadix; ++d) nz += hh[p * kRadix + d] != 0;
+        need[p] = nz > 1;  // a pass whose digit is constant is the identity permutation
+    }
+    // status words: grown (and cleared) on demand; epochs tag every pass
+    if (c->os_status.cap < size_t(nb) * kRadix * 8) {
+        uint64_t *st = c->os_status.ensure<uint64_t>(nb * kRadix);
+        FZ_HIP(hipMemsetAsync(st, 0, c->os_status.cap, c->stream));
+        c->os_epoch = 0;
+    }
+    if (c->os_ticket.cap == 0) {
+        FZ_HIP(hipMemsetAsync(c->os_ticket.ensure<unsigned int>(1), 0, 4, c->stream));
+        c->os_ticket_base = 0;
+    }
     uint64_t *k2 = c->arena.get<uint64_t>(n);
     uint32_t *v2 = vals ? c->arena.get<uint32_t>(n) : nullptr;
-    int64_t *counts = c->arena.get<int64_t>(nb * kRadix);
-    int64_t *offs = c->arena.get<int64_t>(nb * kRadix);
     uint64_t *ka = keys, *kb = k2;
     uint32_t *va = vals, *vb = v2;
     int passes = 0;
-    for (int shift = 0; shift < bits; shift += kRadixBits) {
-        {
-            ProbeScope ps(c, "radix_hist", 8.0 * double(n));
-            k_radix_hist<<<unsigned(nb), kBlock, 0, c->stream>>>(ka, n, shift, counts, nb);
-            FZ_LAUNCH_CHECK();
+    for (int p = 0; p < npass; ++p) {
+        if (!need[p]) continue;
+        if (++c->os_epoch == (1u << 14)) {  // epoch wrap: clear the status words once
+            FZ_HIP(hipMemsetAsync(c->os_status.ptr, 0, c->os_status.cap, c->stream));
+            c->os_epoch = 1;
         }
-        scan_exclusive_i64(c, counts, offs, nb * kRadix, nullptr);
+        const uint64_t epoch = uint64_t(c->os_epoch) << 48;
         {
             // algorithmic traffic of one pass: read + write every key (8 B) and value (4 B)
             ProbeScope ps(c, "radix_scatter", (vals ? 24.0 : 16.0) * double(n));
             if (vals)
-                k_radix_scatter<true><<<unsigned(nb), kBlock, 0, c->stream>>>(ka, va, kb, vb, n, shift, counts, offs,
-                                                                              nb);
+                k_onesweep<true><<<unsigned(nb), kBlock, 0, c->stream>>>(
+                    ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, c->os_status.as<uint64_t>(),
+                    c->os_ticket.as<unsigned int>(), c->os_ticket_base, epoch);
             else
-                k_radix_scatter<false><<<unsigned(nb), kBlock, 0, c->stream>>>(ka, va, kb, vb, n, shift, counts, offs,
-                                                                               nb);
+                k_onesweep<false><<<unsigned(nb), kBlock, 0, c->stream>>>(
+                    ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, c->os_status.as<uint64_t>(),
+                    c->os_ticket.as<unsigned int>(), c->os_ticket_base, epoch);
             FZ_LAUNCH_CHECK();
         }
+        c->os_ticket_base += unsigned(nb);
         std::swap(ka, kb);
         std::swap(va, vb);
         ++passes;
