@@ -89,6 +89,9 @@ def main():
         M = par.agree_max(int(st.max_fuzz_per_project), dev)
         rq1_shard = par.GpuRQ1Shard(eng, M)
         rq3_shard = par.GpuRQ3Shard(eng)
+        rq2c_shard = par.GpuRQ2CountShard(eng)
+        rq4a_shard = par.GpuRQ4aShard(eng, M)
+        own = (rank * len(t.projects) // world, (rank + 1) * len(t.projects) // world)  # weak_shard ids
     rq1_bufs = compute.RQ1Buffers(eng)
     bufs = {"rq2_count": compute.rq2_count_buffers(eng), "rq2_add": compute.rq2_add_buffers(eng),
             "rq3": compute.rq3_buffers(eng), "rq4a": compute.rq4a_buffers(eng), "rq4b": compute.rq4b_buffers(eng)}
@@ -110,7 +113,11 @@ def main():
         if "rq1" in stages:
             part = par.rq1_sharded(rq1_shard, rank, world)[0]
             par.gather_rows({"issue": part["matched_issue"], "build": part["matched_build"]}, world)
-        for name in ("rq2_count", "rq2_add", "rq4a", "rq4b"):
+        if "rq2_count" in stages:
+            par.rq2_count_sharded(rq2c_shard, rank, world, *own, gather_values=False)
+        if "rq4a" in stages:
+            par.rq4a_sharded(rq4a_shard, rank, world, *own)
+        for name in ("rq2_add", "rq4b"):
             if name in stages:
                 launch[name](eng, bufs[name])
         if "rq2_add" in stages:

@@ -201,6 +201,27 @@ typedef struct fz_rq2_count_out {
 
 int fz_rq2_count(fz_ctx *ctx, const fz_rq2_count_out *out);
 
+/* Project-sharded RQ2 count.  A session index i holds the i-th trend value of
+ * every project (project order, rq2_coverage_count.py:330-333), so per-session statistics need the
+ * values of all shards: each shard runs fz_rq2_count_ex with FZ_RQ2C_SKIP_SESSION_STATS (per-project
+ * outputs + its session-major values), the values are exchanged by session index (all-to-all), and
+ * the owner of a session range runs fz_rq2_session_stats on what it received. */
+#define FZ_RQ2C_SKIP_SESSION_STATS 1u  /* no per-session / median-trend / correlation summaries */
+int fz_rq2_count_ex(fz_ctx *ctx, uint32_t flags, const fz_rq2_count_out *out);
+
+/* Per-session statistics (:139-152, :390, :439-440) of n_values (session id, value) pairs, ids in
+ * [0, n_sessions); pairs of one session keep their input order (stable).  average / median:
+ * statistics.mean / statistics.median, percentiles[s * 5 + j]: np.percentile at 5/25/50/75/95,
+ * n_ge100[0] = sessions with >= 100 values.  Empty sessions get NaN.  max_session_len: a host upper
+ * bound of one session's size (e.g. the number of projects), 0 if unknown. */
+int fz_rq2_session_stats(fz_ctx *ctx, const double *values, const int64_t *session_ids, int64_t n_values,
+                         int64_t n_sessions, int64_t max_session_len, double *average, double *median,
+                         double *percentiles, int64_t *n_ge100);
+
+/* scipy.stats.spearmanr(range(n), x) and scipy.stats.shapiro(x) of one device series:
+ * out[0..3] = rho, p, W, p (NaN where scipy returns NaN: n < 2 / constant, n < 3). */
+int fz_series_tests(fz_ctx *ctx, const double *x, int64_t n, double *out);
+
 /* ---- RQ2/RQ3 support (add): rq2_coverage_and_added.py:73-238 ------------------------------- */
 enum { FZ_RQ2A_ELIGIBLE = 0, FZ_RQ2A_ROWS, FZ_RQ2A_RUNS, FZ_RQ2A_NCOUNTS = 4 };
 typedef struct fz_rq2_add_out {
@@ -311,6 +332,14 @@ typedef struct fz_rq4a_out {
 } fz_rq4a_out;
 
 int fz_rq4a(fz_ctx *ctx, const fz_rq4_groups *groups, const fz_rq4a_out *out);
+
+/* Finishing of RQ4a on shard-combined inputs: the per-iteration tables summed over
+ * shards ([max_iter] each), intro[n_projects] (every shard's own projects) and g4_steps[30] summed.
+ * Recomputes counts[FZ_RQ4A_ROWS / AFTER_G1 / AFTER_G2] and every scalars[] entry; other counts
+ * (group sizes, INTRO_POS, HAS_WINDOW, MAX_ITER) are the caller's sums / maxima. */
+int fz_rq4a_finish(fz_ctx *ctx, const int64_t *g1_total, const int64_t *g1_det, const int64_t *g2_total,
+                   const int64_t *g2_det, int64_t max_iter, const int64_t *intro, int64_t n_projects,
+                   const int64_t *g4_steps, int64_t *counts, double *scalars);
 
 /* ---- RQ4b: rq4b_coverage.py:1209-1261 ---------------------------------------------------- */
 enum {

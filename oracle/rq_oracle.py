@@ -429,14 +429,6 @@ def rq4a(t: Tables) -> RQ4aResult:
         tot, det = stats_[g]
         arr[g] = (np.array([tot.get(i, 0) for i in range(1, mx + 1)], np.int64),
                   np.array([len(det.get(i, ())) for i in range(1, mx + 1)], np.int64))
-    rows = common.rq4a_rows(arr["group1"][0], arr["group1"][1], arr["group2"][0], arr["group2"][1])
-    after = {}
-    for key, col in (("g1", 3), ("g2", 6)):
-        rates = [r[col] for r in rows]
-        fb5 = next((i for i, r in enumerate(rates) if r < 5), len(rates))
-        ra = rates[fb5:]
-        after[key] = ((float(np.median(ra)), float(np.subtract(*np.percentile(ra, [75, 25]))))
-                      if ra else None)
     # G4: introduction iteration (:246-299) and pre/post windows (:350-412)
     intro = []
     N = 7
@@ -470,7 +462,27 @@ def rq4a(t: Tables) -> RQ4aResult:
             steps[k][1] += d
             post_any |= d
         trans[0 if (pre_any and post_any) else 1 if pre_any else 2 if post_any else 3] += 1
-    pos = [k for _, k in intro if k > 0]
+    after, istats, overall = rq4a_finish(arr["group1"][0], arr["group1"][1], arr["group2"][0], arr["group2"][1],
+                                         [k for _, k in intro], steps)
+    return RQ4aResult(groups=groups, g1_total=arr["group1"][0], g1_det=arr["group1"][1],
+                      g2_total=arr["group2"][0], g2_det=arr["group2"][1], after=after, intro=intro,
+                      intro_stats=istats, g4_steps={s: tuple(v) for s, v in steps.items()},
+                      g4_transition=tuple(trans), g4_overall=overall, n_g4_analyzed=steps[-1][0],
+                      has_g4_transition=any_window)
+
+
+def rq4a_finish(g1t, g1d, g2t, g2d, intro_values, steps, N=7):
+    """rq4a_bug.py:156-207, :698-747 (rows, rates, after-slices), :246-299 (introduction stats),
+    :412-510 (pooled pre/post rates) from the tables, introduction iterations and step counts."""
+    rows = common.rq4a_rows(g1t, g1d, g2t, g2d)
+    after = {}
+    for key, col in (("g1", 3), ("g2", 6)):
+        rates = [r[col] for r in rows]
+        fb5 = next((i for i, r in enumerate(rates) if r < 5), len(rates))
+        ra = rates[fb5:]
+        after[key] = ((float(np.median(ra)), float(np.subtract(*np.percentile(ra, [75, 25]))))
+                      if ra else None)
+    pos = [k for k in intro_values if k > 0]
     istats = None
     if pos:
         s = pd.Series(pos)
@@ -480,11 +492,7 @@ def rq4a(t: Tables) -> RQ4aResult:
     post_n = sum(steps[s][0] for s in range(1, N + 1))
     post_d = sum(steps[s][1] for s in range(1, N + 1))
     overall = ((pre_d / pre_n * 100) if pre_n else 0, (post_d / post_n * 100) if post_n else 0)
-    return RQ4aResult(groups=groups, g1_total=arr["group1"][0], g1_det=arr["group1"][1],
-                      g2_total=arr["group2"][0], g2_det=arr["group2"][1], after=after, intro=intro,
-                      intro_stats=istats, g4_steps={s: tuple(v) for s, v in steps.items()},
-                      g4_transition=tuple(trans), g4_overall=overall, n_g4_analyzed=steps[-1][0],
-                      has_g4_transition=any_window)
+    return after, istats, overall
 
 
 # --------------------------------------------------------------------------------------- RQ4b

@@ -46,6 +46,29 @@ class _RQ3View(_HostView):
         return out
 
 
+class _RQ2View(_HostView):
+    def run(self):
+        return super().run()
+
+    def session_stats(self, vals, sids, S, max_len):
+        out = self.s.session_stats(vals.to(self.dev), sids.to(self.dev), S, max_len)
+        return {k: v.cpu() for k, v in out.items()}
+
+    def series_tests(self, x):
+        return self.s.series_tests(x.to(self.dev))
+
+    def mean_median(self, x):
+        return self.s.mean_median(x.to(self.dev))
+
+
+class _RQ4aView(_HostView):
+    def finish(self, tables, intro, steps, counts):
+        c = counts.to(self.dev)
+        sc = self.s.finish([x.to(self.dev) for x in tables], intro.to(self.dev), steps.to(self.dev), c)
+        counts.copy_(c.cpu())
+        return sc
+
+
 def _worker(rank, world, port, case, errfile):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -83,7 +106,16 @@ def _check(rank, world, case):
     torch.distributed.all_reduce(elig)
     late = g1.s.bufs.late.cpu().numpy()
     total3, cols3, st3 = par.rq3_sharded(_RQ3View(par.GpuRQ3Shard(eng), eng.dev, rows.issues), rank, world)
+    r2 = par.rq2_count_sharded(_RQ2View(par.GpuRQ2CountShard(eng), eng.dev), rank, world, lo, hi)
+    r4 = par.rq4a_sharded(_RQ4aView(par.GpuRQ4aShard(eng, M), eng.dev), rank, world, lo, hi)
     if rank == 0:
+        ours2 = compute.rq2_count_result(r2["proj"], r2["session_offsets"], r2["session_values"], r2["K"],
+                                         r2["average"], r2["median"], r2["percentiles"], r2["average"],
+                                         (r2["tests"][0], r2["tests"][1], r2["tests"][3]), r2["corr_mm"])
+        assert_same(ours2, orc.rq2_count(t), "rq2_count")
+        ours4 = compute.rq4a_result(r4["counts"], r4["scalars"], r4["member"], r4["tables"], r4["intro"],
+                                    r4["g4_steps"], r4["g4_transition"])
+        assert_same(ours4, orc.rq4a(t), "rq4a")
         ours3 = compute.rq3_result(total3, {k: v.numpy() for k, v in cols3.items()}, st3["describe"].numpy(),
                                    st3["tests"].numpy())
         assert_same(ours3, orc.rq3(t), "rq3")

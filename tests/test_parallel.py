@@ -18,7 +18,7 @@ import torch.multiprocessing as mp
 from tse_amd import parallel as par
 from tse_amd import synth
 from tse_amd.rq import common
-from tse_amd.schema import Tables
+from tse_amd.schema import LIMIT_US, Tables
 
 
 def _free_port():
@@ -121,6 +121,122 @@ class OracleRQ3Shard:
         return orc.rq3_stats(det_pct.numpy(), det_tot.numpy(), non_pct.numpy())
 
 
+class OracleRQ2CountShard:
+    """One rank's RQ2 count on the CPU restatement (per-project columns over the global project
+    axis + the local coverage_by_session_index), and the session / series statistics the exchange
+    needs, computed exactly as rq_oracle.rq2_count does."""
+
+    def __init__(self, t):
+        self.t = t
+
+    def run(self):
+        from oracle import rq_oracle as orc
+        r = orc.rq2_count(self.t)
+        P = len(self.t.projects)
+        el = np.zeros(P, np.int64)
+        el[r.eligible] = 1
+        cols = {"eligible": el, "raw_n": np.zeros(P, np.int64), "n_trend": np.zeros(P, np.int64),
+                "sw_w": np.full(P, np.nan), "sw_p": np.full(P, np.nan), "corr": np.full(P, np.nan)}
+        cols["raw_n"][r.eligible] = r.raw_n
+        cols["n_trend"][r.eligible] = r.n_trend
+        cols["sw_w"][r.eligible] = r.sw_w
+        cols["sw_p"][r.eligible] = r.sw_p
+        cols["corr"][r.eligible[r.raw_n > 0]] = r.corr
+        out = {k: torch.from_numpy(v) for k, v in cols.items()}
+        out["session_offsets"] = torch.from_numpy(r.session_offsets.astype(np.int64))
+        out["session_values"] = torch.from_numpy(r.session_values.astype(np.float64))
+        return out
+
+    def session_stats(self, vals, sids, S, max_len):
+        import statistics
+        v, s_ = vals.numpy(), sids.numpy()
+        avg, med, pct = np.full(S, np.nan), np.full(S, np.nan), np.full(5 * S, np.nan)
+        for i in range(S):
+            x = list(v[s_ == i])
+            if x:
+                avg[i] = statistics.mean(x)
+                med[i] = statistics.median(x)
+                pct[5 * i:5 * i + 5] = [np.percentile(x, q) for q in (5, 25, 50, 75, 95)]
+        T = torch.from_numpy
+        return {"average": T(avg), "median": T(med), "percentiles": T(pct),
+                "ge100": torch.tensor([int(np.sum(np.bincount(s_, minlength=S) >= 100))])}
+
+    def series_tests(self, x):
+        import warnings
+        from scipy import stats
+        m = list(x.numpy())
+        rho = p = w = sp = float("nan")
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            if len(m) > 1:
+                r = stats.spearmanr(list(range(len(m))), m)
+                rho, p = float(r.statistic), float(r.pvalue)
+            if len(m) >= 3:
+                w, sp = (float(z) for z in stats.shapiro(m))
+        return rho, p, w, sp
+
+    def mean_median(self, x):
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            return float(np.mean(x.numpy())), float(np.median(x.numpy()))
+
+
+class OracleRQ4aShard:
+    """One rank's RQ4a on the CPU restatement, in fz_rq4a's output layout."""
+
+    def __init__(self, t, max_iter):
+        self.t, self.M = t, max_iter
+
+    def run(self):
+        from oracle import rq_oracle as orc
+        r = orc.rq4a(self.t)
+        P = len(self.t.projects)
+        c = np.zeros(12, np.int64)
+        c[0] = len(r.g1_total)
+        for g in range(4):
+            c[2 + g] = len(r.groups[f"group{g + 1}"])
+        c[6] = int(r.has_g4_transition)
+        c[9] = sum(1 for _, k in r.intro if k > 0)
+        member = np.zeros(P, np.int64)
+        for g in range(4):
+            member[r.groups[f"group{g + 1}"]] |= 1 << g
+        intro = np.full(P, -1, np.int64)
+        for p, k in r.intro:
+            intro[p] = k
+        steps = np.zeros((15, 2), np.int64)
+        for s_, (a, b) in r.g4_steps.items():
+            steps[s_ + 7] = (a, b)
+        out = {"counts": torch.from_numpy(c), "member": torch.from_numpy(member), "intro": torch.from_numpy(intro),
+               "g4_steps": torch.from_numpy(steps.reshape(-1)),
+               "g4_transition": torch.from_numpy(np.array(r.g4_transition, np.int64))}
+        for k in ("g1_total", "g1_det", "g2_total", "g2_det"):
+            a = np.zeros(self.M, np.int64)
+            a[:len(getattr(r, k))] = getattr(r, k)
+            out[k] = torch.from_numpy(a)
+        return out
+
+    def finish(self, tables, intro, steps, counts):
+        from oracle import rq_oracle as orc
+        M = int(counts[0])
+        t4 = [x.numpy()[:M] for x in tables]
+        st = steps.numpy().reshape(15, 2)
+        sd = {s_: tuple(st[s_ + 7]) for s_ in list(range(-7, 0)) + list(range(1, 8))}
+        iv = [int(k) for k in intro.numpy() if k >= 0]
+        after, istats, overall = orc.rq4a_finish(*t4, iv, sd)
+        rows = common.rq4a_rows(*t4)
+        counts[1] = len(rows)
+        sc = np.full(12, np.nan)
+        for key, n, m in (("g1", 7, 0), ("g2", 8, 2)):
+            counts[n] = 1 if after[key] is not None else 0
+            if after[key] is not None:
+                sc[m], sc[m + 1] = after[key]
+        if istats is not None:
+            sc[4:8] = istats
+        sc[8], sc[9] = overall
+        return sc
+
+
 def _worker(rank, world, port, case, errfile):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -152,6 +268,13 @@ def _check(rank, world, case):
     torch.distributed.all_reduce(any_rerun)
     # RQ3
     total3, cols3, st3 = par.rq3_sharded(OracleRQ3Shard(ts, rows), rank, world)
+    # RQ2 count
+    r2 = par.rq2_count_sharded(OracleRQ2CountShard(ts), rank, world, lo, hi)
+    # RQ4a
+    nF4 = np.bincount(ts.b_project[(ts.b_type == 0) & (ts.b_time < LIMIT_US)].astype(np.int64),
+                      minlength=len(t.projects))
+    r4 = par.rq4a_sharded(OracleRQ4aShard(ts, par.agree_max(int(nF4.max()) if len(nF4) else 1)), rank, world,
+                          lo, hi)
     if rank != 0:
         return
     g = orc.rq1(t)
@@ -177,6 +300,14 @@ def _check(rank, world, case):
         np.testing.assert_array_equal(cols3[k].numpy(), getattr(g3, k), err_msg=k)
     for k, v in st3.items():
         assert_same(v, getattr(g3, k), k)
+    from tse_amd.rq import compute
+    ours2 = compute.rq2_count_result(r2["proj"], r2["session_offsets"], r2["session_values"], r2["K"],
+                                     r2["average"], r2["median"], r2["percentiles"], r2["average"],
+                                     (r2["tests"][0], r2["tests"][1], r2["tests"][3]), r2["corr_mm"])
+    assert_same(ours2, orc.rq2_count(t), "rq2_count")
+    ours4 = compute.rq4a_result(r4["counts"], r4["scalars"], r4["member"], r4["tables"], r4["intro"], r4["g4_steps"],
+                                r4["g4_transition"])
+    assert_same(ours4, orc.rq4a(t), "rq4a")
 
 
 def _spawn(world, case, tmp_path):

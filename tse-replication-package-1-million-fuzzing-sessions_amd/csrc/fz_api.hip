@@ -12,12 +12,17 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_ext *ext, const fz_rq1_out *
 void rq1_finish(fz_ctx *c, int64_t threshold, const int64_t *iter_total, const int64_t *iter_det, int64_t M,
                 int64_t *counts, fz_describe *late);
 void eligibility_counts(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *counts);
-void rq2_count(fz_ctx *c, const fz_rq2_count_out *o);
+void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o);
+void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_ids, int64_t n, int64_t S,
+                       int64_t max_len, double *average, double *median, double *pcts, int64_t *n_ge100);
+void series_tests(fz_ctx *c, const double *x, int64_t n_cap, const int64_t *d_n, double *out);
 void rq2_add(fz_ctx *c, const fz_rq2_add_out *o);
 void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o);
 void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t NI, const int64_t *d_nd,
                const double *non_pct, int64_t NC, const int64_t *d_nn, fz_describe *describe, double *tests);
 void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o);
+void rq4a_finish(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int64_t *g1d, const int64_t *g2t,
+                 const int64_t *g2d, const int64_t *intro, const int64_t *steps, int64_t *counts, double *sc);
 void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o);
 }  // namespace fz
 
@@ -114,7 +119,32 @@ int fz_rq1_finish(fz_ctx *ctx, int64_t min_project_threshold, const int64_t *ite
 }
 
 int fz_rq2_count(fz_ctx *ctx, const fz_rq2_count_out *out) {
-    return guarded(ctx, [&] { fz::rq2_count(ctx, out); });
+    return guarded(ctx, [&] { fz::rq2_count(ctx, 0u, out); });
+}
+
+int fz_rq2_count_ex(fz_ctx *ctx, uint32_t flags, const fz_rq2_count_out *out) {
+    return guarded(ctx, [&] { fz::rq2_count(ctx, flags, out); });
+}
+
+int fz_rq2_session_stats(fz_ctx *ctx, const double *values, const int64_t *session_ids, int64_t n_values,
+                         int64_t n_sessions, int64_t max_session_len, double *average, double *median,
+                         double *percentiles, int64_t *n_ge100) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n_values >= 0 && n_sessions >= 0 && (n_values == 0 || (values && session_ids)) && n_ge100 &&
+                     (n_sessions == 0 || (average && median && percentiles)) && n_sessions < (int64_t(1) << 31),
+                 "fz_rq2_session_stats: bad arguments");
+        fz::rq2_session_stats(ctx, values, session_ids, n_values, n_sessions, max_session_len, average, median,
+                              percentiles, n_ge100);
+    });
+}
+
+int fz_series_tests(fz_ctx *ctx, const double *x, int64_t n, double *out) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(out && n >= 0 && (n == 0 || x), "fz_series_tests: bad arguments");
+        int64_t *d_n = ctx->arena.get<int64_t>(1);
+        fz::set_i64(ctx, d_n, &n, 1);
+        fz::series_tests(ctx, x, n > 0 ? n : 1, d_n, out);
+    });
 }
 
 int fz_rq2_add(fz_ctx *ctx, const fz_rq2_add_out *out) {
@@ -137,14 +167,25 @@ int fz_rq3_stats(fz_ctx *ctx, const double *det_pct, const int64_t *det_tot, int
                  "fz_rq3_stats: bad arguments");
         int64_t *d_n = ctx->arena.get<int64_t>(2);
         const int64_t h[2] = {n_det, n_non};
-        FZ_HIP(hipMemcpyAsync(d_n, h, sizeof(h), hipMemcpyHostToDevice, ctx->stream));
+        fz::set_i64(ctx, d_n, h, 2);
         fz::rq3_stats(ctx, det_pct, det_tot, n_det, d_n, non_pct, n_non, d_n + 1, describe, tests);
-        fz::sync(ctx);  // h lives on this stack frame
     });
 }
 
 int fz_rq4a(fz_ctx *ctx, const fz_rq4_groups *groups, const fz_rq4a_out *out) {
     return guarded(ctx, [&] { fz::rq4a(ctx, groups, out); });
+}
+
+int fz_rq4a_finish(fz_ctx *ctx, const int64_t *g1_total, const int64_t *g1_det, const int64_t *g2_total,
+                   const int64_t *g2_det, int64_t max_iter, const int64_t *intro, int64_t n_projects,
+                   const int64_t *g4_steps, int64_t *counts, double *scalars) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(max_iter >= 0 && n_projects >= 0 && counts && scalars && g4_steps &&
+                     (max_iter == 0 || (g1_total && g1_det && g2_total && g2_det)) && (n_projects == 0 || intro),
+                 "fz_rq4a_finish: bad arguments");
+        fz::rq4a_finish(ctx, max_iter, n_projects, g1_total, g1_det, g2_total, g2_det, intro, g4_steps, counts,
+                        scalars);
+    });
 }
 
 int fz_rq4b(fz_ctx *ctx, const fz_rq4_groups *groups, const fz_rq4b_out *out) {

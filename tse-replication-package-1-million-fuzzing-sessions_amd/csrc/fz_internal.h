@@ -245,5 +245,7 @@ inline unsigned grid_for(int64_t n, int per_block = kBlock, unsigned cap = 8192)
 }
 
 void sync(fz_ctx *c);
+// d[0..n) = v[0..n) (host values passed by value through a kernel argument; n <= 4)
+void set_i64(fz_ctx *c, int64_t *d, const int64_t *v, int n);
 
 }  // namespace fz

@@ -10,6 +10,20 @@ namespace fz {
 
 void sync(fz_ctx *c) { FZ_HIP(hipStreamSynchronize(c->stream)); }
 
+struct I64x4 {
+    int64_t v[4];
+};
+__global__ void k_set_i64(int64_t *d, I64x4 v, int n) {
+    if (threadIdx.x < n) d[threadIdx.x] = v.v[threadIdx.x];
+}
+void set_i64(fz_ctx *c, int64_t *d, const int64_t *v, int n) {
+    FZ_CHECK(n >= 1 && n <= 4, "set_i64: 1..4 values");
+    I64x4 a{};
+    for (int i = 0; i < n; ++i) a.v[i] = v[i];
+    k_set_i64<<<1, 64, 0, c->stream>>>(d, a, n);
+    FZ_LAUNCH_CHECK();
+}
+
 // ------------------------------------------------------------------------------ scan (int64)
 constexpr int kScanItems = 8;
 constexpr int kScanChunk = kBlock * kScanItems;  // 2048 elements per workgroup

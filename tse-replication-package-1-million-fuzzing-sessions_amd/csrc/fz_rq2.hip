@@ -32,7 +32,70 @@ struct NonZeroTotal {  // `if total != 0` (:300-303)
     __device__ bool operator()(int32_t r) const { return total[r] != 0; }
 };
 
-void rq2_count(fz_ctx *c, const fz_rq2_count_out *o) {
+// statistics.mean / median + np.percentile(5, 25, 50, 75, 95) of every session segment; sessions
+// with >= 100 values counted into *d_ge100 (which must be zero on entry)
+void session_stats(fz_ctx *c, const double *sv, const Segs &ses, const int32_t *sseg, double *average, double *median,
+                   double *pcts, int64_t *d_ge100) {
+    ChunkedSegs cs2 = chunked(c, ses);
+    SortedSegs ss2 = seg_sort_f64(c, sv, ses, sseg);
+    const int64_t *soffs = ses.offs;
+    per_seg(c, ses.S, [=] __device__(int64_t i) {
+        if (soffs[i + 1] - soffs[i] >= 100) atomic_add_i64(d_ge100, 1);
+    });
+    seg_mean(c, cs2, sv, average);
+    seg_median(c, ses, ss2.val, median);
+    const double q5[5] = {5.0, 25.0, 50.0, 75.0, 95.0};
+    seg_percentiles(c, ses, ss2.val, q5, 5, pcts);
+}
+
+// spearmanr(range(n), x) and shapiro(x) of x[0, *d_n) (n_cap >= *d_n) -> out = rho, p, W, p
+void series_tests(fz_ctx *c, const double *x, int64_t n_cap, const int64_t *d_n, double *out) {
+    Segs one{1, single_segment(c, d_n), n_cap};
+    ChunkedSegs cs3 = chunked(c, one);
+    int32_t *sg3 = segment_ids(c, one);
+    SortedSegs ss3 = seg_sort_f64(c, x, one, sg3);
+    TieRanks tr3 = seg_tie_ranks(c, cs3, sg3, ss3.val);
+    seg_spearman_index(c, cs3, ss3, tr3, out, out + 1);
+    seg_shapiro(c, cs3, x, ss3, out + 2, out + 3);
+}
+
+__global__ void k_session_keys(const int64_t *__restrict__ sid, int64_t n, uint64_t *__restrict__ keys,
+                               uint32_t *__restrict__ idx) {
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+        keys[i] = uint64_t(sid[i]);
+        idx[i] = uint32_t(i);
+    }
+}
+
+void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_ids, int64_t n, int64_t S,
+                       int64_t max_len, double *average, double *median, double *pcts, int64_t *n_ge100) {
+    hipStream_t st = c->stream;
+    FZ_HIP(hipMemsetAsync(n_ge100, 0, 8, st));
+    uint64_t *key = c->arena.get<uint64_t>(n);
+    uint32_t *idx = c->arena.get<uint32_t>(n);
+    if (n > 0) {
+        k_session_keys<<<grid_for(n), kBlock, 0, st>>>(session_ids, n, key, idx);
+        FZ_LAUNCH_CHECK();
+        radix_sort_pairs(c, key, idx, n, bits_for(uint64_t(S)));  // stable: input order kept per session
+    }
+    double *sv = c->arena.get<double>(n);
+    uint32_t *sid = c->arena.get<uint32_t>(n);
+    int64_t *d_n = c->arena.get<int64_t>(1);
+    int64_t *offs = c->arena.get<int64_t>(S + 1);
+    map_n(c, n > 0 ? n : 1, nullptr, [=] __device__(int64_t k) {
+        if (k == 0) *d_n = n;
+        if (k < n) {
+            sv[k] = values[idx[k]];
+            sid[k] = uint32_t(key[k]);
+        }
+    });
+    k_segment_offsets_dn<<<grid_for(S + 1, kBlock, 1u << 30), kBlock, 0, st>>>(sid, d_n, S, offs);
+    FZ_LAUNCH_CHECK();
+    Segs ses{S, offs, n, max_len};
+    session_stats(c, sv, ses, reinterpret_cast<const int32_t *>(sid), average, median, pcts, n_ge100);
+}
+
+void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     Store &s = c->store;
     FZ_CHECK(s.built, "fz_rq2_count: call fz_store_build first");
     FZ_CHECK(o && o->counts && o->scalars && o->eligible && o->raw_n && o->n_trend && o->sw_w && o->sw_p && o->corr &&
@@ -110,34 +173,24 @@ void rq2_count(fz_ctx *c, const fz_rq2_count_out *o) {
     });
     k_segment_offsets_dn<<<grid_for(M + 1, kBlock, 1u << 30), kBlock, 0, st>>>(sid, d_nt, M, o->session_offsets);
     FZ_LAUNCH_CHECK();
+    if (flags & FZ_RQ2C_SKIP_SESSION_STATS) return;
 
     // per-session statistics (sessions are non-increasing in size: >= 100 is a prefix)
     Segs ses{M, o->session_offsets, NC, P};  // a session holds at most one value per project
-    ChunkedSegs cs2 = chunked(c, ses);
-    const int32_t *sseg = reinterpret_cast<const int32_t *>(sid);
-    SortedSegs ss2 = seg_sort_f64(c, sv, ses, sseg);
-    const int64_t *soffs = o->session_offsets;
-    per_seg(c, M, [=] __device__(int64_t i) {
-        if (soffs[i + 1] - soffs[i] >= 100) atomic_add_i64(&counts[FZ_RQ2C_GE100], 1);
-    });
-    seg_mean(c, cs2, sv, o->average_trend);
-    seg_median(c, ses, ss2.val, o->median_trend);
-    const double q5[5] = {5.0, 25.0, 50.0, 75.0, 95.0};
-    seg_percentiles(c, ses, ss2.val, q5, 5, o->dist_percentiles);
+    session_stats(c, sv, ses, reinterpret_cast<const int32_t *>(sid), o->average_trend, o->median_trend,
+                  o->dist_percentiles, counts + FZ_RQ2C_GE100);
     FZ_HIP(hipMemcpyAsync(o->dist_mean, o->average_trend, size_t(M > 0 ? M : 1) * 8, hipMemcpyDeviceToDevice, st));
 
     // tests on the median trend (one segment of K values)
     double *sc = o->scalars;
     {
-        const int64_t *d_k = counts + FZ_RQ2C_GE100;
-        Segs one{1, single_segment(c, d_k), M};
-        ChunkedSegs cs3 = chunked(c, one);
-        int32_t *sg3 = segment_ids(c, one);
-        SortedSegs ss3 = seg_sort_f64(c, o->median_trend, one, sg3);
-        TieRanks tr3 = seg_tie_ranks(c, cs3, sg3, ss3.val);
-        seg_spearman_index(c, cs3, ss3, tr3, sc + FZ_RQ2C_SP_RHO, sc + FZ_RQ2C_SP_P);
-        double *w3 = c->arena.get<double>(1);
-        seg_shapiro(c, cs3, o->median_trend, ss3, w3, sc + FZ_RQ2C_SW_MEDIAN_P);
+        double *t4 = c->arena.get<double>(4);
+        series_tests(c, o->median_trend, M, counts + FZ_RQ2C_GE100, t4);
+        map_n(c, 1, nullptr, [=] __device__(int64_t) {
+            sc[FZ_RQ2C_SP_RHO] = t4[0];
+            sc[FZ_RQ2C_SP_P] = t4[1];
+            sc[FZ_RQ2C_SW_MEDIAN_P] = t4[3];
+        });
     }
     // mean / median of the valid (non-NaN) per-project correlations
     {

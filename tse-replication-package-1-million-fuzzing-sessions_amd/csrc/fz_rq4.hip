@@ -54,6 +54,9 @@ static void group_members(fz_ctx *c, const fz_rq4_groups *g, const uint8_t *elig
 }
 
 // ------------------------------------------------------------------------------------ RQ4a
+void rq4a_finish(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int64_t *g1d, const int64_t *g2t,
+                 const int64_t *g2d, const int64_t *intro, const int64_t *steps, int64_t *counts, double *sc);
+
 void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
     Store &s = c->store;
     FZ_CHECK(s.built, "fz_rq4a: call fz_store_build first");
@@ -123,8 +126,52 @@ void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
         if (member[p] & 2) atomic_add_i64(&g2d[k - 1], 1);
     });
 
+    // G4: introduction iteration and pre/post windows (:246-299, :350-412)
+    const int64_t *cus = g->corpus_us;
+    int64_t *intro = o->intro, *steps = o->g4_steps, *trans = o->g4_transition;
+    per_seg(c, P, [=] __device__(int64_t p) {
+        if (!(member[p] & 8) || cus[p] == FZ_TS_NULL) return;
+        const int64_t ct = cus[p];
+        const int64_t lo = fboffs[p], hi = fboffs[p + 1], nb = hi - lo;
+        const int64_t npre = lower_bound_i64(fbtime, lo, hi, ct) - lo;
+        intro[p] = npre;
+        if (npre > 0) atomic_add_i64(&counts[FZ_RQ4A_INTRO_POS], 1);
+        if (npre == 0) return;
+        const int64_t idx = npre - 1;
+        if (idx - (kWin - 1) < 0 || idx + kWin >= nb - 1) return;
+        counts[FZ_RQ4A_HAS_WINDOW] = 1;
+        const int64_t i0 = fioffs[p], i1 = fioffs[p + 1];
+        auto any = [&](int64_t a, int64_t b) {  // some issue T with a <= T < b
+            return lower_bound_i64(fitime, i0, i1, b) > lower_bound_i64(fitime, i0, i1, a);
+        };
+        bool pre = false, post = false;
+        for (int k = 1; k <= kWin; ++k) {
+            const bool d1 = any(fbtime[lo + idx - (k - 1)], fbtime[lo + idx - (k - 1) + 1]);
+            atomic_add_i64(&steps[2 * (kWin - k)], 1);
+            if (d1) atomic_add_i64(&steps[2 * (kWin - k) + 1], 1);
+            pre |= d1;
+            const bool d2 = any(fbtime[lo + idx + k], fbtime[lo + idx + k + 1]);
+            atomic_add_i64(&steps[2 * (kWin + k)], 1);
+            if (d2) atomic_add_i64(&steps[2 * (kWin + k) + 1], 1);
+            post |= d2;
+        }
+        atomic_add_i64(&trans[(pre && post) ? 0 : pre ? 1 : post ? 2 : 3], 1);
+    });
+    rq4a_finish(c, M, P, o->g1_total, o->g1_det, o->g2_total, o->g2_det, o->intro, o->g4_steps, counts, sc);
+}
+
+// Finishing of RQ4a from the per-iteration tables, the per-project introduction iterations and the
+// G4 step counts (all shard-additive): kept rows, rates, first rate < 5 and the
+// after-slices (:156-207, :698-747), introduction stats (:246-299) and pre/post rates (:412-510).
+void rq4a_finish(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int64_t *g1d, const int64_t *g2t,
+                 const int64_t *g2d, const int64_t *intro, const int64_t *steps, int64_t *counts, double *sc) {
+    const int64_t MM = M > 0 ? M : 1;
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        counts[FZ_RQ4A_ROWS] = 0;
+        counts[FZ_RQ4A_AFTER_G1] = 0;
+        counts[FZ_RQ4A_AFTER_G2] = 0;
+    });
     // rows with both totals >= 100 (a prefix), rates, first rate < 5, after-slices (:156-207, :698-747)
-    const int64_t *g1t = o->g1_total, *g2t = o->g2_total;
     double *rates = c->arena.get<double>(2 * MM);
     int64_t *first = c->arena.get<int64_t>(2);
     map_n(c, 1, nullptr, [=] __device__(int64_t) { first[0] = first[1] = INT64_MAX; });
@@ -158,37 +205,6 @@ void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
     describe_f64_dn(c, after, MM, nafter, dsc);
     describe_f64_dn(c, after + MM, MM, nafter + 1, dsc + 1);
 
-    // G4: introduction iteration and pre/post windows (:246-299, :350-412)
-    const int64_t *cus = g->corpus_us;
-    int64_t *intro = o->intro, *steps = o->g4_steps, *trans = o->g4_transition;
-    per_seg(c, P, [=] __device__(int64_t p) {
-        if (!(member[p] & 8) || cus[p] == FZ_TS_NULL) return;
-        const int64_t ct = cus[p];
-        const int64_t lo = fboffs[p], hi = fboffs[p + 1], nb = hi - lo;
-        const int64_t npre = lower_bound_i64(fbtime, lo, hi, ct) - lo;
-        intro[p] = npre;
-        if (npre > 0) atomic_add_i64(&counts[FZ_RQ4A_INTRO_POS], 1);
-        if (npre == 0) return;
-        const int64_t idx = npre - 1;
-        if (idx - (kWin - 1) < 0 || idx + kWin >= nb - 1) return;
-        counts[FZ_RQ4A_HAS_WINDOW] = 1;
-        const int64_t i0 = fioffs[p], i1 = fioffs[p + 1];
-        auto any = [&](int64_t a, int64_t b) {  // some issue T with a <= T < b
-            return lower_bound_i64(fitime, i0, i1, b) > lower_bound_i64(fitime, i0, i1, a);
-        };
-        bool pre = false, post = false;
-        for (int k = 1; k <= kWin; ++k) {
-            const bool d1 = any(fbtime[lo + idx - (k - 1)], fbtime[lo + idx - (k - 1) + 1]);
-            atomic_add_i64(&steps[2 * (kWin - k)], 1);
-            if (d1) atomic_add_i64(&steps[2 * (kWin - k) + 1], 1);
-            pre |= d1;
-            const bool d2 = any(fbtime[lo + idx + k], fbtime[lo + idx + k + 1]);
-            atomic_add_i64(&steps[2 * (kWin + k)], 1);
-            if (d2) atomic_add_i64(&steps[2 * (kWin + k) + 1], 1);
-            post |= d2;
-        }
-        atomic_add_i64(&trans[(pre && post) ? 0 : pre ? 1 : post ? 2 : 3], 1);
-    });
     // introduction-iteration stats over the positive ones (pandas Series mean/median/min/max)
     int64_t *pf = c->arena.get<int64_t>(P), *pp = c->arena.get<int64_t>(P), *d_np = c->arena.get<int64_t>(1);
     double *iv = c->arena.get<double>(P);

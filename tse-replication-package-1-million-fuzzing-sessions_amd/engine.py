@@ -68,6 +68,7 @@ class FzRq1Ext(C.Structure):
 FZ_RQ2C_NCOUNTS, FZ_RQ2C_NSCALARS = 8, 8
 RQ2C_ELIGIBLE, RQ2C_SESSIONS, RQ2C_GE100, RQ2C_VALUES = range(4)
 RQ2C_CORR_MEAN, RQ2C_CORR_MEDIAN, RQ2C_SP_RHO, RQ2C_SP_P, RQ2C_SW_MEDIAN_P = range(5)
+FZ_RQ2C_SKIP_SESSION_STATS = 1
 
 
 class FzRq2CountOut(C.Structure):
@@ -137,11 +138,15 @@ SIGNATURES = {
     "fz_rq1_ex": (C.c_int, [_P, _I64, C.POINTER(FzRq1Ext), C.POINTER(FzRq1Out)]),
     "fz_rq1_finish": (C.c_int, [_P, _I64, _P, _P, _I64, _P, _P]),
     "fz_rq2_count": (C.c_int, [_P, C.POINTER(FzRq2CountOut)]),
+    "fz_rq2_count_ex": (C.c_int, [_P, C.c_uint32, C.POINTER(FzRq2CountOut)]),
+    "fz_rq2_session_stats": (C.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P]),
+    "fz_series_tests": (C.c_int, [_P, _P, _I64, _P]),
     "fz_rq2_add": (C.c_int, [_P, C.POINTER(FzRq2AddOut)]),
     "fz_rq3": (C.c_int, [_P, C.POINTER(FzRq3Out)]),
     "fz_rq3_ex": (C.c_int, [_P, C.c_uint32, C.POINTER(FzRq3Out)]),
     "fz_rq3_stats": (C.c_int, [_P, _P, _P, _I64, _P, _I64, _P, _P]),
     "fz_rq4a": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.POINTER(FzRq4aOut)]),
+    "fz_rq4a_finish": (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P]),
     "fz_rq4b": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.POINTER(FzRq4bOut)]),
     "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),
     "fz_probe_end": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),

@@ -152,6 +152,26 @@ def all_gather_v(x):
     return [o[:k] for o, k in zip(all_gather(buf), sizes)]
 
 
+def all_to_all_v(x, send_counts):
+    """Variable all-to-all of a 1-D tensor: x holds the rows for rank 0, then rank 1, ...
+    (send_counts[d] rows each) -> the rows every rank sent here, in source-rank order."""
+    import torch
+    dist = _dist()
+    world = dist.get_world_size()
+    sc = torch.tensor([int(v) for v in send_counts], dtype=torch.int64, device=x.device)
+    rc = torch.cat(all_gather(sc)).reshape(world, world)[:, dist.get_rank()]
+    recv = [int(v) for v in rc.tolist()]
+    send = [int(v) for v in send_counts]
+    if _staged(x):
+        h = x.cpu()
+        out = torch.empty(sum(recv), dtype=x.dtype)
+        dist.all_to_all_single(out, h, recv, send)
+        return out.to(x.device)
+    out = torch.empty(sum(recv), dtype=x.dtype, device=x.device)
+    dist.all_to_all_single(out, x.contiguous(), recv, send)
+    return out
+
+
 def agree_max(v: int, device=None) -> int:
     """MAX over ranks of a host integer (e.g. the RQ1 iteration-axis length, agreed once per load
     so every rank's per-iteration buffers have the same shape)."""
@@ -239,6 +259,116 @@ def rq3_sharded(shard, rank: int, world: int):
     return total, out, st
 
 
+# ----------------------------------------------------------------------------------- RQ2 count
+RQ2C_PROJECT_COLS = ("eligible", "raw_n", "n_trend", "sw_w", "sw_p", "corr")
+
+
+def session_owners(sizes: np.ndarray, world: int) -> List[Tuple[int, int]]:
+    """Contiguous session-index ranges, one per rank, with about equal numbers of values (session
+    sizes are non-increasing, so equal index ranges would not balance)."""
+    M = len(sizes)
+    cum = np.concatenate([[0], np.cumsum(sizes)])
+    cuts = [0]
+    for r in range(1, world):
+        k = int(np.searchsorted(cum, cum[-1] * r / world, "left"))
+        cuts.append(min(max(k, cuts[-1]), M))
+    cuts.append(M)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_values: bool = True):
+    """Exact RQ2 count over project shards (rq2_coverage_count.py:244-483).
+    ``shard.run()`` -> per-project columns over the global project axis (RQ2C_PROJECT_COLS), the
+    local session-major trend values and session offsets; ``shard.session_stats(values, sids, S,
+    max_len)`` -> average / median / percentiles[S * 5] / ge100 of the sessions it owns;
+    ``shard.series_tests(x)`` -> (rho, p, W, p); ``shard.mean_median(x)`` -> (mean, median).
+    Exchange: per-project columns gathered (projects [lo, hi) of every rank), session sizes
+    all-reduced, values all-to-all'd to the owner of their session index, per-session results
+    gathered.  Returns a dict of host numpy arrays (every rank)."""
+    import torch
+    part = shard.run()
+    dev = part["session_values"].device
+    proj = {}
+    for k in RQ2C_PROJECT_COLS:
+        v = part[k][lo:hi]
+        v = v.to(torch.float64) if v.is_floating_point() else v.to(torch.int64)
+        proj[k] = torch.cat(all_gather_v(v)).cpu().numpy() if world > 1 else v.cpu().numpy()
+    offs = part["session_offsets"]
+    m_loc = offs.numel() - 1
+    loc_sizes = (offs[1:] - offs[:-1]).to(torch.int64)
+    M = agree_max(m_loc, dev) if world > 1 else m_loc
+    sizes = torch.zeros(M, dtype=torch.int64, device=dev)
+    sizes[:m_loc] = loc_sizes
+    if world > 1:
+        all_reduce(sizes)
+    sizes_h = sizes.cpu().numpy()
+    own = session_owners(sizes_h, world)
+    nv = int(offs[-1].item())
+    vals = part["session_values"][:nv]
+    sids = torch.repeat_interleave(torch.arange(m_loc, dtype=torch.int64, device=dev), loc_sizes)
+    offs_h = offs.cpu().numpy()
+    send = [int(offs_h[min(b, m_loc)] - offs_h[min(a, m_loc)]) for a, b in own]
+    if world > 1:
+        vals = all_to_all_v(vals, send)
+        sids = all_to_all_v(sids, send)
+    a, b = own[rank]
+    st = shard.session_stats(vals, sids - a, b - a, len(proj["eligible"]))
+    res = {}
+    for k in ("average", "median", "percentiles"):
+        v = st[k][:(b - a) * (5 if k == "percentiles" else 1)]
+        res[k] = torch.cat(all_gather_v(v)).cpu().numpy() if world > 1 else v.cpu().numpy()
+    K = int(np.sum(sizes_h >= 100))
+    tests = shard.series_tests(torch.from_numpy(res["median"][:K].copy()).to(dev))
+    elig = proj["eligible"] != 0
+    corr = proj["corr"][elig][proj["raw_n"][elig] > 0]
+    valid = corr[~np.isnan(corr)]
+    corr_mm = shard.mean_median(torch.from_numpy(valid.copy()).to(dev))
+    out = {"proj": proj, "session_offsets": np.concatenate([[0], np.cumsum(sizes_h)]).astype(np.int64), "K": K,
+           "average": res["average"], "median": res["median"], "percentiles": res["percentiles"],
+           "tests": tests, "corr_mm": corr_mm}
+    if gather_values:  # coverage_by_session_index.csv: every value, session-major, project order
+        if world > 1:
+            gv = torch.cat(all_gather_v(vals)).cpu().numpy()
+            gs = torch.cat(all_gather_v(sids)).cpu().numpy()
+        else:
+            gv, gs = vals.cpu().numpy(), sids.cpu().numpy()
+        out["session_values"] = gv[np.argsort(gs, kind="stable")]
+    return out
+
+
+# ----------------------------------------------------------------------------------------- RQ4a
+RQ4A_MAX_ITER, RQ4A_HAS_WINDOW = 0, 6
+RQ4A_TABLES = ("g1_total", "g1_det", "g2_total", "g2_det")
+
+
+def rq4a_sharded(shard, rank: int, world: int, lo: int, hi: int):
+    """Exact RQ4a over project shards (rq4a_bug.py:653-884).  ``shard.run()`` -> counts, the four
+    per-iteration tables (length agreed across ranks), member / intro over the global project axis,
+    g4_steps[30], g4_transition[4]; ``shard.finish(tables, intro, steps, counts)`` -> scalars (and
+    the recomputed counters, in place).  Group sizes, counters and step/transition counts add over
+    disjoint projects; the iteration axis is a MAX; HAS_WINDOW is an OR."""
+    import torch
+    part = shard.run()
+    counts = part["counts"].clone()
+    tables = [part[k].clone() for k in RQ4A_TABLES]
+    steps, trans = part["g4_steps"].clone(), part["g4_transition"].clone()
+    member = part["member"][lo:hi].to(torch.int64)
+    intro = part["intro"][lo:hi].clone()
+    if world > 1:
+        mx = counts[[RQ4A_MAX_ITER, RQ4A_HAS_WINDOW]].clone()
+        all_reduce(counts)
+        all_reduce(mx, _dist().ReduceOp.MAX)
+        counts[RQ4A_MAX_ITER], counts[RQ4A_HAS_WINDOW] = mx[0], mx[1]
+        for x in tables + [steps, trans]:
+            all_reduce(x)
+        member = torch.cat(all_gather_v(member))
+        intro = torch.cat(all_gather_v(intro))
+    sc = shard.finish(tables, intro, steps, counts)
+    return {"counts": counts.cpu().numpy(), "scalars": np.asarray(sc), "member": member.cpu().numpy(),
+            "tables": [x.cpu().numpy()[:int(counts[RQ4A_MAX_ITER])] for x in tables], "intro": intro.cpu().numpy(),
+            "g4_steps": steps.cpu().numpy(), "g4_transition": trans.cpu().numpy()}
+
+
 # ------------------------------------------------------------------------------------ row gathers
 def gather_rows(cols: dict, world: int) -> dict:
     """Concatenate per-rank row columns in rank (= project) order (RQ2 change rows, RQ1 raw rows)."""
@@ -281,6 +411,78 @@ class GpuRQ1Shard:
         E._check(eng.lib, eng.lib.fz_rq1_finish(eng.ctx, self.threshold, C.c_void_p(it.data_ptr()),
                                                 C.c_void_p(idt.data_ptr()), it.numel(),
                                                 C.c_void_p(counts.data_ptr()), C.c_void_p(self.bufs.late.data_ptr())))
+
+
+class GpuRQ2CountShard:
+    """RQ2 count of one rank on its engine (fz_rq2_count_ex, fz_rq2_session_stats, fz_series_tests)."""
+
+    def __init__(self, eng):
+        import ctypes as C
+        from . import engine as E
+        from .rq import compute
+        self.E, self.C, self.eng = E, C, eng
+        self.bufs = compute.rq2_count_buffers(eng)
+
+    def run(self):
+        E, C, eng, b = self.E, self.C, self.eng, self.bufs
+        E._check(eng.lib, eng.lib.fz_rq2_count_ex(eng.ctx, E.FZ_RQ2C_SKIP_SESSION_STATS, C.byref(b.out)))
+        ns = int(b.counts[E.RQ2C_SESSIONS].item())
+        out = {k: getattr(b, k) for k in RQ2C_PROJECT_COLS}
+        out["session_offsets"] = b.session_offsets[:ns + 1]
+        out["session_values"] = b.session_values
+        return out
+
+    def session_stats(self, vals, sids, S, max_len):
+        E, C, eng = self.E, self.C, self.eng
+        torch = eng.torch
+        avg = torch.empty(max(S, 1), dtype=torch.float64, device=eng.dev)
+        med = torch.empty_like(avg)
+        pct = torch.empty(max(5 * S, 1), dtype=torch.float64, device=eng.dev)
+        ge = torch.zeros(1, dtype=torch.int64, device=eng.dev)
+        vals, sids = vals.contiguous(), sids.contiguous()
+        P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+        E._check(eng.lib, eng.lib.fz_rq2_session_stats(eng.ctx, P(vals), P(sids), vals.numel(), S, max_len, P(avg),
+                                                       P(med), P(pct), P(ge)))
+        return {"average": avg, "median": med, "percentiles": pct, "ge100": ge}
+
+    def series_tests(self, x):
+        E, C, eng = self.E, self.C, self.eng
+        out = eng.torch.empty(4, dtype=eng.torch.float64, device=eng.dev)
+        x = x.contiguous()
+        E._check(eng.lib, eng.lib.fz_series_tests(eng.ctx, C.c_void_p(x.data_ptr()) if x.numel() else None,
+                                                  x.numel(), C.c_void_p(out.data_ptr())))
+        return tuple(float(v) for v in out.cpu().tolist())
+
+    def mean_median(self, x):
+        if x.numel() == 0:
+            return float("nan"), float("nan")
+        d = self.eng.describe(x.contiguous())
+        return float(d.mean), float(d.median)
+
+
+class GpuRQ4aShard:
+    """RQ4a of one rank on its engine (fz_rq4a / fz_rq4a_finish)."""
+
+    def __init__(self, eng, max_iter: int):
+        import ctypes as C
+        from . import engine as E
+        from .rq import compute
+        self.E, self.C, self.eng = E, C, eng
+        self.bufs = compute.rq4a_buffers(eng, max_iter=max_iter)
+
+    def run(self):
+        E, C, eng, b = self.E, self.C, self.eng, self.bufs
+        E._check(eng.lib, eng.lib.fz_rq4a(eng.ctx, C.byref(eng.groups), C.byref(b.out)))
+        return {k: getattr(b, k) for k in ("counts", "member", "intro", "g4_steps", "g4_transition") + RQ4A_TABLES}
+
+    def finish(self, tables, intro, steps, counts):
+        E, C, eng, b = self.E, self.C, self.eng, self.bufs
+        P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        tables = [x.contiguous() for x in tables]
+        intro = intro.contiguous()
+        E._check(eng.lib, eng.lib.fz_rq4a_finish(eng.ctx, *[P(x) for x in tables], tables[0].numel(), P(intro),
+                                                 intro.numel(), P(steps), P(counts), P(b.scalars)))
+        return b.scalars.cpu().numpy()
 
 
 class GpuRQ3Shard:

@@ -120,20 +120,30 @@ def rq2_count_collect(eng: E.Engine, b: OutBuffers) -> RQ2CountResult:
     P = eng.tables.fz.n_projects
     cnt = b.host("counts")
     sc = b.host("scalars")
-    elig = np.nonzero(b.host("eligible", P))[0]
-    raw_n = b.host("raw_n", P)[elig]
     ns, K, nv = int(cnt[E.RQ2C_SESSIONS]), int(cnt[E.RQ2C_GE100]), int(cnt[E.RQ2C_VALUES])
-    corr = b.host("corr", P)[elig][raw_n > 0]
-    pct = b.host("dist_percentiles", 5 * K).reshape(K, 5).T.copy() if K else np.zeros((5, 0))
+    return rq2_count_result(
+        {k: b.host(k, P) for k in ("eligible", "raw_n", "n_trend", "sw_w", "sw_p", "corr")},
+        b.host("session_offsets", ns + 1), b.host("session_values", nv), K, b.host("average_trend", K),
+        b.host("median_trend", K), b.host("dist_percentiles", 5 * K), b.host("dist_mean", K),
+        (float(sc[E.RQ2C_SP_RHO]), float(sc[E.RQ2C_SP_P]), float(sc[E.RQ2C_SW_MEDIAN_P])),
+        (float(sc[E.RQ2C_CORR_MEAN]), float(sc[E.RQ2C_CORR_MEDIAN])))
+
+
+def rq2_count_result(proj, session_offsets, session_values, K, average, median, pct_flat, dist_mean, tests,
+                     corr_mm) -> RQ2CountResult:
+    """RQ2CountResult from per-project columns (full project axis), the session-major values and the
+    per-session / median-trend statistics (host copies; also the sharded recombination)."""
+    elig = np.nonzero(np.asarray(proj["eligible"]))[0]
+    raw_n = np.asarray(proj["raw_n"])[elig]
+    corr = np.asarray(proj["corr"])[elig][raw_n > 0]
+    pct = np.asarray(pct_flat)[:5 * K].reshape(K, 5).T.copy() if K else np.zeros((5, 0))
     return RQ2CountResult(
-        eligible=elig, raw_n=raw_n, n_trend=b.host("n_trend", P)[elig], sw_w=b.host("sw_w", P)[elig],
-        sw_p=b.host("sw_p", P)[elig], corr=corr, session_offsets=b.host("session_offsets", ns + 1),
-        session_values=b.host("session_values", nv), corr_mean=float(sc[E.RQ2C_CORR_MEAN]),
-        corr_median=float(sc[E.RQ2C_CORR_MEDIAN]), ge100=np.arange(K, dtype=np.int64),
-        average_trend=b.host("average_trend", K), median_trend=b.host("median_trend", K),
-        spearman_median=(float(sc[E.RQ2C_SP_RHO]), float(sc[E.RQ2C_SP_P])) if K > 1 else None,
-        shapiro_median_p=float(sc[E.RQ2C_SW_MEDIAN_P]) if K >= 3 else None,
-        dist_percentiles=pct, dist_mean=b.host("dist_mean", K))
+        eligible=elig, raw_n=raw_n, n_trend=np.asarray(proj["n_trend"])[elig], sw_w=np.asarray(proj["sw_w"])[elig],
+        sw_p=np.asarray(proj["sw_p"])[elig], corr=corr, session_offsets=np.asarray(session_offsets),
+        session_values=np.asarray(session_values), corr_mean=float(corr_mm[0]), corr_median=float(corr_mm[1]),
+        ge100=np.arange(K, dtype=np.int64), average_trend=np.asarray(average)[:K], median_trend=np.asarray(median)[:K],
+        spearman_median=(float(tests[0]), float(tests[1])) if K > 1 else None,
+        shapiro_median_p=float(tests[2]) if K >= 3 else None, dist_percentiles=pct, dist_mean=np.asarray(dist_mean)[:K])
 
 
 def rq2_count(eng: E.Engine) -> RQ2CountResult:
@@ -236,10 +246,10 @@ def _groups(member, P):
 
 
 # ----------------------------------------------------------------------------------------- RQ4a
-def rq4a_buffers(eng: E.Engine) -> OutBuffers:
+def rq4a_buffers(eng: E.Engine, max_iter: int = 0) -> OutBuffers:
     torch = eng.torch
     fz, st = eng.tables.fz, eng.stats
-    P, M = fz.n_projects, max(int(st.max_fuzz_per_project), 1)
+    P, M = fz.n_projects, max(int(st.max_fuzz_per_project), int(max_iter), 1)
     f64, i64, u8 = torch.float64, torch.int64, torch.uint8
     return OutBuffers(eng, E.FzRq4aOut, [
         ("counts", E.FZ_RQ4A_NCOUNTS, i64), ("scalars", E.FZ_RQ4A_NSCALARS, f64), ("eligible", P, u8),
@@ -253,23 +263,29 @@ def rq4a_launch(eng: E.Engine, b: OutBuffers):
 
 def rq4a_collect(eng: E.Engine, b: OutBuffers) -> RQ4aResult:
     P = eng.tables.fz.n_projects
-    cnt, sc = b.host("counts"), b.host("scalars")
-    mx = int(cnt[E.RQ4A_MAX_ITER])
-    groups = _groups(b.host("member"), P)
-    intro_a = b.host("intro", P)
-    steps = b.host("g4_steps").reshape(15, 2)
+    mx = int(b.host("counts")[E.RQ4A_MAX_ITER])
+    return rq4a_result(b.host("counts"), b.host("scalars"), b.host("member", P),
+                       [b.host(k, mx) for k in ("g1_total", "g1_det", "g2_total", "g2_det")], b.host("intro", P),
+                       b.host("g4_steps"), b.host("g4_transition"))
+
+
+def rq4a_result(cnt, sc, member, tables, intro_a, steps_flat, transition) -> RQ4aResult:
+    """RQ4aResult from fz_rq4a's outputs (host copies; also the sharded recombination)."""
+    P = len(member)
+    groups = _groups(np.asarray(member), P)
+    steps = np.asarray(steps_flat).reshape(15, 2)
     after = {}
     for key, n, med, iqr in (("g1", E.RQ4A_AFTER_G1, E.RQ4A_AFTER_G1_MEDIAN, E.RQ4A_AFTER_G1_IQR),
                              ("g2", E.RQ4A_AFTER_G2, E.RQ4A_AFTER_G2_MEDIAN, E.RQ4A_AFTER_G2_IQR)):
         after[key] = (float(sc[med]), float(sc[iqr])) if cnt[n] > 0 else None
+    g1t, g1d, g2t, g2d = (np.asarray(x) for x in tables)
     return RQ4aResult(
-        groups=groups, g1_total=b.host("g1_total", mx), g1_det=b.host("g1_det", mx),
-        g2_total=b.host("g2_total", mx), g2_det=b.host("g2_det", mx), after=after,
+        groups=groups, g1_total=g1t, g1_det=g1d, g2_total=g2t, g2_det=g2d, after=after,
         intro=[(p, int(intro_a[p])) for p in groups["group4"] if intro_a[p] >= 0],
         intro_stats=((float(sc[E.RQ4A_INTRO_MEAN]), float(sc[E.RQ4A_INTRO_MEDIAN]), int(sc[E.RQ4A_INTRO_MIN]),
                       int(sc[E.RQ4A_INTRO_MAX])) if cnt[E.RQ4A_INTRO_POS] > 0 else None),
         g4_steps={s: (int(steps[s + 7, 0]), int(steps[s + 7, 1])) for s in list(range(-7, 0)) + list(range(1, 8))},
-        g4_transition=tuple(int(x) for x in b.host("g4_transition")),
+        g4_transition=tuple(int(x) for x in transition),
         g4_overall=(float(sc[E.RQ4A_PRE_RATE]), float(sc[E.RQ4A_POST_RATE])), n_g4_analyzed=int(steps[6, 0]),
         has_g4_transition=bool(cnt[E.RQ4A_HAS_WINDOW]))
 
