@@ -91,6 +91,7 @@ def main():
         rq3_shard = par.GpuRQ3Shard(eng)
         rq2c_shard = par.GpuRQ2CountShard(eng)
         rq4a_shard = par.GpuRQ4aShard(eng, M)
+        rq4b_shard = par.GpuRQ4bShard(eng)
         own = (rank * len(t.projects) // world, (rank + 1) * len(t.projects) // world)  # weak_shard ids
     rq1_bufs = compute.RQ1Buffers(eng)
     bufs = {"rq2_count": compute.rq2_count_buffers(eng), "rq2_add": compute.rq2_add_buffers(eng),
@@ -117,9 +118,10 @@ def main():
             par.rq2_count_sharded(rq2c_shard, rank, world, *own, gather_values=False)
         if "rq4a" in stages:
             par.rq4a_sharded(rq4a_shard, rank, world, *own)
-        for name in ("rq2_add", "rq4b"):
-            if name in stages:
-                launch[name](eng, bufs[name])
+        if "rq4b" in stages:
+            par.rq4b_sharded(rq4b_shard, rank, world)
+        if "rq2_add" in stages:
+            launch["rq2_add"](eng, bufs["rq2_add"])
         if "rq2_add" in stages:
             b = bufs["rq2_add"]
             n_add = int(b.counts[E.RQ2A_ROWS].item())
@@ -199,7 +201,7 @@ def pmc_traffic(probe, config):
     *_pmc_traffic.json, written by scripts/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE
     runs of this bench with the gfx950 FETCH_SIZE correction), or None."""
     import glob
-    kern = {"radix_scatter": "k_radix_scatter"}.get(probe, probe)
+    kern = {"radix_scatter": "k_onesweep"}.get(probe, probe)  # the probe name of the radix pass kernel
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
         try:
             d = json.load(open(path))

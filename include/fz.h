@@ -364,9 +364,34 @@ typedef struct fz_rq4b_out {
     double *pre_median, *post_median; /* [7]                                              :1061-1085 */
     double *init_g2, *init_g1;   /* [n_projects] first coverage per project (sorted ids)   :221-246 */
     double *tests;               /* [FZ_RQ4B_NTESTS] MWU p, Cliff delta, BM, Levene        :248-313 */
+    /* optional (may be NULL): what a shard contributes to the cross-shard recombination */
+    double *trend_values;        /* [n_cov] G1/G2 full coverage series, project-major (date order) */
+    int64_t *trend_offsets;      /* [n_projects + 1] per-project [start, end) into trend_values     */
+    int64_t *delta_order;        /* [n_projects] CSV row (index into groups->order) of each column  */
 } fz_rq4b_out;
 
 int fz_rq4b(fz_ctx *ctx, const fz_rq4_groups *groups, const fz_rq4b_out *out);
+
+/* Project-sharded RQ4b.  A shard runs fz_rq4b_ex with FZ_RQ4B_SKIP_SESSION_STATS
+ * (per-project outputs, trend series, delta columns, initial values; no per-session, delta-median or
+ * initial-coverage statistics); the G1/G2 values are exchanged by session index and the owner of a
+ * session range runs fz_rq4b_session_stats; the initial-coverage samples are gathered for
+ * fz_two_sample_tests. */
+#define FZ_RQ4B_SKIP_SESSION_STATS 1u
+int fz_rq4b_ex(fz_ctx *ctx, const fz_rq4_groups *groups, uint32_t flags, const fz_rq4b_out *out);
+
+/* Per-session G2 (group 0) vs G1 (group 1) statistics (:910-1015) of n_values (session id, group,
+ * value) triples, ids in [0, n_sessions): c2 / c1 counts, g2_q / g1_q [s * 3 + j] np.percentile
+ * 25/50/75 (NaN if empty), p_bm brunnermunzel p (NaN unless both sides >= 5).  max_session_len: host
+ * bound of one session's size per group (e.g. the number of projects), 0 if unknown. */
+int fz_rq4b_session_stats(fz_ctx *ctx, const double *values, const int64_t *session_ids, const uint8_t *groups,
+                          int64_t n_values, int64_t n_sessions, int64_t max_session_len, int64_t *c2, int64_t *c1,
+                          double *g2_q, double *g1_q, double *p_bm);
+
+/* Two-sample tests of rq4b's initial coverage (:248-313) on device samples x (G2) and y (G1):
+ * out[FZ_RQ4B_MWU_P .. FZ_RQ4B_LEVENE_P] = mannwhitneyu two-sided p, Cliff's delta from
+ * mannwhitneyu(greater) U1, brunnermunzel statistic / p, levene W / p. */
+int fz_two_sample_tests(fz_ctx *ctx, const double *x, int64_t nx, const double *y, int64_t ny, double *out);
 
 /* ---- per-kernel probe (bench.py roofline) ------------------------------------------------ */
 /* Start timing every launch of the named kernel (e.g. "radix_scatter", "elig_hist") with HIP

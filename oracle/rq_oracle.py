@@ -496,12 +496,95 @@ def rq4a_finish(g1t, g1d, g2t, g2d, intro_values, steps, N=7):
 
 
 # --------------------------------------------------------------------------------------- RQ4b
+def rq4b_full_series(t: Tables, P: int):
+    """get_full_coverage_trend (rq4b:315-326): coverage > 0 AND date < LIMIT, per project by date."""
+    return _Seg(t.c_project, t.c_date, t.c_coverage_valid & (t.c_coverage > 0) & (t.c_date < LIMIT_US), P)
+
+
+def rq4b_session_stats(s2, s1):
+    """Per-session counts, quartiles and Brunner-Munzel p of G2 (s2[i]) vs G1 (s1[i]) (:910-1015)."""
+    ms = len(s2)
+    c2 = np.array([len(s2[i]) for i in range(ms)], np.int64)
+    c1 = np.array([len(s1[i]) for i in range(ms)], np.int64)
+    q2 = np.full((ms, 3), np.nan)
+    q1 = np.full((ms, 3), np.nan)
+    pb = np.full(ms, np.nan)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for i in range(ms):
+            a, b = s2[i], s1[i]
+            if a:
+                q2[i] = np.percentile(a, [25, 50, 75])
+            if b:
+                q1[i] = np.percentile(b, [25, 50, 75])
+            if len(a) >= 5 and len(b) >= 5:
+                try:
+                    pb[i] = stats.brunnermunzel(a, b, alternative="two-sided")[1]
+                except Exception:
+                    pass
+    return c2, c1, q2, q1, pb
+
+
+def rq4b_last_and_spearman6(c2, c1, q2, q1):
+    """:849-860 (last session with both groups >= 100) and :879-899 (Spearman of the quartiles)."""
+    last = -1
+    for i in range(len(c2)):
+        if c2[i] >= 100 and c1[i] >= 100:
+            last = i
+    sp6 = common.rq4b_spearman6(q2[:last + 1], q1[:last + 1], lambda x, y: stats.spearmanr(x, y)) \
+        if last >= 0 else None
+    return last, sp6
+
+
+def rq4b_deltas(t: Tables, elig, groups, corpus_us):
+    """get_coverage_deltas (:725-797) for G3 u G4 in CSV order -> (projects, pre[7], post[7])."""
+    P = len(t.projects)
+    pos_all = _Seg(t.c_project, t.c_date, t.c_coverage_valid & (t.c_coverage > 0), P)
+    pre = [[] for _ in range(7)]
+    post = [[] for _ in range(7)]
+    projs = []
+    g34 = set(groups["group3"]) | set(groups["group4"])
+    for p in common.corpus_order(t, elig):
+        if p not in g34 or p not in corpus_us:
+            continue
+        cd = (corpus_us[p] // US_PER_DAY) * US_PER_DAY
+        k = pos_all.keys(p)
+        r = pos_all.rows(p)
+        j = int(np.searchsorted(k, cd, "left"))
+        pre_v = t.c_coverage[r[max(0, j - 7):j]][::-1]
+        post_v = t.c_coverage[r[j:j + 7]]
+        if len(pre_v) < 7 or len(post_v) < 7:
+            continue
+        projs.append(p)
+        for i in range(7):
+            pre[i].append(float(pre_v[i]))
+            post[i].append(float(post_v[i]))
+    return projs, [np.array(x) for x in pre], [np.array(x) for x in post]
+
+
+def rq4b_init_tests(a, b):
+    """mannwhitneyu / Cliff's delta / brunnermunzel / levene of the initial coverage (:221-313)."""
+    mwu_p = cliff = bm = lv = None
+    if len(a) and len(b):
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            _, mwu_p = stats.mannwhitneyu(list(a), list(b), alternative="two-sided")
+            u1, _ = stats.mannwhitneyu(list(a), list(b), alternative="greater")
+            cliff = float((2 * u1) / (len(a) * len(b)) - 1)
+            s_, p_ = stats.brunnermunzel(list(a), list(b), alternative="two-sided")
+            bm = (float(s_), float(p_))
+            s_, p_ = stats.levene(list(a), list(b))
+            lv = (float(s_), float(p_))
+        mwu_p = float(mwu_p)
+    return mwu_p, cliff, bm, lv
+
+
 def rq4b(t: Tables) -> RQ4bResult:
     """rq4b_coverage.py:1209-1261 (+ :183-313, :725-1015, :1061-1085)."""
     P = len(t.projects)
     elig = eligible_projects(t)
     groups, corpus_us = common.corpus_groups(t, elig, add_missing_to_g1=False)
-    full = _Seg(t.c_project, t.c_date, t.c_coverage_valid & (t.c_coverage > 0) & (t.c_date < LIMIT_US), P)
+    full = rq4b_full_series(t, P)
     sess = {}
     for g in ("group2", "group1"):                                   # :914-936
         ss = [[]]
@@ -516,76 +599,20 @@ def rq4b(t: Tables) -> RQ4bResult:
     for g in sess:
         if len(sess[g]) < ms:
             sess[g].extend([[] for _ in range(ms - len(sess[g]))])
-    c2 = np.array([len(sess["group2"][i]) for i in range(ms)], np.int64)
-    c1 = np.array([len(sess["group1"][i]) for i in range(ms)], np.int64)
-    q2 = np.full((ms, 3), np.nan)
-    q1 = np.full((ms, 3), np.nan)
-    pb = np.full(ms, np.nan)
-    with warnings.catch_warnings():
-        warnings.simplefilter("ignore")
-        for i in range(ms):
-            a, b = sess["group2"][i], sess["group1"][i]
-            if a:
-                q2[i] = np.percentile(a, [25, 50, 75])
-            if b:
-                q1[i] = np.percentile(b, [25, 50, 75])
-            if len(a) >= 5 and len(b) >= 5:
-                try:
-                    pb[i] = stats.brunnermunzel(a, b, alternative="two-sided")[1]
-                except Exception:
-                    pass
-    last = -1
-    for i in range(ms):
-        if c2[i] >= 100 and c1[i] >= 100:
-            last = i
-    sp6 = common.rq4b_spearman6(q2[:last + 1], q1[:last + 1], lambda x, y: stats.spearmanr(x, y)) \
-        if last >= 0 else None
-    # deltas (:725-797)
-    pos_all = _Seg(t.c_project, t.c_date, t.c_coverage_valid & (t.c_coverage > 0), P)
-    pre = [[] for _ in range(7)]
-    post = [[] for _ in range(7)]
-    nproj = 0
-    g34 = set(groups["group3"]) | set(groups["group4"])
-    for p in common.corpus_order(t, elig):
-        if p not in g34 or p not in corpus_us:
-            continue
-        cd = (corpus_us[p] // US_PER_DAY) * US_PER_DAY
-        k = pos_all.keys(p)
-        r = pos_all.rows(p)
-        j = int(np.searchsorted(k, cd, "left"))
-        pre_v = t.c_coverage[r[max(0, j - 7):j]][::-1]
-        post_v = t.c_coverage[r[j:j + 7]]
-        if len(pre_v) < 7 or len(post_v) < 7:
-            continue
-        nproj += 1
-        for i in range(7):
-            pre[i].append(float(pre_v[i]))
-            post[i].append(float(post_v[i]))
-    pre = [np.array(x) for x in pre]
-    post = [np.array(x) for x in post]
+    c2, c1, q2, q1, pb = rq4b_session_stats(sess["group2"][:ms], sess["group1"][:ms])
+    last, sp6 = rq4b_last_and_spearman6(c2, c1, q2, q1)
+    _, pre, post = rq4b_deltas(t, elig, groups, corpus_us)
     pre_med = [float(np.median(x)) if len(x) else np.nan for x in pre]
     post_med = [float(np.median(x)) if len(x) else np.nan for x in post]
-    # initial coverage (:221-313)
     init = {}
     for g in ("group2", "group1"):
         init[g] = np.array([t.c_coverage[full.rows(p)[0]] for p in sorted(groups[g]) if len(full.rows(p))],
                            np.float64)
     a, b = init["group2"], init["group1"]
-    mwu_p = cliff = bm = lv = None
-    if len(a) and len(b):
-        with warnings.catch_warnings():
-            warnings.simplefilter("ignore")
-            _, mwu_p = stats.mannwhitneyu(list(a), list(b), alternative="two-sided")
-            u1, _ = stats.mannwhitneyu(list(a), list(b), alternative="greater")
-            cliff = float((2 * u1) / (len(a) * len(b)) - 1)
-            s_, p_ = stats.brunnermunzel(list(a), list(b), alternative="two-sided")
-            bm = (float(s_), float(p_))
-            s_, p_ = stats.levene(list(a), list(b))
-            lv = (float(s_), float(p_))
-        mwu_p = float(mwu_p)
+    mwu_p, cliff, bm, lv = rq4b_init_tests(a, b)
     gc = tuple(len(groups[g]) for g in ("group1", "group2", "group3", "group4"))
     return RQ4bResult(group_counts=gc, n_sessions=ms, c2=c2, c1=c1, g2_q=q2, g1_q=q1, p_bm=pb,
-                      last_valid_idx=last, spearman6=sp6, n_delta_projects=nproj, pre_cov=pre, post_cov=post,
+                      last_valid_idx=last, spearman6=sp6, n_delta_projects=len(pre[0]), pre_cov=pre, post_cov=post,
                       pre_median=pre_med, post_median=post_med, n_g2=len(groups["group2"]),
                       n_g1=len(groups["group1"]), init_g2=a, init_g1=b, mwu_p=mwu_p, cliff=cliff, bm=bm,
                       levene=lv)

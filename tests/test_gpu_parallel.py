@@ -69,6 +69,15 @@ class _RQ4aView(_HostView):
         return sc
 
 
+class _RQ4bView(_RQ2View):
+    def session_stats(self, vals, sids, grp, S, max_len):
+        out = self.s.session_stats(vals.to(self.dev), sids.to(self.dev), grp.to(self.dev), S, max_len)
+        return {k: v.cpu() for k, v in out.items()}
+
+    def two_sample(self, x, y):
+        return self.s.two_sample(x.to(self.dev), y.to(self.dev))
+
+
 def _worker(rank, world, port, case, errfile):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -108,6 +117,7 @@ def _check(rank, world, case):
     total3, cols3, st3 = par.rq3_sharded(_RQ3View(par.GpuRQ3Shard(eng), eng.dev, rows.issues), rank, world)
     r2 = par.rq2_count_sharded(_RQ2View(par.GpuRQ2CountShard(eng), eng.dev), rank, world, lo, hi)
     r4 = par.rq4a_sharded(_RQ4aView(par.GpuRQ4aShard(eng, M), eng.dev), rank, world, lo, hi)
+    r4b = par.rq4b_sharded(_RQ4bView(par.GpuRQ4bShard(eng), eng.dev), rank, world)
     if rank == 0:
         ours2 = compute.rq2_count_result(r2["proj"], r2["session_offsets"], r2["session_values"], r2["K"],
                                          r2["average"], r2["median"], r2["percentiles"], r2["average"],
@@ -116,6 +126,10 @@ def _check(rank, world, case):
         ours4 = compute.rq4a_result(r4["counts"], r4["scalars"], r4["member"], r4["tables"], r4["intro"],
                                     r4["g4_steps"], r4["g4_transition"])
         assert_same(ours4, orc.rq4a(t), "rq4a")
+        ours4b = compute.rq4b_result(r4b["counts"], r4b["c2"], r4b["c1"], r4b["g2_q"], r4b["g1_q"], r4b["p_bm"],
+                                     r4b["sp6"], r4b["pre_cov"], r4b["post_cov"], r4b["pre_median"],
+                                     r4b["post_median"], r4b["init_g2"], r4b["init_g1"], r4b["tests"])
+        assert_same(ours4b, orc.rq4b(t), "rq4b")
         ours3 = compute.rq3_result(total3, {k: v.numpy() for k, v in cols3.items()}, st3["describe"].numpy(),
                                    st3["tests"].numpy())
         assert_same(ours3, orc.rq3(t), "rq3")

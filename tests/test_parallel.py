@@ -237,6 +237,65 @@ class OracleRQ4aShard:
         return sc
 
 
+class OracleRQ4bShard(OracleRQ2CountShard):
+    """One rank's RQ4b on the CPU restatement, in fz_rq4b_ex's shard output layout."""
+
+    def run(self):
+        from oracle import rq_oracle as orc
+        t = self.t
+        P = len(t.projects)
+        elig = orc.eligible_projects(t)
+        groups, corpus_us = common.corpus_groups(t, elig, add_missing_to_g1=False)
+        member = np.zeros(P, np.int64)
+        for g in range(4):
+            member[groups[f"group{g + 1}"]] |= 1 << g
+        full = orc.rq4b_full_series(t, P)
+        offs = np.zeros(P + 1, np.int64)
+        vals = []
+        for p in range(P):
+            v = t.c_coverage[full.rows(p)] if member[p] & 3 else np.zeros(0)
+            vals.append(v)
+            offs[p + 1] = offs[p] + len(v)
+        order = common.corpus_columns(t)[2].tolist()
+        projs, pre, post = orc.rq4b_deltas(t, elig, groups, corpus_us)
+        # CSV row of each delta column: the k-th qualifying row of the corpus order
+        dord, k0 = [], 0
+        for p in projs:
+            k0 = order.index(p, k0)
+            dord.append(k0)
+            k0 += 1
+        init = {g: np.array([t.c_coverage[full.rows(p)[0]] for p in sorted(groups[g]) if len(full.rows(p))],
+                            np.float64) for g in ("group2", "group1")}
+        c = np.zeros(12, np.int64)
+        c[par.RQ4B_DELTA_PROJECTS], c[par.RQ4B_INIT_G2], c[par.RQ4B_INIT_G1] = len(projs), len(init["group2"]), \
+            len(init["group1"])
+        for g in range(4):
+            c[5 + g] = len(groups[f"group{g + 1}"])
+        T = lambda a, dt=np.float64: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))  # noqa: E731
+        return {"counts": T(c, np.int64), "member": T(member, np.int64),
+                "trend_values": T(np.concatenate(vals) if vals else np.zeros(0)), "trend_offsets": T(offs, np.int64),
+                "pre_cov": T(np.concatenate(pre) if projs else np.zeros(0)),
+                "post_cov": T(np.concatenate(post) if projs else np.zeros(0)), "delta_order": T(dord, np.int64),
+                "init_g2": T(init["group2"]), "init_g1": T(init["group1"])}
+
+    def session_stats(self, vals, sids, grp, S, max_len):
+        from oracle import rq_oracle as orc
+        v, s_, g_ = vals.numpy(), sids.numpy(), grp.numpy()
+        s2 = [list(v[(s_ == i) & (g_ == 0)]) for i in range(S)]
+        s1 = [list(v[(s_ == i) & (g_ == 1)]) for i in range(S)]
+        c2, c1, q2, q1, pb = orc.rq4b_session_stats(s2, s1)
+        T = torch.from_numpy
+        return {"c2": T(c2), "c1": T(c1), "g2_q": T(q2.reshape(-1)), "g1_q": T(q1.reshape(-1)), "p_bm": T(pb)}
+
+    def two_sample(self, x, y):
+        from oracle import rq_oracle as orc
+        mwu, cliff, bm, lv = orc.rq4b_init_tests(x.numpy(), y.numpy())
+        out = np.full(8, np.nan)
+        if mwu is not None:
+            out[:6] = [mwu, cliff, bm[0], bm[1], lv[0], lv[1]]
+        return out
+
+
 def _worker(rank, world, port, case, errfile):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -275,6 +334,7 @@ def _check(rank, world, case):
                       minlength=len(t.projects))
     r4 = par.rq4a_sharded(OracleRQ4aShard(ts, par.agree_max(int(nF4.max()) if len(nF4) else 1)), rank, world,
                           lo, hi)
+    r4b = par.rq4b_sharded(OracleRQ4bShard(ts), rank, world)
     if rank != 0:
         return
     g = orc.rq1(t)
@@ -308,6 +368,10 @@ def _check(rank, world, case):
     ours4 = compute.rq4a_result(r4["counts"], r4["scalars"], r4["member"], r4["tables"], r4["intro"], r4["g4_steps"],
                                 r4["g4_transition"])
     assert_same(ours4, orc.rq4a(t), "rq4a")
+    ours4b = compute.rq4b_result(r4b["counts"], r4b["c2"], r4b["c1"], r4b["g2_q"], r4b["g1_q"], r4b["p_bm"],
+                                 r4b["sp6"], r4b["pre_cov"], r4b["post_cov"], r4b["pre_median"], r4b["post_median"],
+                                 r4b["init_g2"], r4b["init_g1"], r4b["tests"])
+    assert_same(ours4b, orc.rq4b(t), "rq4b")
 
 
 def _spawn(world, case, tmp_path):

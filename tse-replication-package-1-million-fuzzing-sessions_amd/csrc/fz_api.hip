@@ -23,7 +23,11 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
 void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o);
 void rq4a_finish(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int64_t *g1d, const int64_t *g2t,
                  const int64_t *g2d, const int64_t *intro, const int64_t *steps, int64_t *counts, double *sc);
-void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o);
+void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *o);
+void rq4b_session_stats(fz_ctx *c, const double *values, const int64_t *sid, const uint8_t *grp, int64_t n, int64_t S,
+                        int64_t max_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q, double *pbm);
+void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t *n2, const double *b,
+                      int64_t nb_cap, const int64_t *n1, double *ts);
 }  // namespace fz
 
 namespace {
@@ -189,7 +193,35 @@ int fz_rq4a_finish(fz_ctx *ctx, const int64_t *g1_total, const int64_t *g1_det, 
 }
 
 int fz_rq4b(fz_ctx *ctx, const fz_rq4_groups *groups, const fz_rq4b_out *out) {
-    return guarded(ctx, [&] { fz::rq4b(ctx, groups, out); });
+    return guarded(ctx, [&] { fz::rq4b(ctx, groups, 0u, out); });
+}
+
+int fz_rq4b_ex(fz_ctx *ctx, const fz_rq4_groups *groups, uint32_t flags, const fz_rq4b_out *out) {
+    return guarded(ctx, [&] { fz::rq4b(ctx, groups, flags, out); });
+}
+
+int fz_rq4b_session_stats(fz_ctx *ctx, const double *values, const int64_t *session_ids, const uint8_t *groups,
+                          int64_t n_values, int64_t n_sessions, int64_t max_session_len, int64_t *c2, int64_t *c1,
+                          double *g2_q, double *g1_q, double *p_bm) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n_values >= 0 && n_sessions >= 0 && n_sessions < (int64_t(1) << 30) &&
+                     (n_values == 0 || (values && session_ids && groups)) &&
+                     (n_sessions == 0 || (c2 && c1 && g2_q && g1_q && p_bm)),
+                 "fz_rq4b_session_stats: bad arguments");
+        if (n_sessions == 0) return;
+        fz::rq4b_session_stats(ctx, values, session_ids, groups, n_values, n_sessions, max_session_len, c2, c1, g2_q,
+                               g1_q, p_bm);
+    });
+}
+
+int fz_two_sample_tests(fz_ctx *ctx, const double *x, int64_t nx, const double *y, int64_t ny, double *out) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(out && nx >= 0 && ny >= 0 && (nx == 0 || x) && (ny == 0 || y), "fz_two_sample_tests: bad arguments");
+        int64_t *d_n = ctx->arena.get<int64_t>(2);
+        const int64_t h[2] = {nx, ny};
+        fz::set_i64(ctx, d_n, h, 2);
+        fz::two_sample_tests(ctx, x, nx, d_n, y, ny, d_n + 1, out);
+    });
 }
 
 int fz_probe_begin(fz_ctx *ctx, const char *kernel_name) {

@@ -256,7 +256,116 @@ struct PositiveCoverage34 {  // get_coverage_deltas: coverage > 0, any date (rq4
     }
 };
 
-void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o) {
+// mannwhitneyu (two-sided p; U1 of 'greater' -> Cliff's delta), brunnermunzel and levene of the
+// initial-coverage samples a[0, *n2) (G2) and b[0, *n1) (G1) (rq4b_coverage.py:248-313)
+void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t *n2, const double *b,
+                      int64_t nb_cap, const int64_t *n1, double *ts) {
+    const int64_t cap = (na_cap > 0 ? na_cap : 1) + (nb_cap > 0 ? nb_cap : 1);
+    double *v = c->arena.get<double>(cap);
+    uint8_t *gr = c->arena.get<uint8_t>(cap);
+    map_n(c, cap, nullptr, [=] __device__(int64_t i) {
+        const int64_t na = *n2, nb = *n1;
+        if (i < na) {
+            v[i] = a[i];
+            gr[i] = 0;
+        } else if (i < na + nb) {
+            v[i] = b[i - na];
+            gr[i] = 1;
+        }
+    });
+    int64_t *d_all = c->arena.get<int64_t>(1);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) { *d_all = *n2 + *n1; });
+    Segs one{1, single_segment(c, d_all), cap};
+    int32_t *sid = segment_ids(c, one);
+    double *u1 = c->arena.get<double>(1);
+    RankTestOut rt;
+    rt.mwu_p_two = ts + FZ_RQ4B_MWU_P;
+    rt.u1 = u1;
+    rt.bm_stat = ts + FZ_RQ4B_BM_STAT;
+    rt.bm_p = ts + FZ_RQ4B_BM_P;
+    rt.exact_scratch = c->arena.get<double>(8 * cap + 1);
+    seg_rank_tests(c, v, gr, one, sid, rt);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        ts[FZ_RQ4B_CLIFF] = (2.0 * u1[0]) / (double(*n2) * double(*n1)) - 1.0;
+    });
+    uint64_t *ska = sorted_keys_dn(c, a, na_cap, n2);
+    uint64_t *skb = sorted_keys_dn(c, b, nb_cap, n1);
+    levene_two(c, ska, a, na_cap, n2, skb, b, nb_cap, n1, ts + FZ_RQ4B_LEVENE_W);
+}
+
+// Per-session quartiles / counts / Brunner-Munzel of G2 vs G1 (:910-1015) from values v2 ordered
+// by segment id sid2 = 2 * session + group (group 0 = G2), *d_n live of n_cap
+void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_cap, const int64_t *d_n, int64_t MM,
+                   int64_t max_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q, double *pbm) {
+    hipStream_t st = c->stream;
+    const int64_t S2 = 2 * MM, NC = n_cap, P = max_len;
+    const int64_t *d_nf = d_n;
+    int32_t *sess = c->arena.get<int32_t>(NC);
+    uint8_t *grp2 = c->arena.get<uint8_t>(NC);
+    map_n(c, NC, nullptr, [=] __device__(int64_t k) {
+        sess[k] = int32_t(sid2[k] >> 1);
+        grp2[k] = uint8_t(sid2[k] & 1u);
+    });
+    int64_t *offs2 = c->arena.get<int64_t>(S2 + 1);
+    k_segment_offsets_dn<<<grid_for(S2 + 1, kBlock, 1u << 30), kBlock, 0, st>>>(sid2, d_nf, S2, offs2);
+    FZ_LAUNCH_CHECK();
+    int64_t *soffs = c->arena.get<int64_t>(MM + 1);
+    map_n(c, MM + 1, nullptr, [=] __device__(int64_t i) {
+        soffs[i] = offs2[2 * i];
+        if (i < MM) {
+            c2[i] = offs2[2 * i + 1] - offs2[2 * i];
+            c1[i] = offs2[2 * i + 2] - offs2[2 * i + 1];
+        }
+    });
+    Segs sg2{S2, offs2, NC, P};
+    SortedSegs ss2 = seg_sort_f64(c, v2, sg2, reinterpret_cast<const int32_t *>(sid2));
+    double *qq = c->arena.get<double>(S2 * 3);
+    const double q3[3] = {25.0, 50.0, 75.0};
+    seg_percentiles(c, sg2, ss2.val, q3, 3, qq);
+    map_n(c, MM * 3, nullptr, [=] __device__(int64_t k) {
+        const int64_t i = k / 3, j = k % 3;
+        g2q[k] = qq[(2 * i) * 3 + j];
+        g1q[k] = qq[(2 * i + 1) * 3 + j];
+    });
+    RankTestOut rt;
+    rt.bm_p = pbm;
+    seg_rank_tests(c, v2, grp2, Segs{MM, soffs, NC, P}, sess, rt);
+    map_n(c, MM, nullptr, [=] __device__(int64_t i) {
+        if (!(c2[i] >= 5 && c1[i] >= 5)) pbm[i] = NAN;
+    });
+}
+
+__global__ void k_rq4b_keys(const int64_t *__restrict__ sid, const uint8_t *__restrict__ grp, int64_t n,
+                            uint64_t *__restrict__ keys, uint32_t *__restrict__ idx) {
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+        keys[i] = uint64_t(sid[i]) * 2u + (grp[i] ? 1u : 0u);
+        idx[i] = uint32_t(i);
+    }
+}
+
+void rq4b_session_stats(fz_ctx *c, const double *values, const int64_t *sid, const uint8_t *grp, int64_t n, int64_t S,
+                        int64_t max_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q, double *pbm) {
+    hipStream_t st = c->stream;
+    const int64_t MM = S > 0 ? S : 1;
+    uint64_t *key = c->arena.get<uint64_t>(n);
+    uint32_t *idx = c->arena.get<uint32_t>(n);
+    if (n > 0) {
+        k_rq4b_keys<<<grid_for(n), kBlock, 0, st>>>(sid, grp, n, key, idx);
+        FZ_LAUNCH_CHECK();
+        radix_sort_pairs(c, key, idx, n, bits_for(uint64_t(2 * MM)));
+    }
+    double *v2 = c->arena.get<double>(n);
+    uint32_t *sid2 = c->arena.get<uint32_t>(n);
+    int64_t *d_n = c->arena.get<int64_t>(1);
+    set_i64(c, d_n, &n, 1);
+    map_n(c, n, nullptr, [=] __device__(int64_t k) {
+        v2[k] = values[idx[k]];
+        sid2[k] = uint32_t(key[k]);
+    });
+    rq4b_sessions(c, v2, sid2, n, d_n, MM, max_len > 0 ? max_len : n, c2, c1, g2q, g1q, pbm);
+}
+
+void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *o) {
     Store &s = c->store;
     FZ_CHECK(s.built, "fz_rq4b: call fz_store_build first");
     FZ_CHECK(g && g->member && g->corpus_us && (g->order || g->n_order == 0), "fz_rq4b: null groups");
@@ -288,66 +397,43 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o) {
         atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ4B_SESSIONS]),
                   (unsigned long long)(foffs[p + 1] - foffs[p]));
     });
-    const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
-    const int64_t S2 = 2 * MM;                   // (session, group) segments
-    const int sbits = bits_for(uint64_t(S2 + 1));
-    uint64_t *key = c->arena.get<uint64_t>(NC);
-    uint32_t *idx = c->arena.get<uint32_t>(NC);
-    map_n(c, NC, nullptr, [=] __device__(int64_t j) {
-        if (j < *d_nf) {
-            const uint32_t p = fproj[j];
-            const uint64_t grp = (member[p] & 2) ? 0u : 1u;  // G2 -> x, G1 -> y
-            key[j] = ((uint64_t(j - foffs[p]) * 2u + grp) << pbits) | p;
-        } else {
-            key[j] = uint64_t(S2) << pbits;
-        }
-        idx[j] = uint32_t(j);
-    });
-    radix_sort_pairs(c, key, idx, NC, sbits + pbits);
-    double *v2 = c->arena.get<double>(NC);
-    uint32_t *sid2 = c->arena.get<uint32_t>(NC);
-    int32_t *sess = c->arena.get<int32_t>(NC);
-    uint8_t *grp2 = c->arena.get<uint8_t>(NC);
-    map_n(c, NC, nullptr, [=] __device__(int64_t k) {
-        const uint32_t sg = uint32_t(key[k] >> pbits);
-        sid2[k] = sg;
-        sess[k] = int32_t(sg >> 1);
-        grp2[k] = uint8_t(sg & 1u);
-        if (k < *d_nf) v2[k] = cov[frow[idx[k]]];
-    });
-    int64_t *offs2 = c->arena.get<int64_t>(S2 + 1);
-    k_segment_offsets_dn<<<grid_for(S2 + 1, kBlock, 1u << 30), kBlock, 0, st>>>(sid2, d_nf, S2, offs2);
-    FZ_LAUNCH_CHECK();
-    int64_t *soffs = c->arena.get<int64_t>(MM + 1);
+    if (o->trend_values && o->trend_offsets) {  // the shard's contribution to the session exchange
+        double *tvals = o->trend_values;
+        int64_t *toffs = o->trend_offsets;
+        map_n(c, NC, d_nf, [=] __device__(int64_t j) { tvals[j] = cov[frow[j]]; });
+        map_n(c, P + 1, nullptr, [=] __device__(int64_t p) { toffs[p] = foffs[p]; });
+    }
+    const bool sharded = flags & FZ_RQ4B_SKIP_SESSION_STATS;
     int64_t *c2 = o->c2, *c1 = o->c1;
-    map_n(c, MM + 1, nullptr, [=] __device__(int64_t i) {
-        soffs[i] = offs2[2 * i];
-        if (i < MM) {
-            c2[i] = offs2[2 * i + 1] - offs2[2 * i];
-            c1[i] = offs2[2 * i + 2] - offs2[2 * i + 1];
-        }
-    });
-    Segs sg2{S2, offs2, NC, P};
-    SortedSegs ss2 = seg_sort_f64(c, v2, sg2, reinterpret_cast<const int32_t *>(sid2));
-    double *qq = c->arena.get<double>(S2 * 3);
-    const double q3[3] = {25.0, 50.0, 75.0};
-    seg_percentiles(c, sg2, ss2.val, q3, 3, qq);
     double *g2q = o->g2_q, *g1q = o->g1_q;
-    map_n(c, MM * 3, nullptr, [=] __device__(int64_t k) {
-        const int64_t i = k / 3, j = k % 3;
-        g2q[k] = qq[(2 * i) * 3 + j];
-        g1q[k] = qq[(2 * i + 1) * 3 + j];
-    });
-    {
-        double *pbm = o->p_bm;
-        RankTestOut rt;
-        rt.bm_p = pbm;
-        seg_rank_tests(c, v2, grp2, Segs{MM, soffs, NC, P}, sess, rt);
-        map_n(c, MM, nullptr, [=] __device__(int64_t i) {
-            if (!(c2[i] >= 5 && c1[i] >= 5)) pbm[i] = NAN;
+    if (!sharded) {
+        // (session, group) key per value: G2 -> group 0 (x), G1 -> group 1 (y)
+        const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
+        const int64_t S2 = 2 * MM;
+        const int sbits = bits_for(uint64_t(S2 + 1));
+        uint64_t *key = c->arena.get<uint64_t>(NC);
+        uint32_t *idx = c->arena.get<uint32_t>(NC);
+        map_n(c, NC, nullptr, [=] __device__(int64_t j) {
+            if (j < *d_nf) {
+                const uint32_t p = fproj[j];
+                const uint64_t grp = (member[p] & 2) ? 0u : 1u;
+                key[j] = ((uint64_t(j - foffs[p]) * 2u + grp) << pbits) | p;
+            } else {
+                key[j] = uint64_t(S2) << pbits;
+            }
+            idx[j] = uint32_t(j);
         });
+        radix_sort_pairs(c, key, idx, NC, sbits + pbits);
+        double *v2 = c->arena.get<double>(NC);
+        uint32_t *sid2 = c->arena.get<uint32_t>(NC);
+        map_n(c, NC, nullptr, [=] __device__(int64_t k) {
+            sid2[k] = uint32_t(key[k] >> pbits);
+            if (k < *d_nf) v2[k] = cov[frow[idx[k]]];
+        });
+        rq4b_sessions(c, v2, sid2, NC, d_nf, MM, P, c2, c1, g2q, g1q, o->p_bm);
     }
     // last session with both groups >= 100 (:849-860); Spearman of the quartile sequences (:879-899)
+    if (!sharded) {
     int64_t *lastp1 = c->arena.get<int64_t>(1);
     map_n(c, 1, nullptr, [=] __device__(int64_t) { *lastp1 = 0; });
     map_n(c, MM, nullptr, [=] __device__(int64_t i) {
@@ -378,6 +464,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o) {
             sp[2 * k + 1] = pv[k];
         });
     }
+    }
 
     // ---- coverage deltas around the corpus date for G3 u G4, CSV order (:725-797)
     {
@@ -407,14 +494,17 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o) {
         int64_t *d_nd = counts + FZ_RQ4B_DELTA_PROJECTS;
         scan_exclusive_i64(c, df, dp, NOC, d_nd);
         double *pre = o->pre_cov, *post = o->post_cov;
+        int64_t *dord = o->delta_order;
         map_n(c, NOC, nullptr, [=] __device__(int64_t k) {
             if (!df[k]) return;
             const int64_t n = *d_nd, q = dp[k], j = dj[k];
+            if (dord) dord[q] = k;
             for (int i = 0; i < kWin; ++i) {
                 pre[i * n + q] = cov[pcrow[j - 1 - i]];  // DESC LIMIT 7 before the date
                 post[i * n + q] = cov[pcrow[j + i]];     // first 7 from the date
             }
         });
+        if (!sharded) {
         int64_t *offs7 = c->arena.get<int64_t>(kWin + 1);
         map_n(c, kWin + 1, nullptr, [=] __device__(int64_t i) { offs7[i] = i * (*d_nd); });
         Segs s7{kWin, offs7, int64_t(kWin) * (P > 0 ? P : 1), P};
@@ -423,6 +513,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o) {
         seg_median(c, s7, sp.val, o->pre_median);
         SortedSegs so = seg_sort_f64(c, post, s7, id7);
         seg_median(c, s7, so.val, o->post_median);
+        }
     }
 
     // ---- initial coverage of G2 vs G1 (:221-313)
@@ -443,38 +534,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4b_out *o) {
             if (f2[p]) a[q2[p]] = cov[fr[foffs[p]]];
             if (f1[p]) b[q1[p]] = cov[fr[foffs[p]]];
         });
-        const int64_t cap = 2 * (P > 0 ? P : 1);
-        double *v = c->arena.get<double>(cap);
-        uint8_t *gr = c->arena.get<uint8_t>(cap);
-        map_n(c, cap, nullptr, [=] __device__(int64_t i) {
-            const int64_t na = *n2, nb = *n1;
-            if (i < na) {
-                v[i] = a[i];
-                gr[i] = 0;
-            } else if (i < na + nb) {
-                v[i] = b[i - na];
-                gr[i] = 1;
-            }
-        });
-        int64_t *d_all = c->arena.get<int64_t>(1);
-        map_n(c, 1, nullptr, [=] __device__(int64_t) { *d_all = *n2 + *n1; });
-        Segs one{1, single_segment(c, d_all), cap};
-        int32_t *sid = segment_ids(c, one);
-        double *ts = o->tests;
-        double *u1 = c->arena.get<double>(1);
-        RankTestOut rt;
-        rt.mwu_p_two = ts + FZ_RQ4B_MWU_P;
-        rt.u1 = u1;
-        rt.bm_stat = ts + FZ_RQ4B_BM_STAT;
-        rt.bm_p = ts + FZ_RQ4B_BM_P;
-        rt.exact_scratch = c->arena.get<double>(8 * cap + 1);
-        seg_rank_tests(c, v, gr, one, sid, rt);
-        map_n(c, 1, nullptr, [=] __device__(int64_t) {
-            ts[FZ_RQ4B_CLIFF] = (2.0 * u1[0]) / (double(*n2) * double(*n1)) - 1.0;
-        });
-        uint64_t *ska = sorted_keys_dn(c, a, P, n2);
-        uint64_t *skb = sorted_keys_dn(c, b, P, n1);
-        levene_two(c, ska, a, P, n2, skb, b, P, n1, ts + FZ_RQ4B_LEVENE_W);
+        if (!sharded) two_sample_tests(c, a, P, n2, b, P, n1, o->tests);
     }
 }
 

@@ -118,12 +118,13 @@ FZ_RQ4B_NCOUNTS, FZ_RQ4B_NTESTS = 12, 8
 (RQ4B_SESSIONS, RQ4B_LAST, RQ4B_DELTA_PROJECTS, RQ4B_INIT_G2, RQ4B_INIT_G1, RQ4B_G1, RQ4B_G2, RQ4B_G3,
  RQ4B_G4) = range(9)
 RQ4B_MWU_P, RQ4B_CLIFF, RQ4B_BM_STAT, RQ4B_BM_P, RQ4B_LEVENE_W, RQ4B_LEVENE_P = range(6)
+FZ_RQ4B_SKIP_SESSION_STATS = 1
 
 
 class FzRq4bOut(C.Structure):
     _fields_ = [(n, _P) for n in ("counts", "eligible", "member", "c2", "c1", "g2_q", "g1_q", "p_bm", "spearman6",
                                   "pre_cov", "post_cov", "pre_median", "post_median", "init_g2", "init_g1",
-                                  "tests")]
+                                  "tests", "trend_values", "trend_offsets", "delta_order")]
 
 
 # every symbol include/fz.h declares, with its ctypes signature
@@ -148,6 +149,9 @@ SIGNATURES = {
     "fz_rq4a": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.POINTER(FzRq4aOut)]),
     "fz_rq4a_finish": (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P]),
     "fz_rq4b": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.POINTER(FzRq4bOut)]),
+    "fz_rq4b_ex": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.c_uint32, C.POINTER(FzRq4bOut)]),
+    "fz_rq4b_session_stats": (C.c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P]),
+    "fz_two_sample_tests": (C.c_int, [_P, _P, _I64, _P, _I64, _P]),
     "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),
     "fz_probe_end": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "fz_radix_sort_u64": (C.c_int, [_P, _P, _P, _I64, C.c_int]),

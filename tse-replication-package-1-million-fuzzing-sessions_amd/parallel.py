@@ -369,6 +369,89 @@ def rq4a_sharded(shard, rank: int, world: int, lo: int, hi: int):
             "g4_steps": steps.cpu().numpy(), "g4_transition": trans.cpu().numpy()}
 
 
+# ----------------------------------------------------------------------------------------- RQ4b
+(RQ4B_SESSIONS, RQ4B_LAST, RQ4B_DELTA_PROJECTS, RQ4B_INIT_G2, RQ4B_INIT_G1) = range(5)
+
+
+def rq4b_sharded(shard, rank: int, world: int):
+    """Exact RQ4b over project shards (rq4b_coverage.py:1209-1261).  ``shard.run()`` -> counts,
+    member[P], the G1/G2 full coverage series (trend_values, trend_offsets[P + 1]), the delta columns
+    (pre_cov / post_cov step-major, delta_order = CSV row of each column) and the initial-coverage
+    samples;
+    ``shard.session_stats(values, sids, groups, S, max_len)``, ``shard.series_tests(x)``,
+    ``shard.mean_median(x)`` and ``shard.two_sample(x, y)`` run the statistics.  Exchange: session
+    sizes all-reduced, (value, session, group) triples all-to-all'd to the owner of the session
+    index, per-session results, delta columns (re-ordered by CSV row, :216, :744) and initial samples
+    gathered.  Returns a dict for
+    rq/compute.rq4b_result (host arrays, every rank)."""
+    import torch
+    part = shard.run()
+    counts = part["counts"].clone()
+    dev = counts.device
+    P = part["member"].numel()
+    offs = part["trend_offsets"]
+    lens = (offs[1:] - offs[:-1]).to(torch.int64)
+    n = int(offs[-1].item())
+    vals = part["trend_values"][:n]
+    starts = torch.repeat_interleave(offs[:-1], lens)
+    sids = torch.arange(n, dtype=torch.int64, device=dev) - starts
+    grp = torch.repeat_interleave(((part["member"].to(torch.int64) & 2) == 0).to(torch.uint8), lens)
+    m_loc = int(lens.max().item()) if P > 0 else 0
+    M = agree_max(m_loc, dev) if world > 1 else m_loc
+    sizes = torch.bincount(sids, minlength=M)[:M].to(torch.int64) if n else torch.zeros(M, dtype=torch.int64,
+                                                                                          device=dev)
+    if world > 1:
+        all_reduce(sizes)
+        all_reduce(counts)
+    own = session_owners(sizes.cpu().numpy(), world)
+    if world > 1:  # route every value to the owner of its session index
+        cuts = torch.tensor([b for _, b in own], dtype=torch.int64, device=dev)
+        dest = torch.searchsorted(cuts, sids, right=True)
+        perm = torch.argsort(dest, stable=True)
+        send = torch.bincount(dest, minlength=world).tolist() if n else [0] * world
+        vals, sids, grp = (all_to_all_v(x[perm], send) for x in (vals, sids, grp))
+    a, b = own[rank]
+    st = shard.session_stats(vals, sids - a, grp, b - a, P)
+    res = {}
+    for k, w in (("c2", 1), ("c1", 1), ("g2_q", 3), ("g1_q", 3), ("p_bm", 1)):
+        v = st[k][:(b - a) * w]
+        res[k] = torch.cat(all_gather_v(v)).cpu().numpy() if world > 1 else v.cpu().numpy()
+    c2, c1 = res["c2"], res["c1"]
+    ok = np.nonzero((c2 >= 100) & (c1 >= 100))[0]
+    last = int(ok[-1]) if len(ok) else -1
+    sp6 = np.full(12, np.nan)
+    if last >= 0:
+        q1m, q2m = res["g1_q"].reshape(-1, 3), res["g2_q"].reshape(-1, 3)
+        for k, seq in enumerate([q1m[:last + 1, j] for j in range(3)] + [q2m[:last + 1, j] for j in range(3)]):
+            rho, p = shard.series_tests(torch.from_numpy(np.ascontiguousarray(seq)).to(dev))[:2]
+            sp6[2 * k], sp6[2 * k + 1] = rho, p
+    counts[RQ4B_SESSIONS] = M
+    counts[RQ4B_LAST] = last
+    # coverage deltas: columns of every rank, in corpus CSV order
+    nd = int(part["delta_order"].numel())
+    proj = part["delta_order"]
+    pre = part["pre_cov"][:7 * nd].reshape(7, nd) if nd else torch.zeros(7, 0, dtype=torch.float64, device=dev)
+    post = part["post_cov"][:7 * nd].reshape(7, nd) if nd else torch.zeros(7, 0, dtype=torch.float64, device=dev)
+    if world > 1:
+        proj = torch.cat(all_gather_v(proj))
+        pre = torch.stack([torch.cat(all_gather_v(pre[i].contiguous())) for i in range(7)])
+        post = torch.stack([torch.cat(all_gather_v(post[i].contiguous())) for i in range(7)])
+    order = np.argsort(proj.cpu().numpy(), kind="stable")
+    pre_h, post_h = pre.cpu().numpy()[:, order], post.cpu().numpy()[:, order]
+    counts[RQ4B_DELTA_PROJECTS] = len(order)
+    pre_med = [shard.mean_median(torch.from_numpy(pre_h[i].copy()).to(dev))[1] for i in range(7)]
+    post_med = [shard.mean_median(torch.from_numpy(post_h[i].copy()).to(dev))[1] for i in range(7)]
+    # initial coverage: samples in project order, tests once
+    x, y = part["init_g2"], part["init_g1"]
+    if world > 1:
+        x, y = torch.cat(all_gather_v(x)), torch.cat(all_gather_v(y))
+    tests = shard.two_sample(x, y)
+    return {"counts": counts.cpu().numpy(), "c2": c2, "c1": c1, "g2_q": res["g2_q"], "g1_q": res["g1_q"],
+            "p_bm": res["p_bm"], "sp6": sp6, "pre_cov": [pre_h[i].copy() for i in range(7)],
+            "post_cov": [post_h[i].copy() for i in range(7)], "pre_median": pre_med, "post_median": post_med,
+            "init_g2": x.cpu().numpy(), "init_g1": y.cpu().numpy(), "tests": tests}
+
+
 # ------------------------------------------------------------------------------------ row gathers
 def gather_rows(cols: dict, world: int) -> dict:
     """Concatenate per-rank row columns in rank (= project) order (RQ2 change rows, RQ1 raw rows)."""
@@ -446,18 +529,29 @@ class GpuRQ2CountShard:
         return {"average": avg, "median": med, "percentiles": pct, "ge100": ge}
 
     def series_tests(self, x):
-        E, C, eng = self.E, self.C, self.eng
-        out = eng.torch.empty(4, dtype=eng.torch.float64, device=eng.dev)
-        x = x.contiguous()
-        E._check(eng.lib, eng.lib.fz_series_tests(eng.ctx, C.c_void_p(x.data_ptr()) if x.numel() else None,
-                                                  x.numel(), C.c_void_p(out.data_ptr())))
-        return tuple(float(v) for v in out.cpu().tolist())
+        return gpu_series_tests(self.eng, x)
 
     def mean_median(self, x):
-        if x.numel() == 0:
-            return float("nan"), float("nan")
-        d = self.eng.describe(x.contiguous())
-        return float(d.mean), float(d.median)
+        return gpu_mean_median(self.eng, x)
+
+
+def gpu_series_tests(eng, x):
+    """fz_series_tests: (spearman rho, p, shapiro W, p) of one device series."""
+    import ctypes as C
+    from . import engine as E
+    out = eng.torch.empty(4, dtype=eng.torch.float64, device=eng.dev)
+    x = x.contiguous()
+    E._check(eng.lib, eng.lib.fz_series_tests(eng.ctx, C.c_void_p(x.data_ptr()) if x.numel() else None, x.numel(),
+                                              C.c_void_p(out.data_ptr())))
+    return tuple(float(v) for v in out.cpu().tolist())
+
+
+def gpu_mean_median(eng, x):
+    """(mean, median) of one device vector through fz_describe_f64 (NaN when empty)."""
+    if x.numel() == 0:
+        return float("nan"), float("nan")
+    d = eng.describe(x.contiguous())
+    return float(d.mean), float(d.median)
 
 
 class GpuRQ4aShard:
@@ -483,6 +577,56 @@ class GpuRQ4aShard:
         E._check(eng.lib, eng.lib.fz_rq4a_finish(eng.ctx, *[P(x) for x in tables], tables[0].numel(), P(intro),
                                                  intro.numel(), P(steps), P(counts), P(b.scalars)))
         return b.scalars.cpu().numpy()
+
+
+class GpuRQ4bShard:
+    """RQ4b of one rank on its engine (fz_rq4b_ex, fz_rq4b_session_stats, fz_series_tests,
+    fz_two_sample_tests)."""
+
+    def __init__(self, eng):
+        import ctypes as C
+        from . import engine as E
+        from .rq import compute
+        self.E, self.C, self.eng = E, C, eng
+        self.bufs = compute.rq4b_buffers(eng, shard=True)
+
+    def run(self):
+        E, C, eng, b = self.E, self.C, self.eng, self.bufs
+        E._check(eng.lib, eng.lib.fz_rq4b_ex(eng.ctx, C.byref(eng.groups), E.FZ_RQ4B_SKIP_SESSION_STATS,
+                                             C.byref(b.out)))
+        cnt = b.counts.cpu()
+        nd, n2, n1 = (int(cnt[k]) for k in (E.RQ4B_DELTA_PROJECTS, E.RQ4B_INIT_G2, E.RQ4B_INIT_G1))
+        P = eng.tables.fz.n_projects
+        return {"counts": b.counts, "member": b.member[:P], "trend_values": b.trend_values,
+                "trend_offsets": b.trend_offsets[:P + 1], "pre_cov": b.pre_cov[:7 * nd], "post_cov": b.post_cov[:7 * nd],
+                "delta_order": b.delta_order[:nd], "init_g2": b.init_g2[:n2], "init_g1": b.init_g1[:n1]}
+
+    def session_stats(self, vals, sids, grp, S, max_len):
+        E, C, eng = self.E, self.C, self.eng
+        torch = eng.torch
+        z = lambda n, dt: torch.zeros(max(n, 1), dtype=dt, device=eng.dev)  # noqa: E731
+        out = {"c2": z(S, torch.int64), "c1": z(S, torch.int64), "g2_q": z(3 * S, torch.float64),
+               "g1_q": z(3 * S, torch.float64), "p_bm": z(S, torch.float64)}
+        vals, sids, grp = vals.contiguous(), sids.contiguous(), grp.contiguous()
+        P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+        E._check(eng.lib, eng.lib.fz_rq4b_session_stats(eng.ctx, P(vals), P(sids), P(grp), vals.numel(), S, max_len,
+                                                        *[P(out[k]) for k in ("c2", "c1", "g2_q", "g1_q", "p_bm")]))
+        return out
+
+    def series_tests(self, x):
+        return gpu_series_tests(self.eng, x)
+
+    def mean_median(self, x):
+        return gpu_mean_median(self.eng, x)
+
+    def two_sample(self, x, y):
+        E, C, eng = self.E, self.C, self.eng
+        out = eng.torch.full((E.FZ_RQ4B_NTESTS,), float("nan"), dtype=eng.torch.float64, device=eng.dev)
+        x, y = x.contiguous(), y.contiguous()
+        P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+        if x.numel() and y.numel():
+            E._check(eng.lib, eng.lib.fz_two_sample_tests(eng.ctx, P(x), x.numel(), P(y), y.numel(), P(out)))
+        return out.cpu().numpy()
 
 
 class GpuRQ3Shard:

@@ -88,11 +88,11 @@ def rq1(eng: E.Engine, threshold: int = 100) -> RQ1Result:
 class OutBuffers:
     """Device buffers for one fz_* output struct: spec = [(field, n, torch dtype)] in struct order."""
 
-    def __init__(self, eng: E.Engine, struct_cls, spec):
+    def __init__(self, eng: E.Engine, struct_cls, spec, null=()):
         self.names = [n for n, _, _ in spec]
         for name, n, dt in spec:
             setattr(self, name, eng.zeros(n, dt))
-        self.out = struct_cls(*[C.c_void_p(getattr(self, n).data_ptr()) for n in self.names])
+        self.out = struct_cls(*[None if n in null else C.c_void_p(getattr(self, n).data_ptr()) for n in self.names])
 
     def host(self, name, n=None):
         a = getattr(self, name)
@@ -298,7 +298,8 @@ def rq4a(eng: E.Engine) -> RQ4aResult:
 
 
 # ----------------------------------------------------------------------------------------- RQ4b
-def rq4b_buffers(eng: E.Engine) -> OutBuffers:
+def rq4b_buffers(eng: E.Engine, shard: bool = False) -> OutBuffers:
+    """shard=False leaves the shard-only outputs (trend series, delta projects) NULL."""
     torch = eng.torch
     fz, st = eng.tables.fz, eng.stats
     P, M = fz.n_projects, max(int(st.max_cov_per_project), 1)
@@ -308,7 +309,10 @@ def rq4b_buffers(eng: E.Engine) -> OutBuffers:
         ("counts", E.FZ_RQ4B_NCOUNTS, i64), ("eligible", P, u8), ("member", P, u8), ("c2", M, i64), ("c1", M, i64),
         ("g2_q", 3 * M, f64), ("g1_q", 3 * M, f64), ("p_bm", M, f64), ("spearman6", 12, f64),
         ("pre_cov", 7 * PP, f64), ("post_cov", 7 * PP, f64), ("pre_median", 7, f64), ("post_median", 7, f64),
-        ("init_g2", P, f64), ("init_g1", P, f64), ("tests", E.FZ_RQ4B_NTESTS, f64)])
+        ("init_g2", P, f64), ("init_g1", P, f64), ("tests", E.FZ_RQ4B_NTESTS, f64),
+        ("trend_values", fz.n_cov if shard else 0, f64), ("trend_offsets", P + 1 if shard else 0, i64),
+        ("delta_order", P if shard else 0, i64)], null=() if shard else ("trend_values", "trend_offsets",
+                                                                         "delta_order"))
 
 
 def rq4b_launch(eng: E.Engine, b: OutBuffers):
@@ -316,26 +320,32 @@ def rq4b_launch(eng: E.Engine, b: OutBuffers):
 
 
 def rq4b_collect(eng: E.Engine, b: OutBuffers) -> RQ4bResult:
-    P = eng.tables.fz.n_projects
     cnt, ts = b.host("counts"), b.host("tests")
-    ms, last, nd = int(cnt[E.RQ4B_SESSIONS]), int(cnt[E.RQ4B_LAST]), int(cnt[E.RQ4B_DELTA_PROJECTS])
+    ms, nd = int(cnt[E.RQ4B_SESSIONS]), int(cnt[E.RQ4B_DELTA_PROJECTS])
     n2, n1 = int(cnt[E.RQ4B_INIT_G2]), int(cnt[E.RQ4B_INIT_G1])
-    sp = b.host("spearman6")
     pre, post = b.host("pre_cov"), b.host("post_cov")
-    both = n2 > 0 and n1 > 0
+    return rq4b_result(cnt, b.host("c2", ms), b.host("c1", ms), b.host("g2_q", 3 * ms), b.host("g1_q", 3 * ms),
+                       b.host("p_bm", ms), b.host("spearman6"), [pre[i * nd:(i + 1) * nd].copy() for i in range(7)],
+                       [post[i * nd:(i + 1) * nd].copy() for i in range(7)], b.host("pre_median"),
+                       b.host("post_median"), b.host("init_g2", n2), b.host("init_g1", n1), ts)
+
+
+def rq4b_result(cnt, c2, c1, g2_q, g1_q, p_bm, sp6, pre_cov, post_cov, pre_median, post_median, init_g2, init_g1,
+                tests) -> RQ4bResult:
+    """RQ4bResult from fz_rq4b's outputs (host copies; also the sharded recombination)."""
+    ms, last = len(c2), int(cnt[E.RQ4B_LAST])
+    both = len(init_g2) > 0 and len(init_g1) > 0
     return RQ4bResult(
         group_counts=tuple(int(cnt[k]) for k in (E.RQ4B_G1, E.RQ4B_G2, E.RQ4B_G3, E.RQ4B_G4)), n_sessions=ms,
-        c2=b.host("c2", ms), c1=b.host("c1", ms), g2_q=b.host("g2_q", 3 * ms).reshape(ms, 3),
-        g1_q=b.host("g1_q", 3 * ms).reshape(ms, 3), p_bm=b.host("p_bm", ms), last_valid_idx=last,
-        spearman6=[(float(sp[2 * k]), float(sp[2 * k + 1])) for k in range(6)] if last >= 0 else None,
-        n_delta_projects=nd, pre_cov=[pre[i * nd:(i + 1) * nd].copy() for i in range(7)],
-        post_cov=[post[i * nd:(i + 1) * nd].copy() for i in range(7)],
-        pre_median=[float(x) for x in b.host("pre_median")], post_median=[float(x) for x in b.host("post_median")],
-        n_g2=int(cnt[E.RQ4B_G2]), n_g1=int(cnt[E.RQ4B_G1]), init_g2=b.host("init_g2", n2),
-        init_g1=b.host("init_g1", n1), mwu_p=float(ts[E.RQ4B_MWU_P]) if both else None,
-        cliff=float(ts[E.RQ4B_CLIFF]) if both else None,
-        bm=(float(ts[E.RQ4B_BM_STAT]), float(ts[E.RQ4B_BM_P])) if both else None,
-        levene=(float(ts[E.RQ4B_LEVENE_W]), float(ts[E.RQ4B_LEVENE_P])) if both else None)
+        c2=np.asarray(c2), c1=np.asarray(c1), g2_q=np.asarray(g2_q).reshape(ms, 3),
+        g1_q=np.asarray(g1_q).reshape(ms, 3), p_bm=np.asarray(p_bm), last_valid_idx=last,
+        spearman6=[(float(sp6[2 * k]), float(sp6[2 * k + 1])) for k in range(6)] if last >= 0 else None,
+        n_delta_projects=len(pre_cov[0]) if len(pre_cov) else 0, pre_cov=pre_cov, post_cov=post_cov,
+        pre_median=[float(x) for x in pre_median], post_median=[float(x) for x in post_median],
+        n_g2=int(cnt[E.RQ4B_G2]), n_g1=int(cnt[E.RQ4B_G1]), init_g2=np.asarray(init_g2), init_g1=np.asarray(init_g1),
+        mwu_p=float(tests[E.RQ4B_MWU_P]) if both else None, cliff=float(tests[E.RQ4B_CLIFF]) if both else None,
+        bm=(float(tests[E.RQ4B_BM_STAT]), float(tests[E.RQ4B_BM_P])) if both else None,
+        levene=(float(tests[E.RQ4B_LEVENE_W]), float(tests[E.RQ4B_LEVENE_P])) if both else None)
 
 
 def rq4b(eng: E.Engine) -> RQ4bResult:
