@@ -201,7 +201,7 @@ def pmc_traffic(probe, config):
     *_pmc_traffic.json, written by scripts/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE
     runs of this bench with the gfx950 FETCH_SIZE correction), or None."""
     import glob
-    kern = {"radix_scatter": "k_onesweep"}.get(probe, probe)  # the probe name of the radix pass kernel
+    kern = {"radix_scatter": "k_onesweep<"}.get(probe, probe)  # the radix pass kernel (both variants)
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
         try:
             d = json.load(open(path))
