@@ -10,7 +10,7 @@ for f in *.hip; do
         --cuda-device-only -S "$f" -o "$out/${f%.hip}.s" 2>/dev/null &
 done
 wait
-bad=$(grep -hE "^\s+(s_store|s_buffer_store|s_scratch_store|s_dcache_wb|s_dcache_discard|s_atomic|s_buffer_atomic)" "$out"/*.s | wc -l)
+bad=$( (grep -hE "^\s+(s_store|s_buffer_store|s_scratch_store|s_dcache_wb|s_dcache_discard|s_atomic|s_buffer_atomic)" "$out"/*.s || true) | wc -l)
 echo "device asm: $(cat "$out"/*.s | wc -l) lines, scalar-store instructions: $bad"
 rm -rf "$out"
 [ "$bad" -eq 0 ]

@@ -164,13 +164,10 @@ struct fz_ctx {
     fz::Store store;
     fz::Probe probe;
     int64_t *h_pinned = nullptr;   // small pinned host staging area (32 KiB)
-    // single-pass scan state (fz_prims.hip): tile tickets + per-tile status words; both are left
-    // zeroed by the last workgroup of every scan, so the next scan (or a graph replay) starts clean
-    fz::DevBuf scan_status;        // uint64 [tiles]
-    fz::DevBuf scan_counters;      // uint32 [2]: ticket, done
-    // single-sweep radix passes (fz_prims.hip): per (tile, digit) status words tagged with a pass
-    // epoch, and a never-reset tile ticket counter whose per-launch base the host tracks
-    fz::DevBuf os_status;          // uint64 [tiles * 256]
+    // decoupled look-back state (fz_lookback.h; single-pass scan, compaction, radix passes): status
+    // words tagged with a per-launch epoch, and a never-reset tile ticket counter whose per-launch
+    // base the host tracks
+    fz::DevBuf os_status;          // uint64 [max words of one launch]
     fz::DevBuf os_ticket;          // uint32 [1]
     unsigned int os_ticket_base = 0;
     unsigned int os_epoch = 0;

@@ -4,6 +4,7 @@
 
 #include "fz_device.h"
 #include "fz_internal.h"
+#include "fz_lookback.h"
 #include "fz_views.h"
 
 namespace fz {
@@ -118,27 +119,38 @@ __global__ __launch_bounds__(kScan1Threads) void k_scan_single(const int64_t *__
     if (total && tid == 0) *total = tot;
 }
 
-// Single-pass scan with decoupled look-back.  Workgroups take tile numbers from a ticket counter in
-// the order they start (so every predecessor a tile waits for is already running), publish their
-// aggregate, then walk back over predecessors' status words until an inclusive prefix is found.
-// A status word packs {flag:2, value:62} and is written and polled with agent-scope atomics
-// (global_store/load sc1): the payload travels inside the flag word, so no separate release /
-// acquire is needed (MI355X_MICROARCH.md: 8-byte data+tag granule).  The last workgroup to finish
-// zeroes the status words and counters for the next scan (graph-replay safe).
+Lookback lookback_begin(fz_ctx *c, int64_t words) {
+    if (c->os_status.cap < size_t(words < 1 ? 1 : words) * 8) {
+        uint64_t *st = c->os_status.ensure<uint64_t>(words);
+        FZ_HIP(hipMemsetAsync(st, 0, c->os_status.cap, c->stream));
+        c->os_epoch = 0;
+    }
+    if (c->os_ticket.cap == 0) {
+        FZ_HIP(hipMemsetAsync(c->os_ticket.ensure<unsigned int>(1), 0, 4, c->stream));
+        c->os_ticket_base = 0;
+    }
+    if (++c->os_epoch == (1u << 14)) {  // epoch wrap: clear the status words once
+        FZ_HIP(hipMemsetAsync(c->os_status.ptr, 0, c->os_status.cap, c->stream));
+        c->os_epoch = 1;
+    }
+    return Lookback{c->os_status.as<uint64_t>(), c->os_ticket.as<unsigned int>(), c->os_ticket_base,
+                    uint64_t(c->os_epoch) << 48};
+}
+
+// Single-pass exclusive scan: 4096-element tiles, tile prefixes by decoupled look-back
+// (fz_lookback.h).
 constexpr int kLbItems = 16;
 constexpr int kLbTile = kBlock * kLbItems;  // 4096
-constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbMask = (1ull << 62) - 1ull;
 
 __global__ __launch_bounds__(kBlock) void k_scan_lookback(const int64_t *__restrict__ in, int64_t *__restrict__ out,
-                                                          int64_t n, int64_t ntiles, uint64_t *__restrict__ status,
-                                                          unsigned int *__restrict__ counters,
+                                                          int64_t n, int64_t ntiles, Lookback lb,
                                                           int64_t *__restrict__ total) {
     __shared__ int64_t s_val[kLbTile];
     __shared__ int64_t s_tmp[4];
     __shared__ int64_t s_prefix;
     __shared__ unsigned int s_tile;
     const int tid = threadIdx.x;
-    if (tid == 0) s_tile = atomicAdd(&counters[0], 1u);
+    if (tid == 0) s_tile = lb_take_tile(lb);
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t base = tile * kLbTile;
@@ -156,35 +168,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_lookback(const int64_t *__restr
     int64_t agg;
     const int64_t off = block_excl_scan(run, s_tmp, &agg);
     if (tid < kWave) {
-        // wave 0 publishes this tile's aggregate, then looks back over 64 predecessors per poll:
-        // the nearest inclusive prefix in the window ends the walk, aggregates above it are added
-        // (one wave-wide load + ballot per step instead of one serial load per predecessor)
-        const int lane = tid;
-        int64_t prefix = 0;
-        if (lane == 0)
-            __hip_atomic_store(&status[tile], (tile == 0 ? kLbInc : kLbAgg) | (uint64_t(agg) & kLbMask),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int64_t end = tile; end > 0;) {
-            const int64_t p = end - kWave + lane;  // lane 63 = nearest predecessor
-            const uint64_t w = p >= 0 ? __hip_atomic_load(&status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                      : kLbInc;  // before tile 0: an inclusive prefix of 0
-            const uint64_t flag = w & ~kLbMask;
-            const uint64_t inc = __ballot(flag == kLbInc);
-            const uint64_t empty = __ballot(flag == 0);
-            const int hi = inc ? 63 - __clzll((long long)inc) : -1;  // nearest inclusive lane
-            const uint64_t need = hi >= 0 ? (hi == 63 ? 0ull : ~0ull << (hi + 1)) : ~0ull;
-            if (empty & need) {  // a tile between the inclusive prefix and this one has not published
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            prefix += wave_sum<int64_t>(lane >= (hi < 0 ? 0 : hi) && p >= 0 ? int64_t(w & kLbMask) : 0);
-            if (hi >= 0) break;
-            end -= kWave;
-        }
-        if (lane == 0) {
-            if (tile > 0)
-                __hip_atomic_store(&status[tile], kLbInc | (uint64_t(prefix + agg) & kLbMask), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+        const int64_t prefix = lb_exclusive_prefix(lb, tile, agg);
+        if (tid == 0) {
             s_prefix = prefix;
             if (total && tile == ntiles - 1) *total = prefix + agg;
         }
@@ -196,21 +181,6 @@ __global__ __launch_bounds__(kBlock) void k_scan_lookback(const int64_t *__restr
     for (int i = 0; i < kLbItems; ++i) {
         const int64_t idx = base + i * kBlock + tid;
         if (idx < n) out[idx] = s_val[i * kBlock + tid];
-    }
-    // the last workgroup to finish resets the shared state (all others have finished their walks)
-    __shared__ int s_last;
-    if (tid == 0) {
-        __threadfence();  // this tile's status stores complete before it is counted as done
-        s_last = atomicAdd(&counters[1], 1u) == unsigned(ntiles - 1);
-    }
-    __syncthreads();
-    if (s_last) {
-        for (int64_t p = tid; p < ntiles; p += kBlock)
-            __hip_atomic_store(&status[p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tid == 0) {
-            __hip_atomic_store(&counters[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&counters[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
 }
 
@@ -226,16 +196,10 @@ void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, i
     }
     if (n > kScan1Max) {
         const int64_t ntiles = (n + kLbTile - 1) / kLbTile;
-        if (c->scan_status.cap < size_t(ntiles) * 8 || c->scan_counters.cap == 0) {
-            uint64_t *st = c->scan_status.ensure<uint64_t>(ntiles);
-            unsigned int *ct = c->scan_counters.ensure<unsigned int>(2);
-            FZ_HIP(hipMemsetAsync(st, 0, c->scan_status.cap, c->stream));
-            FZ_HIP(hipMemsetAsync(ct, 0, 8, c->stream));
-        }
-        k_scan_lookback<<<unsigned(ntiles), kBlock, 0, c->stream>>>(in, out, n, ntiles,
-                                                                    c->scan_status.as<uint64_t>(),
-                                                                    c->scan_counters.as<unsigned int>(), out_total);
+        const Lookback lb = lookback_begin(c, ntiles);
+        k_scan_lookback<<<unsigned(ntiles), kBlock, 0, c->stream>>>(in, out, n, ntiles, lb, out_total);
         FZ_LAUNCH_CHECK();
+        lookback_end(c, ntiles);
         return;
     }
     const int64_t nb = (n + kScanChunk - 1) / kScanChunk;
@@ -258,85 +222,6 @@ constexpr int kRadix = 1 << kRadixBits;
 constexpr int kSortItems = 16;
 constexpr int kSortTile = kBlock * kSortItems;  // 4096 keys per workgroup
 
-// Per-tile digit histogram, digit-major: counts[d * nb + tile].
-__global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t *__restrict__ keys, int64_t n, int shift,
-                                                       int64_t *__restrict__ counts, int64_t nb) {
-    __shared__ uint32_t s_hist[kRadix];
-    s_hist[threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t base = int64_t(blockIdx.x) * kSortTile;
-    for (int r = 0; r < kSortItems; ++r) {
-        const int64_t idx = base + r * kBlock + threadIdx.x;
-        const bool valid = idx < n;
-        const uint32_t d = valid ? uint32_t(keys[idx] >> shift) & (kRadix - 1) : 0u;
-        const uint64_t peers = match_digit<kRadixBits>(d, valid);
-        if (valid && (__ffsll((long long)peers) - 1) == lane_id()) atomicAdd(&s_hist[d], uint32_t(__popcll(peers)));
-    }
-    __syncthreads();
-    counts[int64_t(threadIdx.x) * nb + blockIdx.x] = s_hist[threadIdx.x];
-}
-
-// Stable scatter: ranks inside the tile follow row order (round, wave, lane); the tile is staged
-// digit-sorted in LDS and written out in runs (coalesced per digit).
-template <bool HAS_VALS>
-__global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t *__restrict__ keys_in,
-                                                          const uint32_t *__restrict__ vals_in,
-                                                          uint64_t *__restrict__ keys_out,
-                                                          uint32_t *__restrict__ vals_out, int64_t n, int shift,
-                                                          const int64_t *__restrict__ counts,
-                                                          const int64_t *__restrict__ offsets, int64_t nb) {
-    __shared__ uint64_t s_keys[kSortTile];
-    __shared__ uint32_t s_vals[HAS_VALS ? kSortTile : 1];
-    __shared__ uint32_t s_start[kRadix];
-    __shared__ uint32_t s_run[kRadix];
-    __shared__ uint32_t s_wcnt[4][kRadix];
-    __shared__ int64_t s_goff[kRadix];
-    __shared__ uint32_t s_tmp[4];
-
-    const int tid = threadIdx.x;
-    const int w = wave_id();
-    const int64_t base = int64_t(blockIdx.x) * kSortTile;
-    {
-        uint32_t cnt = uint32_t(counts[int64_t(tid) * nb + blockIdx.x]);
-        uint32_t st = block_excl_scan(cnt, s_tmp, (uint32_t *)nullptr);
-        s_start[tid] = st;
-        s_run[tid] = 0;
-        s_goff[tid] = offsets[int64_t(tid) * nb + blockIdx.x];
-    }
-    for (int r = 0; r < kSortItems; ++r) {
-        const int64_t idx = base + r * kBlock + tid;
-        const bool valid = idx < n;
-        uint64_t k = valid ? keys_in[idx] : 0ull;
-        uint32_t v = 0;
-        if (HAS_VALS && valid) v = vals_in[idx];
-        const uint32_t d = uint32_t(k >> shift) & (kRadix - 1);
-        for (int i = 0; i < 4; ++i) s_wcnt[i][tid] = 0;
-        __syncthreads();
-        const uint64_t peers = match_digit<kRadixBits>(d, valid);
-        const uint32_t rank = uint32_t(__popcll(peers & lanemask_lt()));
-        if (valid && (__ffsll((long long)peers) - 1) == lane_id()) s_wcnt[w][d] = uint32_t(__popcll(peers));
-        __syncthreads();
-        if (valid) {
-            uint32_t wpre = 0;
-            for (int i = 0; i < w; ++i) wpre += s_wcnt[i][d];
-            const uint32_t pos = s_start[d] + s_run[d] + wpre + rank;
-            s_keys[pos] = k;
-            if (HAS_VALS) s_vals[pos] = v;
-        }
-        __syncthreads();
-        s_run[tid] += s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
-    }
-    __syncthreads();
-    const int64_t valid_n = (n - base) < kSortTile ? (n - base) : kSortTile;
-    for (int i = tid; i < valid_n; i += kBlock) {
-        const uint64_t k = s_keys[i];
-        const uint32_t d = uint32_t(k >> shift) & (kRadix - 1);
-        const int64_t gpos = s_goff[d] + (i - int64_t(s_start[d]));
-        keys_out[gpos] = k;
-        if (HAS_VALS) vals_out[gpos] = s_vals[i];
-    }
-}
-
 // ---- single-sweep LSD passes (one launch per digit pass) -----------------------------------
 // One histogram kernel counts every pass's digits up front (passes whose digit is the same for
 // all keys are skipped: they are identity permutations).  Each pass is then ONE kernel: a tile
@@ -346,8 +231,6 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t *__rest
 // histogram pass, no device-wide scan of the tile x digit counts.  Epoch tags make stale words
 // from earlier passes invisible, so the status array is never cleared between passes.
 constexpr int kOsMaxPasses = 8;
-constexpr uint64_t kOsAgg = 1ull << 62, kOsInc = 2ull << 62, kOsFlags = 3ull << 62;
-constexpr uint64_t kOsValMask = (1ull << 48) - 1ull, kOsEpochMask = ((1ull << 14) - 1ull) << 48;
 constexpr int kOsWindow = 8;
 
 __global__ __launch_bounds__(kBlock) void k_onesweep_hist(const uint64_t *__restrict__ keys, int64_t n, int npass,
@@ -434,7 +317,7 @@ __global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict_
     const uint32_t cnt = s_run[tid];
     // publish this tile's count of digit tid, then look back for the counts of all earlier tiles
     uint64_t *my = &status[tile * kRadix + tid];
-    __hip_atomic_store(my, (tile == 0 ? kOsInc : kOsAgg) | epoch | uint64_t(cnt), __ATOMIC_RELAXED,
+    __hip_atomic_store(my, (tile == 0 ? kLbInc : kLbAgg) | epoch | uint64_t(cnt), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     s_start[tid] = block_excl_scan(cnt, s_tmp, (uint32_t *)nullptr);
     const int64_t gstart = block_excl_scan(int64_t(ghist[tid]), s_tmp64, (int64_t *)nullptr);
@@ -445,14 +328,14 @@ __global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict_
         for (int j = 0; j < kOsWindow; ++j)
             sw[j] = q - j >= 0 ? __hip_atomic_load(&status[(q - j) * kRadix + tid], __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT)
-                               : (kOsInc | epoch);
+                               : (kLbInc | epoch);
         int j = 0;
         bool done = false;
         for (; j < kOsWindow; ++j) {
             const uint64_t x = sw[j];
-            if ((x & kOsEpochMask) != epoch || !(x & kOsFlags)) break;  // not published yet
-            prefix += int64_t(x & kOsValMask);
-            if ((x & kOsFlags) == kOsInc) {
+            if ((x & kLbEpochMask) != epoch || !(x & kLbFlags)) break;  // not published yet
+            prefix += int64_t(x & kLbVal);
+            if ((x & kLbFlags) == kLbInc) {
                 done = true;
                 break;
             }
@@ -462,7 +345,7 @@ __global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict_
         if (j < kOsWindow) __builtin_amdgcn_s_sleep(1);
     }
     if (tile > 0)
-        __hip_atomic_store(my, kOsInc | epoch | uint64_t(prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(my, kLbInc | epoch | uint64_t(prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_goff[tid] = gstart + prefix - int64_t(s_start[tid]);
     // stage the tile digit-sorted in LDS, then write it out in per-digit runs
 #pragma unroll
@@ -507,16 +390,6 @@ void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int 
         for (int d = 0; d < kRadix; ++d) nz += hh[p * kRadix + d] != 0;
         need[p] = nz > 1;  // a pass whose digit is constant is the identity permutation
     }
-    // status words: grown (and cleared) on demand; epochs tag every pass
-    if (c->os_status.cap < size_t(nb) * kRadix * 8) {
-        uint64_t *st = c->os_status.ensure<uint64_t>(nb * kRadix);
-        FZ_HIP(hipMemsetAsync(st, 0, c->os_status.cap, c->stream));
-        c->os_epoch = 0;
-    }
-    if (c->os_ticket.cap == 0) {
-        FZ_HIP(hipMemsetAsync(c->os_ticket.ensure<unsigned int>(1), 0, 4, c->stream));
-        c->os_ticket_base = 0;
-    }
     uint64_t *k2 = c->arena.get<uint64_t>(n);
     uint32_t *v2 = vals ? c->arena.get<uint32_t>(n) : nullptr;
     uint64_t *ka = keys, *kb = k2;
@@ -524,25 +397,21 @@ void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int 
     int passes = 0;
     for (int p = 0; p < npass; ++p) {
         if (!need[p]) continue;
-        if (++c->os_epoch == (1u << 14)) {  // epoch wrap: clear the status words once
-            FZ_HIP(hipMemsetAsync(c->os_status.ptr, 0, c->os_status.cap, c->stream));
-            c->os_epoch = 1;
-        }
-        const uint64_t epoch = uint64_t(c->os_epoch) << 48;
+        const Lookback lb = lookback_begin(c, nb * kRadix);  // (tile, digit) status words
         {
             // algorithmic traffic of one pass: read + write every key (8 B) and value (4 B)
             ProbeScope ps(c, "radix_scatter", (vals ? 24.0 : 16.0) * double(n));
             if (vals)
-                k_onesweep<true><<<unsigned(nb), kBlock, 0, c->stream>>>(
-                    ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, c->os_status.as<uint64_t>(),
-                    c->os_ticket.as<unsigned int>(), c->os_ticket_base, epoch);
+                k_onesweep<true><<<unsigned(nb), kBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits,
+                                                                         ghist + p * kRadix, lb.status, lb.ticket,
+                                                                         lb.base, lb.epoch);
             else
-                k_onesweep<false><<<unsigned(nb), kBlock, 0, c->stream>>>(
-                    ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, c->os_status.as<uint64_t>(),
-                    c->os_ticket.as<unsigned int>(), c->os_ticket_base, epoch);
+                k_onesweep<false><<<unsigned(nb), kBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits,
+                                                                          ghist + p * kRadix, lb.status, lb.ticket,
+                                                                          lb.base, lb.epoch);
             FZ_LAUNCH_CHECK();
         }
-        c->os_ticket_base += unsigned(nb);
+        lookback_end(c, nb);
         std::swap(ka, kb);
         std::swap(va, vb);
         ++passes;
@@ -786,21 +655,6 @@ void describe_f64(fz_ctx *c, const double *x, int64_t n, fz_describe *dev_out) {
 }
 
 // ----------------------------------------------------------------------- views / compaction
-__global__ __launch_bounds__(kBlock) void k_compact_view(const int32_t *__restrict__ rows,
-                                                         const int64_t *__restrict__ times,
-                                                         const uint32_t *__restrict__ proj, int64_t n,
-                                                         const int64_t *__restrict__ flags,
-                                                         const int64_t *__restrict__ pos, int32_t *__restrict__ orow,
-                                                         int64_t *__restrict__ otime, uint32_t *__restrict__ oproj) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        if (flags[i]) {
-            const int64_t p = pos[i];
-            orow[p] = rows[i];
-            otime[p] = times[i];
-            oproj[p] = proj[i];
-        }
-    }
-}
 
 __global__ __launch_bounds__(kBlock) void k_segment_offsets_dn(const uint32_t *__restrict__ proj,
                                                                const int64_t *__restrict__ d_n, int64_t P,

@@ -8,6 +8,7 @@
 
 #include "fz_device.h"
 #include "fz_internal.h"
+#include "fz_lookback.h"
 
 namespace fz {
 
@@ -21,26 +22,75 @@ struct TmpView {
     int64_t *offs = nullptr;  // [P + 1]
 };
 
-template <typename Pred>
-__global__ __launch_bounds__(kBlock) void k_flag_rows(const int32_t *__restrict__ rows, int64_t n,
-                                                      const int64_t *__restrict__ d_live, Pred pred,
-                                                      int64_t *__restrict__ flags) {
-    const int64_t live = d_live ? *d_live : n;
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
-        flags[i] = (i < live && pred(rows[i])) ? 1 : 0;
-}
-
-__global__ __launch_bounds__(kBlock) void k_compact_view(const int32_t *__restrict__ rows,
-                                                         const int64_t *__restrict__ times,
-                                                         const uint32_t *__restrict__ proj, int64_t n,
-                                                         const int64_t *__restrict__ flags,
-                                                         const int64_t *__restrict__ pos, int32_t *__restrict__ orow,
-                                                         int64_t *__restrict__ otime, uint32_t *__restrict__ oproj);
-
 // Offsets of a project-sorted array whose length is only known on the device.
 __global__ __launch_bounds__(kBlock) void k_segment_offsets_dn(const uint32_t *__restrict__ proj,
                                                                const int64_t *__restrict__ d_n, int64_t P,
                                                                int64_t *__restrict__ offsets);
+
+// Single-pass order-preserving compaction of a view: each 4096-row tile evaluates pred, ranks its
+// kept rows in LDS, gets its output base by decoupled look-back over the preceding tiles, and
+// writes (row, time, proj) of the kept rows; the last tile writes the count.  One launch instead of
+// flag -> device-wide scan -> compact.
+constexpr int kFcItems = 16;
+constexpr int kFcTile = kBlock * kFcItems;
+
+template <typename Pred>
+__global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__restrict__ rows,
+                                                           const int64_t *__restrict__ times,
+                                                           const uint32_t *__restrict__ proj, int64_t n,
+                                                           const int64_t *__restrict__ d_live, Pred pred, Lookback lb,
+                                                           int64_t ntiles, int32_t *__restrict__ orow,
+                                                           int64_t *__restrict__ otime, uint32_t *__restrict__ oproj,
+                                                           int64_t *__restrict__ d_n) {
+    __shared__ int32_t s_pos[kFcTile];
+    __shared__ int32_t s_tmp[4];
+    __shared__ int64_t s_prefix;
+    __shared__ unsigned int s_tile;
+    const int tid = threadIdx.x;
+    if (tid == 0) s_tile = lb_take_tile(lb);
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int64_t base = tile * kFcTile;
+    const int64_t live = d_live ? *d_live : n;
+    for (int i = 0; i < kFcItems; ++i) {
+        const int64_t idx = base + i * kBlock + tid;
+        s_pos[i * kBlock + tid] = (idx < n && idx < live && pred(rows[idx])) ? 1 : 0;
+    }
+    __syncthreads();
+    int32_t loc[kFcItems];
+    int32_t run = 0;
+    for (int i = 0; i < kFcItems; ++i) {
+        loc[i] = run;
+        run += s_pos[tid * kFcItems + i];
+    }
+    int32_t agg;
+    const int32_t off = block_excl_scan(run, s_tmp, &agg);
+    if (tid < kWave) {
+        const int64_t prefix = lb_exclusive_prefix(lb, tile, agg);
+        if (tid == 0) {
+            s_prefix = prefix;
+            if (tile == ntiles - 1) *d_n = prefix + agg;
+        }
+    }
+    __syncthreads();
+    // keep flag in bit 31 of the exclusive in-tile position
+    for (int i = 0; i < kFcItems; ++i) {
+        const int k = tid * kFcItems + i;
+        s_pos[k] = (loc[i] + off) | (s_pos[k] ? int32_t(0x80000000u) : 0);
+    }
+    __syncthreads();
+    const int64_t pre = s_prefix;
+    for (int i = 0; i < kFcItems; ++i) {
+        const int k = i * kBlock + tid;
+        const int32_t v = s_pos[k];
+        if (v < 0) {
+            const int64_t idx = base + k, q = pre + (v & 0x7fffffff);
+            orow[q] = rows[idx];
+            otime[q] = times[idx];
+            oproj[q] = proj[idx];
+        }
+    }
+}
 
 // Rows of src (n rows, in view order; only the first *src_live when given) satisfying pred(row)
 // -> dst (same order).
@@ -53,17 +103,17 @@ void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uin
     dst.time = c->arena.get<int64_t>(n);
     dst.proj = c->arena.get<uint32_t>(n);
     dst.offs = c->arena.get<int64_t>(P + 1);
-    int64_t *flags = c->arena.get<int64_t>(n);
-    int64_t *pos = c->arena.get<int64_t>(n);
     if (n > 0) {
-        k_flag_rows<<<grid_for(n, kBlock, 4096), kBlock, 0, c->stream>>>(rows, n, src_live, pred, flags);
+        const int64_t ntiles = (n + kFcTile - 1) / kFcTile;
+        const Lookback lb = lookback_begin(c, ntiles);
+        k_filter_compact<Pred><<<unsigned(ntiles), kBlock, 0, c->stream>>>(rows, times, proj, n, src_live, pred, lb,
+                                                                          ntiles, dst.row, dst.time, dst.proj,
+                                                                          dst.d_n);
         FZ_LAUNCH_CHECK();
-    }
-    scan_exclusive_i64(c, flags, pos, n, dst.d_n);
-    if (n > 0) {
-        k_compact_view<<<grid_for(n, kBlock, 4096), kBlock, 0, c->stream>>>(rows, times, proj, n, flags, pos,
-                                                                           dst.row, dst.time, dst.proj);
-        FZ_LAUNCH_CHECK();
+        lookback_end(c, ntiles);
+    } else {
+        const int64_t zero = 0;
+        set_i64(c, dst.d_n, &zero, 1);
     }
     k_segment_offsets_dn<<<grid_for(P + 1, kBlock, 1u << 30), kBlock, 0, c->stream>>>(dst.proj, dst.d_n, P, dst.offs);
     FZ_LAUNCH_CHECK();
