@@ -279,42 +279,46 @@ __global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict_
     __shared__ unsigned int s_tile;
 
     const int tid = threadIdx.x;
-    const int w = wave_id();
+    const int w = wave_id(), lane = lane_id();
     if (tid == 0) s_tile = atomicAdd(ticket, 1u) - ticket_base;
-    s_run[tid] = 0;
+    for (int i = 0; i < 4; ++i) s_wcnt[i][tid] = 0;
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t base = tile * kSortTile;
+    // wave w owns the contiguous quarter [w * 1024, (w + 1) * 1024) of the tile; round r covers
+    // its keys r * 64 + lane, so (wave, round, lane) is position order and ranking is stable with
+    // wave-private digit counters - no workgroup barrier inside the ranking loop
+    const int64_t wbase = base + int64_t(w) * (kSortTile / 4);
 
     uint64_t k[kSortItems];
     uint32_t v[kSortItems];
     uint32_t rank[kSortItems];
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
-        const int64_t idx = base + r * kBlock + tid;
+        const int64_t idx = wbase + r * kWave + lane;
         const bool valid = idx < n;
         k[r] = valid ? keys_in[idx] : 0ull;
         v[r] = (HAS_VALS && valid) ? vals_in[idx] : 0u;
     }
-    // stable in-tile ranks: (round, wave, lane) order
+    uint32_t *cnt_w = s_wcnt[w];
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
-        const bool valid = base + r * kBlock + tid < n;
+        const bool valid = wbase + r * kWave + lane < n;
         const uint32_t d = uint32_t(k[r] >> shift) & (kRadix - 1);
-        for (int i = 0; i < 4; ++i) s_wcnt[i][tid] = 0;
-        __syncthreads();
         const uint64_t peers = match_digit<kRadixBits>(d, valid);
-        const uint32_t lrank = uint32_t(__popcll(peers & lanemask_lt()));
-        if (valid && (__ffsll((long long)peers) - 1) == lane_id()) s_wcnt[w][d] = uint32_t(__popcll(peers));
-        __syncthreads();
-        uint32_t wpre = 0;
-        for (int i = 0; i < w; ++i) wpre += s_wcnt[i][d];
-        rank[r] = s_run[d] + wpre + lrank;
-        __syncthreads();
-        s_run[tid] += s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
+        const uint32_t before = valid ? cnt_w[d] : 0u;  // all lanes read before the leader writes
+        rank[r] = before + uint32_t(__popcll(peers & lanemask_lt()));
+        if (valid && (__ffsll((long long)peers) - 1) == lane) cnt_w[d] = before + uint32_t(__popcll(peers));
     }
     __syncthreads();
-    const uint32_t cnt = s_run[tid];
+    // digit tid: tile count and per-wave exclusive offsets (stored back into s_wcnt)
+    uint32_t cnt = 0;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t x = s_wcnt[i][tid];
+        s_wcnt[i][tid] = cnt;
+        cnt += x;
+    }
+    s_run[tid] = cnt;
     // publish this tile's count of digit tid, then look back for the counts of all earlier tiles
     uint64_t *my = &status[tile * kRadix + tid];
     __hip_atomic_store(my, (tile == 0 ? kLbInc : kLbAgg) | epoch | uint64_t(cnt), __ATOMIC_RELAXED,
@@ -350,9 +354,9 @@ __global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict_
     // stage the tile digit-sorted in LDS, then write it out in per-digit runs
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
-        if (base + r * kBlock + tid < n) {
+        if (wbase + r * kWave + lane < n) {
             const uint32_t d = uint32_t(k[r] >> shift) & (kRadix - 1);
-            const uint32_t pos = s_start[d] + rank[r];
+            const uint32_t pos = s_start[d] + cnt_w[d] + rank[r];
             s_keys[pos] = k[r];
             if (HAS_VALS) s_vals[pos] = v[r];
         }
