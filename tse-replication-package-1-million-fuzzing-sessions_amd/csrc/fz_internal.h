@@ -211,6 +211,9 @@ void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, i
 // Stable LSD radix sort of (uint64 key, uint32 value) over bits [0, bits).  Uses arena scratch;
 // the result is written back to keys/vals.
 void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int bits);
+// The same without the copy back: on return keys / vals point at the sorted data (the inputs or
+// arena scratch of the current call).
+void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits);
 // min/max over int64 values skipping FZ_TS_NULL: writes {min, max} to host array.
 void minmax_i64_to_host(fz_ctx *c, const int64_t *const *cols, const int64_t *ns, int ncols,
                         int64_t *host_minmax);

@@ -373,6 +373,16 @@ __global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict_
 }
 
 void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int bits) {
+    uint64_t *k = keys;
+    uint32_t *v = vals;
+    radix_sort_pairs_swap(c, k, v, n, bits);
+    if (k != keys) {
+        FZ_HIP(hipMemcpyAsync(keys, k, size_t(n) * sizeof(uint64_t), hipMemcpyDeviceToDevice, c->stream));
+        if (vals) FZ_HIP(hipMemcpyAsync(vals, v, size_t(n) * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+    }
+}
+
+void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits) {
     if (n <= 1 || bits <= 0) return;
     const int npass = (bits + kRadixBits - 1) / kRadixBits;
     const int64_t nb = (n + kSortTile - 1) / kSortTile;
@@ -420,10 +430,8 @@ void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int 
         std::swap(va, vb);
         ++passes;
     }
-    if (ka != keys) {
-        FZ_HIP(hipMemcpyAsync(keys, ka, size_t(n) * sizeof(uint64_t), hipMemcpyDeviceToDevice, c->stream));
-        if (vals) FZ_HIP(hipMemcpyAsync(vals, va, size_t(n) * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
-    }
+    keys = ka;  // the buffers holding the result (the inputs or arena scratch)
+    vals = va;
     c->store.passes += passes;
 }
 
@@ -629,7 +637,8 @@ uint64_t *sorted_keys_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t
     uint64_t *k = c->arena.get<uint64_t>(nn);
     k_f64_keys<<<grid_for(nn, kBlock, 1024), kBlock, 0, c->stream>>>(x, nmax, d_n, k);
     FZ_LAUNCH_CHECK();
-    radix_sort_pairs(c, k, nullptr, nmax, 64);
+    uint32_t *none = nullptr;
+    radix_sort_pairs_swap(c, k, none, nmax, 64);
     return k;
 }
 

@@ -433,7 +433,7 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_ext *ext_in, const fz_rq1_ou
             k_dedup_ext_keys<<<grid_for(ext.n, kBlock, 2048), kBlock, 0, st>>>(ext, s.num_min, pad, NI, keys, vals);
             FZ_LAUNCH_CHECK();
         }
-        radix_sort_pairs(c, keys, vals, NA, bits_for(pad));
+        radix_sort_pairs_swap(c, keys, vals, NA, bits_for(pad));
         k_dedup_pick<<<g, kBlock, 0, st>>>(vals, keys, mbuild, mbtime, NI, ext, NA, keep);
         FZ_LAUNCH_CHECK();
     }

@@ -76,7 +76,7 @@ void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_i
     if (n > 0) {
         k_session_keys<<<grid_for(n), kBlock, 0, st>>>(session_ids, n, key, idx);
         FZ_LAUNCH_CHECK();
-        radix_sort_pairs(c, key, idx, n, bits_for(uint64_t(S)));  // stable: input order kept per session
+        radix_sort_pairs_swap(c, key, idx, n, bits_for(uint64_t(S)));  // stable: input order kept per session
     }
     double *sv = c->arena.get<double>(n);
     uint32_t *sid = c->arena.get<uint32_t>(n);
@@ -163,7 +163,7 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
         }
         idx[j] = uint32_t(j);
     });
-    radix_sort_pairs(c, key, idx, NC, ibits + pbits);
+    radix_sort_pairs_swap(c, key, idx, NC, ibits + pbits);
     double *sv = o->session_values;
     uint32_t *sid = c->arena.get<uint32_t>(NC);
     map_n(c, NC, nullptr, [=] __device__(int64_t k) {

@@ -352,7 +352,7 @@ void rq4b_session_stats(fz_ctx *c, const double *values, const int64_t *sid, con
     if (n > 0) {
         k_rq4b_keys<<<grid_for(n), kBlock, 0, st>>>(sid, grp, n, key, idx);
         FZ_LAUNCH_CHECK();
-        radix_sort_pairs(c, key, idx, n, bits_for(uint64_t(2 * MM)));
+        radix_sort_pairs_swap(c, key, idx, n, bits_for(uint64_t(2 * MM)));
     }
     double *v2 = c->arena.get<double>(n);
     uint32_t *sid2 = c->arena.get<uint32_t>(n);
@@ -423,7 +423,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
             }
             idx[j] = uint32_t(j);
         });
-        radix_sort_pairs(c, key, idx, NC, sbits + pbits);
+        radix_sort_pairs_swap(c, key, idx, NC, sbits + pbits);
         double *v2 = c->arena.get<double>(NC);
         uint32_t *sid2 = c->arena.get<uint32_t>(NC);
         map_n(c, NC, nullptr, [=] __device__(int64_t k) {

@@ -160,7 +160,7 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
         keys[i] = i < live ? f64_key(src[i]) : ~0ull;
         vals[i] = uint32_t(i);
     });
-    radix_sort_pairs(c, keys, vals, n, 64);
+    radix_sort_pairs_swap(c, keys, vals, n, 64);
     // stage 2: by segment, stable (one segment: already in place)
     if (S > 1) {
         map_n(c, n, nullptr, [=] __device__(int64_t i) {
@@ -168,8 +168,9 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
             const uint32_t j = vals[i];
             keys[i] = int64_t(j) < live ? uint64_t(segid[j]) : uint64_t(S);
         });
-        radix_sort_pairs(c, keys, vals, n, bits_for(uint64_t(S)));
+        radix_sort_pairs_swap(c, keys, vals, n, bits_for(uint64_t(S)));
     }
+    out.pos = reinterpret_cast<int32_t *>(vals);
     double *ov = out.val;
     map_n(c, n, nullptr, [=] __device__(int64_t i) {
         const int64_t live = offs[S];

@@ -200,7 +200,7 @@ static unsigned long long *sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int
     const unsigned g = grid_for(n, kBlock, 4096);
     k_keys_prefix_rows<<<g, kBlock, 0, c->stream>>>(pre, n, keys, vals);
     FZ_LAUNCH_CHECK();
-    radix_sort_pairs(c, keys, vals, n, prefix_bits);
+    radix_sort_pairs_swap(c, keys, vals, n, prefix_bits);
     const int64_t S = int64_t(1) << prefix_bits;
     int64_t *offs = c->arena.get<int64_t>(S + 1);
     k_prefix_offsets<<<grid_for(S + 1, kBlock, 1u << 30), kBlock, 0, c->stream>>>(keys, n, S, offs);
@@ -228,7 +228,7 @@ static void sort_table(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const 
     if (prefix_bits + tbits <= 64) {
         k_keys_full<<<g, kBlock, 0, c->stream>>>(pre, time, n, tmin, tnull, tbits, keys, vals);
         FZ_LAUNCH_CHECK();
-        radix_sort_pairs(c, keys, vals, n, prefix_bits + tbits);
+        radix_sort_pairs_swap(c, keys, vals, n, prefix_bits + tbits);
         const uint64_t pmask = pre.pbits >= 32 ? 0xffffffffull : ((1ull << pre.pbits) - 1ull);
         k_unpack_sorted<<<g, kBlock, 0, c->stream>>>(keys, vals, n, tbits, tmin, tnull, pmask, orow, otime, oproj);
         FZ_LAUNCH_CHECK();
@@ -236,10 +236,10 @@ static void sort_table(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const 
     } else {
         k_keys_time<<<g, kBlock, 0, c->stream>>>(time, n, tmin, tnull, keys, vals);
         FZ_LAUNCH_CHECK();
-        radix_sort_pairs(c, keys, vals, n, tbits);
+        radix_sort_pairs_swap(c, keys, vals, n, tbits);
         k_keys_prefix<<<g, kBlock, 0, c->stream>>>(pre, vals, n, keys);
         FZ_LAUNCH_CHECK();
-        radix_sort_pairs(c, keys, vals, n, prefix_bits);
+        radix_sort_pairs_swap(c, keys, vals, n, prefix_bits);
     }
     k_gather_sorted<<<g, kBlock, 0, c->stream>>>(vals, time, pre.proj, n, orow, otime, oproj);
     FZ_LAUNCH_CHECK();
