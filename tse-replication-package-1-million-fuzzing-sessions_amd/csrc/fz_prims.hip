@@ -11,6 +11,49 @@ namespace fz {
 
 void sync(fz_ctx *c) { FZ_HIP(hipStreamSynchronize(c->stream)); }
 
+constexpr int kMaxFills = 16;
+struct FillList {
+    int n;
+    unsigned char *ptr[kMaxFills];
+    int64_t bytes[kMaxFills];
+    unsigned char value[kMaxFills];
+};
+__global__ __launch_bounds__(kBlock) void k_fill_batch(FillList f) {
+    for (int r = 0; r < f.n; ++r) {
+        unsigned char *p = f.ptr[r];
+        const int64_t nb = f.bytes[r];
+        const unsigned char v = f.value[r];
+        if ((reinterpret_cast<uintptr_t>(p) & 7) == 0) {  // 8-byte stores, byte tail
+            const uint64_t w = 0x0101010101010101ull * v;
+            const int64_t n8 = nb >> 3;
+            for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n8; i += int64_t(gridDim.x) * kBlock)
+                reinterpret_cast<uint64_t *>(p)[i] = w;
+            for (int64_t i = (n8 << 3) + int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nb;
+                 i += int64_t(gridDim.x) * kBlock)
+                p[i] = v;
+        } else {
+            for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nb; i += int64_t(gridDim.x) * kBlock)
+                p[i] = v;
+        }
+    }
+}
+void fill_batch(fz_ctx *c, std::initializer_list<Fill> regions) {
+    FillList f{};
+    int64_t most = 0;
+    for (const Fill &r : regions) {
+        FZ_CHECK(f.n < kMaxFills, "fill_batch: too many regions");
+        if (r.bytes <= 0) continue;
+        f.ptr[f.n] = static_cast<unsigned char *>(r.ptr);
+        f.bytes[f.n] = r.bytes;
+        f.value[f.n] = r.value;
+        most = r.bytes > most ? r.bytes : most;
+        ++f.n;
+    }
+    if (f.n == 0) return;
+    k_fill_batch<<<grid_for((most + 7) / 8, kBlock, 1024), kBlock, 0, c->stream>>>(f);
+    FZ_LAUNCH_CHECK();
+}
+
 struct I64x4 {
     int64_t v[4];
 };
@@ -588,10 +631,9 @@ __device__ inline int64_t upper_bound_u64(const uint64_t *a, int64_t n, uint64_t
     return lo;
 }
 
-__global__ void k_describe_finish(const uint64_t *__restrict__ sk, const int64_t *__restrict__ d_n,
-                                  const double *__restrict__ ms, fz_describe *__restrict__ out) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    const int64_t n = *d_n;
+// fz_describe of n ascending keys sk (global or LDS) with the given mean / std
+__device__ void describe_from_sorted(const uint64_t *sk, int64_t n, double mean, double std,
+                                     fz_describe *__restrict__ out) {
     fz_describe d;
     d.count = n;
     if (n <= 0) {
@@ -601,8 +643,8 @@ __global__ void k_describe_finish(const uint64_t *__restrict__ sk, const int64_t
         *out = d;
         return;
     }
-    d.mean = ms[0];
-    d.std = ms[1];
+    d.mean = mean;
+    d.std = std;
     const uint64_t kneg0 = f64_key(-0.0), kpos0 = f64_key(0.0), kinf = f64_key(INFINITY);
     const int64_t lt0 = lower_bound_u64(sk, n, kneg0);
     const int64_t le0 = upper_bound_u64(sk, n, kpos0);
@@ -631,6 +673,69 @@ __global__ void k_describe_finish(const uint64_t *__restrict__ sk, const int64_t
     *out = d;
 }
 
+__global__ void k_describe_finish(const uint64_t *__restrict__ sk, const int64_t *__restrict__ d_n,
+                                  const double *__restrict__ ms, fz_describe *__restrict__ out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    describe_from_sorted(sk, *d_n, ms[0], ms[1], out);
+}
+
+// The whole describe of n <= 4096 values in one 1024-thread workgroup: LDS bitonic sort of the
+// keys, double-double sums of x and (x - mean)^2 (as k_dd_partial / k_dd_final), finish.
+constexpr int kDescSmall = 4096;
+__device__ inline DD block_dd_sum_1024(DD acc, double *s_hi, double *s_lo) {
+    acc = wave_dd_sum(acc);
+    if (lane_id() == 0) {
+        s_hi[wave_id()] = acc.hi;
+        s_lo[wave_id()] = acc.lo;
+    }
+    __syncthreads();
+    DD t{s_hi[0], s_lo[0]};
+    for (int i = 1; i < kSortBlock / kWave; ++i) t = dd_add(t, DD{s_hi[i], s_lo[i]});
+    __syncthreads();
+    return t;
+}
+
+__global__ __launch_bounds__(kSortBlock) void k_describe_small(const double *__restrict__ x,
+                                                               const int64_t *__restrict__ d_n,
+                                                               fz_describe *__restrict__ out) {
+    __shared__ uint64_t sk[kDescSmall];
+    __shared__ double s_hi[kSortBlock / kWave], s_lo[kSortBlock / kWave];
+    const int tid = threadIdx.x;
+    const int n = int(*d_n);
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    DD acc{0.0, 0.0};
+    for (int i = tid; i < np2; i += kSortBlock) {
+        const double v = i < n ? x[i] : 0.0;
+        sk[i] = i < n ? f64_key(v) : ~0ull;
+        if (i < n) acc = dd_add_d(acc, v);
+    }
+    DD t = block_dd_sum_1024(acc, s_hi, s_lo);
+    const double mean = n > 0 ? (t.hi + t.lo) / double(n) : NAN;
+    acc = DD{0.0, 0.0};
+    for (int i = tid; i < n; i += kSortBlock) {
+        double v = x[i] - mean;
+        v = v * v;
+        acc = dd_add_d(acc, v);
+    }
+    t = block_dd_sum_1024(acc, s_hi, s_lo);
+    const double std = n > 0 ? sqrt((t.hi + t.lo) / double(n)) : NAN;
+    for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int q = tid; q < (np2 >> 1); q += kSortBlock) {
+                const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1)), ixj = i + j;
+                const uint64_t a = sk[i], b = sk[ixj];
+                if ((a > b) == ((i & k) == 0)) {
+                    sk[i] = b;
+                    sk[ixj] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (tid == 0) describe_from_sorted(sk, n, mean, std, out);
+}
+
 uint64_t *sorted_keys_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n) {
     if (nmax <= 4096) return sort_small_keys(c, x, nmax < 1 ? 1 : nmax, d_n);  // one workgroup, LDS
     const int64_t nn = nmax < 1 ? 1 : nmax;
@@ -643,6 +748,11 @@ uint64_t *sorted_keys_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t
 }
 
 void describe_f64_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n, fz_describe *dev_out) {
+    if (nmax <= kDescSmall) {  // one launch
+        k_describe_small<<<1, kSortBlock, 0, c->stream>>>(x, d_n, dev_out);
+        FZ_LAUNCH_CHECK();
+        return;
+    }
     describe_sorted_dn(c, sorted_keys_dn(c, x, nmax, d_n), x, nmax, d_n, dev_out);
 }
 

@@ -345,8 +345,7 @@ __global__ __launch_bounds__(kBlock) void k_late_copy(const double *__restrict__
 void rq1_finish(fz_ctx *c, int64_t threshold, const int64_t *iter_total, const int64_t *iter_det, int64_t M,
                 int64_t *counts, fz_describe *late_out) {
     hipStream_t st = c->stream;
-    FZ_HIP(hipMemsetAsync(counts + FZ_RQ1_KEPT_ITERS, 0, sizeof(int64_t), st));
-    FZ_HIP(hipMemsetAsync(counts + FZ_RQ1_FIRST_DOWN, 0xff, sizeof(int64_t), st));
+    fill_batch(c, {{counts + FZ_RQ1_KEPT_ITERS, 8, 0}, {counts + FZ_RQ1_FIRST_DOWN, 8, 0xff}});
     double *rates = c->arena.get<double>(M);
     double *late = c->arena.get<double>(M);
     int64_t *late_lo = c->arena.get<int64_t>(2);
@@ -374,17 +373,20 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_ext *ext_in, const fz_rq1_ou
     const int64_t P = s.P;
     const int64_t M = s.fuzz.max_seg;
     hipStream_t st = c->stream;
-    FZ_HIP(hipMemsetAsync(o->counts, 0, FZ_RQ1_NCOUNTS * sizeof(int64_t), st));
-    FZ_HIP(hipMemsetAsync(o->counts + FZ_RQ1_FIRST_DOWN, 0xff, sizeof(int64_t), st));
-    FZ_HIP(hipMemsetAsync(o->iter_total, 0, size_t(M > 0 ? M : 1) * 8, st));
-    FZ_HIP(hipMemsetAsync(o->iter_detected, 0, size_t(M > 0 ? M : 1) * 8, st));
+    int64_t *hist = c->arena.get<int64_t>(M + 1);
+    uint8_t *flags = c->arena.get<uint8_t>(4 * P);
+    fill_batch(c, {{o->counts, FZ_RQ1_FIRST_DOWN * 8, 0},
+                   {o->counts + FZ_RQ1_FIRST_DOWN, 8, 0xff},
+                   {o->counts + FZ_RQ1_FIRST_DOWN + 1, (FZ_RQ1_NCOUNTS - FZ_RQ1_FIRST_DOWN - 1) * 8, 0},
+                   {o->iter_total, (M > 0 ? M : 1) * 8, 0},
+                   {o->iter_detected, (M > 0 ? M : 1) * 8, 0},
+                   {hist, (M + 1) * 8, 0},
+                   {flags, 4 * (P > 0 ? P : 1), 0}});
 
     // eligibility (:144-152)
     eligible_projects(c, o->eligible, o->counts + FZ_RQ1_ELIGIBLE);
 
     // phase 1: projects alive at each iteration (:189-203)
-    int64_t *hist = c->arena.get<int64_t>(M + 1);
-    FZ_HIP(hipMemsetAsync(hist, 0, size_t(M + 1) * 8, st));
     if (P > 0) {
         k_iter_hist<<<grid_for(P), kBlock, 0, st>>>(s.fuzz.offs, o->eligible, P, hist, o->counts);
         FZ_LAUNCH_CHECK();
@@ -404,8 +406,6 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_ext *ext_in, const fz_rq1_ou
 
     // issues pass
     const int64_t NI = s.issues.n;
-    uint8_t *flags = c->arena.get<uint8_t>(4 * P);
-    FZ_HIP(hipMemsetAsync(flags, 0, size_t(4 * (P > 0 ? P : 1)), st));
     uint8_t *f_lim = flags, *f_fixlim = flags + P, *f_tgt = flags + 2 * P, *f_match = flags + 3 * P;
     int64_t *mbuild = c->arena.get<int64_t>(NI);
     int64_t *mbtime = c->arena.get<int64_t>(NI);

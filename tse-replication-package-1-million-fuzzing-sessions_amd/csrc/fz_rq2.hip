@@ -256,10 +256,12 @@ void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
              "fz_rq2_add: null output buffer");
     const fz_tables &t = s.t;
     const int64_t P = s.P;
-    hipStream_t st = c->stream;
-    FZ_HIP(hipMemsetAsync(o->counts, 0, FZ_RQ2A_NCOUNTS * 8, st));
-    FZ_HIP(hipMemsetAsync(o->covered_is_float, 0, size_t(P > 0 ? P : 1), st));
-    FZ_HIP(hipMemsetAsync(o->total_is_float, 0, size_t(P > 0 ? P : 1), st));
+    uint8_t *anyc = c->arena.get<uint8_t>(P), *anyt = c->arena.get<uint8_t>(P);
+    fill_batch(c, {{o->counts, FZ_RQ2A_NCOUNTS * 8, 0},
+                   {o->covered_is_float, P > 0 ? P : 1, 0},
+                   {o->total_is_float, P > 0 ? P : 1, 0},
+                   {anyc, P > 0 ? P : 1, 0},
+                   {anyt, P > 0 ? P : 1, 0}});
     eligible_projects(c, o->eligible, o->counts + FZ_RQ2A_ELIGIBLE);
 
     TmpView B, CV;
@@ -271,9 +273,6 @@ void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
     const int64_t *boffs = B.offs, *coffs = CV.offs;
     // pandas upcast flags: a NULL covered/total among the project's fetched coverage rows
     {
-        uint8_t *anyc = c->arena.get<uint8_t>(P), *anyt = c->arena.get<uint8_t>(P);
-        FZ_HIP(hipMemsetAsync(anyc, 0, size_t(P > 0 ? P : 1), st));
-        FZ_HIP(hipMemsetAsync(anyt, 0, size_t(P > 0 ? P : 1), st));
         const int32_t *crow = CV.row;
         const uint32_t *cproj = CV.proj;
         const uint8_t *valid = t.c_valid;

@@ -67,14 +67,18 @@ void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
     const fz_tables &t = s.t;
     const int64_t P = s.P, M = s.fuzz.max_seg, NI = s.issues.n;
     const int64_t MM = M > 0 ? M : 1;
-    hipStream_t st = c->stream;
     int64_t *counts = o->counts;
     double *sc = o->scalars;
-    FZ_HIP(hipMemsetAsync(counts, 0, FZ_RQ4A_NCOUNTS * 8, st));
-    for (int64_t *a : {o->g1_total, o->g1_det, o->g2_total, o->g2_det}) FZ_HIP(hipMemsetAsync(a, 0, MM * 8, st));
-    FZ_HIP(hipMemsetAsync(o->intro, 0xff, size_t(P > 0 ? P : 1) * 8, st));
-    FZ_HIP(hipMemsetAsync(o->g4_steps, 0, 30 * 8, st));
-    FZ_HIP(hipMemsetAsync(o->g4_transition, 0, 4 * 8, st));
+    int64_t *hist = c->arena.get<int64_t>(2 * (M + 1));
+    fill_batch(c, {{counts, FZ_RQ4A_NCOUNTS * 8, 0},
+                   {o->g1_total, MM * 8, 0},
+                   {o->g1_det, MM * 8, 0},
+                   {o->g2_total, MM * 8, 0},
+                   {o->g2_det, MM * 8, 0},
+                   {o->intro, (P > 0 ? P : 1) * 8, 0xff},
+                   {o->g4_steps, 30 * 8, 0},
+                   {o->g4_transition, 4 * 8, 0},
+                   {hist, 2 * (M + 1) * 8, 0}});
     int64_t *scratch = c->arena.get<int64_t>(4);
     eligible_projects(c, o->eligible, scratch);
     group_members(c, g, o->eligible, o->member, counts + FZ_RQ4A_G1, true);
@@ -86,8 +90,6 @@ void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
     const int64_t *fboffs = FB.offs, *fbtime = FB.time, *fioffs = FI.offs, *fitime = FI.time;
 
     // totals[i] += 1 for i = 1..#builds, per group (:339-340)
-    int64_t *hist = c->arena.get<int64_t>(2 * (M + 1));
-    FZ_HIP(hipMemsetAsync(hist, 0, size_t(2 * (M + 1)) * 8, st));
     per_seg(c, P, [=] __device__(int64_t p) {
         const int64_t nb = fboffs[p + 1] - fboffs[p];
         const uint8_t b = member[p];

@@ -97,15 +97,32 @@ __global__ __launch_bounds__(kBlock) void k_count_types(const uint8_t *__restric
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_max_seg(const int64_t *__restrict__ offs, int64_t P,
-                                                    unsigned long long *__restrict__ out) {
-    int64_t m = 0;
-    for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < P; p += int64_t(gridDim.x) * kBlock) {
-        const int64_t l = offs[p + 1] - offs[p];
-        m = l > m ? l : m;
+
+// One workgroup: the longest segment of each of 4 views (out[0..3]) and a copy of the 3
+// long-segment counters (out[4..6]) - one launch and one D2H copy for the host's store stats.
+struct Offs4 {
+    const int64_t *offs[4];
+    const unsigned long long *big[3];
+};
+__global__ __launch_bounds__(kSortBlock) void k_store_stats(Offs4 v, int64_t P, int64_t *__restrict__ out) {
+    __shared__ int64_t s_m[kSortBlock / kWave];
+    for (int i = 0; i < 4; ++i) {
+        int64_t m = 0;
+        for (int64_t p = threadIdx.x; p < P; p += kSortBlock) {
+            const int64_t l = v.offs[i][p + 1] - v.offs[i][p];
+            m = l > m ? l : m;
+        }
+        m = wave_max(m);
+        if (lane_id() == 0) s_m[wave_id()] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t r = 0;
+            for (int w = 0; w < kSortBlock / kWave; ++w) r = s_m[w] > r ? s_m[w] : r;
+            out[i] = r;
+        }
+        __syncthreads();
     }
-    m = wave_max(m);
-    if (lane_id() == 0) atomicMax(out, (unsigned long long)m);
+    if (threadIdx.x < 3) out[4 + threadIdx.x] = int64_t(*v.big[threadIdx.x]);
 }
 
 // ---- fast path: prefix LSD (2 passes) + per-segment LDS sort by (time, row) -----------------
@@ -330,18 +347,12 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     };
     make_views();
     // longest segments (sizes the per-iteration outputs) + rows left for the full-key path
-    unsigned long long *mx = c->arena.get<unsigned long long>(4);
+    int64_t *mx = c->arena.get<int64_t>(8);
     auto read_stats = [&]() {
-        FZ_HIP(hipMemsetAsync(mx, 0, 32, c->stream));
-        const View *vs[4] = {&s.fuzz, &s.covb, &s.cov, &s.issues};
-        for (int i = 0; i < 4; ++i) {
-            if (P <= 0) break;
-            k_max_seg<<<grid_for(P, kBlock, 64), kBlock, 0, c->stream>>>(vs[i]->offs, P, mx + i);
-            FZ_LAUNCH_CHECK();
-        }
-        FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 32, hipMemcpyDeviceToHost, c->stream));
-        for (int k = 0; k < 3; ++k)
-            FZ_HIP(hipMemcpyAsync(c->h_pinned + 4 + k, big[k], 8, hipMemcpyDeviceToHost, c->stream));
+        Offs4 v{{s.fuzz.offs, s.covb.offs, s.cov.offs, s.issues.offs}, {big[0], big[1], big[2]}};
+        k_store_stats<<<1, kSortBlock, 0, c->stream>>>(v, P, mx);
+        FZ_LAUNCH_CHECK();
+        FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 7 * 8, hipMemcpyDeviceToHost, c->stream));
         sync(c);
     };
     read_stats();
