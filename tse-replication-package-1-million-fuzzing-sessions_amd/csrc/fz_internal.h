@@ -142,6 +142,14 @@ struct Store {
     // eligible projects (the GROUP BY/HAVING every script starts from), computed once per load
     DevBuf elig;     // uint8 [P]
     DevBuf n_elig;   // int64 [1]
+    // The tables themselves in sorted order: after the build `t` points at these sorted copies and
+    // every view's row id IS the position in its sorted table, so filters and joins read columns
+    // sequentially instead of gathering through the sort permutation.  perm maps a sorted
+    // position back to the caller's row id (for row-id outputs: matched issues / builds, change
+    // rows, detected issues).
+    DevBuf sb_type, sb_result, sb_group, sb_canon, sc_coverage, sc_covered, sc_total, sc_valid, si_number, si_status;
+    DevBuf b_perm, c_perm, i_perm;
+    const int32_t *bperm = nullptr, *cperm = nullptr, *iperm = nullptr;
 };
 
 // Per-kernel timing probe (fz_probe_begin/end): brackets every launch of ONE named kernel with

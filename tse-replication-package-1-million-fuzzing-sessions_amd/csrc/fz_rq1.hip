@@ -278,13 +278,15 @@ __global__ __launch_bounds__(kBlock) void k_matched_out(View iss, const int64_t 
                                                         const int64_t *__restrict__ mbuild, View fuzz,
                                                         int64_t *__restrict__ out_issue,
                                                         int64_t *__restrict__ out_build, int64_t *__restrict__ it_arr,
-                                                        uint32_t *__restrict__ p_arr, uint8_t *__restrict__ f_match) {
+                                                        uint32_t *__restrict__ p_arr, uint8_t *__restrict__ f_match,
+                                                        const int32_t *__restrict__ iperm,
+                                                        const int32_t *__restrict__ bperm) {
     for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < iss.n; j += int64_t(gridDim.x) * kBlock) {
         if (!keep[j]) continue;
         const int64_t q = pos[j];
         const uint32_t p = iss.proj[j];
-        out_issue[q] = iss.row[j];
-        out_build[q] = mbuild[j];
+        out_issue[q] = iperm[iss.row[j]];
+        out_build[q] = bperm[mbuild[j]];
         const int64_t lo = fuzz.offs[p], hi = fuzz.offs[p + 1];
         it_arr[q] = lower_bound_i64(fuzz.time, lo, hi, iss.time[j]) - lo;
         p_arr[q] = p;
@@ -445,7 +447,7 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_ext *ext_in, const fz_rq1_ou
     if (NI > 0) {
         const unsigned g = grid_for(NI, kBlock, 2048);
         k_matched_out<<<g, kBlock, 0, st>>>(s.issues, keep, pos, mbuild, s.fuzz, o->matched_issue, o->matched_build,
-                                            it_arr, p_arr, f_match);
+                                            it_arr, p_arr, f_match, s.iperm, s.bperm);
         k_distinct_iter<<<g, kBlock, 0, st>>>(it_arr, p_arr, d_nm, o->iter_detected);
         FZ_LAUNCH_CHECK();
     }

@@ -324,6 +324,7 @@ void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
     const int64_t *cov_c = t.c_covered, *cov_t = t.c_total;
     const uint8_t *valid = t.c_valid;
     const fz_rq2_add_out out = *o;
+    const int32_t *bperm = s.bperm, *cperm = s.cperm;  // sorted positions -> the caller's row ids
     map_n(c, NB, nullptr, [=] __device__(int64_t r) {
         if (!pflag[r]) return;
         const int64_t q = ppos[r];
@@ -348,11 +349,11 @@ void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
             dc = (cv1 / tv1) * 100.0 - (cv0 / tv0) * 100.0;
         }
         out.row_project[q] = p;
-        out.row_first_build[q] = f;
-        out.row_end_build[q] = e;
-        out.row_start_build[q] = sb;
-        out.row_cov_i[q] = c0;
-        out.row_cov_i1[q] = c1;
+        out.row_first_build[q] = bperm[f];
+        out.row_end_build[q] = bperm[e];
+        out.row_start_build[q] = bperm[sb];
+        out.row_cov_i[q] = c0 >= 0 ? cperm[c0] : -1;
+        out.row_cov_i1[q] = c1 >= 0 ? cperm[c1] : -1;
         out.diff_total[q] = dt;
         out.diff_coverage[q] = dc;
     });

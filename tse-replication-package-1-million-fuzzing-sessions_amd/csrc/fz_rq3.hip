@@ -143,6 +143,7 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     uint32_t *dproj = c->arena.get<uint32_t>(NI);
     int64_t *dday = c->arena.get<int64_t>(NI);
     const fz_rq3_out out = *o;
+    const int32_t *iperm = s.iperm;  // sorted positions -> the caller's issue row ids
     map_n(c, NI, nullptr, [=] __device__(int64_t j) {
         if (!dflag[j]) return;
         const int64_t q = dpos[j];
@@ -151,7 +152,7 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         out.det_cov[q] = cvd[rb] - cvd[ra];
         out.det_tot[q] = ctot[rb] - ctot[ra];
         out.det_project[q] = iproj[j];
-        out.det_issue[q] = irow[j];
+        out.det_issue[q] = iperm[irow[j]];
         dproj[q] = iproj[j];
         dday[q] = fdiv_day(irts[j]);
     });

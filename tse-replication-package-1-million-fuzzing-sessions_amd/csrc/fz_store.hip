@@ -277,6 +277,91 @@ static View make_view(fz_ctx *c, const int32_t *row, const int64_t *time, const 
 
 void store_eligibility(fz_ctx *c);  // fz_rq1.hip
 
+// Gather every column into its table's sorted order (row ids become positions; perm keeps the
+// caller's ids) and point s.t at the sorted copies.
+__global__ __launch_bounds__(kBlock) void k_sorted_builds(fz_tables t, int64_t n, int32_t *__restrict__ row,
+                                                          int32_t *__restrict__ perm, uint8_t *__restrict__ type,
+                                                          uint8_t *__restrict__ result, int32_t *__restrict__ group,
+                                                          int32_t *__restrict__ canon) {
+    for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < n; k += int64_t(gridDim.x) * kBlock) {
+        const int32_t r = row[k];
+        perm[k] = r;
+        row[k] = int32_t(k);
+        type[k] = t.b_type[r];
+        result[k] = t.b_result[r];
+        group[k] = t.b_group[r];
+        canon[k] = t.b_rev_canon[r];
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_sorted_coverage(fz_tables t, int64_t n, int32_t *__restrict__ row,
+                                                            int32_t *__restrict__ perm, double *__restrict__ cov,
+                                                            int64_t *__restrict__ covered, int64_t *__restrict__ total,
+                                                            uint8_t *__restrict__ valid) {
+    for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < n; k += int64_t(gridDim.x) * kBlock) {
+        const int32_t r = row[k];
+        perm[k] = r;
+        row[k] = int32_t(k);
+        cov[k] = t.c_coverage[r];
+        covered[k] = t.c_covered[r];
+        total[k] = t.c_total[r];
+        valid[k] = t.c_valid[r];
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_sorted_issues(fz_tables t, int64_t n, int32_t *__restrict__ row,
+                                                          int32_t *__restrict__ perm, int64_t *__restrict__ number,
+                                                          uint8_t *__restrict__ status) {
+    for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < n; k += int64_t(gridDim.x) * kBlock) {
+        const int32_t r = row[k];
+        perm[k] = r;
+        row[k] = int32_t(k);
+        number[k] = t.i_number[r];
+        status[k] = t.i_status[r];
+    }
+}
+
+static void materialize_sorted(fz_ctx *c, const fz_tables &in) {
+    Store &s = c->store;
+    const int64_t nb = in.n_builds, nc = in.n_cov, ni = in.n_issues;
+    fz_tables &t = s.t;
+    if (nb > 0) {
+        k_sorted_builds<<<grid_for(nb, kBlock, 4096), kBlock, 0, c->stream>>>(
+            in, nb, s.b_row.as<int32_t>(), s.b_perm.ensure<int32_t>(nb), s.sb_type.ensure<uint8_t>(nb),
+            s.sb_result.ensure<uint8_t>(nb), s.sb_group.ensure<int32_t>(nb), s.sb_canon.ensure<int32_t>(nb));
+        FZ_LAUNCH_CHECK();
+    }
+    if (nc > 0) {
+        k_sorted_coverage<<<grid_for(nc, kBlock, 4096), kBlock, 0, c->stream>>>(
+            in, nc, s.c_row.as<int32_t>(), s.c_perm.ensure<int32_t>(nc), s.sc_coverage.ensure<double>(nc),
+            s.sc_covered.ensure<int64_t>(nc), s.sc_total.ensure<int64_t>(nc), s.sc_valid.ensure<uint8_t>(nc));
+        FZ_LAUNCH_CHECK();
+    }
+    if (ni > 0) {
+        k_sorted_issues<<<grid_for(ni, kBlock, 4096), kBlock, 0, c->stream>>>(
+            in, ni, s.i_row.as<int32_t>(), s.i_perm.ensure<int32_t>(ni), s.si_number.ensure<int64_t>(ni),
+            s.si_status.ensure<uint8_t>(ni));
+        FZ_LAUNCH_CHECK();
+    }
+    s.bperm = s.b_perm.ensure<int32_t>(nb);
+    s.cperm = s.c_perm.ensure<int32_t>(nc);
+    s.iperm = s.i_perm.ensure<int32_t>(ni);
+    t.b_project = s.b_proj.ensure<uint32_t>(nb);
+    t.b_type = s.sb_type.ensure<uint8_t>(nb);
+    t.b_result = s.sb_result.ensure<uint8_t>(nb);
+    t.b_time = s.b_time.ensure<int64_t>(nb);
+    t.b_group = s.sb_group.ensure<int32_t>(nb);
+    t.b_rev_canon = s.sb_canon.ensure<int32_t>(nb);
+    t.c_project = s.c_proj.ensure<uint32_t>(nc);
+    t.c_date = s.c_time.ensure<int64_t>(nc);
+    t.c_coverage = s.sc_coverage.ensure<double>(nc);
+    t.c_covered = s.sc_covered.ensure<int64_t>(nc);
+    t.c_total = s.sc_total.ensure<int64_t>(nc);
+    t.c_valid = s.sc_valid.ensure<uint8_t>(nc);
+    t.i_number = s.si_number.ensure<int64_t>(ni);
+    t.i_project = s.i_proj.ensure<uint32_t>(ni);
+    t.i_rts = s.i_time.ensure<int64_t>(ni);
+    t.i_status = s.si_status.ensure<uint8_t>(ni);
+}
+
 void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     FZ_CHECK(t != nullptr, "fz_store_build: tables is null");
     FZ_CHECK(t->n_projects >= 0 && t->n_builds >= 0 && t->n_cov >= 0 && t->n_issues >= 0, "negative table size");
@@ -369,6 +454,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         make_views();
         read_stats();
     }
+    materialize_sorted(c, *t);
     s.fuzz.max_seg = c->h_pinned[0];
     s.covb.max_seg = c->h_pinned[1];
     s.cov.max_seg = c->h_pinned[2];
