@@ -61,22 +61,33 @@ __global__ __launch_bounds__(kBlock) void k_elig_atomic(const uint32_t *__restri
         if ((valid[i] & FZ_VALID_COVERAGE) && cov[i] > 0.0 && date[i] < limit) atomicAdd(&counts[proj[i]], 1);
 }
 
+// Column sums of the [nb][P] partial table: a workgroup owns 64 projects (one per lane, coalesced
+// rows), its 4 waves split the nb partial rows, LDS adds the 4 wave sums.  part == null: counts
+// are already final (atomic fallback), only the flags are derived.
 __global__ __launch_bounds__(kBlock) void k_elig_sum(const int32_t *__restrict__ part, int nb, int64_t P,
                                                      int32_t *__restrict__ counts, uint8_t *__restrict__ elig,
                                                      int64_t *__restrict__ n_elig) {
-    for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < P; p += int64_t(gridDim.x) * kBlock) {
-        int32_t s = 0;
-        if (part) {
-            for (int b = 0; b < nb; ++b) s += part[int64_t(b) * P + p];
-            if (counts) counts[p] = s;
-        } else {
-            s = counts[p];
-        }
-        if (elig) {
-            const bool e = s >= kEligMin;
-            elig[p] = e;
-            if (e) atomic_add_i64(n_elig, 1);
-        }
+    __shared__ int32_t s_sum[4][kWave];
+    const int64_t p = int64_t(blockIdx.x) * kWave + lane_id();
+    const int w = wave_id();
+    int32_t s = 0;
+    if (part && p < P) {
+#pragma unroll 8
+        for (int b = w; b < nb; b += 4) s += part[int64_t(b) * P + p];
+    }
+    s_sum[w][lane_id()] = s;
+    __syncthreads();
+    if (w != 0 || p >= P) return;
+    if (part) {
+        s = s_sum[0][lane_id()] + s_sum[1][lane_id()] + s_sum[2][lane_id()] + s_sum[3][lane_id()];
+        if (counts) counts[p] = s;
+    } else {
+        s = counts[p];
+    }
+    if (elig) {
+        const bool e = s >= kEligMin;
+        elig[p] = e;
+        if (e) atomic_add_i64(n_elig, 1);
     }
 }
 
@@ -92,13 +103,13 @@ static void eligibility(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *c
         int32_t *part = c->arena.get<int32_t>(int64_t(nb) * P);
         k_elig_hist<<<nb, kBlock, size_t(P) * 4, c->stream>>>(t->c_project, t->c_date, t->c_coverage, t->c_valid,
                                                                t->n_cov, P, limit, part);
-        k_elig_sum<<<grid_for(P), kBlock, 0, c->stream>>>(part, nb, P, counts, elig, n_elig);
+        k_elig_sum<<<unsigned((P + kWave - 1) / kWave), kBlock, 0, c->stream>>>(part, nb, P, counts, elig, n_elig);
     } else {
         if (!counts) counts = c->arena.get<int32_t>(P);
         FZ_HIP(hipMemsetAsync(counts, 0, size_t(P) * 4, c->stream));
         k_elig_atomic<<<grid_for(t->n_cov, kBlock, 2048), kBlock, 0, c->stream>>>(
             t->c_project, t->c_date, t->c_coverage, t->c_valid, t->n_cov, limit, counts);
-        k_elig_sum<<<grid_for(P), kBlock, 0, c->stream>>>(nullptr, 0, P, counts, elig, n_elig);
+        k_elig_sum<<<unsigned((P + kWave - 1) / kWave), kBlock, 0, c->stream>>>(nullptr, 0, P, counts, elig, n_elig);
     }
     FZ_LAUNCH_CHECK();
 }

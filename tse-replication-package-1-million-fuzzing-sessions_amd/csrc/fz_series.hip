@@ -83,27 +83,30 @@ const int64_t *single_segment(fz_ctx *c, const int64_t *d_n) {
 // One workgroup per segment of <= kLdsSortMax values: bitonic network over (key, position) pairs
 // in LDS (48 KiB), padded to a power of two with +inf keys.  Ties may come out in any order -
 // every consumer (ranks, percentiles, rank tests) is invariant to the order inside a tie group.
-__global__ __launch_bounds__(kSortBlock) void k_seg_sort_lds(const double *__restrict__ src,
-                                                         const int64_t *__restrict__ offs, int64_t S,
-                                                         double *__restrict__ out_val, int32_t *__restrict__ out_pos,
-                                                         uint64_t *__restrict__ out_key) {
-    __shared__ uint64_t sk[kLdsSortMax];
-    __shared__ int32_t sp[kLdsSortMax];
+// Two instantiations: BS = 256 threads for segments of <= 1024 values (small LDS footprint, many
+// workgroups per CU) and BS = 1024 for 1025..4096; each skips the other's segments.
+template <int BS, int MAXN>
+__global__ __launch_bounds__(BS) void k_seg_sort_lds(const double *__restrict__ src, const int64_t *__restrict__ offs,
+                                                     int64_t S, double *__restrict__ out_val,
+                                                     int32_t *__restrict__ out_pos, uint64_t *__restrict__ out_key) {
+    __shared__ uint64_t sk[MAXN];
+    __shared__ int32_t sp[MAXN];
+    constexpr int kMinN = MAXN / 4;
     const int tid = threadIdx.x;
     for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
         const int64_t b = offs[s];
         const int n = int(offs[s + 1] - b);
-        if (n <= 0) continue;
+        if (n <= 0 || n > MAXN || (MAXN == kLdsSortMax && n <= kMinN)) continue;
         int np2 = 1;
         while (np2 < n) np2 <<= 1;
-        for (int i = tid; i < np2; i += kSortBlock) {
+        for (int i = tid; i < np2; i += BS) {
             sk[i] = i < n ? f64_key(src[b + i]) : ~0ull;
             sp[i] = i;
         }
         __syncthreads();
         for (int k = 2; k <= np2; k <<= 1) {
             for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int t = tid; t < (np2 >> 1); t += kSortBlock) {  // every thread owns a pair
+                for (int t = tid; t < (np2 >> 1); t += BS) {  // every thread owns a pair
                     const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;  // j = 2^m
                     {
                         const uint64_t a = sk[i], d = sk[ixj];
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(kSortBlock) void k_seg_sort_lds(const double *__res
                 __syncthreads();
             }
         }
-        for (int i = tid; i < n; i += kSortBlock) {
+        for (int i = tid; i < n; i += BS) {
             if (out_val) out_val[b + i] = f64_from_key(sk[i]);
             if (out_pos) out_pos[b + i] = int32_t(b + sp[i]);
             if (out_key) out_key[b + i] = sk[i];
@@ -129,12 +132,20 @@ __global__ __launch_bounds__(kSortBlock) void k_seg_sort_lds(const double *__res
     }
 }
 
+// Every segment of <= kLdsSortMax values (len_bound: a host bound of the longest one).
+static void launch_seg_sort_lds(fz_ctx *c, unsigned g, const double *src, const int64_t *offs, int64_t S,
+                                int64_t len_bound, double *val, int32_t *pos, uint64_t *key) {
+    k_seg_sort_lds<256, 1024><<<g, 256, 0, c->stream>>>(src, offs, S, val, pos, key);
+    if (len_bound > 1024)
+        k_seg_sort_lds<kSortBlock, kLdsSortMax><<<g, kSortBlock, 0, c->stream>>>(src, offs, S, val, pos, key);
+    FZ_LAUNCH_CHECK();
+}
+
 uint64_t *sort_small_keys(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n) {
     uint64_t *k = c->arena.get<uint64_t>(nmax);
     const int64_t *offs = single_segment(c, d_n);
     map_n(c, nmax, nullptr, [=] __device__(int64_t i) { k[i] = ~0ull; });  // entries past *d_n
-    k_seg_sort_lds<<<1, kSortBlock, 0, c->stream>>>(x, offs, 1, nullptr, nullptr, k);
-    FZ_LAUNCH_CHECK();
+    launch_seg_sort_lds(c, 1, x, offs, 1, nmax, nullptr, nullptr, k);
     return k;
 }
 
@@ -146,8 +157,7 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
     if (n <= 0) return out;
     if (sg.len_bound() <= kLdsSortMax) {
         const unsigned g = unsigned(sg.S < 8192 ? (sg.S > 0 ? sg.S : 1) : 8192);
-        k_seg_sort_lds<<<g, kSortBlock, 0, c->stream>>>(src, sg.offs, sg.S, out.val, out.pos, nullptr);
-        FZ_LAUNCH_CHECK();
+        launch_seg_sort_lds(c, g, src, sg.offs, sg.S, sg.len_bound(), out.val, out.pos, nullptr);
         return out;
     }
     uint64_t *keys = c->arena.get<uint64_t>(n);

@@ -149,54 +149,55 @@ __global__ __launch_bounds__(kBlock) void k_prefix_offsets(const uint64_t *__res
     offs[s] = lo;
 }
 
-// One workgroup per prefix segment (<= kSegSortMax rows, already in row order): bitonic sort of
-// (time, position) pairs in LDS - the position tie-break keeps equal times in row order (stable).
-__global__ __launch_bounds__(kSortBlock) void k_seg_time_sort(const uint32_t *__restrict__ rows,
-                                                          const int64_t *__restrict__ time,
-                                                          const int64_t *__restrict__ offs, int64_t S, uint32_t pmask,
-                                                          int32_t *__restrict__ orow, int64_t *__restrict__ otime,
-                                                          uint32_t *__restrict__ oproj,
-                                                          unsigned long long *__restrict__ big) {
-    __shared__ int64_t st[kSegSortMax];
-    __shared__ int32_t si[kSegSortMax];
+// One workgroup per prefix segment, already in row order: bitonic sort of (time, position) pairs in
+// LDS - the position tie-break keeps equal times in row order (stable).  Longer segments are
+// counted into *big (the host re-sorts that table on the full-key path).  (Size-class variants -
+// 256 / 512 / 1024 threads for <= 1024 / 2048 / 4096 rows - measured slower in total: each class
+// launch still walks every segment.)
+template <int BS, int MAXN>
+__global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict__ rows, const int64_t *__restrict__ time,
+                                                      const int64_t *__restrict__ offs, int64_t S, uint32_t pmask,
+                                                      int32_t *__restrict__ orow, int64_t *__restrict__ otime,
+                                                      uint32_t *__restrict__ oproj, unsigned long long *__restrict__ big) {
+    __shared__ int64_t st[MAXN];
+    __shared__ int32_t si[MAXN];
     const int tid = threadIdx.x;
+
     for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
         const int64_t b = offs[s];
         const int64_t len = offs[s + 1] - b;
         if (len <= 0) continue;
-        if (len > kSegSortMax) {  // the host re-sorts the table on the full-key path
+        if (len > MAXN) {
             if (tid == 0) atomicAdd(big, (unsigned long long)len);
             continue;
         }
         const int n = int(len);
         int np2 = 1;
         while (np2 < n) np2 <<= 1;
-        for (int i = tid; i < np2; i += kSortBlock) {
+        for (int i = tid; i < np2; i += BS) {
             st[i] = i < n ? time[rows[b + i]] : INT64_MAX;  // NULL = INT64_MAX sorts last; pads after
             si[i] = i;
         }
         __syncthreads();
         for (int k = 2; k <= np2; k <<= 1) {
             for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int t = tid; t < (np2 >> 1); t += kSortBlock) {  // every thread owns a pair
+                for (int t = tid; t < (np2 >> 1); t += BS) {  // every thread owns pairs
                     const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;  // j = 2^m
-                    {
-                        const int64_t ta = st[i], tb = st[ixj];
-                        const int32_t ia = si[i], ib = si[ixj];
-                        const bool gt = ta > tb || (ta == tb && ia > ib);
-                        if (gt == ((i & k) == 0)) {
-                            st[i] = tb;
-                            st[ixj] = ta;
-                            si[i] = ib;
-                            si[ixj] = ia;
-                        }
+                    const int64_t ta = st[i], tb = st[ixj];
+                    const int32_t ia = si[i], ib = si[ixj];
+                    const bool gt = ta > tb || (ta == tb && ia > ib);
+                    if (gt == ((i & k) == 0)) {
+                        st[i] = tb;
+                        st[ixj] = ta;
+                        si[i] = ib;
+                        si[ixj] = ia;
                     }
                 }
                 __syncthreads();
             }
         }
         const uint32_t p = uint32_t(s) & pmask;
-        for (int i = tid; i < n; i += kSortBlock) {
+        for (int i = tid; i < n; i += BS) {
             orow[b + i] = int32_t(rows[b + si[i]]);
             otime[b + i] = st[i];
             oproj[b + i] = p;
@@ -225,8 +226,9 @@ static unsigned long long *sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int
     const uint32_t pmask = pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << pre.pbits) - 1ull);
     {
         ProbeScope ps(c, "seg_time_sort", 28.0 * double(n));  // row 4 + gathered time 8 + out 16 B
-        k_seg_time_sort<<<unsigned(S < 16384 ? S : 16384), kSortBlock, 0, c->stream>>>(vals, time, offs, S, pmask, orow,
-                                                                                  otime, oproj, big);
+        const unsigned g = unsigned(S < 16384 ? S : 16384);
+        k_seg_time_sort<kSortBlock, kSegSortMax><<<g, kSortBlock, 0, c->stream>>>(vals, time, offs, S, pmask, orow,
+                                                                                    otime, oproj, big);
         FZ_LAUNCH_CHECK();
     }
     return big;
