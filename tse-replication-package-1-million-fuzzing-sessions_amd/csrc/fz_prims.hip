@@ -197,13 +197,18 @@ __global__ __launch_bounds__(kBlock) void k_scan_lookback(const int64_t *__restr
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t base = tile * kLbTile;
+    int64_t x[kLbItems];
+#pragma unroll
     for (int i = 0; i < kLbItems; ++i) {
         const int64_t idx = base + i * kBlock + tid;
-        s_val[i * kBlock + tid] = idx < n ? in[idx] : 0;
+        x[i] = idx < n ? in[idx] : 0;
     }
+#pragma unroll
+    for (int i = 0; i < kLbItems; ++i) s_val[i * kBlock + tid] = x[i];
     __syncthreads();
     int64_t loc[kLbItems];
     int64_t run = 0;
+#pragma unroll
     for (int i = 0; i < kLbItems; ++i) {
         loc[i] = run;
         run += s_val[tid * kLbItems + i];

@@ -52,10 +52,20 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
     const int64_t tile = s_tile;
     const int64_t base = tile * kFcTile;
     const int64_t live = d_live ? *d_live : n;
+    const int64_t lim = live < n ? live : n;
+    // all row loads first, then all predicate gathers: independent loads in flight together
+    // instead of one dependent load chain per item
+    int32_t r[kFcItems];
+    bool keep[kFcItems];
+#pragma unroll
     for (int i = 0; i < kFcItems; ++i) {
         const int64_t idx = base + i * kBlock + tid;
-        s_pos[i * kBlock + tid] = (idx < n && idx < live && pred(rows[idx])) ? 1 : 0;
+        r[i] = idx < lim ? rows[idx] : 0;
     }
+#pragma unroll
+    for (int i = 0; i < kFcItems; ++i) keep[i] = base + i * kBlock + tid < lim && pred(r[i]);
+#pragma unroll
+    for (int i = 0; i < kFcItems; ++i) s_pos[i * kBlock + tid] = keep[i] ? 1 : 0;
     __syncthreads();
     int32_t loc[kFcItems];
     int32_t run = 0;
@@ -80,15 +90,14 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
     }
     __syncthreads();
     const int64_t pre = s_prefix;
+#pragma unroll
     for (int i = 0; i < kFcItems; ++i) {
+        if (!keep[i]) continue;
         const int k = i * kBlock + tid;
-        const int32_t v = s_pos[k];
-        if (v < 0) {
-            const int64_t idx = base + k, q = pre + (v & 0x7fffffff);
-            orow[q] = rows[idx];
-            otime[q] = times[idx];
-            oproj[q] = proj[idx];
-        }
+        const int64_t idx = base + k, q = pre + (s_pos[k] & 0x7fffffff);
+        orow[q] = r[i];
+        otime[q] = times[idx];
+        oproj[q] = proj[idx];
     }
 }
 
