@@ -271,8 +271,8 @@ constexpr int kSortItems = 16;
 constexpr int kSortTile = kBlock * kSortItems;  // 4096 keys per workgroup
 
 // ---- single-sweep LSD passes (one launch per digit pass) -----------------------------------
-// One histogram kernel counts every pass's digits up front (passes whose digit is the same for
-// all keys are skipped: they are identity permutations).  Each pass is then ONE kernel: a tile
+// One histogram kernel counts every pass's digits up front (the global digit bases of every
+// pass, from one read of the keys).  Each pass is then ONE kernel: a tile
 // ranks its 4096 keys (stable: round, wave, lane order), publishes its per-digit counts, and gets
 // its global base per digit by decoupled look-back over the preceding tiles' status words
 // {flag:2, epoch:14, count:48} (tiles in ticket order; 8 predecessors per poll) - no per-tile
@@ -443,14 +443,21 @@ void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t 
         k_onesweep_hist<<<grid_for(n, kBlock * 8, 2048), kBlock, 0, c->stream>>>(keys, n, npass, ghist);
         FZ_LAUNCH_CHECK();
     }
-    unsigned long long *hh = reinterpret_cast<unsigned long long *>(c->h_pinned);
-    FZ_HIP(hipMemcpyAsync(hh, ghist, sizeof(unsigned long long) * npass * kRadix, hipMemcpyDeviceToHost, c->stream));
-    sync(c);
+    // Constant-digit passes are identity permutations.  Finding them needs a host round trip, which
+    // stalls the stream for longer than a pass over a few million keys takes: only large sorts
+    // (>= 4 M keys, where one pass costs ~0.1 ms or more) skip them.
     bool need[kOsMaxPasses];
-    for (int p = 0; p < npass; ++p) {
-        int nz = 0;
-        for (int d = 0; d < kRadix; ++d) nz += hh[p * kRadix + d] != 0;
-        need[p] = nz > 1;  // a pass whose digit is constant is the identity permutation
+    for (int p = 0; p < npass; ++p) need[p] = true;
+    if (n >= (int64_t(1) << 22)) {
+        unsigned long long *hh = reinterpret_cast<unsigned long long *>(c->h_pinned);
+        FZ_HIP(hipMemcpyAsync(hh, ghist, sizeof(unsigned long long) * npass * kRadix, hipMemcpyDeviceToHost,
+                              c->stream));
+        sync(c);
+        for (int p = 0; p < npass; ++p) {
+            int nz = 0;
+            for (int d = 0; d < kRadix; ++d) nz += hh[p * kRadix + d] != 0;
+            need[p] = nz > 1;
+        }
     }
     uint64_t *k2 = c->arena.get<uint64_t>(n);
     uint32_t *v2 = vals ? c->arena.get<uint32_t>(n) : nullptr;
