@@ -77,6 +77,9 @@ class _RQ4bView(_RQ2View):
     def two_sample(self, x, y):
         return self.s.two_sample(x.to(self.dev), y.to(self.dev))
 
+    def row_medians(self, rows):
+        return self.s.row_medians(rows.to(self.dev))
+
 
 def _worker(rank, world, port, case, errfile):
     import torch.distributed as dist

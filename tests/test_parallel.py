@@ -287,6 +287,10 @@ class OracleRQ4bShard(OracleRQ2CountShard):
         T = torch.from_numpy
         return {"c2": T(c2), "c1": T(c1), "g2_q": T(q2.reshape(-1)), "g1_q": T(q1.reshape(-1)), "p_bm": T(pb)}
 
+    def row_medians(self, rows):
+        r = rows.numpy()
+        return np.array([float(np.median(x)) if len(x) else np.nan for x in r])
+
     def two_sample(self, x, y):
         from oracle import rq_oracle as orc
         mwu, cliff, bm, lv = orc.rq4b_init_tests(x.numpy(), y.numpy())

@@ -172,6 +172,38 @@ def all_to_all_v(x, send_counts):
     return out
 
 
+def _i64(x):
+    """int64 image of a column for packing: float64 bit patterns travel unchanged."""
+    import torch
+    return x.view(torch.int64) if x.dtype == torch.float64 else x.to(torch.int64)
+
+
+def _unpack(m, dtypes):
+    import torch
+    return [m[:, j].contiguous().view(torch.float64) if dt == torch.float64 else m[:, j].contiguous()
+            for j, dt in enumerate(dtypes)]
+
+
+def all_gather_cols(cols):
+    """All-gather of k equal-length columns (int / float64) as ONE variable-size collective (a
+    row-major [n, k] int64 block) -> per rank, the list of its k columns (dtypes restored)."""
+    import torch
+    dts = [c.dtype if c.dtype == torch.float64 else torch.int64 for c in cols]
+    block = torch.stack([_i64(c) for c in cols], 1).reshape(-1)
+    return [_unpack(p.reshape(-1, len(cols)), dts) for p in all_gather_v(block)]
+
+
+def all_to_all_cols(cols, send_counts):
+    """Variable all-to-all of k equal-length columns (rows grouped by destination rank) as ONE
+    collective -> the k columns of the rows every rank sent here, in source-rank order."""
+    import torch
+    dts = [c.dtype if c.dtype == torch.float64 else torch.int64 for c in cols]
+    k = len(cols)
+    block = torch.stack([_i64(c) for c in cols], 1).reshape(-1)
+    got = all_to_all_v(block, [int(v) * k for v in send_counts])
+    return _unpack(got.reshape(-1, k), dts)
+
+
 def agree_max(v: int, device=None) -> int:
     """MAX over ranks of a host integer (e.g. the RQ1 iteration-axis length, agreed once per load
     so every rank's per-iteration buffers have the same shape)."""
@@ -194,30 +226,27 @@ def rq1_sharded(shard, rank: int, world: int):
     part = shard.run(None)
     reran = False
     if world > 1:
-        nums = all_gather_v(part["number"])
-        bts = all_gather_v(part["build_time"])
+        got = all_gather_cols([part["number"], part["build_time"]])
         mine = part["number"]
-        en, eb, ef = [], [], []
-        for r in range(world):
-            if r == rank or nums[r].numel() == 0 or mine.numel() == 0:
-                continue
-            hit = torch.isin(nums[r], mine)
-            if bool(hit.any()):
-                en.append(nums[r][hit])
-                eb.append(bts[r][hit])
-                ef.append(torch.full((int(hit.sum()),), 1 if r < rank else 0, dtype=torch.uint8, device=mine.device))
-        if en:
-            part = shard.run((torch.cat(en), torch.cat(eb), torch.cat(ef)))
-            reran = True
+        others = [r for r in range(world) if r != rank and got[r][0].numel()]
+        if others and mine.numel():
+            nums = torch.cat([got[r][0] for r in others])
+            bts = torch.cat([got[r][1] for r in others])
+            before = torch.cat([torch.full((got[r][0].numel(),), 1 if r < rank else 0, dtype=torch.uint8,
+                                           device=mine.device) for r in others])
+            hit = torch.isin(nums, mine)
+            if bool(hit.any()):  # issue numbers shared with another shard: re-run with competitors
+                part = shard.run((nums[hit], bts[hit], before[hit]))
+                reran = True
     counts = part["counts"].clone()
     it, idt = part["iter_total"].clone(), part["iter_detected"].clone()
-    if world > 1:
-        mx = counts[RQ1_MAX_ITER:RQ1_MAX_ITER + 1].clone()
-        all_reduce(counts)
-        all_reduce(mx, dist.ReduceOp.MAX)
-        counts[RQ1_MAX_ITER] = mx[0]
-        all_reduce(it)
-        all_reduce(idt)
+    if world > 1:  # one all-reduce: counters and both per-iteration tables
+        M = it.numel()
+        block = torch.cat([counts, it, idt])
+        all_reduce(block)
+        counts, it, idt = block[:RQ1_NCOUNTS].clone(), block[RQ1_NCOUNTS:RQ1_NCOUNTS + M].clone(), \
+            block[RQ1_NCOUNTS + M:].clone()
+        counts[RQ1_MAX_ITER] = (it > 0).sum()  # iter_total is non-increasing: its support is the max
     shard.finish(counts, it, idt)
     return part, counts, it, idt, reran
 
@@ -239,7 +268,11 @@ def rq3_sharded(shard, rank: int, world: int):
     counts = part["counts"]
     if world > 1:
         cl = [c.cpu().numpy() for c in all_gather(counts)]
-        cols = {k: all_gather_v(part[k]) for k in RQ3_DET_F + RQ3_DET_I + RQ3_NON_F + RQ3_NON_I}
+        cols = {}
+        for keys in (RQ3_DET_F + RQ3_DET_I, RQ3_NON_F + RQ3_NON_I):
+            got = all_gather_cols([part[k] for k in keys])
+            for j, k in enumerate(keys):
+                cols[k] = [got[r][j] for r in range(world)]
     else:
         cl = [counts.cpu().numpy()]
         cols = {k: [part[k]] for k in RQ3_DET_F + RQ3_DET_I + RQ3_NON_F + RQ3_NON_I}
@@ -288,11 +321,12 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     import torch
     part = shard.run()
     dev = part["session_values"].device
-    proj = {}
-    for k in RQ2C_PROJECT_COLS:
-        v = part[k][lo:hi]
-        v = v.to(torch.float64) if v.is_floating_point() else v.to(torch.int64)
-        proj[k] = torch.cat(all_gather_v(v)).cpu().numpy() if world > 1 else v.cpu().numpy()
+    pc = [part[k][lo:hi] for k in RQ2C_PROJECT_COLS]
+    pc = [v.to(torch.float64) if v.is_floating_point() else v.to(torch.int64) for v in pc]
+    if world > 1:
+        got = all_gather_cols(pc)
+        pc = [torch.cat([got[r][j] for r in range(world)]) for j in range(len(pc))]
+    proj = {k: v.cpu().numpy() for k, v in zip(RQ2C_PROJECT_COLS, pc)}
     offs = part["session_offsets"]
     m_loc = offs.numel() - 1
     loc_sizes = (offs[1:] - offs[:-1]).to(torch.int64)
@@ -309,14 +343,16 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     offs_h = offs.cpu().numpy()
     send = [int(offs_h[min(b, m_loc)] - offs_h[min(a, m_loc)]) for a, b in own]
     if world > 1:
-        vals = all_to_all_v(vals, send)
-        sids = all_to_all_v(sids, send)
+        vals, sids = all_to_all_cols([vals, sids], send)
     a, b = own[rank]
     st = shard.session_stats(vals, sids - a, b - a, len(proj["eligible"]))
-    res = {}
-    for k in ("average", "median", "percentiles"):
-        v = st[k][:(b - a) * (5 if k == "percentiles" else 1)]
-        res[k] = torch.cat(all_gather_v(v)).cpu().numpy() if world > 1 else v.cpu().numpy()
+    S = b - a
+    block = torch.cat([st["average"][:S, None], st["median"][:S, None], st["percentiles"][:5 * S].reshape(S, 5)], 1)
+    if world > 1:  # per-session rows (average, median, 5 percentiles) of every owner, session order
+        block = torch.cat([m.reshape(-1, 7).view(torch.float64) for m in all_gather_v(block.reshape(-1).view(
+            torch.int64))])
+    block = block.cpu().numpy()
+    res = {"average": block[:, 0].copy(), "median": block[:, 1].copy(), "percentiles": block[:, 2:].reshape(-1).copy()}
     K = int(np.sum(sizes_h >= 100))
     tests = shard.series_tests(torch.from_numpy(res["median"][:K].copy()).to(dev))
     elig = proj["eligible"] != 0
@@ -328,8 +364,9 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
            "tests": tests, "corr_mm": corr_mm}
     if gather_values:  # coverage_by_session_index.csv: every value, session-major, project order
         if world > 1:
-            gv = torch.cat(all_gather_v(vals)).cpu().numpy()
-            gs = torch.cat(all_gather_v(sids)).cpu().numpy()
+            got = all_gather_cols([vals, sids])
+            gv = torch.cat([g[0] for g in got]).cpu().numpy()
+            gs = torch.cat([g[1] for g in got]).cpu().numpy()
         else:
             gv, gs = vals.cpu().numpy(), sids.cpu().numpy()
         out["session_values"] = gv[np.argsort(gs, kind="stable")]
@@ -354,15 +391,21 @@ def rq4a_sharded(shard, rank: int, world: int, lo: int, hi: int):
     steps, trans = part["g4_steps"].clone(), part["g4_transition"].clone()
     member = part["member"][lo:hi].to(torch.int64)
     intro = part["intro"][lo:hi].clone()
-    if world > 1:
-        mx = counts[[RQ4A_MAX_ITER, RQ4A_HAS_WINDOW]].clone()
-        all_reduce(counts)
-        all_reduce(mx, _dist().ReduceOp.MAX)
-        counts[RQ4A_MAX_ITER], counts[RQ4A_HAS_WINDOW] = mx[0], mx[1]
-        for x in tables + [steps, trans]:
-            all_reduce(x)
-        member = torch.cat(all_gather_v(member))
-        intro = torch.cat(all_gather_v(intro))
+    if world > 1:  # one all-reduce (counters, tables, step and transition counts), one gather
+        parts = [counts] + tables + [steps, trans]
+        block = torch.cat(parts)
+        all_reduce(block)
+        out, o = [], 0
+        for x in parts:
+            out.append(block[o:o + x.numel()].clone())
+            o += x.numel()
+        counts, tables, steps, trans = out[0], out[1:5], out[5], out[6]
+        # the longest G1/G2 build axis is the support of the summed totals; HAS_WINDOW is an OR
+        counts[RQ4A_MAX_ITER] = ((tables[0] + tables[2]) > 0).sum()
+        counts[RQ4A_HAS_WINDOW] = (counts[RQ4A_HAS_WINDOW] > 0).to(counts.dtype)
+        got = all_gather_cols([member, intro])
+        member = torch.cat([g[0] for g in got])
+        intro = torch.cat([g[1] for g in got])
     sc = shard.finish(tables, intro, steps, counts)
     return {"counts": counts.cpu().numpy(), "scalars": np.asarray(sc), "member": member.cpu().numpy(),
             "tables": [x.cpu().numpy()[:int(counts[RQ4A_MAX_ITER])] for x in tables], "intro": intro.cpu().numpy(),
@@ -409,13 +452,20 @@ def rq4b_sharded(shard, rank: int, world: int):
         dest = torch.searchsorted(cuts, sids, right=True)
         perm = torch.argsort(dest, stable=True)
         send = torch.bincount(dest, minlength=world).tolist() if n else [0] * world
-        vals, sids, grp = (all_to_all_v(x[perm], send) for x in (vals, sids, grp))
+        vals, sids, grp = all_to_all_cols([vals[perm], sids[perm], grp[perm]], send)
+        grp = grp.to(torch.uint8)
     a, b = own[rank]
-    st = shard.session_stats(vals, sids - a, grp, b - a, P)
-    res = {}
-    for k, w in (("c2", 1), ("c1", 1), ("g2_q", 3), ("g1_q", 3), ("p_bm", 1)):
-        v = st[k][:(b - a) * w]
-        res[k] = torch.cat(all_gather_v(v)).cpu().numpy() if world > 1 else v.cpu().numpy()
+    S = b - a
+    st = shard.session_stats(vals, sids - a, grp, S, P)
+    # per-session rows (c2, c1, g2 quartiles, g1 quartiles, p_bm) of every owner, session order
+    cols = [st["c2"][:S], st["c1"][:S]] + [st["g2_q"][:3 * S].reshape(S, 3)[:, j] for j in range(3)] + \
+        [st["g1_q"][:3 * S].reshape(S, 3)[:, j] for j in range(3)] + [st["p_bm"][:S]]
+    if world > 1:
+        got = all_gather_cols(cols)
+        cols = [torch.cat([g[j] for g in got]) for j in range(len(cols))]
+    cols = [x.cpu().numpy() for x in cols]
+    res = {"c2": cols[0], "c1": cols[1], "g2_q": np.stack(cols[2:5], 1).reshape(-1),
+           "g1_q": np.stack(cols[5:8], 1).reshape(-1), "p_bm": cols[8]}
     c2, c1 = res["c2"], res["c1"]
     ok = np.nonzero((c2 >= 100) & (c1 >= 100))[0]
     last = int(ok[-1]) if len(ok) else -1
@@ -432,15 +482,15 @@ def rq4b_sharded(shard, rank: int, world: int):
     proj = part["delta_order"]
     pre = part["pre_cov"][:7 * nd].reshape(7, nd) if nd else torch.zeros(7, 0, dtype=torch.float64, device=dev)
     post = part["post_cov"][:7 * nd].reshape(7, nd) if nd else torch.zeros(7, 0, dtype=torch.float64, device=dev)
-    if world > 1:
-        proj = torch.cat(all_gather_v(proj))
-        pre = torch.stack([torch.cat(all_gather_v(pre[i].contiguous())) for i in range(7)])
-        post = torch.stack([torch.cat(all_gather_v(post[i].contiguous())) for i in range(7)])
+    if world > 1:  # one gather: (CSV row, 7 pre, 7 post) per delta column
+        got = all_gather_cols([proj] + [pre[i] for i in range(7)] + [post[i] for i in range(7)])
+        cat = [torch.cat([g[j] for g in got]) for j in range(15)]
+        proj, pre, post = cat[0], torch.stack(cat[1:8]), torch.stack(cat[8:15])
     order = np.argsort(proj.cpu().numpy(), kind="stable")
     pre_h, post_h = pre.cpu().numpy()[:, order], post.cpu().numpy()[:, order]
     counts[RQ4B_DELTA_PROJECTS] = len(order)
-    pre_med = [shard.mean_median(torch.from_numpy(pre_h[i].copy()).to(dev))[1] for i in range(7)]
-    post_med = [shard.mean_median(torch.from_numpy(post_h[i].copy()).to(dev))[1] for i in range(7)]
+    med = shard.row_medians(torch.from_numpy(np.concatenate([pre_h, post_h]).copy()).to(dev))
+    pre_med, post_med = [float(v) for v in med[:7]], [float(v) for v in med[7:]]
     # initial coverage: samples in project order, tests once
     x, y = part["init_g2"], part["init_g1"]
     if world > 1:
@@ -516,23 +566,29 @@ class GpuRQ2CountShard:
         return out
 
     def session_stats(self, vals, sids, S, max_len):
-        E, C, eng = self.E, self.C, self.eng
-        torch = eng.torch
-        avg = torch.empty(max(S, 1), dtype=torch.float64, device=eng.dev)
-        med = torch.empty_like(avg)
-        pct = torch.empty(max(5 * S, 1), dtype=torch.float64, device=eng.dev)
-        ge = torch.zeros(1, dtype=torch.int64, device=eng.dev)
-        vals, sids = vals.contiguous(), sids.contiguous()
-        P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
-        E._check(eng.lib, eng.lib.fz_rq2_session_stats(eng.ctx, P(vals), P(sids), vals.numel(), S, max_len, P(avg),
-                                                       P(med), P(pct), P(ge)))
-        return {"average": avg, "median": med, "percentiles": pct, "ge100": ge}
+        return gpu_session_stats(self.eng, vals, sids, S, max_len)
 
     def series_tests(self, x):
         return gpu_series_tests(self.eng, x)
 
     def mean_median(self, x):
         return gpu_mean_median(self.eng, x)
+
+
+def gpu_session_stats(eng, vals, sids, S, max_len):
+    """fz_rq2_session_stats: per-session mean / median / percentiles of (session id, value) pairs."""
+    import ctypes as C
+    from . import engine as E
+    torch = eng.torch
+    avg = torch.empty(max(S, 1), dtype=torch.float64, device=eng.dev)
+    med = torch.empty_like(avg)
+    pct = torch.empty(max(5 * S, 1), dtype=torch.float64, device=eng.dev)
+    ge = torch.zeros(1, dtype=torch.int64, device=eng.dev)
+    vals, sids = vals.contiguous(), sids.contiguous()
+    P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+    E._check(eng.lib, eng.lib.fz_rq2_session_stats(eng.ctx, P(vals), P(sids), vals.numel(), S, max_len, P(avg), P(med),
+                                                   P(pct), P(ge)))
+    return {"average": avg, "median": med, "percentiles": pct, "ge100": ge}
 
 
 def gpu_series_tests(eng, x):
@@ -618,6 +674,13 @@ class GpuRQ4bShard:
 
     def mean_median(self, x):
         return gpu_mean_median(self.eng, x)
+
+    def row_medians(self, rows):
+        """statistics.median of every row of a [k, n] device block (NaN for n == 0), one call."""
+        k, n = rows.shape
+        sids = self.eng.torch.arange(k, dtype=self.eng.torch.int64, device=self.eng.dev).repeat_interleave(n)
+        out = gpu_session_stats(self.eng, rows.reshape(-1).contiguous(), sids, k, n)
+        return out["median"][:k].cpu().numpy()
 
     def two_sample(self, x, y):
         E, C, eng = self.E, self.C, self.eng
