@@ -13,6 +13,7 @@ rq       the six analysis scripts re-expressed on the engine (same outputs as th
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libfz.so")
+# FZ_LIB_PATH: an alternative build of the same library (tuning variants, scripts/build_variants.sh)
+LIB_PATH = os.environ.get("FZ_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libfz.so")
 
 __all__ = ["PKG_DIR", "LIB_PATH"]

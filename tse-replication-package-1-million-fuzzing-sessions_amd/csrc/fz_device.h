@@ -12,6 +12,20 @@ __device__ inline int lane_id() { return threadIdx.x & 63; }
 __device__ inline int wave_id() { return threadIdx.x >> 6; }
 __device__ inline uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
+// Bitonic networks in LDS map pair q to the elements i = ((q & ~(j-1)) << 1) | (q & (j-1)) and
+// i + j, with pairs q = tid + m * blockDim (blockDim a multiple of 64).  A stage with j <= 64 only
+// touches the 128 elements of one wave's 64 consecutive pairs, so between two such stages the
+// wave's own (in-order) LDS traffic is the only dependency: wait for it, skip the workgroup
+// barrier (63 of the 78 stages of a 4096-entry network).  Call after stage (k, j) of a network of
+// np2 entries; the last stage always ends with the barrier.
+__device__ inline void bitonic_stage_sync(int k, int j, int np2) {
+    const int nj = j > 1 ? (j >> 1) : k;  // the next stage's distance (stage k << 1 starts at k)
+    if (j <= 64 && nj <= 64 && !(j == 1 && k == np2))
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else
+        __syncthreads();
+}
+
 template <typename T>
 __device__ inline T wave_incl_scan(T x) {
     const int lane = lane_id();
@@ -51,7 +65,7 @@ __device__ inline T wave_min(T x) {
 }
 
 // Exclusive scan over a 256-thread block; s_tmp must hold 4 T.  *total receives the block sum.
-template <typename T>
+template <typename T, int NW = 4>  // NW waves per workgroup
 __device__ inline T block_excl_scan(T x, T *s_tmp, T *total) {
     T inc = wave_incl_scan(x);
     const int w = wave_id();
@@ -59,7 +73,7 @@ __device__ inline T block_excl_scan(T x, T *s_tmp, T *total) {
     __syncthreads();
     T woff = 0, tot = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NW; ++i) {  // s_tmp holds one slot per wave
         T v = s_tmp[i];
         if (i < w) woff += v;
         tot += v;
@@ -82,14 +96,19 @@ __device__ inline T block_sum(T x, T *s_tmp) {
 // Lanes of this wave whose `bits`-bit digit equals mine (all 64 lanes must execute this).
 template <int BITS>
 __device__ inline uint64_t match_digit(uint32_t d, bool valid) {
-    uint64_t peers = __ballot(valid);
+    // per bit: one compare for the ballot, then the lane keeps the ballot (bit set) or its
+    // complement (bit clear) by xor with (bit - 1) - 32-bit halves, no 64-bit selects
+    const uint64_t v = __ballot(valid);
+    uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
 #pragma unroll
     for (int b = 0; b < BITS; ++b) {
-        const bool bit = (d >> b) & 1u;
-        const uint64_t bal = __ballot(bit);
-        peers &= bit ? bal : ~bal;
+        const uint32_t bit = (d >> b) & 1u;
+        const uint64_t bal = __ballot(bit != 0u);
+        const uint32_t flip = bit - 1u;  // 0 when set, all ones when clear
+        lo &= uint32_t(bal) ^ flip;
+        hi &= uint32_t(bal >> 32) ^ flip;
     }
-    return peers;
+    return (uint64_t(hi) << 32) | lo;
 }
 
 // ---- double-double (error-free) accumulation -----------------------------------------------

@@ -267,8 +267,20 @@ void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, i
 // ------------------------------------------------------------------------- LSD radix sort
 constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
-constexpr int kSortItems = 16;
-constexpr int kSortTile = kBlock * kSortItems;  // 4096 keys per workgroup
+#ifndef FZ_OS_BLOCK
+#define FZ_OS_BLOCK 512
+#endif
+#ifndef FZ_OS_TILE
+#define FZ_OS_TILE 4096
+#endif
+#ifndef FZ_OS_WINDOW
+#define FZ_OS_WINDOW 8
+#endif
+constexpr int kOsBlock = FZ_OS_BLOCK;        // threads per radix-pass workgroup
+constexpr int kOsWaves = kOsBlock / kWave;
+constexpr int kSortTile = FZ_OS_TILE;        // keys per workgroup
+constexpr int kSortItems = kSortTile / kOsBlock;
+static_assert(kOsBlock >= kRadix && kSortTile % kOsBlock == 0, "radix pass shape");
 
 // ---- single-sweep LSD passes (one launch per digit pass) -----------------------------------
 // One histogram kernel counts every pass's digits up front (the global digit bases of every
@@ -278,8 +290,11 @@ constexpr int kSortTile = kBlock * kSortItems;  // 4096 keys per workgroup
 // {flag:2, epoch:14, count:48} (tiles in ticket order; 8 predecessors per poll) - no per-tile
 // histogram pass, no device-wide scan of the tile x digit counts.  Epoch tags make stale words
 // from earlier passes invisible, so the status array is never cleared between passes.
+// Shape (scripts/radix_micro.py, MI355X): 512 threads (8 waves x 8 rounds) per 4096-key tile -
+// two waves per SIMD hide the ranking loop's LDS round trips (17.8 vs 20.8 us per 650 k-key pass
+// with 4 waves); 8-predecessor polls beat 16/32 (look-back traffic is bandwidth-limited).
 constexpr int kOsMaxPasses = 8;
-constexpr int kOsWindow = 8;
+constexpr int kOsWindow = FZ_OS_WINDOW;
 
 __global__ __launch_bounds__(kBlock) void k_onesweep_hist(const uint64_t *__restrict__ keys, int64_t n, int npass,
                                                           unsigned long long *__restrict__ ghist) {
@@ -309,8 +324,31 @@ __global__ __launch_bounds__(kBlock) void k_onesweep_hist(const uint64_t *__rest
     }
 }
 
+#ifdef FZ_OS_TIMING
+// experiment builds only: wall-clock (100 MHz) phase stamps of three tiles of the last launch
+__device__ unsigned long long g_os_t[3][8];
+__device__ unsigned long long g_os_first;
+#define OS_STAMP(ph)                                                                        \
+    do {                                                                                    \
+        if (tid == 0) {                                                                     \
+            const int sl = tile == 0 ? 0 : (tile == int64_t(gridDim.x) / 2 ? 1 : (tile == int64_t(gridDim.x) - 1 ? 2 : -1)); \
+            if (sl >= 0) g_os_t[sl][ph] = wall_clock64();                                   \
+        }                                                                                   \
+    } while (0)
+extern "C" int fz_debug_os_timing(unsigned long long *out) {
+    hipDeviceSynchronize();
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_os_t), sizeof(g_os_t));
+    hipMemcpyFromSymbol(out + 24, HIP_SYMBOL(g_os_first), sizeof(g_os_first));
+    unsigned long long big = ~0ull;
+    hipMemcpyToSymbol(HIP_SYMBOL(g_os_first), &big, sizeof(big));
+    return 0;
+}
+#else
+#define OS_STAMP(ph) do {} while (0)
+#endif
+
 template <bool HAS_VALS>
-__global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict__ keys_in,
+__global__ __launch_bounds__(kOsBlock) void k_onesweep(const uint64_t *__restrict__ keys_in,
                                                      const uint32_t *__restrict__ vals_in,
                                                      uint64_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
                                                      int64_t n, int shift, const unsigned long long *__restrict__ ghist,
@@ -319,24 +357,30 @@ __global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict_
     __shared__ uint64_t s_keys[kSortTile];
     __shared__ uint32_t s_vals[HAS_VALS ? kSortTile : 1];
     __shared__ uint32_t s_run[kRadix];
-    __shared__ uint32_t s_wcnt[4][kRadix];
+    __shared__ uint32_t s_wcnt[kOsWaves][kRadix];
     __shared__ uint32_t s_start[kRadix];
     __shared__ int64_t s_goff[kRadix];
-    __shared__ uint32_t s_tmp[4];
-    __shared__ int64_t s_tmp64[4];
+    __shared__ uint32_t s_tmp[kOsWaves];
+    __shared__ int64_t s_tmp64[kOsWaves];
     __shared__ unsigned int s_tile;
 
     const int tid = threadIdx.x;
     const int w = wave_id(), lane = lane_id();
     if (tid == 0) s_tile = atomicAdd(ticket, 1u) - ticket_base;
-    for (int i = 0; i < 4; ++i) s_wcnt[i][tid] = 0;
+    const bool dig = tid < kRadix;  // threads [0, 256) own one digit each after the ranking
+    for (int i = tid; i < kOsWaves * kRadix; i += kOsBlock) (&s_wcnt[0][0])[i] = 0;
+    const int64_t gcount = dig ? int64_t(ghist[tid]) : 0;  // issued early: consumed after the ranking
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t base = tile * kSortTile;
-    // wave w owns the contiguous quarter [w * 1024, (w + 1) * 1024) of the tile; round r covers
+#ifdef FZ_OS_TIMING
+    if (tid == 0) atomicMin(&g_os_first, (unsigned long long)wall_clock64());
+#endif
+    OS_STAMP(0);
+    // wave w owns the contiguous slice [w * T/W, (w + 1) * T/W) of the tile; round r covers
     // its keys r * 64 + lane, so (wave, round, lane) is position order and ranking is stable with
     // wave-private digit counters - no workgroup barrier inside the ranking loop
-    const int64_t wbase = base + int64_t(w) * (kSortTile / 4);
+    const int64_t wbase = base + int64_t(w) * (kSortTile / kOsWaves);
 
     uint64_t k[kSortItems];
     uint32_t v[kSortItems];
@@ -349,6 +393,10 @@ __global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict_
         v[r] = (HAS_VALS && valid) ? vals_in[idx] : 0u;
     }
     uint32_t *cnt_w = s_wcnt[w];
+#ifdef FZ_OS_TIMING
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    OS_STAMP(6);
+#endif
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
         const bool valid = wbase + r * kWave + lane < n;
@@ -359,22 +407,30 @@ __global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict_
         if (valid && (__ffsll((long long)peers) - 1) == lane) cnt_w[d] = before + uint32_t(__popcll(peers));
     }
     __syncthreads();
+    OS_STAMP(1);
     // digit tid: tile count and per-wave exclusive offsets (stored back into s_wcnt)
     uint32_t cnt = 0;
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t x = s_wcnt[i][tid];
-        s_wcnt[i][tid] = cnt;
-        cnt += x;
+    uint64_t *my = &status[tile * kRadix + (dig ? tid : 0)];
+    if (dig) {
+        for (int i = 0; i < kOsWaves; ++i) {
+            const uint32_t x = s_wcnt[i][tid];
+            s_wcnt[i][tid] = cnt;
+            cnt += x;
+        }
+        s_run[tid] = cnt;
+        // publish this tile's count of digit tid, then look back for the counts of all earlier tiles
+        __hip_atomic_store(my, (tile == 0 ? kLbInc : kLbAgg) | epoch | uint64_t(cnt), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
-    s_run[tid] = cnt;
-    // publish this tile's count of digit tid, then look back for the counts of all earlier tiles
-    uint64_t *my = &status[tile * kRadix + tid];
-    __hip_atomic_store(my, (tile == 0 ? kLbInc : kLbAgg) | epoch | uint64_t(cnt), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    s_start[tid] = block_excl_scan(cnt, s_tmp, (uint32_t *)nullptr);
-    const int64_t gstart = block_excl_scan(int64_t(ghist[tid]), s_tmp64, (int64_t *)nullptr);
+    const uint32_t tstart = block_excl_scan<uint32_t, kOsWaves>(cnt, s_tmp, (uint32_t *)nullptr);
+    if (dig) s_start[tid] = tstart;  // visible to the scatter after the next scan's barriers
+    const int64_t gstart = block_excl_scan<int64_t, kOsWaves>(gcount, s_tmp64, (int64_t *)nullptr);
+    OS_STAMP(2);
     int64_t prefix = 0;
-    for (int64_t q = tile - 1; q >= 0;) {
+#ifdef FZ_OS_EXPERIMENT_NOLB
+    if (false)
+#endif
+    for (int64_t q = tile - 1; dig && q >= 0;) {
         uint64_t sw[kOsWindow];
 #pragma unroll
         for (int j = 0; j < kOsWindow; ++j)
@@ -396,9 +452,12 @@ __global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict_
         q -= j;
         if (j < kOsWindow) __builtin_amdgcn_s_sleep(1);
     }
-    if (tile > 0)
-        __hip_atomic_store(my, kLbInc | epoch | uint64_t(prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_goff[tid] = gstart + prefix - int64_t(s_start[tid]);
+    if (dig) {
+        if (tile > 0)
+            __hip_atomic_store(my, kLbInc | epoch | uint64_t(prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_goff[tid] = gstart + prefix - int64_t(tstart);
+    }
+    OS_STAMP(3);
     // stage the tile digit-sorted in LDS, then write it out in per-digit runs
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
@@ -410,14 +469,24 @@ __global__ __launch_bounds__(kBlock) void k_onesweep(const uint64_t *__restrict_
         }
     }
     __syncthreads();
+    OS_STAMP(4);
     const int64_t valid_n = (n - base) < kSortTile ? (n - base) : kSortTile;
-    for (int i = tid; i < valid_n; i += kBlock) {
+    for (int i = tid; i < valid_n; i += kOsBlock) {
         const uint64_t kk = s_keys[i];
         const uint32_t d = uint32_t(kk >> shift) & (kRadix - 1);
         const int64_t gpos = s_goff[d] + i;
-        keys_out[gpos] = kk;
-        if (HAS_VALS) vals_out[gpos] = s_vals[i];
+#ifdef FZ_OS_EXPERIMENT_NOWRITE
+        if (gpos < 0)
+#endif
+        {
+            keys_out[gpos] = kk;
+            if (HAS_VALS) vals_out[gpos] = s_vals[i];
+        }
     }
+#ifdef FZ_OS_TIMING
+    __syncthreads();
+    OS_STAMP(5);
+#endif
 }
 
 void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int bits) {
@@ -471,11 +540,11 @@ void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t 
             // algorithmic traffic of one pass: read + write every key (8 B) and value (4 B)
             ProbeScope ps(c, "radix_scatter", (vals ? 24.0 : 16.0) * double(n));
             if (vals)
-                k_onesweep<true><<<unsigned(nb), kBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits,
+                k_onesweep<true><<<unsigned(nb), kOsBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits,
                                                                          ghist + p * kRadix, lb.status, lb.ticket,
                                                                          lb.base, lb.epoch);
             else
-                k_onesweep<false><<<unsigned(nb), kBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits,
+                k_onesweep<false><<<unsigned(nb), kOsBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits,
                                                                           ghist + p * kRadix, lb.status, lb.ticket,
                                                                           lb.base, lb.epoch);
             FZ_LAUNCH_CHECK();
@@ -742,7 +811,7 @@ __global__ __launch_bounds__(kSortBlock) void k_describe_small(const double *__r
                     sk[ixj] = a;
                 }
             }
-            __syncthreads();
+            bitonic_stage_sync(k, j, np2);
         }
     }
     if (tid == 0) describe_from_sorted(sk, n, mean, std, out);

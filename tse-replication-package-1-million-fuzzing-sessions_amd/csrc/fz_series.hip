@@ -120,7 +120,7 @@ __global__ __launch_bounds__(BS) void k_seg_sort_lds(const double *__restrict__ 
                         }
                     }
                 }
-                __syncthreads();
+                bitonic_stage_sync(k, j, np2);
             }
         }
         for (int i = tid; i < n; i += BS) {

@@ -193,7 +193,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict
                         si[ixj] = ia;
                     }
                 }
-                __syncthreads();
+                bitonic_stage_sync(k, j, np2);
             }
         }
         const uint32_t p = uint32_t(s) & pmask;
