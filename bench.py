@@ -35,6 +35,7 @@ PROBE_KERNEL = "radix_scatter"   # dominant kernel of the step (profiles/r01_*_s
 STAGES = ["store", "rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"]
 WORKLOADS = {"c2": "config2: ~1M-session synthetic table",
              "c3": "config3: 100M-row coverage-only table, 10k projects x 10k days",
+             "c4": "config4: rank-statistics stress, 12 coverage series of 1e5/3e5/1e6 points, 256 levels",
              "c5": "config5: Zipf(1.2) rows per project, coverage-only, 10k projects"}
 
 

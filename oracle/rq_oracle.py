@@ -495,6 +495,22 @@ def rq4a_finish(g1t, g1d, g2t, g2d, intro_values, steps, N=7):
     return after, istats, overall
 
 
+def series_tests(x):
+    """(spearman rho, p, shapiro W, p) of one series, as rq2_coverage_count.py:305-322 (per project)
+    and :443-458 (median trend) call scipy: spearmanr(range(n), x) (NaN if n < 2), shapiro(x)
+    (NaN if n < 3; scipy warns, and still answers, above n = 5000)."""
+    x = list(x)
+    rho = pr = w = pw = float("nan")
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        if len(x) >= 2:
+            r = stats.spearmanr(range(len(x)), x)
+            rho, pr = float(r[0]), float(r[1])
+        if len(x) >= 3:
+            w, pw = (float(v) for v in stats.shapiro(x))
+    return rho, pr, w, pw
+
+
 # --------------------------------------------------------------------------------------- RQ4b
 def rq4b_full_series(t: Tables, P: int):
     """get_full_coverage_trend (rq4b:315-326): coverage > 0 AND date < LIMIT, per project by date."""

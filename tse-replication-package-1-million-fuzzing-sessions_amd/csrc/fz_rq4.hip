@@ -297,10 +297,12 @@ void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t 
 
 // Per-session quartiles / counts / Brunner-Munzel of G2 vs G1 (:910-1015) from values v2 ordered
 // by segment id sid2 = 2 * session + group (group 0 = G2), *d_n live of n_cap
+// half_len / sess_len: host bounds of one (session, group) half and of one whole session
 void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_cap, const int64_t *d_n, int64_t MM,
-                   int64_t max_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q, double *pbm) {
+                   int64_t half_len, int64_t sess_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q,
+                   double *pbm) {
     hipStream_t st = c->stream;
-    const int64_t S2 = 2 * MM, NC = n_cap, P = max_len;
+    const int64_t S2 = 2 * MM, NC = n_cap, P = half_len;
     const int64_t *d_nf = d_n;
     int32_t *sess = c->arena.get<int32_t>(NC);
     uint8_t *grp2 = c->arena.get<uint8_t>(NC);
@@ -331,7 +333,7 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
     });
     RankTestOut rt;
     rt.bm_p = pbm;
-    seg_rank_tests(c, v2, grp2, Segs{MM, soffs, NC, P}, sess, rt);
+    seg_rank_tests(c, v2, grp2, Segs{MM, soffs, NC, sess_len}, sess, rt);
     map_n(c, MM, nullptr, [=] __device__(int64_t i) {
         if (!(c2[i] >= 5 && c1[i] >= 5)) pbm[i] = NAN;
     });
@@ -364,7 +366,9 @@ void rq4b_session_stats(fz_ctx *c, const double *values, const int64_t *sid, con
         v2[k] = values[idx[k]];
         sid2[k] = uint32_t(key[k]);
     });
-    rq4b_sessions(c, v2, sid2, n, d_n, MM, max_len > 0 ? max_len : n, c2, c1, g2q, g1q, pbm);
+    // max_len bounds one group of a session: a whole session holds up to twice that
+    const int64_t half = max_len > 0 && max_len < n ? max_len : n;
+    rq4b_sessions(c, v2, sid2, n, d_n, MM, half, 2 * half < n ? 2 * half : n, c2, c1, g2q, g1q, pbm);
 }
 
 void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *o) {
@@ -432,7 +436,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
             sid2[k] = uint32_t(key[k] >> pbits);
             if (k < *d_nf) v2[k] = cov[frow[idx[k]]];
         });
-        rq4b_sessions(c, v2, sid2, NC, d_nf, MM, P, c2, c1, g2q, g1q, o->p_bm);
+        rq4b_sessions(c, v2, sid2, NC, d_nf, MM, P, P, c2, c1, g2q, g1q, o->p_bm);  // <= 1 value per project
     }
     // last session with both groups >= 100 (:849-860); Spearman of the quartile sequences (:879-899)
     if (!sharded) {

@@ -602,6 +602,22 @@ def gpu_series_tests(eng, x):
     return tuple(float(v) for v in out.cpu().tolist())
 
 
+def gpu_rq4b_session_stats(eng, vals, sids, grp, S, max_len):
+    """fz_rq4b_session_stats: per-session G2 (group 0) / G1 (group 1) counts, quartiles and
+    Brunner-Munzel p of (value, session id, group) triples."""
+    import ctypes as C
+    from . import engine as E
+    torch = eng.torch
+    z = lambda n, dt: torch.zeros(max(n, 1), dtype=dt, device=eng.dev)  # noqa: E731
+    out = {"c2": z(S, torch.int64), "c1": z(S, torch.int64), "g2_q": z(3 * S, torch.float64),
+           "g1_q": z(3 * S, torch.float64), "p_bm": z(S, torch.float64)}
+    vals, sids, grp = vals.contiguous(), sids.contiguous(), grp.contiguous()
+    P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+    E._check(eng.lib, eng.lib.fz_rq4b_session_stats(eng.ctx, P(vals), P(sids), P(grp), vals.numel(), S, max_len,
+                                                    *[P(out[k]) for k in ("c2", "c1", "g2_q", "g1_q", "p_bm")]))
+    return out
+
+
 def gpu_mean_median(eng, x):
     """(mean, median) of one device vector through fz_describe_f64 (NaN when empty)."""
     if x.numel() == 0:
@@ -658,16 +674,7 @@ class GpuRQ4bShard:
                 "delta_order": b.delta_order[:nd], "init_g2": b.init_g2[:n2], "init_g1": b.init_g1[:n1]}
 
     def session_stats(self, vals, sids, grp, S, max_len):
-        E, C, eng = self.E, self.C, self.eng
-        torch = eng.torch
-        z = lambda n, dt: torch.zeros(max(n, 1), dtype=dt, device=eng.dev)  # noqa: E731
-        out = {"c2": z(S, torch.int64), "c1": z(S, torch.int64), "g2_q": z(3 * S, torch.float64),
-               "g1_q": z(3 * S, torch.float64), "p_bm": z(S, torch.float64)}
-        vals, sids, grp = vals.contiguous(), sids.contiguous(), grp.contiguous()
-        P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
-        E._check(eng.lib, eng.lib.fz_rq4b_session_stats(eng.ctx, P(vals), P(sids), P(grp), vals.numel(), S, max_len,
-                                                        *[P(out[k]) for k in ("c2", "c1", "g2_q", "g1_q", "p_bm")]))
-        return out
+        return gpu_rq4b_session_stats(self.eng, vals, sids, grp, S, max_len)
 
     def series_tests(self, x):
         return gpu_series_tests(self.eng, x)

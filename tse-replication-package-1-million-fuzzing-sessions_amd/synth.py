@@ -47,6 +47,10 @@ class SynthConfig:
     zipf_s: Optional[float] = None       # config 5: Zipf rows/project
     coverage_only: bool = False          # config 3: only total_coverage rows
     rows_per_project: Optional[int] = None  # config 3: fixed contiguous daily length
+    lengths: Optional[tuple] = None      # config 4: per-project series lengths (cycled)
+    step_us: int = US_PER_DAY            # spacing of consecutive coverage rows
+    tie_levels: Optional[int] = None     # config 4: covered/total on a grid of tie_levels + 1 values
+    trend_mix: bool = False              # config 4: odd projects follow a monotone trend + noise
 
 
 RESULT_P = np.array([0.80, 0.05, 0.05, 0.10])      # Finish, Halfway, HalfWay, Error
@@ -71,7 +75,10 @@ def generate(cfg: SynthConfig) -> Tables:
     names = project_names(P)
     start_day = rng.integers(0, cfg.start_span_days + 1, size=P)
     max_len = (END_US - BASE_US) // US_PER_DAY - start_day
-    if cfg.rows_per_project is not None:
+    if cfg.lengths is not None:
+        length = np.resize(np.asarray(cfg.lengths, dtype=np.int64), P)
+        start_day = np.zeros(P, dtype=np.int64)
+    elif cfg.rows_per_project is not None:
         length = np.full(P, cfg.rows_per_project, dtype=np.int64)
         start_day = np.zeros(P, dtype=np.int64)
     elif cfg.zipf_s is not None:
@@ -91,10 +98,16 @@ def generate(cfg: SynthConfig) -> Tables:
     for p in range(P):
         L = int(length[p])
         d0 = BASE_US + int(start_day[p]) * US_PER_DAY
-        dates = d0 + np.arange(L, dtype=np.int64) * US_PER_DAY
-        total = np.maximum(1, np.round(rng.uniform(500, 2e5) + np.cumsum(
-            rng.normal(0, 60, size=L)))).astype(np.int64)
-        frac = np.clip(rng.uniform(0.1, 0.6) + np.cumsum(rng.normal(0, 0.002, size=L)), 0.0, 1.0)
+        dates = d0 + np.arange(L, dtype=np.int64) * cfg.step_us
+        if cfg.tie_levels:  # heavy ties: constant total, covered on a coarse grid
+            total = np.full(L, cfg.tie_levels, dtype=np.int64)
+        else:
+            total = np.maximum(1, np.round(rng.uniform(500, 2e5) + np.cumsum(
+                rng.normal(0, 60, size=L)))).astype(np.int64)
+        if cfg.trend_mix and p % 2 == 1:  # monotone trend + noise
+            frac = np.clip(np.linspace(0.1, 0.9, L) + rng.normal(0, 0.05, size=L), 0.0, 1.0)
+        else:
+            frac = np.clip(rng.uniform(0.1, 0.6) + np.cumsum(rng.normal(0, 0.002, size=L)), 0.0, 1.0)
         covered = np.clip(np.round(total * frac), 0, total).astype(np.int64)
         zero = rng.random(L) < cfg.p_zero_total
         total[zero] = 0
@@ -251,6 +264,10 @@ CONFIGS = {
     "c3": SynthConfig(n_projects=10_000, seed=11, coverage_only=True, rows_per_project=10_000),
     # config 5: Zipf rows per project
     "c5": SynthConfig(n_projects=10_000, seed=13, coverage_only=True, zipf_s=1.2, len_mean_days=10_000),
+    # config 4 (rank-statistics stress): series of 1e5 / 3e5 / 1e6 points (one row a minute, all
+    # before the analysis limit), 256 coverage levels (heavy ties), every other one a trend + noise
+    "c4": SynthConfig(n_projects=12, seed=17, coverage_only=True, lengths=(100_000, 300_000, 1_000_000),
+                      step_us=60_000_000, tie_levels=255, trend_mix=True),
 }
 
 
