@@ -2,7 +2,7 @@
 set -o pipefail
 V=tse-replication-package-1-million-fuzzing-sessions_amd/csrc/build/variants
 VARIANTS=${VARIANTS:-old new}
-timeout -k 10 200 python -u scripts/radix_micro.py $VARIANTS > gpurun_out/radix_micro.log 2>&1 || exit $?
+[ -n "$NOMICRO" ] || timeout -k 10 200 python -u scripts/radix_micro.py $VARIANTS > gpurun_out/radix_micro.log 2>&1 || exit $?
 if [ -f $V/libfz_timing.so ]; then TIMING=timing timeout -k 10 100 python -u scripts/radix_micro.py >> gpurun_out/radix_micro.log 2>&1 || exit $?; fi
 for v in $VARIANTS; do
   FZ_LIB_PATH=$PWD/$V/libfz_$v.so timeout -k 10 200 python -u bench.py --no-cpu-baseline $BENCH_ARGS > gpurun_out/bench_$v.log 2>&1 || exit $?
