@@ -85,6 +85,10 @@ const int64_t *single_segment(fz_ctx *c, const int64_t *d_n) {
 // every consumer (ranks, percentiles, rank tests) is invariant to the order inside a tie group.
 // Two instantiations: BS = 256 threads for segments of <= 1024 values (small LDS footprint, many
 // workgroups per CU) and BS = 1024 for 1025..4096; each skips the other's segments.
+#ifndef FZ_SL_BLOCK
+#define FZ_SL_BLOCK 1024
+#endif
+constexpr int kLdsSortBlock = FZ_SL_BLOCK;  // threads of the 1025..4096-value class
 template <int BS, int MAXN>
 __global__ __launch_bounds__(BS) void k_seg_sort_lds(const double *__restrict__ src, const int64_t *__restrict__ offs,
                                                      int64_t S, double *__restrict__ out_val,
@@ -137,7 +141,7 @@ static void launch_seg_sort_lds(fz_ctx *c, unsigned g, const double *src, const 
                                 int64_t len_bound, double *val, int32_t *pos, uint64_t *key) {
     k_seg_sort_lds<256, 1024><<<g, 256, 0, c->stream>>>(src, offs, S, val, pos, key);
     if (len_bound > 1024)
-        k_seg_sort_lds<kSortBlock, kLdsSortMax><<<g, kSortBlock, 0, c->stream>>>(src, offs, S, val, pos, key);
+        k_seg_sort_lds<kLdsSortBlock, kLdsSortMax><<<g, kLdsSortBlock, 0, c->stream>>>(src, offs, S, val, pos, key);
     FZ_LAUNCH_CHECK();
 }
 

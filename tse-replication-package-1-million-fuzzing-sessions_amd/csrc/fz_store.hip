@@ -127,6 +127,10 @@ __global__ __launch_bounds__(kSortBlock) void k_store_stats(Offs4 v, int64_t P, 
 
 // ---- fast path: prefix LSD (2 passes) + per-segment LDS sort by (time, row) -----------------
 constexpr int kSegSortMax = 4096;
+#ifndef FZ_TS_BLOCK
+#define FZ_TS_BLOCK 1024
+#endif
+constexpr int kTimeSortBlock = FZ_TS_BLOCK;  // threads of the per-segment time sort
 
 __global__ __launch_bounds__(kBlock) void k_keys_prefix_rows(Prefix pre, int64_t n, uint64_t *__restrict__ keys,
                                                              uint32_t *__restrict__ vals) {
@@ -227,7 +231,7 @@ static unsigned long long *sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int
     {
         ProbeScope ps(c, "seg_time_sort", 28.0 * double(n));  // row 4 + gathered time 8 + out 16 B
         const unsigned g = unsigned(S < 16384 ? S : 16384);
-        k_seg_time_sort<kSortBlock, kSegSortMax><<<g, kSortBlock, 0, c->stream>>>(vals, time, offs, S, pmask, orow,
+        k_seg_time_sort<kTimeSortBlock, kSegSortMax><<<g, kTimeSortBlock, 0, c->stream>>>(vals, time, offs, S, pmask, orow,
                                                                                     otime, oproj, big);
         FZ_LAUNCH_CHECK();
     }
