@@ -53,6 +53,9 @@ def parse():
     # rehearsal on a one-GPU box: several ranks on cuda:0 exchanging over gloo (the driver's
     # multi-GPU runs use the default, RCCL)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    # one rank through the sharded step (exchanges, host syncs, recombination) over a world-1 group:
+    # the floor of the multi-GPU step time on a one-GPU box
+    ap.add_argument("--force-sharded", action="store_true")
     return ap.parse_args()
 
 
@@ -70,12 +73,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.dist_backend == "gloo":
         local = local % max(torch.cuda.device_count(), 1)
-    if world > 1:
+    sharded = world > 1 or args.force_sharded
+    if sharded:
         torch.cuda.set_device(local)
+        init = {} if world > 1 else {"init_method": "tcp://127.0.0.1:29533", "world_size": 1, "rank": 0}
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), **init)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", **init)
     dev = torch.device("cuda", local)
 
     cfg = synth.config(args.config, seed=synth.config(args.config).seed + 1000 * rank)
@@ -90,7 +95,7 @@ def main():
     torch.cuda.synchronize(dev)
     upload_ms = (time.perf_counter() - t_up) * 1e3
     st = eng.build_store()
-    if world > 1:
+    if sharded:
         from tse_amd import parallel as par
         M = par.agree_max(int(st.max_fuzz_per_project), dev)
         rq1_shard = par.GpuRQ1Shard(eng, M)
@@ -109,7 +114,7 @@ def main():
 
     def step():
         eng.build_store()
-        if world == 1:
+        if not sharded:
             if "rq1" in stages:
                 compute.rq1_launch(eng, rq1_bufs)
             for name in ("rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"):
@@ -191,7 +196,7 @@ def main():
             "config": {"workload": f"{WORKLOADS.get(args.config, args.config)} ({args.config}), "
                                    f"{len(t.projects)} projects/rank",
                        "rows_per_rank": t.n_rows, "builds": int(len(t.b_project)), "coverage": int(len(t.c_project)),
-                       "issues": int(len(t.i_project)), "stages": stages, "parallelism": f"project-shard x{world}",
+                       "issues": int(len(t.i_project)), "stages": stages, "parallelism": f"project-shard x{world}" + (" (sharded path)" if sharded and world == 1 else ""),
                        "device_ms_per_step": round(dev_ms / args.steps, 4),
                        # end-to-end (host columns -> HBM upload + one step), per rank: the loader's
                        # PCIe-inclusive rate; `value` is compute-only with inputs resident in HBM
@@ -201,7 +206,7 @@ def main():
         }
         print(json.dumps(out), flush=True)
     eng.close()
-    if world > 1:
+    if sharded:
         dist.destroy_process_group()
     return out
 

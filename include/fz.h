@@ -222,6 +222,13 @@ int fz_rq2_session_stats(fz_ctx *ctx, const double *values, const int64_t *sessi
  * out[0..3] = rho, p, W, p (NaN where scipy returns NaN: n < 2 / constant, n < 3). */
 int fz_series_tests(fz_ctx *ctx, const double *x, int64_t n, double *out);
 
+/* scipy.stats.spearmanr(range(n_s), x_s) of S device series at once (segment s = x[offs[s],
+ * offs[s+1]), n = offs[S] values, max_len a host bound of one segment, 0 if unknown): rho[s], p[s]
+ * (NaN where scipy returns NaN).  Replaces the per-sequence calls of rq4b_coverage.py:879-899 on the
+ * sharded path (the six quartile sequences in one call). */
+int fz_spearman_index_seg(fz_ctx *ctx, const double *x, int64_t n, const int64_t *offs, int64_t S, int64_t max_len,
+                          double *rho, double *p);
+
 /* ---- RQ2/RQ3 support (add): rq2_coverage_and_added.py:73-238 ------------------------------- */
 enum { FZ_RQ2A_ELIGIBLE = 0, FZ_RQ2A_ROWS, FZ_RQ2A_RUNS, FZ_RQ2A_NCOUNTS = 4 };
 typedef struct fz_rq2_add_out {

@@ -70,6 +70,9 @@ class _RQ4aView(_HostView):
 
 
 class _RQ4bView(_RQ2View):
+    def spearman_many(self, seqs):
+        return self.s.spearman_many([x.to(self.dev) for x in seqs])
+
     def session_stats(self, vals, sids, grp, S, max_len):
         out = self.s.session_stats(vals.to(self.dev), sids.to(self.dev), grp.to(self.dev), S, max_len)
         return {k: v.cpu() for k, v in out.items()}

@@ -16,6 +16,8 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o);
 void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_ids, int64_t n, int64_t S,
                        int64_t max_len, double *average, double *median, double *pcts, int64_t *n_ge100);
 void series_tests(fz_ctx *c, const double *x, int64_t n_cap, const int64_t *d_n, double *out);
+void spearman_index_seg(fz_ctx *c, const double *x, int64_t n, const int64_t *offs, int64_t S, int64_t max_len,
+                        double *rho, double *p);
 void rq2_add(fz_ctx *c, const fz_rq2_add_out *o);
 void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o);
 void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t NI, const int64_t *d_nd,
@@ -148,6 +150,15 @@ int fz_series_tests(fz_ctx *ctx, const double *x, int64_t n, double *out) {
         int64_t *d_n = ctx->arena.get<int64_t>(1);
         fz::set_i64(ctx, d_n, &n, 1);
         fz::series_tests(ctx, x, n > 0 ? n : 1, d_n, out);
+    });
+}
+
+int fz_spearman_index_seg(fz_ctx *ctx, const double *x, int64_t n, const int64_t *offs, int64_t S, int64_t max_len,
+                          double *rho, double *p) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(S >= 0 && n >= 0 && (S == 0 || (offs && rho && p)) && (n == 0 || x),
+                 "fz_spearman_index_seg: bad arguments");
+        if (S > 0) fz::spearman_index_seg(ctx, x, n, offs, S, max_len, rho, p);
     });
 }
 

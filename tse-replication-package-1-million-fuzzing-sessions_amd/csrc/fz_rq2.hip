@@ -59,6 +59,16 @@ void series_tests(fz_ctx *c, const double *x, int64_t n_cap, const int64_t *d_n,
     seg_shapiro(c, cs3, x, ss3, out + 2, out + 3);
 }
 
+void spearman_index_seg(fz_ctx *c, const double *x, int64_t n, const int64_t *offs, int64_t S, int64_t max_len,
+                        double *rho, double *p) {
+    Segs sg{S, offs, n > 0 ? n : 1, max_len};
+    ChunkedSegs cs = chunked(c, sg);
+    int32_t *id = segment_ids(c, sg);
+    SortedSegs ss = seg_sort_f64(c, x, sg, id);
+    TieRanks tr = seg_tie_ranks(c, cs, id, ss.val);
+    seg_spearman_index(c, cs, ss, tr, rho, p);
+}
+
 __global__ void k_session_keys(const int64_t *__restrict__ sid, int64_t n, uint64_t *__restrict__ keys,
                                uint32_t *__restrict__ idx) {
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {

@@ -142,6 +142,7 @@ SIGNATURES = {
     "fz_rq2_count_ex": (C.c_int, [_P, C.c_uint32, C.POINTER(FzRq2CountOut)]),
     "fz_rq2_session_stats": (C.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P]),
     "fz_series_tests": (C.c_int, [_P, _P, _I64, _P]),
+    "fz_spearman_index_seg": (C.c_int, [_P, _P, _I64, _P, _I64, _I64, _P, _P]),
     "fz_rq2_add": (C.c_int, [_P, C.POINTER(FzRq2AddOut)]),
     "fz_rq3": (C.c_int, [_P, C.POINTER(FzRq3Out)]),
     "fz_rq3_ex": (C.c_int, [_P, C.c_uint32, C.POINTER(FzRq3Out)]),

@@ -172,6 +172,28 @@ def all_to_all_v(x, send_counts):
     return out
 
 
+def host_many(*ts):
+    """Host numpy copies of several tensors (numpy arrays pass through) with ONE device->host copy:
+    each separate ``.cpu()`` would drain the stream once."""
+    import torch
+    dev = [t for t in ts if isinstance(t, torch.Tensor) and t.is_cuda]
+    if not dev:
+        return [t.numpy().copy() if isinstance(t, torch.Tensor) else np.asarray(t) for t in ts]
+    flat = [t.contiguous().reshape(-1).view(torch.uint8) for t in dev]
+    h = torch.cat(flat).cpu().numpy()
+    out, o, k = [], 0, 0
+    for t in ts:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            nb = flat[k].numel()
+            dt = torch.empty(0, dtype=t.dtype).numpy().dtype
+            out.append(h[o:o + nb].view(dt).reshape(tuple(t.shape)))
+            o += nb
+            k += 1
+        else:
+            out.append(t.numpy().copy() if isinstance(t, torch.Tensor) else np.asarray(t))
+    return out
+
+
 def _i64(x):
     """int64 image of a column for packing: float64 bit patterns travel unchanged."""
     import torch
@@ -326,7 +348,6 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     if world > 1:
         got = all_gather_cols(pc)
         pc = [torch.cat([got[r][j] for r in range(world)]) for j in range(len(pc))]
-    proj = {k: v.cpu().numpy() for k, v in zip(RQ2C_PROJECT_COLS, pc)}
     offs = part["session_offsets"]
     m_loc = offs.numel() - 1
     loc_sizes = (offs[1:] - offs[:-1]).to(torch.int64)
@@ -335,12 +356,13 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     sizes[:m_loc] = loc_sizes
     if world > 1:
         all_reduce(sizes)
-    sizes_h = sizes.cpu().numpy()
+    h = host_many(sizes, offs, *pc)  # one device->host copy
+    sizes_h, offs_h = h[0], h[1]
+    proj = dict(zip(RQ2C_PROJECT_COLS, h[2:]))
     own = session_owners(sizes_h, world)
-    nv = int(offs[-1].item())
+    nv = int(offs_h[-1])
     vals = part["session_values"][:nv]
-    sids = torch.repeat_interleave(torch.arange(m_loc, dtype=torch.int64, device=dev), loc_sizes)
-    offs_h = offs.cpu().numpy()
+    sids = torch.repeat_interleave(torch.arange(m_loc, dtype=torch.int64, device=dev), loc_sizes, output_size=nv)
     send = [int(offs_h[min(b, m_loc)] - offs_h[min(a, m_loc)]) for a, b in own]
     if world > 1:
         vals, sids = all_to_all_cols([vals, sids], send)
@@ -407,9 +429,10 @@ def rq4a_sharded(shard, rank: int, world: int, lo: int, hi: int):
         member = torch.cat([g[0] for g in got])
         intro = torch.cat([g[1] for g in got])
     sc = shard.finish(tables, intro, steps, counts)
-    return {"counts": counts.cpu().numpy(), "scalars": np.asarray(sc), "member": member.cpu().numpy(),
-            "tables": [x.cpu().numpy()[:int(counts[RQ4A_MAX_ITER])] for x in tables], "intro": intro.cpu().numpy(),
-            "g4_steps": steps.cpu().numpy(), "g4_transition": trans.cpu().numpy()}
+    h = host_many(counts, sc, member, intro, steps, trans, *tables)
+    m = int(h[0][RQ4A_MAX_ITER])
+    return {"counts": h[0], "scalars": np.asarray(h[1]), "member": h[2], "tables": [x[:m] for x in h[6:]],
+            "intro": h[3], "g4_steps": h[4], "g4_transition": h[5]}
 
 
 # ----------------------------------------------------------------------------------------- RQ4b
@@ -434,15 +457,16 @@ def rq4b_sharded(shard, rank: int, world: int):
     P = part["member"].numel()
     offs = part["trend_offsets"]
     lens = (offs[1:] - offs[:-1]).to(torch.int64)
-    n = int(offs[-1].item())
+    nm = host_many(torch.stack([offs[-1], lens.max() if P > 0 else offs[-1] * 0]))[0]  # one sync
+    n, m_loc = int(nm[0]), int(nm[1])
     vals = part["trend_values"][:n]
-    starts = torch.repeat_interleave(offs[:-1], lens)
+    starts = torch.repeat_interleave(offs[:-1], lens, output_size=n)
     sids = torch.arange(n, dtype=torch.int64, device=dev) - starts
-    grp = torch.repeat_interleave(((part["member"].to(torch.int64) & 2) == 0).to(torch.uint8), lens)
-    m_loc = int(lens.max().item()) if P > 0 else 0
+    grp = torch.repeat_interleave(((part["member"].to(torch.int64) & 2) == 0).to(torch.uint8), lens, output_size=n)
     M = agree_max(m_loc, dev) if world > 1 else m_loc
-    sizes = torch.bincount(sids, minlength=M)[:M].to(torch.int64) if n else torch.zeros(M, dtype=torch.int64,
-                                                                                          device=dev)
+    sizes = torch.zeros(M, dtype=torch.int64, device=dev)
+    if n:
+        sizes.scatter_add_(0, sids, torch.ones_like(sids))
     if world > 1:
         all_reduce(sizes)
         all_reduce(counts)
@@ -463,18 +487,17 @@ def rq4b_sharded(shard, rank: int, world: int):
     if world > 1:
         got = all_gather_cols(cols)
         cols = [torch.cat([g[j] for g in got]) for j in range(len(cols))]
-    cols = [x.cpu().numpy() for x in cols]
+    dcols = cols
+    cols = host_many(*cols)
     res = {"c2": cols[0], "c1": cols[1], "g2_q": np.stack(cols[2:5], 1).reshape(-1),
            "g1_q": np.stack(cols[5:8], 1).reshape(-1), "p_bm": cols[8]}
     c2, c1 = res["c2"], res["c1"]
     ok = np.nonzero((c2 >= 100) & (c1 >= 100))[0]
     last = int(ok[-1]) if len(ok) else -1
     sp6 = np.full(12, np.nan)
-    if last >= 0:
-        q1m, q2m = res["g1_q"].reshape(-1, 3), res["g2_q"].reshape(-1, 3)
-        for k, seq in enumerate([q1m[:last + 1, j] for j in range(3)] + [q2m[:last + 1, j] for j in range(3)]):
-            rho, p = shard.series_tests(torch.from_numpy(np.ascontiguousarray(seq)).to(dev))[:2]
-            sp6[2 * k], sp6[2 * k + 1] = rho, p
+    if last >= 0:  # Spearman of G1 Q1 / Med / Q3, then G2 Q1 / Med / Q3 (:879-899), one call
+        seqs = [dcols[5 + j][:last + 1] for j in range(3)] + [dcols[2 + j][:last + 1] for j in range(3)]
+        sp6[:] = np.asarray(shard.spearman_many(seqs), dtype=np.float64).reshape(-1)
     counts[RQ4B_SESSIONS] = M
     counts[RQ4B_LAST] = last
     # coverage deltas: columns of every rank, in corpus CSV order
@@ -486,8 +509,9 @@ def rq4b_sharded(shard, rank: int, world: int):
         got = all_gather_cols([proj] + [pre[i] for i in range(7)] + [post[i] for i in range(7)])
         cat = [torch.cat([g[j] for g in got]) for j in range(15)]
         proj, pre, post = cat[0], torch.stack(cat[1:8]), torch.stack(cat[8:15])
-    order = np.argsort(proj.cpu().numpy(), kind="stable")
-    pre_h, post_h = pre.cpu().numpy()[:, order], post.cpu().numpy()[:, order]
+    proj_h, pre_h, post_h = host_many(proj, pre, post)
+    order = np.argsort(proj_h, kind="stable")
+    pre_h, post_h = pre_h[:, order], post_h[:, order]
     counts[RQ4B_DELTA_PROJECTS] = len(order)
     med = shard.row_medians(torch.from_numpy(np.concatenate([pre_h, post_h]).copy()).to(dev))
     pre_med, post_med = [float(v) for v in med[:7]], [float(v) for v in med[7:]]
@@ -496,10 +520,11 @@ def rq4b_sharded(shard, rank: int, world: int):
     if world > 1:
         x, y = torch.cat(all_gather_v(x)), torch.cat(all_gather_v(y))
     tests = shard.two_sample(x, y)
-    return {"counts": counts.cpu().numpy(), "c2": c2, "c1": c1, "g2_q": res["g2_q"], "g1_q": res["g1_q"],
+    counts_h, x_h, y_h = host_many(counts, x, y)
+    return {"counts": counts_h, "c2": c2, "c1": c1, "g2_q": res["g2_q"], "g1_q": res["g1_q"],
             "p_bm": res["p_bm"], "sp6": sp6, "pre_cov": [pre_h[i].copy() for i in range(7)],
             "post_cov": [post_h[i].copy() for i in range(7)], "pre_median": pre_med, "post_median": post_med,
-            "init_g2": x.cpu().numpy(), "init_g1": y.cpu().numpy(), "tests": tests}
+            "init_g2": x_h, "init_g1": y_h, "tests": tests}
 
 
 # ------------------------------------------------------------------------------------ row gathers
@@ -602,6 +627,23 @@ def gpu_series_tests(eng, x):
     return tuple(float(v) for v in out.cpu().tolist())
 
 
+def gpu_spearman_many(eng, seqs):
+    """fz_spearman_index_seg: [(rho, p)] of spearmanr(range(n), x) for several device series."""
+    import ctypes as C
+    from . import engine as E
+    torch = eng.torch
+    S = len(seqs)
+    x = torch.cat([q.reshape(-1).to(torch.float64) for q in seqs]).contiguous()
+    lens = [int(q.numel()) for q in seqs]
+    offs = torch.tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int64, device=eng.dev)
+    out = torch.empty(2 * S, dtype=torch.float64, device=eng.dev)
+    P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+    E._check(eng.lib, eng.lib.fz_spearman_index_seg(eng.ctx, P(x), x.numel(), P(offs), S, max(lens + [1]),
+                                                    P(out[:S]), P(out[S:])))
+    h = out.cpu().numpy()
+    return [(float(h[k]), float(h[S + k])) for k in range(S)]
+
+
 def gpu_rq4b_session_stats(eng, vals, sids, grp, S, max_len):
     """fz_rq4b_session_stats: per-session G2 (group 0) / G1 (group 1) counts, quartiles and
     Brunner-Munzel p of (value, session id, group) triples."""
@@ -648,7 +690,7 @@ class GpuRQ4aShard:
         intro = intro.contiguous()
         E._check(eng.lib, eng.lib.fz_rq4a_finish(eng.ctx, *[P(x) for x in tables], tables[0].numel(), P(intro),
                                                  intro.numel(), P(steps), P(counts), P(b.scalars)))
-        return b.scalars.cpu().numpy()
+        return b.scalars  # device: copied with the other results (parallel.host_many)
 
 
 class GpuRQ4bShard:
@@ -678,6 +720,9 @@ class GpuRQ4bShard:
 
     def series_tests(self, x):
         return gpu_series_tests(self.eng, x)
+
+    def spearman_many(self, seqs):
+        return gpu_spearman_many(self.eng, seqs)
 
     def mean_median(self, x):
         return gpu_mean_median(self.eng, x)
