@@ -406,3 +406,13 @@ def test_shard_bounds_cover_and_balance():
 @pytest.mark.parametrize("world,case", [(2, "collide"), (3, "collide"), (3, "last_shard_no_issues")])
 def test_sharded_rq1_rq3_match_whole_table(world, case, tmp_path):
     _spawn(world, case, tmp_path)
+
+
+def test_host_many_round_trips_dtypes():
+    import torch
+    ts = [torch.arange(5, dtype=torch.int64), torch.tensor([1.5, -2.0]), torch.tensor([[1, 2], [3, 4]], dtype=torch.uint8),
+          np.array([7, 8], dtype=np.int32)]
+    out = par.host_many(*ts)
+    for t, o in zip(ts, out):
+        ref = t.numpy() if isinstance(t, torch.Tensor) else t
+        assert o.dtype == ref.dtype and o.shape == ref.shape and np.array_equal(o, ref)

@@ -289,14 +289,14 @@ def rq3_sharded(shard, rank: int, world: int):
     part = shard.run()
     counts = part["counts"]
     if world > 1:
-        cl = [c.cpu().numpy() for c in all_gather(counts)]
+        cl = host_many(*all_gather(counts))
         cols = {}
         for keys in (RQ3_DET_F + RQ3_DET_I, RQ3_NON_F + RQ3_NON_I):
             got = all_gather_cols([part[k] for k in keys])
             for j, k in enumerate(keys):
                 cols[k] = [got[r][j] for r in range(world)]
     else:
-        cl = [counts.cpu().numpy()]
+        cl = host_many(counts)
         cols = {k: [part[k]] for k in RQ3_DET_F + RQ3_DET_I + RQ3_NON_F + RQ3_NON_I}
     with_issues = [r for r in range(world) if cl[r][RQ3_ISSUES] > 0]
     last = with_issues[-1] if with_issues else -1
@@ -517,8 +517,15 @@ def rq4b_sharded(shard, rank: int, world: int):
     pre_med, post_med = [float(v) for v in med[:7]], [float(v) for v in med[7:]]
     # initial coverage: samples in project order, tests once
     x, y = part["init_g2"], part["init_g1"]
-    if world > 1:
-        x, y = torch.cat(all_gather_v(x)), torch.cat(all_gather_v(y))
+    if world > 1:  # both samples in one variable gather: [len(x), x, y] per rank
+        nx = torch.tensor([x.numel()], dtype=torch.int64, device=x.device)
+        parts = all_gather_v(torch.cat([nx, x.contiguous().view(torch.int64), y.contiguous().view(torch.int64)]))
+        heads = host_many(torch.stack([q[0] for q in parts]))[0]
+        xs, ys = [], []
+        for q, k in zip(parts, heads.tolist()):
+            xs.append(q[1:1 + k].view(torch.float64))
+            ys.append(q[1 + k:].view(torch.float64))
+        x, y = torch.cat(xs), torch.cat(ys)
     tests = shard.two_sample(x, y)
     counts_h, x_h, y_h = host_many(counts, x, y)
     return {"counts": counts_h, "c2": c2, "c1": c1, "g2_q": res["g2_q"], "g1_q": res["g1_q"],
@@ -533,6 +540,10 @@ def gather_rows(cols: dict, world: int) -> dict:
     import torch
     if world == 1:
         return dict(cols)
+    keys = list(cols)
+    if len({int(cols[k].numel()) for k in keys}) == 1:  # equal-length columns: ONE gather
+        got = all_gather_cols([cols[k] for k in keys])
+        return {k: torch.cat([g[j] for g in got]) for j, k in enumerate(keys)}
     return {k: torch.cat(all_gather_v(v)) for k, v in cols.items()}
 
 
