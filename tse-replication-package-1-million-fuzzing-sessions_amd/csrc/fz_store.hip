@@ -153,18 +153,23 @@ __global__ __launch_bounds__(kBlock) void k_prefix_offsets(const uint64_t *__res
     offs[s] = lo;
 }
 
-// One workgroup per prefix segment, already in row order: bitonic sort of (time, position) pairs in
-// LDS - the position tie-break keeps equal times in row order (stable).  Longer segments are
-// counted into *big (the host re-sorts that table on the full-key path).  (Size-class variants -
-// 256 / 512 / 1024 threads for <= 1024 / 2048 / 4096 rows - measured slower in total: each class
-// launch still walks every segment.)
+// One workgroup per prefix segment, already in row order: bitonic sort in LDS of one packed u64 per
+// row, (time - segment min) << 12 | position (NULL times and the power-of-two pads get the top time
+// field): the position tie-break keeps equal times in row order (stable), and each compare-exchange
+// moves one word instead of a (time, position) pair.  Segments longer than MAXN rows, or whose
+// times span 2^52 us or more, are counted into *big (the host re-sorts that table on the full-key
+// path).  (Size-class variants - 256 / 512 / 1024 threads for <= 1024 / 2048 / 4096 rows - measured
+// slower in total: each class launch still walks every segment.)
+constexpr int kTsPosBits = 12;  // positions < 4096 = kSegSortMax
+constexpr uint64_t kTsTop = (uint64_t(1) << (64 - kTsPosBits)) - 1;  // time field of NULL / pad
 template <int BS, int MAXN>
 __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict__ rows, const int64_t *__restrict__ time,
                                                       const int64_t *__restrict__ offs, int64_t S, uint32_t pmask,
                                                       int32_t *__restrict__ orow, int64_t *__restrict__ otime,
                                                       uint32_t *__restrict__ oproj, unsigned long long *__restrict__ big) {
-    __shared__ int64_t st[MAXN];
-    __shared__ int32_t si[MAXN];
+    static_assert(MAXN <= (1 << kTsPosBits), "positions must fit the key");
+    __shared__ uint64_t sk[MAXN];
+    __shared__ int64_t s_lo[BS / kWave], s_hi[BS / kWave];
     const int tid = threadIdx.x;
 
     for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
@@ -178,23 +183,48 @@ __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict
         const int n = int(len);
         int np2 = 1;
         while (np2 < n) np2 <<= 1;
+        // gather the times (raw bits parked in sk) and their min / max over non-NULL rows
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        for (int i = tid; i < n; i += BS) {
+            const int64_t t = time[rows[b + i]];
+            sk[i] = uint64_t(t);
+            if (t != FZ_TS_NULL) {
+                lo = t < lo ? t : lo;
+                hi = t > hi ? t : hi;
+            }
+        }
+        lo = wave_min(lo);
+        hi = wave_max(hi);
+        if (lane_id() == 0) {
+            s_lo[wave_id()] = lo;
+            s_hi[wave_id()] = hi;
+        }
+        __syncthreads();
+        lo = INT64_MAX;
+        hi = INT64_MIN;
+        for (int w = 0; w < BS / kWave; ++w) {
+            lo = s_lo[w] < lo ? s_lo[w] : lo;
+            hi = s_hi[w] > hi ? s_hi[w] : hi;
+        }
+        if (hi >= lo && uint64_t(hi) - uint64_t(lo) >= kTsTop) {  // span too wide for the key
+            if (tid == 0) atomicAdd(big, (unsigned long long)len);
+            __syncthreads();
+            continue;
+        }
         for (int i = tid; i < np2; i += BS) {
-            st[i] = i < n ? time[rows[b + i]] : INT64_MAX;  // NULL = INT64_MAX sorts last; pads after
-            si[i] = i;
+            const int64_t t = i < n ? int64_t(sk[i]) : FZ_TS_NULL;
+            const uint64_t f = t == FZ_TS_NULL ? kTsTop : uint64_t(t - lo);
+            sk[i] = (f << kTsPosBits) | uint64_t(i);
         }
         __syncthreads();
         for (int k = 2; k <= np2; k <<= 1) {
             for (int j = k >> 1; j > 0; j >>= 1) {
                 for (int t = tid; t < (np2 >> 1); t += BS) {  // every thread owns pairs
                     const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;  // j = 2^m
-                    const int64_t ta = st[i], tb = st[ixj];
-                    const int32_t ia = si[i], ib = si[ixj];
-                    const bool gt = ta > tb || (ta == tb && ia > ib);
-                    if (gt == ((i & k) == 0)) {
-                        st[i] = tb;
-                        st[ixj] = ta;
-                        si[i] = ib;
-                        si[ixj] = ia;
+                    const uint64_t ka = sk[i], kb = sk[ixj];
+                    if ((ka > kb) == ((i & k) == 0)) {
+                        sk[i] = kb;
+                        sk[ixj] = ka;
                     }
                 }
                 bitonic_stage_sync(k, j, np2);
@@ -202,8 +232,10 @@ __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict
         }
         const uint32_t p = uint32_t(s) & pmask;
         for (int i = tid; i < n; i += BS) {
-            orow[b + i] = int32_t(rows[b + si[i]]);
-            otime[b + i] = st[i];
+            const uint64_t key = sk[i];
+            const uint64_t f = key >> kTsPosBits;
+            orow[b + i] = int32_t(rows[b + int64_t(key & ((1u << kTsPosBits) - 1))]);
+            otime[b + i] = f == kTsTop ? FZ_TS_NULL : lo + int64_t(f);
             oproj[b + i] = p;
         }
         __syncthreads();
