@@ -300,6 +300,10 @@ static_assert(kOsBlock >= kRadix && kSortTile % kOsBlock == 0, "radix pass shape
 // with 4 waves); 8-predecessor polls beat 16/32 (look-back traffic is bandwidth-limited).
 constexpr int kOsMaxPasses = 8;
 constexpr int kOsWindow = FZ_OS_WINDOW;
+#ifndef FZ_HIST_KPB
+#define FZ_HIST_KPB 2048
+#endif
+constexpr int kHistKeysPerBlock = FZ_HIST_KPB;  // keys per histogram workgroup (its flush is npass x 256 atomics)
 constexpr int kOsGroup = 8;  // tiles per look-back group (one {tiles, sum} word per group and digit)
 
 __global__ __launch_bounds__(kBlock) void k_onesweep_hist(const uint64_t *__restrict__ keys, int64_t n, int npass,
@@ -553,8 +557,8 @@ void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t 
     unsigned long long *gsum = c->arena.get<unsigned long long>(gwords * npass);
     {
         ProbeScope ps(c, "radix_hist", 8.0 * double(n));
-        k_onesweep_hist<<<grid_for(n, kBlock * 8, 2048), kBlock, 0, c->stream>>>(keys, n, npass, ghist, gsum,
-                                                                                gwords * npass);
+        k_onesweep_hist<<<grid_for(n, kHistKeysPerBlock, 2048), kBlock, 0, c->stream>>>(keys, n, npass, ghist, gsum,
+                                                                                       gwords * npass);
         FZ_LAUNCH_CHECK();
     }
     // Constant-digit passes are identity permutations.  Finding them needs a host round trip, which
@@ -905,18 +909,32 @@ void describe_f64(fz_ctx *c, const double *x, int64_t n, fz_describe *dev_out) {
 
 // ----------------------------------------------------------------------- views / compaction
 
-__global__ __launch_bounds__(kBlock) void k_segment_offsets_dn(const uint32_t *__restrict__ proj,
-                                                               const int64_t *__restrict__ d_n, int64_t P,
-                                                               int64_t *__restrict__ offsets) {
-    const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (p > P) return;
-    int64_t lo = 0, hi = *d_n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (int64_t(proj[mid]) < p) lo = mid + 1;
-        else hi = mid;
+// Offsets of a project-sorted array of device length: row i starts the segments (proj[i-1], proj[i]]; the ids
+// below the first row's and above the last row's are filled by id.  One coalesced read of proj
+// instead of a ~20-step dependent binary search per id.
+__global__ __launch_bounds__(kBlock) void k_segment_offsets_rows(const uint32_t *__restrict__ proj,
+                                                                 const int64_t *__restrict__ d_n, int64_t n_cap,
+                                                                 int64_t P, int64_t *__restrict__ offsets) {
+    const int64_t n = *d_n;
+    const int64_t first = n > 0 ? int64_t(proj[0]) : P + 1, last = n > 0 ? int64_t(proj[n - 1]) : -1;
+    const int64_t span = n_cap > P + 1 ? n_cap : P + 1;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < span; i += int64_t(gridDim.x) * kBlock) {
+        if (i <= P) {  // ids before the first row's and after the last row's
+            if (i <= first) offsets[i] = 0;  // lower_bound of the first row's id is 0 too
+            else if (i > last) offsets[i] = n;
+        }
+        if (i > 0 && i < n) {
+            const int64_t pp = int64_t(proj[i - 1]), pc = int64_t(proj[i]);
+            for (int64_t q = pp + 1; q <= pc && q <= P; ++q) offsets[q] = i;  // ids stay in [0, P]
+        }
     }
-    offsets[p] = lo;
+}
+
+void segment_offsets_dn(fz_ctx *c, const uint32_t *sorted_proj, const int64_t *d_n, int64_t n_cap, int64_t P,
+                        int64_t *offsets) {
+    const int64_t span = n_cap > P + 1 ? n_cap : P + 1;
+    k_segment_offsets_rows<<<grid_for(span, kBlock, 4096), kBlock, 0, c->stream>>>(sorted_proj, d_n, n_cap, P, offsets);
+    FZ_LAUNCH_CHECK();
 }
 
 __global__ __launch_bounds__(kBlock) void k_count_flags(const uint8_t *__restrict__ f, int64_t n, int64_t *out) {

@@ -99,8 +99,7 @@ void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_i
             sid[k] = uint32_t(key[k]);
         }
     });
-    k_segment_offsets_dn<<<grid_for(S + 1, kBlock, 1u << 30), kBlock, 0, st>>>(sid, d_n, S, offs);
-    FZ_LAUNCH_CHECK();
+    segment_offsets_dn(c, sid, d_n, n > 0 ? n : 1, S, offs);
     Segs ses{S, offs, n, max_len};
     session_stats(c, sv, ses, reinterpret_cast<const int32_t *>(sid), average, median, pcts, n_ge100);
 }
@@ -181,8 +180,7 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
         sid[k] = uint32_t(key[k] >> pbits);
         if (k < live) sv[k] = tv[idx[k]];
     });
-    k_segment_offsets_dn<<<grid_for(M + 1, kBlock, 1u << 30), kBlock, 0, st>>>(sid, d_nt, M, o->session_offsets);
-    FZ_LAUNCH_CHECK();
+    segment_offsets_dn(c, sid, d_nt, NC, M, o->session_offsets);
     if (flags & FZ_RQ2C_SKIP_SESSION_STATS) return;
 
     // per-session statistics (sessions are non-increasing in size: >= 100 is a prefix)

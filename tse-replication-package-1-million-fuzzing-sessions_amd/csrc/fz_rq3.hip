@@ -157,9 +157,7 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         dday[q] = fdiv_day(irts[j]);
     });
     int64_t *doffs = c->arena.get<int64_t>(P + 1);
-    k_segment_offsets_dn<<<grid_for(P + 1, kBlock, 1u << 30), kBlock, 0, st>>>(dproj, counts + FZ_RQ3_DETECTED, P,
-                                                                              doffs);
-    FZ_LAUNCH_CHECK();
+    segment_offsets_dn(c, dproj, counts + FZ_RQ3_DETECTED, NI, P, doffs);
 
     // ---- non-detected: projects with issues, except the last one (never flushed, :245-257) -
     // unless this is a shard that is not the last one (FZ_RQ3_FLUSH_LAST; the caller decides)

@@ -311,8 +311,7 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
         grp2[k] = uint8_t(sid2[k] & 1u);
     });
     int64_t *offs2 = c->arena.get<int64_t>(S2 + 1);
-    k_segment_offsets_dn<<<grid_for(S2 + 1, kBlock, 1u << 30), kBlock, 0, st>>>(sid2, d_nf, S2, offs2);
-    FZ_LAUNCH_CHECK();
+    segment_offsets_dn(c, sid2, d_nf, NC, S2, offs2);
     int64_t *soffs = c->arena.get<int64_t>(MM + 1);
     map_n(c, MM + 1, nullptr, [=] __device__(int64_t i) {
         soffs[i] = offs2[2 * i];

@@ -22,10 +22,9 @@ struct TmpView {
     int64_t *offs = nullptr;  // [P + 1]
 };
 
-// Offsets of a project-sorted array whose length is only known on the device.
-__global__ __launch_bounds__(kBlock) void k_segment_offsets_dn(const uint32_t *__restrict__ proj,
-                                                               const int64_t *__restrict__ d_n, int64_t P,
-                                                               int64_t *__restrict__ offsets);
+// Offsets [P + 1] of a project-sorted array of device length *d_n <= n_cap (row-parallel).
+void segment_offsets_dn(fz_ctx *c, const uint32_t *sorted_proj, const int64_t *d_n, int64_t n_cap, int64_t P,
+                        int64_t *offsets);
 
 // Single-pass order-preserving compaction of a view: each 4096-row tile evaluates pred, ranks its
 // kept rows in LDS, gets its output base by decoupled look-back over the preceding tiles, and
@@ -124,8 +123,7 @@ void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uin
         const int64_t zero = 0;
         set_i64(c, dst.d_n, &zero, 1);
     }
-    k_segment_offsets_dn<<<grid_for(P + 1, kBlock, 1u << 30), kBlock, 0, c->stream>>>(dst.proj, dst.d_n, P, dst.offs);
-    FZ_LAUNCH_CHECK();
+    segment_offsets_dn(c, dst.proj, dst.d_n, n, P, dst.offs);
 }
 
 // lower_bound of v in a[lo, hi)
