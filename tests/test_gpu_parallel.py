@@ -70,8 +70,8 @@ class _RQ4aView(_HostView):
 
 
 class _RQ4bView(_RQ2View):
-    def spearman_many(self, seqs):
-        return self.s.spearman_many([x.to(self.dev) for x in seqs])
+    def spearman_prefix(self, rows, n):
+        return self.s.spearman_prefix(rows.to(self.dev), n.to(self.dev)).cpu()
 
     def session_stats(self, vals, sids, grp, S, max_len):
         out = self.s.session_stats(vals.to(self.dev), sids.to(self.dev), grp.to(self.dev), S, max_len)

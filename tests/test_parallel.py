@@ -278,8 +278,9 @@ class OracleRQ4bShard(OracleRQ2CountShard):
                 "post_cov": T(np.concatenate(post) if projs else np.zeros(0)), "delta_order": T(dord, np.int64),
                 "init_g2": T(init["group2"]), "init_g1": T(init["group1"])}
 
-    def spearman_many(self, seqs):
-        return [self.series_tests(x)[:2] for x in seqs]
+    def spearman_prefix(self, rows, n):
+        n = int(n)
+        return np.array([self.series_tests(r[:n])[:2] for r in rows])
 
     def session_stats(self, vals, sids, grp, S, max_len):
         from oracle import rq_oracle as orc

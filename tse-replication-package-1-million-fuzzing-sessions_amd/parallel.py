@@ -373,14 +373,15 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     if world > 1:  # per-session rows (average, median, 5 percentiles) of every owner, session order
         block = torch.cat([m.reshape(-1, 7).view(torch.float64) for m in all_gather_v(block.reshape(-1).view(
             torch.int64))])
-    block = block.cpu().numpy()
-    res = {"average": block[:, 0].copy(), "median": block[:, 1].copy(), "percentiles": block[:, 2:].reshape(-1).copy()}
     K = int(np.sum(sizes_h >= 100))
-    tests = shard.series_tests(torch.from_numpy(res["median"][:K].copy()).to(dev))
+    tests = shard.series_tests(block[:K, 1].contiguous())  # median trend of the sessions with >= 100 values
     elig = proj["eligible"] != 0
     corr = proj["corr"][elig][proj["raw_n"][elig] > 0]
     valid = corr[~np.isnan(corr)]
     corr_mm = shard.mean_median(torch.from_numpy(valid.copy()).to(dev))
+    block, tests, corr_mm = host_many(block, tests, corr_mm)  # the one result copy
+    tests, corr_mm = tuple(float(v) for v in tests), tuple(float(v) for v in corr_mm)
+    res = {"average": block[:, 0].copy(), "median": block[:, 1].copy(), "percentiles": block[:, 2:].reshape(-1).copy()}
     out = {"proj": proj, "session_offsets": np.concatenate([[0], np.cumsum(sizes_h)]).astype(np.int64), "K": K,
            "average": res["average"], "median": res["median"], "percentiles": res["percentiles"],
            "tests": tests, "corr_mm": corr_mm}
@@ -442,14 +443,15 @@ def rq4a_sharded(shard, rank: int, world: int, lo: int, hi: int):
 def rq4b_sharded(shard, rank: int, world: int):
     """Exact RQ4b over project shards (rq4b_coverage.py:1209-1261).  ``shard.run()`` -> counts,
     member[P], the G1/G2 full coverage series (trend_values, trend_offsets[P + 1]), the delta columns
-    (pre_cov / post_cov step-major, delta_order = CSV row of each column) and the initial-coverage
-    samples;
-    ``shard.session_stats(values, sids, groups, S, max_len)``, ``shard.series_tests(x)``,
-    ``shard.mean_median(x)`` and ``shard.two_sample(x, y)`` run the statistics.  Exchange: session
-    sizes all-reduced, (value, session, group) triples all-to-all'd to the owner of the session
-    index, per-session results, delta columns (re-ordered by CSV row, :216, :744) and initial samples
-    gathered.  Returns a dict for
-    rq/compute.rq4b_result (host arrays, every rank)."""
+    (pre_cov / post_cov step-major, delta_order = CSV row of each column; at least counts' lengths)
+    and the initial-coverage samples;
+    ``shard.session_stats(values, sids, groups, S, max_len)``, ``shard.spearman_prefix(rows, n)``,
+    ``shard.row_medians(rows)`` and ``shard.two_sample(x, y)`` run the statistics (tensors or arrays
+    in, tensors or arrays out).  Exchange: session sizes all-reduced, (value, session, group) triples
+    all-to-all'd to the owner of the session index, per-session results, delta columns (re-ordered
+    by CSV row, :216, :744) and initial samples gathered.  Intermediates stay on the device; the
+    results are copied to the host once.  Returns a dict for rq/compute.rq4b_result (host arrays,
+    every rank)."""
     import torch
     part = shard.run()
     counts = part["counts"].clone()
@@ -457,8 +459,9 @@ def rq4b_sharded(shard, rank: int, world: int):
     P = part["member"].numel()
     offs = part["trend_offsets"]
     lens = (offs[1:] - offs[:-1]).to(torch.int64)
-    nm = host_many(torch.stack([offs[-1], lens.max() if P > 0 else offs[-1] * 0]))[0]  # one sync
-    n, m_loc = int(nm[0]), int(nm[1])
+    head = torch.stack([offs[-1].to(torch.int64), lens.max() if P > 0 else offs[-1].to(torch.int64) * 0,
+                        counts[RQ4B_DELTA_PROJECTS], counts[RQ4B_INIT_G2], counts[RQ4B_INIT_G1]])
+    n, m_loc, nd, n2, n1 = (int(v) for v in host_many(head)[0])  # one sync for every host-side size
     vals = part["trend_values"][:n]
     starts = torch.repeat_interleave(offs[:-1], lens, output_size=n)
     sids = torch.arange(n, dtype=torch.int64, device=dev) - starts
@@ -470,14 +473,16 @@ def rq4b_sharded(shard, rank: int, world: int):
     if world > 1:
         all_reduce(sizes)
         all_reduce(counts)
-    own = session_owners(sizes.cpu().numpy(), world)
-    if world > 1:  # route every value to the owner of its session index
+        own = session_owners(host_many(sizes)[0], world)
+        # route every value to the owner of its session index
         cuts = torch.tensor([b for _, b in own], dtype=torch.int64, device=dev)
         dest = torch.searchsorted(cuts, sids, right=True)
         perm = torch.argsort(dest, stable=True)
         send = torch.bincount(dest, minlength=world).tolist() if n else [0] * world
         vals, sids, grp = all_to_all_cols([vals[perm], sids[perm], grp[perm]], send)
         grp = grp.to(torch.uint8)
+    else:
+        own = [(0, M)]
     a, b = own[rank]
     S = b - a
     st = shard.session_stats(vals, sids - a, grp, S, P)
@@ -487,36 +492,27 @@ def rq4b_sharded(shard, rank: int, world: int):
     if world > 1:
         got = all_gather_cols(cols)
         cols = [torch.cat([g[j] for g in got]) for j in range(len(cols))]
-    dcols = cols
-    cols = host_many(*cols)
-    res = {"c2": cols[0], "c1": cols[1], "g2_q": np.stack(cols[2:5], 1).reshape(-1),
-           "g1_q": np.stack(cols[5:8], 1).reshape(-1), "p_bm": cols[8]}
-    c2, c1 = res["c2"], res["c1"]
-    ok = np.nonzero((c2 >= 100) & (c1 >= 100))[0]
-    last = int(ok[-1]) if len(ok) else -1
-    sp6 = np.full(12, np.nan)
-    if last >= 0:  # Spearman of G1 Q1 / Med / Q3, then G2 Q1 / Med / Q3 (:879-899), one call
-        seqs = [dcols[5 + j][:last + 1] for j in range(3)] + [dcols[2 + j][:last + 1] for j in range(3)]
-        sp6[:] = np.asarray(shard.spearman_many(seqs), dtype=np.float64).reshape(-1)
-    counts[RQ4B_SESSIONS] = M
-    counts[RQ4B_LAST] = last
+    c2d, c1d = cols[0], cols[1]
+    # last session with both groups >= 100 (:849-860), on the device
+    idx = torch.arange(c2d.numel(), dtype=torch.int64, device=c2d.device)
+    ok = (c2d >= 100) & (c1d >= 100)
+    last_d = torch.where(ok, idx, torch.full_like(idx, -1)).max() if c2d.numel() else torch.tensor(-1)
+    # Spearman of G1 Q1 / Med / Q3, then G2 Q1 / Med / Q3 over sessions 0..last (:879-899), one call
+    quart = torch.stack([cols[5], cols[6], cols[7], cols[2], cols[3], cols[4]]).to(torch.float64)
+    sp = shard.spearman_prefix(quart, last_d + 1)
     # coverage deltas: columns of every rank, in corpus CSV order
-    nd = int(part["delta_order"].numel())
-    proj = part["delta_order"]
-    pre = part["pre_cov"][:7 * nd].reshape(7, nd) if nd else torch.zeros(7, 0, dtype=torch.float64, device=dev)
-    post = part["post_cov"][:7 * nd].reshape(7, nd) if nd else torch.zeros(7, 0, dtype=torch.float64, device=dev)
+    proj = part["delta_order"][:nd]
+    pre = part["pre_cov"][:7 * nd].reshape(7, nd)
+    post = part["post_cov"][:7 * nd].reshape(7, nd)
     if world > 1:  # one gather: (CSV row, 7 pre, 7 post) per delta column
         got = all_gather_cols([proj] + [pre[i] for i in range(7)] + [post[i] for i in range(7)])
         cat = [torch.cat([g[j] for g in got]) for j in range(15)]
         proj, pre, post = cat[0], torch.stack(cat[1:8]), torch.stack(cat[8:15])
-    proj_h, pre_h, post_h = host_many(proj, pre, post)
-    order = np.argsort(proj_h, kind="stable")
-    pre_h, post_h = pre_h[:, order], post_h[:, order]
-    counts[RQ4B_DELTA_PROJECTS] = len(order)
-    med = shard.row_medians(torch.from_numpy(np.concatenate([pre_h, post_h]).copy()).to(dev))
-    pre_med, post_med = [float(v) for v in med[:7]], [float(v) for v in med[7:]]
+    order = torch.argsort(proj, stable=True)
+    pre, post = pre[:, order], post[:, order]
+    med = shard.row_medians(torch.cat([pre, post]).contiguous())
     # initial coverage: samples in project order, tests once
-    x, y = part["init_g2"], part["init_g1"]
+    x, y = part["init_g2"][:n2], part["init_g1"][:n1]
     if world > 1:  # both samples in one variable gather: [len(x), x, y] per rank
         nx = torch.tensor([x.numel()], dtype=torch.int64, device=x.device)
         parts = all_gather_v(torch.cat([nx, x.contiguous().view(torch.int64), y.contiguous().view(torch.int64)]))
@@ -527,11 +523,20 @@ def rq4b_sharded(shard, rank: int, world: int):
             ys.append(q[1 + k:].view(torch.float64))
         x, y = torch.cat(xs), torch.cat(ys)
     tests = shard.two_sample(x, y)
-    counts_h, x_h, y_h = host_many(counts, x, y)
-    return {"counts": counts_h, "c2": c2, "c1": c1, "g2_q": res["g2_q"], "g1_q": res["g1_q"],
-            "p_bm": res["p_bm"], "sp6": sp6, "pre_cov": [pre_h[i].copy() for i in range(7)],
-            "post_cov": [post_h[i].copy() for i in range(7)], "pre_median": pre_med, "post_median": post_med,
-            "init_g2": x_h, "init_g1": y_h, "tests": tests}
+    h = host_many(counts, last_d, sp, pre, post, med, x, y, tests, *cols)  # the one result copy
+    counts_h, last, sp, pre_h, post_h, med, x_h, y_h, tests = h[:9]
+    cols = h[9:]
+    last = int(last)
+    sp6 = np.asarray(sp, dtype=np.float64).reshape(-1) if last >= 0 else np.full(12, np.nan)
+    counts_h[RQ4B_SESSIONS] = M
+    counts_h[RQ4B_LAST] = last
+    counts_h[RQ4B_DELTA_PROJECTS] = pre_h.shape[1]
+    med = np.asarray(med, dtype=np.float64)
+    return {"counts": counts_h, "c2": cols[0], "c1": cols[1], "g2_q": np.stack(cols[2:5], 1).reshape(-1),
+            "g1_q": np.stack(cols[5:8], 1).reshape(-1), "p_bm": cols[8], "sp6": sp6,
+            "pre_cov": [pre_h[i].copy() for i in range(7)], "post_cov": [post_h[i].copy() for i in range(7)],
+            "pre_median": [float(v) for v in med[:7]], "post_median": [float(v) for v in med[7:]],
+            "init_g2": x_h, "init_g1": y_h, "tests": np.asarray(tests, dtype=np.float64)}
 
 
 # ------------------------------------------------------------------------------------ row gathers
@@ -635,24 +640,30 @@ def gpu_series_tests(eng, x):
     x = x.contiguous()
     E._check(eng.lib, eng.lib.fz_series_tests(eng.ctx, C.c_void_p(x.data_ptr()) if x.numel() else None, x.numel(),
                                               C.c_void_p(out.data_ptr())))
-    return tuple(float(v) for v in out.cpu().tolist())
+    return out  # device [4]: read with the other results (host_many)
 
 
-def gpu_spearman_many(eng, seqs):
-    """fz_spearman_index_seg: [(rho, p)] of spearmanr(range(n), x) for several device series."""
+def gpu_spearman_prefix(eng, rows, n):
+    """fz_spearman_index_seg over the first n (a device scalar) entries of every row of a [k, M]
+    device block -> device [k, 2] (rho, p); no host round trip."""
     import ctypes as C
     from . import engine as E
     torch = eng.torch
-    S = len(seqs)
-    x = torch.cat([q.reshape(-1).to(torch.float64) for q in seqs]).contiguous()
-    lens = [int(q.numel()) for q in seqs]
-    offs = torch.tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int64, device=eng.dev)
-    out = torch.empty(2 * S, dtype=torch.float64, device=eng.dev)
+    k, M = rows.shape
+    n = n.to(torch.int64).reshape(()).clamp(min=0, max=M)
+    j = torch.arange(k * M, dtype=torch.int64, device=eng.dev)
+    nn = torch.clamp(n, min=1)
+    src = torch.where(j < k * n, (j // nn) * M + j % nn, torch.zeros_like(j))  # row-major prefixes, packed
+    x = rows.reshape(-1).to(torch.float64)[src].contiguous()
+    offs = (torch.arange(k + 1, dtype=torch.int64, device=eng.dev) * n).contiguous()
+    out = torch.empty(2 * k, dtype=torch.float64, device=eng.dev)
     P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
-    E._check(eng.lib, eng.lib.fz_spearman_index_seg(eng.ctx, P(x), x.numel(), P(offs), S, max(lens + [1]),
-                                                    P(out[:S]), P(out[S:])))
-    h = out.cpu().numpy()
-    return [(float(h[k]), float(h[S + k])) for k in range(S)]
+    if k * M > 0:
+        E._check(eng.lib, eng.lib.fz_spearman_index_seg(eng.ctx, P(x), x.numel(), P(offs), k, M, P(out[:k]),
+                                                        P(out[k:])))
+    else:
+        out.fill_(float("nan"))
+    return torch.stack([out[:k], out[k:]], 1)
 
 
 def gpu_rq4b_session_stats(eng, vals, sids, grp, S, max_len):
@@ -674,9 +685,9 @@ def gpu_rq4b_session_stats(eng, vals, sids, grp, S, max_len):
 def gpu_mean_median(eng, x):
     """(mean, median) of one device vector through fz_describe_f64 (NaN when empty)."""
     if x.numel() == 0:
-        return float("nan"), float("nan")
+        return np.array([np.nan, np.nan])
     d = eng.describe(x.contiguous())
-    return float(d.mean), float(d.median)
+    return np.array([float(d.mean), float(d.median)])
 
 
 class GpuRQ4aShard:
@@ -719,12 +730,10 @@ class GpuRQ4bShard:
         E, C, eng, b = self.E, self.C, self.eng, self.bufs
         E._check(eng.lib, eng.lib.fz_rq4b_ex(eng.ctx, C.byref(eng.groups), E.FZ_RQ4B_SKIP_SESSION_STATS,
                                              C.byref(b.out)))
-        cnt = b.counts.cpu()
-        nd, n2, n1 = (int(cnt[k]) for k in (E.RQ4B_DELTA_PROJECTS, E.RQ4B_INIT_G2, E.RQ4B_INIT_G1))
-        P = eng.tables.fz.n_projects
+        P = eng.tables.fz.n_projects  # column lengths stay on the device (counts); rq4b_sharded slices
         return {"counts": b.counts, "member": b.member[:P], "trend_values": b.trend_values,
-                "trend_offsets": b.trend_offsets[:P + 1], "pre_cov": b.pre_cov[:7 * nd], "post_cov": b.post_cov[:7 * nd],
-                "delta_order": b.delta_order[:nd], "init_g2": b.init_g2[:n2], "init_g1": b.init_g1[:n1]}
+                "trend_offsets": b.trend_offsets[:P + 1], "pre_cov": b.pre_cov, "post_cov": b.post_cov,
+                "delta_order": b.delta_order, "init_g2": b.init_g2, "init_g1": b.init_g1}
 
     def session_stats(self, vals, sids, grp, S, max_len):
         return gpu_rq4b_session_stats(self.eng, vals, sids, grp, S, max_len)
@@ -732,18 +741,18 @@ class GpuRQ4bShard:
     def series_tests(self, x):
         return gpu_series_tests(self.eng, x)
 
-    def spearman_many(self, seqs):
-        return gpu_spearman_many(self.eng, seqs)
+    def spearman_prefix(self, rows, n):
+        return gpu_spearman_prefix(self.eng, rows, n)
 
     def mean_median(self, x):
         return gpu_mean_median(self.eng, x)
 
     def row_medians(self, rows):
-        """statistics.median of every row of a [k, n] device block (NaN for n == 0), one call."""
+        """statistics.median of every row of a [k, n] device block (NaN for n == 0), one call; device."""
         k, n = rows.shape
         sids = self.eng.torch.arange(k, dtype=self.eng.torch.int64, device=self.eng.dev).repeat_interleave(n)
         out = gpu_session_stats(self.eng, rows.reshape(-1).contiguous(), sids, k, n)
-        return out["median"][:k].cpu().numpy()
+        return out["median"][:k]
 
     def two_sample(self, x, y):
         E, C, eng = self.E, self.C, self.eng
@@ -752,7 +761,7 @@ class GpuRQ4bShard:
         P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
         if x.numel() and y.numel():
             E._check(eng.lib, eng.lib.fz_two_sample_tests(eng.ctx, P(x), x.numel(), P(y), y.numel(), P(out)))
-        return out.cpu().numpy()
+        return out  # device: copied with the other results
 
 
 class GpuRQ3Shard:
