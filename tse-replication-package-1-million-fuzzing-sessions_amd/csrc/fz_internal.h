@@ -180,6 +180,10 @@ struct fz_ctx {
     fz::DevBuf os_ticket;          // uint32 [1]
     unsigned int os_ticket_base = 0;
     unsigned int os_epoch = 0;
+    // radix digit totals, two buffers used by alternate sorts: each sort's passes zero the other
+    // one, so the next sort's histogram starts from zero without a memset launch
+    fz::DevBuf os_hist;            // uint64 [2][kOsMaxPasses * 256]
+    int os_hist_cur = -1;          // buffer of the next sort (-1: not allocated / not known zero)
 };
 
 namespace fz {

@@ -368,7 +368,8 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const uint64_t *__restric
                                                      int64_t n, int shift, const unsigned long long *__restrict__ ghist,
                                                      uint64_t *__restrict__ status, unsigned int *__restrict__ ticket,
                                                      unsigned int ticket_base, uint64_t epoch,
-                                                     unsigned long long *__restrict__ gsum) {
+                                                     unsigned long long *__restrict__ gsum,
+                                                     unsigned long long *__restrict__ next_hist) {
     __shared__ uint64_t s_keys[kSortTile];
     __shared__ uint32_t s_vals[HAS_VALS ? kSortTile : 1];
     __shared__ uint32_t s_run[kRadix];
@@ -383,6 +384,8 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const uint64_t *__restric
     const int w = wave_id(), lane = lane_id();
     if (tid == 0) s_tile = atomicAdd(ticket, 1u) - ticket_base;
     const bool dig = tid < kRadix;  // threads [0, 256) own one digit each after the ranking
+    if (next_hist && blockIdx.x == 0)  // the next sort's digit totals start from zero
+        for (int i = tid; i < kOsMaxPasses * kRadix; i += kOsBlock) next_hist[i] = 0ull;
     for (int i = tid; i < kOsWaves * kRadix; i += kOsBlock) (&s_wcnt[0][0])[i] = 0;
     const int64_t gcount = dig ? int64_t(ghist[tid]) : 0;  // issued early: consumed after the ranking
     __syncthreads();
@@ -550,8 +553,14 @@ void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t 
     const int64_t nb = (n + kSortTile - 1) / kSortTile;
     FZ_CHECK(n < (int64_t(1) << 47), "radix_sort_pairs: too many keys");
     // digit totals of every pass (one read of the keys)
-    unsigned long long *ghist = c->arena.get<unsigned long long>(kOsMaxPasses * kRadix);
-    FZ_HIP(hipMemsetAsync(ghist, 0, sizeof(unsigned long long) * kOsMaxPasses * kRadix, c->stream));
+    constexpr int64_t kHistWords = kOsMaxPasses * kRadix;
+    if (c->os_hist_cur < 0) {  // first sort of the context (or after a sort that ran no pass)
+        unsigned long long *h2 = c->os_hist.ensure<unsigned long long>(2 * kHistWords);
+        FZ_HIP(hipMemsetAsync(h2, 0, sizeof(unsigned long long) * 2 * kHistWords, c->stream));
+        c->os_hist_cur = 0;
+    }
+    unsigned long long *ghist = c->os_hist.as<unsigned long long>() + c->os_hist_cur * kHistWords;
+    unsigned long long *next_hist = c->os_hist.as<unsigned long long>() + (1 - c->os_hist_cur) * kHistWords;
     const int64_t ngroups = (nb + kOsGroup - 1) / kOsGroup;
     const int64_t gwords = ngroups * kRadix;  // per pass
     unsigned long long *gsum = c->arena.get<unsigned long long>(gwords * npass);
@@ -591,11 +600,13 @@ void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t 
             if (vals)
                 k_onesweep<true><<<unsigned(nb), kOsBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits,
                                                                            ghist + p * kRadix, lb.status, lb.ticket,
-                                                                           lb.base, lb.epoch, gsum + p * gwords);
+                                                                           lb.base, lb.epoch, gsum + p * gwords,
+                                                                           next_hist);
             else
                 k_onesweep<false><<<unsigned(nb), kOsBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits,
                                                                             ghist + p * kRadix, lb.status, lb.ticket,
-                                                                            lb.base, lb.epoch, gsum + p * gwords);
+                                                                            lb.base, lb.epoch, gsum + p * gwords,
+                                                                            next_hist);
             FZ_LAUNCH_CHECK();
         }
         lookback_end(c, nb);
@@ -606,6 +617,8 @@ void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t 
     keys = ka;  // the buffers holding the result (the inputs or arena scratch)
     vals = va;
     c->store.passes += passes;
+    // the passes zeroed the other buffer: it serves the next sort; with no pass nothing was zeroed
+    c->os_hist_cur = passes > 0 ? 1 - c->os_hist_cur : -1;
 }
 
 // ------------------------------------------------------------------------------- min / max
