@@ -160,13 +160,26 @@ __global__ __launch_bounds__(kBlock) void k_prefix_offsets(const uint64_t *__res
 // times span 2^52 us or more, are counted into *big (the host re-sorts that table on the full-key
 // path).  (Size-class variants - 256 / 512 / 1024 threads for <= 1024 / 2048 / 4096 rows - measured
 // slower in total: each class launch still walks every segment.)
+// Columns the time sort gathers into sorted order as it writes each segment (the materialisation
+// of the sorted store, fused: the random reads overlap other workgroups' sorting).  With perm set,
+// the kernel writes orow[k] = k (row id = sorted position) and perm[k] = the source row.
+constexpr int kMaxGather = 4;
+struct GatherCols {
+    int n = 0;
+    const void *src[kMaxGather] = {};
+    void *dst[kMaxGather] = {};
+    int size[kMaxGather] = {};  // bytes: 1, 4 or 8
+    int32_t *perm = nullptr;
+};
+
 constexpr int kTsPosBits = 12;  // positions < 4096 = kSegSortMax
 constexpr uint64_t kTsTop = (uint64_t(1) << (64 - kTsPosBits)) - 1;  // time field of NULL / pad
 template <int BS, int MAXN>
 __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict__ rows, const int64_t *__restrict__ time,
                                                       const int64_t *__restrict__ offs, int64_t S, uint32_t pmask,
                                                       int32_t *__restrict__ orow, int64_t *__restrict__ otime,
-                                                      uint32_t *__restrict__ oproj, unsigned long long *__restrict__ big) {
+                                                      uint32_t *__restrict__ oproj, unsigned long long *__restrict__ big,
+                                                      GatherCols gc) {
     static_assert(MAXN <= (1 << kTsPosBits), "positions must fit the key");
     __shared__ uint64_t sk[MAXN];
     __shared__ int64_t s_lo[BS / kWave], s_hi[BS / kWave];
@@ -234,9 +247,24 @@ __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict
         for (int i = tid; i < n; i += BS) {
             const uint64_t key = sk[i];
             const uint64_t f = key >> kTsPosBits;
-            orow[b + i] = int32_t(rows[b + int64_t(key & ((1u << kTsPosBits) - 1))]);
-            otime[b + i] = f == kTsTop ? FZ_TS_NULL : lo + int64_t(f);
-            oproj[b + i] = p;
+            const int64_t q = b + i;
+            const int32_t r = int32_t(rows[b + int64_t(key & ((1u << kTsPosBits) - 1))]);
+            otime[q] = f == kTsTop ? FZ_TS_NULL : lo + int64_t(f);
+            oproj[q] = p;
+            if (gc.perm) {
+                gc.perm[q] = r;
+                orow[q] = int32_t(q);
+                for (int j = 0; j < gc.n; ++j) {
+                    if (gc.size[j] == 8)
+                        static_cast<uint64_t *>(gc.dst[j])[q] = static_cast<const uint64_t *>(gc.src[j])[r];
+                    else if (gc.size[j] == 4)
+                        static_cast<uint32_t *>(gc.dst[j])[q] = static_cast<const uint32_t *>(gc.src[j])[r];
+                    else
+                        static_cast<uint8_t *>(gc.dst[j])[q] = static_cast<const uint8_t *>(gc.src[j])[r];
+                }
+            } else {
+                orow[q] = r;
+            }
         }
         __syncthreads();
     }
@@ -245,7 +273,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict
 // Sorts by (prefix, time, row); returns the device counter of rows in segments too long for LDS
 // (non-zero -> the caller re-sorts with sort_table()).
 static unsigned long long *sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time,
-                                           int32_t *orow, int64_t *otime, uint32_t *oproj) {
+                                           int32_t *orow, int64_t *otime, uint32_t *oproj, const GatherCols &gc) {
     unsigned long long *big = c->arena.get<unsigned long long>(1);
     FZ_HIP(hipMemsetAsync(big, 0, 8, c->stream));
     if (n <= 0) return big;
@@ -264,7 +292,7 @@ static unsigned long long *sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int
         ProbeScope ps(c, "seg_time_sort", 28.0 * double(n));  // row 4 + gathered time 8 + out 16 B
         const unsigned g = unsigned(S < 16384 ? S : 16384);
         k_seg_time_sort<kTimeSortBlock, kSegSortMax><<<g, kTimeSortBlock, 0, c->stream>>>(vals, time, offs, S, pmask, orow,
-                                                                                    otime, oproj, big);
+                                                                                    otime, oproj, big, gc);
         FZ_LAUNCH_CHECK();
     }
     return big;
@@ -357,23 +385,25 @@ __global__ __launch_bounds__(kBlock) void k_sorted_issues(fz_tables t, int64_t n
     }
 }
 
-static void materialize_sorted(fz_ctx *c, const fz_tables &in) {
+// gather[k]: table k (builds, coverage, issues) still needs its columns gathered (it was re-sorted
+// on the full-key path; the time sort gathered the others)
+static void materialize_sorted(fz_ctx *c, const fz_tables &in, const bool gather[3]) {
     Store &s = c->store;
     const int64_t nb = in.n_builds, nc = in.n_cov, ni = in.n_issues;
     fz_tables &t = s.t;
-    if (nb > 0) {
+    if (nb > 0 && gather[0]) {
         k_sorted_builds<<<grid_for(nb, kBlock, 4096), kBlock, 0, c->stream>>>(
             in, nb, s.b_row.as<int32_t>(), s.b_perm.ensure<int32_t>(nb), s.sb_type.ensure<uint8_t>(nb),
             s.sb_result.ensure<uint8_t>(nb), s.sb_group.ensure<int32_t>(nb), s.sb_canon.ensure<int32_t>(nb));
         FZ_LAUNCH_CHECK();
     }
-    if (nc > 0) {
+    if (nc > 0 && gather[1]) {
         k_sorted_coverage<<<grid_for(nc, kBlock, 4096), kBlock, 0, c->stream>>>(
             in, nc, s.c_row.as<int32_t>(), s.c_perm.ensure<int32_t>(nc), s.sc_coverage.ensure<double>(nc),
             s.sc_covered.ensure<int64_t>(nc), s.sc_total.ensure<int64_t>(nc), s.sc_valid.ensure<uint8_t>(nc));
         FZ_LAUNCH_CHECK();
     }
-    if (ni > 0) {
+    if (ni > 0 && gather[2]) {
         k_sorted_issues<<<grid_for(ni, kBlock, 4096), kBlock, 0, c->stream>>>(
             in, ni, s.i_row.as<int32_t>(), s.i_perm.ensure<int32_t>(ni), s.si_number.ensure<int64_t>(ni),
             s.si_status.ensure<uint8_t>(ni));
@@ -451,11 +481,34 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         {t->n_issues, Prefix{t->i_project, nullptr, pbits}, pbits, t->i_rts, mm[4], mm[5], &s.i_row, &s.i_time,
          &s.i_proj},
     };
+    GatherCols gcs[3];
+    {
+        const int64_t nb = t->n_builds, nc = t->n_cov, ni = t->n_issues;
+        GatherCols &gb = gcs[0];
+        gb.n = 4;
+        gb.perm = s.b_perm.ensure<int32_t>(nb);
+        gb.src[0] = t->b_type, gb.dst[0] = s.sb_type.ensure<uint8_t>(nb), gb.size[0] = 1;
+        gb.src[1] = t->b_result, gb.dst[1] = s.sb_result.ensure<uint8_t>(nb), gb.size[1] = 1;
+        gb.src[2] = t->b_group, gb.dst[2] = s.sb_group.ensure<int32_t>(nb), gb.size[2] = 4;
+        gb.src[3] = t->b_rev_canon, gb.dst[3] = s.sb_canon.ensure<int32_t>(nb), gb.size[3] = 4;
+        GatherCols &gv = gcs[1];
+        gv.n = 4;
+        gv.perm = s.c_perm.ensure<int32_t>(nc);
+        gv.src[0] = t->c_coverage, gv.dst[0] = s.sc_coverage.ensure<double>(nc), gv.size[0] = 8;
+        gv.src[1] = t->c_covered, gv.dst[1] = s.sc_covered.ensure<int64_t>(nc), gv.size[1] = 8;
+        gv.src[2] = t->c_total, gv.dst[2] = s.sc_total.ensure<int64_t>(nc), gv.size[2] = 8;
+        gv.src[3] = t->c_valid, gv.dst[3] = s.sc_valid.ensure<uint8_t>(nc), gv.size[3] = 1;
+        GatherCols &gi = gcs[2];
+        gi.n = 2;
+        gi.perm = s.i_perm.ensure<int32_t>(ni);
+        gi.src[0] = t->i_number, gi.dst[0] = s.si_number.ensure<int64_t>(ni), gi.size[0] = 8;
+        gi.src[1] = t->i_status, gi.dst[1] = s.si_status.ensure<uint8_t>(ni), gi.size[1] = 1;
+    }
     unsigned long long *big[3];
     for (int k = 0; k < 3; ++k) {
         Tab &b = tabs[k];
         big[k] = sort_table_fast(c, b.n, b.pre, b.pbits_total, b.time, b.row->ensure<int32_t>(b.n),
-                                 b.tm->ensure<int64_t>(b.n), b.pr->ensure<uint32_t>(b.n));
+                                 b.tm->ensure<int64_t>(b.n), b.pr->ensure<uint32_t>(b.n), gcs[k]);
     }
     auto make_views = [&]() {
         int32_t *row = s.b_row.as<int32_t>();
@@ -480,8 +533,10 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     };
     read_stats();
     bool redo = false;
+    bool gather[3] = {false, false, false};
     for (int k = 0; k < 3; ++k) {
-        if (c->h_pinned[4 + k] == 0) continue;  // every segment fit in LDS
+        if (c->h_pinned[4 + k] == 0) continue;  // every segment fit in LDS (columns gathered)
+        gather[k] = true;
         Tab &b = tabs[k];
         sort_table(c, b.n, b.pre, b.pbits_total, b.time, b.tmin, b.tmax, b.row->as<int32_t>(), b.tm->as<int64_t>(),
                    b.pr->as<uint32_t>());
@@ -492,7 +547,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         make_views();
         read_stats();
     }
-    materialize_sorted(c, *t);
+    materialize_sorted(c, *t, gather);
     s.fuzz.max_seg = c->h_pinned[0];
     s.covb.max_seg = c->h_pinned[1];
     s.cov.max_seg = c->h_pinned[2];
