@@ -29,3 +29,54 @@ def test_csv_export_ingest_preserves_results(tmp_path_factory, fn):
     assert np.array_equal(t2.c_coverage, t.c_coverage)
     assert np.array_equal(t2.group_key() == t2.group_key()[0], t.group_key() == t.group_key()[0])
     assert_same(fn(t2), fn(t))
+
+
+def test_copy_text_escapes_roundtrip():
+    s = "a\\b\tc\nd\re\x08f\x0cg\x0bh"
+    enc = store._copy_escape(s)
+    assert "\t" not in enc and "\n" not in enc
+    assert store._copy_unescape(enc) == s
+    assert store._copy_escape(None) == "\\N"
+    assert store._copy_unescape("\\101\\x42\\q") == "ABq"      # octal, hex, any other escaped char
+
+
+@pytest.mark.parametrize("fn", [orc.rq1, orc.rq2_count, orc.rq2_add, orc.rq3, orc.rq4a, orc.rq4b])
+def test_pg_dump_ingest_preserves_results(tmp_path_factory, fn):
+    """A plain-format dump (COPY text blocks, \\N NULLs, escapes in build names, unrelated tables
+    in between) reproduces the tables and every oracle result."""
+    t = goldens.tables("tiny")
+    d = tmp_path_factory.getbasetemp() / "dump"
+    sql = d / "backup_clean.sql"
+    if not sql.exists():
+        d.mkdir(exist_ok=True)
+        t.b_name = t.b_name.copy()
+        t.b_name[0] = "odd\tname\\with\nescapes"
+        store.to_pg_dump(t, str(sql))
+        txt = sql.read_text()
+        # an unrelated table (skipped) and a quoted COPY header, as pg_dump writes for some names
+        txt = txt.replace("CREATE TABLE public.issues",
+                          'COPY public."crash_log" (id, body) FROM stdin;\n1\tx\\ty\n2\t\\N\n\\.\n\n'
+                          "CREATE TABLE public.issues")
+        sql.write_text(txt)
+        (d / "project_corpus_analysis.csv").write_text(t.corpus_csv)
+    t2 = store.from_pg_dump(str(sql))
+    assert t2.projects == t.projects
+    assert t2.b_name[0] == "odd\tname\\with\nescapes"
+    assert np.array_equal(t2.b_time, t.b_time) and np.array_equal(t2.c_date, t.c_date)
+    assert np.array_equal(t2.c_coverage, t.c_coverage)
+    assert np.array_equal(t2.c_covered_valid, t.c_covered_valid) and np.array_equal(t2.i_rts, t.i_rts)
+    assert t2.corpus_csv == t.corpus_csv
+    assert_same(fn(t2), fn(t))
+
+
+def test_pg_dump_errors(tmp_path):
+    p = tmp_path / "bad.sql"
+    p.write_text("COPY public.issues (number, project) FROM stdin;\n1\tx\n")
+    with pytest.raises(ValueError, match="not terminated"):
+        store.from_pg_dump(str(p))
+    p.write_text("COPY public.issues (number, project) FROM stdin;\n1\tx\textra\n\\.\n")
+    with pytest.raises(ValueError, match="fields"):
+        store.from_pg_dump(str(p))
+    p.write_text("SELECT 1;\n")
+    with pytest.raises(ValueError, match="no COPY block"):
+        store.from_pg_dump(str(p))

@@ -27,18 +27,21 @@ SCRIPTS = ["rq1_detection_rate", "rq2_coverage_and_added", "rq2_coverage_count",
 
 def data_source() -> str:
     """Where the drop-ins read the session tables: $FZ_DATA (a columnar directory written by
-    ``store.save_columnar`` or a directory of PostgreSQL CSV exports), default data/columnar."""
+    ``store.save_columnar``, a directory of PostgreSQL CSV exports, or the plain-format dump
+    ``data/database/backup_clean.sql`` itself), default data/columnar."""
     return os.environ.get("FZ_DATA", os.path.join("data", "columnar"))
 
 
 def load_tables(path: Optional[str] = None) -> Tables:
     from .. import store
     path = path or data_source()
+    if os.path.isfile(path):
+        return store.from_pg_dump(path)
     if os.path.exists(os.path.join(path, "meta.json")):
         return store.load_columnar(path)
     if os.path.exists(os.path.join(path, "buildlog_data.csv")):
         return store.from_csv_dir(path)
-    raise FileNotFoundError(f"no session tables at {path!r} (set FZ_DATA to a columnar or CSV-export directory)")
+    raise FileNotFoundError(f"no session tables at {path!r} (set FZ_DATA to a columnar or CSV-export directory or a pg_dump .sql file)")
 
 
 def analyse(name: str, eng: E.Engine, t: Tables, cwd: str) -> render.Rendered:

@@ -13,11 +13,16 @@ Two on-disk forms feed ``schema.Tables`` (which ``engine.Engine.upload`` streams
   (``user_corpus.py:225-233``).  ``from_csv_dir`` dictionary-encodes ``project`` in byte order,
   maps ``build_type`` / ``result`` / ``status`` to the schema codes, parses timestamps to int64
   microseconds (naive), and keeps NULLs as validity bits / ``TS_NULL``.
+* the **plain-format dump** ``data/database/backup_clean.sql`` (README.md:14-15) read directly from
+  its ``COPY ... FROM stdin`` blocks by ``from_pg_dump`` (no PostgreSQL restore needed).
 """
 from __future__ import annotations
 
+import csv
+import io
 import json
 import os
+import re
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -115,8 +120,17 @@ def from_csv_dir(path: str, corpus_csv: Optional[str] = None) -> Tables:
     import pandas as pd
     rd = lambda name: pd.read_csv(os.path.join(path, name + ".csv"), dtype=str, keep_default_na=False,  # noqa: E731
                                   na_values=[""])
-    b, c, i = rd("buildlog_data"), rd("total_coverage"), rd("issues")
     pi = rd("project_info") if os.path.exists(os.path.join(path, "project_info.csv")) else None
+    if corpus_csv is None:
+        cp = os.path.join(path, "project_corpus_analysis.csv")
+        corpus_csv = open(cp).read() if os.path.exists(cp) else ""
+    return _from_frames(rd("buildlog_data"), rd("total_coverage"), rd("issues"), pi, corpus_csv)
+
+
+def _from_frames(b, c, i, pi, corpus_csv: str) -> Tables:
+    """Text frames (one ``str``/NULL cell per value) -> columnar ``Tables``; shared by the CSV-export
+    and the pg_dump ingest."""
+    import pandas as pd
     names = set(b["project"].dropna()) | set(c["project"].dropna()) | set(i["project"].dropna())
     if pi is not None:
         names |= set(pi["project"].dropna())
@@ -132,9 +146,6 @@ def from_csv_dir(path: str, corpus_csv: Optional[str] = None) -> Tables:
     tot, tot_ok = _nullable_int(c["total_line"])
     names_arr = np.empty(len(b), dtype=object)
     names_arr[:] = [None if isinstance(x, float) else x for x in b["name"].tolist()]
-    if corpus_csv is None:
-        cp = os.path.join(path, "project_corpus_analysis.csv")
-        corpus_csv = open(cp).read() if os.path.exists(cp) else ""
     return Tables(
         projects=projects,
         b_project=enc(b["project"]), b_type=_codes(b["build_type"], build_types),
@@ -194,3 +205,154 @@ def to_csv_dir(t: Tables, path: str) -> None:
             w.writerow([t.projects[t.pi_project[k]], ts(t.pi_first_commit[k])])
     with open(os.path.join(path, "project_corpus_analysis.csv"), "w") as f:
         f.write(t.corpus_csv)
+
+
+# ---------------------------------------------------------------------------------- pg_dump ingest
+# The reference's data ships as a plain-format PostgreSQL dump (``data/database/backup_clean.sql``,
+# README.md:14-15) that ``psql`` restores before any script runs.  Each table's rows sit in a
+# ``COPY <table> (<columns>) FROM stdin;`` block of PostgreSQL's text COPY format: one row per line,
+# tab-separated fields, ``\N`` = NULL, backslash escapes for \\ \b \f \n \r \t \v, octal \NNN and
+# hex \xHH, terminated by a ``\.`` line.  ``from_pg_dump`` streams the dump once, keeps only the four
+# tables the analyses read (other tables and all DDL are skipped) and feeds the same converter as
+# the CSV-export ingest, so no database server is needed.
+_DUMP_TABLES = ("buildlog_data", "total_coverage", "issues", "project_info")
+_COPY_RE = re.compile(r'^COPY\s+(?:"?[\w$]+"?\.)?"?(\w+)"?\s*\(([^)]*)\)\s+FROM\s+stdin;\s*$')
+_ESC_RE = re.compile(r"\\(x[0-9A-Fa-f]{1,2}|[0-7]{1,3}|.)")
+_ESC_CHARS = {"b": "\b", "f": "\f", "n": "\n", "r": "\r", "t": "\t", "v": "\v"}
+
+
+def _copy_unescape(field: str) -> str:
+    def rep(m):
+        e = m.group(1)
+        if e[0] == "x":
+            return chr(int(e[1:], 16))
+        if e[0] in "01234567":
+            return chr(int(e, 8) & 0xFF)
+        return _ESC_CHARS.get(e, e)
+    return _ESC_RE.sub(rep, field)
+
+
+def _copy_escape(v) -> str:
+    if v is None:
+        return "\\N"
+    s = str(v)
+    return (s.replace("\\", "\\\\").replace("\t", "\\t").replace("\n", "\\n").replace("\r", "\\r")
+            .replace("\b", "\\b").replace("\f", "\\f").replace("\v", "\\v"))
+
+
+def from_pg_dump(path: str, corpus_csv: Optional[str] = None) -> Tables:
+    """Ingest a plain-format ``pg_dump`` file (see above) into columnar ``Tables``.
+
+    ``corpus_csv``: text of ``project_corpus_analysis.csv`` (``rq4a_bug.py:34``); default: that
+    file next to the dump or under ``../processed_data/csv/`` as in the reference's data layout."""
+    import pandas as pd
+    blocks: Dict[str, List[str]] = {}
+    cols: Dict[str, List[str]] = {}
+    with open(path, encoding="utf-8", newline="\n") as f:
+        it = iter(f)
+        for line in it:
+            if not line.startswith("COPY "):
+                continue
+            m = _COPY_RE.match(line.rstrip("\n"))
+            if m is None:
+                continue
+            name = m.group(1)
+            keep = name in _DUMP_TABLES
+            if keep:
+                cols[name] = [c.strip().strip('"') for c in m.group(2).split(",")]
+                out = blocks.setdefault(name, [])
+                tabs = len(cols[name]) - 1
+            for row in it:
+                if row == "\\.\n" or row == "\\.":
+                    break
+                if keep:
+                    if row.count("\t") != tabs:
+                        raise ValueError(f"{path}: COPY {name}: {row.count(chr(9)) + 1} fields, expected {tabs + 1}")
+                    out.append(row if row.endswith("\n") else row + "\n")
+            else:
+                raise ValueError(f"{path}: COPY {name} block not terminated by \\.")
+    for need in _DUMP_TABLES[:3]:
+        if need not in blocks:
+            raise ValueError(f"{path}: no COPY block for table {need!r}")
+
+    def frame(name):
+        # the C tokenizer splits the block (tabs are always escaped inside fields, so no quoting);
+        # only cells holding a backslash go through the escape decoder
+        if not blocks[name]:
+            return pd.DataFrame({c: pd.Series([], dtype=object) for c in cols[name]})
+        text = "".join(blocks[name])
+        df = pd.read_csv(io.StringIO(text), sep="\t", header=None, names=cols[name], dtype=str,
+                         quoting=csv.QUOTE_NONE, keep_default_na=False, na_values=["\\N"],
+                         skip_blank_lines=False, engine="c")
+        if "\\" not in text.replace("\\N", ""):
+            return df
+        for c in df.columns:
+            col = df[c]
+            esc = col.str.contains("\\", regex=False, na=False)
+            if esc.any():
+                df.loc[esc, c] = col[esc].map(_copy_unescape)
+        return df
+
+    pi = frame("project_info") if "project_info" in blocks else None
+    if corpus_csv is None:
+        base = os.path.dirname(os.path.abspath(path))
+        for cp in (os.path.join(base, "project_corpus_analysis.csv"),
+                   os.path.join(base, "..", "processed_data", "csv", "project_corpus_analysis.csv")):
+            if os.path.exists(cp):
+                corpus_csv = open(cp).read()
+                break
+        else:
+            corpus_csv = ""
+    return _from_frames(frame("buildlog_data"), frame("total_coverage"), frame("issues"), pi, corpus_csv)
+
+
+def to_pg_dump(t: Tables, path: str) -> None:
+    """Write ``Tables`` as a plain-format dump (DDL + one COPY block per table) that ``psql`` can
+    restore and ``from_pg_dump`` reads back; used by tests and to seed a database."""
+    from .schema import us_to_dt
+
+    def ts(v):
+        return None if v == TS_NULL else str(us_to_dt(v))
+
+    def code(vocab, v):
+        return None if v == CODE_NULL else vocab[v]
+
+    def pool(p, k):
+        return None if k < 0 else p[k]
+
+    def block(f, name, ddl, header, it):
+        f.write(f"CREATE TABLE public.{name} (\n    " + ",\n    ".join(ddl) + "\n);\n\n")
+        f.write(f"COPY public.{name} ({', '.join(header)}) FROM stdin;\n")
+        for r in it:
+            f.write("\t".join(_copy_escape(v) for v in r) + "\n")
+        f.write("\\.\n\n")
+
+    P = t.projects
+    with open(path, "w", encoding="utf-8", newline="\n") as f:
+        f.write("--\n-- PostgreSQL database dump\n--\n\nSET client_encoding = 'UTF8';\n"
+                "SET standard_conforming_strings = on;\n\n")
+        block(f, "buildlog_data",
+              ["name text", "project text", "build_type text", "result text",
+               "timecreated timestamp without time zone", "modules text", "revisions text"],
+              ["name", "project", "build_type", "result", "timecreated", "modules", "revisions"],
+              ((t.b_name[k], P[t.b_project[k]], code(t.build_types, t.b_type[k]),
+                code(t.results, t.b_result[k]), ts(t.b_time[k]), pool(t.modules_pool, t.b_modules[k]),
+                pool(t.revisions_pool, t.b_revisions[k])) for k in range(len(t.b_project))))
+        block(f, "total_coverage",
+              ["project text", "date timestamp without time zone", "coverage double precision",
+               "covered_line integer", "total_line integer"],
+              ["project", "date", "coverage", "covered_line", "total_line"],
+              ((P[t.c_project[k]], ts(t.c_date[k]),
+                repr(float(t.c_coverage[k])) if t.c_coverage_valid[k] else None,
+                int(t.c_covered[k]) if t.c_covered_valid[k] else None,
+                int(t.c_total[k]) if t.c_total_valid[k] else None) for k in range(len(t.c_project))))
+        block(f, "issues",
+              ["number bigint", "project text", "rts timestamp without time zone", "status text",
+               "new_id bigint"],
+              ["number", "project", "rts", "status", "new_id"],
+              ((int(t.i_number[k]), P[t.i_project[k]], ts(t.i_rts[k]), code(t.statuses, t.i_status[k]),
+                int(t.i_new_id[k])) for k in range(len(t.i_project))))
+        block(f, "project_info", ["project text", "first_commit_datetime timestamp without time zone"],
+              ["project", "first_commit_datetime"],
+              ((P[t.pi_project[k]], ts(t.pi_first_commit[k])) for k in range(len(t.pi_project))))
+        f.write("--\n-- PostgreSQL database dump complete\n--\n")
