@@ -838,13 +838,19 @@ __device__ inline DD block_dd_sum_1024(DD acc, double *s_hi, double *s_lo) {
     return t;
 }
 
-__global__ __launch_bounds__(kSortBlock) void k_describe_small(const double *__restrict__ x,
-                                                               const int64_t *__restrict__ d_n,
-                                                               fz_describe *__restrict__ out) {
+struct DescSmallArgs {
+    const double *x[kDescBatch];
+    const int64_t *d_n[kDescBatch];
+    fz_describe *out[kDescBatch];
+};
+// one workgroup per job (blockIdx.x)
+__global__ __launch_bounds__(kSortBlock) void k_describe_small(DescSmallArgs a) {
     __shared__ uint64_t sk[kDescSmall];
     __shared__ double s_hi[kSortBlock / kWave], s_lo[kSortBlock / kWave];
     const int tid = threadIdx.x;
-    const int n = int(*d_n);
+    const double *__restrict__ x = a.x[blockIdx.x];
+    fz_describe *__restrict__ out = a.out[blockIdx.x];
+    const int n = int(*a.d_n[blockIdx.x]);
     int np2 = 1;
     while (np2 < n) np2 <<= 1;
     DD acc{0.0, 0.0};
@@ -891,12 +897,29 @@ uint64_t *sorted_keys_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t
 }
 
 void describe_f64_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n, fz_describe *dev_out) {
-    if (nmax <= kDescSmall) {  // one launch
-        k_describe_small<<<1, kSortBlock, 0, c->stream>>>(x, d_n, dev_out);
-        FZ_LAUNCH_CHECK();
-        return;
+    const DescJob j{x, nmax, d_n, dev_out};
+    describe_f64_dn_batch(c, &j, 1);
+}
+
+void describe_f64_dn_batch(fz_ctx *c, const DescJob *jobs, int njobs) {
+    FZ_CHECK(njobs <= kDescBatch, "describe batch larger than kDescBatch");
+    DescSmallArgs a{};
+    int ns = 0;
+    for (int i = 0; i < njobs; ++i) {
+        const DescJob &j = jobs[i];
+        if (j.nmax <= kDescSmall) {
+            a.x[ns] = j.x;
+            a.d_n[ns] = j.d_n;
+            a.out[ns] = j.out;
+            ++ns;
+        } else {
+            describe_sorted_dn(c, sorted_keys_dn(c, j.x, j.nmax, j.d_n), j.x, j.nmax, j.d_n, j.out);
+        }
     }
-    describe_sorted_dn(c, sorted_keys_dn(c, x, nmax, d_n), x, nmax, d_n, dev_out);
+    if (ns > 0) {  // every small job in one launch
+        k_describe_small<<<ns, kSortBlock, 0, c->stream>>>(a);
+        FZ_LAUNCH_CHECK();
+    }
 }
 
 void describe_sorted_dn(fz_ctx *c, const uint64_t *k, const double *x, int64_t nmax, const int64_t *d_n,

@@ -204,8 +204,6 @@ void rq4a_finish(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int6
         if (j < nafter[k]) after[k * MM + j] = rates[k * MM + first[k] + j];
     });
     fz_describe *dsc = c->arena.get<fz_describe>(3);
-    describe_f64_dn(c, after, MM, nafter, dsc);
-    describe_f64_dn(c, after + MM, MM, nafter + 1, dsc + 1);
 
     // introduction-iteration stats over the positive ones (pandas Series mean/median/min/max)
     int64_t *pf = c->arena.get<int64_t>(P), *pp = c->arena.get<int64_t>(P), *d_np = c->arena.get<int64_t>(1);
@@ -215,7 +213,8 @@ void rq4a_finish(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int6
     map_n(c, P, nullptr, [=] __device__(int64_t p) {
         if (pf[p]) iv[pp[p]] = double(intro[p]);
     });
-    describe_f64_dn(c, iv, P, d_np, dsc + 2);
+    const DescJob jobs[3] = {{after, MM, nafter, dsc}, {after + MM, MM, nafter + 1, dsc + 1}, {iv, P, d_np, dsc + 2}};
+    describe_f64_dn_batch(c, jobs, 3);
     map_n(c, 1, nullptr, [=] __device__(int64_t) {
         sc[FZ_RQ4A_AFTER_G1_MEDIAN] = dsc[0].median;
         sc[FZ_RQ4A_AFTER_G1_IQR] = dsc[0].q3 - dsc[0].q1;

@@ -152,6 +152,16 @@ __device__ inline void atomic_add_i64(int64_t *p, int64_t v) {
 void count_flags(fz_ctx *c, const uint8_t *flags, int64_t P, int64_t *out);
 // describe of x[0..*d_n) with nmax a host upper bound (fz_prims.hip).
 void describe_f64_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n, fz_describe *dev_out);
+// up to kDescBatch independent describes; all small ones (nmax <= 4096) share one launch (one
+// workgroup each), larger ones take the multi-launch path.
+constexpr int kDescBatch = 4;
+struct DescJob {
+    const double *x;
+    int64_t nmax;
+    const int64_t *d_n;
+    fz_describe *out;
+};
+void describe_f64_dn_batch(fz_ctx *c, const DescJob *jobs, int njobs);
 // ascending order-preserving keys (f64_key) of x[0..*d_n); entries past *d_n are ~0.
 uint64_t *sorted_keys_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n);
 // the same for nmax <= 4096 in one workgroup (LDS bitonic network, fz_series.hip)
