@@ -622,8 +622,16 @@ void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t 
 }
 
 // ------------------------------------------------------------------------------- min / max
-__global__ __launch_bounds__(kBlock) void k_minmax(const int64_t *__restrict__ x, int64_t n,
-                                                   unsigned long long *__restrict__ mm) {
+// min / max over non-NULL values of up to kMinMaxCols columns in one launch (blockIdx.y = column)
+constexpr int kMinMaxCols = 8;
+struct MinMaxCols {
+    const int64_t *x[kMinMaxCols];
+    int64_t n[kMinMaxCols];
+};
+__global__ __launch_bounds__(kBlock) void k_minmax(MinMaxCols cols, unsigned long long *__restrict__ mm) {
+    const int col = blockIdx.y;
+    const int64_t *__restrict__ x = cols.x[col];
+    const int64_t n = cols.n[col];
     int64_t lo = INT64_MAX, hi = INT64_MIN;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
         const int64_t v = x[i];
@@ -647,22 +655,28 @@ __global__ __launch_bounds__(kBlock) void k_minmax(const int64_t *__restrict__ x
         lo = s_lo[0] < lo ? s_lo[0] : lo;
         hi = s_hi[0] > hi ? s_hi[0] : hi;
         // order-preserving unsigned images so one unsigned atomic min/max covers negatives too
-        atomicMin(&mm[0], (unsigned long long)(lo) ^ 0x8000000000000000ull);
-        atomicMax(&mm[1], (unsigned long long)(hi) ^ 0x8000000000000000ull);
+        atomicMin(&mm[2 * col], (unsigned long long)(lo) ^ 0x8000000000000000ull);
+        atomicMax(&mm[2 * col + 1], (unsigned long long)(hi) ^ 0x8000000000000000ull);
     }
 }
 
 void minmax_i64_to_host(fz_ctx *c, const int64_t *const *cols, const int64_t *ns, int ncols, int64_t *host_minmax) {
+    FZ_CHECK(ncols >= 1 && ncols <= kMinMaxCols, "minmax: 1..8 columns");
     unsigned long long *mm = c->arena.get<unsigned long long>(2 * ncols);
     std::vector<unsigned long long> init(2 * ncols);
+    MinMaxCols mc{};
+    int64_t nmax = 0;
     for (int i = 0; i < ncols; ++i) {
         init[2 * i] = ~0ull;
         init[2 * i + 1] = 0ull;
+        mc.x[i] = cols[i];
+        mc.n[i] = ns[i] > 0 ? ns[i] : 0;
+        nmax = mc.n[i] > nmax ? mc.n[i] : nmax;
     }
     FZ_HIP(hipMemcpyAsync(mm, init.data(), init.size() * 8, hipMemcpyHostToDevice, c->stream));
-    for (int i = 0; i < ncols; ++i) {
-        if (ns[i] <= 0) continue;
-        k_minmax<<<grid_for(ns[i], kBlock * 8, 512), kBlock, 0, c->stream>>>(cols[i], ns[i], mm + 2 * i);
+    if (nmax > 0) {  // one launch for every column
+        const dim3 g(grid_for(nmax, kBlock * 8, 512), unsigned(ncols));
+        k_minmax<<<g, kBlock, 0, c->stream>>>(mc, mm);
         FZ_LAUNCH_CHECK();
     }
     FZ_HIP(hipMemcpyAsync(c->h_pinned, mm, 2 * ncols * 8, hipMemcpyDeviceToHost, c->stream));
@@ -703,16 +717,19 @@ __global__ __launch_bounds__(kBlock) void k_f64_keys(const double *__restrict__ 
         k[i] = i < n ? f64_key(x[i]) : ~0ull;
 }
 
-// Double-double partial sums of x (pass 1) or of (x - mean)^2 (pass 2, mean read from device).
-__global__ __launch_bounds__(kBlock) void k_dd_partial(const double *__restrict__ x, const int64_t *__restrict__ d_n,
-                                                       const double *__restrict__ mean, double *__restrict__ part) {
+// Double-double partial sums of x (pass 1) or of (x - mean)^2 (pass 2, mean read from device);
+// blockIdx.y = job, partials of job j at part[2 * gridDim.x * j ...].
+__global__ __launch_bounds__(kBlock) void k_dd_partial(SortedDescArgs a, const double *__restrict__ ms,
+                                                       double *__restrict__ part) {
     __shared__ double s_hi[4], s_lo[4];
-    const int64_t n = *d_n;
+    const int j = blockIdx.y;
+    const double *__restrict__ x = a.x[j];
+    const int64_t n = *a.d_n[j];
     DD acc{0.0, 0.0};
-    const double m = mean ? *mean : 0.0;
+    const double m = ms ? ms[2 * j] : 0.0;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
         double v = x[i];
-        if (mean) {
+        if (ms) {
             v = v - m;
             v = v * v;
         }
@@ -727,19 +744,22 @@ __global__ __launch_bounds__(kBlock) void k_dd_partial(const double *__restrict_
     if (threadIdx.x == 0) {
         DD t{s_hi[0], s_lo[0]};
         for (int i = 1; i < 4; ++i) t = dd_add(t, DD{s_hi[i], s_lo[i]});
-        part[2 * blockIdx.x] = t.hi;
-        part[2 * blockIdx.x + 1] = t.lo;
+        double *pj = part + 2 * int64_t(gridDim.x) * j;
+        pj[2 * blockIdx.x] = t.hi;
+        pj[2 * blockIdx.x + 1] = t.lo;
     }
 }
 
-// Reduce the partials; writes sum/n to *out (mode 0: mean; mode 1: sqrt(sum/n) = std, ddof 0).
-__global__ __launch_bounds__(kBlock) void k_dd_final(const double *__restrict__ part, int nparts,
-                                                     const int64_t *__restrict__ d_n, int mode,
-                                                     double *__restrict__ out) {
+// Reduce job blockIdx.x's partials; writes sum/n to ms[2 * job + mode] (mode 0: mean; mode 1:
+// sqrt(sum/n) = std, ddof 0).
+__global__ __launch_bounds__(kBlock) void k_dd_final(const double *__restrict__ part, int nparts, SortedDescArgs a,
+                                                     int mode, double *__restrict__ ms) {
     __shared__ double s_hi[4], s_lo[4];
-    const int64_t n = *d_n;
+    const int j = blockIdx.x;
+    const int64_t n = *a.d_n[j];
+    const double *pj = part + 2 * int64_t(nparts) * j;
     DD acc{0.0, 0.0};
-    for (int i = threadIdx.x; i < nparts; i += kBlock) acc = dd_add(acc, DD{part[2 * i], part[2 * i + 1]});
+    for (int i = threadIdx.x; i < nparts; i += kBlock) acc = dd_add(acc, DD{pj[2 * i], pj[2 * i + 1]});
     acc = wave_dd_sum(acc);
     if (lane_id() == 0) {
         s_hi[wave_id()] = acc.hi;
@@ -751,7 +771,7 @@ __global__ __launch_bounds__(kBlock) void k_dd_final(const double *__restrict__ 
         for (int i = 1; i < 4; ++i) t = dd_add(t, DD{s_hi[i], s_lo[i]});
         const double s = t.hi + t.lo;
         const double q = n > 0 ? s / double(n) : NAN;
-        *out = mode == 0 ? q : sqrt(q);
+        ms[2 * j + mode] = mode == 0 ? q : sqrt(q);
     }
 }
 
@@ -816,10 +836,10 @@ __device__ void describe_from_sorted(const uint64_t *sk, int64_t n, double mean,
     *out = d;
 }
 
-__global__ void k_describe_finish(const uint64_t *__restrict__ sk, const int64_t *__restrict__ d_n,
-                                  const double *__restrict__ ms, fz_describe *__restrict__ out) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    describe_from_sorted(sk, *d_n, ms[0], ms[1], out);
+__global__ void k_describe_finish(SortedDescArgs a, const double *__restrict__ ms) {
+    if (threadIdx.x != 0) return;
+    const int j = blockIdx.x;
+    describe_from_sorted(a.k[j], *a.d_n[j], ms[2 * j], ms[2 * j + 1], a.out[j]);
 }
 
 // The whole describe of n <= 4096 values in one 1024-thread workgroup: LDS bitonic sort of the
@@ -904,7 +924,8 @@ void describe_f64_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_
 void describe_f64_dn_batch(fz_ctx *c, const DescJob *jobs, int njobs) {
     FZ_CHECK(njobs <= kDescBatch, "describe batch larger than kDescBatch");
     DescSmallArgs a{};
-    int ns = 0;
+    SortedDescJob big[kDescBatch];
+    int ns = 0, nb = 0;
     for (int i = 0; i < njobs; ++i) {
         const DescJob &j = jobs[i];
         if (j.nmax <= kDescSmall) {
@@ -913,26 +934,44 @@ void describe_f64_dn_batch(fz_ctx *c, const DescJob *jobs, int njobs) {
             a.out[ns] = j.out;
             ++ns;
         } else {
-            describe_sorted_dn(c, sorted_keys_dn(c, j.x, j.nmax, j.d_n), j.x, j.nmax, j.d_n, j.out);
+            big[nb++] = SortedDescJob{sorted_keys_dn(c, j.x, j.nmax, j.d_n), j.x, j.nmax, j.d_n, j.out};
         }
     }
     if (ns > 0) {  // every small job in one launch
         k_describe_small<<<ns, kSortBlock, 0, c->stream>>>(a);
         FZ_LAUNCH_CHECK();
     }
+    if (nb > 0) describe_sorted_dn_batch(c, big, nb);
 }
 
 void describe_sorted_dn(fz_ctx *c, const uint64_t *k, const double *x, int64_t nmax, const int64_t *d_n,
                         fz_describe *dev_out) {
-    const int64_t nn = nmax < 1 ? 1 : nmax;
+    const SortedDescJob j{k, x, nmax, d_n, dev_out};
+    describe_sorted_dn_batch(c, &j, 1);
+}
+
+// The describes of up to kDescBatch sorted samples: five launches in all (two double-double passes
+// of partial + final, one finish), each covering every job (blockIdx.y / blockIdx.x = job).
+void describe_sorted_dn_batch(fz_ctx *c, const SortedDescJob *jobs, int njobs) {
+    FZ_CHECK(njobs >= 1 && njobs <= kDescBatch, "sorted describe batch size");
+    SortedDescArgs a{};
+    int64_t nn = 1;
+    for (int i = 0; i < njobs; ++i) {
+        a.k[i] = jobs[i].k;
+        a.x[i] = jobs[i].x;
+        a.d_n[i] = jobs[i].d_n;
+        a.out[i] = jobs[i].out;
+        nn = jobs[i].nmax > nn ? jobs[i].nmax : nn;
+    }
     const unsigned g = grid_for(nn, kBlock, 1024);
-    double *part = c->arena.get<double>(2 * g);
-    double *ms = c->arena.get<double>(2);
-    k_dd_partial<<<g, kBlock, 0, c->stream>>>(x, d_n, nullptr, part);
-    k_dd_final<<<1, kBlock, 0, c->stream>>>(part, int(g), d_n, 0, ms);
-    k_dd_partial<<<g, kBlock, 0, c->stream>>>(x, d_n, ms, part);
-    k_dd_final<<<1, kBlock, 0, c->stream>>>(part, int(g), d_n, 1, ms + 1);
-    k_describe_finish<<<1, 64, 0, c->stream>>>(k, d_n, ms, dev_out);
+    double *part = c->arena.get<double>(2 * int64_t(g) * njobs);
+    double *ms = c->arena.get<double>(2 * njobs);
+    const dim3 gp(g, unsigned(njobs));
+    k_dd_partial<<<gp, kBlock, 0, c->stream>>>(a, nullptr, part);
+    k_dd_final<<<njobs, kBlock, 0, c->stream>>>(part, int(g), a, 0, ms);
+    k_dd_partial<<<gp, kBlock, 0, c->stream>>>(a, ms, part);
+    k_dd_final<<<njobs, kBlock, 0, c->stream>>>(part, int(g), a, 1, ms);
+    k_describe_finish<<<njobs, 64, 0, c->stream>>>(a, ms);
     FZ_LAUNCH_CHECK();
 }
 

@@ -249,9 +249,10 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
             else skn[i - before[i]] = k;
         });
     }
-    describe_sorted_dn(c, skd, det_pct, NI, d_nd, describe);
-    describe_sorted_dn(c, skn, non_pct, NC, d_nn, describe + 1);
-    describe_f64_dn(c, dtot_f, NI, d_nd, describe + 2);
+    const SortedDescJob jobs[3] = {{skd, det_pct, NI, d_nd, describe},
+                                   {skn, non_pct, NC, d_nn, describe + 1},
+                                   {sorted_keys_dn(c, dtot_f, NI, d_nd), dtot_f, NI, d_nd, describe + 2}};
+    describe_sorted_dn_batch(c, jobs, 3);
     anderson_sorted(c, skd, det_pct, NI, d_nd, tests + FZ_RQ3_AD_DET);
     anderson_sorted(c, skn, non_pct, NC, d_nn, tests + FZ_RQ3_AD_NON);
     levene_two(c, skd, det_pct, NI, d_nd, skn, non_pct, NC, d_nn, tests + FZ_RQ3_LEVENE_W);

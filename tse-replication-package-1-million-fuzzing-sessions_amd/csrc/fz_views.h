@@ -162,6 +162,20 @@ struct DescJob {
     fz_describe *out;
 };
 void describe_f64_dn_batch(fz_ctx *c, const DescJob *jobs, int njobs);
+struct SortedDescJob {
+    const uint64_t *k;  // ascending f64_key of x[0..*d_n)
+    const double *x;
+    int64_t nmax;
+    const int64_t *d_n;
+    fz_describe *out;
+};
+struct SortedDescArgs {
+    const uint64_t *k[kDescBatch];
+    const double *x[kDescBatch];
+    const int64_t *d_n[kDescBatch];
+    fz_describe *out[kDescBatch];
+};
+void describe_sorted_dn_batch(fz_ctx *c, const SortedDescJob *jobs, int njobs);
 // ascending order-preserving keys (f64_key) of x[0..*d_n); entries past *d_n are ~0.
 uint64_t *sorted_keys_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n);
 // the same for nmax <= 4096 in one workgroup (LDS bitonic network, fz_series.hip)
