@@ -300,7 +300,6 @@ void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t 
 void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_cap, const int64_t *d_n, int64_t MM,
                    int64_t half_len, int64_t sess_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q,
                    double *pbm) {
-    hipStream_t st = c->stream;
     const int64_t S2 = 2 * MM, NC = n_cap, P = half_len;
     const int64_t *d_nf = d_n;
     int32_t *sess = c->arena.get<int32_t>(NC);
