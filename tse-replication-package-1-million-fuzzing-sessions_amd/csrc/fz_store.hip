@@ -270,13 +270,11 @@ __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict
     }
 }
 
-// Sorts by (prefix, time, row); returns the device counter of rows in segments too long for LDS
-// (non-zero -> the caller re-sorts with sort_table()).
-static unsigned long long *sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time,
-                                           int32_t *orow, int64_t *otime, uint32_t *oproj, const GatherCols &gc) {
-    unsigned long long *big = c->arena.get<unsigned long long>(1);
-    FZ_HIP(hipMemsetAsync(big, 0, 8, c->stream));
-    if (n <= 0) return big;
+// Sorts by (prefix, time, row); adds to the (zeroed) device counter *big the rows in segments too
+// long for LDS (non-zero -> the caller re-sorts with sort_table()).
+static void sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time, int32_t *orow,
+                            int64_t *otime, uint32_t *oproj, const GatherCols &gc, unsigned long long *big) {
+    if (n <= 0) return;
     uint64_t *keys = c->arena.get<uint64_t>(n);
     uint32_t *vals = c->arena.get<uint32_t>(n);
     const unsigned g = grid_for(n, kBlock, 4096);
@@ -295,7 +293,6 @@ static unsigned long long *sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int
                                                                                     otime, oproj, big, gc);
         FZ_LAUNCH_CHECK();
     }
-    return big;
 }
 
 // Sort one table into (row, time, proj) buffers.
@@ -505,10 +502,13 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         gi.src[1] = t->i_status, gi.dst[1] = s.si_status.ensure<uint8_t>(ni), gi.size[1] = 1;
     }
     unsigned long long *big[3];
+    unsigned long long *big3 = c->arena.get<unsigned long long>(3);
+    FZ_HIP(hipMemsetAsync(big3, 0, 3 * 8, c->stream));  // one zeroing for the three tables' counters
     for (int k = 0; k < 3; ++k) {
         Tab &b = tabs[k];
-        big[k] = sort_table_fast(c, b.n, b.pre, b.pbits_total, b.time, b.row->ensure<int32_t>(b.n),
-                                 b.tm->ensure<int64_t>(b.n), b.pr->ensure<uint32_t>(b.n), gcs[k]);
+        big[k] = big3 + k;
+        sort_table_fast(c, b.n, b.pre, b.pbits_total, b.time, b.row->ensure<int32_t>(b.n), b.tm->ensure<int64_t>(b.n),
+                        b.pr->ensure<uint32_t>(b.n), gcs[k], big[k]);
     }
     auto make_views = [&]() {
         int32_t *row = s.b_row.as<int32_t>();
