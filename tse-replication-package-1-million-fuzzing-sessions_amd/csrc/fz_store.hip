@@ -272,8 +272,12 @@ __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict
 
 // Sorts by (prefix, time, row); adds to the (zeroed) device counter *big the rows in segments too
 // long for LDS (non-zero -> the caller re-sorts with sort_table()).
+// nonempty_bound: host upper bound on the number of non-empty segments (picks the workgroup size).
+constexpr int kTimeSortSmallBlock = 256;
+constexpr int kTimeSortSmallMean = 256;  // mean rows per segment at or below which it is used
 static void sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time, int32_t *orow,
-                            int64_t *otime, uint32_t *oproj, const GatherCols &gc, unsigned long long *big) {
+                            int64_t *otime, uint32_t *oproj, const GatherCols &gc, unsigned long long *big,
+                            int64_t nonempty_bound) {
     if (n <= 0) return;
     uint64_t *keys = c->arena.get<uint64_t>(n);
     uint32_t *vals = c->arena.get<uint32_t>(n);
@@ -289,8 +293,15 @@ static void sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, c
     {
         ProbeScope ps(c, "seg_time_sort", 28.0 * double(n));  // row 4 + gathered time 8 + out 16 B
         const unsigned g = unsigned(S < 16384 ? S : 16384);
-        k_seg_time_sort<kTimeSortBlock, kSegSortMax><<<g, kTimeSortBlock, 0, c->stream>>>(vals, time, offs, S, pmask, orow,
-                                                                                    otime, oproj, big, gc);
+        if (n <= int64_t(kTimeSortSmallMean) * nonempty_bound) {
+            // short segments on average (issues: ~65 rows per project): 256-thread workgroups, five
+            // per CU by LDS instead of two, so the whole table sorts in one round of the grid
+            k_seg_time_sort<kTimeSortSmallBlock, kSegSortMax><<<g, kTimeSortSmallBlock, 0, c->stream>>>(
+                vals, time, offs, S, pmask, orow, otime, oproj, big, gc);
+        } else {
+            k_seg_time_sort<kTimeSortBlock, kSegSortMax><<<g, kTimeSortBlock, 0, c->stream>>>(vals, time, offs, S, pmask,
+                                                                                        orow, otime, oproj, big, gc);
+        }
         FZ_LAUNCH_CHECK();
     }
 }
@@ -507,8 +518,10 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     for (int k = 0; k < 3; ++k) {
         Tab &b = tabs[k];
         big[k] = big3 + k;
+        // non-empty segments: at most one per project (and build type: 2 prefix bits for builds)
+        const int64_t segs = int64_t(P > 0 ? P : 1) * (k == 0 ? 4 : 1);
         sort_table_fast(c, b.n, b.pre, b.pbits_total, b.time, b.row->ensure<int32_t>(b.n), b.tm->ensure<int64_t>(b.n),
-                        b.pr->ensure<uint32_t>(b.n), gcs[k], big[k]);
+                        b.pr->ensure<uint32_t>(b.n), gcs[k], big[k], segs);
     }
     auto make_views = [&]() {
         int32_t *row = s.b_row.as<int32_t>();
