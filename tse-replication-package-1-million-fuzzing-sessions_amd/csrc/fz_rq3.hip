@@ -217,8 +217,13 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
         double *v = c->arena.get<double>(cap);
         uint8_t *g = c->arena.get<uint8_t>(cap);
         const double *dp = det_pct, *np_ = non_pct;
-        map_n(c, cap, nullptr, [=] __device__(int64_t i) {
+        int64_t *oall = c->arena.get<int64_t>(2);  // {0, *d_nd + *d_nn}: the union's one segment
+        map_n(c, cap > 0 ? cap : 1, nullptr, [=] __device__(int64_t i) {
             const int64_t nd = *d_nd, nn = *d_nn;
+            if (i == 0) {
+                oall[0] = 0;
+                oall[1] = nd + nn;
+            }
             if (i < nd) {
                 v[i] = dp[i];
                 g[i] = 0;
@@ -227,9 +232,8 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
                 g[i] = 1;
             }
         });
-        int64_t *d_all = c->arena.get<int64_t>(1);
-        map_n(c, 1, nullptr, [=] __device__(int64_t) { *d_all = *d_nd + *d_nn; });
-        Segs one{1, single_segment(c, d_all), cap};
+        const int64_t *d_all = oall + 1;
+        Segs one{1, oall, cap};
         int32_t *sid = segment_ids(c, one);
         ChunkedSegs cs = chunked(c, one);
         SortedSegs ss = seg_sort_f64(c, v, one, sid);

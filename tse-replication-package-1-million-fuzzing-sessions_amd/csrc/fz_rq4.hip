@@ -264,8 +264,13 @@ void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t 
     const int64_t cap = (na_cap > 0 ? na_cap : 1) + (nb_cap > 0 ? nb_cap : 1);
     double *v = c->arena.get<double>(cap);
     uint8_t *gr = c->arena.get<uint8_t>(cap);
+    int64_t *oall = c->arena.get<int64_t>(2);  // {0, *n2 + *n1}: offsets of the union's one segment
     map_n(c, cap, nullptr, [=] __device__(int64_t i) {
         const int64_t na = *n2, nb = *n1;
+        if (i == 0) {
+            oall[0] = 0;
+            oall[1] = na + nb;
+        }
         if (i < na) {
             v[i] = a[i];
             gr[i] = 0;
@@ -274,9 +279,8 @@ void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t 
             gr[i] = 1;
         }
     });
-    int64_t *d_all = c->arena.get<int64_t>(1);
-    map_n(c, 1, nullptr, [=] __device__(int64_t) { *d_all = *n2 + *n1; });
-    Segs one{1, single_segment(c, d_all), cap};
+    const int64_t *d_all = oall + 1;
+    Segs one{1, oall, cap};
     int32_t *sid = segment_ids(c, one);
     double *u1 = c->arena.get<double>(1);
     RankTestOut rt;
