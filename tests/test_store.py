@@ -80,3 +80,21 @@ def test_pg_dump_errors(tmp_path):
     p.write_text("SELECT 1;\n")
     with pytest.raises(ValueError, match="no COPY block"):
         store.from_pg_dump(str(p))
+
+
+def test_pg_dump_empty_block_and_utc_offsets(tmp_path):
+    """An empty COPY block (no rows) and timestamptz text ('+00' suffix, as a UTC server dumps it)
+    load as an empty table and as naive wall-clock microseconds."""
+    p = tmp_path / "d.sql"
+    p.write_text(
+        "COPY public.buildlog_data (name, project, build_type, result, timecreated, modules, revisions) FROM stdin;\n"
+        "b1\tp\tFuzzing\tFinish\t2020-01-02 03:04:05.000006+00\t{m}\t{r}\n\\.\n"
+        "COPY public.total_coverage (project, date, coverage, covered_line, total_line) FROM stdin;\n"
+        "p\t2020-01-02 00:00:00+00\t12.5\t10\t80\np\t2020-01-03 00:00:00+00\t\\N\t\\N\t\\N\n\\.\n"
+        "COPY public.issues (number, project, rts, status, new_id) FROM stdin;\n\\.\n"
+        "COPY public.project_info (project, first_commit_datetime) FROM stdin;\n\\.\n")
+    t = store.from_pg_dump(str(p), corpus_csv="")
+    assert t.projects == ["p"] and len(t.i_number) == 0 and len(t.pi_project) == 0
+    assert int(t.b_time[0]) == int(np.datetime64("2020-01-02T03:04:05.000006", "us").astype(np.int64))
+    assert t.c_coverage_valid.tolist() == [True, False] and t.c_covered_valid.tolist() == [True, False]
+    assert t.c_coverage[0] == 12.5 and t.modules_pool == ["{m}"]
