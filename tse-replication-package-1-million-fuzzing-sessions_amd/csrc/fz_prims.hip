@@ -686,22 +686,8 @@ void minmax_i64_to_host(fz_ctx *c, const int64_t *const *cols, const int64_t *ns
 }
 
 // ------------------------------------------------------------------------ segment offsets
-__global__ __launch_bounds__(kBlock) void k_segment_offsets(const uint32_t *__restrict__ proj, int64_t n, int64_t P,
-                                                            int64_t *__restrict__ offsets) {
-    const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (p > P) return;
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (int64_t(proj[mid]) < p) lo = mid + 1;
-        else hi = mid;
-    }
-    offsets[p] = lo;
-}
-
 void segment_offsets(fz_ctx *c, const uint32_t *sorted_proj, int64_t n, int64_t P, int64_t *offsets) {
-    k_segment_offsets<<<grid_for(P + 1, kBlock, 1u << 30), kBlock, 0, c->stream>>>(sorted_proj, n, P, offsets);
-    FZ_LAUNCH_CHECK();
+    segment_offsets_dn(c, sorted_proj, nullptr, n < 0 ? 0 : n, P, offsets);  // row-parallel, host length
 }
 
 // -------------------------------------------------------------------------------- describe
@@ -990,7 +976,7 @@ void describe_f64(fz_ctx *c, const double *x, int64_t n, fz_describe *dev_out) {
 __global__ __launch_bounds__(kBlock) void k_segment_offsets_rows(const uint32_t *__restrict__ proj,
                                                                  const int64_t *__restrict__ d_n, int64_t n_cap,
                                                                  int64_t P, int64_t *__restrict__ offsets) {
-    const int64_t n = *d_n;
+    const int64_t n = d_n ? *d_n : n_cap;  // d_n null: the length is the host-known n_cap
     const int64_t first = n > 0 ? int64_t(proj[0]) : P + 1, last = n > 0 ? int64_t(proj[n - 1]) : -1;
     const int64_t span = n_cap > P + 1 ? n_cap : P + 1;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < span; i += int64_t(gridDim.x) * kBlock) {

@@ -22,7 +22,8 @@ struct TmpView {
     int64_t *offs = nullptr;  // [P + 1]
 };
 
-// Offsets [P + 1] of a project-sorted array of device length *d_n <= n_cap (row-parallel).
+// Offsets [P + 1] of a project-sorted array of device length *d_n <= n_cap (row-parallel; d_n null:
+// the length is n_cap).
 void segment_offsets_dn(fz_ctx *c, const uint32_t *sorted_proj, const int64_t *d_n, int64_t n_cap, int64_t P,
                         int64_t *offsets);
 
