@@ -140,17 +140,22 @@ __global__ __launch_bounds__(kBlock) void k_keys_prefix_rows(Prefix pre, int64_t
     }
 }
 
+// offs[s] = first position of prefix s in the prefix-sorted keys (s in [0, S]): row i starts the
+// prefixes (keys[i-1], keys[i]]; one coalesced read of the keys instead of a binary search per s.
 __global__ __launch_bounds__(kBlock) void k_prefix_offsets(const uint64_t *__restrict__ keys, int64_t n, int64_t S,
                                                            int64_t *__restrict__ offs) {
-    const int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (s > S) return;
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (keys[mid] < uint64_t(s)) lo = mid + 1;
-        else hi = mid;
+    const int64_t first = int64_t(keys[0]), last = int64_t(keys[n - 1]);  // n >= 1, keys < S
+    const int64_t span = n > S + 1 ? n : S + 1;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < span; i += int64_t(gridDim.x) * kBlock) {
+        if (i <= S) {
+            if (i <= first) offs[i] = 0;
+            else if (i > last) offs[i] = n;
+        }
+        if (i > 0 && i < n) {
+            const int64_t pp = int64_t(keys[i - 1]), pc = int64_t(keys[i]);
+            for (int64_t q = pp + 1; q <= pc && q <= S; ++q) offs[q] = i;
+        }
     }
-    offs[s] = lo;
 }
 
 // One workgroup per prefix segment, already in row order: bitonic sort in LDS of one packed u64 per
@@ -287,7 +292,7 @@ static void sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, c
     radix_sort_pairs_swap(c, keys, vals, n, prefix_bits);
     const int64_t S = int64_t(1) << prefix_bits;
     int64_t *offs = c->arena.get<int64_t>(S + 1);
-    k_prefix_offsets<<<grid_for(S + 1, kBlock, 1u << 30), kBlock, 0, c->stream>>>(keys, n, S, offs);
+    k_prefix_offsets<<<grid_for(n > S + 1 ? n : S + 1, kBlock, 4096), kBlock, 0, c->stream>>>(keys, n, S, offs);
     FZ_LAUNCH_CHECK();
     const uint32_t pmask = pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << pre.pbits) - 1ull);
     {
