@@ -524,7 +524,12 @@ void seg_median(fz_ctx *c, const Segs &sg, const double *sorted, double *out) {
 void levene_two(fz_ctx *c, const uint64_t *skx, const double *x, int64_t nxm, const int64_t *d_nx,
                        const uint64_t *sky, const double *y, int64_t nym, const int64_t *d_ny, double *out) {
     double *med = c->arena.get<double>(2);
+    int64_t *ox = c->arena.get<int64_t>(2), *oy = c->arena.get<int64_t>(2);  // each sample's one segment
     map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        ox[0] = 0;
+        ox[1] = *d_nx;
+        oy[0] = 0;
+        oy[1] = *d_ny;
         for (int g = 0; g < 2; ++g) {
             const uint64_t *k = g ? sky : skx;
             const int64_t n = g ? *d_ny : *d_nx;
@@ -534,7 +539,7 @@ void levene_two(fz_ctx *c, const uint64_t *skx, const double *x, int64_t nxm, co
         }
     });
     double *zb = c->arena.get<double>(2), *dv = c->arena.get<double>(2);
-    Segs sx{1, single_segment(c, d_nx), nxm}, sy{1, single_segment(c, d_ny), nym};
+    Segs sx{1, ox, nxm}, sy{1, oy, nym};
     ChunkedSegs cx = chunked(c, sx), cy = chunked(c, sy);
     seg_reduce<1>(c, cx, [=] __device__(int64_t i, int32_t, double *v) { v[0] = fabs(x[i] - med[0]); }, zb);
     seg_reduce<1>(c, cy, [=] __device__(int64_t i, int32_t, double *v) { v[0] = fabs(y[i] - med[1]); }, zb + 1);
