@@ -48,9 +48,10 @@ struct CovRowsRq3 {  // covered_line IS NOT NULL AND DATE(date) < '2025-01-09' (
 };
 
 // anderson(x, dist='norm') from ascending keys: A2 and the 5 rounded critical values.
+// offs1: the sample's single-segment offsets {0, *d_n} (written by the caller's union map)
 static void anderson_sorted(fz_ctx *c, const uint64_t *sk, const double *x, int64_t nmax, const int64_t *d_n,
-                            double *out) {
-    Segs one{1, single_segment(c, d_n), nmax};
+                            const int64_t *offs1, double *out) {
+    Segs one{1, offs1, nmax};
     ChunkedSegs cs = chunked(c, one);
     double *ms = c->arena.get<double>(4);
     seg_mean(c, cs, x, ms);  // xbar
@@ -211,6 +212,7 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
     // partition of the sorted union by sample gives each sample's sorted keys (describe,
     // anderson, levene) - instead of three separate device-wide sorts.
     const int64_t cap = NI + NC;
+    int64_t *odet = c->arena.get<int64_t>(2), *onon = c->arena.get<int64_t>(2);
     uint64_t *skd = c->arena.get<uint64_t>(cap);
     uint64_t *skn = c->arena.get<uint64_t>(cap);
     {
@@ -223,6 +225,10 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
             if (i == 0) {
                 oall[0] = 0;
                 oall[1] = nd + nn;
+                odet[0] = 0;  // and each sample's own (Anderson-Darling)
+                odet[1] = nd;
+                onon[0] = 0;
+                onon[1] = nn;
             }
             if (i < nd) {
                 v[i] = dp[i];
@@ -257,8 +263,8 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
                                    {skn, non_pct, NC, d_nn, describe + 1},
                                    {sorted_keys_dn(c, dtot_f, NI, d_nd), dtot_f, NI, d_nd, describe + 2}};
     describe_sorted_dn_batch(c, jobs, 3);
-    anderson_sorted(c, skd, det_pct, NI, d_nd, tests + FZ_RQ3_AD_DET);
-    anderson_sorted(c, skn, non_pct, NC, d_nn, tests + FZ_RQ3_AD_NON);
+    anderson_sorted(c, skd, det_pct, NI, d_nd, odet, tests + FZ_RQ3_AD_DET);
+    anderson_sorted(c, skn, non_pct, NC, d_nn, onon, tests + FZ_RQ3_AD_NON);
     levene_two(c, skd, det_pct, NI, d_nd, skn, non_pct, NC, d_nn, tests + FZ_RQ3_LEVENE_W);
 }
 
