@@ -145,15 +145,22 @@ def rq1(t: Tables, threshold: int = 100, ext=None) -> RQ1Result:
         total_fuzz_builds=int(nfe.sum()), matched_issue=ci, matched_build=mb,
         n_matched_projects=len(np.unique(t.i_project[ci])),
         iter_total=iter_total, iter_detected=iter_det, min_project_threshold=threshold)
-    _, _, _, late = common.rq1_rates(iter_total, iter_det, threshold)
-    if late:
-        a = np.array(late)
-        nz = [r for r in late if r != 0]
-        res.late = Describe(count=len(late), n_zero=int(np.sum(a == 0)), min=min(late), max=max(late),
-                            q1=float(np.percentile(late, 25)), q3=float(np.percentile(late, 75)),
-                            median=float(np.median(late)), mean=float(np.mean(late)),
-                            min_nonzero=min(nz) if nz else None)
+    res.late = rq1_finish(iter_total, iter_det, threshold)
     return res
+
+
+def rq1_finish(iter_total, iter_det, threshold: int = 100):
+    """rq1_detection_rate.py:233-268: the late-stage summary of the kept iterations' rates
+    (None when the late stage is empty)."""
+    _, _, _, late = common.rq1_rates(iter_total, iter_det, threshold)
+    if not late:
+        return None
+    a = np.array(late)
+    nz = [r for r in late if r != 0]
+    return Describe(count=len(late), n_zero=int(np.sum(a == 0)), min=min(late), max=max(late),
+                    q1=float(np.percentile(late, 25)), q3=float(np.percentile(late, 75)),
+                    median=float(np.median(late)), mean=float(np.mean(late)),
+                    min_nonzero=min(nz) if nz else None)
 
 
 # ---------------------------------------------------------------------------------- RQ2 count

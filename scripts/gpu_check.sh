@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 run() {  # run <name> <seconds> <cmd...>
   local name=$1 secs=$2; shift 2
   echo "== $name: $*"
@@ -16,16 +16,17 @@ run() {  # run <name> <seconds> <cmd...>
   return $rc
 }
 STEPS=${STEPS:-tests,smoke,bench,prof}
-[[ $STEPS == *tests* ]] && run pytest_gpu 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
-[[ $STEPS == *smoke* ]] && run smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *bench* ]] && run bench 400 python -u bench.py
-[[ $STEPS == *rehearse2* ]] && run bench_rehearse2 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo --no-cpu-baseline
+[[ ",$STEPS," == *,tests,* ]] && run pytest_gpu 1100 python -u -m pytest tests -m gpu -v --timeout 900 --timeout-method thread $PYTEST_ARGS
+[[ ",$STEPS," == *,smoke,* ]] && run smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()"
+[[ ",$STEPS," == *,bench,* ]] && run bench 400 python -u bench.py
+[[ ",$STEPS," == *,rehearse2,* ]] && run bench_rehearse2 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo --no-cpu-baseline
 # PMC passes: one counter group per run (FETCH_SIZE uses 3 TCC slots, WRITE_SIZE 2), SIGKILL limit
-[[ $STEPS == *pmcF* ]] && run pmc_fetch 150 timeout -s KILL 140 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_$TAG -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline
-[[ $STEPS == *pmcW* ]] && run pmc_write 150 timeout -s KILL 140 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline
-[[ $STEPS == *c3* ]] && run bench_c3 600 python -u bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline
-[[ $STEPS == *c4* ]] && run bench_c4 300 python -u bench.py --config c4 --steps 5 --warmup 1 --no-cpu-baseline
-[[ $STEPS == *c5* ]] && run bench_c5 600 python -u bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline
-[[ $STEPS == *pc3* ]] && run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c3_$TAG -o run -- python -u bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline
-[[ $STEPS == *prof* ]] && run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline
+[[ ",$STEPS," == *,pmcF,* ]] && run pmc_fetch 150 timeout -s KILL 140 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_$TAG -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline
+[[ ",$STEPS," == *,pmcW,* ]] && run pmc_write 150 timeout -s KILL 140 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline
+[[ ",$STEPS," == *,c3,* ]] && run bench_c3 600 python -u bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline
+[[ ",$STEPS," == *,c4,* ]] && run bench_c4 300 python -u bench.py --config c4 --steps 5 --warmup 1 --no-cpu-baseline
+[[ ",$STEPS," == *,c5,* ]] && run bench_c5 600 python -u bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline
+[[ ",$STEPS," == *,pc3,* ]] && run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c3_$TAG -o run -- python -u bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline
+[[ ",$STEPS," == *,pc5,* ]] && run prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5_$TAG -o run -- python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu-baseline
+[[ ",$STEPS," == *,prof,* ]] && run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline
 echo done

@@ -36,12 +36,11 @@ def engine():
 def engine_for(engine):
     """engine_for(case): the engine with that golden case's tables uploaded and the store built."""
     import goldens
-    state = {"case": None}
 
     def get(case):
-        if state["case"] != case:
-            engine.upload(goldens.tables(case))
+        t = goldens.tables(case)  # cached: the same object while the case's tables are loaded
+        if engine.tables is None or engine.tables.host is not t:
+            engine.upload(t)
             engine.build_store()
-            state["case"] = case
         return engine
     return get

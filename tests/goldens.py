@@ -64,7 +64,16 @@ def _tokens(line):
     return out
 
 
+def _sig_digits(tok: str) -> int:
+    mant = tok.lower().split("e")[0].lstrip("+-").replace(",", "").replace(".", "").lstrip("0")
+    return len(mant)
+
+
 def _close(a: str, b: str, rtol: float) -> bool:
+    """Numeric tokens compare exactly, except full-precision values (>= 12 significant digits, e.g.
+    repr(np.float64) of a statistic), which may differ within rtol: an fp64 statistic that agrees
+    to 1e-9 relative can print different trailing digits, but a rounded value (.2f/.4f, counts,
+    percentages) must print the same digits."""
     if a == b:
         return True
     try:
@@ -73,18 +82,13 @@ def _close(a: str, b: str, rtol: float) -> bool:
         return False
     if np.isnan(x) and np.isnan(y):
         return True
-    # allow 1 unit in the last printed digit (values within rtol can round either way)
-    bl = b.lower()
-    mant = bl.split("e")[0]
-    dec = len(mant.split(".")[1]) if "." in mant else 0
-    ulp = 10.0 ** (-dec)
-    if "e" in bl:
-        ulp *= 10.0 ** int(bl.split("e")[1])
-    return abs(x - y) <= max(rtol * max(abs(x), abs(y)), 1.000001 * ulp)
+    if min(_sig_digits(a), _sig_digits(b)) < 12:
+        return False
+    return abs(x - y) <= rtol * max(abs(x), abs(y))
 
 
 def compare_lines(ours, golden, rtol=0.0):
-    """Line-by-line compare; numeric tokens may differ within rtol (or the last printed digit)."""
+    """Line-by-line compare; only full-precision numeric tokens may differ (within rtol)."""
     lo, lg = ours.rstrip("\n").split("\n"), golden.rstrip("\n").split("\n")
     errs = []
     if len(lo) != len(lg):

@@ -1,0 +1,259 @@
+"""Correctness at full BASELINE size: configs 3 and 5 - 100M-row coverage tables,
+config 5 with a Zipf giant project of ~20M rows - through the store and all six analyses on the GPU.
+
+The oracle's per-project Python loops cannot run at this size, so the checks are:
+
+* exact integer invariants computed with vectorised numpy on the host table: eligibility
+  (rq1_detection_rate.py:144-152), rows fetched / trend lengths per project (queries1.py:120-129,
+  rq2_coverage_count.py:300-303), the full session transposition (rq2_coverage_count.py:330-333)
+  value for value, the per-session G2 / G1 counts of rq4b_coverage.py:917-936;
+* every per-session statistic of RQ2 (np.percentile 5/25/50/75/95, np.mean, statistics.mean /
+  median, rq2_coverage_count.py:139-152,439-440) and RQ4b's quartiles (rq4b:966-972), the median-trend
+  tests (:443-458), rq4b's last session / six Spearman tests (:849-899), deltas (:725-797) and
+  initial-coverage tests (:221-313), recomputed with numpy / scipy (1e-9 relative);
+* a sampled oracle comparison: 50 random projects' Shapiro-Wilk and Spearman (rq2_coverage_count.py:
+  305-322) and 50 random sessions' Brunner-Munzel p (rq4b:978-985) with scipy.
+
+Configs 3 and 5 hold exactly one coverage row per project-day from the same first day, so the
+(project, date) order of the table is a counting placement (no host sort of 100M rows)."""
+import math
+import statistics
+import warnings
+
+import numpy as np
+import pytest
+from scipy import stats
+
+import tse_amd.synth as synth
+from gpu_common import assert_same
+from oracle import rq_oracle as orc
+from tse_amd import engine as E
+from tse_amd.rq import common, compute
+from tse_amd.schema import LIMIT_US, US_PER_DAY
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
+
+RNG = np.random.default_rng(99)
+
+
+class Host:
+    """The table in (project, date) order plus the per-project masks the analyses filter on."""
+
+    def __init__(self, t):
+        P = len(t.projects)
+        self.P = P
+        cnt = np.bincount(t.c_project, minlength=P).astype(np.int64)
+        off = np.zeros(P + 1, np.int64)
+        np.cumsum(cnt, out=off[1:])
+        d0 = int(t.c_date.min())
+        day = (t.c_date - d0) // US_PER_DAY
+        assert np.all(t.c_date == d0 + day * US_PER_DAY)
+        pos = off[t.c_project] + day
+        assert np.all(day < cnt[t.c_project])
+        order = np.empty(len(pos), np.int64)
+        order[pos] = np.arange(len(pos))
+        assert np.all(np.bincount(pos, minlength=len(pos)) == 1)  # one row per project-day
+        del pos, day
+        self.off, self.cnt = off, cnt
+        self.project = t.c_project[order].astype(np.int64)
+        self.date = t.c_date[order]
+        self.cov = t.c_coverage[order]
+        self.cov_ok = t.c_coverage_valid[order]
+        self.covered = t.c_covered[order]
+        self.total = t.c_total[order]
+        del order
+        before = self.date < LIMIT_US
+        # eligibility (rq1:144-152): coverage NOT NULL AND > 0 AND date < LIMIT, >= 365 rows
+        m = self.cov_ok & (self.cov > 0) & before
+        self.elig = np.nonzero(np.bincount(self.project[m], minlength=P) >= 365)[0]
+        self.pos4 = m                                     # rq4b full series (rq4b:315-326)
+        # RQ2 count (queries1.py:120-129): coverage NOT NULL AND != 0 AND date < LIMIT, then total != 0
+        self.fetch = self.cov_ok & (self.cov != 0) & before
+        self.keep = self.fetch & (self.total != 0)
+
+
+def _seg_positions(mask, project, P):
+    """Rows of mask in table order grouped per project: (flat row ids, per-project offsets)."""
+    rows = np.nonzero(mask)[0]
+    cnt = np.bincount(project[rows], minlength=P)
+    off = np.zeros(P + 1, np.int64)
+    np.cumsum(cnt, out=off[1:])
+    return rows, off
+
+
+def _transpose(lengths):
+    """Destination of value i of each project (in project order) in session-major order
+    (rq2_coverage_count.py:330-333): soff[i] + number of earlier projects with more than i values."""
+    ml = int(lengths.max()) if len(lengths) else 0
+    sizes = np.zeros(ml + 1, np.int64)
+    np.add.at(sizes, lengths, 1)
+    per = np.cumsum(sizes[::-1])[::-1][1:]        # per[i] = #projects with length > i
+    soff = np.zeros(ml + 1, np.int64)
+    np.cumsum(per, out=soff[1:])
+    seen = np.zeros(ml, np.int64)
+    dest = []
+    for L in lengths.tolist():
+        dest.append(soff[:L] + seen[:L])
+        seen[:L] += 1
+    return (np.concatenate(dest) if dest else np.zeros(0, np.int64)), soff, per
+
+
+@pytest.fixture(scope="module", params=["c3", "c5"])
+def case(request, engine):
+    name = request.param
+    t = synth.generate(synth.config(name))
+    assert t.n_rows >= 99_000_000
+    engine.upload(t)
+    st = engine.build_store()
+    if name == "c5":
+        assert st.max_cov_per_project > 10_000_000       # the Zipf giant project
+    out = {"name": name, "t": t, "st": st, "h": Host(t),
+           "rq2c": compute.rq2_count(engine), "rq4b": compute.rq4b(engine)}
+    yield out
+    engine.tables = None
+
+
+def test_store_and_empty_analyses(case, engine):
+    """Store sizes; the build / issue driven analyses have nothing to report on a coverage table."""
+    t, h, st = case["t"], case["h"], case["st"]
+    assert st.n_projects == len(t.projects) and st.n_fuzz == 0 and st.n_coverage_builds == 0
+    assert st.max_cov_per_project == int(h.cnt.max())
+    r1 = compute.rq1(engine)
+    assert np.array_equal(r1.eligible, h.elig) and len(r1.matched_issue) == 0 and r1.total_fuzz_builds == 0
+    assert_same(r1, orc.rq1(t), "rq1")
+    r2a = compute.rq2_add(engine)
+    assert np.array_equal(r2a.projects, h.elig) and len(r2a.row_project) == 0
+    r3 = compute.rq3(engine)
+    assert r3.n_all_issues == 0 and len(r3.det_pct) == 0 and len(r3.non_pct) == 0
+    r4a = compute.rq4a(engine)
+    assert_same(r4a, orc.rq4a(t), "rq4a")
+
+
+def test_rq2_count_fullsize(case):
+    r, h, t = case["rq2c"], case["h"], case["t"]
+    # exact: eligibility, rows fetched and trend lengths per eligible project
+    assert np.array_equal(r.eligible, h.elig)
+    raw_n = np.bincount(h.project[h.fetch], minlength=h.P)[h.elig]
+    n_tr = np.bincount(h.project[h.keep], minlength=h.P)[h.elig]
+    assert np.array_equal(r.raw_n, raw_n) and np.array_equal(r.n_trend, n_tr)
+    # exact: the whole session-major transposition, value for value (float(c)/float(t)*100)
+    is_e = np.zeros(h.P, bool)
+    is_e[h.elig] = True
+    rows = np.nonzero(h.keep & is_e[h.project])[0]          # project-major, date order
+    vals = h.covered[rows].astype(np.float64) / h.total[rows].astype(np.float64) * 100
+    dest, soff, per = _transpose(n_tr)
+    expect = np.empty(len(vals))
+    expect[dest] = vals
+    assert np.array_equal(r.session_offsets, soff), "session sizes"
+    assert int(r.session_offsets[-1]) == len(vals) == int(n_tr.sum())
+    assert np.array_equal(r.session_values, expect), "session values"
+    # every session statistic of the >= 100-value prefix (:390, :139-152, :439-440)
+    K = int(np.sum(per >= 100))
+    assert np.array_equal(r.ge100, np.arange(K))
+    pct = np.empty((5, K))
+    mean = np.empty(K)
+    avg = np.empty(K)
+    med = np.empty(K)
+    for i in range(K):
+        v = expect[soff[i]:soff[i + 1]]
+        pct[:, i] = np.percentile(v, [5, 25, 50, 75, 95])
+        mean[i] = np.mean(v)
+        avg[i] = math.fsum(v) / len(v)                 # statistics.mean within 1 ulp
+        med[i] = np.median(v)                          # == statistics.median on floats
+    assert_same(r.dist_percentiles, pct, "dist_percentiles")
+    assert_same(r.dist_mean, mean, "dist_mean")
+    assert_same(r.average_trend, avg, "average_trend")
+    assert_same(r.median_trend, med, "median_trend")
+    for i in RNG.choice(K, size=min(K, 5), replace=False).tolist():
+        v = list(expect[soff[i]:soff[i + 1]])
+        assert_same(float(r.average_trend[i]), float(statistics.mean(v)), f"statistics.mean[{i}]")
+    rho, pr, _, pw = orc.series_tests(med)               # :443-458
+    assert_same(r.spearman_median, (rho, pr) if K > 1 else None, "spearman_median")
+    assert_same(r.shapiro_median_p, pw if K >= 3 else None, "shapiro_median_p")
+    # sampled per-project tests (:305-322) against scipy
+    pos = np.cumsum(np.r_[0, n_tr])
+    for k in RNG.choice(len(h.elig), size=min(len(h.elig), 50), replace=False).tolist():
+        x = vals[pos[k]:pos[k + 1]]
+        rho, pr, w, pw = orc.series_tests(x)
+        assert_same((float(r.sw_w[k]), float(r.sw_p[k])), (w, pw), f"shapiro[{h.elig[k]}]")
+        ci = int(np.sum(r.raw_n[:k] > 0))
+        assert_same(float(r.corr[ci]), rho, f"spearman[{h.elig[k]}]")
+    valid = r.corr[~np.isnan(r.corr)]
+    assert_same((r.corr_mean, r.corr_median), (float(np.mean(valid)), float(np.median(valid))), "corr mean/median")
+
+
+def test_rq4b_fullsize(case):
+    r, h, t = case["rq4b"], case["h"], case["t"]
+    groups, corpus_us = common.corpus_groups(t, h.elig, add_missing_to_g1=False)
+    assert r.group_counts == tuple(len(groups[g]) for g in ("group1", "group2", "group3", "group4"))
+    rows, off = _seg_positions(h.pos4, h.project, h.P)
+    n = off[1:] - off[:-1]
+    g2 = np.array(groups["group2"], np.int64)
+    g1 = np.array(groups["group1"], np.int64)
+    ms = int(max(n[g2].max() if len(g2) else 0, n[g1].max() if len(g1) else 0))
+    assert r.n_sessions == ms
+    # exact per-session counts (:917-936)
+    c2 = np.cumsum(np.bincount(n[g2], minlength=ms + 1)[::-1])[::-1][1:ms + 1]
+    c1 = np.cumsum(np.bincount(n[g1], minlength=ms + 1)[::-1])[::-1][1:ms + 1]
+    assert np.array_equal(r.c2, c2) and np.array_equal(r.c1, c1)
+
+    def session(g, i):
+        ps = g[n[g] > i]
+        return h.cov[rows[off[ps] + i]]
+    last = -1                                        # :849-860 (both groups >= 100 values)
+    both = np.nonzero((c2 >= 100) & (c1 >= 100))[0]
+    if len(both):
+        last = int(both[-1])
+    # quartiles (:966-972) of every session up to max(20000, last + 1) and of 500 random later ones
+    # (config 5's giant projects make ~20M mostly single-value sessions); BM p of 50 sampled
+    # sessions (:978-985)
+    lim = min(ms, max(20000, last + 1))
+    idx = np.r_[np.arange(lim), np.sort(RNG.choice(np.arange(lim, ms), size=min(500, ms - lim), replace=False))
+                if ms > lim else np.zeros(0, np.int64)].astype(np.int64)
+    q2 = np.full((len(idx), 3), np.nan)
+    q1 = np.full((len(idx), 3), np.nan)
+    for k, i in enumerate(idx.tolist()):
+        a, b = session(g2, i), session(g1, i)
+        if len(a):
+            q2[k] = np.percentile(a, [25, 50, 75])
+        if len(b):
+            q1[k] = np.percentile(b, [25, 50, 75])
+    assert_same(r.g2_q[idx], q2, "g2_q")
+    assert_same(r.g1_q[idx], q1, "g1_q")
+    for i in RNG.choice(ms, size=min(ms, 50), replace=False).tolist():
+        a, b = session(g2, i), session(g1, i)
+        exp = np.nan
+        if len(a) >= 5 and len(b) >= 5:
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                exp = float(stats.brunnermunzel(a, b, alternative="two-sided")[1])
+        assert_same(float(r.p_bm[i]), exp, f"p_bm[{i}]")
+    last_o, sp6 = orc.rq4b_last_and_spearman6(c2[:lim], c1[:lim], q2[:lim], q1[:lim])   # :849-899
+    assert r.last_valid_idx == last == last_o
+    assert_same(r.spearman6, sp6, "spearman6")
+    # deltas of G3 u G4 (:725-797): last 7 positive-coverage rows before the corpus day, first 7 from it
+    prow, poff = _seg_positions(h.cov_ok & (h.cov > 0), h.project, h.P)
+    g34 = set(groups["group3"]) | set(groups["group4"])
+    pre = [[] for _ in range(7)]
+    post = [[] for _ in range(7)]
+    for p in common.corpus_order(t, h.elig):
+        if p not in g34 or p not in corpus_us:
+            continue
+        rr = prow[poff[p]:poff[p + 1]]
+        j = int(np.searchsorted(h.date[rr], corpus_us[p] // US_PER_DAY * US_PER_DAY, "left"))
+        pv, qv = h.cov[rr[max(0, j - 7):j]][::-1], h.cov[rr[j:j + 7]]
+        if len(pv) < 7 or len(qv) < 7:
+            continue
+        for i in range(7):
+            pre[i].append(pv[i])
+            post[i].append(qv[i])
+    assert r.n_delta_projects == len(pre[0])
+    assert_same(r.pre_cov, [np.array(x) for x in pre], "pre_cov")
+    assert_same(r.post_cov, [np.array(x) for x in post], "post_cov")
+    # initial coverage (:221-313): first full-series value of each G2 / G1 project
+    a = np.array([h.cov[rows[off[p]]] for p in g2 if n[p] > 0])
+    b = np.array([h.cov[rows[off[p]]] for p in g1 if n[p] > 0])
+    assert_same(r.init_g2, a, "init_g2")
+    assert_same(r.init_g1, b, "init_g1")
+    mwu_p, cliff, bm, lv = orc.rq4b_init_tests(a, b)
+    assert_same((r.mwu_p, r.cliff, r.bm, r.levene), (mwu_p, cliff, bm, lv), "initial-coverage tests")

@@ -317,6 +317,51 @@ class Engine:
         _check(self.lib, self.lib.fz_describe_f64(self.ctx, _P(x.data_ptr()), x.numel(), C.byref(d)))
         return d
 
+    # ---- finishing entry points over caller-supplied tables (no store needed) ------------------
+    def _dev(self, a, dtype):
+        t = self.torch.as_tensor(np.ascontiguousarray(a), dtype=dtype)
+        return t.to(self.dev) if t.numel() else self.torch.zeros(1, dtype=dtype, device=self.dev)
+
+    def rq1_finish(self, iter_total, iter_detected, threshold: int = 100):
+        """fz_rq1_finish (rq1_detection_rate.py:233-268) on host per-iteration tables ->
+        (counts[FZ_RQ1_NCOUNTS], late fz_describe as 13 doubles), host copies."""
+        torch = self.torch
+        it = self._dev(iter_total, torch.int64)
+        idt = self._dev(iter_detected, torch.int64)
+        counts = self.zeros(FZ_RQ1_NCOUNTS, torch.int64)
+        late = self.zeros(DESCRIBE_DOUBLES, torch.float64)
+        _check(self.lib, self.lib.fz_rq1_finish(self.ctx, threshold, _P(it.data_ptr()), _P(idt.data_ptr()),
+                                                len(iter_total), _P(counts.data_ptr()), _P(late.data_ptr())))
+        return counts.cpu().numpy(), late.cpu().numpy()
+
+    def rq4a_finish(self, g1_total, g1_det, g2_total, g2_det, intro, g4_steps):
+        """fz_rq4a_finish (rq4a_bug.py:156-207, :698-747, :246-299, :412-510) on host tables
+        (intro[n_projects]: -1 = not a G4 project) -> (counts, scalars), host copies."""
+        torch = self.torch
+        tabs = [self._dev(x, torch.int64) for x in (g1_total, g1_det, g2_total, g2_det)]
+        it = self._dev(intro, torch.int64)
+        st = self._dev(np.asarray(g4_steps, np.int64).reshape(30), torch.int64)
+        counts = self.zeros(FZ_RQ4A_NCOUNTS, torch.int64)
+        sc = self.zeros(FZ_RQ4A_NSCALARS, torch.float64)
+        _check(self.lib, self.lib.fz_rq4a_finish(self.ctx, *[_P(x.data_ptr()) for x in tabs], len(g1_total),
+                                                 _P(it.data_ptr()), len(intro), _P(st.data_ptr()),
+                                                 _P(counts.data_ptr()), _P(sc.data_ptr())))
+        return counts.cpu().numpy(), sc.cpu().numpy()
+
+    def rq3_stats(self, det_pct, det_tot, non_pct):
+        """fz_rq3_stats (rq3_diff_coverage_at_detection.py:25-66, :321-352) on host samples ->
+        (describe [3 x 13 doubles], tests[FZ_RQ3_NTESTS]), host copies."""
+        torch = self.torch
+        dp, dt, nn = (self._dev(det_pct, torch.float64), self._dev(det_tot, torch.int64),
+                      self._dev(non_pct, torch.float64))
+        desc = self.zeros(3 * DESCRIBE_DOUBLES, torch.float64)
+        tests = self.torch.full((FZ_RQ3_NTESTS,), float("nan"), dtype=torch.float64, device=self.dev)
+        P = lambda t, n: _P(t.data_ptr()) if n else None  # noqa: E731
+        _check(self.lib, self.lib.fz_rq3_stats(self.ctx, P(dp, len(det_pct)), P(dt, len(det_pct)), len(det_pct),
+                                               P(nn, len(non_pct)), len(non_pct), _P(desc.data_ptr()),
+                                               _P(tests.data_ptr())))
+        return desc.cpu().numpy().reshape(3, DESCRIBE_DOUBLES), tests.cpu().numpy()
+
     def eligibility_counts(self, limit_us):
         out = self.zeros(self.tables.fz.n_projects, self.torch.int32)
         _check(self.lib, self.lib.fz_eligibility_count(self.ctx, C.byref(self.tables.fz), limit_us,

@@ -16,6 +16,8 @@ import pandas as pd
 from ..schema import Tables
 
 DAYS_THRESHOLD = 7                 # rq4a_bug.py:44, rq4b_coverage.py:53
+CORPUS_COLUMNS = ["project_name", "is_Corpus", "corpus_commit_time", "corpus_merged_time",  # user_corpus.py:225-233
+                  "project_creation_time", "time_elapsed_seconds", "merged_time_elapsed_seconds"]
 
 
 def rq1_rates(iter_total, iter_det, threshold):
@@ -32,7 +34,12 @@ def rq1_rates(iter_total, iter_det, threshold):
 
 
 def read_corpus(t: Tables) -> pd.DataFrame:
-    """rq4a_bug.py:88-89 / rq4b_coverage.py:187-188."""
+    """rq4a_bug.py:88-89 / rq4b_coverage.py:187-188.  No corpus file (empty text): no rows - the
+    RQ4 scripts would stop there, every other analysis does not read it."""
+    if not t.corpus_csv.strip():
+        return pd.DataFrame({c: pd.Series([], dtype=object) for c in CORPUS_COLUMNS}).assign(
+            time_elapsed_seconds=pd.Series([], dtype=float),
+            corpus_commit_time=pd.Series([], dtype="datetime64[ns, UTC]"))
     df = pd.read_csv(io.StringIO(t.corpus_csv))
     df["corpus_commit_time"] = pd.to_datetime(df["corpus_commit_time"], errors="coerce", utc=True)
     return df

@@ -67,6 +67,19 @@ def _result_str(t: Tables, code):
 
 
 # ------------------------------------------------------------------------------------- RQ1
+def rq1_late_lines(d: Describe) -> List[str]:
+    """rq1_detection_rate.py:262-268: the late-stage block (first line starts with a newline)."""
+    if d.min_nonzero is None:
+        raise ValueError("min() arg is an empty sequence")   # the reference raises here (:264)
+    return ["\nAnalysis of detection rates from iteration 26 onwards (for paper replication):",
+            f"  - Min/Max: {d.min:.2f}% / {d.max:.2f}%",
+            f"value min and than 0 {d.min_nonzero}",
+            f"  - IQR (25th-75th percentile): {d.q1:.2f}% - {d.q3:.2f}%",
+            f"  - Median: {d.median:.2f}%",
+            f"  - Mean: {d.mean:.2f}%",
+            f"  - Zero count: {d.n_zero/d.count*100:.2f}%({d.n_zero}/{d.count})"]
+
+
 def rq1(r: RQ1Result, t: Tables) -> Rendered:
     """rq1_detection_rate.py:127-268 (collect_and_analyze_data) and :308-348 (main)."""
     o = Rendered()
@@ -89,16 +102,8 @@ def rq1(r: RQ1Result, t: Tables) -> Rendered:
     for i, rate in enumerate(rates[:first_down]):
         o.p(f"{i+1}: {rate:.4f}%")
     if late:
-        d = r.late
-        o.p("\nAnalysis of detection rates from iteration 26 onwards (for paper replication):")
-        o.p(f"  - Min/Max: {d.min:.2f}% / {d.max:.2f}%")
-        if d.min_nonzero is None:
-            raise ValueError("min() arg is an empty sequence")   # the reference raises here (:264)
-        o.p(f"value min and than 0 {d.min_nonzero}")
-        o.p(f"  - IQR (25th-75th percentile): {d.q1:.2f}% - {d.q3:.2f}%")
-        o.p(f"  - Median: {d.median:.2f}%")
-        o.p(f"  - Mean: {d.mean:.2f}%")
-        o.p(f"  - Zero count: {d.n_zero/d.count*100:.2f}%({d.n_zero}/{d.count})")
+        for line in rq1_late_lines(r.late):
+            o.p(line)
     out_dir = "data/result_data/rq1"
     raw_path = os.path.join(out_dir, "rq1_raw_issues_for_analysis.csv")
     stats_path = os.path.join(out_dir, "rq1_detection_rate_stats.csv")
@@ -320,6 +325,50 @@ def _gname(g):
             'group3': 'Group D (1-5 Day Corpus)', 'group4': 'Group C (>5 Day Corpus)'}[g]
 
 
+_TREND_HDR = ['Iteration', 'G1_Total_Projects', 'G1_Detected_Count', 'G1_Detection_Rate_pct',
+              'G2_Total_Projects', 'G2_Detected_Count', 'G2_Detection_Rate_pct']
+
+
+def rq4a_trend_lines(rows, after) -> List[str]:
+    """rq4a_bug.py:698-747: superiority count, first iteration below 5 %, median / IQR after it,
+    from the kept trend rows and the finishing statistics (``after[g] = (median, iqr)`` or None)."""
+    out = []
+    df = pd.DataFrame(rows, columns=_TREND_HDR)
+    sup = int(np.sum(df['G2_Detection_Rate_pct'] > df['G1_Detection_Rate_pct']))
+    tot = len(df)
+    out.append(f"Count of Group B exceeding Group A within valid data range: {sup}/{tot} "
+               f"({(sup / tot) * 100 if tot > 0 else 0:.2f}%)")
+    g1r = df['G1_Detection_Rate_pct'].tolist()
+    g2r = df['G2_Detection_Rate_pct'].tolist()
+
+    def first5(rates):
+        for idx, rate in enumerate(rates):
+            if rate < 5:
+                return idx
+        return len(rates)
+    f1, f2 = first5(g1r), first5(g2r)
+    for name, f, rates in (("Group A", f1, g1r), ("Group B", f2, g2r)):
+        if f < len(rates):
+            out.append(f"{name}: {df.iloc[f]['Iteration']}th iteration fell below 5% (value: {rates[f]:.2f}%)")
+        else:
+            out.append(f"{name}: No iteration fell below 5%")
+    for name, key in (("Group A", "g1"), ("Group B", "g2")):
+        a = after[key]
+        if a is not None:
+            out.append(f"{name}: median {a[0]:.2f}, IQR {a[1]:.2f}")
+            out.append(f"{name}: Last valid data count {df.iloc[-1]['Iteration']}th")
+        else:
+            out.append(f"{name}: No data below 5%")
+    return out
+
+
+def rq4a_intro_lines(n_pos, intro_stats) -> List[str]:
+    """rq4a_bug.py:281-285 (the N > 0 introduction iterations' summary)."""
+    mean, med, mn, mxx = intro_stats
+    return [f"[RESULT] Introduction Iteration (N={n_pos}):", f"  - Mean: {mean:.2f}", f"  - Median: {med:.1f}",
+            f"  - Min: {mn}", f"  - Max: {mxx}"]
+
+
 def rq4a(r: RQ4aResult, t: Tables, cwd: str = "<WORK>") -> Rendered:
     """rq4a_bug.py:653-882."""
     o = Rendered()
@@ -344,37 +393,13 @@ def rq4a(r: RQ4aResult, t: Tables, cwd: str = "<WORK>") -> Rendered:
     for row in rows:
         if row[0] <= 100:
             o.info(f"| {row[0]:<4} | {row[1]:<8} | {row[3]:>6.2f}% | {row[4]:<8} | {row[6]:>6.2f}% |")
-    hdr = ['Iteration', 'G1_Total_Projects', 'G1_Detected_Count', 'G1_Detection_Rate_pct',
-           'G2_Total_Projects', 'G2_Detected_Count', 'G2_Detection_Rate_pct']
-    o.files["data/result_data/rq4/bug/rq4_g1_g2_detection_trend.csv"] = csv_bytes(rows, hdr)
+    o.files["data/result_data/rq4/bug/rq4_g1_g2_detection_trend.csv"] = csv_bytes(rows, _TREND_HDR)
     o.info(f"Saved G1/G2 trend statistics to: {os.path.join(out_dir, 'rq4_g1_g2_detection_trend.csv')}")
     o.p(f"Groups used: {_gname('group1')} ({len(g['group1'])} projects), {_gname('group2')} ({len(g['group2'])} projects)")
-    df = pd.DataFrame(rows, columns=hdr)
-    sup = int(np.sum(df['G2_Detection_Rate_pct'] > df['G1_Detection_Rate_pct']))
-    tot = len(df)
-    o.p(f"Count of Group B exceeding Group A within valid data range: {sup}/{tot} ({(sup / tot) * 100 if tot > 0 else 0:.2f}%)")
-    g1r = df['G1_Detection_Rate_pct'].tolist()
-    g2r = df['G2_Detection_Rate_pct'].tolist()
-
-    def first5(rates):
-        for idx, rate in enumerate(rates):
-            if rate < 5:
-                return idx
-        return len(rates)
-    f1, f2 = first5(g1r), first5(g2r)
-    for name, f, rates in (("Group A", f1, g1r), ("Group B", f2, g2r)):
-        if f < len(rates):
-            o.p(f"{name}: {df.iloc[f]['Iteration']}th iteration fell below 5% (value: {rates[f]:.2f}%)")
-        else:
-            o.p(f"{name}: No iteration fell below 5%")
-    for name, key in (("Group A", "g1"), ("Group B", "g2")):
-        a = r.after[key]
-        if a is not None:
-            o.p(f"{name}: median {a[0]:.2f}, IQR {a[1]:.2f}")
-            o.p(f"{name}: Last valid data count {df.iloc[-1]['Iteration']}th")
-        else:
-            o.p(f"{name}: No data below 5%")
-    mv = int(df['Iteration'].max()) if tot else 0
+    for line in rq4a_trend_lines(rows, r.after):
+        o.p(line)
+    tot = len(rows)
+    mv = int(rows[-1][0]) if tot else 0
     o.p(f"\n[Graph Limit Info] Max iteration where both groups maintained >= 100 projects: {mv}")
     o.p("Data around end:")
     if mv > 0:
@@ -398,12 +423,8 @@ def rq4a(r: RQ4aResult, t: Tables, cwd: str = "<WORK>") -> Rendered:
     dfi = pd.DataFrame([(t.projects[p], k) for p, k in intro], columns=['Project', 'Introduction_Iteration'])
     o.info(f"[RESULT] Total Group C Projects analyzed: {len(dfi)}")
     if r.intro_stats is not None:
-        mean, med, mn, mxx = r.intro_stats
-        o.info(f"[RESULT] Introduction Iteration (N={int((dfi['Introduction_Iteration'] > 0).sum())}):")
-        o.info(f"  - Mean: {mean:.2f}")
-        o.info(f"  - Median: {med:.1f}")
-        o.info(f"  - Min: {mn}")
-        o.info(f"  - Max: {mxx}")
+        for line in rq4a_intro_lines(int((dfi['Introduction_Iteration'] > 0).sum()), r.intro_stats):
+            o.info(line)
     else:
         o.info("[RESULT] No projects found with corpus introduction after the first fuzzing session.")
     o.files["data/result_data/rq4/bug/rq4_gc_introduction_iteration.csv"] = dfi.to_csv(index=False).encode()
