@@ -31,7 +31,11 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-PROBE_KERNEL = "radix_scatter"   # dominant kernel of the step (profiles/r01_*_stats.csv)
+PROBE_KERNEL = "radix_scatter"   # headline kernel of the roofline object
+# the per-kernel roofline table (a separate probe window after the timed region; algorithmic bytes
+# per launch as DESIGN.md 4 defines them)
+TABLE_KERNELS = ["radix_scatter", "radix_hist", "elig_hist", "seg_time_sort", "seg_merge_sort", "filter_compact",
+                 "seg_reduce"]
 STAGES = ["store", "rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"]
 WORKLOADS = {"c2": "config2: ~1M-session synthetic table",
              "c3": "config3: 100M-row coverage-only table, 10k projects x 10k days",
@@ -56,6 +60,11 @@ def parse():
     # one rank through the sharded step (exchanges, host syncs, recombination) over a world-1 group:
     # the floor of the multi-GPU step time on a one-GPU box
     ap.add_argument("--force-sharded", action="store_true")
+    # strong scaling (BASELINE north_star: 1->8 GPUs on one 100M-row table): every rank builds the
+    # same table and keeps its parallel.shard_bounds project range; value = the whole table's rows
+    ap.add_argument("--strong", action="store_true")
+    # steps of the per-kernel probe window after the timed region (0: no table)
+    ap.add_argument("--probe-steps", type=int, default=5)
     return ap.parse_args()
 
 
@@ -83,10 +92,19 @@ def main():
             dist.init_process_group("gloo", **init)
     dev = torch.device("cuda", local)
 
-    cfg = synth.config(args.config, seed=synth.config(args.config).seed + 1000 * rank)
-    t = synth.generate(cfg)
-    if world > 1:
-        t = weak_shard(t, rank, world)
+    if args.strong:
+        from tse_amd import parallel as par
+        full = synth.generate(synth.config(args.config))
+        lo, hi = par.shard_bounds(full, world)[rank]
+        t = par.take_shard(full, lo, hi)[0]
+        job_rows = full.n_rows
+        del full
+    else:
+        cfg = synth.config(args.config, seed=synth.config(args.config).seed + 1000 * rank)
+        t = synth.generate(cfg)
+        if world > 1:
+            t = weak_shard(t, rank, world)
+        job_rows = None
     eng = E.Engine(local)
     eng.upload(t)  # first upload: pinned-buffer / allocator warm-up
     torch.cuda.synchronize(dev)
@@ -94,6 +112,7 @@ def main():
     eng.upload(t)  # host columns -> HBM (PCIe), timed for the end-to-end rate (never `value`)
     torch.cuda.synchronize(dev)
     upload_ms = (time.perf_counter() - t_up) * 1e3
+    up = eng.upload_timing()  # host staging memcpy vs the H2D copy itself
     st = eng.build_store()
     if sharded:
         from tse_amd import parallel as par
@@ -103,7 +122,10 @@ def main():
         rq2c_shard = par.GpuRQ2CountShard(eng)
         rq4a_shard = par.GpuRQ4aShard(eng, M)
         rq4b_shard = par.GpuRQ4bShard(eng)
-        own = (rank * len(t.projects) // world, (rank + 1) * len(t.projects) // world)  # weak_shard ids
+        if args.strong:
+            own = (lo, hi)
+        else:
+            own = (rank * len(t.projects) // world, (rank + 1) * len(t.projects) // world)  # weak_shard ids
     rq1_bufs = compute.RQ1Buffers(eng)
     bufs = {"rq2_count": compute.rq2_count_buffers(eng), "rq2_add": compute.rq2_add_buffers(eng),
             "rq3": compute.rq3_buffers(eng), "rq4a": compute.rq4a_buffers(eng), "rq4b": compute.rq4b_buffers(eng)}
@@ -164,6 +186,22 @@ def main():
     dev_ms = ev0.elapsed_time(ev1)
     elapsed = wall
     rows = float(t.n_rows)
+    # per-kernel table: a separate window (its HIP events would perturb the timed steps)
+    table = []
+    if args.probe_steps > 0:
+        eng.probe_begin(",".join(TABLE_KERNELS))
+        for _ in range(args.probe_steps):
+            step()
+        eng.probe_end()
+        for k in TABLE_KERNELS:
+            n, ms_k, b_k = eng.probe_get(k)
+            if n == 0 or ms_k <= 0:
+                continue
+            ach = b_k / (ms_k * 1e-3) / 1e9
+            table.append({"kernel": k, "launches_per_step": round(n / args.probe_steps, 2),
+                          "avg_launch_us": round(ms_k / n * 1e3, 3), "bytes_per_launch": round(b_k / n),
+                          "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                          "ms_per_step": round(ms_k / args.probe_steps, 4)})
     if world > 1:
         v = torch.tensor([elapsed, rows], dtype=torch.float64, device=dev)
         tmax = v[:1].clone()
@@ -171,6 +209,8 @@ def main():
         rsum = v[1:].clone()
         par.all_reduce(rsum)
         elapsed, rows = float(tmax.item()), float(rsum.item())
+    if job_rows is not None:  # strong scaling: the whole table, whatever the shard sizes
+        rows = float(job_rows)
 
     out = None
     if rank == 0:
@@ -184,7 +224,7 @@ def main():
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.probe, args.config),
                     "kernel": args.probe,
                     "avg_launch_us": round(avg_ms * 1e3, 3), "bytes_per_launch": probe_bytes / launches,
-                    "launches_per_step": launches / args.steps}
+                    "launches_per_step": launches / args.steps, "kernels": table}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(t, stages)
@@ -192,15 +232,17 @@ def main():
             "metric": "session-rows/sec through RQ1-RQ4 aggregates+stats",
             "value": round(value, 1), "unit": "session-rows/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int64/fp64", "data": "synthetic",
+            "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "int64/fp64", "data": "synthetic",
             "config": {"workload": f"{WORKLOADS.get(args.config, args.config)} ({args.config}), "
-                                   f"{len(t.projects)} projects/rank",
+                                   + (f"one table split over {world} ranks" if args.strong
+                                      else f"{len(t.projects)} projects/rank"),
                        "rows_per_rank": t.n_rows, "builds": int(len(t.b_project)), "coverage": int(len(t.c_project)),
                        "issues": int(len(t.i_project)), "stages": stages, "parallelism": f"project-shard x{world}" + (" (sharded path)" if sharded and world == 1 else ""),
                        "device_ms_per_step": round(dev_ms / args.steps, 4),
                        # end-to-end (host columns -> HBM upload + one step), per rank: the loader's
                        # PCIe-inclusive rate; `value` is compute-only with inputs resident in HBM
-                       "upload_ms": round(upload_ms, 3),
+                       "upload_ms": round(upload_ms, 3), "upload_host_ms": up["host_ms"],
+                       "upload_h2d_ms": up["h2d_ms"], "upload_h2d_gbs": up["h2d_gbs"],
                        "rows_per_s_incl_upload": round(t.n_rows / ((upload_ms + ms_step) * 1e-3), 1)},
             "roofline": roof, "cpu_baseline": cpu,
         }
@@ -229,8 +271,9 @@ def pmc_traffic(probe, config):
 
 def weak_shard(t, rank, world):
     """Rank `rank`'s table as one shard of a world-times-larger job: project ids rank * P + p in a
-    global id space of world * P projects, issue numbers made unique per rank (OSS-Fuzz numbers
-    are unique per tracker; the cross-shard dedup check still runs every step)."""
+    global id space of world * P projects.  Issue numbers keep their values: the ranks draw them
+    from the same range, so numbers collide across shards and the cross-shard ROW_NUMBER dedup
+    (fz_rq1_ex re-run, queries1.py:29-32) happens inside every timed step."""
     import dataclasses
     P = len(t.projects)
     off = np.uint32(rank * P)
@@ -239,7 +282,7 @@ def weak_shard(t, rank, world):
     names = [n if r == rank else f"~{r}-{n}" for r in range(world) for n in t.projects]
     return dataclasses.replace(
         t, projects=names, b_project=t.b_project + off, c_project=t.c_project + off, i_project=t.i_project + off,
-        pi_project=t.pi_project + off, i_number=t.i_number + np.int64(rank) * 100_000_000)
+        pi_project=t.pi_project + off)
 
 
 def cpu_baseline(t, stages):

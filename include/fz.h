@@ -401,11 +401,13 @@ int fz_rq4b_session_stats(fz_ctx *ctx, const double *values, const int64_t *sess
 int fz_two_sample_tests(fz_ctx *ctx, const double *x, int64_t nx, const double *y, int64_t ny, double *out);
 
 /* ---- per-kernel probe (bench.py roofline) ------------------------------------------------ */
-/* Start timing every launch of the named kernel (e.g. "radix_scatter", "elig_hist") with HIP
- * events on the context stream; fz_probe_end synchronises the stream and returns the number of
- * launches, their summed device milliseconds and their summed algorithmic bytes. */
-int fz_probe_begin(fz_ctx *ctx, const char *kernel_name);
+/* Start timing every launch of the named kernels (one name, or several separated by commas, e.g.
+ * "radix_scatter,elig_hist") with HIP events on the context stream; fz_probe_end synchronises the
+ * stream and returns the FIRST name's number of launches, summed device milliseconds and summed
+ * algorithmic bytes; fz_probe_get returns the same for any probed name until the next begin. */
+int fz_probe_begin(fz_ctx *ctx, const char *kernel_names);
 int fz_probe_end(fz_ctx *ctx, int64_t *launches, double *total_ms, double *algo_bytes);
+int fz_probe_get(fz_ctx *ctx, const char *kernel_name, int64_t *launches, double *total_ms, double *algo_bytes);
 
 /* ---- primitives (exported for kernel-level tests and the roofline bench) ----------------- */
 /* Stable LSD radix sort of (key, value) pairs over key bits [0, bits).  keys/vals in place. */

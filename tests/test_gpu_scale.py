@@ -49,3 +49,25 @@ def test_coverage_only_tables(engine, cfg):
     t = synth.generate(cfg)
     assert len(t.b_project) == 0 and len(t.i_project) == 0
     _check_all(engine, t)
+
+
+def test_big_segments_ties_nulls_wide_span(engine):
+    """Store sort edge cases of the segmented merge sort path: projects of > 4096 rows whose times
+    repeat (ORDER BY time keeps row order for ties: rq2_coverage_and_added.py:45-46,67-68 take the
+    first matching row), NULL build times inside them (ASC NULLS LAST) and a short project whose
+    coverage dates span more than the LDS kernel's packed key (~142 years) - checked through every
+    analysis against the oracle."""
+    from tse_amd.schema import TS_NULL, US_PER_DAY, ts_from_str
+    cfg = synth.SynthConfig(n_projects=16, seed=23, zipf_s=1.1, len_mean_days=1500, issues_mean=80,
+                            dup_numbers=2, hex_len=12)
+    t = synth.generate(cfg)
+    week = 7 * US_PER_DAY
+    t.b_time = t.b_time // week * week            # 7 builds of one type share each timestamp
+    t.c_date = t.c_date // (2 * US_PER_DAY) * (2 * US_PER_DAY)  # two coverage rows per date
+    rng = np.random.default_rng(5)
+    t.b_time[rng.choice(len(t.b_time), size=40, replace=False)] = TS_NULL
+    small = int(np.argmin(np.bincount(t.c_project, minlength=16)))
+    rows = np.nonzero(t.c_project == small)[0]
+    t.c_date[rows[:3]] = ts_from_str("2199-06-01")
+    st = _check_all(engine, t)
+    assert st.max_fuzz_per_project > 4096 and st.max_cov_per_project > 4096

@@ -75,3 +75,21 @@ def test_change_analysis_shipped(engine):
     errs = shipped.check_change_files(render.rq2_add(r, t).files)
     assert not errs, "\n".join(errs)
     assert_same(r, orc.rq2_add(t), "rq2_add")
+
+
+@pytest.mark.parametrize("nd", [1, 2, 3])
+def test_rq3_stats_tiny_samples(engine, nd):
+    """fz_rq3_stats with one to three detected changes (a shard's gathered sample can be that small):
+    every statistic as scipy computes it - Anderson-Darling with N = 1 is NaN with scipy's own
+    (negative) critical values, no error - checked against the oracle (scipy 1.15.3)."""
+    rng = np.random.default_rng(nd)
+    det = rng.normal(0, 1, size=nd)
+    tot = rng.integers(-5, 5, size=nd)
+    non = rng.normal(0.2, 2, size=40)
+    desc, tests = engine.rq3_stats(det, tot, non)
+    ref = orc.rq3_stats(det, tot, non)
+    assert_same(compute._describe(E.describe_from_doubles(desc[0])), ref["desc_detected"], "desc_detected")
+    ad = (float(tests[E.RQ3_AD_DET]), tests[E.RQ3_AD_DET + 1:E.RQ3_AD_DET + 6])
+    assert_same(ad, ref["anderson_det"], "anderson_det")
+    assert_same((float(tests[E.RQ3_LEVENE_W]), float(tests[E.RQ3_LEVENE_P])), ref["levene"], "levene")
+    assert_same((float(tests[E.RQ3_BM_STAT]), float(tests[E.RQ3_BM_P])), ref["brunnermunzel"], "brunnermunzel")

@@ -98,3 +98,44 @@ def test_pg_dump_empty_block_and_utc_offsets(tmp_path):
     assert int(t.b_time[0]) == int(np.datetime64("2020-01-02T03:04:05.000006", "us").astype(np.int64))
     assert t.c_coverage_valid.tolist() == [True, False] and t.c_covered_valid.tolist() == [True, False]
     assert t.c_coverage[0] == 12.5 and t.modules_pool == ["{m}"]
+
+
+def test_pg_dump_mixed_utc_offsets(tmp_path):
+    """timestamptz text dumped under a daylight-saving server TimeZone carries different offsets in
+    one column ('+01' in winter, '+02' in summer, also '+05:30'): every value keeps its printed
+    wall-clock time (the analyses compare naive values)."""
+    p = tmp_path / "d.sql"
+    p.write_text(
+        "COPY public.buildlog_data (name, project, build_type, result, timecreated, modules, revisions) FROM stdin;\n"
+        "b1\tp\tFuzzing\tFinish\t2020-01-02 03:04:05.25+01\t{m}\t{r}\n"
+        "b2\tp\tFuzzing\tFinish\t2020-07-02 03:04:05+02\t{m}\t{r}\n"
+        "b3\tp\tCoverage\tFinish\t2020-07-03 10:00:00+05:30\t{m}\t{r}\n\\.\n"
+        "COPY public.total_coverage (project, date, coverage, covered_line, total_line) FROM stdin;\n"
+        "p\t2020-01-02 00:00:00+01\t12.5\t10\t80\np\t2020-07-03 00:00:00+02\t\\N\t\\N\t\\N\n\\.\n"
+        "COPY public.issues (number, project, rts, status, new_id) FROM stdin;\n"
+        "7\tp\t2020-03-29 02:30:00-07\tFixed\t1\n\\.\n")
+    t = store.from_pg_dump(str(p), corpus_csv="")
+    us = lambda s: int(np.datetime64(s, "us").astype(np.int64))  # noqa: E731
+    assert t.b_time.tolist() == [us("2020-01-02T03:04:05.25"), us("2020-07-02T03:04:05"), us("2020-07-03T10:00:00")]
+    assert t.c_date.tolist() == [us("2020-01-02T00:00:00"), us("2020-07-03T00:00:00")]
+    assert t.i_rts.tolist() == [us("2020-03-29T02:30:00")]
+
+
+def test_project_order_override(tmp_path):
+    """ORDER BY project under a locale collation: the caller's order (a name list or a sort key)
+    replaces byte order for the project ids."""
+    p = tmp_path / "d.sql"
+    p.write_text(
+        "COPY public.buildlog_data (name, project, build_type, result, timecreated, modules, revisions) FROM stdin;\n"
+        "b1\tlib-b\tFuzzing\tFinish\t2020-01-02 03:04:05\t{m}\t{r}\n"
+        "b2\tlib_a\tFuzzing\tFinish\t2020-01-02 03:04:05\t{m}\t{r}\n"
+        "b3\tLibC\tFuzzing\tFinish\t2020-01-02 03:04:05\t{m}\t{r}\n\\.\n"
+        "COPY public.total_coverage (project, date, coverage, covered_line, total_line) FROM stdin;\n\\.\n"
+        "COPY public.issues (number, project, rts, status, new_id) FROM stdin;\n\\.\n")
+    assert store.from_pg_dump(str(p), corpus_csv="").projects == ["LibC", "lib-b", "lib_a"]   # bytes
+    t = store.from_pg_dump(str(p), corpus_csv="", project_order=["lib_a", "lib-b", "LibC"])
+    assert t.projects == ["lib_a", "lib-b", "LibC"] and t.b_project.tolist() == [1, 0, 2]
+    t = store.from_pg_dump(str(p), corpus_csv="", project_order=lambda s: s.lower().replace("-", "").replace("_", ""))
+    assert t.projects == ["lib_a", "lib-b", "LibC"]
+    with pytest.raises(ValueError, match="misses"):
+        store.from_pg_dump(str(p), corpus_csv="", project_order=["lib_a"])

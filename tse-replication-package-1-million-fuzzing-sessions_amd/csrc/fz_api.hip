@@ -235,13 +235,28 @@ int fz_two_sample_tests(fz_ctx *ctx, const double *x, int64_t nx, const double *
     });
 }
 
-int fz_probe_begin(fz_ctx *ctx, const char *kernel_name) {
+int fz_probe_begin(fz_ctx *ctx, const char *kernel_names) {
     return guarded(ctx, [&] {
-        FZ_CHECK(kernel_name != nullptr, "fz_probe_begin: null name");
-        ctx->probe.name = kernel_name;
-        ctx->probe.used = 0;
-        ctx->probe.launches = 0;
-        ctx->probe.bytes = 0.0;
+        FZ_CHECK(kernel_names != nullptr, "fz_probe_begin: null name");
+        fz::Probe &p = ctx->probe;
+        p.names.clear();
+        std::string all(kernel_names), cur;
+        for (size_t i = 0; i <= all.size(); ++i) {
+            if (i == all.size() || all[i] == ',') {
+                if (!cur.empty() && p.index(cur.c_str()) < 0) p.names.push_back(cur);
+                cur.clear();
+            } else {
+                cur += all[i];
+            }
+        }
+        FZ_CHECK(!p.names.empty(), "fz_probe_begin: no kernel name");
+        p.used = 0;
+        p.owner.clear();
+        p.deferred.clear();
+        p.counts.ensure<int64_t>(fz::Probe::kMaxCounts);
+        p.launches.assign(p.names.size(), 0);
+        p.bytes.assign(p.names.size(), 0.0);
+        p.ms.assign(p.names.size(), 0.0);
     });
 }
 
@@ -249,17 +264,39 @@ int fz_probe_end(fz_ctx *ctx, int64_t *launches, double *total_ms, double *algo_
     return guarded(ctx, [&] {
         fz::Probe &p = ctx->probe;
         fz::sync(ctx);
-        double ms = 0.0;
         for (size_t i = 0; i + 1 < p.used; i += 2) {
             float e = 0.f;
             FZ_HIP(hipEventElapsedTime(&e, p.pool[i], p.pool[i + 1]));
-            ms += e;
+            p.ms[size_t(p.owner[i / 2])] += e;
         }
-        if (launches) *launches = p.launches;
-        if (total_ms) *total_ms = ms;
-        if (algo_bytes) *algo_bytes = p.bytes;
-        p.name.clear();
+        if (!p.deferred.empty()) {
+            std::vector<int64_t> cnt(p.deferred.size());
+            FZ_HIP(hipMemcpy(cnt.data(), p.counts.as<int64_t>(), cnt.size() * 8, hipMemcpyDeviceToHost));
+            for (size_t i = 0; i < cnt.size(); ++i)
+                p.bytes[size_t(p.deferred[i].owner)] += double(cnt[i]) * p.deferred[i].per_count;
+            p.deferred.clear();
+        }
+        if (launches) *launches = p.launches.empty() ? 0 : p.launches[0];
+        if (total_ms) *total_ms = p.ms.empty() ? 0.0 : p.ms[0];
+        if (algo_bytes) *algo_bytes = p.bytes.empty() ? 0.0 : p.bytes[0];
+        p.results = p.names;  // fz_probe_get reads them until the next fz_probe_begin
+        p.names.clear();
         p.used = 0;
+        p.owner.clear();
+    });
+}
+
+int fz_probe_get(fz_ctx *ctx, const char *kernel_name, int64_t *launches, double *total_ms, double *algo_bytes) {
+    return guarded(ctx, [&] {
+        fz::Probe &p = ctx->probe;
+        FZ_CHECK(kernel_name != nullptr && !p.active(), "fz_probe_get: call after fz_probe_end");
+        int k = -1;
+        for (size_t i = 0; i < p.results.size(); ++i)
+            if (p.results[i] == kernel_name) k = int(i);
+        FZ_CHECK(k >= 0, std::string("fz_probe_get: kernel not probed: ") + kernel_name);
+        if (launches) *launches = p.launches[size_t(k)];
+        if (total_ms) *total_ms = p.ms[size_t(k)];
+        if (algo_bytes) *algo_bytes = p.bytes[size_t(k)];
     });
 }
 

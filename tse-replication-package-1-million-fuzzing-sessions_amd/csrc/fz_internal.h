@@ -137,7 +137,6 @@ struct Store {
     View cov;     // total_coverage by (project, date)                              queries1.py:120-129
     View issues;  // issues by (project, rts), ties in row order                    rq3:219-232
     int64_t passes = 0;
-    int64_t tmin[3] = {0, 0, 0}, tmax[3] = {0, 0, 0};  // builds, coverage, issues (non-NULL)
     int64_t num_min = 0, num_max = 0;                   // issues.number range
     // eligible projects (the GROUP BY/HAVING every script starts from), computed once per load
     DevBuf elig;     // uint8 [P]
@@ -152,16 +151,34 @@ struct Store {
     const int32_t *bperm = nullptr, *cperm = nullptr, *iperm = nullptr;
 };
 
-// Per-kernel timing probe (fz_probe_begin/end): brackets every launch of ONE named kernel with
-// HIP events on the context stream and accumulates its algorithmic bytes, so bench.py can
-// report achieved GB/s for that kernel over the timed region.
+// Per-kernel timing probe (fz_probe_begin/end/get): brackets every launch of the named kernels
+// with HIP events on the context stream and accumulates their algorithmic bytes, so bench.py can
+// report achieved GB/s per kernel.
 struct Probe {
-    std::string name;
-    std::vector<hipEvent_t> pool;  // pairs (start, stop)
+    std::vector<std::string> names;     // probed kernels (empty: probe off)
+    std::vector<hipEvent_t> pool;       // pairs (start, stop)
+    std::vector<int> owner;             // name index of each used pair
     size_t used = 0;
-    int64_t launches = 0;
-    double bytes = 0.0;
-    bool active() const { return !name.empty(); }
+    std::vector<int64_t> launches;
+    std::vector<double> bytes, ms;      // ms: filled by fz_probe_end
+    std::vector<std::string> results;   // names of the last finished probe window (fz_probe_get)
+    // algorithmic bytes that depend on a device count (e.g. rows kept by a filter): each probed
+    // launch's count is copied (async, on the stream) into counts[slot] and added at fz_probe_end
+    // as counts[slot] * per_count to the owner's bytes
+    static constexpr int64_t kMaxCounts = 1 << 16;
+    DevBuf counts;
+    struct Deferred {
+        int owner;
+        int64_t slot;
+        double per_count;
+    };
+    std::vector<Deferred> deferred;
+    bool active() const { return !names.empty(); }
+    int index(const char *n) const {
+        for (size_t i = 0; i < names.size(); ++i)
+            if (names[i] == n) return int(i);
+        return -1;
+    }
 };
 
 }  // namespace fz
@@ -187,13 +204,22 @@ struct fz_ctx {
 };
 
 namespace fz {
-// RAII bracket around one launch of kernel `name` moving `bytes` algorithmic bytes.
+// RAII bracket around one launch of kernel `name` moving `bytes` algorithmic bytes, plus
+// per_count bytes for every unit of the device count *d_count (read when the scope closes, i.e.
+// after the launch, so it may be the launch's own output count).
 struct ProbeScope {
     fz_ctx *c;
     bool on;
-    ProbeScope(fz_ctx *ctx, const char *name, double bytes) : c(ctx), on(false) {
+    int owner = -1;
+    const int64_t *d_count = nullptr;
+    double per_count = 0.0;
+    ProbeScope(fz_ctx *ctx, const char *name, double bytes, const int64_t *count = nullptr, double per = 0.0)
+        : c(ctx), on(false), d_count(count), per_count(per) {
         Probe &p = c->probe;
-        if (!p.active() || p.name != name) return;
+        if (!p.active()) return;
+        const int k = p.index(name);
+        if (k < 0) return;
+        owner = k;
         if (p.used + 2 > p.pool.size()) {
             for (int i = 0; i < 64; ++i) {
                 hipEvent_t e;
@@ -202,14 +228,20 @@ struct ProbeScope {
             }
         }
         FZ_HIP(hipEventRecord(p.pool[p.used], c->stream));
-        p.bytes += bytes;
-        p.launches += 1;
+        p.owner.push_back(k);
+        p.bytes[k] += bytes;
+        p.launches[k] += 1;
         on = true;
     }
     ~ProbeScope() {
-        if (on) {
-            (void)hipEventRecord(c->probe.pool[c->probe.used + 1], c->stream);
-            c->probe.used += 2;
+        if (!on) return;
+        Probe &p = c->probe;
+        (void)hipEventRecord(p.pool[p.used + 1], c->stream);
+        p.used += 2;
+        if (d_count && int64_t(p.deferred.size()) < Probe::kMaxCounts) {
+            const int64_t slot = int64_t(p.deferred.size());
+            (void)hipMemcpyAsync(p.counts.as<int64_t>() + slot, d_count, 8, hipMemcpyDeviceToDevice, c->stream);
+            p.deferred.push_back({owner, slot, per_count});
         }
     }
 };

@@ -28,27 +28,37 @@ __global__ __launch_bounds__(kBlock) void k_copy_elig(const uint8_t *__restrict_
 }
 
 // total_coverage rows: coverage IS NOT NULL AND coverage > 0 AND date < LIMIT, per project.
-// One workgroup per CU streams a contiguous slice into an LDS histogram and writes it as one row
-// of a [blocks][P] partial table (no global atomics, deterministic); k_elig_sum adds the columns.
+// One 1024-thread workgroup per CU (16 waves: enough loads in flight to stream HBM) takes a
+// contiguous slice into an LDS histogram and writes it as one row of a [blocks][P] partial table
+// (no global atomics, deterministic); k_elig_sum adds the columns.  Each thread handles two rows
+// per iteration, their four column loads issued before either predicate.
 constexpr int kEligBlocks = 256;
+constexpr int kEligThreads = 1024;
 constexpr int64_t kEligLdsMax = 16384;  // 64 KiB of int32 bins
 
-__global__ __launch_bounds__(kBlock) void k_elig_hist(const uint32_t *__restrict__ proj,
-                                                      const int64_t *__restrict__ date,
-                                                      const double *__restrict__ cov,
-                                                      const uint8_t *__restrict__ valid, int64_t n, int64_t P,
-                                                      int64_t limit, int32_t *__restrict__ part) {
+__global__ __launch_bounds__(kEligThreads) void k_elig_hist(const uint32_t *__restrict__ proj,
+                                                            const int64_t *__restrict__ date,
+                                                            const double *__restrict__ cov,
+                                                            const uint8_t *__restrict__ valid, int64_t n, int64_t P,
+                                                            int64_t limit, int32_t *__restrict__ part) {
     extern __shared__ int32_t s_hist[];
-    for (int64_t p = threadIdx.x; p < P; p += kBlock) s_hist[p] = 0;
+    for (int64_t p = threadIdx.x; p < P; p += kEligThreads) s_hist[p] = 0;
     __syncthreads();
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t lo = int64_t(blockIdx.x) * per, hi = lo + per < n ? lo + per : n;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
-        const bool ok = (valid[i] & FZ_VALID_COVERAGE) && cov[i] > 0.0 && date[i] < limit;
-        if (ok) atomicAdd(&s_hist[proj[i]], 1);
+    int64_t i = lo + threadIdx.x;
+    for (; i + kEligThreads < hi; i += 2 * kEligThreads) {
+        const int64_t j = i + kEligThreads;
+        const uint8_t va = valid[i], vb = valid[j];
+        const double ca = cov[i], cb = cov[j];
+        const int64_t da = date[i], db = date[j];
+        const uint32_t pa = proj[i], pb = proj[j];
+        if ((va & FZ_VALID_COVERAGE) && ca > 0.0 && da < limit) atomicAdd(&s_hist[pa], 1);
+        if ((vb & FZ_VALID_COVERAGE) && cb > 0.0 && db < limit) atomicAdd(&s_hist[pb], 1);
     }
+    if (i < hi && (valid[i] & FZ_VALID_COVERAGE) && cov[i] > 0.0 && date[i] < limit) atomicAdd(&s_hist[proj[i]], 1);
     __syncthreads();
-    for (int64_t p = threadIdx.x; p < P; p += kBlock) part[int64_t(blockIdx.x) * P + p] = s_hist[p];
+    for (int64_t p = threadIdx.x; p < P; p += kEligThreads) part[int64_t(blockIdx.x) * P + p] = s_hist[p];
 }
 
 // fallback for very many projects: global atomics straight into counts
@@ -101,7 +111,7 @@ static void eligibility(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *c
     if (P <= kEligLdsMax) {
         const int nb = t->n_cov > 0 ? kEligBlocks : 1;
         int32_t *part = c->arena.get<int32_t>(int64_t(nb) * P);
-        k_elig_hist<<<nb, kBlock, size_t(P) * 4, c->stream>>>(t->c_project, t->c_date, t->c_coverage, t->c_valid,
+        k_elig_hist<<<nb, kEligThreads, size_t(P) * 4, c->stream>>>(t->c_project, t->c_date, t->c_coverage, t->c_valid,
                                                                t->n_cov, P, limit, part);
         k_elig_sum<<<unsigned((P + kWave - 1) / kWave), kBlock, 0, c->stream>>>(part, nb, P, counts, elig, n_elig);
     } else {
@@ -170,6 +180,7 @@ __global__ __launch_bounds__(kBlock) void k_iter_total(const int64_t *__restrict
 }
 
 struct ValidFuzzRq1 {  // result IN ('Finish', 'Halfway') AND DATE(timecreated) < LIMIT  (queries1.py:39-43)
+    static constexpr int kBytes = 9;  // column bytes read per row (filter_compact probe)
     const uint8_t *result;
     const int64_t *time;
     __device__ bool operator()(int32_t r) const {

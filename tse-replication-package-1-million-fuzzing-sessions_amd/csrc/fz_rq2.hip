@@ -18,6 +18,7 @@ constexpr int64_t kLimitUs2 = 1736294400000000LL;  // '2025-01-08'
 void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count);
 
 struct CovTrendRows {  // coverage IS NOT NULL AND coverage != 0 AND DATE(date) < LIMIT, eligible only
+    static constexpr int kBytes = 21;  // column bytes read per row (filter_compact probe)
     const uint32_t *proj;
     const double *cov;
     const uint8_t *valid;
@@ -28,6 +29,7 @@ struct CovTrendRows {  // coverage IS NOT NULL AND coverage != 0 AND DATE(date) 
     }
 };
 struct NonZeroTotal {  // `if total != 0` (:300-303)
+    static constexpr int kBytes = 8;  // column bytes read per row (filter_compact probe)
     const int64_t *total;
     __device__ bool operator()(int32_t r) const { return total[r] != 0; }
 };
@@ -156,28 +158,23 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     seg_spearman_index(c, cs, ss, tr, o->corr, nullptr);
     seg_shapiro(c, cs, tv, ss, o->sw_w, o->sw_p);
 
-    // coverage_by_session_index: order by (index within project, project)
-    const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
+    // coverage_by_session_index: order by (index within project, project) - the values are in
+    // project order already, so a stable sort on the index alone keeps projects in order
     const int ibits = bits_for(uint64_t(M));
     uint64_t *key = c->arena.get<uint64_t>(NC);
     uint32_t *idx = c->arena.get<uint32_t>(NC);
     const uint32_t *tproj = T.proj;
     map_n(c, NC, nullptr, [=] __device__(int64_t j) {
         const int64_t live = *d_nt;
-        if (j < live) {
-            const uint32_t p = tproj[j];
-            key[j] = (uint64_t(j - toffs[p]) << pbits) | p;
-        } else {
-            key[j] = uint64_t(M) << pbits;  // past every real index
-        }
+        key[j] = j < live ? uint64_t(j - toffs[tproj[j]]) : uint64_t(M);  // M: past every real index
         idx[j] = uint32_t(j);
     });
-    radix_sort_pairs_swap(c, key, idx, NC, ibits + pbits);
+    radix_sort_pairs_swap(c, key, idx, NC, ibits);
     double *sv = o->session_values;
     uint32_t *sid = c->arena.get<uint32_t>(NC);
     map_n(c, NC, nullptr, [=] __device__(int64_t k) {
         const int64_t live = *d_nt;
-        sid[k] = uint32_t(key[k] >> pbits);
+        sid[k] = uint32_t(key[k]);
         if (k < live) sv[k] = tv[idx[k]];
     });
     segment_offsets_dn(c, sid, d_nt, NC, M, o->session_offsets);
@@ -226,6 +223,7 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
 constexpr int64_t kDayUs = 86400000000LL;
 
 struct CovBuildRows {  // result IN ('HalfWay', 'Finish') AND timecreated < LIMIT (:50-69), eligible
+    static constexpr int kBytes = 13;  // column bytes read per row (filter_compact probe)
     const uint32_t *proj;
     const uint8_t *result;
     const int64_t *time;
@@ -236,6 +234,7 @@ struct CovBuildRows {  // result IN ('HalfWay', 'Finish') AND timecreated < LIMI
     }
 };
 struct CovRowsBeforeLimit {  // GET_COVERAGE_DATA: date < LIMIT, no NULL filter (:30-47), eligible
+    static constexpr int kBytes = 12;  // column bytes read per row (filter_compact probe)
     const uint32_t *proj;
     const int64_t *date;
     const uint8_t *elig;

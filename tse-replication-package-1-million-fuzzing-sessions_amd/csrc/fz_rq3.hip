@@ -26,6 +26,7 @@ __device__ inline int64_t fdiv_day(int64_t a) {
 }
 
 struct FixedIssuesRq3 {  // status fixed, eligible project, rts < LIMIT (:219-232)
+    static constexpr int kBytes = 13;  // column bytes read per row (filter_compact probe)
     const uint32_t *proj;
     const uint8_t *status;
     const int64_t *rts;
@@ -33,15 +34,18 @@ struct FixedIssuesRq3 {  // status fixed, eligible project, rts < LIMIT (:219-23
     __device__ bool operator()(int32_t r) const { return status[r] <= 1 && rts[r] < kLim3 && elig[proj[r]]; }
 };
 struct FuzzRq3 {  // Fuzzing, result IN ('HalfWay', 'Finish'), DATE(timecreated) < '2025-01-08' (:260-261)
+    static constexpr int kBytes = 9;  // column bytes read per row (filter_compact probe)
     const uint8_t *result;
     const int64_t *time;
     __device__ bool operator()(int32_t r) const { return (result[r] == 2 || result[r] == 0) && time[r] < kLim3; }
 };
 struct CovBuildRq3 {  // Coverage, any result, DATE(timecreated) < '2025-01-09' (:262)
+    static constexpr int kBytes = 8;  // column bytes read per row (filter_compact probe)
     const int64_t *time;
     __device__ bool operator()(int32_t r) const { return time[r] < kLim3b; }
 };
 struct CovRowsRq3 {  // covered_line IS NOT NULL AND DATE(date) < '2025-01-09' (:263)
+    static constexpr int kBytes = 9;  // column bytes read per row (filter_compact probe)
     const uint8_t *valid;
     const int64_t *date;
     __device__ bool operator()(int32_t r) const { return (valid[r] & FZ_VALID_COVERED) && date[r] < kLim3b; }

@@ -238,6 +238,7 @@ void rq4a_finish(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int6
 
 // ------------------------------------------------------------------------------------ RQ4b
 struct FullTrendRows {  // get_full_coverage_trend: coverage > 0, date < LIMIT (rq4b:315-326), G1/G2 only
+    static constexpr int kBytes = 21;  // column bytes read per row (filter_compact probe)
     const uint32_t *proj;
     const double *cov;
     const uint8_t *valid;
@@ -248,6 +249,7 @@ struct FullTrendRows {  // get_full_coverage_trend: coverage > 0, date < LIMIT (
     }
 };
 struct PositiveCoverage34 {  // get_coverage_deltas: coverage > 0, any date (rq4b:745-772), G3/G4 only
+    static constexpr int kBytes = 13;  // column bytes read per row (filter_compact probe)
     const uint32_t *proj;
     const double *cov;
     const uint8_t *valid;
@@ -414,8 +416,8 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
     int64_t *c2 = o->c2, *c1 = o->c1;
     double *g2q = o->g2_q, *g1q = o->g1_q;
     if (!sharded) {
-        // (session, group) key per value: G2 -> group 0 (x), G1 -> group 1 (y)
-        const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
+        // (session, group) key per value: G2 -> group 0 (x), G1 -> group 1 (y); the values are in
+        // project order, so the stable sort on (session, group) alone keeps projects in order
         const int64_t S2 = 2 * MM;
         const int sbits = bits_for(uint64_t(S2 + 1));
         uint64_t *key = c->arena.get<uint64_t>(NC);
@@ -424,17 +426,17 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
             if (j < *d_nf) {
                 const uint32_t p = fproj[j];
                 const uint64_t grp = (member[p] & 2) ? 0u : 1u;
-                key[j] = ((uint64_t(j - foffs[p]) * 2u + grp) << pbits) | p;
+                key[j] = uint64_t(j - foffs[p]) * 2u + grp;
             } else {
-                key[j] = uint64_t(S2) << pbits;
+                key[j] = uint64_t(S2);
             }
             idx[j] = uint32_t(j);
         });
-        radix_sort_pairs_swap(c, key, idx, NC, sbits + pbits);
+        radix_sort_pairs_swap(c, key, idx, NC, sbits);
         double *v2 = c->arena.get<double>(NC);
         uint32_t *sid2 = c->arena.get<uint32_t>(NC);
         map_n(c, NC, nullptr, [=] __device__(int64_t k) {
-            sid2[k] = uint32_t(key[k] >> pbits);
+            sid2[k] = uint32_t(key[k]);
             if (k < *d_nf) v2[k] = cov[frow[idx[k]]];
         });
         rq4b_sessions(c, v2, sid2, NC, d_nf, MM, P, P, c2, c1, g2q, g1q, o->p_bm);  // <= 1 value per project

@@ -27,6 +27,25 @@ struct Segs {
 // ones take the device-wide LSD radix path.
 constexpr int64_t kLdsSortMax = 4096;
 
+// Layouts with very many segments (one session per index of the
+// longest project - up to ~2e7 sessions, almost all holding a handful of values) are handled by
+// size class: every kernel visits only its own class's segments (device-built lists), a tiny
+// segment is sorted by one wave (register bitonic network) and reduced by one thread, instead of
+// one workgroup walking every segment.  Used when S > kManySegs.
+constexpr int kMicroSeg = 8;   // sorted by one thread (register sorting network), no list
+constexpr int kTinySeg = 64;   // reduced by one thread; sorted by one wave (9..64 values)
+constexpr int64_t kManySegs = 16384;
+enum { kClassTiny = 0, kClassMid, kClassWide, kClassBig, kClassNonTiny, kNumClasses };
+struct SegLists {
+    bool on = false;
+    int64_t *d_n = nullptr;  // [kNumClasses] device counts
+    int32_t *ids[kNumClasses] = {};
+    int64_t cap[kNumClasses] = {};
+};
+// Lists of segment ids: tiny (kMicroSeg < len <= kTinySeg), mid (<= 1024), wide (<= kLdsSortMax),
+// big (longer) and non-tiny (mid + wide + big).  Order inside a list is unspecified.
+SegLists seg_lists(fz_ctx *c, const Segs &sg);
+
 struct ChunkMap {
     int64_t cap = 0;
     int64_t *d_n = nullptr;
@@ -43,68 +62,98 @@ int32_t *segment_ids(fz_ctx *c, const Segs &sg);
 // ones (cps chunks per segment, chosen on the host when every segment is short) derive chunk k
 // from the offsets - segment k / cps, piece k % cps - so no map kernels run.  With out != null
 // (cps == 1) the chunk sum is the segment result and is written straight to out.
+// Chunks [blockIdx.x, nk) step gridDim.x (nk = *cm.d_n for explicit maps, else nk_host).
 template <int NV, typename F>
 __global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, const int64_t *__restrict__ offs, int64_t cps,
-                                                         F f, double *__restrict__ part, double *__restrict__ out) {
+                                                         int64_t nk_host, F f, double *__restrict__ part,
+                                                         double *__restrict__ out) {
     __shared__ double s_hi[4][NV], s_lo[4][NV];
-    const int64_t k = blockIdx.x;
-    int32_t seg;
-    int64_t b, e;
-    if (cm.d_n) {
-        if (k >= *cm.d_n) return;
-        seg = cm.seg[k];
-        b = cm.begin[k];
-        e = cm.end[k];
-    } else {
-        seg = int32_t(k / cps);
-        b = offs[seg] + (k % cps) * kChunk;
-        e = b + kChunk < offs[seg + 1] ? b + kChunk : offs[seg + 1];
-    }
-    DD acc[NV];
-#pragma unroll
-    for (int v = 0; v < NV; ++v) acc[v] = DD{0.0, 0.0};
-    for (int64_t i = b + threadIdx.x; i < e; i += kBlock) {
-        double x[NV];
-        f(i, seg, x);
-#pragma unroll
-        for (int v = 0; v < NV; ++v) acc[v] = dd_add_d(acc[v], x[v]);
-    }
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        DD r = wave_dd_sum(acc[v]);
-        if (lane_id() == 0) {
-            s_hi[wave_id()][v] = r.hi;
-            s_lo[wave_id()][v] = r.lo;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < NV) {
-        const int v = threadIdx.x;
-        DD t{s_hi[0][v], s_lo[0][v]};
-        for (int w = 1; w < 4; ++w) t = dd_add(t, DD{s_hi[w][v], s_lo[w][v]});
-        if (out) {
-            out[int64_t(seg) * NV + v] = t.hi + t.lo;
+    const int64_t nk = cm.d_n ? *cm.d_n : nk_host;
+    for (int64_t k = blockIdx.x; k < nk; k += gridDim.x) {
+        int32_t seg;
+        int64_t b, e;
+        if (cm.d_n) {
+            seg = cm.seg[k];
+            b = cm.begin[k];
+            e = cm.end[k];
         } else {
-            part[(k * NV + v) * 2] = t.hi;
-            part[(k * NV + v) * 2 + 1] = t.lo;
+            seg = int32_t(k / cps);
+            b = offs[seg] + (k % cps) * kChunk;
+            e = b + kChunk < offs[seg + 1] ? b + kChunk : offs[seg + 1];
         }
+        DD acc[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] = DD{0.0, 0.0};
+        for (int64_t i = b + threadIdx.x; i < e; i += kBlock) {
+            double x[NV];
+            f(i, seg, x);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) acc[v] = dd_add_d(acc[v], x[v]);
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            DD r = wave_dd_sum(acc[v]);
+            if (lane_id() == 0) {
+                s_hi[wave_id()][v] = r.hi;
+                s_lo[wave_id()][v] = r.lo;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < NV) {
+            const int v = threadIdx.x;
+            DD t{s_hi[0][v], s_lo[0][v]};
+            for (int w = 1; w < 4; ++w) t = dd_add(t, DD{s_hi[w][v], s_lo[w][v]});
+            if (out) {
+                out[int64_t(seg) * NV + v] = t.hi + t.lo;
+            } else {
+                part[(k * NV + v) * 2] = t.hi;
+                part[(k * NV + v) * 2 + 1] = t.lo;
+            }
+        }
+        __syncthreads();
     }
 }
 
 // out[s * NV + v] = sum over segment s's chunks (one wave per segment, chunks in order; implicit
-// maps: chunk_off == null, segment s owns chunks [s * cps, (s + 1) * cps)).
+// maps: chunk_off == null, segment s owns chunks [s * cps, (s + 1) * cps)).  With a list, the
+// waves walk the listed segments only (*d_ln of them).
 template <int NV>
 __global__ __launch_bounds__(kBlock) void k_seg_sum(int64_t S, const int64_t *__restrict__ chunk_off, int64_t cps,
-                                                    const double *__restrict__ part, double *__restrict__ out) {
-    const int64_t s = int64_t(blockIdx.x) * 4 + wave_id();
-    if (s >= S) return;
-    const int64_t c0 = chunk_off ? chunk_off[s] : s * cps, c1 = chunk_off ? chunk_off[s + 1] : (s + 1) * cps;
+                                                    const double *__restrict__ part, double *__restrict__ out,
+                                                    const int32_t *__restrict__ list, const int64_t *__restrict__ d_ln) {
+    const int64_t ns = list ? *d_ln : S;
+    for (int64_t w = int64_t(blockIdx.x) * 4 + wave_id(); w < ns; w += int64_t(gridDim.x) * 4) {
+        const int64_t s = list ? list[w] : w;
+        const int64_t c0 = chunk_off ? chunk_off[s] : s * cps, c1 = chunk_off ? chunk_off[s + 1] : (s + 1) * cps;
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        DD acc{0.0, 0.0};
-        for (int64_t k = c0 + lane_id(); k < c1; k += 64) acc = dd_add(acc, DD{part[(k * NV + v) * 2], part[(k * NV + v) * 2 + 1]});
-        acc = wave_dd_sum(acc);
-        if (lane_id() == 0) out[s * NV + v] = acc.hi + acc.lo;
+        for (int v = 0; v < NV; ++v) {
+            DD acc{0.0, 0.0};
+            for (int64_t k = c0 + lane_id(); k < c1; k += 64)
+                acc = dd_add(acc, DD{part[(k * NV + v) * 2], part[(k * NV + v) * 2 + 1]});
+            acc = wave_dd_sum(acc);
+            if (lane_id() == 0) out[s * NV + v] = acc.hi + acc.lo;
+        }
+    }
+}
+
+// Segments of <= kTinySeg values, one thread each (sequential double-double sum).
+template <int NV, typename F>
+__global__ __launch_bounds__(kBlock) void k_tiny_reduce(const int64_t *__restrict__ offs, int64_t S, F f,
+                                                        double *__restrict__ out) {
+    for (int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x; s < S; s += int64_t(gridDim.x) * kBlock) {
+        const int64_t b = offs[s], e = offs[s + 1];
+        if (e - b > kTinySeg) continue;
+        DD acc[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] = DD{0.0, 0.0};
+        for (int64_t i = b; i < e; ++i) {
+            double x[NV];
+            f(i, int32_t(s), x);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) acc[v] = dd_add_d(acc[v], x[v]);
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) out[s * NV + v] = acc[v].hi + acc[v].lo;
     }
 }
 
@@ -115,6 +164,7 @@ struct ChunkedSegs {
     ChunkMap cm;
     int64_t *chunk_off = nullptr;  // [S + 1]
     int64_t cps = 0;               // implicit: chunks per segment
+    SegLists lists;                // on: the map covers only the non-tiny segments (see kManySegs)
 };
 ChunkedSegs chunked(fz_ctx *c, const Segs &sg);
 
@@ -123,16 +173,28 @@ template <int NV, typename F>
 void seg_reduce(fz_ctx *c, const ChunkedSegs &cs, F f, double *out) {
     const int64_t S = cs.sg.S;
     if (S <= 0) return;
+    // algorithmic bytes: NV doubles per live element (offs[S]) in, NV per segment out
+    ProbeScope ps(c, "seg_reduce", 8.0 * NV * double(S), cs.sg.offs + S, 8.0 * NV);
     if (cs.cps == 1) {
-        k_chunk_reduce<NV, F><<<unsigned(S), kBlock, 0, c->stream>>>(cs.cm, cs.sg.offs, 1, f, nullptr, out);
+        k_chunk_reduce<NV, F><<<unsigned(S), kBlock, 0, c->stream>>>(cs.cm, cs.sg.offs, 1, S, f, nullptr, out);
         FZ_LAUNCH_CHECK();
         return;
     }
+    const SegLists &L = cs.lists;
+    if (L.on) {  // tiny segments one thread each; chunks of the others over a persistent grid
+        k_tiny_reduce<NV, F><<<grid_for(S, kBlock, 4096), kBlock, 0, c->stream>>>(cs.sg.offs, S, f, out);
+        FZ_LAUNCH_CHECK();
+    }
     const int64_t blocks = cs.cps > 0 ? S * cs.cps : cs.cm.cap;
     double *part = c->arena.get<double>(blocks * NV * 2);
-    k_chunk_reduce<NV, F><<<unsigned(blocks), kBlock, 0, c->stream>>>(cs.cm, cs.sg.offs, cs.cps, f, part, nullptr);
+    const unsigned g = unsigned(L.on ? (blocks < 8192 ? blocks : 8192) : blocks);
+    k_chunk_reduce<NV, F><<<g, kBlock, 0, c->stream>>>(cs.cm, cs.sg.offs, cs.cps, blocks, f, part, nullptr);
     FZ_LAUNCH_CHECK();
-    k_seg_sum<NV><<<unsigned((S + 3) / 4), kBlock, 0, c->stream>>>(S, cs.chunk_off, cs.cps, part, out);
+    const int64_t nsum = L.on ? L.cap[kClassNonTiny] : S;
+    const unsigned gs = unsigned(L.on ? ((nsum + 3) / 4 < 4096 ? (nsum + 3) / 4 : 4096) : (S + 3) / 4);
+    k_seg_sum<NV><<<gs > 0 ? gs : 1, kBlock, 0, c->stream>>>(S, cs.chunk_off, cs.cps, part, out,
+                                                         L.on ? L.ids[kClassNonTiny] : nullptr,
+                                                         L.on ? L.d_n + kClassNonTiny : nullptr);
     FZ_LAUNCH_CHECK();
 }
 

@@ -1,17 +1,96 @@
 // Segmented series operations (fz_seg.h): chunk maps, segmented sort, tie ranks, Spearman vs
 // index, Shapiro-Wilk, percentiles, means, medians.
 #include "fz_seg.h"
+#include "fz_segsort.h"
 #include "fz_stats.h"
 
 namespace fz {
 
 // ------------------------------------------------------------------------------ chunk maps
-__global__ __launch_bounds__(kBlock) void k_chunk_count(const int64_t *__restrict__ offs, int64_t S,
+// chunks per segment; segments of <= min_len values get none (they are reduced elsewhere)
+__global__ __launch_bounds__(kBlock) void k_chunk_count(const int64_t *__restrict__ offs, int64_t S, int64_t min_len,
                                                         int64_t *__restrict__ cnt) {
     for (int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x; s < S; s += int64_t(gridDim.x) * kBlock) {
         const int64_t len = offs[s + 1] - offs[s];
-        cnt[s] = (len + kChunk - 1) / kChunk;
+        cnt[s] = len > min_len ? (len + kChunk - 1) / kChunk : 0;
     }
+}
+
+// Size-class lists (fz_seg.h SegLists).  Each workgroup owns a contiguous range of segments: it
+// counts its classes (pass 1), reserves its slice of every list with one atomic per class, then
+// writes the ids in order (pass 2) - a few thousand atomics in all instead of one per wave.
+__device__ inline int seg_class(int64_t len) {
+    return len <= kMicroSeg ? -1
+           : len <= kTinySeg ? kClassTiny
+           : len <= 1024 ? kClassMid
+           : len <= kLdsSortMax ? kClassWide : kClassBig;
+}
+__device__ inline bool in_class(int cls, int k) { return k == kClassNonTiny ? cls > kClassTiny : cls == k; }
+
+__global__ __launch_bounds__(kBlock) void k_seg_classes(const int64_t *__restrict__ offs, int64_t S, SegLists L) {
+    __shared__ unsigned long long s_run[kNumClasses];
+    __shared__ unsigned s_wave[4][kNumClasses];
+    const int tid = threadIdx.x, w = wave_id();
+    const int64_t per = (S + gridDim.x - 1) / gridDim.x;
+    const int64_t s0 = int64_t(blockIdx.x) * per, s1 = s0 + per < S ? s0 + per : S;
+    if (tid < kNumClasses) s_run[tid] = 0;
+    __syncthreads();
+    unsigned cnt[kNumClasses] = {};
+    for (int64_t s = s0 + tid; s < s1; s += kBlock) {
+        const int cls = seg_class(offs[s + 1] - offs[s]);
+#pragma unroll
+        for (int k = 0; k < kNumClasses; ++k) cnt[k] += in_class(cls, k);
+    }
+#pragma unroll
+    for (int k = 0; k < kNumClasses; ++k) {
+        const unsigned v = wave_sum(cnt[k]);
+        if (lane_id() == 0 && v) atomicAdd(&s_run[k], (unsigned long long)v);
+    }
+    __syncthreads();
+    if (tid < kNumClasses && s_run[tid])
+        s_run[tid] = atomicAdd(reinterpret_cast<unsigned long long *>(L.d_n + tid), s_run[tid]);
+    __syncthreads();
+    for (int64_t base = s0; base < s1; base += kBlock) {
+        const int64_t s = base + tid;
+        const int cls = s < s1 ? seg_class(offs[s + 1] - offs[s]) : -1;
+        uint64_t m[kNumClasses];
+#pragma unroll
+        for (int k = 0; k < kNumClasses; ++k) {
+            m[k] = __ballot(in_class(cls, k));
+            if (lane_id() == 0) s_wave[w][k] = unsigned(__popcll(m[k]));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kNumClasses; ++k) {
+            if (!in_class(cls, k)) continue;
+            unsigned before = 0;
+            for (int v = 0; v < w; ++v) before += s_wave[v][k];
+            L.ids[k][s_run[k] + before + unsigned(__popcll(m[k] & lanemask_lt()))] = int32_t(s);
+        }
+        __syncthreads();
+        if (tid < kNumClasses) s_run[tid] += s_wave[0][tid] + s_wave[1][tid] + s_wave[2][tid] + s_wave[3][tid];
+        __syncthreads();
+    }
+}
+
+SegLists seg_lists(fz_ctx *c, const Segs &sg) {
+    SegLists L;
+    L.on = true;
+    const int64_t S = sg.S, n = sg.n_cap;
+    auto bound = [&](int64_t minlen) { return (S < n / (minlen + 1) + 1 ? S : n / (minlen + 1) + 1); };
+    L.cap[kClassTiny] = bound(kMicroSeg);
+    L.cap[kClassMid] = bound(kTinySeg);
+    L.cap[kClassWide] = bound(1024);
+    L.cap[kClassBig] = bound(kLdsSortMax);
+    L.cap[kClassNonTiny] = bound(kTinySeg);
+    L.d_n = c->arena.get<int64_t>(kNumClasses);
+    for (int k = 0; k < kNumClasses; ++k) L.ids[k] = c->arena.get<int32_t>(L.cap[k]);
+    FZ_HIP(hipMemsetAsync(L.d_n, 0, kNumClasses * 8, c->stream));
+    if (S > 0) {
+        k_seg_classes<<<grid_for(S, kBlock, 2048), kBlock, 0, c->stream>>>(sg.offs, S, L);
+        FZ_LAUNCH_CHECK();
+    }
+    return L;
 }
 
 __global__ __launch_bounds__(kBlock) void k_chunk_fill(const int64_t *__restrict__ offs, int64_t S,
@@ -32,14 +111,18 @@ ChunkedSegs chunked(fz_ctx *c, const Segs &sg) {
     cs.sg = sg;
     // Short segments: implicit chunks (no map kernels) while the grid stays near the explicit
     // one - an empty chunk's workgroup exits after two offset loads.
+    // (Very many segments: tiny ones are reduced one per thread, an explicit map covers the others.)
+    const bool many = sg.S > kManySegs;
     const int64_t cps = sg.len_bound() > kChunk ? (sg.len_bound() + kChunk - 1) / kChunk : 1;
     const int64_t explicit_cap = sg.S + sg.n_cap / kChunk + 1;
-    if (sg.S > 0 && (cps == 1 || sg.S * cps <= 2 * explicit_cap + 4096) && sg.S * cps < (int64_t(1) << 31)) {
+    if (sg.S > 0 && !many && (cps == 1 || sg.S * cps <= 2 * explicit_cap + 4096) && sg.S * cps < (int64_t(1) << 31)) {
         cs.cps = cps;
         return cs;
     }
     ChunkMap &cm = cs.cm;
-    cm.cap = sg.S + sg.n_cap / kChunk + 1;
+    if (many) cs.lists = seg_lists(c, sg);
+    const int64_t nontiny = sg.S < sg.n_cap / (kTinySeg + 1) + 1 ? sg.S : sg.n_cap / (kTinySeg + 1) + 1;
+    cm.cap = (many ? nontiny : sg.S) + sg.n_cap / kChunk + 1;
     cm.d_n = c->arena.get<int64_t>(1);
     cm.seg = c->arena.get<int32_t>(cm.cap);
     cm.begin = c->arena.get<int64_t>(cm.cap);
@@ -48,7 +131,7 @@ ChunkedSegs chunked(fz_ctx *c, const Segs &sg) {
     int64_t *cnt = c->arena.get<int64_t>(sg.S + 1);
     FZ_HIP(hipMemsetAsync(cnt, 0, size_t(sg.S + 1) * 8, c->stream));
     if (sg.S > 0) {
-        k_chunk_count<<<grid_for(sg.S), kBlock, 0, c->stream>>>(sg.offs, sg.S, cnt);
+        k_chunk_count<<<grid_for(sg.S), kBlock, 0, c->stream>>>(sg.offs, sg.S, many ? kTinySeg : -1, cnt);
         FZ_LAUNCH_CHECK();
     }
     scan_exclusive_i64(c, cnt, cs.chunk_off, sg.S + 1, cm.d_n);
@@ -92,12 +175,15 @@ constexpr int kLdsSortBlock = FZ_SL_BLOCK;  // threads of the 1025..4096-value c
 template <int BS, int MAXN>
 __global__ __launch_bounds__(BS) void k_seg_sort_lds(const double *__restrict__ src, const int64_t *__restrict__ offs,
                                                      int64_t S, double *__restrict__ out_val,
-                                                     int32_t *__restrict__ out_pos, uint64_t *__restrict__ out_key) {
+                                                     int32_t *__restrict__ out_pos, uint64_t *__restrict__ out_key,
+                                                     const int32_t *__restrict__ list, const int64_t *__restrict__ d_ln) {
     __shared__ uint64_t sk[MAXN];
     __shared__ int32_t sp[MAXN];
     constexpr int kMinN = MAXN / 4;
     const int tid = threadIdx.x;
-    for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
+    const int64_t ns = list ? *d_ln : S;
+    for (int64_t w = blockIdx.x; w < ns; w += gridDim.x) {
+        const int64_t s = list ? list[w] : w;
         const int64_t b = offs[s];
         const int n = int(offs[s + 1] - b);
         if (n <= 0 || n > MAXN || (MAXN == kLdsSortMax && n <= kMinN)) continue;
@@ -136,12 +222,103 @@ __global__ __launch_bounds__(BS) void k_seg_sort_lds(const double *__restrict__ 
     }
 }
 
-// Every segment of <= kLdsSortMax values (len_bound: a host bound of the longest one).
+// Every segment of <= kMicroSeg values: one thread each, Batcher's 19-comparator network on
+// (key, position) pairs in registers.
+__device__ inline void ce_kv(uint64_t &ka, uint32_t &pa, uint64_t &kb, uint32_t &pb) {
+    if (kb < ka || (kb == ka && pb < pa)) {
+        const uint64_t tk = ka;
+        const uint32_t tp = pa;
+        ka = kb;
+        pa = pb;
+        kb = tk;
+        pb = tp;
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_seg_sort_micro(const double *__restrict__ src,
+                                                           const int64_t *__restrict__ offs, int64_t S,
+                                                           double *__restrict__ out_val, int32_t *__restrict__ out_pos) {
+    for (int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x; s < S; s += int64_t(gridDim.x) * kBlock) {
+        const int64_t b = offs[s];
+        const int n = int(offs[s + 1] - b);
+        if (n > kMicroSeg || n <= 0) continue;
+        uint64_t k[kMicroSeg];
+        uint32_t p[kMicroSeg];
+#pragma unroll
+        for (int q = 0; q < kMicroSeg; ++q) {
+            k[q] = q < n ? f64_key(src[b + q]) : ~0ull;
+            p[q] = uint32_t(q);
+        }
+        constexpr int net[19][2] = {{0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 2}, {1, 3}, {4, 6}, {5, 7}, {1, 2}, {5, 6},
+                                    {0, 4}, {1, 5}, {2, 6}, {3, 7}, {2, 4}, {3, 5}, {1, 2}, {3, 4}, {5, 6}};
+#pragma unroll
+        for (int c = 0; c < 19; ++c) ce_kv(k[net[c][0]], p[net[c][0]], k[net[c][1]], p[net[c][1]]);
+#pragma unroll
+        for (int q = 0; q < kMicroSeg; ++q) {
+            if (q < n) {
+                if (out_val) out_val[b + q] = f64_from_key(k[q]);
+                if (out_pos) out_pos[b + q] = int32_t(b + p[q]);
+            }
+        }
+    }
+}
+
+// Segments of kMicroSeg < len <= kTinySeg values from a list: one wave each, a 64-lane bitonic
+// network on (key, position) in registers (ties by position: deterministic).
+__global__ __launch_bounds__(kBlock) void k_seg_sort_wave(const double *__restrict__ src,
+                                                          const int64_t *__restrict__ offs,
+                                                          const int32_t *__restrict__ list,
+                                                          const int64_t *__restrict__ d_ln, double *__restrict__ out_val,
+                                                          int32_t *__restrict__ out_pos) {
+    const int64_t ns = *d_ln;
+    const int lane = lane_id();
+    for (int64_t w = int64_t(blockIdx.x) * 4 + wave_id(); w < ns; w += int64_t(gridDim.x) * 4) {
+        const int64_t s = list[w], b = offs[s];
+        const int n = int(offs[s + 1] - b);
+        unsigned long long k = lane < n ? f64_key(src[b + lane]) : ~0ull;
+        unsigned p = unsigned(lane);
+#pragma unroll
+        for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+            for (int j = kk >> 1; j > 0; j >>= 1) {
+                const unsigned long long ok = __shfl_xor(k, j, 64);
+                const unsigned op = __shfl_xor(p, j, 64);
+                const bool other_less = ok < k || (ok == k && op < p);
+                const bool want_min = ((lane & j) == 0) == ((lane & kk) == 0);
+                if (want_min == other_less) {
+                    k = ok;
+                    p = op;
+                }
+            }
+        }
+        if (lane < n) {
+            if (out_val) out_val[b + lane] = f64_from_key(k);
+            if (out_pos) out_pos[b + lane] = int32_t(b + p);
+        }
+    }
+}
+
+// Every segment of <= kLdsSortMax values (len_bound: a host bound of the longest one); with lists,
+// each kernel walks its own size class only.
 static void launch_seg_sort_lds(fz_ctx *c, unsigned g, const double *src, const int64_t *offs, int64_t S,
-                                int64_t len_bound, double *val, int32_t *pos, uint64_t *key) {
-    k_seg_sort_lds<256, 1024><<<g, 256, 0, c->stream>>>(src, offs, S, val, pos, key);
+                                int64_t len_bound, double *val, int32_t *pos, uint64_t *key,
+                                const SegLists *L = nullptr) {
+    if (L && L->on) {
+        auto grid = [](int64_t cap, int64_t lim) { return unsigned(cap < 1 ? 1 : (cap < lim ? cap : lim)); };
+        k_seg_sort_micro<<<grid_for(S, kBlock, 8192), kBlock, 0, c->stream>>>(src, offs, S, val, pos);
+        k_seg_sort_wave<<<grid((L->cap[kClassTiny] + 3) / 4, 8192), kBlock, 0, c->stream>>>(
+            src, offs, L->ids[kClassTiny], L->d_n + kClassTiny, val, pos);
+        k_seg_sort_lds<256, 1024><<<grid(L->cap[kClassMid], 8192), 256, 0, c->stream>>>(
+            src, offs, S, val, pos, key, L->ids[kClassMid], L->d_n + kClassMid);
+        if (len_bound > 1024)
+            k_seg_sort_lds<kLdsSortBlock, kLdsSortMax><<<grid(L->cap[kClassWide], 8192), kLdsSortBlock, 0, c->stream>>>(
+                src, offs, S, val, pos, key, L->ids[kClassWide], L->d_n + kClassWide);
+        FZ_LAUNCH_CHECK();
+        return;
+    }
+    k_seg_sort_lds<256, 1024><<<g, 256, 0, c->stream>>>(src, offs, S, val, pos, key, nullptr, nullptr);
     if (len_bound > 1024)
-        k_seg_sort_lds<kLdsSortBlock, kLdsSortMax><<<g, kLdsSortBlock, 0, c->stream>>>(src, offs, S, val, pos, key);
+        k_seg_sort_lds<kLdsSortBlock, kLdsSortMax><<<g, kLdsSortBlock, 0, c->stream>>>(src, offs, S, val, pos, key,
+                                                                                        nullptr, nullptr);
     FZ_LAUNCH_CHECK();
 }
 
@@ -153,43 +330,35 @@ uint64_t *sort_small_keys(fz_ctx *c, const double *x, int64_t nmax, const int64_
     return k;
 }
 
-SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int32_t *segid) {
+struct F64Key {
+    const double *src;
+    __device__ uint64_t operator()(int64_t i) const { return f64_key(src[i]); }
+};
+struct F64Sink {
+    double *val;
+    int32_t *pos;
+    __device__ void operator()(int32_t, int64_t q, uint64_t k, uint32_t v) const {
+        val[q] = f64_from_key(k);
+        pos[q] = int32_t(v);
+    }
+};
+
+SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int32_t *) {
     const int64_t n = sg.n_cap;
     SortedSegs out;
     out.val = c->arena.get<double>(n);
     out.pos = c->arena.get<int32_t>(n);
-    if (n <= 0) return out;
-    if (sg.len_bound() <= kLdsSortMax) {
-        const unsigned g = unsigned(sg.S < 8192 ? (sg.S > 0 ? sg.S : 1) : 8192);
-        launch_seg_sort_lds(c, g, src, sg.offs, sg.S, sg.len_bound(), out.val, out.pos, nullptr);
-        return out;
-    }
-    uint64_t *keys = c->arena.get<uint64_t>(n);
-    uint32_t *vals = reinterpret_cast<uint32_t *>(out.pos);
-    const int64_t *offs = sg.offs;
-    const int64_t S = sg.S;
-    // stage 1: by value (elements past the live count sort last)
-    map_n(c, n, nullptr, [=] __device__(int64_t i) {
-        const int64_t live = offs[S];
-        keys[i] = i < live ? f64_key(src[i]) : ~0ull;
-        vals[i] = uint32_t(i);
-    });
-    radix_sort_pairs_swap(c, keys, vals, n, 64);
-    // stage 2: by segment, stable (one segment: already in place)
-    if (S > 1) {
-        map_n(c, n, nullptr, [=] __device__(int64_t i) {
-            const int64_t live = offs[S];
-            const uint32_t j = vals[i];
-            keys[i] = int64_t(j) < live ? uint64_t(segid[j]) : uint64_t(S);
-        });
-        radix_sort_pairs_swap(c, keys, vals, n, bits_for(uint64_t(S)));
-    }
-    out.pos = reinterpret_cast<int32_t *>(vals);
-    double *ov = out.val;
-    map_n(c, n, nullptr, [=] __device__(int64_t i) {
-        const int64_t live = offs[S];
-        ov[i] = i < live ? src[vals[i]] : 0.0;
-    });
+    if (n <= 0 || sg.S <= 0) return out;
+    const unsigned g = unsigned(sg.S < 8192 ? sg.S : 8192);
+    // segments of <= kLdsSortMax values: one workgroup each (LDS bitonic; one wave for tiny ones
+    // when there are very many segments); longer ones: the segmented merge sort (fz_segsort.h),
+    // which touches only their rows
+    SegLists L;
+    if (sg.S > kManySegs) L = seg_lists(c, sg);
+    launch_seg_sort_lds(c, g, src, sg.offs, sg.S, sg.len_bound() < kLdsSortMax ? sg.len_bound() : kLdsSortMax,
+                        out.val, out.pos, nullptr, &L);
+    if (sg.len_bound() > kLdsSortMax)
+        sort_big_segments(c, sg.offs, sg.S, n, sg.len_bound(), nullptr, F64Key{src}, F64Sink{out.val, out.pos});
     return out;
 }
 

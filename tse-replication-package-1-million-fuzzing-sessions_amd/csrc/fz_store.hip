@@ -1,12 +1,14 @@
 // The columnar store: replaces the PostgreSQL tables + (project, time) indexes every RQ query
 // scans through dbFile.DB.executeQuery (program/__module/dbFile.py:16-24).
 //
-// fz_store_build sorts each table once with the stable LSD radix sort (fz_prims.hip) on a packed
-// key (build_type | project | time - tmin), NULL timestamps mapped past the maximum so they sort
-// last within their project (PostgreSQL's ASC NULLS LAST).  When the packed key would exceed
-// 64 bits the sort runs in two stable stages (time, then prefix) - LSD order makes that exact.
+// fz_store_build sorts each table once: stable LSD radix passes (fz_prims.hip) on the prefix
+// ([build_type |] project) group the rows by segment in row order, then every segment is sorted by
+// time - in one workgroup (LDS) when it has <= 4096 rows, through the segmented merge sort
+// (fz_segsort.h) otherwise - with NULL timestamps last (PostgreSQL's ASC NULLS LAST) and equal
+// times in row order.  The same kernels gather the tables' columns into the sorted order.
 #include "fz_device.h"
 #include "fz_internal.h"
+#include "fz_segsort.h"
 #include "fz_views.h"
 
 namespace fz {
@@ -25,62 +27,6 @@ struct Prefix {
     }
 };
 
-__global__ __launch_bounds__(kBlock) void k_keys_full(Prefix pre, const int64_t *__restrict__ time, int64_t n,
-                                                      int64_t tmin, uint64_t tnull, int tbits,
-                                                      uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        const int64_t t = time[i];
-        const uint64_t tn = t == FZ_TS_NULL ? tnull : uint64_t(t - tmin);
-        keys[i] = (tbits < 64 ? (pre(i) << tbits) : 0ull) | tn;
-        vals[i] = uint32_t(i);
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_keys_time(const int64_t *__restrict__ time, int64_t n, int64_t tmin,
-                                                      uint64_t tnull, uint64_t *__restrict__ keys,
-                                                      uint32_t *__restrict__ vals) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        const int64_t t = time[i];
-        keys[i] = t == FZ_TS_NULL ? tnull : uint64_t(t - tmin);
-        vals[i] = uint32_t(i);
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_keys_prefix(Prefix pre, const uint32_t *__restrict__ vals, int64_t n,
-                                                        uint64_t *__restrict__ keys) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
-        keys[i] = pre(vals[i]);
-}
-
-__global__ __launch_bounds__(kBlock) void k_gather_sorted(const uint32_t *__restrict__ vals,
-                                                          const int64_t *__restrict__ time,
-                                                          const uint32_t *__restrict__ proj, int64_t n,
-                                                          int32_t *__restrict__ orow, int64_t *__restrict__ otime,
-                                                          uint32_t *__restrict__ oproj) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        const uint32_t r = vals[i];
-        orow[i] = int32_t(r);
-        otime[i] = time[r];
-        oproj[i] = proj[r];
-    }
-}
-
-// Single-stage sorts carry (project, time) in the key: unpack instead of gathering by row id.
-__global__ __launch_bounds__(kBlock) void k_unpack_sorted(const uint64_t *__restrict__ keys,
-                                                          const uint32_t *__restrict__ vals, int64_t n, int tbits,
-                                                          int64_t tmin, uint64_t tnull, uint64_t pmask,
-                                                          int32_t *__restrict__ orow, int64_t *__restrict__ otime,
-                                                          uint32_t *__restrict__ oproj) {
-    const uint64_t tmask = tbits >= 64 ? ~0ull : ((1ull << tbits) - 1ull);
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        const uint64_t k = keys[i];
-        const uint64_t tn = k & tmask;
-        orow[i] = int32_t(vals[i]);
-        otime[i] = tn == tnull ? FZ_TS_NULL : int64_t(tn) + tmin;
-        oproj[i] = tbits >= 64 ? 0u : uint32_t((k >> tbits) & pmask);
-    }
-}
-
 __global__ __launch_bounds__(kBlock) void k_count_types(const uint8_t *__restrict__ type, int64_t n,
                                                         unsigned long long *__restrict__ cnt) {
     __shared__ int64_t s_tmp[4];
@@ -98,11 +44,11 @@ __global__ __launch_bounds__(kBlock) void k_count_types(const uint8_t *__restric
 }
 
 
-// One workgroup: the longest segment of each of 4 views (out[0..3]) and a copy of the 3
-// long-segment counters (out[4..6]) - one launch and one D2H copy for the host's store stats.
+// One workgroup: the longest segment of each of 4 views (out[0..3]) and a copy of the 6
+// merge-sort counters (out[4..9]) - one launch and one D2H copy for the host's store stats.
 struct Offs4 {
     const int64_t *offs[4];
-    const unsigned long long *big[3];
+    const unsigned long long *big;  // [6] merge-sort rows / longest segment per table
 };
 __global__ __launch_bounds__(kSortBlock) void k_store_stats(Offs4 v, int64_t P, int64_t *__restrict__ out) {
     __shared__ int64_t s_m[kSortBlock / kWave];
@@ -122,7 +68,7 @@ __global__ __launch_bounds__(kSortBlock) void k_store_stats(Offs4 v, int64_t P, 
         }
         __syncthreads();
     }
-    if (threadIdx.x < 3) out[4 + threadIdx.x] = int64_t(*v.big[threadIdx.x]);
+    if (threadIdx.x < 6) out[4 + threadIdx.x] = int64_t(v.big[threadIdx.x]);
 }
 
 // ---- fast path: prefix LSD (2 passes) + per-segment LDS sort by (time, row) -----------------
@@ -184,7 +130,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict
                                                       const int64_t *__restrict__ offs, int64_t S, uint32_t pmask,
                                                       int32_t *__restrict__ orow, int64_t *__restrict__ otime,
                                                       uint32_t *__restrict__ oproj, unsigned long long *__restrict__ big,
-                                                      GatherCols gc) {
+                                                      uint8_t *__restrict__ bigflag, GatherCols gc) {
     static_assert(MAXN <= (1 << kTsPosBits), "positions must fit the key");
     __shared__ uint64_t sk[MAXN];
     __shared__ int64_t s_lo[BS / kWave], s_hi[BS / kWave];
@@ -195,7 +141,11 @@ __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict
         const int64_t len = offs[s + 1] - b;
         if (len <= 0) continue;
         if (len > MAXN) {
-            if (tid == 0) atomicAdd(big, (unsigned long long)len);
+            if (tid == 0) {
+                atomicAdd(big, (unsigned long long)len);
+                atomicMax(big + 3, (unsigned long long)len);
+                bigflag[s] = 1;
+            }
             continue;
         }
         const int n = int(len);
@@ -225,7 +175,11 @@ __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict
             hi = s_hi[w] > hi ? s_hi[w] : hi;
         }
         if (hi >= lo && uint64_t(hi) - uint64_t(lo) >= kTsTop) {  // span too wide for the key
-            if (tid == 0) atomicAdd(big, (unsigned long long)len);
+            if (tid == 0) {
+                atomicAdd(big, (unsigned long long)len);
+                atomicMax(big + 3, (unsigned long long)len);
+                bigflag[s] = 1;
+            }
             __syncthreads();
             continue;
         }
@@ -276,14 +230,22 @@ __global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict
 }
 
 // Sorts by (prefix, time, row); adds to the (zeroed) device counter *big the rows in segments too
-// long for LDS (non-zero -> the caller re-sorts with sort_table()).
+// long for LDS (and big[3] = the longest such segment, bigflag[s] = 1): the caller sorts those
+// through the segmented merge sort.
 // nonempty_bound: host upper bound on the number of non-empty segments (picks the workgroup size).
 constexpr int kTimeSortSmallBlock = 256;
 constexpr int kTimeSortSmallMean = 256;  // mean rows per segment at or below which it is used
-static void sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time, int32_t *orow,
-                            int64_t *otime, uint32_t *oproj, const GatherCols &gc, unsigned long long *big,
-                            int64_t nonempty_bound) {
-    if (n <= 0) return;
+struct PrefixSorted {
+    int64_t S = 0;
+    const int64_t *offs = nullptr;   // [S + 1] segment offsets of the prefix-sorted rows
+    const uint32_t *rows = nullptr;  // row ids in (prefix, row) order
+    uint8_t *bigflag = nullptr;      // [S] 1: the segment is left to the merge sort
+};
+static PrefixSorted sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time,
+                                    int32_t *orow, int64_t *otime, uint32_t *oproj, const GatherCols &gc,
+                                    unsigned long long *big, int64_t nonempty_bound) {
+    PrefixSorted ps;
+    if (n <= 0) return ps;
     uint64_t *keys = c->arena.get<uint64_t>(n);
     uint32_t *vals = c->arena.get<uint32_t>(n);
     const unsigned g = grid_for(n, kBlock, 4096);
@@ -294,6 +256,12 @@ static void sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, c
     int64_t *offs = c->arena.get<int64_t>(S + 1);
     k_prefix_offsets<<<grid_for(n > S + 1 ? n : S + 1, kBlock, 4096), kBlock, 0, c->stream>>>(keys, n, S, offs);
     FZ_LAUNCH_CHECK();
+    uint8_t *bigflag = c->arena.get<uint8_t>(S);
+    FZ_HIP(hipMemsetAsync(bigflag, 0, size_t(S), c->stream));
+    ps.S = S;
+    ps.offs = offs;
+    ps.rows = vals;
+    ps.bigflag = bigflag;
     const uint32_t pmask = pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << pre.pbits) - 1ull);
     {
         ProbeScope ps(c, "seg_time_sort", 28.0 * double(n));  // row 4 + gathered time 8 + out 16 B
@@ -302,44 +270,47 @@ static void sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, c
             // short segments on average (issues: ~65 rows per project): 256-thread workgroups, five
             // per CU by LDS instead of two, so the whole table sorts in one round of the grid
             k_seg_time_sort<kTimeSortSmallBlock, kSegSortMax><<<g, kTimeSortSmallBlock, 0, c->stream>>>(
-                vals, time, offs, S, pmask, orow, otime, oproj, big, gc);
+                vals, time, offs, S, pmask, orow, otime, oproj, big, bigflag, gc);
         } else {
-            k_seg_time_sort<kTimeSortBlock, kSegSortMax><<<g, kTimeSortBlock, 0, c->stream>>>(vals, time, offs, S, pmask,
-                                                                                        orow, otime, oproj, big, gc);
+            k_seg_time_sort<kTimeSortBlock, kSegSortMax><<<g, kTimeSortBlock, 0, c->stream>>>(
+                vals, time, offs, S, pmask, orow, otime, oproj, big, bigflag, gc);
         }
         FZ_LAUNCH_CHECK();
     }
+    return ps;
 }
 
-// Sort one table into (row, time, proj) buffers.
-static void sort_table(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time, int64_t tmin,
-                       int64_t tmax, int32_t *orow, int64_t *otime, uint32_t *oproj) {
-    if (n <= 0) return;
-    const uint64_t range = tmax >= tmin ? uint64_t(tmax - tmin) : 0ull;
-    const uint64_t tnull = range + 1;  // NULLs after every real time
-    const int tbits = bits_for(tnull);
-    uint64_t *keys = c->arena.get<uint64_t>(n);
-    uint32_t *vals = c->arena.get<uint32_t>(n);
-    const unsigned g = grid_for(n, kBlock, 4096);
-    if (prefix_bits + tbits <= 64) {
-        k_keys_full<<<g, kBlock, 0, c->stream>>>(pre, time, n, tmin, tnull, tbits, keys, vals);
-        FZ_LAUNCH_CHECK();
-        radix_sort_pairs_swap(c, keys, vals, n, prefix_bits + tbits);
-        const uint64_t pmask = pre.pbits >= 32 ? 0xffffffffull : ((1ull << pre.pbits) - 1ull);
-        k_unpack_sorted<<<g, kBlock, 0, c->stream>>>(keys, vals, n, tbits, tmin, tnull, pmask, orow, otime, oproj);
-        FZ_LAUNCH_CHECK();
-        return;
-    } else {
-        k_keys_time<<<g, kBlock, 0, c->stream>>>(time, n, tmin, tnull, keys, vals);
-        FZ_LAUNCH_CHECK();
-        radix_sort_pairs_swap(c, keys, vals, n, tbits);
-        k_keys_prefix<<<g, kBlock, 0, c->stream>>>(pre, vals, n, keys);
-        FZ_LAUNCH_CHECK();
-        radix_sort_pairs_swap(c, keys, vals, n, prefix_bits);
+// The merge-sort path of the store: key = signed time as an order-preserving u64 (NULL =
+// INT64_MAX -> ~0: last), stable by row; the sink writes what k_seg_time_sort writes for a short
+// segment (time, project, row = position, perm = source row, gathered columns).
+struct StoreTimeKey {
+    const int64_t *time;
+    const uint32_t *rows;
+    __device__ uint64_t operator()(int64_t i) const { return uint64_t(time[rows[i]]) ^ (uint64_t(1) << 63); }
+};
+struct StoreSink {
+    const uint32_t *rows;
+    uint32_t pmask;
+    int32_t *orow;
+    int64_t *otime;
+    uint32_t *oproj;
+    GatherCols gc;
+    __device__ void operator()(int32_t s, int64_t q, uint64_t k, uint32_t v) const {
+        const int32_t r = int32_t(rows[v]);
+        otime[q] = int64_t(k ^ (uint64_t(1) << 63));
+        oproj[q] = uint32_t(s) & pmask;
+        gc.perm[q] = r;
+        orow[q] = int32_t(q);
+        for (int j = 0; j < gc.n; ++j) {
+            if (gc.size[j] == 8)
+                static_cast<uint64_t *>(gc.dst[j])[q] = static_cast<const uint64_t *>(gc.src[j])[r];
+            else if (gc.size[j] == 4)
+                static_cast<uint32_t *>(gc.dst[j])[q] = static_cast<const uint32_t *>(gc.src[j])[r];
+            else
+                static_cast<uint8_t *>(gc.dst[j])[q] = static_cast<const uint8_t *>(gc.src[j])[r];
+        }
     }
-    k_gather_sorted<<<g, kBlock, 0, c->stream>>>(vals, time, pre.proj, n, orow, otime, oproj);
-    FZ_LAUNCH_CHECK();
-}
+};
 
 static View make_view(fz_ctx *c, const int32_t *row, const int64_t *time, const uint32_t *proj, int64_t n, int64_t P,
                       DevBuf &offbuf) {
@@ -356,72 +327,12 @@ static View make_view(fz_ctx *c, const int32_t *row, const int64_t *time, const 
 
 void store_eligibility(fz_ctx *c);  // fz_rq1.hip
 
-// Gather every column into its table's sorted order (row ids become positions; perm keeps the
-// caller's ids) and point s.t at the sorted copies.
-__global__ __launch_bounds__(kBlock) void k_sorted_builds(fz_tables t, int64_t n, int32_t *__restrict__ row,
-                                                          int32_t *__restrict__ perm, uint8_t *__restrict__ type,
-                                                          uint8_t *__restrict__ result, int32_t *__restrict__ group,
-                                                          int32_t *__restrict__ canon) {
-    for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < n; k += int64_t(gridDim.x) * kBlock) {
-        const int32_t r = row[k];
-        perm[k] = r;
-        row[k] = int32_t(k);
-        type[k] = t.b_type[r];
-        result[k] = t.b_result[r];
-        group[k] = t.b_group[r];
-        canon[k] = t.b_rev_canon[r];
-    }
-}
-__global__ __launch_bounds__(kBlock) void k_sorted_coverage(fz_tables t, int64_t n, int32_t *__restrict__ row,
-                                                            int32_t *__restrict__ perm, double *__restrict__ cov,
-                                                            int64_t *__restrict__ covered, int64_t *__restrict__ total,
-                                                            uint8_t *__restrict__ valid) {
-    for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < n; k += int64_t(gridDim.x) * kBlock) {
-        const int32_t r = row[k];
-        perm[k] = r;
-        row[k] = int32_t(k);
-        cov[k] = t.c_coverage[r];
-        covered[k] = t.c_covered[r];
-        total[k] = t.c_total[r];
-        valid[k] = t.c_valid[r];
-    }
-}
-__global__ __launch_bounds__(kBlock) void k_sorted_issues(fz_tables t, int64_t n, int32_t *__restrict__ row,
-                                                          int32_t *__restrict__ perm, int64_t *__restrict__ number,
-                                                          uint8_t *__restrict__ status) {
-    for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < n; k += int64_t(gridDim.x) * kBlock) {
-        const int32_t r = row[k];
-        perm[k] = r;
-        row[k] = int32_t(k);
-        number[k] = t.i_number[r];
-        status[k] = t.i_status[r];
-    }
-}
-
-// gather[k]: table k (builds, coverage, issues) still needs its columns gathered (it was re-sorted
-// on the full-key path; the time sort gathered the others)
-static void materialize_sorted(fz_ctx *c, const fz_tables &in, const bool gather[3]) {
+// Point s.t at the sorted copies of every column (row ids become positions; perm keeps the
+// caller's ids).
+static void materialize_sorted(fz_ctx *c) {
     Store &s = c->store;
-    const int64_t nb = in.n_builds, nc = in.n_cov, ni = in.n_issues;
+    const int64_t nb = s.t.n_builds, nc = s.t.n_cov, ni = s.t.n_issues;
     fz_tables &t = s.t;
-    if (nb > 0 && gather[0]) {
-        k_sorted_builds<<<grid_for(nb, kBlock, 4096), kBlock, 0, c->stream>>>(
-            in, nb, s.b_row.as<int32_t>(), s.b_perm.ensure<int32_t>(nb), s.sb_type.ensure<uint8_t>(nb),
-            s.sb_result.ensure<uint8_t>(nb), s.sb_group.ensure<int32_t>(nb), s.sb_canon.ensure<int32_t>(nb));
-        FZ_LAUNCH_CHECK();
-    }
-    if (nc > 0 && gather[1]) {
-        k_sorted_coverage<<<grid_for(nc, kBlock, 4096), kBlock, 0, c->stream>>>(
-            in, nc, s.c_row.as<int32_t>(), s.c_perm.ensure<int32_t>(nc), s.sc_coverage.ensure<double>(nc),
-            s.sc_covered.ensure<int64_t>(nc), s.sc_total.ensure<int64_t>(nc), s.sc_valid.ensure<uint8_t>(nc));
-        FZ_LAUNCH_CHECK();
-    }
-    if (ni > 0 && gather[2]) {
-        k_sorted_issues<<<grid_for(ni, kBlock, 4096), kBlock, 0, c->stream>>>(
-            in, ni, s.i_row.as<int32_t>(), s.i_perm.ensure<int32_t>(ni), s.si_number.ensure<int64_t>(ni),
-            s.si_status.ensure<uint8_t>(ni));
-        FZ_LAUNCH_CHECK();
-    }
     s.bperm = s.b_perm.ensure<int32_t>(nb);
     s.cperm = s.c_perm.ensure<int32_t>(nc);
     s.iperm = s.i_perm.ensure<int32_t>(ni);
@@ -456,10 +367,10 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     const int64_t P = s.P;
     const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
 
-    // one host round trip: time ranges of the three tables + build-type counts
-    int64_t mm[8];
-    const int64_t *cols[4] = {t->b_time, t->c_date, t->i_rts, t->i_number};
-    const int64_t ns[4] = {t->n_builds, t->n_cov, t->n_issues, t->n_issues};
+    // one host round trip: the issue-number range (RQ1's ROW_NUMBER dedup key) + build-type counts
+    int64_t mm[2];
+    const int64_t *cols[1] = {t->i_number};
+    const int64_t ns[1] = {t->n_issues};
     store_eligibility(c);
     unsigned long long *tcnt = c->arena.get<unsigned long long>(2);
     FZ_HIP(hipMemsetAsync(tcnt, 0, 16, c->stream));
@@ -467,16 +378,12 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         k_count_types<<<grid_for(t->n_builds, kBlock * 8, 512), kBlock, 0, c->stream>>>(t->b_type, t->n_builds, tcnt);
         FZ_LAUNCH_CHECK();
     }
-    minmax_i64_to_host(c, cols, ns, 4, mm);  // syncs the stream
-    s.num_min = mm[6];
-    s.num_max = mm[7];
+    minmax_i64_to_host(c, cols, ns, 1, mm);  // syncs the stream
+    s.num_min = mm[0];
+    s.num_max = mm[1];
     unsigned long long hcnt[2];
     FZ_HIP(hipMemcpy(hcnt, tcnt, 16, hipMemcpyDeviceToHost));
     const int64_t n_fuzz = int64_t(hcnt[0]), n_covb = int64_t(hcnt[1]);
-    for (int i = 0; i < 3; ++i) {
-        s.tmin[i] = mm[2 * i];
-        s.tmax[i] = mm[2 * i + 1];
-    }
 
     // the three tables: (prefix = [type|]project) LSD passes, then each segment sorted by time in LDS
     struct Tab {
@@ -484,14 +391,13 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         Prefix pre;
         int pbits_total;
         const int64_t *time;
-        int64_t tmin, tmax;
         DevBuf *row, *tm, *pr;
     };
     Tab tabs[3] = {
-        {t->n_builds, Prefix{t->b_project, t->b_type, pbits}, pbits + 2, t->b_time, mm[0], mm[1], &s.b_row, &s.b_time,
+        {t->n_builds, Prefix{t->b_project, t->b_type, pbits}, pbits + 2, t->b_time, &s.b_row, &s.b_time,
          &s.b_proj},
-        {t->n_cov, Prefix{t->c_project, nullptr, pbits}, pbits, t->c_date, mm[2], mm[3], &s.c_row, &s.c_time, &s.c_proj},
-        {t->n_issues, Prefix{t->i_project, nullptr, pbits}, pbits, t->i_rts, mm[4], mm[5], &s.i_row, &s.i_time,
+        {t->n_cov, Prefix{t->c_project, nullptr, pbits}, pbits, t->c_date, &s.c_row, &s.c_time, &s.c_proj},
+        {t->n_issues, Prefix{t->i_project, nullptr, pbits}, pbits, t->i_rts, &s.i_row, &s.i_time,
          &s.i_proj},
     };
     GatherCols gcs[3];
@@ -517,16 +423,17 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         gi.src[0] = t->i_number, gi.dst[0] = s.si_number.ensure<int64_t>(ni), gi.size[0] = 8;
         gi.src[1] = t->i_status, gi.dst[1] = s.si_status.ensure<uint8_t>(ni), gi.size[1] = 1;
     }
-    unsigned long long *big[3];
-    unsigned long long *big3 = c->arena.get<unsigned long long>(3);
-    FZ_HIP(hipMemsetAsync(big3, 0, 3 * 8, c->stream));  // one zeroing for the three tables' counters
+    // big3[k]: rows of table k in segments left to the merge sort, big3[3 + k]: the longest such
+    // segment (one zeroing for all six counters)
+    unsigned long long *big3 = c->arena.get<unsigned long long>(6);
+    FZ_HIP(hipMemsetAsync(big3, 0, 6 * 8, c->stream));
+    PrefixSorted pss[3];
     for (int k = 0; k < 3; ++k) {
         Tab &b = tabs[k];
-        big[k] = big3 + k;
         // non-empty segments: at most one per project (and build type: 2 prefix bits for builds)
         const int64_t segs = int64_t(P > 0 ? P : 1) * (k == 0 ? 4 : 1);
-        sort_table_fast(c, b.n, b.pre, b.pbits_total, b.time, b.row->ensure<int32_t>(b.n), b.tm->ensure<int64_t>(b.n),
-                        b.pr->ensure<uint32_t>(b.n), gcs[k], big[k], segs);
+        pss[k] = sort_table_fast(c, b.n, b.pre, b.pbits_total, b.time, b.row->ensure<int32_t>(b.n),
+                                 b.tm->ensure<int64_t>(b.n), b.pr->ensure<uint32_t>(b.n), gcs[k], big3 + k, segs);
     }
     auto make_views = [&]() {
         int32_t *row = s.b_row.as<int32_t>();
@@ -539,33 +446,38 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         s.issues = make_view(c, s.i_row.as<int32_t>(), s.i_time.as<int64_t>(), s.i_proj.as<uint32_t>(), t->n_issues,
                              P, s.off_iss);
     };
-    make_views();
-    // longest segments (sizes the per-iteration outputs) + rows left for the full-key path
-    int64_t *mx = c->arena.get<int64_t>(8);
+    // longest segments (sizes the per-iteration outputs) + the merge-sort counters
+    int64_t *mx = c->arena.get<int64_t>(10);
     auto read_stats = [&]() {
-        Offs4 v{{s.fuzz.offs, s.covb.offs, s.cov.offs, s.issues.offs}, {big[0], big[1], big[2]}};
+        Offs4 v{{s.fuzz.offs, s.covb.offs, s.cov.offs, s.issues.offs}, big3};
         k_store_stats<<<1, kSortBlock, 0, c->stream>>>(v, P, mx);
         FZ_LAUNCH_CHECK();
-        FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 7 * 8, hipMemcpyDeviceToHost, c->stream));
+        FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 10 * 8, hipMemcpyDeviceToHost, c->stream));
         sync(c);
     };
+    // segments the LDS time sort left (longer than 4096 rows, or a time span too wide for its
+    // packed key): segmented merge sort of those rows only, writing the same outputs
+    make_views();
     read_stats();
+    const int64_t bigrows[3] = {c->h_pinned[4], c->h_pinned[5], c->h_pinned[6]};
+    const int64_t bigmax[3] = {c->h_pinned[7], c->h_pinned[8], c->h_pinned[9]};
     bool redo = false;
-    bool gather[3] = {false, false, false};
     for (int k = 0; k < 3; ++k) {
-        if (c->h_pinned[4 + k] == 0) continue;  // every segment fit in LDS (columns gathered)
-        gather[k] = true;
+        if (bigrows[k] == 0) continue;
         Tab &b = tabs[k];
-        sort_table(c, b.n, b.pre, b.pbits_total, b.time, b.tmin, b.tmax, b.row->as<int32_t>(), b.tm->as<int64_t>(),
-                   b.pr->as<uint32_t>());
-        FZ_HIP(hipMemsetAsync(big[k], 0, 8, c->stream));
+        const PrefixSorted &ps = pss[k];
+        const uint32_t pmask = b.pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << b.pre.pbits) - 1ull);
+        ProbeScope probe(c, "seg_merge_sort", 36.0 * double(bigrows[k]));
+        sort_big_segments(c, ps.offs, ps.S, b.n, bigmax[k], ps.bigflag, StoreTimeKey{b.time, ps.rows},
+                          StoreSink{ps.rows, pmask, b.row->as<int32_t>(), b.tm->as<int64_t>(), b.pr->as<uint32_t>(),
+                                    gcs[k]});
         redo = true;
     }
-    if (redo) {
+    if (redo) {  // the merged segments' projects are written now
         make_views();
         read_stats();
     }
-    materialize_sorted(c, *t, gather);
+    materialize_sorted(c);
     s.fuzz.max_seg = c->h_pinned[0];
     s.covb.max_seg = c->h_pinned[1];
     s.cov.max_seg = c->h_pinned[2];

@@ -10,6 +10,8 @@
 #include "fz_internal.h"
 #include "fz_lookback.h"
 
+#include <type_traits>
+
 namespace fz {
 
 // A view whose buffers live in the arena (valid for one public call).
@@ -101,6 +103,16 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
     }
 }
 
+// Algorithmic bytes the predicate reads per row (Pred::kBytes when it declares them).
+template <class P, class = void>
+struct PredBytes {
+    static constexpr double value = 0.0;
+};
+template <class P>
+struct PredBytes<P, std::void_t<decltype(P::kBytes)>> {
+    static constexpr double value = double(P::kBytes);
+};
+
 // Rows of src (n rows, in view order; only the first *src_live when given) satisfying pred(row)
 // -> dst (same order).
 template <typename Pred>
@@ -115,6 +127,9 @@ void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uin
     if (n > 0) {
         const int64_t ntiles = (n + kFcTile - 1) / kFcTile;
         const Lookback lb = lookback_begin(c, ntiles);
+        // per input row: its row id 4 B + the predicate's columns; per kept row: time 8 + project 4
+        // read, (row, time, project) 16 written
+        ProbeScope ps(c, "filter_compact", double(n) * (4.0 + PredBytes<Pred>::value), dst.d_n, 28.0);
         k_filter_compact<Pred><<<unsigned(ntiles), kBlock, 0, c->stream>>>(rows, times, proj, n, src_live, pred, lb,
                                                                           ntiles, dst.row, dst.time, dst.proj,
                                                                           dst.d_n);

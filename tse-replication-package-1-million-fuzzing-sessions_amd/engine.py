@@ -155,6 +155,7 @@ SIGNATURES = {
     "fz_two_sample_tests": (C.c_int, [_P, _P, _I64, _P, _I64, _P]),
     "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),
     "fz_probe_end": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "fz_probe_get": (C.c_int, [_P, C.c_char_p, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "fz_radix_sort_u64": (C.c_int, [_P, _P, _P, _I64, C.c_int]),
     "fz_describe_f64": (C.c_int, [_P, _P, _I64, C.POINTER(FzDescribe)]),
     "fz_eligibility_count": (C.c_int, [_P, C.POINTER(FzTables), _I64, _P]),
@@ -212,10 +213,6 @@ class DeviceTables:
         return self.host.n_rows
 
 
-def _pin(t):
-    return t.pin_memory() if t.numel() > 0 else t
-
-
 class Engine:
     """One engine per GPU: a ``fz_ctx`` bound to torch's current stream on ``device``."""
 
@@ -243,39 +240,90 @@ class Engine:
             pass
 
     # ---- columnar loader: host columns -> HBM -------------------------------------------------
+    _TORCH_DT = {np.dtype(np.int64): "int64", np.dtype(np.int32): "int32", np.dtype(np.uint8): "uint8",
+                 np.dtype(np.float64): "float64"}
+
     def upload(self, t: Tables) -> DeviceTables:
-        """Stream the typed columns to HBM (pinned host staging, async copies on our stream)."""
+        """Stream the typed columns to HBM: every column is copied (host memcpy) into ONE reusable
+        pinned staging buffer at a 256-byte aligned offset, then ONE async H2D copy on the engine
+        stream moves the whole image into a device buffer whose typed slices are the columns.  The
+        dictionary encodings (group key, canonical revisions, corpus columns) come from the table's
+        cache (persisted by store.save_columnar), so a re-upload does no per-row Python work.
+        ``self.upload_ms`` = {"host": staging memcpy, "h2d": the copy's device time}."""
+        import time as _time
         torch = self.torch
+        h0 = _time.perf_counter()
         P = len(t.projects)
         c_valid = (t.c_coverage_valid.astype(np.uint8) * VALID_COVERAGE
                    | t.c_covered_valid.astype(np.uint8) * VALID_COVERED
                    | t.c_total_valid.astype(np.uint8) * VALID_TOTAL)
         pi_count = np.bincount(t.pi_project.astype(np.int64), minlength=P).astype(np.int32)
+        from .rq.common import corpus_columns
+        member, corpus_us, order = corpus_columns(t)
         host = {
             "b_project": t.b_project.view(np.int32), "b_type": t.b_type, "b_result": t.b_result,
-            "b_time": t.b_time, "b_group": t.group_key().astype(np.int32),
-            "b_rev_canon": t.rev_canon().astype(np.int32),
+            "b_time": t.b_time, "b_group": t.group_key(), "b_rev_canon": t.rev_canon(),
             "c_project": t.c_project.view(np.int32), "c_date": t.c_date, "c_coverage": t.c_coverage,
             "c_covered": t.c_covered, "c_total": t.c_total, "c_valid": c_valid,
             "i_number": t.i_number, "i_project": t.i_project.view(np.int32), "i_rts": t.i_rts,
             "i_status": t.i_status, "pi_count": pi_count,
+            "g_member": member, "g_corpus_us": corpus_us, "g_order": order,
         }
-        from .rq.common import corpus_columns
-        member, corpus_us, order = corpus_columns(t)
-        host.update({"g_member": member, "g_corpus_us": corpus_us, "g_order": order})
-        cols = {}
+        layout, total = {}, 0
+        for k, a in host.items():
+            nbytes = int(a.size) * a.dtype.itemsize
+            layout[k] = (total, int(a.size), a.dtype)
+            total += (nbytes + 255) // 256 * 256 or 256
+        stage = self._staging(total)
+        sn = stage.numpy()
+        for k, a in host.items():
+            off, n, dt = layout[k]
+            if n:
+                sn[off:off + n * dt.itemsize] = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
+        h1 = _time.perf_counter()
+        dbuf = torch.empty(total, dtype=torch.uint8, device=self.dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(self.stream):
-            for k, a in host.items():
-                h = _pin(torch.from_numpy(np.ascontiguousarray(a)))
-                cols[k] = h.to(self.dev, non_blocking=True)
-        ptr = {k: _P(v.data_ptr()) for k, v in cols.items() if not k.startswith("g_")}
+            e0.record(self.stream)
+            dbuf.copy_(stage[:total], non_blocking=True)
+            e1.record(self.stream)
+        self._stage_event = e1  # the staging buffer is reused only after this copy has finished
+        cols = {}
+        for k, (off, n, dt) in layout.items():
+            tdt = getattr(torch, self._TORCH_DT[np.dtype(dt)])
+            cols[k] = dbuf[off:off + max(n, 1) * dt.itemsize].view(tdt)
+        cols["_image"] = dbuf
+        ptr = {k: _P(v.data_ptr()) for k, v in cols.items() if not k.startswith(("g_", "_"))}
         fz = FzTables(n_projects=P, n_builds=len(t.b_project), n_cov=len(t.c_project), n_issues=len(t.i_project),
                       **ptr)
         self.tables = DeviceTables(host=t, cols=cols, fz=fz)
         self.groups = FzRq4Groups(member=_P(cols["g_member"].data_ptr()),
                                   corpus_us=_P(cols["g_corpus_us"].data_ptr()),
                                   order=_P(cols["g_order"].data_ptr()), n_order=len(order))
+        self._upload_events = (e0, e1)
+        self._upload_host_ms = (h1 - h0) * 1e3
+        self._upload_bytes = total
         return self.tables
+
+    def upload_timing(self):
+        """After an upload has completed: {"host_ms": staging memcpy + encode lookups, "h2d_ms":
+        device time of the copy, "bytes": image size, "h2d_gbs": its PCIe rate}."""
+        e0, e1 = self._upload_events
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        return {"host_ms": round(self._upload_host_ms, 3), "h2d_ms": round(ms, 3), "bytes": self._upload_bytes,
+                "h2d_gbs": round(self._upload_bytes / (ms * 1e-3) / 1e9, 2) if ms > 0 else None}
+
+    def _staging(self, nbytes):
+        """The pinned host staging buffer (grown, never shrunk; waits for the last copy out of it)."""
+        ev = getattr(self, "_stage_event", None)
+        if ev is not None:
+            ev.synchronize()
+        st = getattr(self, "_stage", None)
+        if st is None or st.numel() < nbytes:
+            st = self.torch.empty(max(nbytes, 1), dtype=self.torch.uint8, pin_memory=True)
+            self._stage = st
+        return st
 
     # ---- store ---------------------------------------------------------------------------------
     def build_store(self, dt: Optional[DeviceTables] = None) -> FzStoreStats:
@@ -310,6 +358,12 @@ class Engine:
         """-> (launches, total device ms, algorithmic bytes) of the probed kernel."""
         n, ms, b = _I64(), C.c_double(), C.c_double()
         _check(self.lib, self.lib.fz_probe_end(self.ctx, C.byref(n), C.byref(ms), C.byref(b)))
+        return int(n.value), float(ms.value), float(b.value)
+
+    def probe_get(self, kernel: str):
+        """After probe_end: (launches, total device ms, algorithmic bytes) of any probed kernel."""
+        n, ms, b = _I64(), C.c_double(), C.c_double()
+        _check(self.lib, self.lib.fz_probe_get(self.ctx, kernel.encode(), C.byref(n), C.byref(ms), C.byref(b)))
         return int(n.value), float(ms.value), float(b.value)
 
     def describe(self, x):

@@ -77,6 +77,11 @@ def corpus_groups(t: Tables, eligible, add_missing_to_g1: bool):
 
 
 def corpus_columns(t: Tables):
+    """Cached per table (see ``Tables.cached``): the columns of ``_corpus_columns``."""
+    return t.cached("corpus_columns", (t.projects, t.corpus_csv), lambda: _corpus_columns(t))
+
+
+def _corpus_columns(t: Tables):
     """Loader of project_corpus_analysis.csv for the GPU path (fz_rq4_groups in include/fz.h).
 
     Eligibility-independent per-project columns, so the device can apply the eligible set itself:

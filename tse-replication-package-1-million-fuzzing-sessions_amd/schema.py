@@ -110,6 +110,18 @@ class Tables:
     statuses: List[str] = field(default_factory=lambda: list(STATUSES))
     # RQ4 corpus CSV, verbatim text (parsed by the RQ4 host code exactly as pandas does)
     corpus_csv: str = ""
+    # derived encodings (group_key / rev_canon / corpus columns), computed once per table and
+    # persisted by store.save_columnar; each entry is keyed by the identity of the inputs it was
+    # derived from, so a table rebuilt around new arrays (a shard, a renamed copy) recomputes
+    derived: dict = field(default_factory=dict, compare=False, repr=False)
+
+    def cached(self, name, inputs, make):
+        hit = self.derived.get(name)
+        if hit is not None and len(hit[0]) == len(inputs) and all(a is b for a, b in zip(hit[0], inputs)):
+            return hit[1]
+        value = make()
+        self.derived[name] = (tuple(inputs), value)  # holds the inputs: identity stays meaningful
+        return value
 
     @property
     def n_rows(self) -> int:
@@ -118,6 +130,9 @@ class Tables:
 
     def rev_canon(self) -> np.ndarray:
         """Per-build id of ``sorted(rev[1:-2].split(','))`` (rq3:280); -1 for NULL."""
+        return self.cached("rev_canon", (self.b_revisions, self.revisions_pool), self._rev_canon)
+
+    def _rev_canon(self) -> np.ndarray:
         canon_of_pool = np.full(len(self.revisions_pool), -1, dtype=np.int32)
         seen = {}
         for k, s in enumerate(self.revisions_pool):
@@ -128,10 +143,14 @@ class Tables:
         out = np.full(len(self.b_revisions), -1, dtype=np.int32)
         ok = self.b_revisions >= 0
         out[ok] = canon_of_pool[self.b_revisions[ok]]
-        return out
+        return out.astype(np.int32)
 
     def group_key(self) -> np.ndarray:
         """Per-build id of ``str(modules) + '_' + str(revisions)`` (rq2_coverage_and_added.py:129)."""
+        return self.cached("group_key", (self.b_modules, self.b_revisions, self.modules_pool, self.revisions_pool),
+                           self._group_key)
+
+    def _group_key(self) -> np.ndarray:
         m = np.where(self.b_modules >= 0, self.b_modules, len(self.modules_pool)).astype(np.int64)
         r = np.where(self.b_revisions >= 0, self.b_revisions, len(self.revisions_pool)).astype(np.int64)
         # the key is the concatenated TEXT: str(None) == 'None', and 'a_b'+'_'+'c' == 'a'+'_'+'b_c'
@@ -144,4 +163,4 @@ class Tables:
         for k, pv in enumerate(upair.tolist()):
             s = str(mp[pv // (len(rp) + 1)]) + "_" + str(rp[pv % (len(rp) + 1)])
             ids[k] = text_id.setdefault(s, len(text_id))
-        return ids[inv.reshape(-1)]
+        return ids[inv.reshape(-1)].astype(np.int32)

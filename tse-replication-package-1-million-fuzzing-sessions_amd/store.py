@@ -35,10 +35,15 @@ _NUMERIC = ["b_project", "b_type", "b_result", "b_time", "b_modules", "b_revisio
             "pi_project", "pi_first_commit"]
 
 
+_DERIVED = {"b_group": Tables.group_key, "b_rev_canon": Tables.rev_canon}  # persisted encodings
+
+
 def save_columnar(t: Tables, path: str) -> None:
     os.makedirs(path, exist_ok=True)
     for name in _NUMERIC:
         np.save(os.path.join(path, name + ".npy"), np.ascontiguousarray(getattr(t, name)), allow_pickle=False)
+    for name, fn in _DERIVED.items():  # the loader's dictionary encodings, computed once here
+        np.save(os.path.join(path, name + ".npy"), np.ascontiguousarray(fn(t)), allow_pickle=False)
     meta = {"projects": t.projects, "modules_pool": t.modules_pool, "revisions_pool": t.revisions_pool,
             "b_name": [None if x is None else str(x) for x in t.b_name.tolist()],
             "build_types": t.build_types, "results": t.results, "statuses": t.statuses,
@@ -54,24 +59,38 @@ def load_columnar(path: str, mmap: bool = True) -> Tables:
             for name in _NUMERIC}
     names = np.empty(len(meta["b_name"]), dtype=object)
     names[:] = meta["b_name"]
-    return Tables(projects=meta["projects"], modules_pool=meta["modules_pool"],
-                  revisions_pool=meta["revisions_pool"], b_name=names, build_types=meta["build_types"],
-                  results=meta["results"], statuses=meta["statuses"], corpus_csv=meta["corpus_csv"],
-                  **{k: np.asarray(v) for k, v in cols.items()})
+    t = Tables(projects=meta["projects"], modules_pool=meta["modules_pool"],
+               revisions_pool=meta["revisions_pool"], b_name=names, build_types=meta["build_types"],
+               results=meta["results"], statuses=meta["statuses"], corpus_csv=meta["corpus_csv"],
+               **{k: np.asarray(v) for k, v in cols.items()})
+    keys = {"b_group": ("group_key", (t.b_modules, t.b_revisions, t.modules_pool, t.revisions_pool)),
+            "b_rev_canon": ("rev_canon", (t.b_revisions, t.revisions_pool))}
+    for name, (entry, inputs) in keys.items():  # persisted encodings (older directories: computed on use)
+        f = os.path.join(path, name + ".npy")
+        if os.path.exists(f):
+            t.derived[entry] = (tuple(inputs), np.load(f, mmap_mode="r" if mmap else None, allow_pickle=False))
+    return t
 
 
 # ---------------------------------------------------------------------------------- CSV ingest
+# a UTC offset after the time of day ('+00', '+02', '-05:30') as a timestamptz column dumps it
+_TZ_SUFFIX = re.compile(r"^(.*\d{2}:\d{2}(?::\d{2}(?:\.\d+)?)?)[+-]\d{2}(?::?\d{2})?$")
+
+
 def _ts(series) -> np.ndarray:
-    """Naive timestamps (text) -> int64 microseconds; NULL -> TS_NULL."""
+    """Timestamps (text) -> int64 microseconds of the printed wall-clock time; NULL -> TS_NULL.
+
+    The analyses compare naive values (the reference's columns are `timestamp without time zone`,
+    SURVEY.md 8(c)); a timestamptz dump prints each value with the server's offset, which differs
+    between rows under daylight saving ('+01' / '+02'), so the offset is dropped before parsing."""
     import pandas as pd
-    dt = pd.to_datetime(series, errors="coerce", format="mixed")
+    text = series.astype(object).where(series.notna(), None)
+    text = text.map(lambda x: _TZ_SUFFIX.sub(r"\1", x) if isinstance(x, str) else x)
+    dt = pd.to_datetime(text, errors="coerce", format="mixed")
     out = np.full(len(series), TS_NULL, dtype=np.int64)
     ok = dt.notna().to_numpy()
     if ok.any():
-        v = dt[ok]
-        if getattr(v.dt, "tz", None) is not None:
-            v = v.dt.tz_localize(None)
-        out[ok] = v.astype("datetime64[us]").astype(np.int64).to_numpy()
+        out[ok] = dt[ok].astype("datetime64[us]").astype(np.int64).to_numpy()
     return out
 
 
@@ -115,8 +134,9 @@ def _nullable_int(series):
     return out, ok
 
 
-def from_csv_dir(path: str, corpus_csv: Optional[str] = None) -> Tables:
-    """Ingest PostgreSQL CSV exports (see module docstring) into columnar ``Tables``."""
+def from_csv_dir(path: str, corpus_csv: Optional[str] = None, project_order=None) -> Tables:
+    """Ingest PostgreSQL CSV exports (see module docstring) into columnar ``Tables``.
+    ``project_order``: see ``_from_frames``."""
     import pandas as pd
     rd = lambda name: pd.read_csv(os.path.join(path, name + ".csv"), dtype=str, keep_default_na=False,  # noqa: E731
                                   na_values=[""])
@@ -124,17 +144,33 @@ def from_csv_dir(path: str, corpus_csv: Optional[str] = None) -> Tables:
     if corpus_csv is None:
         cp = os.path.join(path, "project_corpus_analysis.csv")
         corpus_csv = open(cp).read() if os.path.exists(cp) else ""
-    return _from_frames(rd("buildlog_data"), rd("total_coverage"), rd("issues"), pi, corpus_csv)
+    return _from_frames(rd("buildlog_data"), rd("total_coverage"), rd("issues"), pi, corpus_csv, project_order)
 
 
-def _from_frames(b, c, i, pi, corpus_csv: str) -> Tables:
+def _from_frames(b, c, i, pi, corpus_csv: str, project_order=None) -> Tables:
     """Text frames (one ``str``/NULL cell per value) -> columnar ``Tables``; shared by the CSV-export
-    and the pg_dump ingest."""
+    and the pg_dump ingest.
+
+    Project ids follow ``ORDER BY project`` (the order of every per-project CSV row, and which project
+    RQ3 treats as the last one, rq3:245-257).  Default: byte order, i.e. PostgreSQL under the C
+    collation (and SQLite's BINARY).  A database with a locale collation (e.g. en_US.UTF-8 orders
+    '-', '_' and case differently) is matched by passing ``project_order``: either the list of
+    project names in the server's order (e.g. ``SELECT DISTINCT project ... ORDER BY project``) or
+    a sort-key function over names (e.g. ``locale.strxfrm``)."""
     import pandas as pd
     names = set(b["project"].dropna()) | set(c["project"].dropna()) | set(i["project"].dropna())
     if pi is not None:
         names |= set(pi["project"].dropna())
-    projects = sorted(names, key=lambda s: s.encode())  # byte order == ORDER BY under C collation
+    if project_order is None:
+        projects = sorted(names, key=lambda s: s.encode())  # byte order == ORDER BY under C collation
+    elif callable(project_order):
+        projects = sorted(names, key=project_order)
+    else:
+        rank = {n: k for k, n in enumerate(project_order)}
+        missing = names - set(rank)
+        if missing:
+            raise ValueError(f"project_order misses {len(missing)} project(s), e.g. {sorted(missing)[:3]}")
+        projects = sorted(names, key=rank.__getitem__)
     pid = {n: k for k, n in enumerate(projects)}
     enc = lambda s: np.array([pid[x] for x in s.tolist()], dtype=np.uint32)  # noqa: E731
     build_types, results, statuses = list(BUILD_TYPES), list(RESULTS), list(STATUSES)
@@ -240,11 +276,12 @@ def _copy_escape(v) -> str:
             .replace("\b", "\\b").replace("\f", "\\f").replace("\v", "\\v"))
 
 
-def from_pg_dump(path: str, corpus_csv: Optional[str] = None) -> Tables:
+def from_pg_dump(path: str, corpus_csv: Optional[str] = None, project_order=None) -> Tables:
     """Ingest a plain-format ``pg_dump`` file (see above) into columnar ``Tables``.
 
     ``corpus_csv``: text of ``project_corpus_analysis.csv`` (``rq4a_bug.py:34``); default: that
-    file next to the dump or under ``../processed_data/csv/`` as in the reference's data layout."""
+    file next to the dump or under ``../processed_data/csv/`` as in the reference's data layout.
+    ``project_order``: see ``_from_frames`` (the database's collation)."""
     import pandas as pd
     blocks: Dict[str, List[str]] = {}
     cols: Dict[str, List[str]] = {}
@@ -303,7 +340,8 @@ def from_pg_dump(path: str, corpus_csv: Optional[str] = None) -> Tables:
                 break
         else:
             corpus_csv = ""
-    return _from_frames(frame("buildlog_data"), frame("total_coverage"), frame("issues"), pi, corpus_csv)
+    return _from_frames(frame("buildlog_data"), frame("total_coverage"), frame("issues"), pi, corpus_csv,
+                        project_order)
 
 
 def to_pg_dump(t: Tables, path: str) -> None:
