@@ -259,6 +259,21 @@ void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int 
 // The same without the copy back: on return keys / vals point at the sorted data (the inputs or
 // arena scratch of the current call).
 void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits);
+// Columns that travel with the keys through every pass (each pass records every input position's
+// destination and moves the columns there): on return out[j] holds column j in sorted order.
+constexpr int kMaxPayload = 6;
+struct RadixPayload {
+    int n = 0;
+    const void *in[kMaxPayload] = {};
+    void *out[kMaxPayload] = {};
+    int size[kMaxPayload] = {};  // bytes per element: 1, 4 or 8
+    double bytes() const {
+        double b = 0.0;
+        for (int j = 0; j < n; ++j) b += size[j];
+        return b;
+    }
+};
+void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl);
 // min/max over int64 values skipping FZ_TS_NULL: writes {min, max} to host array.
 void minmax_i64_to_host(fz_ctx *c, const int64_t *const *cols, const int64_t *ns, int ncols,
                         int64_t *host_minmax);

@@ -361,7 +361,30 @@ extern "C" int fz_debug_os_timing(unsigned long long *out) {
 #define OS_STAMP(ph) do {} while (0)
 #endif
 
-template <bool HAS_VALS>
+// One payload column of a radix pass (HAS_PL): the tile's values staged in LDS at their keys'
+// digit-sorted slots, then written out in the same per-digit runs as the keys (coalesced).
+template <typename T>
+__device__ inline void onesweep_move(const T *__restrict__ in, T *__restrict__ out, T *s, const uint16_t *lpos,
+                                     const int32_t *gp, int64_t wbase, int lane, int64_t n, int64_t valid_n, int tid) {
+    T x[kSortItems];
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+        const int64_t idx = wbase + r * kWave + lane;
+        x[r] = idx < n ? in[idx] : T(0);
+    }
+    __syncthreads();  // the previous column (or the keys) has left the LDS
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r)
+        if (wbase + r * kWave + lane < n) s[lpos[r]] = x[r];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < kSortItems; ++m) {
+        const int i = tid + m * kOsBlock;
+        if (i < valid_n) out[gp[m]] = s[i];
+    }
+}
+
+template <bool HAS_VALS, bool HAS_PL>
 __global__ __launch_bounds__(kOsBlock) void k_onesweep(const uint64_t *__restrict__ keys_in,
                                                      const uint32_t *__restrict__ vals_in,
                                                      uint64_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
@@ -369,7 +392,8 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const uint64_t *__restric
                                                      uint64_t *__restrict__ status, unsigned int *__restrict__ ticket,
                                                      unsigned int ticket_base, uint64_t epoch,
                                                      unsigned long long *__restrict__ gsum,
-                                                     unsigned long long *__restrict__ next_hist) {
+                                                     unsigned long long *__restrict__ next_hist,
+                                                     RadixPayload pl) {
     __shared__ uint64_t s_keys[kSortTile];
     __shared__ uint32_t s_vals[HAS_VALS ? kSortTile : 1];
     __shared__ uint32_t s_run[kRadix];
@@ -507,28 +531,51 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const uint64_t *__restric
     }
     OS_STAMP(3);
     // stage the tile digit-sorted in LDS, then write it out in per-digit runs
+    uint16_t lpos[HAS_PL ? kSortItems : 1];  // HAS_PL: LDS slot of item r
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
-        if (wbase + r * kWave + lane < n) {
+        const int64_t idx = wbase + r * kWave + lane;
+        if (idx < n) {
             const uint32_t d = uint32_t(k[r] >> shift) & (kRadix - 1);
             const uint32_t pos = s_start[d] + cnt_w[d] + rank[r];
             s_keys[pos] = k[r];
             if (HAS_VALS) s_vals[pos] = v[r];
+            if (HAS_PL) lpos[r] = uint16_t(pos);
         }
     }
     __syncthreads();
     OS_STAMP(4);
     const int64_t valid_n = (n - base) < kSortTile ? (n - base) : kSortTile;
-    for (int i = tid; i < valid_n; i += kOsBlock) {
-        const uint64_t kk = s_keys[i];
-        const uint32_t d = uint32_t(kk >> shift) & (kRadix - 1);
-        const int64_t gpos = s_goff[d] + i;
+    int32_t gp[HAS_PL ? kSortItems : 1];  // HAS_PL: output position of LDS slot tid + m * kOsBlock
+#pragma unroll
+    for (int m = 0; m < kSortItems; ++m) {
+        const int i = tid + m * kOsBlock;
+        if (i < valid_n) {
+            const uint64_t kk = s_keys[i];
+            const uint32_t d = uint32_t(kk >> shift) & (kRadix - 1);
+            const int64_t gpos = s_goff[d] + i;
 #ifdef FZ_OS_EXPERIMENT_NOWRITE
-        if (gpos < 0)
+            if (gpos < 0)
 #endif
-        {
-            keys_out[gpos] = kk;
-            if (HAS_VALS) vals_out[gpos] = s_vals[i];
+            {
+                keys_out[gpos] = kk;
+                if (HAS_VALS) vals_out[gpos] = s_vals[i];
+            }
+            if (HAS_PL) gp[m] = int32_t(gpos);
+        }
+    }
+    if (HAS_PL) {
+        // the payload columns follow their keys through the same LDS slots and per-digit runs
+        for (int j = 0; j < pl.n; ++j) {
+            if (pl.size[j] == 8)
+                onesweep_move<uint64_t>(static_cast<const uint64_t *>(pl.in[j]), static_cast<uint64_t *>(pl.out[j]),
+                                        s_keys, lpos, gp, wbase, lane, n, valid_n, tid);
+            else if (pl.size[j] == 4)
+                onesweep_move<uint32_t>(static_cast<const uint32_t *>(pl.in[j]), static_cast<uint32_t *>(pl.out[j]),
+                                        reinterpret_cast<uint32_t *>(s_keys), lpos, gp, wbase, lane, n, valid_n, tid);
+            else
+                onesweep_move<uint8_t>(static_cast<const uint8_t *>(pl.in[j]), static_cast<uint8_t *>(pl.out[j]),
+                                       reinterpret_cast<uint8_t *>(s_keys), lpos, gp, wbase, lane, n, valid_n, tid);
         }
     }
 #ifdef FZ_OS_TIMING
@@ -548,6 +595,11 @@ void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int 
 }
 
 void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits) {
+    RadixPayload none;
+    radix_sort_pairs_payload(c, keys, vals, n, bits, none);
+}
+
+void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl) {
     if (n <= 1 || bits <= 0) return;
     const int npass = (bits + kRadixBits - 1) / kRadixBits;
     const int64_t nb = (n + kSortTile - 1) / kSortTile;
@@ -590,32 +642,50 @@ void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t 
     uint32_t *v2 = vals ? c->arena.get<uint32_t>(n) : nullptr;
     uint64_t *ka = keys, *kb = k2;
     uint32_t *va = vals, *vb = v2;
+    FZ_CHECK(pl.n == 0 || n < (int64_t(1) << 31), "radix_sort_pairs_payload: payload sorts are limited to 2^31 keys");
+    void *pbuf[2][kMaxPayload] = {};
+    for (int j = 0; j < pl.n; ++j)  // two scratch copies per column: the passes ping-pong them
+        for (int b = 0; b < 2; ++b) pbuf[b][j] = c->arena.alloc(size_t(n) * size_t(pl.size[j]));
+    int ppass = 0;  // payload passes run: the current columns are pl.in (0) or pbuf[(ppass - 1) & 1]
     int passes = 0;
     for (int p = 0; p < npass; ++p) {
         if (!need[p]) continue;
         const Lookback lb = lookback_begin(c, nb * kRadix);  // (tile, digit) status words
+        RadixPayload step = pl;
+        for (int j = 0; j < pl.n; ++j) {
+            step.in[j] = ppass == 0 ? pl.in[j] : pbuf[(ppass - 1) & 1][j];
+            step.out[j] = pbuf[ppass & 1][j];
+        }
         {
-            // algorithmic traffic of one pass: read + write every key (8 B) and value (4 B)
-            ProbeScope ps(c, "radix_scatter", (vals ? 24.0 : 16.0) * double(n));
-            if (vals)
-                k_onesweep<true><<<unsigned(nb), kOsBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits,
-                                                                           ghist + p * kRadix, lb.status, lb.ticket,
-                                                                           lb.base, lb.epoch, gsum + p * gwords,
-                                                                           next_hist);
-            else
-                k_onesweep<false><<<unsigned(nb), kOsBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits,
-                                                                            ghist + p * kRadix, lb.status, lb.ticket,
-                                                                            lb.base, lb.epoch, gsum + p * gwords,
-                                                                            next_hist);
+            // algorithmic traffic of one pass: read + write every key (8 B), value (4 B) and payload
+            ProbeScope ps(c, "radix_scatter", ((vals ? 24.0 : 16.0) + 2.0 * pl.bytes()) * double(n));
+#define FZ_OS_LAUNCH(V, PL)                                                                                   \
+    k_onesweep<V, PL><<<unsigned(nb), kOsBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, \
+                                                             lb.status, lb.ticket, lb.base, lb.epoch, gsum + p * gwords, \
+                                                             next_hist, step)
+            if (pl.n > 0) {
+                if (vals)
+                    FZ_OS_LAUNCH(true, true);
+                else
+                    FZ_OS_LAUNCH(false, true);
+            } else if (vals) {
+                FZ_OS_LAUNCH(true, false);
+            } else {
+                FZ_OS_LAUNCH(false, false);
+            }
+#undef FZ_OS_LAUNCH
             FZ_LAUNCH_CHECK();
         }
         lookback_end(c, nb);
+        if (pl.n > 0) ++ppass;
         std::swap(ka, kb);
         std::swap(va, vb);
         ++passes;
     }
     keys = ka;  // the buffers holding the result (the inputs or arena scratch)
     vals = va;
+    for (int j = 0; j < pl.n; ++j)  // where each payload column ended (unmoved: the input itself)
+        pl.out[j] = ppass == 0 ? const_cast<void *>(pl.in[j]) : pbuf[(ppass - 1) & 1][j];
     c->store.passes += passes;
     // the passes zeroed the other buffer: it serves the next sort; with no pass nothing was zeroed
     c->os_hist_cur = passes > 0 ? 1 - c->os_hist_cur : -1;
@@ -663,17 +733,18 @@ __global__ __launch_bounds__(kBlock) void k_minmax(MinMaxCols cols, unsigned lon
 void minmax_i64_to_host(fz_ctx *c, const int64_t *const *cols, const int64_t *ns, int ncols, int64_t *host_minmax) {
     FZ_CHECK(ncols >= 1 && ncols <= kMinMaxCols, "minmax: 1..8 columns");
     unsigned long long *mm = c->arena.get<unsigned long long>(2 * ncols);
-    std::vector<unsigned long long> init(2 * ncols);
     MinMaxCols mc{};
     int64_t nmax = 0;
     for (int i = 0; i < ncols; ++i) {
-        init[2 * i] = ~0ull;
-        init[2 * i + 1] = 0ull;
         mc.x[i] = cols[i];
         mc.n[i] = ns[i] > 0 ? ns[i] : 0;
         nmax = mc.n[i] > nmax ? mc.n[i] : nmax;
     }
-    FZ_HIP(hipMemcpyAsync(mm, init.data(), init.size() * 8, hipMemcpyHostToDevice, c->stream));
+    // {min, max} start values through a kernel argument (no pageable host-to-device copy)
+    for (int i = 0; i < ncols; i += 2) {
+        const int64_t init[4] = {-1, 0, -1, 0};
+        set_i64(c, reinterpret_cast<int64_t *>(mm) + 2 * i, init, ncols - i >= 2 ? 4 : 2);
+    }
     if (nmax > 0) {  // one launch for every column
         const dim3 g(grid_for(nmax, kBlock * 8, 512), unsigned(ncols));
         k_minmax<<<g, kBlock, 0, c->stream>>>(mc, mm);

@@ -2,10 +2,11 @@
 // scans through dbFile.DB.executeQuery (program/__module/dbFile.py:16-24).
 //
 // fz_store_build sorts each table once: stable LSD radix passes (fz_prims.hip) on the prefix
-// ([build_type |] project) group the rows by segment in row order, then every segment is sorted by
-// time - in one workgroup (LDS) when it has <= 4096 rows, through the segmented merge sort
-// (fz_segsort.h) otherwise - with NULL timestamps last (PostgreSQL's ASC NULLS LAST) and equal
-// times in row order.  The same kernels gather the tables' columns into the sorted order.
+// ([build_type |] project) group the rows by segment in row order - moving the time column and
+// the other columns with the keys - then every segment is sorted by time in registers (one wave
+// for <= 1024 rows, one workgroup for <= 16384: fz_regsort.h), through the segmented merge sort
+// (fz_segsort.h) when longer, with NULL timestamps last (PostgreSQL's ASC NULLS LAST) and equal
+// times in row order.  One coalesced pass then gathers the tables' columns into sorted order.
 #include "fz_device.h"
 #include "fz_internal.h"
 #include "fz_segsort.h"
@@ -71,13 +72,7 @@ __global__ __launch_bounds__(kSortBlock) void k_store_stats(Offs4 v, int64_t P, 
     if (threadIdx.x < 6) out[4 + threadIdx.x] = int64_t(v.big[threadIdx.x]);
 }
 
-// ---- fast path: prefix LSD (2 passes) + per-segment LDS sort by (time, row) -----------------
-constexpr int kSegSortMax = 4096;
-#ifndef FZ_TS_BLOCK
-#define FZ_TS_BLOCK 1024
-#endif
-constexpr int kTimeSortBlock = FZ_TS_BLOCK;  // threads of the per-segment time sort
-
+// ---- prefix LSD passes (moving the columns) + per-segment register sort by (time, row) -------
 __global__ __launch_bounds__(kBlock) void k_keys_prefix_rows(Prefix pre, int64_t n, uint64_t *__restrict__ keys,
                                                              uint32_t *__restrict__ vals) {
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
@@ -104,16 +99,9 @@ __global__ __launch_bounds__(kBlock) void k_prefix_offsets(const uint64_t *__res
     }
 }
 
-// One workgroup per prefix segment, already in row order: bitonic sort in LDS of one packed u64 per
-// row, (time - segment min) << 12 | position (NULL times and the power-of-two pads get the top time
-// field): the position tie-break keeps equal times in row order (stable), and each compare-exchange
-// moves one word instead of a (time, position) pair.  Segments longer than MAXN rows, or whose
-// times span 2^52 us or more, are counted into *big (the host re-sorts that table on the full-key
-// path).  (Size-class variants - 256 / 512 / 1024 threads for <= 1024 / 2048 / 4096 rows - measured
-// slower in total: each class launch still walks every segment.)
-// Columns the time sort gathers into sorted order as it writes each segment (the materialisation
-// of the sorted store, fused: the random reads overlap other workgroups' sorting).  With perm set,
-// the kernel writes orow[k] = k (row id = sorted position) and perm[k] = the source row.
+// Columns the store materialises in sorted order (k_store_gather, after the sorts): perm[q] =
+// the caller's row id of sorted row q, orow[q] = q (row id = sorted position), dst[j][q] =
+// src[j][spos[q]] with src the prefix-sorted columns.
 constexpr int kMaxGather = 4;
 struct GatherCols {
     int n = 0;
@@ -121,137 +109,238 @@ struct GatherCols {
     void *dst[kMaxGather] = {};
     int size[kMaxGather] = {};  // bytes: 1, 4 or 8
     int32_t *perm = nullptr;
+    double bytes() const {
+        double b = 0.0;
+        for (int j = 0; j < n; ++j) b += size[j];
+        return b;
+    }
 };
 
-constexpr int kTsPosBits = 12;  // positions < 4096 = kSegSortMax
-constexpr uint64_t kTsTop = (uint64_t(1) << (64 - kTsPosBits)) - 1;  // time field of NULL / pad
-template <int BS, int MAXN>
-__global__ __launch_bounds__(BS) void k_seg_time_sort(const uint32_t *__restrict__ rows, const int64_t *__restrict__ time,
-                                                      const int64_t *__restrict__ offs, int64_t S, uint32_t pmask,
-                                                      int32_t *__restrict__ orow, int64_t *__restrict__ otime,
-                                                      uint32_t *__restrict__ oproj, unsigned long long *__restrict__ big,
-                                                      uint8_t *__restrict__ bigflag, GatherCols gc) {
-    static_assert(MAXN <= (1 << kTsPosBits), "positions must fit the key");
-    __shared__ uint64_t sk[MAXN];
-    __shared__ int64_t s_lo[BS / kWave], s_hi[BS / kWave];
-    const int tid = threadIdx.x;
+// What every time sort writes for sorted row q: its time (NULL restored), its project, and the
+// prefix-sorted position it came from (spos: the gather's index).
+struct TimeSortOut {
+    int64_t *otime;
+    uint32_t *oproj;
+    uint32_t *spos;
+    __device__ void put(int64_t q, int64_t t, uint32_t p, int64_t sp) const {
+        otime[q] = t;
+        oproj[q] = p;
+        spos[q] = uint32_t(sp);
+    }
+};
 
+__global__ __launch_bounds__(kBlock) void k_store_gather(const uint32_t *__restrict__ spos,
+                                                         const uint32_t *__restrict__ rows, int64_t n,
+                                                         int32_t *__restrict__ orow, GatherCols gc) {
+    for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < n; q += int64_t(gridDim.x) * kBlock) {
+        const int64_t sp = spos[q];
+        gc.perm[q] = int32_t(rows[sp]);
+        orow[q] = int32_t(q);
+        for (int j = 0; j < gc.n; ++j) {
+            if (gc.size[j] == 8)
+                static_cast<uint64_t *>(gc.dst[j])[q] = static_cast<const uint64_t *>(gc.src[j])[sp];
+            else if (gc.size[j] == 4)
+                static_cast<uint32_t *>(gc.dst[j])[q] = static_cast<const uint32_t *>(gc.src[j])[sp];
+            else
+                static_cast<uint8_t *>(gc.dst[j])[q] = static_cast<const uint8_t *>(gc.src[j])[sp];
+        }
+    }
+}
+
+// A segment the bucket sort cannot take (longer than its largest class, clustered times, or a time
+// span that does not fit its key) goes to the merge sort: counted in *big, flagged in bigflag.
+__device__ inline void flag_big(unsigned long long *big, uint8_t *bigflag, int64_t s, int64_t len) {
+    atomicAdd(big, (unsigned long long)len);
+    atomicMax(big + 3, (unsigned long long)len);
+    bigflag[s] = 1;
+}
+
+constexpr int kBlkPosBits = 14;  // key = time above the segment minimum << 14 | position
+constexpr uint64_t kBlkTop = (uint64_t(1) << (64 - kBlkPosBits)) - 1;  // time field of NULL rows
+
+// Bucket (distribution) sort of one segment per workgroup, for segments of min_len < rows <= MAXN:
+// n rows go to n + 1 buckets by time - the bucket of t is floor((t - min) * n / (span + 1)),
+// monotone in t, NULL times in the last bucket - counted with LDS atomics (the returned count is
+// the row's slot in its bucket), bucket starts by one block scan, and a row's final position is
+// its bucket start plus the number of rows of its bucket with a smaller key (time above the
+// minimum << 14 | position: unique, so equal times keep row order - stable).  O(n) work for
+// times spread over the segment's span (sessions: about one build per day); a segment whose
+// largest bucket holds more than kBucketSkew rows (clustered or NULL-heavy times), or whose span
+// does not fit the key, is flagged for the merge sort instead.  MAXN <= 4096 keeps the keys in LDS;
+// larger classes re-read them from the (prefix-sorted, cache-resident) time column.
+constexpr int kBucketSkew = 32;
+template <int BS, int MAXN>
+__global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restrict__ time,
+                                                        const int64_t *__restrict__ offs, int64_t S, uint32_t pmask,
+                                                        TimeSortOut out, unsigned long long *__restrict__ big,
+                                                        uint8_t *__restrict__ bigflag, int64_t min_len,
+                                                        bool flag_longer) {
+    constexpr int IPT = MAXN / BS;               // rows per thread
+    constexpr int EPT = (MAXN + 1 + BS - 1) / BS;  // buckets per thread in the scan
+    constexpr int NW = BS / kWave;
+    constexpr bool KEYS_LDS = MAXN <= 4096;
+    static_assert(MAXN <= (1 << kBlkPosBits) && MAXN % BS == 0, "bucket sort shape");
+    __shared__ uint32_t s_cnt[EPT * BS + 1];  // bucket counts, then bucket starts (+ sentinel)
+    __shared__ uint16_t s_pos[MAXN];          // rows in bucket order
+    __shared__ uint64_t s_key[KEYS_LDS ? MAXN : 1];
+    __shared__ int64_t s_lo[NW], s_hi[NW];
+    __shared__ uint32_t s_tmp[NW], s_max[NW];
+    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
     for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
         const int64_t b = offs[s];
         const int64_t len = offs[s + 1] - b;
-        if (len <= 0) continue;
+        if (len <= min_len) continue;
         if (len > MAXN) {
-            if (tid == 0) {
-                atomicAdd(big, (unsigned long long)len);
-                atomicMax(big + 3, (unsigned long long)len);
-                bigflag[s] = 1;
-            }
+            if (flag_longer && tid == 0) flag_big(big, bigflag, s, len);
             continue;
         }
         const int n = int(len);
-        int np2 = 1;
-        while (np2 < n) np2 <<= 1;
-        // gather the times (raw bits parked in sk) and their min / max over non-NULL rows
+        int64_t t[IPT];
         int64_t lo = INT64_MAX, hi = INT64_MIN;
-        for (int i = tid; i < n; i += BS) {
-            const int64_t t = time[rows[b + i]];
-            sk[i] = uint64_t(t);
-            if (t != FZ_TS_NULL) {
-                lo = t < lo ? t : lo;
-                hi = t > hi ? t : hi;
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int i = tid + m * BS;
+            t[m] = i < n ? time[b + i] : FZ_TS_NULL;
+            if (t[m] != FZ_TS_NULL) {
+                lo = t[m] < lo ? t[m] : lo;
+                hi = t[m] > hi ? t[m] : hi;
             }
         }
         lo = wave_min(lo);
         hi = wave_max(hi);
-        if (lane_id() == 0) {
-            s_lo[wave_id()] = lo;
-            s_hi[wave_id()] = hi;
+        if (lane == 0) {
+            s_lo[w] = lo;
+            s_hi[w] = hi;
         }
+        for (int j = tid; j < EPT * BS + 1; j += BS) s_cnt[j] = 0u;
         __syncthreads();
         lo = INT64_MAX;
         hi = INT64_MIN;
-        for (int w = 0; w < BS / kWave; ++w) {
-            lo = s_lo[w] < lo ? s_lo[w] : lo;
-            hi = s_hi[w] > hi ? s_hi[w] : hi;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            lo = s_lo[q] < lo ? s_lo[q] : lo;
+            hi = s_hi[q] > hi ? s_hi[q] : hi;
         }
-        if (hi >= lo && uint64_t(hi) - uint64_t(lo) >= kTsTop) {  // span too wide for the key
-            if (tid == 0) {
-                atomicAdd(big, (unsigned long long)len);
-                atomicMax(big + 3, (unsigned long long)len);
-                bigflag[s] = 1;
-            }
+        if (hi >= lo && uint64_t(hi) - uint64_t(lo) >= kBlkTop) {  // span too wide for the key
+            if (tid == 0) flag_big(big, bigflag, s, len);
             __syncthreads();
             continue;
         }
-        for (int i = tid; i < np2; i += BS) {
-            const int64_t t = i < n ? int64_t(sk[i]) : FZ_TS_NULL;
-            const uint64_t f = t == FZ_TS_NULL ? kTsTop : uint64_t(t - lo);
-            sk[i] = (f << kTsPosBits) | uint64_t(i);
-        }
-        __syncthreads();
-        for (int k = 2; k <= np2; k <<= 1) {
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int t = tid; t < (np2 >> 1); t += BS) {  // every thread owns pairs
-                    const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;  // j = 2^m
-                    const uint64_t ka = sk[i], kb = sk[ixj];
-                    if ((ka > kb) == ((i & k) == 0)) {
-                        sk[i] = kb;
-                        sk[ixj] = ka;
-                    }
-                }
-                bitonic_stage_sync(k, j, np2);
+        const double scale = hi >= lo ? double(n) / (double(uint64_t(hi) - uint64_t(lo)) + 1.0) : 0.0;
+        // the row's key: time above the minimum (NULL: top) << 14 | position
+        auto row_key = [&](int64_t tv, int i) -> uint64_t {
+            return ((tv == FZ_TS_NULL ? kBlkTop : uint64_t(tv - lo)) << kBlkPosBits) | uint64_t(i);
+        };
+        uint32_t bs[IPT];  // bucket << 16 | slot in the bucket
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int i = tid + m * BS;
+            const bool null = t[m] == FZ_TS_NULL;
+            uint32_t q = null ? uint32_t(n) : uint32_t(double(uint64_t(t[m] - lo)) * scale);
+            q = q < uint32_t(n) || null ? q : uint32_t(n - 1);
+            bs[m] = q << 16;
+            if (i < n) {
+                bs[m] |= atomicAdd(&s_cnt[q], 1u);
+                if (KEYS_LDS) s_key[i] = row_key(t[m], i);
             }
         }
+        __syncthreads();
+        // bucket starts: each thread scans EPT consecutive buckets; the largest bucket decides skew
+        uint32_t sum = 0, mx = 0;
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {
+            const uint32_t ce = s_cnt[tid * EPT + e];
+            sum += ce;
+            mx = ce > mx ? ce : mx;
+        }
+        mx = wave_max(mx);
+        if (lane == 0) s_max[w] = mx;
+        uint32_t run = block_excl_scan<uint32_t, NW>(sum, s_tmp, (uint32_t *)nullptr);
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {  // (block_excl_scan's barriers ordered every read above)
+            const uint32_t ce = s_cnt[tid * EPT + e];
+            s_cnt[tid * EPT + e] = run;
+            run += ce;
+        }
+        if (tid == 0) s_cnt[EPT * BS] = uint32_t(n);
+        __syncthreads();
+        uint32_t gmax = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) gmax = s_max[q] > gmax ? s_max[q] : gmax;
+        if (gmax > uint32_t(kBucketSkew)) {  // clustered times: the merge sort takes the segment
+            if (tid == 0) flag_big(big, bigflag, s, len);
+            __syncthreads();
+            continue;
+        }
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int i = tid + m * BS;
+            if (i < n) s_pos[s_cnt[bs[m] >> 16] + (bs[m] & 0xffffu)] = uint16_t(i);
+        }
+        __syncthreads();
         const uint32_t p = uint32_t(s) & pmask;
-        for (int i = tid; i < n; i += BS) {
-            const uint64_t key = sk[i];
-            const uint64_t f = key >> kTsPosBits;
-            const int64_t q = b + i;
-            const int32_t r = int32_t(rows[b + int64_t(key & ((1u << kTsPosBits) - 1))]);
-            otime[q] = f == kTsTop ? FZ_TS_NULL : lo + int64_t(f);
-            oproj[q] = p;
-            if (gc.perm) {
-                gc.perm[q] = r;
-                orow[q] = int32_t(q);
-                for (int j = 0; j < gc.n; ++j) {
-                    if (gc.size[j] == 8)
-                        static_cast<uint64_t *>(gc.dst[j])[q] = static_cast<const uint64_t *>(gc.src[j])[r];
-                    else if (gc.size[j] == 4)
-                        static_cast<uint32_t *>(gc.dst[j])[q] = static_cast<const uint32_t *>(gc.src[j])[r];
-                    else
-                        static_cast<uint8_t *>(gc.dst[j])[q] = static_cast<const uint8_t *>(gc.src[j])[r];
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int i = tid + m * BS;
+            if (i >= n) continue;
+            const uint32_t st = s_cnt[bs[m] >> 16], en = s_cnt[(bs[m] >> 16) + 1];
+            const uint64_t key = row_key(t[m], i);
+            uint32_t rank = 0;
+            for (uint32_t x = st; x < en; ++x) {
+                const int ox = s_pos[x];
+                uint64_t kx;
+                if (KEYS_LDS) {
+                    kx = s_key[ox];
+                } else {
+                    kx = row_key(time[b + ox], ox);
                 }
-            } else {
-                orow[q] = r;
+                rank += kx < key;
             }
+            out.put(b + st + rank, t[m], p, b + i);
         }
-        __syncthreads();
+        __syncthreads();  // LDS is reused by the next segment
     }
 }
 
 // Sorts by (prefix, time, row); adds to the (zeroed) device counter *big the rows in segments too
-// long for LDS (and big[3] = the longest such segment, bigflag[s] = 1): the caller sorts those
-// through the segmented merge sort.
-// nonempty_bound: host upper bound on the number of non-empty segments (picks the workgroup size).
-constexpr int kTimeSortSmallBlock = 256;
-constexpr int kTimeSortSmallMean = 256;  // mean rows per segment at or below which it is used
+// long for the register sorts (and big[3] = the longest such segment, bigflag[s] = 1): the caller
+// sorts those through the segmented merge sort, then gathers every table's columns.
 struct PrefixSorted {
+    int64_t n = 0;
     int64_t S = 0;
     const int64_t *offs = nullptr;   // [S + 1] segment offsets of the prefix-sorted rows
     const uint32_t *rows = nullptr;  // row ids in (prefix, row) order
     uint8_t *bigflag = nullptr;      // [S] 1: the segment is left to the merge sort
+    const int64_t *time = nullptr;   // times in (prefix, row) order
+    GatherCols gc;                   // the gathered columns' sources in (prefix, row) order
+    TimeSortOut out{};
 };
 static PrefixSorted sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time,
-                                    int32_t *orow, int64_t *otime, uint32_t *oproj, const GatherCols &gc,
-                                    unsigned long long *big, int64_t nonempty_bound) {
+                                    int64_t *otime, uint32_t *oproj, const GatherCols &gc, unsigned long long *big) {
     PrefixSorted ps;
+    ps.n = n;
     if (n <= 0) return ps;
     uint64_t *keys = c->arena.get<uint64_t>(n);
     uint32_t *vals = c->arena.get<uint32_t>(n);
     const unsigned g = grid_for(n, kBlock, 4096);
     k_keys_prefix_rows<<<g, kBlock, 0, c->stream>>>(pre, n, keys, vals);
     FZ_LAUNCH_CHECK();
-    radix_sort_pairs_swap(c, keys, vals, n, prefix_bits);
+    // the prefix passes move the time column and the gathered columns with the keys (each pass's
+    // writes land in per-digit runs): the time sort and the gather then read every segment's rows
+    // from one contiguous range instead of gathering them from the heap-ordered table
+    RadixPayload pl;
+    pl.n = 1 + gc.n;
+    pl.in[0] = time;
+    pl.size[0] = 8;
+    for (int j = 0; j < gc.n; ++j) {
+        pl.in[1 + j] = gc.src[j];
+        pl.size[1 + j] = gc.size[j];
+    }
+    radix_sort_pairs_payload(c, keys, vals, n, prefix_bits, pl);
+    time = static_cast<const int64_t *>(pl.out[0]);
+    ps.time = time;
+    ps.gc = gc;
+    for (int j = 0; j < gc.n; ++j) ps.gc.src[j] = pl.out[1 + j];
     const int64_t S = int64_t(1) << prefix_bits;
     int64_t *offs = c->arena.get<int64_t>(S + 1);
     k_prefix_offsets<<<grid_for(n > S + 1 ? n : S + 1, kBlock, 4096), kBlock, 0, c->stream>>>(keys, n, S, offs);
@@ -262,53 +351,51 @@ static PrefixSorted sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix
     ps.offs = offs;
     ps.rows = vals;
     ps.bigflag = bigflag;
+    ps.out = TimeSortOut{otime, oproj, c->arena.get<uint32_t>(n)};
     const uint32_t pmask = pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << pre.pbits) - 1ull);
     {
-        ProbeScope ps(c, "seg_time_sort", 28.0 * double(n));  // row 4 + gathered time 8 + out 16 B
-        const unsigned g = unsigned(S < 16384 ? S : 16384);
-        if (n <= int64_t(kTimeSortSmallMean) * nonempty_bound) {
-            // short segments on average (issues: ~65 rows per project): 256-thread workgroups, five
-            // per CU by LDS instead of two, so the whole table sorts in one round of the grid
-            k_seg_time_sort<kTimeSortSmallBlock, kSegSortMax><<<g, kTimeSortSmallBlock, 0, c->stream>>>(
-                vals, time, offs, S, pmask, orow, otime, oproj, big, bigflag, gc);
-        } else {
-            k_seg_time_sort<kTimeSortBlock, kSegSortMax><<<g, kTimeSortBlock, 0, c->stream>>>(
-                vals, time, offs, S, pmask, orow, otime, oproj, big, bigflag, gc);
-        }
+        // algorithmic bytes: time 8 read; time 8 + project 4 + source position 4 written
+        ProbeScope probe(c, "seg_time_sort", 24.0 * double(n));
+        // bucket sorts by length class (each launch skips the others' segments): <= 1024 rows one
+        // 256-thread workgroup each (15 KiB of LDS: many per CU), <= 2048 512 threads, <= 4096
+        // 1024 threads, <= 16384 1024 threads with the keys re-read from memory (LDS: one per CU,
+        // a persistent grid); longer or clustered segments are flagged for the merge sort
+        k_seg_time_bucket<256, 1024><<<unsigned(S < 16384 ? S : 16384), 256, 0, c->stream>>>(
+            time, offs, S, pmask, ps.out, big, bigflag, 0, false);
+        FZ_LAUNCH_CHECK();
+        k_seg_time_bucket<512, 2048><<<unsigned(S < 4096 ? S : 4096), 512, 0, c->stream>>>(
+            time, offs, S, pmask, ps.out, big, bigflag, 1024, false);
+        FZ_LAUNCH_CHECK();
+        k_seg_time_bucket<1024, 4096><<<unsigned(S < 2048 ? S : 2048), 1024, 0, c->stream>>>(
+            time, offs, S, pmask, ps.out, big, bigflag, 2048, false);
+        FZ_LAUNCH_CHECK();
+        k_seg_time_bucket<1024, 16384><<<unsigned(S < 512 ? S : 512), 1024, 0, c->stream>>>(
+            time, offs, S, pmask, ps.out, big, bigflag, 4096, true);
         FZ_LAUNCH_CHECK();
     }
     return ps;
 }
 
+// Gather of every sorted row's columns (after all sorts of the table, merge sort included).
+static void gather_table(fz_ctx *c, const PrefixSorted &ps, int32_t *orow) {
+    if (ps.n <= 0) return;
+    // algorithmic bytes: spos 4 + row id 4 + columns read; perm 4 + row 4 + columns written
+    ProbeScope probe(c, "store_gather", (16.0 + 2.0 * ps.gc.bytes()) * double(ps.n));
+    k_store_gather<<<grid_for(ps.n, kBlock, 8192), kBlock, 0, c->stream>>>(ps.out.spos, ps.rows, ps.n, orow, ps.gc);
+    FZ_LAUNCH_CHECK();
+}
+
 // The merge-sort path of the store: key = signed time as an order-preserving u64 (NULL =
-// INT64_MAX -> ~0: last), stable by row; the sink writes what k_seg_time_sort writes for a short
-// segment (time, project, row = position, perm = source row, gathered columns).
+// INT64_MAX -> ~0: last), stable by row; the sink writes what the register sorts write.
 struct StoreTimeKey {
-    const int64_t *time;
-    const uint32_t *rows;
-    __device__ uint64_t operator()(int64_t i) const { return uint64_t(time[rows[i]]) ^ (uint64_t(1) << 63); }
+    const int64_t *time;  // prefix-sorted times
+    __device__ uint64_t operator()(int64_t i) const { return uint64_t(time[i]) ^ (uint64_t(1) << 63); }
 };
 struct StoreSink {
-    const uint32_t *rows;
     uint32_t pmask;
-    int32_t *orow;
-    int64_t *otime;
-    uint32_t *oproj;
-    GatherCols gc;
+    TimeSortOut out;
     __device__ void operator()(int32_t s, int64_t q, uint64_t k, uint32_t v) const {
-        const int32_t r = int32_t(rows[v]);
-        otime[q] = int64_t(k ^ (uint64_t(1) << 63));
-        oproj[q] = uint32_t(s) & pmask;
-        gc.perm[q] = r;
-        orow[q] = int32_t(q);
-        for (int j = 0; j < gc.n; ++j) {
-            if (gc.size[j] == 8)
-                static_cast<uint64_t *>(gc.dst[j])[q] = static_cast<const uint64_t *>(gc.src[j])[r];
-            else if (gc.size[j] == 4)
-                static_cast<uint32_t *>(gc.dst[j])[q] = static_cast<const uint32_t *>(gc.src[j])[r];
-            else
-                static_cast<uint8_t *>(gc.dst[j])[q] = static_cast<const uint8_t *>(gc.src[j])[r];
-        }
+        out.put(q, int64_t(k ^ (uint64_t(1) << 63)), uint32_t(s) & pmask, v);
     }
 };
 
@@ -378,12 +465,12 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         k_count_types<<<grid_for(t->n_builds, kBlock * 8, 512), kBlock, 0, c->stream>>>(t->b_type, t->n_builds, tcnt);
         FZ_LAUNCH_CHECK();
     }
+    // the counts ride along with the min/max read-back (one stream sync for both)
+    FZ_HIP(hipMemcpyAsync(c->h_pinned + 16, tcnt, 16, hipMemcpyDeviceToHost, c->stream));
     minmax_i64_to_host(c, cols, ns, 1, mm);  // syncs the stream
     s.num_min = mm[0];
     s.num_max = mm[1];
-    unsigned long long hcnt[2];
-    FZ_HIP(hipMemcpy(hcnt, tcnt, 16, hipMemcpyDeviceToHost));
-    const int64_t n_fuzz = int64_t(hcnt[0]), n_covb = int64_t(hcnt[1]);
+    const int64_t n_fuzz = c->h_pinned[16], n_covb = c->h_pinned[17];
 
     // the three tables: (prefix = [type|]project) LSD passes, then each segment sorted by time in LDS
     struct Tab {
@@ -430,10 +517,9 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     PrefixSorted pss[3];
     for (int k = 0; k < 3; ++k) {
         Tab &b = tabs[k];
-        // non-empty segments: at most one per project (and build type: 2 prefix bits for builds)
-        const int64_t segs = int64_t(P > 0 ? P : 1) * (k == 0 ? 4 : 1);
-        pss[k] = sort_table_fast(c, b.n, b.pre, b.pbits_total, b.time, b.row->ensure<int32_t>(b.n),
-                                 b.tm->ensure<int64_t>(b.n), b.pr->ensure<uint32_t>(b.n), gcs[k], big3 + k, segs);
+        b.row->ensure<int32_t>(b.n);
+        pss[k] = sort_table_fast(c, b.n, b.pre, b.pbits_total, b.time, b.tm->ensure<int64_t>(b.n),
+                                 b.pr->ensure<uint32_t>(b.n), gcs[k], big3 + k);
     }
     auto make_views = [&]() {
         int32_t *row = s.b_row.as<int32_t>();
@@ -455,7 +541,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 10 * 8, hipMemcpyDeviceToHost, c->stream));
         sync(c);
     };
-    // segments the LDS time sort left (longer than 4096 rows, or a time span too wide for its
+    // segments the register sorts left (longer than 16384 rows, or a time span too wide for their
     // packed key): segmented merge sort of those rows only, writing the same outputs
     make_views();
     read_stats();
@@ -468,11 +554,11 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         const PrefixSorted &ps = pss[k];
         const uint32_t pmask = b.pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << b.pre.pbits) - 1ull);
         ProbeScope probe(c, "seg_merge_sort", 36.0 * double(bigrows[k]));
-        sort_big_segments(c, ps.offs, ps.S, b.n, bigmax[k], ps.bigflag, StoreTimeKey{b.time, ps.rows},
-                          StoreSink{ps.rows, pmask, b.row->as<int32_t>(), b.tm->as<int64_t>(), b.pr->as<uint32_t>(),
-                                    gcs[k]});
+        sort_big_segments(c, ps.offs, ps.S, b.n, bigmax[k], ps.bigflag, StoreTimeKey{ps.time},
+                          StoreSink{pmask, ps.out});
         redo = true;
     }
+    for (int k = 0; k < 3; ++k) gather_table(c, pss[k], tabs[k].row->as<int32_t>());
     if (redo) {  // the merged segments' projects are written now
         make_views();
         read_stats();
