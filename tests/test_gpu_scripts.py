@@ -21,9 +21,11 @@ def test_all_scripts_tiny(engine, tmp_path, monkeypatch, capsys):
     t = scripts.load_tables()
     work = tmp_path / "work"
     work.mkdir()
+    announced = []
     for name in scripts.SCRIPTS:
         capsys.readouterr()
-        scripts.run(name, engine, t, cwd=str(work))
+        r = scripts.run(name, engine, t, cwd=str(work), figures=True)  # figures: side process, joined
+        announced += [p for p, _ in r.figures]
         out = capsys.readouterr().out
         errs = goldens.compare_lines(out, goldens.text("tiny", name), rtol=1e-9)
         assert not errs, name + "\n" + "\n".join(errs)
@@ -44,3 +46,19 @@ def test_all_scripts_tiny(engine, tmp_path, monkeypatch, capsys):
                 assert ours == gold, rel
             n += 1
     assert n >= 10
+    for p in announced:  # the PDFs the reference writes (drawn from the libfz results)
+        with open(work / p, "rb") as f:
+            assert f.read(5) == b"%PDF-", p
+
+
+def test_all_scripts_medium_figures(engine, tmp_path):
+    """Every figure of the medium case drawn from the GPU results (rq2 per-project trends included)."""
+    t = goldens.tables("medium")
+    pdfs = 0
+    for name in scripts.SCRIPTS:
+        r = scripts.run(name, engine, t, cwd=str(tmp_path), figures=True)
+        for p, _ in r.figures:
+            assert (tmp_path / p).read_bytes()[:5] == b"%PDF-", p
+    for dp, _, fns in os.walk(tmp_path / "data" / "result_data"):
+        pdfs += sum(fn.endswith(".pdf") for fn in fns)
+    assert pdfs >= 12

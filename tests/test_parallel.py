@@ -1,4 +1,4 @@
-"""Project-sharded multi-GPU layer (tse_amd/parallel.py) on CPU: world_size 2 and 3 over gloo.
+"""Project-sharded multi-GPU layer (tse_amd/parallel.py) on CPU: world_size 2, 3 and 8 over gloo.
 
 Each rank runs the exchange drivers over ORACLE shards (the CPU restatement of one rank's local
 analysis); rank 0 checks the recombined result against the oracle on the whole table.  The
@@ -404,7 +404,8 @@ def test_shard_bounds_cover_and_balance():
             assert sizes.max() <= 2.5 * t.n_rows / world
 
 
-@pytest.mark.parametrize("world,case", [(2, "collide"), (3, "collide"), (3, "last_shard_no_issues")])
+@pytest.mark.parametrize("world,case", [(2, "collide"), (3, "collide"), (3, "last_shard_no_issues"), (8, "collide"),
+                                        (8, "last_shard_no_issues")])
 def test_sharded_rq1_rq3_match_whole_table(world, case, tmp_path):
     _spawn(world, case, tmp_path)
 

@@ -6,9 +6,10 @@ reference (``run_all_analysis.sh:13-46``): compute the analysis - here on the GP
 ``logging.basicConfig(level=INFO, format='%(asctime)s [%(levelname)s] %(message)s')``,
 ``rq4a_bug.py:23-28``) and write the same files under ``<cwd>/data/result_data``.
 
-Figures (PDF) are host-side matplotlib in the reference and not part of the hot path; the
-renderer records what each figure would contain (``Rendered.figures``) but this runner does not
-draw them (``compute`` mode of SURVEY.md 7).
+Figures (PDF) are host-side matplotlib in the reference and not part of the hot path: the runner
+hands each script's figure data to a side process (``rq/figures.py``) after the tables and stdout
+are written, at the reference's paths.  ``FZ_FIGURES=0`` skips them (the ``compute`` mode of
+SURVEY.md 7).
 """
 from __future__ import annotations
 
@@ -25,18 +26,30 @@ SCRIPTS = ["rq1_detection_rate", "rq2_coverage_and_added", "rq2_coverage_count",
            "rq3_diff_coverage_at_detection", "rq4a_bug", "rq4b_coverage"]   # run_all_analysis.sh order
 
 
+DUMP = os.path.join("data", "database", "backup_clean.sql")   # README.md:14-15 (restored into PG there)
+COLUMNAR = os.path.join("data", "columnar")
+
+
 def data_source() -> str:
     """Where the drop-ins read the session tables: $FZ_DATA (a columnar directory written by
     ``store.save_columnar``, a directory of PostgreSQL CSV exports, or the plain-format dump
-    ``data/database/backup_clean.sql`` itself), default data/columnar."""
-    return os.environ.get("FZ_DATA", os.path.join("data", "columnar"))
+    itself); else ./data/columnar; else the reference's dump ./data/database/backup_clean.sql."""
+    env = os.environ.get("FZ_DATA")
+    if env:
+        return env
+    if not os.path.exists(os.path.join(COLUMNAR, "meta.json")) and os.path.isfile(DUMP):
+        return DUMP
+    return COLUMNAR
 
 
 def load_tables(path: Optional[str] = None) -> Tables:
     from .. import store
     path = path or data_source()
     if os.path.isfile(path):
-        return store.from_pg_dump(path)
+        t = store.from_pg_dump(path)
+        if path == DUMP and not os.environ.get("FZ_DATA"):
+            store.save_columnar(t, COLUMNAR)  # the next scripts map the columns instead of re-parsing
+        return t
     if os.path.exists(os.path.join(path, "meta.json")):
         return store.load_columnar(path)
     if os.path.exists(os.path.join(path, "buildlog_data.csv")):
@@ -45,22 +58,37 @@ def load_tables(path: Optional[str] = None) -> Tables:
 
 
 def analyse(name: str, eng: E.Engine, t: Tables, cwd: str) -> render.Rendered:
+    return analyse_result(name, eng, t, cwd)[1]
+
+
+def analyse_result(name: str, eng: E.Engine, t: Tables, cwd: str):
+    """(result object, rendered output) of one script."""
     if name == "rq1_detection_rate":
-        return render.rq1(compute.rq1(eng), t)
+        r = compute.rq1(eng)
+        return r, render.rq1(r, t)
     if name == "rq2_coverage_count":
-        return render.rq2_count(compute.rq2_count(eng), t)
+        r = compute.rq2_count(eng)
+        return r, render.rq2_count(r, t)
     if name == "rq2_coverage_and_added":
-        return render.rq2_add(compute.rq2_add(eng), t)
+        r = compute.rq2_add(eng)
+        return r, render.rq2_add(r, t)
     if name == "rq3_diff_coverage_at_detection":
-        return render.rq3(compute.rq3(eng), t)
+        r = compute.rq3(eng)
+        return r, render.rq3(r, t)
     if name == "rq4a_bug":
-        return render.rq4a(compute.rq4a(eng), t, cwd=cwd)
+        r = compute.rq4a(eng)
+        return r, render.rq4a(r, t, cwd=cwd)
     if name == "rq4b_coverage":
         b = compute.rq4b_buffers(eng)
         compute.rq4b_launch(eng, b)
         n_elig = int(b.host("eligible", eng.tables.fz.n_projects).sum())
-        return render.rq4b(compute.rq4b_collect(eng, b), t, n_eligible=n_elig, cwd=cwd)
+        r = compute.rq4b_collect(eng, b)
+        return r, render.rq4b(r, t, n_eligible=n_elig, cwd=cwd)
     raise ValueError(f"unknown script {name!r}")
+
+
+def figures_enabled() -> bool:
+    return os.environ.get("FZ_FIGURES", "1") not in ("0", "", "no", "false")
 
 
 def emit(r: render.Rendered, cwd: str, out=None) -> None:
@@ -83,7 +111,10 @@ def emit(r: render.Rendered, cwd: str, out=None) -> None:
     out.flush()
 
 
-def run(name: str, eng: Optional[E.Engine] = None, t: Optional[Tables] = None, cwd: Optional[str] = None):
+def run(name: str, eng: Optional[E.Engine] = None, t: Optional[Tables] = None, cwd: Optional[str] = None,
+        figures: Optional[bool] = None, pending: Optional[list] = None):
+    """One drop-in script.  Figures are drawn by a side process started after the outputs are
+    written; it is joined before returning unless the caller collects it in `pending`."""
     cwd = cwd or os.getcwd()
     t = t if t is not None else load_tables()
     own = eng is None
@@ -92,24 +123,42 @@ def run(name: str, eng: Optional[E.Engine] = None, t: Optional[Tables] = None, c
     if eng.tables is None or eng.tables.host is not t:
         eng.upload(t)
         eng.build_store()
-    r = analyse(name, eng, t, cwd)
+    res, r = analyse_result(name, eng, t, cwd)
     emit(r, cwd)
     if own:
         eng.close()
+    if figures if figures is not None else figures_enabled():
+        from . import figures as F
+        proc = F.draw_in_side_process([F.spec(name, res, t)], cwd)
+        if pending is not None:
+            pending.append(proc)
+        else:
+            proc.join()
     return r
 
 
+def main_one(name: str) -> int:
+    """`python3 program/research_questions/<name>.py`: one script, argument-less (the tables from
+    data_source(), outputs under the working directory)."""
+    run(name)
+    return 0
+
+
 def main_all(argv=None) -> int:
-    """run_all_analysis.sh: the six scripts in order, one engine, tables loaded once."""
+    """run_all_analysis.sh: the six scripts in order, one engine, tables loaded once; the figure
+    processes run beside the next scripts and are joined at the end."""
     t = load_tables()
     eng = E.Engine(0)
     eng.upload(t)
     eng.build_store()
+    pending = []
     for k, name in enumerate(SCRIPTS, 1):
         print(f"\n[{k}/6] Running {name} ...")
-        run(name, eng, t)
+        run(name, eng, t, pending=pending)
     eng.close()
-    return 0
+    for p in pending:
+        p.join()
+    return 0 if all(p.exitcode == 0 for p in pending) else 1
 
 
 if __name__ == "__main__":
