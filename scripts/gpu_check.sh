@@ -30,5 +30,7 @@ STEPS=${STEPS:-tests,smoke,bench,prof}
 [[ ",$STEPS," == *,pc5,* ]] && run prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5_$TAG -o run -- python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu-baseline
 [[ ",$STEPS," == *,fs2,* ]] && run bench_fs_c2 400 python -u bench.py --force-sharded --no-cpu-baseline
 [[ ",$STEPS," == *,fs3,* ]] && run bench_fs_c3 600 python -u bench.py --config c3 --force-sharded --steps 3 --warmup 1 --no-cpu-baseline
+[[ ",$STEPS," == *,e2e,* ]] && run e2e_c2 600 python -u scripts/e2e_suite.py --config c2
+[[ ",$STEPS," == *,e2enofig,* ]] && run e2e_c2_nofig 600 python -u scripts/e2e_suite.py --config c2 --no-figures
 [[ ",$STEPS," == *,prof,* ]] && run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline
 echo done
