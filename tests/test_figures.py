@@ -48,9 +48,17 @@ def test_figures_drawn(name, tmp_path):
             assert f.read(5) == b"%PDF-", p
 
 
-def test_side_process(tmp_path):
+def test_side_processes(tmp_path):
+    """Several drawing processes: RQ2's per-project figures dealt over them, the rest in one."""
     t = goldens.tables("medium")
-    proc = F.draw_in_side_process([F.spec("rq1_detection_rate", orc.rq1(t), t)], str(tmp_path))
-    proc.join(120)
-    assert proc.exitcode == 0
-    assert (tmp_path / "data" / "result_data" / "rq1" / "rq1_detection_rate.pdf").exists()
+    r2 = orc.rq2_count(t)
+    specs = [F.spec("rq1_detection_rate", orc.rq1(t), t), F.spec("rq2_coverage_count", r2, t)]
+    procs = F.draw_in_side_process(specs, str(tmp_path), workers=3)
+    assert len(procs) >= 2
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    base = tmp_path / "data" / "result_data"
+    assert (base / "rq1" / "rq1_detection_rate.pdf").exists()
+    want = {os.path.basename(p) for p, _ in render.rq2_count(r2, t).figures}
+    assert want and want <= set(os.listdir(base / "rq2" / "projects"))

@@ -134,7 +134,7 @@ def draw(spec: dict, cwd: str) -> list:
         out.append(os.path.join(base, "rq1", "rq1_detection_rate.pdf"))
         _save(fig, out[-1])
         plt.close(fig)
-    elif kind == "rq2":
+    elif kind in ("rq2", "rq2_projects"):
         d = os.path.join(base, "rq2")
         for name, cov, tot in spec["projects"]:
             fig, ax1 = plt.subplots(figsize=(5, 3))
@@ -153,6 +153,8 @@ def draw(spec: dict, cwd: str) -> list:
             out.append(os.path.join(d, "projects", name + ".pdf"))
             _save(fig, out[-1])
             plt.close(fig)
+        if kind == "rq2_projects":
+            return out
         fig = plt.figure(figsize=(5, 3))
         plt.hist(spec["corr"], bins=40, color="skyblue", edgecolor="black", alpha=0.8)
         plt.xlabel("Correlation")
@@ -312,14 +314,37 @@ def spec(name: str, r, t: Tables) -> dict:
     return {"kind": "none"}     # rq2_coverage_and_added draws nothing
 
 
-def draw_in_side_process(specs, cwd: str):
-    """Start a child interpreter that draws the figures (the GPU process never runs matplotlib);
-    returns the Process (join() it before exiting)."""
+def split(specs, workers: int):
+    """The specs cut into `workers` lists of about equal drawing work: the per-project trend
+    figures of RQ2 (hundreds of PDFs, rq2_coverage_count.py:325-327) are dealt round-robin."""
+    parts = [[] for _ in range(max(1, workers))]
+    for sp in specs:
+        if sp.get("kind") == "rq2" and len(parts) > 1 and len(sp["projects"]) > 1:
+            pr = sp["projects"]
+            parts[0].append(dict(sp, projects=pr[0::len(parts)]))
+            for w in range(1, len(parts)):
+                if pr[w::len(parts)]:
+                    parts[w].append({"kind": "rq2_projects", "projects": pr[w::len(parts)]})
+        else:
+            parts[0].append(sp)
+    return [p for p in parts if p]
+
+
+def figure_workers() -> int:
+    return max(1, min(8, int(os.environ.get("FZ_FIGURE_WORKERS", os.cpu_count() or 1))))
+
+
+def draw_in_side_process(specs, cwd: str, workers: int = 1):
+    """Start child interpreters that draw the figures (the GPU process never runs matplotlib);
+    returns the Process list (join() them before exiting)."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
-    p = ctx.Process(target=_draw_all, args=(specs, cwd), daemon=False)
-    p.start()
-    return p
+    procs = []
+    for part in split(specs, workers):
+        p = ctx.Process(target=_draw_all, args=(part, cwd), daemon=False)
+        p.start()
+        procs.append(p)
+    return procs
 
 
 def _draw_all(specs, cwd):

@@ -129,11 +129,12 @@ def run(name: str, eng: Optional[E.Engine] = None, t: Optional[Tables] = None, c
         eng.close()
     if figures if figures is not None else figures_enabled():
         from . import figures as F
-        proc = F.draw_in_side_process([F.spec(name, res, t)], cwd)
+        procs = F.draw_in_side_process([F.spec(name, res, t)], cwd, workers=F.figure_workers())
         if pending is not None:
-            pending.append(proc)
+            pending.extend(procs)
         else:
-            proc.join()
+            for proc in procs:
+                proc.join()
     return r
 
 
