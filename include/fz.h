@@ -400,6 +400,38 @@ int fz_rq4b_session_stats(fz_ctx *ctx, const double *values, const int64_t *sess
  * mannwhitneyu(greater) U1, brunnermunzel statistic / p, levene W / p. */
 int fz_two_sample_tests(fz_ctx *ctx, const double *x, int64_t nx, const double *y, int64_t ny, double *out);
 
+/* ---- build-log analysis ------------------------------------------
+ * Replaces buildlog_analysis(row) of program/preparation/4_get_buildlog_analysis.py:14-246 for a
+ * batch of logs already downloaded: text = the UTF-8 bytes of every log back to back (device),
+ * log_offs[n_logs + 1] its byte offsets (host AND device copies: the host one cuts the work list).
+ * Lines are str.splitlines() lines.  Per log: build_type / result (FZ_BT_* / FZ_BR_*), the project
+ * name as a byte span of text, log_line0 (index of its first line) and a status: 0 analysed,
+ * 1 empty text (the reference returns its defaults, :54-55), 2 one line (the reference raises
+ * IndexError at lines[-2], :230).  The lines the srcmap extraction needs (:162-214) - flags
+ * FZ_BL_SKIP / JQ / OPEN / CLOSE - are listed in ev_* (unordered; *n_events may exceed event_cap:
+ * then call again with room for that many). */
+enum { FZ_BT_NONE = 0, FZ_BT_coverage = 1, FZ_BT_introspector = 2, FZ_BT_FUZZING = 3, FZ_BT_UNKNOWN = 4,
+       FZ_BT_INTROSPECTOR = 5, FZ_BT_COVERAGE = 6 };
+enum { FZ_BR_NONE = 0, FZ_BR_ERROR = 1, FZ_BR_SUCCESS = 2, FZ_BR_UNKNOWN = 3 };
+enum { FZ_BL_SKIP = 1 << 2, FZ_BL_JQ = 1 << 8, FZ_BL_OPEN = 1 << 9, FZ_BL_CLOSE = 1 << 10 };
+typedef struct fz_buildlog_out {
+    int32_t *log_type;      /* [n_logs] device */
+    int32_t *log_result;    /* [n_logs] */
+    int32_t *log_status;    /* [n_logs] */
+    int64_t *log_proj_off;  /* [n_logs] byte offset in text of the project name (-1: none) */
+    int32_t *log_proj_len;  /* [n_logs] */
+    int64_t *log_line0;     /* [n_logs] first line index of the log */
+    int64_t *n_lines;       /* [1] total lines */
+    int64_t *ev_line;       /* [event_cap] line index */
+    int64_t *ev_start;      /* [event_cap] byte offset of the line */
+    int32_t *ev_len;        /* [event_cap] bytes of the line (without its break) */
+    uint32_t *ev_flags;     /* [event_cap] FZ_BL_* */
+    int64_t event_cap;
+    int64_t *n_events;      /* [1] */
+} fz_buildlog_out;
+int fz_buildlog(fz_ctx *ctx, const uint8_t *text, int64_t n_bytes, const int64_t *log_offs_host,
+                const int64_t *log_offs, int64_t n_logs, const fz_buildlog_out *out);
+
 /* ---- per-kernel probe (bench.py roofline) ------------------------------------------------ */
 /* Start timing every launch of the named kernels (one name, or several separated by commas, e.g.
  * "radix_scatter,elig_hist") with HIP events on the context stream; fz_probe_end synchronises the

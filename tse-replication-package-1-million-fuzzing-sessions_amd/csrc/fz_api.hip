@@ -30,6 +30,8 @@ void rq4b_session_stats(fz_ctx *c, const double *values, const int64_t *sid, con
                         int64_t max_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q, double *pbm);
 void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t *n2, const double *b,
                       int64_t nb_cap, const int64_t *n1, double *ts);
+void buildlog(fz_ctx *c, const uint8_t *text, int64_t n_bytes, const int64_t *log_offs_host, const int64_t *log_offs,
+              int64_t n_logs, const fz_buildlog_out *o);
 }  // namespace fz
 
 namespace {
@@ -232,6 +234,14 @@ int fz_two_sample_tests(fz_ctx *ctx, const double *x, int64_t nx, const double *
         const int64_t h[2] = {nx, ny};
         fz::set_i64(ctx, d_n, h, 2);
         fz::two_sample_tests(ctx, x, nx, d_n, y, ny, d_n + 1, out);
+    });
+}
+
+int fz_buildlog(fz_ctx *ctx, const uint8_t *text, int64_t n_bytes, const int64_t *log_offs_host,
+                const int64_t *log_offs, int64_t n_logs, const fz_buildlog_out *out) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n_logs == 0 || (log_offs_host && log_offs && (n_bytes == 0 || text)), "fz_buildlog: bad arguments");
+        fz::buildlog(ctx, text, n_bytes, log_offs_host, log_offs, n_logs, out);
     });
 }
 

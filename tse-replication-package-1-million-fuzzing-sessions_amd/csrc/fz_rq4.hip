@@ -281,7 +281,6 @@ void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t 
             gr[i] = 1;
         }
     });
-    const int64_t *d_all = oall + 1;
     Segs one{1, oall, cap};
     int32_t *sid = segment_ids(c, one);
     double *u1 = c->arena.get<double>(1);

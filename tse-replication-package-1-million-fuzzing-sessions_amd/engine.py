@@ -127,6 +127,12 @@ class FzRq4bOut(C.Structure):
                                   "tests", "trend_values", "trend_offsets", "delta_order")]
 
 
+class FzBuildlogOut(C.Structure):
+    _fields_ = [("log_type", _P), ("log_result", _P), ("log_status", _P), ("log_proj_off", _P), ("log_proj_len", _P),
+                ("log_line0", _P), ("n_lines", _P), ("ev_line", _P), ("ev_start", _P), ("ev_len", _P),
+                ("ev_flags", _P), ("event_cap", _I64), ("n_events", _P)]
+
+
 # every symbol include/fz.h declares, with its ctypes signature
 SIGNATURES = {
     "fz_abi_version": (C.c_int, []),
@@ -153,6 +159,7 @@ SIGNATURES = {
     "fz_rq4b_ex": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.c_uint32, C.POINTER(FzRq4bOut)]),
     "fz_rq4b_session_stats": (C.c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P]),
     "fz_two_sample_tests": (C.c_int, [_P, _P, _I64, _P, _I64, _P]),
+    "fz_buildlog": (C.c_int, [_P, _P, _I64, _P, _P, _I64, C.POINTER(FzBuildlogOut)]),
     "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),
     "fz_probe_end": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "fz_probe_get": (C.c_int, [_P, C.c_char_p, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
