@@ -285,24 +285,48 @@ def weak_shard(t, rank, world):
         pi_project=t.pi_project + off)
 
 
-def cpu_baseline(t, stages):
-    """The oracle port (numpy/scipy, single thread) over the same stages on the same table."""
+def _oracle_stages(t, stages):
     from oracle import rq_oracle as orc
     fns = {"rq1": orc.rq1, "rq2_count": orc.rq2_count, "rq2_add": orc.rq2_add, "rq3": orc.rq3,
            "rq4a": orc.rq4a, "rq4b": orc.rq4b}
-    stages = [s for s in stages if s in fns]
-    t0 = time.perf_counter()
-    reps = 0
-    while True:
-        for s in stages:
+    for s in stages:
+        if s in fns:
             fns[s](t)
-        reps += 1
-        if time.perf_counter() - t0 > 10.0 or reps >= 20:
-            break
-    el = time.perf_counter() - t0
-    return {"value": round(t.n_rows * reps / el, 1), "unit": "session-rows/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/rq_oracle.py {'+'.join(stages)} on the full bench table x{reps} "
-                      f"({el:.1f} s, single-threaded numpy/scipy)"}
+
+
+def _oracle_shard_worker(args):
+    t, stages = args
+    import time as _t
+    t0 = _t.perf_counter()
+    _oracle_stages(t, stages)
+    return _t.perf_counter() - t0
+
+
+def cpu_baseline(t, stages):
+    """The oracle port over the same stages on the same table: one process per host core over
+    contiguous project shards (parallel.shard_bounds; each shard's six analyses, no cross-shard
+    recombination - a lower bound on the multi-core CPU time), timed as the slowest shard; and
+    single-threaded over the whole table (`single_core`)."""
+    import multiprocessing as mp
+    from tse_amd import parallel as par
+    stages = [s for s in stages if s in ("rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b")]
+    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
+    bounds = par.shard_bounds(t, cores)
+    shards = [(par.take_shard(t, lo, hi)[0], stages) for lo, hi in bounds]
+    with mp.get_context("fork").Pool(cores) as pool:
+        pool.map(_oracle_shard_worker, shards[:1])  # warm the workers' imports
+        t0 = time.perf_counter()
+        per = pool.map(_oracle_shard_worker, shards)
+        wall = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    _oracle_stages(t, stages)
+    one = time.perf_counter() - t1
+    return {"value": round(t.n_rows / wall, 1), "unit": "session-rows/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/rq_oracle.py {'+'.join(stages)} on the full bench table, {cores} processes over "
+                      f"project shards (slowest shard {max(per):.1f} s, wall {wall:.1f} s; no cross-shard "
+                      f"recombination)",
+            "single_core": {"value": round(t.n_rows / one, 1), "cores": 1,
+                            "sample": f"the same, one process over the whole table ({one:.1f} s)"}}
 
 
 if __name__ == "__main__":
