@@ -276,12 +276,139 @@ def _copy_escape(v) -> str:
             .replace("\b", "\\b").replace("\f", "\\f").replace("\v", "\\v"))
 
 
-def from_pg_dump(path: str, corpus_csv: Optional[str] = None, project_order=None) -> Tables:
+def _dump_corpus(path: str) -> str:
+    base = os.path.dirname(os.path.abspath(path))
+    for cp in (os.path.join(base, "project_corpus_analysis.csv"),
+               os.path.join(base, "..", "processed_data", "csv", "project_corpus_analysis.csv")):
+        if os.path.exists(cp):
+            return open(cp).read()
+    return ""
+
+
+def from_pg_dump(path: str, corpus_csv: Optional[str] = None, project_order=None, native: Optional[bool] = None,
+                 threads: Optional[int] = None) -> Tables:
     """Ingest a plain-format ``pg_dump`` file (see above) into columnar ``Tables``.
 
     ``corpus_csv``: text of ``project_corpus_analysis.csv`` (``rq4a_bug.py:34``); default: that
     file next to the dump or under ``../processed_data/csv/`` as in the reference's data layout.
-    ``project_order``: see ``_from_frames`` (the database's collation)."""
+    ``project_order``: see ``_from_frames`` (the database's collation).
+    The native parser (csrc/fz_ingest.cpp, ``lib/libfzingest.so``: worker threads over the COPY
+    blocks) is used when built (``native=None``; $FZ_INGEST=python forces this module's pandas
+    path); a dump holding a cell it does not recognise (an unusual timestamp or number format) goes
+    through the pandas path, which is the reference for every cell."""
+    if corpus_csv is None:
+        corpus_csv = _dump_corpus(path)
+    if native is None:
+        native = os.environ.get("FZ_INGEST", "native") != "python" and os.path.exists(_INGEST_LIB)
+    if native:
+        t = _from_pg_dump_native(path, corpus_csv, project_order, threads)
+        if t is not None:
+            return t
+    return _from_pg_dump_pandas(path, corpus_csv, project_order)
+
+
+_INGEST_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libfzingest.so")
+_ingest = None
+
+
+def _ingest_lib():
+    global _ingest
+    if _ingest is None:
+        import ctypes as C
+        lib = C.CDLL(_INGEST_LIB)
+        P, I64 = C.c_void_p, C.c_int64
+        for name, res, args in (("fz_ingest_pg_dump", C.c_int, [C.c_char_p, C.c_int, C.POINTER(P)]),
+                                ("fz_ingest_last_error", C.c_char_p, []), ("fz_ingest_free", None, [P]),
+                                ("fz_ingest_rows", I64, [P, C.c_int]), ("fz_ingest_has", C.c_int, [P, C.c_int]),
+                                ("fz_ingest_count", I64, [P, C.c_int]),
+                                ("fz_ingest_strings", I64, [P, C.c_int, P, P]),
+                                ("fz_ingest_column", C.c_int, [P, C.c_int, P])):
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+        _ingest = lib
+    return _ingest
+
+
+def _from_pg_dump_native(path, corpus_csv, project_order, threads):
+    """libfzingest's columns as ``Tables`` (None when a cell needs the pandas parser)."""
+    import ctypes as C
+    lib = _ingest_lib()
+    h = C.c_void_p()
+    nthreads = threads or max(1, min(32, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
+                                     else os.cpu_count() or 1))
+    if lib.fz_ingest_pg_dump(path.encode(), nthreads, C.byref(h)) != 0:
+        raise ValueError(f"{path}: {lib.fz_ingest_last_error().decode(errors='replace')}")
+    try:
+        if lib.fz_ingest_count(h, -3) > 0:
+            return None
+
+        def strings(which, n=None):
+            n = lib.fz_ingest_count(h, which) if n is None else n
+            total = lib.fz_ingest_strings(h, which, None, None)
+            blob = np.empty(max(total, 1), np.uint8)
+            offs = np.empty(n + 1, np.int64)
+            lib.fz_ingest_strings(h, which, blob.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p))
+            raw = blob[:total].tobytes()
+            return raw, offs
+
+        def str_list(which):
+            raw, offs = strings(which)
+            o = offs.tolist()
+            return [raw[o[k]:o[k + 1]].decode("utf-8") for k in range(len(o) - 1)]
+
+        def col(code, n, dtype):
+            a = np.empty(n, dtype)
+            if n:
+                lib.fz_ingest_column(h, code, a.ctypes.data_as(C.c_void_p))
+            return a
+
+        nb, nc, ni, npi = (lib.fz_ingest_rows(h, k) for k in range(4))
+        projects = str_list(-1)
+        vocab = [str_list(k) for k in range(5)]
+        raw, offs = strings(-2, nb)
+        nnull = col(6, nb, np.uint8).astype(bool)
+        names = np.empty(nb, dtype=object)
+        if raw.isascii():
+            text, o = raw.decode("ascii"), offs.tolist()
+            names[:] = [None if nnull[k] else text[o[k]:o[k + 1]] for k in range(nb)]
+        else:
+            o = offs.tolist()
+            names[:] = [None if nnull[k] else raw[o[k]:o[k + 1]].decode("utf-8") for k in range(nb)]
+        t = Tables(
+            projects=projects,
+            b_project=col(0, nb, np.uint32), b_type=col(1, nb, np.uint8), b_result=col(2, nb, np.uint8),
+            b_time=col(3, nb, np.int64), b_modules=col(4, nb, np.int32), b_revisions=col(5, nb, np.int32),
+            b_name=names, modules_pool=vocab[2], revisions_pool=vocab[3],
+            c_project=col(7, nc, np.uint32), c_date=col(8, nc, np.int64), c_coverage=col(9, nc, np.float64),
+            c_coverage_valid=col(10, nc, np.uint8).astype(bool), c_covered=col(11, nc, np.int64),
+            c_covered_valid=col(12, nc, np.uint8).astype(bool), c_total=col(13, nc, np.int64),
+            c_total_valid=col(14, nc, np.uint8).astype(bool),
+            i_number=col(15, ni, np.int64), i_project=col(16, ni, np.uint32), i_rts=col(17, ni, np.int64),
+            i_status=col(18, ni, np.uint8), i_new_id=col(19, ni, np.int64),
+            pi_project=col(20, npi, np.uint32), pi_first_commit=col(21, npi, np.int64),
+            build_types=vocab[0], results=vocab[1], statuses=vocab[4], corpus_csv=corpus_csv)
+    finally:
+        lib.fz_ingest_free(h)
+    if project_order is not None:  # the database's collation: re-number the byte-ordered ids
+        if callable(project_order):
+            order = sorted(projects, key=project_order)
+        else:
+            rank = {n: k for k, n in enumerate(project_order)}
+            missing = set(projects) - set(rank)
+            if missing:
+                raise ValueError(f"project_order misses {len(missing)} project(s), e.g. {sorted(missing)[:3]}")
+            order = sorted(projects, key=rank.__getitem__)
+        pid = {n: k for k, n in enumerate(order)}
+        remap = np.array([pid[n] for n in projects], dtype=np.uint32)
+        import dataclasses
+        t = dataclasses.replace(t, projects=order, b_project=remap[t.b_project], c_project=remap[t.c_project],
+                                i_project=remap[t.i_project], pi_project=remap[t.pi_project])
+    return t
+
+
+def _from_pg_dump_pandas(path: str, corpus_csv: str, project_order=None) -> Tables:
+    """The dump through pandas' C tokenizer and this module's text converters (the reference
+    parser of every cell; see from_pg_dump)."""
     import pandas as pd
     blocks: Dict[str, List[str]] = {}
     cols: Dict[str, List[str]] = {}
@@ -331,15 +458,6 @@ def from_pg_dump(path: str, corpus_csv: Optional[str] = None, project_order=None
         return df
 
     pi = frame("project_info") if "project_info" in blocks else None
-    if corpus_csv is None:
-        base = os.path.dirname(os.path.abspath(path))
-        for cp in (os.path.join(base, "project_corpus_analysis.csv"),
-                   os.path.join(base, "..", "processed_data", "csv", "project_corpus_analysis.csv")):
-            if os.path.exists(cp):
-                corpus_csv = open(cp).read()
-                break
-        else:
-            corpus_csv = ""
     return _from_frames(frame("buildlog_data"), frame("total_coverage"), frame("issues"), pi, corpus_csv,
                         project_order)
 
