@@ -91,4 +91,6 @@ def test_errors(tmp_path):
     p = tmp_path / "bad.sql"
     p.write_text("COPY public.buildlog_data (name, project) FROM stdin;\nx\ty\n")
     with pytest.raises(ValueError, match="not terminated"):
+        store._from_pg_dump_native(str(p), "", None, 2)
+    with pytest.raises(ValueError, match="not terminated"):  # reported by the pandas path
         store.from_pg_dump(str(p), native=True)

@@ -301,7 +301,10 @@ def from_pg_dump(path: str, corpus_csv: Optional[str] = None, project_order=None
     if native is None:
         native = os.environ.get("FZ_INGEST", "native") != "python" and os.path.exists(_INGEST_LIB)
     if native:
-        t = _from_pg_dump_native(path, corpus_csv, project_order, threads)
+        try:
+            t = _from_pg_dump_native(path, corpus_csv, project_order, threads)
+        except ValueError:  # a malformed dump: the pandas path reports it (same messages as ever)
+            t = None
         if t is not None:
             return t
     return _from_pg_dump_pandas(path, corpus_csv, project_order)
