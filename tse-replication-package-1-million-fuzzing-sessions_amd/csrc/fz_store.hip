@@ -129,10 +129,17 @@ struct TimeSortOut {
     }
 };
 
+// XCD-aware: blocks b and b + 8 share an XCD (round-robin dispatch), so the grid's 8 block
+// groups each stream through one contiguous eighth of the rows - an XCD's rows in flight then come
+// from a few segments whose source ranges stay in its 4 MiB L2 (with the plain grid stride every
+// XCD touched every segment in flight and the reads went to HBM).  gridDim.x: a multiple of 8.
 __global__ __launch_bounds__(kBlock) void k_store_gather(const uint32_t *__restrict__ spos,
                                                          const uint32_t *__restrict__ rows, int64_t n,
                                                          int32_t *__restrict__ orow, GatherCols gc) {
-    for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < n; q += int64_t(gridDim.x) * kBlock) {
+    const int64_t part = (n + 7) / 8;
+    const int64_t g = blockIdx.x % 8, slot = blockIdx.x / 8, slots = gridDim.x / 8;
+    const int64_t lo = g * part, hi = lo + part < n ? lo + part : n;
+    for (int64_t q = lo + slot * kBlock + threadIdx.x; q < hi; q += slots * kBlock) {
         const int64_t sp = spos[q];
         gc.perm[q] = int32_t(rows[sp]);
         orow[q] = int32_t(q);
@@ -381,7 +388,8 @@ static void gather_table(fz_ctx *c, const PrefixSorted &ps, int32_t *orow) {
     if (ps.n <= 0) return;
     // algorithmic bytes: spos 4 + row id 4 + columns read; perm 4 + row 4 + columns written
     ProbeScope probe(c, "store_gather", (16.0 + 2.0 * ps.gc.bytes()) * double(ps.n));
-    k_store_gather<<<grid_for(ps.n, kBlock, 8192), kBlock, 0, c->stream>>>(ps.out.spos, ps.rows, ps.n, orow, ps.gc);
+    const unsigned g = (grid_for(ps.n, kBlock, 8192) + 7u) & ~7u;
+    k_store_gather<<<g, kBlock, 0, c->stream>>>(ps.out.spos, ps.rows, ps.n, orow, ps.gc);
     FZ_LAUNCH_CHECK();
 }
 
