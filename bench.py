@@ -37,6 +37,9 @@ PROBE_KERNEL = "radix_scatter"   # headline kernel of the roofline object (DESIG
 TABLE_KERNELS = ["radix_scatter", "radix_hist", "elig_hist", "seg_time_sort", "seg_merge_sort", "filter_compact",
                  "seg_reduce"]
 STAGES = ["store", "rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"]
+# analyses run concurrently after the store build, one group per child stream (about equal GPU
+# time at config 2; at most 4 streams: GPU_MAX_HW_QUEUES is 4 per process on the box)
+GROUPS = [["rq2_count"], ["rq4b", "rq1"], ["rq3", "rq4a"], ["rq2_add"]]
 WORKLOADS = {"c2": "config2: ~1M-session synthetic table",
              "c3": "config3: 100M-row coverage-only table, 10k projects x 10k days",
              "c4": "config4: rank-statistics stress, 12 coverage series of 1e5/3e5/1e6 points, 256 levels",
@@ -65,6 +68,9 @@ def parse():
     ap.add_argument("--strong", action="store_true")
     # steps of the per-kernel probe window after the timed region (0: no table)
     ap.add_argument("--probe-steps", type=int, default=5)
+    # the analyses one after another on the engine stream (default: concurrently, one child
+    # context + HIP stream + host thread per group of analyses, after the store build)
+    ap.add_argument("--serial", action="store_true")
     return ap.parse_args()
 
 
@@ -133,16 +139,43 @@ def main():
               "rq4a": compute.rq4a_launch, "rq4b": compute.rq4b_launch}
 
     stages = [s for s in STAGES if s in args.stages.split(",")]
+    launch["rq1"] = lambda e, b: compute.rq1_launch(e, b)
+    bufs["rq1"] = rq1_bufs
+    # concurrent analyses: groups of about equal GPU time, one child engine (stream + context over
+    # the same store) and one host thread each (ctypes releases the GIL during every libfz call)
+    groups = [[n for n in g if n in stages] for g in GROUPS]
+    groups = [g for g in groups if g]
+    concurrent = not sharded and not args.serial and len(groups) > 1
+    pool = None
+    if concurrent:
+        from concurrent.futures import ThreadPoolExecutor
+        children = [eng.child() for _ in groups]
+        pool = ThreadPoolExecutor(len(groups))
+
+        def run_group(ch, names):
+            with torch.cuda.stream(ch.stream):
+                for n in names:
+                    launch[n](ch, bufs[n])
+
+    def serial_step():
+        eng.build_store()
+        for name in ("rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"):
+            if name in stages:
+                launch[name](eng, bufs[name])
 
     def step():
-        eng.build_store()
         if not sharded:
-            if "rq1" in stages:
-                compute.rq1_launch(eng, rq1_bufs)
-            for name in ("rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"):
-                if name in stages:
-                    launch[name](eng, bufs[name])
+            if not concurrent:
+                serial_step()
+                return
+            eng.join_children()  # the previous step's analyses have read the store
+            eng.build_store()
+            for ch in children:
+                ch.follow_parent()
+            for f in [pool.submit(run_group, ch, g) for ch, g in zip(children, groups)]:
+                f.result()
             return
+        eng.build_store()
         # sharded: exact RQ1 / RQ3 recombination + row gathers (tse_amd/parallel.py)
         if "rq1" in stages:
             part = par.rq1_sharded(rq1_shard, rank, world)[0]
@@ -171,18 +204,29 @@ def main():
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    eng.probe_begin(args.probe)
+    if not concurrent:
+        eng.probe_begin(args.probe)
     t0 = time.perf_counter()
     ev0.record(eng.stream)
     for _ in range(args.steps):
         step()
+    if concurrent:
+        eng.join_children()
     ev1.record(eng.stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    launches, probe_ms, probe_bytes = eng.probe_end()
+    probe_window = args.steps
+    if not concurrent:
+        launches, probe_ms, probe_bytes = eng.probe_end()
+    else:  # the probe brackets launches on the engine's own context: measure it on serial steps
+        probe_window = max(args.probe_steps, 1)
+        eng.probe_begin(args.probe)
+        for _ in range(probe_window):
+            serial_step()
+        launches, probe_ms, probe_bytes = eng.probe_end()
     dev_ms = ev0.elapsed_time(ev1)
     elapsed = wall
     rows = float(t.n_rows)
@@ -191,7 +235,7 @@ def main():
     if args.probe_steps > 0:
         eng.probe_begin(",".join(TABLE_KERNELS))
         for _ in range(args.probe_steps):
-            step()
+            serial_step() if not sharded else step()
         eng.probe_end()
         for k in TABLE_KERNELS:
             n, ms_k, b_k = eng.probe_get(k)
@@ -224,7 +268,7 @@ def main():
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.probe, args.config),
                     "kernel": args.probe,
                     "avg_launch_us": round(avg_ms * 1e3, 3), "bytes_per_launch": probe_bytes / launches,
-                    "launches_per_step": launches / args.steps, "kernels": table}
+                    "launches_per_step": launches / probe_window, "kernels": table}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(t, stages)
@@ -247,6 +291,8 @@ def main():
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    if pool is not None:
+        pool.shutdown()
     eng.close()
     if sharded:
         dist.destroy_process_group()

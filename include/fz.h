@@ -105,6 +105,11 @@ int fz_abi_version(void);
 const char *fz_last_error(void);
 /* stream: a hipStream_t (NULL = the device's null stream). */
 int fz_ctx_create(int device, void *stream, fz_ctx **out);
+/* A context that runs analyses on its own stream over `parent`'s store (built by the parent; read
+ * only): the six analyses of one store can run concurrently, one child per stream (and host
+ * thread - calls on one context are serialised by the caller).  The parent must outlive it and
+ * must not rebuild its store while a child's work is in flight (order the streams). */
+int fz_ctx_create_child(fz_ctx *parent, void *stream, fz_ctx **out);
 int fz_ctx_destroy(fz_ctx *ctx);
 /* Re-target the context to another stream (e.g. torch's current stream). */
 int fz_ctx_set_stream(fz_ctx *ctx, void *stream);

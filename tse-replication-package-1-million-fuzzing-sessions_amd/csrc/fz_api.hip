@@ -92,6 +92,32 @@ int fz_ctx_create(int device, void *stream, fz_ctx **out) {
     }
 }
 
+int fz_ctx_create_child(fz_ctx *parent, void *stream, fz_ctx **out) {
+    try {
+        if (!out || !parent) throw fz::Error(FZ_E_INVALID, "fz_ctx_create_child: null argument");
+        *out = nullptr;
+        FZ_HIP(hipSetDevice(parent->device));
+        fz_ctx *c = new fz_ctx();
+        c->device = parent->device;
+        c->stream = static_cast<hipStream_t>(stream);
+        c->parent = parent->parent ? parent->parent : parent;
+        void *h = nullptr;
+        if (hipHostMalloc(&h, 32768, hipHostMallocDefault) != hipSuccess) {
+            delete c;
+            throw fz::Error(FZ_E_DEVICE, "fz_ctx_create_child: hipHostMalloc failed");
+        }
+        c->h_pinned = static_cast<int64_t *>(h);
+        *out = c;
+        return FZ_OK;
+    } catch (const fz::Error &e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return FZ_E_INVALID;
+    }
+}
+
 int fz_ctx_destroy(fz_ctx *ctx) {
     if (!ctx) return FZ_OK;
     (void)hipSetDevice(ctx->device);

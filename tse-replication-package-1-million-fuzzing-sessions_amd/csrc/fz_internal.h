@@ -136,7 +136,6 @@ struct Store {
     View covb;    // buildlog_data, build_type = Coverage, by (project, timecreated)
     View cov;     // total_coverage by (project, date)                              queries1.py:120-129
     View issues;  // issues by (project, rts), ties in row order                    rq3:219-232
-    int64_t passes = 0;
     int64_t num_min = 0, num_max = 0;                   // issues.number range
     // eligible projects (the GROUP BY/HAVING every script starts from), computed once per load
     DevBuf elig;     // uint8 [P]
@@ -186,6 +185,10 @@ struct Probe {
 struct fz_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // a child context (fz_ctx_create_child) runs analyses on its own stream over its parent's
+    // store; everything else (arena, probe, look-back state, pinned staging) is its own
+    fz_ctx *parent = nullptr;
+    int64_t sort_passes = 0;       // radix passes run by this context (store statistics)
     fz::Arena arena;
     fz::Store store;
     fz::Probe probe;
@@ -204,6 +207,9 @@ struct fz_ctx {
 };
 
 namespace fz {
+// The store an analysis reads: the context's own, or its parent's for a child context.
+inline Store &store_of(fz_ctx *c) { return c->parent ? c->parent->store : c->store; }
+
 // RAII bracket around one launch of kernel `name` moving `bytes` algorithmic bytes, plus
 // per_count bytes for every unit of the device count *d_count (read when the scope closes, i.e.
 // after the launch, so it may be the launch's own output count).

@@ -686,7 +686,7 @@ void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64
     vals = va;
     for (int j = 0; j < pl.n; ++j)  // where each payload column ended (unmoved: the input itself)
         pl.out[j] = ppass == 0 ? const_cast<void *>(pl.in[j]) : pbuf[(ppass - 1) & 1][j];
-    c->store.passes += passes;
+    c->sort_passes += passes;
     // the passes zeroed the other buffer: it serves the next sort; with no pass nothing was zeroed
     c->os_hist_cur = passes > 0 ? 1 - c->os_hist_cur : -1;
 }

@@ -130,7 +130,7 @@ void eligibility_counts(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *c
 
 // Computed once per fz_store_build (store.elig / store.n_elig).
 void store_eligibility(fz_ctx *c) {
-    Store &s = c->store;
+    Store &s = store_of(c);
     const int64_t P = s.P;
     uint8_t *elig = s.elig.ensure<uint8_t>(P);
     int64_t *n = s.n_elig.ensure<int64_t>(1);
@@ -142,7 +142,7 @@ void store_eligibility(fz_ctx *c) {
 // Every RQ script starts from this set (rq1:144-152, rq2_count:272-280, rq2_add:20-27, rq3:222-226,
 // rq4a:68-80, rq4b:164-181 - the same GROUP BY/HAVING), so the store computes it once per load.
 void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count) {
-    const Store &s = c->store;
+    const Store &s = store_of(c);
     const int64_t P = s.P;
     const uint8_t *src = s.elig.as<uint8_t>();
     const int64_t *n = s.n_elig.as<int64_t>();
@@ -384,7 +384,7 @@ void rq1_finish(fz_ctx *c, int64_t threshold, const int64_t *iter_total, const i
 }
 
 void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_ext *ext_in, const fz_rq1_out *o) {
-    Store &s = c->store;
+    Store &s = store_of(c);
     FZ_CHECK(s.built, "fz_rq1: call fz_store_build first");
     FZ_CHECK(o && o->counts && o->eligible && o->iter_total && o->iter_detected && o->matched_issue &&
                  o->matched_build && o->late,

@@ -107,7 +107,7 @@ void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_i
 }
 
 void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
-    Store &s = c->store;
+    Store &s = store_of(c);
     FZ_CHECK(s.built, "fz_rq2_count: call fz_store_build first");
     FZ_CHECK(o && o->counts && o->scalars && o->eligible && o->raw_n && o->n_trend && o->sw_w && o->sw_p && o->corr &&
                  o->session_offsets && o->session_values && o->average_trend && o->median_trend &&
@@ -255,7 +255,7 @@ __device__ inline int64_t first_row_on_day(const int64_t *ctime, const int32_t *
 }
 
 void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
-    Store &s = c->store;
+    Store &s = store_of(c);
     FZ_CHECK(s.built, "fz_rq2_add: call fz_store_build first");
     FZ_CHECK(o && o->counts && o->eligible && o->row_project && o->row_first_build && o->row_end_build &&
                  o->row_start_build && o->row_cov_i && o->row_cov_i1 && o->diff_total && o->diff_coverage &&

@@ -83,7 +83,7 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
                const double *non_pct, int64_t NC, const int64_t *d_nn, fz_describe *describe, double *tests);
 
 void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
-    Store &s = c->store;
+    Store &s = store_of(c);
     FZ_CHECK(s.built, "fz_rq3: call fz_store_build first");
     FZ_CHECK(o && o->counts && o->eligible && o->det_pct && o->det_cov && o->det_tot && o->det_project &&
                  o->det_issue && o->non_pct && o->non_cov && o->non_tot && o->describe && o->tests,

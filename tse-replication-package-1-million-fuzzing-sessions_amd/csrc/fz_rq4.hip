@@ -40,7 +40,7 @@ struct FixedBeforeLimit {  // get_project_fixed_issues: Fixed*, rts < LIMIT (rq4
 static void group_members(fz_ctx *c, const fz_rq4_groups *g, const uint8_t *elig, uint8_t *member,
                           int64_t *counts4, bool missing_to_g1) {
     const uint8_t *m = g->member;
-    const int64_t P = c->store.P;
+    const int64_t P = store_of(c).P;
     per_seg(c, P, [=] __device__(int64_t p) {
         uint8_t b = 0;
         if (elig[p]) {
@@ -58,7 +58,7 @@ void rq4a_finish(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int6
                  const int64_t *g2d, const int64_t *intro, const int64_t *steps, int64_t *counts, double *sc);
 
 void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
-    Store &s = c->store;
+    Store &s = store_of(c);
     FZ_CHECK(s.built, "fz_rq4a: call fz_store_build first");
     FZ_CHECK(g && g->member && g->corpus_us, "fz_rq4a: null groups");
     FZ_CHECK(o && o->counts && o->scalars && o->eligible && o->member && o->g1_total && o->g1_det && o->g2_total &&
@@ -374,7 +374,7 @@ void rq4b_session_stats(fz_ctx *c, const double *values, const int64_t *sid, con
 }
 
 void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *o) {
-    Store &s = c->store;
+    Store &s = store_of(c);
     FZ_CHECK(s.built, "fz_rq4b: call fz_store_build first");
     FZ_CHECK(g && g->member && g->corpus_us && (g->order || g->n_order == 0), "fz_rq4b: null groups");
     FZ_CHECK(o && o->counts && o->eligible && o->member && o->c2 && o->c1 && o->g2_q && o->g1_q && o->p_bm &&

@@ -451,6 +451,7 @@ static void materialize_sorted(fz_ctx *c) {
 
 void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     FZ_CHECK(t != nullptr, "fz_store_build: tables is null");
+    FZ_CHECK(c->parent == nullptr, "fz_store_build: a child context reads its parent's store");
     FZ_CHECK(t->n_projects >= 0 && t->n_builds >= 0 && t->n_cov >= 0 && t->n_issues >= 0, "negative table size");
     FZ_CHECK(t->n_builds < (int64_t(1) << 31) && t->n_cov < (int64_t(1) << 31) && t->n_issues < (int64_t(1) << 31),
              "tables are limited to 2^31 rows per shard");
@@ -458,7 +459,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     s.built = false;
     s.t = *t;
     s.P = t->n_projects;
-    s.passes = 0;
+    c->sort_passes = 0;
     const int64_t P = s.P;
     const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
 
@@ -583,7 +584,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         stats->n_coverage_builds = n_covb;
         stats->max_fuzz_per_project = s.fuzz.max_seg;
         stats->max_cov_per_project = s.cov.max_seg;
-        stats->sort_passes = s.passes;
+        stats->sort_passes = c->sort_passes;
     }
 }
 

@@ -138,6 +138,7 @@ SIGNATURES = {
     "fz_abi_version": (C.c_int, []),
     "fz_last_error": (C.c_char_p, []),
     "fz_ctx_create": (C.c_int, [C.c_int, _P, C.POINTER(_P)]),
+    "fz_ctx_create_child": (C.c_int, [_P, _P, C.POINTER(_P)]),
     "fz_ctx_destroy": (C.c_int, [_P]),
     "fz_ctx_set_stream": (C.c_int, [_P, _P]),
     "fz_store_build": (C.c_int, [_P, C.POINTER(FzTables), C.POINTER(FzStoreStats)]),
@@ -235,7 +236,45 @@ class Engine:
         self.tables: Optional[DeviceTables] = None
         self.stats: Optional[FzStoreStats] = None
 
+    def child(self) -> "Engine":
+        """An engine for one analysis thread: its own HIP stream and fz context over THIS engine's
+        store (fz_ctx_create_child) - the analyses of one store run concurrently, one child each.
+        Its stream waits for the parent's work enqueued so far (the store build); call
+        ``join_children`` on the parent before it rebuilds the store."""
+        ch = Engine.__new__(Engine)
+        ch.torch, ch.lib, ch.device, ch.dev = self.torch, self.lib, self.device, self.dev
+        ch.stream = self.torch.cuda.Stream(device=self.dev)
+        ctx = _P()
+        _check(self.lib, self.lib.fz_ctx_create_child(self.ctx, _P(ch.stream.cuda_stream), C.byref(ctx)))
+        ch.ctx = ctx
+        ch._parent = self
+        ch._share()
+        self.__dict__.setdefault("_children", []).append(ch)
+        return ch
+
+    def follow_parent(self):
+        """(child) order this child's next work after everything enqueued on the parent stream."""
+        self.stream.wait_stream(self._parent.stream)
+        self._share()
+
+    _SHARED = ("tables", "stats", "groups")
+
+    def _share(self):
+        for k in self._SHARED:
+            if k in self._parent.__dict__:
+                setattr(self, k, getattr(self._parent, k))
+
+    def join_children(self):
+        """(parent) order the parent stream after all its children's enqueued work."""
+        for ch in self.__dict__.get("_children", []):
+            self.stream.wait_stream(ch.stream)
+
     def close(self):
+        for ch in self.__dict__.pop("_children", []):
+            ch.close()
+        parent = self.__dict__.get("_parent")
+        if parent is not None and self in parent.__dict__.get("_children", []):
+            parent._children.remove(self)
         if getattr(self, "ctx", None):
             self.lib.fz_ctx_destroy(self.ctx)
             self.ctx = None
