@@ -245,7 +245,8 @@ def main():
             table.append({"kernel": k, "launches_per_step": round(n / args.probe_steps, 2),
                           "avg_launch_us": round(ms_k / n * 1e3, 3), "bytes_per_launch": round(b_k / n),
                           "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
-                          "ms_per_step": round(ms_k / args.probe_steps, 4)})
+                          "ms_per_step": round(ms_k / args.probe_steps, 4),
+                          "traffic": pmc_traffic(k, args.config)})
     if world > 1:
         v = torch.tensor([elapsed, rows], dtype=torch.float64, device=dev)
         tmax = v[:1].clone()
@@ -300,18 +301,18 @@ def main():
 
 
 def pmc_traffic(probe, config):
-    """HBM bytes per launch of the probed kernel from the committed PMC passes (profiles/
-    *_pmc_traffic.json, written by scripts/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE
-    runs of this bench with the gfx950 FETCH_SIZE correction), or None."""
+    """HBM bytes per launch (probe scope) of a probed kernel from the committed PMC passes
+    (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.py from rocprofv3 FETCH_SIZE /
+    WRITE_SIZE runs of this bench with the gfx950 FETCH_SIZE correction; newest first), or None."""
     import glob
-    kern = {"radix_scatter": "k_onesweep<"}.get(probe, probe)  # the radix pass kernel (both variants)
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if d.get("kernel_match") == kern and d.get("config") == config:
-            return round(float(d["traffic_bytes_per_launch"]))
+        k = d.get("kernels", {}).get(probe)
+        if k and d.get("config") == config:
+            return round(float(k["traffic_bytes_per_launch"]))
     return None
 
 
