@@ -14,6 +14,8 @@
 namespace fz {
 
 constexpr int kChunk = 2048;
+constexpr int kRedItems = kChunk / kBlock;  // elements per thread of one chunk
+static_assert(kChunk % kBlock == 0, "chunk shape");
 
 struct Segs {
     int64_t S = 0;                 // number of segments
@@ -84,11 +86,26 @@ __global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, const int6
         DD acc[NV];
 #pragma unroll
         for (int v = 0; v < NV; ++v) acc[v] = DD{0.0, 0.0};
-        for (int64_t i = b + threadIdx.x; i < e; i += kBlock) {
-            double x[NV];
-            f(i, seg, x);
+        // a chunk is at most kRedItems elements per thread: every element's loads are issued
+        // before the first add (one memory round trip per chunk, not kRedItems dependent ones);
+        // the per-thread addition order (i, i + kBlock, ...) is unchanged
+        for (int64_t i0 = b + threadIdx.x; i0 < e; i0 += int64_t(kBlock) * kRedItems) {
+            double x[kRedItems][NV];
 #pragma unroll
-            for (int v = 0; v < NV; ++v) acc[v] = dd_add_d(acc[v], x[v]);
+            for (int u = 0; u < kRedItems; ++u) {
+                const int64_t i = i0 + int64_t(u) * kBlock;
+                if (i < e) {
+                    f(i, seg, x[u]);
+                } else {
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) x[u][v] = 0.0;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kRedItems; ++u)
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+                    if (i0 + int64_t(u) * kBlock < e) acc[v] = dd_add_d(acc[v], x[u][v]);
         }
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
