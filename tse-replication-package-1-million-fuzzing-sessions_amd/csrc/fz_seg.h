@@ -153,6 +153,48 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum(int64_t S, const int64_t *__
     }
 }
 
+// Segments with very many chunks (a single 1e8-value sample has ~5e4): one wave per segment would
+// add them one lane-stride at a time (~1 ms).  Instead G workgroups per segment each fold a slice
+// of its chunks into one double-double partial (part2[s][g][v]), and k_seg_sum folds the G
+// partials per segment (implicit map, cps = G).
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_seg_fold(int64_t S, const int64_t *__restrict__ chunk_off, int64_t cps,
+                                                     int G, const double *__restrict__ part,
+                                                     double *__restrict__ part2, const int32_t *__restrict__ list,
+                                                     const int64_t *__restrict__ d_ln) {
+    __shared__ double s_hi[4][NV], s_lo[4][NV];
+    const int64_t ns = list ? *d_ln : S;
+    const int64_t w = blockIdx.x / G;
+    const int g = int(blockIdx.x % G);
+    if (w >= ns) return;
+    const int64_t s = list ? list[w] : w;
+    const int64_t c0 = chunk_off ? chunk_off[s] : s * cps, c1 = chunk_off ? chunk_off[s + 1] : (s + 1) * cps;
+    const int64_t span = (c1 - c0 + G - 1) / G;
+    const int64_t k0 = c0 + g * span, k1 = k0 + span < c1 ? k0 + span : c1;
+    DD acc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = DD{0.0, 0.0};
+    for (int64_t k = k0 + threadIdx.x; k < k1; k += kBlock)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] = dd_add(acc[v], DD{part[(k * NV + v) * 2], part[(k * NV + v) * 2 + 1]});
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const DD r = wave_dd_sum(acc[v]);
+        if (lane_id() == 0) {
+            s_hi[wave_id()][v] = r.hi;
+            s_lo[wave_id()][v] = r.lo;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        const int v = threadIdx.x;
+        DD t{s_hi[0][v], s_lo[0][v]};
+        for (int q = 1; q < 4; ++q) t = dd_add(t, DD{s_hi[q][v], s_lo[q][v]});
+        part2[((s * G + g) * NV + v) * 2] = t.hi;
+        part2[((s * G + g) * NV + v) * 2 + 1] = t.lo;
+    }
+}
+
 // Segments of <= kTinySeg values, one thread each (sequential double-double sum).
 template <int NV, typename F>
 __global__ __launch_bounds__(kBlock) void k_tiny_reduce(const int64_t *__restrict__ offs, int64_t S, F f,
@@ -208,10 +250,25 @@ void seg_reduce(fz_ctx *c, const ChunkedSegs &cs, F f, double *out) {
     k_chunk_reduce<NV, F><<<g, kBlock, 0, c->stream>>>(cs.cm, cs.sg.offs, cs.cps, blocks, f, part, nullptr);
     FZ_LAUNCH_CHECK();
     const int64_t nsum = L.on ? L.cap[kClassNonTiny] : S;
+    const int32_t *lst = L.on ? L.ids[kClassNonTiny] : nullptr;
+    const int64_t *dln = L.on ? L.d_n + kClassNonTiny : nullptr;
+    // chunks of the longest segment (host bound): a slice of >= kSliceChunks per fold workgroup
+    constexpr int64_t kSliceChunks = 512;
+    const int64_t maxc = cs.cps > 0 ? cs.cps : (cs.sg.len_bound() + kChunk - 1) / kChunk;
+    const int64_t G = maxc > kSliceChunks ? ((maxc + kSliceChunks - 1) / kSliceChunks < 256
+                                                 ? (maxc + kSliceChunks - 1) / kSliceChunks : 256) : 1;
+    if (G > 1 && nsum * G <= (int64_t(1) << 20)) {
+        double *part2 = c->arena.get<double>(S * G * NV * 2);
+        k_seg_fold<NV><<<unsigned(nsum * G), kBlock, 0, c->stream>>>(S, cs.chunk_off, cs.cps, int(G), part, part2,
+                                                                     lst, dln);
+        FZ_LAUNCH_CHECK();
+        const unsigned gs = unsigned((nsum + 3) / 4 < 4096 ? (nsum + 3) / 4 : 4096);
+        k_seg_sum<NV><<<gs > 0 ? gs : 1, kBlock, 0, c->stream>>>(S, nullptr, G, part2, out, lst, dln);
+        FZ_LAUNCH_CHECK();
+        return;
+    }
     const unsigned gs = unsigned(L.on ? ((nsum + 3) / 4 < 4096 ? (nsum + 3) / 4 : 4096) : (S + 3) / 4);
-    k_seg_sum<NV><<<gs > 0 ? gs : 1, kBlock, 0, c->stream>>>(S, cs.chunk_off, cs.cps, part, out,
-                                                         L.on ? L.ids[kClassNonTiny] : nullptr,
-                                                         L.on ? L.d_n + kClassNonTiny : nullptr);
+    k_seg_sum<NV><<<gs > 0 ? gs : 1, kBlock, 0, c->stream>>>(S, cs.chunk_off, cs.cps, part, out, lst, dln);
     FZ_LAUNCH_CHECK();
 }
 

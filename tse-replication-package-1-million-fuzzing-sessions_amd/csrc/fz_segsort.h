@@ -31,8 +31,9 @@ struct TileMap {
     int64_t *begin = nullptr;  // tile -> first row
 };
 
-// Tiles of the segments with len > kTile (or flag[s] != 0 when flag is given: e.g. a store segment
-// whose time span does not fit the small kernel's key).  n_cap: host bound of offs[S].
+// Tiles of the segments with len > kTile, or, when flag is given, of exactly the segments with
+// flag[s] != 0 (the ones the callers' bucket sorts left: too long, skewed, or a time span that does
+// not fit their key).  n_cap: host bound of offs[S].
 TileMap big_tiles(fz_ctx *c, const int64_t *offs, int64_t S, int64_t n_cap, const uint8_t *flag);
 
 __device__ inline bool kv_less(uint64_t ka, uint32_t va, uint64_t kb, uint32_t vb) {

@@ -8,7 +8,8 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t *__restrict
                                                        const uint8_t *__restrict__ flag, int64_t *__restrict__ cnt) {
     for (int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x; s < S; s += int64_t(gridDim.x) * kBlock) {
         const int64_t len = offs[s + 1] - offs[s];
-        const bool big = len > kTile || (flag != nullptr && flag[s] != 0 && len > 0);
+        // with flags, exactly the flagged segments (the caller's bucket sorts took the others)
+        const bool big = flag != nullptr ? (flag[s] != 0 && len > 0) : len > kTile;
         cnt[s] = big ? (len + kTile - 1) / kTile : 0;
     }
 }

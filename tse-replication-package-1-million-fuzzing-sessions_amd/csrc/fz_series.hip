@@ -297,6 +297,190 @@ __global__ __launch_bounds__(kBlock) void k_seg_sort_wave(const double *__restri
     }
 }
 
+// Value bucket sort, one workgroup per segment of min_len < n <= MAXN values (the store's time
+// sort, fz_store.hip k_seg_time_bucket, over f64 values): n buckets over the segment's range
+// [lo, hi] of the order-preserving image f64_key - the bucket of key k is
+// floor((k - lo) * n / (hi - lo + 1)), monotone in k - counted with LDS atomics (the returned count
+// is the value's slot in its bucket), bucket starts by one block scan, and a value's output slot is
+// its bucket start plus the number of values of its bucket ordered before it by (key, position):
+// a total order, so equal values keep their input order (stable, like the merge sort).  O(n) work
+// for values spread over their range - coverage series and sessions - against the bitonic
+// network's O(n log^2 n) compare-exchanges with a barrier per stage.  A segment whose largest
+// bucket holds more than kValSkew values (ties, clusters) is sorted by the LDS bitonic network on
+// (key, position) inside the same workgroup (MAXN <= 4096: keys in LDS), or flagged for the
+// segmented merge sort (the 16384 class, which re-reads keys from the cache-resident column).
+constexpr int kValSkew = 32;
+template <int BS, int MAXN>
+__global__ __launch_bounds__(BS) void k_seg_val_bucket(const double *__restrict__ src, const int64_t *__restrict__ offs,
+                                                       int64_t S, int64_t min_len, double *__restrict__ out_val,
+                                                       int32_t *__restrict__ out_pos, const int32_t *__restrict__ list,
+                                                       const int64_t *__restrict__ d_ln, uint8_t *__restrict__ bigflag,
+                                                       bool flag_longer) {
+    constexpr int IPT = MAXN / BS;  // values (and buckets in the scan) per thread
+    constexpr int NW = BS / kWave;
+    constexpr bool KEYS_LDS = MAXN <= kLdsSortMax;
+    static_assert(MAXN <= 16384 && MAXN % BS == 0 && (MAXN & (MAXN - 1)) == 0, "value bucket sort shape");
+    __shared__ alignas(8) uint32_t s_cnt[MAXN + 1];  // bucket counts, then starts (+ sentinel); staging
+    __shared__ uint16_t s_pos[MAXN];      // positions in bucket order (bitonic fallback: pair positions)
+    __shared__ uint64_t s_key[KEYS_LDS ? MAXN : 1];
+    __shared__ uint64_t s_lo[NW], s_hi[NW];
+    __shared__ uint32_t s_tmp[NW], s_max[NW];
+    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
+    const int64_t ns = list ? *d_ln : S;
+    for (int64_t it = blockIdx.x; it < ns; it += gridDim.x) {
+        const int64_t s = list ? list[it] : it;
+        const int64_t b = offs[s];
+        const int64_t len = offs[s + 1] - b;
+        if (len <= min_len) continue;
+        if (len > MAXN) {
+            if (flag_longer && tid == 0) bigflag[s] = 1;
+            continue;
+        }
+        const int n = int(len);
+        uint64_t k[IPT];
+        uint64_t lo = ~0ull, hi = 0ull;
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int i = tid + m * BS;
+            k[m] = i < n ? f64_key(src[b + i]) : 0ull;
+            if (i < n) {
+                lo = k[m] < lo ? k[m] : lo;
+                hi = k[m] > hi ? k[m] : hi;
+            }
+        }
+        lo = wave_min(lo);
+        hi = wave_max(hi);
+        if (lane == 0) {
+            s_lo[w] = lo;
+            s_hi[w] = hi;
+        }
+        for (int j = tid; j < MAXN + 1; j += BS) s_cnt[j] = 0u;
+        __syncthreads();
+        lo = ~0ull;
+        hi = 0ull;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            lo = s_lo[q] < lo ? s_lo[q] : lo;
+            hi = s_hi[q] > hi ? s_hi[q] : hi;
+        }
+        const double scale = double(n) / (double(hi - lo) + 1.0);
+        uint32_t bs[IPT];  // bucket << 16 | slot in the bucket
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int i = tid + m * BS;
+            bs[m] = 0u;
+            if (i < n) {
+                uint32_t q = uint32_t(double(k[m] - lo) * scale);
+                q = q < uint32_t(n) ? q : uint32_t(n - 1);
+                bs[m] = (q << 16) | atomicAdd(&s_cnt[q], 1u);
+                if (KEYS_LDS) s_key[i] = k[m];
+            }
+        }
+        __syncthreads();
+        // bucket starts: each thread scans IPT consecutive buckets; the largest bucket decides skew
+        uint32_t sum = 0, mx = 0;
+#pragma unroll
+        for (int e = 0; e < IPT; ++e) {
+            const uint32_t ce = s_cnt[tid * IPT + e];
+            sum += ce;
+            mx = ce > mx ? ce : mx;
+        }
+        mx = wave_max(mx);
+        if (lane == 0) s_max[w] = mx;
+        uint32_t run = block_excl_scan<uint32_t, NW>(sum, s_tmp, (uint32_t *)nullptr);
+#pragma unroll
+        for (int e = 0; e < IPT; ++e) {  // (block_excl_scan's barriers ordered every read above)
+            const uint32_t ce = s_cnt[tid * IPT + e];
+            s_cnt[tid * IPT + e] = run;
+            run += ce;
+        }
+        if (tid == 0) s_cnt[MAXN] = uint32_t(n);
+        __syncthreads();
+        uint32_t gmax = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) gmax = s_max[q] > gmax ? s_max[q] : gmax;
+        if (gmax > uint32_t(kValSkew)) {
+            if constexpr (KEYS_LDS) {
+                // ties / clusters: bitonic network on (key, position), keys already in LDS
+                int np2 = 1;
+                while (np2 < n) np2 <<= 1;
+                for (int i = tid; i < np2; i += BS) {
+                    if (i >= n) s_key[i] = ~0ull;
+                    s_pos[i] = uint16_t(i);
+                }
+                __syncthreads();
+                for (int kk = 2; kk <= np2; kk <<= 1) {
+                    for (int j = kk >> 1; j > 0; j >>= 1) {
+                        for (int t = tid; t < (np2 >> 1); t += BS) {
+                            const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;
+                            const uint64_t ka = s_key[i], kb = s_key[ixj];
+                            const uint16_t pa = s_pos[i], pb = s_pos[ixj];
+                            if ((kb < ka || (kb == ka && pb < pa)) == ((i & kk) == 0)) {
+                                s_key[i] = kb;
+                                s_key[ixj] = ka;
+                                s_pos[i] = pb;
+                                s_pos[ixj] = pa;
+                            }
+                        }
+                        bitonic_stage_sync(kk, j, np2);
+                    }
+                }
+                for (int i = tid; i < n; i += BS) {
+                    out_val[b + i] = f64_from_key(s_key[i]);
+                    out_pos[b + i] = int32_t(b + s_pos[i]);
+                }
+            } else {
+                if (tid == 0) bigflag[s] = 1;
+            }
+            __syncthreads();  // LDS is reused by the next segment
+            continue;
+        }
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int i = tid + m * BS;
+            if (i < n) s_pos[s_cnt[bs[m] >> 16] + (bs[m] & 0xffffu)] = uint16_t(i);
+        }
+        __syncthreads();
+        int32_t dq[IPT];  // sorted position of value i inside the segment
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int i = tid + m * BS;
+            dq[m] = -1;
+            if (i >= n) continue;
+            const uint32_t st = s_cnt[bs[m] >> 16], en = s_cnt[(bs[m] >> 16) + 1];
+            uint32_t rank = 0;
+            for (uint32_t x = st; x < en; ++x) {
+                const int ox = s_pos[x];
+                const uint64_t kx = KEYS_LDS ? s_key[ox] : f64_key(src[b + ox]);
+                rank += (kx < k[m]) || (kx == k[m] && ox < i);
+            }
+            dq[m] = int32_t(st + rank);
+        }
+        __syncthreads();  // the rank loops' LDS reads are done: LDS is staging now
+        // coalesced output: positions, then values, staged in sorted order (u32 slots for the whole
+        // segment in the bucket counts; u64 slots in the key array, or half a segment per round in
+        // the bucket counts when the keys are not in LDS)
+#pragma unroll
+        for (int m = 0; m < IPT; ++m)
+            if (dq[m] >= 0) s_cnt[dq[m]] = uint32_t(b + tid + m * BS);
+        __syncthreads();
+        for (int q = tid; q < n; q += BS) out_pos[b + q] = int32_t(s_cnt[q]);
+        __syncthreads();
+        uint64_t *stg = KEYS_LDS ? s_key : reinterpret_cast<uint64_t *>(s_cnt);
+        constexpr int CAP = KEYS_LDS ? MAXN : MAXN / 2;
+        for (int h = 0; h < n; h += CAP) {
+#pragma unroll
+            for (int m = 0; m < IPT; ++m)
+                if (dq[m] >= h && dq[m] < h + CAP) stg[dq[m] - h] = k[m];
+            __syncthreads();
+            const int e = n - h < CAP ? n - h : CAP;
+            for (int q = tid; q < e; q += BS) out_val[b + h + q] = f64_from_key(stg[q]);
+            __syncthreads();
+        }
+        __syncthreads();  // LDS is reused by the next segment
+    }
+}
+
 // Every segment of <= kLdsSortMax values (len_bound: a host bound of the longest one); with lists,
 // each kernel walks its own size class only.
 static void launch_seg_sort_lds(fz_ctx *c, unsigned g, const double *src, const int64_t *offs, int64_t S,
@@ -349,16 +533,47 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
     out.val = c->arena.get<double>(n);
     out.pos = c->arena.get<int32_t>(n);
     if (n <= 0 || sg.S <= 0) return out;
-    const unsigned g = unsigned(sg.S < 8192 ? sg.S : 8192);
-    // segments of <= kLdsSortMax values: one workgroup each (LDS bitonic; one wave for tiny ones
-    // when there are very many segments); longer ones: the segmented merge sort (fz_segsort.h),
-    // which touches only their rows
+    // segments of <= 16384 values: one workgroup each, value bucket sort by length class (each
+    // launch skips the other classes' segments; one wave / one thread for the tiny ones when there
+    // are very many segments); longer or skewed segments of the 16384 class: the segmented merge
+    // sort (fz_segsort.h), which touches only the flagged segments' rows
+    const int64_t S = sg.S, lb = sg.len_bound();
+    const int64_t *offs = sg.offs;
     SegLists L;
-    if (sg.S > kManySegs) L = seg_lists(c, sg);
-    launch_seg_sort_lds(c, g, src, sg.offs, sg.S, sg.len_bound() < kLdsSortMax ? sg.len_bound() : kLdsSortMax,
-                        out.val, out.pos, nullptr, &L);
-    if (sg.len_bound() > kLdsSortMax)
-        sort_big_segments(c, sg.offs, sg.S, n, sg.len_bound(), nullptr, F64Key{src}, F64Sink{out.val, out.pos});
+    if (S > kManySegs) L = seg_lists(c, sg);
+    uint8_t *flag = nullptr;
+    if (lb > kLdsSortMax) {
+        flag = c->arena.get<uint8_t>(S);
+        FZ_HIP(hipMemsetAsync(flag, 0, size_t(S), c->stream));
+    }
+    auto grid = [](int64_t cap, int64_t lim) { return unsigned(cap < 1 ? 1 : (cap < lim ? cap : lim)); };
+    const bool lists = L.on;
+    const int64_t *dn = L.d_n;
+    auto class_list = [&](int k) { return lists ? L.ids[k] : nullptr; };
+    auto class_n = [&](int k) { return lists ? dn + k : nullptr; };
+    auto class_cap = [&](int k) { return lists ? L.cap[k] : S; };
+    if (lists) {
+        k_seg_sort_micro<<<grid_for(S, kBlock, 8192), kBlock, 0, c->stream>>>(src, offs, S, out.val, out.pos);
+        k_seg_sort_wave<<<grid((L.cap[kClassTiny] + 3) / 4, 8192), kBlock, 0, c->stream>>>(
+            src, offs, L.ids[kClassTiny], dn + kClassTiny, out.val, out.pos);
+        FZ_LAUNCH_CHECK();
+    }
+    k_seg_val_bucket<256, 1024><<<grid(class_cap(kClassMid), 16384), 256, 0, c->stream>>>(
+        src, offs, S, lists ? kTinySeg : 0, out.val, out.pos, class_list(kClassMid), class_n(kClassMid), flag, false);
+    FZ_LAUNCH_CHECK();
+    if (lb > 1024) {
+        k_seg_val_bucket<512, 2048><<<grid(class_cap(kClassWide), 4096), 512, 0, c->stream>>>(
+            src, offs, S, 1024, out.val, out.pos, class_list(kClassWide), class_n(kClassWide), flag, false);
+        k_seg_val_bucket<1024, kLdsSortMax><<<grid(class_cap(kClassWide), 2048), 1024, 0, c->stream>>>(
+            src, offs, S, 2048, out.val, out.pos, class_list(kClassWide), class_n(kClassWide), flag, false);
+        FZ_LAUNCH_CHECK();
+    }
+    if (lb > kLdsSortMax) {
+        k_seg_val_bucket<1024, 16384><<<grid(class_cap(kClassBig), 512), 1024, 0, c->stream>>>(
+            src, offs, S, kLdsSortMax, out.val, out.pos, class_list(kClassBig), class_n(kClassBig), flag, true);
+        FZ_LAUNCH_CHECK();
+        sort_big_segments(c, offs, S, n, lb, flag, F64Key{src}, F64Sink{out.val, out.pos});
+    }
     return out;
 }
 

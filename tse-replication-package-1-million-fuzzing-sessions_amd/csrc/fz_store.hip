@@ -6,7 +6,8 @@
 // the other columns with the keys - then every segment is sorted by time in registers (one wave
 // for <= 1024 rows, one workgroup for <= 16384: fz_regsort.h), through the segmented merge sort
 // (fz_segsort.h) when longer, with NULL timestamps last (PostgreSQL's ASC NULLS LAST) and equal
-// times in row order.  One coalesced pass then gathers the tables' columns into sorted order.
+// times in row order.  The bucket sorts write each sorted row's columns themselves (the segment's
+// rows are contiguous after the prefix passes); one pass then gathers the merge-sorted rows.
 #include "fz_device.h"
 #include "fz_internal.h"
 #include "fz_segsort.h"
@@ -117,7 +118,9 @@ struct GatherCols {
 };
 
 // What every time sort writes for sorted row q: its time (NULL restored), its project, and the
-// prefix-sorted position it came from (spos: the gather's index).
+// prefix-sorted position it came from (spos: the gather's index), or kGathered when the sort
+// gathered the row's columns itself (the bucket sorts; the merge sort leaves them to the gather).
+constexpr uint32_t kGathered = ~0u;
 struct TimeSortOut {
     int64_t *otime;
     uint32_t *oproj;
@@ -140,7 +143,9 @@ __global__ __launch_bounds__(kBlock) void k_store_gather(const uint32_t *__restr
     const int64_t g = blockIdx.x % 8, slot = blockIdx.x / 8, slots = gridDim.x / 8;
     const int64_t lo = g * part, hi = lo + part < n ? lo + part : n;
     for (int64_t q = lo + slot * kBlock + threadIdx.x; q < hi; q += slots * kBlock) {
-        const int64_t sp = spos[q];
+        const uint32_t s32 = spos[q];
+        if (s32 == kGathered) continue;  // a bucket sort wrote this row's columns
+        const int64_t sp = s32;
         gc.perm[q] = int32_t(rows[sp]);
         orow[q] = int32_t(q);
         for (int j = 0; j < gc.n; ++j) {
@@ -181,13 +186,15 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restric
                                                         const int64_t *__restrict__ offs, int64_t S, uint32_t pmask,
                                                         TimeSortOut out, unsigned long long *__restrict__ big,
                                                         uint8_t *__restrict__ bigflag, int64_t min_len,
-                                                        bool flag_longer) {
+                                                        bool flag_longer, const uint32_t *__restrict__ rows,
+                                                        int32_t *__restrict__ orow, GatherCols gc) {
     constexpr int IPT = MAXN / BS;               // rows per thread
     constexpr int EPT = (MAXN + 1 + BS - 1) / BS;  // buckets per thread in the scan
     constexpr int NW = BS / kWave;
     constexpr bool KEYS_LDS = MAXN <= 4096;
     static_assert(MAXN <= (1 << kBlkPosBits) && MAXN % BS == 0, "bucket sort shape");
-    __shared__ uint32_t s_cnt[EPT * BS + 1];  // bucket counts, then bucket starts (+ sentinel)
+    // bucket counts, then bucket starts (+ sentinel); after the ranking: u64 staging of the gather
+    __shared__ alignas(8) uint32_t s_cnt[EPT * BS + 1];
     __shared__ uint16_t s_pos[MAXN];          // rows in bucket order
     __shared__ uint64_t s_key[KEYS_LDS ? MAXN : 1];
     __shared__ int64_t s_lo[NW], s_hi[NW];
@@ -286,9 +293,11 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restric
         }
         __syncthreads();
         const uint32_t p = uint32_t(s) & pmask;
+        int32_t dq[IPT];  // sorted position of row i inside the segment
 #pragma unroll
         for (int m = 0; m < IPT; ++m) {
             const int i = tid + m * BS;
+            dq[m] = -1;
             if (i >= n) continue;
             const uint32_t st = s_cnt[bs[m] >> 16], en = s_cnt[(bs[m] >> 16) + 1];
             const uint64_t key = row_key(t[m], i);
@@ -303,7 +312,50 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restric
                 }
                 rank += kx < key;
             }
-            out.put(b + st + rank, t[m], p, b + i);
+            dq[m] = int32_t(st + rank);
+        }
+        __syncthreads();  // the rank loops' reads of s_cnt / s_pos / s_key are done: LDS is staging now
+        // The gather fused, with coalesced writes: every column of the segment goes through LDS in
+        // sorted order (row i's value to slot dq[m]), then out in sorted order - the sorted rows'
+        // time, caller row id and gathered columns; project, row id and the kGathered marker (which
+        // tells k_store_gather to skip the row) are written directly.  Staging: the key array (8-byte
+        // slots for the whole segment) or the bucket counts (half a segment per round).
+        uint64_t *stg = KEYS_LDS ? s_key : reinterpret_cast<uint64_t *>(s_cnt);
+        constexpr int CAP = KEYS_LDS ? MAXN : MAXN / 2;
+        auto emit = [&](auto val_of, auto store) {
+            for (int h = 0; h < n; h += CAP) {
+#pragma unroll
+                for (int m = 0; m < IPT; ++m)
+                    if (dq[m] >= h && dq[m] < h + CAP) stg[dq[m] - h] = val_of(m);
+                __syncthreads();
+                const int e = n - h < CAP ? n - h : CAP;
+                for (int q = tid; q < e; q += BS) store(b + h + q, stg[q]);
+                __syncthreads();
+            }
+        };
+        for (int q = tid; q < n; q += BS) {
+            out.oproj[b + q] = p;
+            out.spos[b + q] = kGathered;
+            orow[b + q] = int32_t(b + q);
+        }
+        emit([&](int m) { return uint64_t(t[m]); }, [&](int64_t q, uint64_t v) { out.otime[q] = int64_t(v); });
+        emit([&](int m) { return uint64_t(rows[b + tid + m * BS]); },
+             [&](int64_t q, uint64_t v) { gc.perm[q] = int32_t(uint32_t(v)); });
+        for (int j = 0; j < gc.n; ++j) {
+            const int sz = gc.size[j];
+            const void *src = gc.src[j];
+            void *dst = gc.dst[j];
+            emit(
+                [&](int m) -> uint64_t {
+                    const int64_t r = b + tid + m * BS;
+                    return sz == 8 ? static_cast<const uint64_t *>(src)[r]
+                                   : (sz == 4 ? static_cast<const uint32_t *>(src)[r] : static_cast<const uint8_t *>(src)[r]);
+                },
+                [&](int64_t q, uint64_t v) {
+                    if (sz == 8) static_cast<uint64_t *>(dst)[q] = v;
+                    else if (sz == 4) static_cast<uint32_t *>(dst)[q] = uint32_t(v);
+                    else static_cast<uint8_t *>(dst)[q] = uint8_t(v);
+                });
         }
         __syncthreads();  // LDS is reused by the next segment
     }
@@ -323,7 +375,8 @@ struct PrefixSorted {
     TimeSortOut out{};
 };
 static PrefixSorted sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time,
-                                    int64_t *otime, uint32_t *oproj, const GatherCols &gc, unsigned long long *big) {
+                                    int64_t *otime, uint32_t *oproj, int32_t *orow, const GatherCols &gc,
+                                    unsigned long long *big) {
     PrefixSorted ps;
     ps.n = n;
     if (n <= 0) return ps;
@@ -361,23 +414,24 @@ static PrefixSorted sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix
     ps.out = TimeSortOut{otime, oproj, c->arena.get<uint32_t>(n)};
     const uint32_t pmask = pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << pre.pbits) - 1ull);
     {
-        // algorithmic bytes: time 8 read; time 8 + project 4 + source position 4 written
-        ProbeScope probe(c, "seg_time_sort", 24.0 * double(n));
+        // algorithmic bytes: time 8 + row id 4 + columns read; time 8 + project 4 + source position 4
+        // + perm 4 + row 4 + columns written (the gather is fused into the bucket sorts)
+        ProbeScope probe(c, "seg_time_sort", (36.0 + 2.0 * ps.gc.bytes()) * double(n));
         // bucket sorts by length class (each launch skips the others' segments): <= 1024 rows one
         // 256-thread workgroup each (15 KiB of LDS: many per CU), <= 2048 512 threads, <= 4096
         // 1024 threads, <= 16384 1024 threads with the keys re-read from memory (LDS: one per CU,
         // a persistent grid); longer or clustered segments are flagged for the merge sort
         k_seg_time_bucket<256, 1024><<<unsigned(S < 16384 ? S : 16384), 256, 0, c->stream>>>(
-            time, offs, S, pmask, ps.out, big, bigflag, 0, false);
+            time, offs, S, pmask, ps.out, big, bigflag, 0, false, vals, orow, ps.gc);
         FZ_LAUNCH_CHECK();
         k_seg_time_bucket<512, 2048><<<unsigned(S < 4096 ? S : 4096), 512, 0, c->stream>>>(
-            time, offs, S, pmask, ps.out, big, bigflag, 1024, false);
+            time, offs, S, pmask, ps.out, big, bigflag, 1024, false, vals, orow, ps.gc);
         FZ_LAUNCH_CHECK();
         k_seg_time_bucket<1024, 4096><<<unsigned(S < 2048 ? S : 2048), 1024, 0, c->stream>>>(
-            time, offs, S, pmask, ps.out, big, bigflag, 2048, false);
+            time, offs, S, pmask, ps.out, big, bigflag, 2048, false, vals, orow, ps.gc);
         FZ_LAUNCH_CHECK();
         k_seg_time_bucket<1024, 16384><<<unsigned(S < 512 ? S : 512), 1024, 0, c->stream>>>(
-            time, offs, S, pmask, ps.out, big, bigflag, 4096, true);
+            time, offs, S, pmask, ps.out, big, bigflag, 4096, true, vals, orow, ps.gc);
         FZ_LAUNCH_CHECK();
     }
     return ps;
@@ -528,7 +582,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         Tab &b = tabs[k];
         b.row->ensure<int32_t>(b.n);
         pss[k] = sort_table_fast(c, b.n, b.pre, b.pbits_total, b.time, b.tm->ensure<int64_t>(b.n),
-                                 b.pr->ensure<uint32_t>(b.n), gcs[k], big3 + k);
+                                 b.pr->ensure<uint32_t>(b.n), b.row->as<int32_t>(), gcs[k], big3 + k);
     }
     auto make_views = [&]() {
         int32_t *row = s.b_row.as<int32_t>();
@@ -567,7 +621,9 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
                           StoreSink{pmask, ps.out});
         redo = true;
     }
-    for (int k = 0; k < 3; ++k) gather_table(c, pss[k], tabs[k].row->as<int32_t>());
+    // the bucket sorts gathered their segments' columns; the merge-sorted rows are gathered here
+    for (int k = 0; k < 3; ++k)
+        if (bigrows[k] > 0) gather_table(c, pss[k], tabs[k].row->as<int32_t>());
     if (redo) {  // the merged segments' projects are written now
         make_views();
         read_stats();
