@@ -37,9 +37,11 @@ PROBE_KERNEL = "radix_scatter"   # headline kernel of the roofline object (DESIG
 TABLE_KERNELS = ["radix_scatter", "radix_hist", "elig_hist", "seg_time_sort", "seg_merge_sort", "filter_compact",
                  "seg_reduce"]
 STAGES = ["store", "rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"]
-# analyses run concurrently after the store build, one group per child stream (about equal GPU
-# time at config 2; at most 4 streams: GPU_MAX_HW_QUEUES is 4 per process on the box)
-GROUPS = [["rq2_count"], ["rq4b", "rq1"], ["rq3", "rq4a"], ["rq2_add"]]
+# analyses run concurrently after the store build: the first groups on child streams, the last on
+# the engine's own stream after the store build (about equal GPU time at config 2: rq3 0.94 ms,
+# rq4b 0.74, rq2_count 0.66, rq1 + rq4a + rq2_add 0.63 of kernel time; four streams in all -
+# GPU_MAX_HW_QUEUES is 4 per process on the box, a fifth stream would share a hardware queue)
+GROUPS = [["rq3"], ["rq4b"], ["rq2_count"], ["rq1", "rq4a", "rq2_add"]]
 WORKLOADS = {"c2": "config2: ~1M-session synthetic table",
              "c3": "config3: 100M-row coverage-only table, 10k projects x 10k days",
              "c4": "config4: rank-statistics stress, 12 coverage series of 1e5/3e5/1e6 points, 256 levels",
@@ -69,8 +71,11 @@ def parse():
     # steps of the per-kernel probe window after the timed region (0: no table)
     ap.add_argument("--probe-steps", type=int, default=5)
     # the analyses one after another on the engine stream (default: concurrently, one child
-    # context + HIP stream + host thread per group of analyses, after the store build)
+    # context + HIP stream per group of analyses, after the store build)
     ap.add_argument("--serial", action="store_true")
+    # concurrent groups launched call by call from host threads instead of replaying each group's
+    # recorded HIP graph (fz_capture_begin/end, fz_graph_launch)
+    ap.add_argument("--no-graphs", action="store_true")
     return ap.parse_args()
 
 
@@ -147,10 +152,12 @@ def main():
     groups = [g for g in groups if g]
     concurrent = not sharded and not args.serial and len(groups) > 1
     pool = None
+    graphs = None
     if concurrent:
         from concurrent.futures import ThreadPoolExecutor
-        children = [eng.child() for _ in groups]
-        pool = ThreadPoolExecutor(len(groups))
+        # the last group runs on the engine itself (its stream, after the store build)
+        children = [eng.child() for _ in groups[:-1]] + [eng]
+        pool = ThreadPoolExecutor(len(groups) - 1)
 
         def run_group(ch, names):
             with torch.cuda.stream(ch.stream):
@@ -170,9 +177,15 @@ def main():
                 return
             eng.join_children()  # the previous step's analyses have read the store
             eng.build_store()
-            for ch in children:
+            for ch in children[:-1]:
                 ch.follow_parent()
-            for f in [pool.submit(run_group, ch, g) for ch, g in zip(children, groups)]:
+            if graphs is not None:
+                for gr in graphs:
+                    gr.launch()
+                return
+            futs = [pool.submit(run_group, ch, g) for ch, g in zip(children[:-1], groups[:-1])]
+            run_group(eng, groups[-1])
+            for f in futs:
                 f.result()
             return
         eng.build_store()
@@ -196,9 +209,15 @@ def main():
         if "rq3" in stages:
             par.rq3_sharded(rq3_shard, rank, world)
 
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, 1 if concurrent and not args.no_graphs else 0)):
         step()
     torch.cuda.synchronize(dev)
+    if concurrent and not args.no_graphs:
+        # record each group once (warm contexts), then every step replays the recordings
+        graphs = [ch.record(lambda e, names=g: [launch[n](e, bufs[n]) for n in names])
+                  for ch, g in zip(children, groups)]
+        step()  # one untimed replay step
+        torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -294,6 +313,8 @@ def main():
         print(json.dumps(out), flush=True)
     if pool is not None:
         pool.shutdown()
+    for gr in graphs or []:
+        gr.close()
     eng.close()
     if sharded:
         dist.destroy_process_group()

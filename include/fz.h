@@ -446,6 +446,22 @@ int fz_probe_begin(fz_ctx *ctx, const char *kernel_names);
 int fz_probe_end(fz_ctx *ctx, int64_t *launches, double *total_ms, double *algo_bytes);
 int fz_probe_get(fz_ctx *ctx, const char *kernel_name, int64_t *launches, double *total_ms, double *algo_bytes);
 
+/* ---- HIP graphs: record a context's analyses once, replay them per store build ------------- */
+/* A repeated analysis over a store rebuilt in place (same table sizes: same buffers) is a fixed
+ * sequence of launches; recording it as a HIP graph removes the per-launch host work and most of
+ * the inter-kernel gaps (config 2 is launch-latency bound: ~380 launches per step).  Between
+ * fz_capture_begin and fz_capture_end every call on ctx is recorded, not run (no host sync may
+ * occur: not fz_store_build, not fz_probe_*).  The context must be warm - the same calls made once
+ * before, so that no scratch buffer grows while recording.  The graph starts by resetting the
+ * context's look-back / radix state, so every replay is self-contained; fz_graph_launch enqueues
+ * one replay on ctx's current stream (a context on the null stream records on a private stream).
+ * Results are identical to the direct calls'. */
+typedef struct fz_graph fz_graph;
+int fz_capture_begin(fz_ctx *ctx);
+int fz_capture_end(fz_ctx *ctx, fz_graph **out);
+int fz_graph_launch(fz_ctx *ctx, fz_graph *graph);
+int fz_graph_destroy(fz_graph *graph);
+
 /* ---- primitives (exported for kernel-level tests and the roofline bench) ----------------- */
 /* Stable LSD radix sort of (key, value) pairs over key bits [0, bits).  keys/vals in place. */
 int fz_radix_sort_u64(fz_ctx *ctx, uint64_t *keys, uint32_t *vals, int64_t n, int bits);

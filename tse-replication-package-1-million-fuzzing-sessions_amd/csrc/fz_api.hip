@@ -4,6 +4,7 @@
 #include <string>
 
 #include "fz_internal.h"
+#include "fz_lookback.h"
 #include "fz_views.h"
 
 namespace fz {
@@ -33,6 +34,14 @@ void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t 
 void buildlog(fz_ctx *c, const uint8_t *text, int64_t n_bytes, const int64_t *log_offs_host, const int64_t *log_offs,
               int64_t n_logs, const fz_buildlog_out *o);
 }  // namespace fz
+
+struct fz_graph {
+    hipGraph_t graph;
+    hipGraphExec_t exec;
+    // the context's host-side look-back / radix state after one replay
+    unsigned int epoch_end;
+    int hist_end;
+};
 
 namespace {
 thread_local std::string g_err;
@@ -123,6 +132,7 @@ int fz_ctx_destroy(fz_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+    if (ctx->capture_stream) (void)hipStreamDestroy(ctx->capture_stream);
     delete ctx;
     return FZ_OK;
 }
@@ -334,6 +344,70 @@ int fz_probe_get(fz_ctx *ctx, const char *kernel_name, int64_t *launches, double
         if (total_ms) *total_ms = p.ms[size_t(k)];
         if (algo_bytes) *algo_bytes = p.bytes[size_t(k)];
     });
+}
+
+int fz_capture_begin(fz_ctx *ctx) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(!ctx->probe.active(), "fz_capture_begin: a probe window is open");
+        FZ_CHECK(!ctx->capturing, "fz_capture_begin: already recording");
+        // the null stream cannot be recorded: record on a private stream instead (the graph is not
+        // tied to the stream it was recorded on; fz_graph_launch replays it on ctx's own stream)
+        ctx->capture_saved = ctx->stream;
+        if (ctx->stream == nullptr) {
+            if (!ctx->capture_stream) FZ_HIP(hipStreamCreateWithFlags(&ctx->capture_stream, hipStreamNonBlocking));
+            ctx->stream = ctx->capture_stream;
+        }
+        const hipError_t e = hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal);
+        if (e != hipSuccess) ctx->stream = ctx->capture_saved;
+        FZ_HIP(e);
+        ctx->capturing = true;
+        // every replay starts from the same device state: a zero tile ticket (the recorded launches
+        // carry ticket bases from 0), status words with no epoch of this graph, and radix digit
+        // totals zeroed by the first recorded sort
+        fz::lookback_reset(ctx);
+        ctx->os_hist_cur = -1;
+    });
+}
+
+int fz_capture_end(fz_ctx *ctx, fz_graph **out) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(out != nullptr, "fz_capture_end: out is null");
+        *out = nullptr;
+        FZ_CHECK(ctx->capturing, "fz_capture_end: not recording");
+        hipGraph_t g = nullptr;
+        const hipError_t ec = hipStreamEndCapture(ctx->stream, &g);
+        ctx->stream = ctx->capture_saved;
+        ctx->capturing = false;
+        FZ_HIP(ec);
+        hipGraphExec_t x = nullptr;
+        const hipError_t e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+        if (e != hipSuccess) {
+            (void)hipGraphDestroy(g);
+            FZ_HIP(e);
+        }
+        // the host-side look-back / radix state a replay leaves behind (fz_graph_launch restores it,
+        // so direct calls can follow a replay); nothing ran while recording: reset the live state
+        *out = new fz_graph{g, x, ctx->os_epoch, ctx->os_hist_cur};
+        fz::lookback_reset(ctx);
+        ctx->os_hist_cur = -1;
+    });
+}
+
+int fz_graph_launch(fz_ctx *ctx, fz_graph *graph) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(graph != nullptr, "fz_graph_launch: null graph");
+        FZ_HIP(hipGraphLaunch(graph->exec, ctx->stream));
+        ctx->os_epoch = graph->epoch_end;
+        ctx->os_hist_cur = graph->hist_end;
+    });
+}
+
+int fz_graph_destroy(fz_graph *graph) {
+    if (!graph) return FZ_OK;
+    (void)hipGraphExecDestroy(graph->exec);
+    (void)hipGraphDestroy(graph->graph);
+    delete graph;
+    return FZ_OK;
 }
 
 int fz_radix_sort_u64(fz_ctx *ctx, uint64_t *keys, uint32_t *vals, int64_t n, int bits) {

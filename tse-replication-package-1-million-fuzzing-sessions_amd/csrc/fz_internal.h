@@ -194,16 +194,19 @@ struct fz_ctx {
     fz::Probe probe;
     int64_t *h_pinned = nullptr;   // small pinned host staging area (32 KiB)
     // decoupled look-back state (fz_lookback.h; single-pass scan, compaction, radix passes): status
-    // words tagged with a per-launch epoch, and a never-reset tile ticket counter whose per-launch
-    // base the host tracks
+    // words tagged with a per-launch epoch, and a tile ticket counter each launch resets itself
     fz::DevBuf os_status;          // uint64 [max words of one launch]
-    fz::DevBuf os_ticket;          // uint32 [1]
-    unsigned int os_ticket_base = 0;
+    fz::DevBuf os_ticket;          // uint32 [2] self-resetting tile counter
     unsigned int os_epoch = 0;
     // radix digit totals, two buffers used by alternate sorts: each sort's passes zero the other
     // one, so the next sort's histogram starts from zero without a memset launch
     fz::DevBuf os_hist;            // uint64 [2][kOsMaxPasses * 256]
     int os_hist_cur = -1;          // buffer of the next sort (-1: not allocated / not known zero)
+    // HIP graph recording (fz_capture_begin/end): a context on the null stream records on a
+    // private stream; the context's own stream is restored when the recording ends
+    bool capturing = false;
+    hipStream_t capture_stream = nullptr;
+    hipStream_t capture_saved = nullptr;
 };
 
 namespace fz {
@@ -320,5 +323,10 @@ struct Fill {
     unsigned char value;
 };
 void fill_batch(fz_ctx *c, std::initializer_list<Fill> regions);
+// Device-side byte fill / copy kernels on the context stream.  Used instead of hipMemsetAsync /
+// hipMemcpyAsync(D2D) on every path an fz_capture recording may contain: a recorded sequence is
+// then kernels only, replayed in stream order.
+void dev_fill(fz_ctx *c, void *p, unsigned char value, int64_t bytes);
+void dev_copy(fz_ctx *c, void *dst, const void *src, int64_t bytes);
 
 }  // namespace fz

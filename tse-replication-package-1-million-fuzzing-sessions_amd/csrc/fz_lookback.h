@@ -6,8 +6,10 @@
 // with agent-scope atomics: the payload travels inside the flag word, so no separate fence /
 // acquire is needed.  Every launch bumps a 14-bit epoch; a word from an earlier launch has another
 // epoch and reads as "not published", so the status array is never cleared between launches (only
-// when it grows or the epoch wraps).  The ticket counter is never reset either: the host tracks the
-// base each launch starts from.
+// when it grows, the epoch wraps, or a graph recording starts).  The ticket counter resets itself:
+// the workgroup that draws the launch's last ticket sets it back to 0 (every other workgroup of the
+// launch has drawn by then), so each launch starts from 0 with no host-side bookkeeping - which is
+// also what makes a recorded (HIP graph) sequence of look-back launches replayable.
 #pragma once
 
 #include "fz_device.h"
@@ -17,8 +19,7 @@ namespace fz {
 
 struct Lookback {
     uint64_t *status;      // [words] status words of this launch
-    unsigned int *ticket;  // never-reset tile counter
-    unsigned int base;     // ticket value at this launch's first tile
+    unsigned int *ticket;  // self-resetting tile counter (0 between launches)
     uint64_t epoch;        // epoch << 48
 };
 
@@ -27,10 +28,17 @@ constexpr uint64_t kLbVal = (1ull << 48) - 1ull, kLbEpochMask = ((1ull << 14) - 
 
 // Host: prepare `words` status words for one launch (call lookback_end(c, tiles) after it).
 Lookback lookback_begin(fz_ctx *c, int64_t words);
-inline void lookback_end(fz_ctx *c, int64_t tiles) { c->os_ticket_base += unsigned(tiles); }
+inline void lookback_end(fz_ctx *, int64_t) {}
+// Enqueue a reset of the ticket and the status words (device) and of the host base / epoch.
+void lookback_reset(fz_ctx *c);
 
-// Thread 0 of a workgroup: this workgroup's tile index.
-__device__ inline unsigned int lb_take_tile(const Lookback &lb) { return atomicAdd(lb.ticket, 1u) - lb.base; }
+// Thread 0 of a workgroup: this workgroup's tile index (in start order); the last tile of the
+// launch (ntiles workgroups) resets the counter for the next launch.
+__device__ inline unsigned int lb_take_tile(unsigned int *ticket, unsigned int ntiles) {
+    const unsigned int t = atomicAdd(ticket, 1u);
+    if (t == ntiles - 1u) atomicExch(ticket, 0u);
+    return t;
+}
 
 __device__ inline bool lb_ready(uint64_t w, uint64_t epoch) { return (w & kLbEpochMask) == epoch && (w & kLbFlags); }
 

@@ -1,6 +1,8 @@
 // Device-wide primitives: exclusive scan, stable LSD radix sort, min/max, segment offsets,
 // numpy-compatible describe.  All launches go to the context stream; scratch comes from the arena.
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 
 #include "fz_device.h"
 #include "fz_internal.h"
@@ -51,6 +53,27 @@ void fill_batch(fz_ctx *c, std::initializer_list<Fill> regions) {
     }
     if (f.n == 0) return;
     k_fill_batch<<<grid_for((most + 7) / 8, kBlock, 1024), kBlock, 0, c->stream>>>(f);
+    FZ_LAUNCH_CHECK();
+}
+
+__global__ __launch_bounds__(kBlock) void k_copy_bytes(unsigned char *__restrict__ dst,
+                                                       const unsigned char *__restrict__ src, int64_t nb) {
+    if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 7) == 0) {
+        const int64_t n8 = nb >> 3;
+        for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n8; i += int64_t(gridDim.x) * kBlock)
+            reinterpret_cast<uint64_t *>(dst)[i] = reinterpret_cast<const uint64_t *>(src)[i];
+        for (int64_t i = (n8 << 3) + int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nb; i += int64_t(gridDim.x) * kBlock)
+            dst[i] = src[i];
+    } else {
+        for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nb; i += int64_t(gridDim.x) * kBlock)
+            dst[i] = src[i];
+    }
+}
+void dev_fill(fz_ctx *c, void *p, unsigned char value, int64_t bytes) { fill_batch(c, {{p, bytes, value}}); }
+void dev_copy(fz_ctx *c, void *dst, const void *src, int64_t bytes) {
+    if (bytes <= 0) return;
+    k_copy_bytes<<<grid_for((bytes + 7) / 8, kBlock, 4096), kBlock, 0, c->stream>>>(
+        static_cast<unsigned char *>(dst), static_cast<const unsigned char *>(src), bytes);
     FZ_LAUNCH_CHECK();
 }
 
@@ -162,22 +185,47 @@ __global__ __launch_bounds__(kScan1Threads) void k_scan_single(const int64_t *__
     if (total && tid == 0) *total = tot;
 }
 
+// FZ_TRACE=1: host-side trace of the look-back / radix bookkeeping (graph-recording diagnostics)
+static bool trace_on() {
+    static const bool on = std::getenv("FZ_TRACE") != nullptr;
+    return on;
+}
+
 Lookback lookback_begin(fz_ctx *c, int64_t words) {
     if (c->os_status.cap < size_t(words < 1 ? 1 : words) * 8) {
         uint64_t *st = c->os_status.ensure<uint64_t>(words);
-        FZ_HIP(hipMemsetAsync(st, 0, c->os_status.cap, c->stream));
+        dev_fill(c, st, 0, int64_t(c->os_status.cap));
         c->os_epoch = 0;
     }
     if (c->os_ticket.cap == 0) {
-        FZ_HIP(hipMemsetAsync(c->os_ticket.ensure<unsigned int>(1), 0, 4, c->stream));
-        c->os_ticket_base = 0;
+        dev_fill(c, c->os_ticket.ensure<unsigned int>(2), 0, 8);
     }
     if (++c->os_epoch == (1u << 14)) {  // epoch wrap: clear the status words once
-        FZ_HIP(hipMemsetAsync(c->os_status.ptr, 0, c->os_status.cap, c->stream));
+        dev_fill(c, c->os_status.ptr, 0, int64_t(c->os_status.cap));
         c->os_epoch = 1;
     }
-    return Lookback{c->os_status.as<uint64_t>(), c->os_ticket.as<unsigned int>(), c->os_ticket_base,
-                    uint64_t(c->os_epoch) << 48};
+    if (trace_on())
+        std::fprintf(stderr, "[fz] ctx %p lookback words %lld epoch %u status %p cap %zu\n", (void *)c,
+                     (long long)words, c->os_epoch, c->os_status.ptr, c->os_status.cap);
+    return Lookback{c->os_status.as<uint64_t>(), c->os_ticket.as<unsigned int>(), uint64_t(c->os_epoch) << 48};
+}
+
+// Zero the tile ticket and every status word of the context (one kernel: a graph recording starts
+// with it, so each replay finds no status word carrying one of its recorded epochs).
+__global__ __launch_bounds__(kBlock) void k_lb_reset(unsigned int *__restrict__ ticket, uint64_t *__restrict__ status,
+                                                     int64_t words) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && ticket) *ticket = 0u;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < words; i += int64_t(gridDim.x) * kBlock)
+        status[i] = 0ull;
+}
+
+void lookback_reset(fz_ctx *c) {
+    const int64_t words = int64_t(c->os_status.cap / 8);
+    if (!c->os_ticket.cap && !words) return;
+    k_lb_reset<<<grid_for(words, kBlock, 2048), kBlock, 0, c->stream>>>(
+        c->os_ticket.cap ? c->os_ticket.as<unsigned int>() : nullptr, c->os_status.as<uint64_t>(), words);
+    FZ_LAUNCH_CHECK();
+    c->os_epoch = 0;
 }
 
 // Single-pass exclusive scan: 4096-element tiles, tile prefixes by decoupled look-back
@@ -193,7 +241,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_lookback(const int64_t *__restr
     __shared__ int64_t s_prefix;
     __shared__ unsigned int s_tile;
     const int tid = threadIdx.x;
-    if (tid == 0) s_tile = lb_take_tile(lb);
+    if (tid == 0) s_tile = lb_take_tile(lb.ticket, gridDim.x);
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t base = tile * kLbTile;
@@ -234,7 +282,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_lookback(const int64_t *__restr
 
 void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, int64_t *out_total) {
     if (n <= 0) {
-        if (out_total) FZ_HIP(hipMemsetAsync(out_total, 0, sizeof(int64_t), c->stream));
+        if (out_total) dev_fill(c, out_total, 0, sizeof(int64_t));
         return;
     }
     if (n > kScanChunk && n <= kScan1Max) {
@@ -390,7 +438,7 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const uint64_t *__restric
                                                      uint64_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
                                                      int64_t n, int shift, const unsigned long long *__restrict__ ghist,
                                                      uint64_t *__restrict__ status, unsigned int *__restrict__ ticket,
-                                                     unsigned int ticket_base, uint64_t epoch,
+                                                     uint64_t epoch,
                                                      unsigned long long *__restrict__ gsum,
                                                      unsigned long long *__restrict__ next_hist,
                                                      RadixPayload pl) {
@@ -406,7 +454,7 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const uint64_t *__restric
 
     const int tid = threadIdx.x;
     const int w = wave_id(), lane = lane_id();
-    if (tid == 0) s_tile = atomicAdd(ticket, 1u) - ticket_base;
+    if (tid == 0) s_tile = lb_take_tile(ticket, gridDim.x);
     const bool dig = tid < kRadix;  // threads [0, 256) own one digit each after the ranking
     if (next_hist && blockIdx.x == 0)  // the next sort's digit totals start from zero
         for (int i = tid; i < kOsMaxPasses * kRadix; i += kOsBlock) next_hist[i] = 0ull;
@@ -589,8 +637,8 @@ void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int 
     uint32_t *v = vals;
     radix_sort_pairs_swap(c, k, v, n, bits);
     if (k != keys) {
-        FZ_HIP(hipMemcpyAsync(keys, k, size_t(n) * sizeof(uint64_t), hipMemcpyDeviceToDevice, c->stream));
-        if (vals) FZ_HIP(hipMemcpyAsync(vals, v, size_t(n) * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+        dev_copy(c, keys, k, n * int64_t(sizeof(uint64_t)));
+        if (vals) dev_copy(c, vals, v, n * int64_t(sizeof(uint32_t)));
     }
 }
 
@@ -608,9 +656,12 @@ void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64
     constexpr int64_t kHistWords = kOsMaxPasses * kRadix;
     if (c->os_hist_cur < 0) {  // first sort of the context (or after a sort that ran no pass)
         unsigned long long *h2 = c->os_hist.ensure<unsigned long long>(2 * kHistWords);
-        FZ_HIP(hipMemsetAsync(h2, 0, sizeof(unsigned long long) * 2 * kHistWords, c->stream));
+        dev_fill(c, h2, 0, int64_t(sizeof(unsigned long long)) * 2 * kHistWords);
         c->os_hist_cur = 0;
     }
+    if (trace_on())
+        std::fprintf(stderr, "[fz] ctx %p radix n %lld bits %d hist_cur %d hist %p\n", (void *)c, (long long)n, bits,
+                     c->os_hist_cur, c->os_hist.ptr);
     unsigned long long *ghist = c->os_hist.as<unsigned long long>() + c->os_hist_cur * kHistWords;
     unsigned long long *next_hist = c->os_hist.as<unsigned long long>() + (1 - c->os_hist_cur) * kHistWords;
     const int64_t ngroups = (nb + kOsGroup - 1) / kOsGroup;
@@ -624,10 +675,13 @@ void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64
     }
     // Constant-digit passes are identity permutations.  Finding them needs a host round trip, which
     // stalls the stream for longer than a pass over a few million keys takes: only large sorts
-    // (>= 4 M keys, where one pass costs ~0.1 ms or more) skip them.
+    // (>= 4 M keys, where one pass costs ~0.1 ms or more) skip them - not while a graph is being
+    // recorded (no host round trip can happen then: every pass is recorded).
     bool need[kOsMaxPasses];
     for (int p = 0; p < npass; ++p) need[p] = true;
-    if (n >= (int64_t(1) << 22)) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    FZ_HIP(hipStreamIsCapturing(c->stream, &cap));
+    if (n >= (int64_t(1) << 22) && cap == hipStreamCaptureStatusNone) {
         unsigned long long *hh = reinterpret_cast<unsigned long long *>(c->h_pinned);
         FZ_HIP(hipMemcpyAsync(hh, ghist, sizeof(unsigned long long) * npass * kRadix, hipMemcpyDeviceToHost,
                               c->stream));
@@ -661,7 +715,7 @@ void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64
             ProbeScope ps(c, "radix_scatter", ((vals ? 24.0 : 16.0) + 2.0 * pl.bytes()) * double(n));
 #define FZ_OS_LAUNCH(V, PL)                                                                                   \
     k_onesweep<V, PL><<<unsigned(nb), kOsBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, \
-                                                             lb.status, lb.ticket, lb.base, lb.epoch, gsum + p * gwords, \
+                                                             lb.status, lb.ticket, lb.epoch, gsum + p * gwords, \
                                                              next_hist, step)
             if (pl.n > 0) {
                 if (vals)

@@ -116,7 +116,7 @@ static void eligibility(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *c
         k_elig_sum<<<unsigned((P + kWave - 1) / kWave), kBlock, 0, c->stream>>>(part, nb, P, counts, elig, n_elig);
     } else {
         if (!counts) counts = c->arena.get<int32_t>(P);
-        FZ_HIP(hipMemsetAsync(counts, 0, size_t(P) * 4, c->stream));
+        dev_fill(c, counts, 0, P * 4);
         k_elig_atomic<<<grid_for(t->n_cov, kBlock, 2048), kBlock, 0, c->stream>>>(
             t->c_project, t->c_date, t->c_coverage, t->c_valid, t->n_cov, limit, counts);
         k_elig_sum<<<unsigned((P + kWave - 1) / kWave), kBlock, 0, c->stream>>>(nullptr, 0, P, counts, elig, n_elig);
@@ -134,7 +134,7 @@ void store_eligibility(fz_ctx *c) {
     const int64_t P = s.P;
     uint8_t *elig = s.elig.ensure<uint8_t>(P);
     int64_t *n = s.n_elig.ensure<int64_t>(1);
-    FZ_HIP(hipMemsetAsync(n, 0, 8, c->stream));
+    dev_fill(c, n, 0, 8);
     eligibility(c, &s.t, kLimitUs, nullptr, elig, n);
 }
 

@@ -82,7 +82,7 @@ __global__ void k_session_keys(const int64_t *__restrict__ sid, int64_t n, uint6
 void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_ids, int64_t n, int64_t S,
                        int64_t max_len, double *average, double *median, double *pcts, int64_t *n_ge100) {
     hipStream_t st = c->stream;
-    FZ_HIP(hipMemsetAsync(n_ge100, 0, 8, st));
+    dev_fill(c, n_ge100, 0, 8);
     uint64_t *key = c->arena.get<uint64_t>(n);
     uint32_t *idx = c->arena.get<uint32_t>(n);
     if (n > 0) {
@@ -117,8 +117,7 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     const int64_t P = s.P;
     const int64_t M = s.cov.max_seg;  // longest possible trend
     const int64_t NC = s.cov.n;
-    hipStream_t st = c->stream;
-    FZ_HIP(hipMemsetAsync(o->counts, 0, FZ_RQ2C_NCOUNTS * 8, st));
+    dev_fill(c, o->counts, 0, FZ_RQ2C_NCOUNTS * 8);
 
     eligible_projects(c, o->eligible, o->counts + FZ_RQ2C_ELIGIBLE);
     TmpView V, T;
@@ -184,7 +183,7 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     Segs ses{M, o->session_offsets, NC, P};  // a session holds at most one value per project
     session_stats(c, sv, ses, reinterpret_cast<const int32_t *>(sid), o->average_trend, o->median_trend,
                   o->dist_percentiles, counts + FZ_RQ2C_GE100);
-    FZ_HIP(hipMemcpyAsync(o->dist_mean, o->average_trend, size_t(M > 0 ? M : 1) * 8, hipMemcpyDeviceToDevice, st));
+    dev_copy(c, o->dist_mean, o->average_trend, (M > 0 ? M : 1) * 8);
 
     // tests on the median trend (one segment of K values)
     double *sc = o->scalars;

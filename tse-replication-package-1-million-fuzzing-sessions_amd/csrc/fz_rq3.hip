@@ -90,9 +90,8 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
              "fz_rq3: null output buffer");
     const fz_tables &t = s.t;
     const int64_t P = s.P, NI = s.issues.n, NC = s.cov.n;
-    hipStream_t st = c->stream;
     int64_t *counts = o->counts;
-    FZ_HIP(hipMemsetAsync(counts, 0, FZ_RQ3_NCOUNTS * 8, st));
+    dev_fill(c, counts, 0, FZ_RQ3_NCOUNTS * 8);
     eligible_projects(c, o->eligible, counts + FZ_RQ3_ELIGIBLE);
 
     TmpView I, F, CB, TC;

@@ -384,9 +384,8 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
     const fz_tables &t = s.t;
     const int64_t P = s.P, M = s.cov.max_seg, NC = s.cov.n;
     const int64_t MM = M > 0 ? M : 1;
-    hipStream_t st = c->stream;
     int64_t *counts = o->counts;
-    FZ_HIP(hipMemsetAsync(counts, 0, FZ_RQ4B_NCOUNTS * 8, st));
+    dev_fill(c, counts, 0, FZ_RQ4B_NCOUNTS * 8);
     int64_t *scratch = c->arena.get<int64_t>(4);
     eligible_projects(c, o->eligible, scratch);
     group_members(c, g, o->eligible, o->member, counts + FZ_RQ4B_G1, false);

@@ -78,7 +78,7 @@ TileMap big_tiles(fz_ctx *c, const int64_t *offs, int64_t S, int64_t n_cap, cons
     int64_t *toff = c->arena.get<int64_t>(S + 1);
     k_tile_count<<<grid_for(S), kBlock, 0, c->stream>>>(offs, S, flag, cnt);
     FZ_LAUNCH_CHECK();
-    FZ_HIP(hipMemsetAsync(cnt + S, 0, 8, c->stream));
+    dev_fill(c, cnt + S, 0, 8);
     scan_exclusive_i64(c, cnt, toff, S + 1, tm.d_n);
     k_tile_fill<<<grid_for(tm.cap, kBlock, 4096), kBlock, 0, c->stream>>>(offs, S, toff, tm);
     FZ_LAUNCH_CHECK();

@@ -85,7 +85,7 @@ SegLists seg_lists(fz_ctx *c, const Segs &sg) {
     L.cap[kClassNonTiny] = bound(kTinySeg);
     L.d_n = c->arena.get<int64_t>(kNumClasses);
     for (int k = 0; k < kNumClasses; ++k) L.ids[k] = c->arena.get<int32_t>(L.cap[k]);
-    FZ_HIP(hipMemsetAsync(L.d_n, 0, kNumClasses * 8, c->stream));
+    dev_fill(c, L.d_n, 0, kNumClasses * 8);
     if (S > 0) {
         k_seg_classes<<<grid_for(S, kBlock, 2048), kBlock, 0, c->stream>>>(sg.offs, S, L);
         FZ_LAUNCH_CHECK();
@@ -129,7 +129,7 @@ ChunkedSegs chunked(fz_ctx *c, const Segs &sg) {
     cm.end = c->arena.get<int64_t>(cm.cap);
     cs.chunk_off = c->arena.get<int64_t>(sg.S + 1);
     int64_t *cnt = c->arena.get<int64_t>(sg.S + 1);
-    FZ_HIP(hipMemsetAsync(cnt, 0, size_t(sg.S + 1) * 8, c->stream));
+    dev_fill(c, cnt, 0, (sg.S + 1) * 8);
     if (sg.S > 0) {
         k_chunk_count<<<grid_for(sg.S), kBlock, 0, c->stream>>>(sg.offs, sg.S, many ? kTinySeg : -1, cnt);
         FZ_LAUNCH_CHECK();
@@ -449,8 +449,9 @@ __global__ __launch_bounds__(BS) void k_seg_val_bucket(const double *__restrict_
             if (i >= n) continue;
             const uint32_t st = s_cnt[bs[m] >> 16], en = s_cnt[(bs[m] >> 16) + 1];
             uint32_t rank = 0;
-            for (uint32_t x = st; x < en; ++x) {
+            for (uint32_t x = st; en - st > 1 && x < en; ++x) {  // (alone in its bucket: rank 0)
                 const int ox = s_pos[x];
+                if (ox == i) continue;
                 const uint64_t kx = KEYS_LDS ? s_key[ox] : f64_key(src[b + ox]);
                 rank += (kx < k[m]) || (kx == k[m] && ox < i);
             }
@@ -544,7 +545,7 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
     uint8_t *flag = nullptr;
     if (lb > kLdsSortMax) {
         flag = c->arena.get<uint8_t>(S);
-        FZ_HIP(hipMemsetAsync(flag, 0, size_t(S), c->stream));
+        dev_fill(c, flag, 0, S);
     }
     auto grid = [](int64_t cap, int64_t lim) { return unsigned(cap < 1 ? 1 : (cap < lim ? cap : lim)); };
     const bool lists = L.on;

@@ -302,8 +302,10 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restric
             const uint32_t st = s_cnt[bs[m] >> 16], en = s_cnt[(bs[m] >> 16) + 1];
             const uint64_t key = row_key(t[m], i);
             uint32_t rank = 0;
-            for (uint32_t x = st; x < en; ++x) {
+            // (a row alone in its bucket - the common case for evenly spread times - reads nothing)
+            for (uint32_t x = st; en - st > 1 && x < en; ++x) {
                 const int ox = s_pos[x];
+                if (ox == i) continue;
                 uint64_t kx;
                 if (KEYS_LDS) {
                     kx = s_key[ox];
@@ -406,7 +408,7 @@ static PrefixSorted sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix
     k_prefix_offsets<<<grid_for(n > S + 1 ? n : S + 1, kBlock, 4096), kBlock, 0, c->stream>>>(keys, n, S, offs);
     FZ_LAUNCH_CHECK();
     uint8_t *bigflag = c->arena.get<uint8_t>(S);
-    FZ_HIP(hipMemsetAsync(bigflag, 0, size_t(S), c->stream));
+    dev_fill(c, bigflag, 0, S);
     ps.S = S;
     ps.offs = offs;
     ps.rows = vals;
@@ -523,7 +525,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     const int64_t ns[1] = {t->n_issues};
     store_eligibility(c);
     unsigned long long *tcnt = c->arena.get<unsigned long long>(2);
-    FZ_HIP(hipMemsetAsync(tcnt, 0, 16, c->stream));
+    dev_fill(c, tcnt, 0, 16);
     if (t->n_builds > 0) {
         k_count_types<<<grid_for(t->n_builds, kBlock * 8, 512), kBlock, 0, c->stream>>>(t->b_type, t->n_builds, tcnt);
         FZ_LAUNCH_CHECK();
@@ -576,7 +578,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     // big3[k]: rows of table k in segments left to the merge sort, big3[3 + k]: the longest such
     // segment (one zeroing for all six counters)
     unsigned long long *big3 = c->arena.get<unsigned long long>(6);
-    FZ_HIP(hipMemsetAsync(big3, 0, 6 * 8, c->stream));
+    dev_fill(c, big3, 0, 6 * 8);
     PrefixSorted pss[3];
     for (int k = 0; k < 3; ++k) {
         Tab &b = tabs[k];

@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
     __shared__ int64_t s_prefix;
     __shared__ unsigned int s_tile;
     const int tid = threadIdx.x;
-    if (tid == 0) s_tile = lb_take_tile(lb);
+    if (tid == 0) s_tile = lb_take_tile(lb.ticket, gridDim.x);
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t base = tile * kFcTile;

@@ -164,6 +164,10 @@ SIGNATURES = {
     "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),
     "fz_probe_end": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "fz_probe_get": (C.c_int, [_P, C.c_char_p, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "fz_capture_begin": (C.c_int, [_P]),
+    "fz_capture_end": (C.c_int, [_P, C.POINTER(_P)]),
+    "fz_graph_launch": (C.c_int, [_P, _P]),
+    "fz_graph_destroy": (C.c_int, [_P]),
     "fz_radix_sort_u64": (C.c_int, [_P, _P, _P, _I64, C.c_int]),
     "fz_describe_f64": (C.c_int, [_P, _P, _I64, C.POINTER(FzDescribe)]),
     "fz_eligibility_count": (C.c_int, [_P, C.POINTER(FzTables), _I64, _P]),
@@ -221,6 +225,21 @@ class DeviceTables:
         return self.host.n_rows
 
 
+class Graph:
+    """A recorded analysis sequence of one engine (Engine.record)."""
+
+    def __init__(self, eng, handle):
+        self.eng, self.handle = eng, handle
+
+    def launch(self):
+        _check(self.eng.lib, self.eng.lib.fz_graph_launch(self.eng.ctx, self.handle))
+
+    def close(self):
+        if self.handle:
+            self.eng.lib.fz_graph_destroy(self.handle)
+            self.handle = None
+
+
 class Engine:
     """One engine per GPU: a ``fz_ctx`` bound to torch's current stream on ``device``."""
 
@@ -263,6 +282,19 @@ class Engine:
         for k in self._SHARED:
             if k in self._parent.__dict__:
                 setattr(self, k, getattr(self._parent, k))
+
+    def record(self, fn) -> "Graph":
+        """Record ``fn(self)`` - a fixed sequence of analysis launches on this engine (no host
+        sync; warm: run once before) - as a HIP graph (fz_capture_begin/end); ``Graph.launch()``
+        replays it on this engine's stream."""
+        _check(self.lib, self.lib.fz_capture_begin(self.ctx))
+        try:
+            fn(self)
+        finally:
+            g = _P()
+            rc = self.lib.fz_capture_end(self.ctx, C.byref(g))
+        _check(self.lib, rc)
+        return Graph(self, g)
 
     def join_children(self):
         """(parent) order the parent stream after all its children's enqueued work."""
