@@ -29,19 +29,35 @@ struct Prefix {
     }
 };
 
+// Fuzzing / Coverage build counts: 16 type bytes per thread per load, one pair of partial counts
+// per workgroup (no atomics; the host adds the partials after the prologue's one sync).
+constexpr int kTypeBlocks = 192;
 __global__ __launch_bounds__(kBlock) void k_count_types(const uint8_t *__restrict__ type, int64_t n,
-                                                        unsigned long long *__restrict__ cnt) {
+                                                        int64_t *__restrict__ part) {
     __shared__ int64_t s_tmp[4];
     int64_t a = 0, b = 0;
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    const int64_t n16 = (reinterpret_cast<uintptr_t>(type) & 15) == 0 ? n >> 4 : 0;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n16; i += int64_t(gridDim.x) * kBlock) {
+        const uint4 w = reinterpret_cast<const uint4 *>(type)[i];
+        const uint32_t v[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t byte = (v[k] >> (8 * j)) & 0xffu;
+                a += byte == 0u;
+                b += byte == 1u;
+            }
+    }
+    for (int64_t i = (n16 << 4) + int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
         a += type[i] == 0;
         b += type[i] == 1;
     }
     a = block_sum(a, s_tmp);
     b = block_sum(b, s_tmp);
     if (threadIdx.x == 0) {
-        atomicAdd(&cnt[0], (unsigned long long)a);
-        atomicAdd(&cnt[1], (unsigned long long)b);
+        part[2 * blockIdx.x] = a;
+        part[2 * blockIdx.x + 1] = b;
     }
 }
 
@@ -192,6 +208,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restric
     constexpr int EPT = (MAXN + 1 + BS - 1) / BS;  // buckets per thread in the scan
     constexpr int NW = BS / kWave;
     constexpr bool KEYS_LDS = MAXN <= 4096;
+    constexpr bool FUSE = MAXN > 4096;  // this class gathers its segments' columns itself
     static_assert(MAXN <= (1 << kBlkPosBits) && MAXN % BS == 0, "bucket sort shape");
     // bucket counts, then bucket starts (+ sentinel); after the ranking: u64 staging of the gather
     __shared__ alignas(8) uint32_t s_cnt[EPT * BS + 1];
@@ -316,48 +333,86 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restric
             }
             dq[m] = int32_t(st + rank);
         }
+        if constexpr (!FUSE) {
+            // short segments: time, project and source position written to the sorted slot (the
+            // segment's few KiB stay in L2); k_store_gather moves the other columns afterwards
+#pragma unroll
+            for (int m = 0; m < IPT; ++m)
+                if (dq[m] >= 0) out.put(b + dq[m], t[m], p, b + tid + m * BS);
+            __syncthreads();  // LDS is reused by the next segment
+            continue;
+        }
         __syncthreads();  // the rank loops' reads of s_cnt / s_pos / s_key are done: LDS is staging now
-        // The gather fused, with coalesced writes: every column of the segment goes through LDS in
-        // sorted order (row i's value to slot dq[m]), then out in sorted order - the sorted rows'
-        // time, caller row id and gathered columns; project, row id and the kGathered marker (which
-        // tells k_store_gather to skip the row) are written directly.  Staging: the key array (8-byte
-        // slots for the whole segment) or the bucket counts (half a segment per round).
+        // Long segments (config 3: 10k rows) - the gather fused, with coalesced writes: every column
+        // of the segment goes through LDS in sorted order (row i's value to slot dq[m]), then out in
+        // sorted order - the sorted rows' time, caller row id and gathered columns; project, row id and
+        // the kGathered marker (which tells k_store_gather to skip the row) are written directly.
+        // Staging: the key array (8-byte slots for the whole segment) or the bucket counts (half a
+        // segment per round).  (A separate gather would re-read the 250 KB segment at random from
+        // HBM; the short classes' segments stay in L2 and gather faster than they stage.)
         uint64_t *stg = KEYS_LDS ? s_key : reinterpret_cast<uint64_t *>(s_cnt);
         constexpr int CAP = KEYS_LDS ? MAXN : MAXN / 2;
-        auto emit = [&](auto val_of, auto store) {
+        // stage one column (x[m]: row i's value) through LDS in sorted order, write it coalesced
+        auto emit = [&](const uint64_t *x, auto store) {
             for (int h = 0; h < n; h += CAP) {
 #pragma unroll
                 for (int m = 0; m < IPT; ++m)
-                    if (dq[m] >= h && dq[m] < h + CAP) stg[dq[m] - h] = val_of(m);
+                    if (dq[m] >= h && dq[m] < h + CAP) stg[dq[m] - h] = x[m];
                 __syncthreads();
                 const int e = n - h < CAP ? n - h : CAP;
                 for (int q = tid; q < e; q += BS) store(b + h + q, stg[q]);
                 __syncthreads();
             }
         };
+        // the columns: the prefix-sorted caller row ids (-> perm), then the gathered ones; column
+        // j + 1's loads are issued before column j is staged (their latency hides behind it)
+        const int nc = 1 + gc.n;
+        auto src_of = [&](int j) { return j == 0 ? static_cast<const void *>(rows) : gc.src[j - 1]; };
+        auto size_of = [&](int j) { return j == 0 ? 4 : gc.size[j - 1]; };
+        auto load = [&](int j, uint64_t *x) {
+            const void *src = src_of(j);
+            const int sz = size_of(j);
+#pragma unroll
+            for (int m = 0; m < IPT; ++m) {
+                const int64_t r = b + tid + m * BS;
+                x[m] = dq[m] < 0 ? 0ull
+                                 : (sz == 8 ? static_cast<const uint64_t *>(src)[r]
+                                            : (sz == 4 ? static_cast<const uint32_t *>(src)[r]
+                                                       : static_cast<const uint8_t *>(src)[r]));
+            }
+        };
+        // (the 16-rows-per-thread class has no registers for a second column in flight)
+        constexpr bool kPrefetch = IPT <= 8;
+        uint64_t xa[IPT], xb[kPrefetch ? IPT : 1];
+        load(0, xa);
         for (int q = tid; q < n; q += BS) {
             out.oproj[b + q] = p;
             out.spos[b + q] = kGathered;
             orow[b + q] = int32_t(b + q);
         }
-        emit([&](int m) { return uint64_t(t[m]); }, [&](int64_t q, uint64_t v) { out.otime[q] = int64_t(v); });
-        emit([&](int m) { return uint64_t(rows[b + tid + m * BS]); },
-             [&](int64_t q, uint64_t v) { gc.perm[q] = int32_t(uint32_t(v)); });
-        for (int j = 0; j < gc.n; ++j) {
-            const int sz = gc.size[j];
-            const void *src = gc.src[j];
-            void *dst = gc.dst[j];
-            emit(
-                [&](int m) -> uint64_t {
-                    const int64_t r = b + tid + m * BS;
-                    return sz == 8 ? static_cast<const uint64_t *>(src)[r]
-                                   : (sz == 4 ? static_cast<const uint32_t *>(src)[r] : static_cast<const uint8_t *>(src)[r]);
-                },
-                [&](int64_t q, uint64_t v) {
-                    if (sz == 8) static_cast<uint64_t *>(dst)[q] = v;
-                    else if (sz == 4) static_cast<uint32_t *>(dst)[q] = uint32_t(v);
-                    else static_cast<uint8_t *>(dst)[q] = uint8_t(v);
-                });
+        {
+            uint64_t tt[IPT];
+#pragma unroll
+            for (int m = 0; m < IPT; ++m) tt[m] = uint64_t(t[m]);
+            emit(tt, [&](int64_t q, uint64_t v) { out.otime[q] = int64_t(v); });
+        }
+        for (int j = 0; j < nc; ++j) {
+            if constexpr (kPrefetch) {
+                if (j + 1 < nc) load(j + 1, xb);
+            } else if (j > 0) {
+                load(j, xa);
+            }
+            void *dst = j == 0 ? static_cast<void *>(gc.perm) : gc.dst[j - 1];
+            const int sz = size_of(j);
+            emit(xa, [&](int64_t q, uint64_t v) {
+                if (sz == 8) static_cast<uint64_t *>(dst)[q] = v;
+                else if (sz == 4) static_cast<uint32_t *>(dst)[q] = uint32_t(v);
+                else static_cast<uint8_t *>(dst)[q] = uint8_t(v);
+            });
+            if constexpr (kPrefetch) {
+#pragma unroll
+                for (int m = 0; m < IPT; ++m) xa[m] = xb[m];
+            }
         }
         __syncthreads();  // LDS is reused by the next segment
     }
@@ -416,9 +471,10 @@ static PrefixSorted sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix
     ps.out = TimeSortOut{otime, oproj, c->arena.get<uint32_t>(n)};
     const uint32_t pmask = pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << pre.pbits) - 1ull);
     {
-        // algorithmic bytes: time 8 + row id 4 + columns read; time 8 + project 4 + source position 4
-        // + perm 4 + row 4 + columns written (the gather is fused into the bucket sorts)
-        ProbeScope probe(c, "seg_time_sort", (36.0 + 2.0 * ps.gc.bytes()) * double(n));
+        // algorithmic bytes: time 8 read; time 8 + project 4 + source position 4 written (the long
+        // class also moves row id 4 + columns in, perm 4 + row 4 + columns out: counted by the
+        // store_gather probe's bytes for the short classes instead)
+        ProbeScope probe(c, "seg_time_sort", 24.0 * double(n));
         // bucket sorts by length class (each launch skips the others' segments): <= 1024 rows one
         // 256-thread workgroup each (15 KiB of LDS: many per CU), <= 2048 512 threads, <= 4096
         // 1024 threads, <= 16384 1024 threads with the keys re-read from memory (LDS: one per CU,
@@ -432,7 +488,7 @@ static PrefixSorted sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix
         k_seg_time_bucket<1024, 4096><<<unsigned(S < 2048 ? S : 2048), 1024, 0, c->stream>>>(
             time, offs, S, pmask, ps.out, big, bigflag, 2048, false, vals, orow, ps.gc);
         FZ_LAUNCH_CHECK();
-        k_seg_time_bucket<1024, 16384><<<unsigned(S < 512 ? S : 512), 1024, 0, c->stream>>>(
+        k_seg_time_bucket<1024, 16384><<<unsigned(S < 256 ? S : 256), 1024, 0, c->stream>>>(
             time, offs, S, pmask, ps.out, big, bigflag, 4096, true, vals, orow, ps.gc);
         FZ_LAUNCH_CHECK();
     }
@@ -524,18 +580,24 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     const int64_t *cols[1] = {t->i_number};
     const int64_t ns[1] = {t->n_issues};
     store_eligibility(c);
-    unsigned long long *tcnt = c->arena.get<unsigned long long>(2);
-    dev_fill(c, tcnt, 0, 16);
+    const int tblk = int(grid_for(t->n_builds, kBlock * 16, kTypeBlocks));
+    int64_t *tpart = c->arena.get<int64_t>(2 * tblk);
     if (t->n_builds > 0) {
-        k_count_types<<<grid_for(t->n_builds, kBlock * 8, 512), kBlock, 0, c->stream>>>(t->b_type, t->n_builds, tcnt);
+        k_count_types<<<tblk, kBlock, 0, c->stream>>>(t->b_type, t->n_builds, tpart);
         FZ_LAUNCH_CHECK();
+    } else {
+        dev_fill(c, tpart, 0, 16);
     }
-    // the counts ride along with the min/max read-back (one stream sync for both)
-    FZ_HIP(hipMemcpyAsync(c->h_pinned + 16, tcnt, 16, hipMemcpyDeviceToHost, c->stream));
+    // the partial counts ride along with the min/max read-back (one stream sync for both)
+    FZ_HIP(hipMemcpyAsync(c->h_pinned + 64, tpart, size_t(2 * tblk) * 8, hipMemcpyDeviceToHost, c->stream));
     minmax_i64_to_host(c, cols, ns, 1, mm);  // syncs the stream
     s.num_min = mm[0];
     s.num_max = mm[1];
-    const int64_t n_fuzz = c->h_pinned[16], n_covb = c->h_pinned[17];
+    int64_t n_fuzz = 0, n_covb = 0;
+    for (int k = 0; k < (t->n_builds > 0 ? tblk : 1); ++k) {
+        n_fuzz += c->h_pinned[64 + 2 * k];
+        n_covb += c->h_pinned[64 + 2 * k + 1];
+    }
 
     // the three tables: (prefix = [type|]project) LSD passes, then each segment sorted by time in LDS
     struct Tab {
@@ -623,9 +685,9 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
                           StoreSink{pmask, ps.out});
         redo = true;
     }
-    // the bucket sorts gathered their segments' columns; the merge-sorted rows are gathered here
-    for (int k = 0; k < 3; ++k)
-        if (bigrows[k] > 0) gather_table(c, pss[k], tabs[k].row->as<int32_t>());
+    // the long-segment bucket sort gathered its segments' columns; the short classes' and the
+    // merge-sorted rows are gathered here (rows marked kGathered are skipped)
+    for (int k = 0; k < 3; ++k) gather_table(c, pss[k], tabs[k].row->as<int32_t>());
     if (redo) {  // the merged segments' projects are written now
         make_views();
         read_stats();
