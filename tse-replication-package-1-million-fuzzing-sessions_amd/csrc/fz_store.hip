@@ -29,14 +29,17 @@ struct Prefix {
     }
 };
 
-// Fuzzing / Coverage build counts: 16 type bytes per thread per load, one pair of partial counts
-// per workgroup (no atomics; the host adds the partials after the prologue's one sync).
-constexpr int kTypeBlocks = 192;
-__global__ __launch_bounds__(kBlock) void k_count_types(const uint8_t *__restrict__ type, int64_t n,
-                                                        int64_t *__restrict__ part) {
-    __shared__ int64_t s_tmp[4];
+// The store prologue in one launch: per-workgroup Fuzzing / Coverage build counts (16 type bytes
+// per thread per load) and issue-number min / max (NULL skipped), written as partials
+// part[4 * block + {0, 1, 2, 3}] that the host reduces after the prologue's single copy and sync -
+// no atomics, no initialisation launch.
+constexpr int kProBlocks = 192;
+__global__ __launch_bounds__(kBlock) void k_store_prologue(const uint8_t *__restrict__ type, int64_t nb,
+                                                           const int64_t *__restrict__ num, int64_t ni,
+                                                           int64_t *__restrict__ part) {
+    __shared__ int64_t s_tmp[4], s_lo[4], s_hi[4];
     int64_t a = 0, b = 0;
-    const int64_t n16 = (reinterpret_cast<uintptr_t>(type) & 15) == 0 ? n >> 4 : 0;
+    const int64_t n16 = (reinterpret_cast<uintptr_t>(type) & 15) == 0 ? nb >> 4 : 0;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n16; i += int64_t(gridDim.x) * kBlock) {
         const uint4 w = reinterpret_cast<const uint4 *>(type)[i];
         const uint32_t v[4] = {w.x, w.y, w.z, w.w};
@@ -49,15 +52,35 @@ __global__ __launch_bounds__(kBlock) void k_count_types(const uint8_t *__restric
                 b += byte == 1u;
             }
     }
-    for (int64_t i = (n16 << 4) + int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    for (int64_t i = (n16 << 4) + int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nb; i += int64_t(gridDim.x) * kBlock) {
         a += type[i] == 0;
         b += type[i] == 1;
     }
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < ni; i += int64_t(gridDim.x) * kBlock) {
+        const int64_t v = num[i];
+        if (v == FZ_TS_NULL) continue;
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
     a = block_sum(a, s_tmp);
     b = block_sum(b, s_tmp);
+    lo = wave_min(lo);
+    hi = wave_max(hi);
+    if (lane_id() == 0) {
+        s_lo[wave_id()] = lo;
+        s_hi[wave_id()] = hi;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        part[2 * blockIdx.x] = a;
-        part[2 * blockIdx.x + 1] = b;
+        for (int w = 1; w < 4; ++w) {
+            lo = s_lo[w] < lo ? s_lo[w] : lo;
+            hi = s_hi[w] > hi ? s_hi[w] : hi;
+        }
+        part[4 * blockIdx.x] = a;
+        part[4 * blockIdx.x + 1] = b;
+        part[4 * blockIdx.x + 2] = lo;
+        part[4 * blockIdx.x + 3] = hi;
     }
 }
 
@@ -488,7 +511,9 @@ static PrefixSorted sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix
         k_seg_time_bucket<1024, 4096><<<unsigned(S < 2048 ? S : 2048), 1024, 0, c->stream>>>(
             time, offs, S, pmask, ps.out, big, bigflag, 2048, false, vals, orow, ps.gc);
         FZ_LAUNCH_CHECK();
-        k_seg_time_bucket<1024, 16384><<<unsigned(S < 256 ? S : 256), 1024, 0, c->stream>>>(
+        // (a workgroup per CU at most; fewer when the table is too small to hold many long segments)
+        const int64_t g16 = n / 16384 < 8 ? 8 : (n / 16384 > 256 ? 256 : n / 16384);
+        k_seg_time_bucket<1024, 16384><<<unsigned(S < g16 ? S : g16), 1024, 0, c->stream>>>(
             time, offs, S, pmask, ps.out, big, bigflag, 4096, true, vals, orow, ps.gc);
         FZ_LAUNCH_CHECK();
     }
@@ -576,28 +601,25 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
 
     // one host round trip: the issue-number range (RQ1's ROW_NUMBER dedup key) + build-type counts
-    int64_t mm[2];
-    const int64_t *cols[1] = {t->i_number};
-    const int64_t ns[1] = {t->n_issues};
     store_eligibility(c);
-    const int tblk = int(grid_for(t->n_builds, kBlock * 16, kTypeBlocks));
-    int64_t *tpart = c->arena.get<int64_t>(2 * tblk);
-    if (t->n_builds > 0) {
-        k_count_types<<<tblk, kBlock, 0, c->stream>>>(t->b_type, t->n_builds, tpart);
-        FZ_LAUNCH_CHECK();
-    } else {
-        dev_fill(c, tpart, 0, 16);
+    const int64_t nwork = t->n_builds > t->n_issues ? t->n_builds : t->n_issues;
+    const int pblk = int(grid_for(nwork, kBlock * 16, kProBlocks));
+    int64_t *ppart = c->arena.get<int64_t>(4 * pblk);
+    k_store_prologue<<<pblk, kBlock, 0, c->stream>>>(t->b_type, t->n_builds, t->i_number, t->n_issues, ppart);
+    FZ_LAUNCH_CHECK();
+    FZ_HIP(hipMemcpyAsync(c->h_pinned + 64, ppart, size_t(4 * pblk) * 8, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    int64_t n_fuzz = 0, n_covb = 0, nlo = INT64_MAX, nhi = INT64_MIN;
+    for (int k = 0; k < pblk; ++k) {
+        const int64_t *q = c->h_pinned + 64 + 4 * k;
+        n_fuzz += q[0];
+        n_covb += q[1];
+        nlo = q[2] < nlo ? q[2] : nlo;
+        nhi = q[3] > nhi ? q[3] : nhi;
     }
-    // the partial counts ride along with the min/max read-back (one stream sync for both)
-    FZ_HIP(hipMemcpyAsync(c->h_pinned + 64, tpart, size_t(2 * tblk) * 8, hipMemcpyDeviceToHost, c->stream));
-    minmax_i64_to_host(c, cols, ns, 1, mm);  // syncs the stream
-    s.num_min = mm[0];
-    s.num_max = mm[1];
-    int64_t n_fuzz = 0, n_covb = 0;
-    for (int k = 0; k < (t->n_builds > 0 ? tblk : 1); ++k) {
-        n_fuzz += c->h_pinned[64 + 2 * k];
-        n_covb += c->h_pinned[64 + 2 * k + 1];
-    }
+    // (no non-NULL number: the empty range min = INT64_MAX > max = INT64_MIN, as the old read-back gave)
+    s.num_min = nlo;
+    s.num_max = nhi;
 
     // the three tables: (prefix = [type|]project) LSD passes, then each segment sorted by time in LDS
     struct Tab {
