@@ -76,6 +76,8 @@ def parse():
     # concurrent groups launched call by call from host threads instead of replaying each group's
     # recorded HIP graph (fz_capture_begin/end, fz_graph_launch)
     ap.add_argument("--no-graphs", action="store_true")
+    # stream groups, e.g. "rq3|rq4b|rq2_count|rq1,rq4a,rq2_add" (the last on the engine's stream)
+    ap.add_argument("--groups", default="|".join(",".join(g) for g in GROUPS))
     return ap.parse_args()
 
 
@@ -148,7 +150,7 @@ def main():
     bufs["rq1"] = rq1_bufs
     # concurrent analyses: groups of about equal GPU time, one child engine (stream + context over
     # the same store) and one host thread each (ctypes releases the GIL during every libfz call)
-    groups = [[n for n in g if n in stages] for g in GROUPS]
+    groups = [[n for n in g.split(",") if n in stages] for g in args.groups.split("|")]
     groups = [g for g in groups if g]
     concurrent = not sharded and not args.serial and len(groups) > 1
     pool = None
