@@ -42,6 +42,9 @@ STAGES = ["store", "rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"]
 # rq4b 0.74, rq2_count 0.66, rq1 + rq4a + rq2_add 0.63 of kernel time; four streams in all -
 # GPU_MAX_HW_QUEUES is 4 per process on the box, a fifth stream would share a hardware queue)
 GROUPS = [["rq3"], ["rq4b"], ["rq2_count"], ["rq1", "rq4a", "rq2_add"]]
+# RQ3 may also be split: "rq3_main" (samples) and "rq3_stats" (statistics, fz_rq3_stats_dn) in
+# different groups; the stats group's stream then waits for an event recorded after rq3_main
+AFTER = {"rq3_stats": "rq3_main"}
 WORKLOADS = {"c2": "config2: ~1M-session synthetic table",
              "c3": "config3: 100M-row coverage-only table, 10k projects x 10k days",
              "c4": "config4: rank-statistics stress, 12 coverage series of 1e5/3e5/1e6 points, 256 levels",
@@ -148,11 +151,19 @@ def main():
     stages = [s for s in STAGES if s in args.stages.split(",")]
     launch["rq1"] = lambda e, b: compute.rq1_launch(e, b)
     bufs["rq1"] = rq1_bufs
+    launch["rq3_main"], launch["rq3_stats"] = compute.rq3_main_launch, compute.rq3_stats_launch
+    bufs["rq3_main"] = bufs["rq3_stats"] = bufs["rq3"]
     # concurrent analyses: groups of about equal GPU time, one child engine (stream + context over
     # the same store) and one host thread each (ctypes releases the GIL during every libfz call)
-    groups = [[n for n in g.split(",") if n in stages] for g in args.groups.split("|")]
+    known = set(stages) | ({"rq3_main", "rq3_stats"} if "rq3" in stages else set())
+    groups = [[n for n in g.split(",") if n in known] for g in args.groups.split("|")]
     groups = [g for g in groups if g]
     concurrent = not sharded and not args.serial and len(groups) > 1
+    split = any(n in AFTER for g in groups for n in g)
+    # host launch order: groups holding a stage another group waits for come first
+    order = sorted(range(len(groups)), key=lambda i: 0 if any(n in AFTER.values() for n in groups[i]) else 1)
+    if split and (args.no_graphs or not concurrent):
+        raise SystemExit("bench: rq3_main / rq3_stats groupings need the graph path")
     pool = None
     graphs = None
     if concurrent:
@@ -182,8 +193,19 @@ def main():
             for ch in children[:-1]:
                 ch.follow_parent()
             if graphs is not None:
-                for gr in graphs:
-                    gr.launch()
+                # host order: producers' events are recorded before any stream waits on them
+                for gi in order:
+                    for need, gr, mark in graphs[gi]:
+                        if need:
+                            children[gi].stream.wait_event(events[need])
+                        gr.launch()
+                        if mark:
+                            events[mark].record(children[gi].stream)
+                return
+            if split:  # warm-up before the recordings: the groups one after another (dependencies)
+                for gi in order:
+                    run_group(children[gi], groups[gi])
+                    torch.cuda.synchronize(dev)
                 return
             futs = [pool.submit(run_group, ch, g) for ch, g in zip(children[:-1], groups[:-1])]
             run_group(eng, groups[-1])
@@ -215,9 +237,29 @@ def main():
         step()
     torch.cuda.synchronize(dev)
     if concurrent and not args.no_graphs:
-        # record each group once (warm contexts), then every step replays the recordings
-        graphs = [ch.record(lambda e, names=g: [launch[n](e, bufs[n]) for n in names])
-                  for ch, g in zip(children, groups)]
+        # record each group once (warm contexts), then every step replays the recordings; a group
+        # is cut into pieces at a stage that must follow another group's stage (AFTER) and after a
+        # stage another group waits for - one graph per piece, events between them
+        marks = set(AFTER.values())
+        events = {m: torch.cuda.Event() for m in marks}
+        graphs = []
+        for ch, g in zip(children, groups):
+            pieces, cur = [], []
+            for n in g:
+                if n in AFTER and cur:
+                    pieces.append((None if not pieces else pieces[-1][3], cur, None, None))
+                    cur = []
+                cur.append(n)
+                if n in marks:
+                    pieces.append((None, cur, n, None))
+                    cur = []
+            if cur:
+                pieces.append((None, cur, None, None))
+            rec = []
+            for _, names, mark, _ in pieces:
+                need = AFTER.get(names[0])
+                rec.append((need, ch.record(lambda e, names=names: [launch[n](e, bufs[n]) for n in names]), mark))
+            graphs.append(rec)
         step()  # one untimed replay step
         torch.cuda.synchronize(dev)
     if world > 1:
@@ -315,8 +357,9 @@ def main():
         print(json.dumps(out), flush=True)
     if pool is not None:
         pool.shutdown()
-    for gr in graphs or []:
-        gr.close()
+    for rec in graphs or []:
+        for _, gr, _ in rec:
+            gr.close()
     eng.close()
     if sharded:
         dist.destroy_process_group()

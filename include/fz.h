@@ -302,6 +302,13 @@ int fz_rq3_ex(fz_ctx *ctx, uint32_t flags, const fz_rq3_out *out);
  * left unset unless both samples are non-empty). */
 int fz_rq3_stats(fz_ctx *ctx, const double *det_pct, const int64_t *det_tot, int64_t n_det, const double *non_pct,
                  int64_t n_non, fz_describe *describe, double *tests);
+/* The same with the sample lengths on the device (e.g. &counts[FZ_RQ3_DETECTED] and
+ * &counts[FZ_RQ3_NON_DETECTED] of an fz_rq3_ex(FZ_RQ3_SKIP_STATS) call) and host capacities
+ * det_cap >= *d_det, non_cap >= *d_non: no host round trip, so the statistics can run on another
+ * stream (or graph) after the sample extraction. */
+int fz_rq3_stats_dn(fz_ctx *ctx, const double *det_pct, const int64_t *det_tot, int64_t det_cap, const int64_t *d_det,
+                    const double *non_pct, int64_t non_cap, const int64_t *d_non, fz_describe *describe,
+                    double *tests);
 
 /* ---- RQ4 inputs: data/processed_data/csv/project_corpus_analysis.csv (user_corpus.py:225-233) ---
  * Parsed on the host (it is a ~1k-row CSV) into per-project columns, independent of eligibility:

@@ -72,3 +72,44 @@ def test_graph_replay_matches_direct(engine_for, case):
         eng.join_children()
         torch.cuda.synchronize()
         ch.close()
+
+
+@pytest.mark.parametrize("case", goldens.CASES)
+def test_rq3_split_across_streams(engine_for, case):
+    """RQ3's sample extraction (fz_rq3_ex, FZ_RQ3_SKIP_STATS) recorded on a child, its statistics
+    (fz_rq3_stats_dn: device sample lengths) recorded on the engine's own context, ordered by an
+    event between the two streams - the bench's split grouping - equal the direct fz_rq3."""
+    eng = engine_for(case)
+    torch = eng.torch
+    want = compute.rq3(eng)
+    ch = eng.child()
+    try:
+        b = compute.rq3_buffers(eng)
+        ch.follow_parent()
+        compute.rq3_main_launch(ch, b)  # warm both contexts
+        eng.join_children()
+        compute.rq3_stats_launch(eng, b)
+        torch.cuda.synchronize()
+        assert_same(compute.rq3_collect(eng, b), want, "rq3 split (direct)")
+        g_main = ch.record(lambda e: compute.rq3_main_launch(e, b))
+        g_stats = eng.record(lambda e: compute.rq3_stats_launch(e, b))
+        ev = torch.cuda.Event()
+        try:
+            for _ in range(3):
+                _clear(b, torch)
+                eng.join_children()
+                eng.build_store()
+                ch.follow_parent()
+                g_main.launch()
+                ev.record(ch.stream)
+                eng.stream.wait_event(ev)
+                g_stats.launch()
+                torch.cuda.synchronize()
+                assert_same(compute.rq3_collect(eng, b), want, "rq3 split (replay)")
+        finally:
+            g_main.close()
+            g_stats.close()
+    finally:
+        eng.join_children()
+        torch.cuda.synchronize()
+        ch.close()

@@ -225,6 +225,17 @@ int fz_rq3_stats(fz_ctx *ctx, const double *det_pct, const int64_t *det_tot, int
     });
 }
 
+int fz_rq3_stats_dn(fz_ctx *ctx, const double *det_pct, const int64_t *det_tot, int64_t det_cap, const int64_t *d_det,
+                    const double *non_pct, int64_t non_cap, const int64_t *d_non, fz_describe *describe,
+                    double *tests) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(describe && tests && d_det && d_non && det_cap >= 0 && non_cap >= 0 &&
+                     (det_cap == 0 || (det_pct && det_tot)) && (non_cap == 0 || non_pct),
+                 "fz_rq3_stats_dn: bad arguments");
+        fz::rq3_stats(ctx, det_pct, det_tot, det_cap, d_det, non_pct, non_cap, d_non, describe, tests);
+    });
+}
+
 int fz_rq4a(fz_ctx *ctx, const fz_rq4_groups *groups, const fz_rq4a_out *out) {
     return guarded(ctx, [&] { fz::rq4a(ctx, groups, out); });
 }

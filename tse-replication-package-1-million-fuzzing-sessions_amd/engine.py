@@ -154,6 +154,7 @@ SIGNATURES = {
     "fz_rq3": (C.c_int, [_P, C.POINTER(FzRq3Out)]),
     "fz_rq3_ex": (C.c_int, [_P, C.c_uint32, C.POINTER(FzRq3Out)]),
     "fz_rq3_stats": (C.c_int, [_P, _P, _P, _I64, _P, _I64, _P, _P]),
+    "fz_rq3_stats_dn": (C.c_int, [_P, _P, _P, _I64, _P, _P, _I64, _P, _P, _P]),
     "fz_rq4a": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.POINTER(FzRq4aOut)]),
     "fz_rq4a_finish": (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P]),
     "fz_rq4b": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.POINTER(FzRq4bOut)]),

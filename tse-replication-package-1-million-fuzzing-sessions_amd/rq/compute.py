@@ -206,6 +206,21 @@ def rq3_launch(eng: E.Engine, b: OutBuffers):
     E._check(eng.lib, eng.lib.fz_rq3(eng.ctx, C.byref(b.out)))
 
 
+def rq3_main_launch(eng: E.Engine, b: OutBuffers):
+    """fz_rq3_ex without the statistics (the samples and counts only)."""
+    E._check(eng.lib, eng.lib.fz_rq3_ex(eng.ctx, E.FZ_RQ3_SKIP_STATS, C.byref(b.out)))
+
+
+def rq3_stats_launch(eng: E.Engine, b: OutBuffers):
+    """fz_rq3_stats_dn over the samples of a preceding rq3_main_launch (device lengths: may run on
+    another stream ordered after it)."""
+    fz = eng.tables.fz
+    P = lambda t, k=0: C.c_void_p(t.data_ptr() + 8 * k)  # noqa: E731
+    E._check(eng.lib, eng.lib.fz_rq3_stats_dn(eng.ctx, P(b.det_pct), P(b.det_tot), fz.n_issues,
+                                              P(b.counts, E.RQ3_DETECTED), P(b.non_pct), fz.n_cov,
+                                              P(b.counts, E.RQ3_NON_DETECTED), P(b.describe), P(b.tests)))
+
+
 RQ3_COLUMNS = ("det_pct", "det_cov", "det_tot", "det_project", "det_issue", "non_pct", "non_cov", "non_tot")
 
 
