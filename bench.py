@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -371,7 +372,11 @@ def pmc_traffic(probe, config):
     (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.py from rocprofv3 FETCH_SIZE /
     WRITE_SIZE runs of this bench with the gfx950 FETCH_SIZE correction; newest first), or None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
+
+    def version(path):  # r02v10_c2_pmc_traffic.json -> (2, 10): numeric, so v10 sorts after v6
+        m = re.match(r"r(\d+)v(\d+)_", os.path.basename(path))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=version, reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
@@ -407,39 +412,47 @@ def _oracle_stages(t, stages):
             fns[s](t)
 
 
-def _oracle_shard_worker(args):
-    t, stages = args
-    import time as _t
-    t0 = _t.perf_counter()
-    _oracle_stages(t, stages)
-    return _t.perf_counter() - t0
-
-
 def cpu_baseline(t, stages):
-    """The oracle port over the same stages on the same table: one process per host core over
-    contiguous project shards (parallel.shard_bounds; each shard's six analyses, no cross-shard
-    recombination - a lower bound on the multi-core CPU time), timed as the slowest shard; and
-    single-threaded over the whole table (`single_core`)."""
-    import multiprocessing as mp
-    from tse_amd import parallel as par
-    stages = [s for s in stages if s in ("rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b")]
-    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
-    bounds = par.shard_bounds(t, cores)
-    shards = [(par.take_shard(t, lo, hi)[0], stages) for lo, hi in bounds]
-    with mp.get_context("fork").Pool(cores) as pool:
-        pool.map(_oracle_shard_worker, shards[:1])  # warm the workers' imports
-        t0 = time.perf_counter()
-        per = pool.map(_oracle_shard_worker, shards)
-        wall = time.perf_counter() - t0
-    t1 = time.perf_counter()
-    _oracle_stages(t, stages)
-    one = time.perf_counter() - t1
-    return {"value": round(t.n_rows / wall, 1), "unit": "session-rows/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/rq_oracle.py {'+'.join(stages)} on the full bench table, {cores} processes over "
-                      f"project shards (slowest shard {max(per):.1f} s, wall {wall:.1f} s; no cross-shard "
-                      f"recombination)",
-            "single_core": {"value": round(t.n_rows / one, 1), "cores": 1,
-                            "sample": f"the same, one process over the whole table ({one:.1f} s)"}}
+    """The multi-core C++ restatement (oracle/cpu/fz_cpu.cpp: per-project index build + the same
+    analyses, OpenMP over projects / sessions) on the full bench table with the host's CPU share of
+    threads: one untimed run, then repeated runs for >= 3 s, median wall time.  Beside it: the same
+    code on one thread, and the numpy oracle (oracle/rq_oracle.py) single-threaded when the table is
+    small enough to finish in ~10 s (<= 4 M rows)."""
+    from oracle import cpu_baseline as cb
+    stages = [s for s in stages if s in cb.STAGES]
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cores = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or aff), aff))
+    host = cb.HostTables(t)
+
+    def timed(threads, min_s):
+        cb.run(host, stages, threads)  # warm: page faults, thread pool
+        walls, parts = [], []
+        t_end = time.perf_counter() + min_s
+        while len(walls) < 3 or (time.perf_counter() < t_end and len(walls) < 20):
+            t0 = time.perf_counter()
+            _, secs = cb.run(host, stages, threads)
+            walls.append(time.perf_counter() - t0)
+            parts.append(secs)
+        k = int(np.argsort(walls)[len(walls) // 2])
+        return walls[k], parts[k], len(walls)
+
+    wall, parts, reps = timed(cores, 3.0)
+    one, _, reps1 = timed(1, 2.0)
+    out = {"value": round(t.n_rows / wall, 1), "unit": "session-rows/s", "cores": cores, "kind": "port",
+           "sample": f"oracle/cpu/fz_cpu.cpp (C++17, OpenMP, {cores} threads): index build + "
+                     f"{'+'.join(stages)} on the full bench table ({t.n_rows} rows), median of {reps} runs "
+                     f"({wall * 1e3:.1f} ms; " + ", ".join(f"{k} {v * 1e3:.1f}" for k, v in parts.items() if v)
+                     + " ms)",
+           "single_core": {"value": round(t.n_rows / one, 1), "cores": 1,
+                           "sample": f"the same code on one thread, median of {reps1} runs ({one * 1e3:.1f} ms)"}}
+    if t.n_rows <= 4_000_000:
+        t1 = time.perf_counter()
+        _oracle_stages(t, stages)
+        py = time.perf_counter() - t1
+        out["numpy_oracle"] = {"value": round(t.n_rows / py, 1), "cores": 1,
+                               "sample": f"oracle/rq_oracle.py (numpy/scipy, one process) on the same table "
+                                         f"({py:.1f} s)"}
+    return out
 
 
 if __name__ == "__main__":
