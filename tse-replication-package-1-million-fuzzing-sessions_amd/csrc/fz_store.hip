@@ -85,19 +85,29 @@ __global__ __launch_bounds__(kBlock) void k_store_prologue(const uint8_t *__rest
 }
 
 
-// One workgroup: the longest segment of each of 4 views (out[0..3]) and a copy of the 6
-// merge-sort counters (out[4..9]) - one launch and one D2H copy for the host's store stats.
-struct Offs4 {
-    const int64_t *offs[4];
-    const unsigned long long *big;  // [6] merge-sort rows / longest segment per table
+// One workgroup: the four views' per-project offsets (fuzz / coverage builds / coverage / issues)
+// read off the prefix offsets - a view is a contiguous range of one table's prefixes, and the time
+// sorts (merge sort included) keep every row in its prefix's range - their longest segments
+// (out[0..3]) and a copy of the 6 merge-sort counters (out[4..9]): one launch and one D2H copy.
+struct ViewSrc {
+    const int64_t *src[4] = {};  // prefix offsets of the view's table (null: empty table)
+    int64_t first[4] = {};       // prefix of the view's project 0
+    int64_t base[4] = {};        // rows of the table before the view
+    int64_t *dst[4] = {};        // [P + 1]
+    const unsigned long long *big = nullptr;  // [6] merge-sort rows / longest segment per table
 };
-__global__ __launch_bounds__(kSortBlock) void k_store_stats(Offs4 v, int64_t P, int64_t *__restrict__ out) {
+__global__ __launch_bounds__(kSortBlock) void k_store_views(const ViewSrc v, int64_t P, int64_t *__restrict__ out) {
     __shared__ int64_t s_m[kSortBlock / kWave];
     for (int i = 0; i < 4; ++i) {
+        const int64_t *src = v.src[i];
         int64_t m = 0;
-        for (int64_t p = threadIdx.x; p < P; p += kSortBlock) {
-            const int64_t l = v.offs[i][p + 1] - v.offs[i][p];
-            m = l > m ? l : m;
+        for (int64_t p = threadIdx.x; p <= P; p += kSortBlock) {
+            const int64_t o = src ? src[v.first[i] + p] - v.base[i] : 0;
+            v.dst[i][p] = o;
+            if (src && p < P) {
+                const int64_t l = src[v.first[i] + p + 1] - src[v.first[i] + p];
+                m = l > m ? l : m;
+            }
         }
         m = wave_max(m);
         if (lane_id() == 0) s_m[wave_id()] = m;
@@ -113,21 +123,41 @@ __global__ __launch_bounds__(kSortBlock) void k_store_stats(Offs4 v, int64_t P, 
 }
 
 // ---- prefix LSD passes (moving the columns) + per-segment register sort by (time, row) -------
-__global__ __launch_bounds__(kBlock) void k_keys_prefix_rows(Prefix pre, int64_t n, uint64_t *__restrict__ keys,
-                                                             uint32_t *__restrict__ vals) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        keys[i] = pre(i);
-        vals[i] = uint32_t(i);
+// Up to three tables' (prefix, row) keys in one launch: table k's rows are [base[k], base[k + 1])
+// of the combined index.
+struct PrefixKeys {
+    Prefix pre[3];
+    uint64_t *keys[3] = {};
+    uint32_t *vals[3] = {};
+    int64_t base[4] = {0, 0, 0, 0};
+};
+__global__ __launch_bounds__(kBlock) void k_keys_prefix_rows(const PrefixKeys K) {
+    for (int64_t gi = int64_t(blockIdx.x) * kBlock + threadIdx.x; gi < K.base[3]; gi += int64_t(gridDim.x) * kBlock) {
+        const int k = gi >= K.base[2] ? 2 : (gi >= K.base[1] ? 1 : 0);
+        const int64_t i = gi - K.base[k];
+        K.keys[k][i] = K.pre[k](i);
+        K.vals[k][i] = uint32_t(i);
     }
 }
 
 // offs[s] = first position of prefix s in the prefix-sorted keys (s in [0, S]): row i starts the
 // prefixes (keys[i-1], keys[i]]; one coalesced read of the keys instead of a binary search per s.
-__global__ __launch_bounds__(kBlock) void k_prefix_offsets(const uint64_t *__restrict__ keys, int64_t n, int64_t S,
-                                                           int64_t *__restrict__ offs) {
-    const int64_t first = int64_t(keys[0]), last = int64_t(keys[n - 1]);  // n >= 1, keys < S
-    const int64_t span = n > S + 1 ? n : S + 1;
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < span; i += int64_t(gridDim.x) * kBlock) {
+// Up to three tables in one launch: table k covers [base[k], base[k + 1]) = max(n, S + 1) items.
+struct PrefixOffs {
+    const uint64_t *keys[3] = {};
+    int64_t n[3] = {0, 0, 0};
+    int64_t S[3] = {0, 0, 0};
+    int64_t *offs[3] = {};
+    int64_t base[4] = {0, 0, 0, 0};
+};
+__global__ __launch_bounds__(kBlock) void k_prefix_offsets(const PrefixOffs O) {
+    for (int64_t gi = int64_t(blockIdx.x) * kBlock + threadIdx.x; gi < O.base[3]; gi += int64_t(gridDim.x) * kBlock) {
+        const int k = gi >= O.base[2] ? 2 : (gi >= O.base[1] ? 1 : 0);
+        const int64_t i = gi - O.base[k];
+        const uint64_t *keys = O.keys[k];
+        const int64_t n = O.n[k], S = O.S[k];
+        int64_t *offs = O.offs[k];
+        const int64_t first = int64_t(keys[0]), last = int64_t(keys[n - 1]);  // n >= 1, keys < S
         if (i <= S) {
             if (i <= first) offs[i] = 0;
             else if (i > last) offs[i] = n;
@@ -171,22 +201,40 @@ struct TimeSortOut {
     }
 };
 
-// XCD-aware: blocks b and b + 8 share an XCD (round-robin dispatch), so the grid's 8 block
-// groups each stream through one contiguous eighth of the rows - an XCD's rows in flight then come
-// from a few segments whose source ranges stay in its 4 MiB L2 (with the plain grid stride every
-// XCD touched every segment in flight and the reads went to HBM).  gridDim.x: a multiple of 8.
-__global__ __launch_bounds__(kBlock) void k_store_gather(const uint32_t *__restrict__ spos,
-                                                         const uint32_t *__restrict__ rows, int64_t n,
-                                                         int32_t *__restrict__ orow, GatherCols gc) {
+// One table's gather (below) and the three tables' gathers in one launch: table k owns blocks
+// [blk[k], blk[k + 1]), each range a multiple of 8.
+struct GatherTab {
+    const uint32_t *spos = nullptr;
+    const uint32_t *rows = nullptr;
+    int64_t n = 0;
+    int32_t *orow = nullptr;
+    GatherCols gc;
+};
+struct GatherTabs {
+    GatherTab tab[3];
+    unsigned blk[4] = {0, 0, 0, 0};
+};
+
+// XCD-aware: blocks b and b + 8 share an XCD (round-robin dispatch), so a table's 8 block groups
+// each stream through one contiguous eighth of its rows - an XCD's rows in flight then come from a
+// few segments whose source ranges stay in its 4 MiB L2 (with the plain grid stride every XCD
+// touched every segment in flight and the reads went to HBM).
+__global__ __launch_bounds__(kBlock) void k_store_gather(const GatherTabs G) {
+    const unsigned bid = blockIdx.x;
+    const int k = bid >= G.blk[2] ? 2 : (bid >= G.blk[1] ? 1 : 0);
+    const GatherTab &tb = G.tab[k];
+    const GatherCols &gc = tb.gc;
+    const int64_t n = tb.n;
+    const int64_t lb = bid - G.blk[k], nblk = G.blk[k + 1] - G.blk[k];
     const int64_t part = (n + 7) / 8;
-    const int64_t g = blockIdx.x % 8, slot = blockIdx.x / 8, slots = gridDim.x / 8;
+    const int64_t g = lb % 8, slot = lb / 8, slots = nblk / 8;
     const int64_t lo = g * part, hi = lo + part < n ? lo + part : n;
     for (int64_t q = lo + slot * kBlock + threadIdx.x; q < hi; q += slots * kBlock) {
-        const uint32_t s32 = spos[q];
+        const uint32_t s32 = tb.spos[q];
         if (s32 == kGathered) continue;  // a bucket sort wrote this row's columns
         const int64_t sp = s32;
-        gc.perm[q] = int32_t(rows[sp]);
-        orow[q] = int32_t(q);
+        gc.perm[q] = int32_t(tb.rows[sp]);
+        tb.orow[q] = int32_t(q);
         for (int j = 0; j < gc.n; ++j) {
             if (gc.size[j] == 8)
                 static_cast<uint64_t *>(gc.dst[j])[q] = static_cast<const uint64_t *>(gc.src[j])[sp];
@@ -220,13 +268,26 @@ constexpr uint64_t kBlkTop = (uint64_t(1) << (64 - kBlkPosBits)) - 1;  // time f
 // does not fit the key, is flagged for the merge sort instead.  MAXN <= 4096 keeps the keys in LDS;
 // larger classes re-read them from the (prefix-sorted, cache-resident) time column.
 constexpr int kBucketSkew = 32;
+//
+// The three tables share each length class's launch: a workgroup takes combined segment gs and
+// finds its table from the bases (T.tab[k] is read in place from the kernel arguments).
+struct TimeSortTab {
+    const int64_t *time = nullptr;   // prefix-sorted times
+    const int64_t *offs = nullptr;   // [S + 1] segment offsets
+    uint32_t pmask = 0;
+    TimeSortOut out{};
+    unsigned long long *big = nullptr;  // the table's merge-sort counters
+    uint8_t *bigflag = nullptr;
+    const uint32_t *rows = nullptr;  // caller row ids in prefix order
+    int32_t *orow = nullptr;
+    GatherCols gc;
+};
+struct TimeSortTabs {
+    TimeSortTab tab[3];
+    int64_t base[4] = {0, 0, 0, 0};  // combined index of table k's first segment; base[3] = total
+};
 template <int BS, int MAXN>
-__global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restrict__ time,
-                                                        const int64_t *__restrict__ offs, int64_t S, uint32_t pmask,
-                                                        TimeSortOut out, unsigned long long *__restrict__ big,
-                                                        uint8_t *__restrict__ bigflag, int64_t min_len,
-                                                        bool flag_longer, const uint32_t *__restrict__ rows,
-                                                        int32_t *__restrict__ orow, GatherCols gc) {
+__global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, int64_t min_len, bool flag_longer) {
     constexpr int IPT = MAXN / BS;               // rows per thread
     constexpr int EPT = (MAXN + 1 + BS - 1) / BS;  // buckets per thread in the scan
     constexpr int NW = BS / kWave;
@@ -240,9 +301,17 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restric
     __shared__ int64_t s_lo[NW], s_hi[NW];
     __shared__ uint32_t s_tmp[NW], s_max[NW];
     const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
-    for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
-        const int64_t b = offs[s];
-        const int64_t len = offs[s + 1] - b;
+    for (int64_t gs = blockIdx.x; gs < T.base[3]; gs += gridDim.x) {
+        const int k = gs >= T.base[2] ? 2 : (gs >= T.base[1] ? 1 : 0);
+        const TimeSortTab &tb = T.tab[k];
+        const int64_t s = gs - T.base[k];
+        const int64_t *__restrict__ time = tb.time;
+        const TimeSortOut &out = tb.out;
+        const GatherCols &gc = tb.gc;
+        unsigned long long *big = tb.big;
+        uint8_t *bigflag = tb.bigflag;
+        const int64_t b = tb.offs[s];
+        const int64_t len = tb.offs[s + 1] - b;
         if (len <= min_len) continue;
         if (len > MAXN) {
             if (flag_longer && tid == 0) flag_big(big, bigflag, s, len);
@@ -332,7 +401,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restric
             if (i < n) s_pos[s_cnt[bs[m] >> 16] + (bs[m] & 0xffffu)] = uint16_t(i);
         }
         __syncthreads();
-        const uint32_t p = uint32_t(s) & pmask;
+        const uint32_t p = uint32_t(s) & tb.pmask;
         int32_t dq[IPT];  // sorted position of row i inside the segment
 #pragma unroll
         for (int m = 0; m < IPT; ++m) {
@@ -390,7 +459,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restric
         // the columns: the prefix-sorted caller row ids (-> perm), then the gathered ones; column
         // j + 1's loads are issued before column j is staged (their latency hides behind it)
         const int nc = 1 + gc.n;
-        auto src_of = [&](int j) { return j == 0 ? static_cast<const void *>(rows) : gc.src[j - 1]; };
+        auto src_of = [&](int j) { return j == 0 ? static_cast<const void *>(tb.rows) : gc.src[j - 1]; };
         auto size_of = [&](int j) { return j == 0 ? 4 : gc.size[j - 1]; };
         auto load = [&](int j, uint64_t *x) {
             const void *src = src_of(j);
@@ -411,7 +480,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restric
         for (int q = tid; q < n; q += BS) {
             out.oproj[b + q] = p;
             out.spos[b + q] = kGathered;
-            orow[b + q] = int32_t(b + q);
+            tb.orow[b + q] = int32_t(b + q);
         }
         {
             uint64_t tt[IPT];
@@ -441,9 +510,11 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const int64_t *__restric
     }
 }
 
-// Sorts by (prefix, time, row); adds to the (zeroed) device counter *big the rows in segments too
-// long for the register sorts (and big[3] = the longest such segment, bigflag[s] = 1): the caller
-// sorts those through the segmented merge sort, then gathers every table's columns.
+// Prefix-sorts the tables by ([type |] project, row) - the columns riding along; the keys of all
+// three and their segment offsets in one launch each - and sets up their time sort
+// (time_sort_tables, all tables at once): segments too long for the bucket sorts
+// are counted in the (zeroed) device counter *big (big[3] = the longest such segment, bigflag[s] =
+// 1) for the segmented merge sort; every table's columns are then gathered (gather_tables).
 struct PrefixSorted {
     int64_t n = 0;
     int64_t S = 0;
@@ -453,80 +524,142 @@ struct PrefixSorted {
     const int64_t *time = nullptr;   // times in (prefix, row) order
     GatherCols gc;                   // the gathered columns' sources in (prefix, row) order
     TimeSortOut out{};
+    uint32_t pmask = 0;
+    unsigned long long *big = nullptr;
+    int32_t *orow = nullptr;
 };
-static PrefixSorted sort_table_fast(fz_ctx *c, int64_t n, Prefix pre, int prefix_bits, const int64_t *time,
-                                    int64_t *otime, uint32_t *oproj, int32_t *orow, const GatherCols &gc,
-                                    unsigned long long *big) {
-    PrefixSorted ps;
-    ps.n = n;
-    if (n <= 0) return ps;
-    uint64_t *keys = c->arena.get<uint64_t>(n);
-    uint32_t *vals = c->arena.get<uint32_t>(n);
-    const unsigned g = grid_for(n, kBlock, 4096);
-    k_keys_prefix_rows<<<g, kBlock, 0, c->stream>>>(pre, n, keys, vals);
-    FZ_LAUNCH_CHECK();
-    // the prefix passes move the time column and the gathered columns with the keys (each pass's
-    // writes land in per-digit runs): the time sort and the gather then read every segment's rows
-    // from one contiguous range instead of gathering them from the heap-ordered table
-    RadixPayload pl;
-    pl.n = 1 + gc.n;
-    pl.in[0] = time;
-    pl.size[0] = 8;
-    for (int j = 0; j < gc.n; ++j) {
-        pl.in[1 + j] = gc.src[j];
-        pl.size[1 + j] = gc.size[j];
+struct TableIn {
+    int64_t n;
+    Prefix pre;
+    int prefix_bits;
+    const int64_t *time;
+    int64_t *otime;
+    uint32_t *oproj;
+    int32_t *orow;
+    GatherCols gc;
+    unsigned long long *big;
+};
+static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) {
+    PrefixKeys K;
+    for (int k = 0; k < 3; ++k) {
+        const int64_t n = in[k].n > 0 ? in[k].n : 0;
+        K.base[k + 1] = K.base[k] + n;
+        K.pre[k] = in[k].pre;
+        K.keys[k] = n ? c->arena.get<uint64_t>(n) : nullptr;
+        K.vals[k] = n ? c->arena.get<uint32_t>(n) : nullptr;
+        pss[k] = PrefixSorted{};
+        pss[k].n = n;
     }
-    radix_sort_pairs_payload(c, keys, vals, n, prefix_bits, pl);
-    time = static_cast<const int64_t *>(pl.out[0]);
-    ps.time = time;
-    ps.gc = gc;
-    for (int j = 0; j < gc.n; ++j) ps.gc.src[j] = pl.out[1 + j];
-    const int64_t S = int64_t(1) << prefix_bits;
-    int64_t *offs = c->arena.get<int64_t>(S + 1);
-    k_prefix_offsets<<<grid_for(n > S + 1 ? n : S + 1, kBlock, 4096), kBlock, 0, c->stream>>>(keys, n, S, offs);
+    if (K.base[3] == 0) return;
+    k_keys_prefix_rows<<<grid_for(K.base[3], kBlock, 4096), kBlock, 0, c->stream>>>(K);
     FZ_LAUNCH_CHECK();
-    uint8_t *bigflag = c->arena.get<uint8_t>(S);
-    dev_fill(c, bigflag, 0, S);
-    ps.S = S;
-    ps.offs = offs;
-    ps.rows = vals;
-    ps.bigflag = bigflag;
-    ps.out = TimeSortOut{otime, oproj, c->arena.get<uint32_t>(n)};
-    const uint32_t pmask = pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << pre.pbits) - 1ull);
-    {
-        // algorithmic bytes: time 8 read; time 8 + project 4 + source position 4 written (the long
-        // class also moves row id 4 + columns in, perm 4 + row 4 + columns out: counted by the
-        // store_gather probe's bytes for the short classes instead)
-        ProbeScope probe(c, "seg_time_sort", 24.0 * double(n));
-        // bucket sorts by length class (each launch skips the others' segments): <= 1024 rows one
-        // 256-thread workgroup each (15 KiB of LDS: many per CU), <= 2048 512 threads, <= 4096
-        // 1024 threads, <= 16384 1024 threads with the keys re-read from memory (LDS: one per CU,
-        // a persistent grid); longer or clustered segments are flagged for the merge sort
-        k_seg_time_bucket<256, 1024><<<unsigned(S < 16384 ? S : 16384), 256, 0, c->stream>>>(
-            time, offs, S, pmask, ps.out, big, bigflag, 0, false, vals, orow, ps.gc);
-        FZ_LAUNCH_CHECK();
-        k_seg_time_bucket<512, 2048><<<unsigned(S < 4096 ? S : 4096), 512, 0, c->stream>>>(
-            time, offs, S, pmask, ps.out, big, bigflag, 1024, false, vals, orow, ps.gc);
-        FZ_LAUNCH_CHECK();
-        k_seg_time_bucket<1024, 4096><<<unsigned(S < 2048 ? S : 2048), 1024, 0, c->stream>>>(
-            time, offs, S, pmask, ps.out, big, bigflag, 2048, false, vals, orow, ps.gc);
-        FZ_LAUNCH_CHECK();
-        // (a workgroup per CU at most; fewer when the table is too small to hold many long segments)
-        const int64_t g16 = n / 16384 < 8 ? 8 : (n / 16384 > 256 ? 256 : n / 16384);
-        k_seg_time_bucket<1024, 16384><<<unsigned(S < g16 ? S : g16), 1024, 0, c->stream>>>(
-            time, offs, S, pmask, ps.out, big, bigflag, 4096, true, vals, orow, ps.gc);
-        FZ_LAUNCH_CHECK();
+    PrefixOffs O;
+    for (int k = 0; k < 3; ++k) {
+        const TableIn &t = in[k];
+        PrefixSorted &ps = pss[k];
+        const int64_t n = ps.n;
+        O.base[k + 1] = O.base[k];
+        if (n == 0) continue;
+        // the prefix passes move the time column and the gathered columns with the keys (each
+        // pass's writes land in per-digit runs): the time sort and the gather then read every
+        // segment's rows from one contiguous range instead of gathering them from the heap-ordered
+        // table
+        RadixPayload pl;
+        pl.n = 1 + t.gc.n;
+        pl.in[0] = t.time;
+        pl.size[0] = 8;
+        for (int j = 0; j < t.gc.n; ++j) {
+            pl.in[1 + j] = t.gc.src[j];
+            pl.size[1 + j] = t.gc.size[j];
+        }
+        radix_sort_pairs_payload(c, K.keys[k], K.vals[k], n, t.prefix_bits, pl);
+        ps.time = static_cast<const int64_t *>(pl.out[0]);
+        ps.gc = t.gc;
+        for (int j = 0; j < t.gc.n; ++j) ps.gc.src[j] = pl.out[1 + j];
+        const int64_t S = int64_t(1) << t.prefix_bits;
+        ps.S = S;
+        ps.offs = c->arena.get<int64_t>(S + 1);
+        ps.rows = K.vals[k];
+        ps.out = TimeSortOut{t.otime, t.oproj, c->arena.get<uint32_t>(n)};
+        ps.pmask = t.pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << t.pre.pbits) - 1ull);
+        ps.big = t.big;
+        ps.orow = t.orow;
+        O.keys[k] = K.keys[k];
+        O.n[k] = n;
+        O.S[k] = S;
+        O.offs[k] = const_cast<int64_t *>(ps.offs);
+        O.base[k + 1] = O.base[k] + (n > S + 1 ? n : S + 1);
     }
-    return ps;
+    k_prefix_offsets<<<grid_for(O.base[3], kBlock, 4096), kBlock, 0, c->stream>>>(O);
+    FZ_LAUNCH_CHECK();
 }
 
-// Gather of every sorted row's columns (after all sorts of the table, merge sort included).
-static void gather_table(fz_ctx *c, const PrefixSorted &ps, int32_t *orow) {
-    if (ps.n <= 0) return;
-    // algorithmic bytes: spos 4 + row id 4 + columns read; perm 4 + row 4 + columns written
-    ProbeScope probe(c, "store_gather", (16.0 + 2.0 * ps.gc.bytes()) * double(ps.n));
-    const unsigned g = (grid_for(ps.n, kBlock, 8192) + 7u) & ~7u;
-    k_store_gather<<<g, kBlock, 0, c->stream>>>(ps.out.spos, ps.rows, ps.n, orow, ps.gc);
+// Every segment of the three prefix-sorted tables sorted by time: one launch per length class for
+// all tables, the bigflag arrays cleared by one fill.
+static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
+    TimeSortTabs T;
+    int64_t ntot = 0;
+    for (int k = 0; k < 3; ++k) {
+        const PrefixSorted &ps = pss[k];
+        T.base[k + 1] = T.base[k] + ps.S;
+        ntot += ps.n;
+    }
+    const int64_t S = T.base[3];
+    if (S == 0) return;
+    uint8_t *flags = c->arena.get<uint8_t>(S);
+    dev_fill(c, flags, 0, S);
+    for (int k = 0; k < 3; ++k) {
+        PrefixSorted &ps = pss[k];
+        if (ps.S == 0) continue;
+        ps.bigflag = flags + T.base[k];
+        TimeSortTab &tb = T.tab[k];
+        tb.time = ps.time;
+        tb.offs = ps.offs;
+        tb.pmask = ps.pmask;
+        tb.out = ps.out;
+        tb.big = ps.big;
+        tb.bigflag = ps.bigflag;
+        tb.rows = ps.rows;
+        tb.orow = ps.orow;
+        tb.gc = ps.gc;
+    }
+    // algorithmic bytes: time 8 read; time 8 + project 4 + source position 4 written (the long
+    // class also moves row id 4 + columns in, perm 4 + row 4 + columns out: counted by the
+    // store_gather probe's bytes for the short classes instead)
+    ProbeScope probe(c, "seg_time_sort", 24.0 * double(ntot));
+    // bucket sorts by length class (each launch skips the others' segments): <= 1024 rows one
+    // 256-thread workgroup each (15 KiB of LDS: many per CU), <= 2048 512 threads, <= 4096 1024
+    // threads, <= 16384 1024 threads with the keys re-read from memory (LDS: one per CU, a
+    // persistent grid); longer or clustered segments are flagged for the merge sort
+    k_seg_time_bucket<256, 1024><<<unsigned(S < 16384 ? S : 16384), 256, 0, c->stream>>>(T, 0, false);
+    FZ_LAUNCH_CHECK();
+    k_seg_time_bucket<512, 2048><<<unsigned(S < 4096 ? S : 4096), 512, 0, c->stream>>>(T, 1024, false);
+    FZ_LAUNCH_CHECK();
+    k_seg_time_bucket<1024, 4096><<<unsigned(S < 2048 ? S : 2048), 1024, 0, c->stream>>>(T, 2048, false);
+    FZ_LAUNCH_CHECK();
+    // (a workgroup per CU at most; fewer when the tables are too small to hold many long segments)
+    const int64_t g16 = ntot / 16384 < 8 ? 8 : (ntot / 16384 > 256 ? 256 : ntot / 16384);
+    k_seg_time_bucket<1024, 16384><<<unsigned(S < g16 ? S : g16), 1024, 0, c->stream>>>(T, 4096, true);
+    FZ_LAUNCH_CHECK();
+}
+
+// Gather of every sorted row's columns (after all sorts, merge sort included), all tables in one
+// launch, each table's blocks in proportion to its rows.
+static void gather_tables(fz_ctx *c, const PrefixSorted *pss) {
+    GatherTabs G;
+    double bytes = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        const PrefixSorted &ps = pss[k];
+        const unsigned g = ps.n > 0 ? (grid_for(ps.n, kBlock, 8192) + 7u) & ~7u : 0u;
+        G.blk[k + 1] = G.blk[k] + g;
+        if (ps.n <= 0) continue;
+        G.tab[k] = GatherTab{ps.out.spos, ps.rows, ps.n, ps.orow, ps.gc};
+        // algorithmic bytes: spos 4 + row id 4 + columns read; perm 4 + row 4 + columns written
+        bytes += (16.0 + 2.0 * ps.gc.bytes()) * double(ps.n);
+    }
+    if (G.blk[3] == 0) return;
+    ProbeScope probe(c, "store_gather", bytes);
+    k_store_gather<<<G.blk[3], kBlock, 0, c->stream>>>(G);
     FZ_LAUNCH_CHECK();
 }
 
@@ -543,19 +676,6 @@ struct StoreSink {
         out.put(q, int64_t(k ^ (uint64_t(1) << 63)), uint32_t(s) & pmask, v);
     }
 };
-
-static View make_view(fz_ctx *c, const int32_t *row, const int64_t *time, const uint32_t *proj, int64_t n, int64_t P,
-                      DevBuf &offbuf) {
-    View v;
-    v.n = n;
-    v.row = row;
-    v.time = time;
-    v.proj = proj;
-    int64_t *offs = offbuf.ensure<int64_t>(P + 1);
-    segment_offsets(c, proj, n, P, offs);
-    v.offs = offs;
-    return v;
-}
 
 void store_eligibility(fz_ctx *c);  // fz_rq1.hip
 
@@ -664,61 +784,64 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     unsigned long long *big3 = c->arena.get<unsigned long long>(6);
     dev_fill(c, big3, 0, 6 * 8);
     PrefixSorted pss[3];
+    TableIn tin[3];
     for (int k = 0; k < 3; ++k) {
         Tab &b = tabs[k];
-        b.row->ensure<int32_t>(b.n);
-        pss[k] = sort_table_fast(c, b.n, b.pre, b.pbits_total, b.time, b.tm->ensure<int64_t>(b.n),
-                                 b.pr->ensure<uint32_t>(b.n), b.row->as<int32_t>(), gcs[k], big3 + k);
+        tin[k] = TableIn{b.n, b.pre, b.pbits_total, b.time, b.tm->ensure<int64_t>(b.n), b.pr->ensure<uint32_t>(b.n),
+                         b.row->ensure<int32_t>(b.n), gcs[k], big3 + k};
     }
-    auto make_views = [&]() {
-        int32_t *row = s.b_row.as<int32_t>();
-        int64_t *tm = s.b_time.as<int64_t>();
-        uint32_t *pr = s.b_proj.as<uint32_t>();
-        s.fuzz = make_view(c, row, tm, pr, n_fuzz, P, s.off_fuzz);
-        s.covb = make_view(c, row + n_fuzz, tm + n_fuzz, pr + n_fuzz, n_covb, P, s.off_covb);
-        s.cov = make_view(c, s.c_row.as<int32_t>(), s.c_time.as<int64_t>(), s.c_proj.as<uint32_t>(), t->n_cov, P,
-                          s.off_cov);
-        s.issues = make_view(c, s.i_row.as<int32_t>(), s.i_time.as<int64_t>(), s.i_proj.as<uint32_t>(), t->n_issues,
-                             P, s.off_iss);
-    };
-    // longest segments (sizes the per-iteration outputs) + the merge-sort counters
+    prefix_sort_tables(c, tin, pss);
+    time_sort_tables(c, pss);
+    // the views (per-project ranges of the sorted tables) and the longest segments, off the
+    // prefix offsets: builds' prefix is type << pbits | project (Fuzzing 0, Coverage 1)
+    {
+        auto view = [&](View &v, DevBuf &rowb, DevBuf &tmb, DevBuf &prb, int64_t at, int64_t n, DevBuf &offb) {
+            v.n = n;
+            v.row = rowb.as<int32_t>() + at;
+            v.time = tmb.as<int64_t>() + at;
+            v.proj = prb.as<uint32_t>() + at;
+            v.offs = offb.ensure<int64_t>(P + 1);
+        };
+        view(s.fuzz, s.b_row, s.b_time, s.b_proj, 0, n_fuzz, s.off_fuzz);
+        view(s.covb, s.b_row, s.b_time, s.b_proj, n_fuzz, n_covb, s.off_covb);
+        view(s.cov, s.c_row, s.c_time, s.c_proj, 0, t->n_cov, s.off_cov);
+        view(s.issues, s.i_row, s.i_time, s.i_proj, 0, t->n_issues, s.off_iss);
+    }
+    ViewSrc vs;
+    const View *vw[4] = {&s.fuzz, &s.covb, &s.cov, &s.issues};
+    const int tab_of[4] = {0, 0, 1, 2};
+    for (int i = 0; i < 4; ++i) {
+        vs.src[i] = pss[tab_of[i]].offs;
+        vs.first[i] = i == 1 ? (int64_t(1) << pbits) : 0;
+        vs.base[i] = i == 1 ? n_fuzz : 0;
+        vs.dst[i] = const_cast<int64_t *>(vw[i]->offs);
+    }
+    vs.big = big3;
     int64_t *mx = c->arena.get<int64_t>(10);
-    auto read_stats = [&]() {
-        Offs4 v{{s.fuzz.offs, s.covb.offs, s.cov.offs, s.issues.offs}, big3};
-        k_store_stats<<<1, kSortBlock, 0, c->stream>>>(v, P, mx);
-        FZ_LAUNCH_CHECK();
-        FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 10 * 8, hipMemcpyDeviceToHost, c->stream));
-        sync(c);
-    };
-    // segments the register sorts left (longer than 16384 rows, or a time span too wide for their
-    // packed key): segmented merge sort of those rows only, writing the same outputs
-    make_views();
-    read_stats();
+    k_store_views<<<1, kSortBlock, 0, c->stream>>>(vs, P, mx);
+    FZ_LAUNCH_CHECK();
+    FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 10 * 8, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    // segments the bucket sorts left (longer than 16384 rows, clustered, or a time span too wide
+    // for their packed key): segmented merge sort of those rows only, writing the same outputs
+    const int64_t maxseg[4] = {c->h_pinned[0], c->h_pinned[1], c->h_pinned[2], c->h_pinned[3]};
     const int64_t bigrows[3] = {c->h_pinned[4], c->h_pinned[5], c->h_pinned[6]};
     const int64_t bigmax[3] = {c->h_pinned[7], c->h_pinned[8], c->h_pinned[9]};
-    bool redo = false;
     for (int k = 0; k < 3; ++k) {
         if (bigrows[k] == 0) continue;
-        Tab &b = tabs[k];
         const PrefixSorted &ps = pss[k];
-        const uint32_t pmask = b.pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << b.pre.pbits) - 1ull);
         ProbeScope probe(c, "seg_merge_sort", 36.0 * double(bigrows[k]));
-        sort_big_segments(c, ps.offs, ps.S, b.n, bigmax[k], ps.bigflag, StoreTimeKey{ps.time},
-                          StoreSink{pmask, ps.out});
-        redo = true;
+        sort_big_segments(c, ps.offs, ps.S, ps.n, bigmax[k], ps.bigflag, StoreTimeKey{ps.time},
+                          StoreSink{ps.pmask, ps.out});
     }
     // the long-segment bucket sort gathered its segments' columns; the short classes' and the
     // merge-sorted rows are gathered here (rows marked kGathered are skipped)
-    for (int k = 0; k < 3; ++k) gather_table(c, pss[k], tabs[k].row->as<int32_t>());
-    if (redo) {  // the merged segments' projects are written now
-        make_views();
-        read_stats();
-    }
+    gather_tables(c, pss);
     materialize_sorted(c);
-    s.fuzz.max_seg = c->h_pinned[0];
-    s.covb.max_seg = c->h_pinned[1];
-    s.cov.max_seg = c->h_pinned[2];
-    s.issues.max_seg = c->h_pinned[3];
+    s.fuzz.max_seg = maxseg[0];
+    s.covb.max_seg = maxseg[1];
+    s.cov.max_seg = maxseg[2];
+    s.issues.max_seg = maxseg[3];
     s.built = true;
     if (stats) {
         stats->n_projects = P;
