@@ -528,12 +528,46 @@ struct F64Sink {
     }
 };
 
+// One segment [offs[0], offs[1]) of a value array as radix keys: positions before it key 0, after
+// it ~0, so a stable sort of the whole array leaves them where they are and the segment's values
+// sorted in between; payload = the position.
+__global__ __launch_bounds__(kBlock) void k_f64_seg1_keys(const double *__restrict__ x, int64_t n,
+                                                          const int64_t *__restrict__ offs, uint64_t *__restrict__ k,
+                                                          uint32_t *__restrict__ v) {
+    const int64_t lo = offs[0], hi = offs[1];
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        k[i] = i < lo ? 0ull : (i < hi ? f64_key(x[i]) : ~0ull);
+        v[i] = uint32_t(i);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_f64_from_keys(const uint64_t *__restrict__ k, const uint32_t *__restrict__ v,
+                                                          int64_t n, double *__restrict__ val, int32_t *__restrict__ pos) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        val[i] = f64_from_key(k[i]);
+        pos[i] = int32_t(v[i]);
+    }
+}
+
 SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int32_t *) {
     const int64_t n = sg.n_cap;
     SortedSegs out;
     out.val = c->arena.get<double>(n);
     out.pos = c->arena.get<int32_t>(n);
     if (n <= 0 || sg.S <= 0) return out;
+    if (sg.S == 1 && sg.len_bound() > 16384) {
+        // one long segment (RQ3's detected u non-detected union, a long series): the LSD radix sort
+        // (8 passes at HBM rate, stable: ties keep position order, as the merge sort keeps them)
+        // instead of the merge sort's tile sort and log2(n / 4096) merge rounds
+        uint64_t *k = c->arena.get<uint64_t>(n);
+        uint32_t *v = c->arena.get<uint32_t>(n);
+        k_f64_seg1_keys<<<grid_for(n, kBlock, 4096), kBlock, 0, c->stream>>>(src, n, sg.offs, k, v);
+        FZ_LAUNCH_CHECK();
+        radix_sort_pairs_swap(c, k, v, n, 64);
+        k_f64_from_keys<<<grid_for(n, kBlock, 4096), kBlock, 0, c->stream>>>(k, v, n, out.val, out.pos);
+        FZ_LAUNCH_CHECK();
+        return out;
+    }
     // segments of <= 16384 values: one workgroup each, value bucket sort by length class (each
     // launch skips the other classes' segments; one wave / one thread for the tiny ones when there
     // are very many segments); longer or skewed segments of the 16384 class: the segmented merge
