@@ -71,3 +71,29 @@ def test_big_segments_ties_nulls_wide_span(engine):
     t.c_date[rows[:3]] = ts_from_str("2199-06-01")
     st = _check_all(engine, t)
     assert st.max_fuzz_per_project > 4096 and st.max_cov_per_project > 4096
+
+
+def _edge_table(kind):
+    cfg = synth.SynthConfig(n_projects=1 if kind == "one_project" else 30, seed=31, len_uniform=(400, 900),
+                            issues_mean=60, hex_len=12, dup_numbers=0 if kind == "one_project" else 2)
+    t = synth.generate(cfg)
+    if kind == "no_issues":
+        for f in ("i_number", "i_project", "i_rts", "i_status", "i_new_id"):
+            setattr(t, f, getattr(t, f)[:0])
+    elif kind == "other_build_types":
+        # a third build type (sorts after Fuzzing and Coverage in the store's prefix; no view holds it)
+        t.build_types = list(t.build_types) + ["Introspector"]
+        rng = np.random.default_rng(9)
+        t.b_type = t.b_type.copy()
+        t.b_type[rng.random(len(t.b_type)) < 0.05] = 2
+    return t
+
+
+@pytest.mark.parametrize("kind", ["one_project", "no_issues", "other_build_types"])
+def test_store_edge_tables(engine, kind):
+    """The store's shared launches (three tables in one prefix-key / offset / time-sort / gather
+    launch, the views read off the prefix offsets) on degenerate tables: a single project, an empty
+    issues table, builds of a type neither view selects."""
+    t = _edge_table(kind)
+    st = _check_all(engine, t)
+    assert st.n_fuzz == int(np.sum(t.b_type == 0)) and st.n_coverage_builds == int(np.sum(t.b_type == 1))

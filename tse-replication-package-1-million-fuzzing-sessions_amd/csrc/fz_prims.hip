@@ -649,7 +649,10 @@ void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t 
 }
 
 void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl) {
-    if (n <= 1 || bits <= 0) return;
+    if (n <= 1 || bits <= 0) {  // nothing to sort (one key, or a 0-bit key: one project): unmoved
+        for (int j = 0; j < pl.n; ++j) pl.out[j] = const_cast<void *>(pl.in[j]);
+        return;
+    }
     const int npass = (bits + kRadixBits - 1) / kRadixBits;
     const int64_t nb = (n + kSortTile - 1) / kSortTile;
     FZ_CHECK(n < (int64_t(1) << 47), "radix_sort_pairs: too many keys");

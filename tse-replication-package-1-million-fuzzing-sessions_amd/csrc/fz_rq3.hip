@@ -51,34 +51,6 @@ struct CovRowsRq3 {  // covered_line IS NOT NULL AND DATE(date) < '2025-01-09' (
     __device__ bool operator()(int32_t r) const { return (valid[r] & FZ_VALID_COVERED) && date[r] < kLim3b; }
 };
 
-// anderson(x, dist='norm') from ascending keys: A2 and the 5 rounded critical values.
-// offs1: the sample's single-segment offsets {0, *d_n} (written by the caller's union map)
-static void anderson_sorted(fz_ctx *c, const uint64_t *sk, const double *x, int64_t nmax, const int64_t *d_n,
-                            const int64_t *offs1, double *out) {
-    Segs one{1, offs1, nmax};
-    ChunkedSegs cs = chunked(c, one);
-    double *ms = c->arena.get<double>(4);
-    seg_mean(c, cs, x, ms);  // xbar
-    seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t, double *v) {
-        const double d = x[i] - ms[0];
-        v[0] = d * d;
-    }, ms + 1);
-    seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t, double *v) {
-        const double N = double(*d_n);
-        const double s = sqrt(ms[1] / (N - 1.0));  // np.std(ddof=1)
-        const int64_t n = *d_n;
-        const double wi = (f64_from_key(sk[i]) - ms[0]) / s;
-        const double wj = (f64_from_key(sk[n - 1 - i]) - ms[0]) / s;
-        v[0] = (2.0 * double(i + 1) - 1.0) / N * (stats::log_ndtr(wi) + stats::log_ndtr(-wj));
-    }, ms + 2);
-    map_n(c, 1, nullptr, [=] __device__(int64_t) {
-        const double N = double(*d_n);
-        out[0] = -N - ms[2];
-        const double av[5] = {0.576, 0.656, 0.787, 0.918, 1.092};
-        for (int k = 0; k < 5; ++k) out[1 + k] = rint(av[k] / (1.0 + 4.0 / N - 25.0 / N / N) * 1000.0) / 1000.0;
-    });
-}
-
 void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t NI, const int64_t *d_nd,
                const double *non_pct, int64_t NC, const int64_t *d_nn, fz_describe *describe, double *tests);
 
@@ -205,6 +177,68 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
                   counts + FZ_RQ3_NON_DETECTED, o->describe, o->tests);
 }
 
+// anderson(det), anderson(non) (:329, :335) and levene(det, non) (:344) in one set of reductions:
+// the two samples are segments {0, nd, nd + nn} (oseg) of the union v (their sums do not depend on
+// order) and of cat (the union partitioned by sample, each part ascending: medians, A2 terms).
+// Written only when both samples are non-empty.
+static void sample_tests(fz_ctx *c, const double *v, const double *cat, int64_t cap, const int64_t *oseg,
+                         double *tests) {
+    const Segs two{2, oseg, cap};
+    const ChunkedSegs cs = chunked(c, two);
+    double *med = c->arena.get<double>(2);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        for (int s = 0; s < 2; ++s) {
+            const int64_t b = oseg[s], n = oseg[s + 1] - b;
+            med[s] = n <= 0 ? NAN : ((n & 1) ? cat[b + n / 2] : (cat[b + n / 2 - 1] + cat[b + n / 2]) / 2.0);
+        }
+    });
+    double *r1 = c->arena.get<double>(4);  // [s]: sum x, sum |x - median|
+    seg_reduce<2>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
+        x[0] = v[i];
+        x[1] = fabs(v[i] - med[s]);
+    }, r1);
+    double *r2 = c->arena.get<double>(4);  // [s]: sum (x - mean)^2, sum (|x - median| - its mean)^2
+    seg_reduce<2>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
+        const double n = double(oseg[s + 1] - oseg[s]);
+        const double d = v[i] - r1[2 * s] / n;
+        const double e = fabs(v[i] - med[s]) - r1[2 * s + 1] / n;
+        x[0] = d * d;
+        x[1] = e * e;
+    }, r2);
+    double *r3 = c->arena.get<double>(2);  // [s]: sum of the A2 terms (ascending order)
+    seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
+        const int64_t b = oseg[s], n = oseg[s + 1] - b, k = i - b;
+        const double N = double(n), xbar = r1[2 * s] / N;
+        const double sd = sqrt(r2[2 * s] / (N - 1.0));  // np.std(ddof=1)
+        const double wi = (cat[i] - xbar) / sd, wj = (cat[b + n - 1 - k] - xbar) / sd;
+        x[0] = (2.0 * double(k + 1) - 1.0) / N * (stats::log_ndtr(wi) + stats::log_ndtr(-wj));
+    }, r3);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        const double nx = double(oseg[1] - oseg[0]), ny = double(oseg[2] - oseg[1]);
+        if (!(nx > 0.0 && ny > 0.0)) return;
+        const double av[5] = {0.576, 0.656, 0.787, 0.918, 1.092};
+        for (int s = 0; s < 2; ++s) {
+            const double N = s ? ny : nx;
+            double *out = tests + (s ? FZ_RQ3_AD_NON : FZ_RQ3_AD_DET);
+            out[0] = -N - r3[s];
+            for (int k = 0; k < 5; ++k) out[1 + k] = rint(av[k] / (1.0 + 4.0 / N - 25.0 / N / N) * 1000.0) / 1000.0;
+        }
+        // levene([x, y], center='median') (scipy _morestats.py levene)
+        const double zb0 = r1[1] / nx, zb1 = r1[3] / ny, N = nx + ny;
+        double zbar = 0.0;
+        zbar += zb0 * nx;
+        zbar += zb1 * ny;
+        zbar /= N;
+        const double numer = (N - 2.0) * (nx * (zb0 - zbar) * (zb0 - zbar) + ny * (zb1 - zbar) * (zb1 - zbar));
+        double dvar = 0.0;
+        dvar += r2[1];
+        dvar += r2[3];
+        const double W = numer / (1.0 * dvar);
+        tests[FZ_RQ3_LEVENE_W] = W;
+        tests[FZ_RQ3_LEVENE_P] = stats::f1_sf(W, N - 2.0);
+    });
+}
+
 // ---- statistics (:321-352) over samples of device lengths *d_nd <= NI and *d_nn <= NC
 void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t NI, const int64_t *d_nd,
                const double *non_pct, int64_t NC, const int64_t *d_nn, fz_describe *describe, double *tests) {
@@ -215,11 +249,12 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
     // partition of the sorted union by sample gives each sample's sorted keys (describe,
     // anderson, levene) - instead of three separate device-wide sorts.
     const int64_t cap = NI + NC;
-    int64_t *odet = c->arena.get<int64_t>(2), *onon = c->arena.get<int64_t>(2);
+    int64_t *oseg = c->arena.get<int64_t>(3);  // {0, nd, nd + nn}: the samples in the union
     uint64_t *skd = c->arena.get<uint64_t>(cap);
     uint64_t *skn = c->arena.get<uint64_t>(cap);
+    double *v = c->arena.get<double>(cap);
+    double *cat = c->arena.get<double>(cap);
     {
-        double *v = c->arena.get<double>(cap);
         uint8_t *g = c->arena.get<uint8_t>(cap);
         const double *dp = det_pct, *np_ = non_pct;
         int64_t *oall = c->arena.get<int64_t>(2);  // {0, *d_nd + *d_nn}: the union's one segment
@@ -228,10 +263,9 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
             if (i == 0) {
                 oall[0] = 0;
                 oall[1] = nd + nn;
-                odet[0] = 0;  // and each sample's own (Anderson-Darling)
-                odet[1] = nd;
-                onon[0] = 0;
-                onon[1] = nn;
+                oseg[0] = 0;
+                oseg[1] = nd;
+                oseg[2] = nd + nn;
             }
             if (i < nd) {
                 v[i] = dp[i];
@@ -256,19 +290,23 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
         const double *sv = ss.val;
         map_n(c, cap, nullptr, [=] __device__(int64_t i) { isdet[i] = (i < *d_all && g[pos[i]] == 0) ? 1 : 0; });
         scan_exclusive_i64(c, isdet, before, cap, nullptr);
+        const int64_t *d_det = d_nd;
         map_n(c, cap, d_all, [=] __device__(int64_t i) {
             const uint64_t k = f64_key(sv[i]);
-            if (isdet[i]) skd[before[i]] = k;
-            else skn[i - before[i]] = k;
+            if (isdet[i]) {
+                skd[before[i]] = k;
+                cat[before[i]] = sv[i];
+            } else {
+                skn[i - before[i]] = k;
+                cat[*d_det + i - before[i]] = sv[i];
+            }
         });
     }
     const SortedDescJob jobs[3] = {{skd, det_pct, NI, d_nd, describe},
                                    {skn, non_pct, NC, d_nn, describe + 1},
                                    {sorted_keys_dn(c, dtot_f, NI, d_nd), dtot_f, NI, d_nd, describe + 2}};
     describe_sorted_dn_batch(c, jobs, 3);
-    anderson_sorted(c, skd, det_pct, NI, d_nd, odet, tests + FZ_RQ3_AD_DET);
-    anderson_sorted(c, skn, non_pct, NC, d_nn, onon, tests + FZ_RQ3_AD_NON);
-    levene_two(c, skd, det_pct, NI, d_nd, skn, non_pct, NC, d_nn, tests + FZ_RQ3_LEVENE_W);
+    sample_tests(c, v, cat, cap, oseg, tests);
 }
 
 }  // namespace fz
