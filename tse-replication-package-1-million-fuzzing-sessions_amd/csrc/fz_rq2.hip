@@ -56,8 +56,7 @@ void series_tests(fz_ctx *c, const double *x, int64_t n_cap, const int64_t *d_n,
     ChunkedSegs cs3 = chunked(c, one);
     int32_t *sg3 = segment_ids(c, one);
     SortedSegs ss3 = seg_sort_f64(c, x, one, sg3);
-    TieRanks tr3 = seg_tie_ranks(c, cs3, sg3, ss3.val);
-    seg_spearman_index(c, cs3, ss3, tr3, out, out + 1);
+    spearman_index_sorted(c, cs3, sg3, ss3, out, out + 1);
     seg_shapiro(c, cs3, x, ss3, out + 2, out + 3);
 }
 
@@ -67,8 +66,7 @@ void spearman_index_seg(fz_ctx *c, const double *x, int64_t n, const int64_t *of
     ChunkedSegs cs = chunked(c, sg);
     int32_t *id = segment_ids(c, sg);
     SortedSegs ss = seg_sort_f64(c, x, sg, id);
-    TieRanks tr = seg_tie_ranks(c, cs, id, ss.val);
-    seg_spearman_index(c, cs, ss, tr, rho, p);
+    spearman_index_sorted(c, cs, id, ss, rho, p);
 }
 
 __global__ void k_session_keys(const int64_t *__restrict__ sid, int64_t n, uint64_t *__restrict__ keys,
@@ -153,8 +151,7 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     ChunkedSegs cs = chunked(c, sp);
     const int32_t *segid = reinterpret_cast<const int32_t *>(T.proj);
     SortedSegs ss = seg_sort_f64(c, tv, sp, segid);
-    TieRanks tr = seg_tie_ranks(c, cs, segid, ss.val);
-    seg_spearman_index(c, cs, ss, tr, o->corr, nullptr);
+    spearman_index_sorted(c, cs, segid, ss, o->corr, nullptr);
     seg_shapiro(c, cs, tv, ss, o->sw_w, o->sw_p);
 
     // coverage_by_session_index: order by (index within project, project) - the values are in

@@ -246,7 +246,7 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
     const int64_t *dt = det_tot;
     map_n(c, NI, d_nd, [=] __device__(int64_t q) { dtot_f[q] = double(dt[q]); });
     // One sort of det u non serves everything: Brunner-Munzel ranks the union, and a stable
-    // partition of the sorted union by sample gives each sample's sorted keys (describe,
+    // partition of the sorted union by sample gives each sample's sorted values (describe,
     // anderson, levene) - instead of three separate device-wide sorts.
     const int64_t cap = NI + NC;
     int64_t *oseg = c->arena.get<int64_t>(3);  // {0, nd, nd + nn}: the samples in the union
@@ -255,7 +255,6 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
     double *v = c->arena.get<double>(cap);
     double *cat = c->arena.get<double>(cap);
     {
-        uint8_t *g = c->arena.get<uint8_t>(cap);
         const double *dp = det_pct, *np_ = non_pct;
         int64_t *oall = c->arena.get<int64_t>(2);  // {0, *d_nd + *d_nn}: the union's one segment
         map_n(c, cap > 0 ? cap : 1, nullptr, [=] __device__(int64_t i) {
@@ -267,19 +266,18 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
                 oseg[1] = nd;
                 oseg[2] = nd + nn;
             }
-            if (i < nd) {
-                v[i] = dp[i];
-                g[i] = 0;
-            } else if (i < nd + nn) {
-                v[i] = np_[i - nd];
-                g[i] = 1;
-            }
+            if (i < nd) v[i] = dp[i];
+            else if (i < nd + nn) v[i] = np_[i - nd];
         });
         const int64_t *d_all = oall + 1;
         Segs one{1, oall, cap};
         int32_t *sid = segment_ids(c, one);
         ChunkedSegs cs = chunked(c, one);
         SortedSegs ss = seg_sort_f64(c, v, one, sid);
+        // brunnermunzel(det, non) (:349): ranks of the sorted union (det | non: position < nd is det)
+        uint8_t *g = c->arena.get<uint8_t>(cap);
+        const int64_t *d_det0 = d_nd;
+        map_n(c, cap, nullptr, [=] __device__(int64_t i) { g[i] = i < *d_det0 ? 0 : 1; });
         RankTestOut rt;
         rt.bm_stat = tests + FZ_RQ3_BM_STAT;
         rt.bm_p = tests + FZ_RQ3_BM_P;
@@ -288,7 +286,7 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
         int64_t *isdet = c->arena.get<int64_t>(cap), *before = c->arena.get<int64_t>(cap);
         const int32_t *pos = ss.pos;
         const double *sv = ss.val;
-        map_n(c, cap, nullptr, [=] __device__(int64_t i) { isdet[i] = (i < *d_all && g[pos[i]] == 0) ? 1 : 0; });
+        map_n(c, cap, nullptr, [=] __device__(int64_t i) { isdet[i] = (i < *d_all && pos[i] < *d_nd) ? 1 : 0; });
         scan_exclusive_i64(c, isdet, before, cap, nullptr);
         const int64_t *d_det = d_nd;
         map_n(c, cap, d_all, [=] __device__(int64_t i) {

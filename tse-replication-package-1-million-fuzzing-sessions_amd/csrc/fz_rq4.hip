@@ -307,21 +307,11 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
                    double *pbm) {
     const int64_t S2 = 2 * MM, NC = n_cap, P = half_len;
     const int64_t *d_nf = d_n;
-    int32_t *sess = c->arena.get<int32_t>(NC);
-    uint8_t *grp2 = c->arena.get<uint8_t>(NC);
-    map_n(c, NC, nullptr, [=] __device__(int64_t k) {
-        sess[k] = int32_t(sid2[k] >> 1);
-        grp2[k] = uint8_t(sid2[k] & 1u);
-    });
-    int64_t *offs2 = c->arena.get<int64_t>(S2 + 1);
+    int64_t *offs2 = c->arena.get<int64_t>(S2 + 1);  // segment 2i: session i's G2 values, 2i + 1: G1
     segment_offsets_dn(c, sid2, d_nf, NC, S2, offs2);
-    int64_t *soffs = c->arena.get<int64_t>(MM + 1);
-    map_n(c, MM + 1, nullptr, [=] __device__(int64_t i) {
-        soffs[i] = offs2[2 * i];
-        if (i < MM) {
-            c2[i] = offs2[2 * i + 1] - offs2[2 * i];
-            c1[i] = offs2[2 * i + 2] - offs2[2 * i + 1];
-        }
+    map_n(c, MM, nullptr, [=] __device__(int64_t i) {
+        c2[i] = offs2[2 * i + 1] - offs2[2 * i];
+        c1[i] = offs2[2 * i + 2] - offs2[2 * i + 1];
     });
     Segs sg2{S2, offs2, NC, P};
     SortedSegs ss2 = seg_sort_f64(c, v2, sg2, reinterpret_cast<const int32_t *>(sid2));
@@ -333,12 +323,8 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
         g2q[k] = qq[(2 * i) * 3 + j];
         g1q[k] = qq[(2 * i + 1) * 3 + j];
     });
-    RankTestOut rt;
-    rt.bm_p = pbm;
-    seg_rank_tests(c, v2, grp2, Segs{MM, soffs, NC, sess_len}, sess, rt);
-    map_n(c, MM, nullptr, [=] __device__(int64_t i) {
-        if (!(c2[i] >= 5 && c1[i] >= 5)) pbm[i] = NAN;
-    });
+    // per-session Brunner-Munzel on the sorted halves (:978-985; NaN unless both sides >= 5)
+    bm_sorted_halves(c, ss2.val, offs2, MM, 5, pbm);
 }
 
 __global__ void k_rq4b_keys(const int64_t *__restrict__ sid, const uint8_t *__restrict__ grp, int64_t n,
@@ -462,9 +448,8 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
         ChunkedSegs cs6 = chunked(c, s6);
         int32_t *id6 = segment_ids(c, s6);
         SortedSegs ss6 = seg_sort_f64(c, seq, s6, id6);
-        TieRanks tr6 = seg_tie_ranks(c, cs6, id6, ss6.val);
         double *rho = c->arena.get<double>(6), *pv = c->arena.get<double>(6);
-        seg_spearman_index(c, cs6, ss6, tr6, rho, pv);
+        spearman_index_sorted(c, cs6, id6, ss6, rho, pv);
         double *sp = o->spearman6;
         map_n(c, 6, nullptr, [=] __device__(int64_t k) {
             sp[2 * k] = rho[k];

@@ -346,6 +346,15 @@ void seg_rank_tests(fz_ctx *c, const double *vals, const uint8_t *grp, const Seg
 void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, const ChunkedSegs &cs,
                            const int32_t *segid, const RankTestOut &o);
 
+// Brunner-Munzel p of M sessions whose samples are sorted halves: x = sorted[offs2[2i], offs2[2i+1]),
+// y = sorted[offs2[2i+1], offs2[2i+2]); NaN unless both hold >= min_n values.
+void bm_sorted_halves(fz_ctx *c, const double *sorted, const int64_t *offs2, int64_t M, int64_t min_n, double *pbm);
+
+// spearmanr(range(n), x) per segment from the sorted segments: one workgroup per segment when they
+// are short (no tie-rank passes), else seg_tie_ranks + seg_spearman_index.
+void spearman_index_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const SortedSegs &ss, double *rho,
+                           double *pval);
+
 // scipy.stats.levene([x, y]) (center='median') from the samples and their ascending keys
 // -> out[0] = W, out[1] = p (F(1, N-2) survival, cephes fdtrc rounding).
 void levene_two(fz_ctx *c, const uint64_t *skx, const double *x, int64_t nxm, const int64_t *d_nx,

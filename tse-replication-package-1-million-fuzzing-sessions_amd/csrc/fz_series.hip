@@ -779,6 +779,103 @@ void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, 
     });
 }
 
+// Brunner-Munzel p of M sessions whose two samples are already sorted: x = sv[offs2[2i],
+// offs2[2i + 1]), y = sv[offs2[2i + 1], offs2[2i + 2]), both ascending.  One workgroup per session,
+// each thread walking a contiguous run of one half in order (a merge): a value's average rank in
+// the union is its count below in both halves plus the middle of its tie group across both, its
+// within-sample rank the same in its own half - the pointers into the other half only move
+// forward, a new tie group finds its end by binary search.  Then the two sums scipy's
+// brunnermunzel forms (t distribution, two-sided): no union sort, no device-wide rank passes.
+// p = NaN unless both samples hold >= min_n values.
+__device__ inline int64_t lower_bound_d(const double *a, int64_t lo, int64_t hi, double v) {
+    while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if (a[m] < v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+__device__ inline int64_t upper_bound_d(const double *a, int64_t lo, int64_t hi, double v) {
+    while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if (a[m] <= v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+// visit(rc, rw) for this thread's run of a (na values) against the other half b (nb values)
+template <typename F>
+__device__ inline void bm_walk_run(const double *a, int64_t na, const double *b, int64_t nb, int64_t k0, int64_t k1,
+                                   F visit) {
+    if (k0 >= k1) return;
+    double v = a[k0];
+    int64_t la = lower_bound_d(a, 0, k0 + 1, v), ua = upper_bound_d(a, k0, na, v);
+    int64_t lb = lower_bound_d(b, 0, nb, v), ub = upper_bound_d(b, lb, nb, v);
+    for (int64_t k = k0; k < k1; ++k) {
+        if (k > k0 && a[k] != v) {  // a new tie group starts at k
+            v = a[k];
+            la = k;
+            ua = upper_bound_d(a, k, na, v);
+            while (lb < nb && b[lb] < v) ++lb;
+            if (ub < lb) ub = lb;
+            while (ub < nb && b[ub] <= v) ++ub;
+        }
+        const double rc = double(la + lb) + double((ua - la) + (ub - lb) + 1) / 2.0;
+        const double rw = double(la) + double(ua - la + 1) / 2.0;
+        visit(rc, rw);
+    }
+}
+// this thread's share of a (one contiguous run per thread of the workgroup)
+template <typename F>
+__device__ inline void bm_walk(const double *a, int64_t na, const double *b, int64_t nb, F visit) {
+    const int64_t per = (na + kBlock - 1) / kBlock;
+    const int64_t k0 = int64_t(threadIdx.x) * per;
+    bm_walk_run(a, na, b, nb, k0, k0 + per < na ? k0 + per : na, visit);
+}
+__global__ __launch_bounds__(kBlock) void k_bm_sorted_halves(const double *__restrict__ sv,
+                                                             const int64_t *__restrict__ offs2, int64_t M,
+                                                             int64_t min_n, double *__restrict__ pbm) {
+    __shared__ double s_tmp[4];
+    for (int64_t i = blockIdx.x; i < M; i += gridDim.x) {
+        const int64_t x0 = offs2[2 * i], x1 = offs2[2 * i + 1], y1 = offs2[2 * i + 2];
+        const int64_t nx = x1 - x0, ny = y1 - x1;
+        if (nx < min_n || ny < min_n) {
+            if (threadIdx.x == 0) pbm[i] = NAN;
+            continue;
+        }
+        const double *x = sv + x0, *y = sv + x1;
+        double ax = 0.0, ay = 0.0;
+        bm_walk(x, nx, y, ny, [&](double rc, double) { ax += rc; });
+        bm_walk(y, ny, x, nx, [&](double rc, double) { ay += rc; });
+        const double Nx = double(nx), Ny = double(ny);
+        const double rcx = block_sum(ax, s_tmp) / Nx, rcy = block_sum(ay, s_tmp) / Ny;
+        const double wmx = (Nx + 1.0) / 2.0, wmy = (Ny + 1.0) / 2.0;  // mean within-sample rank
+        double bx = 0.0, by = 0.0;
+        bm_walk(x, nx, y, ny, [&](double rc, double rw) {
+            const double d = ((rc - rw) - rcx) + wmx;
+            bx += d * d;
+        });
+        bm_walk(y, ny, x, nx, [&](double rc, double rw) {
+            const double d = ((rc - rw) - rcy) + wmy;
+            by += d * d;
+        });
+        const double Sx = block_sum(bx, s_tmp) / (Nx - 1.0), Sy = block_sum(by, s_tmp) / (Ny - 1.0);
+        if (threadIdx.x == 0) {
+            double w = Nx * Ny * (rcy - rcx);
+            w /= (Nx + Ny) * sqrt(Nx * Sx + Ny * Sy);
+            const double num = (Nx * Sx + Ny * Sy) * (Nx * Sx + Ny * Sy);
+            const double den = (Nx * Sx) * (Nx * Sx) / (Nx - 1.0) + (Ny * Sy) * (Ny * Sy) / (Ny - 1.0);
+            pbm[i] = 2.0 * stats::t_sf(fabs(w), num / den);
+        }
+    }
+}
+
+void bm_sorted_halves(fz_ctx *c, const double *sorted, const int64_t *offs2, int64_t M, int64_t min_n, double *pbm) {
+    if (M <= 0) return;
+    k_bm_sorted_halves<<<unsigned(M < 16384 ? M : 16384), kBlock, 0, c->stream>>>(sorted, offs2, M, min_n, pbm);
+    FZ_LAUNCH_CHECK();
+}
+
 // --------------------------------------------------------------------- Spearman vs index
 void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, const TieRanks &tr, double *rho,
                         double *pval) {
@@ -817,6 +914,77 @@ void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, 
         rho[s] = r;
         if (pval) pval[s] = p;
     });
+}
+
+// scipy.stats.spearmanr(range(n), x) per segment from the sorted segments alone, one workgroup per
+// segment (segments of at most kSpearmanSmall values): each thread walks a run of the sorted values,
+// a tie group's bounds come from one binary search when it starts, and the rank products are summed
+// directly - the same exact half-integer sums as seg_spearman_index, without the device-wide tie
+// rank passes.
+constexpr int64_t kSpearmanSmall = 65536;
+__global__ __launch_bounds__(kBlock) void k_spearman_index_small(const double *__restrict__ sv,
+                                                                 const int32_t *__restrict__ pos,
+                                                                 const int64_t *__restrict__ offs, int64_t S,
+                                                                 double *__restrict__ rho, double *__restrict__ pval) {
+    __shared__ double s_tmp[4];
+    for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
+        const int64_t b = offs[s], n = offs[s + 1] - b;
+        const double m = double(n + 1) / 2.0;
+        double sxy = 0.0, sxx = 0.0, syy = 0.0, ng = 0.0;
+        const int64_t per = (n + kBlock - 1) / kBlock;
+        const int64_t k0 = b + int64_t(threadIdx.x) * per, k1 = k0 + per < b + n ? k0 + per : b + n;
+        if (k0 < k1) {
+            double v = sv[k0];
+            int64_t gs = lower_bound_d(sv, b, k0 + 1, v), ge = upper_bound_d(sv, k0, b + n, v);
+            ng += gs == k0 ? 1.0 : 0.0;
+            for (int64_t j = k0; j < k1; ++j) {
+                if (j > k0 && sv[j] != v) {
+                    v = sv[j];
+                    gs = j;
+                    ge = upper_bound_d(sv, j, b + n, v);
+                    ng += 1.0;
+                }
+                const double rx = double(pos[j] - b + 1) - m;
+                const double ry = double((gs - b) + (ge - b) + 1) / 2.0 - m;
+                sxy += rx * ry;
+                sxx += rx * rx;
+                syy += ry * ry;
+            }
+        }
+        sxy = block_sum(sxy, s_tmp);
+        sxx = block_sum(sxx, s_tmp);
+        syy = block_sum(syy, s_tmp);
+        ng = block_sum(ng, s_tmp);
+        if (threadIdx.x == 0) {
+            double r = NAN, p = NAN;
+            if (n >= 2 && ng > 1.0) {  // as seg_spearman_index
+                const double d = double(n - 1);
+                r = (sxy / d) / sqrt(sxx / d) / sqrt(syy / d);
+                if (r > 1.0) r = 1.0;
+                if (r < -1.0) r = -1.0;
+                const double dof = double(n - 2);
+                double q = dof / ((r + 1.0) * (1.0 - r));
+                if (q < 0.0) q = 0.0;
+                p = 2.0 * stats::t_sf(fabs(r * sqrt(q)), dof);
+            }
+            rho[s] = r;
+            if (pval) pval[s] = p;
+        }
+    }
+}
+
+void spearman_index_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const SortedSegs &ss, double *rho,
+                           double *pval) {
+    const Segs &sg = cs.sg;
+    if (sg.S <= 0) return;
+    if (sg.len_bound() <= kSpearmanSmall) {
+        k_spearman_index_small<<<unsigned(sg.S < 16384 ? sg.S : 16384), kBlock, 0, c->stream>>>(ss.val, ss.pos, sg.offs,
+                                                                                              sg.S, rho, pval);
+        FZ_LAUNCH_CHECK();
+        return;
+    }
+    TieRanks tr = seg_tie_ranks(c, cs, segid, ss.val);
+    seg_spearman_index(c, cs, ss, tr, rho, pval);
 }
 
 // ------------------------------------------------------------------------- Shapiro-Wilk
