@@ -309,9 +309,21 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
     const int64_t *d_nf = d_n;
     int64_t *offs2 = c->arena.get<int64_t>(S2 + 1);  // segment 2i: session i's G2 values, 2i + 1: G1
     segment_offsets_dn(c, sid2, d_nf, NC, S2, offs2);
-    map_n(c, MM, nullptr, [=] __device__(int64_t i) {
-        c2[i] = offs2[2 * i + 1] - offs2[2 * i];
-        c1[i] = offs2[2 * i + 2] - offs2[2 * i + 1];
+    const bool small = P <= kBmHalvesMax;  // Brunner-Munzel from the sorted halves (else rank passes)
+    int32_t *sess = small ? nullptr : c->arena.get<int32_t>(NC);
+    uint8_t *grp2 = small ? nullptr : c->arena.get<uint8_t>(NC);
+    int64_t *soffs = small ? nullptr : c->arena.get<int64_t>(MM + 1);
+    map_n(c, small ? MM : (NC > MM + 1 ? NC : MM + 1), nullptr, [=] __device__(int64_t k) {
+        if (k < MM) {
+            c2[k] = offs2[2 * k + 1] - offs2[2 * k];
+            c1[k] = offs2[2 * k + 2] - offs2[2 * k + 1];
+        }
+        if (small) return;
+        if (k <= MM) soffs[k] = offs2[2 * k];
+        if (k < NC) {
+            sess[k] = int32_t(sid2[k] >> 1);
+            grp2[k] = uint8_t(sid2[k] & 1u);
+        }
     });
     Segs sg2{S2, offs2, NC, P};
     SortedSegs ss2 = seg_sort_f64(c, v2, sg2, reinterpret_cast<const int32_t *>(sid2));
@@ -323,8 +335,17 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
         g2q[k] = qq[(2 * i) * 3 + j];
         g1q[k] = qq[(2 * i + 1) * 3 + j];
     });
-    // per-session Brunner-Munzel on the sorted halves (:978-985; NaN unless both sides >= 5)
-    bm_sorted_halves(c, ss2.val, offs2, MM, 5, pbm);
+    // per-session Brunner-Munzel (:978-985; NaN unless both sides >= 5)
+    if (small) {
+        bm_sorted_halves(c, ss2.val, offs2, MM, 5, pbm);
+        return;
+    }
+    RankTestOut rt;
+    rt.bm_p = pbm;
+    seg_rank_tests(c, v2, grp2, Segs{MM, soffs, NC, sess_len}, sess, rt);
+    map_n(c, MM, nullptr, [=] __device__(int64_t i) {
+        if (!(c2[i] >= 5 && c1[i] >= 5)) pbm[i] = NAN;
+    });
 }
 
 __global__ void k_rq4b_keys(const int64_t *__restrict__ sid, const uint8_t *__restrict__ grp, int64_t n,

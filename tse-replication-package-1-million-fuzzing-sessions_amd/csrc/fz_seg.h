@@ -349,6 +349,7 @@ void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, 
 // Brunner-Munzel p of M sessions whose samples are sorted halves: x = sorted[offs2[2i], offs2[2i+1]),
 // y = sorted[offs2[2i+1], offs2[2i+2]); NaN unless both hold >= min_n values.
 void bm_sorted_halves(fz_ctx *c, const double *sorted, const int64_t *offs2, int64_t M, int64_t min_n, double *pbm);
+constexpr int64_t kBmHalvesMax = 2048;  // bm_sorted_halves is for halves of at most this many values
 
 // spearmanr(range(n), x) per segment from the sorted segments: one workgroup per segment when they
 // are short (no tie-rank passes), else seg_tie_ranks + seg_spearman_index.

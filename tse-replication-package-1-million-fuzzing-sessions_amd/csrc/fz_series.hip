@@ -555,10 +555,13 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
     out.val = c->arena.get<double>(n);
     out.pos = c->arena.get<int32_t>(n);
     if (n <= 0 || sg.S <= 0) return out;
-    if (sg.S == 1 && sg.len_bound() > 16384) {
+    if (sg.S == 1 && sg.len_bound() > 16384 && n < (int64_t(1) << 22)) {
         // one long segment (RQ3's detected u non-detected union, a long series): the LSD radix sort
         // (8 passes at HBM rate, stable: ties keep position order, as the merge sort keeps them)
-        // instead of the merge sort's tile sort and log2(n / 4096) merge rounds
+        // instead of the merge sort's tile sort and log2(n / 4096) merge rounds.  It sorts the whole
+        // capacity, so only below 4 M entries: the merge sort's work follows the live length (a
+        // 100 M-row table's empty RQ3 union), and larger radix sorts would skip constant-digit
+        // passes after a host round trip that a recorded graph cannot make.
         uint64_t *k = c->arena.get<uint64_t>(n);
         uint32_t *v = c->arena.get<uint32_t>(n);
         k_f64_seg1_keys<<<grid_for(n, kBlock, 4096), kBlock, 0, c->stream>>>(src, n, sg.offs, k, v);
@@ -779,6 +782,8 @@ void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, 
     });
 }
 
+// (Used while one half holds at most kBmHalvesMax values - a few per thread: at config 3's 4,000-value
+// halves the per-thread walks are long dependent chains and the device-wide rank passes win.)
 // Brunner-Munzel p of M sessions whose two samples are already sorted: x = sv[offs2[2i],
 // offs2[2i + 1]), y = sv[offs2[2i + 1], offs2[2i + 2]), both ascending.  One workgroup per session,
 // each thread walking a contiguous run of one half in order (a merge): a value's average rank in
@@ -921,7 +926,7 @@ void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, 
 // a tie group's bounds come from one binary search when it starts, and the rank products are summed
 // directly - the same exact half-integer sums as seg_spearman_index, without the device-wide tie
 // rank passes.
-constexpr int64_t kSpearmanSmall = 65536;
+constexpr int64_t kSpearmanSmall = 4096;  // <= 16 values per thread: longer runs are latency chains
 __global__ __launch_bounds__(kBlock) void k_spearman_index_small(const double *__restrict__ sv,
                                                                  const int32_t *__restrict__ pos,
                                                                  const int64_t *__restrict__ offs, int64_t S,
