@@ -97,3 +97,21 @@ def test_store_edge_tables(engine, kind):
     t = _edge_table(kind)
     st = _check_all(engine, t)
     assert st.n_fuzz == int(np.sum(t.b_type == 0)) and st.n_coverage_builds == int(np.sum(t.b_type == 1))
+
+
+def test_long_segments_distribution_pass(engine):
+    """Segments longer than the bucket sorts' 16384 rows go through the store's distribution pass
+    (sub-buckets by time, each sorted by the long bucket class with ties ordered by prefix position):
+    a project of 23k rows per table with repeated timestamps (7 builds share each), NULL times
+    (ASC NULLS LAST) and coverage dates two to a day, checked through every analysis."""
+    from tse_amd.schema import TS_NULL, US_PER_DAY
+    cfg = synth.SynthConfig(n_projects=4, seed=41, zipf_s=1.0, len_mean_days=12000, issues_mean=150,
+                            dup_numbers=2, hex_len=10)
+    t = synth.generate(cfg)
+    week = 7 * US_PER_DAY
+    t.b_time = t.b_time // week * week
+    t.c_date = t.c_date // (2 * US_PER_DAY) * (2 * US_PER_DAY)
+    rng = np.random.default_rng(12)
+    t.b_time[rng.choice(len(t.b_time), size=60, replace=False)] = TS_NULL
+    st = _check_all(engine, t)
+    assert st.max_fuzz_per_project > 16384 and st.max_cov_per_project > 16384

@@ -8,6 +8,8 @@
 // (fz_segsort.h) when longer, with NULL timestamps last (PostgreSQL's ASC NULLS LAST) and equal
 // times in row order.  The bucket sorts write each sorted row's columns themselves (the segment's
 // rows are contiguous after the prefix passes); one pass then gathers the merge-sorted rows.
+#include <vector>
+
 #include "fz_device.h"
 #include "fz_internal.h"
 #include "fz_segsort.h"
@@ -281,6 +283,12 @@ struct TimeSortTab {
     const uint32_t *rows = nullptr;  // caller row ids in prefix order
     int32_t *orow = nullptr;
     GatherCols gc;
+    // sub-bucket pass of long segments (big_segments_bucketed): segment s's rows are written at
+    // output positions + oshift[s], its project is sproj[s], and equal times are ordered by tie[]
+    // (their prefix-order positions) instead of their position in the segment
+    const int64_t *oshift = nullptr;
+    const uint32_t *sproj = nullptr;
+    const uint32_t *tie = nullptr;
 };
 struct TimeSortTabs {
     TimeSortTab tab[3];
@@ -312,6 +320,8 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         uint8_t *bigflag = tb.bigflag;
         const int64_t b = tb.offs[s];
         const int64_t len = tb.offs[s + 1] - b;
+        const uint32_t *tie = KEYS_LDS ? nullptr : tb.tie;  // (the sub-bucket pass runs the long class)
+        const int64_t ob = b + (tb.oshift ? tb.oshift[s] : 0);  // where the sorted rows go
         if (len <= min_len) continue;
         if (len > MAXN) {
             if (flag_longer && tid == 0) flag_big(big, bigflag, s, len);
@@ -344,7 +354,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
             lo = s_lo[q] < lo ? s_lo[q] : lo;
             hi = s_hi[q] > hi ? s_hi[q] : hi;
         }
-        if (hi >= lo && uint64_t(hi) - uint64_t(lo) >= kBlkTop) {  // span too wide for the key
+        if (!tie && hi >= lo && uint64_t(hi) - uint64_t(lo) >= kBlkTop) {  // span too wide for the key
             if (tid == 0) flag_big(big, bigflag, s, len);
             __syncthreads();
             continue;
@@ -390,7 +400,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         uint32_t gmax = 0;
 #pragma unroll
         for (int q = 0; q < NW; ++q) gmax = s_max[q] > gmax ? s_max[q] : gmax;
-        if (gmax > uint32_t(kBucketSkew)) {  // clustered times: the merge sort takes the segment
+        if (!tie && gmax > uint32_t(kBucketSkew)) {  // clustered times: the merge sort takes the segment
             if (tid == 0) flag_big(big, bigflag, s, len);
             __syncthreads();
             continue;
@@ -401,7 +411,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
             if (i < n) s_pos[s_cnt[bs[m] >> 16] + (bs[m] & 0xffffu)] = uint16_t(i);
         }
         __syncthreads();
-        const uint32_t p = uint32_t(s) & tb.pmask;
+        const uint32_t p = tb.sproj ? tb.sproj[s] : uint32_t(s) & tb.pmask;
         int32_t dq[IPT];  // sorted position of row i inside the segment
 #pragma unroll
         for (int m = 0; m < IPT; ++m) {
@@ -410,11 +420,17 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
             if (i >= n) continue;
             const uint32_t st = s_cnt[bs[m] >> 16], en = s_cnt[(bs[m] >> 16) + 1];
             const uint64_t key = row_key(t[m], i);
+            const uint32_t my_tie = tie && en - st > 1 ? tie[b + i] : 0u;
             uint32_t rank = 0;
             // (a row alone in its bucket - the common case for evenly spread times - reads nothing)
             for (uint32_t x = st; en - st > 1 && x < en; ++x) {
                 const int ox = s_pos[x];
                 if (ox == i) continue;
+                if (tie) {  // (time, prefix position): no packed key, any span
+                    const int64_t tx = time[b + ox];
+                    rank += tx < t[m] || (tx == t[m] && tie[b + ox] < my_tie);
+                    continue;
+                }
                 uint64_t kx;
                 if (KEYS_LDS) {
                     kx = s_key[ox];
@@ -430,7 +446,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
             // segment's few KiB stay in L2); k_store_gather moves the other columns afterwards
 #pragma unroll
             for (int m = 0; m < IPT; ++m)
-                if (dq[m] >= 0) out.put(b + dq[m], t[m], p, b + tid + m * BS);
+                if (dq[m] >= 0) out.put(ob + dq[m], t[m], p, b + tid + m * BS);
             __syncthreads();  // LDS is reused by the next segment
             continue;
         }
@@ -452,7 +468,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
                     if (dq[m] >= h && dq[m] < h + CAP) stg[dq[m] - h] = x[m];
                 __syncthreads();
                 const int e = n - h < CAP ? n - h : CAP;
-                for (int q = tid; q < e; q += BS) store(b + h + q, stg[q]);
+                for (int q = tid; q < e; q += BS) store(ob + h + q, stg[q]);
                 __syncthreads();
             }
         };
@@ -478,9 +494,9 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         uint64_t xa[IPT], xb[kPrefetch ? IPT : 1];
         load(0, xa);
         for (int q = tid; q < n; q += BS) {
-            out.oproj[b + q] = p;
-            out.spos[b + q] = kGathered;
-            tb.orow[b + q] = int32_t(b + q);
+            out.oproj[ob + q] = p;
+            out.spos[ob + q] = kGathered;
+            tb.orow[ob + q] = int32_t(ob + q);
         }
         {
             uint64_t tt[IPT];
@@ -663,6 +679,249 @@ static void gather_tables(fz_ctx *c, const PrefixSorted *pss) {
     FZ_LAUNCH_CHECK();
 }
 
+// ---- long segments (> 16384 rows, config 5's Zipf head): one distribution pass --------------
+// A segment the bucket sorts flagged is cut by time into B = ceil(len / 8192) sub-buckets (the
+// bucket of t is floor((t - min) * B / (span + 1)), NULL last): a histogram per 65536-row tile in
+// LDS, one scan, then a scatter that moves every row's time, row id, prefix position and columns
+// into its sub-bucket of a compact copy (appends: each bucket's tail stays in L2).  The long bucket
+// class then sorts every sub-bucket as a segment - equal times ordered by prefix position - and
+// writes time, project, row id and columns to the segment's output range, coalesced.  This replaces
+// the segmented merge sort and the random gather of those rows (config 5: ~8x their algorithmic
+// bytes in HBM traffic).  Declined (the merge sort runs) for a segment of more than 8192 x 8192
+// rows; a sub-bucket that comes out longer than 16384 rows (clustered times) sends the table back
+// to the merge sort as well.
+constexpr int kBigTile = 65536;     // rows per histogram / scatter workgroup
+constexpr int kBigSub = 8192;       // target rows per sub-bucket
+constexpr int kBigMaxSub = 8192;    // sub-buckets per segment (LDS bins)
+struct BigPlan {
+    const int64_t *t_begin, *t_end;  // [tiles] prefix-order row range of the tile
+    const int32_t *t_seg;            // [tiles] big-segment index j of the tile
+    const int64_t *sbase;            // [nb] first sub-bucket of big segment j
+    const int32_t *nsub;             // [nb] sub-buckets of big segment j
+    const int64_t *cstart;           // [nb] compact start of big segment j
+    long long *lo, *hi;              // [nb] time range (non-NULL)
+    int64_t ntiles;
+};
+__device__ inline int big_sub(int64_t t, long long lo, long long hi, int B) {
+    if (t == FZ_TS_NULL || hi < lo) return B - 1;
+    const double q = double(uint64_t(t - lo)) * (double(B) / (double(uint64_t(hi) - uint64_t(lo)) + 1.0));
+    const int k = int(q);
+    return k < B ? k : B - 1;
+}
+__global__ __launch_bounds__(kBlock) void k_big_minmax(const int64_t *__restrict__ time, BigPlan pl) {
+    __shared__ int64_t s_lo[4], s_hi[4];
+    for (int64_t tl = blockIdx.x; tl < pl.ntiles; tl += gridDim.x) {
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        for (int64_t r = pl.t_begin[tl] + threadIdx.x; r < pl.t_end[tl]; r += kBlock) {
+            const int64_t t = time[r];
+            if (t == FZ_TS_NULL) continue;
+            lo = t < lo ? t : lo;
+            hi = t > hi ? t : hi;
+        }
+        lo = wave_min(lo);
+        hi = wave_max(hi);
+        if (lane_id() == 0) {
+            s_lo[wave_id()] = lo;
+            s_hi[wave_id()] = hi;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < 4; ++w) {
+                lo = s_lo[w] < lo ? s_lo[w] : lo;
+                hi = s_hi[w] > hi ? s_hi[w] : hi;
+            }
+            const int j = pl.t_seg[tl];
+            atomicMin(&pl.lo[j], (long long)lo);
+            atomicMax(&pl.hi[j], (long long)hi);
+        }
+        __syncthreads();
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_big_hist(const int64_t *__restrict__ time, BigPlan pl,
+                                                     int64_t *__restrict__ cnt) {
+    __shared__ uint32_t h[kBigMaxSub];
+    for (int64_t tl = blockIdx.x; tl < pl.ntiles; tl += gridDim.x) {
+        const int j = pl.t_seg[tl];
+        const int B = pl.nsub[j];
+        const long long lo = pl.lo[j], hi = pl.hi[j];
+        for (int k = threadIdx.x; k < B; k += kBlock) h[k] = 0u;
+        __syncthreads();
+        for (int64_t r = pl.t_begin[tl] + threadIdx.x; r < pl.t_end[tl]; r += kBlock)
+            atomicAdd(&h[big_sub(time[r], lo, hi, B)], 1u);
+        __syncthreads();
+        for (int k = threadIdx.x; k < B; k += kBlock)
+            if (h[k]) atomicAdd(reinterpret_cast<unsigned long long *>(&cnt[pl.sbase[j] + k]), (unsigned long long)h[k]);
+        __syncthreads();
+    }
+}
+struct BigCompact {
+    int64_t *time;
+    uint32_t *rows;
+    uint32_t *tie;
+    void *col[kMaxGather];
+};
+__global__ __launch_bounds__(kBlock) void k_big_scatter(const int64_t *__restrict__ time,
+                                                        const uint32_t *__restrict__ rows, GatherCols gc, BigPlan pl,
+                                                        unsigned long long *__restrict__ cursor, BigCompact out) {
+    __shared__ uint32_t h[kBigMaxSub];
+    __shared__ int64_t base[kBigMaxSub];
+    for (int64_t tl = blockIdx.x; tl < pl.ntiles; tl += gridDim.x) {
+        const int j = pl.t_seg[tl];
+        const int B = pl.nsub[j];
+        const long long lo = pl.lo[j], hi = pl.hi[j];
+        const int64_t r0 = pl.t_begin[tl], r1 = pl.t_end[tl];
+        for (int k = threadIdx.x; k < B; k += kBlock) h[k] = 0u;
+        __syncthreads();
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += kBlock) atomicAdd(&h[big_sub(time[r], lo, hi, B)], 1u);
+        __syncthreads();
+        // reserve this tile's range of every sub-bucket (compact positions), then place the rows
+        for (int k = threadIdx.x; k < B; k += kBlock) {
+            if (h[k]) base[k] = int64_t(atomicAdd(&cursor[pl.sbase[j] + k], (unsigned long long)h[k]));
+            h[k] = 0u;
+        }
+        __syncthreads();
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += kBlock) {
+            const int64_t t = time[r];
+            const int k = big_sub(t, lo, hi, B);
+            const int64_t d = base[k] + atomicAdd(&h[k], 1u);
+            out.time[d] = t;
+            out.rows[d] = rows[r];
+            out.tie[d] = uint32_t(r);
+            for (int c = 0; c < gc.n; ++c) {
+                if (gc.size[c] == 8)
+                    static_cast<uint64_t *>(out.col[c])[d] = static_cast<const uint64_t *>(gc.src[c])[r];
+                else if (gc.size[c] == 4)
+                    static_cast<uint32_t *>(out.col[c])[d] = static_cast<const uint32_t *>(gc.src[c])[r];
+                else
+                    static_cast<uint8_t *>(out.col[c])[d] = static_cast<const uint8_t *>(gc.src[c])[r];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// The distribution pass for the flagged segments of one prefix-sorted table (bigrows of its rows);
+// false: declined or a sub-bucket overflowed - the caller runs the merge sort (which rewrites every
+// row of the flagged segments, so nothing written here survives).
+static bool big_segments_bucketed(fz_ctx *c, const PrefixSorted &ps, int64_t bigrows) {
+    const int64_t S = ps.S;
+    std::vector<int64_t> offs(S + 1);
+    std::vector<uint8_t> flag(S);
+    FZ_HIP(hipMemcpyAsync(offs.data(), ps.offs, size_t(S + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    FZ_HIP(hipMemcpyAsync(flag.data(), ps.bigflag, size_t(S), hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    std::vector<int64_t> t_begin, t_end, sbase, cstart, oshift_seg;
+    std::vector<int32_t> t_seg, nsub, segid;
+    int64_t nsubs = 0, ncomp = 0;
+    for (int64_t s = 0; s < S; ++s) {
+        const int64_t len = offs[s + 1] - offs[s];
+        if (!flag[s] || len <= 0) continue;
+        const int64_t B = (len + kBigSub - 1) / kBigSub;
+        if (B > kBigMaxSub) return false;
+        const int32_t j = int32_t(segid.size());
+        segid.push_back(int32_t(s));
+        nsub.push_back(int32_t(B));
+        sbase.push_back(nsubs);
+        cstart.push_back(ncomp);
+        for (int64_t r = offs[s]; r < offs[s + 1]; r += kBigTile) {
+            t_begin.push_back(r);
+            t_end.push_back(r + kBigTile < offs[s + 1] ? r + kBigTile : offs[s + 1]);
+            t_seg.push_back(j);
+        }
+        nsubs += B;
+        ncomp += len;
+    }
+    if (segid.empty() || ncomp != bigrows) return false;
+    const int64_t nb = int64_t(segid.size()), nt = int64_t(t_seg.size());
+    // per sub-bucket: big segment, output shift (segment start - compact start), project
+    std::vector<int64_t> sub_shift(nsubs);
+    std::vector<uint32_t> sub_proj(nsubs);
+    for (int64_t j = 0; j < nb; ++j)
+        for (int64_t k = 0; k < nsub[j]; ++k) {
+            sub_shift[sbase[j] + k] = offs[segid[j]] - cstart[j];
+            sub_proj[sbase[j] + k] = uint32_t(segid[j]) & ps.pmask;
+        }
+    auto up = [&](const void *h, size_t bytes) {
+        void *d = c->arena.alloc(bytes);
+        FZ_HIP(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, c->stream));
+        return d;
+    };
+    BigPlan pl;
+    pl.t_begin = static_cast<const int64_t *>(up(t_begin.data(), size_t(nt) * 8));
+    pl.t_end = static_cast<const int64_t *>(up(t_end.data(), size_t(nt) * 8));
+    pl.t_seg = static_cast<const int32_t *>(up(t_seg.data(), size_t(nt) * 4));
+    pl.sbase = static_cast<const int64_t *>(up(sbase.data(), size_t(nb) * 8));
+    pl.nsub = static_cast<const int32_t *>(up(nsub.data(), size_t(nb) * 4));
+    pl.cstart = static_cast<const int64_t *>(up(cstart.data(), size_t(nb) * 8));
+    const int64_t *d_shift = static_cast<const int64_t *>(up(sub_shift.data(), size_t(nsubs) * 8));
+    const uint32_t *d_sproj = static_cast<const uint32_t *>(up(sub_proj.data(), size_t(nsubs) * 4));
+    std::vector<long long> lohi(2 * nb);
+    for (int64_t j = 0; j < nb; ++j) {
+        lohi[j] = INT64_MAX;
+        lohi[nb + j] = INT64_MIN;
+    }
+    long long *d_lohi = static_cast<long long *>(up(lohi.data(), size_t(2 * nb) * 8));
+    pl.lo = d_lohi;
+    pl.hi = d_lohi + nb;
+    pl.ntiles = nt;
+    sync(c);  // the host vectors above die with this function
+    const unsigned grid = unsigned(nt < 4096 ? nt : 4096);
+    k_big_minmax<<<grid, kBlock, 0, c->stream>>>(ps.time, pl);
+    FZ_LAUNCH_CHECK();
+    int64_t *cnt = c->arena.get<int64_t>(nsubs + 1);
+    dev_fill(c, cnt, 0, (nsubs + 1) * 8);
+    k_big_hist<<<grid, kBlock, 0, c->stream>>>(ps.time, pl, cnt);
+    FZ_LAUNCH_CHECK();
+    // sub-bucket offsets in the compact space (big segments back to back, in segment order)
+    int64_t *soffs = c->arena.get<int64_t>(nsubs + 1);
+    scan_exclusive_i64(c, cnt, soffs, nsubs + 1, nullptr);
+    unsigned long long *cursor = c->arena.get<unsigned long long>(nsubs);
+    dev_copy(c, cursor, soffs, nsubs * 8);
+    BigCompact cp;
+    cp.time = c->arena.get<int64_t>(ncomp);
+    cp.rows = c->arena.get<uint32_t>(ncomp);
+    cp.tie = c->arena.get<uint32_t>(ncomp);
+    GatherCols cg = ps.gc;  // the sub-bucket sort reads the compact columns, writes the table's
+    for (int k = 0; k < ps.gc.n; ++k) {
+        cp.col[k] = c->arena.alloc(size_t(ncomp) * size_t(ps.gc.size[k]));
+        cg.src[k] = cp.col[k];
+    }
+    {
+        ProbeScope probe(c, "big_scatter", (2.0 * (8 + 4 + 4) + 2.0 * ps.gc.bytes()) * double(ncomp));
+        k_big_scatter<<<grid, kBlock, 0, c->stream>>>(ps.time, ps.rows, ps.gc, pl, cursor, cp);
+        FZ_LAUNCH_CHECK();
+    }
+    // every sub-bucket a segment of the long bucket class; overflow (> 16384 rows) counted in big
+    unsigned long long *big = c->arena.get<unsigned long long>(6);
+    dev_fill(c, big, 0, 6 * 8);
+    uint8_t *flags = c->arena.get<uint8_t>(nsubs);
+    dev_fill(c, flags, 0, nsubs);
+    TimeSortTabs T;
+    TimeSortTab &tb = T.tab[0];
+    tb.time = cp.time;
+    tb.offs = soffs;
+    tb.pmask = ps.pmask;
+    tb.out = ps.out;
+    tb.big = big;
+    tb.bigflag = flags;
+    tb.rows = cp.rows;
+    tb.orow = ps.orow;
+    tb.gc = cg;
+    tb.oshift = d_shift;
+    tb.sproj = d_sproj;
+    tb.tie = cp.tie;
+    T.base[1] = T.base[2] = T.base[3] = nsubs;
+    {
+        ProbeScope probe(c, "big_sub_sort", 24.0 * double(ncomp));
+        const unsigned g16 = unsigned(nsubs < 256 ? nsubs : 256);
+        k_seg_time_bucket<1024, 16384><<<g16, 1024, 0, c->stream>>>(T, 0, true);
+        FZ_LAUNCH_CHECK();
+    }
+    FZ_HIP(hipMemcpyAsync(c->h_pinned + 16, big, 8, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    return c->h_pinned[16] == 0;
+}
+
 // The merge-sort path of the store: key = signed time as an order-preserving u64 (NULL =
 // INT64_MAX -> ~0: last), stable by row; the sink writes what the register sorts write.
 struct StoreTimeKey {
@@ -830,6 +1089,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     for (int k = 0; k < 3; ++k) {
         if (bigrows[k] == 0) continue;
         const PrefixSorted &ps = pss[k];
+        if (big_segments_bucketed(c, ps, bigrows[k])) continue;
         ProbeScope probe(c, "seg_merge_sort", 36.0 * double(bigrows[k]));
         sort_big_segments(c, ps.offs, ps.S, ps.n, bigmax[k], ps.bigflag, StoreTimeKey{ps.time},
                           StoreSink{ps.pmask, ps.out});
