@@ -690,7 +690,14 @@ static void gather_tables(fz_ctx *c, const PrefixSorted *pss) {
 // bytes in HBM traffic).  Declined (the merge sort runs) for a segment of more than 8192 x 8192
 // rows; a sub-bucket that comes out longer than 16384 rows (clustered times) sends the table back
 // to the merge sort as well.
-constexpr int kBigTile = 65536;     // rows per histogram / scatter workgroup
+#ifndef FZ_BIG_TILE
+#define FZ_BIG_TILE 65536
+#endif
+#ifndef FZ_BIG_BLOCK
+#define FZ_BIG_BLOCK 256
+#endif
+constexpr int kBigTile = FZ_BIG_TILE;    // rows per histogram / scatter workgroup
+constexpr int kBigBlock = FZ_BIG_BLOCK;  // threads of a histogram / scatter workgroup
 constexpr int kBigSub = 8192;       // target rows per sub-bucket
 constexpr int kBigMaxSub = 8192;    // sub-buckets per segment (LDS bins)
 struct BigPlan {
@@ -737,19 +744,19 @@ __global__ __launch_bounds__(kBlock) void k_big_minmax(const int64_t *__restrict
         __syncthreads();
     }
 }
-__global__ __launch_bounds__(kBlock) void k_big_hist(const int64_t *__restrict__ time, BigPlan pl,
+__global__ __launch_bounds__(kBigBlock) void k_big_hist(const int64_t *__restrict__ time, BigPlan pl,
                                                      int64_t *__restrict__ cnt) {
     __shared__ uint32_t h[kBigMaxSub];
     for (int64_t tl = blockIdx.x; tl < pl.ntiles; tl += gridDim.x) {
         const int j = pl.t_seg[tl];
         const int B = pl.nsub[j];
         const long long lo = pl.lo[j], hi = pl.hi[j];
-        for (int k = threadIdx.x; k < B; k += kBlock) h[k] = 0u;
+        for (int k = threadIdx.x; k < B; k += kBigBlock) h[k] = 0u;
         __syncthreads();
-        for (int64_t r = pl.t_begin[tl] + threadIdx.x; r < pl.t_end[tl]; r += kBlock)
+        for (int64_t r = pl.t_begin[tl] + threadIdx.x; r < pl.t_end[tl]; r += kBigBlock)
             atomicAdd(&h[big_sub(time[r], lo, hi, B)], 1u);
         __syncthreads();
-        for (int k = threadIdx.x; k < B; k += kBlock)
+        for (int k = threadIdx.x; k < B; k += kBigBlock)
             if (h[k]) atomicAdd(reinterpret_cast<unsigned long long *>(&cnt[pl.sbase[j] + k]), (unsigned long long)h[k]);
         __syncthreads();
     }
@@ -760,7 +767,7 @@ struct BigCompact {
     uint32_t *tie;
     void *col[kMaxGather];
 };
-__global__ __launch_bounds__(kBlock) void k_big_scatter(const int64_t *__restrict__ time,
+__global__ __launch_bounds__(kBigBlock) void k_big_scatter(const int64_t *__restrict__ time,
                                                         const uint32_t *__restrict__ rows, GatherCols gc, BigPlan pl,
                                                         unsigned long long *__restrict__ cursor, BigCompact out) {
     __shared__ uint32_t h[kBigMaxSub];
@@ -770,17 +777,17 @@ __global__ __launch_bounds__(kBlock) void k_big_scatter(const int64_t *__restric
         const int B = pl.nsub[j];
         const long long lo = pl.lo[j], hi = pl.hi[j];
         const int64_t r0 = pl.t_begin[tl], r1 = pl.t_end[tl];
-        for (int k = threadIdx.x; k < B; k += kBlock) h[k] = 0u;
+        for (int k = threadIdx.x; k < B; k += kBigBlock) h[k] = 0u;
         __syncthreads();
-        for (int64_t r = r0 + threadIdx.x; r < r1; r += kBlock) atomicAdd(&h[big_sub(time[r], lo, hi, B)], 1u);
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += kBigBlock) atomicAdd(&h[big_sub(time[r], lo, hi, B)], 1u);
         __syncthreads();
         // reserve this tile's range of every sub-bucket (compact positions), then place the rows
-        for (int k = threadIdx.x; k < B; k += kBlock) {
+        for (int k = threadIdx.x; k < B; k += kBigBlock) {
             if (h[k]) base[k] = int64_t(atomicAdd(&cursor[pl.sbase[j] + k], (unsigned long long)h[k]));
             h[k] = 0u;
         }
         __syncthreads();
-        for (int64_t r = r0 + threadIdx.x; r < r1; r += kBlock) {
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += kBigBlock) {
             const int64_t t = time[r];
             const int k = big_sub(t, lo, hi, B);
             const int64_t d = base[k] + atomicAdd(&h[k], 1u);
@@ -870,7 +877,7 @@ static bool big_segments_bucketed(fz_ctx *c, const PrefixSorted &ps, int64_t big
     FZ_LAUNCH_CHECK();
     int64_t *cnt = c->arena.get<int64_t>(nsubs + 1);
     dev_fill(c, cnt, 0, (nsubs + 1) * 8);
-    k_big_hist<<<grid, kBlock, 0, c->stream>>>(ps.time, pl, cnt);
+    k_big_hist<<<grid, kBigBlock, 0, c->stream>>>(ps.time, pl, cnt);
     FZ_LAUNCH_CHECK();
     // sub-bucket offsets in the compact space (big segments back to back, in segment order)
     int64_t *soffs = c->arena.get<int64_t>(nsubs + 1);
@@ -888,7 +895,7 @@ static bool big_segments_bucketed(fz_ctx *c, const PrefixSorted &ps, int64_t big
     }
     {
         ProbeScope probe(c, "big_scatter", (2.0 * (8 + 4 + 4) + 2.0 * ps.gc.bytes()) * double(ncomp));
-        k_big_scatter<<<grid, kBlock, 0, c->stream>>>(ps.time, ps.rows, ps.gc, pl, cursor, cp);
+        k_big_scatter<<<grid, kBigBlock, 0, c->stream>>>(ps.time, ps.rows, ps.gc, pl, cursor, cp);
         FZ_LAUNCH_CHECK();
     }
     // every sub-bucket a segment of the long bucket class; overflow (> 16384 rows) counted in big
