@@ -694,7 +694,7 @@ static void gather_tables(fz_ctx *c, const PrefixSorted *pss) {
 #define FZ_BIG_TILE 65536
 #endif
 #ifndef FZ_BIG_BLOCK
-#define FZ_BIG_BLOCK 256
+#define FZ_BIG_BLOCK 1024
 #endif
 constexpr int kBigTile = FZ_BIG_TILE;    // rows per histogram / scatter workgroup
 constexpr int kBigBlock = FZ_BIG_BLOCK;  // threads of a histogram / scatter workgroup
