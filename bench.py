@@ -387,6 +387,21 @@ def pmc_traffic(probe, config):
     return None
 
 
+def cgroup_cpus():
+    """CPUs of the cgroup v2 / v1 CPU quota of this process (None: unlimited or unreadable)."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, q // p)
+    except (OSError, ValueError):
+        return None
+
+
 def weak_shard(t, rank, world):
     """Rank `rank`'s table as one shard of a world-times-larger job: project ids rank * P + p in a
     global id space of world * P projects.  Issue numbers keep their values: the ranks draw them
@@ -420,15 +435,22 @@ def cpu_baseline(t, stages):
     small enough to finish in ~10 s (<= 4 M rows)."""
     from oracle import cpu_baseline as cb
     stages = [s for s in stages if s in cb.STAGES]
-    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    cores = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or aff), aff))
+    host_cpus = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else host_cpus
+    quota = cgroup_cpus()
+    # every core this process may use: the affinity set, capped by the cgroup CPU quota (on the GPU
+    # box os.cpu_count() is the whole machine; the job's share is the quota / OMP_NUM_THREADS)
+    share = min(aff, quota) if quota else aff
+    cores = max(1, min(int(os.environ.get("OMP_NUM_THREADS") or share), aff))
     host = cb.HostTables(t)
+    big = t.n_rows > 20_000_000  # configs 3 / 5: one run is seconds; keep the leg to ~30 s
 
-    def timed(threads, min_s):
-        cb.run(host, stages, threads)  # warm: page faults, thread pool
+    def timed(threads, min_s, reps_min):
+        if not big:
+            cb.run(host, stages, threads)  # warm: page faults, thread pool
         walls, parts = [], []
         t_end = time.perf_counter() + min_s
-        while len(walls) < 3 or (time.perf_counter() < t_end and len(walls) < 20):
+        while len(walls) < reps_min or (time.perf_counter() < t_end and len(walls) < 20):
             t0 = time.perf_counter()
             _, secs = cb.run(host, stages, threads)
             walls.append(time.perf_counter() - t0)
@@ -436,11 +458,14 @@ def cpu_baseline(t, stages):
         k = int(np.argsort(walls)[len(walls) // 2])
         return walls[k], parts[k], len(walls)
 
-    wall, parts, reps = timed(cores, 3.0)
-    one, _, reps1 = timed(1, 2.0)
+    wall, parts, reps = timed(cores, 0.0 if big else 3.0, 2 if big else 3)
+    one, _, reps1 = timed(1, 0.0 if big else 2.0, 1 if big else 3)
+    how = "fastest of" if reps == 2 else "median of"
     out = {"value": round(t.n_rows / wall, 1), "unit": "session-rows/s", "cores": cores, "kind": "port",
-           "sample": f"oracle/cpu/fz_cpu.cpp (C++17, OpenMP, {cores} threads): index build + "
-                     f"{'+'.join(stages)} on the full bench table ({t.n_rows} rows), median of {reps} runs "
+           "host_cpus": host_cpus, "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+           "sample": f"oracle/cpu/fz_cpu.cpp (C++17, OpenMP, {cores} threads = every CPU of this job's share: "
+                     f"affinity {aff}, cgroup quota {quota or 'none'}, machine {host_cpus}): index build + "
+                     f"{'+'.join(stages)} on the full bench table ({t.n_rows} rows), {how} {reps} runs "
                      f"({wall * 1e3:.1f} ms; " + ", ".join(f"{k} {v * 1e3:.1f}" for k, v in parts.items() if v)
                      + " ms)",
            "single_core": {"value": round(t.n_rows / one, 1), "cores": 1,

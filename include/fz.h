@@ -178,6 +178,9 @@ enum {
     FZ_RQ2C_SESSIONS,       /* len(coverage_by_session_index) = max(1, longest trend)  :285,330 */
     FZ_RQ2C_GE100,          /* sessions with >= 100 values (a prefix)                  :390 */
     FZ_RQ2C_VALUES,         /* trend values over all projects                          :300-303 */
+    FZ_RQ2C_NULL_LINES,     /* fetched rows whose float(covered) / float(total) meets a NULL line
+                               count (`x[1] != 0` keeps a None total): the reference raises
+                               TypeError there (:300-303), so the caller must when non-zero */
     FZ_RQ2C_NCOUNTS = 8
 };
 enum {
@@ -263,6 +266,11 @@ enum {
     FZ_RQ3_ELIGIBLE,
     FZ_RQ3_NON_LAST,              /* non-detected rows of the last issue-bearing project (0 unless
                                      FZ_RQ3_FLUSH_LAST; they are the tail of non_*) */
+    FZ_RQ3_NULL_TOTAL,            /* coverage pairs whose `prev[2] > 0 and curr[2] > 0` test meets a NULL
+                                     total_line (rq3:253,297): the reference raises TypeError there, so
+                                     the caller must too when this is non-zero */
+    FZ_RQ3_NULL_LAST,             /* those of them in the flush of the last issue-bearing project
+                                     (0 unless FZ_RQ3_FLUSH_LAST; dropped with FZ_RQ3_NON_LAST) */
     FZ_RQ3_NCOUNTS = 8
 };
 enum {

@@ -182,7 +182,9 @@ def rq2_count(t: Tables) -> RQ2CountResult:
             continue
         cv = t.c_covered[rows].astype(np.float64)
         tt = t.c_total[rows].astype(np.float64)
-        keep = t.c_total[rows] != 0
+        keep = (t.c_total[rows] != 0) | ~t.c_total_valid[rows]  # None != 0 keeps a NULL total
+        if not (t.c_total_valid[rows][keep].all() and t.c_covered_valid[rows][keep].all()):
+            raise TypeError(FLOAT_NONE_MSG)                     # float(None) (:301)
         trend = list(cv[keep] / tt[keep] * 100)                 # :300-303
         n_tr.append(len(trend))
         if len(trend) >= 3:                                     # :305-314
@@ -324,10 +326,20 @@ def rq3_stats(dpct, dtot, npct):
                 brunnermunzel=bm)
 
 
-def rq3(t: Tables, flush_last: bool = False) -> RQ3Result:
+NULL_TOTAL_MSG = "'>' not supported between instances of 'NoneType' and 'int'"
+FLOAT_NONE_MSG = "float() argument must be a string or a real number, not 'NoneType'"
+
+
+def rq3(t: Tables, flush_last: bool = False, on_null: str = "raise") -> RQ3Result:
     """rq3_diff_coverage_at_detection.py:202-360.  ``flush_last`` (fz_rq3_ex FZ_RQ3_FLUSH_LAST, a
     shard that is not the last one): flush the last issue-bearing project too and report its row
-    count in ``n_non_last``."""
+    count in ``n_non_last``.
+
+    NULL total_line: the coverage query filters only ``covered_line IS NOT NULL`` (:263), and the
+    pair test ``prev_cov[2] > 0 and curr_cov[2] > 0`` (:253, :297) raises TypeError on a None
+    total on the left, or on the right after a positive left.  ``on_null="raise"`` raises that
+    TypeError when any examined pair meets one; ``"count"`` (shards) reports them in
+    ``n_null_total`` (``n_null_last`` of them in the final flush of ``flush_last``)."""
     P = len(t.projects)
     elig = eligible_projects(t)
     is_elig = np.zeros(P, bool)
@@ -342,6 +354,13 @@ def rq3(t: Tables, flush_last: bool = False) -> RQ3Result:
     canon = t.rev_canon()
     det = []
     non = []
+    nulls = [0]
+
+    def null_cmp(a, b):                                           # None > 0 raises (:253, :297)
+        if not t.c_total_valid[a] or (t.c_total[a] > 0 and not t.c_total_valid[b]):
+            nulls[0] += 1
+            return True
+        return False
 
     def flush(proj):                                              # :245-257
         rows = tc.rows(proj)
@@ -350,7 +369,9 @@ def rq3(t: Tables, flush_last: bool = False) -> RQ3Result:
             dd = {d[4] // US_PER_DAY for d in det if d[3] == proj}
             for k in range(1, len(rows)):
                 a, b = rows[k - 1], rows[k]
-                if t.c_date[b] // US_PER_DAY not in dd and t.c_total[a] > 0 and t.c_total[b] > 0:
+                if t.c_date[b] // US_PER_DAY in dd or null_cmp(a, b):
+                    continue
+                if t.c_total[a] > 0 and t.c_total[b] > 0:
                     non.append(((t.c_covered[b] / t.c_total[b] - t.c_covered[a] / t.c_total[a]) * 100,
                                 int(t.c_covered[b] - t.c_covered[a]), int(t.c_total[b] - t.c_total[a])))
         return len(non) - n0
@@ -392,10 +413,15 @@ def rq3(t: Tables, flush_last: bool = False) -> RQ3Result:
         if pair is None:
             continue
         a, b = pair
+        if null_cmp(a, b):
+            continue
         if t.c_total[a] > 0 and t.c_total[b] > 0:
             det.append(((t.c_covered[b] / t.c_total[b] - t.c_covered[a] / t.c_total[a]) * 100,
                         int(t.c_covered[b] - t.c_covered[a]), int(t.c_total[b] - t.c_total[a]), p, rts, i))
+    null_before = nulls[0]
     n_last = flush(cur) if (flush_last and cur >= 0) else 0
+    if nulls[0] and on_null == "raise":
+        raise TypeError(NULL_TOTAL_MSG)
     dpct = np.array([d[0] for d in det], np.float64)
     npct = np.array([d[0] for d in non], np.float64)
     dtot = np.array([d[2] for d in det], np.int64)
@@ -403,7 +429,8 @@ def rq3(t: Tables, flush_last: bool = False) -> RQ3Result:
                      det_tot=dtot, det_project=np.array([d[3] for d in det], np.int64),
                      det_issue=np.array([d[5] for d in det], np.int64), non_pct=npct,
                      non_cov=np.array([d[1] for d in non], np.int64), non_tot=np.array([d[2] for d in non], np.int64),
-                     n_non_last=n_last, **rq3_stats(dpct, dtot, npct))
+                     n_non_last=n_last, n_null_total=nulls[0], n_null_last=nulls[0] - null_before,
+                     **rq3_stats(dpct, dtot, npct))
 
 
 # --------------------------------------------------------------------------------------- RQ4a

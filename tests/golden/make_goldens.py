@@ -31,6 +31,8 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 
 import tse_amd.synth as synth  # noqa: E402
+sys.path.insert(0, os.path.dirname(HERE))
+import null_edges  # noqa: E402
 from tse_amd.schema import CODE_NULL, TS_NULL, us_to_dt  # noqa: E402
 
 REFERENCE = "/root/reference"
@@ -145,8 +147,13 @@ def prune_change_analysis(out_dir, keep=6):
 
 
 def run_case(case: str, out_root: str):
-    cfg = synth.config(case)
+    base, edge = null_edges.split(case)
+    cfg = synth.config(base)
     t = synth.generate(cfg)
+    scripts = SCRIPTS
+    if edge:  # NULL line-count edges (tests/null_edges.py): one changed row, two scripts
+        t = null_edges.apply(t, edge)
+        scripts = null_edges.SCRIPTS
     work = tempfile.mkdtemp(prefix=f"fzgold_{case}_")
     os.symlink(os.path.join(REFERENCE, "program"), os.path.join(work, "program"))
     for d in ("fake", "stubs/psycopg2", "data/processed_data/csv"):
@@ -168,10 +175,10 @@ def run_case(case: str, out_root: str):
     shutil.rmtree(out_dir, ignore_errors=True)
     os.makedirs(out_dir)
     meta = {"case": case, "config": {k: (list(v) if isinstance(v, tuple) else v) for k, v in cfg.__dict__.items()},
-            "fingerprint": synth.table_fingerprint(t), "scripts": {}}
+            "fingerprint": null_edges.fingerprint(t) if edge else synth.table_fingerprint(t), "scripts": {}}
     env = dict(os.environ, FAKE_DB=db, MPLBACKEND="Agg", PYTHONDONTWRITEBYTECODE="1",
                PYTHONPATH=os.path.join(work, "stubs"), PYTHONHASHSEED="0")
-    for s in SCRIPTS:
+    for s in scripts:
         t0 = time.time()
         proc = subprocess.run([sys.executable, "-B", "-c", RUNNER % s], cwd=work, env=env,
                               capture_output=True, text=True)
@@ -210,5 +217,7 @@ if __name__ == "__main__":
     if not os.path.isdir(REFERENCE):
         sys.exit("the reference is not present: goldens can only be regenerated in the build container")
     cases = sys.argv[1:] or ["tiny", "medium"]
+    if cases == ["edges"]:
+        cases = ["tiny+" + e for e in null_edges.EDGES]
     for c in cases:
         run_case(c, HERE)

@@ -19,12 +19,23 @@ SCRIPTS = ["rq1_detection_rate", "rq2_coverage_count", "rq2_coverage_and_added",
 
 @lru_cache(maxsize=4)
 def tables(case):
+    """The synthetic table of a golden case ('tiny', 'medium', or 'tiny+<edge>' of null_edges)."""
+    import null_edges
     with open(os.path.join(GOLDEN, case, "meta.json")) as f:
         meta = json.load(f)
-    t = synth.generate(synth.config(case))
-    assert synth.table_fingerprint(t) == meta["fingerprint"], \
+    base, edge = null_edges.split(case)
+    t = synth.generate(synth.config(base))
+    if edge:
+        t = null_edges.apply(t, edge)
+    fp = null_edges.fingerprint(t) if edge else synth.table_fingerprint(t)
+    assert fp == meta["fingerprint"], \
         f"synthetic tables for '{case}' drifted from the golden fixture; regenerate goldens"
     return t
+
+
+def returncode(case, script):
+    with open(os.path.join(GOLDEN, case, "meta.json")) as f:
+        return json.load(f)["scripts"][script]["returncode"]
 
 
 def text(case, script, stream="stdout"):

@@ -127,7 +127,7 @@ def _check(rank, world, case):
     if rank == 0:
         ours2 = compute.rq2_count_result(r2["proj"], r2["session_offsets"], r2["session_values"], r2["K"],
                                          r2["average"], r2["median"], r2["percentiles"], r2["average"],
-                                         (r2["tests"][0], r2["tests"][1], r2["tests"][3]), r2["corr_mm"])
+                                         (r2["tests"][0], r2["tests"][1], r2["tests"][3]), r2["corr_mm"], r2["null_lines"])
         assert_same(ours2, orc.rq2_count(t), "rq2_count")
         ours4 = compute.rq4a_result(r4["counts"], r4["scalars"], r4["member"], r4["tables"], r4["intro"],
                                     r4["g4_steps"], r4["g4_transition"])

@@ -113,5 +113,65 @@ def test_long_segments_distribution_pass(engine):
     t.c_date = t.c_date // (2 * US_PER_DAY) * (2 * US_PER_DAY)
     rng = np.random.default_rng(12)
     t.b_time[rng.choice(len(t.b_time), size=60, replace=False)] = TS_NULL
-    st = _check_all(engine, t)
+    st, merged = _check_all_probed(engine, t)
     assert st.max_fuzz_per_project > 16384 and st.max_cov_per_project > 16384
+    assert merged == 0  # the distribution pass sorted every long segment (no merge-sort fallback)
+
+
+def _check_all_probed(engine, t):
+    """_check_all, with the store's merge-sort launches counted (fz_probe 'seg_merge_sort')."""
+    engine.upload(t)
+    engine.probe_begin("seg_merge_sort")
+    st = engine.build_store()
+    n, _, _ = engine.probe_end()
+    for name, gpu, cpu in STAGES:
+        assert_same(gpu(engine), cpu(t), path=name)
+    return st, n
+
+
+def _giant_table():
+    cfg = synth.SynthConfig(n_projects=4, seed=41, zipf_s=1.0, len_mean_days=12000, issues_mean=150,
+                            dup_numbers=2, hex_len=10)
+    t = synth.generate(cfg)
+    big = int(np.argmax(np.bincount(t.b_project, minlength=4)))
+    return t, big
+
+
+@pytest.mark.parametrize("kind", ["one_timestamp", "nulls"])
+def test_long_segment_repeated_time(engine, kind):
+    """A > 16384-row segment that is mostly ONE timestamp (or NULL): the sub-bucket pass ranks a
+    bucket's rows against each other (quadratic in the bucket), so a bucket of more than 256 equal
+    times makes it decline and the merge sort sorts the table's long segments instead - stable
+    (equal times keep row order, NULLS LAST), checked through every analysis, and timed."""
+    import time
+    from tse_amd.schema import TS_NULL
+    t, big = _giant_table()
+    rows = np.nonzero(t.b_project == big)[0]
+    rng = np.random.default_rng(17)
+    pick = rows[rng.random(len(rows)) < 0.8]
+    t.b_time[pick] = TS_NULL if kind == "nulls" else int(np.median(t.b_time[rows]))
+    crow = np.nonzero(t.c_project == big)[0]
+    t.c_date[crow[: len(crow) * 3 // 4]] = int(t.c_date[crow[0]])
+    engine.upload(t)
+    engine.build_store()  # warm
+    t0 = time.perf_counter()
+    engine.build_store()
+    engine.synchronize()
+    secs = time.perf_counter() - t0
+    st, merged = _check_all_probed(engine, t)
+    assert st.max_fuzz_per_project > 16384 and merged > 0
+    assert secs < 2.0, f"store build took {secs:.2f} s"
+
+
+def test_long_segment_outlier_time_overflows_to_merge_sort(engine):
+    """One far-future timestamp in a > 16384-row segment: the sub-buckets are linear in time, so
+    nearly every row lands in sub-bucket 0, which overflows the long bucket class; the pass reports
+    it and the merge sort rewrites the flagged segments (nothing the pass wrote survives)."""
+    from tse_amd.schema import ts_from_str
+    t, big = _giant_table()
+    rows = np.nonzero(t.b_project == big)[0]
+    t.b_time[rows[len(rows) // 2]] = ts_from_str("2199-06-01")
+    crow = np.nonzero(t.c_project == big)[0]
+    t.c_date[crow[7]] = ts_from_str("2199-06-01")
+    st, merged = _check_all_probed(engine, t)
+    assert st.max_fuzz_per_project > 16384 and merged > 0

@@ -107,10 +107,11 @@ class OracleRQ3Shard:
 
     def run(self):
         from oracle import rq_oracle as orc
-        r = orc.rq3(self.t, flush_last=True)
+        r = orc.rq3(self.t, flush_last=True, on_null="count")
         c = np.zeros(par.RQ3_NCOUNTS, np.int64)
         c[par.RQ3_ISSUES], c[par.RQ3_DETECTED], c[par.RQ3_NON_DETECTED] = r.n_all_issues, len(r.det_pct), len(r.non_pct)
         c[par.RQ3_ELIGIBLE], c[par.RQ3_NON_LAST] = len(orc.eligible_projects(self.t)), r.n_non_last
+        c[par.RQ3_NULL_TOTAL], c[par.RQ3_NULL_LAST] = r.n_null_total, r.n_null_last
         T = lambda a, dt=np.int64: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))  # noqa: E731
         return {"counts": T(c), "det_pct": T(r.det_pct, np.float64), "det_cov": T(r.det_cov), "det_tot": T(r.det_tot),
                 "det_project": T(r.det_project), "det_issue": T(self.rows.issues[r.det_issue]),
@@ -371,7 +372,7 @@ def _check(rank, world, case):
     from tse_amd.rq import compute
     ours2 = compute.rq2_count_result(r2["proj"], r2["session_offsets"], r2["session_values"], r2["K"],
                                      r2["average"], r2["median"], r2["percentiles"], r2["average"],
-                                     (r2["tests"][0], r2["tests"][1], r2["tests"][3]), r2["corr_mm"])
+                                     (r2["tests"][0], r2["tests"][1], r2["tests"][3]), r2["corr_mm"], r2["null_lines"])
     assert_same(ours2, orc.rq2_count(t), "rq2_count")
     ours4 = compute.rq4a_result(r4["counts"], r4["scalars"], r4["member"], r4["tables"], r4["intro"], r4["g4_steps"],
                                 r4["g4_transition"])

@@ -41,7 +41,21 @@ struct fz_graph {
     // the context's host-side look-back / radix state after one replay
     unsigned int epoch_end;
     int hist_end;
+    uint64_t sig;  // ctx_signature() at the end of the recording
 };
+
+namespace {
+// The device state a recording bakes in: the store it reads (the parent's, for a child) and the
+// context's own look-back / radix buffers.  fz_graph_launch refuses a replay after any of them was
+// reallocated or the store was rebuilt over other tables (the graph would use freed memory or
+// stale sizes).
+uint64_t ctx_signature(fz_ctx *c) {
+    uint64_t h = fz::store_of(c).signature();
+    for (const fz::DevBuf *d : {&c->os_status, &c->os_ticket, &c->os_hist})
+        h = (h ^ (reinterpret_cast<uintptr_t>(d->ptr) + 0x9e3779b97f4a7c15ull * d->gen)) * 1099511628211ull;
+    return h;
+}
+}  // namespace
 
 namespace {
 thread_local std::string g_err;
@@ -398,7 +412,7 @@ int fz_capture_end(fz_ctx *ctx, fz_graph **out) {
         }
         // the host-side look-back / radix state a replay leaves behind (fz_graph_launch restores it,
         // so direct calls can follow a replay); nothing ran while recording: reset the live state
-        *out = new fz_graph{g, x, ctx->os_epoch, ctx->os_hist_cur};
+        *out = new fz_graph{g, x, ctx->os_epoch, ctx->os_hist_cur, ctx_signature(ctx)};
         fz::lookback_reset(ctx);
         ctx->os_hist_cur = -1;
     });
@@ -407,6 +421,9 @@ int fz_capture_end(fz_ctx *ctx, fz_graph **out) {
 int fz_graph_launch(fz_ctx *ctx, fz_graph *graph) {
     return guarded(ctx, [&] {
         FZ_CHECK(graph != nullptr, "fz_graph_launch: null graph");
+        FZ_STATE(graph->sig == ctx_signature(ctx),
+                 "fz_graph_launch: the store or a context buffer the recording uses was rebuilt over other "
+                 "tables or reallocated since fz_capture_end; record the graph again");
         FZ_HIP(hipGraphLaunch(graph->exec, ctx->stream));
         ctx->os_epoch = graph->epoch_end;
         ctx->os_hist_cur = graph->hist_end;

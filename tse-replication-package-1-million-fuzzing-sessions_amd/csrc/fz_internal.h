@@ -42,6 +42,12 @@ struct Error : std::runtime_error {
         if (!(cond)) throw ::fz::Error(FZ_E_INVALID, std::string(msg)); \
     } while (0)
 
+// a call out of order (FZ_E_STATE), e.g. a graph replay over a changed store
+#define FZ_STATE(cond, msg)                                              \
+    do {                                                                 \
+        if (!(cond)) throw ::fz::Error(FZ_E_STATE, std::string(msg));   \
+    } while (0)
+
 #define FZ_LAUNCH_CHECK() FZ_HIP(hipGetLastError())
 
 // Grow-only bump allocator over device blocks.
@@ -94,6 +100,7 @@ class Arena {
 struct DevBuf {
     void *ptr = nullptr;
     size_t cap = 0;
+    uint64_t gen = 0;  // bumped by every (re)allocation: a recorded graph holding ptr checks it
     ~DevBuf() {
         if (ptr) (void)hipFree(ptr);
     }
@@ -105,6 +112,7 @@ struct DevBuf {
             ptr = nullptr;
             FZ_HIP(hipMalloc(&ptr, bytes));
             cap = bytes;
+            ++gen;
         }
         return static_cast<T *>(ptr);
     }
@@ -148,6 +156,30 @@ struct Store {
     DevBuf sb_type, sb_result, sb_group, sb_canon, sc_coverage, sc_covered, sc_total, sc_valid, si_number, si_status;
     DevBuf b_perm, c_perm, i_perm;
     const int32_t *bperm = nullptr, *cperm = nullptr, *iperm = nullptr;
+
+    // What a recorded analysis graph bakes in from the store: the sorted tables' pointers and sizes
+    // and the buffers behind them.  Equal signatures = a replay reads what the recording read
+    // (a rebuild over a table of the same shape keeps it; a reallocation or another table does not).
+    uint64_t signature() const {
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+        mix(built);
+        mix(uint64_t(P));
+        const unsigned char *tb = reinterpret_cast<const unsigned char *>(&t);
+        for (size_t i = 0; i < sizeof(t); ++i) mix(tb[i]);
+        for (const DevBuf *d : {&b_row, &b_time, &b_proj, &c_row, &c_time, &c_proj, &i_row, &i_time, &i_proj,
+                                &off_fuzz, &off_covb, &off_cov, &off_iss, &elig, &n_elig, &sb_type, &sb_result,
+                                &sb_group, &sb_canon, &sc_coverage, &sc_covered, &sc_total, &sc_valid, &si_number,
+                                &si_status, &b_perm, &c_perm, &i_perm}) {
+            mix(reinterpret_cast<uintptr_t>(d->ptr));
+            mix(d->gen);
+        }
+        for (const View *v : {&fuzz, &covb, &cov, &issues}) {
+            mix(uint64_t(v->n));
+            mix(uint64_t(v->max_seg));
+        }
+        return h;
+    }
 };
 
 // Per-kernel timing probe (fz_probe_begin/end/get): brackets every launch of the named kernels

@@ -28,10 +28,11 @@ struct CovTrendRows {  // coverage IS NOT NULL AND coverage != 0 AND DATE(date) 
         return (valid[r] & FZ_VALID_COVERAGE) && cov[r] != 0.0 && date[r] < kLimitUs2 && elig[proj[r]];
     }
 };
-struct NonZeroTotal {  // `if total != 0` (:300-303)
-    static constexpr int kBytes = 8;  // column bytes read per row (filter_compact probe)
+struct NonZeroTotal {  // `if x[1] != 0` (:300-303); a NULL total (stored 0) passes: None != 0
+    static constexpr int kBytes = 9;  // column bytes read per row (filter_compact probe)
     const int64_t *total;
-    __device__ bool operator()(int32_t r) const { return total[r] != 0; }
+    const uint8_t *valid;
+    __device__ bool operator()(int32_t r) const { return total[r] != 0 || !(valid[r] & FZ_VALID_TOTAL); }
 };
 
 // statistics.mean / median + np.percentile(5, 25, 50, 75, 95) of every session segment; sessions
@@ -121,7 +122,7 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     TmpView V, T;
     filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P,
                 CovTrendRows{t.c_project, t.c_coverage, t.c_valid, t.c_date, o->eligible}, V);
-    filter_view(c, V.row, V.time, V.proj, NC, P, NonZeroTotal{t.c_total}, T, V.d_n);
+    filter_view(c, V.row, V.time, V.proj, NC, P, NonZeroTotal{t.c_total, t.c_valid}, T, V.d_n);
 
     int64_t *counts = o->counts;
     int64_t *raw_n = o->raw_n, *n_trend = o->n_trend;
@@ -137,8 +138,14 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     const int32_t *trow = T.row;
     const int64_t *cov_c = t.c_covered, *cov_t = t.c_total;
     int64_t *d_nt = T.d_n;
+    const uint8_t *cval = t.c_valid;
     map_n(c, NC, d_nt, [=] __device__(int64_t j) {
         const int32_t r = trow[j];
+        if ((cval[r] & (FZ_VALID_COVERED | FZ_VALID_TOTAL)) != (FZ_VALID_COVERED | FZ_VALID_TOTAL)) {
+            atomic_add_i64(&counts[FZ_RQ2C_NULL_LINES], 1);  // float(None) raises (:301)
+            tv[j] = NAN;
+            return;
+        }
         tv[j] = double(cov_c[r]) / double(cov_t[r]) * 100.0;
     });
     map_n(c, 1, nullptr, [=] __device__(int64_t) {

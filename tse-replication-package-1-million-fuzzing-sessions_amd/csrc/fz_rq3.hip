@@ -87,6 +87,13 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     const int64_t *btime = t.b_time;
     const int32_t *canon = t.b_rev_canon;
     const int64_t *cvd = t.c_covered, *ctot = t.c_total;
+    const uint8_t *cval = t.c_valid;
+    // `prev_cov[2] > 0 and curr_cov[2] > 0` (rq3:253,297) in Python: a NULL total_line (None) on
+    // the left, or on the right after a positive left, raises TypeError (the query filters only
+    // covered_line IS NOT NULL, :263); NULL totals are stored as 0 with the valid bit clear
+    auto null_cmp = [=] __device__(int32_t ra, int32_t rb) {
+        return !(cval[ra] & FZ_VALID_TOTAL) || (ctot[ra] > 0 && !(cval[rb] & FZ_VALID_TOTAL));
+    };
     map_n(c, NI, nullptr, [=] __device__(int64_t j) {
         dflag[j] = 0;
         if (j >= *d_ni) return;
@@ -110,6 +117,10 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         if (kk >= c1 || fdiv_day(TCv.time[kk]) != target) return;
         const int32_t ra = TCv.row[kk - 1], rb = TCv.row[kk];
         if (cvd[rb] == 0) return;      // break without a pair (:291)
+        if (null_cmp(ra, rb)) {
+            atomic_add_i64(&counts[FZ_RQ3_NULL_TOTAL], 1);
+            return;
+        }
         if (!(ctot[ra] > 0 && ctot[rb] > 0)) return;
         dflag[j] = 1;
         pa[j] = ra;
@@ -157,6 +168,11 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         const int64_t lo = doffs[p], hi = doffs[p + 1];
         const int64_t q = lower_bound_i64(dday, lo, hi, day);
         if (q < hi && dday[q] == day) return;  // a detection day of this project
+        if (null_cmp(ra, rb)) {
+            atomic_add_i64(&counts[FZ_RQ3_NULL_TOTAL], 1);
+            if (p == iproj[*d_ni - 1]) atomic_add_i64(&counts[FZ_RQ3_NULL_LAST], 1);
+            return;
+        }
         if (!(ctot[ra] > 0 && ctot[rb] > 0)) return;
         nflag[k] = 1;
         if (p == iproj[*d_ni - 1]) atomic_add_i64(&counts[FZ_RQ3_NON_LAST], 1);

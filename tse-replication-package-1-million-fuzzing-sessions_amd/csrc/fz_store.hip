@@ -270,6 +270,12 @@ constexpr uint64_t kBlkTop = (uint64_t(1) << (64 - kBlkPosBits)) - 1;  // time f
 // does not fit the key, is flagged for the merge sort instead.  MAXN <= 4096 keeps the keys in LDS;
 // larger classes re-read them from the (prefix-sorted, cache-resident) time column.
 constexpr int kBucketSkew = 32;
+// The sub-bucket pass of long segments (tie != null: equal times ordered by prefix position, any
+// span) ranks inside a bucket by re-reading the bucket's rows from global memory - quadratic in the
+// bucket size - so its cap is looser but still bounded: a sub-bucket whose largest bucket holds more
+// than kTieSkew rows (one timestamp or NULL repeated that often) sends the table's long segments
+// to the merge sort (big_segments_bucketed returns false).
+constexpr int kTieSkew = 256;
 //
 // The three tables share each length class's launch: a workgroup takes combined segment gs and
 // finds its table from the bases (T.tab[k] is read in place from the kernel arguments).
@@ -400,7 +406,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         uint32_t gmax = 0;
 #pragma unroll
         for (int q = 0; q < NW; ++q) gmax = s_max[q] > gmax ? s_max[q] : gmax;
-        if (!tie && gmax > uint32_t(kBucketSkew)) {  // clustered times: the merge sort takes the segment
+        if (gmax > uint32_t(tie ? kTieSkew : kBucketSkew)) {  // clustered times: the merge sort takes it
             if (tid == 0) flag_big(big, bigflag, s, len);
             __syncthreads();
             continue;

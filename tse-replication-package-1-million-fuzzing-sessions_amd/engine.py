@@ -66,7 +66,7 @@ class FzRq1Ext(C.Structure):
 
 
 FZ_RQ2C_NCOUNTS, FZ_RQ2C_NSCALARS = 8, 8
-RQ2C_ELIGIBLE, RQ2C_SESSIONS, RQ2C_GE100, RQ2C_VALUES = range(4)
+RQ2C_ELIGIBLE, RQ2C_SESSIONS, RQ2C_GE100, RQ2C_VALUES, RQ2C_NULL_LINES = range(5)
 RQ2C_CORR_MEAN, RQ2C_CORR_MEDIAN, RQ2C_SP_RHO, RQ2C_SP_P, RQ2C_SW_MEDIAN_P = range(5)
 FZ_RQ2C_SKIP_SESSION_STATS = 1
 
@@ -88,7 +88,7 @@ class FzRq2AddOut(C.Structure):
 
 
 FZ_RQ3_NCOUNTS, FZ_RQ3_NTESTS = 8, 16
-RQ3_ISSUES, RQ3_DETECTED, RQ3_NON_DETECTED, RQ3_ELIGIBLE, RQ3_NON_LAST = range(5)
+RQ3_ISSUES, RQ3_DETECTED, RQ3_NON_DETECTED, RQ3_ELIGIBLE, RQ3_NON_LAST, RQ3_NULL_TOTAL, RQ3_NULL_LAST = range(7)
 FZ_RQ3_FLUSH_LAST, FZ_RQ3_SKIP_STATS = 1, 2
 RQ3_AD_DET, RQ3_AD_NON, RQ3_LEVENE_W, RQ3_LEVENE_P, RQ3_BM_STAT, RQ3_BM_P = 0, 6, 12, 13, 14, 15
 

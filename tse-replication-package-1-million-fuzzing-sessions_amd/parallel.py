@@ -47,7 +47,7 @@ from .schema import Tables
  RQ1_MAX_ITER, RQ1_KEPT_ITERS, RQ1_FIRST_DOWN, RQ1_LATE) = range(15)
 RQ1_NCOUNTS = 16
 # fz.h RQ3 counter layout (FZ_RQ3_*)
-RQ3_ISSUES, RQ3_DETECTED, RQ3_NON_DETECTED, RQ3_ELIGIBLE, RQ3_NON_LAST = range(5)
+RQ3_ISSUES, RQ3_DETECTED, RQ3_NON_DETECTED, RQ3_ELIGIBLE, RQ3_NON_LAST, RQ3_NULL_TOTAL, RQ3_NULL_LAST = range(7)
 RQ3_NCOUNTS = 8
 
 
@@ -310,6 +310,10 @@ def rq3_sharded(shard, rank: int, world: int):
     total[RQ3_DETECTED] = out["det_pct"].numel()
     total[RQ3_NON_DETECTED] = out["non_pct"].numel()
     total[RQ3_NON_LAST] = 0
+    # NULL total_line pairs (rq3:253,297 raise TypeError): those of the never-flushed last project
+    # do not count; the caller raises on the rest (compute.rq3_result)
+    total[RQ3_NULL_TOTAL] -= int(cl[last][RQ3_NULL_LAST]) if last >= 0 else 0
+    total[RQ3_NULL_LAST] = 0
     st = shard.stats(out["det_pct"], out["det_tot"], out["non_pct"])
     return total, out, st
 
@@ -352,12 +356,15 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     m_loc = offs.numel() - 1
     loc_sizes = (offs[1:] - offs[:-1]).to(torch.int64)
     M = agree_max(m_loc, dev) if world > 1 else m_loc
-    sizes = torch.zeros(M, dtype=torch.int64, device=dev)
+    # session sizes, then the NULL-line count (rq2_coverage_count.py:300-303 raise), summed at once
+    sizes = torch.zeros(M + 1, dtype=torch.int64, device=dev)
     sizes[:m_loc] = loc_sizes
+    if part.get("null_lines") is not None:
+        sizes[M:] = part["null_lines"].to(torch.int64).reshape(1)
     if world > 1:
         all_reduce(sizes)
     h = host_many(sizes, offs, *pc)  # one device->host copy
-    sizes_h, offs_h = h[0], h[1]
+    sizes_h, null_lines, offs_h = h[0][:M], int(h[0][M]), h[1]
     proj = dict(zip(RQ2C_PROJECT_COLS, h[2:]))
     own = session_owners(sizes_h, world)
     nv = int(offs_h[-1])
@@ -384,7 +391,7 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     res = {"average": block[:, 0].copy(), "median": block[:, 1].copy(), "percentiles": block[:, 2:].reshape(-1).copy()}
     out = {"proj": proj, "session_offsets": np.concatenate([[0], np.cumsum(sizes_h)]).astype(np.int64), "K": K,
            "average": res["average"], "median": res["median"], "percentiles": res["percentiles"],
-           "tests": tests, "corr_mm": corr_mm}
+           "tests": tests, "corr_mm": corr_mm, "null_lines": null_lines}
     if gather_values:  # coverage_by_session_index.csv: every value, session-major, project order
         if world > 1:
             got = all_gather_cols([vals, sids])
@@ -602,6 +609,7 @@ class GpuRQ2CountShard:
         E._check(eng.lib, eng.lib.fz_rq2_count_ex(eng.ctx, E.FZ_RQ2C_SKIP_SESSION_STATS, C.byref(b.out)))
         ns = int(b.counts[E.RQ2C_SESSIONS].item())
         out = {k: getattr(b, k) for k in RQ2C_PROJECT_COLS}
+        out["null_lines"] = b.counts[E.RQ2C_NULL_LINES:E.RQ2C_NULL_LINES + 1]
         out["session_offsets"] = b.session_offsets[:ns + 1]
         out["session_values"] = b.session_values
         return out

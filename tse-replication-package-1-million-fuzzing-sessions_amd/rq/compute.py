@@ -126,13 +126,17 @@ def rq2_count_collect(eng: E.Engine, b: OutBuffers) -> RQ2CountResult:
         b.host("session_offsets", ns + 1), b.host("session_values", nv), K, b.host("average_trend", K),
         b.host("median_trend", K), b.host("dist_percentiles", 5 * K), b.host("dist_mean", K),
         (float(sc[E.RQ2C_SP_RHO]), float(sc[E.RQ2C_SP_P]), float(sc[E.RQ2C_SW_MEDIAN_P])),
-        (float(sc[E.RQ2C_CORR_MEAN]), float(sc[E.RQ2C_CORR_MEDIAN])))
+        (float(sc[E.RQ2C_CORR_MEAN]), float(sc[E.RQ2C_CORR_MEDIAN])), null_lines=int(cnt[E.RQ2C_NULL_LINES]))
 
 
 def rq2_count_result(proj, session_offsets, session_values, K, average, median, pct_flat, dist_mean, tests,
-                     corr_mm) -> RQ2CountResult:
+                     corr_mm, null_lines: int = 0) -> RQ2CountResult:
     """RQ2CountResult from per-project columns (full project axis), the session-major values and the
-    per-session / median-trend statistics (host copies; also the sharded recombination)."""
+    per-session / median-trend statistics (host copies; also the sharded recombination).  Raises
+    TypeError as the reference does (rq2_coverage_count.py:300-303: ``float(None)``) when a fetched
+    row with a non-zero or NULL total_line has a NULL line count (counts[FZ_RQ2C_NULL_LINES])."""
+    if null_lines:
+        raise TypeError("float() argument must be a string or a real number, not 'NoneType'")
     elig = np.nonzero(np.asarray(proj["eligible"]))[0]
     raw_n = np.asarray(proj["raw_n"])[elig]
     corr = np.asarray(proj["corr"])[elig][raw_n > 0]
@@ -232,7 +236,11 @@ def rq3_collect(eng: E.Engine, b: OutBuffers) -> RQ3Result:
 
 
 def rq3_result(cnt, cols, describe_doubles, tests) -> RQ3Result:
-    """RQ3Result from fz_rq3's counters, columns and statistics (also the sharded recombination)."""
+    """RQ3Result from fz_rq3's counters, columns and statistics (also the sharded recombination).
+    Raises TypeError as the reference does (rq3:253,297: ``None > 0``) when a coverage pair it
+    examines has a NULL total_line (counts[FZ_RQ3_NULL_TOTAL])."""
+    if int(cnt[E.RQ3_NULL_TOTAL]) > int(cnt[E.RQ3_NULL_LAST]):
+        raise TypeError("'>' not supported between instances of 'NoneType' and 'int'")
     nd, nn = len(cols["det_pct"]), len(cols["non_pct"])
     desc = np.asarray(describe_doubles).reshape(3, E.DESCRIBE_DOUBLES)
     ts = np.asarray(tests)
@@ -246,7 +254,8 @@ def rq3_result(cnt, cols, describe_doubles, tests) -> RQ3Result:
         anderson_non=(float(ts[E.RQ3_AD_NON]), ts[E.RQ3_AD_NON + 1:E.RQ3_AD_NON + 6].copy()) if both else None,
         levene=(float(ts[E.RQ3_LEVENE_W]), float(ts[E.RQ3_LEVENE_P])) if both else None,
         brunnermunzel=(float(ts[E.RQ3_BM_STAT]), float(ts[E.RQ3_BM_P])) if both else None,
-        n_non_last=int(cnt[E.RQ3_NON_LAST]))
+        n_non_last=int(cnt[E.RQ3_NON_LAST]), n_null_total=int(cnt[E.RQ3_NULL_TOTAL]),
+        n_null_last=int(cnt[E.RQ3_NULL_LAST]))
 
 
 def rq3(eng: E.Engine) -> RQ3Result:

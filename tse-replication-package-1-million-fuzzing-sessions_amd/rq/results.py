@@ -107,6 +107,8 @@ class RQ3Result:
     levene: Optional[Tuple[float, float]]
     brunnermunzel: Optional[Tuple[float, float]]
     n_non_last: int = 0                # sharded runs: non-detected rows of the last project (tail)
+    n_null_total: int = 0              # shards: pairs meeting a NULL total_line (rq3:253,297 raise)
+    n_null_last: int = 0               # shards: those in the last project's flush (dropped with the tail)
 
 
 @dataclass
