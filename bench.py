@@ -35,8 +35,8 @@ HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PROBE_KERNEL = "radix_scatter"   # headline kernel of the roofline object
 # the per-kernel roofline table (a separate probe window after the timed region; algorithmic bytes
 # per launch as DESIGN.md 4 defines them)
-TABLE_KERNELS = ["radix_scatter", "radix_hist", "elig_hist", "seg_time_sort", "seg_merge_sort", "filter_compact",
-                 "seg_reduce"]
+TABLE_KERNELS = ["radix_scatter", "radix_hist", "elig_hist", "seg_time_sort", "store_gather", "big_scatter",
+                 "big_sub_sort", "seg_merge_sort", "filter_compact", "seg_reduce", "seg_value_sort", "scan_i64"]
 STAGES = ["store", "rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"]
 # analyses run concurrently after the store build: the first groups on child streams, the last on
 # the engine's own stream after the store build (about equal GPU time at config 2: rq3 0.94 ms,
@@ -306,11 +306,15 @@ def main():
             if n == 0 or ms_k <= 0:
                 continue
             ach = b_k / (ms_k * 1e-3) / 1e9
-            table.append({"kernel": k, "launches_per_step": round(n / args.probe_steps, 2),
-                          "avg_launch_us": round(ms_k / n * 1e3, 3), "bytes_per_launch": round(b_k / n),
-                          "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
-                          "ms_per_step": round(ms_k / args.probe_steps, 4),
-                          "traffic": pmc_traffic(k, args.config)})
+            tr = pmc_traffic(k, args.config)
+            row = {"kernel": k, "launches_per_step": round(n / args.probe_steps, 2),
+                   "avg_launch_us": round(ms_k / n * 1e3, 3), "bytes_per_launch": round(b_k / n),
+                   "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                   "ms_per_step": round(ms_k / args.probe_steps, 4), "traffic": tr}
+            if tr:  # PMC bytes per launch over this window's launch time, and over the algorithmic bytes
+                row["traffic_gbs"] = round(tr / (ms_k / n * 1e-3) / 1e9, 1)
+                row["traffic_ratio"] = round(tr / (b_k / n), 3) if b_k > 0 else None
+            table.append(row)
     if world > 1:
         v = torch.tensor([elapsed, rows], dtype=torch.float64, device=dev)
         tmax = v[:1].clone()

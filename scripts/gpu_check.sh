@@ -24,6 +24,8 @@ STEPS=${STEPS:-tests,smoke,bench,prof}
 [[ ",$STEPS," == *,pmcF,* ]] && run pmc_fetch 150 timeout -s KILL 140 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_$TAG -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline
 [[ ",$STEPS," == *,pmcW,* ]] && run pmc_write 150 timeout -s KILL 140 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline
 [[ ",$STEPS," == *,c3,* ]] && run bench_c3 600 python -u bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline
+[[ ",$STEPS," == *,c3cpu,* ]] && run bench_c3_cpu 900 python -u bench.py --config c3 --steps 5 --warmup 2
+[[ ",$STEPS," == *,c5cpu,* ]] && run bench_c5_cpu 900 python -u bench.py --config c5 --steps 5 --warmup 2
 [[ ",$STEPS," == *,c4,* ]] && run bench_c4 300 python -u bench.py --config c4 --steps 5 --warmup 1 --no-cpu-baseline
 [[ ",$STEPS," == *,c5,* ]] && run bench_c5 600 python -u bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline
 [[ ",$STEPS," == *,pc3,* ]] && run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c3_$TAG -o run -- python -u bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline

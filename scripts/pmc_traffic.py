@@ -7,22 +7,40 @@ doubled; WRITE_SIZE is taken as is.
     python scripts/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> \
         <config> <out.json>
 
-One probe scope of bench.py (fz_probe) may cover several dispatches (the store's time sort is
-four length-class launches per table): its traffic is the sum over the matching dispatches divided
-by the number of scopes, counted by a kernel that runs exactly once per scope.  bench.py reads
+The PMC runs are `bench.py --serial` (every launch on one stream, so dispatch order is program
+order).  One probe scope of bench.py (fz_probe) may cover several dispatches; each scope below is
+found in the dispatch sequence: it opens at an `open` kernel (or at its first matching kernel when
+it has none), takes the `match` dispatches that follow, and closes at the first dispatch that
+matches neither `match` nor `allow` (or at `close`).  traffic = bytes of the matched dispatches /
+number of scopes.  A kernel that several scopes launch (k_seg_time_bucket: the store's time sort
+and the long-segment sub-bucket sort) is booked to the scope whose opener precedes it, so no
+dispatch is counted twice and traffic / scope time stays a physical rate.  bench.py reads
 <out.json> (profiles/*_pmc_traffic.json) into roofline.traffic and the per-kernel table."""
 import csv
 import json
 import sys
 
-# probe name -> (kernel-name substring of its dispatches, substring of a once-per-scope kernel)
-KERNELS = {
-    "radix_scatter": ("k_onesweep<", "k_onesweep<"),
-    "radix_hist": ("k_onesweep_hist", "k_onesweep_hist"),
-    "elig_hist": ("k_elig_hist", "k_elig_hist"),
-    "filter_compact": ("k_filter_compact", "k_filter_compact"),
-    "seg_time_sort": ("k_seg_time_bucket", "k_prefix_offsets"),
-    "store_gather": ("k_store_gather", "k_store_gather"),
+SCOPES = {
+    "radix_scatter": {"match": ["k_onesweep<"]},
+    "radix_hist": {"match": ["k_onesweep_hist"]},
+    "elig_hist": {"match": ["k_elig_hist"]},
+    "filter_compact": {"match": ["k_filter_compact"]},
+    # the four length-class launches of the store's time sort (all three tables), between the prefix
+    # offsets and the views launch
+    "seg_time_sort": {"open": "k_prefix_offsets", "match": ["k_seg_time_bucket"], "allow": ["k_fill"],
+                      "close": "k_store_views"},
+    "store_gather": {"match": ["k_store_gather"]},
+    "big_scatter": {"match": ["k_big_scatter"]},
+    # the long class over the sub-buckets, right after the scatter (fills of its counters between)
+    "big_sub_sort": {"open": "k_big_scatter", "match": ["k_seg_time_bucket"], "allow": ["k_fill"]},
+    "seg_reduce": {"open": "k_chunk_reduce", "match": ["k_chunk_reduce", "k_seg_fold", "k_seg_sum"],
+                   "pre": ["k_tiny_reduce"]},
+    "scan_i64": {"match": ["k_scan_lookback"]},
+    # seg_sort_f64's bucket path: value bucket classes, then the merge sort of flagged segments
+    "seg_value_sort": {"open": "k_seg_val_bucket<256, 1024>",
+                       "match": ["k_seg_val_bucket", "k_tile_sort", "k_merge_round", "k_merge_splits",
+                                 "k_tile_count", "k_tile_fill", "k_scan"],
+                       "allow": ["k_fill"]},
 }
 
 
@@ -34,27 +52,54 @@ def dispatches(path):
     return [(v[0][0], sum(x for _, x in v)) for _, v in sorted(out.items())]
 
 
-def per_scope(rows, sub, per):
-    n = sum(1 for k, _ in rows if per in k)
-    tot = sum(b for k, b in rows if sub in k)
-    return (tot / n, n) if n else (None, 0)
+def scopes(rows, spec):
+    """(scopes found, bytes of their dispatches) for one scope spec over the dispatch sequence."""
+    match, allow = spec["match"], spec.get("allow", []) + ["__amd_rocclr"]
+    opener, closer, pre = spec.get("open"), spec.get("close"), spec.get("pre", [])
+    has = lambda k, subs: any(s in k for s in subs)  # noqa: E731
+    n, tot, inside, pend = 0, 0.0, False, 0.0
+    for k, b in rows:
+        if opener is None:  # every matching dispatch is one probed launch
+            if has(k, match):
+                n += 1
+                tot += b
+            continue
+        if opener in k:
+            n += 1
+            inside = True
+            tot += pend + (b if has(k, match) else 0.0)
+            pend = 0.0
+            continue
+        if inside:
+            if closer and closer in k:
+                inside = False
+            elif has(k, match):
+                tot += b
+                continue
+            elif has(k, allow):
+                continue
+            else:
+                inside = False
+        pend = b if has(k, pre) else 0.0
+    return n, tot
 
 
 def main():
     fetch_csv, write_csv, config, out = sys.argv[1:5]
     f, w = dispatches(fetch_csv), dispatches(write_csv)
     res = {"config": config, "kernels": {},
-           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
-                     "bench.py; FETCH_SIZE x2 (gfx950 correction); bytes per probe scope",
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of bench.py --serial; "
+                     "FETCH_SIZE x2 (gfx950 correction); bytes per probe scope, scopes found in dispatch order "
+                     "(scripts/pmc_traffic.py SCOPES)",
            "sources": [fetch_csv, write_csv]}
-    for probe, (sub, per) in KERNELS.items():
-        fb, nf = per_scope(f, sub, per)
-        wb, nw = per_scope(w, sub, per)
-        if fb is None or wb is None or nf != nw:
+    for probe, spec in SCOPES.items():
+        nf, fb = scopes(f, spec)
+        nw, wb = scopes(w, spec)
+        if nf == 0 or nf != nw:
             continue
-        res["kernels"][probe] = {"kernel_match": sub, "scopes": nf, "fetch_bytes_per_launch": 2.0 * fb,
-                                 "fetch_raw_bytes_per_launch": fb, "write_bytes_per_launch": wb,
-                                 "traffic_bytes_per_launch": 2.0 * fb + wb}
+        res["kernels"][probe] = {"scope": spec, "scopes": nf, "fetch_bytes_per_launch": 2.0 * fb / nf,
+                                 "fetch_raw_bytes_per_launch": fb / nf, "write_bytes_per_launch": wb / nw,
+                                 "traffic_bytes_per_launch": (2.0 * fb / nf) + wb / nw}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 

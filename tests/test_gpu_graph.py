@@ -113,3 +113,38 @@ def test_rq3_split_across_streams(engine_for, case):
         eng.join_children()
         torch.cuda.synchronize()
         ch.close()
+
+
+def test_replay_refused_after_rebuild_over_other_tables(engine):
+    """A recording holds raw device pointers into the store and the context's buffers: after the
+    store is rebuilt over a larger table (its columns reallocated) a replay is refused with
+    FZ_E_STATE instead of reading freed memory; recording again works."""
+    from tse_amd import engine as E
+    small, big = goldens.tables("tiny"), goldens.tables("medium")
+    engine.upload(small)
+    engine.build_store()
+    b = compute.rq2_count_buffers(engine)
+    compute.rq2_count_launch(engine, b)  # warm
+    engine.synchronize()
+    g = engine.record(lambda e: compute.rq2_count_launch(e, b))
+    try:
+        g.launch()  # same store: accepted
+        engine.synchronize()
+        engine.upload(big)
+        engine.build_store()
+        with pytest.raises(E.FzError, match="record the graph again"):
+            g.launch()
+    finally:
+        g.close()
+    want = compute.rq2_count(engine)
+    b = compute.rq2_count_buffers(engine)
+    compute.rq2_count_launch(engine, b)
+    engine.synchronize()
+    g = engine.record(lambda e: compute.rq2_count_launch(e, b))
+    try:
+        _clear(b, engine.torch)
+        g.launch()
+        engine.synchronize()
+        assert_same(compute.rq2_count_collect(engine, b), want, "rq2_count (re-recorded)")
+    finally:
+        g.close()

@@ -197,7 +197,10 @@ struct Dict {
     }
     int32_t id_field(std::string_view f) {  // a COPY field (escapes decoded)
         if (f.find('\\') == std::string_view::npos) return id_view(f);
-        owned.push_back(unescape(f));
+        std::string s = unescape(f);  // looked up first: a repeated escaped value keeps no copy
+        auto it = index.find(std::string_view(s));
+        if (it != index.end()) return it->second;
+        owned.push_back(std::move(s));
         return id_view(owned.back());
     }
     int32_t id(const std::string &s) {  // owned key (the merge step)

@@ -274,6 +274,13 @@ struct ProbeScope {
         p.launches[k] += 1;
         on = true;
     }
+    // more algorithmic bytes for this scope's kernel, known only after its launch (host side)
+    static void add_bytes(fz_ctx *ctx, const char *name, double bytes) {
+        Probe &p = ctx->probe;
+        if (!p.active()) return;
+        const int k = p.index(name);
+        if (k >= 0) p.bytes[k] += bytes;
+    }
     ~ProbeScope() {
         if (!on) return;
         Probe &p = c->probe;

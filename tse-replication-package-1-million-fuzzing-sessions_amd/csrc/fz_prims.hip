@@ -280,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_lookback(const int64_t *__restr
     }
 }
 
-void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, int64_t *out_total) {
+static void scan_exclusive_impl(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, int64_t *out_total) {
     if (n <= 0) {
         if (out_total) dev_fill(c, out_total, 0, sizeof(int64_t));
         return;
@@ -293,6 +293,9 @@ void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, i
     if (n > kScan1Max) {
         const int64_t ntiles = (n + kLbTile - 1) / kLbTile;
         const Lookback lb = lookback_begin(c, ntiles);
+        // algorithmic bytes: the int64 input read, the int64 output written (the long scans only:
+        // shorter ones are one- or few-workgroup launches)
+        ProbeScope ps(c, "scan_i64", 16.0 * double(n));
         k_scan_lookback<<<unsigned(ntiles), kBlock, 0, c->stream>>>(in, out, n, ntiles, lb, out_total);
         FZ_LAUNCH_CHECK();
         lookback_end(c, ntiles);
@@ -307,9 +310,13 @@ void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, i
     int64_t *sums = c->arena.get<int64_t>(nb);
     k_scan_reduce<<<unsigned(nb), kBlock, 0, c->stream>>>(in, n, sums);
     FZ_LAUNCH_CHECK();
-    scan_exclusive_i64(c, sums, sums, nb, nullptr);  // recursion depth log_2048(n)
+    scan_exclusive_impl(c, sums, sums, nb, nullptr);  // recursion depth log_2048(n)
     k_scan_chunk<<<unsigned(nb), kBlock, 0, c->stream>>>(in, out, n, sums, out_total);
     FZ_LAUNCH_CHECK();
+}
+
+void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, int64_t *out_total) {
+    scan_exclusive_impl(c, in, out, n, out_total);
 }
 
 // ------------------------------------------------------------------------- LSD radix sort

@@ -577,6 +577,8 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
     // sort (fz_segsort.h), which touches only the flagged segments' rows
     const int64_t S = sg.S, lb = sg.len_bound();
     const int64_t *offs = sg.offs;
+    // algorithmic bytes per live value (offs[S]): value 8 read; value 8 + position 4 written
+    ProbeScope ps(c, "seg_value_sort", 0.0, offs + S, 20.0);
     SegLists L;
     if (S > kManySegs) L = seg_lists(c, sg);
     uint8_t *flag = nullptr;

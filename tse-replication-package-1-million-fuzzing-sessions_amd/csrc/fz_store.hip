@@ -90,13 +90,14 @@ __global__ __launch_bounds__(kBlock) void k_store_prologue(const uint8_t *__rest
 // One workgroup: the four views' per-project offsets (fuzz / coverage builds / coverage / issues)
 // read off the prefix offsets - a view is a contiguous range of one table's prefixes, and the time
 // sorts (merge sort included) keep every row in its prefix's range - their longest segments
-// (out[0..3]) and a copy of the 6 merge-sort counters (out[4..9]): one launch and one D2H copy.
+// (out[0..3]) and a copy of the 9 store counters (out[4..12]: merge-sort rows and longest segment
+// per table, rows the long bucket class gathered per table): one launch and one D2H copy.
 struct ViewSrc {
     const int64_t *src[4] = {};  // prefix offsets of the view's table (null: empty table)
     int64_t first[4] = {};       // prefix of the view's project 0
     int64_t base[4] = {};        // rows of the table before the view
     int64_t *dst[4] = {};        // [P + 1]
-    const unsigned long long *big = nullptr;  // [6] merge-sort rows / longest segment per table
+    const unsigned long long *big = nullptr;  // [9] merge-sort rows / longest segment / fused rows
 };
 __global__ __launch_bounds__(kSortBlock) void k_store_views(const ViewSrc v, int64_t P, int64_t *__restrict__ out) {
     __shared__ int64_t s_m[kSortBlock / kWave];
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(kSortBlock) void k_store_views(const ViewSrc v, int
         }
         __syncthreads();
     }
-    if (threadIdx.x < 6) out[4 + threadIdx.x] = int64_t(v.big[threadIdx.x]);
+    if (threadIdx.x < 9) out[4 + threadIdx.x] = int64_t(v.big[threadIdx.x]);
 }
 
 // ---- prefix LSD passes (moving the columns) + per-segment register sort by (time, row) -------
@@ -295,6 +296,8 @@ struct TimeSortTab {
     const int64_t *oshift = nullptr;
     const uint32_t *sproj = nullptr;
     const uint32_t *tie = nullptr;
+    // rows whose columns the long class gathered itself (the probe's algorithmic bytes), or null
+    unsigned long long *fused = nullptr;
 };
 struct TimeSortTabs {
     TimeSortTab tab[3];
@@ -499,6 +502,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         constexpr bool kPrefetch = IPT <= 8;
         uint64_t xa[IPT], xb[kPrefetch ? IPT : 1];
         load(0, xa);
+        if (tid == 0 && tb.fused) atomicAdd(tb.fused, (unsigned long long)n);
         for (int q = tid; q < n; q += BS) {
             out.oproj[ob + q] = p;
             out.spos[ob + q] = kGathered;
@@ -644,10 +648,11 @@ static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
         tb.rows = ps.rows;
         tb.orow = ps.orow;
         tb.gc = ps.gc;
+        tb.fused = ps.big + 6;  // big3[6 + k]
     }
-    // algorithmic bytes: time 8 read; time 8 + project 4 + source position 4 written (the long
-    // class also moves row id 4 + columns in, perm 4 + row 4 + columns out: counted by the
-    // store_gather probe's bytes for the short classes instead)
+    // algorithmic bytes: time 8 read; time 8 + project 4 + source position 4 written; the long
+    // class also moves row id 4 + columns in, perm 4 + row 4 + columns out for its rows (added by
+    // store_build once their count is read back: fused_gather_bytes)
     ProbeScope probe(c, "seg_time_sort", 24.0 * double(ntot));
     // bucket sorts by length class (each launch skips the others' segments): <= 1024 rows one
     // 256-thread workgroup each (15 KiB of LDS: many per CU), <= 2048 512 threads, <= 4096 1024
@@ -667,7 +672,7 @@ static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
 
 // Gather of every sorted row's columns (after all sorts, merge sort included), all tables in one
 // launch, each table's blocks in proportion to its rows.
-static void gather_tables(fz_ctx *c, const PrefixSorted *pss) {
+static void gather_tables(fz_ctx *c, const PrefixSorted *pss, const int64_t *unfused) {
     GatherTabs G;
     double bytes = 0.0;
     for (int k = 0; k < 3; ++k) {
@@ -676,8 +681,9 @@ static void gather_tables(fz_ctx *c, const PrefixSorted *pss) {
         G.blk[k + 1] = G.blk[k] + g;
         if (ps.n <= 0) continue;
         G.tab[k] = GatherTab{ps.out.spos, ps.rows, ps.n, ps.orow, ps.gc};
-        // algorithmic bytes: spos 4 + row id 4 + columns read; perm 4 + row 4 + columns written
-        bytes += (16.0 + 2.0 * ps.gc.bytes()) * double(ps.n);
+        // algorithmic bytes: spos 4 read per row; for the rows it gathers (unfused: the short
+        // classes' and merge-sorted rows) row id 4 + columns read, perm 4 + row 4 + columns written
+        bytes += 4.0 * double(ps.n) + (12.0 + 2.0 * ps.gc.bytes()) * double(unfused[k]);
     }
     if (G.blk[3] == 0) return;
     ProbeScope probe(c, "store_gather", bytes);
@@ -925,7 +931,9 @@ static bool big_segments_bucketed(fz_ctx *c, const PrefixSorted &ps, int64_t big
     tb.tie = cp.tie;
     T.base[1] = T.base[2] = T.base[3] = nsubs;
     {
-        ProbeScope probe(c, "big_sub_sort", 24.0 * double(ncomp));
+        // time 8 read; time 8 + project 4 + marker 4 written; row id 4 + columns read, perm 4 +
+        // row 4 + columns written (the gather is fused)
+        ProbeScope probe(c, "big_sub_sort", (36.0 + 2.0 * ps.gc.bytes()) * double(ncomp));
         const unsigned g16 = unsigned(nsubs < 256 ? nsubs : 256);
         k_seg_time_bucket<1024, 16384><<<g16, 1024, 0, c->stream>>>(T, 0, true);
         FZ_LAUNCH_CHECK();
@@ -1052,9 +1060,9 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         gi.src[1] = t->i_status, gi.dst[1] = s.si_status.ensure<uint8_t>(ni), gi.size[1] = 1;
     }
     // big3[k]: rows of table k in segments left to the merge sort, big3[3 + k]: the longest such
-    // segment (one zeroing for all six counters)
-    unsigned long long *big3 = c->arena.get<unsigned long long>(6);
-    dev_fill(c, big3, 0, 6 * 8);
+    // segment, big3[6 + k]: rows whose columns the long bucket class gathered (one zeroing for all)
+    unsigned long long *big3 = c->arena.get<unsigned long long>(9);
+    dev_fill(c, big3, 0, 9 * 8);
     PrefixSorted pss[3];
     TableIn tin[3];
     for (int k = 0; k < 3; ++k) {
@@ -1089,27 +1097,39 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         vs.dst[i] = const_cast<int64_t *>(vw[i]->offs);
     }
     vs.big = big3;
-    int64_t *mx = c->arena.get<int64_t>(10);
+    int64_t *mx = c->arena.get<int64_t>(13);
     k_store_views<<<1, kSortBlock, 0, c->stream>>>(vs, P, mx);
     FZ_LAUNCH_CHECK();
-    FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 10 * 8, hipMemcpyDeviceToHost, c->stream));
+    FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 13 * 8, hipMemcpyDeviceToHost, c->stream));
     sync(c);
     // segments the bucket sorts left (longer than 16384 rows, clustered, or a time span too wide
     // for their packed key): segmented merge sort of those rows only, writing the same outputs
     const int64_t maxseg[4] = {c->h_pinned[0], c->h_pinned[1], c->h_pinned[2], c->h_pinned[3]};
     const int64_t bigrows[3] = {c->h_pinned[4], c->h_pinned[5], c->h_pinned[6]};
     const int64_t bigmax[3] = {c->h_pinned[7], c->h_pinned[8], c->h_pinned[9]};
+    const int64_t fused[3] = {c->h_pinned[10], c->h_pinned[11], c->h_pinned[12]};
+    // the probes' algorithmic bytes of the gathers: the long bucket class's fused gather, then the
+    // rows left to k_store_gather (short classes and merge-sorted rows)
+    int64_t unfused[3];
+    for (int k = 0; k < 3; ++k) {
+        const double per = 12.0 + 2.0 * pss[k].gc.bytes();  // row 4 + columns in; perm 4 + row 4 + columns out
+        ProbeScope::add_bytes(c, "seg_time_sort", per * double(fused[k]));
+        unfused[k] = pss[k].n - fused[k];
+    }
     for (int k = 0; k < 3; ++k) {
         if (bigrows[k] == 0) continue;
         const PrefixSorted &ps = pss[k];
-        if (big_segments_bucketed(c, ps, bigrows[k])) continue;
+        if (big_segments_bucketed(c, ps, bigrows[k])) {
+            unfused[k] -= bigrows[k];  // the sub-bucket sort gathered them (big_sub_sort)
+            continue;
+        }
         ProbeScope probe(c, "seg_merge_sort", 36.0 * double(bigrows[k]));
         sort_big_segments(c, ps.offs, ps.S, ps.n, bigmax[k], ps.bigflag, StoreTimeKey{ps.time},
                           StoreSink{ps.pmask, ps.out});
     }
     // the long-segment bucket sort gathered its segments' columns; the short classes' and the
     // merge-sorted rows are gathered here (rows marked kGathered are skipped)
-    gather_tables(c, pss);
+    gather_tables(c, pss, unfused);
     materialize_sorted(c);
     s.fuzz.max_seg = maxseg[0];
     s.covb.max_seg = maxseg[1];
