@@ -254,6 +254,7 @@ struct ProbeScope {
     int owner = -1;
     const int64_t *d_count = nullptr;
     double per_count = 0.0;
+    size_t pair = 0;  // index of this scope's (start, stop) events in the pool
     ProbeScope(fz_ctx *ctx, const char *name, double bytes, const int64_t *count = nullptr, double per = 0.0)
         : c(ctx), on(false), d_count(count), per_count(per) {
         Probe &p = c->probe;
@@ -268,7 +269,11 @@ struct ProbeScope {
                 p.pool.push_back(e);
             }
         }
-        FZ_HIP(hipEventRecord(p.pool[p.used], c->stream));
+        // the scope's event pair is reserved now, so a scope opened inside this one (a scan inside
+        // a merge sort) takes the next pair instead of this one's stop event
+        pair = p.used;
+        p.used += 2;
+        FZ_HIP(hipEventRecord(p.pool[pair], c->stream));
         p.owner.push_back(k);
         p.bytes[k] += bytes;
         p.launches[k] += 1;
@@ -284,8 +289,7 @@ struct ProbeScope {
     ~ProbeScope() {
         if (!on) return;
         Probe &p = c->probe;
-        (void)hipEventRecord(p.pool[p.used + 1], c->stream);
-        p.used += 2;
+        (void)hipEventRecord(p.pool[pair + 1], c->stream);
         if (d_count && int64_t(p.deferred.size()) < Probe::kMaxCounts) {
             const int64_t slot = int64_t(p.deferred.size());
             (void)hipMemcpyAsync(p.counts.as<int64_t>() + slot, d_count, 8, hipMemcpyDeviceToDevice, c->stream);

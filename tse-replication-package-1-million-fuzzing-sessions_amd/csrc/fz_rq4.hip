@@ -309,7 +309,10 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
     const int64_t *d_nf = d_n;
     int64_t *offs2 = c->arena.get<int64_t>(S2 + 1);  // segment 2i: session i's G2 values, 2i + 1: G1
     segment_offsets_dn(c, sid2, d_nf, NC, S2, offs2);
-    const bool small = P <= kBmHalvesMax;  // Brunner-Munzel from the sorted halves (else rank passes)
+    // Brunner-Munzel from the sorted halves: per-thread merge walks for short halves, both halves in
+    // LDS for sessions of up to kBmLdsMax values, else the device-wide rank passes
+    const bool lds = P > kBmHalvesMax && sess_len <= kBmLdsMax;
+    const bool small = P <= kBmHalvesMax || lds;
     int32_t *sess = small ? nullptr : c->arena.get<int32_t>(NC);
     uint8_t *grp2 = small ? nullptr : c->arena.get<uint8_t>(NC);
     int64_t *soffs = small ? nullptr : c->arena.get<int64_t>(MM + 1);
@@ -336,6 +339,10 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
         g1q[k] = qq[(2 * i + 1) * 3 + j];
     });
     // per-session Brunner-Munzel (:978-985; NaN unless both sides >= 5)
+    if (lds) {
+        bm_halves_lds(c, ss2.val, offs2, MM, 5, pbm);
+        return;
+    }
     if (small) {
         bm_sorted_halves(c, ss2.val, offs2, MM, 5, pbm);
         return;

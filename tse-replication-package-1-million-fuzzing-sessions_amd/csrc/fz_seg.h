@@ -350,6 +350,9 @@ void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, 
 // y = sorted[offs2[2i+1], offs2[2i+2]); NaN unless both hold >= min_n values.
 void bm_sorted_halves(fz_ctx *c, const double *sorted, const int64_t *offs2, int64_t M, int64_t min_n, double *pbm);
 constexpr int64_t kBmHalvesMax = 2048;  // bm_sorted_halves is for halves of at most this many values
+// the same for sessions of up to kBmLdsMax values (both halves together), staged in LDS
+void bm_halves_lds(fz_ctx *c, const double *sorted, const int64_t *offs2, int64_t M, int64_t min_n, double *pbm);
+constexpr int kBmLdsMax = 12288;
 
 // spearmanr(range(n), x) per segment from the sorted segments: one workgroup per segment when they
 // are short (no tie-rank passes), else seg_tie_ranks + seg_spearman_index.

@@ -883,6 +883,124 @@ void bm_sorted_halves(fz_ctx *c, const double *sorted, const int64_t *offs2, int
     FZ_LAUNCH_CHECK();
 }
 
+// Sum over the NW waves of a workgroup (s_tmp: NW slots).
+template <int NW>
+__device__ inline double block_sum_nw(double x, double *s_tmp) {
+    x = wave_sum(x);
+    if (lane_id() == 0) s_tmp[wave_id()] = x;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += s_tmp[w];
+    __syncthreads();
+    return t;
+}
+
+// Brunner-Munzel of sessions whose sorted halves hold up to kBmLdsMax values together (config 3:
+// ~10^4 values per session, too long for the per-thread merge walks of k_bm_sorted_halves): one
+// 1024-thread workgroup per session stages both halves in LDS (one coalesced read), then every
+// value finds its tie range in its own half and in the other by four binary searches in LDS -
+// independent per value, so a thread's dozen values overlap their searches instead of walking a
+// dependent chain - giving its union rank rc and within-sample rank rw at once; the two sums of
+// scipy's brunnermunzel follow from rc - rw kept in registers.  Replaces the union sort + device-
+// wide tie-rank passes + three segmented reductions of seg_rank_tests for these sessions.
+constexpr int kBmLdsBlock = 1024;
+__global__ __launch_bounds__(kBmLdsBlock) void k_bm_halves_lds(const double *__restrict__ sv,
+                                                              const int64_t *__restrict__ offs2, int64_t M,
+                                                              int64_t min_n, double *__restrict__ pbm) {
+    constexpr int NW = kBmLdsBlock / kWave;
+    constexpr int IPT = kBmLdsMax / kBmLdsBlock;
+    __shared__ double s_v[kBmLdsMax];
+    __shared__ double s_tmp[NW];
+    const int tid = threadIdx.x;
+    for (int64_t i = blockIdx.x; i < M; i += gridDim.x) {
+        const int64_t x0 = offs2[2 * i], x1 = offs2[2 * i + 1], y1 = offs2[2 * i + 2];
+        const int nx = int(x1 - x0), ny = int(y1 - x1), n = nx + ny;
+        if (nx < min_n || ny < min_n) {
+            if (tid == 0) pbm[i] = NAN;
+            continue;
+        }
+        for (int j = tid; j < n; j += kBmLdsBlock) s_v[j] = sv[x0 + j];
+        __syncthreads();
+        const double *X = s_v, *Y = s_v + nx;
+        double d[IPT];
+        double ax = 0.0, ay = 0.0;
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int j = tid + m * kBmLdsBlock;
+            d[m] = 0.0;
+            if (j >= n) continue;
+            const bool inx = j < nx;
+            const double *own = inx ? X : Y, *oth = inx ? Y : X;
+            const int no = inx ? nx : ny, nt = inx ? ny : nx, k = inx ? j : j - nx;
+            const double v = own[k];
+            int la = 0, hi = k;  // first index of v in own (own[k] == v)
+            while (la < hi) {
+                const int md = (la + hi) >> 1;
+                if (own[md] < v) la = md + 1;
+                else hi = md;
+            }
+            int ua = k + 1;  // one past the last index of v in own
+            hi = no;
+            while (ua < hi) {
+                const int md = (ua + hi) >> 1;
+                if (own[md] <= v) ua = md + 1;
+                else hi = md;
+            }
+            int lb = 0;
+            hi = nt;
+            while (lb < hi) {
+                const int md = (lb + hi) >> 1;
+                if (oth[md] < v) lb = md + 1;
+                else hi = md;
+            }
+            int ub = lb;
+            hi = nt;
+            while (ub < hi) {
+                const int md = (ub + hi) >> 1;
+                if (oth[md] <= v) ub = md + 1;
+                else hi = md;
+            }
+            const double rc = double(la + lb) + double((ua - la) + (ub - lb) + 1) / 2.0;
+            const double rw = double(la) + double(ua - la + 1) / 2.0;
+            d[m] = rc - rw;
+            if (inx) ax += rc;
+            else ay += rc;
+        }
+        const double Nx = double(nx), Ny = double(ny);
+        const double rcx = block_sum_nw<NW>(ax, s_tmp) / Nx, rcy = block_sum_nw<NW>(ay, s_tmp) / Ny;
+        const double wmx = (Nx + 1.0) / 2.0, wmy = (Ny + 1.0) / 2.0;  // mean within-sample rank
+        double bx = 0.0, by = 0.0;
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int j = tid + m * kBmLdsBlock;
+            if (j >= n) continue;
+            if (j < nx) {
+                const double e = (d[m] - rcx) + wmx;
+                bx += e * e;
+            } else {
+                const double e = (d[m] - rcy) + wmy;
+                by += e * e;
+            }
+        }
+        const double Sx = block_sum_nw<NW>(bx, s_tmp) / (Nx - 1.0), Sy = block_sum_nw<NW>(by, s_tmp) / (Ny - 1.0);
+        if (tid == 0) {
+            double w = Nx * Ny * (rcy - rcx);
+            w /= (Nx + Ny) * sqrt(Nx * Sx + Ny * Sy);
+            const double num = (Nx * Sx + Ny * Sy) * (Nx * Sx + Ny * Sy);
+            const double den = (Nx * Sx) * (Nx * Sx) / (Nx - 1.0) + (Ny * Sy) * (Ny * Sy) / (Ny - 1.0);
+            pbm[i] = 2.0 * stats::t_sf(fabs(w), num / den);
+        }
+        // (block_sum_nw's trailing barrier: every read of s_v is done before the next session's loads)
+    }
+}
+
+void bm_halves_lds(fz_ctx *c, const double *sorted, const int64_t *offs2, int64_t M, int64_t min_n, double *pbm) {
+    if (M <= 0) return;
+    k_bm_halves_lds<<<unsigned(M < 4096 ? M : 4096), kBmLdsBlock, 0, c->stream>>>(sorted, offs2, M, min_n, pbm);
+    FZ_LAUNCH_CHECK();
+}
+
 // --------------------------------------------------------------------- Spearman vs index
 void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, const TieRanks &tr, double *rho,
                         double *pval) {
