@@ -147,6 +147,7 @@ int fz_ctx_destroy(fz_ctx *ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     if (ctx->capture_stream) (void)hipStreamDestroy(ctx->capture_stream);
+    if (ctx->ev_readback) (void)hipEventDestroy(ctx->ev_readback);
     delete ctx;
     return FZ_OK;
 }

@@ -239,6 +239,9 @@ struct fz_ctx {
     bool capturing = false;
     hipStream_t capture_stream = nullptr;
     hipStream_t capture_saved = nullptr;
+    // the store build's counter read-back (fz_store.hip): the host waits for this event, not for
+    // the stream, so the gather launched after the copies overlaps the round trip
+    hipEvent_t ev_readback = nullptr;
 };
 
 namespace fz {

@@ -315,14 +315,14 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
     const bool small = P <= kBmHalvesMax || lds;
     int32_t *sess = small ? nullptr : c->arena.get<int32_t>(NC);
     uint8_t *grp2 = small ? nullptr : c->arena.get<uint8_t>(NC);
-    int64_t *soffs = small ? nullptr : c->arena.get<int64_t>(MM + 1);
-    map_n(c, small ? MM : (NC > MM + 1 ? NC : MM + 1), nullptr, [=] __device__(int64_t k) {
+    int64_t *soffs = small && !lds ? nullptr : c->arena.get<int64_t>(MM + 1);
+    map_n(c, small ? MM + 1 : (NC > MM + 1 ? NC : MM + 1), nullptr, [=] __device__(int64_t k) {
         if (k < MM) {
             c2[k] = offs2[2 * k + 1] - offs2[2 * k];
             c1[k] = offs2[2 * k + 2] - offs2[2 * k + 1];
         }
+        if (soffs && k <= MM) soffs[k] = offs2[2 * k];
         if (small) return;
-        if (k <= MM) soffs[k] = offs2[2 * k];
         if (k < NC) {
             sess[k] = int32_t(sid2[k] >> 1);
             grp2[k] = uint8_t(sid2[k] & 1u);
@@ -340,7 +340,7 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
     });
     // per-session Brunner-Munzel (:978-985; NaN unless both sides >= 5)
     if (lds) {
-        bm_halves_lds(c, ss2.val, offs2, MM, 5, pbm);
+        bm_halves(c, ss2.val, offs2, soffs, MM, NC, 5, pbm);
         return;
     }
     if (small) {

@@ -227,6 +227,9 @@ struct ChunkedSegs {
 };
 ChunkedSegs chunked(fz_ctx *c, const Segs &sg);
 
+template <int NV>
+void seg_fold_parts(fz_ctx *c, const ChunkedSegs &cs, const double *part, double *out);
+
 // Segmented sum of NV per-element values f(i, seg, x[NV]) -> out[S][NV] (device).
 template <int NV, typename F>
 void seg_reduce(fz_ctx *c, const ChunkedSegs &cs, F f, double *out) {
@@ -249,6 +252,15 @@ void seg_reduce(fz_ctx *c, const ChunkedSegs &cs, F f, double *out) {
     const unsigned g = unsigned(L.on ? (blocks < 8192 ? blocks : 8192) : blocks);
     k_chunk_reduce<NV, F><<<g, kBlock, 0, c->stream>>>(cs.cm, cs.sg.offs, cs.cps, blocks, f, part, nullptr);
     FZ_LAUNCH_CHECK();
+    seg_fold_parts<NV>(c, cs, part, out);
+}
+
+// The fold of a chunked reduction: per-chunk double-double partials part[(k * NV + v) * 2 + {0, 1}]
+// (chunk k of cs's map) -> out[s * NV + v], chunks in order.
+template <int NV>
+void seg_fold_parts(fz_ctx *c, const ChunkedSegs &cs, const double *part, double *out) {
+    const int64_t S = cs.sg.S;
+    const SegLists &L = cs.lists;
     const int64_t nsum = L.on ? L.cap[kClassNonTiny] : S;
     const int32_t *lst = L.on ? L.ids[kClassNonTiny] : nullptr;
     const int64_t *dln = L.on ? L.d_n + kClassNonTiny : nullptr;
@@ -351,7 +363,9 @@ void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, 
 void bm_sorted_halves(fz_ctx *c, const double *sorted, const int64_t *offs2, int64_t M, int64_t min_n, double *pbm);
 constexpr int64_t kBmHalvesMax = 2048;  // bm_sorted_halves is for halves of at most this many values
 // the same for sessions of up to kBmLdsMax values (both halves together), staged in LDS
-void bm_halves_lds(fz_ctx *c, const double *sorted, const int64_t *offs2, int64_t M, int64_t min_n, double *pbm);
+// (soffs[M + 1]: session offsets, soffs[k] = offs2[2k]; n_cap: values of all sessions)
+void bm_halves(fz_ctx *c, const double *sorted, const int64_t *offs2, const int64_t *soffs, int64_t M, int64_t n_cap,
+               int64_t min_n, double *pbm);
 constexpr int kBmLdsMax = 12288;
 
 // spearmanr(range(n), x) per segment from the sorted segments: one workgroup per segment when they

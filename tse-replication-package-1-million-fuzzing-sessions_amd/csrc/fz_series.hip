@@ -896,38 +896,51 @@ __device__ inline double block_sum_nw(double x, double *s_tmp) {
     return t;
 }
 
-// Brunner-Munzel of sessions whose sorted halves hold up to kBmLdsMax values together (config 3:
-// ~10^4 values per session, too long for the per-thread merge walks of k_bm_sorted_halves): one
-// 1024-thread workgroup per session stages both halves in LDS (one coalesced read), then every
-// value finds its tie range in its own half and in the other by four binary searches in LDS -
-// independent per value, so a thread's dozen values overlap their searches instead of walking a
-// dependent chain - giving its union rank rc and within-sample rank rw at once; the two sums of
-// scipy's brunnermunzel follow from rc - rw kept in registers.  Replaces the union sort + device-
-// wide tie-rank passes + three segmented reductions of seg_rank_tests for these sessions.
-constexpr int kBmLdsBlock = 1024;
-__global__ __launch_bounds__(kBmLdsBlock) void k_bm_halves_lds(const double *__restrict__ sv,
-                                                              const int64_t *__restrict__ offs2, int64_t M,
-                                                              int64_t min_n, double *__restrict__ pbm) {
-    constexpr int NW = kBmLdsBlock / kWave;
-    constexpr int IPT = kBmLdsMax / kBmLdsBlock;
-    __shared__ double s_v[kBmLdsMax];
+// The Brunner-Munzel p of one session from its union ranks rc and within-sample ranks rw:
+// d = rc - rw per value, sums as scipy's brunnermunzel forms them (t distribution, two-sided).
+__device__ inline double bm_pvalue(double Nx, double Ny, double rcx, double rcy, double Sx, double Sy) {
+    double w = Nx * Ny * (rcy - rcx);
+    w /= (Nx + Ny) * sqrt(Nx * Sx + Ny * Sy);
+    const double num = (Nx * Sx + Ny * Sy) * (Nx * Sx + Ny * Sy);
+    const double den = (Nx * Sx) * (Nx * Sx) / (Nx - 1.0) + (Ny * Sy) * (Ny * Sy) / (Ny - 1.0);
+    return 2.0 * stats::t_sf(fabs(w), num / den);
+}
+
+// Brunner-Munzel of sessions whose sorted halves hold up to MAXN values together (config 3: ~10^4
+// values per session, too long for the per-thread merge walks of k_bm_sorted_halves): one
+// workgroup per session stages both halves in LDS (one coalesced read), then every value finds its
+// tie range in its own half and in the other by four binary searches in LDS - independent per
+// value, so a thread's values overlap their searches instead of walking a dependent chain - giving
+// its union rank rc and within-sample rank rw at once; the two sums of scipy's brunnermunzel follow
+// from rc - rw kept in registers.  Sessions come from a size-class list (or all M, list null).
+template <int BS, int MAXN>
+__global__ __launch_bounds__(BS) void k_bm_halves_lds(const double *__restrict__ sv, const int64_t *__restrict__ offs2,
+                                                     int64_t M, const int32_t *__restrict__ list,
+                                                     const int64_t *__restrict__ d_ln, int64_t min_n,
+                                                     double *__restrict__ pbm) {
+    constexpr int NW = BS / kWave;
+    constexpr int IPT = MAXN / BS;
+    static_assert(MAXN % BS == 0, "shape");
+    __shared__ double s_v[MAXN];
     __shared__ double s_tmp[NW];
     const int tid = threadIdx.x;
-    for (int64_t i = blockIdx.x; i < M; i += gridDim.x) {
+    const int64_t ns = list ? *d_ln : M;
+    for (int64_t it = blockIdx.x; it < ns; it += gridDim.x) {
+        const int64_t i = list ? list[it] : it;
         const int64_t x0 = offs2[2 * i], x1 = offs2[2 * i + 1], y1 = offs2[2 * i + 2];
         const int nx = int(x1 - x0), ny = int(y1 - x1), n = nx + ny;
-        if (nx < min_n || ny < min_n) {
+        if (nx < min_n || ny < min_n || n > MAXN) {
             if (tid == 0) pbm[i] = NAN;
             continue;
         }
-        for (int j = tid; j < n; j += kBmLdsBlock) s_v[j] = sv[x0 + j];
+        for (int j = tid; j < n; j += BS) s_v[j] = sv[x0 + j];
         __syncthreads();
         const double *X = s_v, *Y = s_v + nx;
         double d[IPT];
         double ax = 0.0, ay = 0.0;
 #pragma unroll
         for (int m = 0; m < IPT; ++m) {
-            const int j = tid + m * kBmLdsBlock;
+            const int j = tid + m * BS;
             d[m] = 0.0;
             if (j >= n) continue;
             const bool inx = j < nx;
@@ -973,7 +986,7 @@ __global__ __launch_bounds__(kBmLdsBlock) void k_bm_halves_lds(const double *__r
         double bx = 0.0, by = 0.0;
 #pragma unroll
         for (int m = 0; m < IPT; ++m) {
-            const int j = tid + m * kBmLdsBlock;
+            const int j = tid + m * BS;
             if (j >= n) continue;
             if (j < nx) {
                 const double e = (d[m] - rcx) + wmx;
@@ -984,20 +997,77 @@ __global__ __launch_bounds__(kBmLdsBlock) void k_bm_halves_lds(const double *__r
             }
         }
         const double Sx = block_sum_nw<NW>(bx, s_tmp) / (Nx - 1.0), Sy = block_sum_nw<NW>(by, s_tmp) / (Ny - 1.0);
-        if (tid == 0) {
-            double w = Nx * Ny * (rcy - rcx);
-            w /= (Nx + Ny) * sqrt(Nx * Sx + Ny * Sy);
-            const double num = (Nx * Sx + Ny * Sy) * (Nx * Sx + Ny * Sy);
-            const double den = (Nx * Sx) * (Nx * Sx) / (Nx - 1.0) + (Ny * Sy) * (Ny * Sy) / (Ny - 1.0);
-            pbm[i] = 2.0 * stats::t_sf(fabs(w), num / den);
-        }
+        if (tid == 0) pbm[i] = bm_pvalue(Nx, Ny, rcx, rcy, Sx, Sy);
         // (block_sum_nw's trailing barrier: every read of s_v is done before the next session's loads)
     }
 }
 
-void bm_halves_lds(fz_ctx *c, const double *sorted, const int64_t *offs2, int64_t M, int64_t min_n, double *pbm) {
+// The same for sessions of at most 64 values (a size-class list): one wave each, a value per lane;
+// its tie ranges are counted against the other lanes' values (64 shuffles, no memory traffic).
+__global__ __launch_bounds__(kBlock) void k_bm_wave(const double *__restrict__ sv, const int64_t *__restrict__ offs2,
+                                                    const int32_t *__restrict__ list, const int64_t *__restrict__ d_ln,
+                                                    int64_t min_n, double *__restrict__ pbm) {
+    const int64_t ns = *d_ln;
+    const int lane = lane_id();
+    for (int64_t it = int64_t(blockIdx.x) * 4 + wave_id(); it < ns; it += int64_t(gridDim.x) * 4) {
+        const int64_t i = list[it];
+        const int64_t x0 = offs2[2 * i], x1 = offs2[2 * i + 1], y1 = offs2[2 * i + 2];
+        const int nx = int(x1 - x0), ny = int(y1 - x1), n = nx + ny;
+        if (nx < min_n || ny < min_n || n > kWave) {
+            if (lane == 0) pbm[i] = NAN;
+            continue;
+        }
+        const bool valid = lane < n, inx = lane < nx;
+        const double v = valid ? sv[x0 + lane] : 0.0;
+        int la = 0, ua = 0, lb = 0, ub = 0;
+        for (int t = 0; t < n; ++t) {
+            const double u = __shfl(v, t, kWave);
+            const bool same = (t < nx) == inx;
+            const int lt = u < v, le = u <= v;
+            la += same ? lt : 0;
+            ua += same ? le : 0;
+            lb += same ? 0 : lt;
+            ub += same ? 0 : le;
+        }
+        const double rc = double(la + lb) + double((ua - la) + (ub - lb) + 1) / 2.0;
+        const double rw = double(la) + double(ua - la + 1) / 2.0;
+        const double d = rc - rw;
+        const double Nx = double(nx), Ny = double(ny);
+        const double rcx = wave_sum(valid && inx ? rc : 0.0) / Nx, rcy = wave_sum(valid && !inx ? rc : 0.0) / Ny;
+        const double e = inx ? (d - rcx) + (Nx + 1.0) / 2.0 : (d - rcy) + (Ny + 1.0) / 2.0;
+        const double Sx = wave_sum(valid && inx ? e * e : 0.0) / (Nx - 1.0);
+        const double Sy = wave_sum(valid && !inx ? e * e : 0.0) / (Ny - 1.0);
+        if (lane == 0) pbm[i] = bm_pvalue(Nx, Ny, rcx, rcy, Sx, Sy);
+    }
+}
+
+// Brunner-Munzel p of M sessions from their sorted halves (offs2 as bm_sorted_halves; soffs[M + 1]:
+// session offsets, soffs[k] = offs2[2k]; n_cap: values in all sessions; every session holds at
+// most kBmLdsMax values).  Few sessions (configs 2 / 3): one workgroup each over all of them.  Very
+// many (config 5's Zipf tail: one session per index of the longest project, ~10^7, nearly all
+// holding a handful of values): size-class lists - sessions of <= 8 values are never tested (both
+// halves need min_n >= 5), <= 64 one wave each, <= 4096 a 256-thread workgroup, longer 1024 threads.
+void bm_halves(fz_ctx *c, const double *sorted, const int64_t *offs2, const int64_t *soffs, int64_t M, int64_t n_cap,
+               int64_t min_n, double *pbm) {
     if (M <= 0) return;
-    k_bm_halves_lds<<<unsigned(M < 4096 ? M : 4096), kBmLdsBlock, 0, c->stream>>>(sorted, offs2, M, min_n, pbm);
+    if (M <= kManySegs) {
+        k_bm_halves_lds<1024, kBmLdsMax><<<unsigned(M < 4096 ? M : 4096), 1024, 0, c->stream>>>(
+            sorted, offs2, M, nullptr, nullptr, min_n, pbm);
+        FZ_LAUNCH_CHECK();
+        return;
+    }
+    static_assert(kMicroSeg < 10, "sessions of <= kMicroSeg values have a half below min_n = 5");
+    map_n(c, M, nullptr, [=] __device__(int64_t i) { pbm[i] = NAN; });
+    const SegLists L = seg_lists(c, Segs{M, soffs, n_cap});
+    auto grid = [](int64_t cap, int64_t lim) { return unsigned(cap < 1 ? 1 : (cap < lim ? cap : lim)); };
+    k_bm_wave<<<grid((L.cap[kClassTiny] + 3) / 4, 8192), kBlock, 0, c->stream>>>(
+        sorted, offs2, L.ids[kClassTiny], L.d_n + kClassTiny, min_n, pbm);
+    k_bm_halves_lds<256, 4096><<<grid(L.cap[kClassMid], 8192), 256, 0, c->stream>>>(
+        sorted, offs2, M, L.ids[kClassMid], L.d_n + kClassMid, min_n, pbm);
+    k_bm_halves_lds<256, 4096><<<grid(L.cap[kClassWide], 4096), 256, 0, c->stream>>>(
+        sorted, offs2, M, L.ids[kClassWide], L.d_n + kClassWide, min_n, pbm);
+    k_bm_halves_lds<1024, kBmLdsMax><<<grid(L.cap[kClassBig], 2048), 1024, 0, c->stream>>>(
+        sorted, offs2, M, L.ids[kClassBig], L.d_n + kClassBig, min_n, pbm);
     FZ_LAUNCH_CHECK();
 }
 
@@ -1098,6 +1168,140 @@ __global__ __launch_bounds__(kBlock) void k_spearman_index_small(const double *_
     }
 }
 
+// spearmanr(range(n), x) sums of long sorted segments, chunk by chunk (the chunked-reduction map,
+// kChunk values per workgroup): the chunk's values and positions are staged in LDS (coalesced),
+// each thread takes kRedItems consecutive ones, and a value's tie group [gs, ge) comes from the
+// tie-start flags - inside the thread, else from a block max-scan of the preceding threads' last
+// start / a reverse min-scan of the following threads' first start, else (a group crossing the
+// chunk's edge) from one binary search at each edge.  Every value's rank is then known in its
+// chunk alone: the double-double partials (sum rx*ry, rx^2, ry^2, tie groups) of each chunk go to
+// the segmented fold.  One launch instead of the device-wide tie-rank passes (flag, scan, group
+// starts, ranks, group count) and the reduction over their arrays.
+constexpr int kSpNV = 4;
+__global__ __launch_bounds__(kBlock) void k_spearman_chunks(ChunkMap cm, const int64_t *__restrict__ offs, int64_t cps,
+                                                            int64_t nk_host, const double *__restrict__ sv,
+                                                            const int32_t *__restrict__ pos, double *__restrict__ part) {
+    constexpr int IPT = kRedItems;
+    __shared__ double s_v[kChunk];
+    __shared__ int32_t s_p[kChunk];
+    __shared__ int64_t s_w[2][4];
+    __shared__ int64_t s_edge[2];
+    __shared__ double s_hi[4][kSpNV], s_lo[4][kSpNV];
+    const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+    const int64_t nk = cm.d_n ? *cm.d_n : nk_host;
+    for (int64_t k = blockIdx.x; k < nk; k += gridDim.x) {
+        int32_t seg;
+        int64_t b, e;
+        if (cm.d_n) {
+            seg = cm.seg[k];
+            b = cm.begin[k];
+            e = cm.end[k];
+        } else {
+            seg = int32_t(k / cps);
+            b = offs[seg] + (k % cps) * kChunk;
+            e = b + kChunk < offs[seg + 1] ? b + kChunk : offs[seg + 1];
+        }
+        const int64_t sb = offs[seg], se = offs[seg + 1];
+        const int len = e > b ? int(e - b) : 0;
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int j = tid + m * kBlock;
+            if (j < len) {
+                s_v[j] = sv[b + j];
+                s_p[j] = pos[b + j];
+            }
+        }
+        // the tie groups crossing the chunk's edges (two lanes of different waves search at once)
+        if (tid == 0) {
+            int64_t gs = b;
+            if (len > 0 && b > sb && sv[b - 1] == sv[b]) gs = lower_bound_d(sv, sb, b, sv[b]);
+            s_edge[0] = gs;
+        } else if (tid == kWave) {
+            int64_t ge = e;
+            if (len > 0 && e < se && sv[e] == sv[e - 1]) ge = upper_bound_d(sv, e, se, sv[e - 1]);
+            s_edge[1] = ge;
+        }
+        __syncthreads();
+        const int64_t head = s_edge[0], tail = s_edge[1];
+        // this thread's run q0 .. q0 + IPT - 1: tie-start flags, first / last start in the run
+        const int q0 = tid * IPT;
+        bool f[IPT];
+        int64_t first = INT64_MAX, last = -1;
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int q = q0 + m;
+            f[m] = q < len && (q == 0 ? head == b : s_v[q] != s_v[q - 1]);
+            if (f[m]) {
+                first = first < b + q ? first : b + q;
+                last = b + q;
+            }
+        }
+        // exclusive max-scan of `last` over the preceding threads, reverse min-scan of `first` over
+        // the following ones (wave shuffles, then the four waves' totals)
+        int64_t incl_max = last, incl_min = first;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const int64_t a = __shfl_up(incl_max, off, kWave);
+            const int64_t d = __shfl_down(incl_min, off, kWave);
+            if (lane >= off) incl_max = a > incl_max ? a : incl_max;
+            if (lane + off < kWave) incl_min = d < incl_min ? d : incl_min;
+        }
+        if (lane == kWave - 1) s_w[0][w] = incl_max;
+        if (lane == 0) s_w[1][w] = incl_min;
+        int64_t before = __shfl_up(incl_max, 1, kWave), after = __shfl_down(incl_min, 1, kWave);
+        if (lane == 0) before = -1;
+        if (lane == kWave - 1) after = INT64_MAX;
+        __syncthreads();
+        for (int q = 0; q < 4; ++q) {
+            if (q < w) before = s_w[0][q] > before ? s_w[0][q] : before;
+            if (q > w) after = s_w[1][q] < after ? s_w[1][q] : after;
+        }
+        if (before < 0) before = head;        // the group continues from before the chunk
+        if (after == INT64_MAX) after = tail;  // ... or past its end
+        // next start after each element of the run (right to left), group start (left to right)
+        int64_t ge[IPT];
+        int64_t nxt = after;
+#pragma unroll
+        for (int m = IPT - 1; m >= 0; --m) {
+            ge[m] = nxt;
+            if (f[m]) nxt = b + q0 + m;
+        }
+        const double mm = double(se - sb + 1) / 2.0;
+        DD acc[kSpNV];
+#pragma unroll
+        for (int v = 0; v < kSpNV; ++v) acc[v] = DD{0.0, 0.0};
+        int64_t gs = before;
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int q = q0 + m;
+            if (q >= len) continue;
+            if (f[m]) gs = b + q;
+            const double rx = double(s_p[q] - sb + 1) - mm;
+            const double ry = double((gs - sb) + (ge[m] - sb) + 1) / 2.0 - mm;
+            acc[0] = dd_add_d(acc[0], rx * ry);
+            acc[1] = dd_add_d(acc[1], rx * rx);
+            acc[2] = dd_add_d(acc[2], ry * ry);
+            acc[3] = dd_add_d(acc[3], f[m] ? 1.0 : 0.0);
+        }
+#pragma unroll
+        for (int v = 0; v < kSpNV; ++v) {
+            const DD r = wave_dd_sum(acc[v]);
+            if (lane == 0) {
+                s_hi[w][v] = r.hi;
+                s_lo[w][v] = r.lo;
+            }
+        }
+        __syncthreads();
+        if (tid < kSpNV) {
+            DD t{s_hi[0][tid], s_lo[0][tid]};
+            for (int q = 1; q < 4; ++q) t = dd_add(t, DD{s_hi[q][tid], s_lo[q][tid]});
+            part[(k * kSpNV + tid) * 2] = t.hi;
+            part[(k * kSpNV + tid) * 2 + 1] = t.lo;
+        }
+        __syncthreads();  // LDS is reused by the next chunk
+    }
+}
+
 void spearman_index_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const SortedSegs &ss, double *rho,
                            double *pval) {
     const Segs &sg = cs.sg;
@@ -1108,8 +1312,41 @@ void spearman_index_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segi
         FZ_LAUNCH_CHECK();
         return;
     }
-    TieRanks tr = seg_tie_ranks(c, cs, segid, ss.val);
-    seg_spearman_index(c, cs, ss, tr, rho, pval);
+    if (cs.lists.on) {  // (very many segments: the size-class lists, device-wide tie ranks)
+        TieRanks tr = seg_tie_ranks(c, cs, segid, ss.val);
+        seg_spearman_index(c, cs, ss, tr, rho, pval);
+        return;
+    }
+    const int64_t S = sg.S;
+    const int64_t *offs = sg.offs;
+    const int64_t blocks = cs.cps > 0 ? S * cs.cps : cs.cm.cap;
+    double *part = c->arena.get<double>(blocks * kSpNV * 2);
+    {
+        // algorithmic bytes per live value: value 8 + position 4 read
+        ProbeScope ps(c, "seg_spearman", 8.0 * kSpNV * double(S), offs + S, 12.0);
+        k_spearman_chunks<<<unsigned(blocks), kBlock, 0, c->stream>>>(cs.cm, offs, cs.cps, blocks, ss.val, ss.pos, part);
+        FZ_LAUNCH_CHECK();
+        double *sums = c->arena.get<double>(S * kSpNV);
+        seg_fold_parts<kSpNV>(c, cs, part, sums);
+        per_seg(c, S, [=] __device__(int64_t s) {  // as seg_spearman_index
+            const int64_t n = offs[s + 1] - offs[s];
+            double r = NAN, p = NAN;
+            if (n >= 2 && sums[kSpNV * s + 3] > 1.0) {
+                const double d = double(n - 1);
+                const double cxy = sums[kSpNV * s] / d, cxx = sums[kSpNV * s + 1] / d, cyy = sums[kSpNV * s + 2] / d;
+                r = cxy / sqrt(cxx) / sqrt(cyy);
+                if (r > 1.0) r = 1.0;
+                if (r < -1.0) r = -1.0;
+                const double dof = double(n - 2);
+                double q = dof / ((r + 1.0) * (1.0 - r));
+                if (q < 0.0) q = 0.0;
+                const double t = r * sqrt(q);
+                p = 2.0 * stats::t_sf(fabs(t), dof);
+            }
+            rho[s] = r;
+            if (pval) pval[s] = p;
+        });
+    }
 }
 
 // ------------------------------------------------------------------------- Shapiro-Wilk

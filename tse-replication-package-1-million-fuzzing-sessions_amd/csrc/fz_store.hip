@@ -31,33 +31,13 @@ struct Prefix {
     }
 };
 
-// The store prologue in one launch: per-workgroup Fuzzing / Coverage build counts (16 type bytes
-// per thread per load) and issue-number min / max (NULL skipped), written as partials
-// part[4 * block + {0, 1, 2, 3}] that the host reduces after the prologue's single copy and sync -
-// no atomics, no initialisation launch.
+// The store prologue: the issues' number min / max (NULL skipped) as per-workgroup partials
+// part[4 * block + {2, 3}] that the host reduces after the build's single read-back - no atomics, no
+// initialisation launch.  (The build-type counts come off the prefix offsets: k_store_views.)
 constexpr int kProBlocks = 192;
-__global__ __launch_bounds__(kBlock) void k_store_prologue(const uint8_t *__restrict__ type, int64_t nb,
-                                                           const int64_t *__restrict__ num, int64_t ni,
+__global__ __launch_bounds__(kBlock) void k_store_prologue(const int64_t *__restrict__ num, int64_t ni,
                                                            int64_t *__restrict__ part) {
-    __shared__ int64_t s_tmp[4], s_lo[4], s_hi[4];
-    int64_t a = 0, b = 0;
-    const int64_t n16 = (reinterpret_cast<uintptr_t>(type) & 15) == 0 ? nb >> 4 : 0;
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n16; i += int64_t(gridDim.x) * kBlock) {
-        const uint4 w = reinterpret_cast<const uint4 *>(type)[i];
-        const uint32_t v[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t byte = (v[k] >> (8 * j)) & 0xffu;
-                a += byte == 0u;
-                b += byte == 1u;
-            }
-    }
-    for (int64_t i = (n16 << 4) + int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nb; i += int64_t(gridDim.x) * kBlock) {
-        a += type[i] == 0;
-        b += type[i] == 1;
-    }
+    __shared__ int64_t s_lo[4], s_hi[4];
     int64_t lo = INT64_MAX, hi = INT64_MIN;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < ni; i += int64_t(gridDim.x) * kBlock) {
         const int64_t v = num[i];
@@ -65,8 +45,6 @@ __global__ __launch_bounds__(kBlock) void k_store_prologue(const uint8_t *__rest
         lo = v < lo ? v : lo;
         hi = v > hi ? v : hi;
     }
-    a = block_sum(a, s_tmp);
-    b = block_sum(b, s_tmp);
     lo = wave_min(lo);
     hi = wave_max(hi);
     if (lane_id() == 0) {
@@ -79,8 +57,6 @@ __global__ __launch_bounds__(kBlock) void k_store_prologue(const uint8_t *__rest
             lo = s_lo[w] < lo ? s_lo[w] : lo;
             hi = s_hi[w] > hi ? s_hi[w] : hi;
         }
-        part[4 * blockIdx.x] = a;
-        part[4 * blockIdx.x + 1] = b;
         part[4 * blockIdx.x + 2] = lo;
         part[4 * blockIdx.x + 3] = hi;
     }
@@ -90,12 +66,13 @@ __global__ __launch_bounds__(kBlock) void k_store_prologue(const uint8_t *__rest
 // One workgroup: the four views' per-project offsets (fuzz / coverage builds / coverage / issues)
 // read off the prefix offsets - a view is a contiguous range of one table's prefixes, and the time
 // sorts (merge sort included) keep every row in its prefix's range - their longest segments
-// (out[0..3]) and a copy of the 9 store counters (out[4..12]: merge-sort rows and longest segment
-// per table, rows the long bucket class gathered per table): one launch and one D2H copy.
+// (out[0..3]), a copy of the 9 store counters (out[4..12]: merge-sort rows and longest segment
+// per table, rows the long bucket class gathered per table) and the views' row counts (out[13..16]):
+// one launch and one D2H copy.  A view starts at its first prefix's offset (the builds' Coverage
+// view after all Fuzzing rows), read here rather than counted beforehand.
 struct ViewSrc {
     const int64_t *src[4] = {};  // prefix offsets of the view's table (null: empty table)
     int64_t first[4] = {};       // prefix of the view's project 0
-    int64_t base[4] = {};        // rows of the table before the view
     int64_t *dst[4] = {};        // [P + 1]
     const unsigned long long *big = nullptr;  // [9] merge-sort rows / longest segment / fused rows
 };
@@ -103,9 +80,11 @@ __global__ __launch_bounds__(kSortBlock) void k_store_views(const ViewSrc v, int
     __shared__ int64_t s_m[kSortBlock / kWave];
     for (int i = 0; i < 4; ++i) {
         const int64_t *src = v.src[i];
+        const int64_t base = src ? src[v.first[i]] : 0;  // rows of the table before the view
+        if (threadIdx.x == 0) out[13 + i] = src ? src[v.first[i] + P] - base : 0;
         int64_t m = 0;
         for (int64_t p = threadIdx.x; p <= P; p += kSortBlock) {
-            const int64_t o = src ? src[v.first[i] + p] - v.base[i] : 0;
+            const int64_t o = src ? src[v.first[i] + p] - base : 0;
             v.dst[i][p] = o;
             if (src && p < P) {
                 const int64_t l = src[v.first[i] + p + 1] - src[v.first[i] + p];
@@ -332,8 +311,15 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         const uint32_t *tie = KEYS_LDS ? nullptr : tb.tie;  // (the sub-bucket pass runs the long class)
         const int64_t ob = b + (tb.oshift ? tb.oshift[s] : 0);  // where the sorted rows go
         if (len <= min_len) continue;
+        // a segment left to the long-segment pass / merge sort: its rows are marked kGathered so
+        // the gather launched before the host has read the counters skips them (the later pass
+        // writes them, or writes their source positions and the gather runs again)
+        auto flag_segment = [&]() {
+            if (tid == 0) flag_big(big, bigflag, s, len);
+            for (int64_t q = tid; q < len; q += BS) out.spos[ob + q] = kGathered;
+        };
         if (len > MAXN) {
-            if (flag_longer && tid == 0) flag_big(big, bigflag, s, len);
+            if (flag_longer) flag_segment();
             continue;
         }
         const int n = int(len);
@@ -364,7 +350,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
             hi = s_hi[q] > hi ? s_hi[q] : hi;
         }
         if (!tie && hi >= lo && uint64_t(hi) - uint64_t(lo) >= kBlkTop) {  // span too wide for the key
-            if (tid == 0) flag_big(big, bigflag, s, len);
+            flag_segment();
             __syncthreads();
             continue;
         }
@@ -410,7 +396,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
 #pragma unroll
         for (int q = 0; q < NW; ++q) gmax = s_max[q] > gmax ? s_max[q] : gmax;
         if (gmax > uint32_t(tie ? kTieSkew : kBucketSkew)) {  // clustered times: the merge sort takes it
-            if (tid == 0) flag_big(big, bigflag, s, len);
+            flag_segment();
             __syncthreads();
             continue;
         }
@@ -672,23 +658,29 @@ static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
 
 // Gather of every sorted row's columns (after all sorts, merge sort included), all tables in one
 // launch, each table's blocks in proportion to its rows.
-static void gather_tables(fz_ctx *c, const PrefixSorted *pss, const int64_t *unfused) {
+// (the probe's algorithmic bytes are added by the caller once the gathered row counts are known:
+// gather_bytes)
+static void gather_tables(fz_ctx *c, const PrefixSorted *pss) {
     GatherTabs G;
-    double bytes = 0.0;
     for (int k = 0; k < 3; ++k) {
         const PrefixSorted &ps = pss[k];
         const unsigned g = ps.n > 0 ? (grid_for(ps.n, kBlock, 8192) + 7u) & ~7u : 0u;
         G.blk[k + 1] = G.blk[k] + g;
         if (ps.n <= 0) continue;
         G.tab[k] = GatherTab{ps.out.spos, ps.rows, ps.n, ps.orow, ps.gc};
-        // algorithmic bytes: spos 4 read per row; for the rows it gathers (unfused: the short
-        // classes' and merge-sorted rows) row id 4 + columns read, perm 4 + row 4 + columns written
-        bytes += 4.0 * double(ps.n) + (12.0 + 2.0 * ps.gc.bytes()) * double(unfused[k]);
     }
     if (G.blk[3] == 0) return;
-    ProbeScope probe(c, "store_gather", bytes);
+    ProbeScope probe(c, "store_gather", 0.0);
     k_store_gather<<<G.blk[3], kBlock, 0, c->stream>>>(G);
     FZ_LAUNCH_CHECK();
+}
+// algorithmic bytes of one gather pass: spos 4 read per row; for the rows it gathers (gathered[k])
+// row id 4 + columns read, perm 4 + row 4 + columns written
+static double gather_bytes(const PrefixSorted *pss, const int64_t *gathered) {
+    double bytes = 0.0;
+    for (int k = 0; k < 3; ++k)
+        if (pss[k].n > 0) bytes += 4.0 * double(pss[k].n) + (12.0 + 2.0 * pss[k].gc.bytes()) * double(gathered[k]);
+    return bytes;
 }
 
 // ---- long segments (> 16384 rows, config 5's Zipf head): one distribution pass --------------
@@ -1000,26 +992,13 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     const int64_t P = s.P;
     const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
 
-    // one host round trip: the issue-number range (RQ1's ROW_NUMBER dedup key) + build-type counts
+    // the issue-number range (RQ1's ROW_NUMBER dedup key) as per-workgroup partials, read back with
+    // the views' counters below (the build's one host round trip)
     store_eligibility(c);
-    const int64_t nwork = t->n_builds > t->n_issues ? t->n_builds : t->n_issues;
-    const int pblk = int(grid_for(nwork, kBlock * 16, kProBlocks));
+    const int pblk = int(grid_for(t->n_issues, kBlock * 16, kProBlocks));
     int64_t *ppart = c->arena.get<int64_t>(4 * pblk);
-    k_store_prologue<<<pblk, kBlock, 0, c->stream>>>(t->b_type, t->n_builds, t->i_number, t->n_issues, ppart);
+    k_store_prologue<<<pblk, kBlock, 0, c->stream>>>(t->i_number, t->n_issues, ppart);
     FZ_LAUNCH_CHECK();
-    FZ_HIP(hipMemcpyAsync(c->h_pinned + 64, ppart, size_t(4 * pblk) * 8, hipMemcpyDeviceToHost, c->stream));
-    sync(c);
-    int64_t n_fuzz = 0, n_covb = 0, nlo = INT64_MAX, nhi = INT64_MIN;
-    for (int k = 0; k < pblk; ++k) {
-        const int64_t *q = c->h_pinned + 64 + 4 * k;
-        n_fuzz += q[0];
-        n_covb += q[1];
-        nlo = q[2] < nlo ? q[2] : nlo;
-        nhi = q[3] > nhi ? q[3] : nhi;
-    }
-    // (no non-NULL number: the empty range min = INT64_MAX > max = INT64_MIN, as the old read-back gave)
-    s.num_min = nlo;
-    s.num_max = nhi;
 
     // the three tables: (prefix = [type|]project) LSD passes, then each segment sorted by time in LDS
     struct Tab {
@@ -1072,64 +1051,85 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     }
     prefix_sort_tables(c, tin, pss);
     time_sort_tables(c, pss);
-    // the views (per-project ranges of the sorted tables) and the longest segments, off the
-    // prefix offsets: builds' prefix is type << pbits | project (Fuzzing 0, Coverage 1)
+    // the views (per-project ranges of the sorted tables): their offsets, longest segments and row
+    // counts off the prefix offsets - builds' prefix is type << pbits | project (Fuzzing 0, Coverage 1)
+    ViewSrc vs;
+    DevBuf *voff[4] = {&s.off_fuzz, &s.off_covb, &s.off_cov, &s.off_iss};
+    const int tab_of[4] = {0, 0, 1, 2};
+    for (int i = 0; i < 4; ++i) {
+        vs.src[i] = pss[tab_of[i]].offs;
+        vs.first[i] = i == 1 ? (int64_t(1) << pbits) : 0;
+        vs.dst[i] = voff[i]->ensure<int64_t>(P + 1);
+    }
+    vs.big = big3;
+    int64_t *mx = c->arena.get<int64_t>(17);
+    k_store_views<<<1, kSortBlock, 0, c->stream>>>(vs, P, mx);
+    FZ_LAUNCH_CHECK();
+    FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 17 * 8, hipMemcpyDeviceToHost, c->stream));
+    FZ_HIP(hipMemcpyAsync(c->h_pinned + 64, ppart, size_t(4 * pblk) * 8, hipMemcpyDeviceToHost, c->stream));
+    if (!c->ev_readback) FZ_HIP(hipEventCreateWithFlags(&c->ev_readback, hipEventDisableTiming));
+    FZ_HIP(hipEventRecord(c->ev_readback, c->stream));
+    // the gather of the short classes' rows, launched before the host reads the counters (rows of
+    // segments left to the long-segment pass / merge sort are marked kGathered: skipped here); the
+    // host's round trip overlaps it
+    gather_tables(c, pss);
+    FZ_HIP(hipEventSynchronize(c->ev_readback));
+    int64_t nlo = INT64_MAX, nhi = INT64_MIN;
+    for (int k = 0; k < pblk; ++k) {
+        const int64_t *q = c->h_pinned + 64 + 4 * k;
+        nlo = q[2] < nlo ? q[2] : nlo;
+        nhi = q[3] > nhi ? q[3] : nhi;
+    }
+    // (no non-NULL number: the empty range min = INT64_MAX > max = INT64_MIN, as the old read-back gave)
+    s.num_min = nlo;
+    s.num_max = nhi;
+    const int64_t maxseg[4] = {c->h_pinned[0], c->h_pinned[1], c->h_pinned[2], c->h_pinned[3]};
+    const int64_t bigrows[3] = {c->h_pinned[4], c->h_pinned[5], c->h_pinned[6]};
+    const int64_t bigmax[3] = {c->h_pinned[7], c->h_pinned[8], c->h_pinned[9]};
+    const int64_t fused[3] = {c->h_pinned[10], c->h_pinned[11], c->h_pinned[12]};
+    const int64_t n_fuzz = c->h_pinned[13], n_covb = c->h_pinned[14];
     {
         auto view = [&](View &v, DevBuf &rowb, DevBuf &tmb, DevBuf &prb, int64_t at, int64_t n, DevBuf &offb) {
             v.n = n;
             v.row = rowb.as<int32_t>() + at;
             v.time = tmb.as<int64_t>() + at;
             v.proj = prb.as<uint32_t>() + at;
-            v.offs = offb.ensure<int64_t>(P + 1);
+            v.offs = offb.as<int64_t>();
         };
         view(s.fuzz, s.b_row, s.b_time, s.b_proj, 0, n_fuzz, s.off_fuzz);
         view(s.covb, s.b_row, s.b_time, s.b_proj, n_fuzz, n_covb, s.off_covb);
         view(s.cov, s.c_row, s.c_time, s.c_proj, 0, t->n_cov, s.off_cov);
         view(s.issues, s.i_row, s.i_time, s.i_proj, 0, t->n_issues, s.off_iss);
     }
-    ViewSrc vs;
-    const View *vw[4] = {&s.fuzz, &s.covb, &s.cov, &s.issues};
-    const int tab_of[4] = {0, 0, 1, 2};
-    for (int i = 0; i < 4; ++i) {
-        vs.src[i] = pss[tab_of[i]].offs;
-        vs.first[i] = i == 1 ? (int64_t(1) << pbits) : 0;
-        vs.base[i] = i == 1 ? n_fuzz : 0;
-        vs.dst[i] = const_cast<int64_t *>(vw[i]->offs);
-    }
-    vs.big = big3;
-    int64_t *mx = c->arena.get<int64_t>(13);
-    k_store_views<<<1, kSortBlock, 0, c->stream>>>(vs, P, mx);
-    FZ_LAUNCH_CHECK();
-    FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 13 * 8, hipMemcpyDeviceToHost, c->stream));
-    sync(c);
-    // segments the bucket sorts left (longer than 16384 rows, clustered, or a time span too wide
-    // for their packed key): segmented merge sort of those rows only, writing the same outputs
-    const int64_t maxseg[4] = {c->h_pinned[0], c->h_pinned[1], c->h_pinned[2], c->h_pinned[3]};
-    const int64_t bigrows[3] = {c->h_pinned[4], c->h_pinned[5], c->h_pinned[6]};
-    const int64_t bigmax[3] = {c->h_pinned[7], c->h_pinned[8], c->h_pinned[9]};
-    const int64_t fused[3] = {c->h_pinned[10], c->h_pinned[11], c->h_pinned[12]};
     // the probes' algorithmic bytes of the gathers: the long bucket class's fused gather, then the
-    // rows left to k_store_gather (short classes and merge-sorted rows)
-    int64_t unfused[3];
+    // rows the gather above moved (short classes; not the flagged segments' rows)
+    int64_t gathered[3];
     for (int k = 0; k < 3; ++k) {
         const double per = 12.0 + 2.0 * pss[k].gc.bytes();  // row 4 + columns in; perm 4 + row 4 + columns out
         ProbeScope::add_bytes(c, "seg_time_sort", per * double(fused[k]));
-        unfused[k] = pss[k].n - fused[k];
+        gathered[k] = pss[k].n - fused[k] - bigrows[k];
     }
+    ProbeScope::add_bytes(c, "store_gather", gather_bytes(pss, gathered));
+    // segments the bucket sorts left (longer than 16384 rows, clustered, or a time span too wide
+    // for their packed key): the long-segment distribution pass (which gathers their columns
+    // itself), else the segmented merge sort of those rows only, writing the same outputs; merged
+    // rows are then gathered by a second gather pass (which redoes the short classes' rows too)
+    bool regather = false, bucketed[3] = {false, false, false};
     for (int k = 0; k < 3; ++k) {
         if (bigrows[k] == 0) continue;
         const PrefixSorted &ps = pss[k];
-        if (big_segments_bucketed(c, ps, bigrows[k])) {
-            unfused[k] -= bigrows[k];  // the sub-bucket sort gathered them (big_sub_sort)
-            continue;
-        }
+        bucketed[k] = big_segments_bucketed(c, ps, bigrows[k]);
+        if (bucketed[k]) continue;
         ProbeScope probe(c, "seg_merge_sort", 36.0 * double(bigrows[k]));
         sort_big_segments(c, ps.offs, ps.S, ps.n, bigmax[k], ps.bigflag, StoreTimeKey{ps.time},
                           StoreSink{ps.pmask, ps.out});
+        regather = true;
     }
-    // the long-segment bucket sort gathered its segments' columns; the short classes' and the
-    // merge-sorted rows are gathered here (rows marked kGathered are skipped)
-    gather_tables(c, pss, unfused);
+    if (regather) {
+        for (int k = 0; k < 3; ++k) gathered[k] = pss[k].n - fused[k] - (bucketed[k] ? bigrows[k] : 0);
+        gather_tables(c, pss);
+        ProbeScope::add_bytes(c, "store_gather", gather_bytes(pss, gathered));
+    }
     materialize_sorted(c);
     s.fuzz.max_seg = maxseg[0];
     s.covb.max_seg = maxseg[1];
