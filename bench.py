@@ -131,14 +131,26 @@ def main():
     upload_ms = (time.perf_counter() - t_up) * 1e3
     up = eng.upload_timing()  # host staging memcpy vs the H2D copy itself
     st = eng.build_store()
+    stages = [s for s in STAGES if s in args.stages.split(",")]
     if sharded:
         from tse_amd import parallel as par
         M = par.agree_max(int(st.max_fuzz_per_project), dev)
-        rq1_shard = par.GpuRQ1Shard(eng, M)
-        rq3_shard = par.GpuRQ3Shard(eng)
-        rq2c_shard = par.GpuRQ2CountShard(eng)
-        rq4a_shard = par.GpuRQ4aShard(eng, M)
-        rq4b_shard = par.GpuRQ4bShard(eng)
+        # the sharded step: every analysis' driver (local kernels + its exchanges) in its own host
+        # thread, on its own child engine (stream + context over the store) and its own process
+        # group of all ranks - their host round trips and collectives overlap instead of queueing
+        # behind each other (--serial: one after another on the engine, the default group)
+        snames = [n for n in ("rq3", "rq4b", "rq2_count", "rq1", "rq4a", "rq2_add") if n in stages]
+        if args.serial:
+            skids = {n: eng for n in snames}
+            sgroups = {n: None for n in snames}
+        else:
+            skids = {n: eng.child() for n in snames}
+            sgroups = {n: dist.new_group(backend=args.dist_backend) for n in snames}
+        rq1_shard = par.GpuRQ1Shard(skids.get("rq1", eng), M)
+        rq3_shard = par.GpuRQ3Shard(skids.get("rq3", eng))
+        rq2c_shard = par.GpuRQ2CountShard(skids.get("rq2_count", eng))
+        rq4a_shard = par.GpuRQ4aShard(skids.get("rq4a", eng), M)
+        rq4b_shard = par.GpuRQ4bShard(skids.get("rq4b", eng))
         if args.strong:
             own = (lo, hi)
         else:
@@ -149,7 +161,6 @@ def main():
     launch = {"rq2_count": compute.rq2_count_launch, "rq2_add": compute.rq2_add_launch, "rq3": compute.rq3_launch,
               "rq4a": compute.rq4a_launch, "rq4b": compute.rq4b_launch}
 
-    stages = [s for s in STAGES if s in args.stages.split(",")]
     launch["rq1"] = lambda e, b: compute.rq1_launch(e, b)
     bufs["rq1"] = rq1_bufs
     launch["rq3_main"], launch["rq3_stats"] = compute.rq3_main_launch, compute.rq3_stats_launch
@@ -167,6 +178,33 @@ def main():
         raise SystemExit("bench: rq3_main / rq3_stats groupings need the graph path")
     pool = None
     graphs = None
+    if sharded:
+        def sh_rq1(e):
+            part = par.rq1_sharded(rq1_shard, rank, world)[0]
+            par.gather_rows({"issue": part["matched_issue"], "build": part["matched_build"]}, world)
+
+        def sh_rq2_add(e):
+            launch["rq2_add"](e, bufs["rq2_add"])
+            b = bufs["rq2_add"]
+            n_add = int(b.counts[E.RQ2A_ROWS].item())
+            par.gather_rows({"project": b.row_project[:n_add], "diff_total": b.diff_total[:n_add],
+                             "diff_coverage": b.diff_coverage[:n_add]}, world)
+        shard_step = {
+            "rq1": sh_rq1,
+            "rq2_count": lambda e: par.rq2_count_sharded(rq2c_shard, rank, world, *own, gather_values=False),
+            "rq4a": lambda e: par.rq4a_sharded(rq4a_shard, rank, world, *own),
+            "rq4b": lambda e: par.rq4b_sharded(rq4b_shard, rank, world),
+            "rq2_add": sh_rq2_add,
+            "rq3": lambda e: par.rq3_sharded(rq3_shard, rank, world),
+        }
+
+        def run_sharded(name):
+            e = skids[name]
+            with torch.cuda.stream(e.stream), par.use_group(sgroups[name]):
+                shard_step[name](e)
+        if not args.serial:
+            from concurrent.futures import ThreadPoolExecutor
+            pool = ThreadPoolExecutor(len(snames))
     if concurrent:
         from concurrent.futures import ThreadPoolExecutor
         # the last group runs on the engine itself (its stream, after the store build)
@@ -213,26 +251,19 @@ def main():
             for f in futs:
                 f.result()
             return
+        # sharded: exact recombination of every script over the ranks (tse_amd/parallel.py)
+        eng.join_children()  # the previous step's drivers have read the store
         eng.build_store()
-        # sharded: exact RQ1 / RQ3 recombination + row gathers (tse_amd/parallel.py)
-        if "rq1" in stages:
-            part = par.rq1_sharded(rq1_shard, rank, world)[0]
-            par.gather_rows({"issue": part["matched_issue"], "build": part["matched_build"]}, world)
-        if "rq2_count" in stages:
-            par.rq2_count_sharded(rq2c_shard, rank, world, *own, gather_values=False)
-        if "rq4a" in stages:
-            par.rq4a_sharded(rq4a_shard, rank, world, *own)
-        if "rq4b" in stages:
-            par.rq4b_sharded(rq4b_shard, rank, world)
-        if "rq2_add" in stages:
-            launch["rq2_add"](eng, bufs["rq2_add"])
-        if "rq2_add" in stages:
-            b = bufs["rq2_add"]
-            n_add = int(b.counts[E.RQ2A_ROWS].item())
-            par.gather_rows({"project": b.row_project[:n_add], "diff_total": b.diff_total[:n_add],
-                             "diff_coverage": b.diff_coverage[:n_add]}, world)
-        if "rq3" in stages:
-            par.rq3_sharded(rq3_shard, rank, world)
+        if pool is None:
+            for n in snames:
+                run_sharded(n)
+            return
+        for ch in set(skids.values()):
+            if ch is not eng:
+                ch.follow_parent()
+        futs = [pool.submit(run_sharded, n) for n in snames]
+        for f in futs:
+            f.result()
 
     for _ in range(max(args.warmup, 1 if concurrent and not args.no_graphs else 0)):
         step()
@@ -268,13 +299,16 @@ def main():
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    if not concurrent:
+    # (the probe brackets launches on the engine's own context: with the analyses on child contexts
+    # it is measured on serial steps after the timed region)
+    on_children = concurrent or (sharded and pool is not None)
+    if not on_children:
         eng.probe_begin(args.probe)
     t0 = time.perf_counter()
     ev0.record(eng.stream)
     for _ in range(args.steps):
         step()
-    if concurrent:
+    if concurrent or sharded:
         eng.join_children()
     ev1.record(eng.stream)
     torch.cuda.synchronize(dev)
@@ -283,7 +317,7 @@ def main():
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     probe_window = args.steps
-    if not concurrent:
+    if not on_children:
         launches, probe_ms, probe_bytes = eng.probe_end()
     else:  # the probe brackets launches on the engine's own context: measure it on serial steps
         probe_window = max(args.probe_steps, 1)
@@ -299,7 +333,7 @@ def main():
     if args.probe_steps > 0:
         eng.probe_begin(",".join(TABLE_KERNELS))
         for _ in range(args.probe_steps):
-            serial_step() if not sharded else step()
+            serial_step() if on_children or not sharded else step()
         eng.probe_end()
         for k in TABLE_KERNELS:
             n, ms_k, b_k = eng.probe_get(k)

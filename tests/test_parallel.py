@@ -305,12 +305,12 @@ class OracleRQ4bShard(OracleRQ2CountShard):
         return out
 
 
-def _worker(rank, world, port, case, errfile):
+def _worker(rank, world, port, case, errfile, threaded=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        _check(rank, world, case)
+        _check(rank, world, case, threaded)
     except BaseException as e:  # report to the parent (mp.spawn only sees the exit code)
         with open(f"{errfile}.{rank}", "w") as f:
             import traceback
@@ -320,30 +320,49 @@ def _worker(rank, world, port, case, errfile):
         dist.destroy_process_group()
 
 
-def _check(rank, world, case):
+def _check(rank, world, case, threaded=False):
     from oracle import rq_oracle as orc
     from gpu_common import assert_same
     t = make_table(case, world)
     lo, hi = par.shard_bounds(t, world)[rank]
     ts, rows = par.take_shard(t, lo, hi)
-    # RQ1
     nF = np.bincount(ts.b_project[ts.b_type == 0].astype(np.int64), minlength=len(t.projects))
     M = par.agree_max(int(nF.max()) if len(nF) else 0)
-    sh = OracleRQ1Shard(ts, rows, max(M, 1))
-    part, counts, it, idt, reran = par.rq1_sharded(sh, rank, world)
-    rows1 = par.gather_rows({"matched_issue": part["matched_issue"], "matched_build": part["matched_build"]}, world)
-    any_rerun = torch.tensor([int(reran)])
-    torch.distributed.all_reduce(any_rerun)
-    # RQ3
-    total3, cols3, st3 = par.rq3_sharded(OracleRQ3Shard(ts, rows), rank, world)
-    # RQ2 count
-    r2 = par.rq2_count_sharded(OracleRQ2CountShard(ts), rank, world, lo, hi)
-    # RQ4a
     nF4 = np.bincount(ts.b_project[(ts.b_type == 0) & (ts.b_time < LIMIT_US)].astype(np.int64),
                       minlength=len(t.projects))
-    r4 = par.rq4a_sharded(OracleRQ4aShard(ts, par.agree_max(int(nF4.max()) if len(nF4) else 1)), rank, world,
-                          lo, hi)
-    r4b = par.rq4b_sharded(OracleRQ4bShard(ts), rank, world)
+    M4 = par.agree_max(int(nF4.max()) if len(nF4) else 1)
+
+    def rq1():
+        sh = OracleRQ1Shard(ts, rows, max(M, 1))
+        part, counts, it, idt, reran = par.rq1_sharded(sh, rank, world)
+        rows1 = par.gather_rows({"matched_issue": part["matched_issue"], "matched_build": part["matched_build"]},
+                                world)
+        any_rerun = torch.tensor([int(reran)])
+        par.all_reduce(any_rerun)
+        return counts, it, idt, rows1, any_rerun
+
+    drivers = {"rq1": rq1,
+               "rq3": lambda: par.rq3_sharded(OracleRQ3Shard(ts, rows), rank, world),
+               "rq2": lambda: par.rq2_count_sharded(OracleRQ2CountShard(ts), rank, world, lo, hi),
+               "rq4a": lambda: par.rq4a_sharded(OracleRQ4aShard(ts, M4), rank, world, lo, hi),
+               "rq4b": lambda: par.rq4b_sharded(OracleRQ4bShard(ts), rank, world)}
+    if threaded:
+        # the bench's sharded step: every driver in its own thread over its own process group (their
+        # collectives interleave differently on every rank)
+        from concurrent.futures import ThreadPoolExecutor
+        groups = {k: torch.distributed.new_group(backend="gloo") for k in drivers}
+
+        def run(k):
+            with par.use_group(groups[k]):
+                return drivers[k]()
+        with ThreadPoolExecutor(len(drivers)) as pool:
+            futs = {k: pool.submit(run, k) for k in (list(drivers)[::-1] if rank % 2 else list(drivers))}
+            res = {k: f.result() for k, f in futs.items()}
+    else:
+        res = {k: f() for k, f in drivers.items()}
+    counts, it, idt, rows1, any_rerun = res["rq1"]
+    total3, cols3, st3 = res["rq3"]
+    r2, r4, r4b = res["rq2"], res["rq4a"], res["rq4b"]
     if rank != 0:
         return
     g = orc.rq1(t)
@@ -383,10 +402,10 @@ def _check(rank, world, case):
     assert_same(ours4b, orc.rq4b(t), "rq4b")
 
 
-def _spawn(world, case, tmp_path):
+def _spawn(world, case, tmp_path, threaded=False):
     errfile = str(tmp_path / "err")
     try:
-        mp.spawn(_worker, args=(world, _free_port(), case, errfile), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), case, errfile, threaded), nprocs=world, join=True)
     except Exception:
         msgs = [open(f"{errfile}.{r}").read() for r in range(world) if os.path.exists(f"{errfile}.{r}")]
         raise AssertionError("\n".join(msgs) or "worker failed")
@@ -409,6 +428,13 @@ def test_shard_bounds_cover_and_balance():
                                         (8, "last_shard_no_issues")])
 def test_sharded_rq1_rq3_match_whole_table(world, case, tmp_path):
     _spawn(world, case, tmp_path)
+
+
+@pytest.mark.parametrize("world,case", [(2, "collide"), (3, "last_shard_no_issues")])
+def test_sharded_drivers_concurrent_groups(world, case, tmp_path):
+    """The five drivers at once, one thread and one process group each (bench.py's sharded step),
+    started in a different order on odd ranks: the same exact results as one after another."""
+    _spawn(world, case, tmp_path, threaded=True)
 
 
 def test_host_many_round_trips_dtypes():

@@ -308,6 +308,10 @@ namespace fz {
 // Device-wide exclusive scan of int64 (in != out allowed). Returns nothing; total written to
 // out_total (device) if non-null.
 void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, int64_t *out_total);
+// The same over the first *d_live elements of a capacity n_cap (device count): elements past them are
+// neither read nor written, except out[live] = the total when live < n_cap.
+void scan_exclusive_i64_dn(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n_cap, const int64_t *d_live,
+                           int64_t *out_total);
 // Stable LSD radix sort of (uint64 key, uint32 value) over bits [0, bits).  Uses arena scratch;
 // the result is written back to keys/vals.
 void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int bits);

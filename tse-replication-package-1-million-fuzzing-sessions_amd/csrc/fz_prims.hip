@@ -233,17 +233,26 @@ void lookback_reset(fz_ctx *c) {
 constexpr int kLbItems = 16;
 constexpr int kLbTile = kBlock * kLbItems;  // 4096
 
+// d_live (optional): only the first *d_live (<= n) elements are scanned - tiles past them exit after
+// drawing their ticket (a capacity-sized launch over a short live prefix costs little), and out[live]
+// receives the total when live < n.
 __global__ __launch_bounds__(kBlock) void k_scan_lookback(const int64_t *__restrict__ in, int64_t *__restrict__ out,
-                                                          int64_t n, int64_t ntiles, Lookback lb,
-                                                          int64_t *__restrict__ total) {
+                                                          int64_t n_cap, int64_t ntiles_cap, Lookback lb,
+                                                          int64_t *__restrict__ total,
+                                                          const int64_t *__restrict__ d_live) {
     __shared__ int64_t s_val[kLbTile];
     __shared__ int64_t s_tmp[4];
     __shared__ int64_t s_prefix;
     __shared__ unsigned int s_tile;
     const int tid = threadIdx.x;
     if (tid == 0) s_tile = lb_take_tile(lb.ticket, gridDim.x);
+    const int64_t live = d_live ? (*d_live < n_cap ? *d_live : n_cap) : n_cap;
+    const int64_t n = live;
+    const int64_t ntiles = live > 0 ? (live + kLbTile - 1) / kLbTile : 1;
+    (void)ntiles_cap;
     __syncthreads();
     const int64_t tile = s_tile;
+    if (tile >= ntiles) return;  // past the live elements (every workgroup drew its ticket)
     const int64_t base = tile * kLbTile;
     int64_t x[kLbItems];
 #pragma unroll
@@ -267,7 +276,10 @@ __global__ __launch_bounds__(kBlock) void k_scan_lookback(const int64_t *__restr
         const int64_t prefix = lb_exclusive_prefix(lb, tile, agg);
         if (tid == 0) {
             s_prefix = prefix;
-            if (total && tile == ntiles - 1) *total = prefix + agg;
+            if (tile == ntiles - 1) {
+                if (total) *total = prefix + agg;
+                if (live < n_cap) out[live] = prefix + agg;
+            }
         }
     }
     __syncthreads();
@@ -296,7 +308,7 @@ static void scan_exclusive_impl(fz_ctx *c, const int64_t *in, int64_t *out, int6
         // algorithmic bytes: the int64 input read, the int64 output written (the long scans only:
         // shorter ones are one- or few-workgroup launches)
         ProbeScope ps(c, "scan_i64", 16.0 * double(n));
-        k_scan_lookback<<<unsigned(ntiles), kBlock, 0, c->stream>>>(in, out, n, ntiles, lb, out_total);
+        k_scan_lookback<<<unsigned(ntiles), kBlock, 0, c->stream>>>(in, out, n, ntiles, lb, out_total, nullptr);
         FZ_LAUNCH_CHECK();
         lookback_end(c, ntiles);
         return;
@@ -317,6 +329,35 @@ static void scan_exclusive_impl(fz_ctx *c, const int64_t *in, int64_t *out, int6
 
 void scan_exclusive_i64(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n, int64_t *out_total) {
     scan_exclusive_impl(c, in, out, n, out_total);
+}
+
+// (the short path of scan_exclusive_i64_dn: the scan ran over the capacity; the live total from it)
+__global__ void k_scan_live_end(const int64_t *__restrict__ in, int64_t *__restrict__ out, int64_t n_cap,
+                                const int64_t *__restrict__ d_live, int64_t *__restrict__ total) {
+    const int64_t live = *d_live < n_cap ? *d_live : n_cap;
+    const int64_t t = live > 0 ? out[live - 1] + in[live - 1] : 0;
+    if (live < n_cap) out[live] = t;
+    if (total) *total = t;
+}
+
+void scan_exclusive_i64_dn(fz_ctx *c, const int64_t *in, int64_t *out, int64_t n_cap, const int64_t *d_live,
+                           int64_t *out_total) {
+    if (n_cap <= kScan1Max || d_live == nullptr) {  // (short: one or few workgroups anyway)
+        scan_exclusive_impl(c, in, out, n_cap, d_live ? nullptr : out_total);
+        if (d_live && n_cap > 0) {
+            k_scan_live_end<<<1, 1, 0, c->stream>>>(in, out, n_cap, d_live, out_total);
+            FZ_LAUNCH_CHECK();
+        } else if (d_live && out_total) {
+            dev_fill(c, out_total, 0, sizeof(int64_t));
+        }
+        return;
+    }
+    const int64_t ntiles = (n_cap + kLbTile - 1) / kLbTile;
+    const Lookback lb = lookback_begin(c, ntiles);
+    ProbeScope ps(c, "scan_i64", 0.0, d_live, 16.0);
+    k_scan_lookback<<<unsigned(ntiles), kBlock, 0, c->stream>>>(in, out, n_cap, ntiles, lb, out_total, d_live);
+    FZ_LAUNCH_CHECK();
+    lookback_end(c, ntiles);
 }
 
 // ------------------------------------------------------------------------- LSD radix sort

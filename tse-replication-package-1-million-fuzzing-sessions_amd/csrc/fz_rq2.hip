@@ -84,10 +84,18 @@ void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_i
     dev_fill(c, n_ge100, 0, 8);
     uint64_t *key = c->arena.get<uint64_t>(n);
     uint32_t *idx = c->arena.get<uint32_t>(n);
+    const double *svals = values;  // the values ride along as the sort's payload (no gather after)
     if (n > 0) {
         k_session_keys<<<grid_for(n), kBlock, 0, st>>>(session_ids, n, key, idx);
         FZ_LAUNCH_CHECK();
-        radix_sort_pairs_swap(c, key, idx, n, bits_for(uint64_t(S)));  // stable: input order kept per session
+        RadixPayload pl;
+        pl.n = 1;
+        pl.in[0] = values;
+        pl.size[0] = 8;
+        uint32_t *no_vals = nullptr;
+        // stable: input order kept per session
+        radix_sort_pairs_payload(c, key, no_vals, n, bits_for(uint64_t(S)), pl);
+        svals = static_cast<const double *>(pl.out[0]);
     }
     double *sv = c->arena.get<double>(n);
     uint32_t *sid = c->arena.get<uint32_t>(n);
@@ -96,7 +104,7 @@ void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_i
     map_n(c, n > 0 ? n : 1, nullptr, [=] __device__(int64_t k) {
         if (k == 0) *d_n = n;
         if (k < n) {
-            sv[k] = values[idx[k]];
+            sv[k] = svals[k];
             sid[k] = uint32_t(key[k]);
         }
     });
@@ -163,22 +171,28 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
 
     // coverage_by_session_index: order by (index within project, project) - the values are in
     // project order already, so a stable sort on the index alone keeps projects in order
+    // (the trend values ride along as the sort's payload, coming out in session order - no random
+    // gather through a permutation afterwards)
     const int ibits = bits_for(uint64_t(M));
     uint64_t *key = c->arena.get<uint64_t>(NC);
-    uint32_t *idx = c->arena.get<uint32_t>(NC);
     const uint32_t *tproj = T.proj;
     map_n(c, NC, nullptr, [=] __device__(int64_t j) {
         const int64_t live = *d_nt;
         key[j] = j < live ? uint64_t(j - toffs[tproj[j]]) : uint64_t(M);  // M: past every real index
-        idx[j] = uint32_t(j);
     });
-    radix_sort_pairs_swap(c, key, idx, NC, ibits);
+    RadixPayload pl;
+    pl.n = 1;
+    pl.in[0] = tv;
+    pl.size[0] = 8;
+    uint32_t *no_vals = nullptr;
+    radix_sort_pairs_payload(c, key, no_vals, NC, ibits, pl);
+    const double *stv = static_cast<const double *>(pl.out[0]);
     double *sv = o->session_values;
     uint32_t *sid = c->arena.get<uint32_t>(NC);
     map_n(c, NC, nullptr, [=] __device__(int64_t k) {
         const int64_t live = *d_nt;
         sid[k] = uint32_t(key[k]);
-        if (k < live) sv[k] = tv[idx[k]];
+        if (k < live) sv[k] = stv[k];
     });
     segment_offsets_dn(c, sid, d_nt, NC, M, o->session_offsets);
     if (flags & FZ_RQ2C_SKIP_SESSION_STATS) return;

@@ -44,11 +44,17 @@ struct CovBuildRq3 {  // Coverage, any result, DATE(timecreated) < '2025-01-09' 
     const int64_t *time;
     __device__ bool operator()(int32_t r) const { return time[r] < kLim3b; }
 };
-struct CovRowsRq3 {  // covered_line IS NOT NULL AND DATE(date) < '2025-01-09' (:263)
-    static constexpr int kBytes = 9;  // column bytes read per row (filter_compact probe)
+struct CovRowsRq3 {  // covered_line IS NOT NULL AND DATE(date) < '2025-01-09' (:263), projects with
+                     // a fixed issue only (the only ones whose rows the per-issue loop reads, :241)
+    static constexpr int kBytes = 13;  // column bytes read per row (filter_compact probe)
     const uint8_t *valid;
     const int64_t *date;
-    __device__ bool operator()(int32_t r) const { return (valid[r] & FZ_VALID_COVERED) && date[r] < kLim3b; }
+    const uint32_t *proj;
+    const int64_t *sel;  // [P + 1] exclusive prefix count of the projects with a fixed issue
+    __device__ bool operator()(int32_t r) const {
+        const uint32_t p = proj[r];
+        return sel[p + 1] != sel[p] && (valid[r] & FZ_VALID_COVERED) && date[r] < kLim3b;
+    }
 };
 
 void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t NI, const int64_t *d_nd,
@@ -71,7 +77,17 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
                 FixedIssuesRq3{t.i_project, t.i_status, t.i_rts, o->eligible}, I);
     filter_view(c, s.fuzz.row, s.fuzz.time, s.fuzz.proj, s.fuzz.n, P, FuzzRq3{t.b_result, t.b_time}, F);
     filter_view(c, s.covb.row, s.covb.time, s.covb.proj, s.covb.n, P, CovBuildRq3{t.b_time}, CB);
-    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P, CovRowsRq3{t.c_valid, t.c_date}, TC);
+    // the coverage rows of the projects with a fixed issue only: the view's tiles of other projects
+    // are skipped unread (config 3 / 5, coverage-only tables: all of them)
+    int64_t *selp = c->arena.get<int64_t>(P + 1);
+    {
+        int64_t *self = c->arena.get<int64_t>(P + 1);
+        const int64_t *ioff = I.offs;
+        map_n(c, P + 1, nullptr, [=] __device__(int64_t p) { self[p] = p < P && ioff[p + 1] > ioff[p] ? 1 : 0; });
+        scan_exclusive_i64(c, self, selp, P + 1, nullptr);
+    }
+    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P, CovRowsRq3{t.c_valid, t.c_date, t.c_project, selp}, TC,
+                nullptr, selp);
 
     // ---- detected: one thread per issue (:241-302)
     int64_t *dflag = c->arena.get<int64_t>(NI);
@@ -156,11 +172,11 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         const uint32_t last = n > 0 ? iproj[n - 1] : 0xffffffffu;
         hasiss[p] = (ioffs[p + 1] > ioffs[p]) && (flush_last || uint32_t(p) != last);
     });
+    // (flags, positions and rows over the live rows of TC only: *TCv.d_n of capacity NC)
     int64_t *nflag = c->arena.get<int64_t>(NC);
     int64_t *npos = c->arena.get<int64_t>(NC);
-    map_n(c, NC, nullptr, [=] __device__(int64_t k) {
+    map_n(c, NC, TCv.d_n, [=] __device__(int64_t k) {
         nflag[k] = 0;
-        if (k >= *TCv.d_n) return;
         const uint32_t p = TCv.proj[k];
         if (!hasiss[p] || k == TCv.offs[p]) return;
         const int32_t ra = TCv.row[k - 1], rb = TCv.row[k];
@@ -177,8 +193,8 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         nflag[k] = 1;
         if (p == iproj[*d_ni - 1]) atomic_add_i64(&counts[FZ_RQ3_NON_LAST], 1);
     });
-    scan_exclusive_i64(c, nflag, npos, NC, counts + FZ_RQ3_NON_DETECTED);
-    map_n(c, NC, nullptr, [=] __device__(int64_t k) {
+    scan_exclusive_i64_dn(c, nflag, npos, NC, TCv.d_n, counts + FZ_RQ3_NON_DETECTED);
+    map_n(c, NC, TCv.d_n, [=] __device__(int64_t k) {
         if (!nflag[k]) return;
         const int64_t q = npos[k];
         const int32_t ra = TCv.row[k - 1], rb = TCv.row[k];
@@ -273,27 +289,29 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
     {
         const double *dp = det_pct, *np_ = non_pct;
         int64_t *oall = c->arena.get<int64_t>(2);  // {0, *d_nd + *d_nn}: the union's one segment
-        map_n(c, cap > 0 ? cap : 1, nullptr, [=] __device__(int64_t i) {
+        map_n(c, 1, nullptr, [=] __device__(int64_t) {
             const int64_t nd = *d_nd, nn = *d_nn;
-            if (i == 0) {
-                oall[0] = 0;
-                oall[1] = nd + nn;
-                oseg[0] = 0;
-                oseg[1] = nd;
-                oseg[2] = nd + nn;
-            }
-            if (i < nd) v[i] = dp[i];
-            else if (i < nd + nn) v[i] = np_[i - nd];
+            oall[0] = 0;
+            oall[1] = nd + nn;
+            oseg[0] = 0;
+            oseg[1] = nd;
+            oseg[2] = nd + nn;
         });
         const int64_t *d_all = oall + 1;
-        Segs one{1, oall, cap};
-        int32_t *sid = segment_ids(c, one);
-        ChunkedSegs cs = chunked(c, one);
-        SortedSegs ss = seg_sort_f64(c, v, one, sid);
-        // brunnermunzel(det, non) (:349): ranks of the sorted union (det | non: position < nd is det)
+        // (every per-element pass over the union runs over its live length *d_all, not the
+        // capacity NI + NC: config 3's union is empty, config 2's ~80 % of it)
+        int32_t *sid = c->arena.get<int32_t>(cap);
         uint8_t *g = c->arena.get<uint8_t>(cap);
         const int64_t *d_det0 = d_nd;
-        map_n(c, cap, nullptr, [=] __device__(int64_t i) { g[i] = i < *d_det0 ? 0 : 1; });
+        map_n(c, cap, d_all, [=] __device__(int64_t i) {
+            const int64_t nd = *d_det0;
+            v[i] = i < nd ? dp[i] : np_[i - nd];
+            sid[i] = 0;
+            g[i] = i < nd ? 0 : 1;  // brunnermunzel(det, non) (:349): position < nd is det
+        });
+        Segs one{1, oall, cap};
+        ChunkedSegs cs = chunked(c, one);
+        SortedSegs ss = seg_sort_f64(c, v, one, sid);
         RankTestOut rt;
         rt.bm_stat = tests + FZ_RQ3_BM_STAT;
         rt.bm_p = tests + FZ_RQ3_BM_P;
@@ -302,8 +320,8 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
         int64_t *isdet = c->arena.get<int64_t>(cap), *before = c->arena.get<int64_t>(cap);
         const int32_t *pos = ss.pos;
         const double *sv = ss.val;
-        map_n(c, cap, nullptr, [=] __device__(int64_t i) { isdet[i] = (i < *d_all && pos[i] < *d_nd) ? 1 : 0; });
-        scan_exclusive_i64(c, isdet, before, cap, nullptr);
+        map_n(c, cap, d_all, [=] __device__(int64_t i) { isdet[i] = pos[i] < *d_nd ? 1 : 0; });
+        scan_exclusive_i64_dn(c, isdet, before, cap, d_all, nullptr);
         const int64_t *d_det = d_nd;
         map_n(c, cap, d_all, [=] __device__(int64_t i) {
             const uint64_t k = f64_key(sv[i]);

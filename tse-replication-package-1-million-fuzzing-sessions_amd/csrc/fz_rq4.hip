@@ -369,17 +369,24 @@ void rq4b_session_stats(fz_ctx *c, const double *values, const int64_t *sid, con
     const int64_t MM = S > 0 ? S : 1;
     uint64_t *key = c->arena.get<uint64_t>(n);
     uint32_t *idx = c->arena.get<uint32_t>(n);
+    const double *svals = values;  // the values ride along as the sort's payload (no gather after)
     if (n > 0) {
         k_rq4b_keys<<<grid_for(n), kBlock, 0, st>>>(sid, grp, n, key, idx);
         FZ_LAUNCH_CHECK();
-        radix_sort_pairs_swap(c, key, idx, n, bits_for(uint64_t(2 * MM)));
+        RadixPayload pl;
+        pl.n = 1;
+        pl.in[0] = values;
+        pl.size[0] = 8;
+        uint32_t *no_vals = nullptr;
+        radix_sort_pairs_payload(c, key, no_vals, n, bits_for(uint64_t(2 * MM)), pl);
+        svals = static_cast<const double *>(pl.out[0]);
     }
     double *v2 = c->arena.get<double>(n);
     uint32_t *sid2 = c->arena.get<uint32_t>(n);
     int64_t *d_n = c->arena.get<int64_t>(1);
     set_i64(c, d_n, &n, 1);
     map_n(c, n, nullptr, [=] __device__(int64_t k) {
-        v2[k] = values[idx[k]];
+        v2[k] = svals[k];
         sid2[k] = uint32_t(key[k]);
     });
     // max_len bounds one group of a session: a whole session holds up to twice that
@@ -430,26 +437,34 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
     if (!sharded) {
         // (session, group) key per value: G2 -> group 0 (x), G1 -> group 1 (y); the values are in
         // project order, so the stable sort on (session, group) alone keeps projects in order
+        // the values (read in view order: rising rows) ride along as the sort's payload - no random
+        // double gather through the permutation afterwards
         const int64_t S2 = 2 * MM;
         const int sbits = bits_for(uint64_t(S2 + 1));
         uint64_t *key = c->arena.get<uint64_t>(NC);
-        uint32_t *idx = c->arena.get<uint32_t>(NC);
+        double *fv = c->arena.get<double>(NC);
         map_n(c, NC, nullptr, [=] __device__(int64_t j) {
             if (j < *d_nf) {
                 const uint32_t p = fproj[j];
                 const uint64_t grp = (member[p] & 2) ? 0u : 1u;
                 key[j] = uint64_t(j - foffs[p]) * 2u + grp;
+                fv[j] = cov[frow[j]];
             } else {
                 key[j] = uint64_t(S2);
             }
-            idx[j] = uint32_t(j);
         });
-        radix_sort_pairs_swap(c, key, idx, NC, sbits);
+        RadixPayload pl;
+        pl.n = 1;
+        pl.in[0] = fv;
+        pl.size[0] = 8;
+        uint32_t *no_vals = nullptr;
+        radix_sort_pairs_payload(c, key, no_vals, NC, sbits, pl);
+        const double *sfv = static_cast<const double *>(pl.out[0]);
         double *v2 = c->arena.get<double>(NC);
         uint32_t *sid2 = c->arena.get<uint32_t>(NC);
         map_n(c, NC, nullptr, [=] __device__(int64_t k) {
             sid2[k] = uint32_t(key[k]);
-            if (k < *d_nf) v2[k] = cov[frow[idx[k]]];
+            if (k < *d_nf) v2[k] = sfv[k];
         });
         rq4b_sessions(c, v2, sid2, NC, d_nf, MM, P, P, c2, c1, g2q, g1q, o->p_bm);  // <= 1 value per project
     }

@@ -249,7 +249,9 @@ void seg_reduce(fz_ctx *c, const ChunkedSegs &cs, F f, double *out) {
     }
     const int64_t blocks = cs.cps > 0 ? S * cs.cps : cs.cm.cap;
     double *part = c->arena.get<double>(blocks * NV * 2);
-    const unsigned g = unsigned(L.on ? (blocks < 8192 ? blocks : 8192) : blocks);
+    // a persistent grid over the chunks (a capacity-sized implicit map of a short live segment -
+    // RQ3's union at config 3 - is mostly empty chunks, each a few loads)
+    const unsigned g = unsigned(blocks < 8192 ? blocks : 8192);
     k_chunk_reduce<NV, F><<<g, kBlock, 0, c->stream>>>(cs.cm, cs.sg.offs, cs.cps, blocks, f, part, nullptr);
     FZ_LAUNCH_CHECK();
     seg_fold_parts<NV>(c, cs, part, out);

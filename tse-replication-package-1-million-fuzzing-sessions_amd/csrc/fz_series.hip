@@ -629,25 +629,20 @@ TieRanks seg_tie_ranks(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, c
     int64_t *flag = c->arena.get<int64_t>(n);
     int64_t *gid = c->arena.get<int64_t>(n);
     int64_t *gstart = c->arena.get<int64_t>(n + 1);
-    map_n(c, n, nullptr, [=] __device__(int64_t i) {
-        const int64_t live = offs[S];
-        if (i >= live) {
-            flag[i] = 0;
-            return;
-        }
+    // (every pass over the live elements offs[S] only: the arrays past them are never read)
+    const int64_t *d_live = offs + S;
+    map_n(c, n, d_live, [=] __device__(int64_t i) {
         const int64_t s = segid[i];
         flag[i] = (i == offs[s] || sorted[i] != sorted[i - 1]) ? 1 : 0;
     });
     int64_t *d_g = c->arena.get<int64_t>(1);
-    scan_exclusive_i64(c, flag, gid, n, d_g);
-    map_n(c, n, nullptr, [=] __device__(int64_t i) {
+    scan_exclusive_i64_dn(c, flag, gid, n, d_live, d_g);
+    map_n(c, n, d_live, [=] __device__(int64_t i) {
         if (flag[i]) gstart[gid[i]] = i;
-        if (i == 0) gstart[*d_g] = offs[S];
+        if (i == offs[S] - 1) gstart[*d_g] = offs[S];  // the sentinel, by the last live element
     });
     double *rank = tr.rank;
-    map_n(c, n, nullptr, [=] __device__(int64_t i) {
-        const int64_t live = offs[S];
-        if (i >= live) return;
+    map_n(c, n, d_live, [=] __device__(int64_t i) {
         const int64_t g = gid[i] + (flag[i] ? 0 : -1);  // exclusive scan: group index of element i
         const int64_t s = segid[i];
         const int64_t a = gstart[g], b = gstart[g + 1];
@@ -681,13 +676,12 @@ void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, 
     int64_t *isx = c->arena.get<int64_t>(n);
     int64_t *cx = c->arena.get<int64_t>(n + 1);
     const int32_t *pos = ss.pos;
-    map_n(c, n, nullptr, [=] __device__(int64_t i) { isx[i] = (i < offs[S] && grp[pos[i]] == 0) ? 1 : 0; });
-    scan_exclusive_i64(c, isx, cx, n, cx + n);
+    map_n(c, n, offs + S, [=] __device__(int64_t i) { isx[i] = grp[pos[i]] == 0 ? 1 : 0; });
+    scan_exclusive_i64_dn(c, isx, cx, n, offs + S, cx + n);  // (cx[live] = the total too)
     // within-sample average rank of every element
     double *rw = c->arena.get<double>(n);
     const int64_t *flag = tr.flag, *gid = tr.gid, *gstart = tr.gstart;
-    map_n(c, n, nullptr, [=] __device__(int64_t i) {
-        if (i >= offs[S]) return;
+    map_n(c, n, offs + S, [=] __device__(int64_t i) {
         const int64_t s = segid[i], s0 = offs[s];
         const int64_t g = gid[i] - 1 + flag[i];
         const int64_t a = gstart[g], b = gstart[g + 1];
@@ -1324,7 +1318,8 @@ void spearman_index_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segi
     {
         // algorithmic bytes per live value: value 8 + position 4 read
         ProbeScope ps(c, "seg_spearman", 8.0 * kSpNV * double(S), offs + S, 12.0);
-        k_spearman_chunks<<<unsigned(blocks), kBlock, 0, c->stream>>>(cs.cm, offs, cs.cps, blocks, ss.val, ss.pos, part);
+        k_spearman_chunks<<<unsigned(blocks < 8192 ? blocks : 8192), kBlock, 0, c->stream>>>(cs.cm, offs, cs.cps, blocks,
+                                                                                             ss.val, ss.pos, part);
         FZ_LAUNCH_CHECK();
         double *sums = c->arena.get<double>(S * kSpNV);
         seg_fold_parts<kSpNV>(c, cs, part, sums);

@@ -43,18 +43,27 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
                                                            const int64_t *__restrict__ d_live, Pred pred, Lookback lb,
                                                            int64_t ntiles, int32_t *__restrict__ orow,
                                                            int64_t *__restrict__ otime, uint32_t *__restrict__ oproj,
-                                                           int64_t *__restrict__ d_n) {
+                                                           int64_t *__restrict__ d_n,
+                                                           const int64_t *__restrict__ sel_prefix) {
     __shared__ int32_t s_pos[kFcTile];
     __shared__ int32_t s_tmp[4];
     __shared__ int64_t s_prefix;
     __shared__ unsigned int s_tile;
+    __shared__ int s_skip;
     const int tid = threadIdx.x;
-    if (tid == 0) s_tile = lb_take_tile(lb.ticket, gridDim.x);
+    const int64_t live = d_live ? *d_live : n;
+    int64_t lim = live < n ? live : n;
+    if (tid == 0) {
+        s_tile = lb_take_tile(lb.ticket, gridDim.x);
+        // (sel_prefix: exclusive prefix count of the selected projects - a tile of the
+        // project-ordered view whose project range holds none keeps nothing: no column is read)
+        const int64_t b0 = int64_t(s_tile) * kFcTile, b1 = b0 + kFcTile < lim ? b0 + kFcTile : lim;
+        s_skip = sel_prefix && (b0 >= b1 || sel_prefix[proj[b1 - 1] + 1] == sel_prefix[proj[b0]]);
+    }
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t base = tile * kFcTile;
-    const int64_t live = d_live ? *d_live : n;
-    const int64_t lim = live < n ? live : n;
+    if (s_skip) lim = 0;
     // all row loads first, then all predicate gathers: independent loads in flight together
     // instead of one dependent load chain per item
     int32_t r[kFcItems];
@@ -115,9 +124,11 @@ struct PredBytes<P, std::void_t<decltype(P::kBytes)>> {
 
 // Rows of src (n rows, in view order; only the first *src_live when given) satisfying pred(row)
 // -> dst (same order).
+// sel_prefix (optional, [P + 1]): exclusive prefix count of the projects pred can keep - tiles of
+// the (project-ordered) view covering none of them are skipped without reading their columns.
 template <typename Pred>
 void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uint32_t *proj, int64_t n, int64_t P,
-                 Pred pred, TmpView &dst, const int64_t *src_live = nullptr) {
+                 Pred pred, TmpView &dst, const int64_t *src_live = nullptr, const int64_t *sel_prefix = nullptr) {
     dst.cap = n;
     dst.d_n = c->arena.get<int64_t>(1);
     dst.row = c->arena.get<int32_t>(n);
@@ -129,10 +140,12 @@ void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uin
         const Lookback lb = lookback_begin(c, ntiles);
         // per input row: its row id 4 B + the predicate's columns; per kept row: time 8 + project 4
         // read, (row, time, project) 16 written
-        ProbeScope ps(c, "filter_compact", double(n) * (4.0 + PredBytes<Pred>::value), dst.d_n, 28.0);
+        // (a selective filter reads only the tiles of its projects: probed apart, kept rows' bytes)
+        ProbeScope ps(c, sel_prefix ? "filter_select" : "filter_compact",
+                      sel_prefix ? 0.0 : double(n) * (4.0 + PredBytes<Pred>::value), dst.d_n, 28.0);
         k_filter_compact<Pred><<<unsigned(ntiles), kBlock, 0, c->stream>>>(rows, times, proj, n, src_live, pred, lb,
                                                                           ntiles, dst.row, dst.time, dst.proj,
-                                                                          dst.d_n);
+                                                                          dst.d_n, sel_prefix);
         FZ_LAUNCH_CHECK();
         lookback_end(c, ntiles);
     } else {

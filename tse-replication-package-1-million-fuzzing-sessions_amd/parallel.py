@@ -103,6 +103,32 @@ def take_shard(t: Tables, lo: int, hi: int) -> Tuple[Tables, ShardRows]:
 
 
 # ---------------------------------------------------------------------------------- collectives
+import threading  # noqa: E402
+
+_local = threading.local()
+
+
+class use_group:
+    """``with use_group(g):`` - this thread's collectives go to process group g (the sharded bench
+    step runs each analysis' driver in its own thread, over its own group of all ranks: collectives
+    of different drivers never interleave on one communicator)."""
+
+    def __init__(self, group):
+        self.group = group
+
+    def __enter__(self):
+        self.prev = getattr(_local, "group", None)
+        _local.group = self.group
+        return self
+
+    def __exit__(self, *exc):
+        _local.group = self.prev
+
+
+def _group():
+    return getattr(_local, "group", None)
+
+
 def _dist():
     import torch.distributed as dist
     return dist
@@ -120,10 +146,10 @@ def all_reduce(x, op=None):
     op = dist.ReduceOp.SUM if op is None else op
     if _staged(x):
         h = x.cpu()
-        dist.all_reduce(h, op=op)
+        dist.all_reduce(h, op=op, group=_group())
         x.copy_(h)
     else:
-        dist.all_reduce(x, op=op)
+        dist.all_reduce(x, op=op, group=_group())
 
 
 def all_gather(x):
@@ -134,10 +160,10 @@ def all_gather(x):
     if _staged(x):
         h = x.cpu()
         outs = [torch.empty_like(h) for _ in range(world)]
-        dist.all_gather(outs, h)
+        dist.all_gather(outs, h, group=_group())
         return [o.to(x.device) for o in outs]
     outs = [torch.empty_like(x) for _ in range(world)]
-    dist.all_gather(outs, x)
+    dist.all_gather(outs, x, group=_group())
     return outs
 
 
@@ -165,10 +191,10 @@ def all_to_all_v(x, send_counts):
     if _staged(x):
         h = x.cpu()
         out = torch.empty(sum(recv), dtype=x.dtype)
-        dist.all_to_all_single(out, h, recv, send)
+        dist.all_to_all_single(out, h, recv, send, group=_group())
         return out.to(x.device)
     out = torch.empty(sum(recv), dtype=x.dtype, device=x.device)
-    dist.all_to_all_single(out, x.contiguous(), recv, send)
+    dist.all_to_all_single(out, x.contiguous(), recv, send, group=_group())
     return out
 
 
