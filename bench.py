@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--no-graphs", action="store_true")
     # stream groups, e.g. "rq3|rq4b|rq2_count|rq1,rq4a,rq2_add" (the last on the engine's stream)
     ap.add_argument("--groups", default="|".join(",".join(g) for g in GROUPS))
+    # the sharded step's host threads (one child engine + process group each), same syntax
+    ap.add_argument("--shard-groups", default="|".join(",".join(g) for g in GROUPS))
     return ap.parse_args()
 
 
@@ -139,13 +141,18 @@ def main():
         # thread, on its own child engine (stream + context over the store) and its own process
         # group of all ranks - their host round trips and collectives overlap instead of queueing
         # behind each other (--serial: one after another on the engine, the default group)
-        snames = [n for n in ("rq3", "rq4b", "rq2_count", "rq1", "rq4a", "rq2_add") if n in stages]
+        sthreads = [[n for n in g.split(",") if n in stages] for g in args.shard_groups.split("|")]
+        sthreads = [g for g in sthreads if g]
+        snames = [n for g in sthreads for n in g]
         if args.serial:
             skids = {n: eng for n in snames}
             sgroups = {n: None for n in snames}
         else:
-            skids = {n: eng.child() for n in snames}
-            sgroups = {n: dist.new_group(backend=args.dist_backend) for n in snames}
+            skids, sgroups = {}, {}
+            for g in sthreads:
+                ch, pg = eng.child(), dist.new_group(backend=args.dist_backend)
+                for n in g:
+                    skids[n], sgroups[n] = ch, pg
         rq1_shard = par.GpuRQ1Shard(skids.get("rq1", eng), M)
         rq3_shard = par.GpuRQ3Shard(skids.get("rq3", eng))
         rq2c_shard = par.GpuRQ2CountShard(skids.get("rq2_count", eng))
@@ -198,13 +205,14 @@ def main():
             "rq3": lambda e: par.rq3_sharded(rq3_shard, rank, world),
         }
 
-        def run_sharded(name):
-            e = skids[name]
-            with torch.cuda.stream(e.stream), par.use_group(sgroups[name]):
-                shard_step[name](e)
+        def run_sharded(names):
+            for name in names:
+                e = skids[name]
+                with torch.cuda.stream(e.stream), par.use_group(sgroups[name]):
+                    shard_step[name](e)
         if not args.serial:
             from concurrent.futures import ThreadPoolExecutor
-            pool = ThreadPoolExecutor(len(snames))
+            pool = ThreadPoolExecutor(len(sthreads))
     if concurrent:
         from concurrent.futures import ThreadPoolExecutor
         # the last group runs on the engine itself (its stream, after the store build)
@@ -255,13 +263,12 @@ def main():
         eng.join_children()  # the previous step's drivers have read the store
         eng.build_store()
         if pool is None:
-            for n in snames:
-                run_sharded(n)
+            run_sharded(snames)
             return
         for ch in set(skids.values()):
             if ch is not eng:
                 ch.follow_parent()
-        futs = [pool.submit(run_sharded, n) for n in snames]
+        futs = [pool.submit(run_sharded, g) for g in sthreads]
         for f in futs:
             f.result()
 

@@ -245,14 +245,16 @@ __global__ __launch_bounds__(kBlock) void k_scan_lookback(const int64_t *__restr
     __shared__ int64_t s_prefix;
     __shared__ unsigned int s_tile;
     const int tid = threadIdx.x;
-    if (tid == 0) s_tile = lb_take_tile(lb.ticket, gridDim.x);
     const int64_t live = d_live ? (*d_live < n_cap ? *d_live : n_cap) : n_cap;
     const int64_t n = live;
     const int64_t ntiles = live > 0 ? (live + kLbTile - 1) / kLbTile : 1;
     (void)ntiles_cap;
+    // workgroups past the live tiles leave before drawing a ticket (no contention on the counter);
+    // the live ones draw tickets 0 .. ntiles - 1 and the last drawer resets the counter
+    if (int64_t(blockIdx.x) >= ntiles) return;
+    if (tid == 0) s_tile = lb_take_tile(lb.ticket, unsigned(ntiles));
     __syncthreads();
     const int64_t tile = s_tile;
-    if (tile >= ntiles) return;  // past the live elements (every workgroup drew its ticket)
     const int64_t base = tile * kLbTile;
     int64_t x[kLbItems];
 #pragma unroll

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
                                                            int64_t ntiles, int32_t *__restrict__ orow,
                                                            int64_t *__restrict__ otime, uint32_t *__restrict__ oproj,
                                                            int64_t *__restrict__ d_n,
-                                                           const int64_t *__restrict__ sel_prefix) {
+                                                           const int64_t *__restrict__ sel_prefix, int64_t n_sel) {
     __shared__ int32_t s_pos[kFcTile];
     __shared__ int32_t s_tmp[4];
     __shared__ int64_t s_prefix;
@@ -53,8 +53,17 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
     const int tid = threadIdx.x;
     const int64_t live = d_live ? *d_live : n;
     int64_t lim = live < n ? live : n;
+    // tiles over the live rows only: workgroups past them leave before drawing a ticket; nothing
+    // selected at all (sel_prefix total 0: configs 3 / 5 have no issue) - every workgroup leaves and
+    // the first writes the empty count
+    ntiles = lim > 0 ? (lim + kFcTile - 1) / kFcTile : 1;
+    if (sel_prefix && sel_prefix[n_sel] == 0) {
+        if (blockIdx.x == 0 && tid == 0) *d_n = 0;
+        return;
+    }
+    if (int64_t(blockIdx.x) >= ntiles) return;
     if (tid == 0) {
-        s_tile = lb_take_tile(lb.ticket, gridDim.x);
+        s_tile = lb_take_tile(lb.ticket, unsigned(ntiles));
         // (sel_prefix: exclusive prefix count of the selected projects - a tile of the
         // project-ordered view whose project range holds none keeps nothing: no column is read)
         const int64_t b0 = int64_t(s_tile) * kFcTile, b1 = b0 + kFcTile < lim ? b0 + kFcTile : lim;
@@ -145,7 +154,7 @@ void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uin
                       sel_prefix ? 0.0 : double(n) * (4.0 + PredBytes<Pred>::value), dst.d_n, 28.0);
         k_filter_compact<Pred><<<unsigned(ntiles), kBlock, 0, c->stream>>>(rows, times, proj, n, src_live, pred, lb,
                                                                           ntiles, dst.row, dst.time, dst.proj,
-                                                                          dst.d_n, sel_prefix);
+                                                                          dst.d_n, sel_prefix, P);
         FZ_LAUNCH_CHECK();
         lookback_end(c, ntiles);
     } else {
