@@ -82,8 +82,9 @@ def parse():
     ap.add_argument("--no-graphs", action="store_true")
     # stream groups, e.g. "rq3|rq4b|rq2_count|rq1,rq4a,rq2_add" (the last on the engine's stream)
     ap.add_argument("--groups", default="|".join(",".join(g) for g in GROUPS))
-    # the sharded step's host threads (one child engine + process group each), same syntax
-    ap.add_argument("--shard-groups", default="|".join(",".join(g) for g in GROUPS))
+    # the sharded step's host threads (one child engine + process group each), same syntax; two
+    # threads measured best (same-box A/B, scripts/gpu_shard_ab.sh: the drivers are host-bound)
+    ap.add_argument("--shard-groups", default="rq3,rq4b|rq2_count,rq1,rq4a,rq2_add")
     return ap.parse_args()
 
 

@@ -290,9 +290,15 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
     constexpr bool KEYS_LDS = MAXN <= 4096;
     constexpr bool FUSE = MAXN > 4096;  // this class gathers its segments' columns itself
     static_assert(MAXN <= (1 << kBlkPosBits) && MAXN % BS == 0, "bucket sort shape");
-    // bucket counts, then bucket starts (+ sentinel); after the ranking: u64 staging of the gather
-    __shared__ alignas(8) uint32_t s_cnt[EPT * BS + 1];
-    __shared__ uint16_t s_pos[MAXN];          // rows in bucket order
+    // 16-bit bucket counts, then bucket starts (+ sentinel; every count and start is <= MAXN <=
+    // 16384), the rows in bucket order; after the ranking the same bytes are the u64 staging of the
+    // fused gather.  (16-bit counters: the 16384-row class fits two workgroups per CU - 67 KiB of LDS
+    // instead of 102 KiB with 32-bit ones.)
+    constexpr int CNT_BYTES = ((EPT * BS + 1) * 2 + 15) / 16 * 16;
+    __shared__ alignas(16) uint8_t s_mem[CNT_BYTES + MAXN * 2];
+    uint16_t *const s_cnt = reinterpret_cast<uint16_t *>(s_mem);
+    uint32_t *const s_cnt32 = reinterpret_cast<uint32_t *>(s_mem);  // word q / 2 holds counters q, q ^ 1
+    uint16_t *const s_pos = reinterpret_cast<uint16_t *>(s_mem + CNT_BYTES);  // rows in bucket order
     __shared__ uint64_t s_key[KEYS_LDS ? MAXN : 1];
     __shared__ int64_t s_lo[NW], s_hi[NW];
     __shared__ uint32_t s_tmp[NW], s_max[NW];
@@ -340,7 +346,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
             s_lo[w] = lo;
             s_hi[w] = hi;
         }
-        for (int j = tid; j < EPT * BS + 1; j += BS) s_cnt[j] = 0u;
+        for (int j = tid; j < CNT_BYTES / 4; j += BS) s_cnt32[j] = 0u;
         __syncthreads();
         lo = INT64_MAX;
         hi = INT64_MIN;
@@ -368,7 +374,8 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
             q = q < uint32_t(n) || null ? q : uint32_t(n - 1);
             bs[m] = q << 16;
             if (i < n) {
-                bs[m] |= atomicAdd(&s_cnt[q], 1u);
+                const uint32_t sh = (q & 1u) * 16u;
+                bs[m] |= (atomicAdd(&s_cnt32[q >> 1], 1u << sh) >> sh) & 0xffffu;
                 if (KEYS_LDS) s_key[i] = row_key(t[m], i);
             }
         }
@@ -387,10 +394,10 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {  // (block_excl_scan's barriers ordered every read above)
             const uint32_t ce = s_cnt[tid * EPT + e];
-            s_cnt[tid * EPT + e] = run;
+            s_cnt[tid * EPT + e] = uint16_t(run);
             run += ce;
         }
-        if (tid == 0) s_cnt[EPT * BS] = uint32_t(n);
+        if (tid == 0) s_cnt[EPT * BS] = uint16_t(n);
         __syncthreads();
         uint32_t gmax = 0;
 #pragma unroll
@@ -453,8 +460,9 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         // Staging: the key array (8-byte slots for the whole segment) or the bucket counts (half a
         // segment per round).  (A separate gather would re-read the 250 KB segment at random from
         // HBM; the short classes' segments stay in L2 and gather faster than they stage.)
-        uint64_t *stg = KEYS_LDS ? s_key : reinterpret_cast<uint64_t *>(s_cnt);
+        uint64_t *stg = KEYS_LDS ? s_key : reinterpret_cast<uint64_t *>(s_mem);
         constexpr int CAP = KEYS_LDS ? MAXN : MAXN / 2;
+        static_assert(KEYS_LDS || (CNT_BYTES + MAXN * 2) / 8 >= CAP, "gather staging");
         // stage one column (x[m]: row i's value) through LDS in sorted order, write it coalesced
         auto emit = [&](const uint64_t *x, auto store) {
             for (int h = 0; h < n; h += CAP) {
@@ -467,11 +475,15 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
                 __syncthreads();
             }
         };
-        // the columns: the prefix-sorted caller row ids (-> perm), then the gathered ones; column
-        // j + 1's loads are issued before column j is staged (their latency hides behind it)
-        const int nc = 1 + gc.n;
-        auto src_of = [&](int j) { return j == 0 ? static_cast<const void *>(tb.rows) : gc.src[j - 1]; };
-        auto size_of = [&](int j) { return j == 0 ? 4 : gc.size[j - 1]; };
+        // the columns: the time (re-read from the segment's cache-resident prefix-sorted times - the
+        // registers holding t[] are free again), the prefix-sorted caller row ids (-> perm), then the
+        // gathered ones; column j + 1's loads are issued before column j is staged (their latency
+        // hides behind it)
+        const int nc = 2 + gc.n;
+        auto src_of = [&](int j) {
+            return j == 0 ? static_cast<const void *>(time) : (j == 1 ? static_cast<const void *>(tb.rows) : gc.src[j - 2]);
+        };
+        auto size_of = [&](int j) { return j == 0 ? 8 : (j == 1 ? 4 : gc.size[j - 2]); };
         auto load = [&](int j, uint64_t *x) {
             const void *src = src_of(j);
             const int sz = size_of(j);
@@ -494,19 +506,13 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
             out.spos[ob + q] = kGathered;
             tb.orow[ob + q] = int32_t(ob + q);
         }
-        {
-            uint64_t tt[IPT];
-#pragma unroll
-            for (int m = 0; m < IPT; ++m) tt[m] = uint64_t(t[m]);
-            emit(tt, [&](int64_t q, uint64_t v) { out.otime[q] = int64_t(v); });
-        }
         for (int j = 0; j < nc; ++j) {
             if constexpr (kPrefetch) {
                 if (j + 1 < nc) load(j + 1, xb);
             } else if (j > 0) {
                 load(j, xa);
             }
-            void *dst = j == 0 ? static_cast<void *>(gc.perm) : gc.dst[j - 1];
+            void *dst = j == 0 ? static_cast<void *>(out.otime) : (j == 1 ? static_cast<void *>(gc.perm) : gc.dst[j - 2]);
             const int sz = size_of(j);
             emit(xa, [&](int64_t q, uint64_t v) {
                 if (sz == 8) static_cast<uint64_t *>(dst)[q] = v;
