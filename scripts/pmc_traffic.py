@@ -24,7 +24,9 @@ SCOPES = {
     "radix_scatter": {"match": ["k_onesweep<"]},
     "radix_hist": {"match": ["k_onesweep_hist"]},
     "elig_hist": {"match": ["k_elig_hist"]},
-    "filter_compact": {"match": ["k_filter_compact"]},
+    # (the selective filters - tiles of unselected projects skipped - are probed apart)
+    "filter_compact": {"match": ["k_filter_compact"], "exclude": ["CovRowsRq3", "PositiveCoverage34"]},
+    "filter_select": {"match": ["k_filter_compact<fz::CovRowsRq3>", "k_filter_compact<fz::PositiveCoverage34>"]},
     # the four length-class launches of the store's time sort (all three tables), between the prefix
     # offsets and the views launch
     "seg_time_sort": {"open": "k_prefix_offsets", "match": ["k_seg_time_bucket"], "allow": ["k_fill"],
@@ -59,7 +61,10 @@ def scopes(rows, spec):
     opener, closer, pre = spec.get("open"), spec.get("close"), spec.get("pre", [])
     has = lambda k, subs: any(s in k for s in subs)  # noqa: E731
     n, tot, inside, pend = 0, 0.0, False, 0.0
+    excl = spec.get("exclude", [])
     for k, b in rows:
+        if excl and has(k, excl):
+            continue
         if opener is None:  # every matching dispatch is one probed launch
             if has(k, match):
                 n += 1

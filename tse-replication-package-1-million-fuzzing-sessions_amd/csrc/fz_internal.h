@@ -333,6 +333,8 @@ struct RadixPayload {
     }
 };
 void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl);
+// the same for keys of at most 32 bits held as uint32 (4 bytes less per key and pass)
+void radix_sort_pairs_payload32(fz_ctx *c, uint32_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl);
 // min/max over int64 values skipping FZ_TS_NULL: writes {min, max} to host array.
 void minmax_i64_to_host(fz_ctx *c, const int64_t *const *cols, const int64_t *ns, int ncols,
                         int64_t *host_minmax);

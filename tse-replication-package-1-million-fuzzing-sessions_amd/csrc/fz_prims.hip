@@ -405,7 +405,8 @@ constexpr int kHistKeysPerBlock = FZ_HIST_KPB;  // keys per histogram workgroup 
 // 8192 keys per workgroup made the small sorts' loops latency-bound: 6 -> 20 us for 65 k keys)
 constexpr int kOsGroup = 8;  // tiles per look-back group (one {tiles, sum} word per group and digit)
 
-__global__ __launch_bounds__(kBlock) void k_onesweep_hist(const uint64_t *__restrict__ keys, int64_t n, int npass,
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void k_onesweep_hist(const KeyT *__restrict__ keys, int64_t n, int npass,
                                                           unsigned long long *__restrict__ ghist,
                                                           unsigned long long *__restrict__ gsum, int64_t gsum_words) {
     __shared__ uint32_t s_h[kOsMaxPasses][kRadix];
@@ -417,7 +418,7 @@ __global__ __launch_bounds__(kBlock) void k_onesweep_hist(const uint64_t *__rest
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i - threadIdx.x < n;
          i += int64_t(gridDim.x) * kBlock) {
         const bool valid = i < n;
-        const uint64_t k = valid ? keys[i] : 0ull;
+        const uint64_t k = valid ? uint64_t(keys[i]) : 0ull;
         for (int p = 0; p < npass; ++p) {
             const uint32_t d = uint32_t(k >> (p * kRadixBits)) & (kRadix - 1);
             // wave-uniform digit (typical for the high digits): one add instead of 64 conflicting
@@ -483,17 +484,20 @@ __device__ inline void onesweep_move(const T *__restrict__ in, T *__restrict__ o
     }
 }
 
-template <bool HAS_VALS, bool HAS_PL>
-__global__ __launch_bounds__(kOsBlock) void k_onesweep(const uint64_t *__restrict__ keys_in,
+// KeyT: uint64_t, or uint32_t for keys of at most 32 bits (the prefix / session-index transposes:
+// 4 bytes per key less to read and write in every pass)
+template <typename KeyT, bool HAS_VALS, bool HAS_PL>
+__global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ keys_in,
                                                      const uint32_t *__restrict__ vals_in,
-                                                     uint64_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
+                                                     KeyT *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
                                                      int64_t n, int shift, const unsigned long long *__restrict__ ghist,
                                                      uint64_t *__restrict__ status, unsigned int *__restrict__ ticket,
                                                      uint64_t epoch,
                                                      unsigned long long *__restrict__ gsum,
                                                      unsigned long long *__restrict__ next_hist,
                                                      RadixPayload pl) {
-    __shared__ uint64_t s_keys[kSortTile];
+    __shared__ uint64_t s_stage[kSortTile];  // the keys, then 8-byte payload columns
+    KeyT *const s_keys = reinterpret_cast<KeyT *>(s_stage);
     __shared__ uint32_t s_vals[HAS_VALS ? kSortTile : 1];
     __shared__ uint32_t s_run[kRadix];
     __shared__ uint32_t s_wcnt[kOsWaves][kRadix];
@@ -523,14 +527,14 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const uint64_t *__restric
     // wave-private digit counters - no workgroup barrier inside the ranking loop
     const int64_t wbase = base + int64_t(w) * (kSortTile / kOsWaves);
 
-    uint64_t k[kSortItems];
+    KeyT k[kSortItems];
     uint32_t v[kSortItems];
     uint32_t rank[kSortItems];
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
         const int64_t idx = wbase + r * kWave + lane;
         const bool valid = idx < n;
-        k[r] = valid ? keys_in[idx] : 0ull;
+        k[r] = valid ? keys_in[idx] : KeyT(0);
         v[r] = (HAS_VALS && valid) ? vals_in[idx] : 0u;
     }
     uint32_t *cnt_w = s_wcnt[w];
@@ -650,7 +654,7 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const uint64_t *__restric
     for (int m = 0; m < kSortItems; ++m) {
         const int i = tid + m * kOsBlock;
         if (i < valid_n) {
-            const uint64_t kk = s_keys[i];
+            const KeyT kk = s_keys[i];
             const uint32_t d = uint32_t(kk >> shift) & (kRadix - 1);
             const int64_t gpos = s_goff[d] + i;
 #ifdef FZ_OS_EXPERIMENT_NOWRITE
@@ -668,13 +672,13 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const uint64_t *__restric
         for (int j = 0; j < pl.n; ++j) {
             if (pl.size[j] == 8)
                 onesweep_move<uint64_t>(static_cast<const uint64_t *>(pl.in[j]), static_cast<uint64_t *>(pl.out[j]),
-                                        s_keys, lpos, gp, wbase, lane, n, valid_n, tid);
+                                        s_stage, lpos, gp, wbase, lane, n, valid_n, tid);
             else if (pl.size[j] == 4)
                 onesweep_move<uint32_t>(static_cast<const uint32_t *>(pl.in[j]), static_cast<uint32_t *>(pl.out[j]),
-                                        reinterpret_cast<uint32_t *>(s_keys), lpos, gp, wbase, lane, n, valid_n, tid);
+                                        reinterpret_cast<uint32_t *>(s_stage), lpos, gp, wbase, lane, n, valid_n, tid);
             else
                 onesweep_move<uint8_t>(static_cast<const uint8_t *>(pl.in[j]), static_cast<uint8_t *>(pl.out[j]),
-                                       reinterpret_cast<uint8_t *>(s_keys), lpos, gp, wbase, lane, n, valid_n, tid);
+                                       reinterpret_cast<uint8_t *>(s_stage), lpos, gp, wbase, lane, n, valid_n, tid);
         }
     }
 #ifdef FZ_OS_TIMING
@@ -698,7 +702,8 @@ void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t 
     radix_sort_pairs_payload(c, keys, vals, n, bits, none);
 }
 
-void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl) {
+template <typename KeyT>
+static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl) {
     if (n <= 1 || bits <= 0) {  // nothing to sort (one key, or a 0-bit key: one project): unmoved
         for (int j = 0; j < pl.n; ++j) pl.out[j] = const_cast<void *>(pl.in[j]);
         return;
@@ -723,8 +728,8 @@ void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64
     unsigned long long *gsum = c->arena.get<unsigned long long>(gwords * npass);
     {
         ProbeScope ps(c, "radix_hist", 8.0 * double(n));
-        k_onesweep_hist<<<grid_for(n, kHistKeysPerBlock, 2048), kBlock, 0, c->stream>>>(keys, n, npass, ghist, gsum,
-                                                                                       gwords * npass);
+        k_onesweep_hist<KeyT><<<grid_for(n, kHistKeysPerBlock, 2048), kBlock, 0, c->stream>>>(keys, n, npass, ghist,
+                                                                                             gsum, gwords * npass);
         FZ_LAUNCH_CHECK();
     }
     // Constant-digit passes are identity permutations.  Finding them needs a host round trip, which
@@ -746,9 +751,9 @@ void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64
             need[p] = nz > 1;
         }
     }
-    uint64_t *k2 = c->arena.get<uint64_t>(n);
+    KeyT *k2 = c->arena.get<KeyT>(n);
     uint32_t *v2 = vals ? c->arena.get<uint32_t>(n) : nullptr;
-    uint64_t *ka = keys, *kb = k2;
+    KeyT *ka = keys, *kb = k2;
     uint32_t *va = vals, *vb = v2;
     FZ_CHECK(pl.n == 0 || n < (int64_t(1) << 31), "radix_sort_pairs_payload: payload sorts are limited to 2^31 keys");
     void *pbuf[2][kMaxPayload] = {};
@@ -766,9 +771,9 @@ void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64
         }
         {
             // algorithmic traffic of one pass: read + write every key (8 B), value (4 B) and payload
-            ProbeScope ps(c, "radix_scatter", ((vals ? 24.0 : 16.0) + 2.0 * pl.bytes()) * double(n));
+            ProbeScope ps(c, "radix_scatter", (2.0 * sizeof(KeyT) + (vals ? 8.0 : 0.0) + 2.0 * pl.bytes()) * double(n));
 #define FZ_OS_LAUNCH(V, PL)                                                                                   \
-    k_onesweep<V, PL><<<unsigned(nb), kOsBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, \
+    k_onesweep<KeyT, V, PL><<<unsigned(nb), kOsBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, \
                                                              lb.status, lb.ticket, lb.epoch, gsum + p * gwords, \
                                                              next_hist, step)
             if (pl.n > 0) {
@@ -797,6 +802,14 @@ void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64
     c->sort_passes += passes;
     // the passes zeroed the other buffer: it serves the next sort; with no pass nothing was zeroed
     c->os_hist_cur = passes > 0 ? 1 - c->os_hist_cur : -1;
+}
+
+void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl) {
+    radix_payload_impl<uint64_t>(c, keys, vals, n, bits, pl);
+}
+void radix_sort_pairs_payload32(fz_ctx *c, uint32_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl) {
+    FZ_CHECK(bits <= 32, "radix_sort_pairs_payload32: keys of more than 32 bits");
+    radix_payload_impl<uint32_t>(c, keys, vals, n, bits, pl);
 }
 
 // ------------------------------------------------------------------------------- min / max

@@ -70,31 +70,28 @@ void spearman_index_seg(fz_ctx *c, const double *x, int64_t n, const int64_t *of
     spearman_index_sorted(c, cs, id, ss, rho, p);
 }
 
-__global__ void k_session_keys(const int64_t *__restrict__ sid, int64_t n, uint64_t *__restrict__ keys,
-                               uint32_t *__restrict__ idx) {
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
-        keys[i] = uint64_t(sid[i]);
-        idx[i] = uint32_t(i);
-    }
+__global__ void k_session_keys(const int64_t *__restrict__ sid, int64_t n, uint32_t *__restrict__ keys) {
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+        keys[i] = uint32_t(sid[i]);
 }
 
 void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_ids, int64_t n, int64_t S,
                        int64_t max_len, double *average, double *median, double *pcts, int64_t *n_ge100) {
     hipStream_t st = c->stream;
     dev_fill(c, n_ge100, 0, 8);
-    uint64_t *key = c->arena.get<uint64_t>(n);
-    uint32_t *idx = c->arena.get<uint32_t>(n);
+    FZ_CHECK(S < (int64_t(1) << 32), "fz_rq2_session_stats: too many sessions");
+    uint32_t *key = c->arena.get<uint32_t>(n);
     const double *svals = values;  // the values ride along as the sort's payload (no gather after)
     if (n > 0) {
-        k_session_keys<<<grid_for(n), kBlock, 0, st>>>(session_ids, n, key, idx);
+        k_session_keys<<<grid_for(n), kBlock, 0, st>>>(session_ids, n, key);
         FZ_LAUNCH_CHECK();
         RadixPayload pl;
         pl.n = 1;
         pl.in[0] = values;
         pl.size[0] = 8;
         uint32_t *no_vals = nullptr;
-        // stable: input order kept per session
-        radix_sort_pairs_payload(c, key, no_vals, n, bits_for(uint64_t(S)), pl);
+        // stable: input order kept per session (32-bit keys: session index < 2^32)
+        radix_sort_pairs_payload32(c, key, no_vals, n, bits_for(uint64_t(S)), pl);
         svals = static_cast<const double *>(pl.out[0]);
     }
     double *sv = c->arena.get<double>(n);
@@ -174,18 +171,18 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     // (the trend values ride along as the sort's payload, coming out in session order - no random
     // gather through a permutation afterwards)
     const int ibits = bits_for(uint64_t(M));
-    uint64_t *key = c->arena.get<uint64_t>(NC);
+    uint32_t *key = c->arena.get<uint32_t>(NC);  // (an index within a project: < 2^31 rows)
     const uint32_t *tproj = T.proj;
     map_n(c, NC, nullptr, [=] __device__(int64_t j) {
         const int64_t live = *d_nt;
-        key[j] = j < live ? uint64_t(j - toffs[tproj[j]]) : uint64_t(M);  // M: past every real index
+        key[j] = j < live ? uint32_t(j - toffs[tproj[j]]) : uint32_t(M);  // M: past every real index
     });
     RadixPayload pl;
     pl.n = 1;
     pl.in[0] = tv;
     pl.size[0] = 8;
     uint32_t *no_vals = nullptr;
-    radix_sort_pairs_payload(c, key, no_vals, NC, ibits, pl);
+    radix_sort_pairs_payload32(c, key, no_vals, NC, ibits, pl);
     const double *stv = static_cast<const double *>(pl.out[0]);
     double *sv = o->session_values;
     uint32_t *sid = c->arena.get<uint32_t>(NC);

@@ -50,10 +50,9 @@ struct CovRowsRq3 {  // covered_line IS NOT NULL AND DATE(date) < '2025-01-09' (
     const uint8_t *valid;
     const int64_t *date;
     const uint32_t *proj;
-    const int64_t *sel;  // [P + 1] exclusive prefix count of the projects with a fixed issue
+    const uint8_t *sel;  // [P] 1: the project has a fixed issue
     __device__ bool operator()(int32_t r) const {
-        const uint32_t p = proj[r];
-        return sel[p + 1] != sel[p] && (valid[r] & FZ_VALID_COVERED) && date[r] < kLim3b;
+        return sel[proj[r]] && (valid[r] & FZ_VALID_COVERED) && date[r] < kLim3b;
     }
 };
 
@@ -79,15 +78,13 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     filter_view(c, s.covb.row, s.covb.time, s.covb.proj, s.covb.n, P, CovBuildRq3{t.b_time}, CB);
     // the coverage rows of the projects with a fixed issue only: the view's tiles of other projects
     // are skipped unread (config 3 / 5, coverage-only tables: all of them)
-    int64_t *selp = c->arena.get<int64_t>(P + 1);
+    uint8_t *self = c->arena.get<uint8_t>(P);
     {
-        int64_t *self = c->arena.get<int64_t>(P + 1);
         const int64_t *ioff = I.offs;
-        map_n(c, P + 1, nullptr, [=] __device__(int64_t p) { self[p] = p < P && ioff[p + 1] > ioff[p] ? 1 : 0; });
-        scan_exclusive_i64(c, self, selp, P + 1, nullptr);
+        map_n(c, P, nullptr, [=] __device__(int64_t p) { self[p] = ioff[p + 1] > ioff[p] ? 1 : 0; });
     }
-    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P, CovRowsRq3{t.c_valid, t.c_date, t.c_project, selp}, TC,
-                nullptr, selp);
+    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P, CovRowsRq3{t.c_valid, t.c_date, t.c_project, self}, TC,
+                nullptr, Selection{self, 1, I.d_n});
 
     // ---- detected: one thread per issue (:241-302)
     int64_t *dflag = c->arena.get<int64_t>(NI);

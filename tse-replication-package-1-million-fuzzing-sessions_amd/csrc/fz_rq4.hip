@@ -356,29 +356,27 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
 }
 
 __global__ void k_rq4b_keys(const int64_t *__restrict__ sid, const uint8_t *__restrict__ grp, int64_t n,
-                            uint64_t *__restrict__ keys, uint32_t *__restrict__ idx) {
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
-        keys[i] = uint64_t(sid[i]) * 2u + (grp[i] ? 1u : 0u);
-        idx[i] = uint32_t(i);
-    }
+                            uint32_t *__restrict__ keys) {
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+        keys[i] = uint32_t(sid[i]) * 2u + (grp[i] ? 1u : 0u);
 }
 
 void rq4b_session_stats(fz_ctx *c, const double *values, const int64_t *sid, const uint8_t *grp, int64_t n, int64_t S,
                         int64_t max_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q, double *pbm) {
     hipStream_t st = c->stream;
     const int64_t MM = S > 0 ? S : 1;
-    uint64_t *key = c->arena.get<uint64_t>(n);
-    uint32_t *idx = c->arena.get<uint32_t>(n);
+    FZ_CHECK(2 * MM < (int64_t(1) << 32), "fz_rq4b_session_stats: too many sessions");
+    uint32_t *key = c->arena.get<uint32_t>(n);
     const double *svals = values;  // the values ride along as the sort's payload (no gather after)
     if (n > 0) {
-        k_rq4b_keys<<<grid_for(n), kBlock, 0, st>>>(sid, grp, n, key, idx);
+        k_rq4b_keys<<<grid_for(n), kBlock, 0, st>>>(sid, grp, n, key);
         FZ_LAUNCH_CHECK();
         RadixPayload pl;
         pl.n = 1;
         pl.in[0] = values;
         pl.size[0] = 8;
         uint32_t *no_vals = nullptr;
-        radix_sort_pairs_payload(c, key, no_vals, n, bits_for(uint64_t(2 * MM)), pl);
+        radix_sort_pairs_payload32(c, key, no_vals, n, bits_for(uint64_t(2 * MM)), pl);
         svals = static_cast<const double *>(pl.out[0]);
     }
     double *v2 = c->arena.get<double>(n);
@@ -441,16 +439,16 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
         // double gather through the permutation afterwards
         const int64_t S2 = 2 * MM;
         const int sbits = bits_for(uint64_t(S2 + 1));
-        uint64_t *key = c->arena.get<uint64_t>(NC);
+        uint32_t *key = c->arena.get<uint32_t>(NC);  // (2 * index + group < 2^32: < 2^31 rows)
         double *fv = c->arena.get<double>(NC);
         map_n(c, NC, nullptr, [=] __device__(int64_t j) {
             if (j < *d_nf) {
                 const uint32_t p = fproj[j];
-                const uint64_t grp = (member[p] & 2) ? 0u : 1u;
-                key[j] = uint64_t(j - foffs[p]) * 2u + grp;
+                const uint32_t grp = (member[p] & 2) ? 0u : 1u;
+                key[j] = uint32_t(j - foffs[p]) * 2u + grp;
                 fv[j] = cov[frow[j]];
             } else {
-                key[j] = uint64_t(S2);
+                key[j] = uint32_t(S2);
             }
         });
         RadixPayload pl;
@@ -458,7 +456,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
         pl.in[0] = fv;
         pl.size[0] = 8;
         uint32_t *no_vals = nullptr;
-        radix_sort_pairs_payload(c, key, no_vals, NC, sbits, pl);
+        radix_sort_pairs_payload32(c, key, no_vals, NC, sbits, pl);
         const double *sfv = static_cast<const double *>(pl.out[0]);
         double *v2 = c->arena.get<double>(NC);
         uint32_t *sid2 = c->arena.get<uint32_t>(NC);
@@ -505,7 +503,8 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
     {
         TmpView PC;
         filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P,
-                    PositiveCoverage34{t.c_project, t.c_coverage, t.c_valid, member}, PC);
+                    PositiveCoverage34{t.c_project, t.c_coverage, t.c_valid, member}, PC, nullptr,
+                    Selection{member, 12});  // (G3 / G4: tiles of other projects skipped)
         const int64_t NO = g->n_order;
         const int64_t NOC = NO > 0 ? NO : 1;
         int64_t *df = c->arena.get<int64_t>(NOC), *dp = c->arena.get<int64_t>(NOC), *dj = c->arena.get<int64_t>(NOC);

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kSortBlock) void k_store_views(const ViewSrc v, int
 // of the combined index.
 struct PrefixKeys {
     Prefix pre[3];
-    uint64_t *keys[3] = {};
+    uint32_t *keys[3] = {};  // ([type |] project: at most 32 bits)
     uint32_t *vals[3] = {};
     int64_t base[4] = {0, 0, 0, 0};
 };
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kBlock) void k_keys_prefix_rows(const PrefixKeys K)
     for (int64_t gi = int64_t(blockIdx.x) * kBlock + threadIdx.x; gi < K.base[3]; gi += int64_t(gridDim.x) * kBlock) {
         const int k = gi >= K.base[2] ? 2 : (gi >= K.base[1] ? 1 : 0);
         const int64_t i = gi - K.base[k];
-        K.keys[k][i] = K.pre[k](i);
+        K.keys[k][i] = uint32_t(K.pre[k](i));
         K.vals[k][i] = uint32_t(i);
     }
 }
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(kBlock) void k_keys_prefix_rows(const PrefixKeys K)
 // prefixes (keys[i-1], keys[i]]; one coalesced read of the keys instead of a binary search per s.
 // Up to three tables in one launch: table k covers [base[k], base[k + 1]) = max(n, S + 1) items.
 struct PrefixOffs {
-    const uint64_t *keys[3] = {};
+    const uint32_t *keys[3] = {};
     int64_t n[3] = {0, 0, 0};
     int64_t S[3] = {0, 0, 0};
     int64_t *offs[3] = {};
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kBlock) void k_prefix_offsets(const PrefixOffs O) {
     for (int64_t gi = int64_t(blockIdx.x) * kBlock + threadIdx.x; gi < O.base[3]; gi += int64_t(gridDim.x) * kBlock) {
         const int k = gi >= O.base[2] ? 2 : (gi >= O.base[1] ? 1 : 0);
         const int64_t i = gi - O.base[k];
-        const uint64_t *keys = O.keys[k];
+        const uint32_t *keys = O.keys[k];
         const int64_t n = O.n[k], S = O.S[k];
         int64_t *offs = O.offs[k];
         const int64_t first = int64_t(keys[0]), last = int64_t(keys[n - 1]);  // n >= 1, keys < S
@@ -563,7 +563,7 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) 
         const int64_t n = in[k].n > 0 ? in[k].n : 0;
         K.base[k + 1] = K.base[k] + n;
         K.pre[k] = in[k].pre;
-        K.keys[k] = n ? c->arena.get<uint64_t>(n) : nullptr;
+        K.keys[k] = n ? c->arena.get<uint32_t>(n) : nullptr;
         K.vals[k] = n ? c->arena.get<uint32_t>(n) : nullptr;
         pss[k] = PrefixSorted{};
         pss[k].n = n;
@@ -590,7 +590,7 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) 
             pl.in[1 + j] = t.gc.src[j];
             pl.size[1 + j] = t.gc.size[j];
         }
-        radix_sort_pairs_payload(c, K.keys[k], K.vals[k], n, t.prefix_bits, pl);
+        radix_sort_pairs_payload32(c, K.keys[k], K.vals[k], n, t.prefix_bits, pl);
         ps.time = static_cast<const int64_t *>(pl.out[0]);
         ps.gc = t.gc;
         for (int j = 0; j < t.gc.n; ++j) ps.gc.src[j] = pl.out[1 + j];

@@ -36,6 +36,22 @@ void segment_offsets_dn(fz_ctx *c, const uint32_t *sorted_proj, const int64_t *d
 constexpr int kFcItems = 16;
 constexpr int kFcTile = kBlock * kFcItems;
 
+// The projects a filter can keep (k_filter_compact's tile skip): flags[p] & mask != 0; count
+// (optional, device) 0 = none at all.
+struct Selection {
+    const uint8_t *flags = nullptr;
+    uint8_t mask = 0xff;
+    const int64_t *count = nullptr;
+    // none of the projects [p0, p1] selected (checked one by one for a few; a tile spanning more
+    // projects is read)
+    __device__ bool none(uint32_t p0, uint32_t p1) const {
+        if (p1 - p0 > 64u) return false;
+        for (uint32_t p = p0; p <= p1; ++p)
+            if (flags[p] & mask) return false;
+        return true;
+    }
+};
+
 template <typename Pred>
 __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__restrict__ rows,
                                                            const int64_t *__restrict__ times,
@@ -43,8 +59,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
                                                            const int64_t *__restrict__ d_live, Pred pred, Lookback lb,
                                                            int64_t ntiles, int32_t *__restrict__ orow,
                                                            int64_t *__restrict__ otime, uint32_t *__restrict__ oproj,
-                                                           int64_t *__restrict__ d_n,
-                                                           const int64_t *__restrict__ sel_prefix, int64_t n_sel) {
+                                                           int64_t *__restrict__ d_n, Selection sel) {
     __shared__ int32_t s_pos[kFcTile];
     __shared__ int32_t s_tmp[4];
     __shared__ int64_t s_prefix;
@@ -54,20 +69,20 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
     const int64_t live = d_live ? *d_live : n;
     int64_t lim = live < n ? live : n;
     // tiles over the live rows only: workgroups past them leave before drawing a ticket; nothing
-    // selected at all (sel_prefix total 0: configs 3 / 5 have no issue) - every workgroup leaves and
+    // selected at all (*sel.count == 0: configs 3 / 5 have no issue) - every workgroup leaves and
     // the first writes the empty count
     ntiles = lim > 0 ? (lim + kFcTile - 1) / kFcTile : 1;
-    if (sel_prefix && sel_prefix[n_sel] == 0) {
+    if (sel.count && *sel.count == 0) {
         if (blockIdx.x == 0 && tid == 0) *d_n = 0;
         return;
     }
     if (int64_t(blockIdx.x) >= ntiles) return;
     if (tid == 0) {
         s_tile = lb_take_tile(lb.ticket, unsigned(ntiles));
-        // (sel_prefix: exclusive prefix count of the selected projects - a tile of the
-        // project-ordered view whose project range holds none keeps nothing: no column is read)
+        // (a tile of the project-ordered view whose few projects are all unselected keeps nothing:
+        // none of its columns is read)
         const int64_t b0 = int64_t(s_tile) * kFcTile, b1 = b0 + kFcTile < lim ? b0 + kFcTile : lim;
-        s_skip = sel_prefix && (b0 >= b1 || sel_prefix[proj[b1 - 1] + 1] == sel_prefix[proj[b0]]);
+        s_skip = sel.flags && (b0 >= b1 || sel.none(proj[b0], proj[b1 - 1]));
     }
     __syncthreads();
     const int64_t tile = s_tile;
@@ -133,11 +148,11 @@ struct PredBytes<P, std::void_t<decltype(P::kBytes)>> {
 
 // Rows of src (n rows, in view order; only the first *src_live when given) satisfying pred(row)
 // -> dst (same order).
-// sel_prefix (optional, [P + 1]): exclusive prefix count of the projects pred can keep - tiles of
-// the (project-ordered) view covering none of them are skipped without reading their columns.
+// sel (optional): the projects pred can keep - tiles of the (project-ordered) view covering none of
+// them are skipped without reading their columns.
 template <typename Pred>
 void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uint32_t *proj, int64_t n, int64_t P,
-                 Pred pred, TmpView &dst, const int64_t *src_live = nullptr, const int64_t *sel_prefix = nullptr) {
+                 Pred pred, TmpView &dst, const int64_t *src_live = nullptr, Selection sel = Selection{}) {
     dst.cap = n;
     dst.d_n = c->arena.get<int64_t>(1);
     dst.row = c->arena.get<int32_t>(n);
@@ -150,11 +165,11 @@ void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uin
         // per input row: its row id 4 B + the predicate's columns; per kept row: time 8 + project 4
         // read, (row, time, project) 16 written
         // (a selective filter reads only the tiles of its projects: probed apart, kept rows' bytes)
-        ProbeScope ps(c, sel_prefix ? "filter_select" : "filter_compact",
-                      sel_prefix ? 0.0 : double(n) * (4.0 + PredBytes<Pred>::value), dst.d_n, 28.0);
+        ProbeScope ps(c, sel.flags ? "filter_select" : "filter_compact",
+                      sel.flags ? 0.0 : double(n) * (4.0 + PredBytes<Pred>::value), dst.d_n, 28.0);
         k_filter_compact<Pred><<<unsigned(ntiles), kBlock, 0, c->stream>>>(rows, times, proj, n, src_live, pred, lb,
                                                                           ntiles, dst.row, dst.time, dst.proj,
-                                                                          dst.d_n, sel_prefix, P);
+                                                                          dst.d_n, sel);
         FZ_LAUNCH_CHECK();
         lookback_end(c, ntiles);
     } else {
