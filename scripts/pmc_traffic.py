@@ -25,8 +25,9 @@ SCOPES = {
     "radix_hist": {"match": ["k_onesweep_hist"]},
     "elig_hist": {"match": ["k_elig_hist"]},
     # (the selective filters - tiles of unselected projects skipped - are probed apart)
-    "filter_compact": {"match": ["k_filter_compact"], "exclude": ["CovRowsRq3", "PositiveCoverage34"]},
-    "filter_select": {"match": ["k_filter_compact<fz::CovRowsRq3>", "k_filter_compact<fz::PositiveCoverage34>"]},
+    "filter_compact": {"match": ["k_filter_compact"], "exclude": ["CovRowsRq3", "PositiveCoverage34", "CovRowsBeforeLimit"]},
+    "filter_select": {"match": ["k_filter_compact<fz::CovRowsRq3>", "k_filter_compact<fz::PositiveCoverage34>",
+                                "k_filter_compact<fz::CovRowsBeforeLimit>"]},
     # the four length-class launches of the store's time sort (all three tables), between the prefix
     # offsets and the views launch
     "seg_time_sort": {"open": "k_prefix_offsets", "match": ["k_seg_time_bucket"], "allow": ["k_fill"],

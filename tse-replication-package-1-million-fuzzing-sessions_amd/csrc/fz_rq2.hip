@@ -251,7 +251,7 @@ struct CovRowsBeforeLimit {  // GET_COVERAGE_DATA: date < LIMIT, no NULL filter 
     static constexpr int kBytes = 12;  // column bytes read per row (filter_compact probe)
     const uint32_t *proj;
     const int64_t *date;
-    const uint8_t *elig;
+    const uint8_t *elig;  // (RQ2 add: the projects with a selected Coverage build - the only ones read)
     __device__ bool operator()(int32_t r) const { return date[r] < kLimitUs2 && elig[proj[r]]; }
 };
 
@@ -288,8 +288,17 @@ void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
     TmpView B, CV;
     filter_view(c, s.covb.row, s.covb.time, s.covb.proj, s.covb.n, P,
                 CovBuildRows{t.b_project, t.b_result, t.b_time, o->eligible}, B);
-    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, s.cov.n, P, CovRowsBeforeLimit{t.c_project, t.c_date, o->eligible},
-                CV);
+    // the coverage rows are read for projects with a selected Coverage build only (their change
+    // points' date joins and pandas upcast flags): the view's other tiles are skipped, all of them
+    // on a table without builds (configs 3 / 5)
+    uint8_t *withb = c->arena.get<uint8_t>(P);
+    {
+        const uint8_t *el = o->eligible;
+        const int64_t *bo = B.offs;
+        map_n(c, P, nullptr, [=] __device__(int64_t p) { withb[p] = el[p] && bo[p + 1] > bo[p] ? 1 : 0; });
+    }
+    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, s.cov.n, P, CovRowsBeforeLimit{t.c_project, t.c_date, withb},
+                CV, nullptr, Selection{withb, 1, B.d_n});
     const int64_t NB = s.covb.n;
     const int64_t *boffs = B.offs, *coffs = CV.offs;
     // pandas upcast flags: a NULL covered/total among the project's fetched coverage rows
