@@ -34,6 +34,20 @@ struct NonZeroTotal {  // `if x[1] != 0` (:300-303); a NULL total (stored 0) pas
     const uint8_t *valid;
     __device__ bool operator()(int32_t r) const { return total[r] != 0 || !(valid[r] & FZ_VALID_TOTAL); }
 };
+// the trend rows (CovTrendRows, then NonZeroTotal) in one filter pass
+struct TrendRows {
+    static constexpr int kBytes = 30;  // column bytes read per row (filter_compact probe)
+    CovTrendRows v;
+    NonZeroTotal nz;
+    __device__ bool operator()(int32_t r) const { return v(r) && nz(r); }
+};
+// raw_n[p]: the project's CovTrendRows rows (the fetched rows, :291-298), counted in the same pass
+struct CountCovTrend {
+    static constexpr bool on = true;
+    int64_t *out;
+    CovTrendRows v;
+    __device__ bool operator()(int32_t r) const { return v(r); }
+};
 
 // statistics.mean / median + np.percentile(5, 25, 50, 75, 95) of every session segment; sessions
 // with >= 100 values counted into *d_ge100 (which must be zero on entry)
@@ -124,16 +138,17 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     dev_fill(c, o->counts, 0, FZ_RQ2C_NCOUNTS * 8);
 
     eligible_projects(c, o->eligible, o->counts + FZ_RQ2C_ELIGIBLE);
-    TmpView V, T;
-    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P,
-                CovTrendRows{t.c_project, t.c_coverage, t.c_valid, t.c_date, o->eligible}, V);
-    filter_view(c, V.row, V.time, V.proj, NC, P, NonZeroTotal{t.c_total, t.c_valid}, T, V.d_n);
-
+    // the trend rows in one pass over the coverage view; the fetched rows per project (raw_n)
+    // counted on the way instead of a first filter whose rows a second one would re-read
     int64_t *counts = o->counts;
     int64_t *raw_n = o->raw_n, *n_trend = o->n_trend;
-    const int64_t *voffs = V.offs, *toffs = T.offs;
+    dev_fill(c, raw_n, 0, (P > 0 ? P : 1) * 8);
+    TmpView T;
+    const CovTrendRows vrows{t.c_project, t.c_coverage, t.c_valid, t.c_date, o->eligible};
+    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P, TrendRows{vrows, NonZeroTotal{t.c_total, t.c_valid}}, T,
+                nullptr, Selection{}, CountCovTrend{raw_n, vrows});
+    const int64_t *toffs = T.offs;
     per_seg(c, P, [=] __device__(int64_t p) {
-        raw_n[p] = voffs[p + 1] - voffs[p];
         const int64_t nt = toffs[p + 1] - toffs[p];
         n_trend[p] = nt;
         atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ2C_SESSIONS]), (unsigned long long)nt);

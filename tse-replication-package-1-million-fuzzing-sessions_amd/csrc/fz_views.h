@@ -52,14 +52,23 @@ struct Selection {
     }
 };
 
-template <typename Pred>
+// A second predicate counted per project while filtering (off by default): out[p] += the rows of
+// project p it holds (one atomic per wave and item where the wave's rows share a project).
+struct NoCount {
+    static constexpr bool on = false;
+    int64_t *out = nullptr;
+    __device__ bool operator()(int32_t) const { return false; }
+};
+
+template <typename Pred, typename Count = NoCount>
 __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__restrict__ rows,
                                                            const int64_t *__restrict__ times,
                                                            const uint32_t *__restrict__ proj, int64_t n,
                                                            const int64_t *__restrict__ d_live, Pred pred, Lookback lb,
                                                            int64_t ntiles, int32_t *__restrict__ orow,
                                                            int64_t *__restrict__ otime, uint32_t *__restrict__ oproj,
-                                                           int64_t *__restrict__ d_n, Selection sel) {
+                                                           int64_t *__restrict__ d_n, Selection sel,
+                                                           Count cnt = Count{}) {
     __shared__ int32_t s_pos[kFcTile];
     __shared__ int32_t s_tmp[4];
     __shared__ int64_t s_prefix;
@@ -99,6 +108,27 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
     }
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) keep[i] = base + i * kBlock + tid < lim && pred(r[i]);
+    if constexpr (Count::on) {
+        const int lane = lane_id();
+#pragma unroll
+        for (int i = 0; i < kFcItems; ++i) {
+            const int64_t idx = base + i * kBlock + tid;
+            const bool valid = idx < lim;
+            const uint64_t act = __ballot(valid);
+            if (!act) continue;  // (wave-uniform)
+            const bool c2 = valid && cnt(r[i]);
+            const uint32_t p = valid ? proj[idx] : 0u;
+            const int first = __ffsll((long long)act) - 1;
+            const uint32_t pf = __shfl(p, first, kWave);
+            const uint64_t m = __ballot(c2);
+            if (__ballot(valid && p == pf) == act) {  // the wave's rows all in one project
+                if (lane == first && m)
+                    atomicAdd(reinterpret_cast<unsigned long long *>(&cnt.out[pf]), (unsigned long long)__popcll(m));
+            } else if (c2) {
+                atomicAdd(reinterpret_cast<unsigned long long *>(&cnt.out[p]), 1ull);
+            }
+        }
+    }
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) s_pos[i * kBlock + tid] = keep[i] ? 1 : 0;
     __syncthreads();
@@ -150,9 +180,10 @@ struct PredBytes<P, std::void_t<decltype(P::kBytes)>> {
 // -> dst (same order).
 // sel (optional): the projects pred can keep - tiles of the (project-ordered) view covering none of
 // them are skipped without reading their columns.
-template <typename Pred>
+template <typename Pred, typename Count = NoCount>
 void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uint32_t *proj, int64_t n, int64_t P,
-                 Pred pred, TmpView &dst, const int64_t *src_live = nullptr, Selection sel = Selection{}) {
+                 Pred pred, TmpView &dst, const int64_t *src_live = nullptr, Selection sel = Selection{},
+                 Count cnt = Count{}) {
     dst.cap = n;
     dst.d_n = c->arena.get<int64_t>(1);
     dst.row = c->arena.get<int32_t>(n);
@@ -167,9 +198,9 @@ void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uin
         // (a selective filter reads only the tiles of its projects: probed apart, kept rows' bytes)
         ProbeScope ps(c, sel.flags ? "filter_select" : "filter_compact",
                       sel.flags ? 0.0 : double(n) * (4.0 + PredBytes<Pred>::value), dst.d_n, 28.0);
-        k_filter_compact<Pred><<<unsigned(ntiles), kBlock, 0, c->stream>>>(rows, times, proj, n, src_live, pred, lb,
+        k_filter_compact<Pred, Count><<<unsigned(ntiles), kBlock, 0, c->stream>>>(rows, times, proj, n, src_live, pred, lb,
                                                                           ntiles, dst.row, dst.time, dst.proj,
-                                                                          dst.d_n, sel);
+                                                                          dst.d_n, sel, cnt);
         FZ_LAUNCH_CHECK();
         lookback_end(c, ntiles);
     } else {
