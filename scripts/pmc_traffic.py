@@ -33,9 +33,11 @@ SCOPES = {
     "seg_time_sort": {"open": "k_prefix_offsets", "match": ["k_seg_time_bucket"], "allow": ["k_fill"],
                       "close": "k_store_views"},
     "store_gather": {"match": ["k_store_gather"]},
-    "big_scatter": {"match": ["k_big_scatter"]},
-    # the long class over the sub-buckets, right after the scatter (fills of its counters between)
-    "big_sub_sort": {"open": "k_big_scatter", "match": ["k_seg_time_bucket"], "allow": ["k_fill"]},
+    "big_compact": {"match": ["k_big_compact"]},
+    # the long class over the sub-buckets, right after the radix passes of the distribution (fills
+    # of its counters between)
+    "big_sub_sort": {"open": "k_big_compact", "match": ["k_seg_time_bucket"],
+                     "allow": ["k_fill", "k_onesweep", "__amd"]},
     "seg_reduce": {"open": "k_chunk_reduce", "match": ["k_chunk_reduce", "k_seg_fold", "k_seg_sum"],
                    "pre": ["k_tiny_reduce"]},
     "seg_spearman": {"open": "k_spearman_chunks", "match": ["k_spearman_chunks", "k_seg_fold", "k_seg_sum"]},

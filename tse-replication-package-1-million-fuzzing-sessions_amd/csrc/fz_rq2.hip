@@ -41,12 +41,15 @@ struct TrendRows {
     NonZeroTotal nz;
     __device__ bool operator()(int32_t r) const { return v(r) && nz(r); }
 };
-// raw_n[p]: the project's CovTrendRows rows (the fetched rows, :291-298), counted in the same pass
-struct CountCovTrend {
+// raw_n[p] (the project's CovTrendRows rows, the fetched rows of :291-298) = its trend rows + the
+// fetched rows the zero-total test drops: only those (rare) are counted in the filter pass - a count
+// of every fetched row would put one atomic per wave on the same project's counter
+struct CountZeroTotal {
     static constexpr bool on = true;
     int64_t *out;
     CovTrendRows v;
-    __device__ bool operator()(int32_t r) const { return v(r); }
+    NonZeroTotal nz;
+    __device__ bool operator()(int32_t r) const { return v(r) && !nz(r); }
 };
 
 // statistics.mean / median + np.percentile(5, 25, 50, 75, 95) of every session segment; sessions
@@ -60,9 +63,8 @@ void session_stats(fz_ctx *c, const double *sv, const Segs &ses, const int32_t *
         if (soffs[i + 1] - soffs[i] >= 100) atomic_add_i64(d_ge100, 1);
     });
     seg_mean(c, cs2, sv, average);
-    seg_median(c, ses, ss2.val, median);
     const double q5[5] = {5.0, 25.0, 50.0, 75.0, 95.0};
-    seg_percentiles(c, ses, ss2.val, q5, 5, pcts);
+    seg_percentiles(c, ses, ss2.val, q5, 5, pcts, median);
 }
 
 // spearmanr(range(n), x) and shapiro(x) of x[0, *d_n) (n_cap >= *d_n) -> out = rho, p, W, p
@@ -145,11 +147,13 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     dev_fill(c, raw_n, 0, (P > 0 ? P : 1) * 8);
     TmpView T;
     const CovTrendRows vrows{t.c_project, t.c_coverage, t.c_valid, t.c_date, o->eligible};
-    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P, TrendRows{vrows, NonZeroTotal{t.c_total, t.c_valid}}, T,
-                nullptr, Selection{}, CountCovTrend{raw_n, vrows});
+    const NonZeroTotal nzt{t.c_total, t.c_valid};
+    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P, TrendRows{vrows, nzt}, T, nullptr, Selection{},
+                CountZeroTotal{raw_n, vrows, nzt});
     const int64_t *toffs = T.offs;
     per_seg(c, P, [=] __device__(int64_t p) {
         const int64_t nt = toffs[p + 1] - toffs[p];
+        raw_n[p] += nt;
         n_trend[p] = nt;
         atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ2C_SESSIONS]), (unsigned long long)nt);
     });

@@ -271,7 +271,10 @@ void seg_fold_parts(fz_ctx *c, const ChunkedSegs &cs, const double *part, double
     const int64_t maxc = cs.cps > 0 ? cs.cps : (cs.sg.len_bound() + kChunk - 1) / kChunk;
     const int64_t G = maxc > kSliceChunks ? ((maxc + kSliceChunks - 1) / kSliceChunks < 256
                                                  ? (maxc + kSliceChunks - 1) / kSliceChunks : 256) : 1;
-    if (G > 1 && nsum * G <= (int64_t(1) << 20)) {
+    // (only while the sliced fold stays a few thousand workgroups: with very many segments - config
+    // 5's ten thousand projects beside one giant - G workgroups for EVERY segment are mostly idle,
+    // and one wave per segment folds even the giant's few thousand chunks faster)
+    if (G > 1 && nsum * G <= 8192) {
         double *part2 = c->arena.get<double>(S * G * NV * 2);
         k_seg_fold<NV><<<unsigned(nsum * G), kBlock, 0, c->stream>>>(S, cs.chunk_off, cs.cps, int(G), part, part2,
                                                                      lst, dln);
@@ -337,7 +340,9 @@ void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, 
 // (NaN where n < 3).
 void seg_shapiro(fz_ctx *c, const ChunkedSegs &cs, const double *src, const SortedSegs &ss, double *w, double *p);
 // numpy.percentile(seg, q[j]) for sorted segments -> out[s * nq + j] (NaN for empty segments).
-void seg_percentiles(fz_ctx *c, const Segs &sg, const double *sorted, const double *q_host, int nq, double *out);
+// (median != null: statistics.median of every segment too, as seg_median, in the same launch)
+void seg_percentiles(fz_ctx *c, const Segs &sg, const double *sorted, const double *q_host, int nq, double *out,
+                     double *median = nullptr);
 // sum / n per segment in double-double (statistics.mean / np.mean within 1 ulp) -> out[S].
 void seg_mean(fz_ctx *c, const ChunkedSegs &cs, const double *vals, double *out);
 // statistics.median / np.median of sorted segments: middle value or (a + b) / 2 -> out[S].

@@ -1426,12 +1426,15 @@ void seg_shapiro(fz_ctx *c, const ChunkedSegs &cs, const double *src, const Sort
 }
 
 // ------------------------------------------------------------- percentiles, means, medians
-void seg_percentiles(fz_ctx *c, const Segs &sg, const double *sorted, const double *q_host, int nq, double *out) {
+void seg_percentiles(fz_ctx *c, const Segs &sg, const double *sorted, const double *q_host, int nq, double *out,
+                     double *median) {
     double q[8];
     for (int j = 0; j < nq && j < 8; ++j) q[j] = q_host[j];
     const int64_t *offs = sg.offs;
     per_seg(c, sg.S, [=] __device__(int64_t s) {
         const int64_t b = offs[s], n = offs[s + 1] - b;
+        if (median)  // (seg_median's value, from the same thread's reads)
+            median[s] = n <= 0 ? NAN : ((n & 1) ? sorted[b + n / 2] : (sorted[b + n / 2 - 1] + sorted[b + n / 2]) / 2.0);
         for (int j = 0; j < nq; ++j) {
             if (n <= 0) {
                 out[s * nq + j] = NAN;

@@ -275,6 +275,9 @@ struct TimeSortTab {
     const int64_t *oshift = nullptr;
     const uint32_t *sproj = nullptr;
     const uint32_t *tie = nullptr;
+    // (tie_pos: equal times ordered by their position in the segment, with the sub-bucket pass's
+    // any-span comparison - its rows arrive in prefix order from the stable radix distribution)
+    bool tie_pos = false;
     // rows whose columns the long class gathered itself (the probe's algorithmic bytes), or null
     unsigned long long *fused = nullptr;
 };
@@ -315,6 +318,8 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         const int64_t b = tb.offs[s];
         const int64_t len = tb.offs[s + 1] - b;
         const uint32_t *tie = KEYS_LDS ? nullptr : tb.tie;  // (the sub-bucket pass runs the long class)
+        const bool tiemode = !KEYS_LDS && (tb.tie || tb.tie_pos);
+        auto tie_of = [&](int idx) { return tie ? tie[b + idx] : uint32_t(idx); };
         const int64_t ob = b + (tb.oshift ? tb.oshift[s] : 0);  // where the sorted rows go
         if (len <= min_len) continue;
         // a segment left to the long-segment pass / merge sort: its rows are marked kGathered so
@@ -355,7 +360,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
             lo = s_lo[q] < lo ? s_lo[q] : lo;
             hi = s_hi[q] > hi ? s_hi[q] : hi;
         }
-        if (!tie && hi >= lo && uint64_t(hi) - uint64_t(lo) >= kBlkTop) {  // span too wide for the key
+        if (!tiemode && hi >= lo && uint64_t(hi) - uint64_t(lo) >= kBlkTop) {  // span too wide for the key
             flag_segment();
             __syncthreads();
             continue;
@@ -402,7 +407,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         uint32_t gmax = 0;
 #pragma unroll
         for (int q = 0; q < NW; ++q) gmax = s_max[q] > gmax ? s_max[q] : gmax;
-        if (gmax > uint32_t(tie ? kTieSkew : kBucketSkew)) {  // clustered times: the merge sort takes it
+        if (gmax > uint32_t(tiemode ? kTieSkew : kBucketSkew)) {  // clustered times: the merge sort takes it
             flag_segment();
             __syncthreads();
             continue;
@@ -422,15 +427,15 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
             if (i >= n) continue;
             const uint32_t st = s_cnt[bs[m] >> 16], en = s_cnt[(bs[m] >> 16) + 1];
             const uint64_t key = row_key(t[m], i);
-            const uint32_t my_tie = tie && en - st > 1 ? tie[b + i] : 0u;
+            const uint32_t my_tie = tiemode && en - st > 1 ? tie_of(i) : 0u;
             uint32_t rank = 0;
             // (a row alone in its bucket - the common case for evenly spread times - reads nothing)
             for (uint32_t x = st; en - st > 1 && x < en; ++x) {
                 const int ox = s_pos[x];
                 if (ox == i) continue;
-                if (tie) {  // (time, prefix position): no packed key, any span
+                if (tiemode) {  // (time, prefix position): no packed key, any span
                     const int64_t tx = time[b + ox];
-                    rank += tx < t[m] || (tx == t[m] && tie[b + ox] < my_tie);
+                    rank += tx < t[m] || (tx == t[m] && tie_of(ox) < my_tie);
                     continue;
                 }
                 uint64_t kx;
@@ -689,17 +694,20 @@ static double gather_bytes(const PrefixSorted *pss, const int64_t *gathered) {
     return bytes;
 }
 
-// ---- long segments (> 16384 rows, config 5's Zipf head): one distribution pass --------------
+// ---- long segments (> 16384 rows, config 5's Zipf head): a distribution by time sub-bucket ----
 // A segment the bucket sorts flagged is cut by time into B = ceil(len / 8192) sub-buckets (the
-// bucket of t is floor((t - min) * B / (span + 1)), NULL last): a histogram per 65536-row tile in
-// LDS, one scan, then a scatter that moves every row's time, row id, prefix position and columns
-// into its sub-bucket of a compact copy (appends: each bucket's tail stays in L2).  The long bucket
-// class then sorts every sub-bucket as a segment - equal times ordered by prefix position - and
-// writes time, project, row id and columns to the segment's output range, coalesced.  This replaces
-// the segmented merge sort and the random gather of those rows (config 5: ~8x their algorithmic
-// bytes in HBM traffic).  Declined (the merge sort runs) for a segment of more than 8192 x 8192
-// rows; a sub-bucket that comes out longer than 16384 rows (clustered times) sends the table back
-// to the merge sort as well.
+// bucket of t is floor((t - min) * B / (span + 1)), NULL last).  The flagged segments' rows are
+// copied back to back with their global sub-bucket id as a 32-bit key (k_big_compact: coalesced
+// both ways), a stable LSD radix sort on that key moves them (time, row id, columns as payload)
+// into sub-bucket order - prefix order kept inside each sub-bucket - and a per-tile LDS histogram
+// gives the sub-bucket offsets.  The long bucket class then sorts every sub-bucket as a segment
+// (equal times by position in the sub-bucket = prefix position) and writes time, project, row id
+// and columns to the segment's output range, coalesced.  This replaces the segmented merge sort
+// and the random gather of those rows (config 5: ~8x their algorithmic bytes in HBM traffic), and
+// since round 3 also the single-pass scatter into the sub-buckets (whole-segment partial-line
+// appends: 8.7 ms per config-5 store).  Declined (the merge sort runs) for a segment of more than
+// 8192 x 8192 rows; a sub-bucket that comes out longer than 16384 rows (clustered times) sends the
+// table back to the merge sort as well.
 #ifndef FZ_BIG_TILE
 #define FZ_BIG_TILE 65536
 #endif
@@ -771,49 +779,45 @@ __global__ __launch_bounds__(kBigBlock) void k_big_hist(const int64_t *__restric
         __syncthreads();
     }
 }
+// The flagged segments' rows copied back to back (compact space, segment order; coalesced both
+// ways), each with its sub-bucket id as a 32-bit radix key: a stable radix sort of the compact rows
+// then groups them by sub-bucket, rows in prefix order inside each (k_big_compact + radix passes
+// instead of a scatter whose per-tile appends of ~30 rows to each of thousands of sub-buckets
+// wrote partial lines across the whole segment - 8.7 ms per store at config 5).
 struct BigCompact {
+    uint32_t *key;
     int64_t *time;
     uint32_t *rows;
-    uint32_t *tie;
     void *col[kMaxGather];
 };
-__global__ __launch_bounds__(kBigBlock) void k_big_scatter(const int64_t *__restrict__ time,
+__global__ __launch_bounds__(kBlock) void k_big_compact(const int64_t *__restrict__ time,
                                                         const uint32_t *__restrict__ rows, GatherCols gc, BigPlan pl,
-                                                        unsigned long long *__restrict__ cursor, BigCompact out) {
-    __shared__ uint32_t h[kBigMaxSub];
-    __shared__ int64_t base[kBigMaxSub];
+                                                        const int64_t *__restrict__ sstart, BigCompact out) {
     for (int64_t tl = blockIdx.x; tl < pl.ntiles; tl += gridDim.x) {
         const int j = pl.t_seg[tl];
         const int B = pl.nsub[j];
         const long long lo = pl.lo[j], hi = pl.hi[j];
         const int64_t r0 = pl.t_begin[tl], r1 = pl.t_end[tl];
-        for (int k = threadIdx.x; k < B; k += kBigBlock) h[k] = 0u;
-        __syncthreads();
-        for (int64_t r = r0 + threadIdx.x; r < r1; r += kBigBlock) atomicAdd(&h[big_sub(time[r], lo, hi, B)], 1u);
-        __syncthreads();
-        // reserve this tile's range of every sub-bucket (compact positions), then place the rows
-        for (int k = threadIdx.x; k < B; k += kBigBlock) {
-            if (h[k]) base[k] = int64_t(atomicAdd(&cursor[pl.sbase[j] + k], (unsigned long long)h[k]));
-            h[k] = 0u;
-        }
-        __syncthreads();
-        for (int64_t r = r0 + threadIdx.x; r < r1; r += kBigBlock) {
-            const int64_t t = time[r];
-            const int k = big_sub(t, lo, hi, B);
-            const int64_t d = base[k] + atomicAdd(&h[k], 1u);
+        const int64_t shift = pl.cstart[j] - sstart[j];
+        const uint32_t kb = uint32_t(pl.sbase[j]);
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += kBlock) {
+            const int64_t t = time[r], d = r + shift;
+            out.key[d] = kb + uint32_t(big_sub(t, lo, hi, B));
             out.time[d] = t;
             out.rows[d] = rows[r];
-            out.tie[d] = uint32_t(r);
-            for (int c = 0; c < gc.n; ++c) {
-                if (gc.size[c] == 8)
+        }
+        for (int c = 0; c < gc.n; ++c) {  // column by column: one type per loop
+            const int sz = gc.size[c];
+            for (int64_t r = r0 + threadIdx.x; r < r1; r += kBlock) {
+                const int64_t d = r + shift;
+                if (sz == 8)
                     static_cast<uint64_t *>(out.col[c])[d] = static_cast<const uint64_t *>(gc.src[c])[r];
-                else if (gc.size[c] == 4)
+                else if (sz == 4)
                     static_cast<uint32_t *>(out.col[c])[d] = static_cast<const uint32_t *>(gc.src[c])[r];
                 else
                     static_cast<uint8_t *>(out.col[c])[d] = static_cast<const uint8_t *>(gc.src[c])[r];
             }
         }
-        __syncthreads();
     }
 }
 
@@ -892,22 +896,39 @@ static bool big_segments_bucketed(fz_ctx *c, const PrefixSorted &ps, int64_t big
     // sub-bucket offsets in the compact space (big segments back to back, in segment order)
     int64_t *soffs = c->arena.get<int64_t>(nsubs + 1);
     scan_exclusive_i64(c, cnt, soffs, nsubs + 1, nullptr);
-    unsigned long long *cursor = c->arena.get<unsigned long long>(nsubs);
-    dev_copy(c, cursor, soffs, nsubs * 8);
+    // the flagged segments' rows back to back with their sub-bucket ids, then the stable radix
+    // sort on the id (rows inside a sub-bucket stay in prefix order: equal times are ordered by
+    // position in the sub-bucket pass - tie_pos)
+    std::vector<int64_t> sst(nb);
+    for (int64_t j = 0; j < nb; ++j) sst[j] = offs[segid[j]];
+    const int64_t *d_sst = static_cast<const int64_t *>(up(sst.data(), size_t(nb) * 8));
     BigCompact cp;
+    cp.key = c->arena.get<uint32_t>(ncomp);
     cp.time = c->arena.get<int64_t>(ncomp);
     cp.rows = c->arena.get<uint32_t>(ncomp);
-    cp.tie = c->arena.get<uint32_t>(ncomp);
-    GatherCols cg = ps.gc;  // the sub-bucket sort reads the compact columns, writes the table's
-    for (int k = 0; k < ps.gc.n; ++k) {
-        cp.col[k] = c->arena.alloc(size_t(ncomp) * size_t(ps.gc.size[k]));
-        cg.src[k] = cp.col[k];
-    }
+    for (int k = 0; k < ps.gc.n; ++k) cp.col[k] = c->arena.alloc(size_t(ncomp) * size_t(ps.gc.size[k]));
     {
-        ProbeScope probe(c, "big_scatter", (2.0 * (8 + 4 + 4) + 2.0 * ps.gc.bytes()) * double(ncomp));
-        k_big_scatter<<<grid, kBigBlock, 0, c->stream>>>(ps.time, ps.rows, ps.gc, pl, cursor, cp);
+        // read time 8 + row id 4 + columns; write key 4 + time 8 + row id 4 + columns
+        ProbeScope probe(c, "big_compact", (28.0 + 2.0 * ps.gc.bytes()) * double(ncomp));
+        k_big_compact<<<grid, kBlock, 0, c->stream>>>(ps.time, ps.rows, ps.gc, pl, d_sst, cp);
         FZ_LAUNCH_CHECK();
     }
+    RadixPayload rpl;
+    rpl.n = 2 + ps.gc.n;
+    rpl.in[0] = cp.time;
+    rpl.size[0] = 8;
+    rpl.in[1] = cp.rows;
+    rpl.size[1] = 4;
+    for (int k = 0; k < ps.gc.n; ++k) {
+        rpl.in[2 + k] = cp.col[k];
+        rpl.size[2 + k] = ps.gc.size[k];
+    }
+    uint32_t *no_vals = nullptr;
+    uint32_t *key = cp.key;
+    radix_sort_pairs_payload32(c, key, no_vals, ncomp, bits_for(uint64_t(nsubs - 1)), rpl);
+    sync(c);  // (the plan's host vectors - sst - die with this function)
+    GatherCols cg = ps.gc;  // the sub-bucket sort reads the sorted compact columns, writes the table's
+    for (int k = 0; k < ps.gc.n; ++k) cg.src[k] = rpl.out[2 + k];
     // every sub-bucket a segment of the long bucket class; overflow (> 16384 rows) counted in big
     unsigned long long *big = c->arena.get<unsigned long long>(6);
     dev_fill(c, big, 0, 6 * 8);
@@ -915,18 +936,18 @@ static bool big_segments_bucketed(fz_ctx *c, const PrefixSorted &ps, int64_t big
     dev_fill(c, flags, 0, nsubs);
     TimeSortTabs T;
     TimeSortTab &tb = T.tab[0];
-    tb.time = cp.time;
+    tb.time = static_cast<const int64_t *>(rpl.out[0]);
     tb.offs = soffs;
     tb.pmask = ps.pmask;
     tb.out = ps.out;
     tb.big = big;
     tb.bigflag = flags;
-    tb.rows = cp.rows;
+    tb.rows = static_cast<const uint32_t *>(rpl.out[1]);
     tb.orow = ps.orow;
     tb.gc = cg;
     tb.oshift = d_shift;
     tb.sproj = d_sproj;
-    tb.tie = cp.tie;
+    tb.tie_pos = true;
     T.base[1] = T.base[2] = T.base[3] = nsubs;
     {
         // time 8 read; time 8 + project 4 + marker 4 written; row id 4 + columns read, perm 4 +
