@@ -41,6 +41,7 @@ SCOPES = {
     "seg_reduce": {"open": "k_chunk_reduce", "match": ["k_chunk_reduce", "k_seg_fold", "k_seg_sum"],
                    "pre": ["k_tiny_reduce"]},
     "seg_spearman": {"open": "k_spearman_chunks", "match": ["k_spearman_chunks", "k_seg_fold", "k_seg_sum"]},
+    "seg_rank_union": {"open": "k_bm_union_chunks<0>", "match": ["k_bm_union_chunks", "k_seg_fold", "k_seg_sum"]},
     "scan_i64": {"match": ["k_scan_lookback"]},
     # seg_sort_f64's bucket path: value bucket classes, then the merge sort of flagged segments
     "seg_value_sort": {"open": "k_seg_val_bucket<256, 1024>",

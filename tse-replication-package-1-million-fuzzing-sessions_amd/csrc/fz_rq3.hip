@@ -298,27 +298,24 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
         // (every per-element pass over the union runs over its live length *d_all, not the
         // capacity NI + NC: config 3's union is empty, config 2's ~80 % of it)
         int32_t *sid = c->arena.get<int32_t>(cap);
-        uint8_t *g = c->arena.get<uint8_t>(cap);
         const int64_t *d_det0 = d_nd;
         map_n(c, cap, d_all, [=] __device__(int64_t i) {
             const int64_t nd = *d_det0;
             v[i] = i < nd ? dp[i] : np_[i - nd];
             sid[i] = 0;
-            g[i] = i < nd ? 0 : 1;  // brunnermunzel(det, non) (:349): position < nd is det
         });
         Segs one{1, oall, cap};
-        ChunkedSegs cs = chunked(c, one);
         SortedSegs ss = seg_sort_f64(c, v, one, sid);
-        RankTestOut rt;
-        rt.bm_stat = tests + FZ_RQ3_BM_STAT;
-        rt.bm_p = tests + FZ_RQ3_BM_P;
-        seg_rank_tests_sorted(c, ss, g, cs, sid, rt);
-        // stable partition of the sorted union into the two samples
-        int64_t *isdet = c->arena.get<int64_t>(cap), *before = c->arena.get<int64_t>(cap);
+        // stable partition of the sorted union into the two samples: before[i] = det values before
+        // union position i (det: source position < nd), before[live] = their total
+        int64_t *isdet = c->arena.get<int64_t>(cap), *before = c->arena.get<int64_t>(cap + 1);
         const int32_t *pos = ss.pos;
         const double *sv = ss.val;
         map_n(c, cap, d_all, [=] __device__(int64_t i) { isdet[i] = pos[i] < *d_nd ? 1 : 0; });
-        scan_exclusive_i64_dn(c, isdet, before, cap, d_all, nullptr);
+        scan_exclusive_i64_dn(c, isdet, before, cap, d_all, before + cap);
+        // brunnermunzel(det, non) (:349): union and within-sample ranks off the sorted union and the
+        // det counts, chunk by chunk
+        bm_union_sorted(c, one, sv, pos, before, d_nd, tests + FZ_RQ3_BM_STAT, tests + FZ_RQ3_BM_P);
         const int64_t *d_det = d_nd;
         map_n(c, cap, d_all, [=] __device__(int64_t i) {
             const uint64_t k = f64_key(sv[i]);

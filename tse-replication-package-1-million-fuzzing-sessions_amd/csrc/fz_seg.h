@@ -375,6 +375,12 @@ void bm_halves(fz_ctx *c, const double *sorted, const int64_t *offs2, const int6
                int64_t min_n, double *pbm);
 constexpr int kBmLdsMax = 12288;
 
+// brunnermunzel(x, y) from the sorted union of the two samples (one segment, Segs one): x = the
+// values whose source position pos[i] < *d_nx; before[i] = x values before union position i,
+// before[live] their total (an exclusive scan) -> *bm_stat, *bm_p (either may be null)
+void bm_union_sorted(fz_ctx *c, const Segs &one, const double *sorted, const int32_t *pos, const int64_t *before,
+                     const int64_t *d_nx, double *bm_stat, double *bm_p);
+
 // spearmanr(range(n), x) per segment from the sorted segments: one workgroup per segment when they
 // are short (no tie-rank passes), else seg_tie_ranks + seg_spearman_index.
 void spearman_index_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const SortedSegs &ss, double *rho,

@@ -1296,6 +1296,166 @@ __global__ __launch_bounds__(kBlock) void k_spearman_chunks(ChunkMap cm, const i
     }
 }
 
+// Brunner-Munzel of two samples from their sorted union (one segment [0, *d_live)): x = the values
+// whose source position pos[i] < *d_nx, y the others; before[i] = the x values before union
+// position i (an exclusive scan, before[live] = their total).  Chunk by chunk as k_spearman_chunks:
+// a value's union tie group [gs, ge) from the tie-start flags (edge binary searches), its union
+// rank rc = (gs + ge + 1) / 2, its within-sample rank rw from the x counts at the group's bounds
+// (before[gs], before[ge]).  PASS 0 sums rc per sample; PASS 1 the squared deviations
+// ((rc - rw) - mean rc) + mean rw per sample (means from PASS 0's sums) - the two reductions of
+// scipy's brunnermunzel, each one launch + the fold, instead of the tie-rank passes, the x-count
+// scan, the within-sample rank map and three segmented reductions.
+constexpr int kBmNV = 2;
+template <int PASS>
+__global__ __launch_bounds__(kBlock) void k_bm_union_chunks(int64_t cps, const int64_t *__restrict__ offs,
+                                                            const double *__restrict__ sv,
+                                                            const int32_t *__restrict__ pos,
+                                                            const int64_t *__restrict__ before,
+                                                            const int64_t *__restrict__ d_nx,
+                                                            const double *__restrict__ sums0,
+                                                            double *__restrict__ part) {
+    constexpr int IPT = kRedItems;
+    __shared__ double s_v[kChunk];
+    __shared__ int64_t s_w[2][4];
+    __shared__ int64_t s_edge[2];
+    __shared__ double s_hi[4][kBmNV], s_lo[4][kBmNV];
+    const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+    const int64_t sb = offs[0], se = offs[1];
+    const int64_t nx = *d_nx, ny = (se - sb) - nx;
+    for (int64_t k = blockIdx.x; k < cps; k += gridDim.x) {
+        const int64_t b = sb + k * kChunk;
+        const int64_t e = b + kChunk < se ? b + kChunk : se;
+        const int len = e > b ? int(e - b) : 0;
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int j = tid + m * kBlock;
+            if (j < len) s_v[j] = sv[b + j];
+        }
+        if (tid == 0) {
+            int64_t gs = b;
+            if (len > 0 && b > sb && sv[b - 1] == sv[b]) gs = lower_bound_d(sv, sb, b, sv[b]);
+            s_edge[0] = gs;
+        } else if (tid == kWave) {
+            int64_t ge = e;
+            if (len > 0 && e < se && sv[e] == sv[e - 1]) ge = upper_bound_d(sv, e, se, sv[e - 1]);
+            s_edge[1] = ge;
+        }
+        __syncthreads();
+        const int64_t head = s_edge[0], tail = s_edge[1];
+        const int q0 = tid * IPT;
+        bool f[IPT];
+        int64_t first = INT64_MAX, last = -1;
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int q = q0 + m;
+            f[m] = q < len && (q == 0 ? head == b : s_v[q] != s_v[q - 1]);
+            if (f[m]) {
+                first = first < b + q ? first : b + q;
+                last = b + q;
+            }
+        }
+        int64_t incl_max = last, incl_min = first;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const int64_t a = __shfl_up(incl_max, off, kWave);
+            const int64_t d = __shfl_down(incl_min, off, kWave);
+            if (lane >= off) incl_max = a > incl_max ? a : incl_max;
+            if (lane + off < kWave) incl_min = d < incl_min ? d : incl_min;
+        }
+        if (lane == kWave - 1) s_w[0][w] = incl_max;
+        if (lane == 0) s_w[1][w] = incl_min;
+        int64_t bef = __shfl_up(incl_max, 1, kWave), aft = __shfl_down(incl_min, 1, kWave);
+        if (lane == 0) bef = -1;
+        if (lane == kWave - 1) aft = INT64_MAX;
+        __syncthreads();
+        for (int q = 0; q < 4; ++q) {
+            if (q < w) bef = s_w[0][q] > bef ? s_w[0][q] : bef;
+            if (q > w) aft = s_w[1][q] < aft ? s_w[1][q] : aft;
+        }
+        if (bef < 0) bef = head;
+        if (aft == INT64_MAX) aft = tail;
+        int64_t ge[IPT];
+        int64_t nxt = aft;
+#pragma unroll
+        for (int m = IPT - 1; m >= 0; --m) {
+            ge[m] = nxt;
+            if (f[m]) nxt = b + q0 + m;
+        }
+        const double Nx = double(nx), Ny = double(ny);
+        DD acc[kBmNV] = {DD{0.0, 0.0}, DD{0.0, 0.0}};
+        int64_t gs = bef;
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int q = q0 + m;
+            if (q >= len) continue;
+            if (f[m]) gs = b + q;
+            const bool isx = pos[b + q] < nx;
+            const double rc = double((gs - sb) + (ge[m] - sb) + 1) / 2.0;
+            if constexpr (PASS == 0) {
+                acc[isx ? 0 : 1] = dd_add_d(acc[isx ? 0 : 1], rc);
+            } else {
+                const int64_t xb = before[gs] - before[sb], xg = before[ge[m]] - before[gs];
+                const int64_t yb = (gs - sb) - xb, yg = (ge[m] - gs) - xg;
+                const double rw = isx ? double(xb) + double(xg + 1) / 2.0 : double(yb) + double(yg + 1) / 2.0;
+                const double cm = isx ? sums0[0] / Nx : sums0[1] / Ny;        // np.mean(rankcx / rankcy)
+                const double wm = isx ? (Nx + 1.0) / 2.0 : (Ny + 1.0) / 2.0;  // np.mean(rankx) (exact)
+                const double d = ((rc - rw) - cm) + wm;
+                acc[isx ? 0 : 1] = dd_add_d(acc[isx ? 0 : 1], d * d);
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < kBmNV; ++v) {
+            const DD r = wave_dd_sum(acc[v]);
+            if (lane == 0) {
+                s_hi[w][v] = r.hi;
+                s_lo[w][v] = r.lo;
+            }
+        }
+        __syncthreads();
+        if (tid < kBmNV) {
+            DD t{s_hi[0][tid], s_lo[0][tid]};
+            for (int q = 1; q < 4; ++q) t = dd_add(t, DD{s_hi[q][tid], s_lo[q][tid]});
+            part[(k * kBmNV + tid) * 2] = t.hi;
+            part[(k * kBmNV + tid) * 2 + 1] = t.lo;
+        }
+        __syncthreads();
+    }
+}
+
+void bm_union_sorted(fz_ctx *c, const Segs &one, const double *sorted, const int32_t *pos, const int64_t *before,
+                     const int64_t *d_nx, double *bm_stat, double *bm_p) {
+    const int64_t cap = one.n_cap;
+    if (cap <= 0) return;
+    const int64_t cps = (cap + kChunk - 1) / kChunk;  // (a capacity-sized map: chunks past the live end are empty)
+    ChunkedSegs cs;
+    cs.sg = one;
+    cs.cps = cps;
+    double *part = c->arena.get<double>(cps * kBmNV * 2);
+    double *s0 = c->arena.get<double>(kBmNV), *s1 = c->arena.get<double>(kBmNV);
+    const unsigned g = unsigned(cps < 8192 ? cps : 8192);
+    const int64_t *offs = one.offs;
+    {
+        ProbeScope ps(c, "seg_rank_union", 0.0, offs + 1, 24.0);  // value 8 + position 4 + x count 8 (+ 4) per value
+        k_bm_union_chunks<0><<<g, kBlock, 0, c->stream>>>(cps, offs, sorted, pos, before, d_nx, nullptr, part);
+        FZ_LAUNCH_CHECK();
+        seg_fold_parts<kBmNV>(c, cs, part, s0);
+        k_bm_union_chunks<1><<<g, kBlock, 0, c->stream>>>(cps, offs, sorted, pos, before, d_nx, s0, part);
+        FZ_LAUNCH_CHECK();
+        seg_fold_parts<kBmNV>(c, cs, part, s1);
+    }
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {  // as seg_rank_tests_sorted's finishing
+        const double nx = double(*d_nx), ny = double(offs[1] - offs[0]) - nx;
+        const double rcx = s0[0] / nx, rcy = s0[1] / ny;
+        const double Sx = s1[0] / (nx - 1.0), Sy = s1[1] / (ny - 1.0);
+        double w = nx * ny * (rcy - rcx);
+        w /= (nx + ny) * sqrt(nx * Sx + ny * Sy);
+        const double num = (nx * Sx + ny * Sy) * (nx * Sx + ny * Sy);
+        const double den = (nx * Sx) * (nx * Sx) / (nx - 1.0) + (ny * Sy) * (ny * Sy) / (ny - 1.0);
+        if (bm_stat) *bm_stat = w;
+        if (bm_p) *bm_p = 2.0 * stats::t_sf(fabs(w), num / den);
+    });
+}
+
 void spearman_index_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const SortedSegs &ss, double *rho,
                            double *pval) {
     const Segs &sg = cs.sg;
