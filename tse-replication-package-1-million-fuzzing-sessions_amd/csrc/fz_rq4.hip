@@ -504,7 +504,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
         TmpView PC;
         filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P,
                     PositiveCoverage34{t.c_project, t.c_coverage, t.c_valid, member}, PC, nullptr,
-                    Selection{member, 12});  // (G3 / G4: tiles of other projects skipped)
+                    Selection{member, 12, nullptr, s.cov.offs});  // (G3 / G4: their rows only, virtual rows)
         const int64_t NO = g->n_order;
         const int64_t NOC = NO > 0 ? NO : 1;
         int64_t *df = c->arena.get<int64_t>(NOC), *dp = c->arena.get<int64_t>(NOC), *dj = c->arena.get<int64_t>(NOC);

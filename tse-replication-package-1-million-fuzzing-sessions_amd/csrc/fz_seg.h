@@ -83,6 +83,13 @@ __global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, const int6
             b = offs[seg] + (k % cps) * kChunk;
             e = b + kChunk < offs[seg + 1] ? b + kChunk : offs[seg + 1];
         }
+        if (b >= e && !out) {  // an empty chunk (past its segment's live end): zero partials, no barriers
+            if (threadIdx.x < NV) {
+                part[(k * NV + threadIdx.x) * 2] = 0.0;
+                part[(k * NV + threadIdx.x) * 2 + 1] = 0.0;
+            }
+            continue;
+        }
         DD acc[NV];
 #pragma unroll
         for (int v = 0; v < NV; ++v) acc[v] = DD{0.0, 0.0};

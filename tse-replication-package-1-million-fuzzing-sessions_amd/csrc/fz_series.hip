@@ -1197,6 +1197,13 @@ __global__ __launch_bounds__(kBlock) void k_spearman_chunks(ChunkMap cm, const i
         }
         const int64_t sb = offs[seg], se = offs[seg + 1];
         const int len = e > b ? int(e - b) : 0;
+        if (len == 0) {  // an empty chunk: zero partials, no barriers
+            if (tid < kSpNV) {
+                part[(k * kSpNV + tid) * 2] = 0.0;
+                part[(k * kSpNV + tid) * 2 + 1] = 0.0;
+            }
+            continue;
+        }
 #pragma unroll
         for (int m = 0; m < IPT; ++m) {
             const int j = tid + m * kBlock;
@@ -1326,6 +1333,13 @@ __global__ __launch_bounds__(kBlock) void k_bm_union_chunks(int64_t cps, const i
         const int64_t b = sb + k * kChunk;
         const int64_t e = b + kChunk < se ? b + kChunk : se;
         const int len = e > b ? int(e - b) : 0;
+        if (len == 0) {  // past the union's live end: zero partials, no barriers
+            if (tid < kBmNV) {
+                part[(k * kBmNV + tid) * 2] = 0.0;
+                part[(k * kBmNV + tid) * 2 + 1] = 0.0;
+            }
+            continue;
+        }
 #pragma unroll
         for (int m = 0; m < IPT; ++m) {
             const int j = tid + m * kBlock;

@@ -42,6 +42,26 @@ struct Selection {
     const uint8_t *flags = nullptr;
     uint8_t mask = 0xff;
     const int64_t *count = nullptr;
+    // view_offs (optional, the view's [P + 1] segment offsets): filter the selected projects' rows
+    // only - a virtual index over their segments back to back (voff, built by filter_view), so the
+    // launch's live tiles cover just those rows (no look-back chain through the skipped ones)
+    const int64_t *view_offs = nullptr;
+    const int64_t *voff = nullptr;  // [P + 1] exclusive prefix of the selected segments' lengths
+    int64_t P = 0;
+    // the view row of virtual row v, walking forward from project p (v only grows per thread)
+    __device__ int64_t phys(int64_t v, int64_t &p) const {
+        if (voff[p + 1] <= v) {  // past p's segment: the next selected segment holding v
+            int64_t lo = p + 1, hi = P;  // voff[lo] <= v < voff[hi + 1] ... find last lo with voff[lo] <= v
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) >> 1;
+                if (voff[mid] <= v) lo = mid;
+                else hi = mid - 1;
+            }
+            p = lo;
+            while (p < P && voff[p + 1] <= v) ++p;  // (skip empty segments ending at v)
+        }
+        return view_offs[p] + (v - voff[p]);
+    }
     // none of the projects [p0, p1] selected (checked one by one for a few; a tile spanning more
     // projects is read)
     __device__ bool none(uint32_t p0, uint32_t p1) const {
@@ -74,6 +94,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
     __shared__ int64_t s_prefix;
     __shared__ unsigned int s_tile;
     __shared__ int s_skip;
+    __shared__ int64_t s_p0;
     const int tid = threadIdx.x;
     const int64_t live = d_live ? *d_live : n;
     int64_t lim = live < n ? live : n;
@@ -86,17 +107,34 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
         return;
     }
     if (int64_t(blockIdx.x) >= ntiles) return;
+    const bool virt = sel.voff != nullptr;
     if (tid == 0) {
         s_tile = lb_take_tile(lb.ticket, unsigned(ntiles));
-        // (a tile of the project-ordered view whose few projects are all unselected keeps nothing:
-        // none of its columns is read)
         const int64_t b0 = int64_t(s_tile) * kFcTile, b1 = b0 + kFcTile < lim ? b0 + kFcTile : lim;
-        s_skip = sel.flags && (b0 >= b1 || sel.none(proj[b0], proj[b1 - 1]));
+        if (virt) {  // the selected segment holding the tile's first virtual row
+            int64_t p = 0;
+            s_p0 = (b0 < b1) ? (sel.phys(b0, p), p) : 0;
+            s_skip = 0;
+        } else {
+            // (a tile of the project-ordered view whose few projects are all unselected keeps
+            // nothing: none of its columns is read)
+            s_skip = sel.flags && (b0 >= b1 || sel.none(proj[b0], proj[b1 - 1]));
+        }
     }
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t base = tile * kFcTile;
     if (s_skip) lim = 0;
+    // view row of item i (virtual mode: through the selected segments)
+    int64_t pidx[kFcItems];
+    {
+        int64_t p = virt ? s_p0 : 0;
+#pragma unroll
+        for (int i = 0; i < kFcItems; ++i) {
+            const int64_t v = base + i * kBlock + tid;
+            pidx[i] = virt && v < lim ? sel.phys(v, p) : v;
+        }
+    }
     // all row loads first, then all predicate gathers: independent loads in flight together
     // instead of one dependent load chain per item
     int32_t r[kFcItems];
@@ -104,7 +142,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) {
         const int64_t idx = base + i * kBlock + tid;
-        r[i] = idx < lim ? rows[idx] : 0;
+        r[i] = idx < lim ? rows[pidx[i]] : 0;
     }
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) keep[i] = base + i * kBlock + tid < lim && pred(r[i]);
@@ -117,7 +155,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
             const uint64_t act = __ballot(valid);
             if (!act) continue;  // (wave-uniform)
             const bool c2 = valid && cnt(r[i]);
-            const uint32_t p = valid ? proj[idx] : 0u;
+            const uint32_t p = valid ? proj[pidx[i]] : 0u;
             const int first = __ffsll((long long)act) - 1;
             const uint32_t pf = __shfl(p, first, kWave);
             const uint64_t m = __ballot(c2);
@@ -159,11 +197,20 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
     for (int i = 0; i < kFcItems; ++i) {
         if (!keep[i]) continue;
         const int k = i * kBlock + tid;
-        const int64_t idx = base + k, q = pre + (s_pos[k] & 0x7fffffff);
+        const int64_t q = pre + (s_pos[k] & 0x7fffffff);
         orow[q] = r[i];
-        otime[q] = times[idx];
-        oproj[q] = proj[idx];
+        otime[q] = times[pidx[i]];
+        oproj[q] = proj[pidx[i]];
     }
+}
+
+// The selected projects' segment lengths (0 for the others; entry P = 0) for the virtual rows.
+template <typename S>
+__global__ __launch_bounds__(kBlock) void k_sel_lengths(const S sel, int64_t P, int64_t *__restrict__ len);
+template <typename S>
+__global__ __launch_bounds__(kBlock) void k_sel_lengths(const S sel, int64_t P, int64_t *__restrict__ len) {
+    for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p <= P; p += int64_t(gridDim.x) * kBlock)
+        len[p] = p < P && (sel.flags[p] & sel.mask) ? sel.view_offs[p + 1] - sel.view_offs[p] : 0;
 }
 
 // Algorithmic bytes the predicate reads per row (Pred::kBytes when it declares them).
@@ -190,6 +237,15 @@ void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uin
     dst.time = c->arena.get<int64_t>(n);
     dst.proj = c->arena.get<uint32_t>(n);
     dst.offs = c->arena.get<int64_t>(P + 1);
+    if (n > 0 && sel.flags && sel.view_offs) {  // the selected segments back to back (virtual rows)
+        int64_t *vl = c->arena.get<int64_t>(P + 1), *voff = c->arena.get<int64_t>(P + 1);
+        k_sel_lengths<Selection><<<grid_for(P + 1), kBlock, 0, c->stream>>>(sel, P, vl);
+        FZ_LAUNCH_CHECK();
+        scan_exclusive_i64(c, vl, voff, P + 1, nullptr);
+        sel.voff = voff;
+        sel.P = P;
+        src_live = voff + P;  // (a view filter: no other live bound)
+    }
     if (n > 0) {
         const int64_t ntiles = (n + kFcTile - 1) / kFcTile;
         const Lookback lb = lookback_begin(c, ntiles);
