@@ -219,6 +219,8 @@ def main():
         # the last group runs on the engine itself (its stream, after the store build)
         children = [eng.child() for _ in groups[:-1]] + [eng]
         pool = ThreadPoolExecutor(len(groups) - 1)
+        # the store build forks its independent sorts onto the (then idle) children
+        eng.set_store_helpers(children[:-1])
 
         def run_group(ch, names):
             with torch.cuda.stream(ch.stream):

@@ -118,6 +118,12 @@ int fz_ctx_set_stream(fz_ctx *ctx, void *stream);
 /* Sorts buildlog_data by (build_type, project, timecreated), total_coverage by (project, date),
  * issues by (project, rts) (stable: ties keep row order), builds per-project segment offsets. */
 int fz_store_build(fz_ctx *ctx, const fz_tables *t, fz_store_stats *stats);
+/* Up to 4 children of ctx (fz_ctx_create_child) that fz_store_build may use while it runs - the
+ * three tables' prefix sorts and the time-sort length classes are independent, and are forked onto
+ * the helpers' streams / contexts (joined before the build returns).  The helpers must be idle
+ * during the build (the caller orders their streams after it, as for any child); n = 0 turns it
+ * off.  No reference counterpart: the PostgreSQL restore builds the indexes one after another. */
+int fz_store_set_helpers(fz_ctx *ctx, fz_ctx *const *helpers, int n);
 
 /* ---- RQ1: rq1_detection_rate.py:101-269 ------------------------------------------------- */
 enum {

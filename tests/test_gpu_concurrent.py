@@ -17,12 +17,18 @@ ANALYSES = {"rq1": compute.rq1, "rq2_count": compute.rq2_count, "rq2_add": compu
 GROUPS = [["rq2_count"], ["rq4b", "rq1"], ["rq3", "rq4a"], ["rq2_add"]]
 
 
+@pytest.mark.parametrize("helpers", [False, True])
 @pytest.mark.parametrize("case", goldens.CASES)
-def test_children_match_serial(engine_for, case):
+def test_children_match_serial(engine_for, case, helpers):
+    """(helpers: the store build also forks its table sorts and time-sort classes onto three of
+    the children - fz_store_set_helpers - as bench.py does; destroying the children removes them
+    as helpers, so the rebuild after close runs on the engine alone.)"""
     eng = engine_for(case)
     torch = eng.torch
     serial = {k: f(eng) for k, f in ANALYSES.items()}
     children = [eng.child() for _ in GROUPS]
+    if helpers:
+        eng.set_store_helpers(children[:3])
 
     def run(ch, names):
         with torch.cuda.stream(ch.stream):
@@ -47,3 +53,7 @@ def test_children_match_serial(engine_for, case):
             ch.close()
     assert not eng.__dict__.get("_children")
     assert_same(compute.rq3(eng), serial["rq3"], "rq3 after children closed")
+    if helpers:
+        eng.build_store()
+        for k in ("rq1", "rq4b"):
+            assert_same(ANALYSES[k](eng), serial[k], f"{k} after a rebuild without the closed helpers")

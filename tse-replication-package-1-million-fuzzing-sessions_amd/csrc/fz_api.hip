@@ -145,15 +145,38 @@ int fz_ctx_destroy(fz_ctx *ctx) {
     if (!ctx) return FZ_OK;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->parent) {  // a destroyed child is no longer a store-build helper of its parent
+        auto &h = ctx->parent->helpers;
+        for (size_t i = 0; i < h.size();)
+            if (h[i] == ctx) h.erase(h.begin() + long(i));
+            else ++i;
+    }
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     if (ctx->capture_stream) (void)hipStreamDestroy(ctx->capture_stream);
     if (ctx->ev_readback) (void)hipEventDestroy(ctx->ev_readback);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    for (hipEvent_t e : ctx->ev_join)
+        if (e) (void)hipEventDestroy(e);
     delete ctx;
     return FZ_OK;
 }
 
 int fz_ctx_set_stream(fz_ctx *ctx, void *stream) {
     return guarded(ctx, [&] { ctx->stream = static_cast<hipStream_t>(stream); });
+}
+
+int fz_store_set_helpers(fz_ctx *ctx, fz_ctx *const *helpers, int n) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n >= 0 && n <= 4 && (n == 0 || helpers != nullptr), "fz_store_set_helpers: 0..4 helpers");
+        FZ_CHECK(ctx->parent == nullptr, "fz_store_set_helpers: the store's own context only");
+        std::vector<fz_ctx *> h;
+        for (int i = 0; i < n; ++i) {
+            FZ_CHECK(helpers[i] != nullptr && helpers[i]->parent == ctx && helpers[i] != ctx,
+                     "fz_store_set_helpers: helpers must be children of this context");
+            h.push_back(helpers[i]);
+        }
+        ctx->helpers = h;
+    });
 }
 
 int fz_store_build(fz_ctx *ctx, const fz_tables *t, fz_store_stats *stats) {

@@ -242,6 +242,10 @@ struct fz_ctx {
     // the store build's counter read-back (fz_store.hip): the host waits for this event, not for
     // the stream, so the gather launched after the copies overlaps the round trip
     hipEvent_t ev_readback = nullptr;
+    // store-build helpers (fz_store_set_helpers: children of this context, idle while the store is
+    // built): the build forks the tables' independent sorts onto their streams / contexts
+    std::vector<fz_ctx *> helpers;
+    hipEvent_t ev_fork = nullptr, ev_join[4] = {};
 };
 
 namespace fz {

@@ -104,6 +104,25 @@ __global__ __launch_bounds__(kSortBlock) void k_store_views(const ViewSrc v, int
     if (threadIdx.x < 9) out[4 + threadIdx.x] = int64_t(v.big[threadIdx.x]);
 }
 
+// ---- fork / join onto the store-build helpers (fz_store_set_helpers) -------------------------
+// Used only while no probe window is open (the probes bracket launches on the context's own
+// stream).  fork: every helper's stream waits for the work enqueued on c so far; join: c waits
+// for everything enqueued on the helpers.
+static int store_helpers(fz_ctx *c) { return c->probe.active() ? 0 : int(c->helpers.size()); }
+static void store_fork(fz_ctx *c) {
+    if (!c->ev_fork) FZ_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    FZ_HIP(hipEventRecord(c->ev_fork, c->stream));
+    for (fz_ctx *h : c->helpers) FZ_HIP(hipStreamWaitEvent(h->stream, c->ev_fork, 0));
+}
+static void store_join(fz_ctx *c) {
+    for (size_t i = 0; i < c->helpers.size(); ++i) {
+        hipEvent_t &e = c->ev_join[i];
+        if (!e) FZ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        FZ_HIP(hipEventRecord(e, c->helpers[i]->stream));
+        FZ_HIP(hipStreamWaitEvent(c->stream, e, 0));
+    }
+}
+
 // ---- prefix LSD passes (moving the columns) + per-segment register sort by (time, row) -------
 // Up to three tables' (prefix, row) keys in one launch: table k's rows are [base[k], base[k + 1])
 // of the combined index.
@@ -576,6 +595,16 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) 
     if (K.base[3] == 0) return;
     k_keys_prefix_rows<<<grid_for(K.base[3], kBlock, 4096), kBlock, 0, c->stream>>>(K);
     FZ_LAUNCH_CHECK();
+    // the coverage and issues tables' radix sorts on two helpers (their own streams, look-back
+    // state and arenas - the sorted columns live in the helper's arena until the gather), the
+    // builds' on c
+    const bool fork = store_helpers(c) >= 2 && in[1].n > 0 && (in[0].n > 0 || in[2].n > 0);
+    fz_ctx *tctx[3] = {c, fork ? c->helpers[0] : c, fork ? c->helpers[1] : c};
+    if (fork) {
+        store_fork(c);
+        c->helpers[0]->arena.reset();
+        c->helpers[1]->arena.reset();
+    }
     PrefixOffs O;
     for (int k = 0; k < 3; ++k) {
         const TableIn &t = in[k];
@@ -595,7 +624,7 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) 
             pl.in[1 + j] = t.gc.src[j];
             pl.size[1 + j] = t.gc.size[j];
         }
-        radix_sort_pairs_payload32(c, K.keys[k], K.vals[k], n, t.prefix_bits, pl);
+        radix_sort_pairs_payload32(tctx[k], K.keys[k], K.vals[k], n, t.prefix_bits, pl);
         ps.time = static_cast<const int64_t *>(pl.out[0]);
         ps.gc = t.gc;
         for (int j = 0; j < t.gc.n; ++j) ps.gc.src[j] = pl.out[1 + j];
@@ -613,6 +642,7 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) 
         O.offs[k] = const_cast<int64_t *>(ps.offs);
         O.base[k + 1] = O.base[k] + (n > S + 1 ? n : S + 1);
     }
+    if (fork) store_join(c);
     k_prefix_offsets<<<grid_for(O.base[3], kBlock, 4096), kBlock, 0, c->stream>>>(O);
     FZ_LAUNCH_CHECK();
 }
@@ -655,16 +685,22 @@ static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
     // 256-thread workgroup each (15 KiB of LDS: many per CU), <= 2048 512 threads, <= 4096 1024
     // threads, <= 16384 1024 threads with the keys re-read from memory (LDS: one per CU, a
     // persistent grid); longer or clustered segments are flagged for the merge sort
-    k_seg_time_bucket<256, 1024><<<unsigned(S < 16384 ? S : 16384), 256, 0, c->stream>>>(T, 0, false);
+    // (with helpers the four class launches run side by side on their streams: disjoint segments,
+    // disjoint output rows, atomic counters)
+    const int nh = store_helpers(c);
+    if (nh > 0) store_fork(c);
+    auto st = [&](int i) { return i > 0 && i <= nh ? c->helpers[i - 1]->stream : c->stream; };
+    k_seg_time_bucket<256, 1024><<<unsigned(S < 16384 ? S : 16384), 256, 0, st(0)>>>(T, 0, false);
     FZ_LAUNCH_CHECK();
-    k_seg_time_bucket<512, 2048><<<unsigned(S < 4096 ? S : 4096), 512, 0, c->stream>>>(T, 1024, false);
+    k_seg_time_bucket<512, 2048><<<unsigned(S < 4096 ? S : 4096), 512, 0, st(1)>>>(T, 1024, false);
     FZ_LAUNCH_CHECK();
-    k_seg_time_bucket<1024, 4096><<<unsigned(S < 2048 ? S : 2048), 1024, 0, c->stream>>>(T, 2048, false);
+    k_seg_time_bucket<1024, 4096><<<unsigned(S < 2048 ? S : 2048), 1024, 0, st(2)>>>(T, 2048, false);
     FZ_LAUNCH_CHECK();
     // (a workgroup per CU at most; fewer when the tables are too small to hold many long segments)
     const int64_t g16 = ntot / 16384 < 8 ? 8 : (ntot / 16384 > 256 ? 256 : ntot / 16384);
-    k_seg_time_bucket<1024, 16384><<<unsigned(S < g16 ? S : g16), 1024, 0, c->stream>>>(T, 4096, true);
+    k_seg_time_bucket<1024, 16384><<<unsigned(S < g16 ? S : g16), 1024, 0, st(3)>>>(T, 4096, true);
     FZ_LAUNCH_CHECK();
+    if (nh > 0) store_join(c);
 }
 
 // Gather of every sorted row's columns (after all sorts, merge sort included), all tables in one

@@ -80,7 +80,9 @@ struct NoCount {
     __device__ bool operator()(int32_t) const { return false; }
 };
 
-template <typename Pred, typename Count = NoCount>
+// VIRT: the rows are the virtual rows of a Selection with view_offs (the selected projects'
+// segments back to back): item i's view row comes from Selection::phys.
+template <typename Pred, typename Count = NoCount, bool VIRT = false>
 __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__restrict__ rows,
                                                            const int64_t *__restrict__ times,
                                                            const uint32_t *__restrict__ proj, int64_t n,
@@ -107,11 +109,10 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
         return;
     }
     if (int64_t(blockIdx.x) >= ntiles) return;
-    const bool virt = sel.voff != nullptr;
     if (tid == 0) {
         s_tile = lb_take_tile(lb.ticket, unsigned(ntiles));
         const int64_t b0 = int64_t(s_tile) * kFcTile, b1 = b0 + kFcTile < lim ? b0 + kFcTile : lim;
-        if (virt) {  // the selected segment holding the tile's first virtual row
+        if (VIRT) {  // the selected segment holding the tile's first virtual row
             int64_t p = 0;
             s_p0 = (b0 < b1) ? (sel.phys(b0, p), p) : 0;
             s_skip = 0;
@@ -125,16 +126,20 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
     const int64_t tile = s_tile;
     const int64_t base = tile * kFcTile;
     if (s_skip) lim = 0;
-    // view row of item i (virtual mode: through the selected segments)
-    int64_t pidx[kFcItems];
-    {
-        int64_t p = virt ? s_p0 : 0;
+    // view row of item i (VIRT: through the selected segments; tables hold < 2^31 rows)
+    int32_t pidx[VIRT ? kFcItems : 1];
+    if constexpr (VIRT) {
+        int64_t p = s_p0;
 #pragma unroll
         for (int i = 0; i < kFcItems; ++i) {
             const int64_t v = base + i * kBlock + tid;
-            pidx[i] = virt && v < lim ? sel.phys(v, p) : v;
+            pidx[i] = int32_t(v < lim ? sel.phys(v, p) : 0);
         }
     }
+    auto row_at = [&](int i) -> int64_t {
+        if constexpr (VIRT) return pidx[i];
+        else return base + i * kBlock + tid;
+    };
     // all row loads first, then all predicate gathers: independent loads in flight together
     // instead of one dependent load chain per item
     int32_t r[kFcItems];
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) {
         const int64_t idx = base + i * kBlock + tid;
-        r[i] = idx < lim ? rows[pidx[i]] : 0;
+        r[i] = idx < lim ? rows[row_at(i)] : 0;
     }
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) keep[i] = base + i * kBlock + tid < lim && pred(r[i]);
@@ -155,10 +160,11 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
             const uint64_t act = __ballot(valid);
             if (!act) continue;  // (wave-uniform)
             const bool c2 = valid && cnt(r[i]);
-            const uint32_t p = valid ? proj[pidx[i]] : 0u;
+            const uint64_t m = __ballot(c2);
+            if (!m) continue;  // (wave-uniform: nothing to count in this item - the common case)
+            const uint32_t p = valid ? proj[row_at(i)] : 0u;
             const int first = __ffsll((long long)act) - 1;
             const uint32_t pf = __shfl(p, first, kWave);
-            const uint64_t m = __ballot(c2);
             if (__ballot(valid && p == pf) == act) {  // the wave's rows all in one project
                 if (lane == first && m)
                     atomicAdd(reinterpret_cast<unsigned long long *>(&cnt.out[pf]), (unsigned long long)__popcll(m));
@@ -199,8 +205,8 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
         const int k = i * kBlock + tid;
         const int64_t q = pre + (s_pos[k] & 0x7fffffff);
         orow[q] = r[i];
-        otime[q] = times[pidx[i]];
-        oproj[q] = proj[pidx[i]];
+        otime[q] = times[row_at(i)];
+        oproj[q] = proj[row_at(i)];
     }
 }
 
@@ -254,9 +260,14 @@ void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uin
         // (a selective filter reads only the tiles of its projects: probed apart, kept rows' bytes)
         ProbeScope ps(c, sel.flags ? "filter_select" : "filter_compact",
                       sel.flags ? 0.0 : double(n) * (4.0 + PredBytes<Pred>::value), dst.d_n, 28.0);
-        k_filter_compact<Pred, Count><<<unsigned(ntiles), kBlock, 0, c->stream>>>(rows, times, proj, n, src_live, pred, lb,
-                                                                          ntiles, dst.row, dst.time, dst.proj,
-                                                                          dst.d_n, sel, cnt);
+        if (sel.voff)
+            k_filter_compact<Pred, Count, true><<<unsigned(ntiles), kBlock, 0, c->stream>>>(rows, times, proj, n, src_live, pred, lb,
+                                                                              ntiles, dst.row, dst.time, dst.proj,
+                                                                              dst.d_n, sel, cnt);
+        else
+            k_filter_compact<Pred, Count><<<unsigned(ntiles), kBlock, 0, c->stream>>>(rows, times, proj, n, src_live, pred, lb,
+                                                                              ntiles, dst.row, dst.time, dst.proj,
+                                                                              dst.d_n, sel, cnt);
         FZ_LAUNCH_CHECK();
         lookback_end(c, ntiles);
     } else {

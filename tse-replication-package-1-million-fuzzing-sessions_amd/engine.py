@@ -142,6 +142,7 @@ SIGNATURES = {
     "fz_ctx_destroy": (C.c_int, [_P]),
     "fz_ctx_set_stream": (C.c_int, [_P, _P]),
     "fz_store_build": (C.c_int, [_P, C.POINTER(FzTables), C.POINTER(FzStoreStats)]),
+    "fz_store_set_helpers": (C.c_int, [_P, C.POINTER(_P), C.c_int]),
     "fz_rq1": (C.c_int, [_P, _I64, C.POINTER(FzRq1Out)]),
     "fz_rq1_ex": (C.c_int, [_P, _I64, C.POINTER(FzRq1Ext), C.POINTER(FzRq1Out)]),
     "fz_rq1_finish": (C.c_int, [_P, _I64, _P, _P, _I64, _P, _P]),
@@ -296,6 +297,14 @@ class Engine:
             rc = self.lib.fz_capture_end(self.ctx, C.byref(g))
         _check(self.lib, rc)
         return Graph(self, g)
+
+    def set_store_helpers(self, helpers):
+        """Let build_store fork its independent sorts onto these children's streams / contexts
+        (fz_store_set_helpers; they must be idle while the store is built - join_children /
+        follow_parent order them as usual).  [] turns it off."""
+        arr = (_P * max(len(helpers), 1))(*[h.ctx for h in helpers])
+        _check(self.lib, self.lib.fz_store_set_helpers(self.ctx, arr, len(helpers)))
+        self._helpers = list(helpers)
 
     def join_children(self):
         """(parent) order the parent stream after all its children's enqueued work."""
