@@ -186,13 +186,16 @@ def main():
         raise SystemExit("bench: rq3_main / rq3_stats groupings need the graph path")
     pool = None
     graphs = None
+    sgraphs = None  # sharded step: one recording of each driver's local kernels
     if sharded:
         def sh_rq1(e):
             part = par.rq1_sharded(rq1_shard, rank, world)[0]
             par.gather_rows({"issue": part["matched_issue"], "build": part["matched_build"]}, world)
 
         def sh_rq2_add(e):
-            launch["rq2_add"](e, bufs["rq2_add"])
+            if not pre_add[0]:
+                launch["rq2_add"](e, bufs["rq2_add"])
+            pre_add[0] = False
             b = bufs["rq2_add"]
             n_add = int(b.counts[E.RQ2A_ROWS].item())
             par.gather_rows({"project": b.row_project[:n_add], "diff_total": b.diff_total[:n_add],
@@ -206,9 +209,29 @@ def main():
             "rq3": lambda e: par.rq3_sharded(rq3_shard, rank, world),
         }
 
+        # the local kernels of every driver (graph-capturable: no host reads), for the recordings
+        pre_add = [False]
+        shards = {"rq1": rq1_shard, "rq3": rq3_shard, "rq2_count": rq2c_shard, "rq4a": rq4a_shard,
+                  "rq4b": rq4b_shard}
+        local = {n: shards[n].launch for n in shards}
+        local["rq2_add"] = lambda: launch["rq2_add"](skids["rq2_add"], bufs["rq2_add"])
+
+        def mark_launched(names):
+            for n in names:
+                if n == "rq2_add":
+                    pre_add[0] = True
+                else:
+                    shards[n].pre = True
+
         def run_sharded(names):
             for name in names:
                 e = skids[name]
+                if sgraphs is not None:
+                    # this driver's local kernels replayed from its recording right before it reads
+                    # them (the next driver's local phase is enqueued only after this one's exchange
+                    # and finishing kernels, as in the eager order)
+                    sgraphs[name].launch()
+                    mark_launched([name])
                 with torch.cuda.stream(e.stream), par.use_group(sgroups[name]):
                     shard_step[name](e)
         if not args.serial:
@@ -275,9 +298,14 @@ def main():
         for f in futs:
             f.result()
 
-    for _ in range(max(args.warmup, 1 if concurrent and not args.no_graphs else 0)):
+    shard_graphs = sharded and pool is not None and not args.no_graphs
+    for _ in range(max(args.warmup, 1 if (concurrent or shard_graphs) and not args.no_graphs else 0)):
         step()
     torch.cuda.synchronize(dev)
+    if shard_graphs:
+        sgraphs = {n: skids[n].record(lambda e, n=n: local[n]()) for n in snames}
+        step()  # one untimed replay step
+        torch.cuda.synchronize(dev)
     if concurrent and not args.no_graphs:
         # record each group once (warm contexts), then every step replays the recordings; a group
         # is cut into pieces at a stage that must follow another group's stage (AFTER) and after a
@@ -409,6 +437,8 @@ def main():
     for rec in graphs or []:
         for _, gr, _ in rec:
             gr.close()
+    for gr in (sgraphs or {}).values():
+        gr.close()
     eng.close()
     if sharded:
         dist.destroy_process_group()

@@ -232,6 +232,24 @@ int fz_rq2_session_stats(fz_ctx *ctx, const double *values, const int64_t *sessi
                          int64_t n_sessions, int64_t max_session_len, double *average, double *median,
                          double *percentiles, int64_t *n_ge100);
 
+/* fz_rq2_session_stats over values already grouped by session: session s holds
+ * values[session_offsets[s], session_offsets[s + 1]) (session_offsets [n_sessions + 1], device,
+ * offsets[0] = 0, in the order the reference pools them - project order).  A shard's
+ * fz_rq2_count_ex output (session_values / session_offsets) and fz_runs_merge's output have this
+ * layout, so the sharded path's owner needs no per-value session ids and no sort. */
+int fz_rq2_session_stats_grouped(fz_ctx *ctx, const double *values, const int64_t *session_offsets, int64_t n_values,
+                                 int64_t n_sessions, int64_t max_session_len, double *average, double *median,
+                                 double *percentiles, int64_t *n_ge100);
+
+/* The session exchange's receive side: n_runs runs (one per source shard, one after another in
+ * `values`), each grouped by segment over n_segments segments, are merged segment by segment:
+ * out = for each segment s, run 0's values of s, then run 1's, ... (sources in rank order = global
+ * project order); out_offsets [n_segments + 1].  run_sizes: device [n_runs * n_segments], run r's
+ * count of segment s at r * n_segments + s.  (No reference counterpart: the reference is one
+ * process; this is what keeps the sharded per-session pools in its project order.) */
+int fz_runs_merge(fz_ctx *ctx, const double *values, const int64_t *run_sizes, int64_t n_runs, int64_t n_segments,
+                  double *out, int64_t *out_offsets);
+
 /* scipy.stats.spearmanr(range(n), x) and scipy.stats.shapiro(x) of one device series:
  * out[0..3] = rho, p, W, p (NaN where scipy returns NaN: n < 2 / constant, n < 3). */
 int fz_series_tests(fz_ctx *ctx, const double *x, int64_t n, double *out);
@@ -398,8 +416,10 @@ typedef struct fz_rq4b_out {
     double *init_g2, *init_g1;   /* [n_projects] first coverage per project (sorted ids)   :221-246 */
     double *tests;               /* [FZ_RQ4B_NTESTS] MWU p, Cliff delta, BM, Levene        :248-313 */
     /* optional (may be NULL): what a shard contributes to the cross-shard recombination */
-    double *trend_values;        /* [n_cov] G1/G2 full coverage series, project-major (date order) */
-    int64_t *trend_offsets;      /* [n_projects + 1] per-project [start, end) into trend_values     */
+    double *trend_values;        /* [n_cov] G1/G2 full coverage values grouped by (session index,
+                                    group): segment 2i = the i-th value of every G2 project, 2i + 1
+                                    = of every G1 project, projects in order inside a segment      */
+    int64_t *trend_offsets;      /* [2 * max_cov_per_project + 1] segment offsets into trend_values */
     int64_t *delta_order;        /* [n_projects] CSV row (index into groups->order) of each column  */
 } fz_rq4b_out;
 
@@ -420,6 +440,14 @@ int fz_rq4b_ex(fz_ctx *ctx, const fz_rq4_groups *groups, uint32_t flags, const f
 int fz_rq4b_session_stats(fz_ctx *ctx, const double *values, const int64_t *session_ids, const uint8_t *groups,
                           int64_t n_values, int64_t n_sessions, int64_t max_session_len, int64_t *c2, int64_t *c1,
                           double *g2_q, double *g1_q, double *p_bm);
+
+/* fz_rq4b_session_stats over values already grouped by (session, group) segment: segment 2s holds
+ * session s's G2 values, 2s + 1 its G1 values, values[segment_offsets[k], segment_offsets[k + 1])
+ * (segment_offsets [2 * n_sessions + 1], device, offsets[0] = 0) - the layout of a shard's
+ * fz_rq4b_ex trend output and of fz_runs_merge over 2 * n_sessions segments. */
+int fz_rq4b_session_stats_grouped(fz_ctx *ctx, const double *values, const int64_t *segment_offsets,
+                                  int64_t n_values, int64_t n_sessions, int64_t max_session_len, int64_t *c2,
+                                  int64_t *c1, double *g2_q, double *g1_q, double *p_bm);
 
 /* Two-sample tests of rq4b's initial coverage (:248-313) on device samples x (G2) and y (G1):
  * out[FZ_RQ4B_MWU_P .. FZ_RQ4B_LEVENE_P] = mannwhitneyu two-sided p, Cliff's delta from

@@ -1,7 +1,8 @@
 """Per-stage kernel time of one serial bench step from a rocprofv3 kernel trace (bench.py --serial:
 every launch on one stream in program order).  A step starts at the store's k_elig_hist; stages
 are cut at each analysis' first kernel (the first launch after the previous stage that matches the
-stage's opener).  usage: stage_breakdown.py TRACE.csv [TOP]"""
+stage's opener).  usage: stage_breakdown.py TRACE.csv [TOP] [STAGE,NAMES]  (the names in launch
+order: the sharded step runs its drivers as bench.py --shard-groups lists them)"""
 import csv
 import sys
 from collections import defaultdict
@@ -15,7 +16,7 @@ step = rows[a:b]
 # stage openers in serial_step order: store, rq1, rq2_count, rq2_add, rq3, rq4a, rq4b (each analysis
 # copies the eligible-project flags first: k_copy_elig)
 cuts = [0] + [i for i, r in enumerate(step) if "k_copy_elig" in r["Kernel_Name"]]
-names = ["store", "rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"]
+names = ["store"] + (sys.argv[3].split(",") if len(sys.argv) > 3 else ["rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"])
 t0 = int(step[0]["Start_Timestamp"])
 print(f"step span {(int(step[-1]['End_Timestamp']) - t0) / 1e3:.1f} us, {len(step)} kernels, cuts {len(cuts)}")
 for si, c0 in enumerate(cuts):

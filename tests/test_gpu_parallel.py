@@ -22,7 +22,7 @@ class _HostView:
 
     def run(self, *a):
         a = tuple(None if x is None else tuple(v.to(self.dev) for v in x) for x in a)
-        return {k: v.cpu() for k, v in self.s.run(*a).items()}
+        return {k: v.cpu() if isinstance(v, torch.Tensor) else v for k, v in self.s.run(*a).items()}
 
     def finish(self, counts, it, idt):
         c, i, d = (x.to(self.dev) for x in (counts, it, idt))
@@ -50,9 +50,12 @@ class _RQ2View(_HostView):
     def run(self):
         return super().run()
 
-    def session_stats(self, vals, sids, S, max_len):
-        out = self.s.session_stats(vals.to(self.dev), sids.to(self.dev), S, max_len)
+    def session_stats_grouped(self, vals, offs, S, max_len):
+        out = self.s.session_stats_grouped(vals.to(self.dev), offs.to(self.dev), S, max_len)
         return {k: v.cpu() for k, v in out.items()}
+
+    def merge_runs(self, vals, runs):
+        return tuple(v.cpu() for v in self.s.merge_runs(vals.to(self.dev), runs.to(self.dev)))
 
     def series_tests(self, x):
         return self.s.series_tests(x.to(self.dev))
@@ -72,10 +75,6 @@ class _RQ4aView(_HostView):
 class _RQ4bView(_RQ2View):
     def spearman_prefix(self, rows, n):
         return self.s.spearman_prefix(rows.to(self.dev), n.to(self.dev)).cpu()
-
-    def session_stats(self, vals, sids, grp, S, max_len):
-        out = self.s.session_stats(vals.to(self.dev), sids.to(self.dev), grp.to(self.dev), S, max_len)
-        return {k: v.cpu() for k, v in out.items()}
 
     def two_sample(self, x, y):
         return self.s.two_sample(x.to(self.dev), y.to(self.dev))

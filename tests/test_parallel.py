@@ -122,6 +122,12 @@ class OracleRQ3Shard:
         return orc.rq3_stats(det_pct.numpy(), det_tot.numpy(), non_pct.numpy())
 
 
+def _offs_to_ids(offs, S):
+    """Segment id of every value of a segment-grouped layout (offsets [S + 1])."""
+    o = offs.to(torch.int64)
+    return torch.repeat_interleave(torch.arange(S, dtype=torch.int64), o[1:S + 1] - o[:S])
+
+
 class OracleRQ2CountShard:
     """One rank's RQ2 count on the CPU restatement (per-project columns over the global project
     axis + the local coverage_by_session_index), and the session / series statistics the exchange
@@ -147,6 +153,12 @@ class OracleRQ2CountShard:
         out["session_offsets"] = torch.from_numpy(r.session_offsets.astype(np.int64))
         out["session_values"] = torch.from_numpy(r.session_values.astype(np.float64))
         return out
+
+    def merge_runs(self, vals, runs):
+        return par.merge_runs_torch(vals, runs)
+
+    def session_stats_grouped(self, vals, offs, S, max_len):
+        return self.session_stats(vals, _offs_to_ids(offs, S), S, max_len)
 
     def session_stats(self, vals, sids, S, max_len):
         import statistics
@@ -251,12 +263,17 @@ class OracleRQ4bShard(OracleRQ2CountShard):
         for g in range(4):
             member[groups[f"group{g + 1}"]] |= 1 << g
         full = orc.rq4b_full_series(t, P)
-        offs = np.zeros(P + 1, np.int64)
-        vals = []
+        # the G1/G2 series grouped by (session index, group) segment, projects in order inside one
+        vals, segs = [], []
         for p in range(P):
             v = t.c_coverage[full.rows(p)] if member[p] & 3 else np.zeros(0)
             vals.append(v)
-            offs[p + 1] = offs[p] + len(v)
+            segs.append(2 * np.arange(len(v), dtype=np.int64) + (0 if member[p] & 2 else 1))
+        vals = np.concatenate(vals) if vals else np.zeros(0)
+        segs = np.concatenate(segs) if segs else np.zeros(0, np.int64)
+        m_loc = int(segs.max()) // 2 + 1 if len(segs) else 0
+        grouped = np.argsort(segs, kind="stable")
+        offs = np.concatenate([[0], np.cumsum(np.bincount(segs, minlength=2 * m_loc))]).astype(np.int64)
         order = common.corpus_columns(t)[2].tolist()
         projs, pre, post = orc.rq4b_deltas(t, elig, groups, corpus_us)
         # CSV row of each delta column: the k-th qualifying row of the corpus order
@@ -270,11 +287,12 @@ class OracleRQ4bShard(OracleRQ2CountShard):
         c = np.zeros(12, np.int64)
         c[par.RQ4B_DELTA_PROJECTS], c[par.RQ4B_INIT_G2], c[par.RQ4B_INIT_G1] = len(projs), len(init["group2"]), \
             len(init["group1"])
+        c[par.RQ4B_SESSIONS] = m_loc
         for g in range(4):
             c[5 + g] = len(groups[f"group{g + 1}"])
         T = lambda a, dt=np.float64: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))  # noqa: E731
         return {"counts": T(c, np.int64), "member": T(member, np.int64),
-                "trend_values": T(np.concatenate(vals) if vals else np.zeros(0)), "trend_offsets": T(offs, np.int64),
+                "trend_values": T(vals[grouped]), "trend_offsets": T(offs, np.int64),
                 "pre_cov": T(np.concatenate(pre) if projs else np.zeros(0)),
                 "post_cov": T(np.concatenate(post) if projs else np.zeros(0)), "delta_order": T(dord, np.int64),
                 "init_g2": T(init["group2"]), "init_g1": T(init["group1"])}
@@ -283,11 +301,11 @@ class OracleRQ4bShard(OracleRQ2CountShard):
         n = int(n)
         return np.array([self.series_tests(r[:n])[:2] for r in rows])
 
-    def session_stats(self, vals, sids, grp, S, max_len):
+    def session_stats_grouped(self, vals, offs2, S, max_len):
         from oracle import rq_oracle as orc
-        v, s_, g_ = vals.numpy(), sids.numpy(), grp.numpy()
-        s2 = [list(v[(s_ == i) & (g_ == 0)]) for i in range(S)]
-        s1 = [list(v[(s_ == i) & (g_ == 1)]) for i in range(S)]
+        v, o = vals.numpy(), offs2.numpy()
+        s2 = [list(v[o[2 * i]:o[2 * i + 1]]) for i in range(S)]
+        s1 = [list(v[o[2 * i + 1]:o[2 * i + 2]]) for i in range(S)]
         c2, c1, q2, q1, pb = orc.rq4b_session_stats(s2, s1)
         T = torch.from_numpy
         return {"c2": T(c2), "c1": T(c1), "g2_q": T(q2.reshape(-1)), "g1_q": T(q1.reshape(-1)), "p_bm": T(pb)}

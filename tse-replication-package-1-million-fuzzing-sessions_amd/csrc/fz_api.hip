@@ -16,7 +16,11 @@ void eligibility_counts(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *c
 void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o);
 void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_ids, int64_t n, int64_t S,
                        int64_t max_len, double *average, double *median, double *pcts, int64_t *n_ge100);
+void rq2_session_stats_grouped(fz_ctx *c, const double *values, const int64_t *offs, int64_t n, int64_t S,
+                               int64_t max_len, double *average, double *median, double *pcts, int64_t *n_ge100);
 void series_tests(fz_ctx *c, const double *x, int64_t n_cap, const int64_t *d_n, double *out);
+void runs_merge(fz_ctx *c, const double *values, const int64_t *sizes, int64_t R, int64_t S, double *out,
+                int64_t *out_offs);
 void spearman_index_seg(fz_ctx *c, const double *x, int64_t n, const int64_t *offs, int64_t S, int64_t max_len,
                         double *rho, double *p);
 void rq2_add(fz_ctx *c, const fz_rq2_add_out *o);
@@ -29,6 +33,8 @@ void rq4a_finish(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int6
 void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *o);
 void rq4b_session_stats(fz_ctx *c, const double *values, const int64_t *sid, const uint8_t *grp, int64_t n, int64_t S,
                         int64_t max_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q, double *pbm);
+void rq4b_session_stats_grouped(fz_ctx *c, const double *values, const int64_t *offs2, int64_t n, int64_t S,
+                                int64_t max_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q, double *pbm);
 void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t *n2, const double *b,
                       int64_t nb_cap, const int64_t *n1, double *ts);
 void buildlog(fz_ctx *c, const uint8_t *text, int64_t n_bytes, const int64_t *log_offs_host, const int64_t *log_offs,
@@ -220,6 +226,27 @@ int fz_rq2_session_stats(fz_ctx *ctx, const double *values, const int64_t *sessi
     });
 }
 
+int fz_rq2_session_stats_grouped(fz_ctx *ctx, const double *values, const int64_t *session_offsets, int64_t n_values,
+                                 int64_t n_sessions, int64_t max_session_len, double *average, double *median,
+                                 double *percentiles, int64_t *n_ge100) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n_values >= 0 && n_sessions >= 0 && (n_values == 0 || values) && n_ge100 && session_offsets &&
+                     (n_sessions == 0 || (average && median && percentiles)) && n_sessions < (int64_t(1) << 31),
+                 "fz_rq2_session_stats_grouped: bad arguments");
+        fz::rq2_session_stats_grouped(ctx, values, session_offsets, n_values, n_sessions, max_session_len, average,
+                                      median, percentiles, n_ge100);
+    });
+}
+
+int fz_runs_merge(fz_ctx *ctx, const double *values, const int64_t *run_sizes, int64_t n_runs, int64_t n_segments,
+                  double *out, int64_t *out_offsets) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n_runs >= 0 && n_segments >= 0 && out_offsets && (n_runs * n_segments == 0 || (run_sizes && values && out)),
+                 "fz_runs_merge: bad arguments");
+        fz::runs_merge(ctx, values, run_sizes, n_runs, n_segments, out, out_offsets);
+    });
+}
+
 int fz_series_tests(fz_ctx *ctx, const double *x, int64_t n, double *out) {
     return guarded(ctx, [&] {
         FZ_CHECK(out && n >= 0 && (n == 0 || x), "fz_series_tests: bad arguments");
@@ -309,6 +336,19 @@ int fz_rq4b_session_stats(fz_ctx *ctx, const double *values, const int64_t *sess
         if (n_sessions == 0) return;
         fz::rq4b_session_stats(ctx, values, session_ids, groups, n_values, n_sessions, max_session_len, c2, c1, g2_q,
                                g1_q, p_bm);
+    });
+}
+
+int fz_rq4b_session_stats_grouped(fz_ctx *ctx, const double *values, const int64_t *segment_offsets,
+                                  int64_t n_values, int64_t n_sessions, int64_t max_session_len, int64_t *c2,
+                                  int64_t *c1, double *g2_q, double *g1_q, double *p_bm) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n_values >= 0 && n_sessions >= 0 && n_sessions < (int64_t(1) << 30) && (n_values == 0 || values) &&
+                     (n_sessions == 0 || (segment_offsets && c2 && c1 && g2_q && g1_q && p_bm)),
+                 "fz_rq4b_session_stats_grouped: bad arguments");
+        if (n_sessions == 0) return;
+        fz::rq4b_session_stats_grouped(ctx, values, segment_offsets, n_values, n_sessions, max_session_len, c2, c1,
+                                       g2_q, g1_q, p_bm);
     });
 }
 

@@ -126,6 +126,16 @@ void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_i
     session_stats(c, sv, ses, reinterpret_cast<const int32_t *>(sid), average, median, pcts, n_ge100);
 }
 
+// The same from values already grouped by session (offs [S + 1], offs[0] = 0) - a shard's
+// fz_rq2_count_ex output or what fz_runs_merge made of the exchanged runs: no key pass, no sort
+void rq2_session_stats_grouped(fz_ctx *c, const double *values, const int64_t *offs, int64_t n, int64_t S,
+                               int64_t max_len, double *average, double *median, double *pcts, int64_t *n_ge100) {
+    dev_fill(c, n_ge100, 0, 8);
+    FZ_CHECK(S < (int64_t(1) << 31), "fz_rq2_session_stats_grouped: too many sessions");
+    Segs ses{S, offs, n, max_len};
+    session_stats(c, values, ses, segment_ids(c, ses), average, median, pcts, n_ge100);
+}
+
 void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     Store &s = store_of(c);
     FZ_CHECK(s.built, "fz_rq2_count: call fz_store_build first");

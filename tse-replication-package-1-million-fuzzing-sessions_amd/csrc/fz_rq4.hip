@@ -302,13 +302,18 @@ void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t 
 // Per-session quartiles / counts / Brunner-Munzel of G2 vs G1 (:910-1015) from values v2 ordered
 // by segment id sid2 = 2 * session + group (group 0 = G2), *d_n live of n_cap
 // half_len / sess_len: host bounds of one (session, group) half and of one whole session
+// (offs2_in: the segment offsets when the caller has them - values grouped by a session exchange)
 void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_cap, const int64_t *d_n, int64_t MM,
                    int64_t half_len, int64_t sess_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q,
-                   double *pbm) {
+                   double *pbm, const int64_t *offs2_in = nullptr) {
     const int64_t S2 = 2 * MM, NC = n_cap, P = half_len;
     const int64_t *d_nf = d_n;
-    int64_t *offs2 = c->arena.get<int64_t>(S2 + 1);  // segment 2i: session i's G2 values, 2i + 1: G1
-    segment_offsets_dn(c, sid2, d_nf, NC, S2, offs2);
+    const int64_t *offs2 = offs2_in;  // segment 2i: session i's G2 values, 2i + 1: G1
+    if (!offs2) {
+        int64_t *o2 = c->arena.get<int64_t>(S2 + 1);
+        segment_offsets_dn(c, sid2, d_nf, NC, S2, o2);
+        offs2 = o2;
+    }
     // Brunner-Munzel from the sorted halves: per-thread merge walks for short halves, both halves in
     // LDS for sessions of up to kBmLdsMax values, else the device-wide rank passes
     const bool lds = P > kBmHalvesMax && sess_len <= kBmLdsMax;
@@ -392,6 +397,19 @@ void rq4b_session_stats(fz_ctx *c, const double *values, const int64_t *sid, con
     rq4b_sessions(c, v2, sid2, n, d_n, MM, half, 2 * half < n ? 2 * half : n, c2, c1, g2q, g1q, pbm);
 }
 
+// The same from values already grouped by (session, group) segment - the layout a shard's
+// fz_rq4b_ex output and fz_runs_merge leave: no key pass and no sort
+void rq4b_session_stats_grouped(fz_ctx *c, const double *values, const int64_t *offs2, int64_t n, int64_t S,
+                                int64_t max_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q, double *pbm) {
+    const int64_t MM = S > 0 ? S : 1;
+    FZ_CHECK(2 * MM < (int64_t(1) << 32), "fz_rq4b_session_stats_grouped: too many sessions");
+    int64_t *d_n = c->arena.get<int64_t>(1);
+    set_i64(c, d_n, &n, 1);
+    const uint32_t *sid2 = reinterpret_cast<const uint32_t *>(segment_ids(c, Segs{2 * MM, offs2, n}));
+    const int64_t half = max_len > 0 && max_len < n ? max_len : n;
+    rq4b_sessions(c, values, sid2, n, d_n, MM, half, 2 * half < n ? 2 * half : n, c2, c1, g2q, g1q, pbm, offs2);
+}
+
 void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *o) {
     Store &s = store_of(c);
     FZ_CHECK(s.built, "fz_rq4b: call fz_store_build first");
@@ -423,16 +441,13 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
         atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ4B_SESSIONS]),
                   (unsigned long long)(foffs[p + 1] - foffs[p]));
     });
-    if (o->trend_values && o->trend_offsets) {  // the shard's contribution to the session exchange
-        double *tvals = o->trend_values;
-        int64_t *toffs = o->trend_offsets;
-        map_n(c, NC, d_nf, [=] __device__(int64_t j) { tvals[j] = cov[frow[j]]; });
-        map_n(c, P + 1, nullptr, [=] __device__(int64_t p) { toffs[p] = foffs[p]; });
-    }
     const bool sharded = flags & FZ_RQ4B_SKIP_SESSION_STATS;
+    // a shard's contribution to the session exchange: its values grouped by (session, group)
+    // segment, as the unsharded path groups them before the statistics
+    const bool contribute = o->trend_values && o->trend_offsets;
     int64_t *c2 = o->c2, *c1 = o->c1;
     double *g2q = o->g2_q, *g1q = o->g1_q;
-    if (!sharded) {
+    if (!sharded || contribute) {
         // (session, group) key per value: G2 -> group 0 (x), G1 -> group 1 (y); the values are in
         // project order, so the stable sort on (session, group) alone keeps projects in order
         // the values (read in view order: rising rows) ride along as the sort's payload - no random
@@ -458,13 +473,16 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
         uint32_t *no_vals = nullptr;
         radix_sort_pairs_payload32(c, key, no_vals, NC, sbits, pl);
         const double *sfv = static_cast<const double *>(pl.out[0]);
-        double *v2 = c->arena.get<double>(NC);
+        double *v2 = contribute ? o->trend_values : c->arena.get<double>(NC);
         uint32_t *sid2 = c->arena.get<uint32_t>(NC);
         map_n(c, NC, nullptr, [=] __device__(int64_t k) {
             sid2[k] = uint32_t(key[k]);
             if (k < *d_nf) v2[k] = sfv[k];
         });
-        rq4b_sessions(c, v2, sid2, NC, d_nf, MM, P, P, c2, c1, g2q, g1q, o->p_bm);  // <= 1 value per project
+        if (contribute) segment_offsets_dn(c, sid2, d_nf, NC, S2, o->trend_offsets);
+        if (!sharded)
+            rq4b_sessions(c, v2, sid2, NC, d_nf, MM, P, P, c2, c1, g2q, g1q, o->p_bm,
+                          contribute ? o->trend_offsets : nullptr);  // <= 1 value per project
     }
     // last session with both groups >= 100 (:849-860); Spearman of the quartile sequences (:879-899)
     if (!sharded) {

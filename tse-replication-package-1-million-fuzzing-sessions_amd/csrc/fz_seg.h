@@ -59,6 +59,11 @@ struct ChunkMap {
 ChunkMap make_chunks(fz_ctx *c, const Segs &sg);
 // seg id of every element (binary search over offsets); elements past offs[S] get S.
 int32_t *segment_ids(fz_ctx *c, const Segs &sg);
+// Segment-major merge of R runs, each grouped by segment: sizes [R * S] (run r's count of segment s
+// at r * S + s), values = the runs one after another -> out (segment s: run 0's values, run 1's,
+// ...) and out_offs [S + 1]
+void runs_merge(fz_ctx *c, const double *values, const int64_t *sizes, int64_t R, int64_t S, double *out,
+                int64_t *out_offs);
 
 // Chunk k of a segmented reduction.  Explicit maps (cm.d_n != null) list the chunks; implicit
 // ones (cps chunks per segment, chosen on the host when every segment is short) derive chunk k

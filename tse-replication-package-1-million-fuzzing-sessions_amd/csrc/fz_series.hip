@@ -1692,4 +1692,46 @@ void levene_two(fz_ctx *c, const uint64_t *skx, const double *x, int64_t nxm, co
     });
 }
 
+// ------------------------------------------------------------------------------ session exchange
+// A session owner receives, from each of R shards, that shard's values of its sessions grouped by
+// segment (session, or session x group) - R runs one after another.  The merge interleaves them
+// segment by segment: segment s holds run 0's values of s, then run 1's, ... (= global project
+// order, the order the single-table path's stable sort gives).  One wave per (run, segment) copies
+// its contiguous values: coalesced reads and writes, no sort.
+__global__ void k_runs_merge(const double *__restrict__ in, const int64_t *__restrict__ sizes,
+                             const int64_t *__restrict__ in_start, const int64_t *__restrict__ out_offs, int64_t R,
+                             int64_t S, double *__restrict__ out) {
+    const int64_t nw = int64_t(gridDim.x) * (blockDim.x / kWave);
+    const int lane = lane_id();
+    for (int64_t q = int64_t(blockIdx.x) * (blockDim.x / kWave) + wave_id(); q < R * S; q += nw) {
+        const int64_t n = sizes[q];
+        if (n == 0) continue;
+        const int64_t r = q / S, s = q - r * S;
+        int64_t dst = out_offs[s];
+        for (int64_t k = 0; k < r; ++k) dst += sizes[k * S + s];
+        const int64_t src = in_start[q];
+        for (int64_t j = lane; j < n; j += kWave) out[dst + j] = in[src + j];
+    }
+}
+
+void runs_merge(fz_ctx *c, const double *values, const int64_t *sizes, int64_t R, int64_t S, double *out,
+                int64_t *out_offs) {
+    int64_t *in_start = c->arena.get<int64_t>(R * S > 0 ? R * S : 1);
+    int64_t *tot = c->arena.get<int64_t>(S + 1);
+    if (R * S > 0) scan_exclusive_i64(c, sizes, in_start, R * S, nullptr);
+    map_n(c, S + 1, nullptr, [=] __device__(int64_t s) {
+        int64_t t = 0;
+        if (s < S)
+            for (int64_t r = 0; r < R; ++r) t += sizes[r * S + s];
+        tot[s] = t;
+    });
+    scan_exclusive_i64(c, tot, out_offs, S + 1, nullptr);
+    if (R * S == 0) return;
+    const int64_t waves = R * S;
+    const int64_t blocks = (waves + kBlock / kWave - 1) / (kBlock / kWave);
+    k_runs_merge<<<unsigned(blocks < 16384 ? blocks : 16384), kBlock, 0, c->stream>>>(values, sizes, in_start,
+                                                                                     out_offs, R, S, out);
+    FZ_LAUNCH_CHECK();
+}
+
 }  // namespace fz

@@ -314,10 +314,12 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
     static_assert(MAXN <= (1 << kBlkPosBits) && MAXN % BS == 0, "bucket sort shape");
     // 16-bit bucket counts, then bucket starts (+ sentinel; every count and start is <= MAXN <=
     // 16384), the rows in bucket order; after the ranking the same bytes are the u64 staging of the
-    // fused gather.  (16-bit counters: the 16384-row class fits two workgroups per CU - 67 KiB of LDS
-    // instead of 102 KiB with 32-bit ones.)
+    // fused gather.  (16-bit counters: 32 KiB of counters and positions for the 16384-row class.)
     constexpr int CNT_BYTES = ((EPT * BS + 1) * 2 + 15) / 16 * 16;
-    __shared__ alignas(16) uint8_t s_mem[CNT_BYTES + MAXN * 2];
+    // (the long class stages a whole segment's column at once in the same bytes: one round per
+    // column instead of two; 128 KiB - one workgroup per CU, as its registers allow anyway)
+    constexpr int MEM_BYTES = KEYS_LDS || CNT_BYTES + MAXN * 2 >= MAXN * 8 ? CNT_BYTES + MAXN * 2 : MAXN * 8;
+    __shared__ alignas(16) uint8_t s_mem[MEM_BYTES];
     uint16_t *const s_cnt = reinterpret_cast<uint16_t *>(s_mem);
     uint32_t *const s_cnt32 = reinterpret_cast<uint32_t *>(s_mem);  // word q / 2 holds counters q, q ^ 1
     uint16_t *const s_pos = reinterpret_cast<uint16_t *>(s_mem + CNT_BYTES);  // rows in bucket order
@@ -445,16 +447,21 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
             dq[m] = -1;
             if (i >= n) continue;
             const uint32_t st = s_cnt[bs[m] >> 16], en = s_cnt[(bs[m] >> 16) + 1];
-            const uint64_t key = row_key(t[m], i);
-            const uint32_t my_tie = tiemode && en - st > 1 ? tie_of(i) : 0u;
+            if (en - st <= 1) {  // alone in its bucket - the common case for evenly spread times
+                dq[m] = int32_t(st);
+                continue;
+            }
+            // (the long class re-reads its own time: t[] need not stay live past the bucketing)
+            const int64_t tm = KEYS_LDS ? t[m] : time[b + i];
+            const uint64_t key = row_key(tm, i);
+            const uint32_t my_tie = tiemode ? tie_of(i) : 0u;
             uint32_t rank = 0;
-            // (a row alone in its bucket - the common case for evenly spread times - reads nothing)
-            for (uint32_t x = st; en - st > 1 && x < en; ++x) {
+            for (uint32_t x = st; x < en; ++x) {
                 const int ox = s_pos[x];
                 if (ox == i) continue;
                 if (tiemode) {  // (time, prefix position): no packed key, any span
                     const int64_t tx = time[b + ox];
-                    rank += tx < t[m] || (tx == t[m] && tie_of(ox) < my_tie);
+                    rank += tx < tm || (tx == tm && tie_of(ox) < my_tie);
                     continue;
                 }
                 uint64_t kx;
@@ -481,12 +488,12 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         // of the segment goes through LDS in sorted order (row i's value to slot dq[m]), then out in
         // sorted order - the sorted rows' time, caller row id and gathered columns; project, row id and
         // the kGathered marker (which tells k_store_gather to skip the row) are written directly.
-        // Staging: the key array (8-byte slots for the whole segment) or the bucket counts (half a
-        // segment per round).  (A separate gather would re-read the 250 KB segment at random from
+        // Staging: the key array (8-byte slots for the whole segment) or, in the long class, the
+        // counter bytes sized for a whole segment's column (one round per column).  (A separate gather would re-read the 250 KB segment at random from
         // HBM; the short classes' segments stay in L2 and gather faster than they stage.)
         uint64_t *stg = KEYS_LDS ? s_key : reinterpret_cast<uint64_t *>(s_mem);
-        constexpr int CAP = KEYS_LDS ? MAXN : MAXN / 2;
-        static_assert(KEYS_LDS || (CNT_BYTES + MAXN * 2) / 8 >= CAP, "gather staging");
+        constexpr int CAP = MAXN;
+        static_assert(KEYS_LDS || MEM_BYTES / 8 >= CAP, "gather staging");
         // stage one column (x[m]: row i's value) through LDS in sorted order, write it coalesced
         auto emit = [&](const uint64_t *x, auto store) {
             for (int h = 0; h < n; h += CAP) {

@@ -149,6 +149,8 @@ SIGNATURES = {
     "fz_rq2_count": (C.c_int, [_P, C.POINTER(FzRq2CountOut)]),
     "fz_rq2_count_ex": (C.c_int, [_P, C.c_uint32, C.POINTER(FzRq2CountOut)]),
     "fz_rq2_session_stats": (C.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P]),
+    "fz_rq2_session_stats_grouped": (C.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P]),
+    "fz_runs_merge": (C.c_int, [_P, _P, _P, _I64, _I64, _P, _P]),
     "fz_series_tests": (C.c_int, [_P, _P, _I64, _P]),
     "fz_spearman_index_seg": (C.c_int, [_P, _P, _I64, _P, _I64, _I64, _P, _P]),
     "fz_rq2_add": (C.c_int, [_P, C.POINTER(FzRq2AddOut)]),
@@ -161,6 +163,7 @@ SIGNATURES = {
     "fz_rq4b": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.POINTER(FzRq4bOut)]),
     "fz_rq4b_ex": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.c_uint32, C.POINTER(FzRq4bOut)]),
     "fz_rq4b_session_stats": (C.c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P]),
+    "fz_rq4b_session_stats_grouped": (C.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P]),
     "fz_two_sample_tests": (C.c_int, [_P, _P, _I64, _P, _I64, _P]),
     "fz_buildlog": (C.c_int, [_P, _P, _I64, _P, _P, _I64, C.POINTER(FzBuildlogOut)]),
     "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),

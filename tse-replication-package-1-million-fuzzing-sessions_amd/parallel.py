@@ -178,15 +178,18 @@ def all_gather_v(x):
     return [o[:k] for o, k in zip(all_gather(buf), sizes)]
 
 
-def all_to_all_v(x, send_counts):
+def all_to_all_v(x, send_counts, recv_counts=None):
     """Variable all-to-all of a 1-D tensor: x holds the rows for rank 0, then rank 1, ...
-    (send_counts[d] rows each) -> the rows every rank sent here, in source-rank order."""
+    (send_counts[d] rows each) -> the rows every rank sent here, in source-rank order.
+    recv_counts: what each rank sends here, when the caller knows it (no count exchange)."""
     import torch
     dist = _dist()
     world = dist.get_world_size()
-    sc = torch.tensor([int(v) for v in send_counts], dtype=torch.int64, device=x.device)
-    rc = torch.cat(all_gather(sc)).reshape(world, world)[:, dist.get_rank()]
-    recv = [int(v) for v in rc.tolist()]
+    if recv_counts is None:
+        sc = torch.tensor([int(v) for v in send_counts], dtype=torch.int64, device=x.device)
+        rc = torch.cat(all_gather(sc)).reshape(world, world)[:, dist.get_rank()]
+        recv_counts = rc.tolist()
+    recv = [int(v) for v in recv_counts]
     send = [int(v) for v in send_counts]
     if _staged(x):
         h = x.cpu()
@@ -321,8 +324,8 @@ def rq3_sharded(shard, rank: int, world: int):
             got = all_gather_cols([part[k] for k in keys])
             for j, k in enumerate(keys):
                 cols[k] = [got[r][j] for r in range(world)]
-    else:
-        cl = host_many(counts)
+    else:  # (a shard that read its counters already hands over the host copy)
+        cl = [part["counts_h"]] if "counts_h" in part else host_many(counts)
         cols = {k: [part[k]] for k in RQ3_DET_F + RQ3_DET_I + RQ3_NON_F + RQ3_NON_I}
     with_issues = [r for r in range(world) if cl[r][RQ3_ISSUES] > 0]
     last = with_issues[-1] if with_issues else -1
@@ -342,6 +345,35 @@ def rq3_sharded(shard, rank: int, world: int):
     total[RQ3_NULL_LAST] = 0
     st = shard.stats(out["det_pct"], out["det_tot"], out["non_pct"])
     return total, out, st
+
+
+# ------------------------------------------------------------------------------ session exchange
+def merge_runs_torch(vals, runs):
+    """fz_runs_merge on any device with torch ops (the CPU tests' shards): vals = R runs one after
+    another, each grouped by segment; runs [R, S] their sizes -> (values segment by segment, run
+    order inside a segment; offsets [S + 1])."""
+    import torch
+    R, S = runs.shape
+    sz = runs.reshape(-1).tolist()
+    st = np.concatenate([[0], np.cumsum(sz)]).astype(np.int64)
+    pieces = [vals[st[r * S + s]:st[r * S + s] + sz[r * S + s]] for s in range(S) for r in range(R)]
+    out = torch.cat(pieces) if pieces else vals[:0]
+    offs = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(runs.sum(0).to(torch.int64).cpu(), 0)])
+    return out, offs.to(vals.device)
+
+
+def exchange_grouped(shard, vals, offs_h, mat, mat_h, own, rank, k=1):
+    """Send this rank's segment-grouped values (k segments per session: offs_h its host offsets) to
+    the owners of their sessions and merge what arrives.  mat [world, k * M] (device) / mat_h (host):
+    every rank's segment sizes; own: the owners' session ranges.  One all-to-all whose receive
+    counts come from mat (no count exchange), then shard.merge_runs -> (values of the sessions
+    [a, b) this rank owns, grouped by segment with the sources in rank order; offsets)."""
+    n_loc = len(offs_h) - 1
+    a, b = own[rank]
+    send = [int(offs_h[min(k * hi, n_loc)] - offs_h[min(k * lo, n_loc)]) for lo, hi in own]
+    recv = [int(v) for v in mat_h[:, k * a:k * b].sum(1)]
+    got = all_to_all_v(vals, send, recv)
+    return shard.merge_runs(got, mat[:, k * a:k * b].contiguous())
 
 
 # ----------------------------------------------------------------------------------- RQ2 count
@@ -364,12 +396,14 @@ def session_owners(sizes: np.ndarray, world: int) -> List[Tuple[int, int]]:
 def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_values: bool = True):
     """Exact RQ2 count over project shards (rq2_coverage_count.py:244-483).
     ``shard.run()`` -> per-project columns over the global project axis (RQ2C_PROJECT_COLS), the
-    local session-major trend values and session offsets; ``shard.session_stats(values, sids, S,
-    max_len)`` -> average / median / percentiles[S * 5] / ge100 of the sessions it owns;
-    ``shard.series_tests(x)`` -> (rho, p, W, p); ``shard.mean_median(x)`` -> (mean, median).
-    Exchange: per-project columns gathered (projects [lo, hi) of every rank), session sizes
-    all-reduced, values all-to-all'd to the owner of their session index, per-session results
-    gathered.  Returns a dict of host numpy arrays (every rank)."""
+    local trend values grouped by session index (project order inside a session) and their session
+    offsets; ``shard.merge_runs(values, runs)`` -> fz_runs_merge; ``shard.session_stats_grouped(
+    values, offsets, S, max_len)`` -> average / median / percentiles[S * 5] / ge100 of the sessions it
+    owns; ``shard.series_tests(x)`` -> (rho, p, W, p); ``shard.mean_median(x)`` -> (mean, median).
+    Exchange: per-project columns and every rank's session sizes gathered (projects [lo, hi) of
+    every rank), each rank's values of a session range sent to its owner as one contiguous slice
+    (all-to-all) and merged in rank order, per-session results gathered.  Returns a dict of host
+    numpy arrays (every rank)."""
     import torch
     part = shard.run()
     dev = part["session_values"].device
@@ -380,28 +414,26 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
         pc = [torch.cat([got[r][j] for r in range(world)]) for j in range(len(pc))]
     offs = part["session_offsets"]
     m_loc = offs.numel() - 1
-    loc_sizes = (offs[1:] - offs[:-1]).to(torch.int64)
     M = agree_max(m_loc, dev) if world > 1 else m_loc
-    # session sizes, then the NULL-line count (rq2_coverage_count.py:300-303 raise), summed at once
-    sizes = torch.zeros(M + 1, dtype=torch.int64, device=dev)
-    sizes[:m_loc] = loc_sizes
+    # this rank's session sizes, then its NULL-line count (rq2_coverage_count.py:300-303 raise)
+    row = torch.zeros(M + 1, dtype=torch.int64, device=dev)
+    row[:m_loc] = offs[1:] - offs[:-1]
     if part.get("null_lines") is not None:
-        sizes[M:] = part["null_lines"].to(torch.int64).reshape(1)
-    if world > 1:
-        all_reduce(sizes)
-    h = host_many(sizes, offs, *pc)  # one device->host copy
-    sizes_h, null_lines, offs_h = h[0][:M], int(h[0][M]), h[1]
+        row[M:] = part["null_lines"].to(torch.int64).reshape(1)
+    mat = torch.stack(all_gather(row)) if world > 1 else row[None]
+    h = host_many(mat, offs, *pc)  # one device->host copy
+    mat_h, offs_h = h[0], h[1]
+    sizes_h, null_lines = mat_h[:, :M].sum(0), int(mat_h[:, M].sum())
     proj = dict(zip(RQ2C_PROJECT_COLS, h[2:]))
     own = session_owners(sizes_h, world)
-    nv = int(offs_h[-1])
-    vals = part["session_values"][:nv]
-    sids = torch.repeat_interleave(torch.arange(m_loc, dtype=torch.int64, device=dev), loc_sizes, output_size=nv)
-    send = [int(offs_h[min(b, m_loc)] - offs_h[min(a, m_loc)]) for a, b in own]
-    if world > 1:
-        vals, sids = all_to_all_cols([vals, sids], send)
     a, b = own[rank]
-    st = shard.session_stats(vals, sids - a, b - a, len(proj["eligible"]))
     S = b - a
+    vals = part["session_values"][:int(offs_h[-1])]
+    if world > 1:
+        vals, goffs = exchange_grouped(shard, vals, offs_h, mat[:, :M], mat_h[:, :M], own, rank)
+    else:
+        goffs = offs
+    st = shard.session_stats_grouped(vals, goffs, S, len(proj["eligible"]))
     block = torch.cat([st["average"][:S, None], st["median"][:S, None], st["percentiles"][:5 * S].reshape(S, 5)], 1)
     if world > 1:  # per-session rows (average, median, 5 percentiles) of every owner, session order
         block = torch.cat([m.reshape(-1, 7).view(torch.float64) for m in all_gather_v(block.reshape(-1).view(
@@ -419,13 +451,8 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
            "average": res["average"], "median": res["median"], "percentiles": res["percentiles"],
            "tests": tests, "corr_mm": corr_mm, "null_lines": null_lines}
     if gather_values:  # coverage_by_session_index.csv: every value, session-major, project order
-        if world > 1:
-            got = all_gather_cols([vals, sids])
-            gv = torch.cat([g[0] for g in got]).cpu().numpy()
-            gs = torch.cat([g[1] for g in got]).cpu().numpy()
-        else:
-            gv, gs = vals.cpu().numpy(), sids.cpu().numpy()
-        out["session_values"] = gv[np.argsort(gs, kind="stable")]
+        gv = torch.cat(all_gather_v(vals)) if world > 1 else vals
+        out["session_values"] = gv.cpu().numpy()
     return out
 
 
@@ -475,50 +502,44 @@ def rq4a_sharded(shard, rank: int, world: int, lo: int, hi: int):
 
 def rq4b_sharded(shard, rank: int, world: int):
     """Exact RQ4b over project shards (rq4b_coverage.py:1209-1261).  ``shard.run()`` -> counts,
-    member[P], the G1/G2 full coverage series (trend_values, trend_offsets[P + 1]), the delta columns
-    (pre_cov / post_cov step-major, delta_order = CSV row of each column; at least counts' lengths)
-    and the initial-coverage samples;
-    ``shard.session_stats(values, sids, groups, S, max_len)``, ``shard.spearman_prefix(rows, n)``,
-    ``shard.row_medians(rows)`` and ``shard.two_sample(x, y)`` run the statistics (tensors or arrays
-    in, tensors or arrays out).  Exchange: session sizes all-reduced, (value, session, group) triples
-    all-to-all'd to the owner of the session index, per-session results, delta columns (re-ordered
-    by CSV row, :216, :744) and initial samples gathered.  Intermediates stay on the device; the
-    results are copied to the host once.  Returns a dict for rq/compute.rq4b_result (host arrays,
-    every rank)."""
+    member[P], the G1/G2 full coverage values grouped by (session index, group) segment
+    (trend_values; trend_offsets over 2 * sessions segments, G2 = group 0; project order inside a
+    segment), the delta columns (pre_cov / post_cov step-major, delta_order = CSV row of each
+    column; at least counts' lengths) and the initial-coverage samples;
+    ``shard.merge_runs(values, runs)``, ``shard.session_stats_grouped(values, offsets, S, max_len)``,
+    ``shard.spearman_prefix(rows, n)``, ``shard.row_medians(rows)`` and ``shard.two_sample(x, y)``
+    run the statistics (tensors or arrays in, tensors or arrays out).  Exchange: every rank's
+    segment sizes gathered, each rank's values of a session range sent to its owner as one
+    contiguous slice (all-to-all) and merged in rank order, per-session results, delta columns
+    (re-ordered by CSV row, :216, :744) and initial samples gathered.  Intermediates stay on the
+    device; the results are copied to the host once.  Returns a dict for rq/compute.rq4b_result
+    (host arrays, every rank)."""
     import torch
     part = shard.run()
     counts = part["counts"].clone()
     dev = counts.device
     P = part["member"].numel()
-    offs = part["trend_offsets"]
-    lens = (offs[1:] - offs[:-1]).to(torch.int64)
-    head = torch.stack([offs[-1].to(torch.int64), lens.max() if P > 0 else offs[-1].to(torch.int64) * 0,
-                        counts[RQ4B_DELTA_PROJECTS], counts[RQ4B_INIT_G2], counts[RQ4B_INIT_G1]])
-    n, m_loc, nd, n2, n1 = (int(v) for v in host_many(head)[0])  # one sync for every host-side size
+    offs_all = part["trend_offsets"]
+    head = torch.stack([counts[RQ4B_SESSIONS], offs_all[-1].to(torch.int64), counts[RQ4B_DELTA_PROJECTS],
+                        counts[RQ4B_INIT_G2], counts[RQ4B_INIT_G1]])
+    m_loc, n, nd, n2, n1 = (int(v) for v in host_many(head)[0])  # one sync for every host-side size
+    offs2 = offs_all[:2 * m_loc + 1]
     vals = part["trend_values"][:n]
-    starts = torch.repeat_interleave(offs[:-1], lens, output_size=n)
-    sids = torch.arange(n, dtype=torch.int64, device=dev) - starts
-    grp = torch.repeat_interleave(((part["member"].to(torch.int64) & 2) == 0).to(torch.uint8), lens, output_size=n)
     M = agree_max(m_loc, dev) if world > 1 else m_loc
-    sizes = torch.zeros(M, dtype=torch.int64, device=dev)
-    if n:
-        sizes.scatter_add_(0, sids, torch.ones_like(sids))
     if world > 1:
-        all_reduce(sizes)
+        row = torch.zeros(2 * M, dtype=torch.int64, device=dev)
+        row[:2 * m_loc] = offs2[1:] - offs2[:-1]
+        mat = torch.stack(all_gather(row))  # [world, 2M]: every rank's (session, group) sizes
         all_reduce(counts)
-        own = session_owners(host_many(sizes)[0], world)
-        # route every value to the owner of its session index
-        cuts = torch.tensor([b for _, b in own], dtype=torch.int64, device=dev)
-        dest = torch.searchsorted(cuts, sids, right=True)
-        perm = torch.argsort(dest, stable=True)
-        send = torch.bincount(dest, minlength=world).tolist() if n else [0] * world
-        vals, sids, grp = all_to_all_cols([vals[perm], sids[perm], grp[perm]], send)
-        grp = grp.to(torch.uint8)
+        mat_h, offs_h = host_many(mat, offs2)
+        own = session_owners(mat_h[:, 0::2].sum(0) + mat_h[:, 1::2].sum(0), world)
+        vals, goffs = exchange_grouped(shard, vals, offs_h, mat, mat_h, own, rank, k=2)
     else:
         own = [(0, M)]
+        goffs = offs2
     a, b = own[rank]
     S = b - a
-    st = shard.session_stats(vals, sids - a, grp, S, P)
+    st = shard.session_stats_grouped(vals, goffs, S, P)
     # per-session rows (c2, c1, g2 quartiles, g1 quartiles, p_bm) of every owner, session order
     cols = [st["c2"][:S], st["c1"][:S]] + [st["g2_q"][:3 * S].reshape(S, 3)[:, j] for j in range(3)] + \
         [st["g1_q"][:3 * S].reshape(S, 3)[:, j] for j in range(3)] + [st["p_bm"][:S]]
@@ -598,7 +619,10 @@ class GpuRQ1Shard:
         self.b_time = eng.tables.cols["b_time"]
         self.i_number = eng.tables.cols["i_number"]
 
-    def run(self, ext):
+    pre = False  # launch() already enqueued the first run (a recorded local phase): run(None) reads it
+
+    def launch(self, ext=None):
+        """The first run's kernels alone (no host read: graph-capturable)."""
         E, C, eng, b = self.E, self.C, self.eng, self.bufs
         keep = None
         if ext is None:
@@ -608,6 +632,12 @@ class GpuRQ1Shard:
             x = E.FzRq1Ext(keep[0].numel(), C.c_void_p(keep[0].data_ptr()), C.c_void_p(keep[1].data_ptr()),
                            C.c_void_p(keep[2].data_ptr()))
         E._check(eng.lib, eng.lib.fz_rq1_ex(eng.ctx, self.threshold, C.byref(x), C.byref(b.out)))
+
+    def run(self, ext):
+        b = self.bufs
+        if ext is not None or not self.pre:
+            self.launch(ext)
+        self.pre = False
         n = int(b.counts[RQ1_MATCHED].item())
         mi, mb = b.matched_issue[:n], b.matched_build[:n]
         return {"counts": b.counts, "iter_total": b.iter_total, "iter_detected": b.iter_detected,
@@ -630,9 +660,17 @@ class GpuRQ2CountShard:
         self.E, self.C, self.eng = E, C, eng
         self.bufs = compute.rq2_count_buffers(eng)
 
-    def run(self):
+    pre = False  # launch() already enqueued this step's local kernels (a recorded local phase)
+
+    def launch(self):
         E, C, eng, b = self.E, self.C, self.eng, self.bufs
         E._check(eng.lib, eng.lib.fz_rq2_count_ex(eng.ctx, E.FZ_RQ2C_SKIP_SESSION_STATS, C.byref(b.out)))
+
+    def run(self):
+        E, b = self.E, self.bufs
+        if not self.pre:
+            self.launch()
+        self.pre = False
         ns = int(b.counts[E.RQ2C_SESSIONS].item())
         out = {k: getattr(b, k) for k in RQ2C_PROJECT_COLS}
         out["null_lines"] = b.counts[E.RQ2C_NULL_LINES:E.RQ2C_NULL_LINES + 1]
@@ -640,14 +678,49 @@ class GpuRQ2CountShard:
         out["session_values"] = b.session_values
         return out
 
-    def session_stats(self, vals, sids, S, max_len):
-        return gpu_session_stats(self.eng, vals, sids, S, max_len)
+    def session_stats_grouped(self, vals, offs, S, max_len):
+        return gpu_session_stats_grouped(self.eng, vals, offs, S, max_len)
+
+    def merge_runs(self, vals, runs):
+        return gpu_merge_runs(self.eng, vals, runs)
 
     def series_tests(self, x):
         return gpu_series_tests(self.eng, x)
 
     def mean_median(self, x):
         return gpu_mean_median(self.eng, x)
+
+
+def gpu_merge_runs(eng, vals, runs):
+    """fz_runs_merge: R runs of segment-grouped values (runs [R, S] device sizes) -> (values
+    segment by segment, offsets [S + 1]); device."""
+    import ctypes as C
+    from . import engine as E
+    torch = eng.torch
+    R, S = runs.shape
+    vals, runs = vals.contiguous(), runs.to(torch.int64).contiguous()
+    out = torch.empty(max(vals.numel(), 1), dtype=torch.float64, device=eng.dev)
+    offs = torch.empty(S + 1, dtype=torch.int64, device=eng.dev)
+    P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+    E._check(eng.lib, eng.lib.fz_runs_merge(eng.ctx, P(vals), P(runs), R, S, P(out), P(offs)))
+    return out[:vals.numel()], offs
+
+
+def gpu_session_stats_grouped(eng, vals, offs, S, max_len):
+    """fz_rq2_session_stats_grouped: per-session mean / median / percentiles of values grouped by
+    session (offsets [S + 1])."""
+    import ctypes as C
+    from . import engine as E
+    torch = eng.torch
+    avg = torch.empty(max(S, 1), dtype=torch.float64, device=eng.dev)
+    med = torch.empty_like(avg)
+    pct = torch.empty(max(5 * S, 1), dtype=torch.float64, device=eng.dev)
+    ge = torch.zeros(1, dtype=torch.int64, device=eng.dev)
+    vals, offs = vals.contiguous(), offs.contiguous()
+    P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+    E._check(eng.lib, eng.lib.fz_rq2_session_stats_grouped(eng.ctx, P(vals), P(offs), vals.numel(), S, max_len,
+                                                           P(avg), P(med), P(pct), P(ge)))
+    return {"average": avg, "median": med, "percentiles": pct, "ge100": ge}
 
 
 def gpu_session_stats(eng, vals, sids, S, max_len):
@@ -716,6 +789,22 @@ def gpu_rq4b_session_stats(eng, vals, sids, grp, S, max_len):
     return out
 
 
+def gpu_rq4b_session_stats_grouped(eng, vals, offs2, S, max_len):
+    """fz_rq4b_session_stats_grouped: the same from values grouped by (session, group) segment
+    (offsets [2 * S + 1])."""
+    import ctypes as C
+    from . import engine as E
+    torch = eng.torch
+    z = lambda n, dt: torch.zeros(max(n, 1), dtype=dt, device=eng.dev)  # noqa: E731
+    out = {"c2": z(S, torch.int64), "c1": z(S, torch.int64), "g2_q": z(3 * S, torch.float64),
+           "g1_q": z(3 * S, torch.float64), "p_bm": z(S, torch.float64)}
+    vals, offs2 = vals.contiguous(), offs2.contiguous()
+    P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+    E._check(eng.lib, eng.lib.fz_rq4b_session_stats_grouped(eng.ctx, P(vals), P(offs2), vals.numel(), S, max_len,
+                                                            *[P(out[k]) for k in ("c2", "c1", "g2_q", "g1_q", "p_bm")]))
+    return out
+
+
 def gpu_mean_median(eng, x):
     """(mean, median) of one device vector through fz_describe_f64 (NaN when empty)."""
     if x.numel() == 0:
@@ -734,9 +823,17 @@ class GpuRQ4aShard:
         self.E, self.C, self.eng = E, C, eng
         self.bufs = compute.rq4a_buffers(eng, max_iter=max_iter)
 
-    def run(self):
+    pre = False  # launch() already enqueued this step's local kernels (a recorded local phase)
+
+    def launch(self):
         E, C, eng, b = self.E, self.C, self.eng, self.bufs
         E._check(eng.lib, eng.lib.fz_rq4a(eng.ctx, C.byref(eng.groups), C.byref(b.out)))
+
+    def run(self):
+        b = self.bufs
+        if not self.pre:
+            self.launch()
+        self.pre = False
         return {k: getattr(b, k) for k in ("counts", "member", "intro", "g4_steps", "g4_transition") + RQ4A_TABLES}
 
     def finish(self, tables, intro, steps, counts):
@@ -760,17 +857,30 @@ class GpuRQ4bShard:
         self.E, self.C, self.eng = E, C, eng
         self.bufs = compute.rq4b_buffers(eng, shard=True)
 
-    def run(self):
+    pre = False  # launch() already enqueued this step's local kernels (a recorded local phase)
+
+    def launch(self):
         E, C, eng, b = self.E, self.C, self.eng, self.bufs
         E._check(eng.lib, eng.lib.fz_rq4b_ex(eng.ctx, C.byref(eng.groups), E.FZ_RQ4B_SKIP_SESSION_STATS,
                                              C.byref(b.out)))
+
+    def run(self):
+        eng, b = self.eng, self.bufs
+        if not self.pre:
+            self.launch()
+        self.pre = False
         P = eng.tables.fz.n_projects  # column lengths stay on the device (counts); rq4b_sharded slices
+        # (trend_offsets: 2 * max_cov_per_project + 1 entries, the segments past the shard's
+        # longest series empty - its last entry is the number of values)
         return {"counts": b.counts, "member": b.member[:P], "trend_values": b.trend_values,
-                "trend_offsets": b.trend_offsets[:P + 1], "pre_cov": b.pre_cov, "post_cov": b.post_cov,
+                "trend_offsets": b.trend_offsets, "pre_cov": b.pre_cov, "post_cov": b.post_cov,
                 "delta_order": b.delta_order, "init_g2": b.init_g2, "init_g1": b.init_g1}
 
-    def session_stats(self, vals, sids, grp, S, max_len):
-        return gpu_rq4b_session_stats(self.eng, vals, sids, grp, S, max_len)
+    def session_stats_grouped(self, vals, offs2, S, max_len):
+        return gpu_rq4b_session_stats_grouped(self.eng, vals, offs2, S, max_len)
+
+    def merge_runs(self, vals, runs):
+        return gpu_merge_runs(self.eng, vals, runs)
 
     def series_tests(self, x):
         return gpu_series_tests(self.eng, x)
@@ -784,8 +894,8 @@ class GpuRQ4bShard:
     def row_medians(self, rows):
         """statistics.median of every row of a [k, n] device block (NaN for n == 0), one call; device."""
         k, n = rows.shape
-        sids = self.eng.torch.arange(k, dtype=self.eng.torch.int64, device=self.eng.dev).repeat_interleave(n)
-        out = gpu_session_stats(self.eng, rows.reshape(-1).contiguous(), sids, k, n)
+        offs = self.eng.torch.arange(k + 1, dtype=self.eng.torch.int64, device=self.eng.dev) * n
+        out = gpu_session_stats_grouped(self.eng, rows.reshape(-1).contiguous(), offs, k, n)
         return out["median"][:k]
 
     def two_sample(self, x, y):
@@ -808,12 +918,20 @@ class GpuRQ3Shard:
         self.E, self.C, self.eng = E, C, eng
         self.bufs = compute.rq3_buffers(eng)
 
-    def run(self):
+    pre = False  # launch() already enqueued this step's local kernels (a recorded local phase)
+
+    def launch(self):
         E, C, eng, b = self.E, self.C, self.eng, self.bufs
         E._check(eng.lib, eng.lib.fz_rq3_ex(eng.ctx, E.FZ_RQ3_FLUSH_LAST | E.FZ_RQ3_SKIP_STATS, C.byref(b.out)))
+
+    def run(self):
+        b = self.bufs
+        if not self.pre:
+            self.launch()
+        self.pre = False
         cnt = b.counts.cpu()
         nd, nn = int(cnt[RQ3_DETECTED]), int(cnt[RQ3_NON_DETECTED])
-        out = {"counts": b.counts}
+        out = {"counts": b.counts, "counts_h": cnt.numpy()}
         for k in RQ3_DET_F + RQ3_DET_I:
             out[k] = getattr(b, k)[:nd]
         for k in RQ3_NON_F + RQ3_NON_I:
