@@ -85,6 +85,7 @@ def parse():
     # the sharded step's host threads (one child engine + process group each), same syntax; two
     # threads measured best (same-box A/B, scripts/gpu_shard_ab.sh: the drivers are host-bound)
     ap.add_argument("--shard-groups", default="rq3,rq4b|rq2_count,rq1,rq4a,rq2_add")
+    ap.add_argument("--shard-graphs", action="store_true")
     return ap.parse_args()
 
 
@@ -223,6 +224,8 @@ def main():
                 else:
                     shards[n].pre = True
 
+        drv_ms = {}  # host wall time per driver (its launches, syncs and collectives), summed over steps
+
         def run_sharded(names):
             for name in names:
                 e = skids[name]
@@ -232,8 +235,10 @@ def main():
                     # and finishing kernels, as in the eager order)
                     sgraphs[name].launch()
                     mark_launched([name])
+                t_d = time.perf_counter()
                 with torch.cuda.stream(e.stream), par.use_group(sgroups[name]):
                     shard_step[name](e)
+                drv_ms[name] = drv_ms.get(name, 0.0) + (time.perf_counter() - t_d) * 1e3
         if not args.serial:
             from concurrent.futures import ThreadPoolExecutor
             pool = ThreadPoolExecutor(len(sthreads))
@@ -298,7 +303,10 @@ def main():
         for f in futs:
             f.result()
 
-    shard_graphs = sharded and pool is not None and not args.no_graphs
+    # (opt-in: replaying each driver's local kernels from a recording measured no faster than the
+    # eager launches - c2 3.79 vs 3.46 ms, c3 22.2 vs 21.8 ms, same box: the drivers' host work
+    # between their reads hides the launches already)
+    shard_graphs = sharded and pool is not None and args.shard_graphs and not args.no_graphs
     for _ in range(max(args.warmup, 1 if (concurrent or shard_graphs) and not args.no_graphs else 0)):
         step()
     torch.cuda.synchronize(dev)
@@ -342,6 +350,8 @@ def main():
     on_children = concurrent or (sharded and pool is not None)
     if not on_children:
         eng.probe_begin(args.probe)
+    if sharded:
+        drv_ms.clear()
     t0 = time.perf_counter()
     ev0.record(eng.stream)
     for _ in range(args.steps):
@@ -354,6 +364,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
+    drv = {k: round(v / args.steps, 3) for k, v in drv_ms.items()} if sharded else None
     probe_window = args.steps
     if not on_children:
         launches, probe_ms, probe_bytes = eng.probe_end()
@@ -375,7 +386,7 @@ def main():
         eng.probe_end()
         for k in TABLE_KERNELS:
             n, ms_k, b_k = eng.probe_get(k)
-            if n == 0 or ms_k <= 0:
+            if n == 0 or ms_k <= 0 or b_k <= 0:  # (no bytes: an empty input's launch, e.g. no issues)
                 continue
             ach = b_k / (ms_k * 1e-3) / 1e9
             tr = pmc_traffic(k, args.config)
@@ -424,6 +435,7 @@ def main():
                        "rows_per_rank": t.n_rows, "builds": int(len(t.b_project)), "coverage": int(len(t.c_project)),
                        "issues": int(len(t.i_project)), "stages": stages, "parallelism": f"project-shard x{world}" + (" (sharded path)" if sharded and world == 1 else ""),
                        "device_ms_per_step": round(dev_ms / args.steps, 4),
+                       **({"driver_host_ms": drv} if drv else {}),
                        # end-to-end (host columns -> HBM upload + one step), per rank: the loader's
                        # PCIe-inclusive rate; `value` is compute-only with inputs resident in HBM
                        "upload_ms": round(upload_ms, 3), "upload_host_ms": up["host_ms"],

@@ -444,10 +444,19 @@ int fz_rq4b_session_stats(fz_ctx *ctx, const double *values, const int64_t *sess
 /* fz_rq4b_session_stats over values already grouped by (session, group) segment: segment 2s holds
  * session s's G2 values, 2s + 1 its G1 values, values[segment_offsets[k], segment_offsets[k + 1])
  * (segment_offsets [2 * n_sessions + 1], device, offsets[0] = 0) - the layout of a shard's
- * fz_rq4b_ex trend output and of fz_runs_merge over 2 * n_sessions segments. */
+ * fz_rq4b_ex trend output and of fz_runs_merge over 2 * n_sessions segments.  max_session_len: host
+ * bound of one WHOLE session (both groups; the number of projects - one value per project), 0 if
+ * unknown. */
 int fz_rq4b_session_stats_grouped(fz_ctx *ctx, const double *values, const int64_t *segment_offsets,
                                   int64_t n_values, int64_t n_sessions, int64_t max_session_len, int64_t *c2,
                                   int64_t *c1, double *g2_q, double *g1_q, double *p_bm);
+
+/* RQ4b's trend tests from the per-session tables (device, n_sessions entries; quartiles [s * 3 + j]):
+ * *last = the last session index with both groups >= 100 (:849-860; -1 if none) and spearman6 =
+ * (rho, p) vs index of G1 Q1 / Med / Q3, then G2 Q1 / Med / Q3 over sessions 0..last (:879-899) -
+ * what fz_rq4b computes after its session statistics, for the sharded path's gathered tables. */
+int fz_rq4b_trends(fz_ctx *ctx, const int64_t *c2, const int64_t *c1, const double *g2_q, const double *g1_q,
+                   int64_t n_sessions, int64_t *last, double *spearman6);
 
 /* Two-sample tests of rq4b's initial coverage (:248-313) on device samples x (G2) and y (G1):
  * out[FZ_RQ4B_MWU_P .. FZ_RQ4B_LEVENE_P] = mannwhitneyu two-sided p, Cliff's delta from
@@ -516,6 +525,9 @@ int fz_graph_destroy(fz_graph *graph);
 int fz_radix_sort_u64(fz_ctx *ctx, uint64_t *keys, uint32_t *vals, int64_t n, int bits);
 /* numpy-compatible describe of a device fp64 vector (sorts a scratch copy). */
 int fz_describe_f64(fz_ctx *ctx, const double *x, int64_t n, fz_describe *host_out);
+/* The same into a device fz_describe (no host read: the sharded drivers copy it with their other
+ * results). */
+int fz_describe_f64_dev(fz_ctx *ctx, const double *x, int64_t n, fz_describe *dev_out);
 /* Per-project count of total_coverage rows with coverage valid, > 0 and date < limit
  * (the GROUP BY/HAVING of rq1_detection_rate.py:144-152), on the unsorted table. */
 int fz_eligibility_count(fz_ctx *ctx, const fz_tables *t, int64_t date_limit, int32_t *counts);

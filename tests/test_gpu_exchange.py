@@ -82,7 +82,8 @@ def test_grouped_session_stats_match_id_path(engine, lengths):
 @pytest.mark.gpu
 @pytest.mark.parametrize("sizes", [[(3, 4), (0, 0), (7, 7), (120, 90), (1, 0), (0, 9)],
                                    [(200, 150)] * 40 + [(6, 5)] * 300,
-                                   [(20_000, 16_000), (5, 30_000), (0, 2)]])
+                                   [(20_000, 16_000), (5, 30_000), (0, 2)],
+                                   [(6000, 5000), (3000, 3000), (7, 9)]])
 def test_rq4b_grouped_matches_oracle(engine, sizes):
     from oracle import rq_oracle as orc
     from tse_amd.parallel import gpu_rq4b_session_stats_grouped
@@ -99,7 +100,7 @@ def test_rq4b_grouped_matches_oracle(engine, sizes):
     S = len(sizes)
     got = gpu_rq4b_session_stats_grouped(engine, torch.from_numpy(np.concatenate(vals)).to(engine.dev),
                                          torch.from_numpy(offs2).to(engine.dev), S,
-                                         max(max(a, b) for a, b in sizes))
+                                         max(a + b for a, b in sizes))  # (bound of a whole session)
     c2, c1, q2, q1, pb = orc.rq4b_session_stats(s2, s1)
     assert_same(got["c2"][:S].cpu().numpy(), c2, path="c2")
     assert_same(got["c1"][:S].cpu().numpy(), c1, path="c1")

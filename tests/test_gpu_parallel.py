@@ -76,6 +76,10 @@ class _RQ4bView(_RQ2View):
     def spearman_prefix(self, rows, n):
         return self.s.spearman_prefix(rows.to(self.dev), n.to(self.dev)).cpu()
 
+    def trends(self, cols):
+        last, sp = self.s.trends([c.to(self.dev) for c in cols])
+        return last.cpu(), sp.cpu()
+
     def two_sample(self, x, y):
         return self.s.two_sample(x.to(self.dev), y.to(self.dev))
 

@@ -35,6 +35,8 @@ void rq4b_session_stats(fz_ctx *c, const double *values, const int64_t *sid, con
                         int64_t max_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q, double *pbm);
 void rq4b_session_stats_grouped(fz_ctx *c, const double *values, const int64_t *offs2, int64_t n, int64_t S,
                                 int64_t max_len, int64_t *c2, int64_t *c1, double *g2q, double *g1q, double *pbm);
+void rq4b_trends(fz_ctx *c, const int64_t *c2, const int64_t *c1, const double *g2q, const double *g1q, int64_t MM,
+                 int64_t *last, double *sp);
 void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t *n2, const double *b,
                       int64_t nb_cap, const int64_t *n1, double *ts);
 void buildlog(fz_ctx *c, const uint8_t *text, int64_t n_bytes, const int64_t *log_offs_host, const int64_t *log_offs,
@@ -506,6 +508,27 @@ int fz_radix_sort_u64(fz_ctx *ctx, uint64_t *keys, uint32_t *vals, int64_t n, in
     return guarded(ctx, [&] {
         FZ_CHECK((keys != nullptr || n == 0) && n >= 0 && bits >= 0 && bits <= 64, "fz_radix_sort_u64: bad arguments");
         fz::radix_sort_pairs(ctx, keys, vals, n, bits);
+    });
+}
+
+int fz_describe_f64_dev(fz_ctx *ctx, const double *x, int64_t n, fz_describe *dev_out) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(dev_out != nullptr && n >= 0 && (x != nullptr || n == 0), "fz_describe_f64_dev: bad arguments");
+        fz::describe_f64(ctx, x, n, dev_out);
+    });
+}
+
+int fz_rq4b_trends(fz_ctx *ctx, const int64_t *c2, const int64_t *c1, const double *g2_q, const double *g1_q,
+                   int64_t n_sessions, int64_t *last, double *spearman6) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n_sessions >= 0 && last && spearman6 && (n_sessions == 0 || (c2 && c1 && g2_q && g1_q)),
+                 "fz_rq4b_trends: bad arguments");
+        if (n_sessions == 0) {
+            const int64_t m1 = -1;
+            fz::set_i64(ctx, last, &m1, 1);
+            return;
+        }
+        fz::rq4b_trends(ctx, c2, c1, g2_q, g1_q, n_sessions, last, spearman6);
     });
 }
 

@@ -406,8 +406,42 @@ void rq4b_session_stats_grouped(fz_ctx *c, const double *values, const int64_t *
     int64_t *d_n = c->arena.get<int64_t>(1);
     set_i64(c, d_n, &n, 1);
     const uint32_t *sid2 = reinterpret_cast<const uint32_t *>(segment_ids(c, Segs{2 * MM, offs2, n}));
-    const int64_t half = max_len > 0 && max_len < n ? max_len : n;
-    rq4b_sessions(c, values, sid2, n, d_n, MM, half, 2 * half < n ? 2 * half : n, c2, c1, g2q, g1q, pbm, offs2);
+    // max_len bounds a whole session (both groups: at most one value per project), so each half too
+    const int64_t sess = max_len > 0 && max_len < n ? max_len : n;
+    rq4b_sessions(c, values, sid2, n, d_n, MM, sess, sess, c2, c1, g2q, g1q, pbm, offs2);
+}
+
+// The last session index with both groups >= 100 (:849-860) -> *last (-1 if none), and Spearman
+// (rho, p) vs index of G1 Q1 / Med / Q3, then G2 Q1 / Med / Q3 over sessions 0..last (:879-899) ->
+// sp[12], from the per-session counts and quartiles of MM sessions (device; no host read)
+void rq4b_trends(fz_ctx *c, const int64_t *c2, const int64_t *c1, const double *g2q, const double *g1q, int64_t MM,
+                 int64_t *last, double *sp) {
+    int64_t *lastp1 = c->arena.get<int64_t>(1);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) { *lastp1 = 0; });
+    map_n(c, MM, nullptr, [=] __device__(int64_t i) {
+        if (c2[i] >= 100 && c1[i] >= 100)
+            atomicMax(reinterpret_cast<unsigned long long *>(lastp1), (unsigned long long)(i + 1));
+    });
+    map_n(c, 1, nullptr, [=] __device__(int64_t) { *last = *lastp1 - 1; });
+    double *seq = c->arena.get<double>(6 * MM);
+    int64_t *offs6 = c->arena.get<int64_t>(7);
+    map_n(c, 7, nullptr, [=] __device__(int64_t k) { offs6[k] = k * (*lastp1); });
+    map_n(c, 6 * MM, nullptr, [=] __device__(int64_t k) {
+        const int64_t n = *lastp1;
+        if (n <= 0 || k >= 6 * n) return;
+        const int64_t sgi = k / n, i = k % n;  // G1 Q1, Med, Q3, then G2 Q1, Med, Q3
+        seq[k] = sgi < 3 ? g1q[i * 3 + sgi] : g2q[i * 3 + sgi - 3];
+    });
+    Segs s6{6, offs6, 6 * MM, MM};
+    ChunkedSegs cs6 = chunked(c, s6);
+    int32_t *id6 = segment_ids(c, s6);
+    SortedSegs ss6 = seg_sort_f64(c, seq, s6, id6);
+    double *rho = c->arena.get<double>(6), *pv = c->arena.get<double>(6);
+    spearman_index_sorted(c, cs6, id6, ss6, rho, pv);
+    map_n(c, 6, nullptr, [=] __device__(int64_t k) {
+        sp[2 * k] = rho[k];
+        sp[2 * k + 1] = pv[k];
+    });
 }
 
 void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *o) {
@@ -485,37 +519,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
                           contribute ? o->trend_offsets : nullptr);  // <= 1 value per project
     }
     // last session with both groups >= 100 (:849-860); Spearman of the quartile sequences (:879-899)
-    if (!sharded) {
-    int64_t *lastp1 = c->arena.get<int64_t>(1);
-    map_n(c, 1, nullptr, [=] __device__(int64_t) { *lastp1 = 0; });
-    map_n(c, MM, nullptr, [=] __device__(int64_t i) {
-        if (c2[i] >= 100 && c1[i] >= 100)
-            atomicMax(reinterpret_cast<unsigned long long *>(lastp1), (unsigned long long)(i + 1));
-    });
-    map_n(c, 1, nullptr, [=] __device__(int64_t) { counts[FZ_RQ4B_LAST] = *lastp1 - 1; });
-    {
-        double *seq = c->arena.get<double>(6 * MM);
-        int64_t *offs6 = c->arena.get<int64_t>(7);
-        map_n(c, 7, nullptr, [=] __device__(int64_t k) { offs6[k] = k * (*lastp1); });
-        map_n(c, 6 * MM, nullptr, [=] __device__(int64_t k) {
-            const int64_t n = *lastp1;
-            if (n <= 0 || k >= 6 * n) return;
-            const int64_t sgi = k / n, i = k % n;  // G1 Q1, Med, Q3, then G2 Q1, Med, Q3
-            seq[k] = sgi < 3 ? g1q[i * 3 + sgi] : g2q[i * 3 + sgi - 3];
-        });
-        Segs s6{6, offs6, 6 * MM, MM};
-        ChunkedSegs cs6 = chunked(c, s6);
-        int32_t *id6 = segment_ids(c, s6);
-        SortedSegs ss6 = seg_sort_f64(c, seq, s6, id6);
-        double *rho = c->arena.get<double>(6), *pv = c->arena.get<double>(6);
-        spearman_index_sorted(c, cs6, id6, ss6, rho, pv);
-        double *sp = o->spearman6;
-        map_n(c, 6, nullptr, [=] __device__(int64_t k) {
-            sp[2 * k] = rho[k];
-            sp[2 * k + 1] = pv[k];
-        });
-    }
-    }
+    if (!sharded) rq4b_trends(c, c2, c1, g2q, g1q, MM, counts + FZ_RQ4B_LAST, o->spearman6);
 
     // ---- coverage deltas around the corpus date for G3 u G4, CSV order (:725-797)
     {

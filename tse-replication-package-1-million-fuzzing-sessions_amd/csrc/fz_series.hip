@@ -142,14 +142,37 @@ ChunkedSegs chunked(fz_ctx *c, const Segs &sg) {
 
 ChunkMap make_chunks(fz_ctx *c, const Segs &sg) { return chunked(c, sg).cm; }
 
+// Segment id of every position (positions past offs[S] get S).  A workgroup takes a chunk of
+// kIdChunk positions: one search finds the segments of its first and last position, and a position
+// searches only between those (none at all when one segment covers the chunk - long sessions);
+// a per-position search over all S + 1 offsets cost ~log2(S) dependent loads per value.
+constexpr int kIdChunk = 4096;
+__global__ __launch_bounds__(kBlock) void k_segment_ids(const int64_t *__restrict__ offs, int64_t S, int64_t n,
+                                                        int32_t *__restrict__ id) {
+    __shared__ int64_t s_rng[2];
+    for (int64_t c0 = int64_t(blockIdx.x) * kIdChunk; c0 < n; c0 += int64_t(gridDim.x) * kIdChunk) {
+        const int64_t c1 = c0 + kIdChunk < n ? c0 + kIdChunk : n;
+        if (threadIdx.x == 0) {
+            const int64_t lo = upper_bound_i64(offs, 0, S + 1, c0) - 1;
+            s_rng[0] = lo;
+            s_rng[1] = upper_bound_i64(offs, lo > 0 ? lo : 0, S + 1, c1 - 1) - 1;
+        }
+        __syncthreads();
+        const int64_t lo = s_rng[0], hi = s_rng[1];
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock) {
+            const int64_t s = lo == hi ? lo : upper_bound_i64(offs, lo > 0 ? lo : 0, hi + 1, i) - 1;
+            id[i] = int32_t(s > S ? S : (s < 0 ? 0 : s));
+        }
+        __syncthreads();  // s_rng is rewritten for the next chunk
+    }
+}
+
 int32_t *segment_ids(fz_ctx *c, const Segs &sg) {
     int32_t *id = c->arena.get<int32_t>(sg.n_cap);
-    const int64_t *offs = sg.offs;
-    const int64_t S = sg.S;
-    map_n(c, sg.n_cap, nullptr, [=] __device__(int64_t i) {
-        const int64_t s = upper_bound_i64(offs, 0, S + 1, i) - 1;
-        id[i] = int32_t(s > S ? S : (s < 0 ? 0 : s));
-    });
+    if (sg.n_cap <= 0) return id;
+    const int64_t chunks = (sg.n_cap + kIdChunk - 1) / kIdChunk;
+    k_segment_ids<<<unsigned(chunks < 8192 ? chunks : 8192), kBlock, 0, c->stream>>>(sg.offs, sg.S, sg.n_cap, id);
+    FZ_LAUNCH_CHECK();
     return id;
 }
 

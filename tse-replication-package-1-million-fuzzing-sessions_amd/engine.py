@@ -164,6 +164,8 @@ SIGNATURES = {
     "fz_rq4b_ex": (C.c_int, [_P, C.POINTER(FzRq4Groups), C.c_uint32, C.POINTER(FzRq4bOut)]),
     "fz_rq4b_session_stats": (C.c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P]),
     "fz_rq4b_session_stats_grouped": (C.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P]),
+    "fz_rq4b_trends": (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P]),
+    "fz_describe_f64_dev": (C.c_int, [_P, _P, _I64, _P]),
     "fz_two_sample_tests": (C.c_int, [_P, _P, _I64, _P, _I64, _P]),
     "fz_buildlog": (C.c_int, [_P, _P, _I64, _P, _P, _I64, C.POINTER(FzBuildlogOut)]),
     "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),

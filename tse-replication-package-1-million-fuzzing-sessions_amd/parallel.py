@@ -546,14 +546,17 @@ def rq4b_sharded(shard, rank: int, world: int):
     if world > 1:
         got = all_gather_cols(cols)
         cols = [torch.cat([g[j] for g in got]) for j in range(len(cols))]
-    c2d, c1d = cols[0], cols[1]
-    # last session with both groups >= 100 (:849-860), on the device
-    idx = torch.arange(c2d.numel(), dtype=torch.int64, device=c2d.device)
-    ok = (c2d >= 100) & (c1d >= 100)
-    last_d = torch.where(ok, idx, torch.full_like(idx, -1)).max() if c2d.numel() else torch.tensor(-1)
-    # Spearman of G1 Q1 / Med / Q3, then G2 Q1 / Med / Q3 over sessions 0..last (:879-899), one call
-    quart = torch.stack([cols[5], cols[6], cols[7], cols[2], cols[3], cols[4]]).to(torch.float64)
-    sp = shard.spearman_prefix(quart, last_d + 1)
+    if hasattr(shard, "trends"):  # one library call (fz_rq4b_trends), device in and out
+        last_d, sp = shard.trends(cols)
+    else:
+        c2d, c1d = cols[0], cols[1]
+        # last session with both groups >= 100 (:849-860), on the device
+        idx = torch.arange(c2d.numel(), dtype=torch.int64, device=c2d.device)
+        ok = (c2d >= 100) & (c1d >= 100)
+        last_d = torch.where(ok, idx, torch.full_like(idx, -1)).max() if c2d.numel() else torch.tensor(-1)
+        # Spearman of G1 Q1 / Med / Q3, then G2 Q1 / Med / Q3 over sessions 0..last (:879-899)
+        quart = torch.stack([cols[5], cols[6], cols[7], cols[2], cols[3], cols[4]]).to(torch.float64)
+        sp = shard.spearman_prefix(quart, last_d + 1)
     # coverage deltas: columns of every rank, in corpus CSV order
     proj = part["delta_order"][:nd]
     pre = part["pre_cov"][:7 * nd].reshape(7, nd)
@@ -806,11 +809,17 @@ def gpu_rq4b_session_stats_grouped(eng, vals, offs2, S, max_len):
 
 
 def gpu_mean_median(eng, x):
-    """(mean, median) of one device vector through fz_describe_f64 (NaN when empty)."""
+    """(mean, median) of one device vector through fz_describe_f64_dev (NaN when empty): a device
+    [2] view, copied with the driver's other results."""
+    import ctypes as C
+    from . import engine as E
     if x.numel() == 0:
         return np.array([np.nan, np.nan])
-    d = eng.describe(x.contiguous())
-    return np.array([float(d.mean), float(d.median)])
+    x = x.contiguous()
+    d = eng.torch.empty(E.DESCRIBE_DOUBLES, dtype=eng.torch.float64, device=eng.dev)
+    E._check(eng.lib, eng.lib.fz_describe_f64_dev(eng.ctx, C.c_void_p(x.data_ptr()), x.numel(),
+                                                  C.c_void_p(d.data_ptr())))
+    return d[4:6]  # fz_describe: count, n_pos, n_zero, n_neg, mean, median, ...
 
 
 class GpuRQ4aShard:
@@ -887,6 +896,21 @@ class GpuRQ4bShard:
 
     def spearman_prefix(self, rows, n):
         return gpu_spearman_prefix(self.eng, rows, n)
+
+    def trends(self, cols):
+        """fz_rq4b_trends over the per-session columns (c2, c1, G2 Q1..Q3, G1 Q1..Q3, p_bm) -> (last
+        session with both groups >= 100 as a device scalar, (rho, p) x 6 device)."""
+        E, C, eng = self.E, self.C, self.eng
+        torch = eng.torch
+        n = cols[0].numel()
+        c2, c1 = cols[0].to(torch.int64).contiguous(), cols[1].to(torch.int64).contiguous()
+        g2 = torch.stack(cols[2:5], 1).reshape(-1).to(torch.float64).contiguous()
+        g1 = torch.stack(cols[5:8], 1).reshape(-1).to(torch.float64).contiguous()
+        last = torch.empty(1, dtype=torch.int64, device=eng.dev)
+        sp = torch.empty(12, dtype=torch.float64, device=eng.dev)
+        P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+        E._check(eng.lib, eng.lib.fz_rq4b_trends(eng.ctx, P(c2), P(c1), P(g2), P(g1), n, P(last), P(sp)))
+        return last[0], sp
 
     def mean_median(self, x):
         return gpu_mean_median(self.eng, x)
