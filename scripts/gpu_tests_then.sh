@@ -10,7 +10,7 @@ echo "pytest rc=$rc"; tail -3 $O/${T}_pytest.log
 [ $rc -ne 0 ] && exit $rc
 for c in ${CONFIGS:-c2 c3}; do
   st=20; [ $c != c2 ] && st=5
-  for mode in ${MODES:-"--force-sharded --serial" "--force-sharded" "--force-sharded --shard-graphs" ""}; do
+  for mode in "--force-sharded --serial" "--force-sharded" "--force-sharded --shard-graphs" ""; do
     timeout -k 10 300 python -u bench.py --config $c --steps $st --warmup 2 --no-cpu-baseline --probe-steps 0 $mode > $O/${T}_b.json 2> $O/${T}_b.err || exit $?
     python3 -c "import json; d=json.loads([l for l in open('$O/${T}_b.json') if l.startswith('{')][-1]); print('$c [$mode]', d['ms_per_step'], d['config'].get('driver_host_ms', ''), flush=True)"
   done
