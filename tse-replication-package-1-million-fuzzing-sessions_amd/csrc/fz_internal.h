@@ -127,7 +127,9 @@ struct DevBuf {
 struct View {
     int64_t n = 0;
     int64_t max_seg = 0;
-    const int32_t *row = nullptr;
+    // view position q is store row row0 + q: the store's columns are gathered into view order, so
+    // a view's row ids are implicit (the filters read no row array)
+    int64_t row0 = 0;
     const int64_t *time = nullptr;
     const uint32_t *proj = nullptr;
     const int64_t *offs = nullptr;
@@ -138,7 +140,7 @@ struct Store {
     bool built = false;
     fz_tables t{};
     int64_t P = 0;
-    DevBuf b_row, b_time, b_proj, c_row, c_time, c_proj, i_row, i_time, i_proj;
+    DevBuf b_time, b_proj, c_time, c_proj, i_time, i_proj;
     DevBuf off_fuzz, off_covb, off_cov, off_iss;
     View fuzz;    // buildlog_data, build_type = Fuzzing, by (project, timecreated)   queries1.py:267-278
     View covb;    // buildlog_data, build_type = Coverage, by (project, timecreated)
@@ -167,7 +169,7 @@ struct Store {
         mix(uint64_t(P));
         const unsigned char *tb = reinterpret_cast<const unsigned char *>(&t);
         for (size_t i = 0; i < sizeof(t); ++i) mix(tb[i]);
-        for (const DevBuf *d : {&b_row, &b_time, &b_proj, &c_row, &c_time, &c_proj, &i_row, &i_time, &i_proj,
+        for (const DevBuf *d : {&b_time, &b_proj, &c_time, &c_proj, &i_time, &i_proj,
                                 &off_fuzz, &off_covb, &off_cov, &off_iss, &elig, &n_elig, &sb_type, &sb_result,
                                 &sb_group, &sb_canon, &sc_coverage, &sc_covered, &sc_total, &sc_valid, &si_number,
                                 &si_status, &b_perm, &c_perm, &i_perm}) {

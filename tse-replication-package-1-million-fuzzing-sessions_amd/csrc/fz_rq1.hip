@@ -200,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void k_issue_pass(View iss, const uint8_t *
                                                        uint8_t *__restrict__ f_tgt, int64_t *__restrict__ mbuild,
                                                        int64_t *__restrict__ mbtime) {
     for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < iss.n; j += int64_t(gridDim.x) * kBlock) {
-        const int32_t r = iss.row[j];
+        const int32_t r = int32_t(iss.row0 + j);
         const uint32_t p = iss.proj[j];
         const int64_t rts = iss.time[j];
         const bool lim = rts < kLimitUs;
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(kBlock) void k_dedup_keys(const int64_t *__restrict
                                                        uint64_t pad, uint64_t *__restrict__ keys,
                                                        uint32_t *__restrict__ vals) {
     for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < n; j += int64_t(gridDim.x) * kBlock) {
-        keys[j] = mbuild[j] >= 0 ? uint64_t(number[iss.row[j]] - nmin) : pad;
+        keys[j] = mbuild[j] >= 0 ? uint64_t(number[iss.row0 + j] - nmin) : pad;
         vals[j] = uint32_t(j);
     }
 }
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(kBlock) void k_matched_out(View iss, const int64_t 
         if (!keep[j]) continue;
         const int64_t q = pos[j];
         const uint32_t p = iss.proj[j];
-        out_issue[q] = iperm[iss.row[j]];
+        out_issue[q] = iperm[iss.row0 + j];
         out_build[q] = bperm[mbuild[j]];
         const int64_t lo = fuzz.offs[p], hi = fuzz.offs[p + 1];
         it_arr[q] = lower_bound_i64(fuzz.time, lo, hi, iss.time[j]) - lo;
@@ -426,7 +426,7 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_ext *ext_in, const fz_rq1_ou
 
     // SAME_DATE_BUILD_ISSUE partner view
     TmpView v1;
-    filter_view(c, s.fuzz.row, s.fuzz.time, s.fuzz.proj, s.fuzz.n, P, ValidFuzzRq1{t.b_result, t.b_time}, v1);
+    filter_view(c, s.fuzz, s.fuzz.n, P, ValidFuzzRq1{t.b_result, t.b_time}, v1);
 
     // issues pass
     const int64_t NI = s.issues.n;

@@ -158,7 +158,7 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     TmpView T;
     const CovTrendRows vrows{t.c_project, t.c_coverage, t.c_valid, t.c_date, o->eligible};
     const NonZeroTotal nzt{t.c_total, t.c_valid};
-    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P, TrendRows{vrows, nzt}, T, nullptr, Selection{},
+    filter_view(c, s.cov, NC, P, TrendRows{vrows, nzt}, T, nullptr, Selection{},
                 CountZeroTotal{raw_n, vrows, nzt});
     const int64_t *toffs = T.offs;
     per_seg(c, P, [=] __device__(int64_t p) {
@@ -315,7 +315,7 @@ void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
     eligible_projects(c, o->eligible, o->counts + FZ_RQ2A_ELIGIBLE);
 
     TmpView B, CV;
-    filter_view(c, s.covb.row, s.covb.time, s.covb.proj, s.covb.n, P,
+    filter_view(c, s.covb, s.covb.n, P,
                 CovBuildRows{t.b_project, t.b_result, t.b_time, o->eligible}, B);
     // the coverage rows are read for projects with a selected Coverage build only (their change
     // points' date joins and pandas upcast flags): the view's other tiles are skipped, all of them
@@ -326,7 +326,7 @@ void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
         const int64_t *bo = B.offs;
         map_n(c, P, nullptr, [=] __device__(int64_t p) { withb[p] = el[p] && bo[p + 1] > bo[p] ? 1 : 0; });
     }
-    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, s.cov.n, P, CovRowsBeforeLimit{t.c_project, t.c_date, withb},
+    filter_view(c, s.cov, s.cov.n, P, CovRowsBeforeLimit{t.c_project, t.c_date, withb},
                 CV, nullptr, Selection{withb, 1, B.d_n});
     const int64_t NB = s.covb.n;
     const int64_t *boffs = B.offs, *coffs = CV.offs;

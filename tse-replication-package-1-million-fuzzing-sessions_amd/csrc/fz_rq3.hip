@@ -72,10 +72,10 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     eligible_projects(c, o->eligible, counts + FZ_RQ3_ELIGIBLE);
 
     TmpView I, F, CB, TC;
-    filter_view(c, s.issues.row, s.issues.time, s.issues.proj, NI, P,
+    filter_view(c, s.issues, NI, P,
                 FixedIssuesRq3{t.i_project, t.i_status, t.i_rts, o->eligible}, I);
-    filter_view(c, s.fuzz.row, s.fuzz.time, s.fuzz.proj, s.fuzz.n, P, FuzzRq3{t.b_result, t.b_time}, F);
-    filter_view(c, s.covb.row, s.covb.time, s.covb.proj, s.covb.n, P, CovBuildRq3{t.b_time}, CB);
+    filter_view(c, s.fuzz, s.fuzz.n, P, FuzzRq3{t.b_result, t.b_time}, F);
+    filter_view(c, s.covb, s.covb.n, P, CovBuildRq3{t.b_time}, CB);
     // the coverage rows of the projects with a fixed issue only: the view's tiles of other projects
     // are skipped unread (config 3 / 5, coverage-only tables: all of them)
     uint8_t *self = c->arena.get<uint8_t>(P);
@@ -83,7 +83,7 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         const int64_t *ioff = I.offs;
         map_n(c, P, nullptr, [=] __device__(int64_t p) { self[p] = ioff[p + 1] > ioff[p] ? 1 : 0; });
     }
-    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P, CovRowsRq3{t.c_valid, t.c_date, t.c_project, self}, TC,
+    filter_view(c, s.cov, NC, P, CovRowsRq3{t.c_valid, t.c_date, t.c_project, self}, TC,
                 nullptr, Selection{self, 1, I.d_n});
 
     // ---- detected: one thread per issue (:241-302)

@@ -85,8 +85,8 @@ void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
     const uint8_t *member = o->member;
 
     TmpView FB, FI;
-    filter_view(c, s.fuzz.row, s.fuzz.time, s.fuzz.proj, s.fuzz.n, P, BuildsBeforeLimit{t.b_time}, FB);
-    filter_view(c, s.issues.row, s.issues.time, s.issues.proj, NI, P, FixedBeforeLimit{t.i_status, t.i_rts}, FI);
+    filter_view(c, s.fuzz, s.fuzz.n, P, BuildsBeforeLimit{t.b_time}, FB);
+    filter_view(c, s.issues, NI, P, FixedBeforeLimit{t.i_status, t.i_rts}, FI);
     const int64_t *fboffs = FB.offs, *fbtime = FB.time, *fioffs = FI.offs, *fitime = FI.time;
 
     // totals[i] += 1 for i = 1..#builds, per group (:339-340)
@@ -465,7 +465,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
 
     // ---- per-session quartiles and Brunner-Munzel, G2 (x) vs G1 (y) (:910-1015)
     TmpView F;
-    filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P,
+    filter_view(c, s.cov, NC, P,
                 FullTrendRows{t.c_project, t.c_coverage, t.c_valid, t.c_date, member}, F);
     const int64_t *foffs = F.offs;
     const int32_t *frow = F.row;
@@ -524,7 +524,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
     // ---- coverage deltas around the corpus date for G3 u G4, CSV order (:725-797)
     {
         TmpView PC;
-        filter_view(c, s.cov.row, s.cov.time, s.cov.proj, NC, P,
+        filter_view(c, s.cov, NC, P,
                     PositiveCoverage34{t.c_project, t.c_coverage, t.c_valid, member}, PC, nullptr,
                     Selection{member, 12, nullptr, s.cov.offs});  // (G3 / G4: their rows only, virtual rows)
         const int64_t NO = g->n_order;

@@ -171,8 +171,8 @@ __global__ __launch_bounds__(kBlock) void k_prefix_offsets(const PrefixOffs O) {
 }
 
 // Columns the store materialises in sorted order (k_store_gather, after the sorts): perm[q] =
-// the caller's row id of sorted row q, orow[q] = q (row id = sorted position), dst[j][q] =
-// src[j][spos[q]] with src the prefix-sorted columns.
+// the caller's row id of sorted row q, dst[j][q] = src[j][spos[q]] with src the prefix-sorted
+// columns.  (Store row id = sorted position: the views' row ids are implicit, View::row0.)
 constexpr int kMaxGather = 4;
 struct GatherCols {
     int n = 0;
@@ -208,7 +208,6 @@ struct GatherTab {
     const uint32_t *spos = nullptr;
     const uint32_t *rows = nullptr;
     int64_t n = 0;
-    int32_t *orow = nullptr;
     GatherCols gc;
 };
 struct GatherTabs {
@@ -235,7 +234,6 @@ __global__ __launch_bounds__(kBlock) void k_store_gather(const GatherTabs G) {
         if (s32 == kGathered) continue;  // a bucket sort wrote this row's columns
         const int64_t sp = s32;
         gc.perm[q] = int32_t(tb.rows[sp]);
-        tb.orow[q] = int32_t(q);
         for (int j = 0; j < gc.n; ++j) {
             if (gc.size[j] == 8)
                 static_cast<uint64_t *>(gc.dst[j])[q] = static_cast<const uint64_t *>(gc.src[j])[sp];
@@ -286,7 +284,6 @@ struct TimeSortTab {
     unsigned long long *big = nullptr;  // the table's merge-sort counters
     uint8_t *bigflag = nullptr;
     const uint32_t *rows = nullptr;  // caller row ids in prefix order
-    int32_t *orow = nullptr;
     GatherCols gc;
     // sub-bucket pass of long segments (big_segments_bucketed): segment s's rows are written at
     // output positions + oshift[s], its project is sproj[s], and equal times are ordered by tie[]
@@ -535,7 +532,6 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         for (int q = tid; q < n; q += BS) {
             out.oproj[ob + q] = p;
             out.spos[ob + q] = kGathered;
-            tb.orow[ob + q] = int32_t(ob + q);
         }
         for (int j = 0; j < nc; ++j) {
             if constexpr (kPrefetch) {
@@ -575,7 +571,6 @@ struct PrefixSorted {
     TimeSortOut out{};
     uint32_t pmask = 0;
     unsigned long long *big = nullptr;
-    int32_t *orow = nullptr;
 };
 struct TableIn {
     int64_t n;
@@ -584,7 +579,6 @@ struct TableIn {
     const int64_t *time;
     int64_t *otime;
     uint32_t *oproj;
-    int32_t *orow;
     GatherCols gc;
     unsigned long long *big;
 };
@@ -642,7 +636,6 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) 
         ps.out = TimeSortOut{t.otime, t.oproj, c->arena.get<uint32_t>(n)};
         ps.pmask = t.pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << t.pre.pbits) - 1ull);
         ps.big = t.big;
-        ps.orow = t.orow;
         O.keys[k] = K.keys[k];
         O.n[k] = n;
         O.S[k] = S;
@@ -680,7 +673,6 @@ static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
         tb.big = ps.big;
         tb.bigflag = ps.bigflag;
         tb.rows = ps.rows;
-        tb.orow = ps.orow;
         tb.gc = ps.gc;
         tb.fused = ps.big + 6;  // big3[6 + k]
     }
@@ -721,7 +713,7 @@ static void gather_tables(fz_ctx *c, const PrefixSorted *pss) {
         const unsigned g = ps.n > 0 ? (grid_for(ps.n, kBlock, 8192) + 7u) & ~7u : 0u;
         G.blk[k + 1] = G.blk[k] + g;
         if (ps.n <= 0) continue;
-        G.tab[k] = GatherTab{ps.out.spos, ps.rows, ps.n, ps.orow, ps.gc};
+        G.tab[k] = GatherTab{ps.out.spos, ps.rows, ps.n, ps.gc};
     }
     if (G.blk[3] == 0) return;
     ProbeScope probe(c, "store_gather", 0.0);
@@ -729,11 +721,11 @@ static void gather_tables(fz_ctx *c, const PrefixSorted *pss) {
     FZ_LAUNCH_CHECK();
 }
 // algorithmic bytes of one gather pass: spos 4 read per row; for the rows it gathers (gathered[k])
-// row id 4 + columns read, perm 4 + row 4 + columns written
+// row id 4 + columns read, perm 4 + columns written
 static double gather_bytes(const PrefixSorted *pss, const int64_t *gathered) {
     double bytes = 0.0;
     for (int k = 0; k < 3; ++k)
-        if (pss[k].n > 0) bytes += 4.0 * double(pss[k].n) + (12.0 + 2.0 * pss[k].gc.bytes()) * double(gathered[k]);
+        if (pss[k].n > 0) bytes += 4.0 * double(pss[k].n) + (8.0 + 2.0 * pss[k].gc.bytes()) * double(gathered[k]);
     return bytes;
 }
 
@@ -986,7 +978,6 @@ static bool big_segments_bucketed(fz_ctx *c, const PrefixSorted &ps, int64_t big
     tb.big = big;
     tb.bigflag = flags;
     tb.rows = static_cast<const uint32_t *>(rpl.out[1]);
-    tb.orow = ps.orow;
     tb.gc = cg;
     tb.oshift = d_shift;
     tb.sproj = d_sproj;
@@ -994,8 +985,8 @@ static bool big_segments_bucketed(fz_ctx *c, const PrefixSorted &ps, int64_t big
     T.base[1] = T.base[2] = T.base[3] = nsubs;
     {
         // time 8 read; time 8 + project 4 + marker 4 written; row id 4 + columns read, perm 4 +
-        // row 4 + columns written (the gather is fused)
-        ProbeScope probe(c, "big_sub_sort", (36.0 + 2.0 * ps.gc.bytes()) * double(ncomp));
+        // columns written (the gather is fused)
+        ProbeScope probe(c, "big_sub_sort", (32.0 + 2.0 * ps.gc.bytes()) * double(ncomp));
         const unsigned g16 = unsigned(nsubs < 256 ? nsubs : 256);
         k_seg_time_bucket<1024, 16384><<<g16, 1024, 0, c->stream>>>(T, 0, true);
         FZ_LAUNCH_CHECK();
@@ -1076,14 +1067,12 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         Prefix pre;
         int pbits_total;
         const int64_t *time;
-        DevBuf *row, *tm, *pr;
+        DevBuf *tm, *pr;
     };
     Tab tabs[3] = {
-        {t->n_builds, Prefix{t->b_project, t->b_type, pbits}, pbits + 2, t->b_time, &s.b_row, &s.b_time,
-         &s.b_proj},
-        {t->n_cov, Prefix{t->c_project, nullptr, pbits}, pbits, t->c_date, &s.c_row, &s.c_time, &s.c_proj},
-        {t->n_issues, Prefix{t->i_project, nullptr, pbits}, pbits, t->i_rts, &s.i_row, &s.i_time,
-         &s.i_proj},
+        {t->n_builds, Prefix{t->b_project, t->b_type, pbits}, pbits + 2, t->b_time, &s.b_time, &s.b_proj},
+        {t->n_cov, Prefix{t->c_project, nullptr, pbits}, pbits, t->c_date, &s.c_time, &s.c_proj},
+        {t->n_issues, Prefix{t->i_project, nullptr, pbits}, pbits, t->i_rts, &s.i_time, &s.i_proj},
     };
     GatherCols gcs[3];
     {
@@ -1117,7 +1106,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     for (int k = 0; k < 3; ++k) {
         Tab &b = tabs[k];
         tin[k] = TableIn{b.n, b.pre, b.pbits_total, b.time, b.tm->ensure<int64_t>(b.n), b.pr->ensure<uint32_t>(b.n),
-                         b.row->ensure<int32_t>(b.n), gcs[k], big3 + k};
+                         gcs[k], big3 + k};
     }
     prefix_sort_tables(c, tin, pss);
     time_sort_tables(c, pss);
@@ -1159,23 +1148,23 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     const int64_t fused[3] = {c->h_pinned[10], c->h_pinned[11], c->h_pinned[12]};
     const int64_t n_fuzz = c->h_pinned[13], n_covb = c->h_pinned[14];
     {
-        auto view = [&](View &v, DevBuf &rowb, DevBuf &tmb, DevBuf &prb, int64_t at, int64_t n, DevBuf &offb) {
+        auto view = [&](View &v, DevBuf &tmb, DevBuf &prb, int64_t at, int64_t n, DevBuf &offb) {
             v.n = n;
-            v.row = rowb.as<int32_t>() + at;
+            v.row0 = at;
             v.time = tmb.as<int64_t>() + at;
             v.proj = prb.as<uint32_t>() + at;
             v.offs = offb.as<int64_t>();
         };
-        view(s.fuzz, s.b_row, s.b_time, s.b_proj, 0, n_fuzz, s.off_fuzz);
-        view(s.covb, s.b_row, s.b_time, s.b_proj, n_fuzz, n_covb, s.off_covb);
-        view(s.cov, s.c_row, s.c_time, s.c_proj, 0, t->n_cov, s.off_cov);
-        view(s.issues, s.i_row, s.i_time, s.i_proj, 0, t->n_issues, s.off_iss);
+        view(s.fuzz, s.b_time, s.b_proj, 0, n_fuzz, s.off_fuzz);
+        view(s.covb, s.b_time, s.b_proj, n_fuzz, n_covb, s.off_covb);
+        view(s.cov, s.c_time, s.c_proj, 0, t->n_cov, s.off_cov);
+        view(s.issues, s.i_time, s.i_proj, 0, t->n_issues, s.off_iss);
     }
     // the probes' algorithmic bytes of the gathers: the long bucket class's fused gather, then the
     // rows the gather above moved (short classes; not the flagged segments' rows)
     int64_t gathered[3];
     for (int k = 0; k < 3; ++k) {
-        const double per = 12.0 + 2.0 * pss[k].gc.bytes();  // row 4 + columns in; perm 4 + row 4 + columns out
+        const double per = 8.0 + 2.0 * pss[k].gc.bytes();  // row 4 + columns in; perm 4 + columns out
         ProbeScope::add_bytes(c, "seg_time_sort", per * double(fused[k]));
         gathered[k] = pss[k].n - fused[k] - bigrows[k];
     }

@@ -83,8 +83,7 @@ struct NoCount {
 // VIRT: the rows are the virtual rows of a Selection with view_offs (the selected projects'
 // segments back to back): item i's view row comes from Selection::phys.
 template <typename Pred, typename Count = NoCount, bool VIRT = false>
-__global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__restrict__ rows,
-                                                           const int64_t *__restrict__ times,
+__global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const int64_t *__restrict__ times,
                                                            const uint32_t *__restrict__ proj, int64_t n,
                                                            const int64_t *__restrict__ d_live, Pred pred, Lookback lb,
                                                            int64_t ntiles, int32_t *__restrict__ orow,
@@ -140,14 +139,14 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const int32_t *__rest
         if constexpr (VIRT) return pidx[i];
         else return base + i * kBlock + tid;
     };
-    // all row loads first, then all predicate gathers: independent loads in flight together
-    // instead of one dependent load chain per item
+    // the store row of every item (implicit: row0 + view position), then all predicate loads:
+    // independent loads in flight together, no row-id load before them
     int32_t r[kFcItems];
     bool keep[kFcItems];
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) {
         const int64_t idx = base + i * kBlock + tid;
-        r[i] = idx < lim ? rows[row_at(i)] : 0;
+        r[i] = idx < lim ? int32_t(row0 + row_at(i)) : 0;
     }
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) keep[i] = base + i * kBlock + tid < lim && pred(r[i]);
@@ -234,9 +233,11 @@ struct PredBytes<P, std::void_t<decltype(P::kBytes)>> {
 // sel (optional): the projects pred can keep - tiles of the (project-ordered) view covering none of
 // them are skipped without reading their columns.
 template <typename Pred, typename Count = NoCount>
-void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uint32_t *proj, int64_t n, int64_t P,
-                 Pred pred, TmpView &dst, const int64_t *src_live = nullptr, Selection sel = Selection{},
-                 Count cnt = Count{}) {
+void filter_view(fz_ctx *c, const View &v, int64_t n, int64_t P, Pred pred, TmpView &dst,
+                 const int64_t *src_live = nullptr, Selection sel = Selection{}, Count cnt = Count{}) {
+    const int64_t *times = v.time;
+    const uint32_t *proj = v.proj;
+    const int64_t row0 = v.row0;
     dst.cap = n;
     dst.d_n = c->arena.get<int64_t>(1);
     dst.row = c->arena.get<int32_t>(n);
@@ -255,17 +256,17 @@ void filter_view(fz_ctx *c, const int32_t *rows, const int64_t *times, const uin
     if (n > 0) {
         const int64_t ntiles = (n + kFcTile - 1) / kFcTile;
         const Lookback lb = lookback_begin(c, ntiles);
-        // per input row: its row id 4 B + the predicate's columns; per kept row: time 8 + project 4
-        // read, (row, time, project) 16 written
+        // per input row: the predicate's columns; per kept row: time 8 + project 4 read, (row, time,
+        // project) 16 written
         // (a selective filter reads only the tiles of its projects: probed apart, kept rows' bytes)
         ProbeScope ps(c, sel.flags ? "filter_select" : "filter_compact",
-                      sel.flags ? 0.0 : double(n) * (4.0 + PredBytes<Pred>::value), dst.d_n, 28.0);
+                      sel.flags ? 0.0 : double(n) * PredBytes<Pred>::value, dst.d_n, 28.0);
         if (sel.voff)
-            k_filter_compact<Pred, Count, true><<<unsigned(ntiles), kBlock, 0, c->stream>>>(rows, times, proj, n, src_live, pred, lb,
+            k_filter_compact<Pred, Count, true><<<unsigned(ntiles), kBlock, 0, c->stream>>>(row0, times, proj, n, src_live, pred, lb,
                                                                               ntiles, dst.row, dst.time, dst.proj,
                                                                               dst.d_n, sel, cnt);
         else
-            k_filter_compact<Pred, Count><<<unsigned(ntiles), kBlock, 0, c->stream>>>(rows, times, proj, n, src_live, pred, lb,
+            k_filter_compact<Pred, Count><<<unsigned(ntiles), kBlock, 0, c->stream>>>(row0, times, proj, n, src_live, pred, lb,
                                                                               ntiles, dst.row, dst.time, dst.proj,
                                                                               dst.d_n, sel, cnt);
         FZ_LAUNCH_CHECK();
