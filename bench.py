@@ -248,7 +248,7 @@ def main():
         children = [eng.child() for _ in groups[:-1]] + [eng]
         pool = ThreadPoolExecutor(len(groups) - 1)
         # the store build forks its independent sorts onto the (then idle) children
-        eng.set_store_helpers(children[:-1])
+        eng.set_store_helpers(children[:-1][:4])  # (the library takes up to four)
 
         def run_group(ch, names):
             with torch.cuda.stream(ch.stream):
