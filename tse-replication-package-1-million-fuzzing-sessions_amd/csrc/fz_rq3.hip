@@ -225,7 +225,7 @@ static void sample_tests(fz_ctx *c, const double *v, const double *cat, int64_t 
     seg_reduce<2>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
         x[0] = v[i];
         x[1] = fabs(v[i] - med[s]);
-    }, r1);
+    }, r1, 8.0);
     double *r2 = c->arena.get<double>(4);  // [s]: sum (x - mean)^2, sum (|x - median| - its mean)^2
     seg_reduce<2>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
         const double n = double(oseg[s + 1] - oseg[s]);
@@ -233,7 +233,7 @@ static void sample_tests(fz_ctx *c, const double *v, const double *cat, int64_t 
         const double e = fabs(v[i] - med[s]) - r1[2 * s + 1] / n;
         x[0] = d * d;
         x[1] = e * e;
-    }, r2);
+    }, r2, 8.0);
     double *r3 = c->arena.get<double>(2);  // [s]: sum of the A2 terms (ascending order)
     seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
         const int64_t b = oseg[s], n = oseg[s + 1] - b, k = i - b;
@@ -241,7 +241,7 @@ static void sample_tests(fz_ctx *c, const double *v, const double *cat, int64_t 
         const double sd = sqrt(r2[2 * s] / (N - 1.0));  // np.std(ddof=1)
         const double wi = (cat[i] - xbar) / sd, wj = (cat[b + n - 1 - k] - xbar) / sd;
         x[0] = (2.0 * double(k + 1) - 1.0) / N * (stats::log_ndtr(wi) + stats::log_ndtr(-wj));
-    }, r3);
+    }, r3, 16.0);  // the value and its mirror
     map_n(c, 1, nullptr, [=] __device__(int64_t) {
         const double nx = double(oseg[1] - oseg[0]), ny = double(oseg[2] - oseg[1]);
         if (!(nx > 0.0 && ny > 0.0)) return;

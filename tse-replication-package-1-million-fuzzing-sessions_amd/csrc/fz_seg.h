@@ -244,11 +244,13 @@ void seg_fold_parts(fz_ctx *c, const ChunkedSegs &cs, const double *part, double
 
 // Segmented sum of NV per-element values f(i, seg, x[NV]) -> out[S][NV] (device).
 template <int NV, typename F>
-void seg_reduce(fz_ctx *c, const ChunkedSegs &cs, F f, double *out) {
+void seg_reduce(fz_ctx *c, const ChunkedSegs &cs, F f, double *out, double in_bytes = -1.0) {
     const int64_t S = cs.sg.S;
     if (S <= 0) return;
-    // algorithmic bytes: NV doubles per live element (offs[S]) in, NV per segment out
-    ProbeScope ps(c, "seg_reduce", 8.0 * NV * double(S), cs.sg.offs + S, 8.0 * NV);
+    // algorithmic bytes: what f reads per live element (offs[S]; in_bytes, default NV doubles - a
+    // functor that computes its terms, e.g. Shapiro-Wilk's normal scores, states fewer), NV
+    // doubles per segment out
+    ProbeScope ps(c, "seg_reduce", 8.0 * NV * double(S), cs.sg.offs + S, in_bytes >= 0.0 ? in_bytes : 8.0 * NV);
     if (cs.cps == 1) {
         k_chunk_reduce<NV, F><<<unsigned(S), kBlock, 0, c->stream>>>(cs.cm, cs.sg.offs, 1, S, f, nullptr, out);
         FZ_LAUNCH_CHECK();

@@ -729,7 +729,7 @@ void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, 
         }
         x[4] = double(tt & ~int64_t((1 << 26) - 1));
         x[5] = double(tt & int64_t((1 << 26) - 1));
-    }, s1);
+    }, s1, 25.0);  // isx 1 + rank 8 + flag 8 (+ group bounds of tied elements)
     double *s2 = c->arena.get<double>(S * 2);
     seg_reduce<2>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
         const double nx = s1[6 * s + 2], ny = s1[6 * s + 3];
@@ -739,7 +739,7 @@ void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, 
         const double d = ((rc[i] - rw[i]) - cm) + wm;
         x[0] = xs ? d * d : 0.0;
         x[1] = xs ? 0.0 : d * d;
-    }, s2);
+    }, s2, 17.0);  // isx 1 + both ranks 16
     per_seg(c, S, [=] __device__(int64_t s) {
         const double nx = s1[6 * s + 2], ny = s1[6 * s + 3];
         const double rcx = s1[6 * s] / nx, rcy = s1[6 * s + 1] / ny;
@@ -1105,7 +1105,7 @@ void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, 
         x[0] = rx * ry;
         x[1] = rx * rx;
         x[2] = ry * ry;
-    }, sums);
+    }, sums, 12.0);  // position 4 + rank 8
     const double *ng = tr.ngroups;
     per_seg(c, S, [=] __device__(int64_t s) {
         const int64_t n = offs[s + 1] - offs[s];
@@ -1557,7 +1557,7 @@ void seg_shapiro(fz_ctx *c, const ChunkedSegs &cs, const double *src, const Sort
         double m = 0.0;
         if (n >= 3 && k <= n / 2) m = stats::sw_m(k, n);
         x[0] = m * m;
-    }, summ2);
+    }, summ2, 0.0);  // (normal scores computed, nothing read per element)
     per_seg(c, S, [=] __device__(int64_t s) {
         const int64_t b = offs[s], n = offs[s + 1] - b;
         if (n < 3) return;
@@ -1587,7 +1587,7 @@ void seg_shapiro(fz_ctx *c, const ChunkedSegs &cs, const double *src, const Sort
         const double range = shift[2 * s + 1];
         x[0] = (v[i] - shift[2 * s]) / range;
         x[1] = stats::sw_coef_at(coef_of(s, n), i - b + 1);
-    }, s1);
+    }, s1, 8.0);
     // pass C: ssa, ssx, sax
     seg_reduce<3>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
         const int64_t b = offs[s], n = offs[s + 1] - b;
@@ -1600,7 +1600,7 @@ void seg_shapiro(fz_ctx *c, const ChunkedSegs &cs, const double *src, const Sort
         x[0] = asa * asa;
         x[1] = xsx * xsx;
         x[2] = asa * xsx;
-    }, s2);
+    }, s2, 8.0);
     per_seg(c, S, [=] __device__(int64_t s) {
         const int64_t n = offs[s + 1] - offs[s];
         if (n < 3) {
