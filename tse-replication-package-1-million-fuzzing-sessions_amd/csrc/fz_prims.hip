@@ -374,6 +374,11 @@ constexpr int kRadix = 1 << kRadixBits;
 #ifndef FZ_OS_WINDOW
 #define FZ_OS_WINDOW 8
 #endif
+// the first payload column loaded with the keys (same-box A/B, scripts/bench_ab.sh: c3 20.73 ->
+// 20.62 ms, c5 30.75 -> 30.66, c2 unchanged; 88 -> 105 VGPRs, occupancy 5 -> 4 waves per SIMD)
+#ifndef FZ_OS_PREFETCH
+#define FZ_OS_PREFETCH 1
+#endif
 constexpr int kOsBlock = FZ_OS_BLOCK;        // threads per radix-pass workgroup
 constexpr int kOsWaves = kOsBlock / kWave;
 constexpr int kSortTile = FZ_OS_TILE;        // keys per workgroup
@@ -463,14 +468,17 @@ extern "C" int fz_debug_os_timing(unsigned long long *out) {
 
 // One payload column of a radix pass (HAS_PL): the tile's values staged in LDS at their keys'
 // digit-sorted slots, then written out in the same per-digit runs as the keys (coalesced).
+// (pre: column 0's values, loaded with the keys before the ranking - its load latency hides
+// behind the ranking and the look-back - or null: loaded here)
 template <typename T>
 __device__ inline void onesweep_move(const T *__restrict__ in, T *__restrict__ out, T *s, const uint16_t *lpos,
-                                     const int32_t *gp, int64_t wbase, int lane, int64_t n, int64_t valid_n, int tid) {
+                                     const int32_t *gp, int64_t wbase, int lane, int64_t n, int64_t valid_n, int tid,
+                                     const uint64_t *pre = nullptr) {
     T x[kSortItems];
 #pragma unroll
     for (int r = 0; r < kSortItems; ++r) {
         const int64_t idx = wbase + r * kWave + lane;
-        x[r] = idx < n ? in[idx] : T(0);
+        x[r] = pre ? T(pre[r]) : (idx < n ? in[idx] : T(0));
     }
     __syncthreads();  // the previous column (or the keys) has left the LDS
 #pragma unroll
@@ -537,6 +545,27 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ 
         k[r] = valid ? keys_in[idx] : KeyT(0);
         v[r] = (HAS_VALS && valid) ? vals_in[idx] : 0u;
     }
+#if FZ_OS_PREFETCH
+    // the first payload column in flight with the keys
+    constexpr bool kPre = HAS_PL;
+    uint64_t p0[kPre ? kSortItems : 1];
+    if constexpr (kPre) {
+        const int sz0 = pl.n > 0 ? pl.size[0] : 0;
+#pragma unroll
+        for (int r = 0; r < kSortItems; ++r) {
+            const int64_t idx = wbase + r * kWave + lane;
+            p0[r] = 0ull;
+            if (idx < n) {
+                if (sz0 == 8) p0[r] = static_cast<const uint64_t *>(pl.in[0])[idx];
+                else if (sz0 == 4) p0[r] = static_cast<const uint32_t *>(pl.in[0])[idx];
+                else if (sz0 == 1) p0[r] = static_cast<const uint8_t *>(pl.in[0])[idx];
+            }
+        }
+    }
+#else
+    constexpr bool kPre = false;
+    const uint64_t *p0 = nullptr;
+#endif
     uint32_t *cnt_w = s_wcnt[w];
 #ifdef FZ_OS_TIMING
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -670,15 +699,18 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ 
     if (HAS_PL) {
         // the payload columns follow their keys through the same LDS slots and per-digit runs
         for (int j = 0; j < pl.n; ++j) {
+            const uint64_t *pre = kPre && j == 0 ? p0 : nullptr;
             if (pl.size[j] == 8)
                 onesweep_move<uint64_t>(static_cast<const uint64_t *>(pl.in[j]), static_cast<uint64_t *>(pl.out[j]),
-                                        s_stage, lpos, gp, wbase, lane, n, valid_n, tid);
+                                        s_stage, lpos, gp, wbase, lane, n, valid_n, tid, pre);
             else if (pl.size[j] == 4)
                 onesweep_move<uint32_t>(static_cast<const uint32_t *>(pl.in[j]), static_cast<uint32_t *>(pl.out[j]),
-                                        reinterpret_cast<uint32_t *>(s_stage), lpos, gp, wbase, lane, n, valid_n, tid);
+                                        reinterpret_cast<uint32_t *>(s_stage), lpos, gp, wbase, lane, n, valid_n, tid,
+                                        pre);
             else
                 onesweep_move<uint8_t>(static_cast<const uint8_t *>(pl.in[j]), static_cast<uint8_t *>(pl.out[j]),
-                                       reinterpret_cast<uint8_t *>(s_stage), lpos, gp, wbase, lane, n, valid_n, tid);
+                                       reinterpret_cast<uint8_t *>(s_stage), lpos, gp, wbase, lane, n, valid_n, tid,
+                                       pre);
         }
     }
 #ifdef FZ_OS_TIMING
