@@ -380,10 +380,10 @@ constexpr int kRadix = 1 << kRadixBits;
 #define FZ_OS_PREFETCH 1
 #endif
 constexpr int kOsBlock = FZ_OS_BLOCK;        // threads per radix-pass workgroup
-constexpr int kOsWaves = kOsBlock / kWave;
 constexpr int kSortTile = FZ_OS_TILE;        // keys per workgroup
-constexpr int kSortItems = kSortTile / kOsBlock;
 static_assert(kOsBlock >= kRadix && kSortTile % kOsBlock == 0, "radix pass shape");
+constexpr int kSortTileBig = 8192, kOsBlockBig = 1024;  // the large sorts' tile shape
+constexpr int64_t kOsBigN = int64_t(1) << 22;            // keys from which a sort takes it
 
 // ---- single-sweep LSD passes (one launch per digit pass) -----------------------------------
 // One histogram kernel counts every pass's digits up front (the global digit bases of every
@@ -470,32 +470,32 @@ extern "C" int fz_debug_os_timing(unsigned long long *out) {
 // digit-sorted slots, then written out in the same per-digit runs as the keys (coalesced).
 // (pre: column 0's values, loaded with the keys before the ranking - its load latency hides
 // behind the ranking and the look-back - or null: loaded here)
-template <typename T>
+template <typename T, int ITEMS, int BLOCK>
 __device__ inline void onesweep_move(const T *__restrict__ in, T *__restrict__ out, T *s, const uint16_t *lpos,
                                      const int32_t *gp, int64_t wbase, int lane, int64_t n, int64_t valid_n, int tid,
                                      const uint64_t *pre = nullptr) {
-    T x[kSortItems];
+    T x[ITEMS];
 #pragma unroll
-    for (int r = 0; r < kSortItems; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const int64_t idx = wbase + r * kWave + lane;
         x[r] = pre ? T(pre[r]) : (idx < n ? in[idx] : T(0));
     }
     __syncthreads();  // the previous column (or the keys) has left the LDS
 #pragma unroll
-    for (int r = 0; r < kSortItems; ++r)
+    for (int r = 0; r < ITEMS; ++r)
         if (wbase + r * kWave + lane < n) s[lpos[r]] = x[r];
     __syncthreads();
 #pragma unroll
-    for (int m = 0; m < kSortItems; ++m) {
-        const int i = tid + m * kOsBlock;
+    for (int m = 0; m < ITEMS; ++m) {
+        const int i = tid + m * BLOCK;
         if (i < valid_n) out[gp[m]] = s[i];
     }
 }
 
 // KeyT: uint64_t, or uint32_t for keys of at most 32 bits (the prefix / session-index transposes:
 // 4 bytes per key less to read and write in every pass)
-template <typename KeyT, bool HAS_VALS, bool HAS_PL>
-__global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ keys_in,
+template <typename KeyT, bool HAS_VALS, bool HAS_PL, int TILE, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_onesweep(const KeyT *__restrict__ keys_in,
                                                      const uint32_t *__restrict__ vals_in,
                                                      KeyT *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
                                                      int64_t n, int shift, const unsigned long long *__restrict__ ghist,
@@ -504,15 +504,17 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ 
                                                      unsigned long long *__restrict__ gsum,
                                                      unsigned long long *__restrict__ next_hist,
                                                      RadixPayload pl) {
-    __shared__ uint64_t s_stage[kSortTile];  // the keys, then 8-byte payload columns
+    constexpr int ITEMS = TILE / BLOCK, WAVES = BLOCK / kWave;
+    static_assert(BLOCK >= kRadix && TILE % BLOCK == 0 && TILE <= 65536, "radix pass shape");
+    __shared__ uint64_t s_stage[TILE];  // the keys, then 8-byte payload columns
     KeyT *const s_keys = reinterpret_cast<KeyT *>(s_stage);
-    __shared__ uint32_t s_vals[HAS_VALS ? kSortTile : 1];
+    __shared__ uint32_t s_vals[HAS_VALS ? TILE : 1];
     __shared__ uint32_t s_run[kRadix];
-    __shared__ uint32_t s_wcnt[kOsWaves][kRadix];
+    __shared__ uint32_t s_wcnt[WAVES][kRadix];
     __shared__ uint32_t s_start[kRadix];
     __shared__ int64_t s_goff[kRadix];
-    __shared__ uint32_t s_tmp[kOsWaves];
-    __shared__ int64_t s_tmp64[kOsWaves];
+    __shared__ uint32_t s_tmp[WAVES];
+    __shared__ int64_t s_tmp64[WAVES];
     __shared__ unsigned int s_tile;
 
     const int tid = threadIdx.x;
@@ -520,12 +522,12 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ 
     if (tid == 0) s_tile = lb_take_tile(ticket, gridDim.x);
     const bool dig = tid < kRadix;  // threads [0, 256) own one digit each after the ranking
     if (next_hist && blockIdx.x == 0)  // the next sort's digit totals start from zero
-        for (int i = tid; i < kOsMaxPasses * kRadix; i += kOsBlock) next_hist[i] = 0ull;
-    for (int i = tid; i < kOsWaves * kRadix; i += kOsBlock) (&s_wcnt[0][0])[i] = 0;
+        for (int i = tid; i < kOsMaxPasses * kRadix; i += BLOCK) next_hist[i] = 0ull;
+    for (int i = tid; i < WAVES * kRadix; i += BLOCK) (&s_wcnt[0][0])[i] = 0;
     const int64_t gcount = dig ? int64_t(ghist[tid]) : 0;  // issued early: consumed after the ranking
     __syncthreads();
     const int64_t tile = s_tile;
-    const int64_t base = tile * kSortTile;
+    const int64_t base = tile * TILE;
 #ifdef FZ_OS_TIMING
     if (tid == 0) atomicMin(&g_os_first, (unsigned long long)wall_clock64());
 #endif
@@ -533,13 +535,13 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ 
     // wave w owns the contiguous slice [w * T/W, (w + 1) * T/W) of the tile; round r covers
     // its keys r * 64 + lane, so (wave, round, lane) is position order and ranking is stable with
     // wave-private digit counters - no workgroup barrier inside the ranking loop
-    const int64_t wbase = base + int64_t(w) * (kSortTile / kOsWaves);
+    const int64_t wbase = base + int64_t(w) * (TILE / WAVES);
 
-    KeyT k[kSortItems];
-    uint32_t v[kSortItems];
-    uint32_t rank[kSortItems];
+    KeyT k[ITEMS];
+    uint32_t v[ITEMS];
+    uint32_t rank[ITEMS];
 #pragma unroll
-    for (int r = 0; r < kSortItems; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const int64_t idx = wbase + r * kWave + lane;
         const bool valid = idx < n;
         k[r] = valid ? keys_in[idx] : KeyT(0);
@@ -548,11 +550,11 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ 
 #if FZ_OS_PREFETCH
     // the first payload column in flight with the keys
     constexpr bool kPre = HAS_PL;
-    uint64_t p0[kPre ? kSortItems : 1];
+    uint64_t p0[kPre ? ITEMS : 1];
     if constexpr (kPre) {
         const int sz0 = pl.n > 0 ? pl.size[0] : 0;
 #pragma unroll
-        for (int r = 0; r < kSortItems; ++r) {
+        for (int r = 0; r < ITEMS; ++r) {
             const int64_t idx = wbase + r * kWave + lane;
             p0[r] = 0ull;
             if (idx < n) {
@@ -572,7 +574,7 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ 
     OS_STAMP(6);
 #endif
 #pragma unroll
-    for (int r = 0; r < kSortItems; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const bool valid = wbase + r * kWave + lane < n;
         const uint32_t d = uint32_t(k[r] >> shift) & (kRadix - 1);
         const uint64_t peers = match_digit<kRadixBits>(d, valid);
@@ -586,7 +588,7 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ 
     uint32_t cnt = 0;
     uint64_t *my = &status[tile * kRadix + (dig ? tid : 0)];
     if (dig) {
-        for (int i = 0; i < kOsWaves; ++i) {
+        for (int i = 0; i < WAVES; ++i) {
             const uint32_t x = s_wcnt[i][tid];
             s_wcnt[i][tid] = cnt;
             cnt += x;
@@ -599,9 +601,9 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ 
         __hip_atomic_fetch_add(&gsum[(tile / kOsGroup) * kRadix + tid], (1ull << 48) | (unsigned long long)cnt,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const uint32_t tstart = block_excl_scan<uint32_t, kOsWaves>(cnt, s_tmp, (uint32_t *)nullptr);
+    const uint32_t tstart = block_excl_scan<uint32_t, WAVES>(cnt, s_tmp, (uint32_t *)nullptr);
     if (dig) s_start[tid] = tstart;  // visible to the scatter after the next scan's barriers
-    const int64_t gstart = block_excl_scan<int64_t, kOsWaves>(gcount, s_tmp64, (int64_t *)nullptr);
+    const int64_t gstart = block_excl_scan<int64_t, WAVES>(gcount, s_tmp64, (int64_t *)nullptr);
     OS_STAMP(2);
     int64_t prefix = 0;
     // (1) the earlier tiles of this tile's group one by one, nearest first, up to an inclusive word
@@ -663,9 +665,9 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ 
     }
     OS_STAMP(3);
     // stage the tile digit-sorted in LDS, then write it out in per-digit runs
-    uint16_t lpos[HAS_PL ? kSortItems : 1];  // HAS_PL: LDS slot of item r
+    uint16_t lpos[HAS_PL ? ITEMS : 1];  // HAS_PL: LDS slot of item r
 #pragma unroll
-    for (int r = 0; r < kSortItems; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const int64_t idx = wbase + r * kWave + lane;
         if (idx < n) {
             const uint32_t d = uint32_t(k[r] >> shift) & (kRadix - 1);
@@ -677,11 +679,11 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ 
     }
     __syncthreads();
     OS_STAMP(4);
-    const int64_t valid_n = (n - base) < kSortTile ? (n - base) : kSortTile;
-    int32_t gp[HAS_PL ? kSortItems : 1];  // HAS_PL: output position of LDS slot tid + m * kOsBlock
+    const int64_t valid_n = (n - base) < TILE ? (n - base) : TILE;
+    int32_t gp[HAS_PL ? ITEMS : 1];  // HAS_PL: output position of LDS slot tid + m * BLOCK
 #pragma unroll
-    for (int m = 0; m < kSortItems; ++m) {
-        const int i = tid + m * kOsBlock;
+    for (int m = 0; m < ITEMS; ++m) {
+        const int i = tid + m * BLOCK;
         if (i < valid_n) {
             const KeyT kk = s_keys[i];
             const uint32_t d = uint32_t(kk >> shift) & (kRadix - 1);
@@ -701,14 +703,14 @@ __global__ __launch_bounds__(kOsBlock) void k_onesweep(const KeyT *__restrict__ 
         for (int j = 0; j < pl.n; ++j) {
             const uint64_t *pre = kPre && j == 0 ? p0 : nullptr;
             if (pl.size[j] == 8)
-                onesweep_move<uint64_t>(static_cast<const uint64_t *>(pl.in[j]), static_cast<uint64_t *>(pl.out[j]),
+                onesweep_move<uint64_t, ITEMS, BLOCK>(static_cast<const uint64_t *>(pl.in[j]), static_cast<uint64_t *>(pl.out[j]),
                                         s_stage, lpos, gp, wbase, lane, n, valid_n, tid, pre);
             else if (pl.size[j] == 4)
-                onesweep_move<uint32_t>(static_cast<const uint32_t *>(pl.in[j]), static_cast<uint32_t *>(pl.out[j]),
+                onesweep_move<uint32_t, ITEMS, BLOCK>(static_cast<const uint32_t *>(pl.in[j]), static_cast<uint32_t *>(pl.out[j]),
                                         reinterpret_cast<uint32_t *>(s_stage), lpos, gp, wbase, lane, n, valid_n, tid,
                                         pre);
             else
-                onesweep_move<uint8_t>(static_cast<const uint8_t *>(pl.in[j]), static_cast<uint8_t *>(pl.out[j]),
+                onesweep_move<uint8_t, ITEMS, BLOCK>(static_cast<const uint8_t *>(pl.in[j]), static_cast<uint8_t *>(pl.out[j]),
                                        reinterpret_cast<uint8_t *>(s_stage), lpos, gp, wbase, lane, n, valid_n, tid,
                                        pre);
         }
@@ -741,7 +743,12 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
         return;
     }
     const int npass = (bits + kRadixBits - 1) / kRadixBits;
-    const int64_t nb = (n + kSortTile - 1) / kSortTile;
+    // large sorts (the 100 M-row tables) take 8192-key tiles of 1024 threads: per-digit runs twice
+    // as long per tile (fewer partial-line writes) and half the look-back work (same-box A/B: c3
+    // 20.5 -> 20.0 ms, c5 30.7 -> 30.0); the small sorts of config 2 keep 4096 x 512
+    const bool big = n >= kOsBigN;
+    const int64_t tile = big ? kSortTileBig : kSortTile;
+    const int64_t nb = (n + tile - 1) / tile;
     FZ_CHECK(n < (int64_t(1) << 47), "radix_sort_pairs: too many keys");
     // digit totals of every pass (one read of the keys)
     constexpr int64_t kHistWords = kOsMaxPasses * kRadix;
@@ -805,9 +812,16 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
             // algorithmic traffic of one pass: read + write every key (8 B), value (4 B) and payload
             ProbeScope ps(c, "radix_scatter", (2.0 * sizeof(KeyT) + (vals ? 8.0 : 0.0) + 2.0 * pl.bytes()) * double(n));
 #define FZ_OS_LAUNCH(V, PL)                                                                                   \
-    k_onesweep<KeyT, V, PL><<<unsigned(nb), kOsBlock, 0, c->stream>>>(ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, \
-                                                             lb.status, lb.ticket, lb.epoch, gsum + p * gwords, \
-                                                             next_hist, step)
+    do {                                                                                                      \
+        if (big)                                                                                              \
+            k_onesweep<KeyT, V, PL, kSortTileBig, kOsBlockBig><<<unsigned(nb), kOsBlockBig, 0, c->stream>>>(   \
+                ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, lb.status, lb.ticket, lb.epoch,          \
+                gsum + p * gwords, next_hist, step);                                                          \
+        else                                                                                                  \
+            k_onesweep<KeyT, V, PL, kSortTile, kOsBlock><<<unsigned(nb), kOsBlock, 0, c->stream>>>(            \
+                ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, lb.status, lb.ticket, lb.epoch,          \
+                gsum + p * gwords, next_hist, step);                                                          \
+    } while (0)
             if (pl.n > 0) {
                 if (vals)
                     FZ_OS_LAUNCH(true, true);

@@ -33,7 +33,10 @@ void segment_offsets_dn(fz_ctx *c, const uint32_t *sorted_proj, const int64_t *d
 // kept rows in LDS, gets its output base by decoupled look-back over the preceding tiles, and
 // writes (row, time, proj) of the kept rows; the last tile writes the count.  One launch instead of
 // flag -> device-wide scan -> compact.
-constexpr int kFcItems = 16;
+#ifndef FZ_FC_ITEMS
+#define FZ_FC_ITEMS 16
+#endif
+constexpr int kFcItems = FZ_FC_ITEMS;
 constexpr int kFcTile = kBlock * kFcItems;
 
 // The projects a filter can keep (k_filter_compact's tile skip): flags[p] & mask != 0; count
