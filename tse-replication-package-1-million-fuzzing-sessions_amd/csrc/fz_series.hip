@@ -333,6 +333,11 @@ __global__ __launch_bounds__(kBlock) void k_seg_sort_wave(const double *__restri
 // (key, position) inside the same workgroup (MAXN <= 4096: keys in LDS), or flagged for the
 // segmented merge sort (the 16384 class, which re-reads keys from the cache-resident column).
 constexpr int kValSkew = 32;
+#ifndef FZ_VB4_BLOCK
+#define FZ_VB4_BLOCK 1024
+#endif
+constexpr int kVb4Block = FZ_VB4_BLOCK;                 // threads per workgroup of the 2049..4096 class
+constexpr int kVb4Grid = 2048 * (1024 / FZ_VB4_BLOCK);  // its persistent grid (same threads in all)
 template <int BS, int MAXN>
 __global__ __launch_bounds__(BS) void k_seg_val_bucket(const double *__restrict__ src, const int64_t *__restrict__ offs,
                                                        int64_t S, int64_t min_len, double *__restrict__ out_val,
@@ -627,7 +632,7 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
     if (lb > 1024) {
         k_seg_val_bucket<512, 2048><<<grid(class_cap(kClassWide), 4096), 512, 0, c->stream>>>(
             src, offs, S, 1024, out.val, out.pos, class_list(kClassWide), class_n(kClassWide), flag, false);
-        k_seg_val_bucket<1024, kLdsSortMax><<<grid(class_cap(kClassWide), 2048), 1024, 0, c->stream>>>(
+        k_seg_val_bucket<kVb4Block, kLdsSortMax><<<grid(class_cap(kClassWide), kVb4Grid), kVb4Block, 0, c->stream>>>(
             src, offs, S, 2048, out.val, out.pos, class_list(kClassWide), class_n(kClassWide), flag, false);
         FZ_LAUNCH_CHECK();
     }
