@@ -86,6 +86,10 @@ def parse():
     # threads measured best (same-box A/B, scripts/gpu_shard_ab.sh: the drivers are host-bound)
     ap.add_argument("--shard-groups", default="rq3,rq4b|rq2_count,rq1,rq4a,rq2_add")
     ap.add_argument("--shard-graphs", action="store_true")
+    # software pipelining of consecutive steps (single-table graph step): LANES engines, each with
+    # its own copy of the table, store, analysis streams and recordings, take the steps in turn, so
+    # one step's store build overlaps the previous step's analyses (1 = off)
+    ap.add_argument("--lanes", type=int, default=1)
     return ap.parse_args()
 
 
@@ -164,16 +168,18 @@ def main():
             own = (lo, hi)
         else:
             own = (rank * len(t.projects) // world, (rank + 1) * len(t.projects) // world)  # weak_shard ids
-    rq1_bufs = compute.RQ1Buffers(eng)
-    bufs = {"rq2_count": compute.rq2_count_buffers(eng), "rq2_add": compute.rq2_add_buffers(eng),
-            "rq3": compute.rq3_buffers(eng), "rq4a": compute.rq4a_buffers(eng), "rq4b": compute.rq4b_buffers(eng)}
+    def make_bufs(e):
+        b = {"rq2_count": compute.rq2_count_buffers(e), "rq2_add": compute.rq2_add_buffers(e),
+             "rq3": compute.rq3_buffers(e), "rq4a": compute.rq4a_buffers(e), "rq4b": compute.rq4b_buffers(e),
+             "rq1": compute.RQ1Buffers(e)}
+        b["rq3_main"] = b["rq3_stats"] = b["rq3"]
+        return b
+    bufs = make_bufs(eng)
     launch = {"rq2_count": compute.rq2_count_launch, "rq2_add": compute.rq2_add_launch, "rq3": compute.rq3_launch,
               "rq4a": compute.rq4a_launch, "rq4b": compute.rq4b_launch}
 
     launch["rq1"] = lambda e, b: compute.rq1_launch(e, b)
-    bufs["rq1"] = rq1_bufs
     launch["rq3_main"], launch["rq3_stats"] = compute.rq3_main_launch, compute.rq3_stats_launch
-    bufs["rq3_main"] = bufs["rq3_stats"] = bufs["rq3"]
     # concurrent analyses: groups of about equal GPU time, one child engine (stream + context over
     # the same store) and one host thread each (ctypes releases the GIL during every libfz call)
     known = set(stages) | ({"rq3_main", "rq3_stats"} if "rq3" in stages else set())
@@ -250,10 +256,13 @@ def main():
         # the store build forks its independent sorts onto the (then idle) children
         eng.set_store_helpers(children[:-1][:4])  # (the library takes up to four)
 
-        def run_group(ch, names):
+        def run_group(ch, names, b=None):
             with torch.cuda.stream(ch.stream):
                 for n in names:
-                    launch[n](ch, bufs[n])
+                    launch[n](ch, (b or bufs)[n])
+
+    lanes = []  # (pipelined steps) the extra engines: eng, bufs, children, graphs, events each
+    lane_turn = [0]
 
     def serial_step():
         eng.build_store()
@@ -266,6 +275,25 @@ def main():
             if not concurrent:
                 serial_step()
                 return
+            if graphs is not None and lanes:
+                # pipelined: the lanes take the steps in turn (lane 0 = eng); a lane's store build
+                # waits only for its own previous analyses, so it overlaps the other lane's
+                L = ([None] + lanes)[lane_turn[0] % (len(lanes) + 1)]
+                lane_turn[0] += 1
+                if L is not None:
+                    le, lch, lgr, lev = L["eng"], L["children"], L["graphs"], L["events"]
+                    le.join_children()
+                    le.build_store()
+                    for ch in lch[:-1]:
+                        ch.follow_parent()
+                    for gi in order:
+                        for need, gr, mark in lgr[gi]:
+                            if need:
+                                lch[gi].stream.wait_event(lev[need])
+                            gr.launch()
+                            if mark:
+                                lev[mark].record(lch[gi].stream)
+                    return
             eng.join_children()  # the previous step's analyses have read the store
             eng.build_store()
             for ch in children[:-1]:
@@ -319,26 +347,48 @@ def main():
         # is cut into pieces at a stage that must follow another group's stage (AFTER) and after a
         # stage another group waits for - one graph per piece, events between them
         marks = set(AFTER.values())
+
+        def record_groups(chs, b):
+            out = []
+            for ch, g in zip(chs, groups):
+                pieces, cur = [], []
+                for n in g:
+                    if n in AFTER and cur:
+                        pieces.append((None if not pieces else pieces[-1][3], cur, None, None))
+                        cur = []
+                    cur.append(n)
+                    if n in marks:
+                        pieces.append((None, cur, n, None))
+                        cur = []
+                if cur:
+                    pieces.append((None, cur, None, None))
+                rec = []
+                for _, names, mark, _ in pieces:
+                    need = AFTER.get(names[0])
+                    rec.append((need, ch.record(lambda e, names=names: [launch[n](e, b[n]) for n in names]), mark))
+                out.append(rec)
+            return out
         events = {m: torch.cuda.Event() for m in marks}
-        graphs = []
-        for ch, g in zip(children, groups):
-            pieces, cur = [], []
-            for n in g:
-                if n in AFTER and cur:
-                    pieces.append((None if not pieces else pieces[-1][3], cur, None, None))
-                    cur = []
-                cur.append(n)
-                if n in marks:
-                    pieces.append((None, cur, n, None))
-                    cur = []
-            if cur:
-                pieces.append((None, cur, None, None))
-            rec = []
-            for _, names, mark, _ in pieces:
-                need = AFTER.get(names[0])
-                rec.append((need, ch.record(lambda e, names=names: [launch[n](e, bufs[n]) for n in names]), mark))
-            graphs.append(rec)
-        step()  # one untimed replay step
+        graphs = record_groups(children, bufs)
+        for _ in range(args.lanes - 1):
+            # another lane: its own engine (table copy, store, streams), warmed once, then recorded
+            e2 = E.Engine(local)
+            e2.upload(t)
+            e2.build_store()
+            b2 = make_bufs(e2)
+            ch2 = [e2.child() for _ in groups[:-1]] + [e2]
+            e2.set_store_helpers(ch2[:-1][:4])
+            e2.join_children()
+            e2.build_store()
+            for ch in ch2[:-1]:
+                ch.follow_parent()
+            for gi in order:
+                run_group(ch2[gi], groups[gi], b2)
+                torch.cuda.synchronize(dev)
+            lanes.append({"eng": e2, "bufs": b2, "children": ch2, "graphs": record_groups(ch2, b2),
+                          "events": {m: torch.cuda.Event() for m in marks}})
+        for _ in range(len(lanes) + 1):
+            step()  # one untimed replay step per lane
         torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -358,6 +408,9 @@ def main():
         step()
     if concurrent or sharded:
         eng.join_children()
+        for L in lanes:
+            L["eng"].join_children()
+            eng.stream.wait_stream(L["eng"].stream)
     ev1.record(eng.stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -451,6 +504,11 @@ def main():
             gr.close()
     for gr in (sgraphs or {}).values():
         gr.close()
+    for L in lanes:
+        for rec in L["graphs"]:
+            for _, gr, _ in rec:
+                gr.close()
+        L["eng"].close()
     eng.close()
     if sharded:
         dist.destroy_process_group()
