@@ -12,7 +12,9 @@ The oracle's per-project Python loops cannot run at this size, so the checks are
   tests (:443-458), rq4b's last session / six Spearman tests (:849-899), deltas (:725-797) and
   initial-coverage tests (:221-313), recomputed with numpy / scipy (1e-9 relative);
 * a sampled oracle comparison: 50 random projects' Shapiro-Wilk and Spearman (rq2_coverage_count.py:
-  305-322) and 50 random sessions' Brunner-Munzel p (rq4b:978-985) with scipy.
+  305-322) and 50 random sessions' Brunner-Munzel p (rq4b:978-985) with scipy;
+* and without sampling, every per-project / per-session statistic of RQ2 count and RQ4b against the
+  multi-core C++ restatement (oracle/cpu/fz_cpu.cpp) on the same table.
 
 Configs 3 and 5 hold exactly one coverage row per project-day from the same first day, so the
 (project, date) order of the table is a counting placement (no host sort of 100M rows)."""
@@ -257,3 +259,52 @@ def test_rq4b_fullsize(case):
     assert_same(r.init_g1, b, "init_g1")
     mwu_p, cliff, bm, lv = orc.rq4b_init_tests(a, b)
     assert_same((r.mwu_p, r.cliff, r.bm, r.levene), (mwu_p, cliff, bm, lv), "initial-coverage tests")
+
+
+def test_every_statistic_vs_cpu_port(case):
+    """No sampling: every per-project Shapiro-Wilk / Spearman, every per-session statistic of RQ2
+    count (the whole session transposition value for value) and every per-session quartile, count and
+    Brunner-Munzel p of RQ4b at full size, against the multi-core C++ restatement of the same scripts
+    (oracle/cpu/fz_cpu.cpp - OpenMP, long-double sums - held to the numpy oracle by
+    tests/test_cpu_baseline.py).  Integers exact, fp64 1e-9 relative (1e-12 absolute)."""
+    import os
+    from oracle import cpu_baseline as cb
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or 16), os.cpu_count() or 1))
+    out, _ = cb.run(cb.HostTables(case["t"]), ("rq2_count", "rq4b"), threads=threads)
+
+    def f(a, b, what):
+        a, b = np.asarray(a, np.float64).reshape(-1), np.asarray(b, np.float64).reshape(-1)
+        assert a.shape == b.shape, (what, a.shape, b.shape)
+        np.testing.assert_allclose(a, b, rtol=1e-9, atol=1e-12, equal_nan=True, err_msg=what)
+
+    def i(a, b, what):
+        a, b = np.asarray(a, np.int64).reshape(-1), np.asarray(b, np.int64).reshape(-1)
+        assert np.array_equal(a, b), what
+
+    r = case["rq2c"]
+    i(out["rq2c_raw_n"], r.raw_n, "rq2c raw_n")
+    i(out["rq2c_n_trend"], r.n_trend, "rq2c n_trend")
+    f(out["rq2c_sw_w"], r.sw_w, "rq2c sw_w")
+    f(out["rq2c_sw_p"], r.sw_p, "rq2c sw_p")
+    f(out["rq2c_corr"], r.corr, "rq2c corr")
+    i(out["rq2c_session_offsets"], r.session_offsets, "rq2c session offsets")
+    f(out["rq2c_session_values"], r.session_values, "rq2c session values")
+    f(out["rq2c_average"], r.average_trend, "rq2c average")
+    f(out["rq2c_median"], r.median_trend, "rq2c median")
+    f(out["rq2c_pct"], r.dist_percentiles, "rq2c percentiles")
+    f(out["rq2c_dist_mean"], r.dist_mean, "rq2c dist mean")
+    sp = r.spearman_median or (np.nan, np.nan)
+    f(out["rq2c_scalars"], [r.corr_mean, r.corr_median, sp[0], sp[1],
+                            np.nan if r.shapiro_median_p is None else r.shapiro_median_p], "rq2c scalars")
+    r = case["rq4b"]
+    i(out["rq4b_c2"], r.c2, "rq4b c2")
+    i(out["rq4b_c1"], r.c1, "rq4b c1")
+    f(out["rq4b_g2_q"], r.g2_q, "rq4b g2 quartiles")
+    f(out["rq4b_g1_q"], r.g1_q, "rq4b g1 quartiles")
+    f(out["rq4b_p_bm"], r.p_bm, "rq4b p_bm")
+    i(out["rq4b_last"], [r.last_valid_idx], "rq4b last")
+    f(out["rq4b_spearman6"], [x for pr in (r.spearman6 or []) for x in pr], "rq4b spearman6")
+    f(out["rq4b_init_g2"], r.init_g2, "rq4b init g2")
+    f(out["rq4b_init_g1"], r.init_g1, "rq4b init g1")
+    tests = [] if r.mwu_p is None else [r.mwu_p, r.cliff, *r.bm, *r.levene]
+    f(out["rq4b_tests"], tests, "rq4b tests")
