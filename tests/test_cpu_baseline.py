@@ -53,8 +53,15 @@ def test_cpu_baseline_matches_oracle(case, threads):
     t, host = case
     out, secs = cb.run(host, threads=threads)
     assert set(secs) == set(cb.TIMES)
+    check_port(out, {"rq1": orc.rq1(t), "rq2_count": orc.rq2_count(t), "rq2_add": orc.rq2_add(t), "rq3": orc.rq3(t),
+                     "rq4a": orc.rq4a(t), "rq4b": orc.rq4b(t)})
+
+
+def check_port(out, res):
+    """Every output of the C++ port (out) against result objects of the six analyses (res: the
+    oracle's, or the GPU engine's - rq/results.py dataclasses, the same fields)."""
     # RQ1
-    r = orc.rq1(t)
+    r = res["rq1"]
     _i(out["rq1_counts"], [r.n_issues_lim, r.n_issues_lim_projects, r.n_fixed_lim, r.n_fixed_lim_projects,
                            len(r.eligible), r.n_without_matching, r.n_target, r.n_target_projects,
                            r.total_fuzz_builds, len(r.matched_issue), r.n_matched_projects], "rq1 counts")
@@ -64,7 +71,7 @@ def test_cpu_baseline_matches_oracle(case, threads):
     _i(out["rq1_matched_build"], r.matched_build, "rq1 matched_build")
     _f(out["rq1_late"], _desc(r.late, rq3=False), "rq1 late")
     # RQ2 count
-    r = orc.rq2_count(t)
+    r = res["rq2_count"]
     _i(out["rq2c_raw_n"], r.raw_n, "rq2c raw_n")
     _i(out["rq2c_n_trend"], r.n_trend, "rq2c n_trend")
     _f(out["rq2c_sw_w"], r.sw_w, "rq2c sw_w")
@@ -80,7 +87,7 @@ def test_cpu_baseline_matches_oracle(case, threads):
     _f(out["rq2c_pct"], r.dist_percentiles, "rq2c percentiles")
     _f(out["rq2c_dist_mean"], r.dist_mean, "rq2c dist mean")
     # RQ2 add
-    r = orc.rq2_add(t)
+    r = res["rq2_add"]
     rows = np.stack([r.row_project, r.row_first_build, r.row_end_build, r.row_start_build, r.row_cov_i,
                      r.row_cov_i1], axis=1) if len(r.row_project) else np.zeros((0, 6), np.int64)
     _i(out["rq2a_rows"], rows, "rq2a rows")
@@ -88,7 +95,7 @@ def test_cpu_baseline_matches_oracle(case, threads):
     _f(out["rq2a_diff_coverage"], r.diff_coverage, "rq2a diff_coverage")
     _i(out["rq2a_flags"], np.stack([r.covered_is_float, r.total_is_float], axis=1), "rq2a flags")
     # RQ3
-    r = orc.rq3(t)
+    r = res["rq3"]
     _i(out["rq3_counts"], [r.n_all_issues, len(r.det_pct), len(r.non_pct)], "rq3 counts")
     _f(out["rq3_det_pct"], r.det_pct, "rq3 det_pct")
     _f(out["rq3_non_pct"], r.non_pct, "rq3 non_pct")
@@ -101,7 +108,7 @@ def test_cpu_baseline_matches_oracle(case, threads):
                  *r.brunnermunzel]
     _f(out["rq3_tests"], tests, "rq3 tests")
     # RQ4a
-    r = orc.rq4a(t)
+    r = res["rq4a"]
     _i(out["rq4a_g1_total"], r.g1_total, "rq4a g1_total")
     _i(out["rq4a_g1_det"], r.g1_det, "rq4a g1_det")
     _i(out["rq4a_g2_total"], r.g2_total, "rq4a g2_total")
@@ -113,7 +120,7 @@ def test_cpu_baseline_matches_oracle(case, threads):
     intro = list(r.intro_stats) if r.intro_stats else [np.nan] * 4
     _f(out["rq4a_scalars"], after + intro + list(r.g4_overall), "rq4a scalars")
     # RQ4b
-    r = orc.rq4b(t)
+    r = res["rq4b"]
     _i(out["rq4b_c2"], r.c2, "rq4b c2")
     _i(out["rq4b_c1"], r.c1, "rq4b c1")
     _f(out["rq4b_g2_q"], r.g2_q, "rq4b g2 quartiles")
