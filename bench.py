@@ -90,6 +90,11 @@ def parse():
     # its own copy of the table, store, analysis streams and recordings, take the steps in turn, so
     # one step's store build overlaps the previous step's analyses (1 = off)
     ap.add_argument("--lanes", type=int, default=1)
+    # strong-scaling rehearsal on one GPU (with --strong --force-sharded at world 1): the step of
+    # rank SHARD_RANK of SHARD_OF over its shard_bounds shard of the table - per-rank compute with
+    # no exchange (the collectives need the other ranks); value = that shard's rows / s
+    ap.add_argument("--shard-of", type=int, default=1)
+    ap.add_argument("--shard-rank", type=int, default=0)
     return ap.parse_args()
 
 
@@ -117,12 +122,16 @@ def main():
             dist.init_process_group("gloo", **init)
     dev = torch.device("cuda", local)
 
+    rehearsal = args.strong and world == 1 and args.shard_of > 1
     if args.strong:
         from tse_amd import parallel as par
         full = synth.generate(synth.config(args.config))
-        lo, hi = par.shard_bounds(full, world)[rank]
+        if rehearsal:
+            lo, hi = par.shard_bounds(full, args.shard_of)[args.shard_rank]
+        else:
+            lo, hi = par.shard_bounds(full, world)[rank]
         t = par.take_shard(full, lo, hi)[0]
-        job_rows = full.n_rows
+        job_rows = full.n_rows if not rehearsal else None
         del full
     else:
         cfg = synth.config(args.config, seed=synth.config(args.config).seed + 1000 * rank)
@@ -483,7 +492,9 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "int64/fp64", "data": "synthetic",
             "config": {"workload": f"{WORKLOADS.get(args.config, args.config)} ({args.config}), "
-                                   + (f"one table split over {world} ranks" if args.strong
+                                   + (f"rank {args.shard_rank} of {args.shard_of}'s shard of one table - strong-scaling "
+                                      f"rehearsal: per-rank compute, no exchange" if rehearsal
+                                      else f"one table split over {world} ranks" if args.strong
                                       else f"{len(t.projects)} projects/rank"),
                        "rows_per_rank": t.n_rows, "builds": int(len(t.b_project)), "coverage": int(len(t.c_project)),
                        "issues": int(len(t.i_project)), "stages": stages, "parallelism": f"project-shard x{world}" + (" (sharded path)" if sharded and world == 1 else ""),
