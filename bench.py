@@ -86,6 +86,10 @@ def parse():
     # threads measured best (same-box A/B, scripts/gpu_shard_ab.sh: the drivers are host-bound)
     ap.add_argument("--shard-groups", default="rq3,rq4b|rq2_count,rq1,rq4a,rq2_add")
     ap.add_argument("--shard-graphs", action="store_true")
+    # the sharded step's local phases (every driver's local kernels) as recordings on the
+    # single-table step's four analysis streams (--groups), launched together before the drivers,
+    # which then read / exchange / finish on their analysis' stream
+    ap.add_argument("--shard-local", choices=["driver", "streams"], default="driver")
     # software pipelining of consecutive steps (single-table graph step): LANES engines, each with
     # its own copy of the table, store, analysis streams and recordings, take the steps in turn, so
     # one step's store build overlaps the previous step's analyses (1 = off)
@@ -168,6 +172,19 @@ def main():
                 ch, pg = eng.child(), dist.new_group(backend=args.dist_backend)
                 for n in g:
                     skids[n], sgroups[n] = ch, pg
+            if args.shard_local == "streams":
+                # one child per analysis group of the single-table step (its stream runs the
+                # group's local phases, then each driver's finishing); the thread's process group
+                # stays the driver's
+                lgroups = [[n for n in g.split(",") if n in snames] for g in args.groups.split("|")]
+                lgroups = [g for g in lgroups if g]
+                lch = []
+                for g in lgroups:
+                    ch = eng.child()
+                    lch.append(ch)
+                    for n in g:
+                        skids[n] = ch
+                eng.set_store_helpers(lch[:4])  # (idle while the store builds: the step joins them first)
         rq1_shard = par.GpuRQ1Shard(skids.get("rq1", eng), M)
         rq3_shard = par.GpuRQ3Shard(skids.get("rq3", eng))
         rq2c_shard = par.GpuRQ2CountShard(skids.get("rq2_count", eng))
@@ -244,7 +261,7 @@ def main():
         def run_sharded(names):
             for name in names:
                 e = skids[name]
-                if sgraphs is not None:
+                if sgraphs is not None and args.shard_local == "driver":
                     # this driver's local kernels replayed from its recording right before it reads
                     # them (the next driver's local phase is enqueued only after this one's exchange
                     # and finishing kernels, as in the eager order)
@@ -336,6 +353,11 @@ def main():
         for ch in set(skids.values()):
             if ch is not eng:
                 ch.follow_parent()
+        if sgraphs is not None and args.shard_local == "streams":
+            # every local phase at once, one recording per analysis group on its own stream
+            for g, gr in sgraphs_local:
+                gr.launch()
+                mark_launched(g)
         futs = [pool.submit(run_sharded, g) for g in sthreads]
         for f in futs:
             f.result()
@@ -343,12 +365,18 @@ def main():
     # (opt-in: replaying each driver's local kernels from a recording measured no faster than the
     # eager launches - c2 3.79 vs 3.46 ms, c3 22.2 vs 21.8 ms, same box: the drivers' host work
     # between their reads hides the launches already)
-    shard_graphs = sharded and pool is not None and args.shard_graphs and not args.no_graphs
+    shard_graphs = sharded and pool is not None and (args.shard_graphs or args.shard_local == "streams") \
+        and not args.no_graphs
+    sgraphs_local = []
     for _ in range(max(args.warmup, 1 if (concurrent or shard_graphs) and not args.no_graphs else 0)):
         step()
     torch.cuda.synchronize(dev)
     if shard_graphs:
-        sgraphs = {n: skids[n].record(lambda e, n=n: local[n]()) for n in snames}
+        if args.shard_local == "streams":
+            sgraphs_local = [(g, skids[g[0]].record(lambda e, g=g: [local[n]() for n in g])) for g in lgroups]
+            sgraphs = {}
+        else:
+            sgraphs = {n: skids[n].record(lambda e, n=n: local[n]()) for n in snames}
         step()  # one untimed replay step
         torch.cuda.synchronize(dev)
     if concurrent and not args.no_graphs:
@@ -514,6 +542,8 @@ def main():
         for _, gr, _ in rec:
             gr.close()
     for gr in (sgraphs or {}).values():
+        gr.close()
+    for _, gr in sgraphs_local:
         gr.close()
     for L in lanes:
         for rec in L["graphs"]:
