@@ -88,8 +88,10 @@ def parse():
     ap.add_argument("--shard-graphs", action="store_true")
     # the sharded step's local phases (every driver's local kernels) as recordings on the
     # single-table step's four analysis streams (--groups), launched together before the drivers,
-    # which then read / exchange / finish on their analysis' stream
-    ap.add_argument("--shard-local", choices=["driver", "streams"], default="driver")
+    # which then read / exchange / finish on their analysis' stream (same-box A/B,
+    # scripts/gpu_shard_local_ab.sh: c2 3.42 -> 2.72 ms, c3 21.1 -> 19.7 ms, an eighth of c3 5.08 ->
+    # 3.95 ms); "driver": each driver launches its own local kernels
+    ap.add_argument("--shard-local", choices=["driver", "streams"], default="streams")
     # software pipelining of consecutive steps (single-table graph step): LANES engines, each with
     # its own copy of the table, store, analysis streams and recordings, take the steps in turn, so
     # one step's store build overlaps the previous step's analyses (1 = off)
