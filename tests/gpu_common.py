@@ -19,8 +19,11 @@ def _close(a, b, rtol=RTOL):
         return a is b
     if isinstance(a, float) or isinstance(b, float):
         a, b = float(a), float(b)
-        if math.isnan(a) and math.isnan(b):
-            return True
+        if math.isnan(a) or math.isnan(b):
+            return math.isnan(a) and math.isnan(b)
+        if math.isinf(a) or math.isinf(b):
+            # non-finite values compare exactly: +inf == +inf only, never inf vs a finite value
+            return a == b
         if 0.0 < a < TAIL and 0.0 < b < TAIL:
             a, b = -math.log(a), -math.log(b)
         return a == b or abs(a - b) <= rtol * max(abs(a), abs(b))
@@ -53,10 +56,15 @@ def assert_same(ours, ref, path="result", rtol=RTOL):
             assert np.array_equal(a, b), f"{path}: integer mismatch at {bad[:10] if bad is not None else '?'}"
         else:
             a, b = a.astype(np.float64), b.astype(np.float64)
+            # non-finite values compare exactly (NaN only with NaN, +-inf only with the same
+            # infinity); the tolerance applies to finite pairs only
+            fin = np.isfinite(a) & np.isfinite(b)
             tail = (a > 0) & (a < TAIL) & (b > 0) & (b < TAIL)
             if tail.any():
                 a, b = np.where(tail, -np.log(np.where(tail, a, 1.0)), a), np.where(tail, -np.log(np.where(tail, b, 1.0)), b)
-            ok = (a == b) | (np.isnan(a) & np.isnan(b)) | (np.abs(a - b) <= rtol * np.maximum(np.abs(a), np.abs(b)))
+            with np.errstate(invalid="ignore", over="ignore"):
+                near = np.abs(a - b) <= rtol * np.maximum(np.abs(a), np.abs(b))
+            ok = (a == b) | (np.isnan(a) & np.isnan(b)) | (fin & near)
             assert ok.all(), f"{path}: float mismatch at {np.nonzero(~ok.ravel())[0][:10]}"
         return
     assert _close(ours, ref, rtol), f"{path}: {ours!r} != {ref!r}"
