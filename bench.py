@@ -36,7 +36,8 @@ PROBE_KERNEL = "radix_scatter"   # headline kernel of the roofline object (DESIG
 # the per-kernel roofline table (a separate probe window after the timed region; algorithmic bytes
 # per launch as DESIGN.md 4 defines them)
 TABLE_KERNELS = ["radix_scatter", "radix_hist", "elig_hist", "seg_time_sort", "store_gather", "big_compact",
-                 "big_sub_sort", "seg_merge_sort", "filter_compact", "filter_select", "seg_reduce", "seg_spearman", "seg_rank_union", "seg_value_sort", "scan_i64"]
+                 "big_sub_sort", "seg_merge_sort", "filter_compact", "filter_select", "seg_reduce", "seg_spearman", "seg_rank_union", "seg_value_sort", "seg_qstats",
+                 "ragged_transpose", "scan_i64"]
 STAGES = ["store", "rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"]
 # analyses run concurrently after the store build: the first groups on child streams, the last on
 # the engine's own stream after the store build (about equal GPU time at config 2: rq3 0.94 ms,
@@ -177,15 +178,22 @@ def main():
             if args.shard_local == "streams":
                 # one child per analysis group of the single-table step (its stream runs the
                 # group's local phases, then each driver's finishing); the thread's process group
-                # stays the driver's
+                # stays the driver's.  libfz calls on one context must come from one thread at a
+                # time (fz.h), so a group whose drivers run in different --shard-groups threads
+                # gets one child per (group, thread) pair
+                thread_of = {n: ti for ti, g in enumerate(sthreads) for n in g}
                 lgroups = [[n for n in g.split(",") if n in snames] for g in args.groups.split("|")]
                 lgroups = [g for g in lgroups if g]
-                lch = []
-                for g in lgroups:
-                    ch = eng.child()
-                    lch.append(ch)
+                lch, by_pair = [], {}
+                for gi, g in enumerate(lgroups):
                     for n in g:
-                        skids[n] = ch
+                        key = (gi, thread_of[n])
+                        if key not in by_pair:
+                            by_pair[key] = eng.child()
+                            lch.append(by_pair[key])
+                        skids[n] = by_pair[key]
+                # the local phases are recorded per child: the drivers of one (group, thread) pair
+                lgroups = [[n for g in lgroups for n in g if skids[n] is ch] for ch in lch]
                 eng.set_store_helpers(lch[:4])  # (idle while the store builds: the step joins them first)
         rq1_shard = par.GpuRQ1Shard(skids.get("rq1", eng), M)
         rq3_shard = par.GpuRQ3Shard(skids.get("rq3", eng))
@@ -248,8 +256,8 @@ def main():
         pre_add = [False]
         shards = {"rq1": rq1_shard, "rq3": rq3_shard, "rq2_count": rq2c_shard, "rq4a": rq4a_shard,
                   "rq4b": rq4b_shard}
-        local = {n: shards[n].launch for n in shards}
-        local["rq2_add"] = lambda: launch["rq2_add"](skids["rq2_add"], bufs["rq2_add"])
+        local_launch = {n: shards[n].launch for n in shards}
+        local_launch["rq2_add"] = lambda: launch["rq2_add"](skids["rq2_add"], bufs["rq2_add"])
 
         def mark_launched(names):
             for n in names:
@@ -375,10 +383,10 @@ def main():
     torch.cuda.synchronize(dev)
     if shard_graphs:
         if args.shard_local == "streams":
-            sgraphs_local = [(g, skids[g[0]].record(lambda e, g=g: [local[n]() for n in g])) for g in lgroups]
+            sgraphs_local = [(g, skids[g[0]].record(lambda e, g=g: [local_launch[n]() for n in g])) for g in lgroups]
             sgraphs = {}
         else:
-            sgraphs = {n: skids[n].record(lambda e, n=n: local[n]()) for n in snames}
+            sgraphs = {n: skids[n].record(lambda e, n=n: local_launch[n]()) for n in snames}
         step()  # one untimed replay step
         torch.cuda.synchronize(dev)
     if concurrent and not args.no_graphs:

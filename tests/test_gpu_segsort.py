@@ -7,6 +7,8 @@ position: scipy.stats.spearmanr(range(n), x), rq2_coverage_count.py:305-322).  S
 on every class boundary; value kinds: spread (bucket path), heavy ties and one dominant value
 (skew fallback), constant, signed values with +-0.0.  Checker: numpy / scipy; bit-exact for the
 order statistics, 1e-9 relative for rho / p."""
+import math
+
 import numpy as np
 import pytest
 from scipy import stats
@@ -30,6 +32,13 @@ def _values(rng, kind, n):
         return x
     if kind == "constant":
         return np.full(n, 3.25)
+    if kind == "cluster":  # most values inside one tiny key interval: the selection refines its bucket
+        x = 50.0 + rng.uniform(0, 1e-9, n)
+        k = rng.random(n) < 0.1
+        x[k] = rng.uniform(0, 100, int(k.sum()))
+        return x
+    if kind == "powers":  # values spread over many binades (keys far from linear in the value)
+        return np.ldexp(1.0, rng.integers(-60, 60, n)) * rng.choice([1.0, 1.5], n)
     x = rng.normal(0, 10, n)  # signed, with both zeros
     x[rng.random(n) < 0.05] = 0.0
     x[rng.random(n) < 0.05] = -0.0
@@ -52,8 +61,16 @@ def _session_stats(engine, segs):
                             len(segs), max(len(s) for s in segs))
     S = len(segs)
     med = got["median"][:S].cpu().numpy()
+    avg = got["average"][:S].cpu().numpy()
     pct = got["percentiles"][:5 * S].cpu().numpy().reshape(S, 5)
+    assert int(got["ge100"][0]) == sum(len(s) >= 100 for s in segs)
     for i, s in enumerate(segs):
+        if len(s) == 0:  # an empty session: every statistic NaN
+            assert np.isnan(med[i]) and np.isnan(avg[i]) and np.isnan(pct[i]).all(), i
+            continue
+        # statistics.mean: the exactly rounded mean (double-double sum), within 1e-12 relative
+        want_mean = math.fsum(s) / len(s)
+        assert abs(avg[i] - want_mean) <= 1e-12 * abs(want_mean) + 1e-300, (i, len(s), avg[i], want_mean)
         # the per-session order of equal values follows the arrival order: compare as multisets
         assert med[i] == np.median(s) or (np.isnan(med[i]) and np.isnan(np.median(s))), (i, len(s))
         want = np.percentile(s, [5, 25, 50, 75, 95])
@@ -106,3 +123,28 @@ def test_many_segments_lists(engine):
     segs = _segments(9, lengths, KINDS)
     _session_stats(engine, segs)
     _spearman(engine, segs[:2000] + segs[-2:])
+
+
+# The per-session statistics by SELECTION (fz_series.hip seg_qstats: no sorted copy) run when no
+# segment exceeds 16384 values (a session holds one value per project); the lists above reach 40000
+# and take the sort path.  Same checks against numpy on lengths up to the selection's bound.
+QS_LENGTHS = [n for n in LENGTHS if n <= 16_384]
+QS_KINDS = KINDS + ["cluster", "powers"]
+
+
+@pytest.mark.parametrize("kind", QS_KINDS)
+def test_session_order_stats_selection(engine, kind):
+    _session_stats(engine, _segments(21 + QS_KINDS.index(kind), QS_LENGTHS, [kind]))
+
+
+def test_session_order_stats_selection_mixed(engine):
+    _session_stats(engine, _segments(6, QS_LENGTHS * 2 + [0, 0, 5], QS_KINDS))
+
+
+def test_session_order_stats_selection_many_segments(engine):
+    """> 16384 segments, sizes in any order (the size-class lists of the workgroup classes), empty
+    segments between them."""
+    rng = np.random.default_rng(4)
+    lengths = rng.choice([0, 1, 3, 8, 9, 40, 64, 65, 300, 1025, 3000, 9000], size=20_000,
+                         p=[.05, .15, .2, .1, .1, .2, .05, .05, .06, .02, .01, .01]).tolist() + [16_384]
+    _session_stats(engine, _segments(10, lengths, QS_KINDS))

@@ -70,8 +70,14 @@ thread_local std::string g_err;
 
 template <typename F>
 int guarded(fz_ctx *c, F &&f) {
+    struct InCall {  // the context's in-call flag for the duration of the call
+        fz_ctx *c;
+        explicit InCall(fz_ctx *x) : c(x) { if (c) c->in_call.fetch_add(1); }
+        ~InCall() { if (c) c->in_call.fetch_sub(1); }
+    };
     try {
         if (!c) throw fz::Error(FZ_E_INVALID, "null fz_ctx");
+        InCall ic(c);
         FZ_HIP(hipSetDevice(c->device));
         c->arena.reset();
         f();

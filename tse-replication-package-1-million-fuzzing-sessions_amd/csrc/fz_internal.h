@@ -10,6 +10,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <initializer_list>
@@ -248,6 +249,10 @@ struct fz_ctx {
     // built): the build forks the tables' independent sorts onto their streams / contexts
     std::vector<fz_ctx *> helpers;
     hipEvent_t ev_fork = nullptr, ev_join[4] = {};
+    // set while a public libfz call runs on this context (fz_api.hip guarded()): the store build
+    // refuses helpers that are inside a call of their own (FZ_E_STATE) instead of racing on their
+    // arena and look-back state
+    std::atomic<int> in_call{0};
 };
 
 namespace fz {

@@ -5,11 +5,12 @@
 //   trend = covered/total*100 (:300-303)                         -> elementwise fp64
 //   shapiro / spearmanr per project (:305-322)                   -> segmented sort + tie ranks +
 //        chunked segmented reductions (fz_series.hip)
-//   coverage_by_session_index transpose (:330-333)               -> radix sort on (index, project)
-//   per-session mean/median/percentiles (:139-152, :439-440)     -> segmented sort per session
+//   coverage_by_session_index transpose (:330-333)               -> ragged transpose (fz_transpose.h)
+//   per-session mean/median/percentiles (:139-152, :439-440)     -> order-statistic selection per session
 //   spearman/shapiro of the median trend (:443-458)              -> the same kernels, one segment
 #include "fz_seg.h"
 #include "fz_stats.h"
+#include "fz_transpose.h"
 
 namespace fz {
 
@@ -54,16 +55,21 @@ struct CountZeroTotal {
 
 // statistics.mean / median + np.percentile(5, 25, 50, 75, 95) of every session segment; sessions
 // with >= 100 values counted into *d_ge100 (which must be zero on entry)
-void session_stats(fz_ctx *c, const double *sv, const Segs &ses, const int32_t *sseg, double *average, double *median,
-                   double *pcts, int64_t *d_ge100) {
+// (*d_ge100 zero on entry)
+void session_stats(fz_ctx *c, const double *sv, const Segs &ses, double *average, double *median, double *pcts,
+                   int64_t *d_ge100) {
+    const double q5[5] = {5.0, 25.0, 50.0, 75.0, 95.0};
+    if (seg_qstats_ok(ses)) {  // order statistics by selection: no sorted copy of the sessions
+        seg_qstats(c, sv, ses, q5, 5, average, median, pcts, d_ge100);
+        return;
+    }
     ChunkedSegs cs2 = chunked(c, ses);
-    SortedSegs ss2 = seg_sort_f64(c, sv, ses, sseg);
+    SortedSegs ss2 = seg_sort_f64(c, sv, ses, nullptr);
     const int64_t *soffs = ses.offs;
     per_seg(c, ses.S, [=] __device__(int64_t i) {
         if (soffs[i + 1] - soffs[i] >= 100) atomic_add_i64(d_ge100, 1);
     });
     seg_mean(c, cs2, sv, average);
-    const double q5[5] = {5.0, 25.0, 50.0, 75.0, 95.0};
     seg_percentiles(c, ses, ss2.val, q5, 5, pcts, median);
 }
 
@@ -123,7 +129,7 @@ void rq2_session_stats(fz_ctx *c, const double *values, const int64_t *session_i
     });
     segment_offsets_dn(c, sid, d_n, n > 0 ? n : 1, S, offs);
     Segs ses{S, offs, n, max_len};
-    session_stats(c, sv, ses, reinterpret_cast<const int32_t *>(sid), average, median, pcts, n_ge100);
+    session_stats(c, sv, ses, average, median, pcts, n_ge100);
 }
 
 // The same from values already grouped by session (offs [S + 1], offs[0] = 0) - a shard's
@@ -133,7 +139,7 @@ void rq2_session_stats_grouped(fz_ctx *c, const double *values, const int64_t *o
     dev_fill(c, n_ge100, 0, 8);
     FZ_CHECK(S < (int64_t(1) << 31), "fz_rq2_session_stats_grouped: too many sessions");
     Segs ses{S, offs, n, max_len};
-    session_stats(c, values, ses, segment_ids(c, ses), average, median, pcts, n_ge100);
+    session_stats(c, values, ses, average, median, pcts, n_ge100);
 }
 
 void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
@@ -195,38 +201,43 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     spearman_index_sorted(c, cs, segid, ss, o->corr, nullptr);
     seg_shapiro(c, cs, tv, ss, o->sw_w, o->sw_p);
 
-    // coverage_by_session_index: order by (index within project, project) - the values are in
-    // project order already, so a stable sort on the index alone keeps projects in order
-    // (the trend values ride along as the sort's payload, coming out in session order - no random
-    // gather through a permutation afterwards)
-    const int ibits = bits_for(uint64_t(M));
-    uint32_t *key = c->arena.get<uint32_t>(NC);  // (an index within a project: < 2^31 rows)
-    const uint32_t *tproj = T.proj;
-    map_n(c, NC, nullptr, [=] __device__(int64_t j) {
-        const int64_t live = *d_nt;
-        key[j] = j < live ? uint32_t(j - toffs[tproj[j]]) : uint32_t(M);  // M: past every real index
-    });
-    RadixPayload pl;
-    pl.n = 1;
-    pl.in[0] = tv;
-    pl.size[0] = 8;
-    uint32_t *no_vals = nullptr;
-    radix_sort_pairs_payload32(c, key, no_vals, NC, ibits, pl);
-    const double *stv = static_cast<const double *>(pl.out[0]);
+    // coverage_by_session_index (:329-333): session i = value i of every project longer than i, in
+    // project order - the ragged transpose (fz_transpose.h) moves each value straight to its slot
     double *sv = o->session_values;
-    uint32_t *sid = c->arena.get<uint32_t>(NC);
-    map_n(c, NC, nullptr, [=] __device__(int64_t k) {
-        const int64_t live = *d_nt;
-        sid[k] = uint32_t(key[k]);
-        if (k < live) sv[k] = stv[k];
-    });
-    segment_offsets_dn(c, sid, d_nt, NC, M, o->session_offsets);
+    if (ragged_transpose_ok(P, M, 1)) {
+        const double *tvc = tv;
+        ragged_transpose<1>(c, T.offs, P, M, NC, [=] __device__(int64_t j) { return tvc[j]; }, RtOneGroup{}, sv,
+                            o->session_offsets);
+    } else {
+        // (tables past the transpose's bounds) order by (index within project, project): the values
+        // are in project order, so a stable radix sort on the index alone keeps projects in order
+        const int ibits = bits_for(uint64_t(M));
+        uint32_t *key = c->arena.get<uint32_t>(NC);  // (an index within a project: < 2^31 rows)
+        const uint32_t *tproj = T.proj;
+        map_n(c, NC, nullptr, [=] __device__(int64_t j) {
+            const int64_t live = *d_nt;
+            key[j] = j < live ? uint32_t(j - toffs[tproj[j]]) : uint32_t(M);  // M: past every real index
+        });
+        RadixPayload pl;
+        pl.n = 1;
+        pl.in[0] = tv;
+        pl.size[0] = 8;
+        uint32_t *no_vals = nullptr;
+        radix_sort_pairs_payload32(c, key, no_vals, NC, ibits, pl);
+        const double *stv = static_cast<const double *>(pl.out[0]);
+        uint32_t *sid = c->arena.get<uint32_t>(NC);
+        map_n(c, NC, nullptr, [=] __device__(int64_t k) {
+            const int64_t live = *d_nt;
+            sid[k] = uint32_t(key[k]);
+            if (k < live) sv[k] = stv[k];
+        });
+        segment_offsets_dn(c, sid, d_nt, NC, M, o->session_offsets);
+    }
     if (flags & FZ_RQ2C_SKIP_SESSION_STATS) return;
 
     // per-session statistics (sessions are non-increasing in size: >= 100 is a prefix)
     Segs ses{M, o->session_offsets, NC, P};  // a session holds at most one value per project
-    session_stats(c, sv, ses, reinterpret_cast<const int32_t *>(sid), o->average_trend, o->median_trend,
-                  o->dist_percentiles, counts + FZ_RQ2C_GE100);
+    session_stats(c, sv, ses, o->average_trend, o->median_trend, o->dist_percentiles, counts + FZ_RQ2C_GE100);
     dev_copy(c, o->dist_mean, o->average_trend, (M > 0 ? M : 1) * 8);
 
     // tests on the median trend (one segment of K values)

@@ -12,6 +12,7 @@
 //         BM / Levene (:221-313)                        -> per-project binary searches + rank tests
 #include "fz_seg.h"
 #include "fz_stats.h"
+#include "fz_transpose.h"
 
 namespace fz {
 
@@ -318,6 +319,8 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
     // LDS for sessions of up to kBmLdsMax values, else the device-wide rank passes
     const bool lds = P > kBmHalvesMax && sess_len <= kBmLdsMax;
     const bool small = P <= kBmHalvesMax || lds;
+    if (!small && !sid2)  // (segment ids only for the device-wide rank passes; null from the transpose)
+        sid2 = reinterpret_cast<const uint32_t *>(segment_ids(c, Segs{S2, offs2, NC}));
     int32_t *sess = small ? nullptr : c->arena.get<int32_t>(NC);
     uint8_t *grp2 = small ? nullptr : c->arena.get<uint8_t>(NC);
     int64_t *soffs = small && !lds ? nullptr : c->arena.get<int64_t>(MM + 1);
@@ -334,7 +337,7 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
         }
     });
     Segs sg2{S2, offs2, NC, P};
-    SortedSegs ss2 = seg_sort_f64(c, v2, sg2, reinterpret_cast<const int32_t *>(sid2));
+    SortedSegs ss2 = seg_sort_f64(c, v2, sg2, nullptr);
     double *qq = c->arena.get<double>(S2 * 3);
     const double q3[3] = {25.0, 50.0, 75.0};
     seg_percentiles(c, sg2, ss2.val, q3, 3, qq);
@@ -482,41 +485,51 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
     int64_t *c2 = o->c2, *c1 = o->c1;
     double *g2q = o->g2_q, *g1q = o->g1_q;
     if (!sharded || contribute) {
-        // (session, group) key per value: G2 -> group 0 (x), G1 -> group 1 (y); the values are in
-        // project order, so the stable sort on (session, group) alone keeps projects in order
-        // the values (read in view order: rising rows) ride along as the sort's payload - no random
-        // double gather through the permutation afterwards
         const int64_t S2 = 2 * MM;
-        const int sbits = bits_for(uint64_t(S2 + 1));
-        uint32_t *key = c->arena.get<uint32_t>(NC);  // (2 * index + group < 2^32: < 2^31 rows)
-        double *fv = c->arena.get<double>(NC);
-        map_n(c, NC, nullptr, [=] __device__(int64_t j) {
-            if (j < *d_nf) {
-                const uint32_t p = fproj[j];
-                const uint32_t grp = (member[p] & 2) ? 0u : 1u;
-                key[j] = uint32_t(j - foffs[p]) * 2u + grp;
-                fv[j] = cov[frow[j]];
-            } else {
-                key[j] = uint32_t(S2);
-            }
-        });
-        RadixPayload pl;
-        pl.n = 1;
-        pl.in[0] = fv;
-        pl.size[0] = 8;
-        uint32_t *no_vals = nullptr;
-        radix_sort_pairs_payload32(c, key, no_vals, NC, sbits, pl);
-        const double *sfv = static_cast<const double *>(pl.out[0]);
-        double *v2 = contribute ? o->trend_values : c->arena.get<double>(NC);
-        uint32_t *sid2 = c->arena.get<uint32_t>(NC);
-        map_n(c, NC, nullptr, [=] __device__(int64_t k) {
-            sid2[k] = uint32_t(key[k]);
-            if (k < *d_nf) v2[k] = sfv[k];
-        });
-        if (contribute) segment_offsets_dn(c, sid2, d_nf, NC, S2, o->trend_offsets);
-        if (!sharded)
-            rq4b_sessions(c, v2, sid2, NC, d_nf, MM, P, P, c2, c1, g2q, g1q, o->p_bm,
-                          contribute ? o->trend_offsets : nullptr);  // <= 1 value per project
+        if (ragged_transpose_ok(P, MM, 2)) {
+            // the ragged transpose (fz_transpose.h): value i of project p straight to segment
+            // (i, group) in project order, read through the view's rows - no sort, no gather pass
+            double *v2 = contribute ? o->trend_values : c->arena.get<double>(NC);
+            int64_t *o2 = contribute ? o->trend_offsets : c->arena.get<int64_t>(S2 + 1);
+            ragged_transpose<2>(c, foffs, P, MM, NC, [=] __device__(int64_t j) { return cov[frow[j]]; },
+                                [=] __device__(int64_t p) { return (member[p] & 2) ? 0 : 1; }, v2, o2);
+            if (!sharded) rq4b_sessions(c, v2, nullptr, NC, d_nf, MM, P, P, c2, c1, g2q, g1q, o->p_bm, o2);
+        } else {
+            // (session, group) key per value: G2 -> group 0 (x), G1 -> group 1 (y); the values are in
+            // project order, so the stable sort on (session, group) alone keeps projects in order
+            // the values (read in view order: rising rows) ride along as the sort's payload - no random
+            // double gather through the permutation afterwards
+            const int sbits = bits_for(uint64_t(S2 + 1));
+            uint32_t *key = c->arena.get<uint32_t>(NC);  // (2 * index + group < 2^32: < 2^31 rows)
+            double *fv = c->arena.get<double>(NC);
+            map_n(c, NC, nullptr, [=] __device__(int64_t j) {
+                if (j < *d_nf) {
+                    const uint32_t p = fproj[j];
+                    const uint32_t grp = (member[p] & 2) ? 0u : 1u;
+                    key[j] = uint32_t(j - foffs[p]) * 2u + grp;
+                    fv[j] = cov[frow[j]];
+                } else {
+                    key[j] = uint32_t(S2);
+                }
+            });
+            RadixPayload pl;
+            pl.n = 1;
+            pl.in[0] = fv;
+            pl.size[0] = 8;
+            uint32_t *no_vals = nullptr;
+            radix_sort_pairs_payload32(c, key, no_vals, NC, sbits, pl);
+            const double *sfv = static_cast<const double *>(pl.out[0]);
+            double *v2 = contribute ? o->trend_values : c->arena.get<double>(NC);
+            uint32_t *sid2 = c->arena.get<uint32_t>(NC);
+            map_n(c, NC, nullptr, [=] __device__(int64_t k) {
+                sid2[k] = uint32_t(key[k]);
+                if (k < *d_nf) v2[k] = sfv[k];
+            });
+            if (contribute) segment_offsets_dn(c, sid2, d_nf, NC, S2, o->trend_offsets);
+            if (!sharded)
+                rq4b_sessions(c, v2, sid2, NC, d_nf, MM, P, P, c2, c1, g2q, g1q, o->p_bm,
+                              contribute ? o->trend_offsets : nullptr);  // <= 1 value per project
+        }
     }
     // last session with both groups >= 100 (:849-860); Spearman of the quartile sequences (:879-899)
     if (!sharded) rq4b_trends(c, c2, c1, g2q, g1q, MM, counts + FZ_RQ4B_LAST, o->spearman6);

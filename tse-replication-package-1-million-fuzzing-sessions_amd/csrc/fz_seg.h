@@ -362,6 +362,14 @@ void seg_mean(fz_ctx *c, const ChunkedSegs &cs, const double *vals, double *out)
 // statistics.median / np.median of sorted segments: middle value or (a + b) / 2 -> out[S].
 void seg_median(fz_ctx *c, const Segs &sg, const double *sorted, double *out);
 
+// statistics.mean (double-double sum / n), statistics.median and numpy.percentile(q[j]) of every
+// segment by selection (no sorted copy): mean[S], median[S], pcts[S * nq]; segments of >= 100
+// values added to *d_ge100.  Segments of at most kQsMax values (seg_qstats_ok).
+constexpr int64_t kQsMax = 16384;
+bool seg_qstats_ok(const Segs &sg);
+void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_host, int nq, double *mean,
+                double *median, double *pcts, int64_t *d_ge100);
+
 // Two-sample rank tests per segment (x = grp 0, y = grp 1): Brunner-Munzel and Mann-Whitney U
 // (asymptotic).  Any output pointer may be null.  All outputs are [S] doubles.
 struct RankTestOut {

@@ -1669,6 +1669,437 @@ void seg_median(fz_ctx *c, const Segs &sg, const double *sorted, double *out) {
     });
 }
 
+// ------------------------------------------------- order statistics without sorting (seg_qstats)
+// RQ2's per-session statistics (rq2_coverage_count.py:139-152, :439-440) need the mean, the
+// median and five percentiles of each session - at most 12 order statistics, not the whole sorted
+// session.  Each segment's order statistics are SELECTED: one read of its values (the mean's
+// double-double sum on the way), a value-bucket histogram over the segment's key range in LDS (the
+// bucket of key k is floor((k - lo) * nb / (hi - lo + 1)), monotone in k, so a bucket holds exactly
+// the values of a key interval), one block scan, and each wanted rank's bucket ranked in one wave.
+// A bucket of more than 64 values (clusters) is refined by re-histogramming its key interval until
+// it holds <= 64 values or one key.  Nothing is written but the statistics.
+struct QsArgs {
+    double q[8];
+    int nq;
+    double *mean, *median, *pcts;  // [S], [S], [S * nq]
+    int64_t *d_ge100;              // += segments of >= 100 values
+};
+constexpr int kQsMaxT = 2 * 8 + 2;  // ranks wanted per segment (two per percentile, two for the median)
+
+// rank t of the nt = 2 + 2 * nq order statistics a segment of n >= 1 values needs: statistics.median
+// reads ranks 0, 1; np_percentile_sorted(q[j]) reads ranks 2 + 2j, 3 + 2j (its prev / next index)
+__device__ inline int64_t qs_rank(int64_t n, const QsArgs &a, int t) {
+    if (t == 0) return n / 2;
+    if (t == 1) return (n & 1) ? n / 2 : n / 2 - 1;
+    const int j = (t - 2) >> 1;
+    const double vi = double(n - 1) * (a.q[j] / 100.0);
+    int64_t r = int64_t(floor(vi)) + ((t - 2) & 1);
+    return r > n - 1 ? n - 1 : (r < 0 ? 0 : r);
+}
+
+// the statistics of one segment from its order statistics get(rank) (ranks from qs_ranks)
+template <typename Get>
+__device__ inline void qs_write(const QsArgs &a, int64_t s, int64_t n, double sum, Get get) {
+    if (n <= 0) {
+        a.mean[s] = NAN;
+        a.median[s] = NAN;
+        for (int j = 0; j < a.nq; ++j) a.pcts[s * a.nq + j] = NAN;
+        return;
+    }
+    a.mean[s] = sum / double(n);
+    a.median[s] = (n & 1) ? get(n / 2) : (get(n / 2 - 1) + get(n / 2)) / 2.0;
+    for (int j = 0; j < a.nq; ++j) a.pcts[s * a.nq + j] = np_percentile_sorted(get, n, a.q[j]);
+}
+
+// Segments of <= kTinySeg values.  Wave v takes 64 consecutive segments (lane l: segment 64v + l):
+// a segment of <= kMicroSeg values is finished by its lane (register sorting network), the others
+// one after another by the whole wave (64-lane bitonic network).  Longer segments are skipped.
+__global__ __launch_bounds__(kBlock) void k_qs_small(const double *__restrict__ src, const int64_t *__restrict__ offs,
+                                                     int64_t S, QsArgs a) {
+    const int lane = lane_id();
+    const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
+    for (int64_t v = int64_t(blockIdx.x) * (kBlock / kWave) + wave_id(); v * 64 < S; v += nwaves) {
+        const int64_t s = v * 64 + lane;
+        const int64_t b = s < S ? offs[s] : 0;
+        const int64_t n = s < S ? offs[s + 1] - b : -1;
+        if (n >= 0 && n <= kMicroSeg) {
+            uint64_t k[kMicroSeg];
+            DD acc{0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < kMicroSeg; ++q) {
+                const double x = q < n ? src[b + q] : 0.0;
+                if (q < n) acc = dd_add_d(acc, x);
+                k[q] = q < n ? f64_key(x) : ~0ull;
+            }
+            constexpr int net[19][2] = {{0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 2}, {1, 3}, {4, 6}, {5, 7}, {1, 2}, {5, 6},
+                                        {0, 4}, {1, 5}, {2, 6}, {3, 7}, {2, 4}, {3, 5}, {1, 2}, {3, 4}, {5, 6}};
+#pragma unroll
+            for (int c = 0; c < 19; ++c) {
+                const uint64_t x = k[net[c][0]], y = k[net[c][1]];
+                k[net[c][0]] = x < y ? x : y;
+                k[net[c][1]] = x < y ? y : x;
+            }
+            auto get = [&](int64_t j) {
+                uint64_t r = k[0];
+#pragma unroll
+                for (int q = 1; q < kMicroSeg; ++q) r = j == q ? k[q] : r;
+                return f64_from_key(r);
+            };
+            qs_write(a, s, n, acc.hi + acc.lo, get);
+        }
+        uint64_t tiny = __ballot(n > kMicroSeg && n <= kTinySeg);
+        while (tiny) {
+            const int l = __ffsll((unsigned long long)tiny) - 1;
+            tiny &= tiny - 1;
+            const int64_t st = v * 64 + l;
+            const int64_t sb = __shfl(b, l, 64);
+            const int sn = int(__shfl(n, l, 64));
+            const double x = lane < sn ? src[sb + lane] : 0.0;
+            DD acc = wave_dd_sum(DD{lane < sn ? x : 0.0, 0.0});
+            unsigned long long key = lane < sn ? f64_key(x) : ~0ull;
+#pragma unroll
+            for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+                for (int j = kk >> 1; j > 0; j >>= 1) {
+                    const unsigned long long ok = __shfl_xor(key, j, 64);
+                    const bool want_min = ((lane & j) == 0) == ((lane & kk) == 0);
+                    if (want_min == (ok < key)) key = ok;
+                }
+            }
+            // every rank any statistic reads, gathered by shuffles (all lanes take part)
+            const int nt = 2 + 2 * a.nq;
+            int rk[kQsMaxT];
+            double rv[kQsMaxT];
+#pragma unroll
+            for (int t = 0; t < kQsMaxT; ++t) {
+                rk[t] = t < nt ? int(qs_rank(sn, a, t)) : -1;
+                rv[t] = f64_from_key(__shfl(key, rk[t] < 0 ? 0 : rk[t], 64));
+            }
+            if (lane == 0) {
+                auto get = [&](int64_t j) {
+                    double r = 0.0;
+#pragma unroll
+                    for (int t = 0; t < kQsMaxT; ++t) r = rk[t] == j ? rv[t] : r;
+                    return r;
+                };
+                qs_write(a, st, sn, acc.hi + acc.lo, get);
+            }
+        }
+    }
+}
+
+// Segments of min_len < n <= MAXN values, one workgroup each: every segment, or (very many
+// segments) those of up to two size-class lists (seg_lists).
+template <int BS, int MAXN>
+__global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src, const int64_t *__restrict__ offs,
+                                                 int64_t S, int64_t min_len, const int32_t *__restrict__ l1,
+                                                 const int64_t *__restrict__ n1, const int32_t *__restrict__ l2,
+                                                 const int64_t *__restrict__ n2, QsArgs a) {
+    constexpr int NW = BS / kWave;
+    constexpr int IPT = MAXN / BS;                // values per thread
+    constexpr int NB = MAXN < 4096 ? MAXN : 4096;  // buckets
+    constexpr int BPT = NB / BS > 0 ? NB / BS : 1;
+    static_assert(MAXN % BS == 0 && NB % BS == 0, "qstats shape");
+    __shared__ uint32_t s_cnt[NB + 1];
+    __shared__ uint8_t s_map[NB];
+    __shared__ uint64_t s_list[kQsMaxT][64];
+    __shared__ uint32_t s_fill[kQsMaxT];
+    __shared__ uint64_t s_lo[NW], s_hi[NW];
+    __shared__ double s_dhi[NW], s_dlo[NW];
+    __shared__ uint32_t s_tmp[NW];
+    __shared__ int64_t s_tb[kQsMaxT], s_toff[kQsMaxT], s_tsz[kQsMaxT];
+    __shared__ int s_tslot[kQsMaxT];
+    __shared__ uint64_t s_res[kQsMaxT];
+    __shared__ int64_t s_r, s_rc;
+    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
+    int64_t ge100 = 0;
+    const int64_t ln1 = l1 ? *n1 : S, ln = l1 ? ln1 + (l2 ? *n2 : 0) : S;
+    for (int64_t it = blockIdx.x; it < ln; it += gridDim.x) {
+        const int64_t s = l1 ? (it < ln1 ? l1[it] : l2[it - ln1]) : it;
+        const int64_t b = offs[s];
+        const int64_t n = offs[s + 1] - b;
+        if (n <= min_len || n > MAXN) continue;
+        uint64_t k[IPT];
+        uint64_t lo = ~0ull, hi = 0ull;
+        DD acc{0.0, 0.0};
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int64_t i = tid + int64_t(m) * BS;
+            const double x = i < n ? src[b + i] : 0.0;
+            k[m] = i < n ? f64_key(x) : 0ull;
+            if (i < n) {
+                acc = dd_add_d(acc, x);
+                lo = k[m] < lo ? k[m] : lo;
+                hi = k[m] > hi ? k[m] : hi;
+            }
+        }
+        lo = wave_min(lo);
+        hi = wave_max(hi);
+        acc = wave_dd_sum(acc);
+        if (lane == 0) {
+            s_lo[w] = lo;
+            s_hi[w] = hi;
+            s_dhi[w] = acc.hi;
+            s_dlo[w] = acc.lo;
+        }
+        const int nb = n < NB ? int(n) : NB;
+        for (int j = tid; j <= nb; j += BS) s_cnt[j] = 0u;
+        for (int j = tid; j < nb; j += BS) s_map[j] = 0xff;
+        __syncthreads();
+        lo = s_lo[0];
+        hi = s_hi[0];
+#pragma unroll
+        for (int q = 1; q < NW; ++q) {
+            lo = s_lo[q] < lo ? s_lo[q] : lo;
+            hi = s_hi[q] > hi ? s_hi[q] : hi;
+        }
+        const int nt = 2 + 2 * a.nq;
+        const double scale = double(nb) / (double(hi - lo) + 1.0);
+        auto bucket = [&](uint64_t key, uint64_t klo, double sc, int nbk) {
+            uint32_t q = uint32_t(double(key - klo) * sc);
+            return q < uint32_t(nbk) ? q : uint32_t(nbk - 1);
+        };
+        if (lo != hi) {
+#pragma unroll
+            for (int m = 0; m < IPT; ++m)
+                if (tid + int64_t(m) * BS < n) atomicAdd(&s_cnt[bucket(k[m], lo, scale, nb)], 1u);
+            __syncthreads();
+            // bucket starts: thread t scans buckets [t * BPT, t * BPT + BPT)
+            uint32_t sum = 0;
+#pragma unroll
+            for (int e = 0; e < BPT; ++e) sum += tid * BPT + e < nb ? s_cnt[tid * BPT + e] : 0u;
+            uint32_t run = block_excl_scan<uint32_t, NW>(sum, s_tmp, (uint32_t *)nullptr);
+#pragma unroll
+            for (int e = 0; e < BPT; ++e) {
+                if (tid * BPT + e < nb) {
+                    const uint32_t ce = s_cnt[tid * BPT + e];
+                    s_cnt[tid * BPT + e] = run;
+                    run += ce;
+                }
+            }
+            if (tid == 0) s_cnt[nb] = uint32_t(n);
+            __syncthreads();
+            if (tid < nt) {  // the bucket holding rank rk[tid]: the last start <= rank
+                const uint32_t r = uint32_t(qs_rank(n, a, tid));
+                int l0 = 0, h0 = nb - 1;
+                while (l0 < h0) {
+                    const int mid = (l0 + h0 + 1) >> 1;
+                    if (s_cnt[mid] <= r) l0 = mid;
+                    else h0 = mid - 1;
+                }
+                s_tb[tid] = l0;
+                s_toff[tid] = int64_t(r) - int64_t(s_cnt[l0]);
+                s_tsz[tid] = int64_t(s_cnt[l0 + 1]) - int64_t(s_cnt[l0]);
+            }
+            __syncthreads();
+            if (tid == 0) {  // one list slot per distinct small target bucket
+                int used = 0;
+                for (int t = 0; t < nt; ++t) {
+                    int slot = -1;
+                    if (s_tsz[t] <= 64) {
+                        for (int u = 0; u < t; ++u)
+                            if (s_tslot[u] >= 0 && s_tb[u] == s_tb[t]) slot = s_tslot[u];
+                        if (slot < 0) {
+                            slot = used++;
+                            s_fill[slot] = 0u;
+                            s_map[s_tb[t]] = uint8_t(slot);
+                        }
+                    }
+                    s_tslot[t] = slot;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int m = 0; m < IPT; ++m) {
+                if (tid + int64_t(m) * BS < n) {
+                    const uint8_t slot = s_map[bucket(k[m], lo, scale, nb)];
+                    if (slot != 0xff) s_list[slot][atomicAdd(&s_fill[slot], 1u)] = k[m];
+                }
+            }
+            __syncthreads();
+            for (int t = w; t < nt; t += NW) {  // rank inside the bucket (ties: any of them)
+                const int slot = s_tslot[t];
+                if (slot < 0) continue;
+                const int sz = int(s_tsz[t]);
+                const uint64_t e = lane < sz ? s_list[slot][lane] : ~0ull;
+                int r = 0;
+                for (int j = 0; j < sz; ++j) {
+                    const uint64_t o = s_list[slot][j];
+                    r += (o < e) || (o == e && j < lane);
+                }
+                if (lane < sz && r == int(s_toff[t])) s_res[t] = e;
+            }
+            __syncthreads();
+            // a target bucket of more than 64 values: narrow its key interval until it holds <= 64
+            // values or one key (uniform control flow: every thread runs the same rounds)
+            for (int t = 0; t < nt; ++t) {
+                if (s_tslot[t] >= 0) continue;
+                // the bucket's key interval [rlo, rhi] (a bucket = the values of one key interval)
+                const uint32_t tb = uint32_t(s_tb[t]);
+                uint64_t rlo = ~0ull, rhi = 0ull;
+#pragma unroll
+                for (int m = 0; m < IPT; ++m)
+                    if (tid + int64_t(m) * BS < n && bucket(k[m], lo, scale, nb) == tb) {
+                        rlo = k[m] < rlo ? k[m] : rlo;
+                        rhi = k[m] > rhi ? k[m] : rhi;
+                    }
+                rlo = wave_min(rlo);
+                rhi = wave_max(rhi);
+                if (lane == 0) {
+                    s_lo[w] = rlo;
+                    s_hi[w] = rhi;
+                }
+                __syncthreads();
+                rlo = s_lo[0];
+                rhi = s_hi[0];
+                for (int q = 1; q < NW; ++q) {
+                    rlo = s_lo[q] < rlo ? s_lo[q] : rlo;
+                    rhi = s_hi[q] > rhi ? s_hi[q] : rhi;
+                }
+                int64_t r = s_toff[t], cnt = s_tsz[t];
+                __syncthreads();
+                while (rlo != rhi && cnt > 64) {
+                    const int nb2 = cnt < NB ? int(cnt) : NB;
+                    const double sc2 = double(nb2) / (double(rhi - rlo) + 1.0);
+                    for (int j = tid; j <= nb2; j += BS) s_cnt[j] = 0u;
+                    __syncthreads();
+#pragma unroll
+                    for (int m = 0; m < IPT; ++m)
+                        if (tid + int64_t(m) * BS < n && k[m] >= rlo && k[m] <= rhi)
+                            atomicAdd(&s_cnt[bucket(k[m], rlo, sc2, nb2)], 1u);
+                    __syncthreads();
+                    if (w == 0) {  // the sub-bucket holding rank r: wave 0 walks 64 buckets per step
+                        int64_t base = 0;
+                        for (int c0 = 0; c0 < nb2; c0 += 64) {
+                            const int j = c0 + lane;
+                            const int64_t cj = j < nb2 ? int64_t(s_cnt[j]) : 0;
+                            const int64_t incl = base + wave_incl_scan(cj);
+                            const uint64_t hit = __ballot(j < nb2 && incl > r);
+                            if (hit) {
+                                const int l = __ffsll((unsigned long long)hit) - 1;
+                                if (lane == l) {
+                                    s_r = r - (incl - cj);
+                                    s_rc = cj;
+                                    s_cnt[NB] = uint32_t(j);
+                                }
+                                break;
+                            }
+                            base = __shfl(incl, 63, 64);
+                        }
+                    }
+                    __syncthreads();
+                    const uint32_t sb = s_cnt[NB];
+                    uint64_t nlo = ~0ull, nhi = 0ull;
+#pragma unroll
+                    for (int m = 0; m < IPT; ++m)
+                        if (tid + int64_t(m) * BS < n && k[m] >= rlo && k[m] <= rhi && bucket(k[m], rlo, sc2, nb2) == sb) {
+                            nlo = k[m] < nlo ? k[m] : nlo;
+                            nhi = k[m] > nhi ? k[m] : nhi;
+                        }
+                    nlo = wave_min(nlo);
+                    nhi = wave_max(nhi);
+                    if (lane == 0) {
+                        s_lo[w] = nlo;
+                        s_hi[w] = nhi;
+                    }
+                    __syncthreads();
+                    nlo = s_lo[0];
+                    nhi = s_hi[0];
+                    for (int q = 1; q < NW; ++q) {
+                        nlo = s_lo[q] < nlo ? s_lo[q] : nlo;
+                        nhi = s_hi[q] > nhi ? s_hi[q] : nhi;
+                    }
+                    r = s_r;
+                    cnt = s_rc;
+                    rlo = nlo;
+                    rhi = nhi;
+                    __syncthreads();
+                }
+                if (rlo == rhi) {
+                    if (tid == 0) s_res[t] = rlo;
+                } else {  // <= 64 values in [rlo, rhi]: list them, one wave ranks them
+                    if (tid == 0) s_fill[0] = 0u;
+                    __syncthreads();
+#pragma unroll
+                    for (int m = 0; m < IPT; ++m)
+                        if (tid + int64_t(m) * BS < n && k[m] >= rlo && k[m] <= rhi)
+                            s_list[0][atomicAdd(&s_fill[0], 1u)] = k[m];
+                    __syncthreads();
+                    if (w == 0) {
+                        const int sz = int(cnt);
+                        const uint64_t e = lane < sz ? s_list[0][lane] : ~0ull;
+                        int rr = 0;
+                        for (int j = 0; j < sz; ++j) {
+                            const uint64_t o = s_list[0][j];
+                            rr += (o < e) || (o == e && j < lane);
+                        }
+                        if (lane < sz && rr == int(r)) s_res[t] = e;
+                    }
+                }
+                __syncthreads();
+            }
+        } else if (tid < nt) {
+            s_res[tid] = lo;  // one distinct key
+        }
+        __syncthreads();
+        if (tid == 0) {
+            DD tot{s_dhi[0], s_dlo[0]};
+            for (int q = 1; q < NW; ++q) tot = dd_add(tot, DD{s_dhi[q], s_dlo[q]});
+            auto get = [&](int64_t j) {
+                uint64_t r = 0;
+                for (int t = 0; t < nt; ++t)
+                    if (qs_rank(n, a, t) == j) r = s_res[t];
+                return f64_from_key(r);
+            };
+            qs_write(a, s, n, tot.hi + tot.lo, get);
+            if (n >= 100) ++ge100;
+        }
+        __syncthreads();  // LDS is reused by the next segment
+    }
+    if (tid == 0 && ge100) atomic_add_i64(a.d_ge100, ge100);
+}
+
+bool seg_qstats_ok(const Segs &sg) { return sg.len_bound() <= kQsMax; }
+
+void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_host, int nq, double *mean,
+                double *median, double *pcts, int64_t *d_ge100) {
+    FZ_CHECK(nq >= 0 && nq <= 8, "seg_qstats: at most 8 percentiles");
+    FZ_CHECK(seg_qstats_ok(sg), "seg_qstats: segment longer than kQsMax");
+    QsArgs a{};
+    for (int j = 0; j < nq; ++j) a.q[j] = q_host[j];
+    a.nq = nq;
+    a.mean = mean;
+    a.median = median;
+    a.pcts = pcts;
+    a.d_ge100 = d_ge100;
+    const int64_t S = sg.S, lb = sg.len_bound();
+    if (S <= 0) return;
+    // algorithmic bytes: the values once (8 B each) + the offsets + the statistics written
+    ProbeScope ps(c, "seg_qstats", double(S) * (8.0 + 8.0 * (2 + nq)), sg.offs + S, 8.0);
+    const int64_t groups = (S + 63) / 64;
+    k_qs_small<<<grid_for(groups, kBlock / kWave, 8192), kBlock, 0, c->stream>>>(vals, sg.offs, S, a);
+    FZ_LAUNCH_CHECK();
+    // the workgroup classes walk their size classes' lists when there are very many segments
+    // (config 5: ~2e7 sessions, almost all of a handful of values)
+    SegLists L;
+    if (lb > kTinySeg && S > kManySegs) L = seg_lists(c, sg);
+    auto grid = [&](int64_t cap, int64_t lim) { return unsigned(cap < 1 ? 1 : (cap < lim ? cap : lim)); };
+    if (lb > kTinySeg) {
+        const int64_t cap = L.on ? L.cap[kClassMid] : S;
+        k_qs_block<256, 1024><<<grid(cap, 8192), 256, 0, c->stream>>>(
+            vals, sg.offs, S, kTinySeg, L.on ? L.ids[kClassMid] : nullptr, L.on ? L.d_n + kClassMid : nullptr,
+            nullptr, nullptr, a);
+        FZ_LAUNCH_CHECK();
+    }
+    if (lb > 1024) {
+        const int64_t cap = L.on ? L.cap[kClassWide] + L.cap[kClassBig] : S;
+        k_qs_block<1024, kQsMax><<<grid(cap, 1024), 1024, 0, c->stream>>>(
+            vals, sg.offs, S, 1024, L.on ? L.ids[kClassWide] : nullptr, L.on ? L.d_n + kClassWide : nullptr,
+            L.on ? L.ids[kClassBig] : nullptr, L.on ? L.d_n + kClassBig : nullptr, a);
+        FZ_LAUNCH_CHECK();
+    }
+}
+
 // levene([x, y], center='median') (scipy _morestats.py levene).
 void levene_two(fz_ctx *c, const uint64_t *skx, const double *x, int64_t nxm, const int64_t *d_nx,
                        const uint64_t *sky, const double *y, int64_t nym, const int64_t *d_ny, double *out) {

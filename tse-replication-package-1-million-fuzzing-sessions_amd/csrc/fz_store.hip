@@ -1042,6 +1042,9 @@ static void materialize_sorted(fz_ctx *c) {
 void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     FZ_CHECK(t != nullptr, "fz_store_build: tables is null");
     FZ_CHECK(c->parent == nullptr, "fz_store_build: a child context reads its parent's store");
+    for (fz_ctx *h : c->helpers)  // the build resets the helpers' arenas and runs sorts on them
+        FZ_STATE(h->in_call.load() == 0, "fz_store_build: a store-build helper is inside a libfz call of its own "
+                                         "(join the helper threads before building the store)");
     FZ_CHECK(t->n_projects >= 0 && t->n_builds >= 0 && t->n_cov >= 0 && t->n_issues >= 0, "negative table size");
     FZ_CHECK(t->n_builds < (int64_t(1) << 31) && t->n_cov < (int64_t(1) << 31) && t->n_issues < (int64_t(1) << 31),
              "tables are limited to 2^31 rows per shard");
