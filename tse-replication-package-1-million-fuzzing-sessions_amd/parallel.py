@@ -340,9 +340,11 @@ def rq3_sharded(shard, rank: int, world: int):
     total[RQ3_NON_DETECTED] = out["non_pct"].numel()
     total[RQ3_NON_LAST] = 0
     # NULL total_line pairs (rq3:253,297 raise TypeError): those of the never-flushed last project
-    # do not count; the caller raises on the rest (compute.rq3_result)
+    # do not count; the rest raise below (as compute.rq3_result does on one table)
     total[RQ3_NULL_TOTAL] -= int(cl[last][RQ3_NULL_LAST]) if last >= 0 else 0
     total[RQ3_NULL_LAST] = 0
+    if total[RQ3_NULL_TOTAL] > 0:  # None > 0 (rq3:253,297): every rank holds the counters, all raise here
+        raise TypeError("'>' not supported between instances of 'NoneType' and 'int'")
     st = shard.stats(out["det_pct"], out["det_tot"], out["non_pct"])
     return total, out, st
 
@@ -424,6 +426,8 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     h = host_many(mat, offs, *pc)  # one device->host copy
     mat_h, offs_h = h[0], h[1]
     sizes_h, null_lines = mat_h[:, :M].sum(0), int(mat_h[:, M].sum())
+    if null_lines:  # float(None) (rq2_coverage_count.py:300-303): every rank holds the sum, all raise here
+        raise TypeError("float() argument must be a string or a real number, not 'NoneType'")
     proj = dict(zip(RQ2C_PROJECT_COLS, h[2:]))
     own = session_owners(sizes_h, world)
     a, b = own[rank]
