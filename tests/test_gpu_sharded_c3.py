@@ -1,5 +1,6 @@
-"""The project-sharded path on the FULL config-3 table (100M coverage rows over
-10k projects, "project-sharded over 2/4/8 MI355X"): two ranks on cuda:0, each holding only its
+"""The project-sharded path on the FULL config-3 and config-5 tables (100M coverage
+rows over 10k projects, "project-sharded over 2/4/8 MI355X"; config 5 Zipf-skewed, its ~20M-row giant
+whole on one shard): two or four ranks on cuda:0, each holding only its
 ``parallel.shard_bounds`` half of the projects, run RQ2-count and RQ4b through libfz
 (fz_rq2_count_ex / fz_rq4b_ex with the session statistics skipped, then the all-to-all by session
 index to the session owners, fz_rq2_session_stats / fz_rq4b_session_stats there, and the gathers)
@@ -56,6 +57,13 @@ def _check(rank, world, name):
     assert t.n_rows >= 99_000_000
     bounds = par.shard_bounds(t, world)
     lo, hi = bounds[rank]
+    if rank == 0:  # the shards' row shares (config 5: the Zipf giant stays whole on one shard)
+        rows = (np.bincount(t.b_project.astype(np.int64), minlength=len(t.projects))
+                + np.bincount(t.c_project.astype(np.int64), minlength=len(t.projects))
+                + np.bincount(t.i_project.astype(np.int64), minlength=len(t.projects)))
+        share = [int(rows[a:b].sum()) / (t.n_rows / world) for a, b in bounds]
+        print(f"{name} world {world}: largest project {int(rows.max()):,} rows; shard shares of the mean "
+              + " ".join(f"{x:.2f}" for x in share), flush=True)
     ts, _ = par.take_shard(t, lo, hi)
     eng = E.Engine(0)
     eng.upload(ts)
@@ -93,11 +101,11 @@ def _check(rank, world, name):
     assert_same(ours4b, ref4b, "rq4b")
 
 
-@pytest.mark.parametrize("name", ["c3"])
-def test_sharded_fullsize_matches_single_gpu(name, tmp_path):
+@pytest.mark.parametrize("name,world", [("c3", 2), ("c3", 4), ("c5", 2), ("c5", 4)])
+def test_sharded_fullsize_matches_single_gpu(name, world, tmp_path):
     errfile = str(tmp_path / "err")
     try:
-        mp.spawn(_worker, args=(2, _free_port(), name, errfile), nprocs=2, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), name, errfile), nprocs=world, join=True)
     except Exception:
-        msgs = [open(f"{errfile}.{r}").read() for r in range(2) if os.path.exists(f"{errfile}.{r}")]
+        msgs = [open(f"{errfile}.{r}").read() for r in range(world) if os.path.exists(f"{errfile}.{r}")]
         raise AssertionError("\n".join(msgs) or "worker failed")

@@ -20,7 +20,7 @@ import numpy as np
 import pandas as pd
 
 from ..schema import CODE_NULL, Tables, us_to_dt
-from . import common
+from . import common, writer
 from .results import (Describe, RQ1Result, RQ2AddResult, RQ2CountResult, RQ3Result, RQ4aResult,
                       RQ4bResult)
 
@@ -159,10 +159,13 @@ def rq2_count(r: RQ2CountResult, t: Tables) -> Rendered:
     csv_path = os.path.join(out_dir, "coverage_by_session_index.csv")
     o.p(f"Saving coverage data per session index to: {csv_path}")
     offs = r.session_offsets
-    vals = r.session_values.tolist()
-    rows = [vals[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
-    o.files[csv_path] = csv_bytes(rows)
-    o.p(f"Successfully saved. Total rows (max sessions): {len(rows)}")
+    nrows = len(offs) - 1
+    if writer.lib() is not None:  # the same bytes from the native writer (rq/writer.py)
+        o.files[csv_path] = writer.float_rows(r.session_values, offs)
+    else:
+        vals = r.session_values.tolist()
+        o.files[csv_path] = csv_bytes([vals[offs[i]:offs[i + 1]] for i in range(nrows)])
+    o.p(f"Successfully saved. Total rows (max sessions): {nrows}")
     o.p("\n--- Analysis of All Project Correlations ---")
     valid = corr[~np.isnan(corr)]
     o.p(f"Total projects processed: {len(corr)}")
@@ -228,6 +231,27 @@ def rq2_add(r: RQ2AddResult, t: Tables) -> Rendered:
             return np.nan
         return float(v) if isf else int(v)
 
+    if writer.lib() is not None:  # every row formatted once, natively (rq/writer.py)
+        body, row_end = writer.change_rows(r, t)
+        hb = csv_bytes([], header)
+        rp = np.asarray(r.row_project, dtype=np.int64)
+        if len(rp):
+            starts = np.concatenate([[0], row_end[:-1]])
+            first = np.concatenate([[True], rp[1:] != rp[:-1]])  # runs of one project
+            run_at = np.nonzero(first)[0]
+            run_end = np.concatenate([run_at[1:], [len(rp)]])
+            pieces = {}
+            for a, b in zip(run_at.tolist(), run_end.tolist()):
+                pieces.setdefault(int(rp[a]), []).append(body[int(starts[a]):int(row_end[b - 1])])
+            for p, parts in pieces.items():
+                o.files[os.path.join(out_dir, "change_analysis", f"{t.projects[p]}.csv")] = hb + b"".join(parts)
+        o.p("\n--- Project processing finished ---\n")
+        if len(rp):
+            path = os.path.join(out_dir, "all_coverage_change_analysis.csv")
+            o.files[path] = hb + body
+            o.p(f"All project change analysis saved to: {path}")
+        o.p("\n--- Main process finished for RQ3 ---")
+        return o
     all_rows = []
     per_project = {}
     for k in range(len(r.row_project)):
