@@ -27,7 +27,7 @@ for s in $STEPS; do
       timeout -k 10 600 python -u bench.py --config $arg --steps $st --warmup 2 --no-cpu-baseline > $O/${T}_bench_$arg.json 2> $O/${T}_bench_$arg.err || exit $?
       python3 -c "import json; d=json.loads([l for l in open('$O/${T}_bench_$arg.json') if l.startswith('{')][-1]); print('$arg', d['ms_per_step'], flush=True)" ;;
     tests)
-      k=""; [ "$arg" != tests ] && k="$arg"
+      k=""; [ "$arg" != tests ] && k="${arg//+/ or }"
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 500 --timeout-method thread ${k:+-k "$k"} > $O/${T}_pytest.log 2>&1; rc=$?
       echo "pytest rc=$rc"; tail -3 $O/${T}_pytest.log; [ $rc -ne 0 ] && exit $rc ;;
   esac

@@ -26,8 +26,9 @@ SCOPES = {
     "elig_hist": {"match": ["k_elig_hist"]},
     # (the selective filters - tiles of unselected projects skipped - are probed apart)
     "filter_compact": {"match": ["k_filter_compact"], "exclude": ["CovRowsRq3", "PositiveCoverage34", "CovRowsBeforeLimit"]},
-    "filter_select": {"match": ["k_filter_compact<fz::CovRowsRq3>", "k_filter_compact<fz::PositiveCoverage34>",
-                                "k_filter_compact<fz::CovRowsBeforeLimit>"]},
+    # (template names go on after the predicate: "k_filter_compact<fz::CovRowsRq3, ...>")
+    "filter_select": {"match": ["k_filter_compact<fz::CovRowsRq3", "k_filter_compact<fz::PositiveCoverage34",
+                                "k_filter_compact<fz::CovRowsBeforeLimit"]},
     # the four length-class launches of the store's time sort (all three tables), between the prefix
     # offsets and the views launch
     "seg_time_sort": {"open": "k_prefix_offsets", "match": ["k_seg_time_bucket"], "allow": ["k_fill"],
@@ -43,6 +44,10 @@ SCOPES = {
     "seg_spearman": {"open": "k_spearman_chunks", "match": ["k_spearman_chunks", "k_seg_fold", "k_seg_sum"]},
     "seg_rank_union": {"open": "k_bm_union_chunks<0>", "match": ["k_bm_union_chunks", "k_seg_fold", "k_seg_sum"]},
     "scan_i64": {"match": ["k_scan_lookback"]},
+    # RQ2's per-session order statistics by selection: the small-segment launch opens the scope
+    # (the size-class lists and the workgroup classes follow)
+    "seg_qstats": {"open": "k_qs_small", "match": ["k_qs_small", "k_qs_block", "k_seg_classes"], "allow": ["k_fill"]},
+    "ragged_transpose": {"match": ["k_rt_move"]},
     # seg_sort_f64's bucket path: value bucket classes, then the merge sort of flagged segments
     "seg_value_sort": {"open": "k_seg_val_bucket<256, 1024>",
                        "match": ["k_seg_val_bucket", "k_tile_sort", "k_merge_round", "k_merge_splits",

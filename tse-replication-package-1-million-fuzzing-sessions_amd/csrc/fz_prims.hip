@@ -1066,9 +1066,10 @@ __global__ void k_describe_finish(SortedDescArgs a, const double *__restrict__ m
     describe_from_sorted(a.k[j], *a.d_n[j], ms[2 * j], ms[2 * j + 1], a.out[j]);
 }
 
-// The whole describe of n <= 4096 values in one 1024-thread workgroup: LDS bitonic sort of the
-// keys, double-double sums of x and (x - mean)^2 (as k_dd_partial / k_dd_final), finish.
-constexpr int kDescSmall = 4096;
+// double-double sum over a 1024-thread workgroup
+// samples of a capacity up to this are described by selection (k_describe_sel: one workgroup,
+// passes over the sample); larger ones sort their keys (radix) first
+constexpr int64_t kDescSelMax = 65536;
 __device__ inline DD block_dd_sum_1024(DD acc, double *s_hi, double *s_lo) {
     acc = wave_dd_sum(acc);
     if (lane_id() == 0) {
@@ -1087,46 +1088,301 @@ struct DescSmallArgs {
     const int64_t *d_n[kDescBatch];
     fz_describe *out[kDescBatch];
 };
-// one workgroup per job (blockIdx.x)
-__global__ __launch_bounds__(kSortBlock) void k_describe_small(DescSmallArgs a) {
-    __shared__ uint64_t sk[kDescSmall];
-    __shared__ double s_hi[kSortBlock / kWave], s_lo[kSortBlock / kWave];
+// ---- describe by selection (one workgroup per sample, no sorted copy) ------------------------
+// The order statistics a describe needs (median, the quartiles' interpolation neighbours, the
+// smallest non-zero value) are selected by value-bucket histograms over the sample's key range:
+// the sample is re-read from global memory (L2-resident for the samples this serves) in each pass -
+// statistics (min / max / sum / sign counts), squared deviations, one histogram, one gather of the
+// wanted buckets - and a wanted bucket of more than 64 values is narrowed by re-histogramming its
+// key interval.  One launch for any live length (rounds 1-3: an LDS bitonic network up to 4096
+// values, a 64-bit radix sort + five launches beyond).
+constexpr int kSelNB = 4096;
+constexpr int kSelMaxT = 8;
+constexpr int kSelBlock = 1024;
+struct SelShared {
+    uint32_t cnt[kSelNB + 1];
+    uint8_t map[kSelNB];
+    uint64_t list[kSelMaxT][64];
+    uint32_t fill[kSelMaxT];
+    uint64_t lo[kSelBlock / kWave], hi[kSelBlock / kWave];
+    uint32_t tmp[kSelBlock / kWave];
+    int64_t rank[kSelMaxT], tb[kSelMaxT], toff[kSelMaxT], tsz[kSelMaxT];
+    int tslot[kSelMaxT];
+    uint64_t res[kSelMaxT];
+    int64_t r, rc;
+    uint32_t sb;
+};
+
+__device__ inline void sel_minmax(uint64_t &lo, uint64_t &hi, SelShared &sh) {
+    constexpr int NW = kSelBlock / kWave;
+    lo = wave_min(lo);
+    hi = wave_max(hi);
+    if (lane_id() == 0) {
+        sh.lo[wave_id()] = lo;
+        sh.hi[wave_id()] = hi;
+    }
+    __syncthreads();
+    lo = sh.lo[0];
+    hi = sh.hi[0];
+    for (int q = 1; q < NW; ++q) {
+        lo = sh.lo[q] < lo ? sh.lo[q] : lo;
+        hi = sh.hi[q] > hi ? sh.hi[q] : hi;
+    }
+    __syncthreads();
+}
+
+__device__ inline uint32_t sel_bucket(uint64_t k, uint64_t lo, double sc, int nb) {
+    const uint32_t q = uint32_t(double(k - lo) * sc);
+    return q < uint32_t(nb) ? q : uint32_t(nb - 1);
+}
+
+// sh.res[t] = the key of rank sh.rank[t] (t < nt) among the n keys key(i), whose min / max are lo / hi
+template <typename KeyF>
+__device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64_t hi, int nt, SelShared &sh) {
+    constexpr int BS = kSelBlock, NW = BS / kWave;
+    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
+    if (lo == hi) {
+        if (tid < nt) sh.res[tid] = lo;
+        __syncthreads();
+        return;
+    }
+    const int nb = n < kSelNB ? int(n) : kSelNB;
+    const double sc = double(nb) / (double(hi - lo) + 1.0);
+    for (int j = tid; j <= nb; j += BS) sh.cnt[j] = 0u;
+    for (int j = tid; j < nb; j += BS) sh.map[j] = 0xff;
+    __syncthreads();
+    for (int64_t i = tid; i < n; i += BS) atomicAdd(&sh.cnt[sel_bucket(key(i), lo, sc, nb)], 1u);
+    __syncthreads();
+    {  // exclusive scan of the bucket counts: thread t takes buckets [t * 4, t * 4 + 4)
+        constexpr int BPT = kSelNB / BS;
+        uint32_t sum = 0;
+        for (int e = 0; e < BPT; ++e) sum += tid * BPT + e < nb ? sh.cnt[tid * BPT + e] : 0u;
+        uint32_t run = block_excl_scan<uint32_t, NW>(sum, sh.tmp, (uint32_t *)nullptr);
+        for (int e = 0; e < BPT; ++e) {
+            if (tid * BPT + e < nb) {
+                const uint32_t ce = sh.cnt[tid * BPT + e];
+                sh.cnt[tid * BPT + e] = run;
+                run += ce;
+            }
+        }
+        if (tid == 0) sh.cnt[nb] = uint32_t(n);
+    }
+    __syncthreads();
+    if (tid < nt) {
+        const uint32_t r = uint32_t(sh.rank[tid]);
+        int l0 = 0, h0 = nb - 1;
+        while (l0 < h0) {
+            const int mid = (l0 + h0 + 1) >> 1;
+            if (sh.cnt[mid] <= r) l0 = mid;
+            else h0 = mid - 1;
+        }
+        sh.tb[tid] = l0;
+        sh.toff[tid] = int64_t(r) - int64_t(sh.cnt[l0]);
+        sh.tsz[tid] = int64_t(sh.cnt[l0 + 1]) - int64_t(sh.cnt[l0]);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int used = 0;
+        for (int t = 0; t < nt; ++t) {
+            int slot = -1;
+            if (sh.tsz[t] <= 64) {
+                for (int u = 0; u < t; ++u)
+                    if (sh.tslot[u] >= 0 && sh.tb[u] == sh.tb[t]) slot = sh.tslot[u];
+                if (slot < 0) {
+                    slot = used++;
+                    sh.fill[slot] = 0u;
+                    sh.map[sh.tb[t]] = uint8_t(slot);
+                }
+            }
+            sh.tslot[t] = slot;
+        }
+    }
+    __syncthreads();
+    for (int64_t i = tid; i < n; i += BS) {
+        const uint64_t k = key(i);
+        const uint8_t slot = sh.map[sel_bucket(k, lo, sc, nb)];
+        if (slot != 0xff) sh.list[slot][atomicAdd(&sh.fill[slot], 1u)] = k;
+    }
+    __syncthreads();
+    auto rank_list = [&](int slot, int sz, int64_t want, int t) {  // one wave
+        const uint64_t e = lane < sz ? sh.list[slot][lane] : ~0ull;
+        int rr = 0;
+        for (int j = 0; j < sz; ++j) {
+            const uint64_t o = sh.list[slot][j];
+            rr += (o < e) || (o == e && j < lane);
+        }
+        if (lane < sz && rr == int(want)) sh.res[t] = e;
+    };
+    for (int t = w; t < nt; t += NW)
+        if (sh.tslot[t] >= 0) rank_list(sh.tslot[t], int(sh.tsz[t]), sh.toff[t], t);
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {  // wide buckets: narrow the key interval (uniform control flow)
+        if (sh.tslot[t] >= 0) continue;
+        const uint32_t tb = uint32_t(sh.tb[t]);
+        uint64_t rlo = ~0ull, rhi = 0ull;
+        for (int64_t i = tid; i < n; i += BS) {
+            const uint64_t k = key(i);
+            if (sel_bucket(k, lo, sc, nb) == tb) {
+                rlo = k < rlo ? k : rlo;
+                rhi = k > rhi ? k : rhi;
+            }
+        }
+        sel_minmax(rlo, rhi, sh);
+        int64_t r = sh.toff[t], cnt = sh.tsz[t];
+        while (rlo != rhi && cnt > 64) {
+            const int nb2 = cnt < kSelNB ? int(cnt) : kSelNB;
+            const double sc2 = double(nb2) / (double(rhi - rlo) + 1.0);
+            for (int j = tid; j <= nb2; j += BS) sh.cnt[j] = 0u;
+            __syncthreads();
+            for (int64_t i = tid; i < n; i += BS) {
+                const uint64_t k = key(i);
+                if (k >= rlo && k <= rhi) atomicAdd(&sh.cnt[sel_bucket(k, rlo, sc2, nb2)], 1u);
+            }
+            __syncthreads();
+            if (w == 0) {  // the sub-bucket holding rank r
+                int64_t base = 0;
+                for (int c0 = 0; c0 < nb2; c0 += 64) {
+                    const int j = c0 + lane;
+                    const int64_t cj = j < nb2 ? int64_t(sh.cnt[j]) : 0;
+                    const int64_t incl = base + wave_incl_scan(cj);
+                    const uint64_t hit = __ballot(j < nb2 && incl > r);
+                    if (hit) {
+                        const int l = __ffsll((unsigned long long)hit) - 1;
+                        if (lane == l) {
+                            sh.r = r - (incl - cj);
+                            sh.rc = cj;
+                            sh.sb = uint32_t(j);
+                        }
+                        break;
+                    }
+                    base = __shfl(incl, 63, 64);
+                }
+            }
+            __syncthreads();
+            const uint32_t sb = sh.sb;
+            uint64_t nlo = ~0ull, nhi = 0ull;
+            for (int64_t i = tid; i < n; i += BS) {
+                const uint64_t k = key(i);
+                if (k >= rlo && k <= rhi && sel_bucket(k, rlo, sc2, nb2) == sb) {
+                    nlo = k < nlo ? k : nlo;
+                    nhi = k > nhi ? k : nhi;
+                }
+            }
+            r = sh.r;
+            cnt = sh.rc;
+            sel_minmax(nlo, nhi, sh);
+            rlo = nlo;
+            rhi = nhi;
+        }
+        if (rlo == rhi) {
+            if (tid == 0) sh.res[t] = rlo;
+        } else {  // <= 64 values in [rlo, rhi]
+            if (tid == 0) sh.fill[0] = 0u;
+            __syncthreads();
+            for (int64_t i = tid; i < n; i += BS) {
+                const uint64_t k = key(i);
+                if (k >= rlo && k <= rhi) sh.list[0][atomicAdd(&sh.fill[0], 1u)] = k;
+            }
+            __syncthreads();
+            if (w == 0) rank_list(0, int(cnt), r, t);
+        }
+        __syncthreads();
+    }
+}
+
+// fz_describe of each job's sample (blockIdx.x = job), any live length
+__global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
+    constexpr int NW = kSelBlock / kWave;
+    __shared__ SelShared sh;
+    __shared__ double s_hi[NW], s_lo[NW];
+    __shared__ unsigned long long s_c[3];
     const int tid = threadIdx.x;
     const double *__restrict__ x = a.x[blockIdx.x];
     fz_describe *__restrict__ out = a.out[blockIdx.x];
-    const int n = int(*a.d_n[blockIdx.x]);
-    int np2 = 1;
-    while (np2 < n) np2 <<= 1;
-    DD acc{0.0, 0.0};
-    for (int i = tid; i < np2; i += kSortBlock) {
-        const double v = i < n ? x[i] : 0.0;
-        sk[i] = i < n ? f64_key(v) : ~0ull;
-        if (i < n) acc = dd_add_d(acc, v);
+    const int64_t n = *a.d_n[blockIdx.x];
+    if (n <= 0) {
+        if (tid == 0) describe_from_sorted(nullptr, 0, 0.0, 0.0, out);
+        return;
     }
-    DD t = block_dd_sum_1024(acc, s_hi, s_lo);
-    const double mean = n > 0 ? (t.hi + t.lo) / double(n) : NAN;
+    const uint64_t kneg0 = f64_key(-0.0), kpos0 = f64_key(0.0), kinf = f64_key(INFINITY);
+    if (tid < 3) s_c[tid] = 0ull;
+    uint64_t lo = ~0ull, hi = 0ull;
+    DD acc{0.0, 0.0};
+    unsigned long long lt0 = 0, le0 = 0, leinf = 0;
+    for (int64_t i = tid; i < n; i += kSelBlock) {
+        const double v = x[i];
+        const uint64_t k = f64_key(v);
+        acc = dd_add_d(acc, v);
+        lo = k < lo ? k : lo;
+        hi = k > hi ? k : hi;
+        lt0 += k < kneg0;
+        le0 += k <= kpos0;
+        leinf += k <= kinf;
+    }
+    sel_minmax(lo, hi, sh);
+    lt0 = wave_sum(lt0);
+    le0 = wave_sum(le0);
+    leinf = wave_sum(leinf);
+    if (lane_id() == 0) {
+        atomicAdd(&s_c[0], lt0);
+        atomicAdd(&s_c[1], le0);
+        atomicAdd(&s_c[2], leinf);
+    }
+    DD t = block_dd_sum_1024(acc, s_hi, s_lo);  // (its barriers order the counters too)
+    const double mean = (t.hi + t.lo) / double(n);
     acc = DD{0.0, 0.0};
-    for (int i = tid; i < n; i += kSortBlock) {
+    for (int64_t i = tid; i < n; i += kSelBlock) {
         double v = x[i] - mean;
         v = v * v;
         acc = dd_add_d(acc, v);
     }
     t = block_dd_sum_1024(acc, s_hi, s_lo);
-    const double std = n > 0 ? sqrt((t.hi + t.lo) / double(n)) : NAN;
-    for (int k = 2; k <= np2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int q = tid; q < (np2 >> 1); q += kSortBlock) {
-                const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1)), ixj = i + j;
-                const uint64_t a = sk[i], b = sk[ixj];
-                if ((a > b) == ((i & k) == 0)) {
-                    sk[i] = b;
-                    sk[ixj] = a;
-                }
-            }
-            bitonic_stage_sync(k, j, np2);
-        }
+    const double std = sqrt((t.hi + t.lo) / double(n));
+    const int64_t c_lt0 = int64_t(s_c[0]), c_le0 = int64_t(s_c[1]), c_leinf = int64_t(s_c[2]);
+    // ranks: median (n / 2, and n / 2 - 1), np.percentile 25 / 75 neighbours, the smallest non-zero
+    if (tid == 0) {
+        auto nb = [&](double q, int up) {
+            const double vi = double(n - 1) * (q / 100.0);
+            int64_t r = int64_t(floor(vi)) + up;
+            return r > n - 1 ? n - 1 : (r < 0 ? 0 : r);
+        };
+        sh.rank[0] = n / 2;
+        sh.rank[1] = (n & 1) ? n / 2 : n / 2 - 1;
+        sh.rank[2] = nb(25.0, 0);
+        sh.rank[3] = nb(25.0, 1);
+        sh.rank[4] = nb(75.0, 0);
+        sh.rank[5] = nb(75.0, 1);
+        sh.rank[6] = c_lt0 > 0 ? 0 : (c_le0 < n ? c_le0 : 0);
     }
-    if (tid == 0) describe_from_sorted(sk, n, mean, std, out);
+    __syncthreads();
+    wg_select_global([=](int64_t i) { return f64_key(x[i]); }, n, lo, hi, 7, sh);
+    if (tid != 0) return;
+    auto get = [&](int64_t j) {
+        uint64_t r = 0;
+        for (int q = 0; q < 7; ++q)
+            if (sh.rank[q] == j) r = sh.res[q];
+        return f64_from_key(r);
+    };
+    fz_describe d;
+    d.count = n;
+    d.mean = mean;
+    d.std = std;
+    d.n_neg = c_lt0;
+    d.n_zero = c_le0 - c_lt0;
+    d.n_pos = c_leinf - c_le0;
+    d.min = f64_from_key(lo);
+    d.max = f64_from_key(hi);
+    d.median = (n & 1) ? get(n / 2) : (get(n / 2 - 1) + get(n / 2)) / 2.0;
+    d.q1 = np_percentile_sorted(get, n, 25.0);
+    d.q3 = np_percentile_sorted(get, n, 75.0);
+    if (c_lt0 > 0 || c_le0 < n) {
+        d.min_nonzero = f64_from_key(sh.res[6]);
+        d.has_nonzero = 1;
+    } else {
+        d.min_nonzero = NAN;
+        d.has_nonzero = 0;
+    }
+    *out = d;
 }
 
 uint64_t *sorted_keys_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n) {
@@ -1152,7 +1408,7 @@ void describe_f64_dn_batch(fz_ctx *c, const DescJob *jobs, int njobs) {
     int ns = 0, nb = 0;
     for (int i = 0; i < njobs; ++i) {
         const DescJob &j = jobs[i];
-        if (j.nmax <= kDescSmall) {
+        if (j.nmax <= kDescSelMax) {  // by selection in one workgroup (any live length; re-reads)
             a.x[ns] = j.x;
             a.d_n[ns] = j.d_n;
             a.out[ns] = j.out;
@@ -1161,8 +1417,8 @@ void describe_f64_dn_batch(fz_ctx *c, const DescJob *jobs, int njobs) {
             big[nb++] = SortedDescJob{sorted_keys_dn(c, j.x, j.nmax, j.d_n), j.x, j.nmax, j.d_n, j.out};
         }
     }
-    if (ns > 0) {  // every small job in one launch
-        k_describe_small<<<ns, kSortBlock, 0, c->stream>>>(a);
+    if (ns > 0) {  // every such job in one launch
+        k_describe_sel<<<ns, kSelBlock, 0, c->stream>>>(a);
         FZ_LAUNCH_CHECK();
     }
     if (nb > 0) describe_sorted_dn_batch(c, big, nb);

@@ -328,10 +328,10 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
             }
         });
     }
-    const SortedDescJob jobs[3] = {{skd, det_pct, NI, d_nd, describe},
-                                   {skn, non_pct, NC, d_nn, describe + 1},
-                                   {sorted_keys_dn(c, dtot_f, NI, d_nd), dtot_f, NI, d_nd, describe + 2}};
-    describe_sorted_dn_batch(c, jobs, 3);
+    const SortedDescJob jobs[2] = {{skd, det_pct, NI, d_nd, describe}, {skn, non_pct, NC, d_nn, describe + 1}};
+    describe_sorted_dn_batch(c, jobs, 2);
+    const DescJob tot{dtot_f, NI, d_nd, describe + 2};  // (by selection: no sort of its own)
+    describe_f64_dn_batch(c, &tot, 1);
     sample_tests(c, v, cat, cap, oseg, tests);
 }
 

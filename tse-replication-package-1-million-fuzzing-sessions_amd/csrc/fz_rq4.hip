@@ -295,9 +295,11 @@ void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t 
     map_n(c, 1, nullptr, [=] __device__(int64_t) {
         ts[FZ_RQ4B_CLIFF] = (2.0 * u1[0]) / (double(*n2) * double(*n1)) - 1.0;
     });
-    uint64_t *ska = sorted_keys_dn(c, a, na_cap, n2);
-    uint64_t *skb = sorted_keys_dn(c, b, nb_cap, n1);
-    levene_two(c, ska, a, na_cap, n2, skb, b, nb_cap, n1, ts + FZ_RQ4B_LEVENE_W);
+    // levene's medians by selection (one launch for both samples, no sorted copies)
+    fz_describe *dd = c->arena.get<fz_describe>(2);
+    const DescJob jobs[2] = {{a, na_cap, n2, dd}, {b, nb_cap, n1, dd + 1}};
+    describe_f64_dn_batch(c, jobs, 2);
+    levene_two_med(c, &dd[0].median, a, na_cap, n2, &dd[1].median, b, nb_cap, n1, ts + FZ_RQ4B_LEVENE_W);
 }
 
 // Per-session quartiles / counts / Brunner-Munzel of G2 vs G1 (:910-1015) from values v2 ordered

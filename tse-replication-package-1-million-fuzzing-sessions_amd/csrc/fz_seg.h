@@ -408,10 +408,10 @@ void bm_union_sorted(fz_ctx *c, const Segs &one, const double *sorted, const int
 void spearman_index_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const SortedSegs &ss, double *rho,
                            double *pval);
 
-// scipy.stats.levene([x, y]) (center='median') from the samples and their ascending keys
-// -> out[0] = W, out[1] = p (F(1, N-2) survival, cephes fdtrc rounding).
-void levene_two(fz_ctx *c, const uint64_t *skx, const double *x, int64_t nxm, const int64_t *d_nx,
-                const uint64_t *sky, const double *y, int64_t nym, const int64_t *d_ny, double *out);
+// scipy.stats.levene([x, y]) (center='median') from the samples and their medians (device
+// scalars) -> out[0] = W, out[1] = p (F(1, N-2) survival, cephes fdtrc rounding).
+void levene_two_med(fz_ctx *c, const double *medx, const double *x, int64_t nxm, const int64_t *d_nx,
+                    const double *medy, const double *y, int64_t nym, const int64_t *d_ny, double *out);
 
 // A device offsets array [0, *d_n] for one segment whose length is known only on the device.
 const int64_t *single_segment(fz_ctx *c, const int64_t *d_n);

@@ -1711,90 +1711,117 @@ __device__ inline void qs_write(const QsArgs &a, int64_t s, int64_t n, double su
     for (int j = 0; j < a.nq; ++j) a.pcts[s * a.nq + j] = np_percentile_sorted(get, n, a.q[j]);
 }
 
-// Segments of <= kTinySeg values.  Wave v takes 64 consecutive segments (lane l: segment 64v + l):
-// a segment of <= kMicroSeg values is finished by its lane (register sorting network), the others
-// one after another by the whole wave (64-lane bitonic network).  Longer segments are skipped.
-__global__ __launch_bounds__(kBlock) void k_qs_small(const double *__restrict__ src, const int64_t *__restrict__ offs,
-                                                     int64_t S, QsArgs a) {
+// Size classes of the selection: lists of the segments too long for one lane (filled by
+// k_qs_micro), one list per class - tiny (one wave each), mid and big (one workgroup each).
+struct QsLists {
+    int32_t *ids[3];
+    int64_t *d_n;  // [3] (zero on entry)
+};
+
+// append segment s to list cls of L when `want` (wave-aggregated: one atomic per wave and class)
+__device__ inline void qs_append(const QsLists &L, int cls, bool want, int64_t s) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const int lane = lane_id();
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(reinterpret_cast<unsigned long long *>(L.d_n + cls),
+                                         (unsigned long long)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (want) L.ids[cls][base + __popcll(m & lanemask_lt())] = int32_t(s);
+}
+
+// One lane per segment (wave v: segments 64v .. 64v + 63, coalesced offset reads): a segment of
+// <= kMicroSeg values is finished by its lane (register sorting network); longer ones go to their
+// class list - tiny (<= kTinySeg), mid (<= 1024), big.
+__global__ __launch_bounds__(kBlock) void k_qs_micro(const double *__restrict__ src, const int64_t *__restrict__ offs,
+                                                     int64_t S, QsArgs a, QsLists L) {
     const int lane = lane_id();
     const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
     for (int64_t v = int64_t(blockIdx.x) * (kBlock / kWave) + wave_id(); v * 64 < S; v += nwaves) {
         const int64_t s = v * 64 + lane;
         const int64_t b = s < S ? offs[s] : 0;
         const int64_t n = s < S ? offs[s + 1] - b : -1;
-        if (n >= 0 && n <= kMicroSeg) {
-            uint64_t k[kMicroSeg];
-            DD acc{0.0, 0.0};
+        qs_append(L, 0, n > kMicroSeg && n <= kTinySeg, s);
+        qs_append(L, 1, n > kTinySeg && n <= 1024, s);
+        qs_append(L, 2, n > 1024, s);
+        if (n < 0 || n > kMicroSeg) continue;
+        uint64_t k[kMicroSeg];
+        DD acc{0.0, 0.0};
 #pragma unroll
-            for (int q = 0; q < kMicroSeg; ++q) {
-                const double x = q < n ? src[b + q] : 0.0;
-                if (q < n) acc = dd_add_d(acc, x);
-                k[q] = q < n ? f64_key(x) : ~0ull;
-            }
-            constexpr int net[19][2] = {{0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 2}, {1, 3}, {4, 6}, {5, 7}, {1, 2}, {5, 6},
-                                        {0, 4}, {1, 5}, {2, 6}, {3, 7}, {2, 4}, {3, 5}, {1, 2}, {3, 4}, {5, 6}};
-#pragma unroll
-            for (int c = 0; c < 19; ++c) {
-                const uint64_t x = k[net[c][0]], y = k[net[c][1]];
-                k[net[c][0]] = x < y ? x : y;
-                k[net[c][1]] = x < y ? y : x;
-            }
-            auto get = [&](int64_t j) {
-                uint64_t r = k[0];
-#pragma unroll
-                for (int q = 1; q < kMicroSeg; ++q) r = j == q ? k[q] : r;
-                return f64_from_key(r);
-            };
-            qs_write(a, s, n, acc.hi + acc.lo, get);
+        for (int q = 0; q < kMicroSeg; ++q) {
+            const double x = q < n ? src[b + q] : 0.0;
+            if (q < n) acc = dd_add_d(acc, x);
+            k[q] = q < n ? f64_key(x) : ~0ull;
         }
-        uint64_t tiny = __ballot(n > kMicroSeg && n <= kTinySeg);
-        while (tiny) {
-            const int l = __ffsll((unsigned long long)tiny) - 1;
-            tiny &= tiny - 1;
-            const int64_t st = v * 64 + l;
-            const int64_t sb = __shfl(b, l, 64);
-            const int sn = int(__shfl(n, l, 64));
-            const double x = lane < sn ? src[sb + lane] : 0.0;
-            DD acc = wave_dd_sum(DD{lane < sn ? x : 0.0, 0.0});
-            unsigned long long key = lane < sn ? f64_key(x) : ~0ull;
+        constexpr int net[19][2] = {{0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 2}, {1, 3}, {4, 6}, {5, 7}, {1, 2}, {5, 6},
+                                    {0, 4}, {1, 5}, {2, 6}, {3, 7}, {2, 4}, {3, 5}, {1, 2}, {3, 4}, {5, 6}};
 #pragma unroll
-            for (int kk = 2; kk <= 64; kk <<= 1) {
+        for (int c = 0; c < 19; ++c) {
+            const uint64_t x = k[net[c][0]], y = k[net[c][1]];
+            k[net[c][0]] = x < y ? x : y;
+            k[net[c][1]] = x < y ? y : x;
+        }
+        auto get = [&](int64_t j) {
+            uint64_t r = k[0];
 #pragma unroll
-                for (int j = kk >> 1; j > 0; j >>= 1) {
-                    const unsigned long long ok = __shfl_xor(key, j, 64);
-                    const bool want_min = ((lane & j) == 0) == ((lane & kk) == 0);
-                    if (want_min == (ok < key)) key = ok;
-                }
+            for (int q = 1; q < kMicroSeg; ++q) r = j == q ? k[q] : r;
+            return f64_from_key(r);
+        };
+        qs_write(a, s, n, acc.hi + acc.lo, get);
+    }
+}
+
+// The tiny list: one wave per segment (64-lane bitonic network on the keys, order statistics
+// gathered by shuffles).
+__global__ __launch_bounds__(kBlock) void k_qs_tiny(const double *__restrict__ src, const int64_t *__restrict__ offs,
+                                                    const int32_t *__restrict__ list, const int64_t *__restrict__ d_ln,
+                                                    QsArgs a) {
+    const int lane = lane_id();
+    const int64_t ns = *d_ln;
+    const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
+    for (int64_t w = int64_t(blockIdx.x) * (kBlock / kWave) + wave_id(); w < ns; w += nwaves) {
+        const int64_t st = list[w];
+        const int64_t sb = offs[st];
+        const int sn = int(offs[st + 1] - sb);
+        const double x = lane < sn ? src[sb + lane] : 0.0;
+        DD acc = wave_dd_sum(DD{lane < sn ? x : 0.0, 0.0});
+        unsigned long long key = lane < sn ? f64_key(x) : ~0ull;
+#pragma unroll
+        for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+            for (int j = kk >> 1; j > 0; j >>= 1) {
+                const unsigned long long ok = __shfl_xor(key, j, 64);
+                const bool want_min = ((lane & j) == 0) == ((lane & kk) == 0);
+                if (want_min == (ok < key)) key = ok;
             }
-            // every rank any statistic reads, gathered by shuffles (all lanes take part)
-            const int nt = 2 + 2 * a.nq;
-            int rk[kQsMaxT];
-            double rv[kQsMaxT];
+        }
+        // every rank any statistic reads, gathered by shuffles (all lanes take part)
+        const int nt = 2 + 2 * a.nq;
+        int rk[kQsMaxT];
+        double rv[kQsMaxT];
 #pragma unroll
-            for (int t = 0; t < kQsMaxT; ++t) {
-                rk[t] = t < nt ? int(qs_rank(sn, a, t)) : -1;
-                rv[t] = f64_from_key(__shfl(key, rk[t] < 0 ? 0 : rk[t], 64));
-            }
-            if (lane == 0) {
-                auto get = [&](int64_t j) {
-                    double r = 0.0;
+        for (int t = 0; t < kQsMaxT; ++t) {
+            rk[t] = t < nt ? int(qs_rank(sn, a, t)) : -1;
+            rv[t] = f64_from_key(__shfl(key, rk[t] < 0 ? 0 : rk[t], 64));
+        }
+        if (lane == 0) {
+            auto get = [&](int64_t j) {
+                double r = 0.0;
 #pragma unroll
-                    for (int t = 0; t < kQsMaxT; ++t) r = rk[t] == j ? rv[t] : r;
-                    return r;
-                };
-                qs_write(a, st, sn, acc.hi + acc.lo, get);
-            }
+                for (int t = 0; t < kQsMaxT; ++t) r = rk[t] == j ? rv[t] : r;
+                return r;
+            };
+            qs_write(a, st, sn, acc.hi + acc.lo, get);
         }
     }
 }
 
-// Segments of min_len < n <= MAXN values, one workgroup each: every segment, or (very many
-// segments) those of up to two size-class lists (seg_lists).
+// The segments of one class list (at most MAXN values each), one workgroup each.
 template <int BS, int MAXN>
 __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src, const int64_t *__restrict__ offs,
-                                                 int64_t S, int64_t min_len, const int32_t *__restrict__ l1,
-                                                 const int64_t *__restrict__ n1, const int32_t *__restrict__ l2,
-                                                 const int64_t *__restrict__ n2, QsArgs a) {
+                                                 const int32_t *__restrict__ list, const int64_t *__restrict__ d_ln,
+                                                 QsArgs a) {
     constexpr int NW = BS / kWave;
     constexpr int IPT = MAXN / BS;                // values per thread
     constexpr int NB = MAXN < 4096 ? MAXN : 4096;  // buckets
@@ -1813,12 +1840,11 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
     __shared__ int64_t s_r, s_rc;
     const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
     int64_t ge100 = 0;
-    const int64_t ln1 = l1 ? *n1 : S, ln = l1 ? ln1 + (l2 ? *n2 : 0) : S;
+    const int64_t ln = *d_ln;
     for (int64_t it = blockIdx.x; it < ln; it += gridDim.x) {
-        const int64_t s = l1 ? (it < ln1 ? l1[it] : l2[it - ln1]) : it;
+        const int64_t s = list[it];
         const int64_t b = offs[s];
         const int64_t n = offs[s + 1] - b;
-        if (n <= min_len || n > MAXN) continue;
         uint64_t k[IPT];
         uint64_t lo = ~0ull, hi = 0ull;
         DD acc{0.0, 0.0};
@@ -2076,33 +2102,35 @@ void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_h
     if (S <= 0) return;
     // algorithmic bytes: the values once (8 B each) + the offsets + the statistics written
     ProbeScope ps(c, "seg_qstats", double(S) * (8.0 + 8.0 * (2 + nq)), sg.offs + S, 8.0);
+    // class lists (capacities: a segment of the class holds more than the class below allows)
+    auto cap = [&](int64_t minlen) { return S < sg.n_cap / (minlen + 1) + 1 ? S : sg.n_cap / (minlen + 1) + 1; };
+    const int64_t caps[3] = {cap(kMicroSeg), lb > kTinySeg ? cap(kTinySeg) : 0, lb > 1024 ? cap(1024) : 0};
+    QsLists L;
+    L.d_n = c->arena.get<int64_t>(3);
+    for (int k = 0; k < 3; ++k) L.ids[k] = c->arena.get<int32_t>(caps[k]);
+    dev_fill(c, L.d_n, 0, 3 * 8);
     const int64_t groups = (S + 63) / 64;
-    k_qs_small<<<grid_for(groups, kBlock / kWave, 8192), kBlock, 0, c->stream>>>(vals, sg.offs, S, a);
+    k_qs_micro<<<grid_for(groups, kBlock / kWave, 8192), kBlock, 0, c->stream>>>(vals, sg.offs, S, a, L);
     FZ_LAUNCH_CHECK();
-    // the workgroup classes walk their size classes' lists when there are very many segments
-    // (config 5: ~2e7 sessions, almost all of a handful of values)
-    SegLists L;
-    if (lb > kTinySeg && S > kManySegs) L = seg_lists(c, sg);
-    auto grid = [&](int64_t cap, int64_t lim) { return unsigned(cap < 1 ? 1 : (cap < lim ? cap : lim)); };
+    auto grid = [](int64_t n, int64_t lim) { return unsigned(n < 1 ? 1 : (n < lim ? n : lim)); };
+    if (lb > kMicroSeg) {
+        k_qs_tiny<<<grid((caps[0] + 3) / 4, 8192), kBlock, 0, c->stream>>>(vals, sg.offs, L.ids[0], L.d_n, a);
+        FZ_LAUNCH_CHECK();
+    }
     if (lb > kTinySeg) {
-        const int64_t cap = L.on ? L.cap[kClassMid] : S;
-        k_qs_block<256, 1024><<<grid(cap, 8192), 256, 0, c->stream>>>(
-            vals, sg.offs, S, kTinySeg, L.on ? L.ids[kClassMid] : nullptr, L.on ? L.d_n + kClassMid : nullptr,
-            nullptr, nullptr, a);
+        k_qs_block<256, 1024><<<grid(caps[1], 8192), 256, 0, c->stream>>>(vals, sg.offs, L.ids[1], L.d_n + 1, a);
         FZ_LAUNCH_CHECK();
     }
     if (lb > 1024) {
-        const int64_t cap = L.on ? L.cap[kClassWide] + L.cap[kClassBig] : S;
-        k_qs_block<1024, kQsMax><<<grid(cap, 1024), 1024, 0, c->stream>>>(
-            vals, sg.offs, S, 1024, L.on ? L.ids[kClassWide] : nullptr, L.on ? L.d_n + kClassWide : nullptr,
-            L.on ? L.ids[kClassBig] : nullptr, L.on ? L.d_n + kClassBig : nullptr, a);
+        k_qs_block<1024, kQsMax><<<grid(caps[2], 1024), 1024, 0, c->stream>>>(vals, sg.offs, L.ids[2], L.d_n + 2, a);
         FZ_LAUNCH_CHECK();
     }
 }
 
-// levene([x, y], center='median') (scipy _morestats.py levene).
-void levene_two(fz_ctx *c, const uint64_t *skx, const double *x, int64_t nxm, const int64_t *d_nx,
-                       const uint64_t *sky, const double *y, int64_t nym, const int64_t *d_ny, double *out) {
+// levene([x, y], center='median') (scipy _morestats.py levene), the two medians given on the
+// device (medx / medy: e.g. fields of fz_describe results)
+void levene_two_med(fz_ctx *c, const double *medx, const double *x, int64_t nxm, const int64_t *d_nx,
+                    const double *medy, const double *y, int64_t nym, const int64_t *d_ny, double *out) {
     double *med = c->arena.get<double>(2);
     int64_t *ox = c->arena.get<int64_t>(2), *oy = c->arena.get<int64_t>(2);  // each sample's one segment
     map_n(c, 1, nullptr, [=] __device__(int64_t) {
@@ -2110,13 +2138,8 @@ void levene_two(fz_ctx *c, const uint64_t *skx, const double *x, int64_t nxm, co
         ox[1] = *d_nx;
         oy[0] = 0;
         oy[1] = *d_ny;
-        for (int g = 0; g < 2; ++g) {
-            const uint64_t *k = g ? sky : skx;
-            const int64_t n = g ? *d_ny : *d_nx;
-            med[g] = n <= 0 ? NAN
-                            : ((n & 1) ? f64_from_key(k[n / 2])
-                                       : (f64_from_key(k[n / 2 - 1]) + f64_from_key(k[n / 2])) / 2.0);
-        }
+        med[0] = *medx;
+        med[1] = *medy;
     });
     double *zb = c->arena.get<double>(2), *dv = c->arena.get<double>(2);
     Segs sx{1, ox, nxm}, sy{1, oy, nym};

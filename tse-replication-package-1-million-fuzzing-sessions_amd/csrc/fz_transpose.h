@@ -49,7 +49,9 @@ __global__ __launch_bounds__(kBlock) void k_rt_keys(const int64_t *__restrict__ 
     }
 }
 
-// stable rank of every key by counting (R <= kRtRankMax): rank = #smaller + #equal before
+// stable rank of every key by counting (R <= kRtRankMax): rank = #smaller + #equal before.  One
+// wave per key: the lanes compare 64 keys at a time (LDS broadcast-free, one key per lane) and the
+// wave sums - a thread walking all R keys alone was latency-bound (42 us at R = 1000)
 template <typename Grp>
 __global__ __launch_bounds__(kBlock) void k_rt_rank(const int64_t *__restrict__ offs, int64_t R, int lb, Grp grp,
                                                     uint32_t *__restrict__ skey, uint32_t *__restrict__ sid) {
@@ -57,16 +59,21 @@ __global__ __launch_bounds__(kBlock) void k_rt_rank(const int64_t *__restrict__ 
     for (int64_t j = threadIdx.x; j < R; j += kBlock)
         s_key[j] = (uint32_t(grp(j)) << lb) | uint32_t(offs[j + 1] - offs[j]);
     __syncthreads();
-    const int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (k >= R) return;
-    const uint32_t mine = s_key[k];
-    uint32_t rank = 0;
-    for (int64_t j = 0; j < R; ++j) {
-        const uint32_t o = s_key[j];
-        rank += (o < mine) || (o == mine && j < k);
+    const int lane = lane_id();
+    const int64_t nw = int64_t(gridDim.x) * (kBlock / kWave);
+    for (int64_t k = int64_t(blockIdx.x) * (kBlock / kWave) + wave_id(); k < R; k += nw) {
+        const uint32_t mine = s_key[k];
+        uint32_t rank = 0;
+        for (int64_t j = lane; j < R; j += kWave) {
+            const uint32_t o = s_key[j];
+            rank += (o < mine) || (o == mine && j < k);
+        }
+        rank = wave_sum(rank);
+        if (lane == 0) {
+            skey[rank] = mine;
+            sid[rank] = uint32_t(k);
+        }
     }
-    skey[rank] = mine;
-    sid[rank] = uint32_t(k);
 }
 
 // pre[b][j] (b in [0, nB], j in [0, R]) = #{j' < j : sid[j'] < 64 b}  (workgroups 0..nB);
@@ -249,7 +256,8 @@ void ragged_transpose(fz_ctx *c, const int64_t *offs, int64_t R, int64_t M, int6
     if (R <= kRtRankMax) {
         skey = c->arena.get<uint32_t>(R);
         sid = c->arena.get<uint32_t>(R);
-        k_rt_rank<Grp><<<unsigned((R + kBlock - 1) / kBlock), kBlock, 0, st>>>(offs, R, lb, grp, skey, sid);
+        const int64_t wg = (R + kBlock / kWave - 1) / (kBlock / kWave);  // one wave per key
+        k_rt_rank<Grp><<<unsigned(wg < 128 ? wg : 128), kBlock, 0, st>>>(offs, R, lb, grp, skey, sid);
         FZ_LAUNCH_CHECK();
     } else {
         skey = c->arena.get<uint32_t>(R);
