@@ -329,6 +329,10 @@ void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int 
 // The same without the copy back: on return keys / vals point at the sorted data (the inputs or
 // arena scratch of the current call).
 void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits);
+// The same over the first *d_live of n_cap keys (device count): the passes' tiles past them leave at
+// once; on return keys / vals [0, *d_live) are sorted, the entries past them undefined.
+void radix_sort_pairs_swap_live(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n_cap, const int64_t *d_live,
+                                int bits);
 // Columns that travel with the keys through every pass (each pass records every input position's
 // destination and moves the columns there): on return out[j] holds column j in sorted order.
 constexpr int kMaxPayload = 6;

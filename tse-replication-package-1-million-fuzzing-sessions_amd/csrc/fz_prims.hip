@@ -411,10 +411,12 @@ constexpr int kHistKeysPerBlock = FZ_HIST_KPB;  // keys per histogram workgroup 
 constexpr int kOsGroup = 8;  // tiles per look-back group (one {tiles, sum} word per group and digit)
 
 template <typename KeyT>
-__global__ __launch_bounds__(kBlock) void k_onesweep_hist(const KeyT *__restrict__ keys, int64_t n, int npass,
+__global__ __launch_bounds__(kBlock) void k_onesweep_hist(const KeyT *__restrict__ keys, int64_t n_cap, int npass,
                                                           unsigned long long *__restrict__ ghist,
-                                                          unsigned long long *__restrict__ gsum, int64_t gsum_words) {
+                                                          unsigned long long *__restrict__ gsum, int64_t gsum_words,
+                                                          const int64_t *__restrict__ d_live) {
     __shared__ uint32_t s_h[kOsMaxPasses][kRadix];
+    const int64_t n = d_live && *d_live < n_cap ? *d_live : n_cap;  // (live-bounded sorts: the first *d_live keys)
     // the passes' look-back group sums start from zero (this launch precedes every pass)
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < gsum_words; i += int64_t(gridDim.x) * kBlock)
         gsum[i] = 0ull;
@@ -503,7 +505,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const KeyT *__restrict__ key
                                                      uint64_t epoch,
                                                      unsigned long long *__restrict__ gsum,
                                                      unsigned long long *__restrict__ next_hist,
-                                                     RadixPayload pl) {
+                                                     RadixPayload pl, const int64_t *__restrict__ d_live) {
     constexpr int ITEMS = TILE / BLOCK, WAVES = BLOCK / kWave;
     static_assert(BLOCK >= kRadix && TILE % BLOCK == 0 && TILE <= 65536, "radix pass shape");
     __shared__ uint64_t s_stage[TILE];  // the keys, then 8-byte payload columns
@@ -525,9 +527,13 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const KeyT *__restrict__ key
         for (int i = tid; i < kOsMaxPasses * kRadix; i += BLOCK) next_hist[i] = 0ull;
     for (int i = tid; i < WAVES * kRadix; i += BLOCK) (&s_wcnt[0][0])[i] = 0;
     const int64_t gcount = dig ? int64_t(ghist[tid]) : 0;  // issued early: consumed after the ranking
+    // live-bounded sorts (d_live): only the first *d_live keys are sorted; the tiles past them leave
+    // after drawing their ticket (no later tile looks back at them), the entries past them untouched
+    if (d_live && *d_live < n) n = *d_live > 0 ? *d_live : 0;
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t base = tile * TILE;
+    if (base >= n) return;
 #ifdef FZ_OS_TIMING
     if (tid == 0) atomicMin(&g_os_first, (unsigned long long)wall_clock64());
 #endif
@@ -736,8 +742,10 @@ void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t 
     radix_sort_pairs_payload(c, keys, vals, n, bits, none);
 }
 
+
 template <typename KeyT>
-static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl) {
+static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl,
+                               const int64_t *d_live = nullptr) {
     if (n <= 1 || bits <= 0) {  // nothing to sort (one key, or a 0-bit key: one project): unmoved
         for (int j = 0; j < pl.n; ++j) pl.out[j] = const_cast<void *>(pl.in[j]);
         return;
@@ -768,7 +776,7 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
     {
         ProbeScope ps(c, "radix_hist", 8.0 * double(n));
         k_onesweep_hist<KeyT><<<grid_for(n, kHistKeysPerBlock, 2048), kBlock, 0, c->stream>>>(keys, n, npass, ghist,
-                                                                                             gsum, gwords * npass);
+                                                                                             gsum, gwords * npass, d_live);
         FZ_LAUNCH_CHECK();
     }
     // Constant-digit passes are identity permutations.  Finding them needs a host round trip, which
@@ -816,11 +824,11 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
         if (big)                                                                                              \
             k_onesweep<KeyT, V, PL, kSortTileBig, kOsBlockBig><<<unsigned(nb), kOsBlockBig, 0, c->stream>>>(   \
                 ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, lb.status, lb.ticket, lb.epoch,          \
-                gsum + p * gwords, next_hist, step);                                                          \
+                gsum + p * gwords, next_hist, step, d_live);                                                  \
         else                                                                                                  \
             k_onesweep<KeyT, V, PL, kSortTile, kOsBlock><<<unsigned(nb), kOsBlock, 0, c->stream>>>(            \
                 ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, lb.status, lb.ticket, lb.epoch,          \
-                gsum + p * gwords, next_hist, step);                                                          \
+                gsum + p * gwords, next_hist, step, d_live);                                                  \
     } while (0)
             if (pl.n > 0) {
                 if (vals)
@@ -852,6 +860,11 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
 
 void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl) {
     radix_payload_impl<uint64_t>(c, keys, vals, n, bits, pl);
+}
+void radix_sort_pairs_swap_live(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n_cap, const int64_t *d_live,
+                                int bits) {
+    RadixPayload none;
+    radix_payload_impl<uint64_t>(c, keys, vals, n_cap, bits, none, d_live);
 }
 void radix_sort_pairs_payload32(fz_ctx *c, uint32_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl) {
     FZ_CHECK(bits <= 32, "radix_sort_pairs_payload32: keys of more than 32 bits");
@@ -1136,6 +1149,28 @@ __device__ inline uint32_t sel_bucket(uint64_t k, uint64_t lo, double sc, int nb
     return q < uint32_t(nb) ? q : uint32_t(nb - 1);
 }
 
+// for every i < n of this thread (i = tid, tid + BS, ...; that order): body(i, load(i)), the loads
+// of kSelU consecutive items issued before their bodies (one memory latency per kSelU items, not
+// one per item)
+constexpr int kSelU = 8;
+template <typename Load, typename Body>
+__device__ inline void sel_for(int64_t n, const Load &load, const Body &body) {
+    using T = decltype(load(int64_t(0)));
+    for (int64_t i0 = threadIdx.x; i0 < n; i0 += int64_t(kSelBlock) * kSelU) {
+        T v[kSelU];
+#pragma unroll
+        for (int u = 0; u < kSelU; ++u) {
+            const int64_t i = i0 + int64_t(u) * kSelBlock;
+            v[u] = i < n ? load(i) : T{};
+        }
+#pragma unroll
+        for (int u = 0; u < kSelU; ++u) {
+            const int64_t i = i0 + int64_t(u) * kSelBlock;
+            if (i < n) body(i, v[u]);
+        }
+    }
+}
+
 // sh.res[t] = the key of rank sh.rank[t] (t < nt) among the n keys key(i), whose min / max are lo / hi
 template <typename KeyF>
 __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64_t hi, int nt, SelShared &sh) {
@@ -1151,7 +1186,7 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
     for (int j = tid; j <= nb; j += BS) sh.cnt[j] = 0u;
     for (int j = tid; j < nb; j += BS) sh.map[j] = 0xff;
     __syncthreads();
-    for (int64_t i = tid; i < n; i += BS) atomicAdd(&sh.cnt[sel_bucket(key(i), lo, sc, nb)], 1u);
+    sel_for(n, key, [&](int64_t, uint64_t k) { atomicAdd(&sh.cnt[sel_bucket(k, lo, sc, nb)], 1u); });
     __syncthreads();
     {  // exclusive scan of the bucket counts: thread t takes buckets [t * 4, t * 4 + 4)
         constexpr int BPT = kSelNB / BS;
@@ -1198,11 +1233,10 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
         }
     }
     __syncthreads();
-    for (int64_t i = tid; i < n; i += BS) {
-        const uint64_t k = key(i);
+    sel_for(n, key, [&](int64_t, uint64_t k) {
         const uint8_t slot = sh.map[sel_bucket(k, lo, sc, nb)];
         if (slot != 0xff) sh.list[slot][atomicAdd(&sh.fill[slot], 1u)] = k;
-    }
+    });
     __syncthreads();
     auto rank_list = [&](int slot, int sz, int64_t want, int t) {  // one wave
         const uint64_t e = lane < sz ? sh.list[slot][lane] : ~0ull;
@@ -1220,13 +1254,12 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
         if (sh.tslot[t] >= 0) continue;
         const uint32_t tb = uint32_t(sh.tb[t]);
         uint64_t rlo = ~0ull, rhi = 0ull;
-        for (int64_t i = tid; i < n; i += BS) {
-            const uint64_t k = key(i);
+        sel_for(n, key, [&](int64_t, uint64_t k) {
             if (sel_bucket(k, lo, sc, nb) == tb) {
                 rlo = k < rlo ? k : rlo;
                 rhi = k > rhi ? k : rhi;
             }
-        }
+        });
         sel_minmax(rlo, rhi, sh);
         int64_t r = sh.toff[t], cnt = sh.tsz[t];
         while (rlo != rhi && cnt > 64) {
@@ -1234,10 +1267,9 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
             const double sc2 = double(nb2) / (double(rhi - rlo) + 1.0);
             for (int j = tid; j <= nb2; j += BS) sh.cnt[j] = 0u;
             __syncthreads();
-            for (int64_t i = tid; i < n; i += BS) {
-                const uint64_t k = key(i);
+            sel_for(n, key, [&](int64_t, uint64_t k) {
                 if (k >= rlo && k <= rhi) atomicAdd(&sh.cnt[sel_bucket(k, rlo, sc2, nb2)], 1u);
-            }
+            });
             __syncthreads();
             if (w == 0) {  // the sub-bucket holding rank r
                 int64_t base = 0;
@@ -1261,13 +1293,12 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
             __syncthreads();
             const uint32_t sb = sh.sb;
             uint64_t nlo = ~0ull, nhi = 0ull;
-            for (int64_t i = tid; i < n; i += BS) {
-                const uint64_t k = key(i);
+            sel_for(n, key, [&](int64_t, uint64_t k) {
                 if (k >= rlo && k <= rhi && sel_bucket(k, rlo, sc2, nb2) == sb) {
                     nlo = k < nlo ? k : nlo;
                     nhi = k > nhi ? k : nhi;
                 }
-            }
+            });
             r = sh.r;
             cnt = sh.rc;
             sel_minmax(nlo, nhi, sh);
@@ -1279,10 +1310,9 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
         } else {  // <= 64 values in [rlo, rhi]
             if (tid == 0) sh.fill[0] = 0u;
             __syncthreads();
-            for (int64_t i = tid; i < n; i += BS) {
-                const uint64_t k = key(i);
+            sel_for(n, key, [&](int64_t, uint64_t k) {
                 if (k >= rlo && k <= rhi) sh.list[0][atomicAdd(&sh.fill[0], 1u)] = k;
-            }
+            });
             __syncthreads();
             if (w == 0) rank_list(0, int(cnt), r, t);
         }
@@ -1309,8 +1339,8 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
     uint64_t lo = ~0ull, hi = 0ull;
     DD acc{0.0, 0.0};
     unsigned long long lt0 = 0, le0 = 0, leinf = 0;
-    for (int64_t i = tid; i < n; i += kSelBlock) {
-        const double v = x[i];
+    auto ld = [=](int64_t i) { return x[i]; };
+    sel_for(n, ld, [&](int64_t, double v) {
         const uint64_t k = f64_key(v);
         acc = dd_add_d(acc, v);
         lo = k < lo ? k : lo;
@@ -1318,7 +1348,7 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
         lt0 += k < kneg0;
         le0 += k <= kpos0;
         leinf += k <= kinf;
-    }
+    });
     sel_minmax(lo, hi, sh);
     lt0 = wave_sum(lt0);
     le0 = wave_sum(le0);
@@ -1331,11 +1361,11 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
     DD t = block_dd_sum_1024(acc, s_hi, s_lo);  // (its barriers order the counters too)
     const double mean = (t.hi + t.lo) / double(n);
     acc = DD{0.0, 0.0};
-    for (int64_t i = tid; i < n; i += kSelBlock) {
-        double v = x[i] - mean;
+    sel_for(n, ld, [&](int64_t, double v) {
+        v = v - mean;
         v = v * v;
         acc = dd_add_d(acc, v);
-    }
+    });
     t = block_dd_sum_1024(acc, s_hi, s_lo);
     const double std = sqrt((t.hi + t.lo) / double(n));
     const int64_t c_lt0 = int64_t(s_c[0]), c_le0 = int64_t(s_c[1]), c_leinf = int64_t(s_c[2]);

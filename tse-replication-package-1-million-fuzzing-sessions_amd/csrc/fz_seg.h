@@ -329,7 +329,8 @@ void map_n(fz_ctx *c, int64_t n_cap, const int64_t *d_n, F f) {
 
 // ---- series operations (fz_series.hip) ----------------------------------------------------
 // Values of each segment sorted ascending (stable: ties keep source order).  pos[i] = source
-// index of sorted element i.  Elements past offs[S] are left at the end.
+// index of sorted element i.  Elements past offs[S] are left at the end (undefined after the radix
+// path of one long segment, which sorts up to offs[1] only).
 struct SortedSegs {
     double *val = nullptr;
     int32_t *pos = nullptr;

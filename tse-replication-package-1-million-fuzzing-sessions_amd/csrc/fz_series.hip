@@ -559,18 +559,22 @@ struct F64Sink {
 // One segment [offs[0], offs[1]) of a value array as radix keys: positions before it key 0, after
 // it ~0, so a stable sort of the whole array leaves them where they are and the segment's values
 // sorted in between; payload = the position.
+// (only the positions before hi are keyed and sorted: the sort is bounded by offs[1], the
+// positions past it are left undefined)
 __global__ __launch_bounds__(kBlock) void k_f64_seg1_keys(const double *__restrict__ x, int64_t n,
                                                           const int64_t *__restrict__ offs, uint64_t *__restrict__ k,
                                                           uint32_t *__restrict__ v) {
-    const int64_t lo = offs[0], hi = offs[1];
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        k[i] = i < lo ? 0ull : (i < hi ? f64_key(x[i]) : ~0ull);
+    const int64_t lo = offs[0], hi = offs[1] < n ? offs[1] : n;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < hi; i += int64_t(gridDim.x) * kBlock) {
+        k[i] = i < lo ? 0ull : f64_key(x[i]);
         v[i] = uint32_t(i);
     }
 }
 
 __global__ __launch_bounds__(kBlock) void k_f64_from_keys(const uint64_t *__restrict__ k, const uint32_t *__restrict__ v,
-                                                          int64_t n, double *__restrict__ val, int32_t *__restrict__ pos) {
+                                                          int64_t n_cap, const int64_t *__restrict__ offs,
+                                                          double *__restrict__ val, int32_t *__restrict__ pos) {
+    const int64_t n = offs[1] < n_cap ? offs[1] : n_cap;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
         val[i] = f64_from_key(k[i]);
         pos[i] = int32_t(v[i]);
@@ -592,10 +596,12 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
         // passes after a host round trip that a recorded graph cannot make.
         uint64_t *k = c->arena.get<uint64_t>(n);
         uint32_t *v = c->arena.get<uint32_t>(n);
+        // (live-bounded: the passes cover the segment's end offs[1], not the capacity - RQ3's union
+        // fills ~80 % of its capacity at config 2)
         k_f64_seg1_keys<<<grid_for(n, kBlock, 4096), kBlock, 0, c->stream>>>(src, n, sg.offs, k, v);
         FZ_LAUNCH_CHECK();
-        radix_sort_pairs_swap(c, k, v, n, 64);
-        k_f64_from_keys<<<grid_for(n, kBlock, 4096), kBlock, 0, c->stream>>>(k, v, n, out.val, out.pos);
+        radix_sort_pairs_swap_live(c, k, v, n, sg.offs + 1, 64);
+        k_f64_from_keys<<<grid_for(n, kBlock, 4096), kBlock, 0, c->stream>>>(k, v, n, sg.offs, out.val, out.pos);
         FZ_LAUNCH_CHECK();
         return out;
     }
