@@ -4,7 +4,9 @@
 #   stages:<cfg> per-stage step times (serial), stage_times.sh
 #   drop:<cfg>   the concurrent step without one analysis group at a time
 #   bench:<cfg>  one bench line (json) on <cfg>
-#   tests[:k]    pytest -m gpu (optionally -k expression)
+#   tests[:k]    pytest -m gpu (optionally -k expression, '+' = or)
+#   pmc:<cfg> sq:<cfg> strong:<cfg> e2e:<cfg> cpu:<cfg>   PMC traffic, SQ counters, strong-scaling
+#                rehearsal, end-to-end drop-ins, bench with the CPU baseline
 # Each GPU step has its own time limit; a fault / abort / timeout ends the script.
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
@@ -26,6 +28,22 @@ for s in $STEPS; do
       st=20; [ "$arg" != c2 ] && st=5
       timeout -k 10 600 python -u bench.py --config $arg --steps $st --warmup 2 --no-cpu-baseline > $O/${T}_bench_$arg.json 2> $O/${T}_bench_$arg.err || exit $?
       python3 -c "import json; d=json.loads([l for l in open('$O/${T}_bench_$arg.json') if l.startswith('{')][-1]); print('$arg', d['ms_per_step'], flush=True)" ;;
+    pmc)  # FETCH_SIZE and WRITE_SIZE in separate passes (serial analyses: program order), then traffic per probe
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $O/${T}_pmc_${arg}_$ctr -o run -- python3 -u bench.py --config $arg --steps 2 --warmup 1 --no-cpu-baseline --probe-steps 1 --serial > $O/${T}_pmc_${arg}_$ctr.log 2>&1 || exit $?
+      done
+      python3 scripts/pmc_traffic.py $(find $O/${T}_pmc_${arg}_FETCH_SIZE -name "*counter_collection.csv" | head -1) $(find $O/${T}_pmc_${arg}_WRITE_SIZE -name "*counter_collection.csv" | head -1) $arg $O/${T}_${arg}_pmc_traffic.json > /dev/null && echo "pmc $arg ok" ;;
+    sq)  # shader-sequencer counters per kernel family (one pass, <= 8 SQ counters)
+      timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VALU --output-format csv -d $O/${T}_sq_$arg -o run -- python3 -u bench.py --config $arg --steps 2 --warmup 1 --no-cpu-baseline --probe-steps 0 --serial > $O/${T}_sq_$arg.log 2>&1 || exit $?
+      python3 scripts/pmc_sq.py $(find $O/${T}_sq_$arg -name "*counter_collection.csv" | head -1) $O/${T}_${arg}_sq.json ;;
+    strong)
+      CONFIG=$arg timeout -k 10 1100 bash scripts/gpu_strong_rehearsal.sh > $O/${T}_strong_$arg.txt 2>&1 || exit $?; cat $O/${T}_strong_$arg.txt ;;
+    e2e)
+      timeout -k 10 900 python -u scripts/e2e_suite.py --config $arg --no-figures > $O/${T}_e2e_$arg.json 2> $O/${T}_e2e_$arg.err || exit $?; tail -1 $O/${T}_e2e_$arg.json ;;
+    cpu)  # bench line with the multi-core C++ CPU baseline
+      st=10; [ "$arg" != c2 ] && st=5
+      timeout -k 10 900 python -u bench.py --config $arg --steps $st --warmup 2 > $O/${T}_cpu_$arg.json 2> $O/${T}_cpu_$arg.err || exit $?
+      python3 -c "import json; d=json.loads([l for l in open('$O/${T}_cpu_$arg.json') if l.startswith('{')][-1]); print('$arg', d['ms_per_step'], d.get('cpu_baseline'), flush=True)" ;;
     tests)
       k=""; [ "$arg" != tests ] && k="${arg//+/ or }"
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 500 --timeout-method thread ${k:+-k "$k"} > $O/${T}_pytest.log 2>&1; rc=$?

@@ -390,6 +390,10 @@ struct Fill {
     unsigned char value;
 };
 void fill_batch(fz_ctx *c, std::initializer_list<Fill> regions);
+// The same plus, in the same launch, a byte copy and one int64 word (*word_src -> *word_dst; a word
+// inside a filled region is written in place of its fill)
+void fill_copy_batch(fz_ctx *c, std::initializer_list<Fill> regions, const void *copy_src, void *copy_dst,
+                     int64_t copy_bytes, const int64_t *word_src = nullptr, int64_t *word_dst = nullptr);
 // Device-side byte fill / copy kernels on the context stream.  Used instead of hipMemsetAsync /
 // hipMemcpyAsync(D2D) on every path an fz_capture recording may contain: a recorded sequence is
 // then kernels only, replayed in stream order.

@@ -19,8 +19,18 @@ struct FillList {
     unsigned char *ptr[kMaxFills];
     int64_t bytes[kMaxFills];
     unsigned char value[kMaxFills];
+    // optional, in the same launch: a byte copy (copy_n bytes copy_src -> copy_dst) and one int64
+    // word (*word_src -> *word_dst); a word that lies inside a filled region takes the place of its
+    // fill there (no ordering between the fill and the word)
+    const unsigned char *copy_src;
+    unsigned char *copy_dst;
+    int64_t copy_n;
+    const int64_t *word_src;
+    int64_t *word_dst;
+    int word_in_fill;
 };
 __global__ __launch_bounds__(kBlock) void k_fill_batch(FillList f) {
+    const int64_t *wdst = f.word_in_fill ? f.word_dst : nullptr;
     for (int r = 0; r < f.n; ++r) {
         unsigned char *p = f.ptr[r];
         const int64_t nb = f.bytes[r];
@@ -28,8 +38,10 @@ __global__ __launch_bounds__(kBlock) void k_fill_batch(FillList f) {
         if ((reinterpret_cast<uintptr_t>(p) & 7) == 0) {  // 8-byte stores, byte tail
             const uint64_t w = 0x0101010101010101ull * v;
             const int64_t n8 = nb >> 3;
-            for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n8; i += int64_t(gridDim.x) * kBlock)
-                reinterpret_cast<uint64_t *>(p)[i] = w;
+            for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n8; i += int64_t(gridDim.x) * kBlock) {
+                uint64_t *q = reinterpret_cast<uint64_t *>(p) + i;
+                *q = (reinterpret_cast<const int64_t *>(q) == wdst) ? uint64_t(*f.word_src) : w;
+            }
             for (int64_t i = (n8 << 3) + int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nb;
                  i += int64_t(gridDim.x) * kBlock)
                 p[i] = v;
@@ -38,10 +50,21 @@ __global__ __launch_bounds__(kBlock) void k_fill_batch(FillList f) {
                 p[i] = v;
         }
     }
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < f.copy_n; i += int64_t(gridDim.x) * kBlock)
+        f.copy_dst[i] = f.copy_src[i];
+    if (f.word_dst && !f.word_in_fill && blockIdx.x == 0 && threadIdx.x == 0) *f.word_dst = *f.word_src;
 }
-void fill_batch(fz_ctx *c, std::initializer_list<Fill> regions) {
+void fill_batch(fz_ctx *c, std::initializer_list<Fill> regions) { fill_copy_batch(c, regions, nullptr, nullptr, 0); }
+
+void fill_copy_batch(fz_ctx *c, std::initializer_list<Fill> regions, const void *copy_src, void *copy_dst,
+                     int64_t copy_bytes, const int64_t *word_src, int64_t *word_dst) {
     FillList f{};
-    int64_t most = 0;
+    f.copy_src = static_cast<const unsigned char *>(copy_src);
+    f.copy_dst = static_cast<unsigned char *>(copy_dst);
+    f.copy_n = copy_src ? copy_bytes : 0;
+    f.word_src = word_src;
+    f.word_dst = word_dst;
+    int64_t most = f.copy_n;
     for (const Fill &r : regions) {
         FZ_CHECK(f.n < kMaxFills, "fill_batch: too many regions");
         if (r.bytes <= 0) continue;
@@ -49,9 +72,15 @@ void fill_batch(fz_ctx *c, std::initializer_list<Fill> regions) {
         f.bytes[f.n] = r.bytes;
         f.value[f.n] = r.value;
         most = r.bytes > most ? r.bytes : most;
+        const char *lo = static_cast<const char *>(r.ptr), *wp = reinterpret_cast<const char *>(word_dst);
+        if (word_dst && wp >= lo && wp < lo + r.bytes) {  // the word replaces its fill (8-byte path only)
+            FZ_CHECK((reinterpret_cast<uintptr_t>(r.ptr) & 7) == 0 && (wp - lo) % 8 == 0 && wp + 8 <= lo + r.bytes,
+                     "fill_copy_batch: the word must be an aligned word of an aligned region");
+            f.word_in_fill = 1;
+        }
         ++f.n;
     }
-    if (f.n == 0) return;
+    if (f.n == 0 && f.copy_n == 0 && !word_dst) return;
     k_fill_batch<<<grid_for((most + 7) / 8, kBlock, 1024), kBlock, 0, c->stream>>>(f);
     FZ_LAUNCH_CHECK();
 }

@@ -141,13 +141,18 @@ void store_eligibility(fz_ctx *c) {
 // elig[p] = project has >= 365 qualifying coverage rows; *d_count = number eligible.
 // Every RQ script starts from this set (rq1:144-152, rq2_count:272-280, rq2_add:20-27, rq3:222-226,
 // rq4a:68-80, rq4b:164-181 - the same GROUP BY/HAVING), so the store computes it once per load.
-void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count) {
+void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count, std::initializer_list<Fill> fills) {
     const Store &s = store_of(c);
     const int64_t P = s.P;
     const uint8_t *src = s.elig.as<uint8_t>();
     const int64_t *n = s.n_elig.as<int64_t>();
-    k_copy_elig<<<grid_for(P > 0 ? P : 1), kBlock, 0, c->stream>>>(src, n, P, elig, d_count);
-    FZ_LAUNCH_CHECK();
+    if (fills.size() == 0) {
+        k_copy_elig<<<grid_for(P > 0 ? P : 1), kBlock, 0, c->stream>>>(src, n, P, elig, d_count);
+        FZ_LAUNCH_CHECK();
+        return;
+    }
+    // the analysis' output / scratch fills, the flags copy and the count in one launch
+    fill_copy_batch(c, fills, src, elig, P, n, d_count);
 }
 
 // Histogram of Fuzzing-build counts over eligible projects; total and max.
@@ -399,16 +404,15 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_ext *ext_in, const fz_rq1_ou
     hipStream_t st = c->stream;
     int64_t *hist = c->arena.get<int64_t>(M + 1);
     uint8_t *flags = c->arena.get<uint8_t>(4 * P);
-    fill_batch(c, {{o->counts, FZ_RQ1_FIRST_DOWN * 8, 0},
-                   {o->counts + FZ_RQ1_FIRST_DOWN, 8, 0xff},
-                   {o->counts + FZ_RQ1_FIRST_DOWN + 1, (FZ_RQ1_NCOUNTS - FZ_RQ1_FIRST_DOWN - 1) * 8, 0},
-                   {o->iter_total, (M > 0 ? M : 1) * 8, 0},
-                   {o->iter_detected, (M > 0 ? M : 1) * 8, 0},
-                   {hist, (M + 1) * 8, 0},
-                   {flags, 4 * (P > 0 ? P : 1), 0}});
-
-    // eligibility (:144-152)
-    eligible_projects(c, o->eligible, o->counts + FZ_RQ1_ELIGIBLE);
+    // eligibility (:144-152), with the output / scratch fills in the same launch
+    eligible_projects(c, o->eligible, o->counts + FZ_RQ1_ELIGIBLE,
+                      {{o->counts, FZ_RQ1_FIRST_DOWN * 8, 0},
+                       {o->counts + FZ_RQ1_FIRST_DOWN, 8, 0xff},
+                       {o->counts + FZ_RQ1_FIRST_DOWN + 1, (FZ_RQ1_NCOUNTS - FZ_RQ1_FIRST_DOWN - 1) * 8, 0},
+                       {o->iter_total, (M > 0 ? M : 1) * 8, 0},
+                       {o->iter_detected, (M > 0 ? M : 1) * 8, 0},
+                       {hist, (M + 1) * 8, 0},
+                       {flags, 4 * (P > 0 ? P : 1), 0}});
 
     // phase 1: projects alive at each iteration (:189-203)
     if (P > 0) {

@@ -16,7 +16,7 @@ namespace fz {
 
 constexpr int64_t kLimitUs2 = 1736294400000000LL;  // '2025-01-08'
 
-void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count);
+void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count, std::initializer_list<Fill> fills = {});
 
 struct CovTrendRows {  // coverage IS NOT NULL AND coverage != 0 AND DATE(date) < LIMIT, eligible only
     static constexpr int kBytes = 21;  // column bytes read per row (filter_compact probe)
@@ -153,14 +153,13 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     const int64_t P = s.P;
     const int64_t M = s.cov.max_seg;  // longest possible trend
     const int64_t NC = s.cov.n;
-    dev_fill(c, o->counts, 0, FZ_RQ2C_NCOUNTS * 8);
-
-    eligible_projects(c, o->eligible, o->counts + FZ_RQ2C_ELIGIBLE);
+    // (the counters and raw_n zeroed in the eligibility copy's launch)
+    eligible_projects(c, o->eligible, o->counts + FZ_RQ2C_ELIGIBLE,
+                      {{o->counts, FZ_RQ2C_NCOUNTS * 8, 0}, {o->raw_n, (P > 0 ? P : 1) * 8, 0}});
     // the trend rows in one pass over the coverage view; the fetched rows per project (raw_n)
     // counted on the way instead of a first filter whose rows a second one would re-read
     int64_t *counts = o->counts;
     int64_t *raw_n = o->raw_n, *n_trend = o->n_trend;
-    dev_fill(c, raw_n, 0, (P > 0 ? P : 1) * 8);
     TmpView T;
     const CovTrendRows vrows{t.c_project, t.c_coverage, t.c_valid, t.c_date, o->eligible};
     const NonZeroTotal nzt{t.c_total, t.c_valid};
@@ -318,12 +317,12 @@ void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
     const fz_tables &t = s.t;
     const int64_t P = s.P;
     uint8_t *anyc = c->arena.get<uint8_t>(P), *anyt = c->arena.get<uint8_t>(P);
-    fill_batch(c, {{o->counts, FZ_RQ2A_NCOUNTS * 8, 0},
-                   {o->covered_is_float, P > 0 ? P : 1, 0},
-                   {o->total_is_float, P > 0 ? P : 1, 0},
-                   {anyc, P > 0 ? P : 1, 0},
-                   {anyt, P > 0 ? P : 1, 0}});
-    eligible_projects(c, o->eligible, o->counts + FZ_RQ2A_ELIGIBLE);
+    eligible_projects(c, o->eligible, o->counts + FZ_RQ2A_ELIGIBLE,
+                      {{o->counts, FZ_RQ2A_NCOUNTS * 8, 0},
+                       {o->covered_is_float, P > 0 ? P : 1, 0},
+                       {o->total_is_float, P > 0 ? P : 1, 0},
+                       {anyc, P > 0 ? P : 1, 0},
+                       {anyt, P > 0 ? P : 1, 0}});
 
     TmpView B, CV;
     filter_view(c, s.covb, s.covb.n, P,

@@ -18,7 +18,7 @@ constexpr int64_t kLim3b = 1736380800000000LL;   // '2025-01-09' (rq3:262-263)
 constexpr int64_t kDay3 = 86400000000LL;
 constexpr int64_t kGapUs = 24LL * 3600LL * 1000000LL;
 
-void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count);
+void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count, std::initializer_list<Fill> fills = {});
 
 __device__ inline int64_t fdiv_day(int64_t a) {
     const int64_t q = a / kDay3;
@@ -68,8 +68,7 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     const fz_tables &t = s.t;
     const int64_t P = s.P, NI = s.issues.n, NC = s.cov.n;
     int64_t *counts = o->counts;
-    dev_fill(c, counts, 0, FZ_RQ3_NCOUNTS * 8);
-    eligible_projects(c, o->eligible, counts + FZ_RQ3_ELIGIBLE);
+    eligible_projects(c, o->eligible, counts + FZ_RQ3_ELIGIBLE, {{counts, FZ_RQ3_NCOUNTS * 8, 0}});
 
     TmpView I, F, CB, TC;
     filter_view(c, s.issues, NI, P,

@@ -20,7 +20,7 @@ constexpr int64_t kLim4 = 1736294400000000LL;  // '2025-01-08'
 constexpr int64_t kDay4 = 86400000000LL;
 constexpr int kWin = 7;                         // ANALYSIS_ITERATIONS / DAYS_THRESHOLD (rq4a:43-46)
 
-void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count);
+void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count, std::initializer_list<Fill> fills = {});
 
 __device__ inline int64_t fdiv4(int64_t a, int64_t b) {
     const int64_t q = a / b;
@@ -71,17 +71,17 @@ void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
     int64_t *counts = o->counts;
     double *sc = o->scalars;
     int64_t *hist = c->arena.get<int64_t>(2 * (M + 1));
-    fill_batch(c, {{counts, FZ_RQ4A_NCOUNTS * 8, 0},
-                   {o->g1_total, MM * 8, 0},
-                   {o->g1_det, MM * 8, 0},
-                   {o->g2_total, MM * 8, 0},
-                   {o->g2_det, MM * 8, 0},
-                   {o->intro, (P > 0 ? P : 1) * 8, 0xff},
-                   {o->g4_steps, 30 * 8, 0},
-                   {o->g4_transition, 4 * 8, 0},
-                   {hist, 2 * (M + 1) * 8, 0}});
     int64_t *scratch = c->arena.get<int64_t>(4);
-    eligible_projects(c, o->eligible, scratch);
+    eligible_projects(c, o->eligible, scratch,
+                      {{counts, FZ_RQ4A_NCOUNTS * 8, 0},
+                       {o->g1_total, MM * 8, 0},
+                       {o->g1_det, MM * 8, 0},
+                       {o->g2_total, MM * 8, 0},
+                       {o->g2_det, MM * 8, 0},
+                       {o->intro, (P > 0 ? P : 1) * 8, 0xff},
+                       {o->g4_steps, 30 * 8, 0},
+                       {o->g4_transition, 4 * 8, 0},
+                       {hist, 2 * (M + 1) * 8, 0}});
     group_members(c, g, o->eligible, o->member, counts + FZ_RQ4A_G1, true);
     const uint8_t *member = o->member;
 
@@ -461,9 +461,8 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
     const int64_t P = s.P, M = s.cov.max_seg, NC = s.cov.n;
     const int64_t MM = M > 0 ? M : 1;
     int64_t *counts = o->counts;
-    dev_fill(c, counts, 0, FZ_RQ4B_NCOUNTS * 8);
     int64_t *scratch = c->arena.get<int64_t>(4);
-    eligible_projects(c, o->eligible, scratch);
+    eligible_projects(c, o->eligible, scratch, {{counts, FZ_RQ4B_NCOUNTS * 8, 0}});
     group_members(c, g, o->eligible, o->member, counts + FZ_RQ4B_G1, false);
     const uint8_t *member = o->member;
     const double *cov = t.c_coverage;

@@ -1058,7 +1058,16 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
 
     // the issue-number range (RQ1's ROW_NUMBER dedup key) as per-workgroup partials, read back with
     // the views' counters below (the build's one host round trip)
-    store_eligibility(c);
+    // the eligibility histogram reads only the input coverage table: on the third store-build
+    // helper beside the prologue and the prefix sorts (joined with the helpers after them, and
+    // again before the build returns)
+    const bool elig_aside = store_helpers(c) >= 3;
+    if (elig_aside) {
+        store_fork(c);
+        store_eligibility(c->helpers[2]);
+    } else {
+        store_eligibility(c);
+    }
     const int pblk = int(grid_for(t->n_issues, kBlock * 16, kProBlocks));
     int64_t *ppart = c->arena.get<int64_t>(4 * pblk);
     k_store_prologue<<<pblk, kBlock, 0, c->stream>>>(t->i_number, t->n_issues, ppart);
@@ -1193,6 +1202,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         ProbeScope::add_bytes(c, "store_gather", gather_bytes(pss, gathered));
     }
     materialize_sorted(c);
+    if (elig_aside) store_join(c);
     s.fuzz.max_seg = maxseg[0];
     s.covb.max_seg = maxseg[1];
     s.cov.max_seg = maxseg[2];

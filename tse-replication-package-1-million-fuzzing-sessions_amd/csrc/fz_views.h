@@ -151,6 +151,17 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const i
         const int64_t idx = base + i * kBlock + tid;
         r[i] = idx < lim ? int32_t(row0 + row_at(i)) : 0;
     }
+    // the output columns of every live item, loaded with the predicate's (almost every row is kept
+    // on the big tables): their latency overlaps the predicate loads instead of following the
+    // look-back as a second dependent round
+    int64_t tm[kFcItems];
+    uint32_t pj[kFcItems];
+#pragma unroll
+    for (int i = 0; i < kFcItems; ++i) {
+        const bool live = base + i * kBlock + tid < lim;
+        tm[i] = live ? times[row_at(i)] : 0;
+        pj[i] = live ? proj[row_at(i)] : 0u;
+    }
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) keep[i] = base + i * kBlock + tid < lim && pred(r[i]);
     if constexpr (Count::on) {
@@ -164,7 +175,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const i
             const bool c2 = valid && cnt(r[i]);
             const uint64_t m = __ballot(c2);
             if (!m) continue;  // (wave-uniform: nothing to count in this item - the common case)
-            const uint32_t p = valid ? proj[row_at(i)] : 0u;
+            const uint32_t p = valid ? pj[i] : 0u;
             const int first = __ffsll((long long)act) - 1;
             const uint32_t pf = __shfl(p, first, kWave);
             if (__ballot(valid && p == pf) == act) {  // the wave's rows all in one project
@@ -207,8 +218,8 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const i
         const int k = i * kBlock + tid;
         const int64_t q = pre + (s_pos[k] & 0x7fffffff);
         orow[q] = r[i];
-        otime[q] = times[row_at(i)];
-        oproj[q] = proj[row_at(i)];
+        otime[q] = tm[i];
+        oproj[q] = pj[i];
     }
 }
 
