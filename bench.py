@@ -243,11 +243,24 @@ def main():
             n_add = int(b.counts[E.RQ2A_ROWS].item())
             par.gather_rows({"project": b.row_project[:n_add], "diff_total": b.diff_total[:n_add],
                              "diff_coverage": b.diff_coverage[:n_add]}, world)
+        # the drivers' final host copies are deferred (parallel.Deferred) and made in one copy at the
+        # end of the step (par.finalize_all): the GPU is drained once, not once per driver
+        pending = []
+
+        def finalize_pending():
+            # the deferred results were produced on the drivers' streams: this stream waits for
+            # them, then one device->host copy of them all
+            cur = torch.cuda.current_stream(dev)
+            for e in {id(x): x for x in skids.values()}.values():
+                cur.wait_stream(e.stream)
+            par.finalize_all(pending)
+            pending.clear()
         shard_step = {
             "rq1": sh_rq1,
-            "rq2_count": lambda e: par.rq2_count_sharded(rq2c_shard, rank, world, *own, gather_values=False),
-            "rq4a": lambda e: par.rq4a_sharded(rq4a_shard, rank, world, *own),
-            "rq4b": lambda e: par.rq4b_sharded(rq4b_shard, rank, world),
+            "rq2_count": lambda e: pending.append(par.rq2_count_sharded(rq2c_shard, rank, world, *own,
+                                                                        gather_values=False, finish_later=True)),
+            "rq4a": lambda e: pending.append(par.rq4a_sharded(rq4a_shard, rank, world, *own, finish_later=True)),
+            "rq4b": lambda e: pending.append(par.rq4b_sharded(rq4b_shard, rank, world, finish_later=True)),
             "rq2_add": sh_rq2_add,
             "rq3": lambda e: par.rq3_sharded(rq3_shard, rank, world),
         }
@@ -359,6 +372,7 @@ def main():
         eng.build_store()
         if pool is None:
             run_sharded(snames)
+            finalize_pending()
             return
         for ch in set(skids.values()):
             if ch is not eng:
@@ -368,9 +382,13 @@ def main():
             for g, gr in sgraphs_local:
                 gr.launch()
                 mark_launched(g)
-        futs = [pool.submit(run_sharded, g) for g in sthreads]
-        for f in futs:
-            f.result()
+        if len(sthreads) == 1:  # one host thread: the drivers in order on this one
+            run_sharded(sthreads[0])
+        else:
+            futs = [pool.submit(run_sharded, g) for g in sthreads]
+            for f in futs:
+                f.result()
+        finalize_pending()
 
     # (opt-in: replaying each driver's local kernels from a recording measured no faster than the
     # eager launches - c2 3.79 vs 3.46 ms, c3 22.2 vs 21.8 ms, same box: the drivers' host work

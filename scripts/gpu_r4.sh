@@ -44,6 +44,11 @@ for s in $STEPS; do
       st=10; [ "$arg" != c2 ] && st=5
       timeout -k 10 900 python -u bench.py --config $arg --steps $st --warmup 2 > $O/${T}_cpu_$arg.json 2> $O/${T}_cpu_$arg.err || exit $?
       python3 -c "import json; d=json.loads([l for l in open('$O/${T}_cpu_$arg.json') if l.startswith('{')][-1]); print('$arg', d['ms_per_step'], d.get('cpu_baseline'), flush=True)" ;;
+    fs|fs1)  # the sharded step at world 1 (fs1: its drivers in one host thread, fixed order)
+      st=20; [ "$arg" != c2 ] && st=5
+      extra=""; [ $kind = fs1 ] && extra="--shard-groups rq3,rq4b,rq2_count,rq1,rq4a,rq2_add"
+      timeout -k 10 600 python -u bench.py --config $arg --steps $st --warmup 2 --no-cpu-baseline --probe-steps 0 --force-sharded $extra > $O/${T}_${kind}_$arg.json 2> $O/${T}_${kind}_$arg.err || exit $?
+      python3 -c "import json; d=json.loads([l for l in open('$O/${T}_${kind}_$arg.json') if l.startswith('{')][-1]); print('$kind $arg', d['ms_per_step'], d['config'].get('driver_host_ms'), flush=True)" ;;
     tests)
       k=""; [ "$arg" != tests ] && k="${arg//+/ or }"
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 500 --timeout-method thread ${k:+-k "$k"} > $O/${T}_pytest.log 2>&1; rc=$?

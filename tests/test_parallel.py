@@ -323,12 +323,12 @@ class OracleRQ4bShard(OracleRQ2CountShard):
         return out
 
 
-def _worker(rank, world, port, case, errfile, threaded=False):
+def _worker(rank, world, port, case, errfile, threaded=False, deferred=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        _check(rank, world, case, threaded)
+        _check(rank, world, case, threaded, deferred)
     except BaseException as e:  # report to the parent (mp.spawn only sees the exit code)
         with open(f"{errfile}.{rank}", "w") as f:
             import traceback
@@ -338,7 +338,7 @@ def _worker(rank, world, port, case, errfile, threaded=False):
         dist.destroy_process_group()
 
 
-def _check(rank, world, case, threaded=False):
+def _check(rank, world, case, threaded=False, deferred=False):
     from oracle import rq_oracle as orc
     from gpu_common import assert_same
     t = make_table(case, world)
@@ -359,11 +359,14 @@ def _check(rank, world, case, threaded=False):
         par.all_reduce(any_rerun)
         return counts, it, idt, rows1, any_rerun
 
+    # deferred: the drivers' final host copies left to one par.finalize_all at the end (the bench's
+    # single-thread sharded step)
     drivers = {"rq1": rq1,
                "rq3": lambda: par.rq3_sharded(OracleRQ3Shard(ts, rows), rank, world),
-               "rq2": lambda: par.rq2_count_sharded(OracleRQ2CountShard(ts), rank, world, lo, hi),
-               "rq4a": lambda: par.rq4a_sharded(OracleRQ4aShard(ts, M4), rank, world, lo, hi),
-               "rq4b": lambda: par.rq4b_sharded(OracleRQ4bShard(ts), rank, world)}
+               "rq2": lambda: par.rq2_count_sharded(OracleRQ2CountShard(ts), rank, world, lo, hi,
+                                                    finish_later=deferred),
+               "rq4a": lambda: par.rq4a_sharded(OracleRQ4aShard(ts, M4), rank, world, lo, hi, finish_later=deferred),
+               "rq4b": lambda: par.rq4b_sharded(OracleRQ4bShard(ts), rank, world, finish_later=deferred)}
     if threaded:
         # the bench's sharded step: every driver in its own thread over its own process group (their
         # collectives interleave differently on every rank)
@@ -378,6 +381,10 @@ def _check(rank, world, case, threaded=False):
             res = {k: f.result() for k, f in futs.items()}
     else:
         res = {k: f() for k, f in drivers.items()}
+    if deferred:
+        ks = list(res)
+        assert any(isinstance(res[k], par.Deferred) for k in ks)
+        res = dict(zip(ks, par.finalize_all([res[k] for k in ks])))
     counts, it, idt, rows1, any_rerun = res["rq1"]
     total3, cols3, st3 = res["rq3"]
     r2, r4, r4b = res["rq2"], res["rq4a"], res["rq4b"]
@@ -420,10 +427,10 @@ def _check(rank, world, case, threaded=False):
     assert_same(ours4b, orc.rq4b(t), "rq4b")
 
 
-def _spawn(world, case, tmp_path, threaded=False):
+def _spawn(world, case, tmp_path, threaded=False, deferred=False):
     errfile = str(tmp_path / "err")
     try:
-        mp.spawn(_worker, args=(world, _free_port(), case, errfile, threaded), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), case, errfile, threaded, deferred), nprocs=world, join=True)
     except Exception:
         msgs = [open(f"{errfile}.{r}").read() for r in range(world) if os.path.exists(f"{errfile}.{r}")]
         raise AssertionError("\n".join(msgs) or "worker failed")
@@ -453,6 +460,14 @@ def test_sharded_drivers_concurrent_groups(world, case, tmp_path):
     """The five drivers at once, one thread and one process group each (bench.py's sharded step),
     started in a different order on odd ranks: the same exact results as one after another."""
     _spawn(world, case, tmp_path, threaded=True)
+
+
+@pytest.mark.parametrize("world,case", [(2, "collide"), (3, "last_shard_no_issues")])
+def test_sharded_drivers_deferred_results(world, case, tmp_path):
+    """The drivers one after another in one thread with their final host copies deferred to one
+    finalize_all (the bench's sharded step: one collective order on every rank): the same exact
+    results."""
+    _spawn(world, case, tmp_path, deferred=True)
 
 
 def test_host_many_round_trips_dtypes():

@@ -223,6 +223,34 @@ def host_many(*ts):
     return out
 
 
+class Deferred:
+    """A driver's result whose device values are copied to the host later, together with other
+    drivers' (``finalize_all``): the sharded step then issues every driver's launches and
+    collectives from one host thread in a fixed order - the same collective order on every rank -
+    and drains the GPU once at the end instead of once per driver."""
+
+    def __init__(self, tensors, finish):
+        self.tensors, self.finish = list(tensors), finish
+
+    def result(self):
+        return self.finish(host_many(*self.tensors))
+
+
+def finalize_all(ds):
+    """The results of several Deferred (or plain values, passed through) with ONE device->host copy."""
+    pend = [d for d in ds if isinstance(d, Deferred)]
+    h = host_many(*[t for d in pend for t in d.tensors]) if pend else []
+    out, o = [], 0
+    for d in ds:
+        if isinstance(d, Deferred):
+            k = len(d.tensors)
+            out.append(d.finish(h[o:o + k]))
+            o += k
+        else:
+            out.append(d)
+    return out
+
+
 def _i64(x):
     """int64 image of a column for packing: float64 bit patterns travel unchanged."""
     import torch
@@ -395,7 +423,8 @@ def session_owners(sizes: np.ndarray, world: int) -> List[Tuple[int, int]]:
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
-def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_values: bool = True):
+def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_values: bool = True,
+                      finish_later: bool = False):
     """Exact RQ2 count over project shards (rq2_coverage_count.py:244-483).
     ``shard.run()`` -> per-project columns over the global project axis (RQ2C_PROJECT_COLS), the
     local trend values grouped by session index (project order inside a session) and their session
@@ -448,16 +477,21 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     corr = proj["corr"][elig][proj["raw_n"][elig] > 0]
     valid = corr[~np.isnan(corr)]
     corr_mm = shard.mean_median(torch.from_numpy(valid.copy()).to(dev))
-    block, tests, corr_mm = host_many(block, tests, corr_mm)  # the one result copy
-    tests, corr_mm = tuple(float(v) for v in tests), tuple(float(v) for v in corr_mm)
-    res = {"average": block[:, 0].copy(), "median": block[:, 1].copy(), "percentiles": block[:, 2:].reshape(-1).copy()}
-    out = {"proj": proj, "session_offsets": np.concatenate([[0], np.cumsum(sizes_h)]).astype(np.int64), "K": K,
-           "average": res["average"], "median": res["median"], "percentiles": res["percentiles"],
-           "tests": tests, "corr_mm": corr_mm, "null_lines": null_lines}
+    tensors = [block, tests, corr_mm]
     if gather_values:  # coverage_by_session_index.csv: every value, session-major, project order
-        gv = torch.cat(all_gather_v(vals)) if world > 1 else vals
-        out["session_values"] = gv.cpu().numpy()
-    return out
+        tensors.append(torch.cat(all_gather_v(vals)) if world > 1 else vals)
+
+    def finish(h):  # (the one result copy)
+        blk = h[0]
+        out = {"proj": proj, "session_offsets": np.concatenate([[0], np.cumsum(sizes_h)]).astype(np.int64), "K": K,
+               "average": blk[:, 0].copy(), "median": blk[:, 1].copy(), "percentiles": blk[:, 2:].reshape(-1).copy(),
+               "tests": tuple(float(v) for v in h[1]), "corr_mm": tuple(float(v) for v in h[2]),
+               "null_lines": null_lines}
+        if gather_values:
+            out["session_values"] = h[3]
+        return out
+    d = Deferred(tensors, finish)
+    return d if finish_later else d.result()
 
 
 # ----------------------------------------------------------------------------------------- RQ4a
@@ -465,7 +499,7 @@ RQ4A_MAX_ITER, RQ4A_HAS_WINDOW = 0, 6
 RQ4A_TABLES = ("g1_total", "g1_det", "g2_total", "g2_det")
 
 
-def rq4a_sharded(shard, rank: int, world: int, lo: int, hi: int):
+def rq4a_sharded(shard, rank: int, world: int, lo: int, hi: int, finish_later: bool = False):
     """Exact RQ4a over project shards (rq4a_bug.py:653-884).  ``shard.run()`` -> counts, the four
     per-iteration tables (length agreed across ranks), member / intro over the global project axis,
     g4_steps[30], g4_transition[4]; ``shard.finish(tables, intro, steps, counts)`` -> scalars (and
@@ -494,17 +528,20 @@ def rq4a_sharded(shard, rank: int, world: int, lo: int, hi: int):
         member = torch.cat([g[0] for g in got])
         intro = torch.cat([g[1] for g in got])
     sc = shard.finish(tables, intro, steps, counts)
-    h = host_many(counts, sc, member, intro, steps, trans, *tables)
-    m = int(h[0][RQ4A_MAX_ITER])
-    return {"counts": h[0], "scalars": np.asarray(h[1]), "member": h[2], "tables": [x[:m] for x in h[6:]],
-            "intro": h[3], "g4_steps": h[4], "g4_transition": h[5]}
+
+    def finish(h):
+        m = int(h[0][RQ4A_MAX_ITER])
+        return {"counts": h[0], "scalars": np.asarray(h[1]), "member": h[2], "tables": [x[:m] for x in h[6:]],
+                "intro": h[3], "g4_steps": h[4], "g4_transition": h[5]}
+    d = Deferred([counts, sc, member, intro, steps, trans, *tables], finish)
+    return d if finish_later else d.result()
 
 
 # ----------------------------------------------------------------------------------------- RQ4b
 (RQ4B_SESSIONS, RQ4B_LAST, RQ4B_DELTA_PROJECTS, RQ4B_INIT_G2, RQ4B_INIT_G1) = range(5)
 
 
-def rq4b_sharded(shard, rank: int, world: int):
+def rq4b_sharded(shard, rank: int, world: int, finish_later: bool = False):
     """Exact RQ4b over project shards (rq4b_coverage.py:1209-1261).  ``shard.run()`` -> counts,
     member[P], the G1/G2 full coverage values grouped by (session index, group) segment
     (trend_values; trend_offsets over 2 * sessions segments, G2 = group 0; project order inside a
@@ -584,20 +621,23 @@ def rq4b_sharded(shard, rank: int, world: int):
             ys.append(q[1 + k:].view(torch.float64))
         x, y = torch.cat(xs), torch.cat(ys)
     tests = shard.two_sample(x, y)
-    h = host_many(counts, last_d, sp, pre, post, med, x, y, tests, *cols)  # the one result copy
-    counts_h, last, sp, pre_h, post_h, med, x_h, y_h, tests = h[:9]
-    cols = h[9:]
-    last = int(last)
-    sp6 = np.asarray(sp, dtype=np.float64).reshape(-1) if last >= 0 else np.full(12, np.nan)
-    counts_h[RQ4B_SESSIONS] = M
-    counts_h[RQ4B_LAST] = last
-    counts_h[RQ4B_DELTA_PROJECTS] = pre_h.shape[1]
-    med = np.asarray(med, dtype=np.float64)
-    return {"counts": counts_h, "c2": cols[0], "c1": cols[1], "g2_q": np.stack(cols[2:5], 1).reshape(-1),
-            "g1_q": np.stack(cols[5:8], 1).reshape(-1), "p_bm": cols[8], "sp6": sp6,
-            "pre_cov": [pre_h[i].copy() for i in range(7)], "post_cov": [post_h[i].copy() for i in range(7)],
-            "pre_median": [float(v) for v in med[:7]], "post_median": [float(v) for v in med[7:]],
-            "init_g2": x_h, "init_g1": y_h, "tests": np.asarray(tests, dtype=np.float64)}
+
+    def finish(h):  # (the one result copy)
+        counts_h, last, sp_h, pre_h, post_h, med_h, x_h, y_h, tests_h = h[:9]
+        cols_h = h[9:]
+        last = int(last)
+        sp6 = np.asarray(sp_h, dtype=np.float64).reshape(-1) if last >= 0 else np.full(12, np.nan)
+        counts_h[RQ4B_SESSIONS] = M
+        counts_h[RQ4B_LAST] = last
+        counts_h[RQ4B_DELTA_PROJECTS] = pre_h.shape[1]
+        med_h = np.asarray(med_h, dtype=np.float64)
+        return {"counts": counts_h, "c2": cols_h[0], "c1": cols_h[1], "g2_q": np.stack(cols_h[2:5], 1).reshape(-1),
+                "g1_q": np.stack(cols_h[5:8], 1).reshape(-1), "p_bm": cols_h[8], "sp6": sp6,
+                "pre_cov": [pre_h[i].copy() for i in range(7)], "post_cov": [post_h[i].copy() for i in range(7)],
+                "pre_median": [float(v) for v in med_h[:7]], "post_median": [float(v) for v in med_h[7:]],
+                "init_g2": x_h, "init_g1": y_h, "tests": np.asarray(tests_h, dtype=np.float64)}
+    d = Deferred([counts, last_d, sp, pre, post, med, x, y, tests, *cols], finish)
+    return d if finish_later else d.result()
 
 
 # ------------------------------------------------------------------------------------ row gathers
