@@ -85,7 +85,11 @@ def parse():
     ap.add_argument("--groups", default="|".join(",".join(g) for g in GROUPS))
     # the sharded step's host threads (one child engine + process group each), same syntax; two
     # threads measured best (same-box A/B, scripts/gpu_shard_ab.sh: the drivers are host-bound)
-    ap.add_argument("--shard-groups", default="rq3,rq4b|rq2_count,rq1,rq4a,rq2_add")
+    # the sharded step's drivers per host thread ("|" between threads); default: ONE thread, the
+    # drivers in this fixed order - every rank issues its collectives in the same order (no
+    # cross-communicator ordering hazard under RCCL), and with the final host copies deferred it
+    # measured faster than two threads (c2 world 1: 2.56 vs 2.91 ms, profiles/r04_sharded_ab.txt)
+    ap.add_argument("--shard-groups", default="rq3,rq4b,rq2_count,rq1,rq4a,rq2_add")
     ap.add_argument("--shard-graphs", action="store_true")
     # the sharded step's local phases (every driver's local kernels) as recordings on the
     # single-table step's four analysis streams (--groups), launched together before the drivers,

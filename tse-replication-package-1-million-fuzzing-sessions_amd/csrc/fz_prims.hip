@@ -1108,23 +1108,9 @@ __global__ void k_describe_finish(SortedDescArgs a, const double *__restrict__ m
     describe_from_sorted(a.k[j], *a.d_n[j], ms[2 * j], ms[2 * j + 1], a.out[j]);
 }
 
-// double-double sum over a 1024-thread workgroup
 // samples of a capacity up to this are described by selection (k_describe_sel: one workgroup,
 // passes over the sample); larger ones sort their keys (radix) first
 constexpr int64_t kDescSelMax = 65536;
-__device__ inline DD block_dd_sum_1024(DD acc, double *s_hi, double *s_lo) {
-    acc = wave_dd_sum(acc);
-    if (lane_id() == 0) {
-        s_hi[wave_id()] = acc.hi;
-        s_lo[wave_id()] = acc.lo;
-    }
-    __syncthreads();
-    DD t{s_hi[0], s_lo[0]};
-    for (int i = 1; i < kSortBlock / kWave; ++i) t = dd_add(t, DD{s_hi[i], s_lo[i]});
-    __syncthreads();
-    return t;
-}
-
 struct DescSmallArgs {
     const double *x[kDescBatch];
     const int64_t *d_n[kDescBatch];
@@ -1140,7 +1126,7 @@ struct DescSmallArgs {
 // values, a 64-bit radix sort + five launches beyond).
 constexpr int kSelNB = 4096;
 constexpr int kSelMaxT = 8;
-constexpr int kSelBlock = 1024;
+constexpr int kSelBlock = 512;  // (8 waves: room for 256 VGPRs, no spills)
 struct SelShared {
     uint32_t cnt[kSelNB + 1];
     uint8_t map[kSelNB];
@@ -1350,9 +1336,23 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
 }
 
 // fz_describe of each job's sample (blockIdx.x = job), any live length
+__device__ inline DD block_dd_sum_sel(DD acc, double *s_hi, double *s_lo) {
+    acc = wave_dd_sum(acc);
+    if (lane_id() == 0) {
+        s_hi[wave_id()] = acc.hi;
+        s_lo[wave_id()] = acc.lo;
+    }
+    __syncthreads();
+    DD t{s_hi[0], s_lo[0]};
+    for (int i = 1; i < kSelBlock / kWave; ++i) t = dd_add(t, DD{s_hi[i], s_lo[i]});
+    __syncthreads();
+    return t;
+}
+constexpr int64_t kSelLds = 12288;  // samples of up to this many values are staged in LDS (96 KiB of keys)
 __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
     constexpr int NW = kSelBlock / kWave;
     __shared__ SelShared sh;
+    __shared__ uint64_t s_keys[kSelLds];
     __shared__ double s_hi[NW], s_lo[NW];
     __shared__ unsigned long long s_c[3];
     const int tid = threadIdx.x;
@@ -1368,9 +1368,12 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
     uint64_t lo = ~0ull, hi = 0ull;
     DD acc{0.0, 0.0};
     unsigned long long lt0 = 0, le0 = 0, leinf = 0;
+    // (a sample that fits is staged in LDS by this first pass: the later passes read LDS)
+    const bool staged = n <= kSelLds;
     auto ld = [=](int64_t i) { return x[i]; };
-    sel_for(n, ld, [&](int64_t, double v) {
+    sel_for(n, ld, [&](int64_t i, double v) {
         const uint64_t k = f64_key(v);
+        if (staged) s_keys[i] = k;
         acc = dd_add_d(acc, v);
         lo = k < lo ? k : lo;
         hi = k > hi ? k : hi;
@@ -1387,15 +1390,17 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
         atomicAdd(&s_c[1], le0);
         atomicAdd(&s_c[2], leinf);
     }
-    DD t = block_dd_sum_1024(acc, s_hi, s_lo);  // (its barriers order the counters too)
+    DD t = block_dd_sum_sel(acc, s_hi, s_lo);  // (its barriers order the counters too)
     const double mean = (t.hi + t.lo) / double(n);
     acc = DD{0.0, 0.0};
-    sel_for(n, ld, [&](int64_t, double v) {
+    auto sq = [&](int64_t, double v) {
         v = v - mean;
         v = v * v;
         acc = dd_add_d(acc, v);
-    });
-    t = block_dd_sum_1024(acc, s_hi, s_lo);
+    };
+    if (staged) sel_for(n, [&](int64_t i) { return f64_from_key(s_keys[i]); }, sq);
+    else sel_for(n, ld, sq);
+    t = block_dd_sum_sel(acc, s_hi, s_lo);
     const double std = sqrt((t.hi + t.lo) / double(n));
     const int64_t c_lt0 = int64_t(s_c[0]), c_le0 = int64_t(s_c[1]), c_leinf = int64_t(s_c[2]);
     // ranks: median (n / 2, and n / 2 - 1), np.percentile 25 / 75 neighbours, the smallest non-zero
@@ -1414,7 +1419,8 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
         sh.rank[6] = c_lt0 > 0 ? 0 : (c_le0 < n ? c_le0 : 0);
     }
     __syncthreads();
-    wg_select_global([=](int64_t i) { return f64_key(x[i]); }, n, lo, hi, 7, sh);
+    if (staged) wg_select_global([&](int64_t i) { return s_keys[i]; }, n, lo, hi, 7, sh);
+    else wg_select_global([=](int64_t i) { return f64_key(x[i]); }, n, lo, hi, 7, sh);
     if (tid != 0) return;
     auto get = [&](int64_t j) {
         uint64_t r = 0;
