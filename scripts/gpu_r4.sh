@@ -49,6 +49,10 @@ for s in $STEPS; do
       extra=""; [ $kind = fs1 ] && extra="--shard-groups rq3,rq4b,rq2_count,rq1,rq4a,rq2_add"
       timeout -k 10 600 python -u bench.py --config $arg --steps $st --warmup 2 --no-cpu-baseline --probe-steps 0 --force-sharded $extra > $O/${T}_${kind}_$arg.json 2> $O/${T}_${kind}_$arg.err || exit $?
       python3 -c "import json; d=json.loads([l for l in open('$O/${T}_${kind}_$arg.json') if l.startswith('{')][-1]); print('$kind $arg', d['ms_per_step'], d['config'].get('driver_host_ms'), flush=True)" ;;
+    grp)  # bench with another grouping of the analyses: grp:<cfg>@<groups> ("|" between streams)
+      cfg=${arg%%@*}; groups=${arg#*@}
+      timeout -k 10 600 python -u bench.py --config $cfg --steps 20 --warmup 2 --no-cpu-baseline --probe-steps 0 --groups "$groups" > $O/${T}_grp.json 2> $O/${T}_grp.err || exit $?
+      python3 -c "import json; d=json.loads([l for l in open('$O/${T}_grp.json') if l.startswith('{')][-1]); print('grp $cfg $groups', d['ms_per_step'], flush=True)" ;;
     tests)
       k=""; [ "$arg" != tests ] && k="${arg//+/ or }"
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 500 --timeout-method thread ${k:+-k "$k"} > $O/${T}_pytest.log 2>&1; rc=$?

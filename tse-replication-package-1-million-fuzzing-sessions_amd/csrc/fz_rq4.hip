@@ -91,15 +91,15 @@ void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
     const int64_t *fboffs = FB.offs, *fbtime = FB.time, *fioffs = FI.offs, *fitime = FI.time;
 
     // totals[i] += 1 for i = 1..#builds, per group (:339-340)
-    per_seg(c, P, [=] __device__(int64_t p) {
-        const int64_t nb = fboffs[p + 1] - fboffs[p];
-        const uint8_t b = member[p];
-        if (nb <= 0) return;
+    // (whole waves: the range is rounded up to 64 so every lane of a wave runs the wave reduction)
+    map_n(c, (P + kWave - 1) / kWave * kWave, nullptr, [=] __device__(int64_t p) {
+        const int64_t nb = p < P ? fboffs[p + 1] - fboffs[p] : 0;
+        const uint8_t b = p < P ? member[p] : 0;
         for (int k = 0; k < 2; ++k)
-            if (b & (1 << k)) {
-                atomic_add_i64(&hist[k * (M + 1) + nb], 1);
-                atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ4A_MAX_ITER]), (unsigned long long)nb);
-            }
+            if (nb > 0 && (b & (1 << k))) atomic_add_i64(&hist[k * (M + 1) + nb], 1);
+        // the longest G1 / G2 series: one atomic per wave, not one per project on one word
+        const unsigned long long mx = wave_max((unsigned long long)((nb > 0 && (b & 3)) ? nb : 0));
+        if (lane_id() == 0 && mx) atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ4A_MAX_ITER]), mx);
     });
     int64_t *rev = c->arena.get<int64_t>(MM), *rex = c->arena.get<int64_t>(MM);
     for (int k = 0; k < 2; ++k) {
@@ -129,36 +129,47 @@ void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
         if (member[p] & 2) atomic_add_i64(&g2d[k - 1], 1);
     });
 
-    // G4: introduction iteration and pre/post windows (:246-299, :350-412)
+    // G4: introduction iteration and pre/post windows (:246-299, :350-412) - one wave per project,
+    // its 2 x kWin window tests on separate lanes (each two dependent binary searches: one thread
+    // walking all fourteen in turn was a 45 us latency chain at config 2)
     const int64_t *cus = g->corpus_us;
     int64_t *intro = o->intro, *steps = o->g4_steps, *trans = o->g4_transition;
-    per_seg(c, P, [=] __device__(int64_t p) {
-        if (!(member[p] & 8) || cus[p] == FZ_TS_NULL) return;
+    static_assert(2 * kWin <= kWave, "one lane per window");
+    map_n(c, P * kWave, nullptr, [=] __device__(int64_t gi) {
+        const int64_t p = gi / kWave;
+        const int lane = int(gi % kWave);
+        if (!(member[p] & 8) || cus[p] == FZ_TS_NULL) return;  // (wave-uniform)
         const int64_t ct = cus[p];
         const int64_t lo = fboffs[p], hi = fboffs[p + 1], nb = hi - lo;
         const int64_t npre = lower_bound_i64(fbtime, lo, hi, ct) - lo;
-        intro[p] = npre;
-        if (npre > 0) atomic_add_i64(&counts[FZ_RQ4A_INTRO_POS], 1);
+        if (lane == 0) {
+            intro[p] = npre;
+            if (npre > 0) atomic_add_i64(&counts[FZ_RQ4A_INTRO_POS], 1);
+        }
         if (npre == 0) return;
         const int64_t idx = npre - 1;
         if (idx - (kWin - 1) < 0 || idx + kWin >= nb - 1) return;
-        counts[FZ_RQ4A_HAS_WINDOW] = 1;
+        if (lane == 0) counts[FZ_RQ4A_HAS_WINDOW] = 1;
         const int64_t i0 = fioffs[p], i1 = fioffs[p + 1];
-        auto any = [&](int64_t a, int64_t b) {  // some issue T with a <= T < b
-            return lower_bound_i64(fitime, i0, i1, b) > lower_bound_i64(fitime, i0, i1, a);
-        };
-        bool pre = false, post = false;
-        for (int k = 1; k <= kWin; ++k) {
-            const bool d1 = any(fbtime[lo + idx - (k - 1)], fbtime[lo + idx - (k - 1) + 1]);
-            atomic_add_i64(&steps[2 * (kWin - k)], 1);
-            if (d1) atomic_add_i64(&steps[2 * (kWin - k) + 1], 1);
-            pre |= d1;
-            const bool d2 = any(fbtime[lo + idx + k], fbtime[lo + idx + k + 1]);
-            atomic_add_i64(&steps[2 * (kWin + k)], 1);
-            if (d2) atomic_add_i64(&steps[2 * (kWin + k) + 1], 1);
-            post |= d2;
+        // lane k - 1 (k = 1..kWin): Pre-k = [t[idx-k+1], t[idx-k+2]); lane kWin + k - 1: Post-k
+        bool det = false;
+        int slot = -1;
+        if (lane < 2 * kWin) {
+            const bool is_pre = lane < kWin;
+            const int k = is_pre ? lane + 1 : lane - kWin + 1;
+            const int64_t a = is_pre ? fbtime[lo + idx - (k - 1)] : fbtime[lo + idx + k];
+            const int64_t b = is_pre ? fbtime[lo + idx - (k - 1) + 1] : fbtime[lo + idx + k + 1];
+            det = lower_bound_i64(fitime, i0, i1, b) > lower_bound_i64(fitime, i0, i1, a);  // an issue in [a, b)
+            slot = is_pre ? kWin - k : kWin + k;
+            atomic_add_i64(&steps[2 * slot], 1);
+            if (det) atomic_add_i64(&steps[2 * slot + 1], 1);
         }
-        atomic_add_i64(&trans[(pre && post) ? 0 : pre ? 1 : post ? 2 : 3], 1);
+        const uint64_t m = __ballot(det);
+        if (lane == 0) {
+            const bool pre = (m & ((1ull << kWin) - 1ull)) != 0ull;
+            const bool post = ((m >> kWin) & ((1ull << kWin) - 1ull)) != 0ull;
+            atomic_add_i64(&trans[(pre && post) ? 0 : pre ? 1 : post ? 2 : 3], 1);
+        }
     });
     rq4a_finish(c, M, P, o->g1_total, o->g1_det, o->g2_total, o->g2_det, o->intro, o->g4_steps, counts, sc);
 }
