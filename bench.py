@@ -37,7 +37,7 @@ PROBE_KERNEL = "radix_scatter"   # headline kernel of the roofline object (DESIG
 # per launch as DESIGN.md 4 defines them)
 TABLE_KERNELS = ["radix_scatter", "radix_hist", "elig_hist", "seg_time_sort", "store_gather", "big_compact",
                  "big_sub_sort", "seg_merge_sort", "filter_compact", "filter_select", "seg_reduce", "seg_spearman", "seg_rank_union", "seg_value_sort", "seg_qstats",
-                 "ragged_transpose", "scan_i64"]
+                 "ragged_transpose", "scan_i64", "describe_select", "spearman_shapiro"]
 STAGES = ["store", "rq1", "rq2_count", "rq2_add", "rq3", "rq4a", "rq4b"]
 # analyses run concurrently after the store build: the first groups on child streams, the last on
 # the engine's own stream after the store build (about equal GPU time at config 2: rq3 0.94 ms,

@@ -37,7 +37,7 @@ for s in $STEPS; do
       timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VALU --output-format csv -d $O/${T}_sq_$arg -o run -- python3 -u bench.py --config $arg --steps 2 --warmup 1 --no-cpu-baseline --probe-steps 0 --serial > $O/${T}_sq_$arg.log 2>&1 || exit $?
       python3 scripts/pmc_sq.py $(find $O/${T}_sq_$arg -name "*counter_collection.csv" | head -1) $O/${T}_${arg}_sq.json ;;
     strong)
-      CONFIG=$arg timeout -k 10 1100 bash scripts/gpu_strong_rehearsal.sh > $O/${T}_strong_$arg.txt 2>&1 || exit $?; cat $O/${T}_strong_$arg.txt ;;
+      CONFIG=${arg%%@*} RANKS=$([ "${arg#*@}" != "$arg" ] && echo all) timeout -k 10 1100 bash scripts/gpu_strong_rehearsal.sh > $O/${T}_strong_$arg.txt 2>&1 || exit $?; cat $O/${T}_strong_$arg.txt ;;
     e2e)
       timeout -k 10 900 python -u scripts/e2e_suite.py --config $arg --no-figures > $O/${T}_e2e_$arg.json 2> $O/${T}_e2e_$arg.err || exit $?; tail -1 $O/${T}_e2e_$arg.json ;;
     cpu)  # bench line with the multi-core C++ CPU baseline

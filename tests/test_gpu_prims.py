@@ -42,3 +42,39 @@ def test_describe_matches_numpy(engine, n, seed):
     d = engine.describe(torch.from_numpy(a).to(engine.dev))
     ours = {k: getattr(d, k) for k in _np_describe(a)}
     assert_same(ours, _np_describe(a))
+
+
+def _gen(kind, n, rng):
+    if kind == "ints":       # RQ3's total-line differences: few hundred distinct integers, heavy ties
+        return np.round(rng.normal(0, 60, size=n)).astype(np.float64)
+    if kind == "const":
+        return np.full(n, 3.25)
+    if kind == "twovals":
+        return np.where(rng.random(n) < 0.5, -1.0, 7.0)
+    if kind == "wide":       # magnitudes from 1e-300 to 1e300 (key buckets span whole binades)
+        return rng.choice([-1.0, 1.0], n) * 10.0 ** rng.uniform(-300, 300, n)
+    if kind == "cluster":    # one dense cluster plus far outliers (re-histogrammed intervals)
+        a = 1.0 + rng.normal(0, 1e-12, n)
+        a[: max(1, n // 50)] = rng.uniform(-1e6, 1e6, max(1, n // 50))
+        return a
+    if kind == "pos":        # no negatives, zeros: the smallest non-zero value is not the minimum
+        a = np.round(rng.exponential(5, n), 1)
+        return a
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["ints", "const", "twovals", "wide", "cluster", "pos"])
+@pytest.mark.parametrize("n", [63, 9022, 12288, 12289, 65536])
+def test_describe_selection_shapes(engine, kind, n):
+    """k_describe_sel's selection paths: samples staged in LDS (<= 12288) or re-read, key buckets
+    holding one value (ties), narrowed intervals of several targets at once, the smallest non-zero."""
+    torch = engine.torch
+    rng = np.random.default_rng(n + len(kind))
+    a = _gen(kind, n, rng)
+    d = engine.describe(torch.from_numpy(a).to(engine.dev))
+    ours = {k: getattr(d, k) for k in _np_describe(a)}
+    assert_same(ours, _np_describe(a))
+    nz = a[a != 0]
+    assert bool(d.has_nonzero) == (len(nz) > 0)
+    if len(nz):
+        assert d.min_nonzero == nz.min()

@@ -1136,6 +1136,14 @@ struct SelShared {
     uint32_t tmp[kSelBlock / kWave];
     int64_t rank[kSelMaxT], tb[kSelMaxT], toff[kSelMaxT], tsz[kSelMaxT];
     int tslot[kSelMaxT];
+    int twide[kSelMaxT];                      // wide target t: its wide-bucket slot
+    unsigned long long wlo[kSelMaxT], whi[kSelMaxT];  // key range of each distinct wide bucket
+    int nwide;
+    // wide target t's state while narrowing: key interval [wl, wh], rank in it, count, sub-bucket
+    unsigned long long wl[kSelMaxT], wh[kSelMaxT];
+    int64_t wr[kSelMaxT], wc[kSelMaxT];
+    uint32_t wsb[kSelMaxT];
+    int wact[kSelMaxT];
     uint64_t res[kSelMaxT];
     int64_t r, rc;
     uint32_t sb;
@@ -1168,18 +1176,18 @@ __device__ inline uint32_t sel_bucket(uint64_t k, uint64_t lo, double sc, int nb
 // of kSelU consecutive items issued before their bodies (one memory latency per kSelU items, not
 // one per item)
 constexpr int kSelU = 8;
-template <typename Load, typename Body>
+template <int U = kSelU, typename Load, typename Body>
 __device__ inline void sel_for(int64_t n, const Load &load, const Body &body) {
     using T = decltype(load(int64_t(0)));
-    for (int64_t i0 = threadIdx.x; i0 < n; i0 += int64_t(kSelBlock) * kSelU) {
-        T v[kSelU];
+    for (int64_t i0 = threadIdx.x; i0 < n; i0 += int64_t(kSelBlock) * U) {
+        T v[U];
 #pragma unroll
-        for (int u = 0; u < kSelU; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int64_t i = i0 + int64_t(u) * kSelBlock;
             v[u] = i < n ? load(i) : T{};
         }
 #pragma unroll
-        for (int u = 0; u < kSelU; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int64_t i = i0 + int64_t(u) * kSelBlock;
             if (i < n) body(i, v[u]);
         }
@@ -1231,27 +1239,64 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
         sh.tsz[tid] = int64_t(sh.cnt[l0 + 1]) - int64_t(sh.cnt[l0]);
     }
     __syncthreads();
-    if (tid == 0) {
-        int used = 0;
+    if (tid == 0) {  // list slots of the narrow buckets (map 0..), slots of the distinct wide ones (0x80 | w)
+        int used = 0, wide = 0;
         for (int t = 0; t < nt; ++t) {
-            int slot = -1;
-            if (sh.tsz[t] <= 64) {
-                for (int u = 0; u < t; ++u)
-                    if (sh.tslot[u] >= 0 && sh.tb[u] == sh.tb[t]) slot = sh.tslot[u];
-                if (slot < 0) {
+            int slot = -1, ws = -1;
+            for (int u = 0; u < t; ++u)
+                if (sh.tb[u] == sh.tb[t]) {
+                    slot = sh.tslot[u];
+                    ws = sh.twide[u];
+                }
+            if (slot < 0 && ws < 0) {
+                if (sh.tsz[t] <= 64) {
                     slot = used++;
                     sh.fill[slot] = 0u;
                     sh.map[sh.tb[t]] = uint8_t(slot);
+                } else {
+                    ws = wide++;
+                    sh.wlo[ws] = ~0ull;
+                    sh.whi[ws] = 0ull;
+                    sh.map[sh.tb[t]] = uint8_t(0x80 | ws);
                 }
             }
             sh.tslot[t] = slot;
+            sh.twide[t] = ws;
         }
+        sh.nwide = wide;
     }
     __syncthreads();
-    sel_for(n, key, [&](int64_t, uint64_t k) {
+    // one pass: the narrow buckets' keys gathered, the wide buckets' key ranges (a wide bucket of
+    // one key - ties - needs nothing more)
+    const int nwide = sh.nwide;
+    uint64_t wlo[kSelMaxT], whi[kSelMaxT];
+#pragma unroll
+    for (int q = 0; q < kSelMaxT; ++q) {
+        wlo[q] = ~0ull;
+        whi[q] = 0ull;
+    }
+    sel_for<4>(n, key, [&](int64_t, uint64_t k) {
         const uint8_t slot = sh.map[sel_bucket(k, lo, sc, nb)];
-        if (slot != 0xff) sh.list[slot][atomicAdd(&sh.fill[slot], 1u)] = k;
+        if (slot < 0x80) {
+            sh.list[slot][atomicAdd(&sh.fill[slot], 1u)] = k;
+        } else if (slot != 0xff) {
+#pragma unroll
+            for (int q = 0; q < kSelMaxT; ++q)
+                if ((slot & 0x7f) == q) {
+                    wlo[q] = k < wlo[q] ? k : wlo[q];
+                    whi[q] = k > whi[q] ? k : whi[q];
+                }
+        }
     });
+#pragma unroll
+    for (int q = 0; q < kSelMaxT; ++q) {
+        if (q >= nwide) break;  // (uniform)
+        const uint64_t a = wave_min(wlo[q]), b = wave_max(whi[q]);
+        if (lane == 0) {
+            atomicMin(&sh.wlo[q], (unsigned long long)a);
+            atomicMax(&sh.whi[q], (unsigned long long)b);
+        }
+    }
     __syncthreads();
     auto rank_list = [&](int slot, int sz, int64_t want, int t) {  // one wave
         const uint64_t e = lane < sz ? sh.list[slot][lane] : ~0ull;
@@ -1265,74 +1310,118 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
     for (int t = w; t < nt; t += NW)
         if (sh.tslot[t] >= 0) rank_list(sh.tslot[t], int(sh.tsz[t]), sh.toff[t], t);
     __syncthreads();
-    for (int t = 0; t < nt; ++t) {  // wide buckets: narrow the key interval (uniform control flow)
-        if (sh.tslot[t] >= 0) continue;
-        const uint32_t tb = uint32_t(sh.tb[t]);
-        uint64_t rlo = ~0ull, rhi = 0ull;
-        sel_for(n, key, [&](int64_t, uint64_t k) {
-            if (sel_bucket(k, lo, sc, nb) == tb) {
-                rlo = k < rlo ? k : rlo;
-                rhi = k > rhi ? k : rhi;
-            }
-        });
-        sel_minmax(rlo, rhi, sh);
-        int64_t r = sh.toff[t], cnt = sh.tsz[t];
-        while (rlo != rhi && cnt > 64) {
-            const int nb2 = cnt < kSelNB ? int(cnt) : kSelNB;
-            const double sc2 = double(nb2) / (double(rhi - rlo) + 1.0);
-            for (int j = tid; j <= nb2; j += BS) sh.cnt[j] = 0u;
-            __syncthreads();
-            sel_for(n, key, [&](int64_t, uint64_t k) {
-                if (k >= rlo && k <= rhi) atomicAdd(&sh.cnt[sel_bucket(k, rlo, sc2, nb2)], 1u);
-            });
-            __syncthreads();
-            if (w == 0) {  // the sub-bucket holding rank r
-                int64_t base = 0;
-                for (int c0 = 0; c0 < nb2; c0 += 64) {
-                    const int j = c0 + lane;
-                    const int64_t cj = j < nb2 ? int64_t(sh.cnt[j]) : 0;
-                    const int64_t incl = base + wave_incl_scan(cj);
-                    const uint64_t hit = __ballot(j < nb2 && incl > r);
-                    if (hit) {
-                        const int l = __ffsll((unsigned long long)hit) - 1;
-                        if (lane == l) {
-                            sh.r = r - (incl - cj);
-                            sh.rc = cj;
-                            sh.sb = uint32_t(j);
-                        }
-                        break;
-                    }
-                    base = __shfl(incl, 63, 64);
-                }
-            }
-            __syncthreads();
-            const uint32_t sb = sh.sb;
-            uint64_t nlo = ~0ull, nhi = 0ull;
-            sel_for(n, key, [&](int64_t, uint64_t k) {
-                if (k >= rlo && k <= rhi && sel_bucket(k, rlo, sc2, nb2) == sb) {
-                    nlo = k < nlo ? k : nlo;
-                    nhi = k > nhi ? k : nhi;
-                }
-            });
-            r = sh.r;
-            cnt = sh.rc;
-            sel_minmax(nlo, nhi, sh);
-            rlo = nlo;
-            rhi = nhi;
+    // wide buckets: every wide target's key interval narrowed in the same passes - per round one
+    // histogram pass (target t's sub-buckets in its own slice of sh.cnt) and one min / max pass over
+    // the sub-bucket holding its rank - until it holds one key or <= 64 values; then one gather of
+    // all the narrow intervals (uniform control flow: the target state is in LDS)
+    constexpr int kSlice = kSelNB / kSelMaxT;
+    if (tid < nt) {
+        const bool wide = sh.tslot[tid] < 0;
+        sh.wr[tid] = sh.toff[tid];
+        sh.wc[tid] = wide ? sh.tsz[tid] : 0;
+        sh.wl[tid] = wide ? sh.wlo[sh.twide[tid]] : 1ull;
+        sh.wh[tid] = wide ? sh.whi[sh.twide[tid]] : 0ull;  // (lo > hi: no key matches)
+    }
+    __syncthreads();
+    auto uni64 = [](uint64_t x) {  // (wave-uniform value -> scalar registers)
+        const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(x)), h = __builtin_amdgcn_readfirstlane(uint32_t(x >> 32));
+        return (uint64_t(h) << 32) | l;
+    };
+    for (;;) {
+        uint64_t al[kSelMaxT], ah[kSelMaxT];
+        double asc[kSelMaxT];
+        int anb[kSelMaxT];
+        bool any = false;
+#pragma unroll
+        for (int t = 0; t < kSelMaxT; ++t) {
+            const bool act = __builtin_amdgcn_readfirstlane(t < nt && sh.wl[t] != sh.wh[t] && sh.wc[t] > 64);
+            any |= act;
+            al[t] = act ? uni64(sh.wl[t]) : 1ull;
+            ah[t] = act ? uni64(sh.wh[t]) : 0ull;
+            anb[t] = act ? __builtin_amdgcn_readfirstlane(sh.wc[t] < kSlice ? int(sh.wc[t]) : kSlice) : 1;
+            asc[t] = act ? __builtin_bit_cast(double, uni64(__builtin_bit_cast(uint64_t, double(anb[t]) / (double(ah[t] - al[t]) + 1.0)))) : 0.0;
         }
-        if (rlo == rhi) {
-            if (tid == 0) sh.res[t] = rlo;
-        } else {  // <= 64 values in [rlo, rhi]
-            if (tid == 0) sh.fill[0] = 0u;
-            __syncthreads();
-            sel_for(n, key, [&](int64_t, uint64_t k) {
-                if (k >= rlo && k <= rhi) sh.list[0][atomicAdd(&sh.fill[0], 1u)] = k;
-            });
-            __syncthreads();
-            if (w == 0) rank_list(0, int(cnt), r, t);
+        if (!any) break;  // (uniform)
+        if (tid < kSelMaxT) sh.wact[tid] = tid < nt && sh.wl[tid] != sh.wh[tid] && sh.wc[tid] > 64;
+        for (int j = tid; j < kSelNB; j += BS) sh.cnt[j] = 0u;
+        __syncthreads();
+        sel_for<4>(n, key, [&](int64_t, uint64_t k) {
+#pragma unroll
+            for (int t = 0; t < kSelMaxT; ++t)
+                if (k >= al[t] && k <= ah[t]) atomicAdd(&sh.cnt[t * kSlice + sel_bucket(k, al[t], asc[t], anb[t])], 1u);
+        });
+        __syncthreads();
+        if (w < kSelMaxT && sh.wact[w]) {  // wave w: the sub-bucket holding target w's rank
+            const int64_t r = sh.wr[w];
+            const int nb2 = sh.wc[w] < kSlice ? int(sh.wc[w]) : kSlice;
+            int64_t base = 0;
+            for (int c0 = 0; c0 < nb2; c0 += 64) {
+                const int j = c0 + lane;
+                const int64_t cj = j < nb2 ? int64_t(sh.cnt[w * kSlice + j]) : 0;
+                const int64_t incl = base + wave_incl_scan(cj);
+                const uint64_t hit = __ballot(j < nb2 && incl > r);
+                if (hit) {
+                    const int l = __ffsll((unsigned long long)hit) - 1;
+                    if (lane == l) {
+                        sh.wr[w] = r - (incl - cj);
+                        sh.wc[w] = cj;
+                        sh.wsb[w] = uint32_t(j);
+                        sh.wlo[w] = ~0ull;
+                        sh.whi[w] = 0ull;
+                    }
+                    break;
+                }
+                base = __shfl(incl, 63, 64);
+            }
+        }
+        __syncthreads();
+        uint32_t asb[kSelMaxT];
+#pragma unroll
+        for (int t = 0; t < kSelMaxT; ++t) asb[t] = al[t] <= ah[t] ? __builtin_amdgcn_readfirstlane(sh.wsb[t]) : 0u;
+        // (a sub-bucket holds few keys - about wc / kSlice: LDS atomics on its bounds, no registers)
+        sel_for<4>(n, key, [&](int64_t, uint64_t k) {
+#pragma unroll
+            for (int t = 0; t < kSelMaxT; ++t)
+                if (k >= al[t] && k <= ah[t] && sel_bucket(k, al[t], asc[t], anb[t]) == asb[t]) {
+                    atomicMin(&sh.wlo[t], (unsigned long long)k);
+                    atomicMax(&sh.whi[t], (unsigned long long)k);
+                }
+        });
+        __syncthreads();
+        if (tid < kSelMaxT && sh.wact[tid]) {
+            sh.wl[tid] = sh.wlo[tid];
+            sh.wh[tid] = sh.whi[tid];
         }
         __syncthreads();
     }
+    // one key left (ties): the result; else <= 64 values in [wl, wh]: one gather for all, ranked
+    bool gather = false;
+    uint64_t gl[kSelMaxT], gh[kSelMaxT];
+#pragma unroll
+    for (int t = 0; t < kSelMaxT; ++t) {
+        const bool wide = t < nt && sh.tslot[t] < 0;
+        const bool g = __builtin_amdgcn_readfirstlane(wide && sh.wl[t] != sh.wh[t]);
+        gather |= g;
+        gl[t] = g ? uni64(sh.wl[t]) : 1ull;
+        gh[t] = g ? uni64(sh.wh[t]) : 0ull;
+    }
+    if (tid < nt && sh.tslot[tid] < 0) {
+        if (sh.wl[tid] == sh.wh[tid]) sh.res[tid] = sh.wl[tid];
+        sh.fill[tid] = 0u;
+    }
+    if (!gather) {  // (uniform)
+        __syncthreads();
+        return;
+    }
+    __syncthreads();
+    sel_for<4>(n, key, [&](int64_t, uint64_t k) {
+#pragma unroll
+        for (int t = 0; t < kSelMaxT; ++t)
+            if (k >= gl[t] && k <= gh[t]) sh.list[t][atomicAdd(&sh.fill[t], 1u)] = k;
+    });
+    __syncthreads();
+    if (w < nt && sh.tslot[w] < 0 && sh.wl[w] != sh.wh[w]) rank_list(w, int(sh.wc[w]), sh.wr[w], w);
+    __syncthreads();
 }
 
 // fz_describe of each job's sample (blockIdx.x = job), any live length
@@ -1483,6 +1572,8 @@ void describe_f64_dn_batch(fz_ctx *c, const DescJob *jobs, int njobs) {
         }
     }
     if (ns > 0) {  // every such job in one launch
+        // (algorithmic bytes: one read of the first job's live values)
+        ProbeScope ps(c, "describe_select", 0.0, a.d_n[0], 8.0);
         k_describe_sel<<<ns, kSelBlock, 0, c->stream>>>(a);
         FZ_LAUNCH_CHECK();
     }

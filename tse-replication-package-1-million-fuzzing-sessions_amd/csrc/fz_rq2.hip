@@ -79,8 +79,7 @@ void series_tests(fz_ctx *c, const double *x, int64_t n_cap, const int64_t *d_n,
     ChunkedSegs cs3 = chunked(c, one);
     int32_t *sg3 = segment_ids(c, one);
     SortedSegs ss3 = seg_sort_f64(c, x, one, sg3);
-    spearman_index_sorted(c, cs3, sg3, ss3, out, out + 1);
-    seg_shapiro(c, cs3, x, ss3, out + 2, out + 3);
+    spearman_shapiro_sorted(c, cs3, sg3, ss3, x, out, out + 1, out + 2, out + 3);
 }
 
 void spearman_index_seg(fz_ctx *c, const double *x, int64_t n, const int64_t *offs, int64_t S, int64_t max_len,
@@ -197,8 +196,7 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     ChunkedSegs cs = chunked(c, sp);
     const int32_t *segid = reinterpret_cast<const int32_t *>(T.proj);
     SortedSegs ss = seg_sort_f64(c, tv, sp, segid);
-    spearman_index_sorted(c, cs, segid, ss, o->corr, nullptr);
-    seg_shapiro(c, cs, tv, ss, o->sw_w, o->sw_p);
+    spearman_shapiro_sorted(c, cs, segid, ss, tv, o->corr, nullptr, o->sw_w, o->sw_p);
 
     // coverage_by_session_index (:329-333): session i = value i of every project longer than i, in
     // project order - the ragged transpose (fz_transpose.h) moves each value straight to its slot

@@ -354,6 +354,10 @@ void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, 
 // scipy.stats.shapiro per segment (src in original order, ss its sorted image) -> W[S], p[S]
 // (NaN where n < 3).
 void seg_shapiro(fz_ctx *c, const ChunkedSegs &cs, const double *src, const SortedSegs &ss, double *w, double *p);
+// spearman_index_sorted (rho, pval; rho null: none) and seg_shapiro of the same sorted segments -
+// one launch, one workgroup per segment, when no segment is longer than kSpearmanSmall values
+void spearman_shapiro_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const SortedSegs &ss,
+                             const double *src, double *rho, double *pval, double *w, double *p);
 // numpy.percentile(seg, q[j]) for sorted segments -> out[s * nq + j] (NaN for empty segments).
 // (median != null: statistics.median of every segment too, as seg_median, in the same launch)
 void seg_percentiles(fz_ctx *c, const Segs &sg, const double *sorted, const double *q_host, int nq, double *out,

@@ -1145,17 +1145,118 @@ void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, 
 // directly - the same exact half-integer sums as seg_spearman_index, without the device-wide tie
 // rank passes.
 constexpr int64_t kSpearmanSmall = 4096;  // <= 16 values per thread: longer runs are latency chains
+constexpr int kSmallPer = int(kSpearmanSmall / kBlock);
+
+// Double-double sums of NV per-thread partials over the workgroup (kBlock threads), the rounded
+// results in every thread.
+template <int NV>
+__device__ inline void block_dd_sums(const DD (&acc)[NV], double (&s_hi)[4][NV], double (&s_lo)[4][NV],
+                                     double (&out)[NV]) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const DD r = wave_dd_sum(acc[v]);
+        if (lane_id() == 0) {
+            s_hi[wave_id()][v] = r.hi;
+            s_lo[wave_id()][v] = r.lo;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        DD t{s_hi[0][v], s_lo[0][v]};
+        for (int w = 1; w < 4; ++w) t = dd_add(t, DD{s_hi[w][v], s_lo[w][v]});
+        out[v] = t.hi + t.lo;
+    }
+    __syncthreads();
+}
+
+// scipy.stats.shapiro (swilk.c) of one sorted segment v[b, b + n) (src: the same values in input
+// order, for y -= x[N // 2]) by the workgroup, each thread over its run [k0, k1) of <= kSmallPer
+// values: the passes of seg_shapiro (sum of m_i^2, then sx / sa, then ssa / ssx / sax), every sum
+// double-double as there; a thread's coefficients stay in registers between the last two passes.
+__device__ inline void shapiro_block(const double *__restrict__ v, const double *__restrict__ src, int64_t b,
+                                     int64_t n, int64_t k0, int64_t k1, double (&s_hi)[4][3],
+                                     double (&s_lo)[4][3], double *w_out, double *p_out) {
+    DD a0[1] = {{0.0, 0.0}};
+    if (n >= 3)
+        for (int64_t k = 1 + threadIdx.x; k <= n / 2; k += kBlock) {
+            const double m = stats::sw_m(k, n);
+            a0[0] = dd_add_d(a0[0], m * m);
+        }
+    double summ2[1];
+    block_dd_sums<1>(a0, reinterpret_cast<double(&)[4][1]>(s_hi), reinterpret_cast<double(&)[4][1]>(s_lo), summ2);
+    if (n < 3) {
+        if (threadIdx.x == 0) {
+            *w_out = NAN;
+            *p_out = NAN;
+        }
+        return;
+    }
+    const stats::SwCoef cf = stats::sw_coef(n, 2.0 * summ2[0]);
+    const double x0 = src[b + n / 2];
+    const double range = (v[b + n - 1] - x0) - (v[b] - x0);
+    double co[kSmallPer], y[kSmallPer];
+    DD a1[2] = {{0.0, 0.0}, {0.0, 0.0}};
+#pragma unroll
+    for (int u = 0; u < kSmallPer; ++u) {
+        const int64_t j = k0 + u;
+        co[u] = y[u] = 0.0;
+        if (j < k1) {
+            y[u] = (v[j] - x0) / range;
+            co[u] = stats::sw_coef_at(cf, j - b + 1);
+            a1[0] = dd_add_d(a1[0], y[u]);
+            a1[1] = dd_add_d(a1[1], co[u]);
+        }
+    }
+    double s1[2];
+    block_dd_sums<2>(a1, reinterpret_cast<double(&)[4][2]>(s_hi), reinterpret_cast<double(&)[4][2]>(s_lo), s1);
+    const double sx = s1[0] / double(n), sa = s1[1] / double(n);
+    DD a2[3] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+#pragma unroll
+    for (int u = 0; u < kSmallPer; ++u) {
+        if (k0 + u < k1) {
+            const double asa = co[u] - sa, xsx = y[u] - sx;
+            a2[0] = dd_add_d(a2[0], asa * asa);
+            a2[1] = dd_add_d(a2[1], xsx * xsx);
+            a2[2] = dd_add_d(a2[2], asa * xsx);
+        }
+    }
+    double s2[3];
+    block_dd_sums<3>(a2, s_hi, s_lo, s2);
+    if (threadIdx.x == 0) {
+        if (range < stats::kSwSmall) {  // zero range: scipy returns (1.0, 1.0)
+            *w_out = 1.0;
+            *p_out = 1.0;
+            return;
+        }
+        const double ssa = s2[0], ssx = s2[1], sax = s2[2];
+        const double ssassx = sqrt(ssa * ssx);
+        const double w1 = (ssassx - sax) * (ssassx + sax) / (ssa * ssx);
+        const double ww = 1.0 - w1;
+        *w_out = ww;
+        *p_out = stats::sw_pvalue(n, ww, w1);
+    }
+}
+
+// (sw_w non-null: Shapiro-Wilk of every segment too, from the same workgroup's pass; rho null:
+// Shapiro-Wilk only)
 __global__ __launch_bounds__(kBlock) void k_spearman_index_small(const double *__restrict__ sv,
                                                                  const int32_t *__restrict__ pos,
                                                                  const int64_t *__restrict__ offs, int64_t S,
-                                                                 double *__restrict__ rho, double *__restrict__ pval) {
+                                                                 double *__restrict__ rho, double *__restrict__ pval,
+                                                                 const double *__restrict__ src = nullptr,
+                                                                 double *__restrict__ sw_w = nullptr,
+                                                                 double *__restrict__ sw_p = nullptr) {
     __shared__ double s_tmp[4];
+    __shared__ double s_hi[4][3], s_lo[4][3];
     for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
         const int64_t b = offs[s], n = offs[s + 1] - b;
         const double m = double(n + 1) / 2.0;
         double sxy = 0.0, sxx = 0.0, syy = 0.0, ng = 0.0;
         const int64_t per = (n + kBlock - 1) / kBlock;
         const int64_t k0 = b + int64_t(threadIdx.x) * per, k1 = k0 + per < b + n ? k0 + per : b + n;
+        if (sw_w) shapiro_block(sv, src, b, n, k0, k1, s_hi, s_lo, sw_w + s, sw_p + s);
+        if (!rho) continue;
         if (k0 < k1) {
             double v = sv[k0];
             int64_t gs = lower_bound_d(sv, b, k0 + 1, v), ge = upper_bound_d(sv, k0, b + n, v);
@@ -1502,6 +1603,22 @@ void bm_union_sorted(fz_ctx *c, const Segs &one, const double *sorted, const int
         if (bm_stat) *bm_stat = w;
         if (bm_p) *bm_p = 2.0 * stats::t_sf(fabs(w), num / den);
     });
+}
+
+void spearman_shapiro_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const SortedSegs &ss,
+                             const double *src, double *rho, double *pval, double *w, double *p) {
+    const Segs &sg = cs.sg;
+    if (sg.S <= 0) return;
+    if (sg.len_bound() <= kSpearmanSmall) {  // both in one launch, one workgroup per segment
+        // algorithmic bytes per live value: sorted value 8 + position 4 + input value 8 read
+        ProbeScope ps(c, "spearman_shapiro", 0.0, sg.offs + sg.S, 20.0);
+        k_spearman_index_small<<<unsigned(sg.S < 16384 ? sg.S : 16384), kBlock, 0, c->stream>>>(
+            ss.val, ss.pos, sg.offs, sg.S, rho, pval, src, w, p);
+        FZ_LAUNCH_CHECK();
+        return;
+    }
+    if (rho) spearman_index_sorted(c, cs, segid, ss, rho, pval);
+    seg_shapiro(c, cs, src, ss, w, p);
 }
 
 void spearman_index_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const SortedSegs &ss, double *rho,

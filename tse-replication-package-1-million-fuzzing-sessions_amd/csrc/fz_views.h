@@ -32,7 +32,10 @@ void segment_offsets_dn(fz_ctx *c, const uint32_t *sorted_proj, const int64_t *d
 // Single-pass order-preserving compaction of a view: each 4096-row tile evaluates pred, ranks its
 // kept rows in LDS, gets its output base by decoupled look-back over the preceding tiles, and
 // writes (row, time, proj) of the kept rows; the last tile writes the count.  One launch instead of
-// flag -> device-wide scan -> compact.
+// flag -> device-wide scan -> compact.  The output's segment offsets [P + 1] come from the same
+// pass: the view is project-ordered, so project q's output segment starts at the kept count before
+// q's first input row - written by the item holding that row (the projects between its
+// predecessor's and its own: empty ones too), the ones past the last live row by the last tile.
 #ifndef FZ_FC_ITEMS
 #define FZ_FC_ITEMS 16
 #endif
@@ -91,9 +94,11 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const i
                                                            const int64_t *__restrict__ d_live, Pred pred, Lookback lb,
                                                            int64_t ntiles, int32_t *__restrict__ orow,
                                                            int64_t *__restrict__ otime, uint32_t *__restrict__ oproj,
-                                                           int64_t *__restrict__ d_n, Selection sel,
-                                                           Count cnt = Count{}) {
+                                                           int64_t *__restrict__ d_n, int64_t *__restrict__ oofs,
+                                                           int64_t P, Selection sel, Count cnt = Count{}) {
     __shared__ int32_t s_pos[kFcTile];
+    __shared__ uint32_t s_pj[kFcTile];  // the items' projects (their predecessors' for the offsets)
+    __shared__ int64_t s_pprev, s_plast;  // project of the row before the tile / of the last live row
     __shared__ int32_t s_tmp[4];
     __shared__ int64_t s_prefix;
     __shared__ unsigned int s_tile;
@@ -107,18 +112,28 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const i
     // the first writes the empty count
     ntiles = lim > 0 ? (lim + kFcTile - 1) / kFcTile : 1;
     if (sel.count && *sel.count == 0) {
-        if (blockIdx.x == 0 && tid == 0) *d_n = 0;
+        if (blockIdx.x == 0) {
+            if (tid == 0) *d_n = 0;
+            for (int64_t q = tid; q <= P; q += kBlock) oofs[q] = 0;
+        }
         return;
     }
     if (int64_t(blockIdx.x) >= ntiles) return;
     if (tid == 0) {
         s_tile = lb_take_tile(lb.ticket, unsigned(ntiles));
         const int64_t b0 = int64_t(s_tile) * kFcTile, b1 = b0 + kFcTile < lim ? b0 + kFcTile : lim;
+        const bool last_tile = int64_t(s_tile) == ntiles - 1;
         if (VIRT) {  // the selected segment holding the tile's first virtual row
             int64_t p = 0;
             s_p0 = (b0 < b1) ? (sel.phys(b0, p), p) : 0;
             s_skip = 0;
+            int64_t q = 0;
+            s_pprev = (b0 > 0 && b0 < b1) ? (sel.phys(b0 - 1, q), q) : -1;
+            q = 0;
+            s_plast = (last_tile && lim > 0) ? (sel.phys(lim - 1, q), q) : -1;
         } else {
+            s_pprev = (b0 > 0 && b0 < b1) ? int64_t(proj[b0 - 1]) : -1;
+            s_plast = (last_tile && lim > 0) ? int64_t(proj[lim - 1]) : -1;
             // (a tile of the project-ordered view whose few projects are all unselected keeps
             // nothing: none of its columns is read)
             s_skip = sel.flags && (b0 >= b1 || sel.none(proj[b0], proj[b1 - 1]));
@@ -127,6 +142,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const i
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t base = tile * kFcTile;
+    const int64_t lim_rows = lim;  // (the live rows, skipped tile or not)
     if (s_skip) lim = 0;
     // view row of item i (VIRT: through the selected segments; tables hold < 2^31 rows)
     int32_t pidx[VIRT ? kFcItems : 1];
@@ -187,7 +203,10 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const i
         }
     }
 #pragma unroll
-    for (int i = 0; i < kFcItems; ++i) s_pos[i * kBlock + tid] = keep[i] ? 1 : 0;
+    for (int i = 0; i < kFcItems; ++i) {
+        s_pos[i * kBlock + tid] = keep[i] ? 1 : 0;
+        s_pj[i * kBlock + tid] = pj[i];
+    }
     __syncthreads();
     int32_t loc[kFcItems];
     int32_t run = 0;
@@ -220,6 +239,27 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const i
         orow[q] = r[i];
         otime[q] = tm[i];
         oproj[q] = pj[i];
+    }
+    // segment offsets: the projects starting in this tile, then (last tile) the ones after its rows
+    if (s_skip) {  // (nothing kept: every project starting here starts at pre)
+        const int64_t b1 = base + kFcTile < lim_rows ? base + kFcTile : lim_rows;
+        const int64_t p1 = b1 > base ? int64_t(proj[b1 - 1]) : s_pprev;
+        for (int64_t q = s_pprev + 1 + tid; q <= p1; q += kBlock) oofs[q] = pre;
+    } else {
+        for (int i = 0; i < kFcItems; ++i) {
+            const int k = i * kBlock + tid;
+            if (base + k >= lim) break;
+            const int64_t pp = k > 0 ? int64_t(s_pj[k - 1]) : s_pprev;
+            const int64_t pc = int64_t(pj[i]);
+            if (pc > pp) {
+                const int64_t o = pre + (s_pos[k] & 0x7fffffff);
+                for (int64_t q = pp + 1; q <= pc; ++q) oofs[q] = o;
+            }
+        }
+    }
+    if (tile == ntiles - 1) {
+        const int64_t tot = pre + agg;
+        for (int64_t q = s_plast + 1 + tid; q <= P; q += kBlock) oofs[q] = tot;
     }
 }
 
@@ -278,18 +318,18 @@ void filter_view(fz_ctx *c, const View &v, int64_t n, int64_t P, Pred pred, TmpV
         if (sel.voff)
             k_filter_compact<Pred, Count, true><<<unsigned(ntiles), kBlock, 0, c->stream>>>(row0, times, proj, n, src_live, pred, lb,
                                                                               ntiles, dst.row, dst.time, dst.proj,
-                                                                              dst.d_n, sel, cnt);
+                                                                              dst.d_n, dst.offs, P, sel, cnt);
         else
             k_filter_compact<Pred, Count><<<unsigned(ntiles), kBlock, 0, c->stream>>>(row0, times, proj, n, src_live, pred, lb,
                                                                               ntiles, dst.row, dst.time, dst.proj,
-                                                                              dst.d_n, sel, cnt);
+                                                                              dst.d_n, dst.offs, P, sel, cnt);
         FZ_LAUNCH_CHECK();
         lookback_end(c, ntiles);
     } else {
         const int64_t zero = 0;
         set_i64(c, dst.d_n, &zero, 1);
+        segment_offsets_dn(c, dst.proj, dst.d_n, n, P, dst.offs);
     }
-    segment_offsets_dn(c, dst.proj, dst.d_n, n, P, dst.offs);
 }
 
 // lower_bound of v in a[lo, hi)
