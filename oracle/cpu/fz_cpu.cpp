@@ -199,8 +199,8 @@ void spearman_index(const vector<double> &x, double *rho, double *p) {
         sxx += dx * dx;
         syy += dy * dy;
     }
-    const double d = double(n - 1);
-    double r = (sxy / d) / std::sqrt(sxx / d) / std::sqrt(syy / d);
+    const double f = 1.0 / double(n - 1);  // (np.cov multiplies by the reciprocal of n - 1)
+    double r = (sxy * f) / std::sqrt(sxx * f) / std::sqrt(syy * f);
     r = std::min(1.0, std::max(-1.0, r));
     const double dof = double(n - 2);
     double q = dof / ((r + 1.0) * (1.0 - r));

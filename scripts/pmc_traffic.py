@@ -46,7 +46,9 @@ SCOPES = {
     "scan_i64": {"match": ["k_scan_lookback"]},
     # RQ2's per-session order statistics by selection: the small-segment launch opens the scope
     # (the size-class lists and the workgroup classes follow)
-    "seg_qstats": {"open": "k_qs_small", "match": ["k_qs_small", "k_qs_block", "k_seg_classes"], "allow": ["k_fill"]},
+    "seg_qstats": {"open": "k_qs_micro", "match": ["k_qs_micro", "k_qs_tiny", "k_qs_block"], "allow": ["k_fill"]},
+    "describe_select": {"match": ["k_describe_sel"]},
+    "spearman_shapiro": {"match": ["k_spearman_index_small"]},
     "ragged_transpose": {"match": ["k_rt_move"]},
     # seg_sort_f64's bucket path: value bucket classes, then the merge sort of flagged segments
     "seg_value_sort": {"open": "k_seg_val_bucket<256, 1024>",

@@ -56,6 +56,43 @@ def test_two_sample_large(engine, nx, ny, shift):
                 [mwu_p, cliff, bm[0], bm[1], lv[0], lv[1]], path="two_sample")
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 100, 1000, 4096])
+@pytest.mark.parametrize("kind", ["ties", "trend", "const"])
+def test_series_tests_small(engine, n, kind):
+    """Series of at most 4096 values: the one-workgroup kernel (LDS sort, Spearman, Shapiro-Wilk)."""
+    from tse_amd.parallel import gpu_series_tests
+    rng = np.random.default_rng(n * 3 + len(kind))
+    x = np.full(n, 42.5) if kind == "const" else (_ties if kind == "ties" else _trend)(rng, n)
+    got = tuple(float(v) for v in gpu_series_tests(engine, _dev(engine, x)).cpu())
+    with np.errstate(all="ignore"):
+        ref = orc.series_tests(x)
+    assert_same(got, ref, path=f"series[{kind},{n}]")
+
+
+@pytest.mark.parametrize("nx,ny,kind", [(5, 7, "cont"), (8, 300, "cont"), (3, 4, "ties"), (1000, 990, "ties"),
+                                         (4096, 4096, "ties"), (4096, 17, "cont"), (2, 2, "cont"), (1, 5, "ties"),
+                                         (4097, 100, "ties")])
+def test_two_sample_small(engine, nx, ny, kind):
+    """The one-workgroup two-sample kernel (both samples <= 4096 values: config 2's per-project
+    initial coverages) and, past 4096, the multi-launch path: the exact Mann-Whitney null
+    distribution (min(nx, ny) <= 8, no ties), heavy ties, one-value samples."""
+    import ctypes as C
+    from tse_amd import engine as E
+    rng = np.random.default_rng(nx * 7 + ny)
+    gen = (lambda n: rng.normal(50, 10, n)) if kind == "cont" else (lambda n: _ties(rng, n))
+    x, y = gen(nx), gen(ny) + 0.3
+    out = engine.torch.full((E.FZ_RQ4B_NTESTS,), float("nan"), dtype=engine.torch.float64, device=engine.dev)
+    dx, dy = _dev(engine, x), _dev(engine, y)
+    E._check(engine.lib, engine.lib.fz_two_sample_tests(engine.ctx, C.c_void_p(dx.data_ptr()), nx,
+                                                        C.c_void_p(dy.data_ptr()), ny, C.c_void_p(out.data_ptr())))
+    got = out.cpu().numpy()
+    with np.errstate(all="ignore"):
+        mwu_p, cliff, bm, lv = orc.rq4b_init_tests(x, y)
+    assert_same([got[E.RQ4B_MWU_P], got[E.RQ4B_CLIFF], got[E.RQ4B_BM_STAT], got[E.RQ4B_BM_P],
+                 got[E.RQ4B_LEVENE_W], got[E.RQ4B_LEVENE_P]],
+                [mwu_p, cliff, bm[0], bm[1], lv[0], lv[1]], path=f"two_sample[{nx},{ny},{kind}]")
+
+
 def test_session_bm_large(engine):
     """fz_rq4b_session_stats with sessions of >= 1e5 values per group (plus small / one-sided ones)."""
     from tse_amd.parallel import gpu_rq4b_session_stats

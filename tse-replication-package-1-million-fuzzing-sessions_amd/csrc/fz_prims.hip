@@ -1657,6 +1657,31 @@ __global__ __launch_bounds__(kBlock) void k_count_flags(const uint8_t *__restric
     if (threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long *>(out), (unsigned long long)acc);
 }
 
+struct FlagSets {
+    const uint8_t *f[4];
+    int64_t *out[4];
+};
+__global__ __launch_bounds__(kBlock) void k_count_flags_n(FlagSets fs, int64_t n) {  // blockIdx.y = set
+    __shared__ int64_t s_tmp[4];
+    const uint8_t *f = fs.f[blockIdx.y];
+    int64_t acc = 0;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+        acc += f[i] != 0;
+    acc = block_sum(acc, s_tmp);
+    if (threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long *>(fs.out[blockIdx.y]), (unsigned long long)acc);
+}
+
+void count_flags_n(fz_ctx *c, const uint8_t *const *flags, int64_t *const *outs, int k, int64_t P) {
+    FZ_CHECK(k >= 1 && k <= 4, "count_flags_n: 1..4 flag arrays");
+    FlagSets fs{};
+    for (int j = 0; j < k; ++j) {
+        fs.f[j] = flags[j];
+        fs.out[j] = outs[j];
+    }
+    k_count_flags_n<<<dim3(grid_for(P, kBlock, 256), unsigned(k)), kBlock, 0, c->stream>>>(fs, P);
+    FZ_LAUNCH_CHECK();
+}
+
 void count_flags(fz_ctx *c, const uint8_t *flags, int64_t P, int64_t *out) {
     k_count_flags<<<grid_for(P, kBlock, 256), kBlock, 0, c->stream>>>(flags, P, out);
     FZ_LAUNCH_CHECK();

@@ -195,6 +195,14 @@ struct ValidFuzzRq1 {  // result IN ('Finish', 'Halfway') AND DATE(timecreated) 
 };
 
 // One pass over the (project, rts)-sorted issues: counts, per-project flags, as-of join.
+// *ctr += the active lanes of this wave with pred (one atomic per wave, by its first active lane)
+__device__ inline void wave_count_add(int64_t *ctr, bool pred) {
+    const uint64_t m = __ballot(pred);
+    if (!m) return;
+    const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+    if (lane_id() == leader) atomicAdd(reinterpret_cast<unsigned long long *>(ctr), (unsigned long long)__popcll(m));
+}
+
 __global__ __launch_bounds__(kBlock) void k_issue_pass(View iss, const uint8_t *__restrict__ status,
                                                        const uint8_t *__restrict__ elig,
                                                        const int32_t *__restrict__ pi_count,
@@ -211,16 +219,15 @@ __global__ __launch_bounds__(kBlock) void k_issue_pass(View iss, const uint8_t *
         const bool lim = rts < kLimitUs;
         const bool fixed = status[r] <= 1;
         const bool el = elig[p];
+        // (the three counters: one atomic per wave each - per-issue atomics on three words serialise)
+        wave_count_add(&counts[FZ_RQ1_ISSUES_LIM], lim);
+        wave_count_add(&counts[FZ_RQ1_FIXED_LIM], lim && fixed);
+        wave_count_add(&counts[FZ_RQ1_TARGET], lim && fixed && el);
         if (lim) {
-            atomic_add_i64(&counts[FZ_RQ1_ISSUES_LIM], 1);
             f_lim[p] = 1;
             if (fixed) {
-                atomic_add_i64(&counts[FZ_RQ1_FIXED_LIM], 1);
                 f_fixlim[p] = 1;
-                if (el) {
-                    atomic_add_i64(&counts[FZ_RQ1_TARGET], 1);
-                    f_tgt[p] = 1;
-                }
+                if (el) f_tgt[p] = 1;
             }
         }
         int64_t mb = -1, bt = 0;
@@ -477,11 +484,11 @@ void rq1(fz_ctx *c, int64_t threshold, const fz_rq1_ext *ext_in, const fz_rq1_ou
         k_distinct_iter<<<g, kBlock, 0, st>>>(it_arr, p_arr, d_nm, o->iter_detected);
         FZ_LAUNCH_CHECK();
     }
-    if (P > 0) {
-        count_flags(c, f_lim, P, o->counts + FZ_RQ1_ISSUES_LIM_PROJECTS);
-        count_flags(c, f_fixlim, P, o->counts + FZ_RQ1_FIXED_LIM_PROJECTS);
-        count_flags(c, f_tgt, P, o->counts + FZ_RQ1_TARGET_PROJECTS);
-        count_flags(c, f_match, P, o->counts + FZ_RQ1_MATCHED_PROJECTS);
+    if (P > 0) {  // the four project flag counts in one launch
+        const uint8_t *fl[4] = {f_lim, f_fixlim, f_tgt, f_match};
+        int64_t *outs[4] = {o->counts + FZ_RQ1_ISSUES_LIM_PROJECTS, o->counts + FZ_RQ1_FIXED_LIM_PROJECTS,
+                            o->counts + FZ_RQ1_TARGET_PROJECTS, o->counts + FZ_RQ1_MATCHED_PROJECTS};
+        count_flags_n(c, fl, outs, 4, P);
     }
 
     // finalize (:233-268)

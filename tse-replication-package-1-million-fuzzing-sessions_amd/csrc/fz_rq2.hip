@@ -56,11 +56,12 @@ struct CountZeroTotal {
 // statistics.mean / median + np.percentile(5, 25, 50, 75, 95) of every session segment; sessions
 // with >= 100 values counted into *d_ge100 (which must be zero on entry)
 // (*d_ge100 zero on entry)
+// (average2 optional: a second copy of the averages)
 void session_stats(fz_ctx *c, const double *sv, const Segs &ses, double *average, double *median, double *pcts,
-                   int64_t *d_ge100) {
+                   int64_t *d_ge100, double *average2 = nullptr) {
     const double q5[5] = {5.0, 25.0, 50.0, 75.0, 95.0};
     if (seg_qstats_ok(ses)) {  // order statistics by selection: no sorted copy of the sessions
-        seg_qstats(c, sv, ses, q5, 5, average, median, pcts, d_ge100);
+        seg_qstats(c, sv, ses, q5, 5, average, median, pcts, d_ge100, average2);
         return;
     }
     ChunkedSegs cs2 = chunked(c, ses);
@@ -71,10 +72,15 @@ void session_stats(fz_ctx *c, const double *sv, const Segs &ses, double *average
     });
     seg_mean(c, cs2, sv, average);
     seg_percentiles(c, ses, ss2.val, q5, 5, pcts, median);
+    if (average2) dev_copy(c, average2, average, (ses.S > 0 ? ses.S : 1) * 8);
 }
 
 // spearmanr(range(n), x) and shapiro(x) of x[0, *d_n) (n_cap >= *d_n) -> out = rho, p, W, p
 void series_tests(fz_ctx *c, const double *x, int64_t n_cap, const int64_t *d_n, double *out) {
+    if (series_small_ok(n_cap)) {  // one workgroup: sort, Spearman and Shapiro-Wilk in LDS
+        series_small(c, x, d_n, out, out + 1, out + 2, out + 3);
+        return;
+    }
     Segs one{1, single_segment(c, d_n), n_cap};
     ChunkedSegs cs3 = chunked(c, one);
     int32_t *sg3 = segment_ids(c, one);
@@ -165,17 +171,25 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     filter_view(c, s.cov, NC, P, TrendRows{vrows, nzt}, T, nullptr, Selection{},
                 CountZeroTotal{raw_n, vrows, nzt});
     const int64_t *toffs = T.offs;
+    int64_t *d_nt = T.d_n;
     per_seg(c, P, [=] __device__(int64_t p) {
         const int64_t nt = toffs[p + 1] - toffs[p];
         raw_n[p] += nt;
         n_trend[p] = nt;
-        atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ2C_SESSIONS]), (unsigned long long)nt);
+        // (sessions start as [[]] (:285): at least one - the max taken with 1)
+        atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ2C_SESSIONS]),
+                  (unsigned long long)(nt > 1 ? nt : 1));
+        if (p == 0) counts[FZ_RQ2C_VALUES] = *d_nt;
     });
+    if (P <= 0)
+        map_n(c, 1, nullptr, [=] __device__(int64_t) {
+            counts[FZ_RQ2C_VALUES] = *d_nt;
+            counts[FZ_RQ2C_SESSIONS] = 1;
+        });
     // trend values in (project, date) order
     double *tv = c->arena.get<double>(NC);
     const int32_t *trow = T.row;
     const int64_t *cov_c = t.c_covered, *cov_t = t.c_total;
-    int64_t *d_nt = T.d_n;
     const uint8_t *cval = t.c_valid;
     map_n(c, NC, d_nt, [=] __device__(int64_t j) {
         const int32_t r = trow[j];
@@ -185,10 +199,6 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
             return;
         }
         tv[j] = double(cov_c[r]) / double(cov_t[r]) * 100.0;
-    });
-    map_n(c, 1, nullptr, [=] __device__(int64_t) {
-        counts[FZ_RQ2C_VALUES] = *d_nt;
-        if (counts[FZ_RQ2C_SESSIONS] < 1) counts[FZ_RQ2C_SESSIONS] = 1;  // starts as [[]] (:285)
     });
 
     // per-project Spearman (vs index) and Shapiro-Wilk
@@ -234,32 +244,32 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
 
     // per-session statistics (sessions are non-increasing in size: >= 100 is a prefix)
     Segs ses{M, o->session_offsets, NC, P};  // a session holds at most one value per project
-    session_stats(c, sv, ses, o->average_trend, o->median_trend, o->dist_percentiles, counts + FZ_RQ2C_GE100);
-    dev_copy(c, o->dist_mean, o->average_trend, (M > 0 ? M : 1) * 8);
+    session_stats(c, sv, ses, o->average_trend, o->median_trend, o->dist_percentiles, counts + FZ_RQ2C_GE100,
+                  o->dist_mean);
 
     // tests on the median trend (one segment of K values)
     double *sc = o->scalars;
     {
         double *t4 = c->arena.get<double>(4);
-        series_tests(c, o->median_trend, M, counts + FZ_RQ2C_GE100, t4);
-        map_n(c, 1, nullptr, [=] __device__(int64_t) {
-            sc[FZ_RQ2C_SP_RHO] = t4[0];
-            sc[FZ_RQ2C_SP_P] = t4[1];
-            sc[FZ_RQ2C_SW_MEDIAN_P] = t4[3];
-        });
+        if (series_small_ok(M)) {  // (straight into the scalars)
+            series_small(c, o->median_trend, counts + FZ_RQ2C_GE100, sc + FZ_RQ2C_SP_RHO, sc + FZ_RQ2C_SP_P, t4 + 2,
+                         sc + FZ_RQ2C_SW_MEDIAN_P);
+        } else {
+            series_tests(c, o->median_trend, M, counts + FZ_RQ2C_GE100, t4);
+            map_n(c, 1, nullptr, [=] __device__(int64_t) {
+                sc[FZ_RQ2C_SP_RHO] = t4[0];
+                sc[FZ_RQ2C_SP_P] = t4[1];
+                sc[FZ_RQ2C_SW_MEDIAN_P] = t4[3];
+            });
+        }
     }
     // mean / median of the valid (non-NaN) per-project correlations
     {
-        int64_t *flag = c->arena.get<int64_t>(P);
-        int64_t *pos = c->arena.get<int64_t>(P);
         int64_t *d_nv = c->arena.get<int64_t>(1);
         const double *corr = o->corr;
-        map_n(c, P, nullptr, [=] __device__(int64_t p) { flag[p] = (raw_n[p] > 0 && !isnan(corr[p])) ? 1 : 0; });
-        scan_exclusive_i64(c, flag, pos, P, d_nv);
-        double *vals = c->arena.get<double>(P);
-        map_n(c, P, nullptr, [=] __device__(int64_t p) {
-            if (flag[p]) vals[pos[p]] = corr[p];
-        });
+        double *vals = c->arena.get<double>(P > 0 ? P : 1);
+        compact_emit(c, P, nullptr, [=] __device__(int64_t p) { return raw_n[p] > 0 && !isnan(corr[p]); },
+                     [=] __device__(int64_t p, int64_t q) { vals[q] = corr[p]; }, d_nv);
         fz_describe *d = c->arena.get<fz_describe>(1);
         describe_f64_dn(c, vals, P, d_nv, d);
         map_n(c, 1, nullptr, [=] __device__(int64_t) {
@@ -355,36 +365,20 @@ void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
             tf[p] = used && anyt[p];
         });
     }
-    // run starts: group = cumsum(key != key.shift()) within the project (:129-131)
-    int64_t *start = c->arena.get<int64_t>(NB);
-    int64_t *rid = c->arena.get<int64_t>(NB);
+    // run starts: group = cumsum(key != key.shift()) within the project (:129-131) - the start
+    // positions compacted in one pass
     int64_t *runpos = c->arena.get<int64_t>(NB + 1);
     int64_t *d_runs = o->counts + FZ_RQ2A_RUNS;
     const int32_t *brow = B.row;
     const uint32_t *bproj = B.proj;
     const int32_t *grp = t.b_group;
     const int64_t *d_nb = B.d_n;
-    map_n(c, NB, nullptr, [=] __device__(int64_t j) {
-        if (j >= *d_nb) {
-            start[j] = 0;
-            return;
-        }
-        const uint32_t p = bproj[j];
-        start[j] = (coffs[p + 1] > coffs[p]) && (j == boffs[p] || grp[brow[j]] != grp[brow[j - 1]]) ? 1 : 0;
-    });
-    scan_exclusive_i64(c, start, rid, NB, d_runs);
-    map_n(c, NB, nullptr, [=] __device__(int64_t j) {
-        if (start[j]) runpos[rid[j]] = j;
-        if (j == 0) runpos[*d_runs] = *d_nb;
-    });
-    // a pair for run r when run r + 1 belongs to the same project
-    int64_t *pflag = c->arena.get<int64_t>(NB);
-    int64_t *ppos = c->arena.get<int64_t>(NB);
-    map_n(c, NB, nullptr, [=] __device__(int64_t r) {
-        const int64_t R = *d_runs;
-        pflag[r] = (r + 1 < R && bproj[runpos[r]] == bproj[runpos[r + 1]]) ? 1 : 0;
-    });
-    scan_exclusive_i64(c, pflag, ppos, NB, o->counts + FZ_RQ2A_ROWS);
+    compact_emit<4>(c, NB, d_nb,
+                 [=] __device__(int64_t j) {
+                     const uint32_t p = bproj[j];
+                     return (coffs[p + 1] > coffs[p]) && (j == boffs[p] || grp[brow[j]] != grp[brow[j - 1]]);
+                 },
+                 [=] __device__(int64_t j, int64_t q) { runpos[q] = j; }, d_runs);
     const int64_t *btime = t.b_time;
     const int64_t *ctime = CV.time;
     const int32_t *crow = CV.row;
@@ -392,9 +386,12 @@ void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
     const uint8_t *valid = t.c_valid;
     const fz_rq2_add_out out = *o;
     const int32_t *bperm = s.bperm, *cperm = s.cperm;  // sorted positions -> the caller's row ids
-    map_n(c, NB, nullptr, [=] __device__(int64_t r) {
-        if (!pflag[r]) return;
-        const int64_t q = ppos[r];
+    // a row for run r when run r + 1 belongs to the same project, rows compacted in the same pass
+    compact_emit<1>(c, NB, d_runs,
+                 [=] __device__(int64_t r) {
+                     return r + 1 < *d_runs && bproj[runpos[r]] == bproj[runpos[r + 1]];
+                 },
+                 [=] __device__(int64_t r, int64_t q) {
         const int64_t j0 = runpos[r], j1 = runpos[r + 1];
         const uint32_t p = bproj[j0];
         const int32_t f = brow[j0], e = brow[j1 - 1], sb = brow[j1];
@@ -423,7 +420,7 @@ void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
         out.row_cov_i1[q] = c1 >= 0 ? cperm[c1] : -1;
         out.diff_total[q] = dt;
         out.diff_coverage[q] = dc;
-    });
+    }, o->counts + FZ_RQ2A_ROWS);
 }
 
 }  // namespace fz

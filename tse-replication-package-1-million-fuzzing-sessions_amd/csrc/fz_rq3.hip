@@ -85,9 +85,7 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     filter_view(c, s.cov, NC, P, CovRowsRq3{t.c_valid, t.c_date, t.c_project, self}, TC,
                 nullptr, Selection{self, 1, I.d_n});
 
-    // ---- detected: one thread per issue (:241-302)
-    int64_t *dflag = c->arena.get<int64_t>(NI);
-    int64_t *dpos = c->arena.get<int64_t>(NI);
+    // ---- detected: one thread per issue (:241-302), the detected ones compacted in the same pass
     int64_t *pa = c->arena.get<int64_t>(NI);  // coverage pair (row a, row b)
     int64_t *pb = c->arena.get<int64_t>(NI);
     const int32_t *irow = I.row;
@@ -106,46 +104,40 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     auto null_cmp = [=] __device__(int32_t ra, int32_t rb) {
         return !(cval[ra] & FZ_VALID_TOTAL) || (ctot[ra] > 0 && !(cval[rb] & FZ_VALID_TOTAL));
     };
-    map_n(c, NI, nullptr, [=] __device__(int64_t j) {
-        dflag[j] = 0;
-        if (j >= *d_ni) return;
+    uint32_t *dproj = c->arena.get<uint32_t>(NI);
+    int64_t *dday = c->arena.get<int64_t>(NI);
+    const fz_rq3_out out = *o;
+    const int32_t *iperm = s.iperm;  // sorted positions -> the caller's issue row ids
+    compact_emit<1>(c, NI, d_ni, [=] __device__(int64_t j) -> bool {
         const uint32_t p = iproj[j];
         const int64_t rts = irts[j];
         const int64_t f0 = Fv.offs[p], f1 = Fv.offs[p + 1];
         const int64_t b0 = CBv.offs[p], b1 = CBv.offs[p + 1];
         const int64_t c0 = TCv.offs[p], c1 = TCv.offs[p + 1];
-        if (f0 == f1 || b0 == b1 || c0 == c1) return;
+        if (f0 == f1 || b0 == b1 || c0 == c1) return false;
         const int64_t k = lower_bound_i64(Fv.time, f0, f1, rts) - 1;  // last fuzz build before rts
-        if (k < f0) return;
+        if (k < f0) return false;
         const int64_t k2 = upper_bound_i64(CBv.time, b0, b1, rts);   // first coverage build after rts
-        if (k2 >= b1) return;
+        if (k2 >= b1) return false;
         const int32_t lf = Fv.row[k], fc = CBv.row[k2];
-        if (!(result[fc] == 2 || result[fc] == 0)) return;
-        if (btime[fc] - btime[lf] > kGapUs) return;  // total_seconds()/3600 > 24 (:277)
-        if (canon[lf] < 0 || canon[lf] != canon[fc]) return;
+        if (!(result[fc] == 2 || result[fc] == 0)) return false;
+        if (btime[fc] - btime[lf] > kGapUs) return false;  // total_seconds()/3600 > 24 (:277)
+        if (canon[lf] < 0 || canon[lf] != canon[fc]) return false;
         const int64_t target = fdiv_day(rts) + 1;
         int64_t kk = lower_bound_i64(TCv.time, c0, c1, target * kDay3);
         if (kk < c0 + 1) kk = c0 + 1;  // the reference scans rows i >= 1
-        if (kk >= c1 || fdiv_day(TCv.time[kk]) != target) return;
+        if (kk >= c1 || fdiv_day(TCv.time[kk]) != target) return false;
         const int32_t ra = TCv.row[kk - 1], rb = TCv.row[kk];
-        if (cvd[rb] == 0) return;      // break without a pair (:291)
+        if (cvd[rb] == 0) return false;      // break without a pair (:291)
         if (null_cmp(ra, rb)) {
             atomic_add_i64(&counts[FZ_RQ3_NULL_TOTAL], 1);
-            return;
+            return false;
         }
-        if (!(ctot[ra] > 0 && ctot[rb] > 0)) return;
-        dflag[j] = 1;
+        if (!(ctot[ra] > 0 && ctot[rb] > 0)) return false;
         pa[j] = ra;
         pb[j] = rb;
-    });
-    scan_exclusive_i64(c, dflag, dpos, NI, counts + FZ_RQ3_DETECTED);
-    uint32_t *dproj = c->arena.get<uint32_t>(NI);
-    int64_t *dday = c->arena.get<int64_t>(NI);
-    const fz_rq3_out out = *o;
-    const int32_t *iperm = s.iperm;  // sorted positions -> the caller's issue row ids
-    map_n(c, NI, nullptr, [=] __device__(int64_t j) {
-        if (!dflag[j]) return;
-        const int64_t q = dpos[j];
+        return true;
+    }, [=] __device__(int64_t j, int64_t q) {
         const int64_t ra = pa[j], rb = pb[j];
         out.det_pct[q] = (double(cvd[rb]) / double(ctot[rb]) - double(cvd[ra]) / double(ctot[ra])) * 100.0;
         out.det_cov[q] = cvd[rb] - cvd[ra];
@@ -154,7 +146,7 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         out.det_issue[q] = iperm[irow[j]];
         dproj[q] = iproj[j];
         dday[q] = fdiv_day(irts[j]);
-    });
+    }, counts + FZ_RQ3_DETECTED);
     int64_t *doffs = c->arena.get<int64_t>(P + 1);
     segment_offsets_dn(c, dproj, counts + FZ_RQ3_DETECTED, NI, P, doffs);
 
@@ -168,36 +160,29 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         const uint32_t last = n > 0 ? iproj[n - 1] : 0xffffffffu;
         hasiss[p] = (ioffs[p + 1] > ioffs[p]) && (flush_last || uint32_t(p) != last);
     });
-    // (flags, positions and rows over the live rows of TC only: *TCv.d_n of capacity NC)
-    int64_t *nflag = c->arena.get<int64_t>(NC);
-    int64_t *npos = c->arena.get<int64_t>(NC);
-    map_n(c, NC, TCv.d_n, [=] __device__(int64_t k) {
-        nflag[k] = 0;
+    // (over the live rows of TC only: *TCv.d_n of capacity NC; the kept pairs compacted in the pass)
+    compact_emit<1>(c, NC, TCv.d_n, [=] __device__(int64_t k) -> bool {
         const uint32_t p = TCv.proj[k];
-        if (!hasiss[p] || k == TCv.offs[p]) return;
+        if (!hasiss[p] || k == TCv.offs[p]) return false;
         const int32_t ra = TCv.row[k - 1], rb = TCv.row[k];
         const int64_t day = fdiv_day(TCv.time[k]);
         const int64_t lo = doffs[p], hi = doffs[p + 1];
         const int64_t q = lower_bound_i64(dday, lo, hi, day);
-        if (q < hi && dday[q] == day) return;  // a detection day of this project
+        if (q < hi && dday[q] == day) return false;  // a detection day of this project
         if (null_cmp(ra, rb)) {
             atomic_add_i64(&counts[FZ_RQ3_NULL_TOTAL], 1);
             if (p == iproj[*d_ni - 1]) atomic_add_i64(&counts[FZ_RQ3_NULL_LAST], 1);
-            return;
+            return false;
         }
-        if (!(ctot[ra] > 0 && ctot[rb] > 0)) return;
-        nflag[k] = 1;
+        if (!(ctot[ra] > 0 && ctot[rb] > 0)) return false;
         if (p == iproj[*d_ni - 1]) atomic_add_i64(&counts[FZ_RQ3_NON_LAST], 1);
-    });
-    scan_exclusive_i64_dn(c, nflag, npos, NC, TCv.d_n, counts + FZ_RQ3_NON_DETECTED);
-    map_n(c, NC, TCv.d_n, [=] __device__(int64_t k) {
-        if (!nflag[k]) return;
-        const int64_t q = npos[k];
+        return true;
+    }, [=] __device__(int64_t k, int64_t q) {
         const int32_t ra = TCv.row[k - 1], rb = TCv.row[k];
         out.non_pct[q] = (double(cvd[rb]) / double(ctot[rb]) - double(cvd[ra]) / double(ctot[ra])) * 100.0;
         out.non_cov[q] = cvd[rb] - cvd[ra];
         out.non_tot[q] = ctot[rb] - ctot[ra];
-    });
+    }, counts + FZ_RQ3_NON_DETECTED);
     map_n(c, 1, nullptr, [=] __device__(int64_t) { counts[FZ_RQ3_ISSUES] = *d_ni; });
 
     if (!(flags & FZ_RQ3_SKIP_STATS))
@@ -272,7 +257,6 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
                const double *non_pct, int64_t NC, const int64_t *d_nn, fz_describe *describe, double *tests) {
     double *dtot_f = c->arena.get<double>(NI);
     const int64_t *dt = det_tot;
-    map_n(c, NI, d_nd, [=] __device__(int64_t q) { dtot_f[q] = double(dt[q]); });
     // One sort of det u non serves everything: Brunner-Munzel ranks the union, and a stable
     // partition of the sorted union by sample gives each sample's sorted values (describe,
     // anderson, levene) - instead of three separate device-wide sorts.
@@ -285,21 +269,22 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
     {
         const double *dp = det_pct, *np_ = non_pct;
         int64_t *oall = c->arena.get<int64_t>(2);  // {0, *d_nd + *d_nn}: the union's one segment
-        map_n(c, 1, nullptr, [=] __device__(int64_t) {
-            const int64_t nd = *d_nd, nn = *d_nn;
-            oall[0] = 0;
-            oall[1] = nd + nn;
-            oseg[0] = 0;
-            oseg[1] = nd;
-            oseg[2] = nd + nn;
-        });
         const int64_t *d_all = oall + 1;
-        // (every per-element pass over the union runs over its live length *d_all, not the
-        // capacity NI + NC: config 3's union is empty, config 2's ~80 % of it)
+        // the union's values and segment bounds and det_tot as doubles in one pass, over the live
+        // elements only (config 3's union is empty, config 2's ~80 % of the capacity NI + NC)
         int32_t *sid = c->arena.get<int32_t>(cap);
         const int64_t *d_det0 = d_nd;
-        map_n(c, cap, d_all, [=] __device__(int64_t i) {
-            const int64_t nd = *d_det0;
+        map_n(c, cap > 0 ? cap : 1, nullptr, [=] __device__(int64_t i) {
+            const int64_t nd = *d_det0, nn = *d_nn;
+            if (i == 0) {
+                oall[0] = 0;
+                oall[1] = nd + nn;
+                oseg[0] = 0;
+                oseg[1] = nd;
+                oseg[2] = nd + nn;
+            }
+            if (i < nd) dtot_f[i] = double(dt[i]);
+            if (i >= nd + nn) return;
             v[i] = i < nd ? dp[i] : np_[i - nd];
             sid[i] = 0;
         });

@@ -58,6 +58,99 @@ static void group_members(fz_ctx *c, const fz_rq4_groups *g, const uint8_t *elig
 void rq4a_finish(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int64_t *g1d, const int64_t *g2t,
                  const int64_t *g2d, const int64_t *intro, const int64_t *steps, int64_t *counts, double *sc);
 
+// ---- one-workgroup versions of RQ4a's table passes (iteration tables and project counts of at most
+// kFinSmall entries - config 2's 1,000 projects and ~4,000 iterations): one launch each instead of
+// a chain of single-purpose maps and scans
+constexpr int64_t kFinSmall = 65536;
+constexpr int kFinBlock = 1024;
+constexpr int kFinWaves = kFinBlock / kWave;
+
+// tot_k[i] = number of projects of group k with more than i builds = sum_{j > i} hist_k[j], i < M
+// (hist_k = hist + k (M + 1), k = 0, 1): a suffix scan, each thread a contiguous run from the top
+__global__ __launch_bounds__(kFinBlock) void k_rq4a_totals(const int64_t *__restrict__ hist, int64_t M,
+                                                          int64_t *__restrict__ t1, int64_t *__restrict__ t2) {
+    __shared__ int64_t s_tmp[kFinWaves];
+    const int tid = threadIdx.x;
+    const int64_t per = (M + kFinBlock - 1) / kFinBlock;
+    // thread tid owns j in [a, b) of 1..M, threads in descending order of j (tid 0 the top run)
+    const int64_t b = M + 1 - int64_t(tid) * per, a = b - per > 1 ? b - per : 1;
+    for (int k = 0; k < 2; ++k) {
+        const int64_t *h = hist + k * (M + 1);
+        int64_t *tot = k == 0 ? t1 : t2;
+        int64_t sum = 0;
+        for (int64_t j = a; j < b; ++j) sum += h[j];
+        int64_t run = block_excl_scan<int64_t, kFinWaves>(b > a ? sum : 0, s_tmp, (int64_t *)nullptr);
+        for (int64_t j = b - 1; j >= a; --j) {
+            run += h[j];
+            tot[j - 1] = run;
+        }
+    }
+}
+
+// rq4a_finish's table part: the kept rows (both totals >= 100: a prefix), their rates and first
+// rate < 5, the after-slices, the positive introduction iterations in project order
+__global__ __launch_bounds__(kFinBlock) void k_rq4a_finish_small(int64_t M, int64_t P, const int64_t *__restrict__ g1t,
+                                                                const int64_t *__restrict__ g1d,
+                                                                const int64_t *__restrict__ g2t,
+                                                                const int64_t *__restrict__ g2d,
+                                                                const int64_t *__restrict__ intro, int64_t *counts,
+                                                                double *__restrict__ rates, double *__restrict__ after,
+                                                                double *__restrict__ iv, int64_t *__restrict__ d_np) {
+    __shared__ int64_t s_tmp[kFinWaves];
+    __shared__ unsigned long long s_rows, s_first[2];
+    const int tid = threadIdx.x;
+    const int64_t MM = M > 0 ? M : 1;
+    if (tid == 0) {
+        s_rows = 0ull;
+        s_first[0] = s_first[1] = ~0ull;
+    }
+    __syncthreads();
+    unsigned long long rows = 0, f0 = ~0ull, f1 = ~0ull;
+    for (int64_t i = tid; i < M; i += kFinBlock) {
+        const int64_t a = g1t[i], b = g2t[i];
+        if (a < 100 || b < 100) continue;
+        ++rows;
+        const double r1 = a > 0 ? double(g1d[i]) / double(a) * 100.0 : 0.0;
+        const double r2 = b > 0 ? double(g2d[i]) / double(b) * 100.0 : 0.0;
+        rates[i] = r1;
+        rates[MM + i] = r2;
+        if (r1 < 5.0 && (unsigned long long)i < f0) f0 = (unsigned long long)i;
+        if (r2 < 5.0 && (unsigned long long)i < f1) f1 = (unsigned long long)i;
+    }
+    rows = wave_sum(rows);
+    f0 = wave_min(f0);
+    f1 = wave_min(f1);
+    if (lane_id() == 0) {
+        atomicAdd(&s_rows, rows);
+        atomicMin(&s_first[0], f0);
+        atomicMin(&s_first[1], f1);
+    }
+    __syncthreads();  // (also orders this block's rates writes before the after-slice reads)
+    const int64_t K = int64_t(s_rows);
+    int64_t fk[2], na[2];
+    for (int k = 0; k < 2; ++k) {
+        fk[k] = s_first[k] == ~0ull ? K : int64_t(s_first[k]);
+        na[k] = K - fk[k];
+    }
+    if (tid == 0) {
+        counts[FZ_RQ4A_ROWS] = K;
+        counts[FZ_RQ4A_AFTER_G1] = na[0];
+        counts[FZ_RQ4A_AFTER_G2] = na[1];
+    }
+    for (int k = 0; k < 2; ++k)
+        for (int64_t j = tid; j < na[k]; j += kFinBlock) after[k * MM + j] = rates[k * MM + fk[k] + j];
+    // positive introduction iterations, in project order
+    const int64_t per = (P + kFinBlock - 1) / kFinBlock;
+    const int64_t p0 = int64_t(tid) * per < P ? int64_t(tid) * per : P, p1 = p0 + per < P ? p0 + per : P;
+    int64_t cnt = 0;
+    for (int64_t p = p0; p < p1; ++p) cnt += intro[p] > 0;
+    int64_t tot;
+    int64_t q = block_excl_scan<int64_t, kFinWaves>(cnt, s_tmp, &tot);
+    for (int64_t p = p0; p < p1; ++p)
+        if (intro[p] > 0) iv[q++] = double(intro[p]);
+    if (tid == 0) *d_np = tot;
+}
+
 void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
     Store &s = store_of(c);
     FZ_CHECK(s.built, "fz_rq4a: call fz_store_build first");
@@ -101,14 +194,19 @@ void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
         const unsigned long long mx = wave_max((unsigned long long)((nb > 0 && (b & 3)) ? nb : 0));
         if (lane_id() == 0 && mx) atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ4A_MAX_ITER]), mx);
     });
-    int64_t *rev = c->arena.get<int64_t>(MM), *rex = c->arena.get<int64_t>(MM);
-    for (int k = 0; k < 2; ++k) {
-        const int64_t *h = hist + k * (M + 1);
-        int64_t *tot = k == 0 ? o->g1_total : o->g2_total;
-        if (M <= 0) break;
-        map_n(c, M, nullptr, [=] __device__(int64_t j) { rev[j] = h[M - j]; });
-        scan_exclusive_i64(c, rev, rex, M, nullptr);
-        map_n(c, M, nullptr, [=] __device__(int64_t i0) { tot[i0] = rex[M - (i0 + 1)] + rev[M - (i0 + 1)]; });
+    if (M > 0 && M <= kFinSmall) {  // one workgroup: both suffix sums
+        k_rq4a_totals<<<1, kFinBlock, 0, c->stream>>>(hist, M, o->g1_total, o->g2_total);
+        FZ_LAUNCH_CHECK();
+    } else {
+        int64_t *rev = c->arena.get<int64_t>(MM), *rex = c->arena.get<int64_t>(MM);
+        for (int k = 0; k < 2; ++k) {
+            const int64_t *h = hist + k * (M + 1);
+            int64_t *tot = k == 0 ? o->g1_total : o->g2_total;
+            if (M <= 0) break;
+            map_n(c, M, nullptr, [=] __device__(int64_t j) { rev[j] = h[M - j]; });
+            scan_exclusive_i64(c, rev, rex, M, nullptr);
+            map_n(c, M, nullptr, [=] __device__(int64_t i0) { tot[i0] = rex[M - (i0 + 1)] + rev[M - (i0 + 1)]; });
+        }
     }
     // detected[k] |= {p}: k = #builds < issue time (:341-346), distinct per (k, p)
     int64_t *kk = c->arena.get<int64_t>(NI);
@@ -174,57 +272,29 @@ void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
     rq4a_finish(c, M, P, o->g1_total, o->g1_det, o->g2_total, o->g2_det, o->intro, o->g4_steps, counts, sc);
 }
 
+static void rq4a_finish_tables(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int64_t *g1d,
+                               const int64_t *g2t, const int64_t *g2d, const int64_t *intro, int64_t *counts,
+                               double *rates, double *after, double *iv, int64_t *d_np);
+
 // Finishing of RQ4a from the per-iteration tables, the per-project introduction iterations and the
 // G4 step counts (all shard-additive): kept rows, rates, first rate < 5 and the
 // after-slices (:156-207, :698-747), introduction stats (:246-299) and pre/post rates (:412-510).
 void rq4a_finish(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int64_t *g1d, const int64_t *g2t,
                  const int64_t *g2d, const int64_t *intro, const int64_t *steps, int64_t *counts, double *sc) {
     const int64_t MM = M > 0 ? M : 1;
-    map_n(c, 1, nullptr, [=] __device__(int64_t) {
-        counts[FZ_RQ4A_ROWS] = 0;
-        counts[FZ_RQ4A_AFTER_G1] = 0;
-        counts[FZ_RQ4A_AFTER_G2] = 0;
-    });
-    // rows with both totals >= 100 (a prefix), rates, first rate < 5, after-slices (:156-207, :698-747)
     double *rates = c->arena.get<double>(2 * MM);
-    int64_t *first = c->arena.get<int64_t>(2);
-    map_n(c, 1, nullptr, [=] __device__(int64_t) { first[0] = first[1] = INT64_MAX; });
-    map_n(c, M, nullptr, [=] __device__(int64_t i) {
-        const int64_t a = g1t[i], b = g2t[i];
-        if (a < 100 || b < 100) return;
-        atomic_add_i64(&counts[FZ_RQ4A_ROWS], 1);
-        const double r1 = a > 0 ? double(g1d[i]) / double(a) * 100.0 : 0.0;
-        const double r2 = b > 0 ? double(g2d[i]) / double(b) * 100.0 : 0.0;
-        rates[i] = r1;
-        rates[MM + i] = r2;
-        if (r1 < 5.0) atomicMin(reinterpret_cast<unsigned long long *>(&first[0]), (unsigned long long)i);
-        if (r2 < 5.0) atomicMin(reinterpret_cast<unsigned long long *>(&first[1]), (unsigned long long)i);
-    });
-    int64_t *nafter = counts + FZ_RQ4A_AFTER_G1;
     double *after = c->arena.get<double>(2 * MM);
-    map_n(c, 1, nullptr, [=] __device__(int64_t) {
-        const int64_t K = counts[FZ_RQ4A_ROWS];
-        for (int k = 0; k < 2; ++k) {
-            const int64_t f = first[k] == INT64_MAX ? K : first[k];
-            nafter[k] = K - f;
-            first[k] = f;
-        }
-    });
-    map_n(c, 2 * MM, nullptr, [=] __device__(int64_t i) {
-        const int k = i >= MM;
-        const int64_t j = i - k * MM;
-        if (j < nafter[k]) after[k * MM + j] = rates[k * MM + first[k] + j];
-    });
+    int64_t *nafter = counts + FZ_RQ4A_AFTER_G1;
     fz_describe *dsc = c->arena.get<fz_describe>(3);
-
-    // introduction-iteration stats over the positive ones (pandas Series mean/median/min/max)
-    int64_t *pf = c->arena.get<int64_t>(P), *pp = c->arena.get<int64_t>(P), *d_np = c->arena.get<int64_t>(1);
-    double *iv = c->arena.get<double>(P);
-    map_n(c, P, nullptr, [=] __device__(int64_t p) { pf[p] = intro[p] > 0 ? 1 : 0; });
-    scan_exclusive_i64(c, pf, pp, P, d_np);
-    map_n(c, P, nullptr, [=] __device__(int64_t p) {
-        if (pf[p]) iv[pp[p]] = double(intro[p]);
-    });
+    double *iv = c->arena.get<double>(P > 0 ? P : 1);
+    int64_t *d_np = c->arena.get<int64_t>(1);
+    if (M <= kFinSmall && P <= kFinSmall) {  // the table part in one workgroup
+        k_rq4a_finish_small<<<1, kFinBlock, 0, c->stream>>>(M, P, g1t, g1d, g2t, g2d, intro, counts, rates, after, iv,
+                                                           d_np);
+        FZ_LAUNCH_CHECK();
+    } else {
+        rq4a_finish_tables(c, M, P, g1t, g1d, g2t, g2d, intro, counts, rates, after, iv, d_np);
+    }
     const DescJob jobs[3] = {{after, MM, nafter, dsc}, {after + MM, MM, nafter + 1, dsc + 1}, {iv, P, d_np, dsc + 2}};
     describe_f64_dn_batch(c, jobs, 3);
     map_n(c, 1, nullptr, [=] __device__(int64_t) {
@@ -245,6 +315,54 @@ void rq4a_finish(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int6
         }
         sc[FZ_RQ4A_PRE_RATE] = pn ? double(pd) / double(pn) * 100.0 : 0.0;
         sc[FZ_RQ4A_POST_RATE] = qn ? double(qd) / double(qn) * 100.0 : 0.0;
+    });
+}
+
+// rq4a_finish's table part for large tables (device-wide maps and scans)
+static void rq4a_finish_tables(fz_ctx *c, int64_t M, int64_t P, const int64_t *g1t, const int64_t *g1d,
+                               const int64_t *g2t, const int64_t *g2d, const int64_t *intro, int64_t *counts,
+                               double *rates, double *after, double *iv, int64_t *d_np) {
+    const int64_t MM = M > 0 ? M : 1;
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        counts[FZ_RQ4A_ROWS] = 0;
+        counts[FZ_RQ4A_AFTER_G1] = 0;
+        counts[FZ_RQ4A_AFTER_G2] = 0;
+    });
+    // rows with both totals >= 100 (a prefix), rates, first rate < 5, after-slices (:156-207, :698-747)
+    int64_t *first = c->arena.get<int64_t>(2);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) { first[0] = first[1] = INT64_MAX; });
+    map_n(c, M, nullptr, [=] __device__(int64_t i) {
+        const int64_t a = g1t[i], b = g2t[i];
+        if (a < 100 || b < 100) return;
+        atomic_add_i64(&counts[FZ_RQ4A_ROWS], 1);
+        const double r1 = a > 0 ? double(g1d[i]) / double(a) * 100.0 : 0.0;
+        const double r2 = b > 0 ? double(g2d[i]) / double(b) * 100.0 : 0.0;
+        rates[i] = r1;
+        rates[MM + i] = r2;
+        if (r1 < 5.0) atomicMin(reinterpret_cast<unsigned long long *>(&first[0]), (unsigned long long)i);
+        if (r2 < 5.0) atomicMin(reinterpret_cast<unsigned long long *>(&first[1]), (unsigned long long)i);
+    });
+    int64_t *nafter = counts + FZ_RQ4A_AFTER_G1;
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        const int64_t K = counts[FZ_RQ4A_ROWS];
+        for (int k = 0; k < 2; ++k) {
+            const int64_t f = first[k] == INT64_MAX ? K : first[k];
+            nafter[k] = K - f;
+            first[k] = f;
+        }
+    });
+    map_n(c, 2 * MM, nullptr, [=] __device__(int64_t i) {
+        const int k = i >= MM;
+        const int64_t j = i - k * MM;
+        if (j < nafter[k]) after[k * MM + j] = rates[k * MM + first[k] + j];
+    });
+
+    // introduction-iteration stats over the positive ones (pandas Series mean/median/min/max)
+    int64_t *pf = c->arena.get<int64_t>(P), *pp = c->arena.get<int64_t>(P);
+    map_n(c, P, nullptr, [=] __device__(int64_t p) { pf[p] = intro[p] > 0 ? 1 : 0; });
+    scan_exclusive_i64(c, pf, pp, P, d_np);
+    map_n(c, P, nullptr, [=] __device__(int64_t p) {
+        if (pf[p]) iv[pp[p]] = double(intro[p]);
     });
 }
 
@@ -275,6 +393,11 @@ struct PositiveCoverage34 {  // get_coverage_deltas: coverage > 0, any date (rq4
 // initial-coverage samples a[0, *n2) (G2) and b[0, *n1) (G1) (rq4b_coverage.py:248-313)
 void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t *n2, const double *b,
                       int64_t nb_cap, const int64_t *n1, double *ts) {
+    if (two_sample_small_ok(na_cap, nb_cap)) {  // small samples (config 2: one per project): one launch
+        two_sample_small(c, a, n2, b, n1, ts + FZ_RQ4B_MWU_P, ts + FZ_RQ4B_BM_STAT, ts + FZ_RQ4B_BM_P,
+                         ts + FZ_RQ4B_CLIFF, ts + FZ_RQ4B_LEVENE_W);
+        return;
+    }
     const int64_t cap = (na_cap > 0 ? na_cap : 1) + (nb_cap > 0 ? nb_cap : 1);
     double *v = c->arena.get<double>(cap);
     uint8_t *gr = c->arena.get<uint8_t>(cap);
@@ -430,8 +553,66 @@ void rq4b_session_stats_grouped(fz_ctx *c, const double *values, const int64_t *
 // The last session index with both groups >= 100 (:849-860) -> *last (-1 if none), and Spearman
 // (rho, p) vs index of G1 Q1 / Med / Q3, then G2 Q1 / Med / Q3 over sessions 0..last (:879-899) ->
 // sp[12], from the per-session counts and quartiles of MM sessions (device; no host read)
+// One workgroup per quartile sequence (sessions of at most kTrendSmall): the last index from the
+// counts (every workgroup), the sequence sorted in LDS by (key, index), Spearman vs index off it.
+constexpr int64_t kTrendSmall = 4096;
+constexpr int kTrendBlock = 512;
+__global__ __launch_bounds__(kTrendBlock) void k_rq4b_trends_small(const int64_t *__restrict__ c2,
+                                                                  const int64_t *__restrict__ c1,
+                                                                  const double *__restrict__ g2q,
+                                                                  const double *__restrict__ g1q, int64_t MM,
+                                                                  int64_t *__restrict__ last, double *__restrict__ sp) {
+    __shared__ uint64_t sk[kTrendSmall];
+    __shared__ int32_t spos[kTrendSmall];
+    __shared__ double s_tmp[kTrendBlock / kWave];
+    __shared__ unsigned long long s_last;
+    const int tid = threadIdx.x, sgi = blockIdx.x;  // G1 Q1, Med, Q3, then G2 Q1, Med, Q3
+    if (tid == 0) s_last = 0ull;
+    __syncthreads();
+    unsigned long long lp = 0;
+    for (int64_t i = tid; i < MM; i += kTrendBlock)
+        if (c2[i] >= 100 && c1[i] >= 100) lp = (unsigned long long)(i + 1);
+    lp = wave_max(lp);
+    if (lane_id() == 0) atomicMax(&s_last, lp);
+    __syncthreads();
+    const int n = int(s_last);
+    if (sgi == 0 && tid == 0) *last = int64_t(n) - 1;
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    for (int i = tid; i < np2; i += kTrendBlock) {
+        sk[i] = i < n ? f64_key(sgi < 3 ? g1q[i * 3 + sgi] : g2q[i * 3 + sgi - 3]) : ~0ull;
+        spos[i] = i;
+    }
+    __syncthreads();
+    for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = tid; t < (np2 >> 1); t += kTrendBlock) {
+                const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;
+                const uint64_t a = sk[i], d = sk[ixj];
+                if ((a > d) == ((i & k) == 0)) {
+                    sk[i] = d;
+                    sk[ixj] = a;
+                    const int32_t q = spos[i];
+                    spos[i] = spos[ixj];
+                    spos[ixj] = q;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    double *sv = reinterpret_cast<double *>(sk);
+    for (int i = tid; i < n; i += kTrendBlock) sv[i] = f64_from_key(sk[i]);
+    __syncthreads();
+    spearman_block<kTrendBlock>(sv, spos, 0, n, s_tmp, sp + 2 * sgi, sp + 2 * sgi + 1);
+}
+
 void rq4b_trends(fz_ctx *c, const int64_t *c2, const int64_t *c1, const double *g2q, const double *g1q, int64_t MM,
                  int64_t *last, double *sp) {
+    if (MM <= kTrendSmall) {  // (config 2: one launch instead of about a dozen)
+        k_rq4b_trends_small<<<6, kTrendBlock, 0, c->stream>>>(c2, c1, g2q, g1q, MM, last, sp);
+        FZ_LAUNCH_CHECK();
+        return;
+    }
     int64_t *lastp1 = c->arena.get<int64_t>(1);
     map_n(c, 1, nullptr, [=] __device__(int64_t) { *lastp1 = 0; });
     map_n(c, MM, nullptr, [=] __device__(int64_t i) {

@@ -9,6 +9,7 @@
 
 #include "fz_device.h"
 #include "fz_internal.h"
+#include "fz_stats.h"
 #include "fz_views.h"
 
 namespace fz {
@@ -354,6 +355,10 @@ void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, 
 // scipy.stats.shapiro per segment (src in original order, ss its sorted image) -> W[S], p[S]
 // (NaN where n < 3).
 void seg_shapiro(fz_ctx *c, const ChunkedSegs &cs, const double *src, const SortedSegs &ss, double *w, double *p);
+// spearmanr(range(n), x) (rho, pv) and shapiro(x) (w, wp) of x[0, *d_n), n_cap <= 4096
+// (series_small_ok), in one launch; every output pointer non-null
+bool series_small_ok(int64_t n_cap);
+void series_small(fz_ctx *c, const double *x, const int64_t *d_n, double *rho, double *pv, double *w, double *wp);
 // spearman_index_sorted (rho, pval; rho null: none) and seg_shapiro of the same sorted segments -
 // one launch, one workgroup per segment, when no segment is longer than kSpearmanSmall values
 void spearman_shapiro_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const SortedSegs &ss,
@@ -372,11 +377,91 @@ void seg_median(fz_ctx *c, const Segs &sg, const double *sorted, double *out);
 // values added to *d_ge100.  Segments of at most kQsMax values (seg_qstats_ok).
 constexpr int64_t kQsMax = 16384;
 bool seg_qstats_ok(const Segs &sg);
+// (mean2 optional: a second copy of the means)
 void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_host, int nq, double *mean,
-                double *median, double *pcts, int64_t *d_ge100);
+                double *median, double *pcts, int64_t *d_ge100, double *mean2 = nullptr);
 
 // Two-sample rank tests per segment (x = grp 0, y = grp 1): Brunner-Munzel and Mann-Whitney U
 // (asymptotic).  Any output pointer may be null.  All outputs are [S] doubles.
+__device__ inline int64_t lower_bound_d(const double *a, int64_t lo, int64_t hi, double v) {
+    while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if (a[m] < v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+__device__ inline int64_t upper_bound_d(const double *a, int64_t lo, int64_t hi, double v) {
+    while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if (a[m] <= v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+
+// scipy.stats.spearmanr(range(n), x) of one sorted segment sv[b, b + n) (pos[j]: the source
+// position of sorted value j; ties in any order) by a workgroup of BS threads, each over a
+// contiguous run: a tie group's bounds from one binary search where it starts, the rank products
+// summed directly (exact half-integer sums).  Thread 0 writes *rho and *pval (when non-null).
+// s_tmp: BS / 64 doubles.
+template <int BS>
+__device__ inline void spearman_block(const double *sv, const int32_t *pos, int64_t b, int64_t n, double *s_tmp,
+                                      double *rho, double *pval) {
+    constexpr int NW = BS / kWave;
+    const double m = double(n + 1) / 2.0;
+    double sxy = 0.0, sxx = 0.0, syy = 0.0, ng = 0.0;
+    const int64_t per = (n + BS - 1) / BS;
+    const int64_t k0 = b + int64_t(threadIdx.x) * per, k1 = k0 + per < b + n ? k0 + per : b + n;
+    if (k0 < k1) {
+        double v = sv[k0];
+        int64_t gs = lower_bound_d(sv, b, k0 + 1, v), ge = upper_bound_d(sv, k0, b + n, v);
+        ng += gs == k0 ? 1.0 : 0.0;
+        for (int64_t j = k0; j < k1; ++j) {
+            if (j > k0 && sv[j] != v) {
+                v = sv[j];
+                gs = j;
+                // (a group of one - the common case - needs no search)
+                ge = (j + 1 < b + n && sv[j + 1] == v) ? upper_bound_d(sv, j + 1, b + n, v) : j + 1;
+                ng += 1.0;
+            }
+            const double rx = double(pos[j] - b + 1) - m;
+            const double ry = double((gs - b) + (ge - b) + 1) / 2.0 - m;
+            sxy += rx * ry;
+            sxx += rx * rx;
+            syy += ry * ry;
+        }
+    }
+    auto bsum = [&](double x) {
+        x = wave_sum(x);
+        if (lane_id() == 0) s_tmp[wave_id()] = x;
+        __syncthreads();
+        double t = s_tmp[0];
+        for (int w = 1; w < NW; ++w) t += s_tmp[w];
+        __syncthreads();
+        return t;
+    };
+    sxy = bsum(sxy);
+    sxx = bsum(sxx);
+    syy = bsum(syy);
+    ng = bsum(ng);
+    if (threadIdx.x == 0) {
+        double r = NAN, p = NAN;
+        if (n >= 2 && ng > 1.0) {  // as seg_spearman_index
+            const double f = 1.0 / double(n - 1);  // (np.cov: times the reciprocal of n - 1)
+            r = (sxy * f) / sqrt(sxx * f) / sqrt(syy * f);
+            if (r > 1.0) r = 1.0;
+            if (r < -1.0) r = -1.0;
+            const double dof = double(n - 2);
+            double q = dof / ((r + 1.0) * (1.0 - r));
+            if (q < 0.0) q = 0.0;
+            p = 2.0 * stats::t_sf(fabs(r * sqrt(q)), dof);
+        }
+        *rho = r;
+        if (pval) *pval = p;
+    }
+}
+
 struct RankTestOut {
     double *bm_stat = nullptr, *bm_p = nullptr;
     double *u1 = nullptr, *mwu_p_two = nullptr, *mwu_p_greater = nullptr, *ties = nullptr;
@@ -415,6 +500,12 @@ void spearman_index_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segi
 
 // scipy.stats.levene([x, y]) (center='median') from the samples and their medians (device
 // scalars) -> out[0] = W, out[1] = p (F(1, N-2) survival, cephes fdtrc rounding).
+// mannwhitneyu (two-sided p), brunnermunzel, Cliff's delta (2 U1 / (nx ny) - 1) and levene
+// (center='median': W, p) of x[0, *d_nx) vs y[0, *d_ny) in one workgroup - samples whose host
+// capacities pass two_sample_small_ok (<= 4096 values each)
+bool two_sample_small_ok(int64_t nx_cap, int64_t ny_cap);
+void two_sample_small(fz_ctx *c, const double *x, const int64_t *d_nx, const double *y, const int64_t *d_ny,
+                      double *mwu_p_two, double *bm_stat, double *bm_p, double *cliff, double *levene);
 void levene_two_med(fz_ctx *c, const double *medx, const double *x, int64_t nxm, const int64_t *d_nx,
                     const double *medy, const double *y, int64_t nym, const int64_t *d_ny, double *out);
 

@@ -651,6 +651,70 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
     return out;
 }
 
+// Brunner-Munzel and Mann-Whitney U of segment s from its sums: s1 = {sum of x's union ranks, of
+// y's, nx, ny, tie term t^3 - t (two exact halves)}, s2 = {sum of x's squared rank deviations, y's}
+// (scipy _stats_py.py brunnermunzel; _mannwhitneyu.py, exact null distribution when allowed)
+__device__ inline void rank_tests_finish(const double *s1, const double *s2, bool single, const RankTestOut &o,
+                                         int64_t s) {
+    const double nx = s1[2], ny = s1[3];
+    const double rcx = s1[0] / nx, rcy = s1[1] / ny;
+    const double Sx = s2[0] / (nx - 1.0), Sy = s2[1] / (ny - 1.0);
+    double w = nx * ny * (rcy - rcx);
+    w /= (nx + ny) * sqrt(nx * Sx + ny * Sy);
+    const double num = (nx * Sx + ny * Sy) * (nx * Sx + ny * Sy);
+    const double den = (nx * Sx) * (nx * Sx) / (nx - 1.0) + (ny * Sy) * (ny * Sy) / (ny - 1.0);
+    const double df = num / den;
+    if (o.bm_stat) o.bm_stat[s] = w;
+    if (o.bm_p) o.bm_p[s] = 2.0 * stats::t_sf(fabs(w), df);
+    if (o.nx) o.nx[s] = nx;
+    if (o.ny) o.ny[s] = ny;
+    // Mann-Whitney U (x vs y)
+    const double R1 = s1[0];
+    const double U1 = R1 - nx * (nx + 1.0) / 2.0;
+    const double U2 = nx * ny - U1;
+    const double nn = nx + ny;
+    const double tie = s1[4] + s1[5];
+    const double mu = nx * ny / 2.0;
+    const double sd = sqrt(nx * ny / 12.0 * ((nn + 1.0) - tie / (nn * (nn - 1.0))));
+    if (o.u1) o.u1[s] = U1;
+    // exact null distribution (scipy _mannwhitneyu._MWU): counts of U = coefficients of the
+    // Gaussian binomial [n1+n2 choose n1]_q, built as prod_k (1 - q^(n2+k)) / (1 - q^k)
+    const bool exact = o.exact_scratch && single && !(nx > 8.0 && ny > 8.0) && !(tie > 0.0);
+    double *conf = o.exact_scratch;
+    int64_t n1 = int64_t(nx < ny ? nx : ny), n2 = int64_t(nx < ny ? ny : nx);
+    double total = 1.0;
+    if (exact) {
+        const int64_t deg = n1 * n2;
+        for (int64_t u = 0; u <= deg; ++u) conf[u] = u == 0 ? 1.0 : 0.0;
+        for (int64_t k = 1; k <= n1; ++k) {
+            const int64_t m = n2 + k;
+            for (int64_t u = deg; u >= m; --u) conf[u] -= conf[u - m];
+            for (int64_t u = k; u <= deg; ++u) conf[u] += conf[u - k];
+        }
+        total = 0.0;
+        for (int64_t u = 0; u <= deg; ++u) total += conf[u];
+    }
+    auto pv = [&](double U, double f) {
+        double p;
+        if (exact) {  // _MWU.sf(U): 1 - cdf(U) + pmf(U) when U < n1*n2 - U, else cdf(n1*n2 - U)
+            const int64_t k = int64_t(U);
+            const int64_t kc = n1 * n2 - k;
+            const int64_t lim = k < kc ? k : kc;
+            double cdf = 0.0;
+            for (int64_t u = 0; u <= lim; ++u) cdf += conf[u] / total;
+            p = k < kc ? 1.0 - cdf + conf[k] / total : cdf;
+        } else {
+            const double z = (U - mu - 0.5) / sd;
+            p = stats::norm_sf(z);
+        }
+        p *= f;
+        return p < 0.0 ? 0.0 : (p > 1.0 ? 1.0 : p);
+    };
+    if (o.mwu_p_two) o.mwu_p_two[s] = pv(U1 > U2 ? U1 : U2, 2.0);
+    if (o.mwu_p_greater) o.mwu_p_greater[s] = pv(U1, 1.0);
+    if (o.ties) o.ties[s] = tie;
+}
+
 // ------------------------------------------------------------------------------ tie ranks
 TieRanks seg_tie_ranks(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const double *sorted) {
     const Segs &sg = cs.sg;
@@ -751,65 +815,7 @@ void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, 
         x[0] = xs ? d * d : 0.0;
         x[1] = xs ? 0.0 : d * d;
     }, s2, 17.0);  // isx 1 + both ranks 16
-    per_seg(c, S, [=] __device__(int64_t s) {
-        const double nx = s1[6 * s + 2], ny = s1[6 * s + 3];
-        const double rcx = s1[6 * s] / nx, rcy = s1[6 * s + 1] / ny;
-        const double Sx = s2[2 * s] / (nx - 1.0), Sy = s2[2 * s + 1] / (ny - 1.0);
-        double w = nx * ny * (rcy - rcx);
-        w /= (nx + ny) * sqrt(nx * Sx + ny * Sy);
-        const double num = (nx * Sx + ny * Sy) * (nx * Sx + ny * Sy);
-        const double den = (nx * Sx) * (nx * Sx) / (nx - 1.0) + (ny * Sy) * (ny * Sy) / (ny - 1.0);
-        const double df = num / den;
-        if (o.bm_stat) o.bm_stat[s] = w;
-        if (o.bm_p) o.bm_p[s] = 2.0 * stats::t_sf(fabs(w), df);
-        if (o.nx) o.nx[s] = nx;
-        if (o.ny) o.ny[s] = ny;
-        // Mann-Whitney U (x vs y)
-        const double R1 = s1[6 * s];
-        const double U1 = R1 - nx * (nx + 1.0) / 2.0;
-        const double U2 = nx * ny - U1;
-        const double nn = nx + ny;
-        const double tie = s1[6 * s + 4] + s1[6 * s + 5];
-        const double mu = nx * ny / 2.0;
-        const double sd = sqrt(nx * ny / 12.0 * ((nn + 1.0) - tie / (nn * (nn - 1.0))));
-        if (o.u1) o.u1[s] = U1;
-        // exact null distribution (scipy _mannwhitneyu._MWU): counts of U = coefficients of the
-        // Gaussian binomial [n1+n2 choose n1]_q, built as prod_k (1 - q^(n2+k)) / (1 - q^k)
-        const bool exact = o.exact_scratch && S == 1 && !(nx > 8.0 && ny > 8.0) && !(tie > 0.0);
-        double *conf = o.exact_scratch;
-        int64_t n1 = int64_t(nx < ny ? nx : ny), n2 = int64_t(nx < ny ? ny : nx);
-        double total = 1.0;
-        if (exact) {
-            const int64_t deg = n1 * n2;
-            for (int64_t u = 0; u <= deg; ++u) conf[u] = u == 0 ? 1.0 : 0.0;
-            for (int64_t k = 1; k <= n1; ++k) {
-                const int64_t m = n2 + k;
-                for (int64_t u = deg; u >= m; --u) conf[u] -= conf[u - m];
-                for (int64_t u = k; u <= deg; ++u) conf[u] += conf[u - k];
-            }
-            total = 0.0;
-            for (int64_t u = 0; u <= deg; ++u) total += conf[u];
-        }
-        auto pv = [&](double U, double f) {
-            double p;
-            if (exact) {  // _MWU.sf(U): 1 - cdf(U) + pmf(U) when U < n1*n2 - U, else cdf(n1*n2 - U)
-                const int64_t k = int64_t(U);
-                const int64_t kc = n1 * n2 - k;
-                const int64_t lim = k < kc ? k : kc;
-                double cdf = 0.0;
-                for (int64_t u = 0; u <= lim; ++u) cdf += conf[u] / total;
-                p = k < kc ? 1.0 - cdf + conf[k] / total : cdf;
-            } else {
-                const double z = (U - mu - 0.5) / sd;
-                p = stats::norm_sf(z);
-            }
-            p *= f;
-            return p < 0.0 ? 0.0 : (p > 1.0 ? 1.0 : p);
-        };
-        if (o.mwu_p_two) o.mwu_p_two[s] = pv(U1 > U2 ? U1 : U2, 2.0);
-        if (o.mwu_p_greater) o.mwu_p_greater[s] = pv(U1, 1.0);
-        if (o.ties) o.ties[s] = tie;
-    });
+    per_seg(c, S, [=] __device__(int64_t s) { rank_tests_finish(s1 + 6 * s, s2 + 2 * s, S == 1, o, s); });
 }
 
 // (Used while one half holds at most kBmHalvesMax values - a few per thread: at config 3's 4,000-value
@@ -822,22 +828,6 @@ void seg_rank_tests_sorted(fz_ctx *c, const SortedSegs &ss, const uint8_t *grp, 
 // forward, a new tie group finds its end by binary search.  Then the two sums scipy's
 // brunnermunzel forms (t distribution, two-sided): no union sort, no device-wide rank passes.
 // p = NaN unless both samples hold >= min_n values.
-__device__ inline int64_t lower_bound_d(const double *a, int64_t lo, int64_t hi, double v) {
-    while (lo < hi) {
-        const int64_t m = (lo + hi) >> 1;
-        if (a[m] < v) lo = m + 1;
-        else hi = m;
-    }
-    return lo;
-}
-__device__ inline int64_t upper_bound_d(const double *a, int64_t lo, int64_t hi, double v) {
-    while (lo < hi) {
-        const int64_t m = (lo + hi) >> 1;
-        if (a[m] <= v) lo = m + 1;
-        else hi = m;
-    }
-    return lo;
-}
 // visit(rc, rw) for this thread's run of a (na values) against the other half b (nb values)
 template <typename F>
 __device__ inline void bm_walk_run(const double *a, int64_t na, const double *b, int64_t nb, int64_t k0, int64_t k1,
@@ -1122,9 +1112,10 @@ void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, 
         const int64_t n = offs[s + 1] - offs[s];
         double r = NAN, p = NAN;
         if (n >= 2 && ng[s] > 1.0) {
-            // np.corrcoef: c01 / std0 / std1 with c = dot(dev, dev.T) / (n - 1)
-            const double d = double(n - 1);
-            const double cxy = sums[3 * s] / d, cxx = sums[3 * s + 1] / d, cyy = sums[3 * s + 2] / d;
+            // np.corrcoef: c01 / std0 / std1 with c = dot(dev, dev.T) * (1 / (n - 1)) (np.cov
+            // multiplies by the reciprocal)
+            const double f = 1.0 / double(n - 1);
+            const double cxy = sums[3 * s] * f, cxx = sums[3 * s + 1] * f, cyy = sums[3 * s + 2] * f;
             r = cxy / sqrt(cxx) / sqrt(cyy);
             if (r > 1.0) r = 1.0;
             if (r < -1.0) r = -1.0;
@@ -1145,12 +1136,11 @@ void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, 
 // directly - the same exact half-integer sums as seg_spearman_index, without the device-wide tie
 // rank passes.
 constexpr int64_t kSpearmanSmall = 4096;  // <= 16 values per thread: longer runs are latency chains
-constexpr int kSmallPer = int(kSpearmanSmall / kBlock);
 
-// Double-double sums of NV per-thread partials over the workgroup (kBlock threads), the rounded
-// results in every thread.
-template <int NV>
-__device__ inline void block_dd_sums(const DD (&acc)[NV], double (&s_hi)[4][NV], double (&s_lo)[4][NV],
+// Double-double sums of NV per-thread partials over the workgroup (NW waves), the rounded results
+// in every thread.
+template <int NV, int NW = 4>
+__device__ inline void block_dd_sums(const DD (&acc)[NV], double (&s_hi)[NW][NV], double (&s_lo)[NW][NV],
                                      double (&out)[NV]) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -1164,7 +1154,7 @@ __device__ inline void block_dd_sums(const DD (&acc)[NV], double (&s_hi)[4][NV],
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         DD t{s_hi[0][v], s_lo[0][v]};
-        for (int w = 1; w < 4; ++w) t = dd_add(t, DD{s_hi[w][v], s_lo[w][v]});
+        for (int w = 1; w < NW; ++w) t = dd_add(t, DD{s_hi[w][v], s_lo[w][v]});
         out[v] = t.hi + t.lo;
     }
     __syncthreads();
@@ -1174,17 +1164,19 @@ __device__ inline void block_dd_sums(const DD (&acc)[NV], double (&s_hi)[4][NV],
 // order, for y -= x[N // 2]) by the workgroup, each thread over its run [k0, k1) of <= kSmallPer
 // values: the passes of seg_shapiro (sum of m_i^2, then sx / sa, then ssa / ssx / sax), every sum
 // double-double as there; a thread's coefficients stay in registers between the last two passes.
+template <int BS = kBlock>
 __device__ inline void shapiro_block(const double *__restrict__ v, const double *__restrict__ src, int64_t b,
-                                     int64_t n, int64_t k0, int64_t k1, double (&s_hi)[4][3],
-                                     double (&s_lo)[4][3], double *w_out, double *p_out) {
+                                     int64_t n, int64_t k0, int64_t k1, double (&s_hi)[BS / kWave][3],
+                                     double (&s_lo)[BS / kWave][3], double *w_out, double *p_out) {
+    constexpr int NW = BS / kWave, PER = int(kSpearmanSmall / BS);
     DD a0[1] = {{0.0, 0.0}};
     if (n >= 3)
-        for (int64_t k = 1 + threadIdx.x; k <= n / 2; k += kBlock) {
+        for (int64_t k = 1 + threadIdx.x; k <= n / 2; k += BS) {
             const double m = stats::sw_m(k, n);
             a0[0] = dd_add_d(a0[0], m * m);
         }
     double summ2[1];
-    block_dd_sums<1>(a0, reinterpret_cast<double(&)[4][1]>(s_hi), reinterpret_cast<double(&)[4][1]>(s_lo), summ2);
+    block_dd_sums<1, NW>(a0, reinterpret_cast<double(&)[NW][1]>(s_hi), reinterpret_cast<double(&)[NW][1]>(s_lo), summ2);
     if (n < 3) {
         if (threadIdx.x == 0) {
             *w_out = NAN;
@@ -1195,10 +1187,10 @@ __device__ inline void shapiro_block(const double *__restrict__ v, const double 
     const stats::SwCoef cf = stats::sw_coef(n, 2.0 * summ2[0]);
     const double x0 = src[b + n / 2];
     const double range = (v[b + n - 1] - x0) - (v[b] - x0);
-    double co[kSmallPer], y[kSmallPer];
+    double co[PER], y[PER];
     DD a1[2] = {{0.0, 0.0}, {0.0, 0.0}};
 #pragma unroll
-    for (int u = 0; u < kSmallPer; ++u) {
+    for (int u = 0; u < PER; ++u) {
         const int64_t j = k0 + u;
         co[u] = y[u] = 0.0;
         if (j < k1) {
@@ -1209,11 +1201,11 @@ __device__ inline void shapiro_block(const double *__restrict__ v, const double 
         }
     }
     double s1[2];
-    block_dd_sums<2>(a1, reinterpret_cast<double(&)[4][2]>(s_hi), reinterpret_cast<double(&)[4][2]>(s_lo), s1);
+    block_dd_sums<2, NW>(a1, reinterpret_cast<double(&)[NW][2]>(s_hi), reinterpret_cast<double(&)[NW][2]>(s_lo), s1);
     const double sx = s1[0] / double(n), sa = s1[1] / double(n);
     DD a2[3] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
 #pragma unroll
-    for (int u = 0; u < kSmallPer; ++u) {
+    for (int u = 0; u < PER; ++u) {
         if (k0 + u < k1) {
             const double asa = co[u] - sa, xsx = y[u] - sx;
             a2[0] = dd_add_d(a2[0], asa * asa);
@@ -1222,7 +1214,7 @@ __device__ inline void shapiro_block(const double *__restrict__ v, const double 
         }
     }
     double s2[3];
-    block_dd_sums<3>(a2, s_hi, s_lo, s2);
+    block_dd_sums<3, NW>(a2, s_hi, s_lo, s2);
     if (threadIdx.x == 0) {
         if (range < stats::kSwSmall) {  // zero range: scipy returns (1.0, 1.0)
             *w_out = 1.0;
@@ -1251,49 +1243,11 @@ __global__ __launch_bounds__(kBlock) void k_spearman_index_small(const double *_
     __shared__ double s_hi[4][3], s_lo[4][3];
     for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
         const int64_t b = offs[s], n = offs[s + 1] - b;
-        const double m = double(n + 1) / 2.0;
-        double sxy = 0.0, sxx = 0.0, syy = 0.0, ng = 0.0;
         const int64_t per = (n + kBlock - 1) / kBlock;
         const int64_t k0 = b + int64_t(threadIdx.x) * per, k1 = k0 + per < b + n ? k0 + per : b + n;
         if (sw_w) shapiro_block(sv, src, b, n, k0, k1, s_hi, s_lo, sw_w + s, sw_p + s);
         if (!rho) continue;
-        if (k0 < k1) {
-            double v = sv[k0];
-            int64_t gs = lower_bound_d(sv, b, k0 + 1, v), ge = upper_bound_d(sv, k0, b + n, v);
-            ng += gs == k0 ? 1.0 : 0.0;
-            for (int64_t j = k0; j < k1; ++j) {
-                if (j > k0 && sv[j] != v) {
-                    v = sv[j];
-                    gs = j;
-                    ge = upper_bound_d(sv, j, b + n, v);
-                    ng += 1.0;
-                }
-                const double rx = double(pos[j] - b + 1) - m;
-                const double ry = double((gs - b) + (ge - b) + 1) / 2.0 - m;
-                sxy += rx * ry;
-                sxx += rx * rx;
-                syy += ry * ry;
-            }
-        }
-        sxy = block_sum(sxy, s_tmp);
-        sxx = block_sum(sxx, s_tmp);
-        syy = block_sum(syy, s_tmp);
-        ng = block_sum(ng, s_tmp);
-        if (threadIdx.x == 0) {
-            double r = NAN, p = NAN;
-            if (n >= 2 && ng > 1.0) {  // as seg_spearman_index
-                const double d = double(n - 1);
-                r = (sxy / d) / sqrt(sxx / d) / sqrt(syy / d);
-                if (r > 1.0) r = 1.0;
-                if (r < -1.0) r = -1.0;
-                const double dof = double(n - 2);
-                double q = dof / ((r + 1.0) * (1.0 - r));
-                if (q < 0.0) q = 0.0;
-                p = 2.0 * stats::t_sf(fabs(r * sqrt(q)), dof);
-            }
-            rho[s] = r;
-            if (pval) pval[s] = p;
-        }
+        spearman_block<kBlock>(sv, pos, b, n, s_tmp, rho + s, pval ? pval + s : nullptr);
     }
 }
 
@@ -1605,6 +1559,58 @@ void bm_union_sorted(fz_ctx *c, const Segs &one, const double *sorted, const int
     });
 }
 
+// spearmanr(range(n), x) and shapiro(x) of one series x[0, *d_n) of at most kSpearmanSmall values
+// in one workgroup: the keys sorted with their positions in LDS (bitonic network), then the
+// per-segment Spearman and Shapiro-Wilk passes over the sorted values in LDS.
+constexpr int kSeriesBlock = 512;
+__global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__restrict__ x,
+                                                               const int64_t *__restrict__ d_n, double *rho,
+                                                               double *pv, double *w, double *wp) {
+    constexpr int BS = kSeriesBlock, NW = BS / kWave;
+    __shared__ uint64_t sk[kSpearmanSmall];
+    __shared__ int32_t spos[kSpearmanSmall];
+    __shared__ double s_tmp[NW];
+    __shared__ double s_hi[NW][3], s_lo[NW][3];
+    const int tid = threadIdx.x;
+    const int n = int(*d_n);
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    for (int i = tid; i < np2; i += BS) {
+        sk[i] = i < n ? f64_key(x[i]) : ~0ull;
+        spos[i] = i;
+    }
+    __syncthreads();
+    for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = tid; t < (np2 >> 1); t += BS) {
+                const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;
+                const uint64_t a = sk[i], d = sk[ixj];
+                if ((a > d) == ((i & k) == 0)) {
+                    sk[i] = d;
+                    sk[ixj] = a;
+                    const int32_t q = spos[i];
+                    spos[i] = spos[ixj];
+                    spos[ixj] = q;
+                }
+            }
+            bitonic_stage_sync(k, j, np2);
+        }
+    }
+    double *sv = reinterpret_cast<double *>(sk);
+    for (int i = tid; i < n; i += BS) sv[i] = f64_from_key(sk[i]);
+    __syncthreads();
+    spearman_block<BS>(sv, spos, 0, n, s_tmp, rho, pv);
+    const int64_t per = (int64_t(n) + BS - 1) / BS;
+    const int64_t k0 = int64_t(tid) * per, k1 = k0 + per < n ? k0 + per : n;
+    shapiro_block<BS>(sv, x, 0, n, k0, k1, s_hi, s_lo, w, wp);
+}
+
+bool series_small_ok(int64_t n_cap) { return n_cap <= kSpearmanSmall; }
+void series_small(fz_ctx *c, const double *x, const int64_t *d_n, double *rho, double *pv, double *w, double *wp) {
+    k_series_small<<<1, kSeriesBlock, 0, c->stream>>>(x, d_n, rho, pv, w, wp);
+    FZ_LAUNCH_CHECK();
+}
+
 void spearman_shapiro_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const SortedSegs &ss,
                              const double *src, double *rho, double *pval, double *w, double *p) {
     const Segs &sg = cs.sg;
@@ -1652,8 +1658,8 @@ void spearman_index_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segi
             const int64_t n = offs[s + 1] - offs[s];
             double r = NAN, p = NAN;
             if (n >= 2 && sums[kSpNV * s + 3] > 1.0) {
-                const double d = double(n - 1);
-                const double cxy = sums[kSpNV * s] / d, cxx = sums[kSpNV * s + 1] / d, cyy = sums[kSpNV * s + 2] / d;
+                const double f = 1.0 / double(n - 1);  // (np.cov: times the reciprocal)
+                const double cxy = sums[kSpNV * s] * f, cxx = sums[kSpNV * s + 1] * f, cyy = sums[kSpNV * s + 2] * f;
                 r = cxy / sqrt(cxx) / sqrt(cyy);
                 if (r > 1.0) r = 1.0;
                 if (r < -1.0) r = -1.0;
@@ -1805,6 +1811,7 @@ struct QsArgs {
     double q[8];
     int nq;
     double *mean, *median, *pcts;  // [S], [S], [S * nq]
+    double *mean2;                 // [S] a second copy of the means (optional)
     int64_t *d_ge100;              // += segments of >= 100 values
 };
 constexpr int kQsMaxT = 2 * 8 + 2;  // ranks wanted per segment (two per percentile, two for the median)
@@ -1825,11 +1832,13 @@ template <typename Get>
 __device__ inline void qs_write(const QsArgs &a, int64_t s, int64_t n, double sum, Get get) {
     if (n <= 0) {
         a.mean[s] = NAN;
+        if (a.mean2) a.mean2[s] = NAN;
         a.median[s] = NAN;
         for (int j = 0; j < a.nq; ++j) a.pcts[s * a.nq + j] = NAN;
         return;
     }
     a.mean[s] = sum / double(n);
+    if (a.mean2) a.mean2[s] = sum / double(n);
     a.median[s] = (n & 1) ? get(n / 2) : (get(n / 2 - 1) + get(n / 2)) / 2.0;
     for (int j = 0; j < a.nq; ++j) a.pcts[s * a.nq + j] = np_percentile_sorted(get, n, a.q[j]);
 }
@@ -2208,16 +2217,73 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
     if (tid == 0 && ge100) atomic_add_i64(a.d_ge100, ge100);
 }
 
+// The mid list (kTinySeg < n <= 1024 values): one 256-thread workgroup per segment sorts the keys
+// in LDS (bitonic network, +inf padding; only its stages of distance >= 128 need a workgroup
+// barrier) and reads the order statistics off the sorted keys - at these lengths a few dozen LDS
+// stages beat the histogram selection's barrier rounds and per-target list ranking (config 2:
+// ~3,000 sessions of <= 1,000 values).
+__global__ __launch_bounds__(256) void k_qs_sort_mid(const double *__restrict__ src, const int64_t *__restrict__ offs,
+                                                     const int32_t *__restrict__ list,
+                                                     const int64_t *__restrict__ d_ln, QsArgs a) {
+    constexpr int BS = 256, MAXN = 1024, NW = BS / kWave;
+    __shared__ uint64_t sk[MAXN];
+    __shared__ double s_dhi[NW], s_dlo[NW];
+    const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+    int64_t ge100 = 0;
+    const int64_t ln = *d_ln;
+    for (int64_t it = blockIdx.x; it < ln; it += gridDim.x) {
+        const int64_t s = list[it];
+        const int64_t b = offs[s];
+        const int n = int(offs[s + 1] - b);
+        int np2 = 64;
+        while (np2 < n) np2 <<= 1;
+        DD acc{0.0, 0.0};
+        for (int i = tid; i < np2; i += BS) {
+            const double x = i < n ? src[b + i] : 0.0;
+            if (i < n) acc = dd_add_d(acc, x);
+            sk[i] = i < n ? f64_key(x) : ~0ull;
+        }
+        acc = wave_dd_sum(acc);
+        if (lane == 0) {
+            s_dhi[w] = acc.hi;
+            s_dlo[w] = acc.lo;
+        }
+        __syncthreads();
+        for (int k = 2; k <= np2; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int t = tid; t < (np2 >> 1); t += BS) {
+                    const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;
+                    const uint64_t u = sk[i], d = sk[ixj];
+                    if ((u > d) == ((i & k) == 0)) {
+                        sk[i] = d;
+                        sk[ixj] = u;
+                    }
+                }
+                bitonic_stage_sync(k, j, np2);
+            }
+        }
+        if (tid == 0) {
+            DD tot{s_dhi[0], s_dlo[0]};
+            for (int q = 1; q < NW; ++q) tot = dd_add(tot, DD{s_dhi[q], s_dlo[q]});
+            qs_write(a, s, n, tot.hi + tot.lo, [&](int64_t j) { return f64_from_key(sk[j]); });
+            if (n >= 100) ++ge100;
+        }
+        __syncthreads();  // LDS is reused by the next segment
+    }
+    if (tid == 0 && ge100) atomic_add_i64(a.d_ge100, ge100);
+}
+
 bool seg_qstats_ok(const Segs &sg) { return sg.len_bound() <= kQsMax; }
 
 void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_host, int nq, double *mean,
-                double *median, double *pcts, int64_t *d_ge100) {
+                double *median, double *pcts, int64_t *d_ge100, double *mean2) {
     FZ_CHECK(nq >= 0 && nq <= 8, "seg_qstats: at most 8 percentiles");
     FZ_CHECK(seg_qstats_ok(sg), "seg_qstats: segment longer than kQsMax");
     QsArgs a{};
     for (int j = 0; j < nq; ++j) a.q[j] = q_host[j];
     a.nq = nq;
     a.mean = mean;
+    a.mean2 = mean2;
     a.median = median;
     a.pcts = pcts;
     a.d_ge100 = d_ge100;
@@ -2241,7 +2307,7 @@ void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_h
         FZ_LAUNCH_CHECK();
     }
     if (lb > kTinySeg) {
-        k_qs_block<256, 1024><<<grid(caps[1], 8192), 256, 0, c->stream>>>(vals, sg.offs, L.ids[1], L.d_n + 1, a);
+        k_qs_sort_mid<<<grid(caps[1], 8192), 256, 0, c->stream>>>(vals, sg.offs, L.ids[1], L.d_n + 1, a);
         FZ_LAUNCH_CHECK();
     }
     if (lb > 1024) {
@@ -2252,6 +2318,23 @@ void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_h
 
 // levene([x, y], center='median') (scipy _morestats.py levene), the two medians given on the
 // device (medx / medy: e.g. fields of fz_describe results)
+// levene([x, y], center='median') (scipy _morestats.py levene) from zb = the mean absolute
+// deviations from each median, dv = the sums of their squared deviations from zb -> out = W, p
+__device__ inline void levene_finish(const double *zb, const double *dv, double nx, double ny, double *out) {
+    const double N = nx + ny;
+    double zbar = 0.0;
+    zbar += zb[0] * nx;
+    zbar += zb[1] * ny;
+    zbar /= N;
+    const double numer = (N - 2.0) * (nx * (zb[0] - zbar) * (zb[0] - zbar) + ny * (zb[1] - zbar) * (zb[1] - zbar));
+    double dvar = 0.0;
+    dvar += dv[0];
+    dvar += dv[1];
+    const double W = numer / (1.0 * dvar);
+    out[0] = W;
+    out[1] = stats::f1_sf(W, N - 2.0);
+}
+
 void levene_two_med(fz_ctx *c, const double *medx, const double *x, int64_t nxm, const int64_t *d_nx,
                     const double *medy, const double *y, int64_t nym, const int64_t *d_ny, double *out) {
     double *med = c->arena.get<double>(2);
@@ -2281,20 +2364,186 @@ void levene_two_med(fz_ctx *c, const double *medx, const double *x, int64_t nxm,
         const double d = fabs(y[i] - med[1]) - zb[1];
         v[0] = d * d;
     }, dv + 1);
-    map_n(c, 1, nullptr, [=] __device__(int64_t) {
-        const double nx = double(*d_nx), ny = double(*d_ny), N = nx + ny;
-        double zbar = 0.0;
-        zbar += zb[0] * nx;
-        zbar += zb[1] * ny;
-        zbar /= N;
-        const double numer = (N - 2.0) * (nx * (zb[0] - zbar) * (zb[0] - zbar) + ny * (zb[1] - zbar) * (zb[1] - zbar));
-        double dvar = 0.0;
-        dvar += dv[0];
-        dvar += dv[1];
-        const double W = numer / (1.0 * dvar);
-        out[0] = W;
-        out[1] = stats::f1_sf(W, N - 2.0);
-    });
+    map_n(c, 1, nullptr, [=] __device__(int64_t) { levene_finish(zb, dv, double(*d_nx), double(*d_ny), out); });
+}
+
+// ------------------------------------------------- two small samples: every test in one workgroup
+// mannwhitneyu, brunnermunzel (union ranks), Cliff's delta and levene(center='median') of x[0, *d_nx)
+// and y[0, *d_ny), each of at most kTwoSmall values: both samples sorted in LDS (one bitonic network
+// over the two halves), a value's union rank / within-sample rank / tie group from binary searches in
+// the two sorted halves, the medians read off them, every sum double-double as on the multi-launch
+// path (seg_rank_tests_sorted, levene_two_med), the same finishing formulas.  One launch instead of
+// about 25.
+constexpr int kTwoSmall = 4096;
+constexpr int kTwoBlock = 512;
+template <int NV>
+__device__ inline void block_dd_sums16(const DD (&acc)[NV], double (*s_hi)[NV], double (*s_lo)[NV], double (&out)[NV]) {
+    constexpr int NW = kTwoBlock / kWave;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const DD r = wave_dd_sum(acc[v]);
+        if (lane_id() == 0) {
+            s_hi[wave_id()][v] = r.hi;
+            s_lo[wave_id()][v] = r.lo;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        DD t{s_hi[0][v], s_lo[0][v]};
+        for (int w = 1; w < NW; ++w) t = dd_add(t, DD{s_hi[w][v], s_lo[w][v]});
+        out[v] = t.hi + t.lo;
+    }
+    __syncthreads();
+}
+__device__ inline int lb_lds(const double *a, int lo, int hi, double v) {
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (a[m] < v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+__device__ inline int ub_lds(const double *a, int lo, int hi, double v) {
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (a[m] <= v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+struct TwoSmallOut {
+    double *mwu_p_two, *bm_stat, *bm_p, *cliff, *levene;  // levene: W, p
+    double *exact_scratch;                              // 8 * kTwoSmall + 1 doubles
+};
+__global__ __launch_bounds__(kTwoBlock) void k_two_sample_small(const double *__restrict__ xin,
+                                                               const int64_t *__restrict__ d_nx,
+                                                               const double *__restrict__ yin,
+                                                               const int64_t *__restrict__ d_ny, TwoSmallOut o) {
+    constexpr int NW = kTwoBlock / kWave;
+    __shared__ uint64_t sk[2 * kTwoSmall];  // x's keys in [0, np2), y's in [np2, 2 np2); then the values
+    __shared__ double s_hi[NW][6], s_lo[NW][6];
+    const int tid = threadIdx.x;
+    const int nx = int(*d_nx), ny = int(*d_ny);
+    int np2 = 1;
+    while (np2 < (nx > ny ? nx : ny)) np2 <<= 1;
+    for (int i = tid; i < np2; i += kTwoBlock) {
+        sk[i] = i < nx ? f64_key(xin[i]) : ~0ull;
+        sk[np2 + i] = i < ny ? f64_key(yin[i]) : ~0ull;
+    }
+    __syncthreads();
+    // one bitonic network of np2 entries on both halves at once (pair q of half q / (np2 / 2))
+    const int hp = np2 >> 1;
+    for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = tid; t < np2; t += kTwoBlock) {
+                const int h = t >= hp ? 1 : 0, q = t - h * hp;
+                const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1)), ixj = i + j;
+                uint64_t *a = sk + h * np2;
+                const uint64_t u = a[i], d = a[ixj];
+                if ((u > d) == ((i & k) == 0)) {
+                    a[i] = d;
+                    a[ixj] = u;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // keys -> values in place (as doubles)
+    double *xs = reinterpret_cast<double *>(sk), *ys = reinterpret_cast<double *>(sk + np2);
+    for (int i = tid; i < np2; i += kTwoBlock) {
+        xs[i] = f64_from_key(sk[i]);
+        ys[i] = f64_from_key(sk[np2 + i]);
+    }
+    __syncthreads();
+    const double Nx = double(nx), Ny = double(ny);
+    // pass 1: union rank sums, tie term (each union tie group once: at its first x value, or at its
+    // first y value when it holds no x)
+    DD a1[6] = {};
+    auto group = [&](const double *a, int na, const double *b, int nb, int i, int &la, int &ua, int &lb, int &ub) {
+        const double v = a[i];
+        la = lb_lds(a, 0, i + 1, v);
+        ua = ub_lds(a, i, na, v);
+        lb = lb_lds(b, 0, nb, v);
+        ub = ub_lds(b, lb, nb, v);
+    };
+    for (int i = tid; i < nx + ny; i += kTwoBlock) {
+        const bool isx = i < nx;
+        const int k = isx ? i : i - nx;
+        int la, ua, lb, ub;
+        if (isx) group(xs, nx, ys, ny, k, la, ua, lb, ub);
+        else group(ys, ny, xs, nx, k, la, ua, lb, ub);
+        const double rc = double(la + lb + ua + ub + 1) / 2.0;
+        if (isx) a1[0] = dd_add_d(a1[0], rc);
+        else a1[1] = dd_add_d(a1[1], rc);
+        if (k == la && (isx || ub == lb)) {  // t^3 - t, int64-exact, in two exactly representable halves
+            const int64_t t = int64_t(ua - la) + int64_t(ub - lb), tt = t * t * t - t;
+            a1[4] = dd_add_d(a1[4], double(tt & ~int64_t((1 << 26) - 1)));
+            a1[5] = dd_add_d(a1[5], double(tt & int64_t((1 << 26) - 1)));
+        }
+    }
+    double s1[6];
+    block_dd_sums16<6>(a1, s_hi, s_lo, s1);
+    s1[2] = Nx;
+    s1[3] = Ny;
+    // pass 2: squared deviations of (union rank - within-sample rank) from their means
+    DD a2[2] = {};
+    const double cmx = s1[0] / Nx, cmy = s1[1] / Ny, wmx = (Nx + 1.0) / 2.0, wmy = (Ny + 1.0) / 2.0;
+    for (int i = tid; i < nx + ny; i += kTwoBlock) {
+        const bool isx = i < nx;
+        const int k = isx ? i : i - nx;
+        int la, ua, lb, ub;
+        if (isx) group(xs, nx, ys, ny, k, la, ua, lb, ub);
+        else group(ys, ny, xs, nx, k, la, ua, lb, ub);
+        const double rc = double(la + lb + ua + ub + 1) / 2.0;
+        const double rw = double(la) + double(ua - la + 1) / 2.0;
+        const double d = ((rc - rw) - (isx ? cmx : cmy)) + (isx ? wmx : wmy);
+        if (isx) a2[0] = dd_add_d(a2[0], d * d);
+        else a2[1] = dd_add_d(a2[1], d * d);
+    }
+    double s2[2];
+    block_dd_sums16<2>(a2, reinterpret_cast<double(*)[2]>(s_hi), reinterpret_cast<double(*)[2]>(s_lo), s2);
+    // levene: medians, mean absolute deviations, their squared deviations
+    const double medx = nx <= 0 ? NAN : ((nx & 1) ? xs[nx / 2] : (xs[nx / 2 - 1] + xs[nx / 2]) / 2.0);
+    const double medy = ny <= 0 ? NAN : ((ny & 1) ? ys[ny / 2] : (ys[ny / 2 - 1] + ys[ny / 2]) / 2.0);
+    DD a3[2] = {};
+    for (int i = tid; i < nx; i += kTwoBlock) a3[0] = dd_add_d(a3[0], fabs(xs[i] - medx));
+    for (int i = tid; i < ny; i += kTwoBlock) a3[1] = dd_add_d(a3[1], fabs(ys[i] - medy));
+    double zb[2];
+    block_dd_sums16<2>(a3, reinterpret_cast<double(*)[2]>(s_hi), reinterpret_cast<double(*)[2]>(s_lo), zb);
+    zb[0] /= Nx;
+    zb[1] /= Ny;
+    DD a4[2] = {};
+    for (int i = tid; i < nx; i += kTwoBlock) {
+        const double d = fabs(xs[i] - medx) - zb[0];
+        a4[0] = dd_add_d(a4[0], d * d);
+    }
+    for (int i = tid; i < ny; i += kTwoBlock) {
+        const double d = fabs(ys[i] - medy) - zb[1];
+        a4[1] = dd_add_d(a4[1], d * d);
+    }
+    double dv[2];
+    block_dd_sums16<2>(a4, reinterpret_cast<double(*)[2]>(s_hi), reinterpret_cast<double(*)[2]>(s_lo), dv);
+    if (tid != 0) return;
+    double u1 = 0.0;
+    RankTestOut ro;
+    ro.mwu_p_two = o.mwu_p_two;
+    ro.u1 = &u1;
+    ro.bm_stat = o.bm_stat;
+    ro.bm_p = o.bm_p;
+    ro.exact_scratch = o.exact_scratch;
+    rank_tests_finish(s1, s2, true, ro, 0);
+    *o.cliff = (2.0 * u1) / (Nx * Ny) - 1.0;
+    levene_finish(zb, dv, Nx, Ny, o.levene);
+}
+
+bool two_sample_small_ok(int64_t nx_cap, int64_t ny_cap) { return nx_cap <= kTwoSmall && ny_cap <= kTwoSmall; }
+
+void two_sample_small(fz_ctx *c, const double *x, const int64_t *d_nx, const double *y, const int64_t *d_ny,
+                      double *mwu_p_two, double *bm_stat, double *bm_p, double *cliff, double *levene) {
+    TwoSmallOut o{mwu_p_two, bm_stat, bm_p, cliff, levene, c->arena.get<double>(8 * kTwoSmall + 1)};
+    k_two_sample_small<<<1, kTwoBlock, 0, c->stream>>>(x, d_nx, y, d_ny, o);
+    FZ_LAUNCH_CHECK();
 }
 
 // ------------------------------------------------------------------------------ session exchange

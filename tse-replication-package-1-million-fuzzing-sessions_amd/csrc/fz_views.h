@@ -332,6 +332,76 @@ void filter_view(fz_ctx *c, const View &v, int64_t n, int64_t P, Pred pred, TmpV
     }
 }
 
+// Ordered stream compaction of the indices i < *d_n (d_n null: n_cap) kept by pred(i): emit(i, q)
+// for each, q = its rank among the kept ones; *d_total (optional) = their number.  One launch -
+// decoupled look-back over 4096-index tiles - instead of a flag map, a device-wide scan and an emit
+// map.  pred may have side effects (write what emit reads back for the same i).  ITEMS indices per
+// thread: 16 for light predicates; a heavy one (binary searches) takes 1 - 4, so that the tiles
+// spread over the whole chip.
+template <int ITEMS, typename Pred, typename Emit>
+__global__ __launch_bounds__(kBlock) void k_compact_emit(int64_t n_cap, const int64_t *__restrict__ d_n, Pred pred,
+                                                         Emit emit, Lookback lb, int64_t *__restrict__ d_total) {
+    constexpr int kCeItems = ITEMS, kCeTile = kBlock * ITEMS;
+    __shared__ int32_t s_pos[kCeTile];
+    __shared__ int32_t s_tmp[4];
+    __shared__ int64_t s_prefix;
+    __shared__ unsigned int s_tile;
+    const int tid = threadIdx.x;
+    const int64_t n = d_n ? (*d_n < n_cap ? *d_n : n_cap) : n_cap;
+    const int64_t ntiles = n > 0 ? (n + kCeTile - 1) / kCeTile : 1;
+    if (int64_t(blockIdx.x) >= ntiles) return;
+    if (tid == 0) s_tile = lb_take_tile(lb.ticket, unsigned(ntiles));
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int64_t base = tile * kCeTile;
+    bool keep[kCeItems];
+#pragma unroll
+    for (int i = 0; i < kCeItems; ++i) {
+        const int64_t idx = base + i * kBlock + tid;
+        keep[i] = idx < n && pred(idx);
+        s_pos[i * kBlock + tid] = keep[i] ? 1 : 0;
+    }
+    __syncthreads();
+    int32_t loc[kCeItems];
+    int32_t run = 0;
+    for (int i = 0; i < kCeItems; ++i) {
+        loc[i] = run;
+        run += s_pos[tid * kCeItems + i];
+    }
+    int32_t agg;
+    const int32_t off = block_excl_scan(run, s_tmp, &agg);
+    if (tid < kWave) {
+        const int64_t prefix = lb_exclusive_prefix(lb, tile, agg);
+        if (tid == 0) {
+            s_prefix = prefix;
+            if (tile == ntiles - 1 && d_total) *d_total = prefix + agg;
+        }
+    }
+    __syncthreads();
+    for (int i = 0; i < kCeItems; ++i) s_pos[tid * kCeItems + i] = loc[i] + off;
+    __syncthreads();
+    const int64_t pre = s_prefix;
+#pragma unroll
+    for (int i = 0; i < kCeItems; ++i)
+        if (keep[i]) emit(base + i * kBlock + tid, pre + s_pos[i * kBlock + tid]);
+}
+template <int ITEMS = 16, typename Pred, typename Emit>
+void compact_emit(fz_ctx *c, int64_t n_cap, const int64_t *d_n, Pred pred, Emit emit, int64_t *d_total) {
+    constexpr int64_t kCeTile = int64_t(kBlock) * ITEMS;
+    if (n_cap <= 0) {
+        if (d_total) {
+            const int64_t zero = 0;
+            set_i64(c, d_total, &zero, 1);
+        }
+        return;
+    }
+    const int64_t ntiles = (n_cap + kCeTile - 1) / kCeTile;
+    const Lookback lb = lookback_begin(c, ntiles);
+    k_compact_emit<ITEMS, Pred, Emit><<<unsigned(ntiles), kBlock, 0, c->stream>>>(n_cap, d_n, pred, emit, lb, d_total);
+    FZ_LAUNCH_CHECK();
+    lookback_end(c, ntiles);
+}
+
 // lower_bound of v in a[lo, hi)
 __device__ inline int64_t lower_bound_i64(const int64_t *a, int64_t lo, int64_t hi, int64_t v) {
     while (lo < hi) {
@@ -356,6 +426,8 @@ __device__ inline void atomic_add_i64(int64_t *p, int64_t v) {
 
 // Count nonzero bytes of flags[0..P) into *out (adds).
 void count_flags(fz_ctx *c, const uint8_t *flags, int64_t P, int64_t *out);
+// the same for k <= 4 flag arrays of P bytes each in one launch (outs[j] += count of flags[j])
+void count_flags_n(fz_ctx *c, const uint8_t *const *flags, int64_t *const *outs, int k, int64_t P);
 // describe of x[0..*d_n) with nmax a host upper bound (fz_prims.hip).
 void describe_f64_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n, fz_describe *dev_out);
 // up to kDescBatch independent describes; all small ones (nmax <= 4096) share one launch (one
