@@ -46,7 +46,7 @@ SCOPES = {
     "scan_i64": {"match": ["k_scan_lookback"]},
     # RQ2's per-session order statistics by selection: the small-segment launch opens the scope
     # (the size-class lists and the workgroup classes follow)
-    "seg_qstats": {"open": "k_qs_micro", "match": ["k_qs_micro", "k_qs_tiny", "k_qs_block"], "allow": ["k_fill"]},
+    "seg_qstats": {"open": "k_qs_micro", "match": ["k_qs_micro", "k_qs_tiny", "k_qs_sort_mid", "k_qs_block"], "allow": ["k_fill"]},
     "describe_select": {"match": ["k_describe_sel"]},
     "spearman_shapiro": {"match": ["k_spearman_index_small"]},
     "ragged_transpose": {"match": ["k_rt_move"]},

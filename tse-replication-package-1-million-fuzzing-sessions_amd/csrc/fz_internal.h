@@ -231,7 +231,7 @@ struct fz_ctx {
     // decoupled look-back state (fz_lookback.h; single-pass scan, compaction, radix passes): status
     // words tagged with a per-launch epoch, and a tile ticket counter each launch resets itself
     fz::DevBuf os_status;          // uint64 [max words of one launch]
-    fz::DevBuf os_ticket;          // uint32 [2] self-resetting tile counter
+    fz::DevBuf os_ticket;          // uint32 [4] self-resetting tile counters
     unsigned int os_epoch = 0;
     // radix digit totals, two buffers used by alternate sorts: each sort's passes zero the other
     // one, so the next sort's histogram starts from zero without a memset launch

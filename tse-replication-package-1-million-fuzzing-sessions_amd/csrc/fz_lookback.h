@@ -29,6 +29,9 @@ constexpr uint64_t kLbVal = (1ull << 48) - 1ull, kLbEpochMask = ((1ull << 14) - 
 // Host: prepare `words` status words for one launch (call lookback_end(c, tiles) after it).
 Lookback lookback_begin(fz_ctx *c, int64_t words);
 inline void lookback_end(fz_ctx *, int64_t) {}
+// The same for k <= 4 look-back passes run side by side in ONE launch: out[j] gets its own status
+// words (words[j]) and its own ticket counter.
+Lookback lookback_begin_n(fz_ctx *c, const int64_t *words, int k, Lookback *out);
 // Enqueue a reset of the ticket and the status words (device) and of the host base / epoch.
 void lookback_reset(fz_ctx *c);
 

@@ -226,8 +226,8 @@ Lookback lookback_begin(fz_ctx *c, int64_t words) {
         dev_fill(c, st, 0, int64_t(c->os_status.cap));
         c->os_epoch = 0;
     }
-    if (c->os_ticket.cap == 0) {
-        dev_fill(c, c->os_ticket.ensure<unsigned int>(2), 0, 8);
+    if (c->os_ticket.cap == 0) {  // (four counters: up to four look-back launches fused in one kernel)
+        dev_fill(c, c->os_ticket.ensure<unsigned int>(4), 0, 16);
     }
     if (++c->os_epoch == (1u << 14)) {  // epoch wrap: clear the status words once
         dev_fill(c, c->os_status.ptr, 0, int64_t(c->os_status.cap));
@@ -239,11 +239,24 @@ Lookback lookback_begin(fz_ctx *c, int64_t words) {
     return Lookback{c->os_status.as<uint64_t>(), c->os_ticket.as<unsigned int>(), uint64_t(c->os_epoch) << 48};
 }
 
-// Zero the tile ticket and every status word of the context (one kernel: a graph recording starts
+Lookback lookback_begin_n(fz_ctx *c, const int64_t *words, int k, Lookback *out) {
+    FZ_CHECK(k >= 1 && k <= 4, "lookback_begin_n: 1..4 launches");
+    int64_t tot = 0;
+    for (int j = 0; j < k; ++j) tot += words[j] > 0 ? words[j] : 1;
+    const Lookback lb = lookback_begin(c, tot);
+    int64_t o = 0;
+    for (int j = 0; j < k; ++j) {
+        out[j] = Lookback{lb.status + o, lb.ticket + j, lb.epoch};
+        o += words[j] > 0 ? words[j] : 1;
+    }
+    return lb;
+}
+
+// Zero the tile tickets and every status word of the context (one kernel: a graph recording starts
 // with it, so each replay finds no status word carrying one of its recorded epochs).
 __global__ __launch_bounds__(kBlock) void k_lb_reset(unsigned int *__restrict__ ticket, uint64_t *__restrict__ status,
                                                      int64_t words) {
-    if (blockIdx.x == 0 && threadIdx.x == 0 && ticket) *ticket = 0u;
+    if (blockIdx.x == 0 && threadIdx.x < 4 && ticket) ticket[threadIdx.x] = 0u;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < words; i += int64_t(gridDim.x) * kBlock)
         status[i] = 0ull;
 }

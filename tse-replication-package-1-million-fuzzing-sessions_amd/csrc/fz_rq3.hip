@@ -71,10 +71,8 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     eligible_projects(c, o->eligible, counts + FZ_RQ3_ELIGIBLE, {{counts, FZ_RQ3_NCOUNTS * 8, 0}});
 
     TmpView I, F, CB, TC;
-    filter_view(c, s.issues, NI, P,
-                FixedIssuesRq3{t.i_project, t.i_status, t.i_rts, o->eligible}, I);
-    filter_view(c, s.fuzz, s.fuzz.n, P, FuzzRq3{t.b_result, t.b_time}, F);
-    filter_view(c, s.covb, s.covb.n, P, CovBuildRq3{t.b_time}, CB);
+    filter_views3(c, P, s.issues, NI, FixedIssuesRq3{t.i_project, t.i_status, t.i_rts, o->eligible}, I, s.fuzz,
+                  s.fuzz.n, FuzzRq3{t.b_result, t.b_time}, F, s.covb, s.covb.n, CovBuildRq3{t.b_time}, CB);
     // the coverage rows of the projects with a fixed issue only: the view's tiles of other projects
     // are skipped unread (config 3 / 5, coverage-only tables: all of them)
     uint8_t *self = c->arena.get<uint8_t>(P);

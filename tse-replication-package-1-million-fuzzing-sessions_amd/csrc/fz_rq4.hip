@@ -179,8 +179,8 @@ void rq4a(fz_ctx *c, const fz_rq4_groups *g, const fz_rq4a_out *o) {
     const uint8_t *member = o->member;
 
     TmpView FB, FI;
-    filter_view(c, s.fuzz, s.fuzz.n, P, BuildsBeforeLimit{t.b_time}, FB);
-    filter_view(c, s.issues, NI, P, FixedBeforeLimit{t.i_status, t.i_rts}, FI);
+    filter_views2(c, P, s.fuzz, s.fuzz.n, BuildsBeforeLimit{t.b_time}, FB, s.issues, NI,
+                  FixedBeforeLimit{t.i_status, t.i_rts}, FI);
     const int64_t *fboffs = FB.offs, *fbtime = FB.time, *fioffs = FI.offs, *fitime = FI.time;
 
     // totals[i] += 1 for i = 1..#builds, per group (:339-340)

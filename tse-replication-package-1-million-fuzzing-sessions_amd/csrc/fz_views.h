@@ -88,22 +88,55 @@ struct NoCount {
 
 // VIRT: the rows are the virtual rows of a Selection with view_offs (the selected projects'
 // segments back to back): item i's view row comes from Selection::phys.
+struct FcShared {
+    int32_t pos[kFcTile];
+    uint32_t pj[kFcTile];  // the items' projects (their predecessors' for the offsets)
+    int64_t pprev, plast;  // project of the row before the tile / of the last live row
+    int32_t tmp[4];
+    int64_t prefix;
+    unsigned int tile;
+    int skip;
+    int64_t p0;
+};
+// One filter launch's arguments (the view, the predicate, the outputs).
 template <typename Pred, typename Count = NoCount, bool VIRT = false>
-__global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const int64_t *__restrict__ times,
-                                                           const uint32_t *__restrict__ proj, int64_t n,
-                                                           const int64_t *__restrict__ d_live, Pred pred, Lookback lb,
-                                                           int64_t ntiles, int32_t *__restrict__ orow,
-                                                           int64_t *__restrict__ otime, uint32_t *__restrict__ oproj,
-                                                           int64_t *__restrict__ d_n, int64_t *__restrict__ oofs,
-                                                           int64_t P, Selection sel, Count cnt = Count{}) {
-    __shared__ int32_t s_pos[kFcTile];
-    __shared__ uint32_t s_pj[kFcTile];  // the items' projects (their predecessors' for the offsets)
-    __shared__ int64_t s_pprev, s_plast;  // project of the row before the tile / of the last live row
-    __shared__ int32_t s_tmp[4];
-    __shared__ int64_t s_prefix;
-    __shared__ unsigned int s_tile;
-    __shared__ int s_skip;
-    __shared__ int64_t s_p0;
+struct FcJob {
+    int64_t row0;
+    const int64_t *times;
+    const uint32_t *proj;
+    int64_t n;
+    const int64_t *d_live;
+    Pred pred;
+    Lookback lb;
+    int64_t ntiles;
+    int32_t *orow;
+    int64_t *otime;
+    uint32_t *oproj;
+    int64_t *d_n;
+    int64_t *oofs;
+    int64_t P;
+    Selection sel;
+    Count cnt;
+};
+// tile `bid` of a filter launch (the workgroup's LDS in sh)
+template <typename Pred, typename Count, bool VIRT>
+__device__ inline void filter_tile(const FcJob<Pred, Count, VIRT> &J, int64_t bid, FcShared &sh) {
+    const int64_t row0 = J.row0;
+    const int64_t *__restrict__ times = J.times;
+    const uint32_t *__restrict__ proj = J.proj;
+    const int64_t n = J.n;
+    const int64_t *__restrict__ d_live = J.d_live;
+    const Pred &pred = J.pred;
+    const Lookback &lb = J.lb;
+    int64_t ntiles = J.ntiles;
+    int32_t *__restrict__ orow = J.orow;
+    int64_t *__restrict__ otime = J.otime;
+    uint32_t *__restrict__ oproj = J.oproj;
+    int64_t *__restrict__ d_n = J.d_n;
+    int64_t *__restrict__ oofs = J.oofs;
+    const int64_t P = J.P;
+    const Selection &sel = J.sel;
+    const Count &cnt = J.cnt;
     const int tid = threadIdx.x;
     const int64_t live = d_live ? *d_live : n;
     int64_t lim = live < n ? live : n;
@@ -112,42 +145,42 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const i
     // the first writes the empty count
     ntiles = lim > 0 ? (lim + kFcTile - 1) / kFcTile : 1;
     if (sel.count && *sel.count == 0) {
-        if (blockIdx.x == 0) {
+        if (bid == 0) {
             if (tid == 0) *d_n = 0;
             for (int64_t q = tid; q <= P; q += kBlock) oofs[q] = 0;
         }
         return;
     }
-    if (int64_t(blockIdx.x) >= ntiles) return;
+    if (int64_t(bid) >= ntiles) return;
     if (tid == 0) {
-        s_tile = lb_take_tile(lb.ticket, unsigned(ntiles));
-        const int64_t b0 = int64_t(s_tile) * kFcTile, b1 = b0 + kFcTile < lim ? b0 + kFcTile : lim;
-        const bool last_tile = int64_t(s_tile) == ntiles - 1;
+        sh.tile = lb_take_tile(lb.ticket, unsigned(ntiles));
+        const int64_t b0 = int64_t(sh.tile) * kFcTile, b1 = b0 + kFcTile < lim ? b0 + kFcTile : lim;
+        const bool last_tile = int64_t(sh.tile) == ntiles - 1;
         if (VIRT) {  // the selected segment holding the tile's first virtual row
             int64_t p = 0;
-            s_p0 = (b0 < b1) ? (sel.phys(b0, p), p) : 0;
-            s_skip = 0;
+            sh.p0 = (b0 < b1) ? (sel.phys(b0, p), p) : 0;
+            sh.skip = 0;
             int64_t q = 0;
-            s_pprev = (b0 > 0 && b0 < b1) ? (sel.phys(b0 - 1, q), q) : -1;
+            sh.pprev = (b0 > 0 && b0 < b1) ? (sel.phys(b0 - 1, q), q) : -1;
             q = 0;
-            s_plast = (last_tile && lim > 0) ? (sel.phys(lim - 1, q), q) : -1;
+            sh.plast = (last_tile && lim > 0) ? (sel.phys(lim - 1, q), q) : -1;
         } else {
-            s_pprev = (b0 > 0 && b0 < b1) ? int64_t(proj[b0 - 1]) : -1;
-            s_plast = (last_tile && lim > 0) ? int64_t(proj[lim - 1]) : -1;
+            sh.pprev = (b0 > 0 && b0 < b1) ? int64_t(proj[b0 - 1]) : -1;
+            sh.plast = (last_tile && lim > 0) ? int64_t(proj[lim - 1]) : -1;
             // (a tile of the project-ordered view whose few projects are all unselected keeps
             // nothing: none of its columns is read)
-            s_skip = sel.flags && (b0 >= b1 || sel.none(proj[b0], proj[b1 - 1]));
+            sh.skip = sel.flags && (b0 >= b1 || sel.none(proj[b0], proj[b1 - 1]));
         }
     }
     __syncthreads();
-    const int64_t tile = s_tile;
+    const int64_t tile = sh.tile;
     const int64_t base = tile * kFcTile;
     const int64_t lim_rows = lim;  // (the live rows, skipped tile or not)
-    if (s_skip) lim = 0;
+    if (sh.skip) lim = 0;
     // view row of item i (VIRT: through the selected segments; tables hold < 2^31 rows)
     int32_t pidx[VIRT ? kFcItems : 1];
     if constexpr (VIRT) {
-        int64_t p = s_p0;
+        int64_t p = sh.p0;
 #pragma unroll
         for (int i = 0; i < kFcItems; ++i) {
             const int64_t v = base + i * kBlock + tid;
@@ -204,22 +237,22 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const i
     }
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) {
-        s_pos[i * kBlock + tid] = keep[i] ? 1 : 0;
-        s_pj[i * kBlock + tid] = pj[i];
+        sh.pos[i * kBlock + tid] = keep[i] ? 1 : 0;
+        sh.pj[i * kBlock + tid] = pj[i];
     }
     __syncthreads();
     int32_t loc[kFcItems];
     int32_t run = 0;
     for (int i = 0; i < kFcItems; ++i) {
         loc[i] = run;
-        run += s_pos[tid * kFcItems + i];
+        run += sh.pos[tid * kFcItems + i];
     }
     int32_t agg;
-    const int32_t off = block_excl_scan(run, s_tmp, &agg);
+    const int32_t off = block_excl_scan(run, sh.tmp, &agg);
     if (tid < kWave) {
         const int64_t prefix = lb_exclusive_prefix(lb, tile, agg);
         if (tid == 0) {
-            s_prefix = prefix;
+            sh.prefix = prefix;
             if (tile == ntiles - 1) *d_n = prefix + agg;
         }
     }
@@ -227,40 +260,59 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(int64_t row0, const i
     // keep flag in bit 31 of the exclusive in-tile position
     for (int i = 0; i < kFcItems; ++i) {
         const int k = tid * kFcItems + i;
-        s_pos[k] = (loc[i] + off) | (s_pos[k] ? int32_t(0x80000000u) : 0);
+        sh.pos[k] = (loc[i] + off) | (sh.pos[k] ? int32_t(0x80000000u) : 0);
     }
     __syncthreads();
-    const int64_t pre = s_prefix;
+    const int64_t pre = sh.prefix;
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) {
         if (!keep[i]) continue;
         const int k = i * kBlock + tid;
-        const int64_t q = pre + (s_pos[k] & 0x7fffffff);
+        const int64_t q = pre + (sh.pos[k] & 0x7fffffff);
         orow[q] = r[i];
         otime[q] = tm[i];
         oproj[q] = pj[i];
     }
     // segment offsets: the projects starting in this tile, then (last tile) the ones after its rows
-    if (s_skip) {  // (nothing kept: every project starting here starts at pre)
+    if (sh.skip) {  // (nothing kept: every project starting here starts at pre)
         const int64_t b1 = base + kFcTile < lim_rows ? base + kFcTile : lim_rows;
-        const int64_t p1 = b1 > base ? int64_t(proj[b1 - 1]) : s_pprev;
-        for (int64_t q = s_pprev + 1 + tid; q <= p1; q += kBlock) oofs[q] = pre;
+        const int64_t p1 = b1 > base ? int64_t(proj[b1 - 1]) : sh.pprev;
+        for (int64_t q = sh.pprev + 1 + tid; q <= p1; q += kBlock) oofs[q] = pre;
     } else {
         for (int i = 0; i < kFcItems; ++i) {
             const int k = i * kBlock + tid;
             if (base + k >= lim) break;
-            const int64_t pp = k > 0 ? int64_t(s_pj[k - 1]) : s_pprev;
+            const int64_t pp = k > 0 ? int64_t(sh.pj[k - 1]) : sh.pprev;
             const int64_t pc = int64_t(pj[i]);
             if (pc > pp) {
-                const int64_t o = pre + (s_pos[k] & 0x7fffffff);
+                const int64_t o = pre + (sh.pos[k] & 0x7fffffff);
                 for (int64_t q = pp + 1; q <= pc; ++q) oofs[q] = o;
             }
         }
     }
     if (tile == ntiles - 1) {
         const int64_t tot = pre + agg;
-        for (int64_t q = s_plast + 1 + tid; q <= P; q += kBlock) oofs[q] = tot;
+        for (int64_t q = sh.plast + 1 + tid; q <= P; q += kBlock) oofs[q] = tot;
     }
+}
+
+
+template <typename Pred, typename Count = NoCount, bool VIRT = false>
+__global__ __launch_bounds__(kBlock) void k_filter_compact(const FcJob<Pred, Count, VIRT> J) {
+    __shared__ FcShared sh;
+    filter_tile(J, int64_t(blockIdx.x), sh);
+}
+
+// Three filters in one launch (blocks [0, g0) the first one's tiles, then the second's, then the
+// third's): independent views filtered back to back by one kernel instead of three.
+template <typename P0, typename P1, typename P2>
+__global__ __launch_bounds__(kBlock) void k_filter_compact3(const FcJob<P0> J0, const FcJob<P1> J1,
+                                                            const FcJob<P2> J2, unsigned g0, unsigned g1) {
+    __shared__ FcShared sh;
+    const unsigned b = blockIdx.x;
+    if (b < g0) filter_tile(J0, int64_t(b), sh);
+    else if (b < g0 + g1) filter_tile(J1, int64_t(b - g0), sh);
+    else filter_tile(J2, int64_t(b - g0 - g1), sh);
 }
 
 // The selected projects' segment lengths (0 for the others; entry P = 0) for the virtual rows.
@@ -316,13 +368,13 @@ void filter_view(fz_ctx *c, const View &v, int64_t n, int64_t P, Pred pred, TmpV
         ProbeScope ps(c, sel.flags ? "filter_select" : "filter_compact",
                       sel.flags ? 0.0 : double(n) * PredBytes<Pred>::value, dst.d_n, 28.0);
         if (sel.voff)
-            k_filter_compact<Pred, Count, true><<<unsigned(ntiles), kBlock, 0, c->stream>>>(row0, times, proj, n, src_live, pred, lb,
-                                                                              ntiles, dst.row, dst.time, dst.proj,
-                                                                              dst.d_n, dst.offs, P, sel, cnt);
+            k_filter_compact<Pred, Count, true><<<unsigned(ntiles), kBlock, 0, c->stream>>>(
+                FcJob<Pred, Count, true>{row0, times, proj, n, src_live, pred, lb, ntiles, dst.row, dst.time, dst.proj,
+                                         dst.d_n, dst.offs, P, sel, cnt});
         else
-            k_filter_compact<Pred, Count><<<unsigned(ntiles), kBlock, 0, c->stream>>>(row0, times, proj, n, src_live, pred, lb,
-                                                                              ntiles, dst.row, dst.time, dst.proj,
-                                                                              dst.d_n, dst.offs, P, sel, cnt);
+            k_filter_compact<Pred, Count><<<unsigned(ntiles), kBlock, 0, c->stream>>>(
+                FcJob<Pred, Count, false>{row0, times, proj, n, src_live, pred, lb, ntiles, dst.row, dst.time, dst.proj,
+                                          dst.d_n, dst.offs, P, sel, cnt});
         FZ_LAUNCH_CHECK();
         lookback_end(c, ntiles);
     } else {
@@ -400,6 +452,79 @@ void compact_emit(fz_ctx *c, int64_t n_cap, const int64_t *d_n, Pred pred, Emit 
     k_compact_emit<ITEMS, Pred, Emit><<<unsigned(ntiles), kBlock, 0, c->stream>>>(n_cap, d_n, pred, emit, lb, d_total);
     FZ_LAUNCH_CHECK();
     lookback_end(c, ntiles);
+}
+
+// Two independent filters in one launch (as filter_views3)
+template <typename P0, typename P1>
+__global__ __launch_bounds__(kBlock) void k_filter_compact2(const FcJob<P0> J0, const FcJob<P1> J1, unsigned g0) {
+    __shared__ FcShared sh;
+    const unsigned b = blockIdx.x;
+    if (b < g0) filter_tile(J0, int64_t(b), sh);
+    else filter_tile(J1, int64_t(b - g0), sh);
+}
+template <typename P0, typename P1>
+void filter_views2(fz_ctx *c, int64_t P, const View &v0, int64_t n0, P0 p0, TmpView &d0, const View &v1, int64_t n1,
+                   P1 p1, TmpView &d1) {
+    TmpView *dst[2] = {&d0, &d1};
+    const int64_t ns[2] = {n0, n1};
+    for (int k = 0; k < 2; ++k) {
+        TmpView &d = *dst[k];
+        const int64_t n = ns[k];
+        d.cap = n;
+        d.d_n = c->arena.get<int64_t>(1);
+        d.row = c->arena.get<int32_t>(n > 0 ? n : 1);
+        d.time = c->arena.get<int64_t>(n > 0 ? n : 1);
+        d.proj = c->arena.get<uint32_t>(n > 0 ? n : 1);
+        d.offs = c->arena.get<int64_t>(P + 1);
+    }
+    const int64_t tiles[2] = {(n0 + kFcTile - 1) / kFcTile > 0 ? (n0 + kFcTile - 1) / kFcTile : 1,
+                              (n1 + kFcTile - 1) / kFcTile > 0 ? (n1 + kFcTile - 1) / kFcTile : 1};
+    Lookback lb[2];
+    lookback_begin_n(c, tiles, 2, lb);
+    ProbeScope ps(c, "filter_compact", double(n0) * PredBytes<P0>::value + double(n1) * PredBytes<P1>::value);
+    const FcJob<P0> j0{v0.row0, v0.time, v0.proj, n0, nullptr, p0, lb[0], tiles[0], d0.row, d0.time, d0.proj, d0.d_n,
+                       d0.offs, P, Selection{}, NoCount{}};
+    const FcJob<P1> j1{v1.row0, v1.time, v1.proj, n1, nullptr, p1, lb[1], tiles[1], d1.row, d1.time, d1.proj, d1.d_n,
+                       d1.offs, P, Selection{}, NoCount{}};
+    k_filter_compact2<P0, P1><<<unsigned(tiles[0] + tiles[1]), kBlock, 0, c->stream>>>(j0, j1, unsigned(tiles[0]));
+    FZ_LAUNCH_CHECK();
+}
+
+// Three independent filters (views v0 / v1 / v2 with n0 / n1 / n2 rows, predicates p0 / p1 / p2,
+// no selection, no second count) in one launch -> d0 / d1 / d2, as three filter_view calls.
+template <typename P0, typename P1, typename P2>
+void filter_views3(fz_ctx *c, int64_t P, const View &v0, int64_t n0, P0 p0, TmpView &d0, const View &v1, int64_t n1,
+                   P1 p1, TmpView &d1, const View &v2, int64_t n2, P2 p2, TmpView &d2) {
+    TmpView *dst[3] = {&d0, &d1, &d2};
+    const int64_t ns[3] = {n0, n1, n2};
+    for (int k = 0; k < 3; ++k) {
+        TmpView &d = *dst[k];
+        const int64_t n = ns[k];
+        d.cap = n;
+        d.d_n = c->arena.get<int64_t>(1);
+        d.row = c->arena.get<int32_t>(n > 0 ? n : 1);
+        d.time = c->arena.get<int64_t>(n > 0 ? n : 1);
+        d.proj = c->arena.get<uint32_t>(n > 0 ? n : 1);
+        d.offs = c->arena.get<int64_t>(P + 1);
+    }
+    // (an empty view still gets one workgroup: it writes the zero count and the offsets)
+    const int64_t tiles[3] = {(n0 + kFcTile - 1) / kFcTile > 0 ? (n0 + kFcTile - 1) / kFcTile : 1,
+                              (n1 + kFcTile - 1) / kFcTile > 0 ? (n1 + kFcTile - 1) / kFcTile : 1,
+                              (n2 + kFcTile - 1) / kFcTile > 0 ? (n2 + kFcTile - 1) / kFcTile : 1};
+    Lookback lb[3];
+    lookback_begin_n(c, tiles, 3, lb);
+    ProbeScope ps(c, "filter_compact",
+                  double(n0) * PredBytes<P0>::value + double(n1) * PredBytes<P1>::value +
+                      double(n2) * PredBytes<P2>::value);
+    const FcJob<P0> j0{v0.row0, v0.time, v0.proj, n0, nullptr, p0, lb[0], tiles[0], d0.row, d0.time, d0.proj, d0.d_n,
+                       d0.offs, P, Selection{}, NoCount{}};
+    const FcJob<P1> j1{v1.row0, v1.time, v1.proj, n1, nullptr, p1, lb[1], tiles[1], d1.row, d1.time, d1.proj, d1.d_n,
+                       d1.offs, P, Selection{}, NoCount{}};
+    const FcJob<P2> j2{v2.row0, v2.time, v2.proj, n2, nullptr, p2, lb[2], tiles[2], d2.row, d2.time, d2.proj, d2.d_n,
+                       d2.offs, P, Selection{}, NoCount{}};
+    k_filter_compact3<P0, P1, P2><<<unsigned(tiles[0] + tiles[1] + tiles[2]), kBlock, 0, c->stream>>>(
+        j0, j1, j2, unsigned(tiles[0]), unsigned(tiles[1]));
+    FZ_LAUNCH_CHECK();
 }
 
 // lower_bound of v in a[lo, hi)

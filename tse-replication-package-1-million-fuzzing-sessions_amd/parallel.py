@@ -53,23 +53,55 @@ RQ3_NCOUNTS = 8
 
 # ------------------------------------------------------------------------------------- sharding
 def shard_bounds(t: Tables, world: int) -> List[Tuple[int, int]]:
-    """Contiguous project-id ranges [lo, hi), one per rank, with about equal session-row counts
-    (prefix sum of per-project rows; a giant project stays whole on one rank and is split across
-    workgroups there)."""
+    """Contiguous project-id ranges [lo, hi), one per rank, minimising the largest shard's
+    session-row count (a giant project stays whole on one rank and is split across workgroups
+    there).  The smallest capacity C for which a greedy left-to-right packing needs at most `world`
+    ranges is found by bisection over the prefix sums (the linear-partition bound: with config 5's
+    20.8 M-row Zipf giant the largest of 4 shards drops from 34.8 M rows - cuts at the equal-rows
+    targets - to the packing optimum); the ranges are then cut at that C, and left empty only when
+    there are fewer projects than ranks."""
     P = len(t.projects)
     rows = (np.bincount(t.b_project.astype(np.int64), minlength=P)
             + np.bincount(t.c_project.astype(np.int64), minlength=P)
             + np.bincount(t.i_project.astype(np.int64), minlength=P)).astype(np.int64)
-    cum = np.concatenate([[0], np.cumsum(rows)])
+    return partition_rows(rows, world)
+
+
+def partition_rows(rows: np.ndarray, world: int) -> List[Tuple[int, int]]:
+    """shard_bounds over per-project row counts: min-max contiguous partition into `world` ranges."""
+    P = len(rows)
+    cum = np.concatenate([[0], np.cumsum(rows)]).astype(np.int64)
     total = int(cum[-1])
-    cuts = [0]
-    for r in range(1, world):
-        target = total * r / world
-        k = int(np.searchsorted(cum, target, "left"))
-        if k > 0 and abs(cum[k - 1] - target) <= abs(cum[min(k, P)] - target):
-            k -= 1
-        cuts.append(min(max(k, cuts[-1]), P))
-    cuts.append(P)
+    if world <= 1 or P == 0:
+        return [(0, P)] + [(P, P)] * (world - 1) if world > 1 else [(0, P)]
+
+    def cuts_for(cap):  # greedy: each range as long as it stays <= cap (a project over cap alone)
+        cuts, lo = [0], 0
+        while lo < P and len(cuts) <= world:
+            hi = int(np.searchsorted(cum, cum[lo] + cap, "right")) - 1
+            hi = max(hi, lo + 1)
+            cuts.append(min(hi, P))
+            lo = cuts[-1]
+        return cuts
+
+    lo_c, hi_c = max(int(rows.max()), -(-total // world)), total
+    while lo_c < hi_c:
+        mid = (lo_c + hi_c) // 2
+        if cuts_for(mid)[-1] >= P and len(cuts_for(mid)) - 1 <= world:
+            hi_c = mid
+        else:
+            lo_c = mid + 1
+    cuts = cuts_for(lo_c)
+    while len(cuts) - 1 < world:  # fewer ranges than ranks: split the largest multi-project range
+        sizes = [(cum[cuts[i + 1]] - cum[cuts[i]], i) for i in range(len(cuts) - 1) if cuts[i + 1] - cuts[i] > 1]
+        if not sizes:
+            cuts.append(P)  # (empty trailing ranges)
+            continue
+        _, i = max(sizes)
+        a, b = cuts[i], cuts[i + 1]
+        mid = int(np.searchsorted(cum, (cum[a] + cum[b]) // 2, "left"))
+        mid = min(max(mid, a + 1), b - 1)
+        cuts.insert(i + 1, mid)
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
