@@ -49,6 +49,11 @@ for s in $STEPS; do
       extra=""; [ $kind = fs1 ] && extra="--shard-groups rq3,rq4b,rq2_count,rq1,rq4a,rq2_add"
       timeout -k 10 600 python -u bench.py --config $arg --steps $st --warmup 2 --no-cpu-baseline --probe-steps 0 --force-sharded $extra > $O/${T}_${kind}_$arg.json 2> $O/${T}_${kind}_$arg.err || exit $?
       python3 -c "import json; d=json.loads([l for l in open('$O/${T}_${kind}_$arg.json') if l.startswith('{')][-1]); print('$kind $arg', d['ms_per_step'], d['config'].get('driver_host_ms'), flush=True)" ;;
+    dmicro)  # describe-by-selection micro-benchmark (default build; phase stamps from the timing variant)
+      timeout -k 10 200 python -u scripts/describe_micro.py > $O/${T}_dmicro.txt 2>&1 || exit $?
+      V=tse-replication-package-1-million-fuzzing-sessions_amd/csrc/build/variants/libfz_desctime.so
+      if [ -f $V ]; then TIMING=1 timeout -k 10 200 python -u scripts/describe_micro.py $V >> $O/${T}_dmicro.txt 2>&1 || exit $?; fi
+      grep '^{' $O/${T}_dmicro.txt ;;
     grp)  # bench with another grouping of the analyses: grp:<cfg>@<groups> ("|" between streams)
       cfg=${arg%%@*}; groups=${arg#*@}
       timeout -k 10 600 python -u bench.py --config $cfg --steps 20 --warmup 2 --no-cpu-baseline --probe-steps 0 --groups "$groups" > $O/${T}_grp.json 2> $O/${T}_grp.err || exit $?

@@ -1207,6 +1207,25 @@ __device__ inline void sel_for(int64_t n, const Load &load, const Body &body) {
     }
 }
 
+#ifdef FZ_DESC_TIMING
+// experiment builds only: wall-clock (100 MHz) phase stamps of the last k_describe_sel workgroup 0
+__device__ unsigned long long g_desc_t[16];
+#define DESC_STAMP(ph)                                                       \
+    do {                                                                     \
+        __syncthreads();                                                     \
+        if (threadIdx.x == 0 && blockIdx.x == 0) g_desc_t[ph] = wall_clock64(); \
+    } while (0)
+extern "C" int fz_debug_desc_timing(unsigned long long *out) {
+    hipDeviceSynchronize();
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_desc_t), sizeof(g_desc_t));
+    return 0;
+}
+#else
+#define DESC_STAMP(ph) \
+    do {               \
+    } while (0)
+#endif
+
 // sh.res[t] = the key of rank sh.rank[t] (t < nt) among the n keys key(i), whose min / max are lo / hi
 template <typename KeyF>
 __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64_t hi, int nt, SelShared &sh) {
@@ -1222,8 +1241,10 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
     for (int j = tid; j <= nb; j += BS) sh.cnt[j] = 0u;
     for (int j = tid; j < nb; j += BS) sh.map[j] = 0xff;
     __syncthreads();
+    DESC_STAMP(3);
     sel_for(n, key, [&](int64_t, uint64_t k) { atomicAdd(&sh.cnt[sel_bucket(k, lo, sc, nb)], 1u); });
     __syncthreads();
+    DESC_STAMP(4);
     {  // exclusive scan of the bucket counts: thread t takes buckets [t * 4, t * 4 + 4)
         constexpr int BPT = kSelNB / BS;
         uint32_t sum = 0;
@@ -1311,6 +1332,7 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
         }
     }
     __syncthreads();
+    DESC_STAMP(5);
     auto rank_list = [&](int slot, int sz, int64_t want, int t) {  // one wave
         const uint64_t e = lane < sz ? sh.list[slot][lane] : ~0ull;
         int rr = 0;
@@ -1327,6 +1349,7 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
     // histogram pass (target t's sub-buckets in its own slice of sh.cnt) and one min / max pass over
     // the sub-bucket holding its rank - until it holds one key or <= 64 values; then one gather of
     // all the narrow intervals (uniform control flow: the target state is in LDS)
+    DESC_STAMP(6);
     constexpr int kSlice = kSelNB / kSelMaxT;
     if (tid < nt) {
         const bool wide = sh.tslot[tid] < 0;
@@ -1407,6 +1430,7 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
         }
         __syncthreads();
     }
+    DESC_STAMP(7);
     // one key left (ties): the result; else <= 64 values in [wl, wh]: one gather for all, ranked
     bool gather = false;
     uint64_t gl[kSelMaxT], gh[kSelMaxT];
@@ -1465,6 +1489,7 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
         if (tid == 0) describe_from_sorted(nullptr, 0, 0.0, 0.0, out);
         return;
     }
+    DESC_STAMP(0);
     const uint64_t kneg0 = f64_key(-0.0), kpos0 = f64_key(0.0), kinf = f64_key(INFINITY);
     if (tid < 3) s_c[tid] = 0ull;
     uint64_t lo = ~0ull, hi = 0ull;
@@ -1493,6 +1518,7 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
         atomicAdd(&s_c[2], leinf);
     }
     DD t = block_dd_sum_sel(acc, s_hi, s_lo);  // (its barriers order the counters too)
+    DESC_STAMP(1);
     const double mean = (t.hi + t.lo) / double(n);
     acc = DD{0.0, 0.0};
     auto sq = [&](int64_t, double v) {
@@ -1503,6 +1529,7 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
     if (staged) sel_for(n, [&](int64_t i) { return f64_from_key(s_keys[i]); }, sq);
     else sel_for(n, ld, sq);
     t = block_dd_sum_sel(acc, s_hi, s_lo);
+    DESC_STAMP(2);
     const double std = sqrt((t.hi + t.lo) / double(n));
     const int64_t c_lt0 = int64_t(s_c[0]), c_le0 = int64_t(s_c[1]), c_leinf = int64_t(s_c[2]);
     // ranks: median (n / 2, and n / 2 - 1), np.percentile 25 / 75 neighbours, the smallest non-zero
@@ -1523,6 +1550,7 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
     __syncthreads();
     if (staged) wg_select_global([&](int64_t i) { return s_keys[i]; }, n, lo, hi, 7, sh);
     else wg_select_global([=](int64_t i) { return f64_key(x[i]); }, n, lo, hi, 7, sh);
+    DESC_STAMP(8);
     if (tid != 0) return;
     auto get = [&](int64_t j) {
         uint64_t r = 0;
@@ -1550,6 +1578,9 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
         d.has_nonzero = 0;
     }
     *out = d;
+#ifdef FZ_DESC_TIMING
+    if (blockIdx.x == 0) g_desc_t[9] = wall_clock64();
+#endif
 }
 
 uint64_t *sorted_keys_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n) {

@@ -240,7 +240,12 @@ def host_many(*ts):
     dev = [t for t in ts if isinstance(t, torch.Tensor) and t.is_cuda]
     if not dev:
         return [t.numpy().copy() if isinstance(t, torch.Tensor) else np.asarray(t) for t in ts]
-    flat = [t.contiguous().reshape(-1).view(torch.uint8) for t in dev]
+    def flat1(t):  # (1-D, unit stride: a one-element column slice can keep its row stride)
+        x = t.reshape(-1)
+        if x.stride(0) != 1 or not x.numel():
+            x = torch.empty(x.numel(), dtype=x.dtype, device=x.device).copy_(x)
+        return x.view(torch.uint8)
+    flat = [flat1(t) for t in dev]
     h = torch.cat(flat).cpu().numpy()
     out, o, k = [], 0, 0
     for t in ts:
