@@ -1322,13 +1322,27 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
                 }
         }
     });
+    // (the slots' wave reductions two at a time, interleaved: independent shuffle chains)
 #pragma unroll
-    for (int q = 0; q < kSelMaxT; ++q) {
-        if (q >= nwide) break;  // (uniform)
-        const uint64_t a = wave_min(wlo[q]), b = wave_max(whi[q]);
-        if (lane == 0) {
-            atomicMin(&sh.wlo[q], (unsigned long long)a);
-            atomicMax(&sh.whi[q], (unsigned long long)b);
+    for (int q0 = 0; q0 < kSelMaxT; q0 += 2) {
+        if (q0 < nwide) {  // (uniform)
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint64_t a0 = __shfl_xor(wlo[q0], off, 64), b0 = __shfl_xor(whi[q0], off, 64);
+                const uint64_t a1 = __shfl_xor(wlo[q0 + 1], off, 64), b1 = __shfl_xor(whi[q0 + 1], off, 64);
+                wlo[q0] = a0 < wlo[q0] ? a0 : wlo[q0];
+                whi[q0] = b0 > whi[q0] ? b0 : whi[q0];
+                wlo[q0 + 1] = a1 < wlo[q0 + 1] ? a1 : wlo[q0 + 1];
+                whi[q0 + 1] = b1 > whi[q0 + 1] ? b1 : whi[q0 + 1];
+            }
+            if (lane == 0) {
+                atomicMin(&sh.wlo[q0], (unsigned long long)wlo[q0]);
+                atomicMax(&sh.whi[q0], (unsigned long long)whi[q0]);
+                if (q0 + 1 < nwide) {
+                    atomicMin(&sh.wlo[q0 + 1], (unsigned long long)wlo[q0 + 1]);
+                    atomicMax(&sh.whi[q0 + 1], (unsigned long long)whi[q0 + 1]);
+                }
+            }
         }
     }
     __syncthreads();
@@ -1387,27 +1401,37 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
                 if (k >= al[t] && k <= ah[t]) atomicAdd(&sh.cnt[t * kSlice + sel_bucket(k, al[t], asc[t], anb[t])], 1u);
         });
         __syncthreads();
+        static_assert(kSlice == kWave * (kSlice / kWave), "a slice is a whole number of lanes' runs");
         if (w < kSelMaxT && sh.wact[w]) {  // wave w: the sub-bucket holding target w's rank
-            const int64_t r = sh.wr[w];
+            // lane l sums its run of kSlice / 64 sub-buckets, ONE 32-bit wave scan over the runs,
+            // the lane whose run holds the rank walks it (instead of a dependent scan per 64)
+            constexpr int RUN = kSlice / kWave;
+            const uint32_t r = uint32_t(sh.wr[w]);
             const int nb2 = sh.wc[w] < kSlice ? int(sh.wc[w]) : kSlice;
-            int64_t base = 0;
-            for (int c0 = 0; c0 < nb2; c0 += 64) {
-                const int j = c0 + lane;
-                const int64_t cj = j < nb2 ? int64_t(sh.cnt[w * kSlice + j]) : 0;
-                const int64_t incl = base + wave_incl_scan(cj);
-                const uint64_t hit = __ballot(j < nb2 && incl > r);
-                if (hit) {
-                    const int l = __ffsll((unsigned long long)hit) - 1;
-                    if (lane == l) {
-                        sh.wr[w] = r - (incl - cj);
-                        sh.wc[w] = cj;
-                        sh.wsb[w] = uint32_t(j);
+            uint32_t cnt[RUN], sum = 0;
+#pragma unroll
+            for (int e = 0; e < RUN; ++e) {
+                const int j = lane * RUN + e;
+                cnt[e] = j < nb2 ? sh.cnt[w * kSlice + j] : 0u;
+                sum += cnt[e];
+            }
+            const uint32_t incl = wave_incl_scan(sum);
+            const uint64_t hit = __ballot(incl > r);
+            const int l = __ffsll((unsigned long long)hit) - 1;  // (the rank is below the total)
+            if (lane == l) {
+                uint32_t before = incl - sum;
+#pragma unroll
+                for (int e = 0; e < RUN; ++e) {
+                    if (before + cnt[e] > r) {
+                        sh.wr[w] = int64_t(r - before);
+                        sh.wc[w] = int64_t(cnt[e]);
+                        sh.wsb[w] = uint32_t(lane * RUN + e);
                         sh.wlo[w] = ~0ull;
                         sh.whi[w] = 0ull;
+                        break;
                     }
-                    break;
+                    before += cnt[e];
                 }
-                base = __shfl(incl, 63, 64);
             }
         }
         __syncthreads();
