@@ -46,10 +46,14 @@ def main():
         row = {"sample": name, "n": len(a), "ok": bool(ok), "us": round(ms / max(launches, 1) * 1e3, 2)}
         if timing:
             import ctypes as C
-            buf = (C.c_ulonglong * 16)()
+            buf = (C.c_ulonglong * 32)()
             eng.lib.fz_debug_desc_timing(buf)
-            t = [int(v) for v in buf[:10]]
+            t = [int(v) for v in buf[:32]]
             row["phase_us"] = [round((t[i] - t[i - 1]) / 100.0, 2) for i in range(1, 10)]
+            # every stamp relative to the start (us; stamps 10-13 inside the first selection step,
+            # 16-21 / 22-27 the first two refinement rounds; stale values from earlier samples
+            # where a phase did not run)
+            row["stamps_us"] = {i: round((t[i] - t[0]) / 100.0, 2) for i in range(1, 32) if t[i] >= t[0]}
         print(json.dumps(row), flush=True)
     eng.close()
 

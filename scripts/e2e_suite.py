@@ -49,9 +49,15 @@ def main():
     pending = []
     per = {}
     with open(os.path.join(work, "stdout.txt"), "w") as out, contextlib.redirect_stdout(out):
+        errors = {}
         for name in scripts.SCRIPTS:
             ts = time.perf_counter()
-            scripts.run(name, eng, tab, cwd=work, figures=not args.no_figures, pending=pending)
+            try:
+                scripts.run(name, eng, tab, cwd=work, figures=not args.no_figures, pending=pending)
+            except Exception as e:  # noqa: BLE001 - the reference script raises the same on such a table
+                # (e.g. rq1_detection_rate.py's percentage of linked issues on a table without
+                # issues: ZeroDivisionError, exit status 1) - record it and go on, as run_all does
+                errors[name] = type(e).__name__
             per[name] = round(time.perf_counter() - ts, 3)
     tf = time.perf_counter()
     for p in pending:
@@ -63,7 +69,7 @@ def main():
     print(json.dumps({"config": args.config, "rows": rows, "figures": not args.no_figures,
                       "total_s": round(total, 3), "rows_per_s": round(rows / total, 1),
                       **{k: round(v, 3) for k, v in times.items()}, "scripts_s": per,
-                      "files_written": nfiles, "reference_suite_s": 379.0,
+                      "files_written": nfiles, "script_errors": errors, "reference_suite_s": 379.0,
                       "speedup_vs_reference": round(379.0 / total, 1)}), flush=True)
 
 

@@ -1209,11 +1209,11 @@ __device__ inline void sel_for(int64_t n, const Load &load, const Body &body) {
 
 #ifdef FZ_DESC_TIMING
 // experiment builds only: wall-clock (100 MHz) phase stamps of the last k_describe_sel workgroup 0
-__device__ unsigned long long g_desc_t[16];
+__device__ unsigned long long g_desc_t[32];
 #define DESC_STAMP(ph)                                                       \
     do {                                                                     \
         __syncthreads();                                                     \
-        if (threadIdx.x == 0 && blockIdx.x == 0) g_desc_t[ph] = wall_clock64(); \
+        if (threadIdx.x == 0 && blockIdx.x == 0) g_desc_t[ph] = wall_clock64();     \
     } while (0)
 extern "C" int fz_debug_desc_timing(unsigned long long *out) {
     hipDeviceSynchronize();
@@ -1260,6 +1260,7 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
         if (tid == 0) sh.cnt[nb] = uint32_t(n);
     }
     __syncthreads();
+    DESC_STAMP(10);
     if (tid < nt) {
         const uint32_t r = uint32_t(sh.rank[tid]);
         int l0 = 0, h0 = nb - 1;
@@ -1273,6 +1274,7 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
         sh.tsz[tid] = int64_t(sh.cnt[l0 + 1]) - int64_t(sh.cnt[l0]);
     }
     __syncthreads();
+    DESC_STAMP(11);
     if (tid == 0) {  // list slots of the narrow buckets (map 0..), slots of the distinct wide ones (0x80 | w)
         int used = 0, wide = 0;
         for (int t = 0; t < nt; ++t) {
@@ -1300,6 +1302,7 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
         sh.nwide = wide;
     }
     __syncthreads();
+    DESC_STAMP(12);
     // one pass: the narrow buckets' keys gathered, the wide buckets' key ranges (a wide bucket of
     // one key - ties - needs nothing more)
     const int nwide = sh.nwide;
@@ -1322,6 +1325,7 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
                 }
         }
     });
+    DESC_STAMP(13);
     // (the slots' wave reductions two at a time, interleaved: independent shuffle chains)
 #pragma unroll
     for (int q0 = 0; q0 < kSelMaxT; q0 += 2) {
@@ -1377,7 +1381,22 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
         const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(x)), h = __builtin_amdgcn_readfirstlane(uint32_t(x >> 32));
         return (uint64_t(h) << 32) | l;
     };
+#ifdef FZ_DESC_TIMING
+    int round = 0;
+#endif
     for (;;) {
+#ifdef FZ_DESC_TIMING
+        const int rs = round < 2 ? 16 + 6 * round : -1;
+        ++round;
+#define RSTAMP(k) \
+    do {          \
+        if (rs >= 0) DESC_STAMP(rs + (k)); \
+    } while (0)
+#else
+#define RSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
         uint64_t al[kSelMaxT], ah[kSelMaxT];
         double asc[kSelMaxT];
         int anb[kSelMaxT];
@@ -1392,15 +1411,18 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
             asc[t] = act ? __builtin_bit_cast(double, uni64(__builtin_bit_cast(uint64_t, double(anb[t]) / (double(ah[t] - al[t]) + 1.0)))) : 0.0;
         }
         if (!any) break;  // (uniform)
+        RSTAMP(0);
         if (tid < kSelMaxT) sh.wact[tid] = tid < nt && sh.wl[tid] != sh.wh[tid] && sh.wc[tid] > 64;
         for (int j = tid; j < kSelNB; j += BS) sh.cnt[j] = 0u;
         __syncthreads();
+        RSTAMP(1);
         sel_for<4>(n, key, [&](int64_t, uint64_t k) {
 #pragma unroll
             for (int t = 0; t < kSelMaxT; ++t)
                 if (k >= al[t] && k <= ah[t]) atomicAdd(&sh.cnt[t * kSlice + sel_bucket(k, al[t], asc[t], anb[t])], 1u);
         });
         __syncthreads();
+        RSTAMP(2);
         static_assert(kSlice == kWave * (kSlice / kWave), "a slice is a whole number of lanes' runs");
         if (w < kSelMaxT && sh.wact[w]) {  // wave w: the sub-bucket holding target w's rank
             // lane l sums its run of kSlice / 64 sub-buckets, ONE 32-bit wave scan over the runs,
@@ -1435,6 +1457,7 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
             }
         }
         __syncthreads();
+        RSTAMP(3);
         uint32_t asb[kSelMaxT];
 #pragma unroll
         for (int t = 0; t < kSelMaxT; ++t) asb[t] = al[t] <= ah[t] ? __builtin_amdgcn_readfirstlane(sh.wsb[t]) : 0u;
@@ -1448,12 +1471,15 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
                 }
         });
         __syncthreads();
+        RSTAMP(4);
         if (tid < kSelMaxT && sh.wact[tid]) {
             sh.wl[tid] = sh.wlo[tid];
             sh.wh[tid] = sh.whi[tid];
         }
         __syncthreads();
+        RSTAMP(5);
     }
+#undef RSTAMP
     DESC_STAMP(7);
     // one key left (ties): the result; else <= 64 values in [wl, wh]: one gather for all, ranked
     bool gather = false;

@@ -2126,23 +2126,29 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
                         if (tid + int64_t(m) * BS < n && k[m] >= rlo && k[m] <= rhi)
                             atomicAdd(&s_cnt[bucket(k[m], rlo, sc2, nb2)], 1u);
                     __syncthreads();
-                    if (w == 0) {  // the sub-bucket holding rank r: wave 0 walks 64 buckets per step
-                        int64_t base = 0;
-                        for (int c0 = 0; c0 < nb2; c0 += 64) {
-                            const int j = c0 + lane;
-                            const int64_t cj = j < nb2 ? int64_t(s_cnt[j]) : 0;
-                            const int64_t incl = base + wave_incl_scan(cj);
-                            const uint64_t hit = __ballot(j < nb2 && incl > r);
-                            if (hit) {
-                                const int l = __ffsll((unsigned long long)hit) - 1;
-                                if (lane == l) {
-                                    s_r = r - (incl - cj);
-                                    s_rc = cj;
-                                    s_cnt[NB] = uint32_t(j);
+                    {  // the sub-bucket holding rank r: thread t sums buckets [t * BPT, t * BPT + BPT),
+                       // one block scan, the thread whose run holds r walks it (not a dependent wave
+                       // scan per 64 buckets)
+                        uint32_t cb[BPT], sum = 0;
+#pragma unroll
+                        for (int e = 0; e < BPT; ++e) {
+                            const int j = tid * BPT + e;
+                            cb[e] = j < nb2 ? s_cnt[j] : 0u;
+                            sum += cb[e];
+                        }
+                        const uint32_t run = block_excl_scan<uint32_t, NW>(sum, s_tmp, (uint32_t *)nullptr);
+                        const uint32_t rr = uint32_t(r);
+                        if (rr >= run && rr < run + sum) {
+                            uint32_t before = run;
+#pragma unroll
+                            for (int e = 0; e < BPT; ++e) {
+                                if (rr >= before && rr < before + cb[e]) {
+                                    s_r = int64_t(rr - before);
+                                    s_rc = int64_t(cb[e]);
+                                    s_cnt[NB] = uint32_t(tid * BPT + e);
                                 }
-                                break;
+                                before += cb[e];
                             }
-                            base = __shfl(incl, 63, 64);
                         }
                     }
                     __syncthreads();
