@@ -49,6 +49,9 @@ for s in $STEPS; do
       extra=""; [ $kind = fs1 ] && extra="--shard-groups rq3,rq4b,rq2_count,rq1,rq4a,rq2_add"
       timeout -k 10 600 python -u bench.py --config $arg --steps $st --warmup 2 --no-cpu-baseline --probe-steps 0 --force-sharded $extra > $O/${T}_${kind}_$arg.json 2> $O/${T}_${kind}_$arg.err || exit $?
       python3 -c "import json; d=json.loads([l for l in open('$O/${T}_${kind}_$arg.json') if l.startswith('{')][-1]); print('$kind $arg', d['ms_per_step'], d['config'].get('driver_host_ms'), flush=True)" ;;
+    sprobe)  # the store build's host vs GPU time
+      timeout -k 10 300 python -u scripts/store_probe.py --config $arg > $O/${T}_sprobe_$arg.txt 2>&1 || exit $?
+      grep '^{' $O/${T}_sprobe_$arg.txt ;;
     dmicro)  # describe-by-selection micro-benchmark (default build; phase stamps from the timing variant)
       timeout -k 10 200 python -u scripts/describe_micro.py > $O/${T}_dmicro.txt 2>&1 || exit $?
       V=tse-replication-package-1-million-fuzzing-sessions_amd/csrc/build/variants/libfz_desctime.so

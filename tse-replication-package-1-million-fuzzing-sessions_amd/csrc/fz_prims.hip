@@ -1238,11 +1238,22 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
     }
     const int nb = n < kSelNB ? int(n) : kSelNB;
     const double sc = double(nb) / (double(hi - lo) + 1.0);
+    // first level linear in VALUE when the range is finite (then a bucket rarely holds more than a
+    // few distinct values: integer data - ties - gets one value per bucket, dense centres spread),
+    // else linear in key; either is monotone in the key order, so a bucket is a key interval
+    const double vlo = f64_from_key(lo), vhi = f64_from_key(hi);
+    const bool vlin = isfinite(vlo) && isfinite(vhi) && isfinite(vhi - vlo) && vhi > vlo;
+    const double vsc = vlin ? double(nb) / (vhi - vlo) : 0.0;
+    auto bucket1 = [&](uint64_t k) -> uint32_t {
+        if (!vlin) return sel_bucket(k, lo, sc, nb);
+        const double q = (f64_from_key(k) - vlo) * vsc;  // (>= 0; NaN keys lie above hi: not here)
+        return q < double(nb - 1) ? uint32_t(q) : uint32_t(nb - 1);
+    };
     for (int j = tid; j <= nb; j += BS) sh.cnt[j] = 0u;
     for (int j = tid; j < nb; j += BS) sh.map[j] = 0xff;
     __syncthreads();
     DESC_STAMP(3);
-    sel_for(n, key, [&](int64_t, uint64_t k) { atomicAdd(&sh.cnt[sel_bucket(k, lo, sc, nb)], 1u); });
+    sel_for(n, key, [&](int64_t, uint64_t k) { atomicAdd(&sh.cnt[bucket1(k)], 1u); });
     __syncthreads();
     DESC_STAMP(4);
     {  // exclusive scan of the bucket counts: thread t takes buckets [t * 4, t * 4 + 4)
@@ -1313,7 +1324,7 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
         whi[q] = 0ull;
     }
     sel_for<4>(n, key, [&](int64_t, uint64_t k) {
-        const uint8_t slot = sh.map[sel_bucket(k, lo, sc, nb)];
+        const uint8_t slot = sh.map[bucket1(k)];
         if (slot < 0x80) {
             sh.list[slot][atomicAdd(&sh.fill[slot], 1u)] = k;
         } else if (slot != 0xff) {
@@ -1466,8 +1477,10 @@ __device__ void wg_select_global(const KeyF &key, int64_t n, uint64_t lo, uint64
 #pragma unroll
             for (int t = 0; t < kSelMaxT; ++t)
                 if (k >= al[t] && k <= ah[t] && sel_bucket(k, al[t], asc[t], anb[t]) == asb[t]) {
-                    atomicMin(&sh.wlo[t], (unsigned long long)k);
-                    atomicMax(&sh.whi[t], (unsigned long long)k);
+                    // (ties: once a bound holds the key, its copies only read - no serialised
+                    // atomics on one word)
+                    if (k < sh.wlo[t]) atomicMin(&sh.wlo[t], (unsigned long long)k);
+                    if (k > sh.whi[t]) atomicMax(&sh.whi[t], (unsigned long long)k);
                 }
         });
         __syncthreads();

@@ -2017,10 +2017,20 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
             uint32_t q = uint32_t(double(key - klo) * sc);
             return q < uint32_t(nbk) ? q : uint32_t(nbk - 1);
         };
+        // the first level linear in VALUE when the range is finite (coverage percentages: dense
+        // centres spread, repeated values one per bucket), else in key - monotone either way
+        const double vlo = f64_from_key(lo), vhi = f64_from_key(hi);
+        const bool vlin = isfinite(vlo) && isfinite(vhi) && isfinite(vhi - vlo) && vhi > vlo;
+        const double vsc = vlin ? double(nb) / (vhi - vlo) : 0.0;
+        auto bucket1 = [&](uint64_t key) -> uint32_t {
+            if (!vlin) return bucket(key, lo, scale, nb);
+            const double q = (f64_from_key(key) - vlo) * vsc;
+            return q < double(nb - 1) ? uint32_t(q) : uint32_t(nb - 1);
+        };
         if (lo != hi) {
 #pragma unroll
             for (int m = 0; m < IPT; ++m)
-                if (tid + int64_t(m) * BS < n) atomicAdd(&s_cnt[bucket(k[m], lo, scale, nb)], 1u);
+                if (tid + int64_t(m) * BS < n) atomicAdd(&s_cnt[bucket1(k[m])], 1u);
             __syncthreads();
             // bucket starts: thread t scans buckets [t * BPT, t * BPT + BPT)
             uint32_t sum = 0;
@@ -2070,7 +2080,7 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
 #pragma unroll
             for (int m = 0; m < IPT; ++m) {
                 if (tid + int64_t(m) * BS < n) {
-                    const uint8_t slot = s_map[bucket(k[m], lo, scale, nb)];
+                    const uint8_t slot = s_map[bucket1(k[m])];
                     if (slot != 0xff) s_list[slot][atomicAdd(&s_fill[slot], 1u)] = k[m];
                 }
             }
@@ -2097,7 +2107,7 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
                 uint64_t rlo = ~0ull, rhi = 0ull;
 #pragma unroll
                 for (int m = 0; m < IPT; ++m)
-                    if (tid + int64_t(m) * BS < n && bucket(k[m], lo, scale, nb) == tb) {
+                    if (tid + int64_t(m) * BS < n && bucket1(k[m]) == tb) {
                         rlo = k[m] < rlo ? k[m] : rlo;
                         rhi = k[m] > rhi ? k[m] : rhi;
                     }
