@@ -118,6 +118,9 @@ int fz_ctx_create(int device, void *stream, fz_ctx **out) {
             throw fz::Error(FZ_E_DEVICE, "fz_ctx_create: hipHostMalloc failed");
         }
         c->h_pinned = static_cast<int64_t *>(h);
+        void *dh = nullptr;
+        FZ_HIP(hipHostGetDevicePointer(&dh, h, 0));
+        c->d_pinned = static_cast<int64_t *>(dh);
         *out = c;
         return FZ_OK;
     } catch (const fz::Error &e) {
@@ -144,6 +147,9 @@ int fz_ctx_create_child(fz_ctx *parent, void *stream, fz_ctx **out) {
             throw fz::Error(FZ_E_DEVICE, "fz_ctx_create_child: hipHostMalloc failed");
         }
         c->h_pinned = static_cast<int64_t *>(h);
+        void *dh = nullptr;
+        FZ_HIP(hipHostGetDevicePointer(&dh, h, 0));
+        c->d_pinned = static_cast<int64_t *>(dh);
         *out = c;
         return FZ_OK;
     } catch (const fz::Error &e) {

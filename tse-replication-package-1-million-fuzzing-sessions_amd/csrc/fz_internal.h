@@ -228,10 +228,12 @@ struct fz_ctx {
     fz::Store store;
     fz::Probe probe;
     int64_t *h_pinned = nullptr;   // small pinned host staging area (32 KiB)
+    int64_t *d_pinned = nullptr;   // the same area's device address (kernels write read-backs straight to it)
     // decoupled look-back state (fz_lookback.h; single-pass scan, compaction, radix passes): status
     // words tagged with a per-launch epoch, and a tile ticket counter each launch resets itself
     fz::DevBuf os_status;          // uint64 [max words of one launch]
     fz::DevBuf os_ticket;          // uint32 [4] self-resetting tile counters
+    bool lb_pending = false;       // a look-back reset is owed (the next fill batch or look-back use runs it)
     unsigned int os_epoch = 0;
     // radix digit totals, two buffers used by alternate sorts: each sort's passes zero the other
     // one, so the next sort's histogram starts from zero without a memset launch

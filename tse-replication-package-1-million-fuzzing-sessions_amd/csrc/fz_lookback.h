@@ -32,8 +32,11 @@ inline void lookback_end(fz_ctx *, int64_t) {}
 // The same for k <= 4 look-back passes run side by side in ONE launch: out[j] gets its own status
 // words (words[j]) and its own ticket counter.
 Lookback lookback_begin_n(fz_ctx *c, const int64_t *words, int k, Lookback *out);
-// Enqueue a reset of the ticket and the status words (device) and of the host base / epoch.
+// Reset the host epoch now and owe the device reset of the ticket and the status words: the
+// context's next fill_batch zeroes them with its own regions, else the next lookback_begin launches
+// the reset first (lookback_flush).
 void lookback_reset(fz_ctx *c);
+void lookback_flush(fz_ctx *c);
 
 // Thread 0 of a workgroup: this workgroup's tile index (in start order); the last tile of the
 // launch (ntiles workgroups) resets the counter for the next launch.

@@ -13,7 +13,7 @@ namespace fz {
 
 void sync(fz_ctx *c) { FZ_HIP(hipStreamSynchronize(c->stream)); }
 
-constexpr int kMaxFills = 16;
+constexpr int kMaxFills = 18;
 struct FillList {
     int n;
     unsigned char *ptr[kMaxFills];
@@ -79,6 +79,20 @@ void fill_copy_batch(fz_ctx *c, std::initializer_list<Fill> regions, const void 
             f.word_in_fill = 1;
         }
         ++f.n;
+    }
+    if (c->lb_pending && f.n + 2 <= kMaxFills) {
+        // an owed look-back reset (lookback_reset) rides along: the tickets and status words are two
+        // more zero regions
+        c->lb_pending = false;
+        const Fill owed[2] = {{c->os_ticket.ptr, int64_t(c->os_ticket.cap), 0}, {c->os_status.ptr, int64_t(c->os_status.cap), 0}};
+        for (const Fill &r : owed) {
+            if (!r.ptr || r.bytes <= 0) continue;
+            f.ptr[f.n] = static_cast<unsigned char *>(r.ptr);
+            f.bytes[f.n] = r.bytes;
+            f.value[f.n] = 0;
+            most = r.bytes > most ? r.bytes : most;
+            ++f.n;
+        }
     }
     if (f.n == 0 && f.copy_n == 0 && !word_dst) return;
     k_fill_batch<<<grid_for((most + 7) / 8, kBlock, 1024), kBlock, 0, c->stream>>>(f);
@@ -221,6 +235,7 @@ static bool trace_on() {
 }
 
 Lookback lookback_begin(fz_ctx *c, int64_t words) {
+    if (c->lb_pending) lookback_flush(c);
     if (c->os_status.cap < size_t(words < 1 ? 1 : words) * 8) {
         uint64_t *st = c->os_status.ensure<uint64_t>(words);
         dev_fill(c, st, 0, int64_t(c->os_status.cap));
@@ -261,13 +276,19 @@ __global__ __launch_bounds__(kBlock) void k_lb_reset(unsigned int *__restrict__ 
         status[i] = 0ull;
 }
 
+// The reset is owed rather than launched: the context's next fill batch carries it (two more zero
+// regions, one launch fewer at the head of a recording), else the next look-back use launches it.
 void lookback_reset(fz_ctx *c) {
+    c->lb_pending = true;
+    c->os_epoch = 0;
+}
+void lookback_flush(fz_ctx *c) {
+    c->lb_pending = false;
     const int64_t words = int64_t(c->os_status.cap / 8);
     if (!c->os_ticket.cap && !words) return;
     k_lb_reset<<<grid_for(words, kBlock, 2048), kBlock, 0, c->stream>>>(
         c->os_ticket.cap ? c->os_ticket.as<unsigned int>() : nullptr, c->os_status.as<uint64_t>(), words);
     FZ_LAUNCH_CHECK();
-    c->os_epoch = 0;
 }
 
 // Single-pass exclusive scan: 4096-element tiles, tile prefixes by decoupled look-back

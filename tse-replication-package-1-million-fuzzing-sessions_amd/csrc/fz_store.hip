@@ -67,17 +67,40 @@ __global__ __launch_bounds__(kBlock) void k_store_prologue(const int64_t *__rest
 // read off the prefix offsets - a view is a contiguous range of one table's prefixes, and the time
 // sorts (merge sort included) keep every row in its prefix's range - their longest segments
 // (out[0..3]), a copy of the 9 store counters (out[4..12]: merge-sort rows and longest segment
-// per table, rows the long bucket class gathered per table) and the views' row counts (out[13..16]):
-// one launch and one D2H copy.  A view starts at its first prefix's offset (the builds' Coverage
-// view after all Fuzzing rows), read here rather than counted beforehand.
+// per table, rows the long bucket class gathered per table), the views' row counts (out[13..16])
+// and the issue-number range off the prologue's partials (out[17..18]), written straight to the
+// pinned read-back area: one launch, no copy.  A view starts at its first prefix's offset (the
+// builds' Coverage view after all Fuzzing rows), read here rather than counted beforehand.
 struct ViewSrc {
     const int64_t *src[4] = {};  // prefix offsets of the view's table (null: empty table)
     int64_t first[4] = {};       // prefix of the view's project 0
     int64_t *dst[4] = {};        // [P + 1]
     const unsigned long long *big = nullptr;  // [9] merge-sort rows / longest segment / fused rows
 };
-__global__ __launch_bounds__(kSortBlock) void k_store_views(const ViewSrc v, int64_t P, int64_t *__restrict__ out) {
+__global__ __launch_bounds__(kSortBlock) void k_store_views(const ViewSrc v, int64_t P, const int64_t *__restrict__ part,
+                                                           int pblk, int64_t *__restrict__ out) {
     __shared__ int64_t s_m[kSortBlock / kWave];
+    __shared__ int64_t s_n[2][kSortBlock / kWave];
+    {  // the prologue's issue-number partials: min (out[17]) and max (out[18])
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        for (int b = threadIdx.x; b < pblk; b += kSortBlock) {
+            const int64_t l = part[4 * b + 2], h = part[4 * b + 3];
+            lo = l < lo ? l : lo;
+            hi = h > hi ? h : hi;
+        }
+        lo = wave_min(lo);
+        hi = wave_max(hi);
+        if (lane_id() == 0) s_n[0][wave_id()] = lo, s_n[1][wave_id()] = hi;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < kSortBlock / kWave; ++w) {
+                lo = s_n[0][w] < lo ? s_n[0][w] : lo;
+                hi = s_n[1][w] > hi ? s_n[1][w] : hi;
+            }
+            out[17] = lo;
+            out[18] = hi;
+        }
+    }
     for (int i = 0; i < 4; ++i) {
         const int64_t *src = v.src[i];
         const int64_t base = src ? src[v.first[i]] : 0;  // rows of the table before the view
@@ -1133,11 +1156,10 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         vs.dst[i] = voff[i]->ensure<int64_t>(P + 1);
     }
     vs.big = big3;
-    int64_t *mx = c->arena.get<int64_t>(17);
-    k_store_views<<<1, kSortBlock, 0, c->stream>>>(vs, P, mx);
+    // (written straight into the pinned read-back area through its device address: two blit copies
+    // fewer in front of the gather and the host's wake-up)
+    k_store_views<<<1, kSortBlock, 0, c->stream>>>(vs, P, ppart, pblk, c->d_pinned);
     FZ_LAUNCH_CHECK();
-    FZ_HIP(hipMemcpyAsync(c->h_pinned, mx, 17 * 8, hipMemcpyDeviceToHost, c->stream));
-    FZ_HIP(hipMemcpyAsync(c->h_pinned + 64, ppart, size_t(4 * pblk) * 8, hipMemcpyDeviceToHost, c->stream));
     if (!c->ev_readback) FZ_HIP(hipEventCreateWithFlags(&c->ev_readback, hipEventDisableTiming));
     FZ_HIP(hipEventRecord(c->ev_readback, c->stream));
     // the gather of the short classes' rows, launched before the host reads the counters (rows of
@@ -1145,15 +1167,9 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     // host's round trip overlaps it
     gather_tables(c, pss);
     FZ_HIP(hipEventSynchronize(c->ev_readback));
-    int64_t nlo = INT64_MAX, nhi = INT64_MIN;
-    for (int k = 0; k < pblk; ++k) {
-        const int64_t *q = c->h_pinned + 64 + 4 * k;
-        nlo = q[2] < nlo ? q[2] : nlo;
-        nhi = q[3] > nhi ? q[3] : nhi;
-    }
     // (no non-NULL number: the empty range min = INT64_MAX > max = INT64_MIN, as the old read-back gave)
-    s.num_min = nlo;
-    s.num_max = nhi;
+    s.num_min = c->h_pinned[17];
+    s.num_max = c->h_pinned[18];
     const int64_t maxseg[4] = {c->h_pinned[0], c->h_pinned[1], c->h_pinned[2], c->h_pinned[3]};
     const int64_t bigrows[3] = {c->h_pinned[4], c->h_pinned[5], c->h_pinned[6]};
     const int64_t bigmax[3] = {c->h_pinned[7], c->h_pinned[8], c->h_pinned[9]};
