@@ -254,6 +254,31 @@ int fz_runs_merge(fz_ctx *ctx, const double *values, const int64_t *run_sizes, i
  * out[0..3] = rho, p, W, p (NaN where scipy returns NaN: n < 2 / constant, n < 3). */
 int fz_series_tests(fz_ctx *ctx, const double *x, int64_t n, double *out);
 
+/* Read-back of many small device arrays at once (the sharded drivers' per-step host reads): piece i
+ * copies n elements of elem_bytes (1, 2, 4 or 8) bytes, `stride` elements apart, from device src to
+ * host_out + dst_offset (8-byte elements at 8-byte aligned offsets), on the current device.  One
+ * launch on `stream` writing the process's pinned staging area through its device address, one
+ * synchronisation of `stream`,
+ * then one host copy into host_out [total_bytes] - instead of a gather kernel per strided slice, a
+ * concatenation and a blit copy.  (No reference counterpart: the reference is one process.) */
+typedef struct fz_host_piece {
+    const void *src;
+    int64_t n;
+    int64_t stride;
+    int64_t dst_offset;
+    int32_t elem_bytes;
+    int32_t pad_;
+} fz_host_piece;
+int fz_gather_to_host(void *stream, const fz_host_piece *pieces, int n_pieces, void *host_out, int64_t total_bytes);
+
+/* The sharded RQ2-count tail in one call (rq2_coverage_count.py:335-372): fz_series_tests of the
+ * first k entries of the gathered median trend (the sessions with >= 100 values) -> out[0..3], and
+ * the mean / median of the per-project correlations of eligible projects with raw_n > 0 and a
+ * non-NaN correlation (n_projects entries each, device) -> out[4], out[5] (NaN when none).  Device
+ * in, device out, no host read. */
+int fz_rq2_count_tail(fz_ctx *ctx, const double *median_trend, int64_t k, const double *corr, const int64_t *raw_n,
+                      const int64_t *eligible, int64_t n_projects, double *out);
+
 /* scipy.stats.spearmanr(range(n_s), x_s) of S device series at once (segment s = x[offs[s],
  * offs[s+1]), n = offs[S] values, max_len a host bound of one segment, 0 if unknown): rho[s], p[s]
  * (NaN where scipy returns NaN).  Replaces the per-sequence calls of rq4b_coverage.py:879-899 on the
@@ -462,6 +487,20 @@ int fz_rq4b_trends(fz_ctx *ctx, const int64_t *c2, const int64_t *c1, const doub
  * out[FZ_RQ4B_MWU_P .. FZ_RQ4B_LEVENE_P] = mannwhitneyu two-sided p, Cliff's delta from
  * mannwhitneyu(greater) U1, brunnermunzel statistic / p, levene W / p. */
 int fz_two_sample_tests(fz_ctx *ctx, const double *x, int64_t nx, const double *y, int64_t ny, double *out);
+
+/* The sharded RQ4b tail in one call, after the session exchange and the gathers (the statistics
+ * fz_rq4b computes after its session tables, rq4b_coverage.py:725-797, :849-899, :221-313):
+ * fz_rq4b_trends over n_sessions per-session rows -> *last, spearman6; the n_delta delta columns
+ * (pre_cov / post_cov [7 * n_delta], row-major: window i of column q at i * n_delta + q) put in CSV
+ * order by their keys delta_order[n_delta] (distinct, < n_order) -> pre_out / post_out (same
+ * layout), with statistics.median of each of the 14 rows -> medians14 (pre rows, then post; NaN when
+ * n_delta == 0); fz_two_sample_tests(init_g2, init_g1) -> tests (NaN unless both are non-empty).
+ * Device in, device out, no host read. */
+int fz_rq4b_tail(fz_ctx *ctx, const int64_t *c2, const int64_t *c1, const double *g2_q, const double *g1_q,
+                 int64_t n_sessions, const int64_t *delta_order, const double *pre_cov, const double *post_cov,
+                 int64_t n_delta, int64_t n_order, const double *init_g2, int64_t n2, const double *init_g1, int64_t n1,
+                 int64_t *last, double *spearman6, double *pre_out, double *post_out, double *medians14,
+                 double *tests);
 
 /* ---- build-log analysis ------------------------------------------
  * Replaces buildlog_analysis(row) of program/preparation/4_get_buildlog_analysis.py:14-246 for a

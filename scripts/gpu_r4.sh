@@ -49,6 +49,14 @@ for s in $STEPS; do
       extra=""; [ $kind = fs1 ] && extra="--shard-groups rq3,rq4b,rq2_count,rq1,rq4a,rq2_add"
       timeout -k 10 600 python -u bench.py --config $arg --steps $st --warmup 2 --no-cpu-baseline --probe-steps 0 --force-sharded $extra > $O/${T}_${kind}_$arg.json 2> $O/${T}_${kind}_$arg.err || exit $?
       python3 -c "import json; d=json.loads([l for l in open('$O/${T}_${kind}_$arg.json') if l.startswith('{')][-1]); print('$kind $arg', d['ms_per_step'], d['config'].get('driver_host_ms'), flush=True)" ;;
+    profs)  # kernel trace of a serial step over some stages: profs:<cfg>@<stages>
+      cfg=${arg%%@*}; sts=${arg#*@}
+      timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/${T}_profs_$cfg -o run -- python3 -u bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline --probe-steps 0 --serial --stages $sts > $O/${T}_profs_$cfg.log 2>&1 || exit $?
+      echo "profs $cfg $sts ok" ;;
+    envb)  # bench line under one runtime environment variable: envb:<cfg>@VAR=VALUE
+      cfg=${arg%%@*}; kv=${arg#*@}; st=20; [ "$cfg" != c2 ] && st=5
+      env "$kv" timeout -k 10 600 python -u bench.py --config $cfg --steps $st --warmup 2 --no-cpu-baseline > $O/${T}_envb.json 2> $O/${T}_envb.err || exit $?
+      python3 -c "import json; d=json.loads([l for l in open('$O/${T}_envb.json') if l.startswith('{')][-1]); print('envb $cfg $kv', d['ms_per_step'], flush=True)" ;;
     fsprof)  # the sharded step at world 1 under cProfile (host time per function; pstats offline)
       timeout -k 10 600 python -u -m cProfile -o $O/${T}_fsprof_$arg.prof bench.py --config $arg --steps 100 --warmup 2 --no-cpu-baseline --probe-steps 0 --force-sharded > $O/${T}_fsprof_$arg.json 2> $O/${T}_fsprof_$arg.err || exit $?
       python3 -c "import pstats; pstats.Stats('$O/${T}_fsprof_$arg.prof').sort_stats('tottime').print_stats(25)" > $O/${T}_fsprof_$arg.txt && head -60 $O/${T}_fsprof_$arg.txt ;;

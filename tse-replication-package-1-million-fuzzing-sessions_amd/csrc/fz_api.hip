@@ -1,6 +1,7 @@
 // Public C ABI (include/fz.h): error capture, context lifetime, and thin wrappers that reset the
 // scratch arena and forward to the implementation.
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "fz_internal.h"
@@ -39,6 +40,12 @@ void rq4b_trends(fz_ctx *c, const int64_t *c2, const int64_t *c1, const double *
                  int64_t *last, double *sp);
 void two_sample_tests(fz_ctx *c, const double *a, int64_t na_cap, const int64_t *n2, const double *b,
                       int64_t nb_cap, const int64_t *n1, double *ts);
+void rq2_count_tail(fz_ctx *c, const double *median_trend, int64_t k, const double *corr, const int64_t *raw_n,
+                    const int64_t *eligible, int64_t P, double *out);
+void rq4b_tail(fz_ctx *c, const int64_t *c2, const int64_t *c1, const double *g2q, const double *g1q, int64_t M,
+               const int64_t *order, const double *pre, const double *post, int64_t nd, int64_t n_order,
+               const double *x, int64_t nx, const double *y, int64_t ny, int64_t *last, double *sp, double *pre_out,
+               double *post_out, double *med14, double *tests);
 void buildlog(fz_ctx *c, const uint8_t *text, int64_t n_bytes, const int64_t *log_offs_host, const int64_t *log_offs,
               int64_t n_logs, const fz_buildlog_out *o);
 }  // namespace fz
@@ -542,6 +549,126 @@ int fz_rq4b_trends(fz_ctx *ctx, const int64_t *c2, const int64_t *c1, const doub
         }
         fz::rq4b_trends(ctx, c2, c1, g2_q, g1_q, n_sessions, last, spearman6);
     });
+}
+
+int fz_rq2_count_tail(fz_ctx *ctx, const double *median_trend, int64_t k, const double *corr, const int64_t *raw_n,
+                      const int64_t *eligible, int64_t n_projects, double *out) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(out && k >= 0 && n_projects >= 0 && (k == 0 || median_trend) &&
+                     (n_projects == 0 || (corr && raw_n && eligible)),
+                 "fz_rq2_count_tail: bad arguments");
+        fz::rq2_count_tail(ctx, median_trend, k, corr, raw_n, eligible, n_projects, out);
+    });
+}
+
+int fz_rq4b_tail(fz_ctx *ctx, const int64_t *c2, const int64_t *c1, const double *g2_q, const double *g1_q,
+                 int64_t n_sessions, const int64_t *delta_order, const double *pre_cov, const double *post_cov,
+                 int64_t n_delta, int64_t n_order, const double *init_g2, int64_t n2, const double *init_g1, int64_t n1,
+                 int64_t *last, double *spearman6, double *pre_out, double *post_out, double *medians14,
+                 double *tests) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n_sessions >= 0 && n_delta >= 0 && n_order >= 0 && n2 >= 0 && n1 >= 0 && last && spearman6 &&
+                     medians14 && tests && (n_sessions == 0 || (c2 && c1 && g2_q && g1_q)) &&
+                     (n_delta == 0 || (delta_order && pre_cov && post_cov && pre_out && post_out)) &&
+                     n_delta <= n_order && (n2 == 0 || init_g2) && (n1 == 0 || init_g1),
+                 "fz_rq4b_tail: bad arguments");
+        fz::rq4b_tail(ctx, c2, c1, g2_q, g1_q, n_sessions, delta_order, pre_cov, post_cov, n_delta, n_order, init_g2,
+                      n2, init_g1, n1, last, spearman6, pre_out, post_out, medians14, tests);
+    });
+}
+
+// ---- fz_gather_to_host: many small device arrays -> one host buffer, one launch, one sync
+namespace {
+constexpr int kGatherPieces = 48;
+struct GatherList {
+    const unsigned char *src[kGatherPieces];
+    int64_t n[kGatherPieces];       // elements
+    int64_t stride[kGatherPieces];  // elements
+    int64_t dst[kGatherPieces];     // byte offset
+    int32_t elem[kGatherPieces];    // bytes: 1, 2, 4 or 8
+    int count;
+};
+// one row of workgroups per piece; 8-byte elements move as words, the others byte by byte
+__global__ __launch_bounds__(256) void k_gather_to_host(const GatherList g, unsigned char *__restrict__ out) {
+    const int k = blockIdx.y;
+    if (k >= g.count) return;
+    const unsigned char *src = g.src[k];
+    const int64_t n = g.n[k], st = g.stride[k];
+    const int e = g.elem[k];
+    unsigned char *dst = out + g.dst[k];
+    const int64_t step = int64_t(gridDim.x) * blockDim.x;
+    if (e == 8) {
+        for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += step)
+            reinterpret_cast<uint64_t *>(dst)[i] = reinterpret_cast<const uint64_t *>(src)[i * st];
+    } else {
+        for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n * e; i += step)
+            dst[i] = src[(i / e) * st * e + i % e];
+    }
+}
+}  // namespace
+
+int fz_gather_to_host(void *stream, const fz_host_piece *pieces, int n_pieces, void *host_out, int64_t total_bytes) {
+    // one pinned staging area for the process (mapped: kernels write it through its device address),
+    // grown on demand; the lock makes concurrent callers take turns
+    static std::mutex mu;
+    static void *h_area = nullptr, *d_area = nullptr;
+    static size_t cap = 0;
+    try {
+        FZ_CHECK(n_pieces >= 0 && total_bytes >= 0 && (n_pieces == 0 || pieces) && (total_bytes == 0 || host_out),
+                 "fz_gather_to_host: bad arguments");
+        for (int i = 0; i < n_pieces; ++i) {
+            const fz_host_piece &p = pieces[i];
+            const int e = p.elem_bytes;
+            FZ_CHECK((e == 1 || e == 2 || e == 4 || e == 8) && p.n >= 0 && p.stride >= 1 && p.dst_offset >= 0 &&
+                         p.dst_offset + p.n * e <= total_bytes && (p.n == 0 || p.src) &&
+                         (e != 8 || p.dst_offset % 8 == 0),
+                     "fz_gather_to_host: bad piece");
+        }
+        if (total_bytes == 0) return FZ_OK;
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        std::lock_guard<std::mutex> lk(mu);
+        if (size_t(total_bytes) > cap) {
+            if (h_area) {
+                FZ_HIP(hipDeviceSynchronize());
+                FZ_HIP(hipHostFree(h_area));
+                h_area = d_area = nullptr;
+                cap = 0;
+            }
+            const size_t want = size_t(total_bytes) < (size_t(1) << 20) ? (size_t(1) << 20) : size_t(total_bytes) * 2;
+            FZ_HIP(hipHostMalloc(&h_area, want, hipHostMallocMapped | hipHostMallocPortable));
+            FZ_HIP(hipHostGetDevicePointer(&d_area, h_area, 0));
+            cap = want;
+        }
+        for (int b = 0; b < n_pieces; b += kGatherPieces) {
+            GatherList g{};
+            int64_t most = 0;
+            for (int i = b; i < n_pieces && i < b + kGatherPieces; ++i) {
+                const fz_host_piece &p = pieces[i];
+                const int k = g.count++;
+                g.src[k] = static_cast<const unsigned char *>(p.src);
+                g.n[k] = p.n;
+                g.stride[k] = p.stride;
+                g.dst[k] = p.dst_offset;
+                g.elem[k] = p.elem_bytes;
+                const int64_t w = p.elem_bytes == 8 ? p.n : p.n * p.elem_bytes;
+                most = w > most ? w : most;
+            }
+            if (most == 0) continue;
+            const int64_t gx64 = (most + 255) / 256;
+            const dim3 grid(unsigned(gx64 < 64 ? gx64 : 64), unsigned(g.count));
+            k_gather_to_host<<<grid, 256, 0, st>>>(g, static_cast<unsigned char *>(d_area));
+            FZ_LAUNCH_CHECK();
+        }
+        FZ_HIP(hipStreamSynchronize(st));
+        std::memcpy(host_out, h_area, size_t(total_bytes));
+        return FZ_OK;
+    } catch (const fz::Error &e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return FZ_E_INVALID;
+    }
 }
 
 int fz_describe_f64(fz_ctx *ctx, const double *x, int64_t n, fz_describe *host_out) {

@@ -279,6 +279,32 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     }
 }
 
+// The sharded step's RQ2-count tail, after the session exchange and the gather of the per-session
+// rows (rq2_coverage_count.py:335-372): the tests on the first k entries of the median trend and
+// the mean / median of the valid per-project correlations (eligible, raw_n > 0, not NaN) -
+// out[0..3] as fz_series_tests, out[4..5] mean and median; one library call instead of the
+// driver's slicing, host-side mask and upload.
+void rq2_count_tail(fz_ctx *c, const double *median_trend, int64_t k, const double *corr, const int64_t *raw_n,
+                    const int64_t *eligible, int64_t P, double *out) {
+    int64_t *d_k = c->arena.get<int64_t>(1);
+    set_i64(c, d_k, &k, 1);
+    if (series_small_ok(k > 0 ? k : 1))
+        series_small(c, median_trend, d_k, out, out + 1, out + 2, out + 3);
+    else
+        series_tests(c, median_trend, k > 0 ? k : 1, d_k, out);
+    int64_t *d_nv = c->arena.get<int64_t>(1);
+    double *vals = c->arena.get<double>(P > 0 ? P : 1);
+    compact_emit(c, P, nullptr,
+                 [=] __device__(int64_t p) { return eligible[p] != 0 && raw_n[p] > 0 && !isnan(corr[p]); },
+                 [=] __device__(int64_t p, int64_t q) { vals[q] = corr[p]; }, d_nv);
+    fz_describe *d = c->arena.get<fz_describe>(1);
+    describe_f64_dn(c, vals, P, d_nv, d);
+    map_n(c, 1, nullptr, [=] __device__(int64_t) {
+        out[4] = d->mean;
+        out[5] = d->median;
+    });
+}
+
 // ------------------------------------------------------------------------------ RQ2 (add)
 // rq2_coverage_and_added.py:73-238: change points of (modules, revisions) over Coverage builds.
 constexpr int64_t kDayUs = 86400000000LL;

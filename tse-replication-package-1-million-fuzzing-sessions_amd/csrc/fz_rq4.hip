@@ -18,6 +18,8 @@ namespace fz {
 
 constexpr int64_t kLim4 = 1736294400000000LL;  // '2025-01-08'
 constexpr int64_t kDay4 = 86400000000LL;
+void rq2_session_stats_grouped(fz_ctx *c, const double *values, const int64_t *offs, int64_t n, int64_t S,
+                               int64_t max_len, double *average, double *median, double *pcts, int64_t *n_ge100);
 constexpr int kWin = 7;                         // ANALYSIS_ITERATIONS / DAYS_THRESHOLD (rq4a:43-46)
 
 void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count, std::initializer_list<Fill> fills = {});
@@ -639,6 +641,57 @@ void rq4b_trends(fz_ctx *c, const int64_t *c2, const int64_t *c1, const double *
         sp[2 * k] = rho[k];
         sp[2 * k + 1] = pv[k];
     });
+}
+
+// The sharded step's RQ4b tail, after the session exchange and the gathers: the trends over the
+// per-session columns of all M sessions (:849-899), the delta columns put in corpus CSV order
+// (:725-797; their keys delta_order[nd] are distinct CSV rows < n_order: scattered by key, then
+// compacted in key order - stable, no sort) with the medians of their 14 rows (:797), and the
+// initial-coverage tests (:221-313; NaN unless both samples are non-empty) - one call instead of
+// the driver's stack / argsort / gather / median / test launches.
+void rq4b_tail(fz_ctx *c, const int64_t *c2, const int64_t *c1, const double *g2q, const double *g1q, int64_t M,
+               const int64_t *order, const double *pre, const double *post, int64_t nd, int64_t n_order,
+               const double *x, int64_t nx, const double *y, int64_t ny, int64_t *last, double *sp, double *pre_out,
+               double *post_out, double *med14, double *tests) {
+    if (M > 0) {
+        rq4b_trends(c, c2, c1, g2q, g1q, M, last, sp);
+    } else {
+        const int64_t m1 = -1;
+        set_i64(c, last, &m1, 1);
+    }
+    // the columns in key order: slot[k] = 1 + the column holding key k (0: none)
+    const int64_t NO = n_order > 0 ? n_order : 1;
+    int64_t *slot = c->arena.get<int64_t>(NO);
+    int64_t *perm = c->arena.get<int64_t>(nd > 0 ? nd : 1);
+    int64_t *offs = c->arena.get<int64_t>(2 * kWin + 1);
+    fill_batch(c, {{slot, NO * 8, 0}});
+    if (nd > 0) {
+        map_n(c, nd, nullptr, [=] __device__(int64_t i) { slot[order[i]] = i + 1; });
+        compact_emit<1>(c, NO, nullptr, [=] __device__(int64_t k) { return slot[k] != 0; },
+                        [=] __device__(int64_t k, int64_t q) { perm[q] = slot[k] - 1; }, nullptr);
+    }
+    // pre rows then post rows, [14, nd] row-major, and the 15 row offsets
+    double *rows = c->arena.get<double>(2 * kWin * (nd > 0 ? nd : 1));
+    map_n(c, 2 * kWin * nd > 2 * kWin + 1 ? 2 * kWin * nd : 2 * kWin + 1, nullptr, [=] __device__(int64_t k) {
+        if (k <= 2 * kWin) offs[k] = k * nd;
+        if (k >= 2 * kWin * nd) return;
+        const int64_t r = k / nd, j = k % nd;
+        const int64_t src = (r % kWin) * nd + perm[j];
+        const double v = r < kWin ? pre[src] : post[src];
+        rows[k] = v;
+        (r < kWin ? pre_out : post_out)[k - (r < kWin ? 0 : kWin * nd)] = v;
+    });
+    double *avg = c->arena.get<double>(2 * kWin), *pct = c->arena.get<double>(10 * kWin);
+    int64_t *ge = c->arena.get<int64_t>(1);
+    rq2_session_stats_grouped(c, rows, offs, 2 * kWin * nd, 2 * kWin, nd, avg, med14, pct, ge);
+    if (nx > 0 && ny > 0) {
+        int64_t *d_n = c->arena.get<int64_t>(2);
+        const int64_t h[2] = {nx, ny};
+        set_i64(c, d_n, h, 2);
+        two_sample_tests(c, x, nx, d_n, y, ny, d_n + 1, tests);
+    } else {
+        map_n(c, FZ_RQ4B_NTESTS, nullptr, [=] __device__(int64_t k) { tests[k] = NAN; });
+    }
 }
 
 void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *o) {

@@ -98,6 +98,11 @@ class FzRq3Out(C.Structure):
                                   "non_pct", "non_cov", "non_tot", "describe", "tests")]
 
 
+class FzHostPiece(C.Structure):  # fz_host_piece (fz_gather_to_host)
+    _fields_ = [("src", _P), ("n", _I64), ("stride", _I64), ("dst_offset", _I64), ("elem_bytes", C.c_int32),
+                ("pad_", C.c_int32)]
+
+
 class FzRq4Groups(C.Structure):
     _fields_ = [("member", _P), ("corpus_us", _P), ("order", _P), ("n_order", _I64)]
 
@@ -167,6 +172,10 @@ SIGNATURES = {
     "fz_rq4b_trends": (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P]),
     "fz_describe_f64_dev": (C.c_int, [_P, _P, _I64, _P]),
     "fz_two_sample_tests": (C.c_int, [_P, _P, _I64, _P, _I64, _P]),
+    "fz_rq2_count_tail": (C.c_int, [_P, _P, _I64, _P, _P, _P, _I64, _P]),
+    "fz_gather_to_host": (C.c_int, [_P, _P, C.c_int, _P, _I64]),
+    "fz_rq4b_tail": (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P, _P, _I64, _I64, _P, _I64, _P, _I64,
+                              _P, _P, _P, _P, _P, _P]),
     "fz_buildlog": (C.c_int, [_P, _P, _I64, _P, _P, _I64, C.POINTER(FzBuildlogOut)]),
     "fz_probe_begin": (C.c_int, [_P, C.c_char_p]),
     "fz_probe_end": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),

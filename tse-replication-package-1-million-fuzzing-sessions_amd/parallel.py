@@ -233,27 +233,48 @@ def all_to_all_v(x, send_counts, recv_counts=None):
     return out
 
 
+_NP_DTYPES = {}
+
+
 def host_many(*ts):
-    """Host numpy copies of several tensors (numpy arrays pass through) with ONE device->host copy:
-    each separate ``.cpu()`` would drain the stream once."""
+    """Host numpy copies of several tensors (numpy arrays pass through) with ONE device->host read:
+    each separate ``.cpu()`` would drain the stream once.  Device tensors go through libfz's
+    fz_gather_to_host (one launch over every piece - strided 1-D slices read in place - into a
+    pinned area, one sync); CPU tensors (the gloo tests' shards) are copied directly."""
     import torch
     dev = [t for t in ts if isinstance(t, torch.Tensor) and t.is_cuda]
     if not dev:
         return [t.numpy().copy() if isinstance(t, torch.Tensor) else np.asarray(t) for t in ts]
-    def flat1(t):  # (1-D, unit stride: a one-element column slice can keep its row stride)
-        x = t.reshape(-1)
-        if x.stride(0) != 1 or not x.numel():
-            x = torch.empty(x.numel(), dtype=x.dtype, device=x.device).copy_(x)
-        return x.view(torch.uint8)
-    flat = [flat1(t) for t in dev]
-    h = torch.cat(flat).cpu().numpy()
-    out, o, k = [], 0, 0
+    import ctypes as C
+    from . import engine as E
+    lib = E.load_library()
+    keep, pieces, o = [], [], 0
+    for t in dev:
+        n, e = t.numel(), t.element_size()
+        if n <= 1 or t.is_contiguous():
+            stride = 1
+        elif t.dim() == 1 and t.stride(0) > 0:
+            stride = t.stride(0)
+        else:  # (a strided block: one contiguous copy)
+            t = t.contiguous()
+            stride = 1
+        keep.append(t)
+        o = (o + 7) & ~7
+        pieces.append(E.FzHostPiece(t.data_ptr() if n else None, n, max(stride, 1), o, e, 0))
+        o += n * e
+    buf = np.empty(max(o, 1), np.uint8)
+    arr = (E.FzHostPiece * len(pieces))(*pieces)
+    with torch.cuda.device(dev[0].device):
+        stream = torch.cuda.current_stream(dev[0].device).cuda_stream
+        E._check(lib, lib.fz_gather_to_host(C.c_void_p(stream), arr, len(pieces), C.c_void_p(buf.ctypes.data), o))
+    out, k = [], 0
     for t in ts:
         if isinstance(t, torch.Tensor) and t.is_cuda:
-            nb = flat[k].numel()
-            dt = torch.empty(0, dtype=t.dtype).numpy().dtype
-            out.append(h[o:o + nb].view(dt).reshape(tuple(t.shape)))
-            o += nb
+            p = pieces[k]
+            dt = _NP_DTYPES.get(t.dtype)
+            if dt is None:
+                dt = _NP_DTYPES[t.dtype] = torch.empty(0, dtype=t.dtype).numpy().dtype
+            out.append(buf[p.dst_offset:p.dst_offset + p.n * p.elem_bytes].view(dt).reshape(tuple(t.shape)))
             k += 1
         else:
             out.append(t.numpy().copy() if isinstance(t, torch.Tensor) else np.asarray(t))
@@ -509,11 +530,16 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
         block = torch.cat([m.reshape(-1, 7).view(torch.float64) for m in all_gather_v(block.reshape(-1).view(
             torch.int64))])
     K = int(np.sum(sizes_h >= 100))
-    tests = shard.series_tests(block[:K, 1].contiguous())  # median trend of the sessions with >= 100 values
-    elig = proj["eligible"] != 0
-    corr = proj["corr"][elig][proj["raw_n"][elig] > 0]
-    valid = corr[~np.isnan(corr)]
-    corr_mm = shard.mean_median(torch.from_numpy(valid.copy()).to(dev))
+    if hasattr(shard, "tail"):  # one library call (fz_rq2_count_tail), device in and out
+        med = st["median"][:S] if world == 1 else block[:, 1].contiguous()
+        tail = shard.tail(med, K, pc[5], pc[1], pc[0])
+        tests, corr_mm = tail[:4], tail[4:6]
+    else:
+        tests = shard.series_tests(block[:K, 1].contiguous())  # median trend of the sessions with >= 100 values
+        elig = proj["eligible"] != 0
+        corr = proj["corr"][elig][proj["raw_n"][elig] > 0]
+        valid = corr[~np.isnan(corr)]
+        corr_mm = shard.mean_median(torch.from_numpy(valid.copy()).to(dev))
     tensors = [block, tests, corr_mm]
     if gather_values:  # coverage_by_session_index.csv: every value, session-major, project order
         tensors.append(torch.cat(all_gather_v(vals)) if world > 1 else vals)
@@ -624,28 +650,14 @@ def rq4b_sharded(shard, rank: int, world: int, finish_later: bool = False):
     if world > 1:
         got = all_gather_cols(cols)
         cols = [torch.cat([g[j] for g in got]) for j in range(len(cols))]
-    if hasattr(shard, "trends"):  # one library call (fz_rq4b_trends), device in and out
-        last_d, sp = shard.trends(cols)
-    else:
-        c2d, c1d = cols[0], cols[1]
-        # last session with both groups >= 100 (:849-860), on the device
-        idx = torch.arange(c2d.numel(), dtype=torch.int64, device=c2d.device)
-        ok = (c2d >= 100) & (c1d >= 100)
-        last_d = torch.where(ok, idx, torch.full_like(idx, -1)).max() if c2d.numel() else torch.tensor(-1)
-        # Spearman of G1 Q1 / Med / Q3, then G2 Q1 / Med / Q3 over sessions 0..last (:879-899)
-        quart = torch.stack([cols[5], cols[6], cols[7], cols[2], cols[3], cols[4]]).to(torch.float64)
-        sp = shard.spearman_prefix(quart, last_d + 1)
-    # coverage deltas: columns of every rank, in corpus CSV order
+    # coverage deltas: columns of every rank (CSV row, 7 pre, 7 post), put in corpus CSV order below
     proj = part["delta_order"][:nd]
     pre = part["pre_cov"][:7 * nd].reshape(7, nd)
     post = part["post_cov"][:7 * nd].reshape(7, nd)
-    if world > 1:  # one gather: (CSV row, 7 pre, 7 post) per delta column
+    if world > 1:  # one gather
         got = all_gather_cols([proj] + [pre[i] for i in range(7)] + [post[i] for i in range(7)])
         cat = [torch.cat([g[j] for g in got]) for j in range(15)]
         proj, pre, post = cat[0], torch.stack(cat[1:8]), torch.stack(cat[8:15])
-    order = torch.argsort(proj, stable=True)
-    pre, post = pre[:, order], post[:, order]
-    med = shard.row_medians(torch.cat([pre, post]).contiguous())
     # initial coverage: samples in project order, tests once
     x, y = part["init_g2"][:n2], part["init_g1"][:n1]
     if world > 1:  # both samples in one variable gather: [len(x), x, y] per rank
@@ -657,7 +669,30 @@ def rq4b_sharded(shard, rank: int, world: int, finish_later: bool = False):
             xs.append(q[1:1 + k].view(torch.float64))
             ys.append(q[1 + k:].view(torch.float64))
         x, y = torch.cat(xs), torch.cat(ys)
-    tests = shard.two_sample(x, y)
+    if hasattr(shard, "tail"):
+        # trends, delta columns in CSV order with their medians, initial-coverage tests: one library
+        # call (fz_rq4b_tail), device in and out
+        if world > 1:  # (the gathered quartile columns back to [session, 3] rows)
+            g2q, g1q = torch.stack(cols[2:5], 1).reshape(-1), torch.stack(cols[5:8], 1).reshape(-1)
+        else:
+            g2q, g1q = st["g2_q"][:3 * S], st["g1_q"][:3 * S]
+        last_d, sp, pre, post, med, tests = shard.tail(cols[0], cols[1], g2q, g1q, proj, pre, post, x, y)
+    else:
+        if hasattr(shard, "trends"):  # one library call (fz_rq4b_trends), device in and out
+            last_d, sp = shard.trends(cols)
+        else:
+            c2d, c1d = cols[0], cols[1]
+            # last session with both groups >= 100 (:849-860), on the device
+            idx = torch.arange(c2d.numel(), dtype=torch.int64, device=c2d.device)
+            ok = (c2d >= 100) & (c1d >= 100)
+            last_d = torch.where(ok, idx, torch.full_like(idx, -1)).max() if c2d.numel() else torch.tensor(-1)
+            # Spearman of G1 Q1 / Med / Q3, then G2 Q1 / Med / Q3 over sessions 0..last (:879-899)
+            quart = torch.stack([cols[5], cols[6], cols[7], cols[2], cols[3], cols[4]]).to(torch.float64)
+            sp = shard.spearman_prefix(quart, last_d + 1)
+        order = torch.argsort(proj, stable=True)
+        pre, post = pre[:, order], post[:, order]
+        med = shard.row_medians(torch.cat([pre, post]).contiguous())
+        tests = shard.two_sample(x, y)
 
     def finish(h):  # (the one result copy)
         counts_h, last, sp_h, pre_h, post_h, med_h, x_h, y_h, tests_h = h[:9]
@@ -773,6 +808,19 @@ class GpuRQ2CountShard:
 
     def mean_median(self, x):
         return gpu_mean_median(self.eng, x)
+
+    def tail(self, median, k, corr, raw_n, eligible):
+        """fz_rq2_count_tail: the median-trend tests over median[:k] and the valid correlations'
+        (mean, median) -> device [6] (rho, p, W, p, mean, median)."""
+        E, C, eng = self.E, self.C, self.eng
+        torch = eng.torch
+        out = torch.empty(6, dtype=torch.float64, device=eng.dev)
+        median, corr = median.contiguous(), corr.to(torch.float64).contiguous()
+        raw_n, eligible = raw_n.to(torch.int64).contiguous(), eligible.to(torch.int64).contiguous()
+        P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+        E._check(eng.lib, eng.lib.fz_rq2_count_tail(eng.ctx, P(median), k, P(corr), P(raw_n), P(eligible), corr.numel(),
+                                                    P(out)))
+        return out
 
 
 def gpu_merge_runs(eng, vals, runs):
@@ -1002,6 +1050,29 @@ class GpuRQ4bShard:
         offs = self.eng.torch.arange(k + 1, dtype=self.eng.torch.int64, device=self.eng.dev) * n
         out = gpu_session_stats_grouped(self.eng, rows.reshape(-1).contiguous(), offs, k, n)
         return out["median"][:k]
+
+    def tail(self, c2, c1, g2q, g1q, order, pre, post, x, y):
+        """fz_rq4b_tail: trends over the per-session columns, the delta columns ([7, nd] each) in CSV
+        order by `order` with the medians of their 14 rows, the initial-coverage tests -> device
+        (last, spearman6 [12], pre [7, nd], post [7, nd], medians [14], tests)."""
+        E, C, eng = self.E, self.C, self.eng
+        torch = eng.torch
+        M, nd = c2.numel(), order.numel()
+        c2, c1 = c2.to(torch.int64).contiguous(), c1.to(torch.int64).contiguous()
+        g2q, g1q = g2q.to(torch.float64).contiguous(), g1q.to(torch.float64).contiguous()
+        order = order.to(torch.int64).contiguous()
+        pre, post = pre.to(torch.float64).contiguous(), post.to(torch.float64).contiguous()
+        x, y = x.contiguous(), y.contiguous()
+        last = torch.empty(1, dtype=torch.int64, device=eng.dev)
+        res = torch.empty(12 + 14 + E.FZ_RQ4B_NTESTS + 14 * max(nd, 1), dtype=torch.float64, device=eng.dev)
+        sp, med, tests = res[:12], res[12:26], res[26:26 + E.FZ_RQ4B_NTESTS]
+        po = res[26 + E.FZ_RQ4B_NTESTS:]
+        pre_o, post_o = po[:7 * nd].view(7, nd), po[7 * nd:14 * nd].view(7, nd)
+        P = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None  # noqa: E731
+        E._check(eng.lib, eng.lib.fz_rq4b_tail(eng.ctx, P(c2), P(c1), P(g2q), P(g1q), M, P(order), P(pre), P(post), nd,
+                                               int(eng.groups.n_order), P(x), x.numel(), P(y), y.numel(), P(last),
+                                               P(sp), P(pre_o), P(post_o), P(med), P(tests)))
+        return last[0], sp, pre_o, post_o, med, tests
 
     def two_sample(self, x, y):
         E, C, eng = self.E, self.C, self.eng
