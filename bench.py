@@ -349,11 +349,13 @@ def main():
                     return
             eng.join_children()  # the previous step's analyses have read the store
             eng.build_store()
-            for ch in children[:-1]:
-                ch.follow_parent()
             if graphs is not None:
-                # host order: producers' events are recorded before any stream waits on them
+                # host order: producers' events are recorded before any stream waits on them; each
+                # child follows the store right before its first replay (the critical group's
+                # replay is enqueued first, ahead of the other children's stream waits)
                 for gi in order:
+                    if children[gi] is not eng:
+                        children[gi].follow_parent()
                     for need, gr, mark in graphs[gi]:
                         if need:
                             children[gi].stream.wait_event(events[need])
@@ -361,6 +363,8 @@ def main():
                         if mark:
                             events[mark].record(children[gi].stream)
                 return
+            for ch in children[:-1]:
+                ch.follow_parent()
             if split:  # warm-up before the recordings: the groups one after another (dependencies)
                 for gi in order:
                     run_group(children[gi], groups[gi])

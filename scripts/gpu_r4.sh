@@ -53,6 +53,18 @@ for s in $STEPS; do
       cfg=${arg%%@*}; sts=${arg#*@}
       timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/${T}_profs_$cfg -o run -- python3 -u bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline --probe-steps 0 --serial --stages $sts > $O/${T}_profs_$cfg.log 2>&1 || exit $?
       echo "profs $cfg $sts ok" ;;
+    sho)  # sharded step (one rank) with a driver order: sho:<cfg>@<N>@<order>  (N = 0: the whole
+          # table through --force-sharded; N > 0: shard 0 of N, --strong --force-sharded; order "x":
+          # the default); sho:<cfg>@<N>@single: shard 0 of N through the single-table step
+      IFS=@ read -r cfg n ord <<< "$arg"
+      extra="--force-sharded"; [ "$n" != 0 ] && extra="$extra --strong --shard-of $n --shard-rank 0"
+      [ "$ord" = single ] && extra="--strong --shard-of $n --shard-rank 0"
+      [ "$ord" != x ] && [ "$ord" != single ] && extra="$extra --shard-groups $ord"
+      st=20; [ "$cfg" != c2 ] && st=10
+      timeout -k 10 400 python -u bench.py --config $cfg --steps $st --warmup 2 --no-cpu-baseline --probe-steps 0 $extra > $O/${T}_sho.json 2> $O/${T}_sho.err || exit $?
+      python3 -c "import json; d=json.loads([l for l in open('$O/${T}_sho.json') if l.startswith('{')][-1]); print('sho $cfg $n $ord', d['ms_per_step'], d['config'].get('driver_host_ms'), flush=True)" ;;
+    ab)  # same-box A/B of library variants: ab:<name>+<name>... (base = lib/libfz.so), BENCH_ARGS
+      VARIANTS="${arg//+/ }" timeout -k 10 900 bash scripts/bench_ab.sh > $O/${T}_ab.txt 2>&1 || exit $?; cat $O/${T}_ab.txt ;;
     envb)  # bench line under one runtime environment variable: envb:<cfg>@VAR=VALUE
       cfg=${arg%%@*}; kv=${arg#*@}; st=20; [ "$cfg" != c2 ] && st=5
       env "$kv" timeout -k 10 600 python -u bench.py --config $cfg --steps $st --warmup 2 --no-cpu-baseline > $O/${T}_envb.json 2> $O/${T}_envb.err || exit $?

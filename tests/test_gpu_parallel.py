@@ -157,3 +157,27 @@ def test_gpu_sharded_rq1_rq3(case, tmp_path):
     except Exception:
         msgs = [open(f"{errfile}.{r}").read() for r in range(2) if os.path.exists(f"{errfile}.{r}")]
         raise AssertionError("\n".join(msgs) or "worker failed")
+
+
+def test_host_many_gather():
+    """parallel.host_many (fz_gather_to_host): contiguous, strided 1-D column slices, a strided 2-D
+    block, 0-d, empty and one-element tensors of every element size, mixed with CPU tensors and
+    numpy arrays - the same values as .cpu(), several reads in a row (the staging area is reused)."""
+    from tse_amd import parallel as par
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(5)
+    blk = torch.randn(97, 5, generator=g, dtype=torch.float64).to(dev)
+    ts = [blk[:, 2], blk[:, 0], blk, blk[::3], torch.arange(1000, dtype=torch.int64, device=dev)[7::13],
+          torch.randint(0, 255, (77,), generator=g, dtype=torch.uint8).to(dev),
+          torch.randint(-9, 9, (33,), generator=g, dtype=torch.int32).to(dev)[::2],
+          torch.tensor(3.5, dtype=torch.float64, device=dev), torch.empty(0, dtype=torch.int64, device=dev),
+          torch.tensor([True, False, True], device=dev), torch.ones(1, 3, dtype=torch.float32, device=dev)[:, 1],
+          torch.arange(5).to(torch.int16).to(dev), torch.arange(4), np.arange(3.0)]
+    for _ in range(3):
+        got = par.host_many(*ts)
+        for t, h in zip(ts, got):
+            want = t.cpu().numpy() if isinstance(t, torch.Tensor) else t
+            assert h.dtype == want.dtype and h.shape == want.shape
+            np.testing.assert_array_equal(h, want)
+    big = torch.randn(3_000_000, dtype=torch.float64, device=dev)  # (grows the staging area)
+    np.testing.assert_array_equal(par.host_many(big[::2], big[:5])[0], big[::2].cpu().numpy())

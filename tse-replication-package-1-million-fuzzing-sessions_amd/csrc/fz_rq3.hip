@@ -25,6 +25,37 @@ __device__ inline int64_t fdiv_day(int64_t a) {
     return (a % kDay3 != 0 && a < 0) ? q - 1 : q;
 }
 
+// Three independent binary searches over non-empty ranges [lo, hi) in lock step: each round issues
+// the three probes' loads together, so one issue's searches cost one chain of ~log2(range) dependent
+// loads instead of three (the detected pass runs one thread per issue - about one wave per SIMD -
+// and is bound by that load latency).  upper: first index with a[i] > v, else first with a[i] >= v.
+struct Probe3 {
+    const int64_t *a;
+    int64_t lo, hi, v;
+    bool upper;
+};
+__device__ inline void search3(Probe3 &x, Probe3 &y, Probe3 &z) {
+    const int64_t xl = x.hi - 1, yl = y.hi - 1, zl = z.hi - 1;  // clamps for a finished search's probe
+    while (x.lo < x.hi || y.lo < y.hi || z.lo < z.hi) {
+        const int64_t mx = x.lo < x.hi ? (x.lo + x.hi) >> 1 : (x.lo < xl ? x.lo : xl);
+        const int64_t my = y.lo < y.hi ? (y.lo + y.hi) >> 1 : (y.lo < yl ? y.lo : yl);
+        const int64_t mz = z.lo < z.hi ? (z.lo + z.hi) >> 1 : (z.lo < zl ? z.lo : zl);
+        const int64_t ax = x.a[mx], ay = y.a[my], az = z.a[mz];
+        if (x.lo < x.hi) {
+            if (x.upper ? ax <= x.v : ax < x.v) x.lo = mx + 1;
+            else x.hi = mx;
+        }
+        if (y.lo < y.hi) {
+            if (y.upper ? ay <= y.v : ay < y.v) y.lo = my + 1;
+            else y.hi = my;
+        }
+        if (z.lo < z.hi) {
+            if (z.upper ? az <= z.v : az < z.v) z.lo = mz + 1;
+            else z.hi = mz;
+        }
+    }
+}
+
 struct FixedIssuesRq3 {  // status fixed, eligible project, rts < LIMIT (:219-232)
     static constexpr int kBytes = 13;  // column bytes read per row (filter_compact probe)
     const uint32_t *proj;
@@ -113,19 +144,24 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         const int64_t b0 = CBv.offs[p], b1 = CBv.offs[p + 1];
         const int64_t c0 = TCv.offs[p], c1 = TCv.offs[p + 1];
         if (f0 == f1 || b0 == b1 || c0 == c1) return false;
-        const int64_t k = lower_bound_i64(Fv.time, f0, f1, rts) - 1;  // last fuzz build before rts
-        if (k < f0) return false;
-        const int64_t k2 = upper_bound_i64(CBv.time, b0, b1, rts);   // first coverage build after rts
-        if (k2 >= b1) return false;
+        // the last fuzz build before rts, the first coverage build after rts, the first coverage
+        // row on day rts + 1: three searches at once (the conditions below are side-effect free,
+        // so testing them after all three lookups keeps the reference's outcome)
+        const int64_t target = fdiv_day(rts) + 1;
+        Probe3 sf{Fv.time, f0, f1, rts, false}, sb{CBv.time, b0, b1, rts, true}, sc{TCv.time, c0, c1, target * kDay3, false};
+        search3(sf, sb, sc);
+        const int64_t k = sf.lo - 1, k2 = sb.lo;
+        int64_t kk = sc.lo;
+        if (k < f0 || k2 >= b1) return false;
+        if (kk < c0 + 1) kk = c0 + 1;  // the reference scans rows i >= 1
+        if (kk >= c1) return false;
         const int32_t lf = Fv.row[k], fc = CBv.row[k2];
+        const int64_t tkk = TCv.time[kk];
+        const int32_t ra = TCv.row[kk - 1], rb = TCv.row[kk];
         if (!(result[fc] == 2 || result[fc] == 0)) return false;
         if (btime[fc] - btime[lf] > kGapUs) return false;  // total_seconds()/3600 > 24 (:277)
         if (canon[lf] < 0 || canon[lf] != canon[fc]) return false;
-        const int64_t target = fdiv_day(rts) + 1;
-        int64_t kk = lower_bound_i64(TCv.time, c0, c1, target * kDay3);
-        if (kk < c0 + 1) kk = c0 + 1;  // the reference scans rows i >= 1
-        if (kk >= c1 || fdiv_day(TCv.time[kk]) != target) return false;
-        const int32_t ra = TCv.row[kk - 1], rb = TCv.row[kk];
+        if (fdiv_day(tkk) != target) return false;
         if (cvd[rb] == 0) return false;      // break without a pair (:291)
         if (null_cmp(ra, rb)) {
             atomic_add_i64(&counts[FZ_RQ3_NULL_TOTAL], 1);
