@@ -22,6 +22,10 @@ for s in $STEPS; do
       python3 scripts/kstats.py "$f" $((st + 3)) 40 > $O/${T}_kstats_$arg.txt; head -30 $O/${T}_kstats_$arg.txt ;;
     stages)
       CONFIG=$arg timeout -k 10 900 bash scripts/stage_times.sh > $O/${T}_stages_$arg.txt 2>&1 || exit $?; cat $O/${T}_stages_$arg.txt ;;
+    st8)  # per-stage serial step times of shard 0 of 8 (the strong rehearsal's per-rank table)
+      CONFIG=$arg EXTRA="--strong --shard-of 8 --shard-rank 0" timeout -k 10 900 bash scripts/stage_times.sh > $O/${T}_st8_$arg.txt 2>&1 || exit $?; cat $O/${T}_st8_$arg.txt ;;
+    drop8)  # the concurrent step of shard 0 of 8 without one analysis group at a time
+      CONFIG=$arg DROP=1 EXTRA="--strong --shard-of 8 --shard-rank 0" timeout -k 10 900 bash scripts/stage_times.sh > $O/${T}_drop8_$arg.txt 2>&1 || exit $?; cat $O/${T}_drop8_$arg.txt ;;
     drop)
       CONFIG=$arg DROP=1 timeout -k 10 900 bash scripts/stage_times.sh > $O/${T}_drop_$arg.txt 2>&1 || exit $?; cat $O/${T}_drop_$arg.txt ;;
     bench)
@@ -49,9 +53,10 @@ for s in $STEPS; do
       extra=""; [ $kind = fs1 ] && extra="--shard-groups rq3,rq4b,rq2_count,rq1,rq4a,rq2_add"
       timeout -k 10 600 python -u bench.py --config $arg --steps $st --warmup 2 --no-cpu-baseline --probe-steps 0 --force-sharded $extra > $O/${T}_${kind}_$arg.json 2> $O/${T}_${kind}_$arg.err || exit $?
       python3 -c "import json; d=json.loads([l for l in open('$O/${T}_${kind}_$arg.json') if l.startswith('{')][-1]); print('$kind $arg', d['ms_per_step'], d['config'].get('driver_host_ms'), flush=True)" ;;
-    profs)  # kernel trace of a serial step over some stages: profs:<cfg>@<stages>
-      cfg=${arg%%@*}; sts=${arg#*@}
-      timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/${T}_profs_$cfg -o run -- python3 -u bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline --probe-steps 0 --serial --stages $sts > $O/${T}_profs_$cfg.log 2>&1 || exit $?
+    profs)  # kernel trace of a serial step over some stages: profs:<cfg>@<stages>[@<shards of N: shard 0>]
+      IFS=@ read -r cfg sts nsh <<< "$arg"
+      extra=""; [ -n "$nsh" ] && extra="--strong --shard-of $nsh --shard-rank 0"
+      timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/${T}_profs_$cfg$nsh -o run -- python3 -u bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline --probe-steps 0 --serial --stages $sts $extra > $O/${T}_profs_$cfg$nsh.log 2>&1 || exit $?
       echo "profs $cfg $sts ok" ;;
     sho)  # sharded step (one rank) with a driver order: sho:<cfg>@<N>@<order>  (N = 0: the whole
           # table through --force-sharded; N > 0: shard 0 of N, --strong --force-sharded; order "x":

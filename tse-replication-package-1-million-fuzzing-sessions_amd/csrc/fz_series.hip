@@ -1846,8 +1846,8 @@ __device__ inline void qs_write(const QsArgs &a, int64_t s, int64_t n, double su
 // Size classes of the selection: lists of the segments too long for one lane (filled by
 // k_qs_micro), one list per class - tiny (one wave each), mid and big (one workgroup each).
 struct QsLists {
-    int32_t *ids[3];
-    int64_t *d_n;  // [3] (zero on entry)
+    int32_t *ids[4];
+    int64_t *d_n;  // [4] (zero on entry)
 };
 
 // append segment s to list cls of L when `want` (wave-aggregated: one atomic per wave and class)
@@ -1865,7 +1865,7 @@ __device__ inline void qs_append(const QsLists &L, int cls, bool want, int64_t s
 
 // One lane per segment (wave v: segments 64v .. 64v + 63, coalesced offset reads): a segment of
 // <= kMicroSeg values is finished by its lane (register sorting network); longer ones go to their
-// class list - tiny (<= kTinySeg), mid (<= 1024), big.
+// class list - tiny (<= kTinySeg), mid (<= 1024), block (<= 2048), big.
 __global__ __launch_bounds__(kBlock) void k_qs_micro(const double *__restrict__ src, const int64_t *__restrict__ offs,
                                                      int64_t S, QsArgs a, QsLists L) {
     const int lane = lane_id();
@@ -1876,7 +1876,8 @@ __global__ __launch_bounds__(kBlock) void k_qs_micro(const double *__restrict__ 
         const int64_t n = s < S ? offs[s + 1] - b : -1;
         qs_append(L, 0, n > kMicroSeg && n <= kTinySeg, s);
         qs_append(L, 1, n > kTinySeg && n <= 1024, s);
-        qs_append(L, 2, n > 1024, s);
+        qs_append(L, 2, n > 2048, s);
+        qs_append(L, 3, n > 1024 && n <= 2048, s);
         if (n < 0 || n > kMicroSeg) continue;
         uint64_t k[kMicroSeg];
         DD acc{0.0, 0.0};
@@ -2309,11 +2310,12 @@ void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_h
     ProbeScope ps(c, "seg_qstats", double(S) * (8.0 + 8.0 * (2 + nq)), sg.offs + S, 8.0);
     // class lists (capacities: a segment of the class holds more than the class below allows)
     auto cap = [&](int64_t minlen) { return S < sg.n_cap / (minlen + 1) + 1 ? S : sg.n_cap / (minlen + 1) + 1; };
-    const int64_t caps[3] = {cap(kMicroSeg), lb > kTinySeg ? cap(kTinySeg) : 0, lb > 1024 ? cap(1024) : 0};
+    const int64_t caps[4] = {cap(kMicroSeg), lb > kTinySeg ? cap(kTinySeg) : 0, lb > 2048 ? cap(2048) : 0,
+                             lb > 1024 ? cap(1024) : 0};
     QsLists L;
-    L.d_n = c->arena.get<int64_t>(3);
-    for (int k = 0; k < 3; ++k) L.ids[k] = c->arena.get<int32_t>(caps[k]);
-    dev_fill(c, L.d_n, 0, 3 * 8);
+    L.d_n = c->arena.get<int64_t>(4);
+    for (int k = 0; k < 4; ++k) L.ids[k] = c->arena.get<int32_t>(caps[k]);
+    dev_fill(c, L.d_n, 0, 4 * 8);
     const int64_t groups = (S + 63) / 64;
     k_qs_micro<<<grid_for(groups, kBlock / kWave, 8192), kBlock, 0, c->stream>>>(vals, sg.offs, S, a, L);
     FZ_LAUNCH_CHECK();
@@ -2327,6 +2329,13 @@ void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_h
         FZ_LAUNCH_CHECK();
     }
     if (lb > 1024) {
+        // 1025 - 2048 values (a session of config 3's one-per-project values: 1,250 at an eighth of
+        // the table): 256-thread workgroups with 8 values per thread - several per CU in flight, where
+        // the 1024-thread class held one workgroup per CU with 15 of its 16 value slots per thread idle
+        k_qs_block<256, 2048><<<grid(caps[3], 8192), 256, 0, c->stream>>>(vals, sg.offs, L.ids[3], L.d_n + 3, a);
+        FZ_LAUNCH_CHECK();
+    }
+    if (lb > 2048) {
         k_qs_block<1024, kQsMax><<<grid(caps[2], 1024), 1024, 0, c->stream>>>(vals, sg.offs, L.ids[2], L.d_n + 2, a);
         FZ_LAUNCH_CHECK();
     }
