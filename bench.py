@@ -244,9 +244,10 @@ def main():
                 launch["rq2_add"](e, bufs["rq2_add"])
             pre_add[0] = False
             b = bufs["rq2_add"]
-            n_add = int(b.counts[E.RQ2A_ROWS].item())
-            par.gather_rows({"project": b.row_project[:n_add], "diff_total": b.diff_total[:n_add],
-                             "diff_coverage": b.diff_coverage[:n_add]}, world)
+            if world > 1:  # (one rank: its rows are the result - nothing to read or gather)
+                n_add = int(b.counts[E.RQ2A_ROWS].item())
+                par.gather_rows({"project": b.row_project[:n_add], "diff_total": b.diff_total[:n_add],
+                                 "diff_coverage": b.diff_coverage[:n_add]}, world)
         # the drivers' final host copies are deferred (parallel.Deferred) and made in one copy at the
         # end of the step (par.finalize_all): the GPU is drained once, not once per driver
         pending = []

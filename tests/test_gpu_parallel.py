@@ -24,6 +24,10 @@ class _HostView:
         a = tuple(None if x is None else tuple(v.to(self.dev) for v in x) for x in a)
         return {k: v.cpu() if isinstance(v, torch.Tensor) else v for k, v in self.s.run(*a).items()}
 
+    def numbers(self, part):
+        got = self.s.numbers({k: part[k].to(self.dev) for k in ("matched_issue", "matched_build")})
+        return {k: v.cpu() for k, v in got.items()}
+
     def finish(self, counts, it, idt):
         c, i, d = (x.to(self.dev) for x in (counts, it, idt))
         self.s.finish(c, i, d)

@@ -363,6 +363,8 @@ def rq1_sharded(shard, rank: int, world: int):
     part = shard.run(None)
     reran = False
     if world > 1:
+        if "number" not in part:  # (the GPU shard gathers the matches' numbers / times on demand)
+            part.update(shard.numbers(part))
         got = all_gather_cols([part["number"], part["build_time"]])
         mine = part["number"]
         others = [r for r in range(world) if r != rank and got[r][0].numel()]
@@ -420,7 +422,7 @@ def rq3_sharded(shard, rank: int, world: int):
         for k in RQ3_NON_F + RQ3_NON_I:
             v = cols[k][last]
             cols[k][last] = v[:v.numel() - drop]
-    out = {k: torch.cat(v) for k, v in cols.items()}
+    out = {k: (torch.cat(v) if len(v) > 1 else v[0]) for k, v in cols.items()}
     total = np.sum(np.stack(cl), axis=0)
     total[RQ3_DETECTED] = out["det_pct"].numel()
     total[RQ3_NON_DETECTED] = out["non_pct"].numel()
@@ -504,15 +506,22 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     offs = part["session_offsets"]
     m_loc = offs.numel() - 1
     M = agree_max(m_loc, dev) if world > 1 else m_loc
-    # this rank's session sizes, then its NULL-line count (rq2_coverage_count.py:300-303 raise)
-    row = torch.zeros(M + 1, dtype=torch.int64, device=dev)
-    row[:m_loc] = offs[1:] - offs[:-1]
-    if part.get("null_lines") is not None:
-        row[M:] = part["null_lines"].to(torch.int64).reshape(1)
-    mat = torch.stack(all_gather(row)) if world > 1 else row[None]
-    h = host_many(mat, offs, *pc)  # one device->host copy
-    mat_h, offs_h = h[0], h[1]
-    sizes_h, null_lines = mat_h[:, :M].sum(0), int(mat_h[:, M].sum())
+    nl = part.get("null_lines")
+    if world > 1:
+        # this rank's session sizes, then its NULL-line count (rq2_coverage_count.py:300-303 raise)
+        row = torch.zeros(M + 1, dtype=torch.int64, device=dev)
+        row[:m_loc] = offs[1:] - offs[:-1]
+        if nl is not None:
+            row[M:] = nl.to(torch.int64).reshape(1)
+        mat = torch.stack(all_gather(row))
+        h = host_many(mat, offs, *pc)  # one device->host copy
+        mat_h, offs_h = h[0], h[1]
+        sizes_h, null_lines = mat_h[:, :M].sum(0), int(mat_h[:, M].sum())
+    else:  # (one rank: the sizes are the offsets' differences)
+        h = host_many(offs, nl if nl is not None else np.zeros(1, np.int64), *pc)
+        offs_h = h[0]
+        mat_h = np.diff(offs_h)[None]
+        sizes_h, null_lines = mat_h[0], int(np.sum(h[1]))
     if null_lines:  # float(None) (rq2_coverage_count.py:300-303): every rank holds the sum, all raise here
         raise TypeError("float() argument must be a string or a real number, not 'NoneType'")
     proj = dict(zip(RQ2C_PROJECT_COLS, h[2:]))
@@ -760,7 +769,11 @@ class GpuRQ1Shard:
         n = int(b.counts[RQ1_MATCHED].item())
         mi, mb = b.matched_issue[:n], b.matched_build[:n]
         return {"counts": b.counts, "iter_total": b.iter_total, "iter_detected": b.iter_detected,
-                "number": self.i_number[mi], "build_time": self.b_time[mb], "matched_issue": mi, "matched_build": mb}
+                "matched_issue": mi, "matched_build": mb}
+
+    def numbers(self, part):
+        """The issue numbers / build times of a run's matches (the cross-shard exchange's columns)."""
+        return {"number": self.i_number[part["matched_issue"]], "build_time": self.b_time[part["matched_build"]]}
 
     def finish(self, counts, it, idt):
         E, C, eng = self.E, self.C, self.eng
