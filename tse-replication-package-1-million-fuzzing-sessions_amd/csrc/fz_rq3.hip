@@ -17,6 +17,12 @@ constexpr int64_t kLim3 = 1736294400000000LL;    // '2025-01-08'
 constexpr int64_t kLim3b = 1736380800000000LL;   // '2025-01-09' (rq3:262-263)
 constexpr int64_t kDay3 = 86400000000LL;
 constexpr int64_t kGapUs = 24LL * 3600LL * 1000000LL;
+#ifndef FZ_RQ3_A2_MAP
+#define FZ_RQ3_A2_MAP 1  // the Anderson-Darling terms by a full-width map (0: inside the reduction)
+#endif
+#ifndef FZ_RQ3_NON_ITEMS
+#define FZ_RQ3_NON_ITEMS 4  // coverage rows per thread of the non-detected pass
+#endif
 
 void eligible_projects(fz_ctx *c, uint8_t *elig, int64_t *d_count, std::initializer_list<Fill> fills = {});
 
@@ -137,7 +143,7 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     int64_t *dday = c->arena.get<int64_t>(NI);
     const fz_rq3_out out = *o;
     const int32_t *iperm = s.iperm;  // sorted positions -> the caller's issue row ids
-    compact_emit<1>(c, NI, d_ni, [=] __device__(int64_t j) -> bool {
+    auto detected = [=] __device__(int64_t j) -> bool {
         const uint32_t p = iproj[j];
         const int64_t rts = irts[j];
         const int64_t f0 = Fv.offs[p], f1 = Fv.offs[p + 1];
@@ -171,7 +177,8 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         pa[j] = ra;
         pb[j] = rb;
         return true;
-    }, [=] __device__(int64_t j, int64_t q) {
+    };
+    compact_emit<1>(c, NI, d_ni, detected, [=] __device__(int64_t j, int64_t q) {
         const int64_t ra = pa[j], rb = pb[j];
         out.det_pct[q] = (double(cvd[rb]) / double(ctot[rb]) - double(cvd[ra]) / double(ctot[ra])) * 100.0;
         out.det_cov[q] = cvd[rb] - cvd[ra];
@@ -195,7 +202,8 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         hasiss[p] = (ioffs[p + 1] > ioffs[p]) && (flush_last || uint32_t(p) != last);
     });
     // (over the live rows of TC only: *TCv.d_n of capacity NC; the kept pairs compacted in the pass)
-    compact_emit<1>(c, NC, TCv.d_n, [=] __device__(int64_t k) -> bool {
+    // (several rows per thread: their loads overlap, and fewer tiles to look back over)
+    compact_emit<FZ_RQ3_NON_ITEMS>(c, NC, TCv.d_n, [=] __device__(int64_t k) -> bool {
         const uint32_t p = TCv.proj[k];
         if (!hasiss[p] || k == TCv.offs[p]) return false;
         const int32_t ra = TCv.row[k - 1], rb = TCv.row[k];
@@ -253,13 +261,30 @@ static void sample_tests(fz_ctx *c, const double *v, const double *cat, int64_t 
         x[1] = e * e;
     }, r2, 8.0);
     double *r3 = c->arena.get<double>(2);  // [s]: sum of the A2 terms (ascending order)
-    seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
+    // the terms (two log_ndtr each) by a map over every element - a thread each, the whole chip -
+    // then summed in the reduction's usual order; inside the chunked reduction's 8-per-thread loop
+    // the dependent fp64 chains of one wave per SIMD were latency-bound (config 2: 37 us -> ~10)
+#if FZ_RQ3_A2_MAP
+    double *a2 = c->arena.get<double>(cap > 0 ? cap : 1);
+    map_n(c, cap > 0 ? cap : 1, oseg + 2, [=] __device__(int64_t i) {
+        const int s = i < oseg[1] ? 0 : 1;
         const int64_t b = oseg[s], n = oseg[s + 1] - b, k = i - b;
         const double N = double(n), xbar = r1[2 * s] / N;
         const double sd = sqrt(r2[2 * s] / (N - 1.0));  // np.std(ddof=1)
         const double wi = (cat[i] - xbar) / sd, wj = (cat[b + n - 1 - k] - xbar) / sd;
+        a2[i] = (2.0 * double(k + 1) - 1.0) / N * (stats::log_ndtr(wi) + stats::log_ndtr(-wj));
+    });
+    seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t, double *x) { x[0] = a2[i]; }, r3, 24.0);
+    // (algorithmic bytes: the value and its mirror read, the term written and read back)
+#else  // (A/B build: the terms inside the chunked reduction)
+    seg_reduce<1>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
+        const int64_t b = oseg[s], n = oseg[s + 1] - b, k = i - b;
+        const double N = double(n), xbar = r1[2 * s] / N;
+        const double sd = sqrt(r2[2 * s] / (N - 1.0));
+        const double wi = (cat[i] - xbar) / sd, wj = (cat[b + n - 1 - k] - xbar) / sd;
         x[0] = (2.0 * double(k + 1) - 1.0) / N * (stats::log_ndtr(wi) + stats::log_ndtr(-wj));
-    }, r3, 16.0);  // the value and its mirror
+    }, r3, 16.0);
+#endif
     map_n(c, 1, nullptr, [=] __device__(int64_t) {
         const double nx = double(oseg[1] - oseg[0]), ny = double(oseg[2] - oseg[1]);
         if (!(nx > 0.0 && ny > 0.0)) return;
