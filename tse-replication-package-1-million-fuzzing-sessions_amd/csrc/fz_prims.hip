@@ -446,6 +446,14 @@ constexpr int kOsBlock = FZ_OS_BLOCK;        // threads per radix-pass workgroup
 constexpr int kSortTile = FZ_OS_TILE;        // keys per workgroup
 static_assert(kOsBlock >= kRadix && kSortTile % kOsBlock == 0, "radix pass shape");
 constexpr int kSortTileBig = 8192, kOsBlockBig = 1024;  // the large sorts' tile shape
+#ifndef FZ_OS_TILE_NP
+#define FZ_OS_TILE_NP FZ_OS_TILE
+#endif
+#ifndef FZ_OS_BLOCK_NP
+#define FZ_OS_BLOCK_NP FZ_OS_BLOCK
+#endif
+// sorts without payload columns below kOsBigN keys (RQ3's union: ~790 k 64-bit keys at config 2)
+constexpr int kSortTileNp = FZ_OS_TILE_NP, kOsBlockNp = FZ_OS_BLOCK_NP;
 constexpr int64_t kOsBigN = int64_t(1) << 22;            // keys from which a sort takes it
 
 // ---- single-sweep LSD passes (one launch per digit pass) -----------------------------------
@@ -818,7 +826,8 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
     // as long per tile (fewer partial-line writes) and half the look-back work (same-box A/B: c3
     // 20.5 -> 20.0 ms, c5 30.7 -> 30.0); the small sorts of config 2 keep 4096 x 512
     const bool big = n >= kOsBigN;
-    const int64_t tile = big ? kSortTileBig : kSortTile;
+    const bool np = !big && pl.n == 0 && kSortTileNp != kSortTile;  // (the no-payload tile shape)
+    const int64_t tile = big ? kSortTileBig : (np ? kSortTileNp : kSortTile);
     const int64_t nb = (n + tile - 1) / tile;
     FZ_CHECK(n < (int64_t(1) << 47), "radix_sort_pairs: too many keys");
     // digit totals of every pass (one read of the keys)
@@ -888,6 +897,10 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
     do {                                                                                                      \
         if (big)                                                                                              \
             k_onesweep<KeyT, V, PL, kSortTileBig, kOsBlockBig><<<unsigned(nb), kOsBlockBig, 0, c->stream>>>(   \
+                ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, lb.status, lb.ticket, lb.epoch,          \
+                gsum + p * gwords, next_hist, step, d_live);                                                  \
+        else if (!PL && np)                                                                                   \
+            k_onesweep<KeyT, V, false, kSortTileNp, kOsBlockNp><<<unsigned(nb), kOsBlockNp, 0, c->stream>>>(   \
                 ka, va, kb, vb, n, p * kRadixBits, ghist + p * kRadix, lb.status, lb.ticket, lb.epoch,          \
                 gsum + p * gwords, next_hist, step, d_live);                                                  \
         else                                                                                                  \
@@ -1097,8 +1110,10 @@ __device__ inline int64_t upper_bound_u64(const uint64_t *a, int64_t n, uint64_t
 }
 
 // fz_describe of n ascending keys sk (global or LDS) with the given mean / std
+// (bounds, optional: the sample's {lower_bound(-0.0), upper_bound(+0.0), upper_bound(+inf)} found
+// by the caller - three lanes' searches at once instead of three one after another)
 __device__ void describe_from_sorted(const uint64_t *sk, int64_t n, double mean, double std,
-                                     fz_describe *__restrict__ out) {
+                                     fz_describe *__restrict__ out, const int64_t *bounds = nullptr) {
     fz_describe d;
     d.count = n;
     if (n <= 0) {
@@ -1111,9 +1126,9 @@ __device__ void describe_from_sorted(const uint64_t *sk, int64_t n, double mean,
     d.mean = mean;
     d.std = std;
     const uint64_t kneg0 = f64_key(-0.0), kpos0 = f64_key(0.0), kinf = f64_key(INFINITY);
-    const int64_t lt0 = lower_bound_u64(sk, n, kneg0);
-    const int64_t le0 = upper_bound_u64(sk, n, kpos0);
-    const int64_t leinf = upper_bound_u64(sk, n, kinf);
+    const int64_t lt0 = bounds ? bounds[0] : lower_bound_u64(sk, n, kneg0);
+    const int64_t le0 = bounds ? bounds[1] : upper_bound_u64(sk, n, kpos0);
+    const int64_t leinf = bounds ? bounds[2] : upper_bound_u64(sk, n, kinf);
     d.n_neg = lt0;
     d.n_zero = le0 - lt0;
     d.n_pos = leinf - le0;
@@ -1139,9 +1154,17 @@ __device__ void describe_from_sorted(const uint64_t *sk, int64_t n, double mean,
 }
 
 __global__ void k_describe_finish(SortedDescArgs a, const double *__restrict__ ms) {
-    if (threadIdx.x != 0) return;
-    const int j = blockIdx.x;
-    describe_from_sorted(a.k[j], *a.d_n[j], ms[2 * j], ms[2 * j + 1], a.out[j]);
+    const int j = blockIdx.x, lane = threadIdx.x;
+    const uint64_t *sk = a.k[j];
+    const int64_t n = *a.d_n[j];
+    // lanes 0 / 1 / 2: the sign-class bounds, one binary search each
+    int64_t b = 0;
+    if (lane < 3 && n > 0) {
+        const uint64_t kv = lane == 0 ? f64_key(-0.0) : (lane == 1 ? f64_key(0.0) : f64_key(INFINITY));
+        b = lane == 0 ? lower_bound_u64(sk, n, kv) : upper_bound_u64(sk, n, kv);
+    }
+    const int64_t bounds[3] = {__shfl(b, 0, 64), __shfl(b, 1, 64), __shfl(b, 2, 64)};
+    if (lane == 0) describe_from_sorted(sk, n, ms[2 * j], ms[2 * j + 1], a.out[j], bounds);
 }
 
 // samples of a capacity up to this are described by selection (k_describe_sel: one workgroup,
