@@ -35,6 +35,9 @@ struct Prefix {
 // part[4 * block + {2, 3}] that the host reduces after the build's single read-back - no atomics, no
 // initialisation launch.  (The build-type counts come off the prefix offsets: k_store_views.)
 constexpr int kProBlocks = 192;
+#ifndef FZ_SPIN_READBACK
+#define FZ_SPIN_READBACK 1
+#endif
 __global__ __launch_bounds__(kBlock) void k_store_prologue(const int64_t *__restrict__ num, int64_t ni,
                                                            int64_t *__restrict__ part) {
     __shared__ int64_t s_lo[4], s_hi[4];
@@ -1166,7 +1169,17 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     // segments left to the long-segment pass / merge sort are marked kGathered: skipped here); the
     // host's round trip overlaps it
     gather_tables(c, pss);
+#if FZ_SPIN_READBACK
+    // spin on the event rather than a blocking wait: the analyses' launches follow this read-back,
+    // and a blocking wait's wake-up latency idles the GPU after the gather
+    for (;;) {
+        const hipError_t q = hipEventQuery(c->ev_readback);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) FZ_HIP(q);
+    }
+#else
     FZ_HIP(hipEventSynchronize(c->ev_readback));
+#endif
     // (no non-NULL number: the empty range min = INT64_MAX > max = INT64_MIN, as the old read-back gave)
     s.num_min = c->h_pinned[17];
     s.num_max = c->h_pinned[18];
