@@ -659,13 +659,7 @@ int fz_gather_to_host(void *stream, const fz_host_piece *pieces, int n_pieces, v
             k_gather_to_host<<<grid, 256, 0, st>>>(g, static_cast<unsigned char *>(d_area));
             FZ_LAUNCH_CHECK();
         }
-        // (spin: the caller's next launches wait on this read; a blocking wait's wake-up would add
-        // its latency to every one of the sharded step's host reads)
-        for (;;) {
-            const hipError_t q = hipStreamQuery(st);
-            if (q == hipSuccess) break;
-            if (q != hipErrorNotReady) FZ_HIP(q);
-        }
+        FZ_HIP(hipStreamSynchronize(st));
         std::memcpy(host_out, h_area, size_t(total_bytes));
         return FZ_OK;
     } catch (const fz::Error &e) {

@@ -343,6 +343,9 @@ struct RadixPayload {
     const void *in[kMaxPayload] = {};
     void *out[kMaxPayload] = {};
     int size[kMaxPayload] = {};  // bytes per element: 1, 4 or 8
+    // (host-side option) no constant-digit read-back for this sort: the store's project-prefix
+    // sorts, enqueued ahead of the build's own read-back, whose digits all vary in practice
+    bool no_digit_probe = false;
     double bytes() const {
         double b = 0.0;
         for (int j = 0; j < n; ++j) b += size[j];

@@ -854,14 +854,14 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
     // Constant-digit passes are identity permutations.  Finding them needs a host round trip, which
     // stalls the stream for longer than a pass over a few million keys takes: only large sorts
     // (>= 4 M keys, where one pass costs ~0.1 ms or more) skip them - not while a graph is being
-    // recorded (no host round trip can happen then: every pass is recorded) - and not for keys of
-    // one or two digits (the store's project prefixes, whose digits all vary in practice): there the
-    // round trip stalls the stream for a pass it almost never saves.
+    // recorded (no host round trip can happen then: every pass is recorded) - and not when the
+    // caller says the digits all vary (pl.no_digit_probe: the store's project-prefix sorts, where
+    // the round trip would stall the stream for a pass it never saves).
     bool need[kOsMaxPasses];
     for (int p = 0; p < npass; ++p) need[p] = true;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     FZ_HIP(hipStreamIsCapturing(c->stream, &cap));
-    if (n >= (int64_t(1) << 22) && npass >= 3 && cap == hipStreamCaptureStatusNone) {
+    if (n >= (int64_t(1) << 22) && !pl.no_digit_probe && cap == hipStreamCaptureStatusNone) {
         unsigned long long *hh = reinterpret_cast<unsigned long long *>(c->h_pinned);
         FZ_HIP(hipMemcpyAsync(hh, ghist, sizeof(unsigned long long) * npass * kRadix, hipMemcpyDeviceToHost,
                               c->stream));

@@ -36,7 +36,7 @@ struct Prefix {
 // initialisation launch.  (The build-type counts come off the prefix offsets: k_store_views.)
 constexpr int kProBlocks = 192;
 #ifndef FZ_SPIN_READBACK
-#define FZ_SPIN_READBACK 1
+#define FZ_SPIN_READBACK 0  // (same-box A/B at config 2: 1.240 / 1.241 ms spinning, 1.240 / 1.243 blocking)
 #endif
 __global__ __launch_bounds__(kBlock) void k_store_prologue(const int64_t *__restrict__ num, int64_t ni,
                                                            int64_t *__restrict__ part) {
@@ -644,6 +644,7 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) 
         // segment's rows from one contiguous range instead of gathering them from the heap-ordered
         // table
         RadixPayload pl;
+        pl.no_digit_probe = true;
         pl.n = 1 + t.gc.n;
         pl.in[0] = t.time;
         pl.size[0] = 8;
