@@ -183,5 +183,10 @@ def test_host_many_gather():
             want = t.cpu().numpy() if isinstance(t, torch.Tensor) else t
             assert h.dtype == want.dtype and h.shape == want.shape
             np.testing.assert_array_equal(h, want)
-    big = torch.randn(3_000_000, dtype=torch.float64, device=dev)  # (grows the staging area)
-    np.testing.assert_array_equal(par.host_many(big[::2], big[:5])[0], big[::2].cpu().numpy())
+    big = torch.randn(3_000_000, dtype=torch.float64, device=dev)  # (the bulk path: DMA copy)
+    got = par.host_many(big[::2], big[:5], torch.tensor(7, device=dev), np.arange(2))
+    np.testing.assert_array_equal(got[0], big[::2].cpu().numpy())
+    np.testing.assert_array_equal(got[1], big[:5].cpu().numpy())
+    assert got[2] == 7 and list(got[3]) == [0, 1]
+    mid = torch.randn(300_000, dtype=torch.float64, device=dev)  # (grows the pinned staging area)
+    np.testing.assert_array_equal(par.host_many(mid[::3], mid[1::2])[1], mid[1::2].cpu().numpy())

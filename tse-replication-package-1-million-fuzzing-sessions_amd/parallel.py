@@ -234,6 +234,35 @@ def all_to_all_v(x, send_counts, recv_counts=None):
 
 
 _NP_DTYPES = {}
+# above this many bytes a read goes through one concatenation and a DMA copy instead: kernel stores
+# into host memory win for the small per-step reads, the copy engine for bulk (a Zipf giant's
+# millions of session offsets)
+_GATHER_MAX_BYTES = 4 << 20
+
+
+def _host_many_dma(ts, dev):
+    import torch
+
+    def flat1(t):  # (1-D, unit stride: a one-element column slice can keep its row stride)
+        x = t.reshape(-1)
+        if x.stride(0) != 1 or not x.numel():
+            x = torch.empty(x.numel(), dtype=x.dtype, device=x.device).copy_(x)
+        return x.view(torch.uint8)
+    flat = [flat1(t) for t in dev]
+    h = torch.cat(flat).cpu().numpy()
+    out, o, k = [], 0, 0
+    for t in ts:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            nb = flat[k].numel()
+            dt = _NP_DTYPES.get(t.dtype)
+            if dt is None:
+                dt = _NP_DTYPES[t.dtype] = torch.empty(0, dtype=t.dtype).numpy().dtype
+            out.append(h[o:o + nb].view(dt).reshape(tuple(t.shape)))
+            o += nb
+            k += 1
+        else:
+            out.append(t.numpy().copy() if isinstance(t, torch.Tensor) else np.asarray(t))
+    return out
 
 
 def host_many(*ts):
@@ -245,6 +274,8 @@ def host_many(*ts):
     dev = [t for t in ts if isinstance(t, torch.Tensor) and t.is_cuda]
     if not dev:
         return [t.numpy().copy() if isinstance(t, torch.Tensor) else np.asarray(t) for t in ts]
+    if sum(t.numel() * t.element_size() for t in dev) > _GATHER_MAX_BYTES:
+        return _host_many_dma(ts, dev)
     import ctypes as C
     from . import engine as E
     lib = E.load_library()
