@@ -55,7 +55,9 @@ for s in $STEPS; do
       python3 -c "import json; d=json.loads([l for l in open('$O/${T}_${kind}_$arg.json') if l.startswith('{')][-1]); print('$kind $arg', d['ms_per_step'], d['config'].get('driver_host_ms'), flush=True)" ;;
     profs)  # kernel trace of a serial step over some stages: profs:<cfg>@<stages>[@<shards of N: shard 0>]
       IFS=@ read -r cfg sts nsh <<< "$arg"
-      extra=""; [ -n "$nsh" ] && extra="--strong --shard-of $nsh --shard-rank 0"
+      nof=${nsh%%/*}; nrk=0; [ "$nsh" != "$nof" ] && nrk=${nsh#*/}  # N or N/rank
+      extra=""; [ -n "$nsh" ] && extra="--strong --shard-of $nof --shard-rank $nrk"
+      nsh=${nsh//\//_}
       timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/${T}_profs_$cfg$nsh -o run -- python3 -u bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline --probe-steps 0 --serial --stages $sts $extra > $O/${T}_profs_$cfg$nsh.log 2>&1 || exit $?
       echo "profs $cfg $sts ok" ;;
     sho)  # sharded step (one rank) with a driver order: sho:<cfg>@<N>@<order>  (N = 0: the whole
