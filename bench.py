@@ -352,11 +352,14 @@ def main():
             eng.build_store()
             if graphs is not None:
                 # host order: producers' events are recorded before any stream waits on them; each
-                # child follows the store right before its first replay (the critical group's
-                # replay is enqueued first, ahead of the other children's stream waits)
+                # child follows the store (one event recorded after the build, waited on by each
+                # child) right before its first replay - the critical group's replay is enqueued
+                # first, ahead of the other children's stream waits
+                store_done.record(eng.stream)
                 for gi in order:
                     if children[gi] is not eng:
-                        children[gi].follow_parent()
+                        children[gi].stream.wait_event(store_done)
+                        children[gi]._share()
                     for need, gr, mark in graphs[gi]:
                         if need:
                             children[gi].stream.wait_event(events[need])
@@ -443,6 +446,7 @@ def main():
                 out.append(rec)
             return out
         events = {m: torch.cuda.Event() for m in marks}
+        store_done = torch.cuda.Event()  # (recorded after each step's store build)
         graphs = record_groups(children, bufs)
         for _ in range(args.lanes - 1):
             # another lane: its own engine (table copy, store, streams), warmed once, then recorded
