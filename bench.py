@@ -170,6 +170,11 @@ def main():
         sthreads = [[n for n in g.split(",") if n in stages] for g in args.shard_groups.split("|")]
         sthreads = [g for g in sthreads if g]
         snames = [n for g in sthreads for n in g]
+        if len(sthreads) > 1 and world > 1 and args.dist_backend == "nccl" and not args.serial:
+            # one communicator per host thread: RCCL collectives of different communicators issued
+            # in different orders on different ranks can deadlock once their kernels share one of
+            # the process' four hardware queues - one driver thread, one order
+            raise SystemExit("bench: --shard-groups with several threads is refused over RCCL at world > 1")
         if args.serial:
             skids = {n: eng for n in snames}
             sgroups = {n: None for n in snames}
@@ -204,6 +209,7 @@ def main():
         rq2c_shard = par.GpuRQ2CountShard(skids.get("rq2_count", eng))
         rq4a_shard = par.GpuRQ4aShard(skids.get("rq4a", eng), M)
         rq4b_shard = par.GpuRQ4bShard(skids.get("rq4b", eng))
+        rq2a_shard = par.GpuRQ2AddShard(skids.get("rq2_add", eng))
         if args.strong:
             own = (lo, hi)
         else:
@@ -240,14 +246,12 @@ def main():
             par.gather_rows({"issue": part["matched_issue"], "build": part["matched_build"]}, world)
 
         def sh_rq2_add(e):
-            if not pre_add[0]:
-                launch["rq2_add"](e, bufs["rq2_add"])
-            pre_add[0] = False
-            b = bufs["rq2_add"]
-            if world > 1:  # (one rank: its rows are the result - nothing to read or gather)
-                n_add = int(b.counts[E.RQ2A_ROWS].item())
-                par.gather_rows({"project": b.row_project[:n_add], "diff_total": b.diff_total[:n_add],
-                                 "diff_coverage": b.diff_coverage[:n_add]}, world)
+            if world > 1:  # flags OR-reduced, change rows gathered in rank order
+                par.rq2_add_sharded(rq2a_shard, rank, world)
+                return
+            if not rq2a_shard.pre:  # (one rank: its rows are the result - nothing to read or gather)
+                rq2a_shard.launch()
+            rq2a_shard.pre = False
         # the drivers' final host copies are deferred (parallel.Deferred) and made in one copy at the
         # end of the step (par.finalize_all): the GPU is drained once, not once per driver
         pending = []
@@ -271,18 +275,13 @@ def main():
         }
 
         # the local kernels of every driver (graph-capturable: no host reads), for the recordings
-        pre_add = [False]
         shards = {"rq1": rq1_shard, "rq3": rq3_shard, "rq2_count": rq2c_shard, "rq4a": rq4a_shard,
-                  "rq4b": rq4b_shard}
+                  "rq4b": rq4b_shard, "rq2_add": rq2a_shard}
         local_launch = {n: shards[n].launch for n in shards}
-        local_launch["rq2_add"] = lambda: launch["rq2_add"](skids["rq2_add"], bufs["rq2_add"])
 
         def mark_launched(names):
             for n in names:
-                if n == "rq2_add":
-                    pre_add[0] = True
-                else:
-                    shards[n].pre = True
+                shards[n].pre = True
 
         drv_ms = {}  # host wall time per driver (its launches, syncs and collectives), summed over steps
 

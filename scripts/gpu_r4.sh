@@ -19,7 +19,7 @@ for s in $STEPS; do
       st=20; [ "$arg" != c2 ] && st=3
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_prof_$arg -o run -- python3 -u bench.py --config $arg --steps $st --warmup 2 --no-cpu-baseline > $O/${T}_prof_$arg.log 2>&1 || exit $?
       f=$(ls $O/${T}_prof_$arg/*/run_kernel_stats.csv 2>/dev/null | head -1); [ -z "$f" ] && f=$(find $O/${T}_prof_$arg -name "*kernel_stats.csv" | head -1)
-      python3 scripts/kstats.py "$f" $((st + 3)) 40 > $O/${T}_kstats_$arg.txt; head -30 $O/${T}_kstats_$arg.txt ;;
+      python3 scripts/kstats.py "$f" auto 40 > $O/${T}_kstats_$arg.txt; head -30 $O/${T}_kstats_$arg.txt ;;
     stages)
       CONFIG=$arg timeout -k 10 900 bash scripts/stage_times.sh > $O/${T}_stages_$arg.txt 2>&1 || exit $?; cat $O/${T}_stages_$arg.txt ;;
     st8)  # per-stage serial step times of shard 0 of 8 (the strong rehearsal's per-rank table)

@@ -11,8 +11,10 @@ The oracle's per-project Python loops cannot run at this size, so the checks are
   median, rq2_coverage_count.py:139-152,439-440) and RQ4b's quartiles (rq4b:966-972), the median-trend
   tests (:443-458), rq4b's last session / six Spearman tests (:849-899), deltas (:725-797) and
   initial-coverage tests (:221-313), recomputed with numpy / scipy (1e-9 relative);
-* a sampled oracle comparison: 50 random projects' Shapiro-Wilk and Spearman (rq2_coverage_count.py:
-  305-322) and 50 random sessions' Brunner-Munzel p (rq4b:978-985) with scipy;
+* a sampled oracle comparison independent of the product's special functions: 500 random projects'
+  Shapiro-Wilk W / p and Spearman (rq2_coverage_count.py:305-322) and 500 random sessions'
+  Brunner-Munzel p (rq4b:978-985) with scipy (the C++ port below shares csrc/fz_stats.h with the
+  kernels; scipy does not);
 * and without sampling, every per-project / per-session statistic of RQ2 count and RQ4b against the
   multi-core C++ restatement (oracle/cpu/fz_cpu.cpp) on the same table.
 
@@ -174,7 +176,7 @@ def test_rq2_count_fullsize(case):
     assert_same(r.shapiro_median_p, pw if K >= 3 else None, "shapiro_median_p")
     # sampled per-project tests (:305-322) against scipy
     pos = np.cumsum(np.r_[0, n_tr])
-    for k in RNG.choice(len(h.elig), size=min(len(h.elig), 50), replace=False).tolist():
+    for k in RNG.choice(len(h.elig), size=min(len(h.elig), 500), replace=False).tolist():
         x = vals[pos[k]:pos[k + 1]]
         rho, pr, w, pw = orc.series_tests(x)
         assert_same((float(r.sw_w[k]), float(r.sw_p[k])), (w, pw), f"shapiro[{h.elig[k]}]")
@@ -207,8 +209,8 @@ def test_rq4b_fullsize(case):
     if len(both):
         last = int(both[-1])
     # quartiles (:966-972) of every session up to max(20000, last + 1) and of 500 random later ones
-    # (config 5's giant projects make ~20M mostly single-value sessions); BM p of 50 sampled
-    # sessions (:978-985)
+    # (config 5's giant projects make ~20M mostly single-value sessions); BM p of 500 sampled
+    # sessions (:978-985) with scipy
     lim = min(ms, max(20000, last + 1))
     idx = np.r_[np.arange(lim), np.sort(RNG.choice(np.arange(lim, ms), size=min(500, ms - lim), replace=False))
                 if ms > lim else np.zeros(0, np.int64)].astype(np.int64)
@@ -222,7 +224,7 @@ def test_rq4b_fullsize(case):
             q1[k] = np.percentile(b, [25, 50, 75])
     assert_same(r.g2_q[idx], q2, "g2_q")
     assert_same(r.g1_q[idx], q1, "g1_q")
-    for i in RNG.choice(ms, size=min(ms, 50), replace=False).tolist():
+    for i in RNG.choice(ms, size=min(ms, 500), replace=False).tolist():
         a, b = session(g2, i), session(g1, i)
         exp = np.nan
         if len(a) >= 5 and len(b) >= 5:

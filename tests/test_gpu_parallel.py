@@ -68,6 +68,23 @@ class _RQ2View(_HostView):
         return self.s.mean_median(x.to(self.dev))
 
 
+class _RQ2AddView(_HostView):
+    """... and maps the shard's build / coverage row ids to the whole table's (-1 kept)."""
+
+    def __init__(self, shard, dev, rows):
+        super().__init__(shard, dev)
+        self.rows = rows
+
+    def run(self):
+        out = {k: v.cpu() for k, v in self.s.run().items()}
+        for k, tab in (("row_first_build", self.rows.builds), ("row_end_build", self.rows.builds),
+                       ("row_start_build", self.rows.builds), ("row_cov_i", self.rows.coverage),
+                       ("row_cov_i1", self.rows.coverage)):
+            ids = out[k].numpy()
+            out[k] = torch.from_numpy(np.where(ids >= 0, tab[np.maximum(ids, 0)], -1).astype(np.int64))
+        return out
+
+
 class _RQ4aView(_HostView):
     def finish(self, tables, intro, steps, counts):
         c = counts.to(self.dev)
@@ -106,13 +123,21 @@ def _worker(rank, world, port, case, errfile):
         dist.destroy_process_group()
 
 
+def _table(case, world):
+    if case == "c2_collide":  # the full config-2 table, 4,000 issue numbers reused across projects
+        from tse_amd import synth
+        return synth.generate(synth.config("c2", dup_numbers=4000))
+    return make_table(case, world)
+
+
 def _check(rank, world, case):
     from gpu_common import assert_same
     from oracle import rq_oracle as orc
+    from test_parallel import rq2_add_result
     from tse_amd import engine as E
     from tse_amd import parallel as par
     from tse_amd.rq import compute
-    t = make_table(case, world)
+    t = _table(case, world)
     lo, hi = par.shard_bounds(t, world)[rank]
     ts, rows = par.take_shard(t, lo, hi)
     eng = E.Engine(0)
@@ -131,36 +156,68 @@ def _check(rank, world, case):
     r2 = par.rq2_count_sharded(_RQ2View(par.GpuRQ2CountShard(eng), eng.dev), rank, world, lo, hi)
     r4 = par.rq4a_sharded(_RQ4aView(par.GpuRQ4aShard(eng, M), eng.dev), rank, world, lo, hi)
     r4b = par.rq4b_sharded(_RQ4bView(par.GpuRQ4bShard(eng), eng.dev), rank, world)
+    r2a = par.rq2_add_sharded(_RQ2AddView(par.GpuRQ2AddShard(eng), eng.dev, rows), rank, world)
+    any_rerun = torch.tensor([int(reran)])
+    torch.distributed.all_reduce(any_rerun)
     if rank == 0:
+        if case == "c2_collide":
+            # the whole table on one engine (compute.*: the single-GPU path, pinned to the oracle by
+            # test_gpu_scale / test_gpu_rq*): every driver's recombination must equal it
+            assert int(any_rerun) > 0, "the table was built to need the cross-shard ROW_NUMBER dedup"
+            one = E.Engine(0)
+            one.upload(t)
+            one.build_store()
+            ref = {"rq1": compute.rq1(one), "rq2_count": compute.rq2_count(one), "rq2_add": compute.rq2_add(one),
+                   "rq3": compute.rq3(one), "rq4a": compute.rq4a(one), "rq4b": compute.rq4b(one)}
+            one.close()
+            assert len(ref["rq1"].matched_issue) > 0 and len(ref["rq2_add"].row_project) > 0
+            assert len(ref["rq3"].det_pct) > 0 and ref["rq4b"].n_sessions > 0
+        else:
+            ref = {"rq1": orc.rq1(t), "rq2_count": orc.rq2_count(t), "rq2_add": orc.rq2_add(t), "rq3": orc.rq3(t),
+                   "rq4a": orc.rq4a(t), "rq4b": orc.rq4b(t)}
+        assert_same(rq2_add_result(*r2a), ref["rq2_add"], "rq2_add")
         ours2 = compute.rq2_count_result(r2["proj"], r2["session_offsets"], r2["session_values"], r2["K"],
                                          r2["average"], r2["median"], r2["percentiles"], r2["average"],
                                          (r2["tests"][0], r2["tests"][1], r2["tests"][3]), r2["corr_mm"], r2["null_lines"])
-        assert_same(ours2, orc.rq2_count(t), "rq2_count")
+        assert_same(ours2, ref["rq2_count"], "rq2_count")
         ours4 = compute.rq4a_result(r4["counts"], r4["scalars"], r4["member"], r4["tables"], r4["intro"],
                                     r4["g4_steps"], r4["g4_transition"])
-        assert_same(ours4, orc.rq4a(t), "rq4a")
+        assert_same(ours4, ref["rq4a"], "rq4a")
         ours4b = compute.rq4b_result(r4b["counts"], r4b["c2"], r4b["c1"], r4b["g2_q"], r4b["g1_q"], r4b["p_bm"],
                                      r4b["sp6"], r4b["pre_cov"], r4b["post_cov"], r4b["pre_median"],
                                      r4b["post_median"], r4b["init_g2"], r4b["init_g1"], r4b["tests"])
-        assert_same(ours4b, orc.rq4b(t), "rq4b")
+        assert_same(ours4b, ref["rq4b"], "rq4b")
         ours3 = compute.rq3_result(total3, {k: v.numpy() for k, v in cols3.items()}, st3["describe"].numpy(),
                                    st3["tests"].numpy())
-        assert_same(ours3, orc.rq3(t), "rq3")
+        assert_same(ours3, ref["rq3"], "rq3")
         ours1 = compute.rq1_result(counts.numpy(), it.numpy()[:int(counts[E.RQ1_MAX_ITER])],
                                    idt.numpy()[:int(counts[E.RQ1_MAX_ITER])], late, rows1["matched_issue"].numpy(),
                                    rows1["matched_build"].numpy(), np.nonzero(elig.numpy())[0])
-        assert_same(ours1, orc.rq1(t), "rq1")
+        assert_same(ours1, ref["rq1"], "rq1")
     eng.close()
+
+
+def _spawn(case, world, tmp_path):
+    errfile = str(tmp_path / "err")
+    try:
+        mp.spawn(_worker, args=(world, _free_port(), case, errfile), nprocs=world, join=True)
+    except Exception:
+        msgs = [open(f"{errfile}.{r}").read() for r in range(world) if os.path.exists(f"{errfile}.{r}")]
+        raise AssertionError("\n".join(msgs) or "worker failed")
 
 
 @pytest.mark.parametrize("case", ["collide", "last_shard_no_issues"])
 def test_gpu_sharded_rq1_rq3(case, tmp_path):
-    errfile = str(tmp_path / "err")
-    try:
-        mp.spawn(_worker, args=(2, _free_port(), case, errfile), nprocs=2, join=True)
-    except Exception:
-        msgs = [open(f"{errfile}.{r}").read() for r in range(2) if os.path.exists(f"{errfile}.{r}")]
-        raise AssertionError("\n".join(msgs) or "worker failed")
+    _spawn(case, 2, tmp_path)
+
+
+@pytest.mark.timeout(900)
+def test_gpu_sharded_six_drivers_c2_world4(tmp_path):
+    """All six sharded drivers on the full config-2 table over four ranks on cuda:0, issue numbers
+    reused across projects (and so across shards: the cross-shard ROW_NUMBER re-run of
+    queries1.py:29-32 happens), recombined and compared with the single-GPU analyses of the whole
+    table - RQ1 counters / tables / rows, RQ2 count and add, RQ3 samples + statistics, RQ4a, RQ4b."""
+    _spawn("c2_collide", 4, tmp_path)
 
 
 def test_host_many_gather():
@@ -190,3 +247,68 @@ def test_host_many_gather():
     assert got[2] == 7 and list(got[3]) == [0, 1]
     mid = torch.randn(300_000, dtype=torch.float64, device=dev)  # (grows the pinned staging area)
     np.testing.assert_array_equal(par.host_many(mid[::3], mid[1::2])[1], mid[1::2].cpu().numpy())
+
+
+def _deferred_worker(rank, world, port, errfile):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _deferred_check(rank, world)
+    except BaseException:
+        import traceback
+        with open(f"{errfile}.{rank}", "w") as f:
+            f.write(traceback.format_exc())
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _deferred_check(rank, world):
+    """bench.py's sharded step: the GPU shards' device tensors straight into the drivers (gloo stages
+    them through the host), RQ2 count / RQ4a / RQ4b each on its own child engine's stream with
+    finish_later=True, one finalize_all after this stream waits for the children - equal to the
+    eager drivers on the parent engine."""
+    from gpu_common import assert_same
+    from tse_amd import engine as E
+    from tse_amd import parallel as par
+    t = make_table("collide", world)
+    lo, hi = par.shard_bounds(t, world)[rank]
+    ts, _ = par.take_shard(t, lo, hi)
+    eng = E.Engine(0)
+    eng.upload(ts)
+    st = eng.build_store()
+    M = par.agree_max(int(st.max_fuzz_per_project), eng.dev)
+    with torch.cuda.stream(eng.stream):
+        eager = [par.rq2_count_sharded(par.GpuRQ2CountShard(eng), rank, world, lo, hi),
+                 par.rq4a_sharded(par.GpuRQ4aShard(eng, M), rank, world, lo, hi),
+                 par.rq4b_sharded(par.GpuRQ4bShard(eng), rank, world)]
+    for _ in range(2):  # (twice: the shards' buffers are reused by the second step)
+        kids = [eng.child() for _ in range(3)]
+        pend = []
+        with torch.cuda.stream(kids[0].stream):
+            pend.append(par.rq2_count_sharded(par.GpuRQ2CountShard(kids[0]), rank, world, lo, hi,
+                                              finish_later=True))
+        with torch.cuda.stream(kids[1].stream):
+            pend.append(par.rq4a_sharded(par.GpuRQ4aShard(kids[1], M), rank, world, lo, hi, finish_later=True))
+        with torch.cuda.stream(kids[2].stream):
+            pend.append(par.rq4b_sharded(par.GpuRQ4bShard(kids[2]), rank, world, finish_later=True))
+        assert all(isinstance(d, par.Deferred) for d in pend)
+        cur = torch.cuda.current_stream(eng.dev)
+        for k in kids:
+            cur.wait_stream(k.stream)
+        got = par.finalize_all(pend)
+        for name, a, b in zip(("rq2_count", "rq4a", "rq4b"), got, eager):
+            assert_same(a, b, name)
+        for k in kids:
+            k.close()
+    eng.close()
+
+
+def test_gpu_sharded_deferred_matches_eager(tmp_path):
+    errfile = str(tmp_path / "err")
+    try:
+        mp.spawn(_deferred_worker, args=(2, _free_port(), errfile), nprocs=2, join=True)
+    except Exception:
+        msgs = [open(f"{errfile}.{r}").read() for r in range(2) if os.path.exists(f"{errfile}.{r}")]
+        raise AssertionError("\n".join(msgs) or "worker failed")

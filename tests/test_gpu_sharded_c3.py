@@ -1,6 +1,6 @@
 """The project-sharded path on the FULL config-3 and config-5 tables (100M coverage
 rows over 10k projects, "project-sharded over 2/4/8 MI355X"; config 5 Zipf-skewed, its ~20M-row giant
-whole on one shard): two or four ranks on cuda:0, each holding only its
+whole on one shard): two, four or eight ranks on cuda:0, each holding only its
 ``parallel.shard_bounds`` half of the projects, run RQ2-count and RQ4b through libfz
 (fz_rq2_count_ex / fz_rq4b_ex with the session statistics skipped, then the all-to-all by session
 index to the session owners, fz_rq2_session_stats / fz_rq4b_session_stats there, and the gathers)
@@ -101,7 +101,7 @@ def _check(rank, world, name):
     assert_same(ours4b, ref4b, "rq4b")
 
 
-@pytest.mark.parametrize("name,world", [("c3", 2), ("c3", 4), ("c5", 2), ("c5", 4)])
+@pytest.mark.parametrize("name,world", [("c3", 2), ("c3", 4), ("c3", 8), ("c5", 2), ("c5", 4), ("c5", 8)])
 def test_sharded_fullsize_matches_single_gpu(name, world, tmp_path):
     errfile = str(tmp_path / "err")
     try:

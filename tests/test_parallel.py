@@ -195,6 +195,44 @@ class OracleRQ2CountShard:
             return float(np.mean(x.numpy())), float(np.median(x.numpy()))
 
 
+class OracleRQ2AddShard:
+    """One rank's RQ2 add on the CPU restatement: flags over the global project axis, change rows
+    with global build / coverage row ids (-1 kept)."""
+
+    def __init__(self, t, rows):
+        self.t, self.rows = t, rows
+
+    def run(self):
+        from oracle import rq_oracle as orc
+        return rq2_add_part(orc.rq2_add(self.t), len(self.t.projects), self.rows)
+
+
+def rq2_add_part(r, P, rows):
+    """An RQ2AddResult of one shard in rq2_add_sharded's run() layout, row ids mapped to the table's."""
+    def gid(ids, table):
+        ids = np.asarray(ids, np.int64)
+        return np.where(ids >= 0, table[np.maximum(ids, 0)] if len(table) else ids, -1).astype(np.int64)
+    el = np.zeros(P, np.int64)
+    el[r.projects] = 1
+    T = lambda a, dt=np.int64: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))  # noqa: E731
+    return {"eligible": T(el), "covered_is_float": T(r.covered_is_float), "total_is_float": T(r.total_is_float),
+            "row_project": T(r.row_project), "row_first_build": T(gid(r.row_first_build, rows.builds)),
+            "row_end_build": T(gid(r.row_end_build, rows.builds)),
+            "row_start_build": T(gid(r.row_start_build, rows.builds)),
+            "row_cov_i": T(gid(r.row_cov_i, rows.coverage)), "row_cov_i1": T(gid(r.row_cov_i1, rows.coverage)),
+            "diff_total": T(r.diff_total, np.float64), "diff_coverage": T(r.diff_coverage, np.float64)}
+
+
+def rq2_add_result(flags, cols):
+    """The recombined RQ2AddResult of rq2_add_sharded's output."""
+    from tse_amd.rq.results import RQ2AddResult
+    f = {k: np.asarray(v) for k, v in flags.items()}
+    return RQ2AddResult(projects=np.nonzero(f["eligible"])[0],
+                        **{k: np.asarray(cols[k]) for k in par.RQ2A_ROW_COLS},
+                        covered_is_float=f["covered_is_float"].astype(bool),
+                        total_is_float=f["total_is_float"].astype(bool))
+
+
 class OracleRQ4aShard:
     """One rank's RQ4a on the CPU restatement, in fz_rq4a's output layout."""
 
@@ -363,6 +401,7 @@ def _check(rank, world, case, threaded=False, deferred=False):
     # single-thread sharded step)
     drivers = {"rq1": rq1,
                "rq3": lambda: par.rq3_sharded(OracleRQ3Shard(ts, rows), rank, world),
+               "rq2a": lambda: par.rq2_add_sharded(OracleRQ2AddShard(ts, rows), rank, world),
                "rq2": lambda: par.rq2_count_sharded(OracleRQ2CountShard(ts), rank, world, lo, hi,
                                                     finish_later=deferred),
                "rq4a": lambda: par.rq4a_sharded(OracleRQ4aShard(ts, M4), rank, world, lo, hi, finish_later=deferred),
@@ -390,6 +429,7 @@ def _check(rank, world, case, threaded=False, deferred=False):
     r2, r4, r4b = res["rq2"], res["rq4a"], res["rq4b"]
     if rank != 0:
         return
+    assert_same(rq2_add_result(*res["rq2a"]), orc.rq2_add(t), "rq2_add")
     g = orc.rq1(t)
     assert int(any_rerun) > 0, "the table was built to need the cross-shard dedup"
     c = counts.numpy()

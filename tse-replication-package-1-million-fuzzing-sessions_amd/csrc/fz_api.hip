@@ -1,6 +1,7 @@
 // Public C ABI (include/fz.h): error capture, context lifetime, and thin wrappers that reset the
 // scratch arena and forward to the implementation.
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -608,11 +609,18 @@ __global__ __launch_bounds__(256) void k_gather_to_host(const GatherList g, unsi
 }  // namespace
 
 int fz_gather_to_host(void *stream, const fz_host_piece *pieces, int n_pieces, void *host_out, int64_t total_bytes) {
-    // one pinned staging area for the process (mapped: kernels write it through its device address),
-    // grown on demand; the lock makes concurrent callers take turns
+    // one pinned staging area per device (mapped: kernels write it through its device address),
+    // allocated at parallel.host_many's 4 MiB cap and grown only for a larger caller; the lock makes
+    // concurrent callers take turns.  Every use ends with a sync of its own stream and the copy out
+    // before the lock is released, so the area is idle whenever a caller holds the lock: growing it
+    // needs no device-wide synchronisation (other threads' streams keep running)
+    struct Area {
+        void *h = nullptr, *d = nullptr;
+        size_t cap = 0;
+    };
     static std::mutex mu;
-    static void *h_area = nullptr, *d_area = nullptr;
-    static size_t cap = 0;
+    static std::map<int, Area> areas;
+    constexpr size_t kAreaMin = size_t(4) << 20;
     try {
         FZ_CHECK(n_pieces >= 0 && total_bytes >= 0 && (n_pieces == 0 || pieces) && (total_bytes == 0 || host_out),
                  "fz_gather_to_host: bad arguments");
@@ -626,19 +634,21 @@ int fz_gather_to_host(void *stream, const fz_host_piece *pieces, int n_pieces, v
         }
         if (total_bytes == 0) return FZ_OK;
         hipStream_t st = static_cast<hipStream_t>(stream);
+        int dev = 0;
+        FZ_HIP(hipGetDevice(&dev));
         std::lock_guard<std::mutex> lk(mu);
-        if (size_t(total_bytes) > cap) {
-            if (h_area) {
-                FZ_HIP(hipDeviceSynchronize());
-                FZ_HIP(hipHostFree(h_area));
-                h_area = d_area = nullptr;
-                cap = 0;
+        Area &a = areas[dev];
+        if (size_t(total_bytes) > a.cap) {
+            if (a.h) {  // (idle: its last user synchronised its stream before releasing the lock)
+                FZ_HIP(hipHostFree(a.h));
+                a = Area{};
             }
-            const size_t want = size_t(total_bytes) < (size_t(1) << 20) ? (size_t(1) << 20) : size_t(total_bytes) * 2;
-            FZ_HIP(hipHostMalloc(&h_area, want, hipHostMallocMapped | hipHostMallocPortable));
-            FZ_HIP(hipHostGetDevicePointer(&d_area, h_area, 0));
-            cap = want;
+            const size_t want = size_t(total_bytes) <= kAreaMin ? kAreaMin : size_t(total_bytes) * 2;
+            FZ_HIP(hipHostMalloc(&a.h, want, hipHostMallocMapped | hipHostMallocPortable));
+            FZ_HIP(hipHostGetDevicePointer(&a.d, a.h, 0));
+            a.cap = want;
         }
+        void *h_area = a.h, *d_area = a.d;
         for (int b = 0; b < n_pieces; b += kGatherPieces) {
             GatherList g{};
             int64_t most = 0;

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -152,41 +153,62 @@ char *put_pool(char *p, const char *blob, const int64_t *off, int64_t id) {
 
 char *put_i64(char *p, int64_t v) { return std::to_chars(p, p + 24, v).ptr; }
 
-// rows [r0, r1) formatted by fmt(row, char *p) -> end, into per-worker strings, then concatenated
+// rows [r0, r1) formatted by fmt(row, char *p) -> end.  Each worker formats its row range into a
+// chain of 1 MiB blocks (a new block when the next row's bound does not fit), so its scratch is the
+// exact output plus at most one row bound per block - not a worst-case-sized, zero-filled string -
+// and the blocks are then copied to `out` at the workers' prefix-summed offsets
 template <typename Bound, typename Fmt>
 int64_t parallel_rows(int64_t n, int nthreads, char *out, int64_t cap, int64_t *row_end, Bound bound, Fmt fmt) {
     if (nthreads < 1) nthreads = 1;
     if (n < 4096) nthreads = 1;
     if (nthreads > 64) nthreads = 64;
-    std::vector<std::string> parts(static_cast<size_t>(nthreads));
+    constexpr int64_t kBlock = int64_t(1) << 20;
+    struct Block {
+        std::unique_ptr<char[]> buf;
+        int64_t used = 0, cap = 0;
+    };
+    std::vector<std::vector<Block>> parts(static_cast<size_t>(nthreads));
+    std::vector<int64_t> sizes(static_cast<size_t>(nthreads), 0);
     std::vector<std::thread> th;
     auto work = [&](int w) {
         const int64_t r0 = n * w / nthreads, r1 = n * (w + 1) / nthreads;
-        int64_t b = 0;
-        for (int64_t r = r0; r < r1; ++r) b += bound(r);
-        std::string &s = parts[size_t(w)];
-        s.resize(size_t(b));
-        char *p = s.data();
+        std::vector<Block> &bl = parts[size_t(w)];
+        int64_t done = 0;  // bytes of the finished blocks
         for (int64_t r = r0; r < r1; ++r) {
-            p = fmt(r, p);
-            if (row_end) row_end[r] = int64_t(p - s.data());  // (local; shifted below)
+            const int64_t b = bound(r);
+            if (bl.empty() || bl.back().used + b > bl.back().cap) {
+                if (!bl.empty()) done += bl.back().used;
+                Block nb;
+                nb.cap = b > kBlock ? b : kBlock;
+                nb.buf.reset(new char[size_t(nb.cap)]);
+                bl.push_back(std::move(nb));
+            }
+            Block &k = bl.back();
+            char *p = fmt(r, k.buf.get() + k.used);
+            k.used = int64_t(p - k.buf.get());
+            if (row_end) row_end[r] = done + k.used;  // (local; shifted below)
         }
-        s.resize(size_t(p - s.data()));
+        sizes[size_t(w)] = done + (bl.empty() ? 0 : bl.back().used);
     };
     for (int w = 1; w < nthreads; ++w) th.emplace_back(work, w);
     work(0);
     for (auto &t : th) t.join();
     int64_t total = 0;
-    for (auto &s : parts) total += int64_t(s.size());
+    for (int64_t v : sizes) total += v;
     if (total > cap) return -1;
     int64_t o = 0;
     for (int w = 0; w < nthreads; ++w) {
-        std::memcpy(out + o, parts[size_t(w)].data(), parts[size_t(w)].size());
+        int64_t q = o;
+        for (const Block &k : parts[size_t(w)]) {
+            std::memcpy(out + q, k.buf.get(), size_t(k.used));
+            q += k.used;
+        }
         if (row_end && o) {
             const int64_t r0 = n * w / nthreads, r1 = n * (w + 1) / nthreads;
             for (int64_t r = r0; r < r1; ++r) row_end[r] += o;
         }
-        o += int64_t(parts[size_t(w)].size());
+        parts[size_t(w)].clear();
+        o += sizes[size_t(w)];
     }
     return total;
 }

@@ -26,7 +26,8 @@ RQ3 (``rq3_sharded``)
       every rank runs with ``FZ_RQ3_FLUSH_LAST`` and the tail of the last rank with issues is
       dropped;
     * the statistics run once over the gathered samples (``fz_rq3_stats``).
-RQ2 coverage-and-added (``gather_rows``): per-project change rows, concatenated in rank order.
+RQ2 coverage-and-added (``rq2_add_sharded``): per-project change rows, concatenated in rank order;
+    the per-project flags OR-combined.
 
 The drivers take a *shard* object (``run`` / ``finish`` / ``stats``) so the same exchange code runs
 over the GPU engine (``GpuRQ1Shard``, ``GpuRQ3Shard``) and, in the CPU tests, over the oracle.
@@ -432,7 +433,9 @@ def rq3_sharded(shard, rank: int, world: int):
     """Exact RQ3 over project shards.  ``shard.run()`` runs with FZ_RQ3_FLUSH_LAST and returns
     counts[RQ3_NCOUNTS] int64 plus the det_* / non_* columns (sliced to their lengths);
     ``shard.stats(det_pct, det_tot, non_pct)`` runs the statistics over the gathered samples.
-    Returns (counts, columns dict, stats) - columns in global project order."""
+    Returns (counts, columns dict, stats) - columns in global project order.  At world 1 (one piece,
+    no concatenation) the columns ALIAS the shard's persistent buffers: they are valid until the
+    shard's next run; a caller that keeps a step's samples past that clones them."""
     import torch
     part = shard.run()
     counts = part["counts"]
@@ -466,6 +469,28 @@ def rq3_sharded(shard, rank: int, world: int):
         raise TypeError("'>' not supported between instances of 'NoneType' and 'int'")
     st = shard.stats(out["det_pct"], out["det_tot"], out["non_pct"])
     return total, out, st
+
+
+# ------------------------------------------------------------------------------------- RQ2 add
+RQ2A_ROW_COLS = ("row_project", "row_first_build", "row_end_build", "row_start_build", "row_cov_i", "row_cov_i1",
+                 "diff_total", "diff_coverage")
+RQ2A_FLAGS = ("eligible", "covered_is_float", "total_is_float")
+
+
+def rq2_add_sharded(shard, rank: int, world: int):
+    """Exact RQ2 add over project shards.  rq2_coverage_and_added.py:73-238 runs one project at a
+    time - a project's change rows read only its own Coverage builds and coverage rows - so the
+    result is the shards' rows concatenated in rank (= project) order, and the per-project flags
+    (eligible, the covered / total float upcasts) summed over disjoint project ranges (= OR).
+    ``shard.run()`` returns the flags [P] and the RQ2A_ROW_COLS columns of this rank's rows (row ids
+    in whatever id space the caller wants gathered).  Returns (flags dict of [P] int64, rows dict)."""
+    import torch
+    part = shard.run()
+    flags = torch.stack([part[k].to(torch.int64) for k in RQ2A_FLAGS])
+    if world > 1:
+        all_reduce(flags)
+    rows = gather_rows({k: part[k] for k in RQ2A_ROW_COLS}, world)
+    return dict(zip(RQ2A_FLAGS, flags)), rows
 
 
 # ------------------------------------------------------------------------------ session exchange
@@ -1026,6 +1051,32 @@ class GpuRQ4aShard:
         E._check(eng.lib, eng.lib.fz_rq4a_finish(eng.ctx, *[P(x) for x in tables], tables[0].numel(), P(intro),
                                                  intro.numel(), P(steps), P(counts), P(b.scalars)))
         return b.scalars  # device: copied with the other results (parallel.host_many)
+
+
+class GpuRQ2AddShard:
+    """RQ2 add of one rank on its engine (fz_rq2_add): the flags and the change rows, sliced on the
+    device to the row count (one host read of the counter)."""
+
+    def __init__(self, eng):
+        from . import engine as E
+        from .rq import compute
+        self.E, self.eng, self.compute = E, eng, compute
+        self.bufs = compute.rq2_add_buffers(eng)
+
+    pre = False  # launch() already enqueued this step's kernels (a recorded local phase)
+
+    def launch(self):
+        self.compute.rq2_add_launch(self.eng, self.bufs)
+
+    def run(self):
+        b, P = self.bufs, self.eng.tables.fz.n_projects
+        if not self.pre:
+            self.launch()
+        self.pre = False
+        n = int(host_many(b.counts[self.E.RQ2A_ROWS])[0])
+        out = {k: getattr(b, k)[:P] for k in RQ2A_FLAGS}
+        out.update({k: getattr(b, k)[:n] for k in RQ2A_ROW_COLS})
+        return out
 
 
 class GpuRQ4bShard:
