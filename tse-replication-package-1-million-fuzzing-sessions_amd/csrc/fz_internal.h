@@ -270,7 +270,14 @@ struct ProbeScope {
     int owner = -1;
     const int64_t *d_count = nullptr;
     double per_count = 0.0;
+    const int64_t *d_count2 = nullptr;  // (a second device count, add_count)
+    double per_count2 = 0.0;
     size_t pair = 0;  // index of this scope's (start, stop) events in the pool
+    // per bytes more for every unit of another device count (read when the scope closes)
+    void add_count(const int64_t *count, double per) {
+        d_count2 = count;
+        per_count2 = per;
+    }
     ProbeScope(fz_ctx *ctx, const char *name, double bytes, const int64_t *count = nullptr, double per = 0.0)
         : c(ctx), on(false), d_count(count), per_count(per) {
         Probe &p = c->probe;
@@ -306,10 +313,13 @@ struct ProbeScope {
         if (!on) return;
         Probe &p = c->probe;
         (void)hipEventRecord(p.pool[pair + 1], c->stream);
-        if (d_count && int64_t(p.deferred.size()) < Probe::kMaxCounts) {
+        const int64_t *dc[2] = {d_count, d_count2};
+        const double pc[2] = {per_count, per_count2};
+        for (int i = 0; i < 2; ++i) {
+            if (!on || !dc[i] || int64_t(p.deferred.size()) >= Probe::kMaxCounts) continue;
             const int64_t slot = int64_t(p.deferred.size());
-            (void)hipMemcpyAsync(p.counts.as<int64_t>() + slot, d_count, 8, hipMemcpyDeviceToDevice, c->stream);
-            p.deferred.push_back({owner, slot, per_count});
+            (void)hipMemcpyAsync(p.counts.as<int64_t>() + slot, dc[i], 8, hipMemcpyDeviceToDevice, c->stream);
+            p.deferred.push_back({owner, slot, pc[i]});
         }
     }
 };

@@ -190,7 +190,7 @@ struct ValidFuzzRq1 {  // result IN ('Finish', 'Halfway') AND DATE(timecreated) 
     const int64_t *time;
     __device__ bool operator()(int32_t r) const {
         const uint8_t x = result[r];
-        return (x == 0 || x == 1) && time[r] < kLimitUs;
+        return (x <= 1) & (time[r] < kLimitUs);
     }
 };
 

@@ -26,21 +26,21 @@ struct CovTrendRows {  // coverage IS NOT NULL AND coverage != 0 AND DATE(date) 
     const int64_t *date;
     const uint8_t *elig;
     __device__ bool operator()(int32_t r) const {
-        return (valid[r] & FZ_VALID_COVERAGE) && cov[r] != 0.0 && date[r] < kLimitUs2 && elig[proj[r]];
+        return bool(valid[r] & FZ_VALID_COVERAGE) & (cov[r] != 0.0) & (date[r] < kLimitUs2) & bool(elig[proj[r]]);
     }
 };
 struct NonZeroTotal {  // `if x[1] != 0` (:300-303); a NULL total (stored 0) passes: None != 0
     static constexpr int kBytes = 9;  // column bytes read per row (filter_compact probe)
     const int64_t *total;
     const uint8_t *valid;
-    __device__ bool operator()(int32_t r) const { return total[r] != 0 || !(valid[r] & FZ_VALID_TOTAL); }
+    __device__ bool operator()(int32_t r) const { return (total[r] != 0) | !(valid[r] & FZ_VALID_TOTAL); }
 };
 // the trend rows (CovTrendRows, then NonZeroTotal) in one filter pass
 struct TrendRows {
     static constexpr int kBytes = 30;  // column bytes read per row (filter_compact probe)
     CovTrendRows v;
     NonZeroTotal nz;
-    __device__ bool operator()(int32_t r) const { return v(r) && nz(r); }
+    __device__ bool operator()(int32_t r) const { return bool(int(v(r)) & int(nz(r))); }
 };
 // raw_n[p] (the project's CovTrendRows rows, the fetched rows of :291-298) = its trend rows + the
 // fetched rows the zero-total test drops: only those (rare) are counted in the filter pass - a count
@@ -50,7 +50,29 @@ struct CountZeroTotal {
     int64_t *out;
     CovTrendRows v;
     NonZeroTotal nz;
-    __device__ bool operator()(int32_t r) const { return v(r) && !nz(r); }
+    __device__ bool operator()(int32_t r) const { return bool(int(v(r)) & int(!nz(r))); }
+};
+
+// What the trend filter writes per kept row: the trend value covered / total * 100 (:300-303) and
+// the project (the per-project sort's segment id) - read from the row while it is filtered, instead
+// of a (row, time, project) copy and a map that gathers the two line counts through it.  A NULL line
+// count makes the reference's float(None) raise (:301): counted, NaN stored.
+struct TrendEmit {
+    static constexpr bool kTime = false;
+    double *tv;
+    uint32_t *oproj;
+    const int64_t *covered, *total;
+    const uint8_t *valid;
+    int64_t *null_lines;
+    __device__ void operator()(int64_t q, int32_t r, int64_t, uint32_t pj) const {
+        oproj[q] = pj;
+        if ((valid[r] & (FZ_VALID_COVERED | FZ_VALID_TOTAL)) != (FZ_VALID_COVERED | FZ_VALID_TOTAL)) {
+            atomicAdd(reinterpret_cast<unsigned long long *>(null_lines), 1ull);
+            tv[q] = NAN;
+            return;
+        }
+        tv[q] = double(covered[r]) / double(total[r]) * 100.0;
+    }
 };
 
 // statistics.mean / median + np.percentile(5, 25, 50, 75, 95) of every session segment; sessions
@@ -168,8 +190,15 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     TmpView T;
     const CovTrendRows vrows{t.c_project, t.c_coverage, t.c_valid, t.c_date, o->eligible};
     const NonZeroTotal nzt{t.c_total, t.c_valid};
-    filter_view(c, s.cov, NC, P, TrendRows{vrows, nzt}, T, nullptr, Selection{},
-                CountZeroTotal{raw_n, vrows, nzt});
+    // trend values in (project, date) order, written by the filter itself
+    double *tv = c->arena.get<double>(NC);
+    T.proj = c->arena.get<uint32_t>(NC);
+    const TrendEmit te{tv, T.proj, t.c_covered, t.c_total, t.c_valid, counts + FZ_RQ2C_NULL_LINES};
+    // (an index range scan: the eligible projects' rows before the date limit only; per kept row:
+    // covered 8 + total 8 + valid 1 read, value 8 + project 4 written)
+    filter_view(c, s.cov, NC, P, TrendRows{vrows, nzt}, T, nullptr,
+                Selection::segments(o->eligible, 1, nullptr, s.cov.offs, kLimitUs2),
+                CountZeroTotal{raw_n, vrows, nzt}, &te, 29.0);
     const int64_t *toffs = T.offs;
     int64_t *d_nt = T.d_n;
     per_seg(c, P, [=] __device__(int64_t p) {
@@ -186,20 +215,6 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
             counts[FZ_RQ2C_VALUES] = *d_nt;
             counts[FZ_RQ2C_SESSIONS] = 1;
         });
-    // trend values in (project, date) order
-    double *tv = c->arena.get<double>(NC);
-    const int32_t *trow = T.row;
-    const int64_t *cov_c = t.c_covered, *cov_t = t.c_total;
-    const uint8_t *cval = t.c_valid;
-    map_n(c, NC, d_nt, [=] __device__(int64_t j) {
-        const int32_t r = trow[j];
-        if ((cval[r] & (FZ_VALID_COVERED | FZ_VALID_TOTAL)) != (FZ_VALID_COVERED | FZ_VALID_TOTAL)) {
-            atomic_add_i64(&counts[FZ_RQ2C_NULL_LINES], 1);  // float(None) raises (:301)
-            tv[j] = NAN;
-            return;
-        }
-        tv[j] = double(cov_c[r]) / double(cov_t[r]) * 100.0;
-    });
 
     // per-project Spearman (vs index) and Shapiro-Wilk
     Segs sp{P, T.offs, NC, M};
@@ -317,7 +332,7 @@ struct CovBuildRows {  // result IN ('HalfWay', 'Finish') AND timecreated < LIMI
     const uint8_t *elig;
     __device__ bool operator()(int32_t r) const {
         const uint8_t x = result[r];
-        return (x == 2 || x == 0) && time[r] < kLimitUs2 && elig[proj[r]];
+        return ((x == 2) | (x == 0)) & (time[r] < kLimitUs2) & bool(elig[proj[r]]);
     }
 };
 struct CovRowsBeforeLimit {  // GET_COVERAGE_DATA: date < LIMIT, no NULL filter (:30-47), eligible
@@ -325,7 +340,7 @@ struct CovRowsBeforeLimit {  // GET_COVERAGE_DATA: date < LIMIT, no NULL filter 
     const uint32_t *proj;
     const int64_t *date;
     const uint8_t *elig;  // (RQ2 add: the projects with a selected Coverage build - the only ones read)
-    __device__ bool operator()(int32_t r) const { return date[r] < kLimitUs2 && elig[proj[r]]; }
+    __device__ bool operator()(int32_t r) const { return (date[r] < kLimitUs2) & bool(elig[proj[r]]); }
 };
 
 __device__ inline int64_t floor_div(int64_t a, int64_t b) {
@@ -371,7 +386,7 @@ void rq2_add(fz_ctx *c, const fz_rq2_add_out *o) {
         map_n(c, P, nullptr, [=] __device__(int64_t p) { withb[p] = el[p] && bo[p + 1] > bo[p] ? 1 : 0; });
     }
     filter_view(c, s.cov, s.cov.n, P, CovRowsBeforeLimit{t.c_project, t.c_date, withb},
-                CV, nullptr, Selection{withb, 1, B.d_n});
+                CV, nullptr, Selection::segments(withb, 1, B.d_n, s.cov.offs, kLimitUs2));
     const int64_t NB = s.covb.n;
     const int64_t *boffs = B.offs, *coffs = CV.offs;
     // pandas upcast flags: a NULL covered/total among the project's fetched coverage rows

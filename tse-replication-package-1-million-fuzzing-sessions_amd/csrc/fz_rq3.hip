@@ -68,13 +68,13 @@ struct FixedIssuesRq3 {  // status fixed, eligible project, rts < LIMIT (:219-23
     const uint8_t *status;
     const int64_t *rts;
     const uint8_t *elig;
-    __device__ bool operator()(int32_t r) const { return status[r] <= 1 && rts[r] < kLim3 && elig[proj[r]]; }
+    __device__ bool operator()(int32_t r) const { return (status[r] <= 1) & (rts[r] < kLim3) & bool(elig[proj[r]]); }
 };
 struct FuzzRq3 {  // Fuzzing, result IN ('HalfWay', 'Finish'), DATE(timecreated) < '2025-01-08' (:260-261)
     static constexpr int kBytes = 9;  // column bytes read per row (filter_compact probe)
     const uint8_t *result;
     const int64_t *time;
-    __device__ bool operator()(int32_t r) const { return (result[r] == 2 || result[r] == 0) && time[r] < kLim3; }
+    __device__ bool operator()(int32_t r) const { return ((result[r] == 2) | (result[r] == 0)) & (time[r] < kLim3); }
 };
 struct CovBuildRq3 {  // Coverage, any result, DATE(timecreated) < '2025-01-09' (:262)
     static constexpr int kBytes = 8;  // column bytes read per row (filter_compact probe)
@@ -89,7 +89,7 @@ struct CovRowsRq3 {  // covered_line IS NOT NULL AND DATE(date) < '2025-01-09' (
     const uint32_t *proj;
     const uint8_t *sel;  // [P] 1: the project has a fixed issue
     __device__ bool operator()(int32_t r) const {
-        return sel[proj[r]] && (valid[r] & FZ_VALID_COVERED) && date[r] < kLim3b;
+        return bool(sel[proj[r]]) & bool(valid[r] & FZ_VALID_COVERED) & (date[r] < kLim3b);
     }
 };
 
@@ -118,7 +118,7 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         map_n(c, P, nullptr, [=] __device__(int64_t p) { self[p] = ioff[p + 1] > ioff[p] ? 1 : 0; });
     }
     filter_view(c, s.cov, NC, P, CovRowsRq3{t.c_valid, t.c_date, t.c_project, self}, TC,
-                nullptr, Selection{self, 1, I.d_n});
+                nullptr, Selection::segments(self, 1, I.d_n, s.cov.offs, kLim3b));
 
     // ---- detected: one thread per issue (:241-302), the detected ones compacted in the same pass
     int64_t *pa = c->arena.get<int64_t>(NI);  // coverage pair (row a, row b)

@@ -36,7 +36,7 @@ struct BuildsBeforeLimit {  // get_project_fuzzing_builds: Fuzzing, any result, 
 struct FixedBeforeLimit {  // get_project_fixed_issues: Fixed*, rts < LIMIT (rq4a:140-153)
     const uint8_t *status;
     const int64_t *rts;
-    __device__ bool operator()(int32_t r) const { return status[r] <= 1 && rts[r] < kLim4; }
+    __device__ bool operator()(int32_t r) const { return (status[r] <= 1) & (rts[r] < kLim4); }
 };
 
 // eligible group membership; rq4a (missing_to_g1) also puts CSV-missing eligible projects in G1
@@ -377,7 +377,18 @@ struct FullTrendRows {  // get_full_coverage_trend: coverage > 0, date < LIMIT (
     const int64_t *date;
     const uint8_t *member;
     __device__ bool operator()(int32_t r) const {
-        return (valid[r] & FZ_VALID_COVERAGE) && cov[r] > 0.0 && date[r] < kLim4 && (member[proj[r]] & 3);
+        return bool(valid[r] & FZ_VALID_COVERAGE) & (cov[r] > 0.0) & (date[r] < kLim4) & bool(member[proj[r]] & 3);
+    }
+};
+// A filter emitter: the kept row's coverage value and its project (rq4b's full series).
+struct ValueProjEmit {
+    static constexpr bool kTime = false;
+    double *val;
+    uint32_t *oproj;
+    const double *cov;
+    __device__ void operator()(int64_t q, int32_t r, int64_t, uint32_t pj) const {
+        val[q] = cov[r];
+        oproj[q] = pj;
     }
 };
 struct PositiveCoverage34 {  // get_coverage_deltas: coverage > 0, any date (rq4b:745-772), G3/G4 only
@@ -387,7 +398,7 @@ struct PositiveCoverage34 {  // get_coverage_deltas: coverage > 0, any date (rq4
     const uint8_t *valid;
     const uint8_t *member;
     __device__ bool operator()(int32_t r) const {
-        return (valid[r] & FZ_VALID_COVERAGE) && cov[r] > 0.0 && (member[proj[r]] & 12);
+        return bool(valid[r] & FZ_VALID_COVERAGE) & (cov[r] > 0.0) & bool(member[proj[r]] & 12);
     }
 };
 
@@ -713,11 +724,17 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
     const double *cov = t.c_coverage;
 
     // ---- per-session quartiles and Brunner-Munzel, G2 (x) vs G1 (y) (:910-1015)
+    // the filter writes each kept row's coverage value and project itself (no (row, time, project)
+    // copy gathered through afterwards); G1 / G2 projects' rows before the limit only (range scan)
     TmpView F;
+    double *fval = c->arena.get<double>(NC);
+    F.proj = c->arena.get<uint32_t>(NC);
+    const ValueProjEmit fe{fval, F.proj, cov};
     filter_view(c, s.cov, NC, P,
-                FullTrendRows{t.c_project, t.c_coverage, t.c_valid, t.c_date, member}, F);
+                FullTrendRows{t.c_project, t.c_coverage, t.c_valid, t.c_date, member}, F, nullptr,
+                Selection::segments(member, 3, nullptr, s.cov.offs, kLim4), NoCount{}, &fe, 20.0);
     const int64_t *foffs = F.offs;
-    const int32_t *frow = F.row;
+    const double *fv0 = fval;
     const uint32_t *fproj = F.proj;
     const int64_t *d_nf = F.d_n;
     per_seg(c, P, [=] __device__(int64_t p) {
@@ -737,7 +754,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
             // (i, group) in project order, read through the view's rows - no sort, no gather pass
             double *v2 = contribute ? o->trend_values : c->arena.get<double>(NC);
             int64_t *o2 = contribute ? o->trend_offsets : c->arena.get<int64_t>(S2 + 1);
-            ragged_transpose<2>(c, foffs, P, MM, NC, [=] __device__(int64_t j) { return cov[frow[j]]; },
+            ragged_transpose<2>(c, foffs, P, MM, NC, [=] __device__(int64_t j) { return fv0[j]; },
                                 [=] __device__(int64_t p) { return (member[p] & 2) ? 0 : 1; }, v2, o2);
             if (!sharded) rq4b_sessions(c, v2, nullptr, NC, d_nf, MM, P, P, c2, c1, g2q, g1q, o->p_bm, o2);
         } else {
@@ -753,7 +770,7 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
                     const uint32_t p = fproj[j];
                     const uint32_t grp = (member[p] & 2) ? 0u : 1u;
                     key[j] = uint32_t(j - foffs[p]) * 2u + grp;
-                    fv[j] = cov[frow[j]];
+                    fv[j] = fv0[j];
                 } else {
                     key[j] = uint32_t(S2);
                 }
@@ -844,10 +861,9 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
         scan_exclusive_i64(c, f2, q2, P, n2);
         scan_exclusive_i64(c, f1, q1, P, n1);
         double *a = o->init_g2, *b = o->init_g1;
-        const int32_t *fr = frow;
         map_n(c, P, nullptr, [=] __device__(int64_t p) {
-            if (f2[p]) a[q2[p]] = cov[fr[foffs[p]]];
-            if (f1[p]) b[q1[p]] = cov[fr[foffs[p]]];
+            if (f2[p]) a[q2[p]] = fv0[foffs[p]];
+            if (f1[p]) b[q1[p]] = fv0[foffs[p]];
         });
         if (!sharded) two_sample_tests(c, a, P, n2, b, P, n1, o->tests);
     }

@@ -39,8 +39,22 @@ void segment_offsets_dn(fz_ctx *c, const uint32_t *sorted_proj, const int64_t *d
 #ifndef FZ_FC_ITEMS
 #define FZ_FC_ITEMS 16
 #endif
+#ifndef FZ_FC_BLOCK
+#define FZ_FC_BLOCK 256
+#endif
 constexpr int kFcItems = FZ_FC_ITEMS;
-constexpr int kFcTile = kBlock * kFcItems;
+constexpr int kFcBlock = FZ_FC_BLOCK;  // threads of a filter workgroup (tile = kFcBlock x kFcItems rows)
+constexpr int kFcTile = kFcBlock * kFcItems;
+
+// lower_bound of v in a[lo, hi)
+__device__ inline int64_t lower_bound_i64(const int64_t *a, int64_t lo, int64_t hi, int64_t v) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
 
 // The projects a filter can keep (k_filter_compact's tile skip): flags[p] & mask != 0; count
 // (optional, device) 0 = none at all.
@@ -54,6 +68,27 @@ struct Selection {
     const int64_t *view_offs = nullptr;
     const int64_t *voff = nullptr;  // [P + 1] exclusive prefix of the selected segments' lengths
     int64_t P = 0;
+    // time bound (with view_offs): a selected segment's virtual rows are only those with view time
+    // < lim - a prefix of the segment, since the view is time-ordered inside each project (NULL
+    // times, INT64_MAX, sort last and fail every `<`).  The reference's per-project queries
+    // "WHERE project = X AND date < LIMIT ORDER BY date" (queries1.py:120-129, rq4b_coverage.py:
+    // 315-326, rq2_coverage_and_added.py:30-47, rq3:263) are index range scans over (project,
+    // date): the rows past the bound are never read.  (lim_time: the view's time column, set by
+    // filter_view.)
+    bool has_lim = false;
+    int64_t lim = 0;
+    const int64_t *lim_time = nullptr;
+    static Selection segments(const uint8_t *flags, uint8_t mask, const int64_t *count, const int64_t *view_offs,
+                              int64_t time_lim) {
+        Selection s;
+        s.flags = flags;
+        s.mask = mask;
+        s.count = count;
+        s.view_offs = view_offs;
+        s.has_lim = true;
+        s.lim = time_lim;
+        return s;
+    }
     // the view row of virtual row v, walking forward from project p (v only grows per thread)
     __device__ int64_t phys(int64_t v, int64_t &p) const {
         if (voff[p + 1] <= v) {  // past p's segment: the next selected segment holding v
@@ -92,14 +127,31 @@ struct FcShared {
     int32_t pos[kFcTile];
     uint32_t pj[kFcTile];  // the items' projects (their predecessors' for the offsets)
     int64_t pprev, plast;  // project of the row before the tile / of the last live row
-    int32_t tmp[4];
+    int32_t tmp[kFcBlock / kWave];
     int64_t prefix;
     unsigned int tile;
     int skip;
     int64_t p0;
 };
+// What a filter writes for kept row q (its rank among the kept rows): by default the view row's
+// store row id, time and project (a TmpView); an analysis may pass its own emitter to write what
+// it reads next straight from the row (e.g. RQ2 count's trend value), instead of a (row, time,
+// project) copy and a second pass that gathers through it.  kTime = false: the time column is
+// not loaded.
+struct RowTimeProj {
+    static constexpr bool kTime = true;
+    int32_t *orow;
+    int64_t *otime;
+    uint32_t *oproj;
+    __device__ void operator()(int64_t q, int32_t r, int64_t tm, uint32_t pj) const {
+        orow[q] = r;
+        otime[q] = tm;
+        oproj[q] = pj;
+    }
+};
+
 // One filter launch's arguments (the view, the predicate, the outputs).
-template <typename Pred, typename Count = NoCount, bool VIRT = false>
+template <typename Pred, typename Count = NoCount, bool VIRT = false, typename Emit = RowTimeProj>
 struct FcJob {
     int64_t row0;
     const int64_t *times;
@@ -109,9 +161,7 @@ struct FcJob {
     Pred pred;
     Lookback lb;
     int64_t ntiles;
-    int32_t *orow;
-    int64_t *otime;
-    uint32_t *oproj;
+    Emit out;
     int64_t *d_n;
     int64_t *oofs;
     int64_t P;
@@ -119,8 +169,8 @@ struct FcJob {
     Count cnt;
 };
 // tile `bid` of a filter launch (the workgroup's LDS in sh)
-template <typename Pred, typename Count, bool VIRT>
-__device__ inline void filter_tile(const FcJob<Pred, Count, VIRT> &J, int64_t bid, FcShared &sh) {
+template <typename Pred, typename Count, bool VIRT, typename Emit>
+__device__ inline void filter_tile(const FcJob<Pred, Count, VIRT, Emit> &J, int64_t bid, FcShared &sh) {
     const int64_t row0 = J.row0;
     const int64_t *__restrict__ times = J.times;
     const uint32_t *__restrict__ proj = J.proj;
@@ -129,9 +179,6 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT> &J, int64_t bi
     const Pred &pred = J.pred;
     const Lookback &lb = J.lb;
     int64_t ntiles = J.ntiles;
-    int32_t *__restrict__ orow = J.orow;
-    int64_t *__restrict__ otime = J.otime;
-    uint32_t *__restrict__ oproj = J.oproj;
     int64_t *__restrict__ d_n = J.d_n;
     int64_t *__restrict__ oofs = J.oofs;
     const int64_t P = J.P;
@@ -147,7 +194,7 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT> &J, int64_t bi
     if (sel.count && *sel.count == 0) {
         if (bid == 0) {
             if (tid == 0) *d_n = 0;
-            for (int64_t q = tid; q <= P; q += kBlock) oofs[q] = 0;
+            for (int64_t q = tid; q <= P; q += kFcBlock) oofs[q] = 0;
         }
         return;
     }
@@ -180,16 +227,31 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT> &J, int64_t bi
     // view row of item i (VIRT: through the selected segments; tables hold < 2^31 rows)
     int32_t pidx[VIRT ? kFcItems : 1];
     if constexpr (VIRT) {
+        // the current segment's end and view shift kept in registers: a load only when an item
+        // crosses into a later segment (not three dependent loads per item)
         int64_t p = sh.p0;
+        int64_t vend = 0, shift = 0;
+        if (base < lim) {
+            vend = sel.voff[p + 1];
+            shift = sel.view_offs[p] - sel.voff[p];
+        }
 #pragma unroll
         for (int i = 0; i < kFcItems; ++i) {
-            const int64_t v = base + i * kBlock + tid;
-            pidx[i] = int32_t(v < lim ? sel.phys(v, p) : 0);
+            const int64_t v = base + i * kFcBlock + tid;
+            pidx[i] = 0;
+            if (v < lim) {
+                if (v >= vend) {
+                    sel.phys(v, p);
+                    vend = sel.voff[p + 1];
+                    shift = sel.view_offs[p] - sel.voff[p];
+                }
+                pidx[i] = int32_t(v + shift);
+            }
         }
     }
     auto row_at = [&](int i) -> int64_t {
         if constexpr (VIRT) return pidx[i];
-        else return base + i * kBlock + tid;
+        else return base + i * kFcBlock + tid;
     };
     // the store row of every item (implicit: row0 + view position), then all predicate loads:
     // independent loads in flight together, no row-id load before them
@@ -197,8 +259,8 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT> &J, int64_t bi
     bool keep[kFcItems];
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) {
-        const int64_t idx = base + i * kBlock + tid;
-        r[i] = idx < lim ? int32_t(row0 + row_at(i)) : 0;
+        const int64_t idx = base + i * kFcBlock + tid;
+        r[i] = int32_t(row0 + (idx < lim ? row_at(i) : 0));
     }
     // the output columns of every live item, loaded with the predicate's (almost every row is kept
     // on the big tables): their latency overlaps the predicate loads instead of following the
@@ -207,17 +269,28 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT> &J, int64_t bi
     uint32_t pj[kFcItems];
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) {
-        const bool live = base + i * kBlock + tid < lim;
-        tm[i] = live ? times[row_at(i)] : 0;
+        const bool live = base + i * kFcBlock + tid < lim;
+        tm[i] = Emit::kTime && live ? times[row_at(i)] : 0;
         pj[i] = live ? proj[row_at(i)] : 0u;
     }
+    // every item's predicate evaluated without a branch (the predicates are branch-free too: `&`,
+    // not `&&`), so the compiler issues all items' column loads before the first wait - a short-
+    // circuit chain per item was one dependent memory round trip per column and item; items past
+    // the live rows read row r = row0 (in bounds) and are masked
+    if (base < lim) {
 #pragma unroll
-    for (int i = 0; i < kFcItems; ++i) keep[i] = base + i * kBlock + tid < lim && pred(r[i]);
+        for (int i = 0; i < kFcItems; ++i) keep[i] = pred(r[i]);
+#pragma unroll
+        for (int i = 0; i < kFcItems; ++i) keep[i] = keep[i] & (base + i * kFcBlock + tid < lim);
+    } else {
+#pragma unroll
+        for (int i = 0; i < kFcItems; ++i) keep[i] = false;
+    }
     if constexpr (Count::on) {
         const int lane = lane_id();
 #pragma unroll
         for (int i = 0; i < kFcItems; ++i) {
-            const int64_t idx = base + i * kBlock + tid;
+            const int64_t idx = base + i * kFcBlock + tid;
             const bool valid = idx < lim;
             const uint64_t act = __ballot(valid);
             if (!act) continue;  // (wave-uniform)
@@ -237,8 +310,8 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT> &J, int64_t bi
     }
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) {
-        sh.pos[i * kBlock + tid] = keep[i] ? 1 : 0;
-        sh.pj[i * kBlock + tid] = pj[i];
+        sh.pos[i * kFcBlock + tid] = keep[i] ? 1 : 0;
+        sh.pj[i * kFcBlock + tid] = pj[i];
     }
     __syncthreads();
     int32_t loc[kFcItems];
@@ -248,7 +321,7 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT> &J, int64_t bi
         run += sh.pos[tid * kFcItems + i];
     }
     int32_t agg;
-    const int32_t off = block_excl_scan(run, sh.tmp, &agg);
+    const int32_t off = block_excl_scan<int32_t, kFcBlock / kWave>(run, sh.tmp, &agg);
     if (tid < kWave) {
         const int64_t prefix = lb_exclusive_prefix(lb, tile, agg);
         if (tid == 0) {
@@ -267,20 +340,18 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT> &J, int64_t bi
 #pragma unroll
     for (int i = 0; i < kFcItems; ++i) {
         if (!keep[i]) continue;
-        const int k = i * kBlock + tid;
+        const int k = i * kFcBlock + tid;
         const int64_t q = pre + (sh.pos[k] & 0x7fffffff);
-        orow[q] = r[i];
-        otime[q] = tm[i];
-        oproj[q] = pj[i];
+        J.out(q, r[i], tm[i], pj[i]);
     }
     // segment offsets: the projects starting in this tile, then (last tile) the ones after its rows
     if (sh.skip) {  // (nothing kept: every project starting here starts at pre)
         const int64_t b1 = base + kFcTile < lim_rows ? base + kFcTile : lim_rows;
         const int64_t p1 = b1 > base ? int64_t(proj[b1 - 1]) : sh.pprev;
-        for (int64_t q = sh.pprev + 1 + tid; q <= p1; q += kBlock) oofs[q] = pre;
+        for (int64_t q = sh.pprev + 1 + tid; q <= p1; q += kFcBlock) oofs[q] = pre;
     } else {
         for (int i = 0; i < kFcItems; ++i) {
-            const int k = i * kBlock + tid;
+            const int k = i * kFcBlock + tid;
             if (base + k >= lim) break;
             const int64_t pp = k > 0 ? int64_t(sh.pj[k - 1]) : sh.pprev;
             const int64_t pc = int64_t(pj[i]);
@@ -292,13 +363,13 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT> &J, int64_t bi
     }
     if (tile == ntiles - 1) {
         const int64_t tot = pre + agg;
-        for (int64_t q = sh.plast + 1 + tid; q <= P; q += kBlock) oofs[q] = tot;
+        for (int64_t q = sh.plast + 1 + tid; q <= P; q += kFcBlock) oofs[q] = tot;
     }
 }
 
 
-template <typename Pred, typename Count = NoCount, bool VIRT = false>
-__global__ __launch_bounds__(kBlock) void k_filter_compact(const FcJob<Pred, Count, VIRT> J) {
+template <typename Pred, typename Count = NoCount, bool VIRT = false, typename Emit = RowTimeProj>
+__global__ __launch_bounds__(kFcBlock) void k_filter_compact(const FcJob<Pred, Count, VIRT, Emit> J) {
     __shared__ FcShared sh;
     filter_tile(J, int64_t(blockIdx.x), sh);
 }
@@ -306,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_compact(const FcJob<Pred, Cou
 // Three filters in one launch (blocks [0, g0) the first one's tiles, then the second's, then the
 // third's): independent views filtered back to back by one kernel instead of three.
 template <typename P0, typename P1, typename P2>
-__global__ __launch_bounds__(kBlock) void k_filter_compact3(const FcJob<P0> J0, const FcJob<P1> J1,
+__global__ __launch_bounds__(kFcBlock) void k_filter_compact3(const FcJob<P0> J0, const FcJob<P1> J1,
                                                             const FcJob<P2> J2, unsigned g0, unsigned g1) {
     __shared__ FcShared sh;
     const unsigned b = blockIdx.x;
@@ -320,8 +391,42 @@ template <typename S>
 __global__ __launch_bounds__(kBlock) void k_sel_lengths(const S sel, int64_t P, int64_t *__restrict__ len);
 template <typename S>
 __global__ __launch_bounds__(kBlock) void k_sel_lengths(const S sel, int64_t P, int64_t *__restrict__ len) {
-    for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p <= P; p += int64_t(gridDim.x) * kBlock)
-        len[p] = p < P && (sel.flags[p] & sel.mask) ? sel.view_offs[p + 1] - sel.view_offs[p] : 0;
+    for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p <= P; p += int64_t(gridDim.x) * kBlock) {
+        int64_t l = 0;
+        if (p < P && (sel.flags[p] & sel.mask)) {
+            const int64_t a = sel.view_offs[p], b = sel.view_offs[p + 1];
+            l = (sel.has_lim ? lower_bound_i64(sel.lim_time, a, b, sel.lim) : b) - a;
+        }
+        len[p] = l;
+    }
+}
+
+// The same lengths and their exclusive prefix (voff, [P + 1]) in ONE workgroup when the project axis
+// is small (one launch instead of a lengths map + a device-wide scan: config 2's filters are launch-
+// latency bound): each thread its run of consecutive projects, one block scan.
+constexpr int kSvBlock = 1024;
+constexpr int64_t kSvOneWg = int64_t(kSvBlock) * 64;
+template <typename S>
+__global__ __launch_bounds__(kSvBlock) void k_sel_voff(const S sel, int64_t P, int64_t *__restrict__ voff) {
+    __shared__ int64_t s_tmp[kSvBlock / kWave];
+    const int64_t per = (P + 1 + kSvBlock - 1) / kSvBlock;
+    const int64_t p0 = int64_t(threadIdx.x) * per, p1 = p0 + per < P + 1 ? p0 + per : P + 1;
+    int64_t sum = 0;
+    for (int64_t p = p0; p < p1; ++p) {
+        int64_t l = 0;
+        if (p < P && (sel.flags[p] & sel.mask)) {
+            const int64_t a = sel.view_offs[p], b = sel.view_offs[p + 1];
+            l = (sel.has_lim ? lower_bound_i64(sel.lim_time, a, b, sel.lim) : b) - a;
+        }
+        voff[p] = l;  // (this thread's own entries: read back below by the same thread)
+        sum += l;
+    }
+    int64_t run = block_excl_scan<int64_t, kSvBlock / kWave>(sum, s_tmp, (int64_t *)nullptr);
+    for (int64_t p = p0; p < p1; ++p) {
+        const int64_t l = voff[p];
+        voff[p] = run;
+        run += l;
+    }
 }
 
 // Algorithmic bytes the predicate reads per row (Pred::kBytes when it declares them).
@@ -338,23 +443,39 @@ struct PredBytes<P, std::void_t<decltype(P::kBytes)>> {
 // -> dst (same order).
 // sel (optional): the projects pred can keep - tiles of the (project-ordered) view covering none of
 // them are skipped without reading their columns.
-template <typename Pred, typename Count = NoCount>
+// emit (optional): what to write per kept row instead of dst.row / time / proj (which are then
+// not allocated; dst.d_n and dst.offs are written as always); bytes_out = its bytes per kept row
+// (the probe's booking)
+template <typename Pred, typename Count = NoCount, typename Emit = RowTimeProj>
 void filter_view(fz_ctx *c, const View &v, int64_t n, int64_t P, Pred pred, TmpView &dst,
-                 const int64_t *src_live = nullptr, Selection sel = Selection{}, Count cnt = Count{}) {
+                 const int64_t *src_live = nullptr, Selection sel = Selection{}, Count cnt = Count{},
+                 const Emit *emit = nullptr, double bytes_out = 0.0) {
     const int64_t *times = v.time;
     const uint32_t *proj = v.proj;
     const int64_t row0 = v.row0;
     dst.cap = n;
     dst.d_n = c->arena.get<int64_t>(1);
-    dst.row = c->arena.get<int32_t>(n);
-    dst.time = c->arena.get<int64_t>(n);
-    dst.proj = c->arena.get<uint32_t>(n);
+    if (!emit) {
+        dst.row = c->arena.get<int32_t>(n);
+        dst.time = c->arena.get<int64_t>(n);
+        dst.proj = c->arena.get<uint32_t>(n);
+    }
     dst.offs = c->arena.get<int64_t>(P + 1);
+    Emit out{};
+    if (emit) out = *emit;
+    else if constexpr (std::is_same<Emit, RowTimeProj>::value) out = RowTimeProj{dst.row, dst.time, dst.proj};
+    if (sel.has_lim) sel.lim_time = times;
     if (n > 0 && sel.flags && sel.view_offs) {  // the selected segments back to back (virtual rows)
-        int64_t *vl = c->arena.get<int64_t>(P + 1), *voff = c->arena.get<int64_t>(P + 1);
-        k_sel_lengths<Selection><<<grid_for(P + 1), kBlock, 0, c->stream>>>(sel, P, vl);
-        FZ_LAUNCH_CHECK();
-        scan_exclusive_i64(c, vl, voff, P + 1, nullptr);
+        int64_t *voff = c->arena.get<int64_t>(P + 1);
+        if (P + 1 <= kSvOneWg) {
+            k_sel_voff<Selection><<<1, kSvBlock, 0, c->stream>>>(sel, P, voff);
+            FZ_LAUNCH_CHECK();
+        } else {
+            int64_t *vl = c->arena.get<int64_t>(P + 1);
+            k_sel_lengths<Selection><<<grid_for(P + 1), kBlock, 0, c->stream>>>(sel, P, vl);
+            FZ_LAUNCH_CHECK();
+            scan_exclusive_i64(c, vl, voff, P + 1, nullptr);
+        }
         sel.voff = voff;
         sel.P = P;
         src_live = voff + P;  // (a view filter: no other live bound)
@@ -365,21 +486,26 @@ void filter_view(fz_ctx *c, const View &v, int64_t n, int64_t P, Pred pred, TmpV
         // per input row: the predicate's columns; per kept row: time 8 + project 4 read, (row, time,
         // project) 16 written
         // (a selective filter reads only the tiles of its projects: probed apart, kept rows' bytes)
-        ProbeScope ps(c, sel.flags ? "filter_select" : "filter_compact",
-                      sel.flags ? 0.0 : double(n) * PredBytes<Pred>::value, dst.d_n, 28.0);
+        // (a time-bounded view is a range scan: its virtual rows' predicate bytes are booked from
+        // their device count - the rows past the bound are not read)
+        const bool ranged = sel.voff && sel.has_lim;
+        ProbeScope ps(c, sel.flags && !ranged ? "filter_select" : "filter_compact",
+                      sel.flags ? 0.0 : double(n) * PredBytes<Pred>::value, dst.d_n, emit ? bytes_out : 28.0);
+        if (ranged) ps.add_count(sel.voff + P, PredBytes<Pred>::value);
         if (sel.voff)
-            k_filter_compact<Pred, Count, true><<<unsigned(ntiles), kBlock, 0, c->stream>>>(
-                FcJob<Pred, Count, true>{row0, times, proj, n, src_live, pred, lb, ntiles, dst.row, dst.time, dst.proj,
-                                         dst.d_n, dst.offs, P, sel, cnt});
+            k_filter_compact<Pred, Count, true, Emit><<<unsigned(ntiles), kFcBlock, 0, c->stream>>>(
+                FcJob<Pred, Count, true, Emit>{row0, times, proj, n, src_live, pred, lb, ntiles, out, dst.d_n, dst.offs, P,
+                                               sel, cnt});
         else
-            k_filter_compact<Pred, Count><<<unsigned(ntiles), kBlock, 0, c->stream>>>(
-                FcJob<Pred, Count, false>{row0, times, proj, n, src_live, pred, lb, ntiles, dst.row, dst.time, dst.proj,
-                                          dst.d_n, dst.offs, P, sel, cnt});
+            k_filter_compact<Pred, Count, false, Emit><<<unsigned(ntiles), kFcBlock, 0, c->stream>>>(
+                FcJob<Pred, Count, false, Emit>{row0, times, proj, n, src_live, pred, lb, ntiles, out, dst.d_n, dst.offs,
+                                                P, sel, cnt});
         FZ_LAUNCH_CHECK();
         lookback_end(c, ntiles);
     } else {
         const int64_t zero = 0;
         set_i64(c, dst.d_n, &zero, 1);
+        if (!dst.proj) dst.proj = c->arena.get<uint32_t>(1);
         segment_offsets_dn(c, dst.proj, dst.d_n, n, P, dst.offs);
     }
 }
@@ -456,7 +582,7 @@ void compact_emit(fz_ctx *c, int64_t n_cap, const int64_t *d_n, Pred pred, Emit 
 
 // Two independent filters in one launch (as filter_views3)
 template <typename P0, typename P1>
-__global__ __launch_bounds__(kBlock) void k_filter_compact2(const FcJob<P0> J0, const FcJob<P1> J1, unsigned g0) {
+__global__ __launch_bounds__(kFcBlock) void k_filter_compact2(const FcJob<P0> J0, const FcJob<P1> J1, unsigned g0) {
     __shared__ FcShared sh;
     const unsigned b = blockIdx.x;
     if (b < g0) filter_tile(J0, int64_t(b), sh);
@@ -482,11 +608,13 @@ void filter_views2(fz_ctx *c, int64_t P, const View &v0, int64_t n0, P0 p0, TmpV
     Lookback lb[2];
     lookback_begin_n(c, tiles, 2, lb);
     ProbeScope ps(c, "filter_compact", double(n0) * PredBytes<P0>::value + double(n1) * PredBytes<P1>::value);
-    const FcJob<P0> j0{v0.row0, v0.time, v0.proj, n0, nullptr, p0, lb[0], tiles[0], d0.row, d0.time, d0.proj, d0.d_n,
+    const FcJob<P0> j0{v0.row0, v0.time, v0.proj, n0, nullptr, p0, lb[0], tiles[0],
+                       RowTimeProj{d0.row, d0.time, d0.proj}, d0.d_n,
                        d0.offs, P, Selection{}, NoCount{}};
-    const FcJob<P1> j1{v1.row0, v1.time, v1.proj, n1, nullptr, p1, lb[1], tiles[1], d1.row, d1.time, d1.proj, d1.d_n,
+    const FcJob<P1> j1{v1.row0, v1.time, v1.proj, n1, nullptr, p1, lb[1], tiles[1],
+                       RowTimeProj{d1.row, d1.time, d1.proj}, d1.d_n,
                        d1.offs, P, Selection{}, NoCount{}};
-    k_filter_compact2<P0, P1><<<unsigned(tiles[0] + tiles[1]), kBlock, 0, c->stream>>>(j0, j1, unsigned(tiles[0]));
+    k_filter_compact2<P0, P1><<<unsigned(tiles[0] + tiles[1]), kFcBlock, 0, c->stream>>>(j0, j1, unsigned(tiles[0]));
     FZ_LAUNCH_CHECK();
 }
 
@@ -516,26 +644,20 @@ void filter_views3(fz_ctx *c, int64_t P, const View &v0, int64_t n0, P0 p0, TmpV
     ProbeScope ps(c, "filter_compact",
                   double(n0) * PredBytes<P0>::value + double(n1) * PredBytes<P1>::value +
                       double(n2) * PredBytes<P2>::value);
-    const FcJob<P0> j0{v0.row0, v0.time, v0.proj, n0, nullptr, p0, lb[0], tiles[0], d0.row, d0.time, d0.proj, d0.d_n,
+    const FcJob<P0> j0{v0.row0, v0.time, v0.proj, n0, nullptr, p0, lb[0], tiles[0],
+                       RowTimeProj{d0.row, d0.time, d0.proj}, d0.d_n,
                        d0.offs, P, Selection{}, NoCount{}};
-    const FcJob<P1> j1{v1.row0, v1.time, v1.proj, n1, nullptr, p1, lb[1], tiles[1], d1.row, d1.time, d1.proj, d1.d_n,
+    const FcJob<P1> j1{v1.row0, v1.time, v1.proj, n1, nullptr, p1, lb[1], tiles[1],
+                       RowTimeProj{d1.row, d1.time, d1.proj}, d1.d_n,
                        d1.offs, P, Selection{}, NoCount{}};
-    const FcJob<P2> j2{v2.row0, v2.time, v2.proj, n2, nullptr, p2, lb[2], tiles[2], d2.row, d2.time, d2.proj, d2.d_n,
+    const FcJob<P2> j2{v2.row0, v2.time, v2.proj, n2, nullptr, p2, lb[2], tiles[2],
+                       RowTimeProj{d2.row, d2.time, d2.proj}, d2.d_n,
                        d2.offs, P, Selection{}, NoCount{}};
-    k_filter_compact3<P0, P1, P2><<<unsigned(tiles[0] + tiles[1] + tiles[2]), kBlock, 0, c->stream>>>(
+    k_filter_compact3<P0, P1, P2><<<unsigned(tiles[0] + tiles[1] + tiles[2]), kFcBlock, 0, c->stream>>>(
         j0, j1, j2, unsigned(tiles[0]), unsigned(tiles[1]));
     FZ_LAUNCH_CHECK();
 }
 
-// lower_bound of v in a[lo, hi)
-__device__ inline int64_t lower_bound_i64(const int64_t *a, int64_t lo, int64_t hi, int64_t v) {
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (a[mid] < v) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
 __device__ inline int64_t upper_bound_i64(const int64_t *a, int64_t lo, int64_t hi, int64_t v) {
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
