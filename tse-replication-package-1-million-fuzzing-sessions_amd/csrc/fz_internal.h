@@ -365,6 +365,11 @@ struct RadixPayload {
 void radix_sort_pairs_payload(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl);
 // the same for keys of at most 32 bits held as uint32 (4 bytes less per key and pass)
 void radix_sort_pairs_payload32(fz_ctx *c, uint32_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl);
+// The same sort of (key_src[i], i): the keys read from a read-only column, the values the rows'
+// positions - nothing copied beforehand.  keys / vals: two caller scratch buffers of n entries (the
+// passes ping-pong through them and one arena pair); on return they point at the sorted result.
+void radix_sort_rows_payload32(fz_ctx *c, const uint32_t *key_src, uint32_t *&keys, uint32_t *&vals, int64_t n,
+                               int bits, RadixPayload &pl);
 // min/max over int64 values skipping FZ_TS_NULL: writes {min, max} to host array.
 void minmax_i64_to_host(fz_ctx *c, const int64_t *const *cols, const int64_t *ns, int ncols,
                         int64_t *host_minmax);

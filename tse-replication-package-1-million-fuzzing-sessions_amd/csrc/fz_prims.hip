@@ -622,7 +622,8 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const KeyT *__restrict__ key
         const int64_t idx = wbase + r * kWave + lane;
         const bool valid = idx < n;
         k[r] = valid ? keys_in[idx] : KeyT(0);
-        v[r] = (HAS_VALS && valid) ? vals_in[idx] : 0u;
+        // (no vals_in: the values are the keys' positions - a sort's first pass over row ids)
+        v[r] = (HAS_VALS && valid) ? (vals_in ? vals_in[idx] : uint32_t(idx)) : 0u;
     }
 #if FZ_OS_PREFETCH
     // the first payload column in flight with the keys
@@ -814,10 +815,14 @@ void radix_sort_pairs_swap(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int64_t 
 }
 
 
+// key_src (optional): the first pass reads the keys from this read-only array (never written; the
+// passes ping-pong between two scratch buffers) and takes the values as the keys' positions (vals
+// must be non-null: set to the result buffer) - no key / row-id copy made beforehand.
 template <typename KeyT>
 static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl,
-                               const int64_t *d_live = nullptr) {
+                               const int64_t *d_live = nullptr, const KeyT *key_src = nullptr) {
     if (n <= 1 || bits <= 0) {  // nothing to sort (one key, or a 0-bit key: one project): unmoved
+        FZ_CHECK(!key_src, "radix sort from a read-only key source needs a pass");
         for (int j = 0; j < pl.n; ++j) pl.out[j] = const_cast<void *>(pl.in[j]);
         return;
     }
@@ -847,8 +852,8 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
     unsigned long long *gsum = c->arena.get<unsigned long long>(gwords * npass);
     {
         ProbeScope ps(c, "radix_hist", 8.0 * double(n));
-        k_onesweep_hist<KeyT><<<grid_for(n, kHistKeysPerBlock, 2048), kBlock, 0, c->stream>>>(keys, n, npass, ghist,
-                                                                                             gsum, gwords * npass, d_live);
+        k_onesweep_hist<KeyT><<<grid_for(n, kHistKeysPerBlock, 2048), kBlock, 0, c->stream>>>(
+            key_src ? key_src : keys, n, npass, ghist, gsum, gwords * npass, d_live);
         FZ_LAUNCH_CHECK();
     }
     // Constant-digit passes are identity permutations.  Finding them needs a host round trip, which
@@ -861,7 +866,7 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
     for (int p = 0; p < npass; ++p) need[p] = true;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     FZ_HIP(hipStreamIsCapturing(c->stream, &cap));
-    if (n >= (int64_t(1) << 22) && !pl.no_digit_probe && cap == hipStreamCaptureStatusNone) {
+    if (n >= (int64_t(1) << 22) && !pl.no_digit_probe && !key_src && cap == hipStreamCaptureStatusNone) {
         unsigned long long *hh = reinterpret_cast<unsigned long long *>(c->h_pinned);
         FZ_HIP(hipMemcpyAsync(hh, ghist, sizeof(unsigned long long) * npass * kRadix, hipMemcpyDeviceToHost,
                               c->stream));
@@ -876,6 +881,12 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
     uint32_t *v2 = vals ? c->arena.get<uint32_t>(n) : nullptr;
     KeyT *ka = keys, *kb = k2;
     uint32_t *va = vals, *vb = v2;
+    if (key_src) {  // first pass: the source keys and implicit positions -> k2 / v2; then k2 <-> keys
+        FZ_CHECK(vals != nullptr, "radix sort from a key source: a value buffer is required");
+        ka = const_cast<KeyT *>(key_src);
+        va = nullptr;
+    }
+    bool first = true;
     FZ_CHECK(pl.n == 0 || n < (int64_t(1) << 31), "radix_sort_pairs_payload: payload sorts are limited to 2^31 keys");
     void *pbuf[2][kMaxPayload] = {};
     for (int j = 0; j < pl.n; ++j)  // two scratch copies per column: the passes ping-pong them
@@ -923,10 +934,19 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
         }
         lookback_end(c, nb);
         if (pl.n > 0) ++ppass;
-        std::swap(ka, kb);
-        std::swap(va, vb);
+        if (key_src && first) {  // (the source is never written: the caller's buffers take its place)
+            ka = kb;
+            va = vb;
+            kb = keys;
+            vb = vals;
+        } else {
+            std::swap(ka, kb);
+            std::swap(va, vb);
+        }
+        first = false;
         ++passes;
     }
+    FZ_CHECK(!key_src || passes > 0, "radix sort from a read-only key source ran no pass");
     keys = ka;  // the buffers holding the result (the inputs or arena scratch)
     vals = va;
     for (int j = 0; j < pl.n; ++j)  // where each payload column ended (unmoved: the input itself)
@@ -947,6 +967,11 @@ void radix_sort_pairs_swap_live(fz_ctx *c, uint64_t *&keys, uint32_t *&vals, int
 void radix_sort_pairs_payload32(fz_ctx *c, uint32_t *&keys, uint32_t *&vals, int64_t n, int bits, RadixPayload &pl) {
     FZ_CHECK(bits <= 32, "radix_sort_pairs_payload32: keys of more than 32 bits");
     radix_payload_impl<uint32_t>(c, keys, vals, n, bits, pl);
+}
+void radix_sort_rows_payload32(fz_ctx *c, const uint32_t *key_src, uint32_t *&keys, uint32_t *&vals, int64_t n,
+                               int bits, RadixPayload &pl) {
+    FZ_CHECK(bits <= 32 && bits > 0 && n > 1, "radix_sort_rows_payload32: bad key width or size");
+    radix_payload_impl<uint32_t>(c, keys, vals, n, bits, pl, nullptr, key_src);
 }
 
 // ------------------------------------------------------------------------------- min / max

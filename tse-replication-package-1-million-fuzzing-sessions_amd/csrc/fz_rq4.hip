@@ -487,14 +487,8 @@ void rq4b_sessions(fz_ctx *c, const double *v2, const uint32_t *sid2, int64_t n_
     });
     Segs sg2{S2, offs2, NC, P};
     SortedSegs ss2 = seg_sort_f64(c, v2, sg2, nullptr);
-    double *qq = c->arena.get<double>(S2 * 3);
     const double q3[3] = {25.0, 50.0, 75.0};
-    seg_percentiles(c, sg2, ss2.val, q3, 3, qq);
-    map_n(c, MM * 3, nullptr, [=] __device__(int64_t k) {
-        const int64_t i = k / 3, j = k % 3;
-        g2q[k] = qq[(2 * i) * 3 + j];
-        g1q[k] = qq[(2 * i + 1) * 3 + j];
-    });
+    seg_percentiles(c, sg2, ss2.val, q3, 3, g2q, nullptr, g1q);  // (segment 2i -> G2 row i, 2i + 1 -> G1)
     // per-session Brunner-Munzel (:978-985; NaN unless both sides >= 5)
     if (lds) {
         bm_halves(c, ss2.val, offs2, soffs, MM, NC, 5, pbm);

@@ -96,12 +96,14 @@ __global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, const int6
             }
             continue;
         }
-        DD acc[NV];
+        // two independent double-double accumulators per value (even / odd items), added at the
+        // end: the dependent add chain per thread is half as long (the kernel waits on these
+        // chains, not on memory: SQ_WAIT_INST_ANY); the order is fixed - deterministic
+        DD acc[NV], acc2[NV];
 #pragma unroll
-        for (int v = 0; v < NV; ++v) acc[v] = DD{0.0, 0.0};
+        for (int v = 0; v < NV; ++v) acc[v] = acc2[v] = DD{0.0, 0.0};
         // a chunk is at most kRedItems elements per thread: every element's loads are issued
-        // before the first add (one memory round trip per chunk, not kRedItems dependent ones);
-        // the per-thread addition order (i, i + kBlock, ...) is unchanged
+        // before the first add (one memory round trip per chunk, not kRedItems dependent ones)
         for (int64_t i0 = b + threadIdx.x; i0 < e; i0 += int64_t(kBlock) * kRedItems) {
             double x[kRedItems][NV];
 #pragma unroll
@@ -115,14 +117,16 @@ __global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, const int6
                 }
             }
 #pragma unroll
-            for (int u = 0; u < kRedItems; ++u)
+            for (int u = 0; u < kRedItems; u += 2)
 #pragma unroll
-                for (int v = 0; v < NV; ++v)
+                for (int v = 0; v < NV; ++v) {
                     if (i0 + int64_t(u) * kBlock < e) acc[v] = dd_add_d(acc[v], x[u][v]);
+                    if (i0 + int64_t(u + 1) * kBlock < e) acc2[v] = dd_add_d(acc2[v], x[u + 1][v]);
+                }
         }
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
-            DD r = wave_dd_sum(acc[v]);
+            DD r = wave_dd_sum(dd_add(acc[v], acc2[v]));
             if (lane_id() == 0) {
                 s_hi[wave_id()][v] = r.hi;
                 s_lo[wave_id()][v] = r.lo;
@@ -364,9 +368,11 @@ void series_small(fz_ctx *c, const double *x, const int64_t *d_n, double *rho, d
 void spearman_shapiro_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segid, const SortedSegs &ss,
                              const double *src, double *rho, double *pval, double *w, double *p);
 // numpy.percentile(seg, q[j]) for sorted segments -> out[s * nq + j] (NaN for empty segments).
-// (median != null: statistics.median of every segment too, as seg_median, in the same launch)
+// (median != null: statistics.median of every segment too, as seg_median, in the same launch;
+// out2 != null: segments in (even, odd) pairs written to two tables, segment s to
+// (s odd ? out2 : out)[(s / 2) * nq + j] - RQ4b's G2 / G1 quartile columns, no copy afterwards)
 void seg_percentiles(fz_ctx *c, const Segs &sg, const double *sorted, const double *q_host, int nq, double *out,
-                     double *median = nullptr);
+                     double *median = nullptr, double *out2 = nullptr);
 // sum / n per segment in double-double (statistics.mean / np.mean within 1 ulp) -> out[S].
 void seg_mean(fz_ctx *c, const ChunkedSegs &cs, const double *vals, double *out);
 // statistics.median / np.median of sorted segments: middle value or (a + b) / 2 -> out[S].

@@ -1758,7 +1758,7 @@ void seg_shapiro(fz_ctx *c, const ChunkedSegs &cs, const double *src, const Sort
 
 // ------------------------------------------------------------- percentiles, means, medians
 void seg_percentiles(fz_ctx *c, const Segs &sg, const double *sorted, const double *q_host, int nq, double *out,
-                     double *median) {
+                     double *median, double *out2) {
     double q[8];
     for (int j = 0; j < nq && j < 8; ++j) q[j] = q_host[j];
     const int64_t *offs = sg.offs;
@@ -1766,12 +1766,13 @@ void seg_percentiles(fz_ctx *c, const Segs &sg, const double *sorted, const doub
         const int64_t b = offs[s], n = offs[s + 1] - b;
         if (median)  // (seg_median's value, from the same thread's reads)
             median[s] = n <= 0 ? NAN : ((n & 1) ? sorted[b + n / 2] : (sorted[b + n / 2 - 1] + sorted[b + n / 2]) / 2.0);
+        double *o = out2 ? ((s & 1) ? out2 : out) + (s >> 1) * nq : out + s * nq;
         for (int j = 0; j < nq; ++j) {
             if (n <= 0) {
-                out[s * nq + j] = NAN;
+                o[j] = NAN;
                 continue;
             }
-            out[s * nq + j] = np_percentile_sorted([&](int64_t k) { return sorted[b + k]; }, n, q[j]);
+            o[j] = np_percentile_sorted([&](int64_t k) { return sorted[b + k]; }, n, q[j]);
         }
     });
 }

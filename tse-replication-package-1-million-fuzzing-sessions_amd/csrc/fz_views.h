@@ -429,6 +429,12 @@ __global__ __launch_bounds__(kSvBlock) void k_sel_voff(const S sel, int64_t P, i
     }
 }
 
+// Views of fewer rows than this take time-bounded selections as plain filters (no range scan).
+#ifndef FZ_RANGE_SCAN_MIN
+#define FZ_RANGE_SCAN_MIN (int64_t(1) << 22)
+#endif
+constexpr int64_t kRangeScanMin = FZ_RANGE_SCAN_MIN;
+
 // Algorithmic bytes the predicate reads per row (Pred::kBytes when it declares them).
 template <class P, class = void>
 struct PredBytes {
@@ -464,10 +470,19 @@ void filter_view(fz_ctx *c, const View &v, int64_t n, int64_t P, Pred pred, TmpV
     Emit out{};
     if (emit) out = *emit;
     else if constexpr (std::is_same<Emit, RowTimeProj>::value) out = RowTimeProj{dst.row, dst.time, dst.proj};
+    if (sel.has_lim && n < kRangeScanMin) {
+        // a small view: the plain filter (the predicate tests the bound itself) - the virtual-row
+        // setup is one more launch on the analyses' latency-bound chains (config 2)
+        sel.has_lim = false;
+        sel.view_offs = nullptr;
+        if (!sel.count) sel.flags = nullptr;
+    }
     if (sel.has_lim) sel.lim_time = times;
     if (n > 0 && sel.flags && sel.view_offs) {  // the selected segments back to back (virtual rows)
         int64_t *voff = c->arena.get<int64_t>(P + 1);
-        if (P + 1 <= kSvOneWg) {
+        // (one workgroup when the segments' lengths are offset differences; the time-bounded
+        // lengths are binary searches - one thread per project across the chip, then the scan)
+        if (P + 1 <= kSvOneWg && !sel.has_lim) {
             k_sel_voff<Selection><<<1, kSvBlock, 0, c->stream>>>(sel, P, voff);
             FZ_LAUNCH_CHECK();
         } else {
