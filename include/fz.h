@@ -424,6 +424,7 @@ enum {
     FZ_RQ4B_DELTA_PROJECTS,      /* G3/G4 projects with 7 + 7 coverage points              :725-797 */
     FZ_RQ4B_INIT_G2, FZ_RQ4B_INIT_G1,  /* initial-coverage sample sizes                    :221-246 */
     FZ_RQ4B_G1, FZ_RQ4B_G2, FZ_RQ4B_G3, FZ_RQ4B_G4,
+    FZ_RQ4B_VALUES,              /* G1/G2 series values (= trend_offsets[2 * sessions])            */
     FZ_RQ4B_NCOUNTS = 12
 };
 enum { FZ_RQ4B_MWU_P = 0, FZ_RQ4B_CLIFF, FZ_RQ4B_BM_STAT, FZ_RQ4B_BM_P, FZ_RQ4B_LEVENE_W, FZ_RQ4B_LEVENE_P,
@@ -432,7 +433,9 @@ typedef struct fz_rq4b_out {
     int64_t *counts;             /* [FZ_RQ4B_NCOUNTS] */
     uint8_t *eligible;           /* [n_projects] */
     uint8_t *member;             /* [n_projects] bit g: project in G(g+1) (eligible, rq4b rules) */
-    int64_t *c2, *c1;            /* [max_cov_per_project] values per session index, G2 / G1 */
+    int64_t *c2, *c1;            /* [max_cov_per_project] values per session index, G2 / G1 (the
+                                    per-session arrays are written up to counts[FZ_RQ4B_SESSIONS]:
+                                    at most the rows of one project before the date limit)      */
     double *g2_q, *g1_q;         /* [max_cov_per_project * 3] np.percentile 25/50/75        :966-972 */
     double *p_bm;                /* [max_cov_per_project] brunnermunzel p, NaN if a side < 5 :978-985 */
     double *spearman6;           /* [12] (rho, p): G1 Q1, Med, Q3, G2 Q1, Med, Q3            :879-899 */
@@ -444,7 +447,8 @@ typedef struct fz_rq4b_out {
     double *trend_values;        /* [n_cov] G1/G2 full coverage values grouped by (session index,
                                     group): segment 2i = the i-th value of every G2 project, 2i + 1
                                     = of every G1 project, projects in order inside a segment      */
-    int64_t *trend_offsets;      /* [2 * max_cov_per_project + 1] segment offsets into trend_values */
+    int64_t *trend_offsets;      /* [2 * max_cov_per_project + 1] segment offsets into trend_values;
+                                    entries past 2 * counts[FZ_RQ4B_SESSIONS] unspecified          */
     int64_t *delta_order;        /* [n_projects] CSV row (index into groups->order) of each column  */
 } fz_rq4b_out;
 

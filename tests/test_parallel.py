@@ -326,6 +326,7 @@ class OracleRQ4bShard(OracleRQ2CountShard):
         c[par.RQ4B_DELTA_PROJECTS], c[par.RQ4B_INIT_G2], c[par.RQ4B_INIT_G1] = len(projs), len(init["group2"]), \
             len(init["group1"])
         c[par.RQ4B_SESSIONS] = m_loc
+        c[par.RQ4B_VALUES] = len(vals)
         for g in range(4):
             c[5 + g] = len(groups[f"group{g + 1}"])
         T = lambda a, dt=np.float64: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))  # noqa: E731

@@ -128,6 +128,11 @@ struct DevBuf {
 struct View {
     int64_t n = 0;
     int64_t max_seg = 0;
+    // (coverage view) the most rows of one project dated before the analyses' limit (2025-01-08,
+    // queries1.py:3): every RQ2-count / RQ4b session axis is at most this long - their per-session
+    // arrays, transposes and statistics are sized by it, not by the longest segment (config 5: a
+    // 20.8 M-row project of which 2,960 rows precede the limit)
+    int64_t lim_seg = 0;
     // view position q is store row row0 + q: the store's columns are gathered into view order, so
     // a view's row ids are implicit (the filters read no row array)
     int64_t row0 = 0;
@@ -150,7 +155,7 @@ struct Store {
     int64_t num_min = 0, num_max = 0;                   // issues.number range
     // eligible projects (the GROUP BY/HAVING every script starts from), computed once per load
     DevBuf elig;     // uint8 [P]
-    DevBuf n_elig;   // int64 [1]
+    DevBuf n_elig;   // int64 [2]: eligible projects, the most rows of one project before the limit
     // The tables themselves in sorted order: after the build `t` points at these sorted copies and
     // every view's row id IS the position in its sorted table, so filters and joins read columns
     // sequentially instead of gathering through the sort permutation.  perm maps a sorted
@@ -180,6 +185,7 @@ struct Store {
         for (const View *v : {&fuzz, &covb, &cov, &issues}) {
             mix(uint64_t(v->n));
             mix(uint64_t(v->max_seg));
+            mix(uint64_t(v->lim_seg));
         }
         return h;
     }

@@ -36,13 +36,17 @@ constexpr int kEligBlocks = 256;
 constexpr int kEligThreads = 1024;
 constexpr int64_t kEligLdsMax = 16384;  // 64 KiB of int32 bins
 
+// (part2 != null: a second histogram of every row before the limit, any validity - the store's
+// bound on the analyses' session axes, View::lim_seg - in the second half of the LDS)
 __global__ __launch_bounds__(kEligThreads) void k_elig_hist(const uint32_t *__restrict__ proj,
                                                             const int64_t *__restrict__ date,
                                                             const double *__restrict__ cov,
                                                             const uint8_t *__restrict__ valid, int64_t n, int64_t P,
-                                                            int64_t limit, int32_t *__restrict__ part) {
+                                                            int64_t limit, int32_t *__restrict__ part,
+                                                            int32_t *__restrict__ part2) {
     extern __shared__ int32_t s_hist[];
-    for (int64_t p = threadIdx.x; p < P; p += kEligThreads) s_hist[p] = 0;
+    int32_t *const s_h2 = s_hist + P;
+    for (int64_t p = threadIdx.x; p < (part2 ? 2 * P : P); p += kEligThreads) s_hist[p] = 0;
     __syncthreads();
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t lo = int64_t(blockIdx.x) * per, hi = lo + per < n ? lo + per : n;
@@ -55,10 +59,19 @@ __global__ __launch_bounds__(kEligThreads) void k_elig_hist(const uint32_t *__re
         const uint32_t pa = proj[i], pb = proj[j];
         if ((va & FZ_VALID_COVERAGE) && ca > 0.0 && da < limit) atomicAdd(&s_hist[pa], 1);
         if ((vb & FZ_VALID_COVERAGE) && cb > 0.0 && db < limit) atomicAdd(&s_hist[pb], 1);
+        if (part2) {
+            if (da < limit) atomicAdd(&s_h2[pa], 1);
+            if (db < limit) atomicAdd(&s_h2[pb], 1);
+        }
     }
-    if (i < hi && (valid[i] & FZ_VALID_COVERAGE) && cov[i] > 0.0 && date[i] < limit) atomicAdd(&s_hist[proj[i]], 1);
+    if (i < hi) {
+        if ((valid[i] & FZ_VALID_COVERAGE) && cov[i] > 0.0 && date[i] < limit) atomicAdd(&s_hist[proj[i]], 1);
+        if (part2 && date[i] < limit) atomicAdd(&s_h2[proj[i]], 1);
+    }
     __syncthreads();
     for (int64_t p = threadIdx.x; p < P; p += kEligThreads) part[int64_t(blockIdx.x) * P + p] = s_hist[p];
+    if (part2)
+        for (int64_t p = threadIdx.x; p < P; p += kEligThreads) part2[int64_t(blockIdx.x) * P + p] = s_h2[p];
 }
 
 // fallback for very many projects: global atomics straight into counts
@@ -66,28 +79,49 @@ __global__ __launch_bounds__(kBlock) void k_elig_atomic(const uint32_t *__restri
                                                         const int64_t *__restrict__ date,
                                                         const double *__restrict__ cov,
                                                         const uint8_t *__restrict__ valid, int64_t n, int64_t limit,
-                                                        int32_t *__restrict__ counts) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+                                                        int32_t *__restrict__ counts, int32_t *__restrict__ counts2) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
         if ((valid[i] & FZ_VALID_COVERAGE) && cov[i] > 0.0 && date[i] < limit) atomicAdd(&counts[proj[i]], 1);
+        if (counts2 && date[i] < limit) atomicAdd(&counts2[proj[i]], 1);
+    }
 }
 
 // Column sums of the [nb][P] partial table: a workgroup owns 64 projects (one per lane, coalesced
 // rows), its 4 waves split the nb partial rows, LDS adds the 4 wave sums.  part == null: counts
 // are already final (atomic fallback), only the flags are derived.
+// (part2 / counts2 != null: the before-limit histogram's column sums too, their maximum atomically
+// into *lim_max - zero on entry)
 __global__ __launch_bounds__(kBlock) void k_elig_sum(const int32_t *__restrict__ part, int nb, int64_t P,
                                                      int32_t *__restrict__ counts, uint8_t *__restrict__ elig,
-                                                     int64_t *__restrict__ n_elig) {
+                                                     int64_t *__restrict__ n_elig, const int32_t *__restrict__ part2,
+                                                     const int32_t *__restrict__ counts2,
+                                                     int64_t *__restrict__ lim_max) {
     __shared__ int32_t s_sum[4][kWave];
+    __shared__ int32_t s_sum2[4][kWave];
     const int64_t p = int64_t(blockIdx.x) * kWave + lane_id();
     const int w = wave_id();
-    int32_t s = 0;
+    int32_t s = 0, s2 = 0;
     if (part && p < P) {
 #pragma unroll 8
         for (int b = w; b < nb; b += 4) s += part[int64_t(b) * P + p];
+        if (part2)
+#pragma unroll 8
+            for (int b = w; b < nb; b += 4) s2 += part2[int64_t(b) * P + p];
     }
     s_sum[w][lane_id()] = s;
+    s_sum2[w][lane_id()] = s2;
     __syncthreads();
-    if (w != 0 || p >= P) return;
+    if (w != 0) return;
+    if (lim_max) {
+        int64_t m = 0;
+        if (p < P)
+            m = part ? int64_t(s_sum2[0][lane_id()] + s_sum2[1][lane_id()] + s_sum2[2][lane_id()] + s_sum2[3][lane_id()])
+                     : int64_t(counts2[p]);
+        m = wave_max(m);
+        if (lane_id() == 0 && m > 0)
+            atomicMax(reinterpret_cast<unsigned long long *>(lim_max), (unsigned long long)m);
+    }
+    if (p >= P) return;
     if (part) {
         s = s_sum[0][lane_id()] + s_sum[1][lane_id()] + s_sum[2][lane_id()] + s_sum[3][lane_id()];
         if (counts) counts[p] = s;
@@ -101,9 +135,10 @@ __global__ __launch_bounds__(kBlock) void k_elig_sum(const int32_t *__restrict__
     }
 }
 
-// counts[p] (and, if elig != null, elig[p] = counts >= 365 with *n_elig += #eligible)
+// counts[p] (and, if elig != null, elig[p] = counts >= 365 with *n_elig += #eligible; if lim_max !=
+// null, *lim_max (zero on entry) = the most rows of one project dated before the limit)
 static void eligibility(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *counts, uint8_t *elig,
-                        int64_t *n_elig) {
+                        int64_t *n_elig, int64_t *lim_max = nullptr) {
     const int64_t P = t->n_projects;
     if (P <= 0) return;
     // algorithmic bytes: project 4 + date 8 + coverage 8 + validity 1 per row
@@ -111,15 +146,29 @@ static void eligibility(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *c
     if (P <= kEligLdsMax) {
         const int nb = t->n_cov > 0 ? kEligBlocks : 1;
         int32_t *part = c->arena.get<int32_t>(int64_t(nb) * P);
-        k_elig_hist<<<nb, kEligThreads, size_t(P) * 4, c->stream>>>(t->c_project, t->c_date, t->c_coverage, t->c_valid,
-                                                               t->n_cov, P, limit, part);
-        k_elig_sum<<<unsigned((P + kWave - 1) / kWave), kBlock, 0, c->stream>>>(part, nb, P, counts, elig, n_elig);
+        int32_t *part2 = lim_max ? c->arena.get<int32_t>(int64_t(nb) * P) : nullptr;
+        const size_t lds = size_t(P) * 4 * (lim_max ? 2 : 1);
+        if (lds > 65536) {  // (both histograms of up to 16384 bins: up to 128 KiB of the CU's 160)
+            static bool raised = false;
+            if (!raised) {
+                FZ_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_elig_hist),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(2 * kEligLdsMax * 4)));
+                raised = true;
+            }
+        }
+        k_elig_hist<<<nb, kEligThreads, lds, c->stream>>>(
+            t->c_project, t->c_date, t->c_coverage, t->c_valid, t->n_cov, P, limit, part, part2);
+        k_elig_sum<<<unsigned((P + kWave - 1) / kWave), kBlock, 0, c->stream>>>(part, nb, P, counts, elig, n_elig,
+                                                                               part2, nullptr, lim_max);
     } else {
         if (!counts) counts = c->arena.get<int32_t>(P);
+        int32_t *counts2 = lim_max ? c->arena.get<int32_t>(P) : nullptr;
         dev_fill(c, counts, 0, P * 4);
+        if (counts2) dev_fill(c, counts2, 0, P * 4);
         k_elig_atomic<<<grid_for(t->n_cov, kBlock, 2048), kBlock, 0, c->stream>>>(
-            t->c_project, t->c_date, t->c_coverage, t->c_valid, t->n_cov, limit, counts);
-        k_elig_sum<<<unsigned((P + kWave - 1) / kWave), kBlock, 0, c->stream>>>(nullptr, 0, P, counts, elig, n_elig);
+            t->c_project, t->c_date, t->c_coverage, t->c_valid, t->n_cov, limit, counts, counts2);
+        k_elig_sum<<<unsigned((P + kWave - 1) / kWave), kBlock, 0, c->stream>>>(nullptr, 0, P, counts, elig, n_elig,
+                                                                               nullptr, counts2, lim_max);
     }
     FZ_LAUNCH_CHECK();
 }
@@ -133,9 +182,9 @@ void store_eligibility(fz_ctx *c) {
     Store &s = store_of(c);
     const int64_t P = s.P;
     uint8_t *elig = s.elig.ensure<uint8_t>(P);
-    int64_t *n = s.n_elig.ensure<int64_t>(1);
-    dev_fill(c, n, 0, 8);
-    eligibility(c, &s.t, kLimitUs, nullptr, elig, n);
+    int64_t *n = s.n_elig.ensure<int64_t>(2);
+    dev_fill(c, n, 0, 16);
+    eligibility(c, &s.t, kLimitUs, nullptr, elig, n, n + 1);
 }
 
 // elig[p] = project has >= 365 qualifying coverage rows; *d_count = number eligible.

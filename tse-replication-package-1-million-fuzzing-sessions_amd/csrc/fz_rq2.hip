@@ -178,7 +178,7 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
              "fz_rq2_count: null output buffer");
     const fz_tables &t = s.t;
     const int64_t P = s.P;
-    const int64_t M = s.cov.max_seg;  // longest possible trend
+    const int64_t M = s.cov.lim_seg;  // longest possible trend (rows before the date limit)
     const int64_t NC = s.cov.n;
     // (the counters and raw_n zeroed in the eligibility copy's launch)
     eligible_projects(c, o->eligible, o->counts + FZ_RQ2C_ELIGIBLE,

@@ -708,7 +708,8 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
                  o->init_g1 && o->tests,
              "fz_rq4b: null output buffer");
     const fz_tables &t = s.t;
-    const int64_t P = s.P, M = s.cov.max_seg, NC = s.cov.n;
+    // (session axis: at most the rows of one project before the date limit)
+    const int64_t P = s.P, M = s.cov.lim_seg, NC = s.cov.n;
     const int64_t MM = M > 0 ? M : 1;
     int64_t *counts = o->counts;
     int64_t *scratch = c->arena.get<int64_t>(4);
@@ -731,9 +732,11 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
     const double *fv0 = fval;
     const uint32_t *fproj = F.proj;
     const int64_t *d_nf = F.d_n;
-    per_seg(c, P, [=] __device__(int64_t p) {
-        atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ4B_SESSIONS]),
-                  (unsigned long long)(foffs[p + 1] - foffs[p]));
+    per_seg(c, P > 0 ? P : 1, [=] __device__(int64_t p) {
+        if (p < P)
+            atomicMax(reinterpret_cast<unsigned long long *>(&counts[FZ_RQ4B_SESSIONS]),
+                      (unsigned long long)(foffs[p + 1] - foffs[p]));
+        if (p == 0) counts[FZ_RQ4B_VALUES] = *d_nf;
     });
     const bool sharded = flags & FZ_RQ4B_SKIP_SESSION_STATS;
     // a shard's contribution to the session exchange: its values grouped by (session, group)

@@ -75,6 +75,7 @@ __global__ __launch_bounds__(kBlock) void k_store_prologue(const int64_t *__rest
 // pinned read-back area: one launch, no copy.  A view starts at its first prefix's offset (the
 // builds' Coverage view after all Fuzzing rows), read here rather than counted beforehand.
 struct ViewSrc {
+    const int64_t *lim_max = nullptr;  // the eligibility pass's most rows of a project before the limit
     const int64_t *src[4] = {};  // prefix offsets of the view's table (null: empty table)
     int64_t first[4] = {};       // prefix of the view's project 0
     int64_t *dst[4] = {};        // [P + 1]
@@ -128,6 +129,7 @@ __global__ __launch_bounds__(kSortBlock) void k_store_views(const ViewSrc v, int
         __syncthreads();
     }
     if (threadIdx.x < 9) out[4 + threadIdx.x] = int64_t(v.big[threadIdx.x]);
+    if (threadIdx.x == 0) out[19] = v.lim_max ? *v.lim_max : 0;
 }
 
 // ---- fork / join onto the store-build helpers (fz_store_set_helpers) -------------------------
@@ -312,6 +314,9 @@ constexpr uint64_t kBlkTop = (uint64_t(1) << (64 - kBlkPosBits)) - 1;  // time f
 // does not fit the key, is flagged for the merge sort instead.  MAXN <= 4096 keeps the keys in LDS;
 // larger classes re-read them from the (prefix-sorted, cache-resident) time column.
 constexpr int kBucketSkew = 32;
+#ifndef FZ_LONG_FUSE
+#define FZ_LONG_FUSE 1  // the 16384-row class gathers its columns itself (0: k_store_gather does)
+#endif
 // The sub-bucket pass of long segments (tie != null: equal times ordered by prefix position, any
 // span) ranks inside a bucket by re-reading the bucket's rows from global memory - quadratic in the
 // bucket size - so its cap is looser but still bounded: a sub-bucket whose largest bucket holds more
@@ -347,12 +352,12 @@ struct TimeSortTabs {
     int64_t base[4] = {0, 0, 0, 0};  // combined index of table k's first segment; base[3] = total
 };
 template <int BS, int MAXN>
-__global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, int64_t min_len, bool flag_longer) {
+__device__ __forceinline__ void seg_time_bucket(const TimeSortTabs &T, int64_t min_len, bool flag_longer) {
     constexpr int IPT = MAXN / BS;               // rows per thread
     constexpr int EPT = (MAXN + 1 + BS - 1) / BS;  // buckets per thread in the scan
     constexpr int NW = BS / kWave;
     constexpr bool KEYS_LDS = MAXN <= 4096;
-    constexpr bool FUSE = MAXN > 4096;  // this class gathers its segments' columns itself
+    constexpr bool FUSE = MAXN > 4096 && FZ_LONG_FUSE;  // this class gathers its segments' columns itself
     static_assert(MAXN <= (1 << kBlkPosBits) && MAXN % BS == 0, "bucket sort shape");
     // 16-bit bucket counts, then bucket starts (+ sentinel; every count and start is <= MAXN <=
     // 16384), the rows in bucket order; after the ranking the same bytes are the u64 staging of the
@@ -360,7 +365,8 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
     constexpr int CNT_BYTES = ((EPT * BS + 1) * 2 + 15) / 16 * 16;
     // (the long class stages a whole segment's column at once in the same bytes: one round per
     // column instead of two; 128 KiB - one workgroup per CU, as its registers allow anyway)
-    constexpr int MEM_BYTES = KEYS_LDS || CNT_BYTES + MAXN * 2 >= MAXN * 8 ? CNT_BYTES + MAXN * 2 : MAXN * 8;
+    constexpr int MEM_BYTES =
+        KEYS_LDS || !FUSE || CNT_BYTES + MAXN * 2 >= MAXN * 8 ? CNT_BYTES + MAXN * 2 : MAXN * 8;
     __shared__ alignas(16) uint8_t s_mem[MEM_BYTES];
     uint16_t *const s_cnt = reinterpret_cast<uint16_t *>(s_mem);
     uint32_t *const s_cnt32 = reinterpret_cast<uint32_t *>(s_mem);  // word q / 2 holds counters q, q ^ 1
@@ -397,15 +403,27 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
             continue;
         }
         const int n = int(len);
-        int64_t t[IPT];
+        // (LEAN - the unfused long class: the times are not kept in registers but re-read from the
+        // segment's cache-resident column where needed, so two workgroups fit a CU)
+        constexpr bool LEAN = !KEYS_LDS && !FUSE;
+        int64_t t[LEAN ? 1 : IPT];
+        auto tm_at = [&](int m) -> int64_t {
+            if constexpr (LEAN) {
+                const int i = tid + m * BS;
+                return i < n ? time[b + i] : FZ_TS_NULL;
+            } else {
+                return t[m];
+            }
+        };
         int64_t lo = INT64_MAX, hi = INT64_MIN;
 #pragma unroll
         for (int m = 0; m < IPT; ++m) {
             const int i = tid + m * BS;
-            t[m] = i < n ? time[b + i] : FZ_TS_NULL;
-            if (t[m] != FZ_TS_NULL) {
-                lo = t[m] < lo ? t[m] : lo;
-                hi = t[m] > hi ? t[m] : hi;
+            const int64_t tv = i < n ? time[b + i] : FZ_TS_NULL;
+            if constexpr (!LEAN) t[m] = tv;
+            if (tv != FZ_TS_NULL) {
+                lo = tv < lo ? tv : lo;
+                hi = tv > hi ? tv : hi;
             }
         }
         lo = wave_min(lo);
@@ -437,14 +455,15 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
 #pragma unroll
         for (int m = 0; m < IPT; ++m) {
             const int i = tid + m * BS;
-            const bool null = t[m] == FZ_TS_NULL;
-            uint32_t q = null ? uint32_t(n) : uint32_t(double(uint64_t(t[m] - lo)) * scale);
+            const int64_t tv = tm_at(m);
+            const bool null = tv == FZ_TS_NULL;
+            uint32_t q = null ? uint32_t(n) : uint32_t(double(uint64_t(tv - lo)) * scale);
             q = q < uint32_t(n) || null ? q : uint32_t(n - 1);
             bs[m] = q << 16;
             if (i < n) {
                 const uint32_t sh = (q & 1u) * 16u;
                 bs[m] |= (atomicAdd(&s_cnt32[q >> 1], 1u << sh) >> sh) & 0xffffu;
-                if (KEYS_LDS) s_key[i] = row_key(t[m], i);
+                if (KEYS_LDS) s_key[i] = row_key(tv, i);
             }
         }
         __syncthreads();
@@ -494,7 +513,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
                 continue;
             }
             // (the long class re-reads its own time: t[] need not stay live past the bucketing)
-            const int64_t tm = KEYS_LDS ? t[m] : time[b + i];
+            const int64_t tm = KEYS_LDS ? tm_at(m) : time[b + i];
             const uint64_t key = row_key(tm, i);
             const uint32_t my_tie = tiemode ? tie_of(i) : 0u;
             uint32_t rank = 0;
@@ -519,9 +538,11 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         if constexpr (!FUSE) {
             // short segments: time, project and source position written to the sorted slot (the
             // segment's few KiB stay in L2); k_store_gather moves the other columns afterwards
+            // (the classes without their keys in LDS re-read the segment's cache-resident times
+            // here: t[] is not live past the bucketing - fewer registers, more workgroups per CU)
 #pragma unroll
             for (int m = 0; m < IPT; ++m)
-                if (dq[m] >= 0) out.put(ob + dq[m], t[m], p, b + tid + m * BS);
+                if (dq[m] >= 0) out.put(ob + dq[m], KEYS_LDS ? tm_at(m) : time[b + tid + m * BS], p, b + tid + m * BS);
             __syncthreads();  // LDS is reused by the next segment
             continue;
         }
@@ -535,7 +556,7 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         // HBM; the short classes' segments stay in L2 and gather faster than they stage.)
         uint64_t *stg = KEYS_LDS ? s_key : reinterpret_cast<uint64_t *>(s_mem);
         constexpr int CAP = MAXN;
-        static_assert(KEYS_LDS || MEM_BYTES / 8 >= CAP, "gather staging");
+        static_assert(!FUSE || KEYS_LDS || MEM_BYTES / 8 >= CAP, "gather staging");
         // stage one column (x[m]: row i's value) through LDS in sorted order, write it coalesced
         auto emit = [&](const uint64_t *x, auto store) {
             for (int h = 0; h < n; h += CAP) {
@@ -599,6 +620,23 @@ __global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, in
         __syncthreads();  // LDS is reused by the next segment
     }
 }
+
+template <int BS, int MAXN>
+__global__ __launch_bounds__(BS) void k_seg_time_bucket(const TimeSortTabs T, int64_t min_len, bool flag_longer) {
+    seg_time_bucket<BS, MAXN>(T, min_len, flag_longer);
+}
+#if !FZ_LONG_FUSE
+// (the unfused long class at two workgroups per CU: its LDS (68 KB) allows it, its registers must
+// fit 64 per lane)
+#ifndef FZ_LONG_WPE
+#define FZ_LONG_WPE 8
+#endif
+template <int BS, int MAXN>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(FZ_LONG_WPE, FZ_LONG_WPE))) void k_seg_time_bucket2(
+    const TimeSortTabs T, int64_t min_len, bool flag_longer) {
+    seg_time_bucket<BS, MAXN>(T, min_len, flag_longer);
+}
+#endif
 
 // Prefix-sorts the tables by ([type |] project, row) - the columns riding along; the keys of all
 // three and their segment offsets in one launch each - and sets up their time sort
@@ -766,7 +804,11 @@ static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
     FZ_LAUNCH_CHECK();
     // (a workgroup per CU at most; fewer when the tables are too small to hold many long segments)
     const int64_t g16 = ntot / 16384 < 8 ? 8 : (ntot / 16384 > 256 ? 256 : ntot / 16384);
+#if FZ_LONG_FUSE
     k_seg_time_bucket<1024, 16384><<<unsigned(S < g16 ? S : g16), 1024, 0, st(3)>>>(T, 4096, true);
+#else
+    k_seg_time_bucket2<1024, 16384><<<unsigned(S < 2 * g16 ? S : 2 * g16), 1024, 0, st(3)>>>(T, 4096, true);
+#endif
     FZ_LAUNCH_CHECK();
     if (nh > 0) store_join(c);
 }
@@ -1130,7 +1172,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     // the eligibility histogram reads only the input coverage table: on the third store-build
     // helper beside the prologue and the prefix sorts (joined with the helpers after them, and
     // again before the build returns)
-    const bool elig_aside = store_helpers(c) >= 3;
+    bool elig_aside = store_helpers(c) >= 3;
     if (elig_aside) {
         store_fork(c);
         store_eligibility(c->helpers[2]);
@@ -1202,6 +1244,13 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         vs.dst[i] = voff[i]->ensure<int64_t>(P + 1);
     }
     vs.big = big3;
+    vs.lim_max = s.n_elig.as<int64_t>() + 1;
+    // (the eligibility pass on its helper is long done - the prefix and time sorts outlast it - and
+    // its bound travels with this read-back)
+    if (elig_aside) {
+        store_join(c);
+        elig_aside = false;
+    }
     // (written straight into the pinned read-back area through its device address: two blit copies
     // fewer in front of the gather and the host's wake-up)
     k_store_views<<<1, kSortBlock, 0, c->stream>>>(vs, P, ppart, pblk, c->d_pinned);
@@ -1281,6 +1330,8 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     s.fuzz.max_seg = maxseg[0];
     s.covb.max_seg = maxseg[1];
     s.cov.max_seg = maxseg[2];
+    // (at least 1 when the table has rows: the analyses keep one - empty - session, rq2_count:285)
+    s.cov.lim_seg = c->h_pinned[19] < maxseg[2] ? (c->h_pinned[19] > 0 ? c->h_pinned[19] : 1) : maxseg[2];
     s.issues.max_seg = maxseg[3];
     s.built = true;
     if (stats) {

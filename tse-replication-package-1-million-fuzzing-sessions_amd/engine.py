@@ -121,7 +121,7 @@ class FzRq4aOut(C.Structure):
 
 FZ_RQ4B_NCOUNTS, FZ_RQ4B_NTESTS = 12, 8
 (RQ4B_SESSIONS, RQ4B_LAST, RQ4B_DELTA_PROJECTS, RQ4B_INIT_G2, RQ4B_INIT_G1, RQ4B_G1, RQ4B_G2, RQ4B_G3,
- RQ4B_G4) = range(9)
+ RQ4B_G4, RQ4B_VALUES) = range(10)
 RQ4B_MWU_P, RQ4B_CLIFF, RQ4B_BM_STAT, RQ4B_BM_P, RQ4B_LEVENE_W, RQ4B_LEVENE_P = range(6)
 FZ_RQ4B_SKIP_SESSION_STATS = 1
 

@@ -667,6 +667,7 @@ def rq4a_sharded(shard, rank: int, world: int, lo: int, hi: int, finish_later: b
 
 # ----------------------------------------------------------------------------------------- RQ4b
 (RQ4B_SESSIONS, RQ4B_LAST, RQ4B_DELTA_PROJECTS, RQ4B_INIT_G2, RQ4B_INIT_G1) = range(5)
+RQ4B_VALUES = 9
 
 
 def rq4b_sharded(shard, rank: int, world: int, finish_later: bool = False):
@@ -689,7 +690,8 @@ def rq4b_sharded(shard, rank: int, world: int, finish_later: bool = False):
     dev = counts.device
     P = part["member"].numel()
     offs_all = part["trend_offsets"]
-    head = torch.stack([counts[RQ4B_SESSIONS], offs_all[-1].to(torch.int64), counts[RQ4B_DELTA_PROJECTS],
+    # (the values' count from the counters: trend_offsets is written up to the shard's session count)
+    head = torch.stack([counts[RQ4B_SESSIONS], counts[RQ4B_VALUES], counts[RQ4B_DELTA_PROJECTS],
                         counts[RQ4B_INIT_G2], counts[RQ4B_INIT_G1]])
     m_loc, n, nd, n2, n1 = (int(v) for v in host_many(head)[0])  # one sync for every host-side size
     offs2 = offs_all[:2 * m_loc + 1]
@@ -1103,8 +1105,8 @@ class GpuRQ4bShard:
             self.launch()
         self.pre = False
         P = eng.tables.fz.n_projects  # column lengths stay on the device (counts); rq4b_sharded slices
-        # (trend_offsets: 2 * max_cov_per_project + 1 entries, the segments past the shard's
-        # longest series empty - its last entry is the number of values)
+        # (trend_offsets: 2 * max_cov_per_project + 1 entries, written up to 2 * the shard's session
+        # count - counts[RQ4B_VALUES] is the number of values)
         return {"counts": b.counts, "member": b.member[:P], "trend_values": b.trend_values,
                 "trend_offsets": b.trend_offsets, "pre_cov": b.pre_cov, "post_cov": b.post_cov,
                 "delta_order": b.delta_order, "init_g2": b.init_g2, "init_g1": b.init_g1}
