@@ -314,9 +314,6 @@ constexpr uint64_t kBlkTop = (uint64_t(1) << (64 - kBlkPosBits)) - 1;  // time f
 // does not fit the key, is flagged for the merge sort instead.  MAXN <= 4096 keeps the keys in LDS;
 // larger classes re-read them from the (prefix-sorted, cache-resident) time column.
 constexpr int kBucketSkew = 32;
-#ifndef FZ_LONG_SCATTER
-#define FZ_LONG_SCATTER 0
-#endif
 #ifndef FZ_LONG_FUSE
 #define FZ_LONG_FUSE 1  // the 16384-row class gathers its columns itself (0: k_store_gather does)
 #endif
@@ -562,14 +559,6 @@ __device__ __forceinline__ void seg_time_bucket(const TimeSortTabs &T, int64_t m
         static_assert(!FUSE || KEYS_LDS || MEM_BYTES / 8 >= CAP, "gather staging");
         // stage one column (x[m]: row i's value) through LDS in sorted order, write it coalesced
         auto emit = [&](const uint64_t *x, auto store) {
-#if FZ_LONG_SCATTER
-            if constexpr (!KEYS_LDS) {  // (experiment: each row written straight to its sorted slot)
-#pragma unroll
-                for (int m = 0; m < IPT; ++m)
-                    if (dq[m] >= 0) store(ob + dq[m], x[m]);
-                return;
-            }
-#endif
             for (int h = 0; h < n; h += CAP) {
 #pragma unroll
                 for (int m = 0; m < IPT; ++m)

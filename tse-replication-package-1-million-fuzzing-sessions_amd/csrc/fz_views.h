@@ -470,6 +470,10 @@ void filter_view(fz_ctx *c, const View &v, int64_t n, int64_t P, Pred pred, TmpV
     Emit out{};
     if (emit) out = *emit;
     else if constexpr (std::is_same<Emit, RowTimeProj>::value) out = RowTimeProj{dst.row, dst.time, dst.proj};
+    // (probe name: the filters of a few projects - a count given, or a project selection without a
+    // time bound - are "filter_select" (scripts/pmc_traffic.py scopes them by predicate), the rest
+    // "filter_compact", whether or not the range scan applies at this size)
+    const bool selective = sel.count || (sel.flags && !sel.has_lim);
     if (sel.has_lim && n < kRangeScanMin) {
         // a small view: the plain filter (the predicate tests the bound itself) - the virtual-row
         // setup is one more launch on the analyses' latency-bound chains (config 2)
@@ -504,7 +508,7 @@ void filter_view(fz_ctx *c, const View &v, int64_t n, int64_t P, Pred pred, TmpV
         // (a time-bounded view is a range scan: its virtual rows' predicate bytes are booked from
         // their device count - the rows past the bound are not read)
         const bool ranged = sel.voff && sel.has_lim;
-        ProbeScope ps(c, sel.flags && !ranged ? "filter_select" : "filter_compact",
+        ProbeScope ps(c, selective ? "filter_select" : "filter_compact",
                       sel.flags ? 0.0 : double(n) * PredBytes<Pred>::value, dst.d_n, emit ? bytes_out : 28.0);
         if (ranged) ps.add_count(sel.voff + P, PredBytes<Pred>::value);
         if (sel.voff)
