@@ -275,6 +275,152 @@ __device__ inline uint32_t classify(const Line &L, int &cap_off, int &cap_len) {
     return f;
 }
 
+// The same classification in ONE scan of the line (the "Starting Step #N" lines - a few per log -
+// keep the pattern-by-pattern code above): every pattern of :120-214 starts with one of eleven
+// bytes, so a byte that is none of them (a constant 256-bit set, no memory) costs one test; at a
+// trigger byte only that byte's patterns are matched, and what the reference's searches depend on
+// is recorded as positions - the first image / GCS occurrence with a non-empty capture, the first
+// "Step #N: Pulling image" and the first "Step #N:", the first "compile-" and the last "-x86_64",
+// the first "/report/" and the last ".html", the earliest quote a jq_inplace candidate needs and
+// the last quote - and folded after the scan exactly as the searches would (pattern-by-pattern:
+// ~12 scans of every line).
+__device__ inline bool trigger_byte(int b) {
+    // 'A' 'N' 'E' 'S' '/' 'U' 'c' '-' 'P' 'j' '.' '\''
+    constexpr uint64_t lo = (1ull << '/') | (1ull << '-') | (1ull << '.') | (1ull << '\'');
+    constexpr uint64_t hi = (1ull << ('A' - 64)) | (1ull << ('N' - 64)) | (1ull << ('E' - 64)) | (1ull << ('S' - 64)) |
+                            (1ull << ('U' - 64)) | (1ull << ('c' - 64)) | (1ull << ('P' - 64)) | (1ull << ('j' - 64));
+    return b < 64 ? ((lo >> b) & 1ull) != 0 : (b < 128 && ((hi >> (b - 64)) & 1ull) != 0);
+}
+
+__device__ inline uint32_t classify1(const Line &L, int &cap_off, int &cap_len) {
+    if (match_at(L, 0, "Starting Step #") >= 0 && digits(L, 15) > 0) return classify(L, cap_off, cap_len);
+    const int n = L.n;
+    int img_off = -1, img_len = 0, gcs_off = -1, gcs_len = 0;
+    bool has_error = false, unable = false, pushdone = false;
+    int pull_set = -1;         // set value of the first "Step #N: Pulling image: ...base-runner"
+    int step_colon = -1;       // end of the first "Step #N:" (the JSON-open test)
+    int first_compile = -1, last_x86 = -1, first_report = -1, last_html = -1;
+    int jq_need = INT_MAX, last_quote = -1;  // a jq_inplace candidate needs a quote at >= jq_need
+    for (int k = 0; k < n; ++k) {
+        const int b = L.p[k];
+        if (!trigger_byte(b)) continue;
+        switch (b) {
+        case 'A':
+            if (img_off < 0 && match_at(L, k, kImage) >= 0) {
+                const int st = k + plen(kImage);
+                int e = st, w;
+                while (e < n && L.p[e] != ':' && (w = ws_at(L, e)) == 0) e += utf8_len(L.p[e]);
+                if (e > st) img_off = st, img_len = e - st;
+            }
+            break;
+        case 'N':
+            if (gcs_off < 0 && match_at(L, k, kGcs) >= 0) {
+                const int st = k + plen(kGcs);
+                int e = st;
+                while (e < n && L.p[e] != '/') ++e;
+                if (e > st && match_at(L, e, "/textcov_reports") >= 0) gcs_off = st, gcs_len = e - st;
+            }
+            break;
+        case 'E':
+            if (!has_error && match_at(L, k, "ERROR") >= 0) has_error = true;
+            break;
+        case 'S':
+            if ((pull_set < 0 || step_colon < 0) && match_at(L, k, "Step #") >= 0) {
+                const int d = digits(L, k + 6);
+                if (d > 0) {
+                    if (pull_set < 0 && match_at(L, k + 6 + d, ": Pulling image: gcr\x01io/oss-fuzz-base/base-runner") >= 0)
+                        pull_set = (d == 1 && L.p[k + 6] == '0')   ? BT_INTRO
+                                   : (d == 1 && L.p[k + 6] == '4') ? BT_COV
+                                   : (d == 1 && L.p[k + 6] == '5') ? BT_FUZZ
+                                                                    : BT_UNKNOWN;
+                    if (step_colon < 0 && L.at(k + 6 + d) == ':') step_colon = k + 7 + d;
+                }
+            }
+            break;
+        case '/':
+            if (first_report < 0 && match_at(L, k, "/report/") >= 0) first_report = k;
+            break;
+        case '.':
+            if (match_at(L, k, ".html") >= 0) last_html = k;
+            break;
+        case 'U':
+            if (!unable && match_at(L, k, "Unable to find image 'gcr\x01io/oss-fuzz-base/base-runner:latest' locally") >= 0)
+                unable = true;
+            break;
+        case 'c':
+            if (first_compile < 0 && match_at(L, k, "compile-") >= 0) first_compile = k;
+            break;
+        case '-':
+            if (match_at(L, k, "-x86_64") >= 0) last_x86 = k;
+            break;
+        case 'P':
+            if (!pushdone && match_at(L, k, "PUSH") >= 0) {
+                int q = k + 4, w;
+                while ((w = ws_at(L, q)) > 0) q += w;
+                if (match_at(L, q, "DONE") >= 0) pushdone = true;
+            }
+            break;
+        case 'j':
+            if (match_at(L, k, "jq_inplace ") >= 0) {
+                const int x = k + 11;
+                int y = x;
+                while (y < n && L.p[y] != ' ') ++y;
+                if (y > x && L.at(y + 1) == '\'') jq_need = y + 2 < jq_need ? y + 2 : jq_need;
+            }
+            break;
+        default:  // '\''
+            last_quote = k;
+            break;
+        }
+    }
+    uint32_t f = 0;
+    cap_off = -1;
+    cap_len = 0;
+    if (img_off >= 0) {
+        f |= BL_IMAGE, cap_off = img_off, cap_len = img_len;
+    } else if (gcs_off >= 0) {
+        f |= BL_IMAGE, cap_off = gcs_off, cap_len = gcs_len;
+    }
+    int sb = 0, se = n;
+    strip(L, sb, se);
+    if (equals(L, sb, se, "ERROR")) f |= BL_EQ_ERROR;
+    if (equals(L, sb, se, "PUSH")) f |= BL_EQ_PUSH;
+    if (equals(L, sb, se, "DONE")) f |= BL_EQ_DONE;
+    if (equals(L, sb, se, "ERROR: context deadline exceeded")) f |= BL_EQ_DEADLINE;
+    if (has_error) f |= BL_HAS_ERROR;
+    // :120-152 in the reference's order: each later test overrides the value
+    uint32_t set = pull_set >= 0 ? uint32_t(pull_set) : BT_NONE;
+    if (first_report >= 0 && last_html >= first_report + 8) set = BT_COV;
+    if (unable) set = BT_FUZZ;
+    if (first_compile >= 0 && last_x86 >= first_compile + 9) {  // compile_value: group(2) of the greedy match
+        int p = -1;
+        for (int k = last_x86 - 1; k >= first_compile + 8; --k)
+            if (L.p[k] == '-') {
+                p = k;
+                break;
+            }
+        if (p >= 0) {
+            const int b = p + 1, e = last_x86;
+            set = (equals(L, b, e, "address") || equals(L, b, e, "memory") || equals(L, b, e, "undefined") ||
+                   equals(L, b, e, "none"))
+                      ? BT_FUZZ
+                  : equals(L, b, e, "coverage")     ? BT_COV
+                  : equals(L, b, e, "introspector") ? BT_INTRO
+                                                    : BT_UNKNOWN;
+        }
+    }
+    if (pushdone) f |= BL_PUSHDONE;
+    f |= set << kSetShift;
+    if (last_quote >= jq_need) f |= BL_JQ;
+    if (se > sb && L.p[se - 1] == '}') f |= BL_CLOSE;
+    if (se > sb && L.p[se - 1] == '{' && step_colon >= 0) {
+        int b = step_colon, e = n;
+        strip(L, b, e);
+        if (e == b + 1 && L.p[b] == '{') f |= BL_OPEN;
+    }
+    return f;
+}
+
 // ---- 1. line starts -------------------------------------------------------------------------
 // A byte chunk of one log (host-built list: every chunk lies inside one log).
 struct LogChunks {
@@ -337,6 +483,9 @@ __device__ inline bool break_at(const uint8_t *t, int64_t i, int64_t le) {
 // coalesced 16-byte loads, then every lane scans its own line there; a span longer than the wave's
 // buffer (very long lines) is read from global memory instead.
 constexpr int kWaveBuf = 8192;
+#ifndef FZ_BL_ONEPASS
+#define FZ_BL_ONEPASS 1  // (0: the pattern-by-pattern classification, for A/B)
+#endif
 __global__ __launch_bounds__(kBlock) void k_line_classify(const uint8_t *__restrict__ t, int64_t n_bytes,
                                                           const int64_t *__restrict__ log_offs, int64_t n_logs,
                                                           const int64_t *__restrict__ line_start,
@@ -373,7 +522,7 @@ __global__ __launch_bounds__(kBlock) void k_line_classify(const uint8_t *__restr
             const Line L{lp, int(e)};
             e += s;
             int co, cl;
-            line_flags[l] = classify(L, co, cl);
+            line_flags[l] = FZ_BL_ONEPASS ? classify1(L, co, cl) : classify(L, co, cl);
             line_len[l] = int32_t(e - s);
             line_cap[l] = co < 0 ? -1 : ((int64_t(co) << 32) | int64_t(cl));
         }
