@@ -137,13 +137,14 @@ def main():
     if args.strong:
         from tse_amd import parallel as par
         full = synth.generate(synth.config(args.config))
-        if rehearsal:
-            lo, hi = par.shard_bounds(full, args.shard_of)[args.shard_rank]
-        else:
-            lo, hi = par.shard_bounds(full, world)[rank]
-        t = par.take_shard(full, lo, hi)[0]
+        # project shards, a giant project's rows that no analysis reads spread over the ranks
+        # (parallel.split_plan: config 5's Zipf giant)
+        plan = par.split_plan(full, args.shard_of if rehearsal else world)
+        r = args.shard_rank if rehearsal else rank
+        lo, hi = plan.bounds[r]
+        t = par.take_split(full, plan, r)[0]
         job_rows = full.n_rows if not rehearsal else None
-        del full
+        del full, plan
     else:
         cfg = synth.config(args.config, seed=synth.config(args.config).seed + 1000 * rank)
         t = synth.generate(cfg)

@@ -1,7 +1,8 @@
 """The project-sharded path on the FULL config-3 and config-5 tables (100M coverage
 rows over 10k projects, "project-sharded over 2/4/8 MI355X"; config 5 Zipf-skewed, its ~20M-row giant
-whole on one shard): two, four or eight ranks on cuda:0, each holding only its
-``parallel.shard_bounds`` half of the projects, run RQ2-count and RQ4b through libfz
+whole on its owner's shard, its coverage rows no analysis reads spread over the ranks at eight ranks -
+parallel.split_plan): two, four or eight ranks on cuda:0, each holding only its
+``parallel.split_plan`` share of the projects, run RQ2-count and RQ4b through libfz
 (fz_rq2_count_ex / fz_rq4b_ex with the session statistics skipped, then the all-to-all by session
 index to the session owners, fz_rq2_session_stats / fz_rq4b_session_stats there, and the gathers)
 over gloo - the same driver code bench.py runs over RCCL.  Rank 0 then builds the whole table on
@@ -55,16 +56,23 @@ def _check(rank, world, name):
     t0 = time.perf_counter()
     t = synth.generate(synth.config(name))
     assert t.n_rows >= 99_000_000
-    bounds = par.shard_bounds(t, world)
+    # project shards; a project larger than a rank's share (config 5's Zipf giant at 8 ranks) keeps
+    # every row an analysis reads on its owner and has its other coverage rows spread over the
+    # ranks (parallel.split_plan)
+    plan = par.split_plan(t, world)
+    bounds = plan.bounds
     lo, hi = bounds[rank]
-    if rank == 0:  # the shards' row shares (config 5: the Zipf giant stays whole on one shard)
+    if rank == 0:
         rows = (np.bincount(t.b_project.astype(np.int64), minlength=len(t.projects))
                 + np.bincount(t.c_project.astype(np.int64), minlength=len(t.projects))
                 + np.bincount(t.i_project.astype(np.int64), minlength=len(t.projects)))
-        share = [int(rows[a:b].sum()) / (t.n_rows / world) for a, b in bounds]
-        print(f"{name} world {world}: largest project {int(rows.max()):,} rows; shard shares of the mean "
-              + " ".join(f"{x:.2f}" for x in share), flush=True)
-    ts, _ = par.take_shard(t, lo, hi)
+        share = [(len(b) + len(c) + len(i)) / (t.n_rows / world)
+                 for b, c, i in zip(plan.builds, plan.coverage, plan.issues)]
+        print(f"{name} world {world}: largest project {int(rows.max()):,} rows, {plan.moved:,} rows moved off "
+              f"their owner; shard shares of the mean " + " ".join(f"{x:.2f}" for x in share), flush=True)
+        if name == "c5" and world == 8:
+            assert plan.moved > 0 and max(share) < 1.05, "the Zipf giant's movable rows were meant to spread"
+    ts, _ = par.take_split(t, plan, rank)
     eng = E.Engine(0)
     eng.upload(ts)
     eng.build_store()

@@ -57,6 +57,8 @@ def make_table(case: str, world: int) -> Tables:
                i_number=inum, i_project=ip, i_rts=irts, i_status=ist, i_new_id=inew, pi_project=t.pi_project,
                pi_first_commit=t.pi_first_commit, build_types=t.build_types, results=t.results,
                statuses=t.statuses, corpus_csv=t.corpus_csv)
+    if case == "giant":
+        t = add_giant(t)
     if case == "last_shard_no_issues":
         lo, _ = par.shard_bounds(t, world)[-1]
         keep = t.i_project.astype(np.int64) < lo
@@ -64,6 +66,49 @@ def make_table(case: str, world: int) -> Tables:
         t = dataclasses.replace(t, i_number=t.i_number[keep], i_project=t.i_project[keep], i_rts=t.i_rts[keep],
                                 i_status=t.i_status[keep], i_new_id=t.i_new_id[keep])
     return t
+
+
+def add_giant(t: Tables, extra: int = 90000) -> Tables:
+    """The tiny table with one eligible project grown into a Zipf-like giant: `extra` more daily
+    coverage rows after its last one (past the analyses' date bounds; NULL and non-positive rows
+    among them), and its corpus commit moved into those rows (group 4: the delta window of
+    rq4b_coverage.py:745-772 then lies among the rows split_plan would move).  Issue numbers and
+    builds unchanged."""
+    import dataclasses
+    import datetime as dt
+    from oracle import rq_oracle as orc
+    from tse_amd.schema import US_PER_DAY
+    elig = orc.eligible_projects(t)
+    g = int(elig[0])
+    rng = np.random.default_rng(77)
+    last = int(t.c_date[t.c_project == g].max())
+    d0 = max(last + US_PER_DAY, par.SPLIT_BOUND_US + 3 * US_PER_DAY)
+    dates = d0 + np.arange(extra, dtype=np.int64) * US_PER_DAY
+    total = rng.integers(1000, 5000, size=extra).astype(np.int64)
+    covered = (total * rng.uniform(0.0, 0.8, size=extra)).astype(np.int64)
+    covered[::97] = 0                                  # zero coverage (not positive)
+    valid = rng.random(extra) < 0.9
+    cov = np.where(valid, covered / total * 100.0, 0.0)
+    cat = lambda a, b: np.concatenate([a, b.astype(a.dtype)])  # noqa: E731
+    t = dataclasses.replace(
+        t, c_project=cat(t.c_project, np.full(extra, g)), c_date=cat(t.c_date, dates), c_coverage=cat(t.c_coverage, cov),
+        c_coverage_valid=cat(t.c_coverage_valid, valid), c_covered=cat(t.c_covered, np.where(valid, covered, 0)),
+        c_covered_valid=cat(t.c_covered_valid, valid), c_total=cat(t.c_total, np.where(valid, total, 0)),
+        c_total_valid=cat(t.c_total_valid, valid))
+    # corpus commit 500 days into the new rows: the project becomes group 4 (>= 7 days after creation)
+    lines = t.corpus_csv.splitlines()
+    name = t.projects[g]
+    cc = dt.datetime(1970, 1, 1) + dt.timedelta(microseconds=int(dates[500]) + 3_600_000_000)
+    for k, ln in enumerate(lines):
+        if ln.startswith(name + ","):
+            f = ln.split(",")
+            cre = dt.datetime.fromisoformat(f[4])
+            el = (cc.replace(tzinfo=cre.tzinfo) - cre).total_seconds()
+            lines[k] = f"{name},True,{cc.isoformat()}+00:00,,{f[4]},{float(int(el))},"
+            break
+    else:
+        lines.append(f"{name},True,{cc.isoformat()}+00:00,,{cc.isoformat()}+00:00,{float(30 * 86400)},")
+    return dataclasses.replace(t, corpus_csv="\n".join(lines) + "\n")
 
 
 class OracleRQ1Shard:
@@ -381,8 +426,14 @@ def _check(rank, world, case, threaded=False, deferred=False):
     from oracle import rq_oracle as orc
     from gpu_common import assert_same
     t = make_table(case, world)
-    lo, hi = par.shard_bounds(t, world)[rank]
-    ts, rows = par.take_shard(t, lo, hi)
+    if case == "giant":  # the giant's movable coverage rows spread over the ranks (split_plan)
+        plan = par.split_plan(t, world)
+        assert plan.moved > 0, "the giant's rows past the date bounds were meant to move"
+        lo, hi = plan.bounds[rank]
+        ts, rows = par.take_split(t, plan, rank)
+    else:
+        lo, hi = par.shard_bounds(t, world)[rank]
+        ts, rows = par.take_shard(t, lo, hi)
     nF = np.bincount(ts.b_project[ts.b_type == 0].astype(np.int64), minlength=len(t.projects))
     M = par.agree_max(int(nF.max()) if len(nF) else 0)
     nF4 = np.bincount(ts.b_project[(ts.b_type == 0) & (ts.b_time < LIMIT_US)].astype(np.int64),
@@ -432,7 +483,7 @@ def _check(rank, world, case, threaded=False, deferred=False):
         return
     assert_same(rq2_add_result(*res["rq2a"]), orc.rq2_add(t), "rq2_add")
     g = orc.rq1(t)
-    assert int(any_rerun) > 0, "the table was built to need the cross-shard dedup"
+    assert case == "giant" or int(any_rerun) > 0, "the table was built to need the cross-shard dedup"
     c = counts.numpy()
     assert c[par.RQ1_ISSUES_LIM] == g.n_issues_lim and c[par.RQ1_ISSUES_LIM_PROJECTS] == g.n_issues_lim_projects
     assert c[par.RQ1_FIXED_LIM] == g.n_fixed_lim and c[par.RQ1_FIXED_LIM_PROJECTS] == g.n_fixed_lim_projects
@@ -491,7 +542,7 @@ def test_shard_bounds_cover_and_balance():
 
 
 @pytest.mark.parametrize("world,case", [(2, "collide"), (3, "collide"), (3, "last_shard_no_issues"), (8, "collide"),
-                                        (8, "last_shard_no_issues")])
+                                        (8, "last_shard_no_issues"), (2, "giant"), (3, "giant"), (8, "giant")])
 def test_sharded_rq1_rq3_match_whole_table(world, case, tmp_path):
     _spawn(world, case, tmp_path)
 

@@ -40,7 +40,7 @@ from typing import List, Tuple
 
 import numpy as np
 
-from .schema import Tables
+from .schema import LIMIT_US, RQ3_LIMIT_US, TS_NULL, US_PER_DAY, Tables
 
 # fz.h RQ1 counter layout (FZ_RQ1_*)
 (RQ1_ISSUES_LIM, RQ1_ISSUES_LIM_PROJECTS, RQ1_FIXED_LIM, RQ1_FIXED_LIM_PROJECTS, RQ1_ELIGIBLE,
@@ -124,6 +124,127 @@ def take_shard(t: Tables, lo: int, hi: int) -> Tuple[Tables, ShardRows]:
         return np.nonzero((p >= lo) & (p < hi))[0]
     b, c, i = sel(t.b_project), sel(t.c_project), sel(t.i_project)
     pi = sel(t.pi_project)
+    s = dataclasses.replace(
+        t, b_project=t.b_project[b], b_type=t.b_type[b], b_result=t.b_result[b], b_time=t.b_time[b],
+        b_modules=t.b_modules[b], b_revisions=t.b_revisions[b], b_name=t.b_name[b],
+        c_project=t.c_project[c], c_date=t.c_date[c], c_coverage=t.c_coverage[c],
+        c_coverage_valid=t.c_coverage_valid[c], c_covered=t.c_covered[c], c_covered_valid=t.c_covered_valid[c],
+        c_total=t.c_total[c], c_total_valid=t.c_total_valid[c],
+        i_number=t.i_number[i], i_project=t.i_project[i], i_rts=t.i_rts[i], i_status=t.i_status[i],
+        i_new_id=t.i_new_id[i], pi_project=t.pi_project[pi], pi_first_commit=t.pi_first_commit[pi])
+    return s, ShardRows(lo, hi, b, c, i)
+
+
+# ------------------------------------------------------------------------- giant projects split
+# A project larger than one rank's share (config 5's Zipf giant: 20.8 M of 100 M rows) would make
+# its rank the slowest whatever the cut.  Every analysis reads a coverage row only when it is dated
+# before a bound (the latest is RQ3's DATE(date) < '2025-01-09', rq3:263; the others use
+# '2025-01-08', queries1.py:3) or when it lies in RQ4b's coverage-delta window (the last 7 positive
+# rows before the corpus day and the first 7 from it, rq4b_coverage.py:745-772).  So a giant's
+# other coverage rows - "movable" - are read by no analysis: they can sit on any rank.  There
+# their project has no row before the eligibility date bound, so it is never eligible (>= 365 rows,
+# rq1:144-152) and enters no analysis, while the rank's store still holds and sorts them: the
+# store's work follows the rows, the analyses' stay with the owner.  The owner keeps the giant's
+# builds, issues, every coverage row before the bound and the delta window; the movable rows are
+# spread over the ranks in date order to even out their row counts.
+SPLIT_BOUND_US = int(max(LIMIT_US, RQ3_LIMIT_US))
+DELTA_WINDOW = 7
+
+
+@dataclass
+class SplitPlan:
+    """Per rank: its own project range [lo, hi) and the global row ids it holds of each table."""
+    bounds: List[Tuple[int, int]]
+    builds: List[np.ndarray]
+    coverage: List[np.ndarray]
+    issues: List[np.ndarray]
+    info: List[np.ndarray]
+    moved: int  # coverage rows placed on another rank than their project's owner
+
+
+def _giant_must(t: Tables, rows: np.ndarray, p: int, corpus_us) -> np.ndarray:
+    """Mask over a project's coverage rows (global ids `rows`, ascending): the rows an analysis may
+    read - dated before SPLIT_BOUND_US, or in the delta window around the corpus day."""
+    date = t.c_date[rows]
+    must = date < SPLIT_BOUND_US
+    cu = int(corpus_us[p])
+    if cu != TS_NULL:
+        pos = np.nonzero(t.c_coverage_valid[rows] & (t.c_coverage[rows] > 0))[0]
+        if len(pos):
+            o = pos[np.argsort(date[pos], kind="stable")]      # positive rows by (date, row)
+            j = int(np.searchsorted(date[o], (cu // US_PER_DAY) * US_PER_DAY, "left"))
+            must[o[max(0, j - DELTA_WINDOW):j + DELTA_WINDOW]] = True
+    return must
+
+
+def split_plan(t: Tables, world: int) -> SplitPlan:
+    """shard_bounds with the giants' movable coverage rows spread over the ranks (see above)."""
+    from .rq.common import corpus_columns
+    P = len(t.projects)
+    nb = np.bincount(t.b_project.astype(np.int64), minlength=P)
+    nc = np.bincount(t.c_project.astype(np.int64), minlength=P)
+    ni = np.bincount(t.i_project.astype(np.int64), minlength=P)
+    total = (nb + nc + ni).astype(np.int64)
+    target = -(-int(total.sum()) // max(world, 1))
+    # (projects over half a share: a contiguous cut around one of them leaves its range unbalanced -
+    # config 5 at four ranks: largest share 1.17 of the mean with the 20.8 M-row giant whole)
+    giants = np.nonzero(total > target // 2)[0] if world > 1 else np.zeros(0, np.int64)
+    movable = {}
+    if len(giants):
+        corpus_us = corpus_columns(t)[1]
+        sel = np.nonzero(np.isin(t.c_project, giants.astype(t.c_project.dtype)))[0]
+        gp = t.c_project[sel].astype(np.int64)
+        order = np.argsort(gp, kind="stable")
+        sel, gp = sel[order], gp[order]
+        starts = np.searchsorted(gp, giants)
+        ends = np.searchsorted(gp, giants, "right")
+        for p, a, b in zip(giants.tolist(), starts.tolist(), ends.tolist()):
+            rows = sel[a:b]
+            m = rows[~_giant_must(t, rows, p, corpus_us)]
+            if len(m):
+                movable[p] = m[np.argsort(t.c_date[m], kind="stable")]  # date order
+    weight = total.copy()
+    for p, m in movable.items():
+        weight[p] -= len(m)
+    bounds = partition_rows(weight, world)
+    load = np.array([int(weight[a:b].sum()) for a, b in bounds], np.int64)
+    incoming = [[] for _ in range(world)]
+    out_of = {}
+    for p, m in movable.items():
+        owner = next(r for r, (a, b) in enumerate(bounds) if a <= p < b)
+        k = 0
+        while k < len(m):
+            # the least-loaded rank takes the next date range, up to the mean share
+            r = int(np.argmin(load))
+            take = max(1, min(len(m) - k, target - int(load[r]))) if load[r] < target else len(m) - k
+            if r != owner:
+                incoming[r].append(m[k:k + take])
+                out_of.setdefault(p, []).append(m[k:k + take])
+            load[r] += take
+            k += take
+    moved_out = np.sort(np.concatenate([x for v in out_of.values() for x in v])) if out_of else np.zeros(0, np.int64)
+
+    def sel_rows(proj, lo, hi):
+        p = proj.astype(np.int64)
+        return np.nonzero((p >= lo) & (p < hi))[0]
+    B, C, I, PI = [], [], [], []
+    for r, (lo, hi) in enumerate(bounds):
+        B.append(sel_rows(t.b_project, lo, hi))
+        own = sel_rows(t.c_project, lo, hi)
+        if len(moved_out):
+            own = own[~np.isin(own, moved_out, assume_unique=True)]
+        extra = np.concatenate(incoming[r]) if incoming[r] else np.zeros(0, np.int64)
+        C.append(np.sort(np.concatenate([own, extra])) if len(extra) else own)
+        I.append(sel_rows(t.i_project, lo, hi))
+        PI.append(sel_rows(t.pi_project, lo, hi))
+    return SplitPlan(bounds, B, C, I, PI, int(len(moved_out)))
+
+
+def take_split(t: Tables, plan: SplitPlan, rank: int) -> Tuple[Tables, ShardRows]:
+    """Rank `rank`'s table of a split plan (rows in their original order; ids, pools and the
+    corpus CSV global) and the global ids of its rows."""
+    b, c, i, pi = plan.builds[rank], plan.coverage[rank], plan.issues[rank], plan.info[rank]
+    lo, hi = plan.bounds[rank]
     s = dataclasses.replace(
         t, b_project=t.b_project[b], b_type=t.b_type[b], b_result=t.b_result[b], b_time=t.b_time[b],
         b_modules=t.b_modules[b], b_revisions=t.b_revisions[b], b_name=t.b_name[b],
