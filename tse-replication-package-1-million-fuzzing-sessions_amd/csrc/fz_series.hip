@@ -1164,15 +1164,18 @@ __device__ inline void block_dd_sums(const DD (&acc)[NV], double (&s_hi)[NW][NV]
 // order, for y -= x[N // 2]) by the workgroup, each thread over its run [k0, k1) of <= kSmallPer
 // values: the passes of seg_shapiro (sum of m_i^2, then sx / sa, then ssa / ssx / sax), every sum
 // double-double as there; a thread's coefficients stay in registers between the last two passes.
+// s_m (LDS, kSpearmanSmall / 2 doubles): the normal scores m_k (k <= n / 2) of the first pass,
+// reused by the coefficients of the second - one ppnd per score instead of one per score and pass
 template <int BS = kBlock>
 __device__ inline void shapiro_block(const double *__restrict__ v, const double *__restrict__ src, int64_t b,
                                      int64_t n, int64_t k0, int64_t k1, double (&s_hi)[BS / kWave][3],
-                                     double (&s_lo)[BS / kWave][3], double *w_out, double *p_out) {
+                                     double (&s_lo)[BS / kWave][3], double *s_m, double *w_out, double *p_out) {
     constexpr int NW = BS / kWave, PER = int(kSpearmanSmall / BS);
     DD a0[1] = {{0.0, 0.0}};
     if (n >= 3)
         for (int64_t k = 1 + threadIdx.x; k <= n / 2; k += BS) {
             const double m = stats::sw_m(k, n);
+            s_m[k - 1] = m;
             a0[0] = dd_add_d(a0[0], m * m);
         }
     double summ2[1];
@@ -1195,7 +1198,10 @@ __device__ inline void shapiro_block(const double *__restrict__ v, const double 
         co[u] = y[u] = 0.0;
         if (j < k1) {
             y[u] = (v[j] - x0) / range;
-            co[u] = stats::sw_coef_at(cf, j - b + 1);
+            // stats::sw_coef_at(cf, i) with the pass-A score of the mirrored index
+            const int64_t i = j - b + 1, jm = n + 1 - i, k = i < jm ? i : jm;
+            const double a = i == jm ? 0.0 : stats::sw_a_m(cf, k, s_m[k - 1]);
+            co[u] = i == jm ? 0.0 : (i > jm ? a : -a);
             a1[0] = dd_add_d(a1[0], y[u]);
             a1[1] = dd_add_d(a1[1], co[u]);
         }
@@ -1241,11 +1247,12 @@ __global__ __launch_bounds__(kBlock) void k_spearman_index_small(const double *_
                                                                  double *__restrict__ sw_p = nullptr) {
     __shared__ double s_tmp[4];
     __shared__ double s_hi[4][3], s_lo[4][3];
+    __shared__ double s_m[kSpearmanSmall / 2];
     for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
         const int64_t b = offs[s], n = offs[s + 1] - b;
         const int64_t per = (n + kBlock - 1) / kBlock;
         const int64_t k0 = b + int64_t(threadIdx.x) * per, k1 = k0 + per < b + n ? k0 + per : b + n;
-        if (sw_w) shapiro_block(sv, src, b, n, k0, k1, s_hi, s_lo, sw_w + s, sw_p + s);
+        if (sw_w) shapiro_block(sv, src, b, n, k0, k1, s_hi, s_lo, s_m, sw_w + s, sw_p + s);
         if (!rho) continue;
         spearman_block<kBlock>(sv, pos, b, n, s_tmp, rho + s, pval ? pval + s : nullptr);
     }
@@ -1571,6 +1578,7 @@ __global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__r
     __shared__ int32_t spos[kSpearmanSmall];
     __shared__ double s_tmp[NW];
     __shared__ double s_hi[NW][3], s_lo[NW][3];
+    __shared__ double s_m[kSpearmanSmall / 2];
     const int tid = threadIdx.x;
     const int n = int(*d_n);
     int np2 = 1;
@@ -1602,7 +1610,7 @@ __global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__r
     spearman_block<BS>(sv, spos, 0, n, s_tmp, rho, pv);
     const int64_t per = (int64_t(n) + BS - 1) / BS;
     const int64_t k0 = int64_t(tid) * per, k1 = k0 + per < n ? k0 + per : n;
-    shapiro_block<BS>(sv, x, 0, n, k0, k1, s_hi, s_lo, w, wp);
+    shapiro_block<BS>(sv, x, 0, n, k0, k1, s_hi, s_lo, s_m, w, wp);
 }
 
 bool series_small_ok(int64_t n_cap) { return n_cap <= kSpearmanSmall; }

@@ -135,6 +135,14 @@ FZ_HD inline double sw_a(const SwCoef &c, int64_t k) {
     return -sw_m(k, c.n) / c.fac;
 }
 
+// sw_a from a precomputed normal score m = sw_m(k, n) (the same arithmetic, no ppnd call).
+FZ_HD inline double sw_a_m(const SwCoef &c, int64_t k, double m) {
+    if (k == 1) return c.a1;
+    if (k == 2 && c.i1 == 3) return c.a2;
+    if (c.n == 3) return 0.0;
+    return -m / c.fac;
+}
+
 // Signed coefficient of the sample at sorted 1-based position i (mirror j = n + 1 - i).
 FZ_HD inline double sw_coef_at(const SwCoef &c, int64_t i) {
     const int64_t j = c.n + 1 - i;
