@@ -571,6 +571,11 @@ int fz_describe_f64(fz_ctx *ctx, const double *x, int64_t n, fz_describe *host_o
 /* The same into a device fz_describe (no host read: the sharded drivers copy it with their other
  * results). */
 int fz_describe_f64_dev(fz_ctx *ctx, const double *x, int64_t n, fz_describe *dev_out);
+/* Stable sort of a device fp64 vector by (value, position): val = the values ascending (NaN
+ * last), pos = their positions - the single-segment sort RQ3's statistics run over the detected u
+ * non-detected union (rq3:321-352; scipy / numpy sort the samples themselves).  val / pos device
+ * arrays of n. */
+int fz_sort_f64(fz_ctx *ctx, const double *x, int64_t n, double *val, int32_t *pos);
 /* Per-project count of total_coverage rows with coverage valid, > 0 and date < limit
  * (the GROUP BY/HAVING of rq1_detection_rate.py:144-152), on the unsorted table. */
 int fz_eligibility_count(fz_ctx *ctx, const fz_tables *t, int64_t date_limit, int32_t *counts);

@@ -27,6 +27,59 @@ def test_radix_sort_stable(engine, n, bits, seed):
     assert np.array_equal(dv.cpu().numpy().view(np.uint32), v[order])
 
 
+def _f64_keys(x):
+    u = x.view(np.uint64)
+    return np.where(u >> np.uint64(63) != 0, ~u, u | np.uint64(1 << 63))
+
+
+def _sort_input(kind, n, rng):
+    if kind == "rq3like":  # percentage-point changes: zeros, ties, rounding noise around them
+        a = np.where(rng.random(n) < 0.4, 0.0, (rng.integers(0, 400, n) + 1) / rng.integers(300, 2000, n) * 100.0)
+        return np.where(rng.random(n) < 0.5, -a, a) + np.where(rng.random(n) < 0.1, 1e-15, 0.0)
+    if kind == "normal":
+        return np.round(rng.normal(0, 3, size=n), 2)
+    if kind == "allsame":
+        return np.full(n, 2.5)
+    if kind == "sorted":
+        return np.sort(rng.normal(size=n))
+    if kind == "reverse":
+        return np.sort(rng.normal(size=n))[::-1].copy()
+    if kind == "special":  # NaN last, -0.0 before +0.0, infinities at the ends
+        a = rng.normal(size=n)
+        k = rng.integers(0, 6, size=n)
+        a[k == 0] = np.nan
+        a[k == 1] = -0.0
+        a[k == 2] = 0.0
+        a[k == 3] = np.inf
+        a[k == 4] = -np.inf
+        return a
+    if kind in ("cluster", "cluster_tied"):  # the strided samples spread, everything else in one range
+        # bucket far past the LDS capacity: the run / merge path
+        a = 0.5 + np.arange(n) * 1e-12 if kind == "cluster" else np.full(n, 0.5)
+        sp = (np.arange(4096, dtype=np.int64) * n) // 4096
+        a[sp] = rng.uniform(-1e6, 1e6, size=len(sp))
+        return a
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind,n,seed", [
+    ("rq3like", 16_385, 0), ("rq3like", 790_000, 1), ("rq3like", 1_310_720, 2), ("rq3like", 2_000_000, 3),
+    ("normal", 100_003, 4), ("allsame", 50_000, 5), ("sorted", 300_000, 6), ("reverse", 300_000, 7),
+    ("special", 200_000, 8), ("cluster", 100_003, 9), ("cluster_tied", 60_000, 10), ("rq3like", 5, 11)])
+def test_sort_f64_stable(engine, kind, n, seed):
+    """fz_sort_f64 (the single-segment sort of RQ3's union: splitter buckets + one scatter pass +
+    LDS bucket sorts up to 1.3 M values, the LSD radix sort beyond) = numpy's stable argsort of the
+    order-preserving keys, bit for bit."""
+    torch = engine.torch
+    x = _sort_input(kind, n, np.random.default_rng(seed))
+    dx = torch.from_numpy(x).to(engine.dev)
+    val, pos = engine.sort_f64(dx)
+    engine.synchronize()
+    order = np.argsort(_f64_keys(x), kind="stable")
+    assert np.array_equal(pos.cpu().numpy(), order.astype(np.int32))
+    assert np.array_equal(val.cpu().numpy().view(np.uint64), x[order].view(np.uint64))
+
+
 def _np_describe(a):
     return dict(count=len(a), n_pos=int((a > 0).sum()), n_zero=int((a == 0).sum()), n_neg=int((a < 0).sum()),
                 mean=float(np.mean(a)), median=float(np.median(a)), std=float(np.std(a)), min=float(a.min()),

@@ -7,6 +7,7 @@
 
 #include "fz_internal.h"
 #include "fz_lookback.h"
+#include "fz_seg.h"
 #include "fz_views.h"
 
 namespace fz {
@@ -528,6 +529,23 @@ int fz_radix_sort_u64(fz_ctx *ctx, uint64_t *keys, uint32_t *vals, int64_t n, in
     return guarded(ctx, [&] {
         FZ_CHECK((keys != nullptr || n == 0) && n >= 0 && bits >= 0 && bits <= 64, "fz_radix_sort_u64: bad arguments");
         fz::radix_sort_pairs(ctx, keys, vals, n, bits);
+    });
+}
+
+int fz_sort_f64(fz_ctx *ctx, const double *x, int64_t n, double *val, int32_t *pos) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n >= 0 && n < (int64_t(1) << 31) && (n == 0 || (x && val && pos)), "fz_sort_f64: bad arguments");
+        if (n == 0) return;
+        int64_t *offs = ctx->arena.get<int64_t>(2);
+        const int64_t h[2] = {0, n};
+        fz::set_i64(ctx, offs, h, 2);
+        fz::Segs one;
+        one.S = 1;
+        one.offs = offs;
+        one.n_cap = n;
+        const fz::SortedSegs s = fz::seg_sort_f64(ctx, x, one, nullptr);
+        fz::dev_copy(ctx, val, s.val, n * int64_t(sizeof(double)));
+        fz::dev_copy(ctx, pos, s.pos, n * int64_t(sizeof(int32_t)));
     });
 }
 

@@ -974,6 +974,385 @@ void radix_sort_rows_payload32(fz_ctx *c, const uint32_t *key_src, uint32_t *&ke
     radix_payload_impl<uint32_t>(c, keys, vals, n, bits, pl, nullptr, key_src);
 }
 
+// ----------------------------------------------------------- sample sort of one segment (fp64)
+// One segment [offs[0], offs[1]) of up to a few million doubles (RQ3's detected u non-detected
+// union: ~0.8 M values at config 2) sorted stably by (value, position) in five launches instead
+// of the LSD radix sort's eleven (keys, histogram, eight 8-bit passes, values) - each of those
+// passes a latency-bound look-back over ~200 tiles, ~15 us apart from ~10 us of launch gap:
+//  1. one workgroup sorts 4096 strided samples and takes every 32nd as a splitter (127);
+//  2. every value gets its bucket: 2i for keys strictly between splitters i-1 and i, 2i+1 for
+//     keys equal to splitter i (a heavy tie - the zeros - lands whole in an equality bucket, which
+//     needs no sort); positions before the segment get digit 255;
+//  3. one stable onesweep pass over the 8-bit bucket ids (positions implicit, the values as the
+//     payload) groups the segment by bucket, position order kept inside each bucket;
+//  4. one workgroup per bucket: an equality bucket is copied, the others sorted in LDS by an LSD
+//     radix sort over the key bytes that differ inside the bucket (stable: ties keep position
+//     order); a bucket past the LDS capacity (12 K values: sampling noise, rare at <= 6 K expected,
+//     or clustered values) as LDS-sorted runs merged by its workgroup in global memory.
+// The output is the stable sort's, element for element (val / pos defined on [offs[0], offs[1])).
+constexpr int kSsSamples = 4096;
+constexpr int kSsSplit = 127;
+constexpr int kSsBuckets = 2 * kSsSplit + 1;  // 255: bucket ids fit an 8-bit digit, 255 = outside
+constexpr int kSsBlock = 1024;
+constexpr int kSsWaves = kSsBlock / kWave;
+constexpr int kSsIpt = 12;
+constexpr int kSsMax = kSsBlock * kSsIpt;  // values one workgroup sorts in LDS
+static_assert(kSsMax <= 65536, "bucket-local indices are 16-bit");
+
+__global__ __launch_bounds__(kSsBlock) void k_ss_splitters(const double *__restrict__ src,
+                                                            const int64_t *__restrict__ offs, int64_t n_cap,
+                                                            uint64_t *__restrict__ spl,
+                                                            unsigned long long *__restrict__ counts,
+                                                            unsigned long long *__restrict__ gsum, int64_t gsum_words,
+                                                            int64_t *__restrict__ d_hi) {
+    __shared__ uint64_t s[kSsSamples];
+    const int tid = threadIdx.x;
+    const int64_t lo = offs[0] > 0 ? offs[0] : 0, hi = offs[1] < n_cap ? offs[1] : n_cap;
+    const int64_t m = hi > lo ? hi - lo : 0;
+    // (the scatter pass's digit totals and look-back group sums start from zero)
+    for (int i = tid; i < 256; i += kSsBlock) counts[i] = i == 255 ? (unsigned long long)(m > 0 ? lo : 0) : 0ull;
+    for (int64_t i = tid; i < gsum_words; i += kSsBlock) gsum[i] = 0ull;
+    for (int j = tid; j < kSsSamples; j += kSsBlock)
+        s[j] = m > 0 ? f64_key(src[lo + (int64_t(j) * m) / kSsSamples]) : ~0ull;
+    __syncthreads();
+    for (int k = 2; k <= kSsSamples; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = tid; t < kSsSamples / 2; t += kSsBlock) {
+                const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;
+                const uint64_t a = s[i], b = s[ixj];
+                if ((b < a) == ((i & k) == 0)) {
+                    s[i] = b;
+                    s[ixj] = a;
+                }
+            }
+            bitonic_stage_sync(k, j, kSsSamples);
+        }
+    if (tid < kSsSplit) spl[tid] = s[(tid + 1) * (kSsSamples / (kSsSplit + 1))];
+    if (tid == 0) *d_hi = m > 0 ? hi : 0;
+}
+
+// bucket of key k: 2p + 1 when k equals splitter p, else 2p (p = splitters below k)
+__device__ inline uint32_t ss_bucket(const uint64_t *s_spl, uint64_t k) {
+    int p = 0;
+#pragma unroll
+    for (int step = 64; step > 0; step >>= 1)
+        if (p + step <= kSsSplit && s_spl[p + step - 1] < k) p += step;
+    return (p < kSsSplit && s_spl[p] == k) ? uint32_t(2 * p + 1) : uint32_t(2 * p);
+}
+
+__global__ __launch_bounds__(kBlock) void k_ss_ids(const double *__restrict__ src, const int64_t *__restrict__ offs,
+                                                    const int64_t *__restrict__ d_hi, const uint64_t *__restrict__ spl,
+                                                    uint32_t *__restrict__ ids, unsigned long long *__restrict__ counts) {
+    __shared__ uint64_t s_spl[kSsSplit];
+    __shared__ uint32_t s_h[256];
+    for (int i = threadIdx.x; i < kSsSplit; i += kBlock) s_spl[i] = spl[i];
+    for (int i = threadIdx.x; i < 256; i += kBlock) s_h[i] = 0u;
+    __syncthreads();
+    const int64_t lo = offs[0] > 0 ? offs[0] : 0, hi = *d_hi;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i - threadIdx.x < hi;
+         i += int64_t(gridDim.x) * kBlock) {
+        const bool valid = i < hi;
+        const bool in = valid && i >= lo;
+        const uint32_t b = in ? ss_bucket(s_spl, f64_key(src[i])) : 255u;
+        if (valid) ids[i] = b;
+        // (counted in LDS; a wave of one bucket - a run of tied values - adds once)
+        const uint32_t b0 = __shfl(b, 0, 64);
+        const uint64_t act = __ballot(in);
+        if (__ballot(in && b == b0) == act) {
+            if (lane_id() == 0 && act) atomicAdd(&s_h[b0], uint32_t(__popcll(act)));
+        } else if (in) {
+            atomicAdd(&s_h[b], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSsBuckets; i += kBlock)
+        if (s_h[i]) atomicAdd(&counts[i], (unsigned long long)s_h[i]);
+}
+
+// LDS workspace of one bucket sort: keys exchanged as two 32-bit halves
+struct SsShared {
+    uint32_t x[kSsMax];
+    uint16_t ix[kSsMax];
+    uint32_t wcnt[kSsWaves][256];
+    uint32_t start[256];
+    uint32_t tmp[kSsWaves];
+    uint64_t orw[kSsWaves];
+};
+
+// Stable LSD radix sort of n <= kSsMax (key, index) pairs held in registers, element
+// q = wave * 1024 + round * 64 + lane; only the key bytes that differ among the pairs are passes.
+__device__ inline void ss_lds_sort(uint64_t (&k)[kSsIpt], uint16_t (&ix)[kSsIpt], int n, uint64_t kref, SsShared &sh) {
+    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
+    const int wbase = w * (kSsMax / kSsWaves);
+    // the bytes that vary: OR of (key ^ kref), kref = one of the keys (the first)
+    uint64_t dif = 0;
+#pragma unroll
+    for (int r = 0; r < kSsIpt; ++r)
+        if (wbase + r * kWave + lane < n) dif |= k[r] ^ kref;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dif |= __shfl_xor(dif, off, 64);
+    if (lane == 0) sh.orw[w] = dif;
+    __syncthreads();
+    dif = 0;
+#pragma unroll
+    for (int i = 0; i < kSsWaves; ++i) dif |= sh.orw[i];
+    for (int byte = 0; byte < 8; ++byte) {
+        if (!((dif >> (8 * byte)) & 0xffull)) continue;
+        const int shift = 8 * byte;
+        for (int i = tid; i < kSsWaves * 256; i += kSsBlock) (&sh.wcnt[0][0])[i] = 0u;
+        __syncthreads();
+        uint32_t *cnt_w = sh.wcnt[w];
+        uint32_t dst[kSsIpt];
+#pragma unroll
+        for (int r = 0; r < kSsIpt; ++r) {
+            const bool valid = wbase + r * kWave + lane < n;
+            const uint32_t d = uint32_t(k[r] >> shift) & 255u;
+            const uint64_t peers = match_digit<8>(d, valid);
+            const uint32_t before = valid ? cnt_w[d] : 0u;  // all lanes read before the leader writes
+            dst[r] = before + uint32_t(__popcll(peers & lanemask_lt()));
+            if (valid && (__ffsll((long long)peers) - 1) == lane) cnt_w[d] = before + uint32_t(__popcll(peers));
+        }
+        __syncthreads();
+        uint32_t tot = 0;
+        if (tid < 256)
+            for (int i = 0; i < kSsWaves; ++i) {
+                const uint32_t x = sh.wcnt[i][tid];
+                sh.wcnt[i][tid] = tot;
+                tot += x;
+            }
+        const uint32_t st = block_excl_scan<uint32_t, kSsWaves>(tot, sh.tmp, (uint32_t *)nullptr);
+        if (tid < 256) sh.start[tid] = st;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kSsIpt; ++r) {
+            if (wbase + r * kWave + lane < n) {
+                const uint32_t d = uint32_t(k[r] >> shift) & 255u;
+                dst[r] += sh.start[d] + cnt_w[d];
+                sh.x[dst[r]] = uint32_t(k[r] >> 32);
+                sh.ix[dst[r]] = ix[r];
+            }
+        }
+        __syncthreads();
+        // (the high words land in k's high halves at once: the low halves still go out from k)
+#pragma unroll
+        for (int r = 0; r < kSsIpt; ++r) {
+            const int q = wbase + r * kWave + lane;
+            if (q < n) {
+                k[r] = (uint64_t(sh.x[q]) << 32) | (k[r] & 0xffffffffull);
+                ix[r] = sh.ix[q];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kSsIpt; ++r)
+            if (wbase + r * kWave + lane < n) sh.x[dst[r]] = uint32_t(k[r]);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kSsIpt; ++r) {
+            const int q = wbase + r * kWave + lane;
+            if (q < n) k[r] = (k[r] & 0xffffffff00000000ull) | sh.x[q];
+        }
+        __syncthreads();
+    }
+    __syncthreads();  // (no pass: sh.orw is read; the next call writes it)
+}
+
+// Bucket b's start in bucket order and its length (every thread; wave-uniform values).
+__device__ inline void ss_bucket_range(const unsigned long long *__restrict__ counts, int b, int64_t &base,
+                                       int64_t &len) {
+    __shared__ int64_t s_t64[kSsWaves];
+    __shared__ int64_t s_base, s_len;
+    const int tid = threadIdx.x;
+    const int64_t cnt = tid < kSsBuckets ? int64_t(counts[tid]) : 0;
+    const int64_t st = block_excl_scan<int64_t, kSsWaves>(cnt, s_t64, (int64_t *)nullptr);
+    if (tid == b) {
+        s_base = st;
+        s_len = cnt;
+    }
+    __syncthreads();
+    auto uni = [](int64_t x) {  // (scalar registers for the bounds and the pointers made from them)
+        const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(x)),
+                       h = __builtin_amdgcn_readfirstlane(uint32_t(uint64_t(x) >> 32));
+        return int64_t((uint64_t(h) << 32) | l);
+    };
+    base = uni(s_base);
+    len = uni(s_len);
+}
+
+// One workgroup per bucket (bucketed values vin / absolute positions pin, in bucket order): an
+// equality bucket copied, a range bucket of <= kSsMax values sorted in LDS; longer ones are left
+// to k_ss_runs.
+__global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long long *__restrict__ counts,
+                                                          const int64_t *__restrict__ offs,
+                                                          const double *__restrict__ vin, const uint32_t *__restrict__ pin,
+                                                          double *__restrict__ val, int32_t *__restrict__ pos) {
+    __shared__ SsShared sh;
+    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
+    const int b = blockIdx.x;
+    int64_t base, len;
+    ss_bucket_range(counts, b, base, len);
+    const bool eq = (b & 1) || len == 1;  // equality bucket: every key the same, in position order
+    if (len == 0 || (!eq && len > kSsMax)) return;
+    const int64_t lo = offs[0] > 0 ? offs[0] : 0;
+    double *ov = val + lo + base;
+    int32_t *op = pos + lo + base;
+    if (eq) {
+        for (int64_t q = tid; q < len; q += kSsBlock) {
+            ov[q] = vin[base + q];
+            op[q] = int32_t(pin[base + q]);
+        }
+        return;
+    }
+    const int wbase = w * (kSsMax / kSsWaves);
+    const int n = int(len);
+    uint64_t k[kSsIpt];
+    uint16_t ix[kSsIpt];
+#pragma unroll
+    for (int r = 0; r < kSsIpt; ++r) {
+        const int q = wbase + r * kWave + lane;
+        k[r] = q < n ? f64_key(vin[base + q]) : 0ull;
+        ix[r] = uint16_t(q);
+    }
+    ss_lds_sort(k, ix, n, f64_key(vin[base]), sh);
+#pragma unroll
+    for (int r = 0; r < kSsIpt; ++r) {
+        const int q = wbase + r * kWave + lane;
+        if (q < n) {
+            ov[q] = f64_from_key(k[r]);
+            op[q] = int32_t(pin[base + ix[r]]);
+        }
+    }
+}
+
+// A range bucket past the LDS capacity (sampling noise; clustered values): runs of kSsMax values
+// sorted in LDS into (ka, ia), then merged pairwise by the workgroup - a merge path per thread,
+// ties from the left run first (stable).  Every other bucket's workgroup leaves at once.
+__global__ __launch_bounds__(kSsBlock) void k_ss_runs(const unsigned long long *__restrict__ counts,
+                                                       const int64_t *__restrict__ offs,
+                                                       const double *__restrict__ vin, const uint32_t *__restrict__ pin,
+                                                       uint64_t *__restrict__ ka, uint32_t *__restrict__ ia,
+                                                       uint64_t *__restrict__ kb, uint32_t *__restrict__ ib,
+                                                       double *__restrict__ val, int32_t *__restrict__ pos) {
+    __shared__ SsShared sh;
+    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
+    const int b = blockIdx.x;
+    int64_t base, len;
+    ss_bucket_range(counts, b, base, len);
+    if ((b & 1) || len <= kSsMax) return;
+    const int64_t lo = offs[0] > 0 ? offs[0] : 0;
+    double *ov = val + lo + base;
+    int32_t *op = pos + lo + base;
+    const int wbase = w * (kSsMax / kSsWaves);
+    uint64_t *ks = ka + base, *kd = kb + base;
+    uint32_t *is = ia + base, *id = ib + base;
+    for (int64_t c0 = 0; c0 < len; c0 += kSsMax) {
+        const int n = int(len - c0 < kSsMax ? len - c0 : kSsMax);
+        uint64_t k[kSsIpt];
+        uint16_t ix[kSsIpt];
+#pragma unroll
+        for (int r = 0; r < kSsIpt; ++r) {
+            const int q = wbase + r * kWave + lane;
+            k[r] = q < n ? f64_key(vin[base + c0 + q]) : 0ull;
+            ix[r] = uint16_t(q);
+        }
+        ss_lds_sort(k, ix, n, f64_key(vin[base + c0]), sh);
+#pragma unroll
+        for (int r = 0; r < kSsIpt; ++r) {
+            const int q = wbase + r * kWave + lane;
+            if (q < n) {
+                ks[c0 + q] = k[r];
+                is[c0 + q] = uint32_t(c0) + ix[r];
+            }
+        }
+    }
+    __syncthreads();
+    for (int64_t width = kSsMax; width < len; width <<= 1) {
+        for (int64_t s0 = 0; s0 < len; s0 += 2 * width) {
+            const int64_t a1 = s0 + width < len ? s0 + width : len, b1 = s0 + 2 * width < len ? s0 + 2 * width : len;
+            const int64_t na = a1 - s0, nb = b1 - a1, tot = na + nb;
+            const uint64_t *A = ks + s0, *B = ks + a1;
+            const int64_t per = (tot + kSsBlock - 1) / kSsBlock;
+            const int64_t d0 = int64_t(tid) * per;
+            if (d0 >= tot) continue;
+            const int64_t d1 = d0 + per < tot ? d0 + per : tot;
+            int64_t l = d0 - nb > 0 ? d0 - nb : 0, h = d0 < na ? d0 : na;
+            while (l < h) {  // A elements among the first d0 outputs
+                const int64_t mid = (l + h) >> 1;
+                if (A[mid] <= B[d0 - mid - 1]) l = mid + 1;
+                else h = mid;
+            }
+            int64_t i = l, j = d0 - l;
+            for (int64_t d = d0; d < d1; ++d) {
+                const bool ta = j >= nb || (i < na && A[i] <= B[j]);
+                kd[s0 + d] = ta ? A[i] : B[j];
+                id[s0 + d] = ta ? is[s0 + i] : is[a1 + j];
+                if (ta) ++i;
+                else ++j;
+            }
+        }
+        __syncthreads();
+        uint64_t *tk = ks;
+        ks = kd;
+        kd = tk;
+        uint32_t *ti = is;
+        is = id;
+        id = ti;
+    }
+    for (int64_t q = tid; q < len; q += kSsBlock) {
+        ov[q] = f64_from_key(ks[q]);
+        op[q] = int32_t(pin[base + is[q]]);
+    }
+}
+
+bool sample_sort_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("FZ_SAMPLE_SORT");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
+void sample_sort_f64_seg1(fz_ctx *c, const double *src, const int64_t *offs, int64_t n_cap, double *val,
+                          int32_t *pos) {
+    FZ_CHECK(n_cap > 0 && n_cap < (int64_t(1) << 31), "sample_sort_f64_seg1: 1 .. 2^31 - 1 positions");
+    uint64_t *spl = c->arena.get<uint64_t>(kSsSplit + 1);
+    unsigned long long *counts = c->arena.get<unsigned long long>(256);
+    int64_t *d_hi = c->arena.get<int64_t>(1);
+    uint32_t *ids = c->arena.get<uint32_t>(n_cap);
+    uint32_t *kout = c->arena.get<uint32_t>(n_cap);
+    uint32_t *pin = c->arena.get<uint32_t>(n_cap);
+    double *vin = c->arena.get<double>(n_cap);
+    uint64_t *ka = c->arena.get<uint64_t>(n_cap), *kb = c->arena.get<uint64_t>(n_cap);
+    uint32_t *ia = c->arena.get<uint32_t>(n_cap), *ib = c->arena.get<uint32_t>(n_cap);
+    const int64_t nb = (n_cap + kSortTile - 1) / kSortTile;
+    const int64_t gwords = ((nb + kOsGroup - 1) / kOsGroup) * kRadix;
+    unsigned long long *gsum = c->arena.get<unsigned long long>(gwords);
+    k_ss_splitters<<<1, kSsBlock, 0, c->stream>>>(src, offs, n_cap, spl, counts, gsum, gwords, d_hi);
+    k_ss_ids<<<grid_for(n_cap, kBlock, 2048), kBlock, 0, c->stream>>>(src, offs, d_hi, spl, ids, counts);
+    FZ_LAUNCH_CHECK();
+    const Lookback lb = lookback_begin(c, nb * kRadix);
+    RadixPayload pl;
+    pl.n = 1;
+    pl.in[0] = src;
+    pl.size[0] = 8;
+    pl.out[0] = vin;
+    {
+        // algorithmic traffic: bucket id 4 + value 8 read, bucket id 4 + position 4 + value 8 written
+        ProbeScope ps(c, "radix_scatter", 0.0, d_hi, 28.0);
+        k_onesweep<uint32_t, true, true, kSortTile, kOsBlock><<<unsigned(nb), kOsBlock, 0, c->stream>>>(
+            ids, nullptr, kout, pin, n_cap, 0, counts, lb.status, lb.ticket, lb.epoch, gsum, nullptr, pl, d_hi);
+        FZ_LAUNCH_CHECK();
+    }
+    lookback_end(c, nb);
+    {
+        // algorithmic traffic per value: value 8 + position 4 read, value 8 + position 4 written
+        ProbeScope ps(c, "seg_sample_sort", 0.0, d_hi, 24.0);
+        k_ss_buckets<<<kSsBuckets, kSsBlock, 0, c->stream>>>(counts, offs, vin, pin, val, pos);
+        k_ss_runs<<<kSsBuckets, kSsBlock, 0, c->stream>>>(counts, offs, vin, pin, ka, ia, kb, ib, val, pos);
+        FZ_LAUNCH_CHECK();
+    }
+}
+
 // ------------------------------------------------------------------------------- min / max
 // min / max over non-NULL values of up to kMinMaxCols columns in one launch (blockIdx.y = column)
 constexpr int kMinMaxCols = 8;

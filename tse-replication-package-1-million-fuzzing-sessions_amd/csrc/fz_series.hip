@@ -581,12 +581,22 @@ __global__ __launch_bounds__(kBlock) void k_f64_from_keys(const uint64_t *__rest
     }
 }
 
+// (the sample sort's range buckets average 1/128 of the live values - 10 K at 1.3 M, against its
+// LDS capacity of 12 K; a longer bucket takes the slower in-workgroup merge; config 2: 1.01 M
+// capacity, ~0.8 M live)
+constexpr int64_t kSampleSortMax = int64_t(5) << 18;
 SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int32_t *) {
     const int64_t n = sg.n_cap;
     SortedSegs out;
     out.val = c->arena.get<double>(n);
     out.pos = c->arena.get<int32_t>(n);
     if (n <= 0 || sg.S <= 0) return out;
+    if (sg.S == 1 && sg.len_bound() > 16384 && n <= kSampleSortMax && sample_sort_on()) {
+        // one long segment of up to 1.3 M values (RQ3's union): splitter buckets, one scatter pass
+        // and an LDS sort per bucket - five launches (fz_prims.hip sample_sort_f64_seg1)
+        sample_sort_f64_seg1(c, src, sg.offs, n, out.val, out.pos);
+        return out;
+    }
     if (sg.S == 1 && sg.len_bound() > 16384 && n < (int64_t(1) << 22)) {
         // one long segment (RQ3's detected u non-detected union, a long series): the LSD radix sort
         // (8 passes at HBM rate, stable: ties keep position order, as the merge sort keeps them)

@@ -185,6 +185,7 @@ SIGNATURES = {
     "fz_graph_launch": (C.c_int, [_P, _P]),
     "fz_graph_destroy": (C.c_int, [_P]),
     "fz_radix_sort_u64": (C.c_int, [_P, _P, _P, _I64, C.c_int]),
+    "fz_sort_f64": (C.c_int, [_P, _P, _I64, _P, _P]),
     "fz_describe_f64": (C.c_int, [_P, _P, _I64, C.POINTER(FzDescribe)]),
     "fz_eligibility_count": (C.c_int, [_P, C.POINTER(FzTables), _I64, _P]),
 }
@@ -452,6 +453,15 @@ class Engine:
         n = keys.numel()
         _check(self.lib, self.lib.fz_radix_sort_u64(self.ctx, _P(keys.data_ptr()),
                                                    _P(vals.data_ptr()) if vals is not None else None, n, bits))
+
+    def sort_f64(self, x):
+        """Stable sort of a device float64 vector: (values ascending, int32 positions)."""
+        n = x.numel()
+        val = self.torch.empty(max(n, 1), dtype=self.torch.float64, device=self.dev)
+        pos = self.torch.empty(max(n, 1), dtype=self.torch.int32, device=self.dev)
+        _check(self.lib, self.lib.fz_sort_f64(self.ctx, _P(x.data_ptr()) if n else None, n,
+                                              _P(val.data_ptr()), _P(pos.data_ptr())))
+        return val[:n], pos[:n]
 
     def probe_begin(self, kernel: str):
         _check(self.lib, self.lib.fz_probe_begin(self.ctx, kernel.encode()))

@@ -146,7 +146,11 @@ def take_shard(t: Tables, lo: int, hi: int) -> Tuple[Tables, ShardRows]:
 # rq1:144-152) and enters no analysis, while the rank's store still holds and sorts them: the
 # store's work follows the rows, the analyses' stay with the owner.  The owner keeps the giant's
 # builds, issues, every coverage row before the bound and the delta window; the movable rows are
-# spread over the ranks in date order to even out their row counts.
+# spread over the ranks in date order to even out their row counts - the owner's share first, the
+# earliest ones: its rows of the giant stay one run of dates.  (A gap in a segment's dates - the
+# owner's pre-bound rows and a far-off movable range - packs most of the segment into a few of
+# the store's time sub-buckets, which overflow into the merge sort: config 5's owner at eight
+# ranks took 6.4 ms against 4.3-4.7 for the others.)
 SPLIT_BOUND_US = int(max(LIMIT_US, RQ3_LIMIT_US))
 DELTA_WINDOW = 7
 
@@ -212,7 +216,8 @@ def split_plan(t: Tables, world: int) -> SplitPlan:
     out_of = {}
     for p, m in movable.items():
         owner = next(r for r, (a, b) in enumerate(bounds) if a <= p < b)
-        k = 0
+        k = min(len(m), max(0, target - int(load[owner])))  # the owner's share: the earliest rows
+        load[owner] += k
         while k < len(m):
             # the least-loaded rank takes the next date range, up to the mean share
             r = int(np.argmin(load))
