@@ -68,7 +68,7 @@ namespace {
 // stale sizes).
 uint64_t ctx_signature(fz_ctx *c) {
     uint64_t h = fz::store_of(c).signature();
-    for (const fz::DevBuf *d : {&c->os_status, &c->os_ticket, &c->os_hist})
+    for (const fz::DevBuf *d : {&c->os_status, &c->os_ticket, &c->os_hist, &c->seg_tickets})
         h = (h ^ (reinterpret_cast<uintptr_t>(d->ptr) + 0x9e3779b97f4a7c15ull * d->gen)) * 1099511628211ull;
     return h;
 }

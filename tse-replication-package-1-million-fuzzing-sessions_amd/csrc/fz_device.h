@@ -26,6 +26,13 @@ __device__ inline void bitonic_stage_sync(int k, int j, int np2) {
         __syncthreads();
 }
 
+// A write-through (sc1) 8-byte store: another workgroup may read it after a ticket / flag hand-off
+// (the storing wave drains its stores before the ticket add, the reader acquires after it).
+__device__ inline void store_wt(double *p, double x) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), __builtin_bit_cast(unsigned long long, x),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <typename T>
 __device__ inline T wave_incl_scan(T x) {
     const int lane = lane_id();

@@ -244,6 +244,9 @@ struct fz_ctx {
     // radix digit totals, two buffers used by alternate sorts: each sort's passes zero the other
     // one, so the next sort's histogram starts from zero without a memset launch
     fz::DevBuf os_hist;            // uint64 [2][kOsMaxPasses * 256]
+    // per-segment arrival tickets of the chunked reductions whose last chunk folds its segment
+    // (fz_seg.h seg_reduce): zero between launches - each segment's last arriver resets its word
+    fz::DevBuf seg_tickets;        // uint32 [segments]
     int os_hist_cur = -1;          // buffer of the next sort (-1: not allocated / not known zero)
     // HIP graph recording (fz_capture_begin/end): a context on the null stream records on a
     // private stream; the context's own stream is restored when the recording ends
@@ -380,6 +383,11 @@ void radix_sort_pairs_payload32(fz_ctx *c, uint32_t *&keys, uint32_t *&vals, int
 void sample_sort_f64_seg1(fz_ctx *c, const double *src, const int64_t *offs, int64_t n_cap, double *val,
                           int32_t *pos);
 bool sample_sort_on();  // FZ_SAMPLE_SORT=0: the LSD radix path instead (A/B builds of one library)
+// Reductions whose last-arriving block folds the partials (one launch fewer each): FZ_FUSED_FOLD=0
+// runs the separate fold kernels instead.  seg_tickets: the context's zeroed per-segment ticket
+// words (each fold resets its own), or null while a graph is recorded and they would have to grow.
+bool fused_fold_on();
+unsigned *seg_tickets(fz_ctx *c, int64_t S);
 void radix_sort_rows_payload32(fz_ctx *c, const uint32_t *key_src, uint32_t *&keys, uint32_t *&vals, int64_t n,
                                int bits, RadixPayload &pl);
 // min/max over int64 values skipping FZ_TS_NULL: writes {min, max} to host array.

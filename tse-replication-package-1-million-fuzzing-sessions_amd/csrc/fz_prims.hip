@@ -1438,9 +1438,33 @@ __global__ __launch_bounds__(kBlock) void k_f64_keys(const double *__restrict__ 
 
 // Double-double partial sums of x (pass 1) or of (x - mean)^2 (pass 2, mean read from device);
 // blockIdx.y = job, partials of job j at part[2 * gridDim.x * j ...].
-__global__ __launch_bounds__(kBlock) void k_dd_partial(SortedDescArgs a, const double *__restrict__ ms,
-                                                       double *__restrict__ part) {
+// Job j's partial sums -> ms[2 * j + mode] (mode 0: mean; mode 1: sqrt(sum / n) = std, ddof 0):
+// the per-block partials summed by one block, in block order - by k_dd_final, or (tickets) by the
+// block that arrives last, stores write-through + one agent-scope ticket add per block.
+__device__ inline void dd_final_block(const double *pj, int nparts, int64_t n, int mode, double *ms_slot) {
     __shared__ double s_hi[4], s_lo[4];
+    DD acc{0.0, 0.0};
+    for (int i = threadIdx.x; i < nparts; i += kBlock) acc = dd_add(acc, DD{pj[2 * i], pj[2 * i + 1]});
+    acc = wave_dd_sum(acc);
+    if (lane_id() == 0) {
+        s_hi[wave_id()] = acc.hi;
+        s_lo[wave_id()] = acc.lo;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        DD t{s_hi[0], s_lo[0]};
+        for (int i = 1; i < 4; ++i) t = dd_add(t, DD{s_hi[i], s_lo[i]});
+        const double s = t.hi + t.lo;
+        const double q = n > 0 ? s / double(n) : NAN;
+        *ms_slot = mode == 0 ? q : sqrt(q);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_dd_partial(SortedDescArgs a, const double *__restrict__ ms,
+                                                       double *__restrict__ part, unsigned *tickets = nullptr,
+                                                       int mode = 0, double *ms_out = nullptr) {
+    __shared__ double s_hi[4], s_lo[4];
+    __shared__ int s_last;
     const int j = blockIdx.y;
     const double *__restrict__ x = a.x[j];
     const int64_t n = *a.d_n[j];
@@ -1460,38 +1484,36 @@ __global__ __launch_bounds__(kBlock) void k_dd_partial(SortedDescArgs a, const d
         s_lo[wave_id()] = acc.lo;
     }
     __syncthreads();
+    double *pj = part + 2 * int64_t(gridDim.x) * j;
     if (threadIdx.x == 0) {
         DD t{s_hi[0], s_lo[0]};
         for (int i = 1; i < 4; ++i) t = dd_add(t, DD{s_hi[i], s_lo[i]});
-        double *pj = part + 2 * int64_t(gridDim.x) * j;
-        pj[2 * blockIdx.x] = t.hi;
-        pj[2 * blockIdx.x + 1] = t.lo;
+        if (tickets) {
+            store_wt(&pj[2 * blockIdx.x], t.hi);
+            store_wt(&pj[2 * blockIdx.x + 1], t.lo);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned old = __hip_atomic_fetch_add(&tickets[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = old == gridDim.x - 1;
+            if (s_last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&tickets[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else {
+            pj[2 * blockIdx.x] = t.hi;
+            pj[2 * blockIdx.x + 1] = t.lo;
+        }
     }
+    if (!tickets) return;
+    __syncthreads();
+    if (s_last) dd_final_block(pj, int(gridDim.x), n, mode, ms_out + 2 * j + mode);
 }
 
-// Reduce job blockIdx.x's partials; writes sum/n to ms[2 * job + mode] (mode 0: mean; mode 1:
-// sqrt(sum/n) = std, ddof 0).
+// Reduce job blockIdx.x's partials into ms[2 * job + mode].
 __global__ __launch_bounds__(kBlock) void k_dd_final(const double *__restrict__ part, int nparts, SortedDescArgs a,
                                                      int mode, double *__restrict__ ms) {
-    __shared__ double s_hi[4], s_lo[4];
     const int j = blockIdx.x;
-    const int64_t n = *a.d_n[j];
-    const double *pj = part + 2 * int64_t(nparts) * j;
-    DD acc{0.0, 0.0};
-    for (int i = threadIdx.x; i < nparts; i += kBlock) acc = dd_add(acc, DD{pj[2 * i], pj[2 * i + 1]});
-    acc = wave_dd_sum(acc);
-    if (lane_id() == 0) {
-        s_hi[wave_id()] = acc.hi;
-        s_lo[wave_id()] = acc.lo;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        DD t{s_hi[0], s_lo[0]};
-        for (int i = 1; i < 4; ++i) t = dd_add(t, DD{s_hi[i], s_lo[i]});
-        const double s = t.hi + t.lo;
-        const double q = n > 0 ? s / double(n) : NAN;
-        ms[2 * j + mode] = mode == 0 ? q : sqrt(q);
-    }
+    dd_final_block(part + 2 * int64_t(nparts) * j, nparts, *a.d_n[j], mode, ms + 2 * j + mode);
 }
 
 __device__ inline int64_t lower_bound_u64(const uint64_t *a, int64_t n, uint64_t v) {
@@ -2160,10 +2182,17 @@ void describe_sorted_dn_batch(fz_ctx *c, const SortedDescJob *jobs, int njobs) {
     double *part = c->arena.get<double>(2 * int64_t(g) * njobs);
     double *ms = c->arena.get<double>(2 * njobs);
     const dim3 gp(g, unsigned(njobs));
-    k_dd_partial<<<gp, kBlock, 0, c->stream>>>(a, nullptr, part);
-    k_dd_final<<<njobs, kBlock, 0, c->stream>>>(part, int(g), a, 0, ms);
-    k_dd_partial<<<gp, kBlock, 0, c->stream>>>(a, ms, part);
-    k_dd_final<<<njobs, kBlock, 0, c->stream>>>(part, int(g), a, 1, ms);
+    // (the last block of each job folds its partials: no k_dd_final launches)
+    unsigned *tk = fused_fold_on() && g <= 1024 ? seg_tickets(c, njobs) : nullptr;
+    if (tk) {
+        k_dd_partial<<<gp, kBlock, 0, c->stream>>>(a, nullptr, part, tk, 0, ms);
+        k_dd_partial<<<gp, kBlock, 0, c->stream>>>(a, ms, part, tk, 1, ms);
+    } else {
+        k_dd_partial<<<gp, kBlock, 0, c->stream>>>(a, nullptr, part);
+        k_dd_final<<<njobs, kBlock, 0, c->stream>>>(part, int(g), a, 0, ms);
+        k_dd_partial<<<gp, kBlock, 0, c->stream>>>(a, ms, part);
+        k_dd_final<<<njobs, kBlock, 0, c->stream>>>(part, int(g), a, 1, ms);
+    }
     k_describe_finish<<<njobs, 64, 0, c->stream>>>(a, ms);
     FZ_LAUNCH_CHECK();
 }

@@ -144,6 +144,7 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     const fz_rq3_out out = *o;
     const int32_t *iperm = s.iperm;  // sorted positions -> the caller's issue row ids
     auto detected = [=] __device__(int64_t j) -> bool {
+        if (j == 0) counts[FZ_RQ3_ISSUES] = *d_ni;  // (no issues: the zero fill stands)
         const uint32_t p = iproj[j];
         const int64_t rts = irts[j];
         const int64_t f0 = Fv.offs[p], f1 = Fv.offs[p + 1];
@@ -193,19 +194,15 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
 
     // ---- non-detected: projects with issues, except the last one (never flushed, :245-257) -
     // unless this is a shard that is not the last one (FZ_RQ3_FLUSH_LAST; the caller decides)
-    uint8_t *hasiss = c->arena.get<uint8_t>(P);
     const int64_t *ioffs = I.offs;
     const bool flush_last = flags & FZ_RQ3_FLUSH_LAST;
-    per_seg(c, P, [=] __device__(int64_t p) {
-        const int64_t n = *d_ni;
-        const uint32_t last = n > 0 ? iproj[n - 1] : 0xffffffffu;
-        hasiss[p] = (ioffs[p + 1] > ioffs[p]) && (flush_last || uint32_t(p) != last);
-    });
     // (over the live rows of TC only: *TCv.d_n of capacity NC; the kept pairs compacted in the pass)
     // (several rows per thread: their loads overlap, and fewer tiles to look back over)
     compact_emit<FZ_RQ3_NON_ITEMS>(c, NC, TCv.d_n, [=] __device__(int64_t k) -> bool {
         const uint32_t p = TCv.proj[k];
-        if (!hasiss[p] || k == TCv.offs[p]) return false;
+        const int64_t ni = *d_ni;
+        const bool hasiss = (ioffs[p + 1] > ioffs[p]) && (flush_last || ni <= 0 || p != iproj[ni - 1]);
+        if (!hasiss || k == TCv.offs[p]) return false;
         const int32_t ra = TCv.row[k - 1], rb = TCv.row[k];
         const int64_t day = fdiv_day(TCv.time[k]);
         const int64_t lo = doffs[p], hi = doffs[p + 1];
@@ -225,7 +222,6 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         out.non_cov[q] = cvd[rb] - cvd[ra];
         out.non_tot[q] = ctot[rb] - ctot[ra];
     }, counts + FZ_RQ3_NON_DETECTED);
-    map_n(c, 1, nullptr, [=] __device__(int64_t) { counts[FZ_RQ3_ISSUES] = *d_ni; });
 
     if (!(flags & FZ_RQ3_SKIP_STATS))
         rq3_stats(c, o->det_pct, o->det_tot, NI, counts + FZ_RQ3_DETECTED, o->non_pct, NC,
@@ -240,23 +236,21 @@ static void sample_tests(fz_ctx *c, const double *v, const double *cat, int64_t 
                          double *tests) {
     const Segs two{2, oseg, cap};
     const ChunkedSegs cs = chunked(c, two);
-    double *med = c->arena.get<double>(2);
-    map_n(c, 1, nullptr, [=] __device__(int64_t) {
-        for (int s = 0; s < 2; ++s) {
-            const int64_t b = oseg[s], n = oseg[s + 1] - b;
-            med[s] = n <= 0 ? NAN : ((n & 1) ? cat[b + n / 2] : (cat[b + n / 2 - 1] + cat[b + n / 2]) / 2.0);
-        }
-    });
+    // sample s's median from its sorted part of cat (computed where it is used: no launch of its own)
+    auto med = [=] __device__(int32_t s) {
+        const int64_t b = oseg[s], n = oseg[s + 1] - b;
+        return n <= 0 ? NAN : ((n & 1) ? cat[b + n / 2] : (cat[b + n / 2 - 1] + cat[b + n / 2]) / 2.0);
+    };
     double *r1 = c->arena.get<double>(4);  // [s]: sum x, sum |x - median|
     seg_reduce<2>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
         x[0] = v[i];
-        x[1] = fabs(v[i] - med[s]);
+        x[1] = fabs(v[i] - med(s));
     }, r1, 8.0);
     double *r2 = c->arena.get<double>(4);  // [s]: sum (x - mean)^2, sum (|x - median| - its mean)^2
     seg_reduce<2>(c, cs, [=] __device__(int64_t i, int32_t s, double *x) {
         const double n = double(oseg[s + 1] - oseg[s]);
         const double d = v[i] - r1[2 * s] / n;
-        const double e = fabs(v[i] - med[s]) - r1[2 * s + 1] / n;
+        const double e = fabs(v[i] - med(s)) - r1[2 * s + 1] / n;
         x[0] = d * d;
         x[1] = e * e;
     }, r2, 8.0);

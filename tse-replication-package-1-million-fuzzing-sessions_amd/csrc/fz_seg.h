@@ -71,12 +71,41 @@ void runs_merge(fz_ctx *c, const double *values, const int64_t *sizes, int64_t R
 // from the offsets - segment k / cps, piece k % cps - so no map kernels run.  With out != null
 // (cps == 1) the chunk sum is the segment result and is written straight to out.
 // Chunks [blockIdx.x, nk) step gridDim.x (nk = *cm.d_n for explicit maps, else nk_host).
+// With tickets (implicit maps, part and out both set) the chunk that completes its segment folds
+// the segment's partials itself - in k_seg_sum's order, so the same bits - instead of a k_seg_sum
+// launch: partials stored write-through and drained, then one agent-scope ticket add per chunk;
+// the last arriver's acquire, fold and ticket reset (MI355X hand-off: sc1 payload + counter).
+// (true in wave 0 of the workgroup that folded)
+template <int NV>
+__device__ inline bool chunk_arrive(unsigned *tickets, const double *part, double *out, int32_t seg, int64_t cps) {
+    if (threadIdx.x >= kWave) return false;  // wave 0 stored the partials
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned old = 0;
+    if (threadIdx.x == 0)
+        old = __hip_atomic_fetch_add(&tickets[seg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, 0, 64);
+    if (old != unsigned(cps - 1)) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int64_t c0 = int64_t(seg) * cps, c1 = c0 + cps;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        DD acc{0.0, 0.0};
+        for (int64_t k = c0 + lane_id(); k < c1; k += 64)
+            acc = dd_add(acc, DD{part[(k * NV + v) * 2], part[(k * NV + v) * 2 + 1]});
+        acc = wave_dd_sum(acc);
+        if (lane_id() == 0) out[int64_t(seg) * NV + v] = acc.hi + acc.lo;
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(&tickets[seg], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
 template <int NV, typename F>
 __global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, const int64_t *__restrict__ offs, int64_t cps,
                                                          int64_t nk_host, F f, double *__restrict__ part,
-                                                         double *__restrict__ out) {
+                                                         double *__restrict__ out, unsigned *tickets = nullptr) {
     __shared__ double s_hi[4][NV], s_lo[4][NV];
     const int64_t nk = cm.d_n ? *cm.d_n : nk_host;
+    const bool fold = tickets != nullptr;
     for (int64_t k = blockIdx.x; k < nk; k += gridDim.x) {
         int32_t seg;
         int64_t b, e;
@@ -89,11 +118,17 @@ __global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, const int6
             b = offs[seg] + (k % cps) * kChunk;
             e = b + kChunk < offs[seg + 1] ? b + kChunk : offs[seg + 1];
         }
-        if (b >= e && !out) {  // an empty chunk (past its segment's live end): zero partials, no barriers
+        if (b >= e && (!out || fold)) {  // an empty chunk (past its segment's live end): zero partials, no barriers
             if (threadIdx.x < NV) {
-                part[(k * NV + threadIdx.x) * 2] = 0.0;
-                part[(k * NV + threadIdx.x) * 2 + 1] = 0.0;
+                if (fold) {
+                    store_wt(&part[(k * NV + threadIdx.x) * 2], 0.0);
+                    store_wt(&part[(k * NV + threadIdx.x) * 2 + 1], 0.0);
+                } else {
+                    part[(k * NV + threadIdx.x) * 2] = 0.0;
+                    part[(k * NV + threadIdx.x) * 2 + 1] = 0.0;
+                }
             }
+            if (fold) chunk_arrive<NV>(tickets, part, out, seg, cps);
             continue;
         }
         // two independent double-double accumulators per value (even / odd items), added at the
@@ -137,13 +172,17 @@ __global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, const int6
             const int v = threadIdx.x;
             DD t{s_hi[0][v], s_lo[0][v]};
             for (int w = 1; w < 4; ++w) t = dd_add(t, DD{s_hi[w][v], s_lo[w][v]});
-            if (out) {
+            if (fold) {
+                store_wt(&part[(k * NV + v) * 2], t.hi);
+                store_wt(&part[(k * NV + v) * 2 + 1], t.lo);
+            } else if (out) {
                 out[int64_t(seg) * NV + v] = t.hi + t.lo;
             } else {
                 part[(k * NV + v) * 2] = t.hi;
                 part[(k * NV + v) * 2 + 1] = t.lo;
             }
         }
+        if (fold) chunk_arrive<NV>(tickets, part, out, seg, cps);
         __syncthreads();
     }
 }
@@ -247,6 +286,10 @@ ChunkedSegs chunked(fz_ctx *c, const Segs &sg);
 template <int NV>
 void seg_fold_parts(fz_ctx *c, const ChunkedSegs &cs, const double *part, double *out);
 
+// Chunks per segment up to which a chunked reduction's last chunk folds its segment (one wave,
+// a few dependent double-double adds per lane); longer ones take k_seg_fold + k_seg_sum.
+constexpr int64_t kFoldChunks = 512;
+
 // Segmented sum of NV per-element values f(i, seg, x[NV]) -> out[S][NV] (device).
 template <int NV, typename F>
 void seg_reduce(fz_ctx *c, const ChunkedSegs &cs, F f, double *out, double in_bytes = -1.0) {
@@ -271,9 +314,12 @@ void seg_reduce(fz_ctx *c, const ChunkedSegs &cs, F f, double *out, double in_by
     // a persistent grid over the chunks (a capacity-sized implicit map of a short live segment -
     // RQ3's union at config 3 - is mostly empty chunks, each a few loads)
     const unsigned g = unsigned(blocks < 8192 ? blocks : 8192);
-    k_chunk_reduce<NV, F><<<g, kBlock, 0, c->stream>>>(cs.cm, cs.sg.offs, cs.cps, blocks, f, part, nullptr);
+    // implicit maps of a few hundred chunks per segment: the last chunk folds (one launch fewer)
+    unsigned *tickets = fused_fold_on() && cs.cps > 1 && cs.cps <= kFoldChunks && !L.on ? seg_tickets(c, S) : nullptr;
+    k_chunk_reduce<NV, F><<<g, kBlock, 0, c->stream>>>(cs.cm, cs.sg.offs, cs.cps, blocks, f, part,
+                                                       tickets ? out : nullptr, tickets);
     FZ_LAUNCH_CHECK();
-    seg_fold_parts<NV>(c, cs, part, out);
+    if (!tickets) seg_fold_parts<NV>(c, cs, part, out);
 }
 
 // The fold of a chunked reduction: per-chunk double-double partials part[(k * NV + v) * 2 + {0, 1}]

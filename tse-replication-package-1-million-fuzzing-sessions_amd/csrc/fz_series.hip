@@ -142,6 +142,28 @@ ChunkedSegs chunked(fz_ctx *c, const Segs &sg) {
 
 ChunkMap make_chunks(fz_ctx *c, const Segs &sg) { return chunked(c, sg).cm; }
 
+bool fused_fold_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("FZ_FUSED_FOLD");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
+unsigned *seg_tickets(fz_ctx *c, int64_t S) {
+    // (grown rarely - the first sizes already cover the analyses' reductions - and zeroed once: a
+    // recording made after a growth stays valid, one made before it is refused at replay)
+    if (c->seg_tickets.cap < size_t(S) * sizeof(unsigned)) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        FZ_HIP(hipStreamIsCapturing(c->stream, &cap));
+        if (cap != hipStreamCaptureStatusNone) return nullptr;  // (no allocation while recording: unfused)
+        const int64_t n = S > 16384 ? S : 16384;
+        unsigned *t = c->seg_tickets.ensure<unsigned>(n);
+        dev_fill(c, t, 0, n * int64_t(sizeof(unsigned)));
+    }
+    return c->seg_tickets.as<unsigned>();
+}
+
 // Segment id of every position (positions past offs[S] get S).  A workgroup takes a chunk of
 // kIdChunk positions: one search finds the segments of its first and last position, and a position
 // searches only between those (none at all when one segment covers the chunk - long sessions);
@@ -1419,6 +1441,21 @@ __global__ __launch_bounds__(kBlock) void k_spearman_chunks(ChunkMap cm, const i
 // scipy's brunnermunzel, each one launch + the fold, instead of the tie-rank passes, the x-count
 // scan, the within-sample rank map and three segmented reductions.
 constexpr int kBmNV = 2;
+// brunnermunzel(x, y) from the union-rank sums s0 = {sum rank_c(x), sum rank_c(y)} and the squared
+// deviation sums s1 (scipy _stats_py.py brunnermunzel, alternative two-sided, t distribution)
+__device__ inline void bm_finish(int64_t nx_, int64_t ny_, const double *s0, const double *s1, double *bm_stat,
+                                 double *bm_p) {
+    const double nx = double(nx_), ny = double(ny_);
+    const double rcx = s0[0] / nx, rcy = s0[1] / ny;
+    const double Sx = s1[0] / (nx - 1.0), Sy = s1[1] / (ny - 1.0);
+    double w = nx * ny * (rcy - rcx);
+    w /= (nx + ny) * sqrt(nx * Sx + ny * Sy);
+    const double num = (nx * Sx + ny * Sy) * (nx * Sx + ny * Sy);
+    const double den = (nx * Sx) * (nx * Sx) / (nx - 1.0) + (ny * Sy) * (ny * Sy) / (ny - 1.0);
+    if (bm_stat) *bm_stat = w;
+    if (bm_p) *bm_p = 2.0 * stats::t_sf(fabs(w), num / den);
+}
+
 template <int PASS>
 __global__ __launch_bounds__(kBlock) void k_bm_union_chunks(int64_t cps, const int64_t *__restrict__ offs,
                                                             const double *__restrict__ sv,
@@ -1426,8 +1463,10 @@ __global__ __launch_bounds__(kBlock) void k_bm_union_chunks(int64_t cps, const i
                                                             const int64_t *__restrict__ before,
                                                             const int64_t *__restrict__ d_nx,
                                                             const double *__restrict__ sums0,
-                                                            double *__restrict__ part) {
+                                                            double *__restrict__ part, unsigned *tickets,
+                                                            double *fold_out, double *bm_stat, double *bm_p) {
     constexpr int IPT = kRedItems;
+    const bool fold = tickets != nullptr;
     __shared__ double s_v[kChunk];
     __shared__ int64_t s_w[2][4];
     __shared__ int64_t s_edge[2];
@@ -1441,9 +1480,11 @@ __global__ __launch_bounds__(kBlock) void k_bm_union_chunks(int64_t cps, const i
         const int len = e > b ? int(e - b) : 0;
         if (len == 0) {  // past the union's live end: zero partials, no barriers
             if (tid < kBmNV) {
-                part[(k * kBmNV + tid) * 2] = 0.0;
-                part[(k * kBmNV + tid) * 2 + 1] = 0.0;
+                store_wt(&part[(k * kBmNV + tid) * 2], 0.0);
+                store_wt(&part[(k * kBmNV + tid) * 2 + 1], 0.0);
             }
+            if (fold && chunk_arrive<kBmNV>(tickets, part, fold_out, 0, cps) && PASS == 1 && tid == 0)
+                bm_finish(nx, ny, sums0, fold_out, bm_stat, bm_p);
             continue;
         }
 #pragma unroll
@@ -1535,9 +1576,11 @@ __global__ __launch_bounds__(kBlock) void k_bm_union_chunks(int64_t cps, const i
         if (tid < kBmNV) {
             DD t{s_hi[0][tid], s_lo[0][tid]};
             for (int q = 1; q < 4; ++q) t = dd_add(t, DD{s_hi[q][tid], s_lo[q][tid]});
-            part[(k * kBmNV + tid) * 2] = t.hi;
-            part[(k * kBmNV + tid) * 2 + 1] = t.lo;
+            store_wt(&part[(k * kBmNV + tid) * 2], t.hi);
+            store_wt(&part[(k * kBmNV + tid) * 2 + 1], t.lo);
         }
+        if (fold && chunk_arrive<kBmNV>(tickets, part, fold_out, 0, cps) && PASS == 1 && tid == 0)
+            bm_finish(nx, ny, sums0, fold_out, bm_stat, bm_p);
         __syncthreads();
     }
 }
@@ -1554,26 +1597,24 @@ void bm_union_sorted(fz_ctx *c, const Segs &one, const double *sorted, const int
     double *s0 = c->arena.get<double>(kBmNV), *s1 = c->arena.get<double>(kBmNV);
     const unsigned g = unsigned(cps < 8192 ? cps : 8192);
     const int64_t *offs = one.offs;
+    // (a few hundred chunks: the last chunk of each pass folds the sums - and, in the second pass,
+    // finishes the test - in place of k_seg_sum and the finishing launch)
+    unsigned *tickets = fused_fold_on() && cps <= kFoldChunks ? seg_tickets(c, 1) : nullptr;
     {
         ProbeScope ps(c, "seg_rank_union", 0.0, offs + 1, 24.0);  // value 8 + position 4 + x count 8 (+ 4) per value
-        k_bm_union_chunks<0><<<g, kBlock, 0, c->stream>>>(cps, offs, sorted, pos, before, d_nx, nullptr, part);
+        k_bm_union_chunks<0><<<g, kBlock, 0, c->stream>>>(cps, offs, sorted, pos, before, d_nx, nullptr, part,
+                                                          tickets, s0, nullptr, nullptr);
         FZ_LAUNCH_CHECK();
-        seg_fold_parts<kBmNV>(c, cs, part, s0);
-        k_bm_union_chunks<1><<<g, kBlock, 0, c->stream>>>(cps, offs, sorted, pos, before, d_nx, s0, part);
+        if (!tickets) seg_fold_parts<kBmNV>(c, cs, part, s0);
+        k_bm_union_chunks<1><<<g, kBlock, 0, c->stream>>>(cps, offs, sorted, pos, before, d_nx, s0, part,
+                                                          tickets, s1, bm_stat, bm_p);
         FZ_LAUNCH_CHECK();
-        seg_fold_parts<kBmNV>(c, cs, part, s1);
+        if (!tickets) seg_fold_parts<kBmNV>(c, cs, part, s1);
     }
-    map_n(c, 1, nullptr, [=] __device__(int64_t) {  // as seg_rank_tests_sorted's finishing
-        const double nx = double(*d_nx), ny = double(offs[1] - offs[0]) - nx;
-        const double rcx = s0[0] / nx, rcy = s0[1] / ny;
-        const double Sx = s1[0] / (nx - 1.0), Sy = s1[1] / (ny - 1.0);
-        double w = nx * ny * (rcy - rcx);
-        w /= (nx + ny) * sqrt(nx * Sx + ny * Sy);
-        const double num = (nx * Sx + ny * Sy) * (nx * Sx + ny * Sy);
-        const double den = (nx * Sx) * (nx * Sx) / (nx - 1.0) + (ny * Sy) * (ny * Sy) / (ny - 1.0);
-        if (bm_stat) *bm_stat = w;
-        if (bm_p) *bm_p = 2.0 * stats::t_sf(fabs(w), num / den);
-    });
+    if (!tickets)
+        map_n(c, 1, nullptr, [=] __device__(int64_t) {  // as seg_rank_tests_sorted's finishing
+            bm_finish(*d_nx, (offs[1] - offs[0]) - *d_nx, s0, s1, bm_stat, bm_p);
+        });
 }
 
 // spearmanr(range(n), x) and shapiro(x) of one series x[0, *d_n) of at most kSpearmanSmall values
