@@ -377,9 +377,9 @@ void radix_sort_pairs_payload32(fz_ctx *c, uint32_t *&keys, uint32_t *&vals, int
 // The same sort of (key_src[i], i): the keys read from a read-only column, the values the rows'
 // positions - nothing copied beforehand.  keys / vals: two caller scratch buffers of n entries (the
 // passes ping-pong through them and one arena pair); on return they point at the sorted result.
-// Stable sort of one segment [offs[0], offs[1]) of doubles by (value, position) - splitter
-// buckets from a sorted sample, one onesweep scatter pass, an LDS sort per bucket (fz_prims.hip);
-// val / pos are written on [offs[0], offs[1]) only.  n_cap: host bound of offs[1], < 2^31.
+// Stable sort of one segment [0, offs[1]) of doubles by (value, position) - splitter buckets from
+// a sorted sample, one onesweep scatter pass, an LDS sort per bucket (fz_prims.hip).  offs[0] must
+// be 0; val / pos are written on [0, offs[1]) only.  n_cap: host bound of offs[1], < 2^31.
 void sample_sort_f64_seg1(fz_ctx *c, const double *src, const int64_t *offs, int64_t n_cap, double *val,
                           int32_t *pos);
 bool sample_sort_on();  // FZ_SAMPLE_SORT=0: the LSD radix path instead (A/B builds of one library)

@@ -975,29 +975,32 @@ void radix_sort_rows_payload32(fz_ctx *c, const uint32_t *key_src, uint32_t *&ke
 }
 
 // ----------------------------------------------------------- sample sort of one segment (fp64)
-// One segment [offs[0], offs[1]) of up to a few million doubles (RQ3's detected u non-detected
-// union: ~0.8 M values at config 2) sorted stably by (value, position) in five launches instead
-// of the LSD radix sort's eleven (keys, histogram, eight 8-bit passes, values) - each of those
-// passes a latency-bound look-back over ~200 tiles, ~15 us apart from ~10 us of launch gap:
-//  1. one workgroup sorts 4096 strided samples and takes every 32nd as a splitter (127);
+// One segment [0, offs[1]) of up to ~1.3 M doubles (RQ3's detected u non-detected union: ~0.8 M
+// values at config 2) sorted stably by (value, position) in five launches instead of the LSD radix
+// sort's eleven (keys, histogram, eight 8-bit passes, values) - each of those passes a
+// latency-bound look-back over ~200 tiles, ~15 us apart from ~10 us of launch gap:
+//  1. one workgroup sorts 2048 strided samples (a bitonic network in registers and shuffles, LDS
+//     only for the 10 stages that cross waves) and takes every 16th as a splitter (127);
 //  2. every value gets its bucket: 2i for keys strictly between splitters i-1 and i, 2i+1 for
 //     keys equal to splitter i (a heavy tie - the zeros - lands whole in an equality bucket, which
-//     needs no sort); positions before the segment get digit 255;
+//     needs no sort), and the bucket counts (one LDS add per run of equal buckets in a wave);
 //  3. one stable onesweep pass over the 8-bit bucket ids (positions implicit, the values as the
-//     payload) groups the segment by bucket, position order kept inside each bucket;
-//  4. one workgroup per bucket: an equality bucket is copied, the others sorted in LDS by an LSD
-//     radix sort over the key bytes that differ inside the bucket (stable: ties keep position
-//     order); a bucket past the LDS capacity (12 K values: sampling noise, rare at <= 6 K expected,
-//     or clustered values) as LDS-sorted runs merged by its workgroup in global memory.
-// The output is the stable sort's, element for element (val / pos defined on [offs[0], offs[1])).
-constexpr int kSsSamples = 4096;
+//     payload) writes the segment in bucket order straight into val / pos - position order kept
+//     inside each bucket, so an equality bucket is already final;
+//  4. one workgroup per range bucket sorts it in place in LDS by an LSD radix sort over the key
+//     bytes that differ inside the bucket (stable: ties keep position order); a bucket past the
+//     LDS capacity (12 K values: sampling noise, or clustered values) is sorted by k_ss_runs as
+//     LDS-sorted runs merged by its workgroup in global memory.
+// The output is the stable sort's, element for element.
+constexpr int kSsSamples = 2048;
 constexpr int kSsSplit = 127;
-constexpr int kSsBuckets = 2 * kSsSplit + 1;  // 255: bucket ids fit an 8-bit digit, 255 = outside
+constexpr int kSsBuckets = 2 * kSsSplit + 1;  // 255: bucket ids fit an 8-bit digit
 constexpr int kSsBlock = 1024;
 constexpr int kSsWaves = kSsBlock / kWave;
 constexpr int kSsIpt = 12;
 constexpr int kSsMax = kSsBlock * kSsIpt;  // values one workgroup sorts in LDS
 static_assert(kSsMax <= 65536, "bucket-local indices are 16-bit");
+static_assert(kSsSamples == 2 * kSsBlock, "two samples per thread");
 
 __global__ __launch_bounds__(kSsBlock) void k_ss_splitters(const double *__restrict__ src,
                                                             const int64_t *__restrict__ offs, int64_t n_cap,
@@ -1006,29 +1009,51 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_splitters(const double *__restr
                                                             unsigned long long *__restrict__ gsum, int64_t gsum_words,
                                                             int64_t *__restrict__ d_hi) {
     __shared__ uint64_t s[kSsSamples];
-    const int tid = threadIdx.x;
-    const int64_t lo = offs[0] > 0 ? offs[0] : 0, hi = offs[1] < n_cap ? offs[1] : n_cap;
-    const int64_t m = hi > lo ? hi - lo : 0;
+    const int tid = threadIdx.x, lane = lane_id();
+    const int64_t hi = offs[1] < n_cap ? (offs[1] > 0 ? offs[1] : 0) : n_cap;
     // (the scatter pass's digit totals and look-back group sums start from zero)
-    for (int i = tid; i < 256; i += kSsBlock) counts[i] = i == 255 ? (unsigned long long)(m > 0 ? lo : 0) : 0ull;
+    for (int i = tid; i < 256; i += kSsBlock) counts[i] = 0ull;
     for (int64_t i = tid; i < gsum_words; i += kSsBlock) gsum[i] = 0ull;
-    for (int j = tid; j < kSsSamples; j += kSsBlock)
-        s[j] = m > 0 ? f64_key(src[lo + (int64_t(j) * m) / kSsSamples]) : ~0ull;
-    __syncthreads();
-    for (int k = 2; k <= kSsSamples; k <<= 1)
+    // thread t holds samples 2t, 2t + 1 (strided positions of the segment)
+    uint64_t x[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int j = 2 * tid + h;
+        x[h] = hi > 0 ? f64_key(src[(int64_t(j) * hi) / kSsSamples]) : ~0ull;
+    }
+    // bitonic network: element e = 2t + h; stage (k, j) pairs e with e ^ j, ascending where e & k == 0
+    for (int k = 2; k <= kSsSamples; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int t = tid; t < kSsSamples / 2; t += kSsBlock) {
-                const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;
-                const uint64_t a = s[i], b = s[ixj];
-                if ((b < a) == ((i & k) == 0)) {
-                    s[i] = b;
-                    s[ixj] = a;
-                }
+            uint64_t y[2];
+            if (j == 1) {
+                y[0] = x[1];
+                y[1] = x[0];
+            } else if ((j >> 1) < kWave) {  // partner thread t ^ (j / 2): same wave
+#pragma unroll
+                for (int h = 0; h < 2; ++h) y[h] = __shfl_xor(x[h], j >> 1, 64);
+            } else {  // across waves: through LDS
+                s[2 * tid] = x[0];
+                s[2 * tid + 1] = x[1];
+                __syncthreads();
+#pragma unroll
+                for (int h = 0; h < 2; ++h) y[h] = s[(2 * tid + h) ^ j];
+                __syncthreads();
             }
-            bitonic_stage_sync(k, j, kSsSamples);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e = 2 * tid + h;
+                const bool up = (e & k) == 0, low = (e & j) == 0;
+                const uint64_t mn = x[h] < y[h] ? x[h] : y[h], mx = x[h] < y[h] ? y[h] : x[h];
+                x[h] = (low == up) ? mn : mx;
+            }
         }
+    }
+    s[2 * tid] = x[0];
+    s[2 * tid + 1] = x[1];
+    __syncthreads();
     if (tid < kSsSplit) spl[tid] = s[(tid + 1) * (kSsSamples / (kSsSplit + 1))];
-    if (tid == 0) *d_hi = m > 0 ? hi : 0;
+    if (tid == 0) *d_hi = hi;
+    (void)lane;
 }
 
 // bucket of key k: 2p + 1 when k equals splitter p, else 2p (p = splitters below k)
@@ -1040,29 +1065,24 @@ __device__ inline uint32_t ss_bucket(const uint64_t *s_spl, uint64_t k) {
     return (p < kSsSplit && s_spl[p] == k) ? uint32_t(2 * p + 1) : uint32_t(2 * p);
 }
 
-__global__ __launch_bounds__(kBlock) void k_ss_ids(const double *__restrict__ src, const int64_t *__restrict__ offs,
-                                                    const int64_t *__restrict__ d_hi, const uint64_t *__restrict__ spl,
-                                                    uint32_t *__restrict__ ids, unsigned long long *__restrict__ counts) {
+__global__ __launch_bounds__(kBlock) void k_ss_ids(const double *__restrict__ src, const int64_t *__restrict__ d_hi,
+                                                    const uint64_t *__restrict__ spl, uint32_t *__restrict__ ids,
+                                                    unsigned long long *__restrict__ counts) {
     __shared__ uint64_t s_spl[kSsSplit];
     __shared__ uint32_t s_h[256];
     for (int i = threadIdx.x; i < kSsSplit; i += kBlock) s_spl[i] = spl[i];
     for (int i = threadIdx.x; i < 256; i += kBlock) s_h[i] = 0u;
     __syncthreads();
-    const int64_t lo = offs[0] > 0 ? offs[0] : 0, hi = *d_hi;
+    const int64_t hi = *d_hi;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i - threadIdx.x < hi;
          i += int64_t(gridDim.x) * kBlock) {
         const bool valid = i < hi;
-        const bool in = valid && i >= lo;
-        const uint32_t b = in ? ss_bucket(s_spl, f64_key(src[i])) : 255u;
+        const uint32_t b = valid ? ss_bucket(s_spl, f64_key(src[i])) : 0u;
         if (valid) ids[i] = b;
-        // (counted in LDS; a wave of one bucket - a run of tied values - adds once)
-        const uint32_t b0 = __shfl(b, 0, 64);
-        const uint64_t act = __ballot(in);
-        if (__ballot(in && b == b0) == act) {
-            if (lane_id() == 0 && act) atomicAdd(&s_h[b0], uint32_t(__popcll(act)));
-        } else if (in) {
-            atomicAdd(&s_h[b], 1u);
-        }
+        // one LDS add per distinct bucket of the wave (the zeros' bucket is a third of the
+        // non-detected sample: per-lane adds to it serialised)
+        const uint64_t peers = match_digit<8>(b, valid);
+        if (valid && (__ffsll((long long)peers) - 1) == lane_id()) atomicAdd(&s_h[b], uint32_t(__popcll(peers)));
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kSsBuckets; i += kBlock)
@@ -1179,30 +1199,20 @@ __device__ inline void ss_bucket_range(const unsigned long long *__restrict__ co
     len = uni(s_len);
 }
 
-// One workgroup per bucket (bucketed values vin / absolute positions pin, in bucket order): an
-// equality bucket copied, a range bucket of <= kSsMax values sorted in LDS; longer ones are left
-// to k_ss_runs.
+// One workgroup per range bucket of <= kSsMax values, sorted in place in val / pos (bucket order
+// on entry; the bucket's positions are read before any is written).  Equality buckets are final;
+// longer range buckets are k_ss_runs'.
 __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long long *__restrict__ counts,
-                                                          const int64_t *__restrict__ offs,
-                                                          const double *__restrict__ vin, const uint32_t *__restrict__ pin,
                                                           double *__restrict__ val, int32_t *__restrict__ pos) {
     __shared__ SsShared sh;
-    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
+    const int w = wave_id(), lane = lane_id();
     const int b = blockIdx.x;
+    if (b & 1) return;  // (an equality bucket: one key, already in position order)
     int64_t base, len;
     ss_bucket_range(counts, b, base, len);
-    const bool eq = (b & 1) || len == 1;  // equality bucket: every key the same, in position order
-    if (len == 0 || (!eq && len > kSsMax)) return;
-    const int64_t lo = offs[0] > 0 ? offs[0] : 0;
-    double *ov = val + lo + base;
-    int32_t *op = pos + lo + base;
-    if (eq) {
-        for (int64_t q = tid; q < len; q += kSsBlock) {
-            ov[q] = vin[base + q];
-            op[q] = int32_t(pin[base + q]);
-        }
-        return;
-    }
+    if (len <= 1 || len > kSsMax) return;
+    double *v = val + base;
+    int32_t *ps = pos + base;
     const int wbase = w * (kSsMax / kSsWaves);
     const int n = int(len);
     uint64_t k[kSsIpt];
@@ -1210,38 +1220,44 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
 #pragma unroll
     for (int r = 0; r < kSsIpt; ++r) {
         const int q = wbase + r * kWave + lane;
-        k[r] = q < n ? f64_key(vin[base + q]) : 0ull;
+        k[r] = q < n ? f64_key(v[q]) : 0ull;
         ix[r] = uint16_t(q);
     }
-    ss_lds_sort(k, ix, n, f64_key(vin[base]), sh);
+    ss_lds_sort(k, ix, n, f64_key(v[0]), sh);
+    int32_t np[kSsIpt];
+#pragma unroll
+    for (int r = 0; r < kSsIpt; ++r) {
+        const int q = wbase + r * kWave + lane;
+        np[r] = q < n ? ps[ix[r]] : 0;
+    }
+    __syncthreads();  // every position read before any is overwritten
 #pragma unroll
     for (int r = 0; r < kSsIpt; ++r) {
         const int q = wbase + r * kWave + lane;
         if (q < n) {
-            ov[q] = f64_from_key(k[r]);
-            op[q] = int32_t(pin[base + ix[r]]);
+            v[q] = f64_from_key(k[r]);
+            ps[q] = np[r];
         }
     }
 }
 
-// A range bucket past the LDS capacity (sampling noise; clustered values): runs of kSsMax values
-// sorted in LDS into (ka, ia), then merged pairwise by the workgroup - a merge path per thread,
-// ties from the left run first (stable).  Every other bucket's workgroup leaves at once.
+// A range bucket past the LDS capacity: runs of kSsMax values sorted in LDS into (ka, ia) - keys
+// and original positions - then merged pairwise by the workgroup (a merge path per thread, ties
+// from the left run first: stable), the result written back over the bucket.  Every other
+// bucket's workgroup leaves at once.
 __global__ __launch_bounds__(kSsBlock) void k_ss_runs(const unsigned long long *__restrict__ counts,
-                                                       const int64_t *__restrict__ offs,
-                                                       const double *__restrict__ vin, const uint32_t *__restrict__ pin,
                                                        uint64_t *__restrict__ ka, uint32_t *__restrict__ ia,
                                                        uint64_t *__restrict__ kb, uint32_t *__restrict__ ib,
                                                        double *__restrict__ val, int32_t *__restrict__ pos) {
     __shared__ SsShared sh;
     const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
     const int b = blockIdx.x;
+    if (b & 1) return;
     int64_t base, len;
     ss_bucket_range(counts, b, base, len);
-    if ((b & 1) || len <= kSsMax) return;
-    const int64_t lo = offs[0] > 0 ? offs[0] : 0;
-    double *ov = val + lo + base;
-    int32_t *op = pos + lo + base;
+    if (len <= kSsMax) return;
+    double *v = val + base;
+    int32_t *ps = pos + base;
     const int wbase = w * (kSsMax / kSsWaves);
     uint64_t *ks = ka + base, *kd = kb + base;
     uint32_t *is = ia + base, *id = ib + base;
@@ -1252,16 +1268,16 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_runs(const unsigned long long *
 #pragma unroll
         for (int r = 0; r < kSsIpt; ++r) {
             const int q = wbase + r * kWave + lane;
-            k[r] = q < n ? f64_key(vin[base + c0 + q]) : 0ull;
+            k[r] = q < n ? f64_key(v[c0 + q]) : 0ull;
             ix[r] = uint16_t(q);
         }
-        ss_lds_sort(k, ix, n, f64_key(vin[base + c0]), sh);
+        ss_lds_sort(k, ix, n, f64_key(v[c0]), sh);
 #pragma unroll
         for (int r = 0; r < kSsIpt; ++r) {
             const int q = wbase + r * kWave + lane;
             if (q < n) {
                 ks[c0 + q] = k[r];
-                is[c0 + q] = uint32_t(c0) + ix[r];
+                is[c0 + q] = uint32_t(ps[c0 + ix[r]]);
             }
         }
     }
@@ -1299,8 +1315,8 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_runs(const unsigned long long *
         id = ti;
     }
     for (int64_t q = tid; q < len; q += kSsBlock) {
-        ov[q] = f64_from_key(ks[q]);
-        op[q] = int32_t(pin[base + is[q]]);
+        v[q] = f64_from_key(ks[q]);
+        ps[q] = int32_t(is[q]);
     }
 }
 
@@ -1320,35 +1336,34 @@ void sample_sort_f64_seg1(fz_ctx *c, const double *src, const int64_t *offs, int
     int64_t *d_hi = c->arena.get<int64_t>(1);
     uint32_t *ids = c->arena.get<uint32_t>(n_cap);
     uint32_t *kout = c->arena.get<uint32_t>(n_cap);
-    uint32_t *pin = c->arena.get<uint32_t>(n_cap);
-    double *vin = c->arena.get<double>(n_cap);
     uint64_t *ka = c->arena.get<uint64_t>(n_cap), *kb = c->arena.get<uint64_t>(n_cap);
     uint32_t *ia = c->arena.get<uint32_t>(n_cap), *ib = c->arena.get<uint32_t>(n_cap);
     const int64_t nb = (n_cap + kSortTile - 1) / kSortTile;
     const int64_t gwords = ((nb + kOsGroup - 1) / kOsGroup) * kRadix;
     unsigned long long *gsum = c->arena.get<unsigned long long>(gwords);
     k_ss_splitters<<<1, kSsBlock, 0, c->stream>>>(src, offs, n_cap, spl, counts, gsum, gwords, d_hi);
-    k_ss_ids<<<grid_for(n_cap, kBlock, 2048), kBlock, 0, c->stream>>>(src, offs, d_hi, spl, ids, counts);
+    k_ss_ids<<<grid_for(n_cap, kBlock, 2048), kBlock, 0, c->stream>>>(src, d_hi, spl, ids, counts);
     FZ_LAUNCH_CHECK();
     const Lookback lb = lookback_begin(c, nb * kRadix);
     RadixPayload pl;
     pl.n = 1;
     pl.in[0] = src;
     pl.size[0] = 8;
-    pl.out[0] = vin;
+    pl.out[0] = val;
     {
         // algorithmic traffic: bucket id 4 + value 8 read, bucket id 4 + position 4 + value 8 written
         ProbeScope ps(c, "radix_scatter", 0.0, d_hi, 28.0);
         k_onesweep<uint32_t, true, true, kSortTile, kOsBlock><<<unsigned(nb), kOsBlock, 0, c->stream>>>(
-            ids, nullptr, kout, pin, n_cap, 0, counts, lb.status, lb.ticket, lb.epoch, gsum, nullptr, pl, d_hi);
+            ids, nullptr, kout, reinterpret_cast<uint32_t *>(pos), n_cap, 0, counts, lb.status, lb.ticket, lb.epoch,
+            gsum, nullptr, pl, d_hi);
         FZ_LAUNCH_CHECK();
     }
     lookback_end(c, nb);
     {
-        // algorithmic traffic per value: value 8 + position 4 read, value 8 + position 4 written
+        // algorithmic traffic per value: value 8 + position 4 read and written (range buckets)
         ProbeScope ps(c, "seg_sample_sort", 0.0, d_hi, 24.0);
-        k_ss_buckets<<<kSsBuckets, kSsBlock, 0, c->stream>>>(counts, offs, vin, pin, val, pos);
-        k_ss_runs<<<kSsBuckets, kSsBlock, 0, c->stream>>>(counts, offs, vin, pin, ka, ia, kb, ib, val, pos);
+        k_ss_buckets<<<kSsBuckets, kSsBlock, 0, c->stream>>>(counts, val, pos);
+        k_ss_runs<<<kSsBuckets, kSsBlock, 0, c->stream>>>(counts, ka, ia, kb, ib, val, pos);
         FZ_LAUNCH_CHECK();
     }
 }

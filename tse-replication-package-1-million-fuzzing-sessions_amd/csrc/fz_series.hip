@@ -615,7 +615,8 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
     if (n <= 0 || sg.S <= 0) return out;
     if (sg.S == 1 && sg.len_bound() > 16384 && n <= kSampleSortMax && sample_sort_on()) {
         // one long segment of up to 1.3 M values (RQ3's union): splitter buckets, one scatter pass
-        // and an LDS sort per bucket - five launches (fz_prims.hip sample_sort_f64_seg1)
+        // and an LDS sort per bucket - five launches (fz_prims.hip sample_sort_f64_seg1; every
+        // single-segment caller's segment starts at 0: single_segment, RQ3's union, fz_sort_f64)
         sample_sort_f64_seg1(c, src, sg.offs, n, out.val, out.pos);
         return out;
     }
@@ -2019,7 +2020,11 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
     constexpr int IPT = MAXN / BS;                // values per thread
     constexpr int NB = MAXN < 4096 ? MAXN : 4096;  // buckets
     constexpr int BPT = NB / BS > 0 ? NB / BS : 1;
+    // (the 16384 class keeps the keys in LDS: 16 per thread in registers spilled - 31 VGPRs of
+    // scratch per lane, 2.6x the algorithmic bytes in HBM traffic at config 3)
+    constexpr bool KEYS_LDS = MAXN > 2048;
     static_assert(MAXN % BS == 0 && NB % BS == 0, "qstats shape");
+    __shared__ uint64_t s_keys[KEYS_LDS ? MAXN : 1];
     __shared__ uint32_t s_cnt[NB + 1];
     __shared__ uint8_t s_map[NB];
     __shared__ uint64_t s_list[kQsMaxT][64];
@@ -2038,18 +2043,20 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
         const int64_t s = list[it];
         const int64_t b = offs[s];
         const int64_t n = offs[s + 1] - b;
-        uint64_t k[IPT];
+        uint64_t kr[KEYS_LDS ? 1 : IPT];
+        auto K = [&](int m) -> uint64_t & { return KEYS_LDS ? s_keys[tid + m * BS] : kr[m]; };
         uint64_t lo = ~0ull, hi = 0ull;
         DD acc{0.0, 0.0};
 #pragma unroll
         for (int m = 0; m < IPT; ++m) {
             const int64_t i = tid + int64_t(m) * BS;
             const double x = i < n ? src[b + i] : 0.0;
-            k[m] = i < n ? f64_key(x) : 0ull;
+            const uint64_t km = i < n ? f64_key(x) : 0ull;
+            K(m) = km;
             if (i < n) {
                 acc = dd_add_d(acc, x);
-                lo = k[m] < lo ? k[m] : lo;
-                hi = k[m] > hi ? k[m] : hi;
+                lo = km < lo ? km : lo;
+                hi = km > hi ? km : hi;
             }
         }
         lo = wave_min(lo);
@@ -2091,7 +2098,7 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
         if (lo != hi) {
 #pragma unroll
             for (int m = 0; m < IPT; ++m)
-                if (tid + int64_t(m) * BS < n) atomicAdd(&s_cnt[bucket1(k[m])], 1u);
+                if (tid + int64_t(m) * BS < n) atomicAdd(&s_cnt[bucket1(K(m))], 1u);
             __syncthreads();
             // bucket starts: thread t scans buckets [t * BPT, t * BPT + BPT)
             uint32_t sum = 0;
@@ -2141,8 +2148,8 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
 #pragma unroll
             for (int m = 0; m < IPT; ++m) {
                 if (tid + int64_t(m) * BS < n) {
-                    const uint8_t slot = s_map[bucket1(k[m])];
-                    if (slot != 0xff) s_list[slot][atomicAdd(&s_fill[slot], 1u)] = k[m];
+                    const uint8_t slot = s_map[bucket1(K(m))];
+                    if (slot != 0xff) s_list[slot][atomicAdd(&s_fill[slot], 1u)] = K(m);
                 }
             }
             __syncthreads();
@@ -2168,9 +2175,9 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
                 uint64_t rlo = ~0ull, rhi = 0ull;
 #pragma unroll
                 for (int m = 0; m < IPT; ++m)
-                    if (tid + int64_t(m) * BS < n && bucket1(k[m]) == tb) {
-                        rlo = k[m] < rlo ? k[m] : rlo;
-                        rhi = k[m] > rhi ? k[m] : rhi;
+                    if (tid + int64_t(m) * BS < n && bucket1(K(m)) == tb) {
+                        rlo = K(m) < rlo ? K(m) : rlo;
+                        rhi = K(m) > rhi ? K(m) : rhi;
                     }
                 rlo = wave_min(rlo);
                 rhi = wave_max(rhi);
@@ -2194,8 +2201,8 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
                     __syncthreads();
 #pragma unroll
                     for (int m = 0; m < IPT; ++m)
-                        if (tid + int64_t(m) * BS < n && k[m] >= rlo && k[m] <= rhi)
-                            atomicAdd(&s_cnt[bucket(k[m], rlo, sc2, nb2)], 1u);
+                        if (tid + int64_t(m) * BS < n && K(m) >= rlo && K(m) <= rhi)
+                            atomicAdd(&s_cnt[bucket(K(m), rlo, sc2, nb2)], 1u);
                     __syncthreads();
                     {  // the sub-bucket holding rank r: thread t sums buckets [t * BPT, t * BPT + BPT),
                        // one block scan, the thread whose run holds r walks it (not a dependent wave
@@ -2227,9 +2234,9 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
                     uint64_t nlo = ~0ull, nhi = 0ull;
 #pragma unroll
                     for (int m = 0; m < IPT; ++m)
-                        if (tid + int64_t(m) * BS < n && k[m] >= rlo && k[m] <= rhi && bucket(k[m], rlo, sc2, nb2) == sb) {
-                            nlo = k[m] < nlo ? k[m] : nlo;
-                            nhi = k[m] > nhi ? k[m] : nhi;
+                        if (tid + int64_t(m) * BS < n && K(m) >= rlo && K(m) <= rhi && bucket(K(m), rlo, sc2, nb2) == sb) {
+                            nlo = K(m) < nlo ? K(m) : nlo;
+                            nhi = K(m) > nhi ? K(m) : nhi;
                         }
                     nlo = wave_min(nlo);
                     nhi = wave_max(nhi);
@@ -2257,8 +2264,8 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
                     __syncthreads();
 #pragma unroll
                     for (int m = 0; m < IPT; ++m)
-                        if (tid + int64_t(m) * BS < n && k[m] >= rlo && k[m] <= rhi)
-                            s_list[0][atomicAdd(&s_fill[0], 1u)] = k[m];
+                        if (tid + int64_t(m) * BS < n && K(m) >= rlo && K(m) <= rhi)
+                            s_list[0][atomicAdd(&s_fill[0], 1u)] = K(m);
                     __syncthreads();
                     if (w == 0) {
                         const int sz = int(cnt);
@@ -2351,6 +2358,10 @@ __global__ __launch_bounds__(256) void k_qs_sort_mid(const double *__restrict__ 
 }
 
 bool seg_qstats_ok(const Segs &sg) { return sg.len_bound() <= kQsMax; }
+#ifndef FZ_QS_BIG_BLOCK
+#define FZ_QS_BIG_BLOCK 512
+#endif
+constexpr int kQsBigBlock = FZ_QS_BIG_BLOCK;  // threads of the 2049 .. kQsMax class
 
 void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_host, int nq, double *mean,
                 double *median, double *pcts, int64_t *d_ge100, double *mean2) {
@@ -2396,7 +2407,10 @@ void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_h
         FZ_LAUNCH_CHECK();
     }
     if (lb > 2048) {
-        k_qs_block<1024, kQsMax><<<grid(caps[2], 1024), 1024, 0, c->stream>>>(vals, sg.offs, L.ids[2], L.d_n + 2, a);
+        // (512 threads, keys in LDS: 203 VGPRs and no scratch; at 1024 threads the kernel spilled 17-31
+        // VGPRs per lane, keys in registers or in LDS)
+        k_qs_block<kQsBigBlock, kQsMax><<<grid(caps[2], 1024), kQsBigBlock, 0, c->stream>>>(vals, sg.offs, L.ids[2],
+                                                                                           L.d_n + 2, a);
         FZ_LAUNCH_CHECK();
     }
 }
