@@ -1280,6 +1280,10 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     const int64_t bigmax[3] = {c->h_pinned[7], c->h_pinned[8], c->h_pinned[9]};
     const int64_t fused[3] = {c->h_pinned[10], c->h_pinned[11], c->h_pinned[12]};
     const int64_t n_fuzz = c->h_pinned[13], n_covb = c->h_pinned[14];
+    // (read now: the long-segment pass below reuses the pinned area - its radix sort's digit
+    // read-back overwrote word 19, and config 5's shards got the longest segment as their session
+    // bound, 39 K instead of 2,960 rows)
+    const int64_t lim_rows = c->h_pinned[19];
     {
         auto view = [&](View &v, DevBuf &tmb, DevBuf &prb, int64_t at, int64_t n, DevBuf &offb) {
             v.n = n;
@@ -1331,7 +1335,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     s.covb.max_seg = maxseg[1];
     s.cov.max_seg = maxseg[2];
     // (at least 1 when the table has rows: the analyses keep one - empty - session, rq2_count:285)
-    s.cov.lim_seg = c->h_pinned[19] < maxseg[2] ? (c->h_pinned[19] > 0 ? c->h_pinned[19] : 1) : maxseg[2];
+    s.cov.lim_seg = lim_rows < maxseg[2] ? (lim_rows > 0 ? lim_rows : 1) : maxseg[2];
     s.issues.max_seg = maxseg[3];
     s.built = true;
     if (stats) {
