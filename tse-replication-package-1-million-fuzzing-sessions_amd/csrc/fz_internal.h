@@ -383,8 +383,8 @@ void radix_sort_pairs_payload32(fz_ctx *c, uint32_t *&keys, uint32_t *&vals, int
 void sample_sort_f64_seg1(fz_ctx *c, const double *src, const int64_t *offs, int64_t n_cap, double *val,
                           int32_t *pos);
 bool sample_sort_on();  // FZ_SAMPLE_SORT=0: the LSD radix path instead (A/B builds of one library)
-// Reductions whose last-arriving block folds the partials (one launch fewer each): FZ_FUSED_FOLD=0
-// runs the separate fold kernels instead.  seg_tickets: the context's zeroed per-segment ticket
+// Reductions whose last-arriving block folds the partials (one launch fewer each) when
+// FZ_FUSED_FOLD=1 - off by default (measured slower at config 2, fz_series.hip).  seg_tickets: the context's zeroed per-segment ticket
 // words (each fold resets its own), or null while a graph is recorded and they would have to grow.
 bool fused_fold_on();
 unsigned *seg_tickets(fz_ctx *c, int64_t S);

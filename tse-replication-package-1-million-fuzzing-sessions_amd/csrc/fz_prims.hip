@@ -1065,17 +1065,17 @@ __device__ inline uint32_t ss_bucket(const uint64_t *s_spl, uint64_t k) {
     return (p < kSsSplit && s_spl[p] == k) ? uint32_t(2 * p + 1) : uint32_t(2 * p);
 }
 
-__global__ __launch_bounds__(kBlock) void k_ss_ids(const double *__restrict__ src, const int64_t *__restrict__ d_hi,
+__global__ __launch_bounds__(kSsBlock) void k_ss_ids(const double *__restrict__ src, const int64_t *__restrict__ d_hi,
                                                     const uint64_t *__restrict__ spl, uint32_t *__restrict__ ids,
                                                     unsigned long long *__restrict__ counts) {
     __shared__ uint64_t s_spl[kSsSplit];
     __shared__ uint32_t s_h[256];
-    for (int i = threadIdx.x; i < kSsSplit; i += kBlock) s_spl[i] = spl[i];
-    for (int i = threadIdx.x; i < 256; i += kBlock) s_h[i] = 0u;
+    for (int i = threadIdx.x; i < kSsSplit; i += kSsBlock) s_spl[i] = spl[i];
+    for (int i = threadIdx.x; i < 256; i += kSsBlock) s_h[i] = 0u;
     __syncthreads();
     const int64_t hi = *d_hi;
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i - threadIdx.x < hi;
-         i += int64_t(gridDim.x) * kBlock) {
+    for (int64_t i = int64_t(blockIdx.x) * kSsBlock + threadIdx.x; i - threadIdx.x < hi;
+         i += int64_t(gridDim.x) * kSsBlock) {
         const bool valid = i < hi;
         const uint32_t b = valid ? ss_bucket(s_spl, f64_key(src[i])) : 0u;
         if (valid) ids[i] = b;
@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(kBlock) void k_ss_ids(const double *__restrict__ sr
         if (valid && (__ffsll((long long)peers) - 1) == lane_id()) atomicAdd(&s_h[b], uint32_t(__popcll(peers)));
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < kSsBuckets; i += kBlock)
+    for (int i = threadIdx.x; i < kSsBuckets; i += kSsBlock)
         if (s_h[i]) atomicAdd(&counts[i], (unsigned long long)s_h[i]);
 }
 
@@ -1201,11 +1201,27 @@ __device__ inline void ss_bucket_range(const unsigned long long *__restrict__ co
 
 // One workgroup per range bucket of <= kSsMax values, sorted in place in val / pos (bucket order
 // on entry; the bucket's positions are read before any is written).  Equality buckets are final;
-// longer range buckets are k_ss_runs'.
+// longer range buckets are k_ss_runs'.  A range bucket lies between two sample quantiles, so its
+// values are spread: a counting sort into n value sub-buckets (linear in value when the range is
+// finite, else in key), each value's rank inside its sub-bucket by comparison (key, then position:
+// stable) - O(n) work and five barriers.  A sub-bucket of more than kSsSkew values (a run of one
+// repeated value that no sample hit) sends the bucket to the LSD radix sort in LDS instead.
+constexpr int kSsSkew = 128;
+struct SsVbShared {  // the value-bucket sort's LDS (aliases SsShared: one or the other per bucket)
+    uint64_t key[kSsMax];
+    uint16_t pos[kSsMax];                   // values in sub-bucket order (bucket-local index)
+    uint32_t cnt[(kSsMax + 2 + 1) / 2];     // 16-bit sub-bucket counters, then starts (+ sentinel)
+};
+union SsLds {
+    SsShared lsd;
+    SsVbShared vb;
+};
 __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long long *__restrict__ counts,
                                                           double *__restrict__ val, int32_t *__restrict__ pos) {
-    __shared__ SsShared sh;
-    const int w = wave_id(), lane = lane_id();
+    __shared__ SsLds L;
+    __shared__ uint64_t s_lo[kSsWaves], s_hi[kSsWaves];
+    __shared__ uint32_t s_tmp[kSsWaves], s_max[kSsWaves];
+    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
     const int b = blockIdx.x;
     if (b & 1) return;  // (an equality bucket: one key, already in position order)
     int64_t base, len;
@@ -1215,28 +1231,134 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
     int32_t *ps = pos + base;
     const int wbase = w * (kSsMax / kSsWaves);
     const int n = int(len);
+    uint16_t *const cnt16 = reinterpret_cast<uint16_t *>(L.vb.cnt);
     uint64_t k[kSsIpt];
-    uint16_t ix[kSsIpt];
+    int32_t np[kSsIpt];
+    uint64_t lo = ~0ull, hi = 0ull;
 #pragma unroll
     for (int r = 0; r < kSsIpt; ++r) {
         const int q = wbase + r * kWave + lane;
         k[r] = q < n ? f64_key(v[q]) : 0ull;
-        ix[r] = uint16_t(q);
-    }
-    ss_lds_sort(k, ix, n, f64_key(v[0]), sh);
-    int32_t np[kSsIpt];
-#pragma unroll
-    for (int r = 0; r < kSsIpt; ++r) {
-        const int q = wbase + r * kWave + lane;
-        np[r] = q < n ? ps[ix[r]] : 0;
-    }
-    __syncthreads();  // every position read before any is overwritten
-#pragma unroll
-    for (int r = 0; r < kSsIpt; ++r) {
-        const int q = wbase + r * kWave + lane;
+        np[r] = q < n ? ps[q] : 0;
         if (q < n) {
-            v[q] = f64_from_key(k[r]);
-            ps[q] = np[r];
+            lo = k[r] < lo ? k[r] : lo;
+            hi = k[r] > hi ? k[r] : hi;
+        }
+    }
+    lo = wave_min(lo);
+    hi = wave_max(hi);
+    if (lane == 0) {
+        s_lo[w] = lo;
+        s_hi[w] = hi;
+    }
+    for (int j = tid; j < (n + 2) / 2; j += kSsBlock) L.vb.cnt[j] = 0u;
+    __syncthreads();
+    lo = ~0ull;
+    hi = 0ull;
+#pragma unroll
+    for (int q = 0; q < kSsWaves; ++q) {
+        lo = s_lo[q] < lo ? s_lo[q] : lo;
+        hi = s_hi[q] > hi ? s_hi[q] : hi;
+    }
+    // sub-bucket of a key: linear in value over a finite range (spread values stay spread), else in key
+    const double vlo = f64_from_key(lo), vhi = f64_from_key(hi);
+    const bool vlin = isfinite(vlo) && isfinite(vhi) && isfinite(vhi - vlo) && vhi > vlo;
+    const double vsc = vlin ? double(n) / (vhi - vlo) : 0.0, ksc = double(n) / (double(hi - lo) + 1.0);
+    auto sub = [&](uint64_t key) -> uint32_t {
+        const double qd = vlin ? (f64_from_key(key) - vlo) * vsc : double(key - lo) * ksc;
+        return qd < double(n - 1) ? (qd > 0.0 ? uint32_t(qd) : 0u) : uint32_t(n - 1);
+    };
+    uint32_t bs[kSsIpt];  // sub-bucket << 16 | slot in it
+#pragma unroll
+    for (int r = 0; r < kSsIpt; ++r) {
+        const int q = wbase + r * kWave + lane;
+        bs[r] = 0u;
+        if (q < n) {
+            const uint32_t sb = sub(k[r]);
+            const uint32_t sh = (sb & 1u) * 16u;
+            bs[r] = (sb << 16) | ((atomicAdd(&L.vb.cnt[sb >> 1], 1u << sh) >> sh) & 0xffffu);
+            L.vb.key[q] = k[r];
+        }
+    }
+    __syncthreads();
+    // sub-bucket starts: thread t scans EPT consecutive counters; the largest decides the fallback
+    constexpr int EPT = (kSsMax + 1 + kSsBlock - 1) / kSsBlock;
+    uint32_t sum = 0, mx = 0;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+        const int j = tid * EPT + e;
+        const uint32_t ce = j < n ? cnt16[j] : 0u;
+        sum += ce;
+        mx = ce > mx ? ce : mx;
+    }
+    mx = wave_max(mx);
+    if (lane == 0) s_max[w] = mx;
+    uint32_t run = block_excl_scan<uint32_t, kSsWaves>(sum, s_tmp, (uint32_t *)nullptr);
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {  // (block_excl_scan's barriers ordered every read above)
+        const int j = tid * EPT + e;
+        if (j < n) {
+            const uint32_t ce = cnt16[j];
+            cnt16[j] = uint16_t(run);
+            run += ce;
+        }
+    }
+    if (tid == 0) cnt16[n] = uint16_t(n);
+    __syncthreads();
+    uint32_t gmax = 0;
+#pragma unroll
+    for (int q = 0; q < kSsWaves; ++q) gmax = s_max[q] > gmax ? s_max[q] : gmax;
+    int32_t dq[kSsIpt];
+    if (gmax > uint32_t(kSsSkew)) {
+        // (a long run of one value: the radix sort, whose cost does not depend on the spread)
+        __syncthreads();
+        uint16_t ix[kSsIpt];
+#pragma unroll
+        for (int r = 0; r < kSsIpt; ++r) ix[r] = uint16_t(wbase + r * kWave + lane);
+        ss_lds_sort(k, ix, n, lo, L.lsd);
+        int32_t pp[kSsIpt];
+#pragma unroll
+        for (int r = 0; r < kSsIpt; ++r) {
+            const int q = wbase + r * kWave + lane;
+            pp[r] = q < n ? ps[ix[r]] : 0;
+        }
+        __syncthreads();  // every position read before any is overwritten
+#pragma unroll
+        for (int r = 0; r < kSsIpt; ++r) {
+            const int q = wbase + r * kWave + lane;
+            if (q < n) {
+                v[q] = f64_from_key(k[r]);
+                ps[q] = pp[r];
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < kSsIpt; ++r) {
+        const int q = wbase + r * kWave + lane;
+        if (q < n) L.vb.pos[cnt16[bs[r] >> 16] + (bs[r] & 0xffffu)] = uint16_t(q);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSsIpt; ++r) {
+        const int q = wbase + r * kWave + lane;
+        dq[r] = -1;
+        if (q >= n) continue;
+        const uint32_t st = cnt16[bs[r] >> 16], en = cnt16[(bs[r] >> 16) + 1];
+        uint32_t rank = 0;
+        for (uint32_t x = st; en - st > 1 && x < en; ++x) {  // (alone in its sub-bucket: rank 0)
+            const int ox = L.vb.pos[x];
+            const uint64_t kx = L.vb.key[ox];
+            rank += (kx < k[r]) || (kx == k[r] && ox < q);
+        }
+        dq[r] = int32_t(st + rank);
+    }
+    // (every value and position of the bucket was read into registers at the start)
+#pragma unroll
+    for (int r = 0; r < kSsIpt; ++r) {
+        if (dq[r] >= 0) {
+            v[dq[r]] = f64_from_key(k[r]);
+            ps[dq[r]] = np[r];
         }
     }
 }
@@ -1342,7 +1464,9 @@ void sample_sort_f64_seg1(fz_ctx *c, const double *src, const int64_t *offs, int
     const int64_t gwords = ((nb + kOsGroup - 1) / kOsGroup) * kRadix;
     unsigned long long *gsum = c->arena.get<unsigned long long>(gwords);
     k_ss_splitters<<<1, kSsBlock, 0, c->stream>>>(src, offs, n_cap, spl, counts, gsum, gwords, d_hi);
-    k_ss_ids<<<grid_for(n_cap, kBlock, 2048), kBlock, 0, c->stream>>>(src, d_hi, spl, ids, counts);
+    // (256 workgroups: each adds its 255 bucket counts to the totals with global atomics - 2,048
+    // workgroups' adds serialised on the 255 words, 47 us at config 2)
+    k_ss_ids<<<grid_for(n_cap, kSsBlock, 256), kSsBlock, 0, c->stream>>>(src, d_hi, spl, ids, counts);
     FZ_LAUNCH_CHECK();
     const Lookback lb = lookback_begin(c, nb * kRadix);
     RadixPayload pl;

@@ -142,10 +142,13 @@ ChunkedSegs chunked(fz_ctx *c, const Segs &sg) {
 
 ChunkMap make_chunks(fz_ctx *c, const Segs &sg) { return chunked(c, sg).cm; }
 
+// (off by default: same-box A/B at config 2, 1.239 ms/step with the separate fold launches against
+// 1.274 with the last-arriver folds - the write-through stores and the ticket round trip in every
+// workgroup cost more than the launches they save; FZ_FUSED_FOLD=1 turns them on)
 bool fused_fold_on() {
     static const bool on = [] {
         const char *e = std::getenv("FZ_FUSED_FOLD");
-        return !e || std::atoi(e) != 0;
+        return e && std::atoi(e) != 0;
     }();
     return on;
 }
@@ -603,18 +606,19 @@ __global__ __launch_bounds__(kBlock) void k_f64_from_keys(const uint64_t *__rest
     }
 }
 
-// (the sample sort's range buckets average 1/128 of the live values - 10 K at 1.3 M, against its
-// LDS capacity of 12 K; a longer bucket takes the slower in-workgroup merge; config 2: 1.01 M
-// capacity, ~0.8 M live)
-constexpr int64_t kSampleSortMax = int64_t(5) << 18;
+// (the sample sort's work follows the live length - config 3 / 5's empty RQ3 union of 1e8 capacity
+// costs five short launches, where the merge sort's tile and merge rounds were ~25 - and its range
+// buckets average 1/128 of the live values: 6 K at config 2's 0.8 M, against an LDS capacity of
+// 12 K; a longer bucket - a live union of several million - takes the slower in-workgroup merge)
+constexpr int64_t kSampleSortMax = (int64_t(1) << 31) - 1;
 SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int32_t *) {
     const int64_t n = sg.n_cap;
     SortedSegs out;
     out.val = c->arena.get<double>(n);
     out.pos = c->arena.get<int32_t>(n);
     if (n <= 0 || sg.S <= 0) return out;
-    if (sg.S == 1 && sg.len_bound() > 16384 && n <= kSampleSortMax && sample_sort_on()) {
-        // one long segment of up to 1.3 M values (RQ3's union): splitter buckets, one scatter pass
+    if (sg.S == 1 && sg.len_bound() > 16384 && n < kSampleSortMax && sample_sort_on()) {
+        // one long segment (RQ3's union, a long series): splitter buckets, one scatter pass
         // and an LDS sort per bucket - five launches (fz_prims.hip sample_sort_f64_seg1; every
         // single-segment caller's segment starts at 0: single_segment, RQ3's union, fz_sort_f64)
         sample_sort_f64_seg1(c, src, sg.offs, n, out.val, out.pos);
