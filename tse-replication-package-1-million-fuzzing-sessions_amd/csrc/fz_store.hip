@@ -879,15 +879,32 @@ __device__ inline int big_sub(int64_t t, long long lo, long long hi, int B) {
     const int k = int(q);
     return k < B ? k : B - 1;
 }
+// (the min / max and compaction passes split every tile over kBigSplit workgroups, each with
+// several rows' loads in flight per thread: one workgroup per 64 K-row tile left most CUs idle and
+// waited on one load at a time - k_big_compact at 15 % of HBM on config 5's giant shard)
+constexpr int kBigSplit = 8;
+__device__ inline void big_slice(const BigPlan &pl, int64_t tl, int part, int64_t &r0, int64_t &r1) {
+    const int64_t b = pl.t_begin[tl], e = pl.t_end[tl], span = (e - b + kBigSplit - 1) / kBigSplit;
+    r0 = b + part * span;
+    r1 = r0 + span < e ? r0 + span : e;
+}
 __global__ __launch_bounds__(kBlock) void k_big_minmax(const int64_t *__restrict__ time, BigPlan pl) {
     __shared__ int64_t s_lo[4], s_hi[4];
-    for (int64_t tl = blockIdx.x; tl < pl.ntiles; tl += gridDim.x) {
+    for (int64_t g = blockIdx.x; g < pl.ntiles * kBigSplit; g += gridDim.x) {
+        const int64_t tl = g / kBigSplit;
+        int64_t r0, r1;
+        big_slice(pl, tl, int(g % kBigSplit), r0, r1);
         int64_t lo = INT64_MAX, hi = INT64_MIN;
-        for (int64_t r = pl.t_begin[tl] + threadIdx.x; r < pl.t_end[tl]; r += kBlock) {
-            const int64_t t = time[r];
-            if (t == FZ_TS_NULL) continue;
-            lo = t < lo ? t : lo;
-            hi = t > hi ? t : hi;
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += 4 * kBlock) {
+            int64_t t[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t[u] = r + u * kBlock < r1 ? time[r + u * kBlock] : FZ_TS_NULL;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (t[u] == FZ_TS_NULL) continue;
+                lo = t[u] < lo ? t[u] : lo;
+                hi = t[u] > hi ? t[u] : hi;
+            }
         }
         lo = wave_min(lo);
         hi = wave_max(hi);
@@ -939,29 +956,56 @@ struct BigCompact {
 __global__ __launch_bounds__(kBlock) void k_big_compact(const int64_t *__restrict__ time,
                                                         const uint32_t *__restrict__ rows, GatherCols gc, BigPlan pl,
                                                         const int64_t *__restrict__ sstart, BigCompact out) {
-    for (int64_t tl = blockIdx.x; tl < pl.ntiles; tl += gridDim.x) {
+    constexpr int U = 4;  // rows per thread in flight
+    for (int64_t g = blockIdx.x; g < pl.ntiles * kBigSplit; g += gridDim.x) {
+        const int64_t tl = g / kBigSplit;
+        int64_t r0, r1;
+        big_slice(pl, tl, int(g % kBigSplit), r0, r1);
         const int j = pl.t_seg[tl];
         const int B = pl.nsub[j];
         const long long lo = pl.lo[j], hi = pl.hi[j];
-        const int64_t r0 = pl.t_begin[tl], r1 = pl.t_end[tl];
         const int64_t shift = pl.cstart[j] - sstart[j];
         const uint32_t kb = uint32_t(pl.sbase[j]);
-        for (int64_t r = r0 + threadIdx.x; r < r1; r += kBlock) {
-            const int64_t t = time[r], d = r + shift;
-            out.key[d] = kb + uint32_t(big_sub(t, lo, hi, B));
-            out.time[d] = t;
-            out.rows[d] = rows[r];
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += U * kBlock) {
+            int64_t t[U];
+            uint32_t rw[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t ru = r + u * kBlock;
+                t[u] = ru < r1 ? time[ru] : 0;
+                rw[u] = ru < r1 ? rows[ru] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t ru = r + u * kBlock;
+                if (ru >= r1) continue;
+                const int64_t d = ru + shift;
+                out.key[d] = kb + uint32_t(big_sub(t[u], lo, hi, B));
+                out.time[d] = t[u];
+                out.rows[d] = rw[u];
+            }
         }
         for (int c = 0; c < gc.n; ++c) {  // column by column: one type per loop
             const int sz = gc.size[c];
-            for (int64_t r = r0 + threadIdx.x; r < r1; r += kBlock) {
-                const int64_t d = r + shift;
-                if (sz == 8)
-                    static_cast<uint64_t *>(out.col[c])[d] = static_cast<const uint64_t *>(gc.src[c])[r];
-                else if (sz == 4)
-                    static_cast<uint32_t *>(out.col[c])[d] = static_cast<const uint32_t *>(gc.src[c])[r];
-                else
-                    static_cast<uint8_t *>(out.col[c])[d] = static_cast<const uint8_t *>(gc.src[c])[r];
+            for (int64_t r = r0 + threadIdx.x; r < r1; r += U * kBlock) {
+                uint64_t x[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int64_t ru = r + u * kBlock;
+                    x[u] = ru >= r1 ? 0ull
+                                    : (sz == 8 ? static_cast<const uint64_t *>(gc.src[c])[ru]
+                                               : (sz == 4 ? static_cast<const uint32_t *>(gc.src[c])[ru]
+                                                          : static_cast<const uint8_t *>(gc.src[c])[ru]));
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int64_t ru = r + u * kBlock;
+                    if (ru >= r1) continue;
+                    const int64_t d = ru + shift;
+                    if (sz == 8) static_cast<uint64_t *>(out.col[c])[d] = x[u];
+                    else if (sz == 4) static_cast<uint32_t *>(out.col[c])[d] = uint32_t(x[u]);
+                    else static_cast<uint8_t *>(out.col[c])[d] = uint8_t(x[u]);
+                }
             }
         }
     }
@@ -1033,7 +1077,8 @@ static bool big_segments_bucketed(fz_ctx *c, const PrefixSorted &ps, int64_t big
     pl.ntiles = nt;
     sync(c);  // the host vectors above die with this function
     const unsigned grid = unsigned(nt < 4096 ? nt : 4096);
-    k_big_minmax<<<grid, kBlock, 0, c->stream>>>(ps.time, pl);
+    const unsigned gsplit = unsigned(nt * kBigSplit < 8192 ? nt * kBigSplit : 8192);
+    k_big_minmax<<<gsplit, kBlock, 0, c->stream>>>(ps.time, pl);
     FZ_LAUNCH_CHECK();
     int64_t *cnt = c->arena.get<int64_t>(nsubs + 1);
     dev_fill(c, cnt, 0, (nsubs + 1) * 8);
@@ -1056,7 +1101,7 @@ static bool big_segments_bucketed(fz_ctx *c, const PrefixSorted &ps, int64_t big
     {
         // read time 8 + row id 4 + columns; write key 4 + time 8 + row id 4 + columns
         ProbeScope probe(c, "big_compact", (28.0 + 2.0 * ps.gc.bytes()) * double(ncomp));
-        k_big_compact<<<grid, kBlock, 0, c->stream>>>(ps.time, ps.rows, ps.gc, pl, d_sst, cp);
+        k_big_compact<<<gsplit, kBlock, 0, c->stream>>>(ps.time, ps.rows, ps.gc, pl, d_sst, cp);
         FZ_LAUNCH_CHECK();
     }
     RadixPayload rpl;
