@@ -479,6 +479,10 @@ constexpr int kOsWindow = FZ_OS_WINDOW;
 #endif
 constexpr int kHistKeysPerBlock = FZ_HIST_KPB;  // keys per histogram workgroup (its flush is npass x 256 atomics;
 // 8192 keys per workgroup made the small sorts' loops latency-bound: 6 -> 20 us for 65 k keys)
+#ifndef FZ_HIST_MAXB
+#define FZ_HIST_MAXB 256
+#endif
+constexpr int kHistMaxBlocks = FZ_HIST_MAXB;
 constexpr int kOsGroup = 8;  // tiles per look-back group (one {tiles, sum} word per group and digit)
 
 template <typename KeyT>
@@ -872,7 +876,9 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
     unsigned long long *gsum = c->arena.get<unsigned long long>(gwords * npass);
     {
         ProbeScope ps(c, "radix_hist", 8.0 * double(n));
-        k_onesweep_hist<KeyT><<<grid_for(n, kHistKeysPerBlock, 2048), kBlock, 0, c->stream>>>(
+        // (at most 256 workgroups: each adds its npass x 256 digit counts with global atomics, and
+        // 2,048 workgroups' adds serialised on those words - 64 us for 12.5 M keys)
+        k_onesweep_hist<KeyT><<<grid_for(n, kHistKeysPerBlock, kHistMaxBlocks), kBlock, 0, c->stream>>>(
             key_src ? key_src : keys, n, npass, ghist, gsum, gwords * npass, d_live);
         FZ_LAUNCH_CHECK();
     }
