@@ -33,6 +33,20 @@ __device__ inline void store_wt(double *p, double x) {
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// offs[q] = v for q in [a, e] of every lane's range (a > e: none), each range stored by the whole
+// wave 64 entries a round (all 64 lanes must call it): a lane whose range spans thousands of ids -
+// the ids before a shard's first project, the gap between a table's two prefix types - no longer
+// stores them one by one on its own
+__device__ inline void wave_fill_ranges(int64_t *offs, int64_t a, int64_t e, int64_t v) {
+    uint64_t m = __ballot(a <= e);
+    while (m) {
+        const int l = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int64_t A = __shfl(a, l, 64), E = __shfl(e, l, 64), V = __shfl(v, l, 64);
+        for (int64_t q = A + lane_id(); q <= E; q += 64) offs[q] = V;
+    }
+}
+
 template <typename T>
 __device__ inline T wave_incl_scan(T x) {
     const int lane = lane_id();

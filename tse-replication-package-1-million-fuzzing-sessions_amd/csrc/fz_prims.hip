@@ -2389,15 +2389,21 @@ __global__ __launch_bounds__(kBlock) void k_segment_offsets_rows(const uint32_t 
     const int64_t n = d_n ? *d_n : n_cap;  // d_n null: the length is the host-known n_cap
     const int64_t first = n > 0 ? int64_t(proj[0]) : P + 1, last = n > 0 ? int64_t(proj[n - 1]) : -1;
     const int64_t span = n_cap > P + 1 ? n_cap : P + 1;
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < span; i += int64_t(gridDim.x) * kBlock) {
-        if (i <= P) {  // ids before the first row's and after the last row's
+    // (wave-uniform trip count: the waves fill the gaps between consecutive rows' ids together)
+    for (int64_t i0 = int64_t(blockIdx.x) * kBlock + (threadIdx.x & ~(kWave - 1)); i0 < span;
+         i0 += int64_t(gridDim.x) * kBlock) {
+        const int64_t i = i0 + lane_id();
+        if (i <= P && i < span) {  // ids before the first row's and after the last row's
             if (i <= first) offsets[i] = 0;  // lower_bound of the first row's id is 0 too
             else if (i > last) offsets[i] = n;
         }
-        if (i > 0 && i < n) {
+        int64_t a = 1, e = 0;
+        if (i > 0 && i < n && i < span) {
             const int64_t pp = int64_t(proj[i - 1]), pc = int64_t(proj[i]);
-            for (int64_t q = pp + 1; q <= pc && q <= P; ++q) offsets[q] = i;  // ids stay in [0, P]
+            a = pp + 1;
+            e = pc < P ? pc : P;  // ids stay in [0, P]
         }
+        wave_fill_ranges(offsets, a, e, i);
     }
 }
 

@@ -182,20 +182,33 @@ struct PrefixOffs {
     int64_t base[4] = {0, 0, 0, 0};
 };
 __global__ __launch_bounds__(kBlock) void k_prefix_offsets(const PrefixOffs O) {
-    for (int64_t gi = int64_t(blockIdx.x) * kBlock + threadIdx.x; gi < O.base[3]; gi += int64_t(gridDim.x) * kBlock) {
+    // (wave-uniform trip count: the gaps between consecutive keys are filled by whole waves; a wave
+    // straddling two tables fills each lane's range in its own table's offsets, one table a round)
+    for (int64_t g0 = int64_t(blockIdx.x) * kBlock + (threadIdx.x & ~(kWave - 1)); g0 < O.base[3];
+         g0 += int64_t(gridDim.x) * kBlock) {
+        const int64_t gi = g0 + lane_id();
+        const bool in = gi < O.base[3];
         const int k = gi >= O.base[2] ? 2 : (gi >= O.base[1] ? 1 : 0);
-        const int64_t i = gi - O.base[k];
-        const uint32_t *keys = O.keys[k];
-        const int64_t n = O.n[k], S = O.S[k];
-        int64_t *offs = O.offs[k];
-        const int64_t first = int64_t(keys[0]), last = int64_t(keys[n - 1]);  // n >= 1, keys < S
-        if (i <= S) {
-            if (i <= first) offs[i] = 0;
-            else if (i > last) offs[i] = n;
+        int64_t a = 1, e = 0, i = 0;
+        if (in) {
+            i = gi - O.base[k];
+            const uint32_t *keys = O.keys[k];
+            const int64_t n = O.n[k], S = O.S[k];
+            int64_t *offs = O.offs[k];
+            const int64_t first = int64_t(keys[0]), last = int64_t(keys[n - 1]);  // n >= 1, keys < S
+            if (i <= S) {
+                if (i <= first) offs[i] = 0;
+                else if (i > last) offs[i] = n;
+            }
+            if (i > 0 && i < n) {
+                const int64_t pp = int64_t(keys[i - 1]), pc = int64_t(keys[i]);
+                a = pp + 1;
+                e = pc < S ? pc : S;
+            }
         }
-        if (i > 0 && i < n) {
-            const int64_t pp = int64_t(keys[i - 1]), pc = int64_t(keys[i]);
-            for (int64_t q = pp + 1; q <= pc && q <= S; ++q) offs[q] = i;
+        for (int t = 0; t < 3; ++t) {  // (uniform: every lane takes part in each table's round)
+            const bool mine = in && k == t;
+            wave_fill_ranges(O.offs[t], mine ? a : 1, mine ? e : 0, i);
         }
     }
 }

@@ -352,13 +352,17 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT, Emit> &J, int6
     } else {
         for (int i = 0; i < kFcItems; ++i) {
             const int k = i * kFcBlock + tid;
-            if (base + k >= lim) break;
-            const int64_t pp = k > 0 ? int64_t(sh.pj[k - 1]) : sh.pprev;
-            const int64_t pc = int64_t(pj[i]);
-            if (pc > pp) {
-                const int64_t o = pre + (sh.pos[k] & 0x7fffffff);
-                for (int64_t q = pp + 1; q <= pc; ++q) oofs[q] = o;
+            int64_t a = 1, e = 0, o = 0;
+            if (base + k < lim) {
+                const int64_t pp = k > 0 ? int64_t(sh.pj[k - 1]) : sh.pprev;
+                const int64_t pc = int64_t(pj[i]);
+                if (pc > pp) {
+                    a = pp + 1;
+                    e = pc;
+                    o = pre + (sh.pos[k] & 0x7fffffff);
+                }
             }
+            wave_fill_ranges(oofs, a, e, o);
         }
     }
     if (tile == ntiles - 1) {
