@@ -64,8 +64,9 @@ for s in $STEPS; do
           # table through --force-sharded; N > 0: shard 0 of N, --strong --force-sharded; order "x":
           # the default); sho:<cfg>@<N>@single: shard 0 of N through the single-table step
       IFS=@ read -r cfg n ord <<< "$arg"
-      extra="--force-sharded"; [ "$n" != 0 ] && extra="$extra --strong --shard-of $n --shard-rank 0"
-      [ "$ord" = single ] && extra="--strong --shard-of $n --shard-rank 0"
+      nr=0; [ "${n#*/}" != "$n" ] && nr=${n#*/} && n=${n%%/*}  # N or N/rank
+      extra="--force-sharded"; [ "$n" != 0 ] && extra="$extra --strong --shard-of $n --shard-rank $nr"
+      [ "$ord" = single ] && extra="--strong --shard-of $n --shard-rank $nr"
       [ "$ord" != x ] && [ "$ord" != single ] && extra="$extra --shard-groups $ord"
       st=20; [ "$cfg" != c2 ] && st=10
       timeout -k 10 400 python -u bench.py --config $cfg --steps $st --warmup 2 --no-cpu-baseline --probe-steps 0 $extra > $O/${T}_sho.json 2> $O/${T}_sho.err || exit $?
