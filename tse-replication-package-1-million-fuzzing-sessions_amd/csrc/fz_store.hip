@@ -136,7 +136,15 @@ __global__ __launch_bounds__(kSortBlock) void k_store_views(const ViewSrc v, int
 // Used only while no probe window is open (the probes bracket launches on the context's own
 // stream).  fork: every helper's stream waits for the work enqueued on c so far; join: c waits
 // for everything enqueued on the helpers.
-static int store_helpers(fz_ctx *c) { return c->probe.active() ? 0 : int(c->helpers.size()); }
+// (FZ_STORE_FORK=0: no fork - the same-box A/B of the store's helper streams)
+static bool store_fork_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("FZ_STORE_FORK");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
+static int store_helpers(fz_ctx *c) { return c->probe.active() || !store_fork_on() ? 0 : int(c->helpers.size()); }
 static void store_fork(fz_ctx *c) {
     if (!c->ev_fork) FZ_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     FZ_HIP(hipEventRecord(c->ev_fork, c->stream));
