@@ -1227,30 +1227,37 @@ __device__ inline void shapiro_block(const double *__restrict__ v, const double 
     const stats::SwCoef cf = stats::sw_coef(n, 2.0 * summ2[0]);
     const double x0 = src[b + n / 2];
     const double range = (v[b + n - 1] - x0) - (v[b] - x0);
-    double co[PER], y[PER];
+    // value j's scaled deviation and signed coefficient (stats::sw_coef_at with the pass-A score of
+    // the mirrored index), computed again in the last pass instead of held: two PER-double arrays
+    // per thread took the kernel to 235 VGPRs (two workgroups per CU)
+    auto yc = [&](int64_t j, double &y, double &co) {
+        y = (v[j] - x0) / range;
+        const int64_t i = j - b + 1, jm = n + 1 - i, k = i < jm ? i : jm;
+        const double a = i == jm ? 0.0 : stats::sw_a_m(cf, k, s_m[k - 1]);
+        co = i == jm ? 0.0 : (i > jm ? a : -a);
+    };
     DD a1[2] = {{0.0, 0.0}, {0.0, 0.0}};
-#pragma unroll
+#pragma unroll 4
     for (int u = 0; u < PER; ++u) {
         const int64_t j = k0 + u;
-        co[u] = y[u] = 0.0;
         if (j < k1) {
-            y[u] = (v[j] - x0) / range;
-            // stats::sw_coef_at(cf, i) with the pass-A score of the mirrored index
-            const int64_t i = j - b + 1, jm = n + 1 - i, k = i < jm ? i : jm;
-            const double a = i == jm ? 0.0 : stats::sw_a_m(cf, k, s_m[k - 1]);
-            co[u] = i == jm ? 0.0 : (i > jm ? a : -a);
-            a1[0] = dd_add_d(a1[0], y[u]);
-            a1[1] = dd_add_d(a1[1], co[u]);
+            double y, co;
+            yc(j, y, co);
+            a1[0] = dd_add_d(a1[0], y);
+            a1[1] = dd_add_d(a1[1], co);
         }
     }
     double s1[2];
     block_dd_sums<2, NW>(a1, reinterpret_cast<double(&)[NW][2]>(s_hi), reinterpret_cast<double(&)[NW][2]>(s_lo), s1);
     const double sx = s1[0] / double(n), sa = s1[1] / double(n);
     DD a2[3] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
-#pragma unroll
+#pragma unroll 4
     for (int u = 0; u < PER; ++u) {
-        if (k0 + u < k1) {
-            const double asa = co[u] - sa, xsx = y[u] - sx;
+        const int64_t j = k0 + u;
+        if (j < k1) {
+            double y, co;
+            yc(j, y, co);
+            const double asa = co - sa, xsx = y - sx;
             a2[0] = dd_add_d(a2[0], asa * asa);
             a2[1] = dd_add_d(a2[1], xsx * xsx);
             a2[2] = dd_add_d(a2[2], asa * xsx);
