@@ -1630,13 +1630,18 @@ void bm_union_sorted(fz_ctx *c, const Segs &one, const double *sorted, const int
 }
 
 // spearmanr(range(n), x) and shapiro(x) of one series x[0, *d_n) of at most kSpearmanSmall values
-// in one workgroup: the keys sorted with their positions in LDS (bitonic network), then the
-// per-segment Spearman and Shapiro-Wilk passes over the sorted values in LDS.
-constexpr int kSeriesBlock = 512;
+// in one workgroup: the keys sorted with their positions by a bitonic network held in registers
+// (eight elements per thread: stages of distance 1-4 inside a thread, 8-256 by shuffles inside a
+// wave, only the 6 of distance >= 512 through LDS with barriers - the whole network in LDS took
+// 78 barrier stages, ~30 us of RQ2 count's chain), then the Spearman and Shapiro-Wilk passes over
+// the sorted values in LDS.  (Equal keys keep either order: the tie groups are ranked as groups.)
+constexpr int kSeriesBlock = 512;  // (1,024 threads spilled 120 VGPRs: the statistics' code)
+constexpr int kSeriesE = int(kSpearmanSmall) / kSeriesBlock;  // elements per thread
+static_assert(kSeriesE == 8, "series network shape");
 __global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__restrict__ x,
                                                                const int64_t *__restrict__ d_n, double *rho,
                                                                double *pv, double *w, double *wp) {
-    constexpr int BS = kSeriesBlock, NW = BS / kWave;
+    constexpr int BS = kSeriesBlock, NW = BS / kWave, E = kSeriesE;
     __shared__ uint64_t sk[kSpearmanSmall];
     __shared__ int32_t spos[kSpearmanSmall];
     __shared__ double s_tmp[NW];
@@ -1644,31 +1649,70 @@ __global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__r
     __shared__ double s_m[kSpearmanSmall / 2];
     const int tid = threadIdx.x;
     const int n = int(*d_n);
-    int np2 = 1;
-    while (np2 < n) np2 <<= 1;
-    for (int i = tid; i < np2; i += BS) {
-        sk[i] = i < n ? f64_key(x[i]) : ~0ull;
-        spos[i] = i;
+    uint64_t k[E];
+    int32_t ps[E];
+#pragma unroll
+    for (int h = 0; h < E; ++h) {
+        const int e = E * tid + h;
+        k[h] = e < n ? f64_key(x[e]) : ~0ull;
+        ps[h] = e;
     }
-    __syncthreads();
-    for (int k = 2; k <= np2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int t = tid; t < (np2 >> 1); t += BS) {
-                const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ixj = i + j;
-                const uint64_t a = sk[i], d = sk[ixj];
-                if ((a > d) == ((i & k) == 0)) {
-                    sk[i] = d;
-                    sk[ixj] = a;
-                    const int32_t q = spos[i];
-                    spos[i] = spos[ixj];
-                    spos[ixj] = q;
+    // element e = E * tid + h; stage (kk, j) pairs e with e ^ j, ascending where e & kk == 0: the
+    // lower element keeps the smaller key, the upper the larger (equal keys: each keeps its own)
+    auto settle = [&](int h, uint64_t y, int32_t yp, int kk, int j) {
+        const int e = E * tid + h;
+        const bool up = (e & kk) == 0, low = (e & j) == 0;
+        const bool take = (low == up) ? (y < k[h]) : (y > k[h]);
+        if (take) {
+            k[h] = y;
+            ps[h] = yp;
+        }
+    };
+    for (int kk = 2; kk <= int(kSpearmanSmall); kk <<= 1) {
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            if (j < E) {
+                uint64_t y[E];
+                int32_t yp[E];
+#pragma unroll
+                for (int h = 0; h < E; ++h) {
+                    y[h] = k[h ^ j];
+                    yp[h] = ps[h ^ j];
                 }
+#pragma unroll
+                for (int h = 0; h < E; ++h) settle(h, y[h], yp[h], kk, j);
+            } else if (j / E < kWave) {
+#pragma unroll
+                for (int h = 0; h < E; ++h) {
+                    const uint64_t y = __shfl_xor(k[h], j / E, 64);
+                    const int32_t yp = __shfl_xor(ps[h], j / E, 64);
+                    settle(h, y, yp, kk, j);
+                }
+            } else {
+#pragma unroll
+                for (int h = 0; h < E; ++h) {
+                    sk[E * tid + h] = k[h];
+                    spos[E * tid + h] = ps[h];
+                }
+                __syncthreads();
+                uint64_t y[E];
+                int32_t yp[E];
+#pragma unroll
+                for (int h = 0; h < E; ++h) {
+                    y[h] = sk[(E * tid + h) ^ j];
+                    yp[h] = spos[(E * tid + h) ^ j];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int h = 0; h < E; ++h) settle(h, y[h], yp[h], kk, j);
             }
-            bitonic_stage_sync(k, j, np2);
         }
     }
     double *sv = reinterpret_cast<double *>(sk);
-    for (int i = tid; i < n; i += BS) sv[i] = f64_from_key(sk[i]);
+#pragma unroll
+    for (int h = 0; h < E; ++h) {
+        sv[E * tid + h] = f64_from_key(k[h]);
+        spos[E * tid + h] = ps[h];
+    }
     __syncthreads();
     spearman_block<BS>(sv, spos, 0, n, s_tmp, rho, pv);
     const int64_t per = (int64_t(n) + BS - 1) / BS;
