@@ -452,6 +452,14 @@ __device__ inline int64_t upper_bound_d(const double *a, int64_t lo, int64_t hi,
     return lo;
 }
 
+// The special functions called once per segment by one thread, kept out of line: inlined, their
+// code set the register count of every per-segment kernel that finishes a test (the Spearman /
+// Shapiro-Wilk kernel: 175 VGPRs, two workgroups per CU)
+__device__ __noinline__ inline double t_sf_once(double t, double df) { return stats::t_sf(t, df); }
+__device__ __noinline__ inline double sw_pvalue_once(int64_t n, double w, double w1) {
+    return stats::sw_pvalue(n, w, w1);
+}
+
 // scipy.stats.spearmanr(range(n), x) of one sorted segment sv[b, b + n) (pos[j]: the source
 // position of sorted value j; ties in any order) by a workgroup of BS threads, each over a
 // contiguous run: a tie group's bounds from one binary search where it starts, the rank products
@@ -507,7 +515,7 @@ __device__ inline void spearman_block(const double *sv, const int32_t *pos, int6
             const double dof = double(n - 2);
             double q = dof / ((r + 1.0) * (1.0 - r));
             if (q < 0.0) q = 0.0;
-            p = 2.0 * stats::t_sf(fabs(r * sqrt(q)), dof);
+            p = 2.0 * t_sf_once(fabs(r * sqrt(q)), dof);
         }
         *rho = r;
         if (pval) *pval = p;

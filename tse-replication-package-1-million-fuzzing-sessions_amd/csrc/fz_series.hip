@@ -702,7 +702,7 @@ __device__ inline void rank_tests_finish(const double *s1, const double *s2, boo
     const double den = (nx * Sx) * (nx * Sx) / (nx - 1.0) + (ny * Sy) * (ny * Sy) / (ny - 1.0);
     const double df = num / den;
     if (o.bm_stat) o.bm_stat[s] = w;
-    if (o.bm_p) o.bm_p[s] = 2.0 * stats::t_sf(fabs(w), df);
+    if (o.bm_p) o.bm_p[s] = 2.0 * t_sf_once(fabs(w), df);
     if (o.nx) o.nx[s] = nx;
     if (o.ny) o.ny[s] = ny;
     // Mann-Whitney U (x vs y)
@@ -927,7 +927,7 @@ __global__ __launch_bounds__(kBlock) void k_bm_sorted_halves(const double *__res
             w /= (Nx + Ny) * sqrt(Nx * Sx + Ny * Sy);
             const double num = (Nx * Sx + Ny * Sy) * (Nx * Sx + Ny * Sy);
             const double den = (Nx * Sx) * (Nx * Sx) / (Nx - 1.0) + (Ny * Sy) * (Ny * Sy) / (Ny - 1.0);
-            pbm[i] = 2.0 * stats::t_sf(fabs(w), num / den);
+            pbm[i] = 2.0 * t_sf_once(fabs(w), num / den);
         }
     }
 }
@@ -958,7 +958,7 @@ __device__ inline double bm_pvalue(double Nx, double Ny, double rcx, double rcy,
     w /= (Nx + Ny) * sqrt(Nx * Sx + Ny * Sy);
     const double num = (Nx * Sx + Ny * Sy) * (Nx * Sx + Ny * Sy);
     const double den = (Nx * Sx) * (Nx * Sx) / (Nx - 1.0) + (Ny * Sy) * (Ny * Sy) / (Ny - 1.0);
-    return 2.0 * stats::t_sf(fabs(w), num / den);
+    return 2.0 * t_sf_once(fabs(w), num / den);
 }
 
 // Brunner-Munzel of sessions whose sorted halves hold up to MAXN values together (config 3: ~10^4
@@ -1160,7 +1160,7 @@ void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, 
             double q = dof / ((r + 1.0) * (1.0 - r));
             if (q < 0.0) q = 0.0;  // numpy clip(0); NaN stays NaN
             const double t = r * sqrt(q);
-            p = 2.0 * stats::t_sf(fabs(t), dof);
+            p = 2.0 * t_sf_once(fabs(t), dof);
         }
         rho[s] = r;
         if (pval) pval[s] = p;
@@ -1276,7 +1276,7 @@ __device__ inline void shapiro_block(const double *__restrict__ v, const double 
         const double w1 = (ssassx - sax) * (ssassx + sax) / (ssa * ssx);
         const double ww = 1.0 - w1;
         *w_out = ww;
-        *p_out = stats::sw_pvalue(n, ww, w1);
+        *p_out = sw_pvalue_once(n, ww, w1);
     }
 }
 
@@ -1465,7 +1465,7 @@ __device__ inline void bm_finish(int64_t nx_, int64_t ny_, const double *s0, con
     const double num = (nx * Sx + ny * Sy) * (nx * Sx + ny * Sy);
     const double den = (nx * Sx) * (nx * Sx) / (nx - 1.0) + (ny * Sy) * (ny * Sy) / (ny - 1.0);
     if (bm_stat) *bm_stat = w;
-    if (bm_p) *bm_p = 2.0 * stats::t_sf(fabs(w), num / den);
+    if (bm_p) *bm_p = 2.0 * t_sf_once(fabs(w), num / den);
 }
 
 template <int PASS>
@@ -1782,7 +1782,7 @@ void spearman_index_sorted(fz_ctx *c, const ChunkedSegs &cs, const int32_t *segi
                 double q = dof / ((r + 1.0) * (1.0 - r));
                 if (q < 0.0) q = 0.0;
                 const double t = r * sqrt(q);
-                p = 2.0 * stats::t_sf(fabs(t), dof);
+                p = 2.0 * t_sf_once(fabs(t), dof);
             }
             rho[s] = r;
             if (pval) pval[s] = p;
@@ -1867,7 +1867,7 @@ void seg_shapiro(fz_ctx *c, const ChunkedSegs &cs, const double *src, const Sort
         const double w1 = (ssassx - sax) * (ssassx + sax) / (ssa * ssx);
         const double ww = 1.0 - w1;
         w[s] = ww;
-        p[s] = stats::sw_pvalue(n, ww, w1);
+        p[s] = sw_pvalue_once(n, ww, w1);
     });
 }
 
