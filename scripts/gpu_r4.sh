@@ -71,6 +71,8 @@ for s in $STEPS; do
       st=20; [ "$cfg" != c2 ] && st=10
       timeout -k 10 400 python -u bench.py --config $cfg --steps $st --warmup 2 --no-cpu-baseline --probe-steps 0 $extra > $O/${T}_sho.json 2> $O/${T}_sho.err || exit $?
       python3 -c "import json; d=json.loads([l for l in open('$O/${T}_sho.json') if l.startswith('{')][-1]); print('sho $cfg $n $ord', d['ms_per_step'], d['config'].get('driver_host_ms'), flush=True)" ;;
+    storeab)  # the store build with and without its helper fork (FZ_STORE_FORK), scripts/store_ab.sh
+      CONFIG=$arg timeout -k 10 900 bash scripts/store_ab.sh > $O/${T}_storeab_$arg.txt 2>&1 || exit $?; cat $O/${T}_storeab_$arg.txt ;;
     ab)  # same-box A/B of library variants: ab:<name>+<name>... (base = lib/libfz.so), BENCH_ARGS
       VARIANTS="${arg//+/ }" timeout -k 10 900 bash scripts/bench_ab.sh > $O/${T}_ab.txt 2>&1 || exit $?; cat $O/${T}_ab.txt ;;
     envb)  # bench line under one runtime environment variable: envb:<cfg>@VAR=VALUE
