@@ -136,11 +136,15 @@ __global__ __launch_bounds__(kSortBlock) void k_store_views(const ViewSrc v, int
 // Used only while no probe window is open (the probes bracket launches on the context's own
 // stream).  fork: every helper's stream waits for the work enqueued on c so far; join: c waits
 // for everything enqueued on the helpers.
-// (FZ_STORE_FORK=0: no fork - the same-box A/B of the store's helper streams)
+// The fork onto the helpers is off by default: same-box A/B at config 2 (scripts/store_ab.sh,
+// profiles/r05_c2_store_fork_ab.txt) - the store alone 0.473 / 0.476 ms with the fork, 0.476 /
+// 0.475 without; the whole step 1.202 / 1.206 with, 1.173 / 1.176 without (the helpers are the
+// analysis groups' streams: the store's cross-stream waits delay their graphs).  FZ_STORE_FORK=1
+// turns it on.
 static bool store_fork_on() {
     static const bool on = [] {
         const char *e = std::getenv("FZ_STORE_FORK");
-        return !e || std::atoi(e) != 0;
+        return e && std::atoi(e) != 0;
     }();
     return on;
 }
