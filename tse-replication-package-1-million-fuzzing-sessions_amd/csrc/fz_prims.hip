@@ -2184,6 +2184,62 @@ __device__ inline DD block_dd_sum_sel(DD acc, double *s_hi, double *s_lo) {
     return t;
 }
 constexpr int64_t kSelLds = 12288;  // samples of up to this many values are staged in LDS (96 KiB of keys)
+
+// Sort the staged keys s[0, kSelBlock * E) ascending (entries at >= n read as ~0) by a bitonic
+// network held in registers: E keys per thread, stages of distance < E inside a thread, < 64 E by
+// shuffles inside a wave, only the 6 longest through LDS.  (Samples of <= 8,192 values: their
+// order statistics straight off the sorted keys - the selection's histogram and narrowing rounds
+// took 18-33 us per describe at config 2, four describes on the analyses' chains.)
+template <int E>
+__device__ inline void wg_bitonic_keys(uint64_t *s, int64_t n) {
+    const int tid = threadIdx.x;
+    uint64_t k[E];
+#pragma unroll
+    for (int h = 0; h < E; ++h) {
+        const int e = E * tid + h;
+        k[h] = e < n ? s[e] : ~0ull;
+    }
+    __syncthreads();
+    for (int kk = 2; kk <= kSelBlock * E; kk <<= 1) {
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            if (j < E) {
+#pragma unroll
+                for (int h = 0; h < E; ++h) {
+                    if (h & j) continue;
+                    const bool up = ((E * tid + h) & kk) == 0;
+                    const uint64_t a = k[h], b = k[h | j];
+                    if ((a > b) == up) {
+                        k[h] = b;
+                        k[h | j] = a;
+                    }
+                }
+                continue;
+            }
+            uint64_t y[E];
+            if (j / E < kWave) {
+#pragma unroll
+                for (int h = 0; h < E; ++h) y[h] = __shfl_xor(k[h], j / E, 64);
+            } else {
+#pragma unroll
+                for (int h = 0; h < E; ++h) s[E * tid + h] = k[h];
+                __syncthreads();
+#pragma unroll
+                for (int h = 0; h < E; ++h) y[h] = s[(E * tid + h) ^ j];
+                __syncthreads();
+            }
+#pragma unroll
+            for (int h = 0; h < E; ++h) {
+                const int e = E * tid + h;
+                const bool up = (e & kk) == 0, low = (e & j) == 0;
+                const uint64_t mn = k[h] < y[h] ? k[h] : y[h], mx = k[h] < y[h] ? y[h] : k[h];
+                k[h] = (low == up) ? mn : mx;
+            }
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < E; ++h) s[E * tid + h] = k[h];
+    __syncthreads();
+}
 __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
     constexpr int NW = kSelBlock / kWave;
     __shared__ SelShared sh;
@@ -2257,8 +2313,16 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
         sh.rank[6] = c_lt0 > 0 ? 0 : (c_le0 < n ? c_le0 : 0);
     }
     __syncthreads();
-    if (staged) wg_select_global([&](int64_t i) { return s_keys[i]; }, n, lo, hi, 7, sh);
-    else wg_select_global([=](int64_t i) { return f64_key(x[i]); }, n, lo, hi, 7, sh);
+    if (n <= int64_t(kSelBlock) * 16) {  // (the keys are staged: kSelLds >= 8,192)
+        if (n <= int64_t(kSelBlock) * 8) wg_bitonic_keys<8>(s_keys, n);
+        else wg_bitonic_keys<16>(s_keys, n);
+        if (tid < 7) sh.res[tid] = s_keys[sh.rank[tid]];
+        __syncthreads();
+    } else if (staged) {
+        wg_select_global([&](int64_t i) { return s_keys[i]; }, n, lo, hi, 7, sh);
+    } else {
+        wg_select_global([=](int64_t i) { return f64_key(x[i]); }, n, lo, hi, 7, sh);
+    }
     DESC_STAMP(8);
     if (tid != 0) return;
     auto get = [&](int64_t j) {
