@@ -2397,6 +2397,19 @@ void describe_f64_dn_batch(fz_ctx *c, const DescJob *jobs, int njobs) {
     if (nb > 0) describe_sorted_dn_batch(c, big, nb);
 }
 
+void describe_sorted_dn_finish(fz_ctx *c, const SortedDescJob *jobs, int njobs, const double *ms) {
+    FZ_CHECK(njobs >= 1 && njobs <= kDescBatch, "sorted describe batch size");
+    SortedDescArgs a{};
+    for (int i = 0; i < njobs; ++i) {
+        a.k[i] = jobs[i].k;
+        a.x[i] = jobs[i].x;
+        a.d_n[i] = jobs[i].d_n;
+        a.out[i] = jobs[i].out;
+    }
+    k_describe_finish<<<njobs, 64, 0, c->stream>>>(a, ms);
+    FZ_LAUNCH_CHECK();
+}
+
 void describe_sorted_dn(fz_ctx *c, const uint64_t *k, const double *x, int64_t nmax, const int64_t *d_n,
                         fz_describe *dev_out) {
     const SortedDescJob j{k, x, nmax, d_n, dev_out};

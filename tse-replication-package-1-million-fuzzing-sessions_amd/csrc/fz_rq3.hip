@@ -232,8 +232,10 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
 // the two samples are segments {0, nd, nd + nn} (oseg) of the union v (their sums do not depend on
 // order) and of cat (the union partitioned by sample, each part ascending: medians, A2 terms).
 // Written only when both samples are non-empty.
+// (ms: the two samples' describe moments from the same sums - mean = sum x / n, sqrt(sum of squared
+// deviations / n) - so the describes need no double-double passes of their own)
 static void sample_tests(fz_ctx *c, const double *v, const double *cat, int64_t cap, const int64_t *oseg,
-                         double *tests) {
+                         double *tests, double *ms) {
     const Segs two{2, oseg, cap};
     const ChunkedSegs cs = chunked(c, two);
     // sample s's median from its sorted part of cat (computed where it is used: no launch of its own)
@@ -281,6 +283,11 @@ static void sample_tests(fz_ctx *c, const double *v, const double *cat, int64_t 
 #endif
     map_n(c, 1, nullptr, [=] __device__(int64_t) {
         const double nx = double(oseg[1] - oseg[0]), ny = double(oseg[2] - oseg[1]);
+        for (int s = 0; s < 2; ++s) {
+            const double ns = s ? ny : nx;
+            ms[2 * s] = ns > 0.0 ? r1[2 * s] / ns : NAN;
+            ms[2 * s + 1] = ns > 0.0 ? sqrt(r2[2 * s] / ns) : NAN;
+        }
         if (!(nx > 0.0 && ny > 0.0)) return;
         const double av[5] = {0.576, 0.656, 0.787, 0.918, 1.092};
         for (int s = 0; s < 2; ++s) {
@@ -365,11 +372,14 @@ void rq3_stats(fz_ctx *c, const double *det_pct, const int64_t *det_tot, int64_t
             }
         });
     }
-    const SortedDescJob jobs[2] = {{skd, det_pct, NI, d_nd, describe}, {skn, non_pct, NC, d_nn, describe + 1}};
-    describe_sorted_dn_batch(c, jobs, 2);
     const DescJob tot{dtot_f, NI, d_nd, describe + 2};  // (by selection: no sort of its own)
     describe_f64_dn_batch(c, &tot, 1);
-    sample_tests(c, v, cat, cap, oseg, tests);
+    // the samples' describes: their order statistics off the sorted keys, mean / std from the
+    // Levene / Anderson-Darling sums (sample_tests) - one finishing launch
+    double *ms = c->arena.get<double>(4);
+    sample_tests(c, v, cat, cap, oseg, tests, ms);
+    const SortedDescJob jobs[2] = {{skd, det_pct, NI, d_nd, describe}, {skn, non_pct, NC, d_nn, describe + 1}};
+    describe_sorted_dn_finish(c, jobs, 2, ms);
 }
 
 }  // namespace fz

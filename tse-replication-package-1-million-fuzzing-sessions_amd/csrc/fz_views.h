@@ -724,6 +724,9 @@ struct SortedDescArgs {
     fz_describe *out[kDescBatch];
 };
 void describe_sorted_dn_batch(fz_ctx *c, const SortedDescJob *jobs, int njobs);
+// The same with each job's mean and standard deviation given (ms[2j], ms[2j + 1] = sqrt(sum of
+// squared deviations / n)): only the finishing launch.
+void describe_sorted_dn_finish(fz_ctx *c, const SortedDescJob *jobs, int njobs, const double *ms);
 // ascending order-preserving keys (f64_key) of x[0..*d_n); entries past *d_n are ~0.
 uint64_t *sorted_keys_dn(fz_ctx *c, const double *x, int64_t nmax, const int64_t *d_n);
 // the same for nmax <= 4096 in one workgroup (LDS bitonic network, fz_series.hip)
