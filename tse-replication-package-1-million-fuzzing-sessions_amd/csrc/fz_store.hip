@@ -136,19 +136,27 @@ __global__ __launch_bounds__(kSortBlock) void k_store_views(const ViewSrc v, int
 // Used only while no probe window is open (the probes bracket launches on the context's own
 // stream).  fork: every helper's stream waits for the work enqueued on c so far; join: c waits
 // for everything enqueued on the helpers.
-// The fork onto the helpers is off by default: same-box A/B at config 2 (scripts/store_ab.sh,
+// The fork onto the helpers only for large tables: same-box A/B at config 2 (scripts/store_ab.sh,
 // profiles/r05_c2_store_fork_ab.txt) - the store alone 0.473 / 0.476 ms with the fork, 0.476 /
 // 0.475 without; the whole step 1.202 / 1.206 with, 1.173 / 1.176 without (the helpers are the
-// analysis groups' streams: the store's cross-stream waits delay their graphs).  FZ_STORE_FORK=1
-// turns it on.
-static bool store_fork_on() {
-    static const bool on = [] {
+// analysis groups' streams: the store's cross-stream waits delay their graphs); configs 3 / 5
+// (1e8 rows: the eligibility pass, ~0.4 ms, beside the prefix sort, the time-sort classes side by
+// side) 13.1 / 17.8 ms with it, 14.0 / 19.6 without.  FZ_STORE_FORK=1 / 0 forces it on / off.
+constexpr int64_t kForkMinRows = int64_t(1) << 22;
+static int store_fork_mode() {  // -1: by size, 0: off, 1: on
+    static const int m = [] {
         const char *e = std::getenv("FZ_STORE_FORK");
-        return e && std::atoi(e) != 0;
+        return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
     }();
-    return on;
+    return m;
 }
-static int store_helpers(fz_ctx *c) { return c->probe.active() || !store_fork_on() ? 0 : int(c->helpers.size()); }
+static int store_helpers(fz_ctx *c) {
+    if (c->probe.active()) return 0;
+    const int m = store_fork_mode();
+    const fz_tables &t = store_of(c).t;
+    const bool big = t.n_builds + t.n_cov + t.n_issues >= kForkMinRows;
+    return (m == 1 || (m < 0 && big)) ? int(c->helpers.size()) : 0;
+}
 static void store_fork(fz_ctx *c) {
     if (!c->ev_fork) FZ_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     FZ_HIP(hipEventRecord(c->ev_fork, c->stream));
