@@ -22,8 +22,11 @@ def main():
     sizes = [int(x) for x in os.environ.get("SIZES", "262144,650000,1000000,4000000,16000000").split(",")]
     bits = int(os.environ.get("BITS", "32"))
     reps = int(os.environ.get("REPS", "10"))
+    probe = os.environ.get("PROBE", "radix_scatter")
     rng = np.random.default_rng(1)
     data = {n: rng.integers(0, 1 << bits, size=n, dtype=np.uint64) for n in sizes}
+    if os.environ.get("KIND") == "sorted":
+        data = {n: np.sort(v) for n, v in data.items()}
     for name in names:
         eng = E.Engine(0, lib_path=os.path.join(VDIR, f"libfz_{name}.so"))
         torch = eng.torch
@@ -42,7 +45,7 @@ def main():
                 if not ok:
                     row[str(n)] = "MISMATCH"
                     continue
-            eng.probe_begin("radix_scatter")
+            eng.probe_begin(probe)
             for _ in range(reps):
                 dk.copy_(dk0)
                 dv.copy_(dv0)
@@ -50,7 +53,7 @@ def main():
             eng.synchronize()
             launches, ms, nbytes = eng.probe_end()
             us = ms / launches * 1e3
-            row[str(n)] = {"us_per_pass": round(us, 2), "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1)}
+            row[str(n)] = {"launches": launches // reps, "us_per_pass": round(us, 2), "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1)}
         print(json.dumps(row), flush=True)
         eng.close()
 
