@@ -94,6 +94,13 @@ for s in $STEPS; do
       cfg=${arg%%@*}; groups=${arg#*@}
       timeout -k 10 600 python -u bench.py --config $cfg --steps 20 --warmup 2 --no-cpu-baseline --probe-steps 0 --groups "$groups" > $O/${T}_grp.json 2> $O/${T}_grp.err || exit $?
       python3 -c "import json; d=json.loads([l for l in open('$O/${T}_grp.json') if l.startswith('{')][-1]); print('grp $cfg $groups', d['ms_per_step'], flush=True)" ;;
+    micro)  # radix micro-benchmark over library variants: micro:<v1>+<v2>... (SIZES, BITS, PROBE, KIND)
+      timeout -k 10 400 python -u scripts/radix_micro.py ${arg//+/ } > $O/${T}_micro.txt 2>&1 || exit $?; cat $O/${T}_micro.txt ;;
+    smicro)  # k_series_small micro-benchmark (default build, then the FZ_SERIES_TIMING variant sertime)
+      timeout -k 10 200 python -u scripts/series_micro.py > $O/${T}_smicro.txt 2>&1 || exit $?
+      V=tse-replication-package-1-million-fuzzing-sessions_amd/csrc/build/variants/libfz_sertime.so
+      if [ -f $V ]; then timeout -k 10 200 python -u scripts/series_micro.py $V >> $O/${T}_smicro.txt 2>&1 || exit $?; fi
+      grep '^{' $O/${T}_smicro.txt ;;
     tests)
       k=""; [ "$arg" != tests ] && k="${arg//+/ or }"
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 500 --timeout-method thread ${k:+-k "$k"} > $O/${T}_pytest.log 2>&1; rc=$?

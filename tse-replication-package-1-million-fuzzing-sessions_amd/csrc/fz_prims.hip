@@ -483,6 +483,10 @@ constexpr int kHistKeysPerBlock = FZ_HIST_KPB;  // keys per histogram workgroup 
 #define FZ_HIST_MAXB 256
 #endif
 constexpr int kHistMaxBlocks = FZ_HIST_MAXB;
+#ifndef FZ_HIST_BIGB
+#define FZ_HIST_BIGB 2048
+#endif
+constexpr unsigned kHistBigBlocks = FZ_HIST_BIGB;  // (sorts of >= 4 M keys)
 constexpr int kOsGroup = 8;  // tiles per look-back group (one {tiles, sum} word per group and digit)
 
 template <typename KeyT>
@@ -880,7 +884,7 @@ static void radix_payload_impl(fz_ctx *c, KeyT *&keys, uint32_t *&vals, int64_t 
         // with global atomics, and more workgroups' adds serialised on those words; larger sorts
         // keep 2,048, the occupancy their streaming needs: capped at 256, configs 3 / 5 took 13.9 /
         // 19.4 ms instead of 13.1 / 17.8, same box)
-        const unsigned hblocks = n >= (int64_t(1) << 22) ? 2048u : unsigned(kHistMaxBlocks);
+        const unsigned hblocks = n >= (int64_t(1) << 22) ? kHistBigBlocks : unsigned(kHistMaxBlocks);
         k_onesweep_hist<KeyT><<<grid_for(n, kHistKeysPerBlock, hblocks), kBlock, 0, c->stream>>>(
             key_src ? key_src : keys, n, npass, ghist, gsum, gwords * npass, d_live);
         FZ_LAUNCH_CHECK();

@@ -223,8 +223,11 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
         out.non_tot[q] = ctot[rb] - ctot[ra];
     }, counts + FZ_RQ3_NON_DETECTED);
 
+    // (no issue at all - configs 3 / 5, coverage-only: both samples are empty whatever the coverage
+    // table holds, so the statistics run over a zero capacity instead of the 1e8-row one - the
+    // capacity-sized reduction maps walked ~1e5 empty chunks per launch)
     if (!(flags & FZ_RQ3_SKIP_STATS))
-        rq3_stats(c, o->det_pct, o->det_tot, NI, counts + FZ_RQ3_DETECTED, o->non_pct, NC,
+        rq3_stats(c, o->det_pct, o->det_tot, NI, counts + FZ_RQ3_DETECTED, o->non_pct, NI > 0 ? NC : 0,
                   counts + FZ_RQ3_NON_DETECTED, o->describe, o->tests);
 }
 

@@ -1635,6 +1635,24 @@ void bm_union_sorted(fz_ctx *c, const Segs &one, const double *sorted, const int
 // wave, only the 6 of distance >= 512 through LDS with barriers - the whole network in LDS took
 // 78 barrier stages, ~30 us of RQ2 count's chain), then the Spearman and Shapiro-Wilk passes over
 // the sorted values in LDS.  (Equal keys keep either order: the tie groups are ranked as groups.)
+#ifdef FZ_SERIES_TIMING
+// experiment builds only: wall-clock (100 MHz) phase stamps of the last k_series_small launch
+__device__ unsigned long long g_series_t[8];
+#define SERIES_STAMP(ph)                                        \
+    do {                                                        \
+        __syncthreads();                                        \
+        if (threadIdx.x == 0) g_series_t[ph] = wall_clock64(); \
+    } while (0)
+extern "C" int fz_debug_series_timing(unsigned long long *out) {
+    hipDeviceSynchronize();
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_series_t), sizeof(g_series_t));
+    return 0;
+}
+#else
+#define SERIES_STAMP(ph) \
+    do {                 \
+    } while (0)
+#endif
 constexpr int kSeriesBlock = 512;  // (1,024 threads spilled 120 VGPRs: the statistics' code)
 constexpr int kSeriesE = int(kSpearmanSmall) / kSeriesBlock;  // elements per thread
 static_assert(kSeriesE == 8, "series network shape");
@@ -1648,6 +1666,7 @@ __global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__r
     __shared__ double s_hi[NW][3], s_lo[NW][3];
     __shared__ double s_m[kSpearmanSmall / 2];
     const int tid = threadIdx.x;
+    SERIES_STAMP(0);
     const int n = int(*d_n);
     uint64_t k[E];
     int32_t ps[E];
@@ -1714,10 +1733,13 @@ __global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__r
         spos[E * tid + h] = ps[h];
     }
     __syncthreads();
+    SERIES_STAMP(1);
     spearman_block<BS>(sv, spos, 0, n, s_tmp, rho, pv);
+    SERIES_STAMP(2);
     const int64_t per = (int64_t(n) + BS - 1) / BS;
     const int64_t k0 = int64_t(tid) * per, k1 = k0 + per < n ? k0 + per : n;
     shapiro_block<BS>(sv, x, 0, n, k0, k1, s_hi, s_lo, s_m, w, wp);
+    SERIES_STAMP(3);
 }
 
 bool series_small_ok(int64_t n_cap) { return n_cap <= kSpearmanSmall; }

@@ -379,6 +379,9 @@ struct TimeSortTab {
     bool tie_pos = false;
     // rows whose columns the long class gathered itself (the probe's algorithmic bytes), or null
     unsigned long long *fused = nullptr;
+    // spos already holds kGathered for every row (time_sort_tables fills it before the class
+    // launches): flagged segments and the long class's fused rows need not write it
+    bool prefilled = false;
 };
 struct TimeSortTabs {
     TimeSortTab tab[3];
@@ -429,7 +432,8 @@ __device__ __forceinline__ void seg_time_bucket(const TimeSortTabs &T, int64_t m
         // writes them, or writes their source positions and the gather runs again)
         auto flag_segment = [&]() {
             if (tid == 0) flag_big(big, bigflag, s, len);
-            for (int64_t q = tid; q < len; q += BS) out.spos[ob + q] = kGathered;
+            if (!tb.prefilled)
+                for (int64_t q = tid; q < len; q += BS) out.spos[ob + q] = kGathered;
         };
         if (len > MAXN) {
             if (flag_longer) flag_segment();
@@ -630,7 +634,7 @@ __device__ __forceinline__ void seg_time_bucket(const TimeSortTabs &T, int64_t m
         if (tid == 0 && tb.fused) atomicAdd(tb.fused, (unsigned long long)n);
         for (int q = tid; q < n; q += BS) {
             out.oproj[ob + q] = p;
-            out.spos[ob + q] = kGathered;
+            if (!tb.prefilled) out.spos[ob + q] = kGathered;
         }
         for (int j = 0; j < nc; ++j) {
             if constexpr (kPrefetch) {
@@ -789,6 +793,9 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) 
 
 // Every segment of the three prefix-sorted tables sorted by time: one launch per length class for
 // all tables, the bigflag arrays cleared by one fill.
+#ifndef FZ_SPOS_PREFILL
+#define FZ_SPOS_PREFILL 1
+#endif
 static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
     TimeSortTabs T;
     int64_t ntot = 0;
@@ -800,7 +807,6 @@ static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
     const int64_t S = T.base[3];
     if (S == 0) return;
     uint8_t *flags = c->arena.get<uint8_t>(S);
-    dev_fill(c, flags, 0, S);
     for (int k = 0; k < 3; ++k) {
         PrefixSorted &ps = pss[k];
         if (ps.S == 0) continue;
@@ -815,7 +821,16 @@ static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
         tb.rows = ps.rows;
         tb.gc = ps.gc;
         tb.fused = ps.big + 6;  // big3[6 + k]
+        tb.prefilled = FZ_SPOS_PREFILL;
     }
+    // every row's source position starts as kGathered (one fill of all three tables): the bucket
+    // sorts overwrite the rows they sort; a segment they leave to the long-segment pass or the merge
+    // sort keeps the marker without a write of its own (a workgroup marking config 5's 20.8 M-row
+    // giant alone took ~1 ms, the long class's whole launch waiting on it)
+    // (the bigflag arrays cleared in the same launch)
+    const int64_t pf = FZ_SPOS_PREFILL ? 4 : 0;
+    fill_batch(c, {{flags, S, 0}, {pss[0].out.spos, pss[0].n * pf, 0xff}, {pss[1].out.spos, pss[1].n * pf, 0xff},
+                   {pss[2].out.spos, pss[2].n * pf, 0xff}});
     // algorithmic bytes: time 8 read; time 8 + project 4 + source position 4 written; the long
     // class also moves row id 4 + columns in, perm 4 + row 4 + columns out for its rows (added by
     // store_build once their count is read back: fused_gather_bytes)
