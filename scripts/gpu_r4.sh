@@ -98,9 +98,11 @@ for s in $STEPS; do
       timeout -k 10 400 python -u scripts/radix_micro.py ${arg//+/ } > $O/${T}_micro.txt 2>&1 || exit $?; cat $O/${T}_micro.txt ;;
     smicro)  # k_series_small micro-benchmark (default build, then the FZ_SERIES_TIMING variant sertime)
       timeout -k 10 200 python -u scripts/series_micro.py > $O/${T}_smicro.txt 2>&1 || exit $?
-      V=tse-replication-package-1-million-fuzzing-sessions_amd/csrc/build/variants/libfz_sertime.so
-      if [ -f $V ]; then timeout -k 10 200 python -u scripts/series_micro.py $V >> $O/${T}_smicro.txt 2>&1 || exit $?; fi
-      grep '^{' $O/${T}_smicro.txt ;;
+      for v in sertime sertimend; do
+        V=tse-replication-package-1-million-fuzzing-sessions_amd/csrc/build/variants/libfz_$v.so
+        if [ -f $V ]; then echo "# $v" >> $O/${T}_smicro.txt; timeout -k 10 200 python -u scripts/series_micro.py $V >> $O/${T}_smicro.txt 2>&1 || exit $?; fi
+      done
+      grep '^[{#]' $O/${T}_smicro.txt ;;
     tests)
       k=""; [ "$arg" != tests ] && k="${arg//+/ or }"
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 500 --timeout-method thread ${k:+-k "$k"} > $O/${T}_pytest.log 2>&1; rc=$?

@@ -33,6 +33,16 @@ __device__ inline void store_wt(double *p, double x) {
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Wave priority of the one-workgroup kernels that finish an analysis chain (describes, the
+// small-series tests, the finishing tables): their waves share CUs with the other streams' bulk
+// kernels; FZ_CHAIN_PRIO=1 raises their issue priority (s_setprio 3).
+#ifndef FZ_CHAIN_PRIO
+#define FZ_CHAIN_PRIO 0
+#endif
+__device__ inline void chain_prio() {
+    if constexpr (FZ_CHAIN_PRIO != 0) __builtin_amdgcn_s_setprio(3);
+}
+
 // offs[q] = v for q in [a, e] of every lane's range (a > e: none), each range stored by the whole
 // wave 64 entries a round (all 64 lanes must call it): a lane whose range spans thousands of ids -
 // the ids before a shard's first project, the gap between a table's two prefix types - no longer

@@ -1041,6 +1041,7 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_splitters(const double *__restr
                                                             unsigned long long *__restrict__ counts,
                                                             unsigned long long *__restrict__ gsum, int64_t gsum_words,
                                                             int64_t *__restrict__ d_hi) {
+    chain_prio();
     __shared__ uint64_t s[kSsSamples];
     const int tid = threadIdx.x, lane = lane_id();
     const int64_t hi = offs[1] < n_cap ? (offs[1] > 0 ? offs[1] : 0) : n_cap;
@@ -1055,7 +1056,10 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_splitters(const double *__restr
         x[h] = hi > 0 ? f64_key(src[(int64_t(j) * hi) / kSsSamples]) : ~0ull;
     }
     // bitonic network: element e = 2t + h; stage (k, j) pairs e with e ^ j, ascending where e & k == 0
+    // (unrolled: each stage's kind - in-thread, shuffle or LDS - is resolved at compile time)
+#pragma unroll
     for (int k = 2; k <= kSsSamples; k <<= 1) {
+#pragma unroll
         for (int j = k >> 1; j > 0; j >>= 1) {
             uint64_t y[2];
             if (j == 1) {
@@ -1761,6 +1765,7 @@ __device__ void describe_from_sorted(const uint64_t *sk, int64_t n, double mean,
 }
 
 __global__ void k_describe_finish(SortedDescArgs a, const double *__restrict__ ms) {
+    chain_prio();
     const int j = blockIdx.x, lane = threadIdx.x;
     const uint64_t *sk = a.k[j];
     const int64_t n = *a.d_n[j];
@@ -2207,7 +2212,10 @@ __device__ inline void wg_bitonic_keys(uint64_t *s, int64_t n) {
         k[h] = e < n ? s[e] : ~0ull;
     }
     __syncthreads();
+    // (unrolled: constant distances, direct register indexing in the in-thread stages)
+#pragma unroll
     for (int kk = 2; kk <= kSelBlock * E; kk <<= 1) {
+#pragma unroll
         for (int j = kk >> 1; j > 0; j >>= 1) {
             if (j < E) {
 #pragma unroll
@@ -2248,6 +2256,7 @@ __device__ inline void wg_bitonic_keys(uint64_t *s, int64_t n) {
     __syncthreads();
 }
 __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
+    chain_prio();
     constexpr int NW = kSelBlock / kWave;
     __shared__ SelShared sh;
     __shared__ uint64_t s_keys[kSelLds];

@@ -98,6 +98,7 @@ __global__ __launch_bounds__(kFinBlock) void k_rq4a_finish_small(int64_t M, int6
                                                                 const int64_t *__restrict__ intro, int64_t *counts,
                                                                 double *__restrict__ rates, double *__restrict__ after,
                                                                 double *__restrict__ iv, int64_t *__restrict__ d_np) {
+    chain_prio();
     __shared__ int64_t s_tmp[kFinWaves];
     __shared__ unsigned long long s_rows, s_first[2];
     const int tid = threadIdx.x;
@@ -569,6 +570,7 @@ __global__ __launch_bounds__(kTrendBlock) void k_rq4b_trends_small(const int64_t
                                                                   const double *__restrict__ g2q,
                                                                   const double *__restrict__ g1q, int64_t MM,
                                                                   int64_t *__restrict__ last, double *__restrict__ sp) {
+    chain_prio();
     __shared__ uint64_t sk[kTrendSmall];
     __shared__ int32_t spos[kTrendSmall];
     __shared__ double s_tmp[kTrendBlock / kWave];

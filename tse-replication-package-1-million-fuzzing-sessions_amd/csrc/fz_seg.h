@@ -463,11 +463,19 @@ __device__ __noinline__ inline double sw_pvalue_once(int64_t n, double w, double
 // scipy.stats.spearmanr(range(n), x) of one sorted segment sv[b, b + n) (pos[j]: the source
 // position of sorted value j; ties in any order) by a workgroup of BS threads, each over a
 // contiguous run: a tie group's bounds from one binary search where it starts, the rank products
-// summed directly (exact half-integer sums).  Thread 0 writes *rho and *pval (when non-null).
-// s_tmp: BS / 64 doubles.
+// summed directly (exact half-integer sums).  Thread 0 writes *rho and *pval (when non-null);
+// with defer_p the p-value is left to the caller (spearman_p of the returned t statistic, every
+// thread holds it): a kernel that also runs Shapiro-Wilk computes the two p-values on different
+// waves after both passes instead of one after the other.  s_tmp: BS / 64 doubles.
+struct SpearmanT {
+    double t = 0.0, dof = -1.0;  // dof < 0: no p-value (NaN)
+};
+__device__ inline double spearman_p(const SpearmanT &st) {
+    return st.dof < 0.0 ? NAN : 2.0 * t_sf_once(fabs(st.t), st.dof);
+}
 template <int BS>
-__device__ inline void spearman_block(const double *sv, const int32_t *pos, int64_t b, int64_t n, double *s_tmp,
-                                      double *rho, double *pval) {
+__device__ inline SpearmanT spearman_block(const double *sv, const int32_t *pos, int64_t b, int64_t n, double *s_tmp,
+                                           double *rho, double *pval, bool defer_p = false) {
     constexpr int NW = BS / kWave;
     const double m = double(n + 1) / 2.0;
     double sxy = 0.0, sxx = 0.0, syy = 0.0, ng = 0.0;
@@ -505,21 +513,23 @@ __device__ inline void spearman_block(const double *sv, const int32_t *pos, int6
     sxx = bsum(sxx);
     syy = bsum(syy);
     ng = bsum(ng);
-    if (threadIdx.x == 0) {
-        double r = NAN, p = NAN;
-        if (n >= 2 && ng > 1.0) {  // as seg_spearman_index
-            const double f = 1.0 / double(n - 1);  // (np.cov: times the reciprocal of n - 1)
-            r = (sxy * f) / sqrt(sxx * f) / sqrt(syy * f);
-            if (r > 1.0) r = 1.0;
-            if (r < -1.0) r = -1.0;
-            const double dof = double(n - 2);
-            double q = dof / ((r + 1.0) * (1.0 - r));
-            if (q < 0.0) q = 0.0;
-            p = 2.0 * t_sf_once(fabs(r * sqrt(q)), dof);
-        }
-        *rho = r;
-        if (pval) *pval = p;
+    double r = NAN;
+    SpearmanT st;
+    if (n >= 2 && ng > 1.0) {  // as seg_spearman_index
+        const double f = 1.0 / double(n - 1);  // (np.cov: times the reciprocal of n - 1)
+        r = (sxy * f) / sqrt(sxx * f) / sqrt(syy * f);
+        if (r > 1.0) r = 1.0;
+        if (r < -1.0) r = -1.0;
+        st.dof = double(n - 2);
+        double q = st.dof / ((r + 1.0) * (1.0 - r));
+        if (q < 0.0) q = 0.0;
+        st.t = r * sqrt(q);
     }
+    if (threadIdx.x == 0) {
+        *rho = r;
+        if (pval && !defer_p) *pval = spearman_p(st);
+    }
+    return st;
 }
 
 struct RankTestOut {

@@ -1172,6 +1172,10 @@ void seg_spearman_index(fz_ctx *c, const ChunkedSegs &cs, const SortedSegs &ss, 
 // a tie group's bounds come from one binary search when it starts, and the rank products are summed
 // directly - the same exact half-integer sums as seg_spearman_index, without the device-wide tie
 // rank passes.
+#ifndef FZ_SERIES_DEFER
+#define FZ_SERIES_DEFER 1
+#endif
+constexpr bool kSeriesDefer = FZ_SERIES_DEFER;
 constexpr int64_t kSpearmanSmall = 4096;  // <= 16 values per thread: longer runs are latency chains
 
 // Double-double sums of NV per-thread partials over the workgroup (NW waves), the rounded results
@@ -1296,9 +1300,16 @@ __global__ __launch_bounds__(kBlock) void k_spearman_index_small(const double *_
         const int64_t b = offs[s], n = offs[s + 1] - b;
         const int64_t per = (n + kBlock - 1) / kBlock;
         const int64_t k0 = b + int64_t(threadIdx.x) * per, k1 = k0 + per < b + n ? k0 + per : b + n;
-        if (sw_w) shapiro_block(sv, src, b, n, k0, k1, s_hi, s_lo, s_m, sw_w + s, sw_p + s);
-        if (!rho) continue;
-        spearman_block<kBlock>(sv, pos, b, n, s_tmp, rho + s, pval ? pval + s : nullptr);
+        if (!kSeriesDefer || !sw_w || !rho) {
+            if (sw_w) shapiro_block(sv, src, b, n, k0, k1, s_hi, s_lo, s_m, sw_w + s, sw_p + s);
+            if (rho) spearman_block<kBlock>(sv, pos, b, n, s_tmp, rho + s, pval ? pval + s : nullptr);
+            continue;
+        }
+        // both: the Spearman sums first, then Shapiro-Wilk, the two p-values on different waves
+        // (thread 0: Shapiro-Wilk's, the last thread: Spearman's)
+        const SpearmanT st = spearman_block<kBlock>(sv, pos, b, n, s_tmp, rho + s, pval ? pval + s : nullptr, true);
+        shapiro_block(sv, src, b, n, k0, k1, s_hi, s_lo, s_m, sw_w + s, sw_p + s);
+        if (pval && threadIdx.x == kBlock - 1) pval[s] = spearman_p(st);
     }
 }
 
@@ -1659,6 +1670,7 @@ static_assert(kSeriesE == 8, "series network shape");
 __global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__restrict__ x,
                                                                const int64_t *__restrict__ d_n, double *rho,
                                                                double *pv, double *w, double *wp) {
+    chain_prio();
     constexpr int BS = kSeriesBlock, NW = BS / kWave, E = kSeriesE;
     __shared__ uint64_t sk[kSpearmanSmall];
     __shared__ int32_t spos[kSpearmanSmall];
@@ -1670,11 +1682,19 @@ __global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__r
     const int n = int(*d_n);
     uint64_t k[E];
     int32_t ps[E];
+    {  // (all E loads in flight at once: a guarded load per element waited on each in turn)
+        double v[E];
 #pragma unroll
-    for (int h = 0; h < E; ++h) {
-        const int e = E * tid + h;
-        k[h] = e < n ? f64_key(x[e]) : ~0ull;
-        ps[h] = e;
+        for (int h = 0; h < E; ++h) {
+            const int e = E * tid + h;
+            v[h] = n > 0 ? x[e < n ? e : 0] : 0.0;
+        }
+#pragma unroll
+        for (int h = 0; h < E; ++h) {
+            const int e = E * tid + h;
+            k[h] = e < n ? f64_key(v[h]) : ~0ull;
+            ps[h] = e;
+        }
     }
     // element e = E * tid + h; stage (kk, j) pairs e with e ^ j, ascending where e & kk == 0: the
     // lower element keeps the smaller key, the upper the larger (equal keys: each keeps its own)
@@ -1687,7 +1707,11 @@ __global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__r
             ps[h] = yp;
         }
     };
+    // (both loops unrolled: every stage's distance is a constant - the in-thread stages index
+    // registers directly instead of through indirect register moves)
+#pragma unroll
     for (int kk = 2; kk <= int(kSpearmanSmall); kk <<= 1) {
+#pragma unroll
         for (int j = kk >> 1; j > 0; j >>= 1) {
             if (j < E) {
                 uint64_t y[E];
@@ -1734,11 +1758,13 @@ __global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__r
     }
     __syncthreads();
     SERIES_STAMP(1);
-    spearman_block<BS>(sv, spos, 0, n, s_tmp, rho, pv);
+    const SpearmanT st = spearman_block<BS>(sv, spos, 0, n, s_tmp, rho, pv, kSeriesDefer);
     SERIES_STAMP(2);
     const int64_t per = (int64_t(n) + BS - 1) / BS;
     const int64_t k0 = int64_t(tid) * per, k1 = k0 + per < n ? k0 + per : n;
     shapiro_block<BS>(sv, x, 0, n, k0, k1, s_hi, s_lo, s_m, w, wp);
+    // (the Spearman p-value on the last wave while thread 0 finishes the Shapiro-Wilk one)
+    if (kSeriesDefer && pv && tid == BS - 1) *pv = spearman_p(st);
     SERIES_STAMP(3);
 }
 
@@ -2596,6 +2622,7 @@ __global__ __launch_bounds__(kTwoBlock) void k_two_sample_small(const double *__
                                                                const int64_t *__restrict__ d_nx,
                                                                const double *__restrict__ yin,
                                                                const int64_t *__restrict__ d_ny, TwoSmallOut o) {
+    chain_prio();
     constexpr int NW = kTwoBlock / kWave;
     __shared__ uint64_t sk[2 * kTwoSmall];  // x's keys in [0, np2), y's in [np2, 2 np2); then the values
     __shared__ double s_hi[NW][6], s_lo[NW][6];
