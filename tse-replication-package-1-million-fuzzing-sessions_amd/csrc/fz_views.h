@@ -131,8 +131,16 @@ struct FcShared {
     int64_t prefix;
     unsigned int tile;
     int skip;
-    int64_t p0;
+    int64_t p0, p1;  // (VIRT) the selected segments holding the tile's first and last virtual rows
 };
+// (VIRT) a tile whose rows span at most this many segments (empty ones included) stages their
+// virtual offsets in LDS (in sh.pos, before it holds the keep flags): an item crossing into a
+// later segment searches LDS instead of the [P + 1] offsets in global memory - a tile of the Zipf
+// tail's small projects crossed on nearly every item, 14 dependent global loads a crossing
+#ifndef FZ_FC_VOFF_LDS
+#define FZ_FC_VOFF_LDS 1
+#endif
+constexpr int kFcVoffLds = FZ_FC_VOFF_LDS ? kFcTile / 2 - 1 : 0;
 // What a filter writes for kept row q (its rank among the kept rows): by default the view row's
 // store row id, time and project (a TmpView); an analysis may pass its own emitter to write what
 // it reads next straight from the row (e.g. RQ2 count's trend value), instead of a (row, time,
@@ -206,6 +214,7 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT, Emit> &J, int6
         if (VIRT) {  // the selected segment holding the tile's first virtual row
             int64_t p = 0;
             sh.p0 = (b0 < b1) ? (sel.phys(b0, p), p) : 0;
+            sh.p1 = (b0 < b1) ? (sel.phys(b1 - 1, p), p) : 0;  // (p: from the first row's segment on)
             sh.skip = 0;
             int64_t q = 0;
             sh.pprev = (b0 > 0 && b0 < b1) ? (sel.phys(b0 - 1, q), q) : -1;
@@ -229,7 +238,14 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT, Emit> &J, int6
     if constexpr (VIRT) {
         // the current segment's end and view shift kept in registers: a load only when an item
         // crosses into a later segment (not three dependent loads per item)
-        int64_t p = sh.p0;
+        const int64_t p0 = sh.p0, nseg = sh.p1 - p0 + 1;
+        int64_t *const s_voff = reinterpret_cast<int64_t *>(sh.pos);  // voff[p0 .. p1 + 1]
+        const bool staged = base < lim && nseg > 1 && nseg + 1 <= kFcVoffLds;  // (block-uniform)
+        if (staged) {
+            for (int64_t q = tid; q <= nseg; q += kFcBlock) s_voff[q] = sel.voff[p0 + q];
+            __syncthreads();
+        }
+        int64_t p = p0;
         int64_t vend = 0, shift = 0;
         if (base < lim) {
             vend = sel.voff[p + 1];
@@ -241,13 +257,26 @@ __device__ inline void filter_tile(const FcJob<Pred, Count, VIRT, Emit> &J, int6
             pidx[i] = 0;
             if (v < lim) {
                 if (v >= vend) {
-                    sel.phys(v, p);
-                    vend = sel.voff[p + 1];
-                    shift = sel.view_offs[p] - sel.voff[p];
+                    if (staged) {  // last q in (p - p0, nseg) with voff[p0 + q] <= v, in LDS
+                        int64_t lo = p - p0 + 1, hi = nseg - 1;
+                        while (lo < hi) {
+                            const int64_t mid = (lo + hi + 1) >> 1;
+                            if (s_voff[mid] <= v) lo = mid;
+                            else hi = mid - 1;
+                        }
+                        p = p0 + lo;
+                        vend = s_voff[lo + 1];
+                        shift = sel.view_offs[p] - s_voff[lo];
+                    } else {
+                        sel.phys(v, p);
+                        vend = sel.voff[p + 1];
+                        shift = sel.view_offs[p] - sel.voff[p];
+                    }
                 }
                 pidx[i] = int32_t(v + shift);
             }
         }
+        if (staged) __syncthreads();  // (sh.pos is the keep flags' next)
     }
     auto row_at = [&](int i) -> int64_t {
         if constexpr (VIRT) return pidx[i];
