@@ -793,6 +793,10 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) 
 
 // Every segment of the three prefix-sorted tables sorted by time: one launch per length class for
 // all tables, the bigflag arrays cleared by one fill.
+#ifndef FZ_TS_MID
+#define FZ_TS_MID 1
+#endif
+constexpr bool kTsMid = FZ_TS_MID;  // the 12,288-row time-sort class
 #ifndef FZ_SPOS_PREFILL
 #define FZ_SPOS_PREFILL 1
 #endif
@@ -853,7 +857,13 @@ static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
     // (a workgroup per CU at most; fewer when the tables are too small to hold many long segments)
     const int64_t g16 = ntot / 16384 < 8 ? 8 : (ntot / 16384 > 256 ? 256 : ntot / 16384);
 #if FZ_LONG_FUSE
-    k_seg_time_bucket<1024, 16384><<<unsigned(S < g16 ? S : g16), 1024, 0, st(3)>>>(T, 4096, true);
+    if (kTsMid) {
+        // 4,097-12,288 rows at 12 rows per thread: the 16-row class needs 128 VGPRs and spilled 29
+        // of them to scratch; longer segments take the 16-row class after it (same stream)
+        k_seg_time_bucket<1024, 12288><<<unsigned(S < g16 ? S : g16), 1024, 0, st(3)>>>(T, 4096, false);
+        FZ_LAUNCH_CHECK();
+    }
+    k_seg_time_bucket<1024, 16384><<<unsigned(S < g16 ? S : g16), 1024, 0, st(3)>>>(T, kTsMid ? 12288 : 4096, true);
 #else
     k_seg_time_bucket2<1024, 16384><<<unsigned(S < 2 * g16 ? S : 2 * g16), 1024, 0, st(3)>>>(T, 4096, true);
 #endif
@@ -1192,7 +1202,11 @@ static bool big_segments_bucketed(fz_ctx *c, const PrefixSorted &ps, int64_t big
         // columns written (the gather is fused)
         ProbeScope probe(c, "big_sub_sort", (32.0 + 2.0 * ps.gc.bytes()) * double(ncomp));
         const unsigned g16 = unsigned(nsubs < 256 ? nsubs : 256);
-        k_seg_time_bucket<1024, 16384><<<g16, 1024, 0, c->stream>>>(T, 0, true);
+        if (kTsMid) {  // (sub-buckets of <= 12,288 rows in the class without spills, then the rest)
+            k_seg_time_bucket<1024, 12288><<<g16, 1024, 0, c->stream>>>(T, 0, false);
+            FZ_LAUNCH_CHECK();
+        }
+        k_seg_time_bucket<1024, 16384><<<g16, 1024, 0, c->stream>>>(T, kTsMid ? 12288 : 0, true);
         FZ_LAUNCH_CHECK();
     }
     FZ_HIP(hipMemcpyAsync(c->h_pinned + 16, big, 8, hipMemcpyDeviceToHost, c->stream));
