@@ -350,6 +350,9 @@ constexpr int kBucketSkew = 32;
 #ifndef FZ_LONG_FUSE
 #define FZ_LONG_FUSE 1  // the 16384-row class gathers its columns itself (0: k_store_gather does)
 #endif
+#ifndef FZ_TS_PF
+#define FZ_TS_PF 8  // long classes of at most this many rows per thread prefetch the next column
+#endif
 // The sub-bucket pass of long segments (tie != null: equal times ordered by prefix position, any
 // span) ranks inside a bucket by re-reading the bucket's rows from global memory - quadratic in the
 // bucket size - so its cap is looser but still bounded: a sub-bucket whose largest bucket holds more
@@ -628,7 +631,7 @@ __device__ __forceinline__ void seg_time_bucket(const TimeSortTabs &T, int64_t m
             }
         };
         // (the 16-rows-per-thread class has no registers for a second column in flight)
-        constexpr bool kPrefetch = IPT <= 8;
+        constexpr bool kPrefetch = IPT <= FZ_TS_PF;
         uint64_t xa[IPT], xb[kPrefetch ? IPT : 1];
         load(0, xa);
         if (tid == 0 && tb.fused) atomicAdd(tb.fused, (unsigned long long)n);
