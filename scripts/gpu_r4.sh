@@ -37,6 +37,18 @@ for s in $STEPS; do
         timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $O/${T}_pmc_${arg}_$ctr -o run -- python3 -u bench.py --config $arg --steps 2 --warmup 1 --no-cpu-baseline --probe-steps 1 --serial > $O/${T}_pmc_${arg}_$ctr.log 2>&1 || exit $?
       done
       python3 scripts/pmc_traffic.py $(find $O/${T}_pmc_${arg}_FETCH_SIZE -name "*counter_collection.csv" | head -1) $(find $O/${T}_pmc_${arg}_WRITE_SIZE -name "*counter_collection.csv" | head -1) $arg $O/${T}_${arg}_pmc_traffic.json > /dev/null && echo "pmc $arg ok" ;;
+    calib)  # FETCH_SIZE / WRITE_SIZE per access width on known byte counts (scripts/pmc_calib.hip)
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d $O/${T}_calib_$ctr -o run -- scripts/build/pmc_calib > $O/${T}_calib_$ctr.log 2>&1 || exit $?
+      done
+      python3 scripts/pmc_calib.py $(find $O/${T}_calib_FETCH_SIZE -name "*counter_collection.csv" | head -1) $(find $O/${T}_calib_WRITE_SIZE -name "*counter_collection.csv" | head -1) $O/${T}_calib_FETCH_SIZE.log $O/${T}_pmc_calib.json ;;
+    pmck)  # counter bytes per kernel name of a serial step over some stages: pmck:<cfg>@<stages>[@<N>]
+      IFS=@ read -r cfg sts nsh <<< "$arg"
+      extra=""; [ -n "$nsh" ] && extra="--strong --shard-of $nsh --shard-rank 0"
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $O/${T}_pmck_${cfg}_$ctr -o run -- python3 -u bench.py --config $cfg --steps 1 --warmup 1 --no-cpu-baseline --probe-steps 0 --serial --stages $sts $extra > $O/${T}_pmck_${cfg}_$ctr.log 2>&1 || exit $?
+      done
+      python3 scripts/pmc_by_kernel.py $(find $O/${T}_pmck_${cfg}_FETCH_SIZE -name "*counter_collection.csv" | head -1) $(find $O/${T}_pmck_${cfg}_WRITE_SIZE -name "*counter_collection.csv" | head -1) $O/${T}_pmck_$cfg.json > $O/${T}_pmck_$cfg.txt && head -25 $O/${T}_pmck_$cfg.txt ;;
     sq)  # shader-sequencer counters per kernel family (one pass, <= 8 SQ counters)
       timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VALU --output-format csv -d $O/${T}_sq_$arg -o run -- python3 -u bench.py --config $arg --steps 2 --warmup 1 --no-cpu-baseline --probe-steps 0 --serial > $O/${T}_sq_$arg.log 2>&1 || exit $?
       python3 scripts/pmc_sq.py $(find $O/${T}_sq_$arg -name "*counter_collection.csv" | head -1) $O/${T}_${arg}_sq.json ;;
