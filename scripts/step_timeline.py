@@ -27,3 +27,15 @@ for k, rs in sorted(by.items(), key=lambda kv: int(kv[1][0]["Start_Timestamp"]))
     last = rs[-1]["Kernel_Name"].split("(")[0][:50]
     print(f"queue {k[0]:>3} stream {k[1]:>3}: {len(rs):4d} kernels  {s:8.1f} -> {e:8.1f} us  busy {busy:8.1f}  "
           f"first {first} | last {last}")
+# STREAM_DUMP=1: every kernel of the stream that ends last (the critical path), with its start /
+# end relative to the step and the gap to the previous kernel of that stream
+import os  # noqa: E402
+if os.environ.get("STREAM_DUMP"):
+    last = max(by.items(), key=lambda kv: max(int(r["End_Timestamp"]) for r in kv[1]))
+    prev = None
+    print(f"-- critical stream {last[0]}")
+    for r in last[1]:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        gap = (s - prev) / 1e3 if prev is not None else 0.0
+        prev = e
+        print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} us  gap {gap:6.1f}  {r['Kernel_Name'].split('(')[0][:90]}")

@@ -59,10 +59,25 @@ def _sort_input(kind, n, rng):
         sp = (np.arange(4096, dtype=np.int64) * n) // 4096
         a[sp] = rng.uniform(-1e6, 1e6, size=len(sp))
         return a
+    if kind.startswith("tie_"):  # runs of one value that no strided sample hits, inside one range
+        # bucket of <= 12,288 values, past the bucket's comparison-ranking thresholds (FZ_SS_SKEW /
+        # FZ_SS_WORK): the LDS radix sort of the bucket, stable for the ties
+        a = rng.normal(size=n)
+        sp = (np.arange(4096, dtype=np.int64) * n) // 4096
+        free = np.setdiff1d(np.arange(n), sp)
+        runs = {"tie_rank": [(0.1234, 1000), (0.12345, 1000)], "tie_fallback": [(0.1234, 3000)],
+                "tie_work": [(0.1234, 1500), (0.12345, 1500), (0.123456, 1500)]}[kind]
+        at = rng.permutation(free)
+        o = 0
+        for v, m in runs:
+            a[at[o:o + m]] = v
+            o += m
+        return a
     raise ValueError(kind)
 
 
 @pytest.mark.parametrize("kind,n,seed", [
+    ("tie_rank", 100_000, 12), ("tie_fallback", 100_000, 13), ("tie_work", 100_000, 14),
     ("rq3like", 16_385, 0), ("rq3like", 790_000, 1), ("rq3like", 1_310_720, 2), ("rq3like", 2_000_000, 3),
     ("normal", 100_003, 4), ("allsame", 50_000, 5), ("sorted", 300_000, 6), ("reverse", 300_000, 7),
     ("special", 200_000, 8), ("cluster", 100_003, 9), ("cluster_tied", 60_000, 10), ("rq3like", 5, 11)])

@@ -1250,9 +1250,23 @@ __device__ inline void ss_bucket_range(const unsigned long long *__restrict__ co
 // longer range buckets are k_ss_runs'.  A range bucket lies between two sample quantiles, so its
 // values are spread: a counting sort into n value sub-buckets (linear in value when the range is
 // finite, else in key), each value's rank inside its sub-bucket by comparison (key, then position:
-// stable) - O(n) work and five barriers.  A sub-bucket of more than kSsSkew values (a run of one
-// repeated value that no sample hit) sends the bucket to the LSD radix sort in LDS instead.
-constexpr int kSsSkew = 128;
+// stable) - O(n) work and five barriers.  A sub-bucket of more than kSsSkew values, or sub-buckets
+// whose squared sizes sum past kSsWork (long runs of repeated values that no sample hit), send the
+// bucket to the LSD radix sort in LDS instead.
+// (measured at config 2, same box: thresholds of 2,048 values / 4 M squared values ranked RQ3's
+// union's tie runs by comparison - k_ss_buckets 454 us, the step 1.48 ms - against 90 us / 1.16 ms
+// with the LDS radix sort taking every bucket with a sub-bucket of more than 128 values)
+#ifndef FZ_SS_SKEW
+#define FZ_SS_SKEW 128
+#endif
+#ifndef FZ_SS_WORK
+#define FZ_SS_WORK 0x7fffffff
+#endif
+constexpr int kSsSkew = FZ_SS_SKEW;  // largest sub-bucket ranked by comparison
+constexpr int kSsWork = FZ_SS_WORK;  // sum of squared sub-bucket sizes ranked by comparison
+#ifndef FZ_SS_STRIDED
+#define FZ_SS_STRIDED 1  // (0: wave-contiguous items, the A/B baseline)
+#endif
 struct SsVbShared {  // the value-bucket sort's LDS (aliases SsShared: one or the other per bucket)
     uint64_t key[kSsMax];
     uint16_t pos[kSsMax];                   // values in sub-bucket order (bucket-local index)
@@ -1266,7 +1280,7 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
                                                           double *__restrict__ val, int32_t *__restrict__ pos) {
     __shared__ SsLds L;
     __shared__ uint64_t s_lo[kSsWaves], s_hi[kSsWaves];
-    __shared__ uint32_t s_tmp[kSsWaves], s_max[kSsWaves];
+    __shared__ uint32_t s_tmp[kSsWaves], s_max[kSsWaves], s_sq[kSsWaves];
     const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
     const int b = blockIdx.x;
     if (b & 1) return;  // (an equality bucket: one key, already in position order)
@@ -1281,9 +1295,14 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
     uint64_t k[kSsIpt];
     int32_t np[kSsIpt];
     uint64_t lo = ~0ull, hi = 0ull;
+    // value q of the bucket is thread q % kSsBlock's item q / kSsBlock (block-strided: a bucket of a
+    // few thousand values keeps every wave busy - with wave-contiguous items, config 2's ~4 K-value
+    // buckets ran on 5 of the 16 waves, 12 dependent items each); the LDS radix fallback below
+    // re-reads its wave-contiguous layout
+    auto qof = [&](int r) { return FZ_SS_STRIDED ? r * kSsBlock + tid : wbase + r * kWave + lane; };
 #pragma unroll
     for (int r = 0; r < kSsIpt; ++r) {
-        const int q = wbase + r * kWave + lane;
+        const int q = qof(r);
         k[r] = q < n ? f64_key(v[q]) : 0ull;
         np[r] = q < n ? ps[q] : 0;
         if (q < n) {
@@ -1317,28 +1336,32 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
     uint32_t bs[kSsIpt];  // sub-bucket << 16 | slot in it
 #pragma unroll
     for (int r = 0; r < kSsIpt; ++r) {
-        const int q = wbase + r * kWave + lane;
+        const int q = qof(r);
         bs[r] = 0u;
         if (q < n) {
             const uint32_t sb = sub(k[r]);
             const uint32_t sh = (sb & 1u) * 16u;
             bs[r] = (sb << 16) | ((atomicAdd(&L.vb.cnt[sb >> 1], 1u << sh) >> sh) & 0xffffu);
-            L.vb.key[q] = k[r];
         }
     }
     __syncthreads();
     // sub-bucket starts: thread t scans EPT consecutive counters; the largest decides the fallback
     constexpr int EPT = (kSsMax + 1 + kSsBlock - 1) / kSsBlock;
-    uint32_t sum = 0, mx = 0;
+    uint32_t sum = 0, mx = 0, sq = 0;
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
         const int j = tid * EPT + e;
         const uint32_t ce = j < n ? cnt16[j] : 0u;
         sum += ce;
+        sq += ce > 1u ? ce * ce : 0u;  // (<= n^2 < 2^28)
         mx = ce > mx ? ce : mx;
     }
     mx = wave_max(mx);
-    if (lane == 0) s_max[w] = mx;
+    sq = wave_sum(sq);
+    if (lane == 0) {
+        s_max[w] = mx;
+        s_sq[w] = sq;
+    }
     uint32_t run = block_excl_scan<uint32_t, kSsWaves>(sum, s_tmp, (uint32_t *)nullptr);
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {  // (block_excl_scan's barriers ordered every read above)
@@ -1351,16 +1374,26 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
     }
     if (tid == 0) cnt16[n] = uint16_t(n);
     __syncthreads();
-    uint32_t gmax = 0;
+    uint32_t gmax = 0, gsq = 0;
 #pragma unroll
-    for (int q = 0; q < kSsWaves; ++q) gmax = s_max[q] > gmax ? s_max[q] : gmax;
+    for (int q = 0; q < kSsWaves; ++q) {
+        gmax = s_max[q] > gmax ? s_max[q] : gmax;
+        gsq += s_sq[q];
+    }
     int32_t dq[kSsIpt];
-    if (gmax > uint32_t(kSsSkew)) {
+    // the in-sub-bucket ranking costs sum(m^2) comparisons over the block (m values in a
+    // sub-bucket) and about m LDS round trips per item of the longest sub-bucket: past a few hundred
+    // tied values the LDS radix sort below is cheaper (FZ_SS_SKEW / FZ_SS_WORK)
+    if (gmax > uint32_t(kSsSkew) || gsq > uint32_t(kSsWork)) {
         // (a long run of one value: the radix sort, whose cost does not depend on the spread)
         __syncthreads();
         uint16_t ix[kSsIpt];
 #pragma unroll
-        for (int r = 0; r < kSsIpt; ++r) ix[r] = uint16_t(wbase + r * kWave + lane);
+        for (int r = 0; r < kSsIpt; ++r) {  // (nothing written yet: v holds the bucket as on entry)
+            const int q = wbase + r * kWave + lane;
+            ix[r] = uint16_t(q);
+            k[r] = q < n ? f64_key(v[q]) : 0ull;
+        }
         ss_lds_sort(k, ix, n, lo, L.lsd);
         int32_t pp[kSsIpt];
 #pragma unroll
@@ -1381,20 +1414,24 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
     }
 #pragma unroll
     for (int r = 0; r < kSsIpt; ++r) {
-        const int q = wbase + r * kWave + lane;
-        if (q < n) L.vb.pos[cnt16[bs[r] >> 16] + (bs[r] & 0xffffu)] = uint16_t(q);
+        const int q = qof(r);
+        if (q < n) {
+            const uint32_t slot = cnt16[bs[r] >> 16] + (bs[r] & 0xffffu);
+            L.vb.pos[slot] = uint16_t(q);
+            L.vb.key[slot] = k[r];  // (slot order: the ranking reads key and position at x together)
+        }
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSsIpt; ++r) {
-        const int q = wbase + r * kWave + lane;
+        const int q = qof(r);
         dq[r] = -1;
         if (q >= n) continue;
         const uint32_t st = cnt16[bs[r] >> 16], en = cnt16[(bs[r] >> 16) + 1];
         uint32_t rank = 0;
         for (uint32_t x = st; en - st > 1 && x < en; ++x) {  // (alone in its sub-bucket: rank 0)
             const int ox = L.vb.pos[x];
-            const uint64_t kx = L.vb.key[ox];
+            const uint64_t kx = L.vb.key[x];
             rank += (kx < k[r]) || (kx == k[r] && ox < q);
         }
         dq[r] = int32_t(st + rank);
