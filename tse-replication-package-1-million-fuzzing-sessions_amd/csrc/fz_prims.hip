@@ -1146,15 +1146,20 @@ struct SsShared {
 };
 
 // Stable LSD radix sort of n <= kSsMax (key, index) pairs held in registers, element
-// q = wave * 1024 + round * 64 + lane; only the key bytes that differ among the pairs are passes.
+// q = ss_q(R, round) = wave * R * 64 + round * 64 + lane for rounds < R = ss_rounds(n): every wave
+// holds a run of R * 64 elements, so a bucket of a few thousand keeps all 16 waves busy and the
+// rounds past R (no element) are skipped; only the key bytes that differ among the pairs are passes.
+__device__ inline int ss_rounds(int n) { return (n + kSsBlock - 1) / kSsBlock; }
+__device__ inline int ss_q(int R, int r) { return wave_id() * R * kWave + r * kWave + lane_id(); }
 __device__ inline void ss_lds_sort(uint64_t (&k)[kSsIpt], uint16_t (&ix)[kSsIpt], int n, uint64_t kref, SsShared &sh) {
     const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
-    const int wbase = w * (kSsMax / kSsWaves);
+    const int R = ss_rounds(n);
+    const int wbase = w * R * kWave;
     // the bytes that vary: OR of (key ^ kref), kref = one of the keys (the first)
     uint64_t dif = 0;
 #pragma unroll
     for (int r = 0; r < kSsIpt; ++r)
-        if (wbase + r * kWave + lane < n) dif |= k[r] ^ kref;
+        if (r < R && wbase + r * kWave + lane < n) dif |= k[r] ^ kref;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) dif |= __shfl_xor(dif, off, 64);
     if (lane == 0) sh.orw[w] = dif;
@@ -1171,12 +1176,15 @@ __device__ inline void ss_lds_sort(uint64_t (&k)[kSsIpt], uint16_t (&ix)[kSsIpt]
         uint32_t dst[kSsIpt];
 #pragma unroll
         for (int r = 0; r < kSsIpt; ++r) {
-            const bool valid = wbase + r * kWave + lane < n;
-            const uint32_t d = uint32_t(k[r] >> shift) & 255u;
-            const uint64_t peers = match_digit<8>(d, valid);
-            const uint32_t before = valid ? cnt_w[d] : 0u;  // all lanes read before the leader writes
-            dst[r] = before + uint32_t(__popcll(peers & lanemask_lt()));
-            if (valid && (__ffsll((long long)peers) - 1) == lane) cnt_w[d] = before + uint32_t(__popcll(peers));
+            dst[r] = 0u;
+            if (r < R) {  // (uniform: the rounds past R hold no element)
+                const bool valid = wbase + r * kWave + lane < n;
+                const uint32_t d = uint32_t(k[r] >> shift) & 255u;
+                const uint64_t peers = match_digit<8>(d, valid);
+                const uint32_t before = valid ? cnt_w[d] : 0u;  // all lanes read before the leader writes
+                dst[r] = before + uint32_t(__popcll(peers & lanemask_lt()));
+                if (valid && (__ffsll((long long)peers) - 1) == lane) cnt_w[d] = before + uint32_t(__popcll(peers));
+            }
         }
         __syncthreads();
         uint32_t tot = 0;
@@ -1191,7 +1199,7 @@ __device__ inline void ss_lds_sort(uint64_t (&k)[kSsIpt], uint16_t (&ix)[kSsIpt]
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < kSsIpt; ++r) {
-            if (wbase + r * kWave + lane < n) {
+            if (r < R && wbase + r * kWave + lane < n) {
                 const uint32_t d = uint32_t(k[r] >> shift) & 255u;
                 dst[r] += sh.start[d] + cnt_w[d];
                 sh.x[dst[r]] = uint32_t(k[r] >> 32);
@@ -1203,7 +1211,7 @@ __device__ inline void ss_lds_sort(uint64_t (&k)[kSsIpt], uint16_t (&ix)[kSsIpt]
 #pragma unroll
         for (int r = 0; r < kSsIpt; ++r) {
             const int q = wbase + r * kWave + lane;
-            if (q < n) {
+            if (r < R && q < n) {
                 k[r] = (uint64_t(sh.x[q]) << 32) | (k[r] & 0xffffffffull);
                 ix[r] = sh.ix[q];
             }
@@ -1211,12 +1219,12 @@ __device__ inline void ss_lds_sort(uint64_t (&k)[kSsIpt], uint16_t (&ix)[kSsIpt]
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < kSsIpt; ++r)
-            if (wbase + r * kWave + lane < n) sh.x[dst[r]] = uint32_t(k[r]);
+            if (r < R && wbase + r * kWave + lane < n) sh.x[dst[r]] = uint32_t(k[r]);
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < kSsIpt; ++r) {
             const int q = wbase + r * kWave + lane;
-            if (q < n) k[r] = (k[r] & 0xffffffff00000000ull) | sh.x[q];
+            if (r < R && q < n) k[r] = (k[r] & 0xffffffff00000000ull) | sh.x[q];
         }
         __syncthreads();
     }
@@ -1388,24 +1396,25 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
         // (a long run of one value: the radix sort, whose cost does not depend on the spread)
         __syncthreads();
         uint16_t ix[kSsIpt];
+        const int R = ss_rounds(n);  // (ss_lds_sort's layout: a run of R * 64 values per wave)
 #pragma unroll
         for (int r = 0; r < kSsIpt; ++r) {  // (nothing written yet: v holds the bucket as on entry)
-            const int q = wbase + r * kWave + lane;
+            const int q = ss_q(R, r);
             ix[r] = uint16_t(q);
-            k[r] = q < n ? f64_key(v[q]) : 0ull;
+            k[r] = r < R && q < n ? f64_key(v[q]) : 0ull;
         }
         ss_lds_sort(k, ix, n, lo, L.lsd);
         int32_t pp[kSsIpt];
 #pragma unroll
         for (int r = 0; r < kSsIpt; ++r) {
-            const int q = wbase + r * kWave + lane;
-            pp[r] = q < n ? ps[ix[r]] : 0;
+            const int q = ss_q(R, r);
+            pp[r] = r < R && q < n ? ps[ix[r]] : 0;
         }
         __syncthreads();  // every position read before any is overwritten
 #pragma unroll
         for (int r = 0; r < kSsIpt; ++r) {
-            const int q = wbase + r * kWave + lane;
-            if (q < n) {
+            const int q = ss_q(R, r);
+            if (r < R && q < n) {
                 v[q] = f64_from_key(k[r]);
                 ps[q] = pp[r];
             }
@@ -1429,10 +1438,17 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
         if (q >= n) continue;
         const uint32_t st = cnt16[bs[r] >> 16], en = cnt16[(bs[r] >> 16) + 1];
         uint32_t rank = 0;
-        for (uint32_t x = st; en - st > 1 && x < en; ++x) {  // (alone in its sub-bucket: rank 0)
-            const int ox = L.vb.pos[x];
-            const uint64_t kx = L.vb.key[x];
-            rank += (kx < k[r]) || (kx == k[r] && ox < q);
+        if (en - st > 1) {  // (alone in its sub-bucket: rank 0)
+            // four slots' key / position reads in flight together (the lanes of a wave walk
+            // sub-buckets of different lengths: one LDS round trip per slot was ~240 cycles)
+            auto before = [&](uint64_t kx, int ox) { return uint32_t((kx < k[r]) || (kx == k[r] && ox < q)); };
+            uint32_t x = st;
+            for (; x + 4 <= en; x += 4) {
+                const int o0 = L.vb.pos[x], o1 = L.vb.pos[x + 1], o2 = L.vb.pos[x + 2], o3 = L.vb.pos[x + 3];
+                const uint64_t k0 = L.vb.key[x], k1 = L.vb.key[x + 1], k2 = L.vb.key[x + 2], k3 = L.vb.key[x + 3];
+                rank += before(k0, o0) + before(k1, o1) + before(k2, o2) + before(k3, o3);
+            }
+            for (; x < en; ++x) rank += before(L.vb.key[x], L.vb.pos[x]);
         }
         dq[r] = int32_t(st + rank);
     }
@@ -1455,7 +1471,7 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_runs(const unsigned long long *
                                                        uint64_t *__restrict__ kb, uint32_t *__restrict__ ib,
                                                        double *__restrict__ val, int32_t *__restrict__ pos) {
     __shared__ SsShared sh;
-    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
+    const int tid = threadIdx.x;
     const int b = blockIdx.x;
     if (b & 1) return;
     int64_t base, len;
@@ -1463,24 +1479,24 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_runs(const unsigned long long *
     if (len <= kSsMax) return;
     double *v = val + base;
     int32_t *ps = pos + base;
-    const int wbase = w * (kSsMax / kSsWaves);
     uint64_t *ks = ka + base, *kd = kb + base;
     uint32_t *is = ia + base, *id = ib + base;
     for (int64_t c0 = 0; c0 < len; c0 += kSsMax) {
         const int n = int(len - c0 < kSsMax ? len - c0 : kSsMax);
+        const int R = ss_rounds(n);
         uint64_t k[kSsIpt];
         uint16_t ix[kSsIpt];
 #pragma unroll
         for (int r = 0; r < kSsIpt; ++r) {
-            const int q = wbase + r * kWave + lane;
-            k[r] = q < n ? f64_key(v[c0 + q]) : 0ull;
+            const int q = ss_q(R, r);
+            k[r] = r < R && q < n ? f64_key(v[c0 + q]) : 0ull;
             ix[r] = uint16_t(q);
         }
         ss_lds_sort(k, ix, n, f64_key(v[c0]), sh);
 #pragma unroll
         for (int r = 0; r < kSsIpt; ++r) {
-            const int q = wbase + r * kWave + lane;
-            if (q < n) {
+            const int q = ss_q(R, r);
+            if (r < R && q < n) {
                 ks[c0 + q] = k[r];
                 is[c0 + q] = uint32_t(ps[c0 + ix[r]]);
             }
