@@ -1267,6 +1267,9 @@ __device__ inline void ss_bucket_range(const unsigned long long *__restrict__ co
 #ifndef FZ_SS_SKEW
 #define FZ_SS_SKEW 128
 #endif
+#ifndef FZ_SS_TAIL_KEY
+#define FZ_SS_TAIL_KEY 1  // the two tail buckets' sub-buckets linear in key, not in value
+#endif
 #ifndef FZ_SS_WORK
 #define FZ_SS_WORK 0x7fffffff
 #endif
@@ -1301,7 +1304,6 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
     const int n = int(len);
     uint16_t *const cnt16 = reinterpret_cast<uint16_t *>(L.vb.cnt);
     uint64_t k[kSsIpt];
-    int32_t np[kSsIpt];
     uint64_t lo = ~0ull, hi = 0ull;
     // value q of the bucket is thread q % kSsBlock's item q / kSsBlock (block-strided: a bucket of a
     // few thousand values keeps every wave busy - with wave-contiguous items, config 2's ~4 K-value
@@ -1312,7 +1314,6 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
     for (int r = 0; r < kSsIpt; ++r) {
         const int q = qof(r);
         k[r] = q < n ? f64_key(v[q]) : 0ull;
-        np[r] = q < n ? ps[q] : 0;
         if (q < n) {
             lo = k[r] < lo ? k[r] : lo;
             hi = k[r] > hi ? k[r] : hi;
@@ -1333,9 +1334,15 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
         lo = s_lo[q] < lo ? s_lo[q] : lo;
         hi = s_hi[q] > hi ? s_hi[q] : hi;
     }
-    // sub-bucket of a key: linear in value over a finite range (spread values stay spread), else in key
+    // sub-bucket of a key: linear in value over a finite range (spread values stay spread), else in
+    // key.  The two tail buckets (below the first splitter, above the last) are bucketed in key
+    // always: unbounded on one side, they are dense near their inner end - config 2's union: -50 ..
+    // -0.5 and 0.5 .. 50 put 515 / 545 values into one value-linear sub-bucket (the LDS radix sort,
+    // ~88 us for the launch), while the key - the float's exponent and mantissa - spreads them about
+    // logarithmically (largest sub-bucket 47 / 42)
+    const bool tail = FZ_SS_TAIL_KEY && (b == 0 || b == 2 * kSsSplit);
     const double vlo = f64_from_key(lo), vhi = f64_from_key(hi);
-    const bool vlin = isfinite(vlo) && isfinite(vhi) && isfinite(vhi - vlo) && vhi > vlo;
+    const bool vlin = !tail && isfinite(vlo) && isfinite(vhi) && isfinite(vhi - vlo) && vhi > vlo;
     const double vsc = vlin ? double(n) / (vhi - vlo) : 0.0, ksc = double(n) / (double(hi - lo) + 1.0);
     auto sub = [&](uint64_t key) -> uint32_t {
         const double qd = vlin ? (f64_from_key(key) - vlo) * vsc : double(key - lo) * ksc;
@@ -1452,7 +1459,12 @@ __global__ __launch_bounds__(kSsBlock) void k_ss_buckets(const unsigned long lon
         }
         dq[r] = int32_t(st + rank);
     }
-    // (every value and position of the bucket was read into registers at the start)
+    // (the values were read into registers at the start; the positions are read only now - not
+    // live through the counting and ranking: 48 VGPRs spilled with them - and all before any write)
+    int32_t np[kSsIpt];
+#pragma unroll
+    for (int r = 0; r < kSsIpt; ++r) np[r] = dq[r] >= 0 ? ps[qof(r)] : 0;
+    __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSsIpt; ++r) {
         if (dq[r] >= 0) {
