@@ -199,22 +199,31 @@ void rq3(fz_ctx *c, uint32_t flags, const fz_rq3_out *o) {
     // (over the live rows of TC only: *TCv.d_n of capacity NC; the kept pairs compacted in the pass)
     // (several rows per thread: their loads overlap, and fewer tiles to look back over)
     compact_emit<FZ_RQ3_NON_ITEMS>(c, NC, TCv.d_n, [=] __device__(int64_t k) -> bool {
+        // every load that depends on the row alone first - the project's bounds, the row pair's
+        // validity and totals (in range for any k < n) - so the loads of a thread's items overlap
+        // instead of one dependent round trip after each test; then the tests in the reference's
+        // order, the NULL counts (side effects) only where the reference reaches them
         const uint32_t p = TCv.proj[k];
+        const int32_t rb = TCv.row[k], ra = TCv.row[k > 0 ? k - 1 : k];
+        const int64_t tk = TCv.time[k];
         const int64_t ni = *d_ni;
-        const bool hasiss = (ioffs[p + 1] > ioffs[p]) && (flush_last || ni <= 0 || p != iproj[ni - 1]);
-        if (!hasiss || k == TCv.offs[p]) return false;
-        const int32_t ra = TCv.row[k - 1], rb = TCv.row[k];
-        const int64_t day = fdiv_day(TCv.time[k]);
-        const int64_t lo = doffs[p], hi = doffs[p + 1];
+        const int64_t i0 = ioffs[p], i1 = ioffs[p + 1], o0 = TCv.offs[p], lo = doffs[p], hi = doffs[p + 1];
+        const uint32_t plast = ni > 0 ? iproj[ni - 1] : 0xffffffffu;
+        const uint8_t va = cval[ra], vb = cval[rb];
+        const int64_t ta = ctot[ra], tb = ctot[rb];
+        const bool hasiss = (i1 > i0) & (flush_last | (ni <= 0) | (p != plast));
+        if (!hasiss | (k == o0)) return false;
+        const int64_t day = fdiv_day(tk);
         const int64_t q = lower_bound_i64(dday, lo, hi, day);
         if (q < hi && dday[q] == day) return false;  // a detection day of this project
-        if (null_cmp(ra, rb)) {
+        const bool last = p == plast;  // (ni > 0 here: a project with issues)
+        if (!(va & FZ_VALID_TOTAL) | ((ta > 0) & !(vb & FZ_VALID_TOTAL))) {  // null_cmp(ra, rb)
             atomic_add_i64(&counts[FZ_RQ3_NULL_TOTAL], 1);
-            if (p == iproj[*d_ni - 1]) atomic_add_i64(&counts[FZ_RQ3_NULL_LAST], 1);
+            if (last) atomic_add_i64(&counts[FZ_RQ3_NULL_LAST], 1);
             return false;
         }
-        if (!(ctot[ra] > 0 && ctot[rb] > 0)) return false;
-        if (p == iproj[*d_ni - 1]) atomic_add_i64(&counts[FZ_RQ3_NON_LAST], 1);
+        if (!((ta > 0) & (tb > 0))) return false;
+        if (last) atomic_add_i64(&counts[FZ_RQ3_NON_LAST], 1);
         return true;
     }, [=] __device__(int64_t k, int64_t q) {
         const int32_t ra = TCv.row[k - 1], rb = TCv.row[k];
