@@ -50,7 +50,11 @@ AFTER = {"rq3_stats": "rq3_main"}
 WORKLOADS = {"c2": "config2: ~1M-session synthetic table",
              "c3": "config3: 100M-row coverage-only table, 10k projects x 10k days",
              "c4": "config4: rank-statistics stress, 12 coverage series of 1e5/3e5/1e6 points, 256 levels",
-             "c5": "config5: Zipf(1.2) rows per project, coverage-only, 10k projects"}
+             "c5": "config5: Zipf(1.2) rows per project, coverage-only, 10k projects",
+             "c3L": "config3 live rows: 100M-row coverage-only table, 10k projects x 10k rows 6 h apart "
+                    "(every row before the analysis limit)",
+             "c5L": "config5 live rows: Zipf(1.2) rows per project, coverage-only, 10k projects, rows 10 s "
+                    "apart (every row, the 20.8M-row giant's too, before the analysis limit)"}
 
 
 def parse():
@@ -566,7 +570,12 @@ def main():
                                       else f"one table split over {world} ranks" if args.strong
                                       else f"{len(t.projects)} projects/rank"),
                        "rows_per_rank": t.n_rows, "builds": int(len(t.b_project)), "coverage": int(len(t.c_project)),
-                       "issues": int(len(t.i_project)), "stages": stages, "parallelism": f"project-shard x{world}" + (" (sharded path)" if sharded and world == 1 else ""),
+                       "issues": int(len(t.i_project)),
+                       # rows an analysis can read: every build and issue row, and the coverage rows
+                       # dated before the latest bound any script applies (RQ3's DATE(date) <
+                       # '2025-01-09', rq3:263; the others '2025-01-08', queries1.py:3) - configs 3 / 5
+                       # put most of their rows after it, where only the store sorts them
+                       "rows_analysed": rows_analysed(t), "stages": stages, "parallelism": f"project-shard x{world}" + (" (sharded path)" if sharded and world == 1 else ""),
                        "device_ms_per_step": round(dev_ms / args.steps, 4),
                        **({"driver_host_ms": drv} if drv else {}),
                        # end-to-end (host columns -> HBM upload + one step), per rank: the loader's
@@ -615,6 +624,11 @@ def pmc_traffic(probe, config):
         if k and d.get("config") == config:
             return round(float(k["traffic_bytes_per_launch"]))
     return None
+
+
+def rows_analysed(t):
+    from tse_amd.schema import RQ3_LIMIT_US
+    return int(len(t.b_project) + len(t.i_project) + np.count_nonzero(t.c_date < RQ3_LIMIT_US))
 
 
 def cgroup_cpus():

@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round-6 GPU steps.  STEPS: any of "full" (test_gpu_fullsize on K), "tests" (pytest TESTS),
+# "bench" (bench.py on each of BENCH configs, with the CPU baseline), "strong" (strong rehearsal of
+# CONFIG at NS shards, every shard).  Each step under its own time limit; the first failure ends it.
+cd "$(dirname "$0")/.." || exit 1
+export TMPDIR=/tmp
+O=gpurun_out; mkdir -p $O
+T=${TAG:-r6}
+for s in ${STEPS:-full bench}; do
+  case $s in
+    full)
+      timeout -k 10 ${FULL_S:-800} python -u -m pytest tests/test_gpu_fullsize.py -k "${K:-c3L or c5L}" -m gpu -x -v -s \
+        --timeout 900 --timeout-method thread > $O/${T}_full.log 2>&1
+      rc=$?; echo "full rc $rc"; tail -2 $O/${T}_full.log; [ $rc -ne 0 ] && exit $rc ;;
+    tests)
+      timeout -k 10 ${TESTS_S:-800} python -u -m pytest $TESTS -m gpu -x -v -s --timeout 600 --timeout-method thread \
+        > $O/${T}_tests.log 2>&1
+      rc=$?; echo "tests rc $rc"; tail -2 $O/${T}_tests.log; [ $rc -ne 0 ] && exit $rc ;;
+    bench)
+      for c in ${BENCH:-c3L c5L c4}; do
+        st=10; [ $c = c2 ] && st=20
+        timeout -k 10 ${BENCH_S:-400} python -u bench.py --config $c --steps $st --warmup 2 $BENCH_ARGS \
+          > $O/${T}_bench_$c.json 2> $O/${T}_bench_$c.err
+        rc=$?; echo "bench $c rc $rc $(grep -o '"ms_per_step": [0-9.]*' $O/${T}_bench_$c.json | head -1)"
+        [ $rc -ne 0 ] && { tail -5 $O/${T}_bench_$c.err; exit $rc; }
+      done ;;
+    strong)
+      C=${CONFIG:-c3L}
+      for n in ${NS:-1 8}; do
+        for r in $(seq 0 $((n - 1))); do
+          timeout -k 10 300 python -u bench.py --config $C --steps 10 --warmup 2 --no-cpu-baseline --probe-steps 0 \
+            --strong --force-sharded --shard-of $n --shard-rank $r > $O/${T}_sr.json 2> $O/${T}_sr.err || { tail -5 $O/${T}_sr.err; exit 1; }
+          python3 -c "import json; d=json.loads([l for l in open('$O/${T}_sr.json') if l.startswith('{')][-1]); print('$C shard $r of $n', d['ms_per_step'], d['config']['rows_per_rank'], flush=True)" | tee -a $O/${T}_strong_$C.txt
+        done
+      done ;;
+  esac
+done
+echo done

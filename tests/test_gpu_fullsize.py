@@ -19,7 +19,10 @@ The oracle's per-project Python loops cannot run at this size, so the checks are
   multi-core C++ restatement (oracle/cpu/fz_cpu.cpp) on the same table.
 
 Configs 3 and 5 hold exactly one coverage row per project-day from the same first day, so the
-(project, date) order of the table is a counting placement (no host sort of 100M rows)."""
+(project, date) order of the table is a counting placement (no host sort of 100M rows).  Their
+live-row variants c3L / c5L (synth.py) space the rows six hours / ten seconds apart, so every row
+precedes the analysis limit and reaches RQ2-count and RQ4b: config 5L's 20.8M-row Zipf giant is one
+20.8M-value trend (Shapiro-Wilk / Spearman of one series) and 20.8M sessions of the transposition."""
 import math
 import statistics
 import warnings
@@ -43,15 +46,16 @@ RNG = np.random.default_rng(99)
 class Host:
     """The table in (project, date) order plus the per-project masks the analyses filter on."""
 
-    def __init__(self, t):
+    def __init__(self, t, name):
         P = len(t.projects)
         self.P = P
         cnt = np.bincount(t.c_project, minlength=P).astype(np.int64)
         off = np.zeros(P + 1, np.int64)
         np.cumsum(cnt, out=off[1:])
         d0 = int(t.c_date.min())
-        day = (t.c_date - d0) // US_PER_DAY
-        assert np.all(t.c_date == d0 + day * US_PER_DAY)
+        step = synth.CONFIGS[name].step_us
+        day = (t.c_date - d0) // step
+        assert np.all(t.c_date == d0 + day * step)
         pos = off[t.c_project] + day
         assert np.all(day < cnt[t.c_project])
         order = np.empty(len(pos), np.int64)
@@ -102,17 +106,27 @@ def _transpose(lengths):
     return (np.concatenate(dest) if dest else np.zeros(0, np.int64)), soff, per
 
 
-@pytest.fixture(scope="module", params=["c3", "c5"])
+@pytest.fixture(scope="module", params=["c3", "c5", "c3L", "c5L"])
 def case(request, engine):
+    import time
     name = request.param
+    t0 = time.perf_counter()
     t = synth.generate(synth.config(name))
     assert t.n_rows >= 99_000_000
+    print(f"\n{name}: generated {t.n_rows:,} rows in {time.perf_counter() - t0:.1f} s", flush=True)
     engine.upload(t)
     st = engine.build_store()
-    if name == "c5":
+    if name.startswith("c5"):
         assert st.max_cov_per_project > 10_000_000       # the Zipf giant project
-    out = {"name": name, "t": t, "st": st, "h": Host(t),
-           "rq2c": compute.rq2_count(engine), "rq4b": compute.rq4b(engine)}
+    h = Host(t, name)
+    if name.endswith("L"):                               # live rows: every row before the limit
+        assert int(t.c_date.max()) < LIMIT_US
+        assert int(st.max_cov_per_project) == int(h.cnt.max())
+    r2 = compute.rq2_count(engine)
+    print(f"{name}: store + RQ2-count {time.perf_counter() - t0:.1f} s", flush=True)
+    r4 = compute.rq4b(engine)
+    print(f"{name}: RQ4b {time.perf_counter() - t0:.1f} s", flush=True)
+    out = {"name": name, "t": t, "st": st, "h": h, "rq2c": r2, "rq4b": r4}
     yield out
     engine.tables = None
 

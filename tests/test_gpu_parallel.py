@@ -138,8 +138,16 @@ def _check(rank, world, case):
     from tse_amd import parallel as par
     from tse_amd.rq import compute
     t = _table(case, world)
-    lo, hi = par.shard_bounds(t, world)[rank]
-    ts, rows = par.take_shard(t, lo, hi)
+    if case == "giant":
+        # a giant project's coverage rows that no analysis reads spread over the ranks
+        # (parallel.split_plan): shards then hold rows of a project they do not own
+        plan = par.split_plan(t, world)
+        assert plan.moved > 0, "the giant's rows past the date bounds were meant to move"
+        lo, hi = plan.bounds[rank]
+        ts, rows = par.take_split(t, plan, rank)
+    else:
+        lo, hi = par.shard_bounds(t, world)[rank]
+        ts, rows = par.take_shard(t, lo, hi)
     eng = E.Engine(0)
     eng.upload(ts)
     st = eng.build_store()
@@ -209,6 +217,15 @@ def _spawn(case, world, tmp_path):
 @pytest.mark.parametrize("case", ["collide", "last_shard_no_issues"])
 def test_gpu_sharded_rq1_rq3(case, tmp_path):
     _spawn(case, 2, tmp_path)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_split_giant_six_drivers(world, tmp_path):
+    """All six drivers on GPU shards cut by parallel.split_plan: a giant project's movable coverage
+    rows (past every date bound and outside RQ4b's delta window) sit on ranks that do not own it, so
+    RQ1, RQ2 add, RQ3 and RQ4a run on stores holding another owner's rows - recombined results
+    against the oracle on the whole table."""
+    _spawn("giant", world, tmp_path)
 
 
 @pytest.mark.timeout(900)

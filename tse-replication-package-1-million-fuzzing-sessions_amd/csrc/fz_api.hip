@@ -667,6 +667,16 @@ int fz_gather_to_host(void *stream, const fz_host_piece *pieces, int n_pieces, v
             a.cap = want;
         }
         void *h_area = a.h, *d_area = a.d;
+        // a launch that fails part way (FZ_LAUNCH_CHECK throws) may leave earlier gathers writing
+        // the area: drain the stream before the lock is released on that path too, so the next
+        // caller never frees or reuses an area a kernel still writes
+        struct DrainOnThrow {
+            hipStream_t st;
+            bool armed = true;
+            ~DrainOnThrow() {
+                if (armed) (void)hipStreamSynchronize(st);
+            }
+        } drain{st};
         for (int b = 0; b < n_pieces; b += kGatherPieces) {
             GatherList g{};
             int64_t most = 0;
@@ -687,6 +697,7 @@ int fz_gather_to_host(void *stream, const fz_host_piece *pieces, int n_pieces, v
             k_gather_to_host<<<grid, 256, 0, st>>>(g, static_cast<unsigned char *>(d_area));
             FZ_LAUNCH_CHECK();
         }
+        drain.armed = false;
         FZ_HIP(hipStreamSynchronize(st));
         std::memcpy(host_out, h_area, size_t(total_bytes));
         return FZ_OK;

@@ -148,14 +148,11 @@ static void eligibility(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *c
         int32_t *part = c->arena.get<int32_t>(int64_t(nb) * P);
         int32_t *part2 = lim_max ? c->arena.get<int32_t>(int64_t(nb) * P) : nullptr;
         const size_t lds = size_t(P) * 4 * (lim_max ? 2 : 1);
-        if (lds > 65536) {  // (both histograms of up to 16384 bins: up to 128 KiB of the CU's 160)
-            static bool raised = false;
-            if (!raised) {
-                FZ_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_elig_hist),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(2 * kEligLdsMax * 4)));
-                raised = true;
-            }
-        }
+        if (lds > 65536)  // (both histograms of up to 16384 bins: up to 128 KiB of the CU's 160)
+            // function attributes are per device: set on every such launch (cheap), never cached
+            // in a process-wide flag that a second device or a concurrent build would race on
+            FZ_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_elig_hist),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(2 * kEligLdsMax * 4)));
         k_elig_hist<<<nb, kEligThreads, lds, c->stream>>>(
             t->c_project, t->c_date, t->c_coverage, t->c_valid, t->n_cov, P, limit, part, part2);
         k_elig_sum<<<unsigned((P + kWave - 1) / kWave), kBlock, 0, c->stream>>>(part, nb, P, counts, elig, n_elig,

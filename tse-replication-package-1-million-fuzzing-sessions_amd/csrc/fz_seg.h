@@ -16,6 +16,8 @@ namespace fz {
 
 constexpr int kChunk = 2048;
 constexpr int kRedItems = kChunk / kBlock;  // elements per thread of one chunk
+// (k_chunk_reduce takes the items in even / odd pairs: x[u], x[u + 1])
+static_assert(kRedItems % 2 == 0, "k_chunk_reduce reads items in pairs");
 static_assert(kChunk % kBlock == 0, "chunk shape");
 
 struct Segs {
@@ -133,7 +135,10 @@ __global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, const int6
         }
         // two independent double-double accumulators per value (even / odd items), added at the
         // end: the dependent add chain per thread is half as long (the kernel waits on these
-        // chains, not on memory: SQ_WAIT_INST_ANY); the order is fixed - deterministic
+        // chains, not on memory: SQ_WAIT_INST_ANY).  This changed the per-thread
+        // summation order of round 4 (one accumulator): the order is still fixed, so results are
+        // deterministic run to run, and the double-double sums agree with the single-chain ones to
+        // well within the 1e-9 parity tolerance, but not bit for bit
         DD acc[NV], acc2[NV];
 #pragma unroll
         for (int v = 0; v < NV; ++v) acc[v] = acc2[v] = DD{0.0, 0.0};

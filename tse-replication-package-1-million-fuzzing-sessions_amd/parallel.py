@@ -177,7 +177,13 @@ def _giant_must(t: Tables, rows: np.ndarray, p: int, corpus_us) -> np.ndarray:
         if len(pos):
             o = pos[np.argsort(date[pos], kind="stable")]      # positive rows by (date, row)
             j = int(np.searchsorted(date[o], (cu // US_PER_DAY) * US_PER_DAY, "left"))
-            must[o[max(0, j - DELTA_WINDOW):j + DELTA_WINDOW]] = True
+            w = o[max(0, j - DELTA_WINDOW):j + DELTA_WINDOW]
+            must[w] = True
+            if len(w):
+                # every positive row sharing a date with the window's first or last row stays too:
+                # which of equal-date rows the ORDER BY date ... LIMIT 7 picks is then irrelevant
+                edge = (date[pos] == date[w[0]]) | (date[pos] == date[w[-1]])
+                must[pos[edge]] = True
     return must
 
 

@@ -264,6 +264,15 @@ CONFIGS = {
     "c3": SynthConfig(n_projects=10_000, seed=11, coverage_only=True, rows_per_project=10_000),
     # config 5: Zipf rows per project
     "c5": SynthConfig(n_projects=10_000, seed=13, coverage_only=True, zipf_s=1.2, len_mean_days=10_000),
+    # live-row variants of configs 3 and 5: the same 100M rows, projects, seeds and Zipf giant, but
+    # rows spaced below a day so EVERY row precedes the analysis limit (queries1.py:3 '2025-01-08' =
+    # day 2,960 of the series) and reaches the analyses - config 3 daily puts 70 % and config 5 88 %
+    # of the rows past the limit, where only the store sorts them.  c3L: 10,000 rows six hours apart
+    # (2,500 days); c5L: ten seconds apart (the 20.8M-row giant spans 2,408 days)
+    "c3L": SynthConfig(n_projects=10_000, seed=11, coverage_only=True, rows_per_project=10_000,
+                       step_us=6 * HOUR_US),
+    "c5L": SynthConfig(n_projects=10_000, seed=13, coverage_only=True, zipf_s=1.2, len_mean_days=10_000,
+                       step_us=10_000_000),
     # config 4 (rank-statistics stress): series of 1e5 / 3e5 / 1e6 points (one row a minute, all
     # before the analysis limit), 256 coverage levels (heavy ties), every other one a trend + noise
     "c4": SynthConfig(n_projects=12, seed=17, coverage_only=True, lengths=(100_000, 300_000, 1_000_000),
