@@ -24,6 +24,14 @@ for s in ${STEPS:-full bench}; do
         rc=$?; echo "bench $c rc $rc $(grep -o '"ms_per_step": [0-9.]*' $O/${T}_bench_$c.json | head -1)"
         [ $rc -ne 0 ] && { tail -5 $O/${T}_bench_$c.err; exit $rc; }
       done ;;
+    prof)
+      for c in ${PROF:-c5L}; do
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_prof_$c -o run -- python3 -u bench.py \
+          --config $c --steps 3 --warmup 1 --no-cpu-baseline --probe-steps 0 > $O/${T}_prof_$c.log 2>&1
+        rc=$?; echo "prof $c rc $rc"; [ $rc -ne 0 ] && { tail -5 $O/${T}_prof_$c.log; exit $rc; }
+        python3 scripts/kstats.py $(find $O/${T}_prof_$c -name '*kernel_stats.csv' | head -1) auto 40 > $O/${T}_kstats_$c.txt
+        head -25 $O/${T}_kstats_$c.txt
+      done ;;
     strong)
       C=${CONFIG:-c3L}
       for n in ${NS:-1 8}; do

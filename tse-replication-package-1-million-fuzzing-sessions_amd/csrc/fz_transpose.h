@@ -19,7 +19,12 @@
 //   4. the move: one workgroup per tile of 64 runs x 64 sessions stages the tile in LDS (reads:
 //      each run's 64 consecutive values, 512 B per wave load), then each wave writes one session at
 //      a time: the block's live runs of a group are consecutive in their segment (ballot + popcount
-//      gives a lane's slot), so the writes are runs of up to 512 B as well.
+//      gives a lane's slot), so the writes are runs of up to 512 B as well;
+//   5. a block's single-run tail: past its second-longest run only its longest run is live, and a
+//      64 x 64 tile would move 64 values (one live lane per session, a binary search and 128
+//      offset loads per tile - config 5L's 20.8M-value giant: 325 k such tiles, 4.7 ms).  Those
+//      sessions go kRtTail at a time, one value per thread: its value read and its slot written
+//      coalesced (dest = the segment's offset + the earlier blocks' live runs of its group).
 //
 // Algorithmic traffic (probe "ragged_transpose"): 8 B read + 8 B written per value, plus 8 B per
 // segment offset.
@@ -33,6 +38,7 @@ constexpr int kRtRuns = 64;        // runs per tile (one per lane)
 constexpr int kRtSess = 64;        // sessions per tile
 constexpr int kRtRankMax = 2048;   // runs ranked by counting in one launch; more: the radix sort
 constexpr int64_t kRtTableMax = int64_t(1) << 26;  // pre[] entries (4 B each) before the fallback
+constexpr int kRtTail = 4096;      // sessions per single-run tail tile (kBlock threads x 16)
 
 // the transpose applies when its tables stay small (R runs, M sessions, G groups)
 inline bool ragged_transpose_ok(int64_t R, int64_t M, int G) {
@@ -86,7 +92,8 @@ static __global__ __launch_bounds__(kRtTabBlock) void k_rt_tables(const uint32_t
                                                            const int64_t *__restrict__ offs, int64_t R, int lb,
                                                            int64_t nB, uint32_t *__restrict__ pre,
                                                            int64_t *__restrict__ plen, int64_t *__restrict__ gs,
-                                                           int64_t *__restrict__ tpre) {
+                                                           int64_t *__restrict__ tpre, int64_t *__restrict__ tdense,
+                                                           int32_t *__restrict__ trun) {
     constexpr int NW = kRtTabBlock / kWave;
     __shared__ int64_t s_tmp[NW];
     const int64_t b = blockIdx.x;
@@ -127,18 +134,30 @@ static __global__ __launch_bounds__(kRtTabBlock) void k_rt_tables(const uint32_t
         }
         return;
     }
-    // tile counts: wave w takes blocks w, w + NW, ...; the block scan folds them in order
+    // tile counts: thread bb takes block bb; the block scan folds them in order.  A block's dense
+    // tiles cover the sessions below its second-longest run (rounded up to whole tiles), its tail
+    // tiles the rest of its longest run (kRtTail sessions each)
     for (int64_t b0 = 0; b0 < nB; b0 += kRtTabBlock) {
         const int64_t bb = b0 + threadIdx.x;
         int64_t tiles = 0;
         if (bb < nB) {
-            int64_t mx = 0;
+            int64_t mx = 0, mx2 = 0, arg = bb * kRtRuns;
             const int64_t k1 = (bb + 1) * kRtRuns < R ? (bb + 1) * kRtRuns : R;
             for (int64_t k = bb * kRtRuns; k < k1; ++k) {
                 const int64_t len = offs[k + 1] - offs[k];
-                mx = len > mx ? len : mx;
+                if (len > mx) {
+                    mx2 = mx;
+                    mx = len;
+                    arg = k;
+                } else if (len > mx2) {
+                    mx2 = len;
+                }
             }
-            tiles = (mx + kRtSess - 1) / kRtSess;
+            const int64_t dense = (mx2 + kRtSess - 1) / kRtSess;
+            const int64_t rest = mx - dense * kRtSess;
+            tiles = dense + (rest > 0 ? (rest + kRtTail - 1) / kRtTail : 0);
+            tdense[bb] = dense;
+            trun[bb] = int32_t(arg);
         }
         int64_t tot;
         const int64_t ex = block_excl_scan<int64_t, NW>(tiles, s_tmp, &tot);
@@ -184,7 +203,8 @@ template <int G, typename In, typename Grp>
 __global__ __launch_bounds__(kBlock) void k_rt_move(const int64_t *__restrict__ offs, int64_t R, int64_t M, In in,
                                                     Grp grp, const uint32_t *__restrict__ pre,
                                                     const int64_t *__restrict__ gs, const int64_t *__restrict__ tpre,
-                                                    int64_t nB, const int64_t *__restrict__ soffs,
+                                                    int64_t nB, const int64_t *__restrict__ tdense,
+                                                    const int32_t *__restrict__ trun, const int64_t *__restrict__ soffs,
                                                     const int32_t *__restrict__ cidx, double *__restrict__ out) {
     __shared__ double s_v[kRtRuns][kRtSess + 1];
     __shared__ int64_t s_base[G][kRtSess];
@@ -200,7 +220,19 @@ __global__ __launch_bounds__(kBlock) void k_rt_move(const int64_t *__restrict__ 
             else hi = mid - 1;
         }
         const int64_t b = lo;
-        const int64_t i0 = (t - tpre[b]) * kRtSess;
+        const int64_t tb = t - tpre[b], nd = tdense[b];
+        if (tb >= nd) {  // the block's single-run tail: one session per thread, no LDS
+            const int64_t k = trun[b];
+            const int64_t st = offs[k], len = offs[k + 1] - st;
+            const int g = G == 2 ? grp(k) : 0;
+            const uint32_t *prow = pre + b * (R + 1);
+            const uint32_t before_end = prow[gs[g + 1]];
+            const int64_t ib = nd * kRtSess + (tb - nd) * int64_t(kRtTail);
+            for (int64_t i = ib + threadIdx.x; i < ib + kRtTail && i < len; i += kBlock)
+                out[soffs[i * G + g] + int64_t(before_end) - int64_t(prow[cidx[i * G + g]])] = in(st + i);
+            continue;  // (no LDS used: no barrier owed)
+        }
+        const int64_t i0 = tb * kRtSess;
         const int64_t k0 = b * kRtRuns;
         // stage: wave w loads runs w, w + NW, ...: 64 consecutive values each
         for (int r = w; r < kRtRuns; r += NW) {
@@ -271,7 +303,10 @@ void ragged_transpose(fz_ctx *c, const int64_t *offs, int64_t R, int64_t M, int6
     int64_t *plen = c->arena.get<int64_t>(R + 1);
     int64_t *gs = c->arena.get<int64_t>(3);
     int64_t *tpre = c->arena.get<int64_t>(nB + 1);
-    k_rt_tables<<<unsigned(nB + 3), kRtTabBlock, 0, st>>>(skey, sid, offs, R, lb, nB, pre, plen, gs, tpre);
+    int64_t *tdense = c->arena.get<int64_t>(nB);
+    int32_t *trun = c->arena.get<int32_t>(nB);
+    k_rt_tables<<<unsigned(nB + 3), kRtTabBlock, 0, st>>>(skey, sid, offs, R, lb, nB, pre, plen, gs, tpre, tdense,
+                                                          trun);
     FZ_LAUNCH_CHECK();
     int32_t *cidx = c->arena.get<int32_t>(M * G);
     k_rt_offsets<<<grid_for(M + 1, kBlock, 16384), kBlock, 0, st>>>(skey, plen, gs, lb, G, M, out_offs, cidx);
@@ -280,7 +315,7 @@ void ragged_transpose(fz_ctx *c, const int64_t *offs, int64_t R, int64_t M, int6
     const int64_t tiles_cap = nB + n_cap / kRtSess + 1;
     ProbeScope ps(c, "ragged_transpose", 8.0 * double(M * G + 1), offs + R, 16.0);
     k_rt_move<G, In, Grp><<<unsigned(tiles_cap < 4096 ? tiles_cap : 4096), kBlock, 0, st>>>(
-        offs, R, M, in, grp, pre, gs, tpre, nB, out_offs, cidx, out);
+        offs, R, M, in, grp, pre, gs, tpre, nB, tdense, trun, out_offs, cidx, out);
     FZ_LAUNCH_CHECK();
 }
 
