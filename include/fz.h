@@ -221,6 +221,10 @@ int fz_rq2_count(fz_ctx *ctx, const fz_rq2_count_out *out);
  * outputs + its session-major values), the values are exchanged by session index (all-to-all), and
  * the owner of a session range runs fz_rq2_session_stats on what it received. */
 #define FZ_RQ2C_SKIP_SESSION_STATS 1u  /* no per-session / median-trend / correlation summaries */
+/* (with SKIP_SESSION_STATS) the trend values project-major instead of session-major: session_values
+ * = every eligible project's values in (project, date) order, project p's n_trend[p] of them after the
+ * earlier projects' (session_offsets not written) - the runs fz_pack_runs sends to the session owners */
+#define FZ_RQ2C_PROJECT_MAJOR 2u
 int fz_rq2_count_ex(fz_ctx *ctx, uint32_t flags, const fz_rq2_count_out *out);
 
 /* Per-session statistics (:139-152, :390, :439-440) of n_values (session id, value) pairs, ids in
@@ -460,6 +464,10 @@ int fz_rq4b(fz_ctx *ctx, const fz_rq4_groups *groups, const fz_rq4b_out *out);
  * session range runs fz_rq4b_session_stats; the initial-coverage samples are gathered for
  * fz_two_sample_tests. */
 #define FZ_RQ4B_SKIP_SESSION_STATS 1u
+/* (with SKIP_SESSION_STATS) the G1/G2 series project-major: trend_values = their values in
+ * (project, date) order, trend_offsets[0 .. n_projects] = per-project offsets into them (capacity
+ * n_projects + 1) - the runs of the project-major session exchange */
+#define FZ_RQ4B_PROJECT_MAJOR 2u
 int fz_rq4b_ex(fz_ctx *ctx, const fz_rq4_groups *groups, uint32_t flags, const fz_rq4b_out *out);
 
 /* Per-session G2 (group 0) vs G1 (group 1) statistics (:910-1015) of n_values (session id, group,
@@ -505,6 +513,68 @@ int fz_rq4b_tail(fz_ctx *ctx, const int64_t *c2, const int64_t *c1, const double
                  int64_t n_delta, int64_t n_order, const double *init_g2, int64_t n2, const double *init_g1, int64_t n1,
                  int64_t *last, double *spearman6, double *pre_out, double *post_out, double *medians14,
                  double *tests);
+
+/* ---- a project cut across ranks (config 5's Zipf giant) --------
+ * A coverage-only project larger than one rank's share is cut into date ranges on consecutive ranks
+ * (tse_amd/parallel.py live_plan).  The reference reads it as one series (queries1.py:120-129,
+ * rq2_coverage_count.py:292-333); these calls keep its eligibility, its sessions and its
+ * per-project tests exact across the cut.  (No reference counterpart: the reference is one process.) */
+
+/* out[i] = the store's count of qualifying coverage rows (coverage valid, > 0, date < 2025-01-08:
+ * rq1:144-152) of project proj[i] on this rank (device in, device out). */
+int fz_store_elig_counts(fz_ctx *ctx, const int32_t *proj, int64_t n, int64_t *out);
+/* Overrides the store's eligibility of the distinct projects proj[i] by flag[i] (device) until the
+ * next fz_store_build - the flags of the whole project's summed counts, set on its first piece's
+ * rank, cleared on the others; every analysis after it reads the overridden set.  ctx: the context
+ * that built the store. */
+int fz_store_set_eligible(fz_ctx *ctx, const int32_t *proj, const uint8_t *flag, int64_t n);
+
+/* One project's filtered coverage values on this rank, date order (out: capacity the project's rows
+ * here).  FZ_PIECE_RQ2: RQ2-count's trend values (coverage NOT NULL AND != 0 AND date < LIMIT, then
+ * total != 0; covered / total * 100, NaN for a NULL line count) with counts[0..2] = values, fetched
+ * rows, NULL-line rows; FZ_PIECE_RQ4B: rq4b's full series (coverage > 0, date < LIMIT,
+ * rq4b_coverage.py:315-326) with counts[0..2] = values, values, 0.  counts: device [3]. */
+enum { FZ_PIECE_RQ2 = 0, FZ_PIECE_RQ4B = 1 };
+int fz_piece_values(fz_ctx *ctx, int64_t project, int kind, double *out, int64_t *counts);
+
+/* The project-major session exchange's send side: run r = desc[r].len values at (src 0: a, 1: b) +
+ * src_off covering sessions [base, base + len); the slice of run r for destination d (sessions
+ * [cuts[d], cuts[d + 1]), d < n_dest) is written at out + table[d * (n_runs + 1) + r].  in_off[r]:
+ * exclusive prefix of the runs' lengths; n_values their total.  Every pointer device. */
+typedef struct fz_run_desc {
+    int64_t src_off;
+    int64_t len;
+    int64_t base;
+    int32_t src;
+    int32_t pad_;
+} fz_run_desc;
+int fz_pack_runs(fz_ctx *ctx, const double *a, const double *b, const fz_run_desc *desc, const int64_t *in_off,
+                 int64_t n_runs, const int64_t *cuts, int n_dest, const int64_t *table, int64_t n_values, double *out);
+
+/* The receive side: n_runs runs (run k = values[run_offs[k], run_offs[k + 1]) in project order, all
+ * starting at the owner's first session; group run_group[k] (0 = G2, 1 = G1) when n_groups == 2,
+ * else null) -> out = value i of every run longer than i, runs in order, grouped by segment (session
+ * i, group) with out_offs [n_sessions * n_groups + 1] - coverage_by_session_index (:329-333) and
+ * rq4b_coverage.py:917-931 over the owner's session range.  n_values = run_offs[n_runs]. */
+int fz_transpose_runs(fz_ctx *ctx, const double *values, const int64_t *run_offs, const uint8_t *run_group,
+                      int64_t n_runs, int n_groups, int64_t n_sessions, int64_t n_values, double *out,
+                      int64_t *out_offs);
+
+/* spearmanr(range(n), x) and shapiro(x) (rq2_coverage_count.py:305-322) of one n-value series whose
+ * values are sorted in buckets over ranks (ties never cross a bucket): this rank's bucket holds m
+ * values sorted ascending at global sorted positions [g0, g0 + m), gidx[j] the series index of value
+ * j.  Three passes; after each, every rank combines the buckets' partials in bucket order:
+ *   fz_series_dist_partials(pass, ...) -> part [FZ_DIST_PART_WIDTH(pass)] (device)
+ *   fz_series_dist_combine(pass, parts [k * width], k, n, params, result)
+ * params: device [FZ_DIST_PARAMS] state between passes; result: device [4] = rho, p (after pass 0),
+ * W, p (after pass 2) - scipy's values as fz_series_tests gives them.  x0_src: device pointer to
+ * series value n / 2 (scipy's y -= x[N // 2]) on the rank that holds it, else null. */
+#define FZ_DIST_PARAMS 10
+#define FZ_DIST_PART_WIDTH(pass) ((pass) == 0 ? 14 : ((pass) == 1 ? 4 : 6))
+int fz_series_dist_partials(fz_ctx *ctx, int pass, const double *sorted, const int64_t *gidx, int64_t m, int64_t g0,
+                            int64_t n, const double *params, const double *x0_src, double *part);
+int fz_series_dist_combine(fz_ctx *ctx, int pass, const double *parts, int64_t k, int64_t n, double *params,
+                           double *result);
 
 /* ---- build-log analysis ------------------------------------------
  * Replaces buildlog_analysis(row) of program/preparation/4_get_buildlog_analysis.py:14-246 for a

@@ -48,6 +48,17 @@ void rq4b_tail(fz_ctx *c, const int64_t *c2, const int64_t *c1, const double *g2
                const int64_t *order, const double *pre, const double *post, int64_t nd, int64_t n_order,
                const double *x, int64_t nx, const double *y, int64_t ny, int64_t *last, double *sp, double *pre_out,
                double *post_out, double *med14, double *tests);
+void store_elig_counts(fz_ctx *c, const int32_t *proj, int64_t n, int64_t *out);
+void store_set_eligible(fz_ctx *c, const int32_t *proj, const uint8_t *flag, int64_t n);
+void piece_values(fz_ctx *c, int64_t project, int kind, double *out, int64_t *counts);
+void pack_runs(fz_ctx *c, const double *a, const double *b, const fz_run_desc *runs, const int64_t *in_off, int64_t R,
+               const int64_t *cuts, int W, const int64_t *table, int64_t n, double *out);
+void transpose_runs(fz_ctx *c, const double *vals, const int64_t *offs, const uint8_t *grp, int64_t R, int G,
+                    int64_t M, int64_t n, double *out, int64_t *out_offs);
+void series_dist_partials(fz_ctx *c, int pass, const double *sorted, const int64_t *gidx, int64_t m, int64_t g0,
+                          int64_t n, const double *params, const double *x0_src, double *part);
+void series_dist_combine(fz_ctx *c, int pass, const double *part, int64_t k, int64_t n, double *params,
+                         double *result);
 void buildlog(fz_ctx *c, const uint8_t *text, int64_t n_bytes, const int64_t *log_offs_host, const int64_t *log_offs,
               int64_t n_logs, const fz_buildlog_out *o);
 }  // namespace fz
@@ -593,6 +604,64 @@ int fz_rq4b_tail(fz_ctx *ctx, const int64_t *c2, const int64_t *c1, const double
                  "fz_rq4b_tail: bad arguments");
         fz::rq4b_tail(ctx, c2, c1, g2_q, g1_q, n_sessions, delta_order, pre_cov, post_cov, n_delta, n_order, init_g2,
                       n2, init_g1, n1, last, spearman6, pre_out, post_out, medians14, tests);
+    });
+}
+
+int fz_store_elig_counts(fz_ctx *ctx, const int32_t *proj, int64_t n, int64_t *out) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n >= 0 && (n == 0 || (proj && out)), "fz_store_elig_counts: bad arguments");
+        fz::store_elig_counts(ctx, proj, n, out);
+    });
+}
+
+int fz_store_set_eligible(fz_ctx *ctx, const int32_t *proj, const uint8_t *flag, int64_t n) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n >= 0 && (n == 0 || (proj && flag)), "fz_store_set_eligible: bad arguments");
+        fz::store_set_eligible(ctx, proj, flag, n);
+    });
+}
+
+int fz_piece_values(fz_ctx *ctx, int64_t project, int kind, double *out, int64_t *counts) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(out && counts, "fz_piece_values: bad arguments");
+        fz::piece_values(ctx, project, kind, out, counts);
+    });
+}
+
+int fz_pack_runs(fz_ctx *ctx, const double *a, const double *b, const fz_run_desc *desc, const int64_t *in_off,
+                 int64_t n_runs, const int64_t *cuts, int n_dest, const int64_t *table, int64_t n_values, double *out) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n_runs >= 0 && n_dest >= 1 && n_values >= 0 &&
+                     (n_values == 0 || (desc && in_off && cuts && table && out && (a || b))),
+                 "fz_pack_runs: bad arguments");
+        fz::pack_runs(ctx, a, b, desc, in_off, n_runs, cuts, n_dest, table, n_values, out);
+    });
+}
+
+int fz_transpose_runs(fz_ctx *ctx, const double *values, const int64_t *run_offs, const uint8_t *run_group,
+                      int64_t n_runs, int n_groups, int64_t n_sessions, int64_t n_values, double *out,
+                      int64_t *out_offs) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(n_runs >= 0 && n_sessions >= 0 && n_values >= 0 && out_offs && (n_groups == 1 || n_groups == 2) &&
+                     (n_runs == 0 || (run_offs && (n_values == 0 || (values && out)) && (n_groups == 1 || run_group))),
+                 "fz_transpose_runs: bad arguments");
+        fz::transpose_runs(ctx, values, run_offs, run_group, n_runs, n_groups, n_sessions, n_values, out, out_offs);
+    });
+}
+
+int fz_series_dist_partials(fz_ctx *ctx, int pass, const double *sorted, const int64_t *gidx, int64_t m, int64_t g0,
+                            int64_t n, const double *params, const double *x0_src, double *part) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(part && (m == 0 || (sorted && gidx)) && (pass == 0 || params), "fz_series_dist_partials: bad arguments");
+        fz::series_dist_partials(ctx, pass, sorted, gidx, m, g0, n, params, x0_src, part);
+    });
+}
+
+int fz_series_dist_combine(fz_ctx *ctx, int pass, const double *parts, int64_t k, int64_t n, double *params,
+                           double *result) {
+    return guarded(ctx, [&] {
+        FZ_CHECK(parts != nullptr, "fz_series_dist_combine: bad arguments");
+        fz::series_dist_combine(ctx, pass, parts, k, n, params, result);
     });
 }
 

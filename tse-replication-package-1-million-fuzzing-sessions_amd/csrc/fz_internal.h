@@ -156,6 +156,7 @@ struct Store {
     // eligible projects (the GROUP BY/HAVING every script starts from), computed once per load
     DevBuf elig;     // uint8 [P]
     DevBuf n_elig;   // int64 [2]: eligible projects, the most rows of one project before the limit
+    DevBuf elig_cnt; // int32 [P]: each project's qualifying rows (a project cut across ranks sums them)
     // The tables themselves in sorted order: after the build `t` points at these sorted copies and
     // every view's row id IS the position in its sorted table, so filters and joins read columns
     // sequentially instead of gathering through the sort permutation.  perm maps a sorted
@@ -176,7 +177,7 @@ struct Store {
         const unsigned char *tb = reinterpret_cast<const unsigned char *>(&t);
         for (size_t i = 0; i < sizeof(t); ++i) mix(tb[i]);
         for (const DevBuf *d : {&b_time, &b_proj, &c_time, &c_proj, &i_time, &i_proj,
-                                &off_fuzz, &off_covb, &off_cov, &off_iss, &elig, &n_elig, &sb_type, &sb_result,
+                                &off_fuzz, &off_covb, &off_cov, &off_iss, &elig, &n_elig, &elig_cnt, &sb_type, &sb_result,
                                 &sb_group, &sb_canon, &sc_coverage, &sc_covered, &sc_total, &sc_valid, &si_number,
                                 &si_status, &b_perm, &c_perm, &i_perm}) {
             mix(reinterpret_cast<uintptr_t>(d->ptr));

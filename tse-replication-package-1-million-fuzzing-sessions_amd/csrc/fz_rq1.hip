@@ -180,8 +180,9 @@ void store_eligibility(fz_ctx *c) {
     const int64_t P = s.P;
     uint8_t *elig = s.elig.ensure<uint8_t>(P);
     int64_t *n = s.n_elig.ensure<int64_t>(2);
+    int32_t *cnt = s.elig_cnt.ensure<int32_t>(P);  // (kept: fz_store_elig_counts reads them)
     dev_fill(c, n, 0, 16);
-    eligibility(c, &s.t, kLimitUs, nullptr, elig, n, n + 1);
+    eligibility(c, &s.t, kLimitUs, cnt, elig, n, n + 1);
 }
 
 // elig[p] = project has >= 365 qualifying coverage rows; *d_count = number eligible.

@@ -190,8 +190,10 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     TmpView T;
     const CovTrendRows vrows{t.c_project, t.c_coverage, t.c_valid, t.c_date, o->eligible};
     const NonZeroTotal nzt{t.c_total, t.c_valid};
-    // trend values in (project, date) order, written by the filter itself
-    double *tv = c->arena.get<double>(NC);
+    // trend values in (project, date) order, written by the filter itself (project-major output:
+    // straight into the caller's session_values - the runs of the sharded session exchange)
+    const bool pmajor = (flags & FZ_RQ2C_PROJECT_MAJOR) && (flags & FZ_RQ2C_SKIP_SESSION_STATS);
+    double *tv = pmajor ? o->session_values : c->arena.get<double>(NC);
     T.proj = c->arena.get<uint32_t>(NC);
     const TrendEmit te{tv, T.proj, t.c_covered, t.c_total, t.c_valid, counts + FZ_RQ2C_NULL_LINES};
     // (an index range scan: the eligible projects' rows before the date limit only; per kept row:
@@ -222,6 +224,7 @@ void rq2_count(fz_ctx *c, uint32_t flags, const fz_rq2_count_out *o) {
     const int32_t *segid = reinterpret_cast<const int32_t *>(T.proj);
     SortedSegs ss = seg_sort_f64(c, tv, sp, segid);
     spearman_shapiro_sorted(c, cs, segid, ss, tv, o->corr, nullptr, o->sw_w, o->sw_p);
+    if (pmajor) return;
 
     // coverage_by_session_index (:329-333): session i = value i of every project longer than i, in
     // project order - the ragged transpose (fz_transpose.h) moves each value straight to its slot

@@ -724,7 +724,11 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
     // the filter writes each kept row's coverage value and project itself (no (row, time, project)
     // copy gathered through afterwards); G1 / G2 projects' rows before the limit only (range scan)
     TmpView F;
-    double *fval = c->arena.get<double>(NC);
+    // (project-major output: the filter writes the series into the caller's trend_values, the
+    // per-project offsets follow into trend_offsets - the runs of the sharded session exchange)
+    const bool pmajor = (flags & FZ_RQ4B_PROJECT_MAJOR) && (flags & FZ_RQ4B_SKIP_SESSION_STATS) && o->trend_values &&
+                        o->trend_offsets;
+    double *fval = pmajor ? o->trend_values : c->arena.get<double>(NC);
     F.proj = c->arena.get<uint32_t>(NC);
     const ValueProjEmit fe{fval, F.proj, cov};
     filter_view(c, s.cov, NC, P,
@@ -743,10 +747,11 @@ void rq4b(fz_ctx *c, const fz_rq4_groups *g, uint32_t flags, const fz_rq4b_out *
     const bool sharded = flags & FZ_RQ4B_SKIP_SESSION_STATS;
     // a shard's contribution to the session exchange: its values grouped by (session, group)
     // segment, as the unsharded path groups them before the statistics
-    const bool contribute = o->trend_values && o->trend_offsets;
+    const bool contribute = o->trend_values && o->trend_offsets && !pmajor;
+    if (pmajor) dev_copy(c, o->trend_offsets, foffs, (P + 1) * int64_t(sizeof(int64_t)));
     int64_t *c2 = o->c2, *c1 = o->c1;
     double *g2q = o->g2_q, *g1q = o->g1_q;
-    if (!sharded || contribute) {
+    if (!sharded || (contribute && !pmajor)) {
         const int64_t S2 = 2 * MM;
         if (ragged_transpose_ok(P, MM, 2)) {
             // the ragged transpose (fz_transpose.h): value i of project p straight to segment
