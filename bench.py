@@ -138,15 +138,19 @@ def main():
     dev = torch.device("cuda", local)
 
     rehearsal = args.strong and world == 1 and args.shard_of > 1
+    cont, cut, cont_base = -1, [], (None, None)
     if args.strong:
         from tse_amd import parallel as par
         full = synth.generate(synth.config(args.config))
-        # project shards, a giant project's rows that no analysis reads spread over the ranks
-        # (parallel.split_plan: config 5's Zipf giant)
-        plan = par.split_plan(full, args.shard_of if rehearsal else world)
+        # project shards of about equal rows; a project larger than one share (config 5's Zipf
+        # giant) cut into date-range pieces over consecutive ranks (parallel.live_plan)
+        plan = par.live_plan(full, args.shard_of if rehearsal else world)
         r = args.shard_rank if rehearsal else rank
         lo, hi = plan.bounds[r]
         t = par.take_split(full, plan, r)[0]
+        cont, cut = plan.cont[r], list(plan.cut)
+        if rehearsal:  # (no other rank to exchange with: the session bases another rank would send)
+            cont_base = par.cut_trend_bases(full, plan, r)
         job_rows = full.n_rows if not rehearsal else None
         del full, plan
     else:
@@ -211,9 +215,10 @@ def main():
                 eng.set_store_helpers(lch[:4])  # (idle while the store builds: the step joins them first)
         rq1_shard = par.GpuRQ1Shard(skids.get("rq1", eng), M)
         rq3_shard = par.GpuRQ3Shard(skids.get("rq3", eng))
-        rq2c_shard = par.GpuRQ2CountShard(skids.get("rq2_count", eng))
+        rq2c_shard = par.GpuRQ2CountShard(skids.get("rq2_count", eng), cont)
         rq4a_shard = par.GpuRQ4aShard(skids.get("rq4a", eng), M)
-        rq4b_shard = par.GpuRQ4bShard(skids.get("rq4b", eng))
+        rq4b_shard = par.GpuRQ4bShard(skids.get("rq4b", eng), cont)
+        elig_ctl = par.GpuEligibility(eng)
         rq2a_shard = par.GpuRQ2AddShard(skids.get("rq2_add", eng))
         if args.strong:
             own = (lo, hi)
@@ -272,9 +277,11 @@ def main():
         shard_step = {
             "rq1": sh_rq1,
             "rq2_count": lambda e: pending.append(par.rq2_count_sharded(rq2c_shard, rank, world, *own,
-                                                                        gather_values=False, finish_later=True)),
+                                                                        gather_values=False, finish_later=True,
+                                                                        cont=cont, cont_base=cont_base[0])),
             "rq4a": lambda e: pending.append(par.rq4a_sharded(rq4a_shard, rank, world, *own, finish_later=True)),
-            "rq4b": lambda e: pending.append(par.rq4b_sharded(rq4b_shard, rank, world, finish_later=True)),
+            "rq4b": lambda e: pending.append(par.rq4b_sharded(rq4b_shard, rank, world, *own, finish_later=True,
+                                                              cont=cont, cont_base=cont_base[1])),
             "rq2_add": sh_rq2_add,
             "rq3": lambda e: par.rq3_sharded(rq3_shard, rank, world),
         }
@@ -386,6 +393,9 @@ def main():
         # sharded: exact recombination of every script over the ranks (tse_amd/parallel.py)
         eng.join_children()  # the previous step's drivers have read the store
         eng.build_store()
+        # a cut project's eligibility over all of its pieces (one all-reduce, before the analyses)
+        with torch.cuda.stream(eng.stream):
+            par.fix_cut_eligibility(elig_ctl, cut, *own, world)
         if pool is None:
             run_sharded(snames)
             finalize_pending()

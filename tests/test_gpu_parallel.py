@@ -50,24 +50,6 @@ class _RQ3View(_HostView):
         return out
 
 
-class _RQ2View(_HostView):
-    def run(self):
-        return super().run()
-
-    def session_stats_grouped(self, vals, offs, S, max_len):
-        out = self.s.session_stats_grouped(vals.to(self.dev), offs.to(self.dev), S, max_len)
-        return {k: v.cpu() for k, v in out.items()}
-
-    def merge_runs(self, vals, runs):
-        return tuple(v.cpu() for v in self.s.merge_runs(vals.to(self.dev), runs.to(self.dev)))
-
-    def series_tests(self, x):
-        return self.s.series_tests(x.to(self.dev))
-
-    def mean_median(self, x):
-        return self.s.mean_median(x.to(self.dev))
-
-
 class _RQ2AddView(_HostView):
     """... and maps the shard's build / coverage row ids to the whole table's (-1 kept)."""
 
@@ -93,21 +75,6 @@ class _RQ4aView(_HostView):
         return sc
 
 
-class _RQ4bView(_RQ2View):
-    def spearman_prefix(self, rows, n):
-        return self.s.spearman_prefix(rows.to(self.dev), n.to(self.dev)).cpu()
-
-    def trends(self, cols):
-        last, sp = self.s.trends([c.to(self.dev) for c in cols])
-        return last.cpu(), sp.cpu()
-
-    def two_sample(self, x, y):
-        return self.s.two_sample(x.to(self.dev), y.to(self.dev))
-
-    def row_medians(self, rows):
-        return self.s.row_medians(rows.to(self.dev))
-
-
 def _worker(rank, world, port, case, errfile):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -130,6 +97,7 @@ def _table(case, world):
     return make_table(case, world)
 
 
+
 def _check(rank, world, case):
     from gpu_common import assert_same
     from oracle import rq_oracle as orc
@@ -138,7 +106,16 @@ def _check(rank, world, case):
     from tse_amd import parallel as par
     from tse_amd.rq import compute
     t = _table(case, world)
-    if case == "giant":
+    cont = -1
+    if case == "live_giant":
+        # a coverage-only project larger than a rank's share, every row before the limit: cut into
+        # date-range pieces (parallel.live_plan); its eligibility summed over the pieces
+        plan = par.live_plan(t, world)
+        assert len(plan.cut) == 1 and plan.moved > 0, "the live giant was meant to be cut"
+        lo, hi = plan.bounds[rank]
+        ts, rows = par.take_split(t, plan, rank)
+        cont = plan.cont[rank]
+    elif case == "giant":
         # a giant project's coverage rows that no analysis reads spread over the ranks
         # (parallel.split_plan): shards then hold rows of a project they do not own
         plan = par.split_plan(t, world)
@@ -151,6 +128,8 @@ def _check(rank, world, case):
     eng = E.Engine(0)
     eng.upload(ts)
     st = eng.build_store()
+    if case == "live_giant":
+        par.fix_cut_eligibility(par.GpuEligibility(eng), plan.cut, lo, hi, world)
     M = par.agree_max(int(st.max_fuzz_per_project))
     g1 = _HostView(par.GpuRQ1Shard(eng, M), eng.dev)
     part, counts, it, idt, reran = par.rq1_sharded(g1, rank, world)
@@ -161,9 +140,11 @@ def _check(rank, world, case):
     torch.distributed.all_reduce(elig)
     late = g1.s.bufs.late.cpu().numpy()
     total3, cols3, st3 = par.rq3_sharded(_RQ3View(par.GpuRQ3Shard(eng), eng.dev, rows.issues), rank, world)
-    r2 = par.rq2_count_sharded(_RQ2View(par.GpuRQ2CountShard(eng), eng.dev), rank, world, lo, hi)
+    # (RQ2 count / RQ4b: the GPU shards straight into the drivers - gloo stages device tensors through
+    # the host)
+    r2 = par.rq2_count_sharded(par.GpuRQ2CountShard(eng, cont), rank, world, lo, hi, cont=cont)
     r4 = par.rq4a_sharded(_RQ4aView(par.GpuRQ4aShard(eng, M), eng.dev), rank, world, lo, hi)
-    r4b = par.rq4b_sharded(_RQ4bView(par.GpuRQ4bShard(eng), eng.dev), rank, world)
+    r4b = par.rq4b_sharded(par.GpuRQ4bShard(eng, cont), rank, world, lo=lo, hi=hi, cont=cont)
     r2a = par.rq2_add_sharded(_RQ2AddView(par.GpuRQ2AddShard(eng), eng.dev, rows), rank, world)
     any_rerun = torch.tensor([int(reran)])
     torch.distributed.all_reduce(any_rerun)
@@ -217,6 +198,17 @@ def _spawn(case, world, tmp_path):
 @pytest.mark.parametrize("case", ["collide", "last_shard_no_issues"])
 def test_gpu_sharded_rq1_rq3(case, tmp_path):
     _spawn(case, 2, tmp_path)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_gpu_live_giant_cut_six_drivers(world, tmp_path):
+    """All six drivers on GPU shards of parallel.live_plan: a coverage-only project larger than a
+    rank's share, every row before the limit (read by RQ2 count and RQ4b), cut into date-range pieces
+    over consecutive ranks - its eligibility summed over the pieces (fz_store_elig_counts /
+    fz_store_set_eligible), its sessions through the project-major exchange (fz_piece_values,
+    fz_pack_runs, fz_transpose_runs) and its Spearman / Shapiro-Wilk from value buckets
+    (fz_series_dist_*) - recombined results against the oracle on the whole table."""
+    _spawn("live_giant", world, tmp_path)
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -299,7 +291,7 @@ def _deferred_check(rank, world):
     with torch.cuda.stream(eng.stream):
         eager = [par.rq2_count_sharded(par.GpuRQ2CountShard(eng), rank, world, lo, hi),
                  par.rq4a_sharded(par.GpuRQ4aShard(eng, M), rank, world, lo, hi),
-                 par.rq4b_sharded(par.GpuRQ4bShard(eng), rank, world)]
+                 par.rq4b_sharded(par.GpuRQ4bShard(eng), rank, world, lo=lo, hi=hi)]
     for _ in range(2):  # (twice: the shards' buffers are reused by the second step)
         kids = [eng.child() for _ in range(3)]
         pend = []
@@ -309,7 +301,7 @@ def _deferred_check(rank, world):
         with torch.cuda.stream(kids[1].stream):
             pend.append(par.rq4a_sharded(par.GpuRQ4aShard(kids[1], M), rank, world, lo, hi, finish_later=True))
         with torch.cuda.stream(kids[2].stream):
-            pend.append(par.rq4b_sharded(par.GpuRQ4bShard(kids[2]), rank, world, finish_later=True))
+            pend.append(par.rq4b_sharded(par.GpuRQ4bShard(kids[2]), rank, world, lo=lo, hi=hi, finish_later=True))
         assert all(isinstance(d, par.Deferred) for d in pend)
         cur = torch.cuda.current_stream(eng.dev)
         for k in kids:

@@ -1,12 +1,13 @@
-"""The project-sharded path on the FULL config-3 and config-5 tables (100M coverage
-rows over 10k projects, "project-sharded over 2/4/8 MI355X"; config 5 Zipf-skewed, its ~20M-row giant
-whole on its owner's shard, its coverage rows no analysis reads spread over the ranks at eight ranks -
-parallel.split_plan): two, four or eight ranks on cuda:0, each holding only its
-``parallel.split_plan`` share of the projects, run RQ2-count and RQ4b through libfz
-(fz_rq2_count_ex / fz_rq4b_ex with the session statistics skipped, then the all-to-all by session
-index to the session owners, fz_rq2_session_stats / fz_rq4b_session_stats there, and the gathers)
-over gloo - the same driver code bench.py runs over RCCL.  Rank 0 then builds the whole table on
-one engine and requires the recombined results to equal the single-GPU ones, which
+"""The project-sharded path on the FULL 100M-row tables ("100M coverage rows over
+10k projects, project-sharded over 2/4/8 MI355X"): configs 3 and 5 and their live-row variants c3L /
+c5L (every row before the analysis limit, synth.py).  Two, four or eight ranks on cuda:0, each
+holding its ``parallel.live_plan`` share - a project larger than one share (config 5's 20.8M-row
+Zipf giant) cut into date-range pieces over consecutive ranks, its eligibility summed over the
+pieces - run RQ2-count and RQ4b through libfz (fz_rq2_count_ex / fz_rq4b_ex project-major, the
+project-major session exchange to the session owners, fz_rq2_session_stats_grouped /
+fz_rq4b_session_stats_grouped there, a cut project's Spearman / Shapiro-Wilk from value buckets,
+the gathers) over gloo - the same driver code bench.py runs over RCCL.  Rank 0 then builds the whole
+table on one engine and requires the recombined results to equal the single-GPU ones, which
 test_gpu_fullsize.py pins to numpy / scipy at this size:
 
 * the session transposition of rq2_coverage_count.py:329-333 - offsets and every value, exact;
@@ -22,7 +23,6 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from test_gpu_parallel import _RQ2View, _RQ4bView
 from test_parallel import _free_port
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
@@ -56,10 +56,9 @@ def _check(rank, world, name):
     t0 = time.perf_counter()
     t = synth.generate(synth.config(name))
     assert t.n_rows >= 99_000_000
-    # project shards; a project larger than a rank's share (config 5's Zipf giant at 8 ranks) keeps
-    # every row an analysis reads on its owner and has its other coverage rows spread over the
-    # ranks (parallel.split_plan)
-    plan = par.split_plan(t, world)
+    # project shards; a project larger than a rank's share (config 5's Zipf giant) cut into date-range
+    # pieces over consecutive ranks (parallel.live_plan)
+    plan = par.live_plan(t, world)
     bounds = plan.bounds
     lo, hi = bounds[rank]
     if rank == 0:
@@ -68,16 +67,19 @@ def _check(rank, world, name):
                 + np.bincount(t.i_project.astype(np.int64), minlength=len(t.projects)))
         share = [(len(b) + len(c) + len(i)) / (t.n_rows / world)
                  for b, c, i in zip(plan.builds, plan.coverage, plan.issues)]
-        print(f"{name} world {world}: largest project {int(rows.max()):,} rows, {plan.moved:,} rows moved off "
-              f"their owner; shard shares of the mean " + " ".join(f"{x:.2f}" for x in share), flush=True)
-        if name == "c5" and world == 8:
-            assert plan.moved > 0 and max(share) < 1.05, "the Zipf giant's movable rows were meant to spread"
+        print(f"{name} world {world}: largest project {int(rows.max()):,} rows, cut projects {plan.cut} over "
+              f"{[plan.ranks[p] for p in plan.cut]}, {plan.moved:,} rows off their owner; shard shares of the mean "
+              + " ".join(f"{x:.2f}" for x in share), flush=True)
+        if name.startswith("c5") and world == 8:
+            assert plan.moved > 0 and max(share) < 1.15, "the Zipf giant was meant to be cut"
     ts, _ = par.take_split(t, plan, rank)
+    cont = plan.cont[rank]
     eng = E.Engine(0)
     eng.upload(ts)
     eng.build_store()
-    r2 = par.rq2_count_sharded(_RQ2View(par.GpuRQ2CountShard(eng), eng.dev), rank, world, lo, hi)
-    r4b = par.rq4b_sharded(_RQ4bView(par.GpuRQ4bShard(eng), eng.dev), rank, world)
+    par.fix_cut_eligibility(par.GpuEligibility(eng), plan.cut, lo, hi, world)
+    r2 = par.rq2_count_sharded(par.GpuRQ2CountShard(eng, cont), rank, world, lo, hi, cont=cont)
+    r4b = par.rq4b_sharded(par.GpuRQ4bShard(eng, cont), rank, world, lo=lo, hi=hi, cont=cont)
     eng.close()
     del ts, eng
     print(f"rank {rank}: shard [{lo}, {hi}) of {len(t.projects)} projects, sharded RQ2-count + RQ4b "
@@ -109,7 +111,8 @@ def _check(rank, world, name):
     assert_same(ours4b, ref4b, "rq4b")
 
 
-@pytest.mark.parametrize("name,world", [("c3", 2), ("c3", 4), ("c3", 8), ("c5", 2), ("c5", 4), ("c5", 8)])
+@pytest.mark.parametrize("name,world", [("c3", 2), ("c3", 8), ("c5", 4), ("c5", 8), ("c3L", 4), ("c5L", 2),
+                                        ("c5L", 8)])
 def test_sharded_fullsize_matches_single_gpu(name, world, tmp_path):
     errfile = str(tmp_path / "err")
     try:

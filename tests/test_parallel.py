@@ -59,6 +59,8 @@ def make_table(case: str, world: int) -> Tables:
                statuses=t.statuses, corpus_csv=t.corpus_csv)
     if case == "giant":
         t = add_giant(t)
+    if case == "live_giant":
+        t = add_live_giant(t)
     if case == "last_shard_no_issues":
         lo, _ = par.shard_bounds(t, world)[-1]
         keep = t.i_project.astype(np.int64) < lo
@@ -111,13 +113,170 @@ def add_giant(t: Tables, extra: int = 90000) -> Tables:
     return dataclasses.replace(t, corpus_csv="\n".join(lines) + "\n")
 
 
+def add_live_giant(t: Tables, extra: int = 80000) -> Tables:
+    """A coverage-only project (its builds and issues dropped) grown to `extra` more coverage rows ten
+    minutes apart BEFORE its first row - all of them before the analysis limit, so every analysis
+    that reads coverage reads them (rq2_coverage_count.py:292-333 and rq4b's full series) - and put
+    in rq4b's group 2: larger than a rank's share at worlds 2, 3 and 8, live_plan cuts it into
+    pieces.  (NULL rows and zero coverage among the new rows.)"""
+    import dataclasses
+    from oracle import rq_oracle as orc
+    elig = orc.eligible_projects(t)
+    g = int(elig[3])
+    rng = np.random.default_rng(91)
+    first = int(t.c_date[t.c_project == g].min())
+    dates = first - (np.arange(extra, dtype=np.int64)[::-1] + 1) * 600_000_000
+    total = rng.integers(1000, 5000, size=extra).astype(np.int64)
+    covered = (total * rng.uniform(0.0, 0.8, size=extra)).astype(np.int64)
+    covered[::89] = 0
+    total[::1999] = 0                                  # zero total: kept only by raw_n (:300-303)
+    covered[::1999] = 0
+    valid = rng.random(extra) < 0.93
+    cov = np.where(valid & (total > 0), covered / np.maximum(total, 1) * 100.0, 0.0)
+    cat = lambda a, b: np.concatenate([a, b.astype(a.dtype)])  # noqa: E731
+    kb, ki = t.b_project != g, t.i_project != g
+    t = dataclasses.replace(
+        t, c_project=cat(t.c_project, np.full(extra, g)), c_date=cat(t.c_date, dates), c_coverage=cat(t.c_coverage, cov),
+        c_coverage_valid=cat(t.c_coverage_valid, valid), c_covered=cat(t.c_covered, np.where(valid, covered, 0)),
+        c_covered_valid=cat(t.c_covered_valid, valid), c_total=cat(t.c_total, np.where(valid, total, 0)),
+        c_total_valid=cat(t.c_total_valid, valid),
+        b_project=t.b_project[kb], b_type=t.b_type[kb], b_result=t.b_result[kb], b_time=t.b_time[kb],
+        b_modules=t.b_modules[kb], b_revisions=t.b_revisions[kb], b_name=t.b_name[kb],
+        i_number=t.i_number[ki], i_project=t.i_project[ki], i_rts=t.i_rts[ki], i_status=t.i_status[ki],
+        i_new_id=t.i_new_id[ki])
+    lines = t.corpus_csv.splitlines()
+    name = t.projects[g]
+    for k, ln in enumerate(lines):
+        if ln.startswith(name + ","):
+            f = ln.split(",")
+            lines[k] = f"{name},True,{f[4]},,{f[4]},0.0,"  # group 2: corpus at creation (rq4b:183-219)
+            break
+    else:  # (not in the CSV: a row in group 2)
+        lines.append(f"{name},True,2016-01-01T00:00:00+00:00,,2016-01-01T00:00:00+00:00,0.0,")
+    return dataclasses.replace(t, corpus_csv="\n".join(lines) + "\n")
+
+
+import contextlib  # noqa: E402
+
+
+@contextlib.contextmanager
+def elig_override(ov):
+    """The oracle's eligible set with the cut projects' flags of parallel.fix_cut_eligibility (its
+    functions look eligible_projects up at call time)."""
+    from oracle import rq_oracle as orc
+    if not ov:
+        yield
+        return
+    orig = orc.eligible_projects
+
+    def patched(t):
+        e = set(orig(t).tolist())
+        for p, f in ov.items():
+            (e.add if f else e.discard)(p)
+        return np.array(sorted(e), np.int64)
+    orc.eligible_projects = patched
+    try:
+        yield
+    finally:
+        orc.eligible_projects = orig
+
+
+class OracleEligibility:
+    """fix_cut_eligibility's store access on a rank's oracle table: its qualifying-row counts and an
+    override the rank's oracle shards apply (elig_override)."""
+
+    def __init__(self, t, ov):
+        self.t, self.ov = t, ov
+
+    def elig_counts(self, ids):
+        t = self.t
+        m = t.c_coverage_valid & (t.c_coverage > 0) & (t.c_date < LIMIT_US)
+        cnt = np.bincount(t.c_project[m].astype(np.int64), minlength=len(t.projects))
+        return torch.from_numpy(cnt[np.asarray(ids, np.int64)].astype(np.int64))
+
+    def set_eligible(self, ids, flags):
+        for p, f in zip(np.asarray(ids).tolist(), np.asarray(flags).tolist()):
+            self.ov[int(p)] = bool(f)
+
+
+class OracleExchange:
+    """The project-major exchange primitives and a cut project's tests in numpy / scipy (what
+    fz_pack_runs, fz_transpose_runs, fz_sort_f64 and fz_series_dist_* do on the GPU)."""
+
+    def pack(self, a, b, runs, sl, own, n):
+        out = np.zeros(n)
+        dst = np.concatenate([[0], np.cumsum(sl.sum(1))[:-1]])
+        for j, (src, off, ln, base) in enumerate(runs):
+            x = (a if src == 0 else b).numpy()
+            for d, (lo, hi) in enumerate(own):
+                s0, s1 = max(base, lo), min(base + ln, hi)
+                if s1 > s0:
+                    at = int(dst[d] + sl[d, :j].sum())
+                    out[at:at + s1 - s0] = x[off + s0 - base:off + s1 - base]
+        return torch.from_numpy(out)
+
+    def transpose(self, vals, roffs, grp, S):
+        G = 1 if grp is None else 2
+        v = vals.numpy()
+        lens = np.diff(roffs)
+        key = np.concatenate([np.arange(ln) * G + (0 if grp is None else int(grp[k])) for k, ln in enumerate(lens)]) \
+            if len(lens) else np.zeros(0, np.int64)
+        o = np.argsort(key, kind="stable")
+        offs = np.concatenate([[0], np.cumsum(np.bincount(key, minlength=S * G))]).astype(np.int64)
+        return torch.from_numpy(v[o].copy()), torch.from_numpy(offs[:S * G + 1])
+
+    def sort(self, x):
+        o = np.argsort(x.numpy(), kind="stable")
+        return torch.from_numpy(x.numpy()[o]), torch.from_numpy(o.astype(np.int32))
+
+    def dist_state(self):
+        return np.zeros(10), np.full(4, np.nan)
+
+    def dist_partials(self, ps, v, g, m, g0, n, params, x0):
+        # (the bucket itself: values and their series indices; the combine rebuilds the series)
+        return torch.cat([v, g.to(torch.float64)]) if ps == 0 else torch.zeros(0, dtype=torch.float64)
+
+    def dist_combine(self, ps, parts, k, n, params, result, sizes=None):
+        if ps != 0:
+            return
+        p = parts.numpy()
+        x = np.empty(n)
+        o = 0
+        for m in np.asarray(sizes).tolist():
+            x[p[o + m:o + 2 * m].astype(np.int64)] = p[o:o + m]
+            o += 2 * m
+        result[:] = OracleRQ2CountShard.series_tests(None, torch.from_numpy(x))
+
+
+def _trend_values(t, p):
+    """RQ2 count's trend of project p on this table (queries1.py:120-129, rq2_coverage_count.py:
+    300-303) and its fetched rows / NULL-line rows."""
+    m = (t.c_project == p) & t.c_coverage_valid & (t.c_coverage != 0) & (t.c_date < LIMIT_US)
+    rows = np.nonzero(m)[0]
+    rows = rows[np.argsort(t.c_date[rows], kind="stable")]
+    keep = (t.c_total[rows] != 0) | ~t.c_total_valid[rows]
+    kr = rows[keep]
+    null = int((~(t.c_total_valid[kr] & t.c_covered_valid[kr])).sum())
+    vals = t.c_covered[kr].astype(np.float64) / t.c_total[kr].astype(np.float64) * 100
+    return vals, len(rows), null
+
+
+def _series_values(t, p):
+    """rq4b's full series of project p on this table (coverage > 0, date < LIMIT, rq4b:315-326)."""
+    m = (t.c_project == p) & t.c_coverage_valid & (t.c_coverage > 0) & (t.c_date < LIMIT_US)
+    rows = np.nonzero(m)[0]
+    return t.c_coverage[rows[np.argsort(t.c_date[rows], kind="stable")]]
+
+
 class OracleRQ1Shard:
-    def __init__(self, t, rows, max_iter, threshold=100):
+    def __init__(self, t, rows, max_iter, threshold=100, ov=None):
+        self.ov = ov
         self.t, self.rows, self.M, self.threshold = t, rows, max_iter, threshold
 
     def run(self, ext):
         from oracle import rq_oracle as orc
-        r = orc.rq1(self.t, self.threshold, ext=None if ext is None else tuple(x.numpy() for x in ext))
+        with elig_override(self.ov):
+            r = orc.rq1(self.t, self.threshold, ext=None if ext is None else tuple(x.numpy() for x in ext))
         self.result = r
         c = np.zeros(par.RQ1_NCOUNTS, np.int64)
         c[par.RQ1_ISSUES_LIM], c[par.RQ1_ISSUES_LIM_PROJECTS] = r.n_issues_lim, r.n_issues_lim_projects
@@ -147,12 +306,14 @@ class OracleRQ1Shard:
 
 
 class OracleRQ3Shard:
-    def __init__(self, t, rows):
+    def __init__(self, t, rows, ov=None):
+        self.ov = ov
         self.t, self.rows = t, rows
 
     def run(self):
         from oracle import rq_oracle as orc
-        r = orc.rq3(self.t, flush_last=True, on_null="count")
+        with elig_override(self.ov):
+            r = orc.rq3(self.t, flush_last=True, on_null="count")
         c = np.zeros(par.RQ3_NCOUNTS, np.int64)
         c[par.RQ3_ISSUES], c[par.RQ3_DETECTED], c[par.RQ3_NON_DETECTED] = r.n_all_issues, len(r.det_pct), len(r.non_pct)
         c[par.RQ3_ELIGIBLE], c[par.RQ3_NON_LAST] = len(orc.eligible_projects(self.t)), r.n_non_last
@@ -173,17 +334,18 @@ def _offs_to_ids(offs, S):
     return torch.repeat_interleave(torch.arange(S, dtype=torch.int64), o[1:S + 1] - o[:S])
 
 
-class OracleRQ2CountShard:
+class OracleRQ2CountShard(OracleExchange):
     """One rank's RQ2 count on the CPU restatement (per-project columns over the global project
-    axis + the local coverage_by_session_index), and the session / series statistics the exchange
+    axis + the local trend values project-major), and the session / series statistics the exchange
     needs, computed exactly as rq_oracle.rq2_count does."""
 
-    def __init__(self, t):
-        self.t = t
+    def __init__(self, t, cont=-1, ov=None):
+        self.t, self.cont, self.ov = t, cont, ov
 
     def run(self):
         from oracle import rq_oracle as orc
-        r = orc.rq2_count(self.t)
+        with elig_override(self.ov):
+            r = orc.rq2_count(self.t)
         P = len(self.t.projects)
         el = np.zeros(P, np.int64)
         el[r.eligible] = 1
@@ -195,8 +357,13 @@ class OracleRQ2CountShard:
         cols["sw_p"][r.eligible] = r.sw_p
         cols["corr"][r.eligible[r.raw_n > 0]] = r.corr
         out = {k: torch.from_numpy(v) for k, v in cols.items()}
-        out["session_offsets"] = torch.from_numpy(r.session_offsets.astype(np.int64))
-        out["session_values"] = torch.from_numpy(r.session_values.astype(np.float64))
+        vals = [_trend_values(self.t, p)[0] for p in r.eligible.tolist()]
+        out["values"] = torch.from_numpy(np.concatenate(vals) if vals else np.zeros(0))
+        out["null_lines"] = torch.zeros(1, dtype=torch.int64)
+        if self.cont >= 0:
+            v, raw, null = _trend_values(self.t, self.cont)
+            out["piece_values"] = torch.from_numpy(v)
+            out["piece_counts"] = torch.tensor([len(v), raw, null], dtype=torch.int64)
         return out
 
     def merge_runs(self, vals, runs):
@@ -244,12 +411,13 @@ class OracleRQ2AddShard:
     """One rank's RQ2 add on the CPU restatement: flags over the global project axis, change rows
     with global build / coverage row ids (-1 kept)."""
 
-    def __init__(self, t, rows):
-        self.t, self.rows = t, rows
+    def __init__(self, t, rows, ov=None):
+        self.t, self.rows, self.ov = t, rows, ov
 
     def run(self):
         from oracle import rq_oracle as orc
-        return rq2_add_part(orc.rq2_add(self.t), len(self.t.projects), self.rows)
+        with elig_override(self.ov):
+            return rq2_add_part(orc.rq2_add(self.t), len(self.t.projects), self.rows)
 
 
 def rq2_add_part(r, P, rows):
@@ -281,12 +449,14 @@ def rq2_add_result(flags, cols):
 class OracleRQ4aShard:
     """One rank's RQ4a on the CPU restatement, in fz_rq4a's output layout."""
 
-    def __init__(self, t, max_iter):
+    def __init__(self, t, max_iter, ov=None):
+        self.ov = ov
         self.t, self.M = t, max_iter
 
     def run(self):
         from oracle import rq_oracle as orc
-        r = orc.rq4a(self.t)
+        with elig_override(self.ov):
+            r = orc.rq4a(self.t)
         P = len(self.t.projects)
         c = np.zeros(12, np.int64)
         c[0] = len(r.g1_total)
@@ -337,6 +507,10 @@ class OracleRQ4bShard(OracleRQ2CountShard):
     """One rank's RQ4b on the CPU restatement, in fz_rq4b_ex's shard output layout."""
 
     def run(self):
+        with elig_override(self.ov):
+            return self._run()
+
+    def _run(self):
         from oracle import rq_oracle as orc
         t = self.t
         P = len(t.projects)
@@ -346,17 +520,11 @@ class OracleRQ4bShard(OracleRQ2CountShard):
         for g in range(4):
             member[groups[f"group{g + 1}"]] |= 1 << g
         full = orc.rq4b_full_series(t, P)
-        # the G1/G2 series grouped by (session index, group) segment, projects in order inside one
-        vals, segs = [], []
-        for p in range(P):
-            v = t.c_coverage[full.rows(p)] if member[p] & 3 else np.zeros(0)
-            vals.append(v)
-            segs.append(2 * np.arange(len(v), dtype=np.int64) + (0 if member[p] & 2 else 1))
+        # the G1/G2 series project-major (project order, date order inside one)
+        vals = [t.c_coverage[full.rows(p)] if member[p] & 3 else np.zeros(0) for p in range(P)]
+        offs = np.concatenate([[0], np.cumsum([len(v) for v in vals])]).astype(np.int64)
+        m_loc = max([len(v) for v in vals] + [0])
         vals = np.concatenate(vals) if vals else np.zeros(0)
-        segs = np.concatenate(segs) if segs else np.zeros(0, np.int64)
-        m_loc = int(segs.max()) // 2 + 1 if len(segs) else 0
-        grouped = np.argsort(segs, kind="stable")
-        offs = np.concatenate([[0], np.cumsum(np.bincount(segs, minlength=2 * m_loc))]).astype(np.int64)
         order = common.corpus_columns(t)[2].tolist()
         projs, pre, post = orc.rq4b_deltas(t, elig, groups, corpus_us)
         # CSV row of each delta column: the k-th qualifying row of the corpus order
@@ -375,11 +543,16 @@ class OracleRQ4bShard(OracleRQ2CountShard):
         for g in range(4):
             c[5 + g] = len(groups[f"group{g + 1}"])
         T = lambda a, dt=np.float64: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))  # noqa: E731
-        return {"counts": T(c, np.int64), "member": T(member, np.int64),
-                "trend_values": T(vals[grouped]), "trend_offsets": T(offs, np.int64),
+        out = {"counts": T(c, np.int64), "member": T(member, np.int64),
+                "trend_values": T(vals), "trend_offsets": T(offs, np.int64),
                 "pre_cov": T(np.concatenate(pre) if projs else np.zeros(0)),
                 "post_cov": T(np.concatenate(post) if projs else np.zeros(0)), "delta_order": T(dord, np.int64),
                 "init_g2": T(init["group2"]), "init_g1": T(init["group1"])}
+        if self.cont >= 0:
+            v = _series_values(t, self.cont)
+            out["piece_values"] = T(v)
+            out["piece_counts"] = torch.tensor([len(v), len(v), 0], dtype=torch.int64)
+        return out
 
     def spearman_prefix(self, rows, n):
         n = int(n)
@@ -426,11 +599,19 @@ def _check(rank, world, case, threaded=False, deferred=False):
     from oracle import rq_oracle as orc
     from gpu_common import assert_same
     t = make_table(case, world)
+    cont, ov = -1, {}
     if case == "giant":  # the giant's movable coverage rows spread over the ranks (split_plan)
         plan = par.split_plan(t, world)
         assert plan.moved > 0, "the giant's rows past the date bounds were meant to move"
         lo, hi = plan.bounds[rank]
         ts, rows = par.take_split(t, plan, rank)
+    elif case == "live_giant":  # the live giant cut into date-range pieces (live_plan)
+        plan = par.live_plan(t, world)
+        assert len(plan.cut) == 1 and plan.moved > 0, "the live giant was meant to be cut"
+        lo, hi = plan.bounds[rank]
+        ts, rows = par.take_split(t, plan, rank)
+        cont = plan.cont[rank]
+        par.fix_cut_eligibility(OracleEligibility(ts, ov), plan.cut, lo, hi, world)
     else:
         lo, hi = par.shard_bounds(t, world)[rank]
         ts, rows = par.take_shard(t, lo, hi)
@@ -441,7 +622,7 @@ def _check(rank, world, case, threaded=False, deferred=False):
     M4 = par.agree_max(int(nF4.max()) if len(nF4) else 1)
 
     def rq1():
-        sh = OracleRQ1Shard(ts, rows, max(M, 1))
+        sh = OracleRQ1Shard(ts, rows, max(M, 1), ov=ov)
         part, counts, it, idt, reran = par.rq1_sharded(sh, rank, world)
         rows1 = par.gather_rows({"matched_issue": part["matched_issue"], "matched_build": part["matched_build"]},
                                 world)
@@ -452,12 +633,14 @@ def _check(rank, world, case, threaded=False, deferred=False):
     # deferred: the drivers' final host copies left to one par.finalize_all at the end (the bench's
     # single-thread sharded step)
     drivers = {"rq1": rq1,
-               "rq3": lambda: par.rq3_sharded(OracleRQ3Shard(ts, rows), rank, world),
-               "rq2a": lambda: par.rq2_add_sharded(OracleRQ2AddShard(ts, rows), rank, world),
-               "rq2": lambda: par.rq2_count_sharded(OracleRQ2CountShard(ts), rank, world, lo, hi,
-                                                    finish_later=deferred),
-               "rq4a": lambda: par.rq4a_sharded(OracleRQ4aShard(ts, M4), rank, world, lo, hi, finish_later=deferred),
-               "rq4b": lambda: par.rq4b_sharded(OracleRQ4bShard(ts), rank, world, finish_later=deferred)}
+               "rq3": lambda: par.rq3_sharded(OracleRQ3Shard(ts, rows, ov=ov), rank, world),
+               "rq2a": lambda: par.rq2_add_sharded(OracleRQ2AddShard(ts, rows, ov=ov), rank, world),
+               "rq2": lambda: par.rq2_count_sharded(OracleRQ2CountShard(ts, cont, ov), rank, world, lo, hi,
+                                                    finish_later=deferred, cont=cont),
+               "rq4a": lambda: par.rq4a_sharded(OracleRQ4aShard(ts, M4, ov=ov), rank, world, lo, hi,
+                                                finish_later=deferred),
+               "rq4b": lambda: par.rq4b_sharded(OracleRQ4bShard(ts, cont, ov), rank, world, lo=lo, hi=hi,
+                                                finish_later=deferred, cont=cont)}
     if threaded:
         # the bench's sharded step: every driver in its own thread over its own process group (their
         # collectives interleave differently on every rank)
@@ -483,7 +666,7 @@ def _check(rank, world, case, threaded=False, deferred=False):
         return
     assert_same(rq2_add_result(*res["rq2a"]), orc.rq2_add(t), "rq2_add")
     g = orc.rq1(t)
-    assert case == "giant" or int(any_rerun) > 0, "the table was built to need the cross-shard dedup"
+    assert case in ("giant", "live_giant") or int(any_rerun) > 0, "the table was built to need the cross-shard dedup"
     c = counts.numpy()
     assert c[par.RQ1_ISSUES_LIM] == g.n_issues_lim and c[par.RQ1_ISSUES_LIM_PROJECTS] == g.n_issues_lim_projects
     assert c[par.RQ1_FIXED_LIM] == g.n_fixed_lim and c[par.RQ1_FIXED_LIM_PROJECTS] == g.n_fixed_lim_projects
@@ -542,7 +725,8 @@ def test_shard_bounds_cover_and_balance():
 
 
 @pytest.mark.parametrize("world,case", [(2, "collide"), (3, "collide"), (3, "last_shard_no_issues"), (8, "collide"),
-                                        (8, "last_shard_no_issues"), (2, "giant"), (3, "giant"), (8, "giant")])
+                                        (8, "last_shard_no_issues"), (2, "giant"), (3, "giant"), (8, "giant"),
+                                        (2, "live_giant"), (3, "live_giant"), (8, "live_giant")])
 def test_sharded_rq1_rq3_match_whole_table(world, case, tmp_path):
     _spawn(world, case, tmp_path)
 

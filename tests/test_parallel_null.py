@@ -34,8 +34,7 @@ class OracleRQ2CountShardNull(OracleRQ2CountShard):
                 cols[k] = torch.zeros(len(t.projects), dtype=torch.int64)
             for k in ("sw_w", "sw_p", "corr"):
                 cols[k] = torch.full((len(t.projects),), float("nan"), dtype=torch.float64)
-            cols["session_offsets"] = torch.zeros(1, dtype=torch.int64)
-            cols["session_values"] = torch.zeros(0, dtype=torch.float64)
+            cols["values"] = torch.zeros(0, dtype=torch.float64)
             out = cols
         else:
             out = super().run()

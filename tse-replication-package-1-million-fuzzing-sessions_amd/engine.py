@@ -69,6 +69,7 @@ FZ_RQ2C_NCOUNTS, FZ_RQ2C_NSCALARS = 8, 8
 RQ2C_ELIGIBLE, RQ2C_SESSIONS, RQ2C_GE100, RQ2C_VALUES, RQ2C_NULL_LINES = range(5)
 RQ2C_CORR_MEAN, RQ2C_CORR_MEDIAN, RQ2C_SP_RHO, RQ2C_SP_P, RQ2C_SW_MEDIAN_P = range(5)
 FZ_RQ2C_SKIP_SESSION_STATS = 1
+FZ_RQ2C_PROJECT_MAJOR = 2
 
 
 class FzRq2CountOut(C.Structure):
@@ -124,6 +125,10 @@ FZ_RQ4B_NCOUNTS, FZ_RQ4B_NTESTS = 12, 8
  RQ4B_G4, RQ4B_VALUES) = range(10)
 RQ4B_MWU_P, RQ4B_CLIFF, RQ4B_BM_STAT, RQ4B_BM_P, RQ4B_LEVENE_W, RQ4B_LEVENE_P = range(6)
 FZ_RQ4B_SKIP_SESSION_STATS = 1
+FZ_RQ4B_PROJECT_MAJOR = 2
+FZ_PIECE_RQ2, FZ_PIECE_RQ4B = 0, 1
+FZ_DIST_PARAMS = 10
+DIST_PART_WIDTH = (14, 4, 6)  # FZ_DIST_PART_WIDTH(pass)
 
 
 class FzRq4bOut(C.Structure):
@@ -188,6 +193,13 @@ SIGNATURES = {
     "fz_sort_f64": (C.c_int, [_P, _P, _I64, _P, _P]),
     "fz_describe_f64": (C.c_int, [_P, _P, _I64, C.POINTER(FzDescribe)]),
     "fz_eligibility_count": (C.c_int, [_P, C.POINTER(FzTables), _I64, _P]),
+    "fz_store_elig_counts": (C.c_int, [_P, _P, _I64, _P]),
+    "fz_store_set_eligible": (C.c_int, [_P, _P, _P, _I64]),
+    "fz_piece_values": (C.c_int, [_P, _I64, C.c_int, _P, _P]),
+    "fz_pack_runs": (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, C.c_int, _P, _I64, _P]),
+    "fz_transpose_runs": (C.c_int, [_P, _P, _P, _P, _I64, C.c_int, _I64, _I64, _P, _P]),
+    "fz_series_dist_partials": (C.c_int, [_P, C.c_int, _P, _P, _I64, _I64, _I64, _P, _P, _P]),
+    "fz_series_dist_combine": (C.c_int, [_P, C.c_int, _P, _I64, _I64, _P, _P]),
 }
 
 _lib = None

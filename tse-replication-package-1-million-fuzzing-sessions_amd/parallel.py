@@ -267,6 +267,147 @@ def take_split(t: Tables, plan: SplitPlan, rank: int) -> Tuple[Tables, ShardRows
     return s, ShardRows(lo, hi, b, c, i)
 
 
+# ------------------------------------------------------------- live split: a project cut in pieces
+# split_plan above moves only rows no analysis reads.  When the rows of a project larger than one
+# rank's share ARE read (config 5's live-row variant: every one of the giant's 20.8 M rows precedes
+# the analysis limit), the project is cut into date ranges ("pieces") on consecutive ranks.  The
+# reference reads it as one series (queries1.py:120-129), value i of session i
+# (rq2_coverage_count.py:329-333, rq4b_coverage.py:917-931) and one shapiro / spearmanr
+# (rq2_coverage_count.py:305-322); the sharded drivers keep all of that exact across the cut:
+#   * eligibility (rq1:144-152): the pieces' counts summed every step (fix_cut_eligibility), the
+#     project eligible on its first piece's rank only (its owner), ineligible on the others;
+#   * sessions: every rank sends its runs - a project's values with the session index they start at
+#     (a later piece starts where the earlier pieces' values end) - to the session owners, which
+#     transpose the runs they receive (project-major exchange, _exchange_runs);
+#   * the cut project's Spearman / Shapiro-Wilk: its values sorted in value buckets over the piece
+#     ranks, per-bucket partial sums at their global sorted positions (_series_tests_cut).
+# A project is cut only when no analysis needs its rows in one place beyond that: it has no builds
+# and no issues (RQ1, RQ3, RQ2-add and RQ4a read nothing of it but its eligibility) and is not in
+# rq4b's group 3 / 4 (whose delta window, rq4b_coverage.py:745-772, is a date range of the series).
+@dataclass
+class LivePlan:
+    """Per rank r: bounds[r] = its own project range (a cut project belongs to its first piece's
+    rank), the global row ids it holds of each table (builds / coverage / issues / info), cont[r] =
+    the cut project whose later piece leads rank r's coverage rows (-1: none); cut = the cut
+    projects (ascending) and ranks[p] = the ranks holding project p's pieces in date order."""
+    bounds: List[Tuple[int, int]]
+    builds: List[np.ndarray]
+    coverage: List[np.ndarray]
+    issues: List[np.ndarray]
+    info: List[np.ndarray]
+    cont: List[int]
+    cut: List[int]
+    ranks: dict
+    moved: int  # coverage rows held by another rank than their project's owner
+
+
+def live_plan(t: Tables, world: int) -> LivePlan:
+    """Contiguous shards of about equal rows, a project larger than one share cut into pieces of
+    about one share each (in (date, row) order) when the rules above allow it; then the min-max
+    contiguous partition (partition_rows) over the sequence of whole projects and pieces."""
+    from .rq.common import corpus_groups
+    P = len(t.projects)
+    cp = t.c_project.astype(np.int64)
+    nb = np.bincount(t.b_project.astype(np.int64), minlength=P)
+    nc = np.bincount(cp, minlength=P)
+    ni = np.bincount(t.i_project.astype(np.int64), minlength=P)
+    total = (nb + nc + ni).astype(np.int64)
+    target = -(-int(total.sum()) // max(world, 1))
+    pieces = {}  # p -> [row ids of each piece], date order
+    if world > 1:
+        big = np.nonzero((total > target) & (nb == 0) & (ni == 0))[0]
+        if len(big):
+            q = t.c_coverage_valid & (t.c_coverage > 0) & (t.c_date < LIMIT_US)
+            elig = np.nonzero(np.bincount(cp[q], minlength=P) >= 365)[0]
+            groups, _ = corpus_groups(t, elig, add_missing_to_g1=False)
+            g34 = set(groups["group3"]) | set(groups["group4"])
+            g12 = set(groups["group1"]) | set(groups["group2"])
+            for p in big.tolist():
+                if p in g34:
+                    continue
+                rows = np.nonzero(cp == p)[0]
+                rows = rows[np.argsort(t.c_date[rows], kind="stable")]
+                # pieces of an eighth of a share: the partition below balances the ranks to within
+                # that, and a rank's consecutive pieces of the project are one piece
+                k = -(-len(rows) // max(target // 8, 1))
+                cuts = [len(rows) * j // k for j in range(k + 1)]
+                if p in g12:  # rq4b's initial coverage (:230-240) is the first piece's first value
+                    f = np.nonzero(q[rows])[0]
+                    if len(f):
+                        cuts = [0] + [c for c in cuts[1:] if c > f[0]]
+                pieces[p] = [rows[cuts[j]:cuts[j + 1]] for j in range(len(cuts) - 1) if cuts[j + 1] > cuts[j]]
+    # units: whole projects and pieces, in project order
+    u_proj, u_w, u_piece = [], [], []
+    for p in range(P):
+        if p in pieces:
+            for j, r in enumerate(pieces[p]):
+                u_proj.append(p)
+                u_w.append(len(r))
+                u_piece.append(j)
+        else:
+            u_proj.append(p)
+            u_w.append(int(total[p]))
+            u_piece.append(-1)
+    u_proj, u_piece = np.array(u_proj, np.int64), np.array(u_piece, np.int64)
+    ub = partition_rows(np.array(u_w, np.int64), world)
+    head_unit = np.searchsorted(u_proj, np.arange(P), "left")  # first unit of each project
+    lo = [int(np.searchsorted(head_unit, a, "left")) for a, _ in ub]
+    bounds = [(lo[r], lo[r + 1] if r + 1 < world else P) for r in range(world)]
+    cont, ranks = [], {}
+    for r, (a, b) in enumerate(ub):
+        cont.append(int(u_proj[a]) if a < b and u_piece[a] > 0 else -1)
+        for u in range(a, b):
+            if u_piece[u] >= 0:
+                ranks.setdefault(int(u_proj[u]), [])
+                if r not in ranks[int(u_proj[u])]:
+                    ranks[int(u_proj[u])].append(r)
+    cut = sorted(p for p, rs in ranks.items() if len(rs) > 1)
+    ranks = {p: ranks[p] for p in cut}
+
+    def sel(proj, a, b):
+        x = proj.astype(np.int64)
+        return np.nonzero((x >= a) & (x < b))[0]
+    is_cut = np.zeros(P, bool)
+    is_cut[cut] = True
+    # (pieces of a project that all landed on one rank: the project is whole there)
+    for p in [p for p in pieces if p not in ranks]:
+        del pieces[p]
+    B, Cv, I, PI = [], [], [], []
+    moved = 0
+    for r, (a, b) in enumerate(bounds):
+        B.append(sel(t.b_project, a, b))
+        own = sel(t.c_project, a, b)
+        own = own[~is_cut[cp[own]]]
+        extra = []
+        for u in range(*ub[r]):
+            p = int(u_proj[u])
+            if is_cut[p]:
+                extra.append(pieces[p][int(u_piece[u])])
+                if ranks[p][0] != r:
+                    moved += len(extra[-1])
+        Cv.append(np.sort(np.concatenate([own] + extra)) if extra else own)
+        I.append(sel(t.i_project, a, b))
+        PI.append(sel(t.pi_project, a, b))
+    return LivePlan(bounds, B, Cv, I, PI, cont, cut, ranks, moved)
+
+
+def cut_trend_bases(t: Tables, plan: LivePlan, rank: int):
+    """(one-GPU rehearsals, no exchange) the session base of rank `rank`'s leading piece: the RQ2
+    trend values (queries1.py:120-129 rows, total != 0, rq2_coverage_count.py:300-303) and the rq4b
+    series values (rq4b:315-326 rows) of the same project's pieces on earlier ranks - what the
+    drivers exchange on a real run.  -> (rq2 base, rq4b base), (0, 0) without a leading piece."""
+    p = plan.cont[rank]
+    if p < 0:
+        return 0, 0
+    rows = np.concatenate([plan.coverage[r] for r in plan.ranks[p] if r < rank])
+    rows = rows[t.c_project[rows].astype(np.int64) == p]
+    before = t.c_date[rows] < LIMIT_US
+    fetched = t.c_coverage_valid[rows] & (t.c_coverage[rows] != 0) & before
+    trend = fetched & ((t.c_total[rows] != 0) | ~t.c_total_valid[rows])
+    series = t.c_coverage_valid[rows] & (t.c_coverage[rows] > 0) & before
+    return int(trend.sum()), int(series.sum())
+
+
 # ---------------------------------------------------------------------------------- collectives
 import threading  # noqa: E402
 
@@ -671,62 +812,262 @@ def session_owners(sizes: np.ndarray, world: int) -> List[Tuple[int, int]]:
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
+def _owner_cuts(lengths: np.ndarray, world: int, M: int) -> List[Tuple[int, int]]:
+    """session_owners from the runs' lengths alone (O(projects), no per-session array): session i
+    holds one value of every run longer than i, so the values of sessions [0, k) number
+    cum(k) = sum(min(len, k)) - cut at the equal-values targets, as session_owners does."""
+    L = np.sort(np.asarray(lengths, np.int64)[np.asarray(lengths) > 0])
+    S = np.concatenate([[0], np.cumsum(L)]).astype(np.int64)
+
+    def cum(k):
+        j = int(np.searchsorted(L, k, "right"))
+        return int(S[j]) + k * (len(L) - j)
+    total = cum(M)
+    cuts = [0]
+    for r in range(1, world):
+        x = total * r / world
+        a, b = 0, M  # smallest k with cum(k) >= x
+        while a < b:
+            m = (a + b) // 2
+            if cum(m) >= x:
+                b = m
+            else:
+                a = m + 1
+        cuts.append(min(max(a, cuts[-1]), M))
+    cuts.append(M)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+@dataclass
+class _Runs:
+    """The project-major exchange of one analysis: every rank's runs (a project's values in date
+    order and the session they start at), from per-project counts gathered once."""
+    world: int
+    bounds: List[Tuple[int, int]]   # each rank's own project range
+    n_loc: np.ndarray                # [P] values of each project on its owner (its only / first piece)
+    cont: np.ndarray                 # [world] the cut project leading each rank's rows (-1)
+    cont_n: np.ndarray               # [world] that piece's values
+    n: np.ndarray = None             # [P] global values per project
+    cont_base: np.ndarray = None     # [world] the session the leading piece starts at
+
+    def __post_init__(self):
+        self.n = self.n_loc.copy()
+        self.cont_base = np.zeros(self.world, np.int64)
+        for r in range(self.world):
+            p = int(self.cont[r])
+            if p >= 0:
+                self.cont_base[r] = self.n[p]  # (the earlier pieces' values, owner's first)
+                self.n[p] += int(self.cont_n[r])
+
+    def runs_of(self, r):
+        """(src, src_off, len, base) of rank r's runs in project order: its leading piece (src 1:
+        fz_piece_values' buffer), then its own projects (src 0: the project-major values)."""
+        out = []
+        if self.cont[r] >= 0 and self.cont_n[r] > 0:
+            out.append((1, 0, int(self.cont_n[r]), int(self.cont_base[r])))
+        a, b = self.bounds[r]
+        nl = self.n_loc[a:b]
+        off = np.concatenate([[0], np.cumsum(nl)])
+        for k in np.nonzero(nl > 0)[0].tolist():
+            out.append((0, int(off[k]), int(nl[k]), 0))
+        return out
+
+    @staticmethod
+    def slices(runs, own):
+        """[dest, run] values of each run in each destination's session range."""
+        if not runs:
+            return np.zeros((len(own), 0), np.int64)
+        base = np.array([x[3] for x in runs], np.int64)
+        end = base + np.array([x[2] for x in runs], np.int64)
+        a = np.array([o[0] for o in own], np.int64)[:, None]
+        b = np.array([o[1] for o in own], np.int64)[:, None]
+        return np.maximum(0, np.minimum(end[None], b) - np.maximum(base[None], a))
+
+
+def _exchange_runs(shard, runs: _Runs, rank, own, a_vals, b_vals, group_of=None):
+    """Send this rank's runs to the owners of their sessions (one all-to-all of packed slices,
+    fz_pack_runs) and transpose what arrives (fz_transpose_runs) -> (the owner's values grouped by
+    segment (session, group), offsets [S * G + 1]).  group_of: [P] run group (0 = G2, 1 = G1) or
+    None (one group)."""
+    import torch
+    world = runs.world
+    mine = runs.runs_of(rank)
+    sl = _Runs.slices(mine, own)                      # [world, R]
+    send = sl.sum(1)
+    a, b = own[rank]
+    recv = np.array([_Runs.slices(runs.runs_of(s), [own[rank]])[0].sum() for s in range(world)], np.int64)
+    if world > 1:
+        packed = shard.pack(a_vals, b_vals, mine, sl, own, int(send.sum()))
+        got = all_to_all_v(packed, send.tolist(), recv.tolist())
+    else:  # (one rank: every session is its own; its runs in order are already the owner's runs)
+        got = shard.pack(a_vals, b_vals, mine, sl, own, int(send.sum()))
+    # the owner's runs: every project longer than its first session, in project order (a cut
+    # project's pieces arrive one after another, in date order: one run)
+    n = runs.n
+    live = np.nonzero(n > a)[0]
+    lens = np.minimum(n[live], b) - a
+    roffs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    grp = None if group_of is None else np.asarray(group_of)[live].astype(np.uint8)
+    return shard.transpose(got, roffs, grp, b - a)
+
+
+def _series_tests_cut(shard, p, holders, piece, base, n, rank, dev):
+    """spearmanr(range(n), x) / shapiro(x) (rq2_coverage_count.py:305-322) of cut project p, whose
+    n values lie in date-range pieces on the ranks `holders` (this rank's piece: `piece` from series
+    index `base`, or None).  Value buckets over the holders from a sorted sample of every piece
+    (ties never cross a bucket: a value goes to the first bucket whose upper splitter it does not
+    exceed), one all-to-all of (value, series index), a sort per bucket, then the three passes of
+    partial sums and their ordered combination (fz_series_dist_*) -> device [4] (rho, p, W, p) on
+    every rank."""
+    import torch
+    k = len(holders)
+    j = holders.index(rank) if rank in holders else -1
+    f64 = torch.float64
+    if j >= 0 and piece.numel():
+        val, pos = shard.sort(piece)
+        gidx = pos.to(torch.int64) + base
+        m = val.numel()
+        ns = min(256, m)
+        samp = val[torch.div(torch.arange(ns, device=val.device) * m, ns, rounding_mode="floor")]
+        head = torch.tensor([float(m)], dtype=f64, device=val.device)
+    else:
+        val = torch.zeros(0, dtype=f64, device=dev)
+        gidx = torch.zeros(0, dtype=torch.int64, device=dev)
+        samp = val
+        head = torch.zeros(0, dtype=f64, device=dev)
+    got = all_gather_v(torch.cat([head, samp.to(f64)]))
+    gh = host_many(*got)
+    xs, ws = [], []
+    for g in gh:
+        if len(g):
+            m_r, s_r = int(g[0]), g[1:]
+            xs.append(s_r)
+            ws.append(np.full(len(s_r), m_r / max(len(s_r), 1)))
+    xs = np.concatenate(xs) if xs else np.zeros(0)
+    ws = np.concatenate(ws) if ws else np.zeros(0)
+    o = np.argsort(xs, kind="stable")
+    xs, cw = xs[o], np.cumsum(ws[o])
+    tot = cw[-1] if len(cw) else 0.0
+    spl = np.array([xs[min(int(np.searchsorted(cw, tot * q / k, "left")), len(xs) - 1)] for q in range(1, k)]
+                   if len(xs) else np.zeros(0))
+    # this piece's bucket boundaries, every rank's (the all-to-all's counts)
+    if j >= 0 and val.numel():
+        sd = torch.as_tensor(spl, dtype=f64, device=val.device)
+        bnd = torch.searchsorted(val, sd, right=True) if len(spl) else torch.zeros(0, dtype=torch.int64, device=dev)
+        bnd = torch.cat([torch.zeros(1, dtype=torch.int64, device=val.device), bnd.to(torch.int64),
+                         torch.tensor([val.numel()], dtype=torch.int64, device=val.device)])
+    else:
+        bnd = torch.zeros(k + 1, dtype=torch.int64, device=dev)
+    allb = host_many(*all_gather(bnd))                 # [world][k + 1]
+    world = len(allb)
+    cnt = np.stack([np.diff(x) for x in allb])          # [world, k]: source -> bucket
+    sizes = cnt.sum(0)
+    send = np.zeros(world, np.int64)
+    recv = np.zeros(world, np.int64)
+    for q, h in enumerate(holders):
+        send[h] = cnt[rank, q] if j >= 0 else 0
+    if j >= 0:
+        recv[:] = cnt[:, j]
+    rv = all_to_all_cols([val, gidx], send.tolist()) if world > 1 else [val, gidx]
+    m = int(sizes[j]) if j >= 0 else 0
+    g0 = int(sizes[:j].sum()) if j >= 0 else 0
+    if j >= 0 and m:
+        v2, p2 = shard.sort(rv[0])
+        g2 = rv[1][p2.to(torch.int64)]
+    else:
+        v2, g2 = torch.zeros(0, dtype=f64, device=dev), torch.zeros(0, dtype=torch.int64, device=dev)
+    # scipy's y -= x[N // 2]: the series value at index n // 2, from the piece holding it
+    x0 = None
+    if j >= 0 and piece is not None and base <= n // 2 < base + piece.numel():
+        x0 = piece[n // 2 - base:n // 2 - base + 1]
+    params, result = shard.dist_state()
+    for ps in range(3):
+        part = shard.dist_partials(ps, v2, g2, m, g0, n, params, x0 if ps == 0 else None) if j >= 0 else \
+            torch.zeros(0, dtype=f64, device=dev)
+        parts = torch.cat(all_gather_v(part)) if world > 1 else part
+        shard.dist_combine(ps, parts, k, n, params, result, sizes)
+    return result
+
+
 def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_values: bool = True,
-                      finish_later: bool = False):
+                      finish_later: bool = False, cont: int = -1, cont_base=None):
     """Exact RQ2 count over project shards (rq2_coverage_count.py:244-483).
     ``shard.run()`` -> per-project columns over the global project axis (RQ2C_PROJECT_COLS), the
-    local trend values grouped by session index (project order inside a session) and their session
-    offsets; ``shard.merge_runs(values, runs)`` -> fz_runs_merge; ``shard.session_stats_grouped(
-    values, offsets, S, max_len)`` -> average / median / percentiles[S * 5] / ge100 of the sessions it
-    owns; ``shard.series_tests(x)`` -> (rho, p, W, p); ``shard.mean_median(x)`` -> (mean, median).
-    Exchange: per-project columns and every rank's session sizes gathered (projects [lo, hi) of
-    every rank), each rank's values of a session range sent to its owner as one contiguous slice
-    (all-to-all) and merged in rank order, per-session results gathered.  Returns a dict of host
-    numpy arrays (every rank)."""
+    local trend values project-major ("values": the eligible projects' values in (project, date)
+    order, n_trend[p] each), "null_lines"; with a leading piece of cut project `cont`,
+    "piece_values" / "piece_counts" (fz_piece_values).  Exchange (project-major, _exchange_runs):
+    per-project columns and the pieces' counts gathered, each rank's runs sent to the owners of their
+    sessions (one all-to-all), the owner's transpose + session statistics
+    (``shard.session_stats_grouped``), per-session results gathered; a cut project's tests from its
+    pieces (_series_tests_cut).  cont_base: (one-GPU rehearsal, world 1) the leading piece's session
+    base.  Returns a dict of host numpy arrays (every rank)."""
     import torch
     part = shard.run()
-    dev = part["session_values"].device
+    vals_a = part["values"]
+    dev = vals_a.device
     pc = [part[k][lo:hi] for k in RQ2C_PROJECT_COLS]
     pc = [v.to(torch.float64) if v.is_floating_point() else v.to(torch.int64) for v in pc]
+    nl = part.get("null_lines")
+    nl = nl.to(torch.int64).reshape(-1)[:1] if nl is not None else torch.zeros(1, dtype=torch.int64, device=dev)
+    vals_b = part.get("piece_values")
+    pcnt = part.get("piece_counts")
+    if pcnt is None or cont < 0:
+        pcnt = torch.zeros(3, dtype=torch.int64, device=dev)
+    info = torch.cat([torch.tensor([cont, lo, hi], dtype=torch.int64, device=dev), pcnt.to(torch.int64), nl])
     if world > 1:
         got = all_gather_cols(pc)
         pc = [torch.cat([got[r][j] for r in range(world)]) for j in range(len(pc))]
-    offs = part["session_offsets"]
-    m_loc = offs.numel() - 1
-    M = agree_max(m_loc, dev) if world > 1 else m_loc
-    nl = part.get("null_lines")
-    if world > 1:
-        # this rank's session sizes, then its NULL-line count (rq2_coverage_count.py:300-303 raise)
-        row = torch.zeros(M + 1, dtype=torch.int64, device=dev)
-        row[:m_loc] = offs[1:] - offs[:-1]
-        if nl is not None:
-            row[M:] = nl.to(torch.int64).reshape(1)
-        mat = torch.stack(all_gather(row))
-        h = host_many(mat, offs, *pc)  # one device->host copy
-        mat_h, offs_h = h[0], h[1]
-        sizes_h, null_lines = mat_h[:, :M].sum(0), int(mat_h[:, M].sum())
-    else:  # (one rank: the sizes are the offsets' differences)
-        h = host_many(offs, nl if nl is not None else np.zeros(1, np.int64), *pc)
-        offs_h = h[0]
-        mat_h = np.diff(offs_h)[None]
-        sizes_h, null_lines = mat_h[0], int(np.sum(h[1]))
+        info_all = torch.stack(all_gather(info))
+    else:
+        info_all = info[None]
+    h = host_many(info_all, *pc)  # one device->host copy
+    info_h = h[0]
+    proj = dict(zip(RQ2C_PROJECT_COLS, h[1:]))
+    bounds = [(int(x[1]), int(x[2])) for x in info_h]
+    conts, cont_n, cont_raw = info_h[:, 0], info_h[:, 3], info_h[:, 4]
+    null_lines = int(info_h[:, 5].sum() + info_h[:, 6].sum())
     if null_lines:  # float(None) (rq2_coverage_count.py:300-303): every rank holds the sum, all raise here
         raise TypeError("float() argument must be a string or a real number, not 'NoneType'")
-    proj = dict(zip(RQ2C_PROJECT_COLS, h[2:]))
-    own = session_owners(sizes_h, world)
+    runs = _Runs(world, bounds, proj["n_trend"].astype(np.int64), conts.astype(np.int64), cont_n.astype(np.int64))
+    if world == 1 and cont >= 0 and cont_base is not None:  # (rehearsal: the base another rank would send)
+        runs.cont_base[0] = int(cont_base)
+    # a cut project's columns: counts summed over its pieces, tests from all of its values
+    cut = sorted({int(p) for p in conts.tolist() if p >= 0})
+    for p in cut:
+        proj["raw_n"][p] += int(cont_raw[conts == p].sum())
+        proj["n_trend"][p] = runs.n[p]
+    M = max(1, int(runs.n.max()) if len(runs.n) else 0)  # (sessions start as [[]], :285)
+    own = _owner_cuts(runs.n, world, M)
     a, b = own[rank]
     S = b - a
-    vals = part["session_values"][:int(offs_h[-1])]
-    if world > 1:
-        vals, goffs = exchange_grouped(shard, vals, offs_h, mat[:, :M], mat_h[:, :M], own, rank)
-    else:
-        goffs = offs
+    vals, goffs = _exchange_runs(shard, runs, rank, own, vals_a, vals_b)
     st = shard.session_stats_grouped(vals, goffs, S, len(proj["eligible"]))
     block = torch.cat([st["average"][:S, None], st["median"][:S, None], st["percentiles"][:5 * S].reshape(S, 5)], 1)
     if world > 1:  # per-session rows (average, median, 5 percentiles) of every owner, session order
         block = torch.cat([m.reshape(-1, 7).view(torch.float64) for m in all_gather_v(block.reshape(-1).view(
             torch.int64))])
-    K = int(np.sum(sizes_h >= 100))
+    # sessions with >= 100 values: a prefix, as long as the 100th longest run (:390)
+    srt = np.sort(runs.n)[::-1]
+    K = int(srt[99]) if len(srt) >= 100 else 0
+    K = min(K, M)
+    for p in cut:  # its Spearman / Shapiro-Wilk over every piece (:305-322), patched on every rank
+        holders = [r for r in range(world) if bounds[r][0] <= p < bounds[r][1] or conts[r] == p]
+        if world == 1:
+            holders = [0]
+        if rank in holders:
+            if bounds[rank][0] <= p < bounds[rank][1]:
+                off = int(runs.n_loc[bounds[rank][0]:p].sum())
+                piece, base = vals_a[off:off + int(runs.n_loc[p])], 0
+            else:
+                piece, base = vals_b[:int(cont_n[rank])], int(runs.cont_base[rank])
+        else:
+            piece, base = None, 0
+        res = host_many(_series_tests_cut(shard, p, holders, piece, base, int(runs.n[p]), rank, dev))[0]
+        proj["corr"][p], proj["sw_w"][p], proj["sw_p"][p] = res[0], res[2], res[3]
+        for j, key in ((5, "corr"), (3, "sw_w"), (4, "sw_p")):
+            pc[j][p] = float(proj[key][p])
+        pc[1][p] = int(proj["raw_n"][p])
+        pc[2][p] = int(proj["n_trend"][p])
     if hasattr(shard, "tail"):  # one library call (fz_rq2_count_tail), device in and out
         med = st["median"][:S] if world == 1 else block[:, 1].contiguous()
         tail = shard.tail(med, K, pc[5], pc[1], pc[0])
@@ -740,15 +1081,19 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     tensors = [block, tests, corr_mm]
     if gather_values:  # coverage_by_session_index.csv: every value, session-major, project order
         tensors.append(torch.cat(all_gather_v(vals)) if world > 1 else vals)
+    n_glob = runs.n
 
     def finish(h):  # (the one result copy)
         blk = h[0]
-        out = {"proj": proj, "session_offsets": np.concatenate([[0], np.cumsum(sizes_h)]).astype(np.int64), "K": K,
-               "average": blk[:, 0].copy(), "median": blk[:, 1].copy(), "percentiles": blk[:, 2:].reshape(-1).copy(),
-               "tests": tuple(float(v) for v in h[1]), "corr_mm": tuple(float(v) for v in h[2]),
-               "null_lines": null_lines}
+        out = {"proj": proj, "K": K, "average": blk[:, 0].copy(), "median": blk[:, 1].copy(),
+               "percentiles": blk[:, 2:].reshape(-1).copy(), "tests": tuple(float(v) for v in h[1]),
+               "corr_mm": tuple(float(v) for v in h[2]), "null_lines": null_lines}
         if gather_values:
             out["session_values"] = h[3]
+            sizes = np.zeros(M + 1, np.int64)  # session i holds one value of every run longer than i
+            np.add.at(sizes, np.minimum(n_glob, M), 1)
+            per = np.cumsum(sizes[::-1])[::-1][1:]
+            out["session_offsets"] = np.concatenate([[0], np.cumsum(per)]).astype(np.int64)
         return out
     d = Deferred(tensors, finish)
     return d if finish_later else d.result()
@@ -802,44 +1147,57 @@ def rq4a_sharded(shard, rank: int, world: int, lo: int, hi: int, finish_later: b
 RQ4B_VALUES = 9
 
 
-def rq4b_sharded(shard, rank: int, world: int, finish_later: bool = False):
+def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, finish_later: bool = False,
+                 cont: int = -1, cont_base=None):
     """Exact RQ4b over project shards (rq4b_coverage.py:1209-1261).  ``shard.run()`` -> counts,
-    member[P], the G1/G2 full coverage values grouped by (session index, group) segment
-    (trend_values; trend_offsets over 2 * sessions segments, G2 = group 0; project order inside a
-    segment), the delta columns (pre_cov / post_cov step-major, delta_order = CSV row of each
-    column; at least counts' lengths) and the initial-coverage samples;
-    ``shard.merge_runs(values, runs)``, ``shard.session_stats_grouped(values, offsets, S, max_len)``,
-    ``shard.spearman_prefix(rows, n)``, ``shard.row_medians(rows)`` and ``shard.two_sample(x, y)``
-    run the statistics (tensors or arrays in, tensors or arrays out).  Exchange: every rank's
-    segment sizes gathered, each rank's values of a session range sent to its owner as one
-    contiguous slice (all-to-all) and merged in rank order, per-session results, delta columns
-    (re-ordered by CSV row, :216, :744) and initial samples gathered.  Intermediates stay on the
-    device; the results are copied to the host once.  Returns a dict for rq/compute.rq4b_result
-    (host arrays, every rank)."""
+    member[P], the G1/G2 full coverage values project-major (trend_values, trend_offsets [P + 1]),
+    the delta columns (pre_cov / post_cov step-major, delta_order = CSV row of each column; at least
+    counts' lengths) and the initial-coverage samples; with a leading piece of cut project `cont`,
+    "piece_values" / "piece_counts" (fz_piece_values, rq4b kind).  ``shard.session_stats_grouped``,
+    ``shard.tail`` (or spearman_prefix / row_medians / two_sample) run the statistics.  Exchange:
+    per-project members and series lengths over the rank's own range [lo, hi) gathered (default: the
+    whole axis when world == 1), each rank's runs sent to their sessions' owners and transposed there
+    by (session, group) (_exchange_runs), per-session results, delta columns (re-ordered by CSV row,
+    :216, :744) and initial samples gathered.  Intermediates stay on the device; the results are
+    copied to the host once.  Returns a dict for rq/compute.rq4b_result (host arrays, every rank)."""
     import torch
     part = shard.run()
     counts = part["counts"].clone()
     dev = counts.device
     P = part["member"].numel()
-    offs_all = part["trend_offsets"]
-    # (the values' count from the counters: trend_offsets is written up to the shard's session count)
-    head = torch.stack([counts[RQ4B_SESSIONS], counts[RQ4B_VALUES], counts[RQ4B_DELTA_PROJECTS],
-                        counts[RQ4B_INIT_G2], counts[RQ4B_INIT_G1]])
-    m_loc, n, nd, n2, n1 = (int(v) for v in host_many(head)[0])  # one sync for every host-side size
-    offs2 = offs_all[:2 * m_loc + 1]
-    vals = part["trend_values"][:n]
-    M = agree_max(m_loc, dev) if world > 1 else m_loc
+    if lo is None:
+        if world > 1:
+            raise ValueError("rq4b_sharded: the rank's own project range (lo, hi) is needed at world > 1")
+        lo, hi = 0, P
+    toffs = part["trend_offsets"][:P + 1]
+    nloc = (toffs[1:] - toffs[:-1])[lo:hi].to(torch.int64)
+    member = part["member"][lo:hi].to(torch.int64)
+    vals_a = part["trend_values"]
+    vals_b = part.get("piece_values")
+    pcnt = part.get("piece_counts")
+    if pcnt is None or cont < 0:
+        pcnt = torch.zeros(3, dtype=torch.int64, device=dev)
+    info = torch.cat([torch.tensor([cont, lo, hi], dtype=torch.int64, device=dev), pcnt.to(torch.int64)])
     if world > 1:
-        row = torch.zeros(2 * M, dtype=torch.int64, device=dev)
-        row[:2 * m_loc] = offs2[1:] - offs2[:-1]
-        mat = torch.stack(all_gather(row))  # [world, 2M]: every rank's (session, group) sizes
+        got = all_gather_cols([member, nloc])
+        member = torch.cat([g[0] for g in got])
+        nloc = torch.cat([g[1] for g in got])
+        info_all = torch.stack(all_gather(info))
         all_reduce(counts)
-        mat_h, offs_h = host_many(mat, offs2)
-        own = session_owners(mat_h[:, 0::2].sum(0) + mat_h[:, 1::2].sum(0), world)
-        vals, goffs = exchange_grouped(shard, vals, offs_h, mat, mat_h, own, rank, k=2)
     else:
-        own = [(0, M)]
-        goffs = offs2
+        info_all = info[None]
+    info_h, member_h, nloc_h = host_many(info_all, member, nloc)
+    bounds = [(int(x[1]), int(x[2])) for x in info_h]
+    conts, cont_n = info_h[:, 0].astype(np.int64), info_h[:, 3].astype(np.int64)
+    # (a leading piece of a project outside G1 / G2 contributes no series)
+    cont_n = np.where((conts >= 0) & ((member_h[np.maximum(conts, 0)] & 3) != 0), cont_n, 0)
+    runs = _Runs(world, bounds, nloc_h.astype(np.int64), conts, cont_n)
+    if world == 1 and cont >= 0 and cont_base is not None:  # (rehearsal: the base another rank would send)
+        runs.cont_base[0] = int(cont_base)
+    M = int(runs.n.max()) if len(runs.n) else 0
+    own = _owner_cuts(runs.n, world, M) if world > 1 else [(0, M)]
+    group = np.where((member_h & 2) != 0, 0, 1)  # G2 -> segment 2s, G1 -> 2s + 1
+    vals, goffs = _exchange_runs(shard, runs, rank, own, vals_a, vals_b, group_of=group)
     a, b = own[rank]
     S = b - a
     st = shard.session_stats_grouped(vals, goffs, S, P)
@@ -850,6 +1208,9 @@ def rq4b_sharded(shard, rank: int, world: int, finish_later: bool = False):
         got = all_gather_cols(cols)
         cols = [torch.cat([g[j] for g in got]) for j in range(len(cols))]
     # coverage deltas: columns of every rank (CSV row, 7 pre, 7 post), put in corpus CSV order below
+    nd, n2, n1 = (int(v) for v in host_many(torch.stack([part["counts"][RQ4B_DELTA_PROJECTS],
+                                                          part["counts"][RQ4B_INIT_G2],
+                                                          part["counts"][RQ4B_INIT_G1]]))[0])
     proj = part["delta_order"][:nd]
     pre = part["pre_cov"][:7 * nd].reshape(7, nd)
     post = part["post_cov"][:7 * nd].reshape(7, nd)
@@ -909,6 +1270,55 @@ def rq4b_sharded(shard, rank: int, world: int, finish_later: bool = False):
                 "init_g2": x_h, "init_g1": y_h, "tests": np.asarray(tests_h, dtype=np.float64)}
     d = Deferred([counts, last_d, sp, pre, post, med, x, y, tests, *cols], finish)
     return d if finish_later else d.result()
+
+
+# ------------------------------------------------------------------------- cut projects' eligibility
+def fix_cut_eligibility(ctl, cut, lo: int, hi: int, world: int):
+    """GROUP BY project HAVING COUNT(*) >= 365 (rq1:144-152) of the cut projects (ascending, every
+    rank the same list) over all of their pieces: this store's counts summed over the ranks (one
+    all-reduce), the project eligible on its owner (lo <= p < hi) when the sum allows, ineligible on
+    a rank that holds only a later piece.  ctl: .elig_counts(ids) -> device int64 counts,
+    .set_eligible(ids, flags).  Run after every store build, before the analyses."""
+    import torch
+    if not cut:
+        return
+    ids = np.asarray(cut, np.int64)
+    cnt = ctl.elig_counts(ids)
+    if world > 1:
+        all_reduce(cnt)
+    own = torch.as_tensor(((ids >= lo) & (ids < hi)).astype(np.uint8), device=cnt.device)
+    ctl.set_eligible(ids, ((cnt >= 365).to(torch.uint8) & own))
+
+
+class GpuEligibility:
+    """fix_cut_eligibility's store access on a GPU engine (fz_store_elig_counts /
+    fz_store_set_eligible; device in, device out)."""
+
+    def __init__(self, eng):
+        import ctypes as C
+        from . import engine as E
+        self.E, self.C, self.eng = E, C, eng
+        self._ids = None
+
+    def _dev_ids(self, ids):
+        torch = self.eng.torch
+        if self._ids is None or self._ids[0] != tuple(ids.tolist()):
+            self._ids = (tuple(ids.tolist()), torch.as_tensor(ids.astype(np.int32), device=self.eng.dev))
+        return self._ids[1]
+
+    def elig_counts(self, ids):
+        torch = self.eng.torch
+        d = self._dev_ids(ids)
+        out = torch.empty(len(ids), dtype=torch.int64, device=self.eng.dev)
+        self.E._check(self.eng.lib, self.eng.lib.fz_store_elig_counts(self.eng.ctx, self.C.c_void_p(d.data_ptr()),
+                                                                      len(ids), self.C.c_void_p(out.data_ptr())))
+        return out
+
+    def set_eligible(self, ids, flags):
+        d = self._dev_ids(ids)
+        flags = flags.contiguous()
+        self.E._check(self.eng.lib, self.eng.lib.fz_store_set_eligible(self.eng.ctx, self.C.c_void_p(d.data_ptr()),
+                                                                       self.C.c_void_p(flags.data_ptr()), len(ids)))
 
 
 # ------------------------------------------------------------------------------------ row gathers
@@ -972,32 +1382,129 @@ class GpuRQ1Shard:
                                                 C.c_void_p(counts.data_ptr()), C.c_void_p(self.bufs.late.data_ptr())))
 
 
-class GpuRQ2CountShard:
-    """RQ2 count of one rank on its engine (fz_rq2_count_ex, fz_rq2_session_stats, fz_series_tests)."""
+class _GpuExchange:
+    """The project-major session exchange and a cut project's tests on one engine (fz_piece_values,
+    fz_pack_runs, fz_transpose_runs, fz_sort_f64, fz_series_dist_*): the shard methods the drivers
+    call (the CPU tests' oracle shards implement the same with numpy)."""
 
-    def __init__(self, eng):
+    def _piece(self, kind):
+        """This rank's leading piece of cut project self.cont: its filtered values (device)."""
+        E, C, eng = self.E, self.C, self.eng
+        torch = eng.torch
+        st = eng.stats
+        cap = max(int(st.max_cov_per_project), 1)
+        if getattr(self, "_pv", None) is None or self._pv.numel() < cap:
+            self._pv = torch.empty(cap, dtype=torch.float64, device=eng.dev)
+            self._pc = torch.zeros(3, dtype=torch.int64, device=eng.dev)
+        E._check(eng.lib, eng.lib.fz_piece_values(eng.ctx, int(self.cont), kind, C.c_void_p(self._pv.data_ptr()),
+                                                  C.c_void_p(self._pc.data_ptr())))
+
+    def pack(self, a, b, runs, sl, own, n):
+        """fz_pack_runs: this rank's runs (src, src_off, len, base) sliced by the owners' session
+        ranges (sl [world, R] values per slice) -> one buffer, destination-major."""
+        E, C, eng = self.E, self.C, self.eng
+        torch = eng.torch
+        out = torch.empty(max(n, 1), dtype=torch.float64, device=eng.dev)
+        R = len(runs)
+        if n == 0 or R == 0:
+            return out[:0]
+        desc = np.zeros((R, 4), np.int64)
+        desc[:, 0] = [x[1] for x in runs]
+        desc[:, 1] = [x[2] for x in runs]
+        desc[:, 2] = [x[3] for x in runs]
+        desc[:, 3] = [x[0] for x in runs]  # (src int32, pad 0: one little-endian int64)
+        in_off = np.concatenate([[0], np.cumsum(desc[:, 1])[:-1]]).astype(np.int64)
+        W = sl.shape[0]
+        dst = np.concatenate([[0], np.cumsum(sl.sum(1))[:-1]]).astype(np.int64)
+        table = np.zeros((W, R + 1), np.int64)
+        table[:, 1:] = np.cumsum(sl, 1)
+        table += dst[:, None]
+        cuts = np.array([o[0] for o in own] + [own[-1][1]], np.int64)
+        h = np.concatenate([desc.reshape(-1), in_off, cuts, table.reshape(-1)])
+        d = torch.from_numpy(h).to(eng.dev, non_blocking=False)
+        o1 = desc.size
+        o2 = o1 + R
+        o3 = o2 + W + 1
+        P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        a = a if a is not None and a.numel() else None
+        b = b if b is not None and b.numel() else None
+        E._check(eng.lib, eng.lib.fz_pack_runs(eng.ctx, P(a) if a is not None else None,
+                                               P(b) if b is not None else None, P(d), P(d[o1:]), R, P(d[o2:]), W,
+                                               P(d[o3:]), n, P(out)))
+        return out[:n]
+
+    def transpose(self, vals, roffs, grp, S):
+        """fz_transpose_runs: the owner's runs (offsets roffs, host) -> (values grouped by (session,
+        group) segment, offsets [S * G + 1]) over its S sessions (device)."""
+        E, C, eng = self.E, self.C, self.eng
+        torch = eng.torch
+        G = 1 if grp is None else 2
+        R = len(roffs) - 1
+        n = int(roffs[-1])
+        out = torch.empty(max(n, 1), dtype=torch.float64, device=eng.dev)
+        offs = torch.empty(max(S, 1) * G + 1, dtype=torch.int64, device=eng.dev)
+        ro = torch.from_numpy(np.ascontiguousarray(roffs, np.int64)).to(eng.dev)
+        gd = torch.from_numpy(np.ascontiguousarray(grp, np.uint8)).to(eng.dev) if G == 2 and R else None
+        vals = vals.contiguous()
+        P = lambda t: C.c_void_p(t.data_ptr()) if t is not None and t.numel() else None  # noqa: E731
+        E._check(eng.lib, eng.lib.fz_transpose_runs(eng.ctx, P(vals), P(ro), P(gd), R, G, S, n, P(out), P(offs)))
+        return out[:n], offs[:S * G + 1]
+
+    def sort(self, x):
+        return self.eng.sort_f64(x.contiguous())
+
+    def dist_state(self):
+        torch = self.eng.torch
+        return (torch.zeros(self.E.FZ_DIST_PARAMS, dtype=torch.float64, device=self.eng.dev),
+                torch.full((4,), float("nan"), dtype=torch.float64, device=self.eng.dev))
+
+    def dist_partials(self, ps, v, g, m, g0, n, params, x0):
+        E, C, eng = self.E, self.C, self.eng
+        torch = eng.torch
+        part = torch.empty(E.DIST_PART_WIDTH[ps], dtype=torch.float64, device=eng.dev)
+        P = lambda t: C.c_void_p(t.data_ptr()) if t is not None and t.numel() else None  # noqa: E731
+        E._check(eng.lib, eng.lib.fz_series_dist_partials(eng.ctx, ps, P(v.contiguous()), P(g.contiguous()), m, g0, n,
+                                                          P(params), P(x0), P(part)))
+        return part
+
+    def dist_combine(self, ps, parts, k, n, params, result, sizes=None):
+        E, C, eng = self.E, self.C, self.eng
+        E._check(eng.lib, eng.lib.fz_series_dist_combine(eng.ctx, ps, C.c_void_p(parts.contiguous().data_ptr()), k, n,
+                                                         C.c_void_p(params.data_ptr()),
+                                                         C.c_void_p(result.data_ptr())))
+
+
+class GpuRQ2CountShard(_GpuExchange):
+    """RQ2 count of one rank on its engine (fz_rq2_count_ex project-major, fz_piece_values for a
+    leading piece of a cut project, the exchange primitives, fz_rq2_session_stats_grouped,
+    fz_rq2_count_tail)."""
+
+    def __init__(self, eng, cont: int = -1):
         import ctypes as C
         from . import engine as E
         from .rq import compute
-        self.E, self.C, self.eng = E, C, eng
+        self.E, self.C, self.eng, self.cont = E, C, eng, int(cont)
         self.bufs = compute.rq2_count_buffers(eng)
 
     pre = False  # launch() already enqueued this step's local kernels (a recorded local phase)
 
     def launch(self):
         E, C, eng, b = self.E, self.C, self.eng, self.bufs
-        E._check(eng.lib, eng.lib.fz_rq2_count_ex(eng.ctx, E.FZ_RQ2C_SKIP_SESSION_STATS, C.byref(b.out)))
+        E._check(eng.lib, eng.lib.fz_rq2_count_ex(eng.ctx, E.FZ_RQ2C_SKIP_SESSION_STATS | E.FZ_RQ2C_PROJECT_MAJOR,
+                                                  C.byref(b.out)))
+        if self.cont >= 0:
+            self._piece(E.FZ_PIECE_RQ2)
 
     def run(self):
         E, b = self.E, self.bufs
         if not self.pre:
             self.launch()
         self.pre = False
-        ns = int(b.counts[E.RQ2C_SESSIONS].item())
         out = {k: getattr(b, k) for k in RQ2C_PROJECT_COLS}
         out["null_lines"] = b.counts[E.RQ2C_NULL_LINES:E.RQ2C_NULL_LINES + 1]
-        out["session_offsets"] = b.session_offsets[:ns + 1]
-        out["session_values"] = b.session_values
+        out["values"] = b.session_values
+        if self.cont >= 0:
+            out["piece_values"], out["piece_counts"] = self._pv, self._pc
         return out
 
     def session_stats_grouped(self, vals, offs, S, max_len):
@@ -1213,23 +1720,25 @@ class GpuRQ2AddShard:
         return out
 
 
-class GpuRQ4bShard:
-    """RQ4b of one rank on its engine (fz_rq4b_ex, fz_rq4b_session_stats, fz_series_tests,
-    fz_two_sample_tests)."""
+class GpuRQ4bShard(_GpuExchange):
+    """RQ4b of one rank on its engine (fz_rq4b_ex project-major, fz_piece_values for a leading piece
+    of a cut project, the exchange primitives, fz_rq4b_session_stats_grouped, fz_rq4b_tail)."""
 
-    def __init__(self, eng):
+    def __init__(self, eng, cont: int = -1):
         import ctypes as C
         from . import engine as E
         from .rq import compute
-        self.E, self.C, self.eng = E, C, eng
+        self.E, self.C, self.eng, self.cont = E, C, eng, int(cont)
         self.bufs = compute.rq4b_buffers(eng, shard=True)
 
     pre = False  # launch() already enqueued this step's local kernels (a recorded local phase)
 
     def launch(self):
         E, C, eng, b = self.E, self.C, self.eng, self.bufs
-        E._check(eng.lib, eng.lib.fz_rq4b_ex(eng.ctx, C.byref(eng.groups), E.FZ_RQ4B_SKIP_SESSION_STATS,
-                                             C.byref(b.out)))
+        E._check(eng.lib, eng.lib.fz_rq4b_ex(eng.ctx, C.byref(eng.groups),
+                                             E.FZ_RQ4B_SKIP_SESSION_STATS | E.FZ_RQ4B_PROJECT_MAJOR, C.byref(b.out)))
+        if self.cont >= 0:
+            self._piece(E.FZ_PIECE_RQ4B)
 
     def run(self):
         eng, b = self.eng, self.bufs
@@ -1237,11 +1746,12 @@ class GpuRQ4bShard:
             self.launch()
         self.pre = False
         P = eng.tables.fz.n_projects  # column lengths stay on the device (counts); rq4b_sharded slices
-        # (trend_offsets: 2 * max_cov_per_project + 1 entries, written up to 2 * the shard's session
-        # count - counts[RQ4B_VALUES] is the number of values)
-        return {"counts": b.counts, "member": b.member[:P], "trend_values": b.trend_values,
-                "trend_offsets": b.trend_offsets, "pre_cov": b.pre_cov, "post_cov": b.post_cov,
-                "delta_order": b.delta_order, "init_g2": b.init_g2, "init_g1": b.init_g1}
+        out = {"counts": b.counts, "member": b.member[:P], "trend_values": b.trend_values,
+               "trend_offsets": b.trend_offsets, "pre_cov": b.pre_cov, "post_cov": b.post_cov,
+               "delta_order": b.delta_order, "init_g2": b.init_g2, "init_g1": b.init_g1}
+        if self.cont >= 0:
+            out["piece_values"], out["piece_counts"] = self._pv, self._pc
+        return out
 
     def session_stats_grouped(self, vals, offs2, S, max_len):
         return gpu_rq4b_session_stats_grouped(self.eng, vals, offs2, S, max_len)

@@ -334,7 +334,7 @@ def rq4b_buffers(eng: E.Engine, shard: bool = False) -> OutBuffers:
         ("g2_q", 3 * M, f64), ("g1_q", 3 * M, f64), ("p_bm", M, f64), ("spearman6", 12, f64),
         ("pre_cov", 7 * PP, f64), ("post_cov", 7 * PP, f64), ("pre_median", 7, f64), ("post_median", 7, f64),
         ("init_g2", P, f64), ("init_g1", P, f64), ("tests", E.FZ_RQ4B_NTESTS, f64),
-        ("trend_values", fz.n_cov if shard else 0, f64), ("trend_offsets", 2 * M + 1 if shard else 0, i64),
+        ("trend_values", fz.n_cov if shard else 0, f64), ("trend_offsets", max(2 * M, P) + 1 if shard else 0, i64),
         ("delta_order", P if shard else 0, i64)], null=() if shard else ("trend_values", "trend_offsets",
                                                                          "delta_order"))
 
