@@ -278,10 +278,12 @@ def main():
             "rq1": sh_rq1,
             "rq2_count": lambda e: pending.append(par.rq2_count_sharded(rq2c_shard, rank, world, *own,
                                                                         gather_values=False, finish_later=True,
-                                                                        cont=cont, cont_base=cont_base[0])),
+                                                                        cont=cont, cont_base=cont_base[0],
+                                                                        host_sessions=False)),
             "rq4a": lambda e: pending.append(par.rq4a_sharded(rq4a_shard, rank, world, *own, finish_later=True)),
             "rq4b": lambda e: pending.append(par.rq4b_sharded(rq4b_shard, rank, world, *own, finish_later=True,
-                                                              cont=cont, cont_base=cont_base[1])),
+                                                              cont=cont, cont_base=cont_base[1],
+                                                              host_sessions=False)),
             "rq2_add": sh_rq2_add,
             "rq3": lambda e: par.rq3_sharded(rq3_shard, rank, world),
         }

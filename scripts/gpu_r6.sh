@@ -32,6 +32,16 @@ for s in ${STEPS:-full bench}; do
         python3 scripts/kstats.py $(find $O/${T}_prof_$c -name '*kernel_stats.csv' | head -1) auto 40 > $O/${T}_kstats_$c.txt
         head -25 $O/${T}_kstats_$c.txt
       done ;;
+    ab)  # same-box A/B: ABSETS = bench argument sets separated by ';' (e.g. " ;--lanes 2"), ROUNDS rounds
+      IFS=';' read -ra SETS <<< "${ABSETS:- }"
+      for r in $(seq 1 ${ROUNDS:-2}); do
+        for i in "${!SETS[@]}"; do
+          a="${SETS[$i]}"
+          timeout -k 10 300 python -u bench.py --config ${ABCONF:-c2} --steps ${ABSTEPS:-50} --warmup 3 --no-cpu-baseline \
+            --probe-steps 0 $a > $O/${T}_ab_${i}_$r.log 2>&1 || { tail -5 $O/${T}_ab_${i}_$r.log; exit 1; }
+          echo "ab[$i] '$a' r$r $(grep -o '"ms_per_step": [0-9.]*' $O/${T}_ab_${i}_$r.log)" | tee -a $O/${T}_ab.txt
+        done
+      done ;;
     strong)
       C=${CONFIG:-c3L}
       for n in ${NS:-1 8}; do

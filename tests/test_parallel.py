@@ -724,7 +724,7 @@ def test_shard_bounds_cover_and_balance():
             assert sizes.max() <= 2.5 * t.n_rows / world
 
 
-@pytest.mark.parametrize("world,case", [(2, "collide"), (3, "collide"), (3, "last_shard_no_issues"), (8, "collide"),
+@pytest.mark.parametrize("world,case", [(1, "collide"), (2, "collide"), (3, "collide"), (3, "last_shard_no_issues"), (8, "collide"),
                                         (8, "last_shard_no_issues"), (2, "giant"), (3, "giant"), (8, "giant"),
                                         (2, "live_giant"), (3, "live_giant"), (8, "live_giant")])
 def test_sharded_rq1_rq3_match_whole_table(world, case, tmp_path):

@@ -2008,10 +2008,12 @@ __device__ inline void qs_write(const QsArgs &a, int64_t s, int64_t n, double su
 }
 
 // Size classes of the selection: lists of the segments too long for one lane (filled by
-// k_qs_micro), one list per class - tiny (one wave each), mid and big (one workgroup each).
+// k_qs_micro), one list per class - tiny (33-64 values: one wave each; 9-16 / 17-32 values: a
+// quarter / half of a wave each), mid and big (one workgroup each).
+enum { kQsTiny = 0, kQsMid = 1, kQsBig = 2, kQsBlock = 3, kQsTiny16 = 4, kQsTiny32 = 5, kQsLists = 6 };
 struct QsLists {
-    int32_t *ids[4];
-    int64_t *d_n;  // [4] (zero on entry)
+    int32_t *ids[kQsLists];
+    int64_t *d_n;  // [kQsLists] (zero on entry)
 };
 
 // append segment s to list cls of L when `want` (wave-aggregated: one atomic per wave and class)
@@ -2038,7 +2040,9 @@ __global__ __launch_bounds__(kBlock) void k_qs_micro(const double *__restrict__ 
         const int64_t s = v * 64 + lane;
         const int64_t b = s < S ? offs[s] : 0;
         const int64_t n = s < S ? offs[s + 1] - b : -1;
-        qs_append(L, 0, n > kMicroSeg && n <= kTinySeg, s);
+        qs_append(L, kQsTiny16, n > kMicroSeg && n <= 16, s);
+        qs_append(L, kQsTiny32, n > 16 && n <= 32, s);
+        qs_append(L, kQsTiny, n > 32 && n <= kTinySeg, s);
         qs_append(L, 1, n > kTinySeg && n <= 1024, s);
         qs_append(L, 2, n > 2048, s);
         qs_append(L, 3, n > 1024 && n <= 2048, s);
@@ -2069,27 +2073,40 @@ __global__ __launch_bounds__(kBlock) void k_qs_micro(const double *__restrict__ 
     }
 }
 
-// The tiny list: one wave per segment (64-lane bitonic network on the keys, order statistics
-// gathered by shuffles).
+// The tiny lists: GW lanes per segment, 64 / GW segments per wave (GW-lane bitonic network on the
+// keys, order statistics gathered by shuffles).  Sessions of 9-16 values - most of the tall
+// session layouts' tail (config 5L: ~1.3 M sessions of 9-64 values) - take a quarter of a wave
+// each: a quarter of the waves and 10 network stages instead of 21.
+template <int GW>
 __global__ __launch_bounds__(kBlock) void k_qs_tiny(const double *__restrict__ src, const int64_t *__restrict__ offs,
                                                     const int32_t *__restrict__ list, const int64_t *__restrict__ d_ln,
                                                     QsArgs a) {
+    static_assert(GW == 16 || GW == 32 || GW == 64, "group width");
+    constexpr int PER = kWave / GW;
     const int lane = lane_id();
+    const int sub = lane & (GW - 1), grp = lane / GW;
     const int64_t ns = *d_ln;
     const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
-    for (int64_t w = int64_t(blockIdx.x) * (kBlock / kWave) + wave_id(); w < ns; w += nwaves) {
-        const int64_t st = list[w];
-        const int64_t sb = offs[st];
-        const int sn = int(offs[st + 1] - sb);
-        const double x = lane < sn ? src[sb + lane] : 0.0;
-        DD acc = wave_dd_sum(DD{lane < sn ? x : 0.0, 0.0});
-        unsigned long long key = lane < sn ? f64_key(x) : ~0ull;
+    for (int64_t w = int64_t(blockIdx.x) * (kBlock / kWave) + wave_id(); w * PER < ns; w += nwaves) {
+        const int64_t idx = w * PER + grp;
+        const bool have = idx < ns;
+        const int64_t st = have ? list[idx] : 0;
+        const int64_t sb = have ? offs[st] : 0;
+        const int sn = have ? int(offs[st + 1] - sb) : 0;
+        const double x = sub < sn ? src[sb + sub] : 0.0;
+        DD acc{sub < sn ? x : 0.0, 0.0};
 #pragma unroll
-        for (int kk = 2; kk <= 64; kk <<= 1) {
+        for (int off = GW / 2; off > 0; off >>= 1) {
+            DD y{__shfl_xor(acc.hi, off, 64), __shfl_xor(acc.lo, off, 64)};
+            acc = dd_add(acc, y);
+        }
+        unsigned long long key = sub < sn ? f64_key(x) : ~0ull;
+#pragma unroll
+        for (int kk = 2; kk <= GW; kk <<= 1) {
 #pragma unroll
             for (int j = kk >> 1; j > 0; j >>= 1) {
                 const unsigned long long ok = __shfl_xor(key, j, 64);
-                const bool want_min = ((lane & j) == 0) == ((lane & kk) == 0);
+                const bool want_min = ((sub & j) == 0) == ((sub & kk) == 0);
                 if (want_min == (ok < key)) key = ok;
             }
         }
@@ -2099,10 +2116,10 @@ __global__ __launch_bounds__(kBlock) void k_qs_tiny(const double *__restrict__ s
         double rv[kQsMaxT];
 #pragma unroll
         for (int t = 0; t < kQsMaxT; ++t) {
-            rk[t] = t < nt ? int(qs_rank(sn, a, t)) : -1;
-            rv[t] = f64_from_key(__shfl(key, rk[t] < 0 ? 0 : rk[t], 64));
+            rk[t] = t < nt && sn > 0 ? int(qs_rank(sn, a, t)) : -1;
+            rv[t] = f64_from_key(__shfl(key, grp * GW + (rk[t] < 0 ? 0 : rk[t]), 64));
         }
-        if (lane == 0) {
+        if (sub == 0 && have) {
             auto get = [&](int64_t j) {
                 double r = 0.0;
 #pragma unroll
@@ -2484,18 +2501,30 @@ void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_h
     ProbeScope ps(c, "seg_qstats", double(S) * (8.0 + 8.0 * (2 + nq)), sg.offs + S, 8.0);
     // class lists (capacities: a segment of the class holds more than the class below allows)
     auto cap = [&](int64_t minlen) { return S < sg.n_cap / (minlen + 1) + 1 ? S : sg.n_cap / (minlen + 1) + 1; };
-    const int64_t caps[4] = {cap(kMicroSeg), lb > kTinySeg ? cap(kTinySeg) : 0, lb > 2048 ? cap(2048) : 0,
-                             lb > 1024 ? cap(1024) : 0};
+    const int64_t caps[kQsLists] = {lb > 32 ? cap(32) : 0, lb > kTinySeg ? cap(kTinySeg) : 0,
+                                    lb > 2048 ? cap(2048) : 0, lb > 1024 ? cap(1024) : 0, cap(kMicroSeg),
+                                    lb > 16 ? cap(16) : 0};
     QsLists L;
-    L.d_n = c->arena.get<int64_t>(4);
-    for (int k = 0; k < 4; ++k) L.ids[k] = c->arena.get<int32_t>(caps[k]);
-    dev_fill(c, L.d_n, 0, 4 * 8);
+    L.d_n = c->arena.get<int64_t>(kQsLists);
+    for (int k = 0; k < kQsLists; ++k) L.ids[k] = c->arena.get<int32_t>(caps[k]);
+    dev_fill(c, L.d_n, 0, kQsLists * 8);
     const int64_t groups = (S + 63) / 64;
     k_qs_micro<<<grid_for(groups, kBlock / kWave, 8192), kBlock, 0, c->stream>>>(vals, sg.offs, S, a, L);
     FZ_LAUNCH_CHECK();
     auto grid = [](int64_t n, int64_t lim) { return unsigned(n < 1 ? 1 : (n < lim ? n : lim)); };
     if (lb > kMicroSeg) {
-        k_qs_tiny<<<grid((caps[0] + 3) / 4, 8192), kBlock, 0, c->stream>>>(vals, sg.offs, L.ids[0], L.d_n, a);
+        k_qs_tiny<16><<<grid((caps[kQsTiny16] + 15) / 16, 8192), kBlock, 0, c->stream>>>(
+            vals, sg.offs, L.ids[kQsTiny16], L.d_n + kQsTiny16, a);
+        FZ_LAUNCH_CHECK();
+    }
+    if (lb > 16) {
+        k_qs_tiny<32><<<grid((caps[kQsTiny32] + 7) / 8, 8192), kBlock, 0, c->stream>>>(
+            vals, sg.offs, L.ids[kQsTiny32], L.d_n + kQsTiny32, a);
+        FZ_LAUNCH_CHECK();
+    }
+    if (lb > 32) {
+        k_qs_tiny<64><<<grid((caps[kQsTiny] + 3) / 4, 8192), kBlock, 0, c->stream>>>(vals, sg.offs, L.ids[kQsTiny],
+                                                                                      L.d_n + kQsTiny, a);
         FZ_LAUNCH_CHECK();
     }
     if (lb > kTinySeg) {

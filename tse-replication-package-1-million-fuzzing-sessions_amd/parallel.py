@@ -899,7 +899,9 @@ def _exchange_runs(shard, runs: _Runs, rank, own, a_vals, b_vals, group_of=None)
     if world > 1:
         packed = shard.pack(a_vals, b_vals, mine, sl, own, int(send.sum()))
         got = all_to_all_v(packed, send.tolist(), recv.tolist())
-    else:  # (one rank: every session is its own; its runs in order are already the owner's runs)
+    elif all(x[0] == 0 for x in mine):  # (one rank, no leading piece: the project-major values ARE its runs)
+        got = a_vals[:int(send.sum())]
+    else:  # (one rank with a leading piece: that piece's run first, then its own projects')
         got = shard.pack(a_vals, b_vals, mine, sl, own, int(send.sum()))
     # the owner's runs: every project longer than its first session, in project order (a cut
     # project's pieces arrive one after another, in date order: one run)
@@ -990,7 +992,7 @@ def _series_tests_cut(shard, p, holders, piece, base, n, rank, dev):
 
 
 def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_values: bool = True,
-                      finish_later: bool = False, cont: int = -1, cont_base=None):
+                      finish_later: bool = False, cont: int = -1, cont_base=None, host_sessions: bool = True):
     """Exact RQ2 count over project shards (rq2_coverage_count.py:244-483).
     ``shard.run()`` -> per-project columns over the global project axis (RQ2C_PROJECT_COLS), the
     local trend values project-major ("values": the eligible projects' values in (project, date)
@@ -1000,12 +1002,16 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     sessions (one all-to-all), the owner's transpose + session statistics
     (``shard.session_stats_grouped``), per-session results gathered; a cut project's tests from its
     pieces (_series_tests_cut).  cont_base: (one-GPU rehearsal, world 1) the leading piece's session
-    base.  Returns a dict of host numpy arrays (every rank)."""
+    base.  host_sessions=False leaves the per-session rows on the device ("sessions": [S, 7] average,
+    median, 5 percentiles - config 5L's 20.8 M sessions are 1.2 GB) as the single-table step leaves its
+    results in HBM.  Returns a dict of host numpy arrays (every rank)."""
     import torch
     part = shard.run()
     vals_a = part["values"]
     dev = vals_a.device
-    pc = [part[k][lo:hi] for k in RQ2C_PROJECT_COLS]
+    # (every rank's own range gathered into the global axis; one rank - a one-GPU rehearsal of one
+    # shard too - keeps its columns over the global axis: the other ranks' projects are absent, zero)
+    pc = [part[k][lo:hi] if world > 1 else part[k] for k in RQ2C_PROJECT_COLS]
     pc = [v.to(torch.float64) if v.is_floating_point() else v.to(torch.int64) for v in pc]
     nl = part.get("null_lines")
     nl = nl.to(torch.int64).reshape(-1)[:1] if nl is not None else torch.zeros(1, dtype=torch.int64, device=dev)
@@ -1078,7 +1084,7 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
         corr = proj["corr"][elig][proj["raw_n"][elig] > 0]
         valid = corr[~np.isnan(corr)]
         corr_mm = shard.mean_median(torch.from_numpy(valid.copy()).to(dev))
-    tensors = [block, tests, corr_mm]
+    tensors = [block if host_sessions else block[:0], tests, corr_mm]
     if gather_values:  # coverage_by_session_index.csv: every value, session-major, project order
         tensors.append(torch.cat(all_gather_v(vals)) if world > 1 else vals)
     n_glob = runs.n
@@ -1088,6 +1094,8 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
         out = {"proj": proj, "K": K, "average": blk[:, 0].copy(), "median": blk[:, 1].copy(),
                "percentiles": blk[:, 2:].reshape(-1).copy(), "tests": tuple(float(v) for v in h[1]),
                "corr_mm": tuple(float(v) for v in h[2]), "null_lines": null_lines}
+        if not host_sessions:
+            out["sessions"] = block
         if gather_values:
             out["session_values"] = h[3]
             sizes = np.zeros(M + 1, np.int64)  # session i holds one value of every run longer than i
@@ -1148,7 +1156,7 @@ RQ4B_VALUES = 9
 
 
 def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, finish_later: bool = False,
-                 cont: int = -1, cont_base=None):
+                 cont: int = -1, cont_base=None, host_sessions: bool = True):
     """Exact RQ4b over project shards (rq4b_coverage.py:1209-1261).  ``shard.run()`` -> counts,
     member[P], the G1/G2 full coverage values project-major (trend_values, trend_offsets [P + 1]),
     the delta columns (pre_cov / post_cov step-major, delta_order = CSV row of each column; at least
@@ -1159,7 +1167,8 @@ def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, f
     whole axis when world == 1), each rank's runs sent to their sessions' owners and transposed there
     by (session, group) (_exchange_runs), per-session results, delta columns (re-ordered by CSV row,
     :216, :744) and initial samples gathered.  Intermediates stay on the device; the results are
-    copied to the host once.  Returns a dict for rq/compute.rq4b_result (host arrays, every rank)."""
+    copied to the host once (host_sessions=False: the per-session columns stay on the device,
+    "sessions").  Returns a dict for rq/compute.rq4b_result (host arrays, every rank)."""
     import torch
     part = shard.run()
     counts = part["counts"].clone()
@@ -1170,8 +1179,10 @@ def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, f
             raise ValueError("rq4b_sharded: the rank's own project range (lo, hi) is needed at world > 1")
         lo, hi = 0, P
     toffs = part["trend_offsets"][:P + 1]
-    nloc = (toffs[1:] - toffs[:-1])[lo:hi].to(torch.int64)
-    member = part["member"][lo:hi].to(torch.int64)
+    # (own ranges gathered into the global axis; one rank keeps its columns over the global axis)
+    nloc = (toffs[1:] - toffs[:-1])[lo:hi] if world > 1 else toffs[1:] - toffs[:-1]
+    nloc = nloc.to(torch.int64)
+    member = (part["member"][lo:hi] if world > 1 else part["member"]).to(torch.int64)
     vals_a = part["trend_values"]
     vals_b = part.get("piece_values")
     pcnt = part.get("piece_counts")
@@ -1256,19 +1267,22 @@ def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, f
 
     def finish(h):  # (the one result copy)
         counts_h, last, sp_h, pre_h, post_h, med_h, x_h, y_h, tests_h = h[:9]
-        cols_h = h[9:]
+        cols_h = h[9:] if host_sessions else [np.zeros(0)] * 9
         last = int(last)
         sp6 = np.asarray(sp_h, dtype=np.float64).reshape(-1) if last >= 0 else np.full(12, np.nan)
         counts_h[RQ4B_SESSIONS] = M
         counts_h[RQ4B_LAST] = last
         counts_h[RQ4B_DELTA_PROJECTS] = pre_h.shape[1]
         med_h = np.asarray(med_h, dtype=np.float64)
-        return {"counts": counts_h, "c2": cols_h[0], "c1": cols_h[1], "g2_q": np.stack(cols_h[2:5], 1).reshape(-1),
-                "g1_q": np.stack(cols_h[5:8], 1).reshape(-1), "p_bm": cols_h[8], "sp6": sp6,
-                "pre_cov": [pre_h[i].copy() for i in range(7)], "post_cov": [post_h[i].copy() for i in range(7)],
-                "pre_median": [float(v) for v in med_h[:7]], "post_median": [float(v) for v in med_h[7:]],
-                "init_g2": x_h, "init_g1": y_h, "tests": np.asarray(tests_h, dtype=np.float64)}
-    d = Deferred([counts, last_d, sp, pre, post, med, x, y, tests, *cols], finish)
+        out = {"counts": counts_h, "c2": cols_h[0], "c1": cols_h[1], "g2_q": np.stack(cols_h[2:5], 1).reshape(-1),
+               "g1_q": np.stack(cols_h[5:8], 1).reshape(-1), "p_bm": cols_h[8], "sp6": sp6,
+               "pre_cov": [pre_h[i].copy() for i in range(7)], "post_cov": [post_h[i].copy() for i in range(7)],
+               "pre_median": [float(v) for v in med_h[:7]], "post_median": [float(v) for v in med_h[7:]],
+               "init_g2": x_h, "init_g1": y_h, "tests": np.asarray(tests_h, dtype=np.float64)}
+        if not host_sessions:
+            out["sessions"] = cols
+        return out
+    d = Deferred([counts, last_d, sp, pre, post, med, x, y, tests] + (list(cols) if host_sessions else []), finish)
     return d if finish_later else d.result()
 
 
