@@ -138,7 +138,7 @@ def main():
     dev = torch.device("cuda", local)
 
     rehearsal = args.strong and world == 1 and args.shard_of > 1
-    cont, cut, cont_base = -1, [], (None, None)
+    cont, cut = -1, []
     if args.strong:
         from tse_amd import parallel as par
         full = synth.generate(synth.config(args.config))
@@ -149,8 +149,6 @@ def main():
         lo, hi = plan.bounds[r]
         t = par.take_split(full, plan, r)[0]
         cont, cut = plan.cont[r], list(plan.cut)
-        if rehearsal:  # (no other rank to exchange with: the session bases another rank would send)
-            cont_base = par.cut_trend_bases(full, plan, r)
         job_rows = full.n_rows if not rehearsal else None
         del full, plan
     else:
@@ -278,12 +276,10 @@ def main():
             "rq1": sh_rq1,
             "rq2_count": lambda e: pending.append(par.rq2_count_sharded(rq2c_shard, rank, world, *own,
                                                                         gather_values=False, finish_later=True,
-                                                                        cont=cont, cont_base=cont_base[0],
-                                                                        host_sessions=False)),
+                                                                        cont=cont, host_sessions=False)),
             "rq4a": lambda e: pending.append(par.rq4a_sharded(rq4a_shard, rank, world, *own, finish_later=True)),
             "rq4b": lambda e: pending.append(par.rq4b_sharded(rq4b_shard, rank, world, *own, finish_later=True,
-                                                              cont=cont, cont_base=cont_base[1],
-                                                              host_sessions=False)),
+                                                              cont=cont, host_sessions=False)),
             "rq2_add": sh_rq2_add,
             "rq3": lambda e: par.rq3_sharded(rq3_shard, rank, world),
         }
@@ -596,6 +592,8 @@ def main():
                        "upload_h2d_ms": up["h2d_ms"], "upload_h2d_gbs": up["h2d_gbs"],
                        "rows_per_s_incl_upload": round(t.n_rows / ((upload_ms + ms_step) * 1e-3), 1)},
             "roofline": roof, "cpu_baseline": cpu,
+            # (committed rehearsals, not this run: the strong-scaling figures beside this line's mode)
+            "strong_rehearsal": strong_rehearsals(),
         }
         print(json.dumps(out), flush=True)
     if pool is not None:
@@ -616,6 +614,23 @@ def main():
     if sharded:
         dist.destroy_process_group()
     return out
+
+
+def strong_rehearsals():
+    """The newest committed one-GPU strong-scaling rehearsals (profiles/r*_<config>_strong.json,
+    scripts/strong_summary.py: per N the slowest of the N shards' sharded steps = an N-GPU run's
+    per-rank compute before any exchange), beside this line's own scaling mode."""
+    import glob
+    out = {}
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_strong.json"))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("config"):
+            out[d["config"]] = {"T_ms": d.get("T_ms"), "efficiency": d.get("efficiency"),
+                                "source": os.path.relpath(path, REPO)}
+    return out or None
 
 
 def pmc_traffic(probe, config):

@@ -703,6 +703,54 @@ def _check(rank, world, case, threaded=False, deferred=False):
     assert_same(ours4b, orc.rq4b(t), "rq4b")
 
 
+def _rehearse(rank, world, port, case, errfile, threaded=False, deferred=False):
+    """bench.py --strong --shard-of W at world 1: every shard of a W-rank live_plan run alone (its
+    leading piece, without the earlier pieces, starts at session 0).  The runs the owner transposes
+    must be exactly what the pack sends - the shard holding only the giant's later piece once read
+    past its packed values on the GPU; the piece's values are a contiguous date range of the
+    project's trend values."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        t = make_table("live_giant", 1)
+        plan = par.live_plan(t, world)
+        p_cut = int(plan.cut[0])
+        full = _trend_values(t, p_cut)[0]
+        seen = 0
+        for r in range(world):
+            lo, hi = plan.bounds[r]
+            ts, rows = par.take_split(t, plan, r)
+            cont = plan.cont[r]
+            ov = {}
+            par.fix_cut_eligibility(OracleEligibility(ts, ov), plan.cut, lo, hi, 1)
+            r2 = par.rq2_count_sharded(OracleRQ2CountShard(ts, cont, ov), 0, 1, lo, hi, cont=cont)
+            par.rq4b_sharded(OracleRQ4bShard(ts, cont, ov), 0, 1, lo=lo, hi=hi, cont=cont)
+            if cont == p_cut:
+                seen += 1
+                piece = _trend_values(ts, p_cut)[0]
+                assert len(piece) and int(r2["proj"]["n_trend"][p_cut]) == len(piece)
+                b0 = sum(len(_trend_values(par.take_split(t, plan, q)[0], p_cut)[0]) for q in plan.ranks[p_cut] if q < r)
+                assert b0 > 0 and np.array_equal(full[b0:b0 + len(piece)], piece, equal_nan=True)
+        assert seen >= 1, "no rank held a continuation piece"
+    except BaseException:
+        with open(f"{errfile}.{rank}", "w") as f:
+            import traceback
+            f.write(traceback.format_exc())
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_one_gpu_rehearsal_shards_of_live_giant(tmp_path):
+    errfile = str(tmp_path / "err")
+    try:
+        mp.spawn(_rehearse, args=(3, _free_port(), "live_giant", errfile), nprocs=1, join=True)
+    except Exception:
+        msgs = [open(f"{errfile}.0").read()] if os.path.exists(f"{errfile}.0") else []
+        raise AssertionError("\n".join(msgs) or "worker failed")
+
+
 def _spawn(world, case, tmp_path, threaded=False, deferred=False):
     errfile = str(tmp_path / "err")
     try:

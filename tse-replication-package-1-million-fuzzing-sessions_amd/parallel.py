@@ -391,23 +391,6 @@ def live_plan(t: Tables, world: int) -> LivePlan:
     return LivePlan(bounds, B, Cv, I, PI, cont, cut, ranks, moved)
 
 
-def cut_trend_bases(t: Tables, plan: LivePlan, rank: int):
-    """(one-GPU rehearsals, no exchange) the session base of rank `rank`'s leading piece: the RQ2
-    trend values (queries1.py:120-129 rows, total != 0, rq2_coverage_count.py:300-303) and the rq4b
-    series values (rq4b:315-326 rows) of the same project's pieces on earlier ranks - what the
-    drivers exchange on a real run.  -> (rq2 base, rq4b base), (0, 0) without a leading piece."""
-    p = plan.cont[rank]
-    if p < 0:
-        return 0, 0
-    rows = np.concatenate([plan.coverage[r] for r in plan.ranks[p] if r < rank])
-    rows = rows[t.c_project[rows].astype(np.int64) == p]
-    before = t.c_date[rows] < LIMIT_US
-    fetched = t.c_coverage_valid[rows] & (t.c_coverage[rows] != 0) & before
-    trend = fetched & ((t.c_total[rows] != 0) | ~t.c_total_valid[rows])
-    series = t.c_coverage_valid[rows] & (t.c_coverage[rows] > 0) & before
-    return int(trend.sum()), int(series.sum())
-
-
 # ---------------------------------------------------------------------------------- collectives
 import threading  # noqa: E402
 
@@ -856,7 +839,9 @@ class _Runs:
         for r in range(self.world):
             p = int(self.cont[r])
             if p >= 0:
-                self.cont_base[r] = self.n[p]  # (the earlier pieces' values, owner's first)
+                # (the earlier pieces' values, owner's first; a one-GPU rehearsal of one shard has
+                # no earlier piece: its leading piece starts at session 0, its runs are what it packs)
+                self.cont_base[r] = self.n[p]
                 self.n[p] += int(self.cont_n[r])
 
     def runs_of(self, r):
@@ -909,6 +894,11 @@ def _exchange_runs(shard, runs: _Runs, rank, own, a_vals, b_vals, group_of=None)
     live = np.nonzero(n > a)[0]
     lens = np.minimum(n[live], b) - a
     roffs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    # (every rank derives the same runs from the same gathered counts: what arrives is exactly what
+    # the owner's runs hold - checked before any kernel reads it)
+    if int(recv.sum()) != int(roffs[-1]) or int(got.numel()) < int(roffs[-1]):
+        raise RuntimeError(f"session exchange: {int(got.numel())} values received for runs of {int(roffs[-1])} "
+                           f"(sessions [{a}, {b}))")
     grp = None if group_of is None else np.asarray(group_of)[live].astype(np.uint8)
     return shard.transpose(got, roffs, grp, b - a)
 
@@ -992,7 +982,7 @@ def _series_tests_cut(shard, p, holders, piece, base, n, rank, dev):
 
 
 def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_values: bool = True,
-                      finish_later: bool = False, cont: int = -1, cont_base=None, host_sessions: bool = True):
+                      finish_later: bool = False, cont: int = -1, host_sessions: bool = True):
     """Exact RQ2 count over project shards (rq2_coverage_count.py:244-483).
     ``shard.run()`` -> per-project columns over the global project axis (RQ2C_PROJECT_COLS), the
     local trend values project-major ("values": the eligible projects' values in (project, date)
@@ -1001,8 +991,7 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     per-project columns and the pieces' counts gathered, each rank's runs sent to the owners of their
     sessions (one all-to-all), the owner's transpose + session statistics
     (``shard.session_stats_grouped``), per-session results gathered; a cut project's tests from its
-    pieces (_series_tests_cut).  cont_base: (one-GPU rehearsal, world 1) the leading piece's session
-    base.  host_sessions=False leaves the per-session rows on the device ("sessions": [S, 7] average,
+    pieces (_series_tests_cut).  host_sessions=False leaves the per-session rows on the device ("sessions": [S, 7] average,
     median, 5 percentiles - config 5L's 20.8 M sessions are 1.2 GB) as the single-table step leaves its
     results in HBM.  Returns a dict of host numpy arrays (every rank)."""
     import torch
@@ -1035,8 +1024,6 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     if null_lines:  # float(None) (rq2_coverage_count.py:300-303): every rank holds the sum, all raise here
         raise TypeError("float() argument must be a string or a real number, not 'NoneType'")
     runs = _Runs(world, bounds, proj["n_trend"].astype(np.int64), conts.astype(np.int64), cont_n.astype(np.int64))
-    if world == 1 and cont >= 0 and cont_base is not None:  # (rehearsal: the base another rank would send)
-        runs.cont_base[0] = int(cont_base)
     # a cut project's columns: counts summed over its pieces, tests from all of its values
     cut = sorted({int(p) for p in conts.tolist() if p >= 0})
     for p in cut:
@@ -1156,7 +1143,7 @@ RQ4B_VALUES = 9
 
 
 def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, finish_later: bool = False,
-                 cont: int = -1, cont_base=None, host_sessions: bool = True):
+                 cont: int = -1, host_sessions: bool = True):
     """Exact RQ4b over project shards (rq4b_coverage.py:1209-1261).  ``shard.run()`` -> counts,
     member[P], the G1/G2 full coverage values project-major (trend_values, trend_offsets [P + 1]),
     the delta columns (pre_cov / post_cov step-major, delta_order = CSV row of each column; at least
@@ -1203,8 +1190,6 @@ def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, f
     # (a leading piece of a project outside G1 / G2 contributes no series)
     cont_n = np.where((conts >= 0) & ((member_h[np.maximum(conts, 0)] & 3) != 0), cont_n, 0)
     runs = _Runs(world, bounds, nloc_h.astype(np.int64), conts, cont_n)
-    if world == 1 and cont >= 0 and cont_base is not None:  # (rehearsal: the base another rank would send)
-        runs.cont_base[0] = int(cont_base)
     M = int(runs.n.max()) if len(runs.n) else 0
     own = _owner_cuts(runs.n, world, M) if world > 1 else [(0, M)]
     group = np.where((member_h & 2) != 0, 0, 1)  # G2 -> segment 2s, G1 -> 2s + 1
@@ -1455,6 +1440,8 @@ class _GpuExchange:
         G = 1 if grp is None else 2
         R = len(roffs) - 1
         n = int(roffs[-1])
+        if vals.numel() < n or (G == 2 and len(grp) != R) or np.any(np.diff(roffs) > S):
+            raise ValueError("transpose: runs exceed the values or the session range")
         out = torch.empty(max(n, 1), dtype=torch.float64, device=eng.dev)
         offs = torch.empty(max(S, 1) * G + 1, dtype=torch.int64, device=eng.dev)
         ro = torch.from_numpy(np.ascontiguousarray(roffs, np.int64)).to(eng.dev)
