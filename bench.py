@@ -110,6 +110,7 @@ def parse():
     # no exchange (the collectives need the other ranks); value = that shard's rows / s
     ap.add_argument("--shard-of", type=int, default=1)
     ap.add_argument("--shard-rank", type=int, default=0)
+    ap.add_argument("--cprofile", default="", help="write a cProfile summary of the timed steps (host time) here")
     return ap.parse_args()
 
 
@@ -492,6 +493,11 @@ def main():
         eng.probe_begin(args.probe)
     if sharded:
         drv_ms.clear()
+    prof = None
+    if args.cprofile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     ev0.record(eng.stream)
     for _ in range(args.steps):
@@ -507,6 +513,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
+    if prof is not None:
+        prof.disable()
+        import io
+        import pstats
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(45)
+        pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(60)
+        with open(args.cprofile, "w") as f:
+            f.write(f"{args.steps} steps, wall {wall * 1e3:.2f} ms\n" + buf.getvalue())
     drv = {k: round(v / args.steps, 3) for k, v in drv_ms.items()} if sharded else None
     probe_window = args.steps
     if not on_children:

@@ -27,7 +27,7 @@ for s in ${STEPS:-full bench}; do
     prof)
       for c in ${PROF:-c5L}; do
         timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_prof_$c -o run -- python3 -u bench.py \
-          --config $c --steps 3 --warmup 1 --no-cpu-baseline --probe-steps 0 > $O/${T}_prof_$c.log 2>&1
+          --config $c --steps 3 --warmup 1 --no-cpu-baseline --probe-steps 0 $PROF_ARGS > $O/${T}_prof_$c.log 2>&1
         rc=$?; echo "prof $c rc $rc"; [ $rc -ne 0 ] && { tail -5 $O/${T}_prof_$c.log; exit $rc; }
         python3 scripts/kstats.py $(find $O/${T}_prof_$c -name '*kernel_stats.csv' | head -1) auto 40 > $O/${T}_kstats_$c.txt
         head -25 $O/${T}_kstats_$c.txt

@@ -146,6 +146,17 @@ def _check(rank, world, case):
     r4 = par.rq4a_sharded(_RQ4aView(par.GpuRQ4aShard(eng, M), eng.dev), rank, world, lo, hi)
     r4b = par.rq4b_sharded(par.GpuRQ4bShard(eng, cont), rank, world, lo=lo, hi=hi, cont=cont)
     r2a = par.rq2_add_sharded(_RQ2AddView(par.GpuRQ2AddShard(eng), eng.dev, rows), rank, world)
+    if case in ("c2_collide", "live_giant"):
+        # the bench's step (host_sessions=False): per-session rows left on their owners, only the
+        # prefixes the tails read gathered (config 2: K and the trends' prefix are non-empty)
+        from test_parallel import _check_owner_sessions
+        if case == "c2_collide":
+            assert r2["K"] > 0 and int(r4b["counts"][par.RQ4B_LAST]) >= 0
+        _check_owner_sessions(rank, world, case, r2, r4b, lambda: (
+            par.rq2_count_sharded(par.GpuRQ2CountShard(eng, cont), rank, world, lo, hi, cont=cont,
+                                  host_sessions=False),
+            par.rq4b_sharded(par.GpuRQ4bShard(eng, cont), rank, world, lo=lo, hi=hi, cont=cont,
+                             host_sessions=False)))
     any_rerun = torch.tensor([int(reran)])
     torch.distributed.all_reduce(any_rerun)
     if rank == 0:

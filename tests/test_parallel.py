@@ -662,6 +662,12 @@ def _check(rank, world, case, threaded=False, deferred=False):
     counts, it, idt, rows1, any_rerun = res["rq1"]
     total3, cols3, st3 = res["rq3"]
     r2, r4, r4b = res["rq2"], res["rq4a"], res["rq4b"]
+    if not threaded and not deferred and case in ("collide", "live_giant"):
+        _check_owner_sessions(rank, world, case, r2, r4b, lambda: (
+            par.rq2_count_sharded(OracleRQ2CountShard(ts, cont, ov), rank, world, lo, hi, cont=cont,
+                                  host_sessions=False),
+            par.rq4b_sharded(OracleRQ4bShard(ts, cont, ov), rank, world, lo=lo, hi=hi, cont=cont,
+                             host_sessions=False)))
     if rank != 0:
         return
     assert_same(rq2_add_result(*res["rq2a"]), orc.rq2_add(t), "rq2_add")
@@ -701,6 +707,29 @@ def _check(rank, world, case, threaded=False, deferred=False):
                                  r4b["sp6"], r4b["pre_cov"], r4b["post_cov"], r4b["pre_median"], r4b["post_median"],
                                  r4b["init_g2"], r4b["init_g1"], r4b["tests"])
     assert_same(ours4b, orc.rq4b(t), "rq4b")
+
+
+def _check_owner_sessions(rank, world, case, r2, r4b, again):
+    """host_sessions=False (the bench's step): the per-session rows stay on their owners and only the
+    prefixes the tails read are gathered - the same tests, and the owners' rows in session order are
+    the gathered ones."""
+    r2o, r4o = again()
+    assert r2o["K"] == r2["K"]
+    np.testing.assert_array_equal(np.array(r2o["tests"] + r2o["corr_mm"]), np.array(r2["tests"] + r2["corr_mm"]))
+    np.testing.assert_array_equal(r4o["sp6"], r4b["sp6"])
+    np.testing.assert_array_equal(r4o["counts"], r4b["counts"])
+    nt = 6  # (MWU p, Cliff, BM stat / p, Levene W / p; the last two of FZ_RQ4B_NTESTS slots are padding)
+    np.testing.assert_array_equal(r4o["tests"][:nt], r4b["tests"][:nt])
+    s2, s4 = r2o["sessions"], r4o["sessions"]
+    h = lambda x: x.cpu().numpy()  # noqa: E731
+    a, b = s2["range"]
+    np.testing.assert_array_equal(h(s2["median"]), r2["median"][a:b])
+    np.testing.assert_array_equal(h(s2["average"]), r2["average"][a:b])
+    np.testing.assert_array_equal(h(s2["percentiles"]), r2["percentiles"][5 * a:5 * b])
+    a, b = s4["range"]
+    np.testing.assert_array_equal(h(s4["cols"][0]), r4b["c2"][a:b])
+    np.testing.assert_array_equal(h(s4["cols"][1]), r4b["c1"][a:b])
+    np.testing.assert_array_equal(h(s4["cols"][8]), r4b["p_bm"][a:b])
 
 
 def _rehearse(rank, world, port, case, errfile, threaded=False, deferred=False):

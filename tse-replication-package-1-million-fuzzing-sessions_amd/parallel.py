@@ -845,25 +845,28 @@ class _Runs:
                 self.n[p] += int(self.cont_n[r])
 
     def runs_of(self, r):
-        """(src, src_off, len, base) of rank r's runs in project order: its leading piece (src 1:
-        fz_piece_values' buffer), then its own projects (src 0: the project-major values)."""
-        out = []
-        if self.cont[r] >= 0 and self.cont_n[r] > 0:
-            out.append((1, 0, int(self.cont_n[r]), int(self.cont_base[r])))
+        """[R, 4] int64 rows (src, src_off, len, base) of rank r's runs in project order: its leading
+        piece (src 1: fz_piece_values' buffer), then its own projects (src 0: the project-major
+        values)."""
         a, b = self.bounds[r]
-        nl = self.n_loc[a:b]
-        off = np.concatenate([[0], np.cumsum(nl)])
-        for k in np.nonzero(nl > 0)[0].tolist():
-            out.append((0, int(off[k]), int(nl[k]), 0))
+        nl = np.asarray(self.n_loc[a:b], np.int64)
+        off = np.cumsum(nl) - nl
+        k = np.nonzero(nl > 0)[0]
+        out = np.zeros((len(k), 4), np.int64)
+        out[:, 1], out[:, 2] = off[k], nl[k]
+        if self.cont[r] >= 0 and self.cont_n[r] > 0:
+            lead = np.array([[1, 0, int(self.cont_n[r]), int(self.cont_base[r])]], np.int64)
+            out = np.concatenate([lead, out])
         return out
 
     @staticmethod
     def slices(runs, own):
         """[dest, run] values of each run in each destination's session range."""
-        if not runs:
+        runs = np.asarray(runs, np.int64).reshape(-1, 4)
+        if not len(runs):
             return np.zeros((len(own), 0), np.int64)
-        base = np.array([x[3] for x in runs], np.int64)
-        end = base + np.array([x[2] for x in runs], np.int64)
+        base = runs[:, 3]
+        end = base + runs[:, 2]
         a = np.array([o[0] for o in own], np.int64)[:, None]
         b = np.array([o[1] for o in own], np.int64)[:, None]
         return np.maximum(0, np.minimum(end[None], b) - np.maximum(base[None], a))
@@ -880,11 +883,12 @@ def _exchange_runs(shard, runs: _Runs, rank, own, a_vals, b_vals, group_of=None)
     sl = _Runs.slices(mine, own)                      # [world, R]
     send = sl.sum(1)
     a, b = own[rank]
-    recv = np.array([_Runs.slices(runs.runs_of(s), [own[rank]])[0].sum() for s in range(world)], np.int64)
+    recv = np.array([_Runs.slices(mine if s == rank else runs.runs_of(s), [own[rank]])[0].sum()
+                     for s in range(world)], np.int64)
     if world > 1:
         packed = shard.pack(a_vals, b_vals, mine, sl, own, int(send.sum()))
         got = all_to_all_v(packed, send.tolist(), recv.tolist())
-    elif all(x[0] == 0 for x in mine):  # (one rank, no leading piece: the project-major values ARE its runs)
+    elif not np.any(mine[:, 0]):  # (one rank, no leading piece: the project-major values ARE its runs)
         got = a_vals[:int(send.sum())]
     else:  # (one rank with a leading piece: that piece's run first, then its own projects')
         got = shard.pack(a_vals, b_vals, mine, sl, own, int(send.sum()))
@@ -991,9 +995,11 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     per-project columns and the pieces' counts gathered, each rank's runs sent to the owners of their
     sessions (one all-to-all), the owner's transpose + session statistics
     (``shard.session_stats_grouped``), per-session results gathered; a cut project's tests from its
-    pieces (_series_tests_cut).  host_sessions=False leaves the per-session rows on the device ("sessions": [S, 7] average,
-    median, 5 percentiles - config 5L's 20.8 M sessions are 1.2 GB) as the single-table step leaves its
-    results in HBM.  Returns a dict of host numpy arrays (every rank)."""
+    pieces (_series_tests_cut).  host_sessions=False leaves the per-session rows on their owners'
+    devices ("sessions": the owner's session range and its average / median / percentile columns -
+    config 5L's 20.8 M sessions are 1.2 GB) as the single-table step leaves its results in HBM; only
+    the medians of sessions [0, K) the tail reads are gathered.  Returns a dict of host numpy arrays
+    (every rank)."""
     import torch
     part = shard.run()
     vals_a = part["values"]
@@ -1035,14 +1041,24 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     S = b - a
     vals, goffs = _exchange_runs(shard, runs, rank, own, vals_a, vals_b)
     st = shard.session_stats_grouped(vals, goffs, S, len(proj["eligible"]))
-    block = torch.cat([st["average"][:S, None], st["median"][:S, None], st["percentiles"][:5 * S].reshape(S, 5)], 1)
-    if world > 1:  # per-session rows (average, median, 5 percentiles) of every owner, session order
-        block = torch.cat([m.reshape(-1, 7).view(torch.float64) for m in all_gather_v(block.reshape(-1).view(
-            torch.int64))])
     # sessions with >= 100 values: a prefix, as long as the 100th longest run (:390)
     srt = np.sort(runs.n)[::-1]
     K = int(srt[99]) if len(srt) >= 100 else 0
     K = min(K, M)
+    med_k = None
+    if host_sessions:
+        block = torch.cat([st["average"][:S, None], st["median"][:S, None], st["percentiles"][:5 * S].reshape(S, 5)],
+                          1)
+        if world > 1:  # per-session rows (average, median, 5 percentiles) of every owner, session order
+            block = torch.cat([m.reshape(-1, 7).view(torch.float64) for m in all_gather_v(block.reshape(-1).view(
+                torch.int64))])
+    else:
+        # the per-session rows stay on their owners (session range own[rank]); the tail's median
+        # trend needs sessions [0, K) only: each owner's part of that prefix gathered
+        block = torch.zeros((0, 7), dtype=torch.float64, device=dev)
+        if world > 1:
+            kk = max(0, min(b, K) - a)
+            med_k = torch.cat(all_gather_v(st["median"][:kk].contiguous().view(torch.int64))).view(torch.float64)
     for p in cut:  # its Spearman / Shapiro-Wilk over every piece (:305-322), patched on every rank
         holders = [r for r in range(world) if bounds[r][0] <= p < bounds[r][1] or conts[r] == p]
         if world == 1:
@@ -1062,11 +1078,12 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
         pc[1][p] = int(proj["raw_n"][p])
         pc[2][p] = int(proj["n_trend"][p])
     if hasattr(shard, "tail"):  # one library call (fz_rq2_count_tail), device in and out
-        med = st["median"][:S] if world == 1 else block[:, 1].contiguous()
+        med = st["median"][:S] if world == 1 else (med_k if med_k is not None else block[:, 1].contiguous())
         tail = shard.tail(med, K, pc[5], pc[1], pc[0])
         tests, corr_mm = tail[:4], tail[4:6]
     else:
-        tests = shard.series_tests(block[:K, 1].contiguous())  # median trend of the sessions with >= 100 values
+        med = st["median"][:S] if world == 1 else (med_k if med_k is not None else block[:, 1])
+        tests = shard.series_tests(med[:K].contiguous())  # median trend of the sessions with >= 100 values
         elig = proj["eligible"] != 0
         corr = proj["corr"][elig][proj["raw_n"][elig] > 0]
         valid = corr[~np.isnan(corr)]
@@ -1081,8 +1098,9 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
         out = {"proj": proj, "K": K, "average": blk[:, 0].copy(), "median": blk[:, 1].copy(),
                "percentiles": blk[:, 2:].reshape(-1).copy(), "tests": tuple(float(v) for v in h[1]),
                "corr_mm": tuple(float(v) for v in h[2]), "null_lines": null_lines}
-        if not host_sessions:
-            out["sessions"] = block
+        if not host_sessions:  # (this owner's sessions [a, b): device columns)
+            out["sessions"] = {"range": (a, b), "average": st["average"][:S], "median": st["median"][:S],
+                               "percentiles": st["percentiles"][:5 * S]}
         if gather_values:
             out["session_values"] = h[3]
             sizes = np.zeros(M + 1, np.int64)  # session i holds one value of every run longer than i
@@ -1154,8 +1172,8 @@ def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, f
     whole axis when world == 1), each rank's runs sent to their sessions' owners and transposed there
     by (session, group) (_exchange_runs), per-session results, delta columns (re-ordered by CSV row,
     :216, :744) and initial samples gathered.  Intermediates stay on the device; the results are
-    copied to the host once (host_sessions=False: the per-session columns stay on the device,
-    "sessions").  Returns a dict for rq/compute.rq4b_result (host arrays, every rank)."""
+    copied to the host once (host_sessions=False: the per-session columns stay on their owners,
+    "sessions"; only the prefix of sessions the trends read is gathered).  Returns a dict for rq/compute.rq4b_result (host arrays, every rank)."""
     import torch
     part = shard.run()
     counts = part["counts"].clone()
@@ -1200,8 +1218,20 @@ def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, f
     # per-session rows (c2, c1, g2 quartiles, g1 quartiles, p_bm) of every owner, session order
     cols = [st["c2"][:S], st["c1"][:S]] + [st["g2_q"][:3 * S].reshape(S, 3)[:, j] for j in range(3)] + \
         [st["g1_q"][:3 * S].reshape(S, 3)[:, j] for j in range(3)] + [st["p_bm"][:S]]
+    own_cols = cols
     if world > 1:
-        got = all_gather_cols(cols)
+        if host_sessions:
+            got = all_gather_cols(cols)
+        else:
+            # the trends read sessions with both groups >= 100 (:849-860): a prefix of length L, the
+            # shorter of the two groups' 100th longest series - each owner's part of it gathered, the
+            # per-session rows stay on their owners
+            def hundredth(x):
+                x = np.sort(x)[::-1]
+                return int(x[99]) if len(x) >= 100 else 0
+            L = min(hundredth(runs.n[group == 0]), hundredth(runs.n[group == 1]), M)
+            kk = max(0, min(b, L) - a)
+            got = all_gather_cols([x[:kk] for x in cols])
         cols = [torch.cat([g[j] for g in got]) for j in range(len(cols))]
     # coverage deltas: columns of every rank (CSV row, 7 pre, 7 post), put in corpus CSV order below
     nd, n2, n1 = (int(v) for v in host_many(torch.stack([part["counts"][RQ4B_DELTA_PROJECTS],
@@ -1264,8 +1294,8 @@ def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, f
                "pre_cov": [pre_h[i].copy() for i in range(7)], "post_cov": [post_h[i].copy() for i in range(7)],
                "pre_median": [float(v) for v in med_h[:7]], "post_median": [float(v) for v in med_h[7:]],
                "init_g2": x_h, "init_g1": y_h, "tests": np.asarray(tests_h, dtype=np.float64)}
-        if not host_sessions:
-            out["sessions"] = cols
+        if not host_sessions:  # (this owner's sessions [a, b): device columns)
+            out["sessions"] = {"range": (a, b), "cols": own_cols}
         return out
     d = Deferred([counts, last_d, sp, pre, post, med, x, y, tests] + (list(cols) if host_sessions else []), finish)
     return d if finish_later else d.result()
@@ -1404,14 +1434,12 @@ class _GpuExchange:
         E, C, eng = self.E, self.C, self.eng
         torch = eng.torch
         out = torch.empty(max(n, 1), dtype=torch.float64, device=eng.dev)
+        runs = np.asarray(runs, np.int64).reshape(-1, 4)
         R = len(runs)
         if n == 0 or R == 0:
             return out[:0]
-        desc = np.zeros((R, 4), np.int64)
-        desc[:, 0] = [x[1] for x in runs]
-        desc[:, 1] = [x[2] for x in runs]
-        desc[:, 2] = [x[3] for x in runs]
-        desc[:, 3] = [x[0] for x in runs]  # (src int32, pad 0: one little-endian int64)
+        # fz_run_desc rows: src_off, len, base, src (int32, pad 0: one little-endian int64)
+        desc = np.ascontiguousarray(runs[:, [1, 2, 3, 0]])
         in_off = np.concatenate([[0], np.cumsum(desc[:, 1])[:-1]]).astype(np.int64)
         W = sl.shape[0]
         dst = np.concatenate([[0], np.cumsum(sl.sum(1))[:-1]]).astype(np.int64)
