@@ -37,8 +37,11 @@ for s in ${STEPS:-full bench}; do
       for r in $(seq 1 ${ROUNDS:-2}); do
         for i in "${!SETS[@]}"; do
           a="${SETS[$i]}"
-          timeout -k 10 300 python -u bench.py --config ${ABCONF:-c2} --steps ${ABSTEPS:-50} --warmup 3 --no-cpu-baseline \
-            --probe-steps 0 $a > $O/${T}_ab_${i}_$r.log 2>&1 || { tail -5 $O/${T}_ab_${i}_$r.log; exit 1; }
+          # (a set may start with VAR=value words: the environment of that run, e.g. FZ_LIB_PATH=...)
+          envs=(); args=()
+          for w in $a; do if [[ ${#args[@]} -eq 0 && $w == *=* && $w != -* ]]; then envs+=("$w"); else args+=("$w"); fi; done
+          timeout -k 10 300 env "${envs[@]}" python -u bench.py --config ${ABCONF:-c2} --steps ${ABSTEPS:-50} --warmup 3 --no-cpu-baseline \
+            --probe-steps 0 "${args[@]}" > $O/${T}_ab_${i}_$r.log 2>&1 || { tail -5 $O/${T}_ab_${i}_$r.log; exit 1; }
           echo "ab[$i] '$a' r$r $(grep -o '"ms_per_step": [0-9.]*' $O/${T}_ab_${i}_$r.log)" | tee -a $O/${T}_ab.txt
         done
       done ;;

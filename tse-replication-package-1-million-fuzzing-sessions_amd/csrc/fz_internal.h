@@ -391,6 +391,22 @@ bool fused_fold_on();
 unsigned *seg_tickets(fz_ctx *c, int64_t S);
 void radix_sort_rows_payload32(fz_ctx *c, const uint32_t *key_src, uint32_t *&keys, uint32_t *&vals, int64_t n,
                                int bits, RadixPayload &pl);
+// Up to three such sorts (32-bit keys, values, payload columns) in shared launches: one histogram
+// launch for all, then one launch per digit pass over every table that has that digit.  Per table:
+// key_src (optional, as radix_sort_rows_payload32: the first pass reads the keys there and takes the
+// positions as values) or keys + vals (caller buffers of n entries, overwritten); on return keys /
+// vals / pl.out point at the sorted data.  hist0: [3][8][256] u64 digit totals, zeroed by the caller.
+struct RadixTab {
+    const uint32_t *key_src = nullptr;
+    uint32_t *keys = nullptr;
+    uint32_t *vals = nullptr;
+    int64_t n = 0;
+    int bits = 0;
+    RadixPayload pl;
+    int npass = 0;  // (set by the sort)
+};
+constexpr int64_t kRadixTabHistWords = 3 * 8 * 256;
+void radix_sort_tables_payload32(fz_ctx *c, RadixTab *tabs, int nt, unsigned long long *hist0);
 // min/max over int64 values skipping FZ_TS_NULL: writes {min, max} to host array.
 void minmax_i64_to_host(fz_ctx *c, const int64_t *const *cols, const int64_t *ns, int ncols,
                         int64_t *host_minmax);

@@ -593,46 +593,43 @@ __device__ inline void onesweep_move(const T *__restrict__ in, T *__restrict__ o
     }
 }
 
-// KeyT: uint64_t, or uint32_t for keys of at most 32 bits (the prefix / session-index transposes:
-// 4 bytes per key less to read and write in every pass)
-template <typename KeyT, bool HAS_VALS, bool HAS_PL, int TILE, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_onesweep(const KeyT *__restrict__ keys_in,
-                                                     const uint32_t *__restrict__ vals_in,
-                                                     KeyT *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
-                                                     int64_t n, int shift, const unsigned long long *__restrict__ ghist,
-                                                     uint64_t *__restrict__ status, unsigned int *__restrict__ ticket,
-                                                     uint64_t epoch,
-                                                     unsigned long long *__restrict__ gsum,
-                                                     unsigned long long *__restrict__ next_hist,
-                                                     RadixPayload pl, const int64_t *__restrict__ d_live) {
-    constexpr int ITEMS = TILE / BLOCK, WAVES = BLOCK / kWave;
-    static_assert(BLOCK >= kRadix && TILE % BLOCK == 0 && TILE <= 65536, "radix pass shape");
-    __shared__ uint64_t s_stage[TILE];  // the keys, then 8-byte payload columns
-    KeyT *const s_keys = reinterpret_cast<KeyT *>(s_stage);
-    __shared__ uint32_t s_vals[HAS_VALS ? TILE : 1];
-    __shared__ uint32_t s_run[kRadix];
-    __shared__ uint32_t s_wcnt[WAVES][kRadix];
-    __shared__ uint32_t s_start[kRadix];
-    __shared__ int64_t s_goff[kRadix];
-    __shared__ uint32_t s_tmp[WAVES];
-    __shared__ int64_t s_tmp64[WAVES];
-    __shared__ unsigned int s_tile;
+// One tile of a radix pass (k_onesweep: one sort; k_onesweep_tabs: a tile of one of up to three
+// tables' sorts in a shared launch).  The LDS arrays are the caller's (static __shared__ in the
+// kernels: one set per workgroup).
+template <typename KeyT, bool HAS_VALS, int TILE, int BLOCK>
+struct OsShared {
+    static constexpr int WAVES = BLOCK / kWave;
+    uint64_t stage[TILE];  // the keys, then 8-byte payload columns
+    uint32_t vals[HAS_VALS ? TILE : 1];
+    uint32_t run[kRadix];
+    uint32_t wcnt[WAVES][kRadix];
+    uint32_t start[kRadix];
+    int64_t goff[kRadix];
+    uint32_t tmp[WAVES];
+    int64_t tmp64[WAVES];
+};
 
+template <typename KeyT, bool HAS_VALS, bool HAS_PL, int TILE, int BLOCK>
+__device__ __forceinline__ void onesweep_tile(OsShared<KeyT, HAS_VALS, TILE, BLOCK> &sh, const int64_t tile,
+                                              const KeyT *__restrict__ keys_in, const uint32_t *__restrict__ vals_in,
+                                              KeyT *__restrict__ keys_out, uint32_t *__restrict__ vals_out, int64_t n,
+                                              int shift, const int64_t gcount, uint64_t *__restrict__ status,
+                                              uint64_t epoch, unsigned long long *__restrict__ gsum,
+                                              const RadixPayload &pl) {
+    constexpr int ITEMS = TILE / BLOCK, WAVES = BLOCK / kWave;
+    KeyT *const s_keys = reinterpret_cast<KeyT *>(sh.stage);
+    uint64_t *const s_stage = sh.stage;
+    uint32_t *const s_vals = sh.vals;
+    uint32_t *const s_run = sh.run;
+    uint32_t(*const s_wcnt)[kRadix] = sh.wcnt;
+    uint32_t *const s_start = sh.start;
+    int64_t *const s_goff = sh.goff;
+    uint32_t *const s_tmp = sh.tmp;
+    int64_t *const s_tmp64 = sh.tmp64;
     const int tid = threadIdx.x;
     const int w = wave_id(), lane = lane_id();
-    if (tid == 0) s_tile = lb_take_tile(ticket, gridDim.x);
     const bool dig = tid < kRadix;  // threads [0, 256) own one digit each after the ranking
-    if (next_hist && blockIdx.x == 0)  // the next sort's digit totals start from zero
-        for (int i = tid; i < kOsMaxPasses * kRadix; i += BLOCK) next_hist[i] = 0ull;
-    for (int i = tid; i < WAVES * kRadix; i += BLOCK) (&s_wcnt[0][0])[i] = 0;
-    const int64_t gcount = dig ? int64_t(ghist[tid]) : 0;  // issued early: consumed after the ranking
-    // live-bounded sorts (d_live): only the first *d_live keys are sorted; the tiles past them leave
-    // after drawing their ticket (no later tile looks back at them), the entries past them untouched
-    if (d_live && *d_live < n) n = *d_live > 0 ? *d_live : 0;
-    __syncthreads();
-    const int64_t tile = s_tile;
     const int64_t base = tile * TILE;
-    if (base >= n) return;
 #ifdef FZ_OS_TIMING
     if (tid == 0) atomicMin(&g_os_first, (unsigned long long)wall_clock64());
 #endif
@@ -825,6 +822,284 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const KeyT *__restrict__ key
     __syncthreads();
     OS_STAMP(5);
 #endif
+}
+
+// KeyT: uint64_t, or uint32_t for keys of at most 32 bits (the prefix / session-index transposes:
+// 4 bytes per key less to read and write in every pass)
+template <typename KeyT, bool HAS_VALS, bool HAS_PL, int TILE, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_onesweep(const KeyT *__restrict__ keys_in,
+                                                     const uint32_t *__restrict__ vals_in,
+                                                     KeyT *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
+                                                     int64_t n, int shift, const unsigned long long *__restrict__ ghist,
+                                                     uint64_t *__restrict__ status, unsigned int *__restrict__ ticket,
+                                                     uint64_t epoch,
+                                                     unsigned long long *__restrict__ gsum,
+                                                     unsigned long long *__restrict__ next_hist,
+                                                     RadixPayload pl, const int64_t *__restrict__ d_live) {
+    static_assert(BLOCK >= kRadix && TILE % BLOCK == 0 && TILE <= 65536, "radix pass shape");
+    __shared__ OsShared<KeyT, HAS_VALS, TILE, BLOCK> sh;
+    __shared__ unsigned int s_tile;
+    const int tid = threadIdx.x;
+    if (tid == 0) s_tile = lb_take_tile(ticket, gridDim.x);
+    const bool dig = tid < kRadix;
+    if (next_hist && blockIdx.x == 0)  // the next sort's digit totals start from zero
+        for (int i = tid; i < kOsMaxPasses * kRadix; i += BLOCK) next_hist[i] = 0ull;
+    for (int i = tid; i < OsShared<KeyT, HAS_VALS, TILE, BLOCK>::WAVES * kRadix; i += BLOCK) (&sh.wcnt[0][0])[i] = 0;
+    const int64_t gcount = dig ? int64_t(ghist[tid]) : 0;  // issued early: consumed after the ranking
+    // live-bounded sorts (d_live): only the first *d_live keys are sorted; the tiles past them leave
+    // after drawing their ticket (no later tile looks back at them), the entries past them untouched
+    if (d_live && *d_live < n) n = *d_live > 0 ? *d_live : 0;
+    __syncthreads();
+    const int64_t tile = s_tile;
+    if (tile * TILE >= n) return;
+    onesweep_tile<KeyT, HAS_VALS, HAS_PL, TILE, BLOCK>(sh, tile, keys_in, vals_in, keys_out, vals_out, n, shift, gcount,
+                                                       status, epoch, gsum, pl);
+}
+
+// ---- up to three tables' sorts in shared launches (the store's prefix sorts) ----------------
+// One histogram launch counts every table's digits (table k's workgroups [hb[k], hb[k + 1])), then
+// each pass is ONE launch over all tables that have that digit: tile t of the launch (ticket order)
+// is tile t - tile0[k] of table k, which looks back only over its own table's tiles (their own
+// status words and group sums) - three sorts' launch latencies and look-back tails become one.
+constexpr int kOsMaxTabs = 3;
+static_assert(kRadixTabHistWords == kOsMaxTabs * kOsMaxPasses * kRadix, "fz_internal.h kRadixTabHistWords");
+struct OsTab {
+    const uint32_t *keys_in = nullptr;
+    const uint32_t *vals_in = nullptr;  // null: the keys' positions (a first pass over row ids)
+    uint32_t *keys_out = nullptr;
+    uint32_t *vals_out = nullptr;
+    int64_t n = 0;
+    int npass = 0;
+    const unsigned long long *ghist = nullptr;  // [npass][kRadix] digit totals (zeroed before the histogram)
+    unsigned long long *gsum = nullptr;         // [npass][groups][kRadix] look-back group sums
+    int64_t gwords = 0;                         // groups * kRadix
+    uint64_t *status = nullptr;                 // this table's (tile, digit) status words
+    RadixPayload pl;
+};
+struct OsTabs {
+    OsTab t[kOsMaxTabs];
+    int nt = 0;
+    int64_t tile0[kOsMaxTabs + 1] = {0, 0, 0, 0};  // (pass launches) global tile range of table k
+    unsigned hb[kOsMaxTabs + 1] = {0, 0, 0, 0};    // (histogram launch) workgroup range of table k
+};
+
+__global__ __launch_bounds__(kBlock) void k_onesweep_hist_tabs(const OsTabs T) {
+    __shared__ uint32_t s_h[kOsMaxPasses][kRadix];
+    int k = 0;
+    while (k + 1 < T.nt && blockIdx.x >= T.hb[k + 1]) ++k;
+    const OsTab &tb = T.t[k];
+    const unsigned blk = blockIdx.x - T.hb[k], nblk = T.hb[k + 1] - T.hb[k];
+    const int npass = tb.npass;
+    const int64_t n = tb.n;
+    const uint32_t *keys = tb.keys_in;
+    unsigned long long *gh = const_cast<unsigned long long *>(tb.ghist);
+    // (this launch precedes every pass: the passes' group sums start from zero)
+    for (int64_t i = int64_t(blk) * kBlock + threadIdx.x; i < tb.gwords * npass; i += int64_t(nblk) * kBlock)
+        tb.gsum[i] = 0ull;
+    for (int i = threadIdx.x; i < kOsMaxPasses * kRadix; i += kBlock) (&s_h[0][0])[i] = 0u;
+    __syncthreads();
+    constexpr int kHistUnroll = 8;
+    const int64_t stride = int64_t(nblk) * kBlock;
+    for (int64_t i0 = int64_t(blk) * kBlock + threadIdx.x; i0 - threadIdx.x < n; i0 += stride * kHistUnroll) {
+        uint32_t kk[kHistUnroll];
+#pragma unroll
+        for (int u = 0; u < kHistUnroll; ++u) {
+            const int64_t i = i0 + u * stride;
+            kk[u] = i < n ? keys[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kHistUnroll; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i - threadIdx.x >= n) break;  // (wave-uniform)
+            const bool valid = i < n;
+            for (int p = 0; p < npass; ++p) {
+                const uint32_t d = (kk[u] >> (p * kRadixBits)) & (kRadix - 1);
+                const uint32_t d0 = __shfl(d, 0, 64);
+                const uint64_t act = __ballot(valid);
+                if (__ballot(valid && d == d0) == act) {
+                    if (lane_id() == 0 && act) atomicAdd(&s_h[p][d0], uint32_t(__popcll(act)));
+                } else if (p == npass - 1 && npass > 1) {
+                    const uint64_t peers = match_digit<kRadixBits>(d, valid);
+                    if (valid && (__ffsll((long long)peers) - 1) == lane_id())
+                        atomicAdd(&s_h[p][d], uint32_t(__popcll(peers)));
+                } else if (valid) {
+                    atomicAdd(&s_h[p][d], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < npass * kRadix; i += kBlock) {
+        const uint32_t v = (&s_h[0][0])[i];
+        if (v) atomicAdd(&gh[i], (unsigned long long)v);
+    }
+}
+
+template <bool HAS_PL, int TILE, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_onesweep_tabs(const OsTabs T, int pass, unsigned int *__restrict__ ticket,
+                                                         uint64_t epoch) {
+    __shared__ OsShared<uint32_t, true, TILE, BLOCK> sh;
+    __shared__ unsigned int s_tile;
+    const int tid = threadIdx.x;
+    if (tid == 0) s_tile = lb_take_tile(ticket, gridDim.x);
+    for (int i = tid; i < OsShared<uint32_t, true, TILE, BLOCK>::WAVES * kRadix; i += BLOCK) (&sh.wcnt[0][0])[i] = 0;
+    __syncthreads();
+    const int64_t g = s_tile;
+    int k = 0;
+    while (k + 1 < T.nt && g >= T.tile0[k + 1]) ++k;
+    const OsTab &tb = T.t[k];
+    const int64_t tile = g - T.tile0[k];
+    if (tile * TILE >= tb.n) return;
+    const int64_t gcount = tid < kRadix ? int64_t(tb.ghist[pass * kRadix + tid]) : 0;
+    onesweep_tile<uint32_t, true, HAS_PL, TILE, BLOCK>(sh, tile, tb.keys_in, tb.vals_in, tb.keys_out, tb.vals_out,
+                                                       tb.n, pass * kRadixBits, gcount, tb.status, epoch,
+                                                       tb.gsum + pass * tb.gwords, tb.pl);
+}
+
+void radix_sort_tables_payload32(fz_ctx *c, RadixTab *tabs, int nt, unsigned long long *hist0) {
+    FZ_CHECK(nt >= 1 && nt <= kOsMaxTabs, "radix_sort_tables: 1..3 tables");
+    int64_t nmax = 0, ntot = 0;
+    int npass_max = 0;
+    for (int k = 0; k < nt; ++k) {
+        RadixTab &r = tabs[k];
+        FZ_CHECK(r.bits >= 0 && r.bits <= 32 && r.n >= 0 && r.n < (int64_t(1) << 31) && (r.n == 0 || r.vals),
+                 "radix_sort_tables: bad table");
+        r.npass = (r.n > 1 && r.bits > 0) ? (r.bits + kRadixBits - 1) / kRadixBits : 0;
+        if (r.npass == 0) {  // unmoved (at most one key or a 0-bit key)
+            FZ_CHECK(!r.key_src, "radix sort from a read-only key source needs a pass");
+            for (int j = 0; j < r.pl.n; ++j) r.pl.out[j] = const_cast<void *>(r.pl.in[j]);
+        }
+        nmax = r.n > nmax ? r.n : nmax;
+        ntot += r.npass ? r.n : 0;
+        npass_max = r.npass > npass_max ? r.npass : npass_max;
+    }
+    if (npass_max == 0) return;
+    const bool big = nmax >= kOsBigN;
+    const int64_t tile = big ? kSortTileBig : kSortTile;
+    // per table: tiles, look-back groups, the digit totals (hist0: zeroed [nt][kOsMaxPasses][kRadix]),
+    // group sums; ping-pong scratch for keys, values and payload columns
+    OsTabs T;
+    T.nt = nt;
+    int64_t nb[kOsMaxTabs] = {}, gw[kOsMaxTabs] = {};
+    void *pbuf[kOsMaxTabs][2][kMaxPayload] = {};
+    uint32_t *k2[kOsMaxTabs] = {}, *v2[kOsMaxTabs] = {};
+    for (int k = 0; k < nt; ++k) {
+        RadixTab &r = tabs[k];
+        OsTab &o = T.t[k];
+        nb[k] = r.npass ? (r.n + tile - 1) / tile : 0;
+        gw[k] = ((nb[k] + kOsGroup - 1) / kOsGroup) * kRadix;
+        o.n = r.npass ? r.n : 0;
+        o.npass = r.npass;
+        o.ghist = hist0 + int64_t(k) * kOsMaxPasses * kRadix;
+        o.gwords = gw[k];
+        o.gsum = r.npass ? c->arena.get<unsigned long long>(gw[k] * r.npass) : nullptr;
+        o.keys_in = r.key_src ? r.key_src : r.keys;
+        if (!r.npass) continue;
+        k2[k] = c->arena.get<uint32_t>(r.n);
+        v2[k] = c->arena.get<uint32_t>(r.n);
+        for (int j = 0; j < r.pl.n; ++j)
+            for (int b = 0; b < 2; ++b) pbuf[k][b][j] = c->arena.alloc(size_t(r.n) * size_t(r.pl.size[j]));
+    }
+    // histogram: workgroups in proportion to each table's keys
+    {
+        double hbytes = 0.0;
+        unsigned at = 0;
+        const unsigned hblocks_all = ntot >= (int64_t(1) << 22) ? kHistBigBlocks : unsigned(kHistMaxBlocks);
+        for (int k = 0; k < nt; ++k) {
+            T.hb[k] = at;
+            if (T.t[k].n > 0) {
+                unsigned b = unsigned(double(hblocks_all) * double(T.t[k].n) / double(ntot > 0 ? ntot : 1));
+                const unsigned need = unsigned((T.t[k].n + kHistKeysPerBlock - 1) / kHistKeysPerBlock);
+                b = b < 1 ? 1 : (b > need ? need : b);
+                at += b;
+                hbytes += 4.0 * double(T.t[k].n);
+            }
+        }
+        T.hb[nt] = at;
+        for (int k = nt + 1; k <= kOsMaxTabs; ++k) T.hb[k] = at;
+        ProbeScope ps(c, "radix_hist", hbytes);
+        k_onesweep_hist_tabs<<<at, kBlock, 0, c->stream>>>(T);
+        FZ_LAUNCH_CHECK();
+    }
+    // the passes: table k's current keys / values / columns
+    const uint32_t *ka[kOsMaxTabs], *va[kOsMaxTabs];
+    uint32_t *kb[kOsMaxTabs], *vb[kOsMaxTabs];
+    for (int k = 0; k < nt; ++k) {
+        RadixTab &r = tabs[k];
+        ka[k] = r.key_src ? r.key_src : r.keys;
+        va[k] = r.key_src ? nullptr : r.vals;
+        kb[k] = k2[k];
+        vb[k] = v2[k];
+    }
+    int passes = 0;
+    for (int p = 0; p < npass_max; ++p) {
+        OsTabs P = T;
+        int64_t tiles = 0;
+        double bytes = 0.0;
+        bool any_pl = false;
+        for (int k = 0; k < nt; ++k) {
+            RadixTab &r = tabs[k];
+            OsTab &o = P.t[k];
+            P.tile0[k] = tiles;
+            if (p >= r.npass) {  // (this table's sort has no such digit: no tiles in this launch)
+                o.n = 0;
+                continue;
+            }
+            o.keys_in = ka[k];
+            o.vals_in = va[k];
+            o.keys_out = kb[k];
+            o.vals_out = vb[k];
+            o.pl = r.pl;
+            for (int j = 0; j < r.pl.n; ++j) {
+                o.pl.in[j] = p == 0 ? r.pl.in[j] : pbuf[k][(p - 1) & 1][j];
+                o.pl.out[j] = pbuf[k][p & 1][j];
+            }
+            any_pl = any_pl || r.pl.n > 0;
+            tiles += nb[k];
+            bytes += (16.0 + 2.0 * r.pl.bytes()) * double(r.n);
+        }
+        for (int k = nt; k <= kOsMaxTabs; ++k) P.tile0[k] = tiles;
+        P.tile0[nt] = tiles;
+        const Lookback lb = lookback_begin(c, tiles * kRadix);
+        for (int k = 0; k < nt; ++k) P.t[k].status = lb.status + P.tile0[k] * kRadix;
+        {
+            ProbeScope ps(c, "radix_scatter", bytes);
+            if (big) {
+                if (any_pl) k_onesweep_tabs<true, kSortTileBig, kOsBlockBig><<<unsigned(tiles), kOsBlockBig, 0, c->stream>>>(P, p, lb.ticket, lb.epoch);
+                else k_onesweep_tabs<false, kSortTileBig, kOsBlockBig><<<unsigned(tiles), kOsBlockBig, 0, c->stream>>>(P, p, lb.ticket, lb.epoch);
+            } else {
+                if (any_pl) k_onesweep_tabs<true, kSortTile, kOsBlock><<<unsigned(tiles), kOsBlock, 0, c->stream>>>(P, p, lb.ticket, lb.epoch);
+                else k_onesweep_tabs<false, kSortTile, kOsBlock><<<unsigned(tiles), kOsBlock, 0, c->stream>>>(P, p, lb.ticket, lb.epoch);
+            }
+            FZ_LAUNCH_CHECK();
+        }
+        lookback_end(c, tiles);
+        ++passes;
+        for (int k = 0; k < nt; ++k) {
+            RadixTab &r = tabs[k];
+            if (p >= r.npass) continue;
+            if (p == 0 && r.key_src) {  // (the source is never written: the caller's buffers take its place)
+                ka[k] = kb[k];
+                va[k] = vb[k];
+                kb[k] = r.keys;
+                vb[k] = r.vals;
+            } else {
+                const uint32_t *tk = ka[k], *tv = va[k];
+                ka[k] = kb[k];
+                va[k] = vb[k];
+                kb[k] = const_cast<uint32_t *>(tk);
+                vb[k] = const_cast<uint32_t *>(tv);
+            }
+        }
+    }
+    for (int k = 0; k < nt; ++k) {
+        RadixTab &r = tabs[k];
+        if (!r.npass) continue;
+        r.keys = const_cast<uint32_t *>(ka[k]);
+        r.vals = const_cast<uint32_t *>(va[k]);
+        for (int j = 0; j < r.pl.n; ++j) r.pl.out[j] = pbuf[k][(r.npass - 1) & 1][j];
+    }
+    c->sort_passes += passes;
 }
 
 void radix_sort_pairs(fz_ctx *c, uint64_t *keys, uint32_t *vals, int64_t n, int bits) {

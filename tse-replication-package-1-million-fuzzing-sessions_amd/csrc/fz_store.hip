@@ -705,11 +705,11 @@ struct TableIn {
     GatherCols gc;
     unsigned long long *big;
 };
-static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) {
+static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss, unsigned long long *hist0) {
     PrefixKeys K;
     // a prefix that is the project alone (coverage, issues) is sorted straight from the table's
-    // project column with implicit row ids (radix_sort_rows_payload32): no key / row-id copy pass
-    // (0.42 ms at config 3); the builds' (type | project) keys are made by k_keys_prefix_rows
+    // project column with implicit row ids (key_src): no key / row-id copy pass (0.42 ms at config
+    // 3); the builds' (type | project) keys are made by k_keys_prefix_rows
     bool direct[3];
     int64_t total = 0;
     for (int k = 0; k < 3; ++k) {
@@ -728,16 +728,30 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) 
         k_keys_prefix_rows<<<grid_for(K.base[3], kBlock, 4096), kBlock, 0, c->stream>>>(K);
         FZ_LAUNCH_CHECK();
     }
-    // the coverage and issues tables' radix sorts on two helpers (their own streams, look-back
-    // state and arenas - the sorted columns live in the helper's arena until the gather), the
-    // builds' on c
-    const bool fork = store_helpers(c) >= 2 && in[1].n > 0 && (in[0].n > 0 || in[2].n > 0);
-    fz_ctx *tctx[3] = {c, fork ? c->helpers[0] : c, fork ? c->helpers[1] : c};
-    if (fork) {
-        store_fork(c);
-        c->helpers[0]->arena.reset();
-        c->helpers[1]->arena.reset();
+    // the three tables' radix sorts share their launches (one histogram launch, one launch per
+    // digit pass): config 2's nine launches - each a few-tile look-back tail plus a launch gap -
+    // become three.  The prefix passes move the time column and the gathered columns with the keys
+    // (each pass's writes land in per-digit runs): the time sort and the gather then read every
+    // segment's rows from one contiguous range instead of gathering them from the heap-ordered table
+    RadixTab rt[3];
+    for (int k = 0; k < 3; ++k) {
+        const TableIn &t = in[k];
+        RadixTab &r = rt[k];
+        r.n = pss[k].n;
+        r.bits = r.n > 1 ? t.prefix_bits : 0;
+        r.key_src = direct[k] ? t.pre.proj : nullptr;
+        r.keys = K.keys[k];
+        r.vals = K.vals[k];
+        r.pl.no_digit_probe = true;
+        r.pl.n = 1 + t.gc.n;
+        r.pl.in[0] = t.time;
+        r.pl.size[0] = 8;
+        for (int j = 0; j < t.gc.n; ++j) {
+            r.pl.in[1 + j] = t.gc.src[j];
+            r.pl.size[1 + j] = t.gc.size[j];
+        }
     }
+    radix_sort_tables_payload32(c, rt, 3, hist0);
     PrefixOffs O;
     for (int k = 0; k < 3; ++k) {
         const TableIn &t = in[k];
@@ -745,26 +759,11 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) 
         const int64_t n = ps.n;
         O.base[k + 1] = O.base[k];
         if (n == 0) continue;
-        // the prefix passes move the time column and the gathered columns with the keys (each
-        // pass's writes land in per-digit runs): the time sort and the gather then read every
-        // segment's rows from one contiguous range instead of gathering them from the heap-ordered
-        // table
-        RadixPayload pl;
-        pl.no_digit_probe = true;
-        pl.n = 1 + t.gc.n;
-        pl.in[0] = t.time;
-        pl.size[0] = 8;
-        for (int j = 0; j < t.gc.n; ++j) {
-            pl.in[1 + j] = t.gc.src[j];
-            pl.size[1 + j] = t.gc.size[j];
-        }
-        if (direct[k])
-            radix_sort_rows_payload32(tctx[k], t.pre.proj, K.keys[k], K.vals[k], n, t.prefix_bits, pl);
-        else
-            radix_sort_pairs_payload32(tctx[k], K.keys[k], K.vals[k], n, t.prefix_bits, pl);
-        ps.time = static_cast<const int64_t *>(pl.out[0]);
+        K.keys[k] = rt[k].keys;
+        K.vals[k] = rt[k].vals;
+        ps.time = static_cast<const int64_t *>(rt[k].pl.out[0]);
         ps.gc = t.gc;
-        for (int j = 0; j < t.gc.n; ++j) ps.gc.src[j] = pl.out[1 + j];
+        for (int j = 0; j < t.gc.n; ++j) ps.gc.src[j] = rt[k].pl.out[1 + j];
         const int64_t S = int64_t(1) << t.prefix_bits;
         ps.S = S;
         ps.offs = c->arena.get<int64_t>(S + 1);
@@ -778,7 +777,6 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss) 
         O.offs[k] = const_cast<int64_t *>(ps.offs);
         O.base[k + 1] = O.base[k] + (n > S + 1 ? n : S + 1);
     }
-    if (fork) store_join(c);
     // per prefix binary searches when the tables hold many rows per prefix (O(S log n) instead of a
     // pass over every key: 0.37 ms at config 3)
     int64_t nall = 0, sall = 0;
@@ -1332,8 +1330,9 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     }
     // big3[k]: rows of table k in segments left to the merge sort, big3[3 + k]: the longest such
     // segment, big3[6 + k]: rows whose columns the long bucket class gathered (one zeroing for all)
-    unsigned long long *big3 = c->arena.get<unsigned long long>(9);
-    dev_fill(c, big3, 0, 9 * 8);
+    unsigned long long *big3 = c->arena.get<unsigned long long>(9 + kRadixTabHistWords);
+    unsigned long long *hist0 = big3 + 9;  // the prefix sorts' digit totals (zeroed with the counters)
+    dev_fill(c, big3, 0, (9 + kRadixTabHistWords) * 8);
     PrefixSorted pss[3];
     TableIn tin[3];
     for (int k = 0; k < 3; ++k) {
@@ -1341,7 +1340,7 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         tin[k] = TableIn{b.n, b.pre, b.pbits_total, b.time, b.tm->ensure<int64_t>(b.n), b.pr->ensure<uint32_t>(b.n),
                          gcs[k], big3 + k};
     }
-    prefix_sort_tables(c, tin, pss);
+    prefix_sort_tables(c, tin, pss, hist0);
     time_sort_tables(c, pss);
     // the views (per-project ranges of the sorted tables): their offsets, longest segments and row
     // counts off the prefix offsets - builds' prefix is type << pbits | project (Fuzzing 0, Coverage 1)
