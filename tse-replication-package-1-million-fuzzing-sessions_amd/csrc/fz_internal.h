@@ -398,6 +398,8 @@ void radix_sort_rows_payload32(fz_ctx *c, const uint32_t *key_src, uint32_t *&ke
 // vals / pl.out point at the sorted data.  hist0: [3][8][256] u64 digit totals, zeroed by the caller.
 struct RadixTab {
     const uint32_t *key_src = nullptr;
+    const uint8_t *type_src = nullptr;  // (with key_src) key = key_src | min(type, 2) << type_shift
+    int type_shift = 0;
     uint32_t *keys = nullptr;
     uint32_t *vals = nullptr;
     int64_t n = 0;
@@ -406,7 +408,16 @@ struct RadixTab {
     int npass = 0;  // (set by the sort)
 };
 constexpr int64_t kRadixTabHistWords = 3 * 8 * 256;
-void radix_sort_tables_payload32(fz_ctx *c, RadixTab *tabs, int nt, unsigned long long *hist0);
+// side: (optional) a min / max of an int64 column (FZ_TS_NULL skipped) in the histogram launch's
+// extra workgroups - partials part[4 * b + {2, 3}] for b < blocks
+struct RadixSideMinMax {
+    const int64_t *src = nullptr;
+    int64_t n = 0;
+    int64_t *part = nullptr;
+    unsigned blocks = 0;
+};
+void radix_sort_tables_payload32(fz_ctx *c, RadixTab *tabs, int nt, unsigned long long *hist0,
+                                 const RadixSideMinMax *side = nullptr);
 // min/max over int64 values skipping FZ_TS_NULL: writes {min, max} to host array.
 void minmax_i64_to_host(fz_ctx *c, const int64_t *const *cols, const int64_t *ns, int ncols,
                         int64_t *host_minmax);

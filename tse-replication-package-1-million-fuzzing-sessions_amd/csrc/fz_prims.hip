@@ -615,7 +615,8 @@ __device__ __forceinline__ void onesweep_tile(OsShared<KeyT, HAS_VALS, TILE, BLO
                                               KeyT *__restrict__ keys_out, uint32_t *__restrict__ vals_out, int64_t n,
                                               int shift, const int64_t gcount, uint64_t *__restrict__ status,
                                               uint64_t epoch, unsigned long long *__restrict__ gsum,
-                                              const RadixPayload &pl) {
+                                              const RadixPayload &pl, const uint8_t *__restrict__ type_src = nullptr,
+                                              int type_shift = 0) {
     constexpr int ITEMS = TILE / BLOCK, WAVES = BLOCK / kWave;
     KeyT *const s_keys = reinterpret_cast<KeyT *>(sh.stage);
     uint64_t *const s_stage = sh.stage;
@@ -647,6 +648,12 @@ __device__ __forceinline__ void onesweep_tile(OsShared<KeyT, HAS_VALS, TILE, BLO
         const int64_t idx = wbase + r * kWave + lane;
         const bool valid = idx < n;
         k[r] = valid ? keys_in[idx] : KeyT(0);
+        // (type_src: the key is [type |] project, made here from the two columns - the builds'
+        // (Fuzzing 0, Coverage 1, any other type 2) << pbits | project of the store's prefix sort)
+        if (type_src && valid) {
+            const uint32_t ty = type_src[idx];
+            k[r] |= KeyT(ty > 1u ? 2u : ty) << type_shift;
+        }
         // (no vals_in: the values are the keys' positions - a sort's first pass over row ids)
         v[r] = (HAS_VALS && valid) ? (vals_in ? vals_in[idx] : uint32_t(idx)) : 0u;
     }
@@ -874,10 +881,13 @@ struct OsTab {
     unsigned long long *gsum = nullptr;         // [npass][groups][kRadix] look-back group sums
     int64_t gwords = 0;                         // groups * kRadix
     uint64_t *status = nullptr;                 // this table's (tile, digit) status words
+    const uint8_t *type_src = nullptr;          // (first pass / histogram) key |= min(type, 2) << type_shift
+    int type_shift = 0;
     RadixPayload pl;
 };
 struct OsTabs {
     OsTab t[kOsMaxTabs];
+    RadixSideMinMax side;  // (histogram launch) blocks [hb[nt], hb[nt] + side.blocks): its partials
     int nt = 0;
     int64_t tile0[kOsMaxTabs + 1] = {0, 0, 0, 0};  // (pass launches) global tile range of table k
     unsigned hb[kOsMaxTabs + 1] = {0, 0, 0, 0};    // (histogram launch) workgroup range of table k
@@ -885,6 +895,36 @@ struct OsTabs {
 
 __global__ __launch_bounds__(kBlock) void k_onesweep_hist_tabs(const OsTabs T) {
     __shared__ uint32_t s_h[kOsMaxPasses][kRadix];
+    if (blockIdx.x >= T.hb[T.nt]) {
+        // the side job: min / max of an int64 column skipping FZ_TS_NULL, per-workgroup partials
+        // part[4 * b + {2, 3}] (the store's issue-number range; one launch fewer than its own)
+        __shared__ int64_t s_lo[kBlock / kWave], s_hi[kBlock / kWave];
+        const RadixSideMinMax &sd = T.side;
+        const unsigned b = blockIdx.x - T.hb[T.nt];
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        for (int64_t i = int64_t(b) * kBlock + threadIdx.x; i < sd.n; i += int64_t(sd.blocks) * kBlock) {
+            const int64_t v = sd.src[i];
+            if (v == FZ_TS_NULL) continue;
+            lo = v < lo ? v : lo;
+            hi = v > hi ? v : hi;
+        }
+        lo = wave_min(lo);
+        hi = wave_max(hi);
+        if (lane_id() == 0) {
+            s_lo[wave_id()] = lo;
+            s_hi[wave_id()] = hi;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < kBlock / kWave; ++w) {
+                lo = s_lo[w] < lo ? s_lo[w] : lo;
+                hi = s_hi[w] > hi ? s_hi[w] : hi;
+            }
+            sd.part[4 * b + 2] = lo;
+            sd.part[4 * b + 3] = hi;
+        }
+        return;
+    }
     int k = 0;
     while (k + 1 < T.nt && blockIdx.x >= T.hb[k + 1]) ++k;
     const OsTab &tb = T.t[k];
@@ -906,6 +946,10 @@ __global__ __launch_bounds__(kBlock) void k_onesweep_hist_tabs(const OsTabs T) {
         for (int u = 0; u < kHistUnroll; ++u) {
             const int64_t i = i0 + u * stride;
             kk[u] = i < n ? keys[i] : 0u;
+            if (tb.type_src && i < n) {
+                const uint32_t ty = tb.type_src[i];
+                kk[u] |= (ty > 1u ? 2u : ty) << tb.type_shift;
+            }
         }
 #pragma unroll
         for (int u = 0; u < kHistUnroll; ++u) {
@@ -953,16 +997,19 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep_tabs(const OsTabs T, int pas
     const int64_t gcount = tid < kRadix ? int64_t(tb.ghist[pass * kRadix + tid]) : 0;
     onesweep_tile<uint32_t, true, HAS_PL, TILE, BLOCK>(sh, tile, tb.keys_in, tb.vals_in, tb.keys_out, tb.vals_out,
                                                        tb.n, pass * kRadixBits, gcount, tb.status, epoch,
-                                                       tb.gsum + pass * tb.gwords, tb.pl);
+                                                       tb.gsum + pass * tb.gwords, tb.pl,
+                                                       pass == 0 ? tb.type_src : nullptr, tb.type_shift);
 }
 
-void radix_sort_tables_payload32(fz_ctx *c, RadixTab *tabs, int nt, unsigned long long *hist0) {
+void radix_sort_tables_payload32(fz_ctx *c, RadixTab *tabs, int nt, unsigned long long *hist0,
+                                 const RadixSideMinMax *side) {
     FZ_CHECK(nt >= 1 && nt <= kOsMaxTabs, "radix_sort_tables: 1..3 tables");
     int64_t nmax = 0, ntot = 0;
     int npass_max = 0;
     for (int k = 0; k < nt; ++k) {
         RadixTab &r = tabs[k];
-        FZ_CHECK(r.bits >= 0 && r.bits <= 32 && r.n >= 0 && r.n < (int64_t(1) << 31) && (r.n == 0 || r.vals),
+        FZ_CHECK(r.bits >= 0 && r.bits <= 32 && r.n >= 0 && r.n < (int64_t(1) << 31) && (r.n == 0 || r.vals) &&
+                     (!r.type_src || r.key_src),
                  "radix_sort_tables: bad table");
         r.npass = (r.n > 1 && r.bits > 0) ? (r.bits + kRadixBits - 1) / kRadixBits : 0;
         if (r.npass == 0) {  // unmoved (at most one key or a 0-bit key)
@@ -973,7 +1020,10 @@ void radix_sort_tables_payload32(fz_ctx *c, RadixTab *tabs, int nt, unsigned lon
         ntot += r.npass ? r.n : 0;
         npass_max = r.npass > npass_max ? r.npass : npass_max;
     }
-    if (npass_max == 0) return;
+    if (npass_max == 0) {
+        FZ_CHECK(!side || side->blocks == 0, "radix_sort_tables: a side job needs a sort");
+        return;
+    }
     const bool big = nmax >= kOsBigN;
     const int64_t tile = big ? kSortTileBig : kSortTile;
     // per table: tiles, look-back groups, the digit totals (hist0: zeroed [nt][kOsMaxPasses][kRadix]),
@@ -994,6 +1044,8 @@ void radix_sort_tables_payload32(fz_ctx *c, RadixTab *tabs, int nt, unsigned lon
         o.gwords = gw[k];
         o.gsum = r.npass ? c->arena.get<unsigned long long>(gw[k] * r.npass) : nullptr;
         o.keys_in = r.key_src ? r.key_src : r.keys;
+        o.type_src = r.type_src;
+        o.type_shift = r.type_shift;
         if (!r.npass) continue;
         k2[k] = c->arena.get<uint32_t>(r.n);
         v2[k] = c->arena.get<uint32_t>(r.n);
@@ -1017,8 +1069,9 @@ void radix_sort_tables_payload32(fz_ctx *c, RadixTab *tabs, int nt, unsigned lon
         }
         T.hb[nt] = at;
         for (int k = nt + 1; k <= kOsMaxTabs; ++k) T.hb[k] = at;
+        if (side) T.side = *side;
         ProbeScope ps(c, "radix_hist", hbytes);
-        k_onesweep_hist_tabs<<<at, kBlock, 0, c->stream>>>(T);
+        k_onesweep_hist_tabs<<<at + T.side.blocks, kBlock, 0, c->stream>>>(T);
         FZ_LAUNCH_CHECK();
     }
     // the passes: table k's current keys / values / columns

@@ -175,13 +175,14 @@ void eligibility_counts(fz_ctx *c, const fz_tables *t, int64_t limit, int32_t *c
 }
 
 // Computed once per fz_store_build (store.elig / store.n_elig).
-void store_eligibility(fz_ctx *c) {
+// zeroed: the caller's fill already cleared the two counters (s.n_elig, allocated beforehand)
+void store_eligibility(fz_ctx *c, bool zeroed) {
     Store &s = store_of(c);
     const int64_t P = s.P;
     uint8_t *elig = s.elig.ensure<uint8_t>(P);
     int64_t *n = s.n_elig.ensure<int64_t>(2);
     int32_t *cnt = s.elig_cnt.ensure<int32_t>(P);  // (kept: fz_store_elig_counts reads them)
-    dev_fill(c, n, 0, 16);
+    if (!zeroed) dev_fill(c, n, 0, 16);
     eligibility(c, &s.t, kLimitUs, cnt, elig, n, n + 1);
 }
 

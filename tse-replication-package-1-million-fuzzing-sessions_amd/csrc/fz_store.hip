@@ -347,6 +347,13 @@ constexpr uint64_t kBlkTop = (uint64_t(1) << (64 - kBlkPosBits)) - 1;  // time f
 // does not fit the key, is flagged for the merge sort instead.  MAXN <= 4096 keeps the keys in LDS;
 // larger classes re-read them from the (prefix-sorted, cache-resident) time column.
 constexpr int kBucketSkew = 32;
+#ifndef FZ_TS_DIRECT
+// 1: the short classes write every column themselves, no gather pass - measured slower (same box,
+// config 2: store 0.470 vs 0.410 ms, profiles/r06_c2_ts_direct_ab.txt): the scattered partial-line
+// writes cost more than the gather's coalesced ones
+#define FZ_TS_DIRECT 0
+#endif
+constexpr bool kTsDirect = FZ_TS_DIRECT;
 #ifndef FZ_LONG_FUSE
 #define FZ_LONG_FUSE 1  // the 16384-row class gathers its columns itself (0: k_store_gather does)
 #endif
@@ -576,13 +583,39 @@ __device__ __forceinline__ void seg_time_bucket(const TimeSortTabs &T, int64_t m
             dq[m] = int32_t(st + rank);
         }
         if constexpr (!FUSE) {
-            // short segments: time, project and source position written to the sorted slot (the
-            // segment's few KiB stay in L2); k_store_gather moves the other columns afterwards
-            // (the classes without their keys in LDS re-read the segment's cache-resident times
-            // here: t[] is not live past the bucketing - fewer registers, more workgroups per CU)
+            if constexpr (KEYS_LDS && kTsDirect) {
+                // short segments (<= 4096 rows): every column written straight to the row's sorted
+                // slot - the segment's source rows are contiguous (prefix order) and its output range
+                // a few KiB that the partial-line writes fill in L2 - so no gather pass follows
+                // (spos keeps the prefilled kGathered marker)
+                if (tid == 0 && tb.fused) atomicAdd(tb.fused, (unsigned long long)n);
 #pragma unroll
-            for (int m = 0; m < IPT; ++m)
-                if (dq[m] >= 0) out.put(ob + dq[m], KEYS_LDS ? tm_at(m) : time[b + tid + m * BS], p, b + tid + m * BS);
+                for (int m = 0; m < IPT; ++m) {
+                    if (dq[m] < 0) continue;
+                    const int64_t q = ob + dq[m], r = b + tid + m * BS;
+                    out.otime[q] = tm_at(m);
+                    out.oproj[q] = p;
+                    if (!tb.prefilled) out.spos[q] = kGathered;
+                    gc.perm[q] = int32_t(tb.rows[r]);
+                    for (int j = 0; j < gc.n; ++j) {
+                        if (gc.size[j] == 8)
+                            static_cast<uint64_t *>(gc.dst[j])[q] = static_cast<const uint64_t *>(gc.src[j])[r];
+                        else if (gc.size[j] == 4)
+                            static_cast<uint32_t *>(gc.dst[j])[q] = static_cast<const uint32_t *>(gc.src[j])[r];
+                        else
+                            static_cast<uint8_t *>(gc.dst[j])[q] = static_cast<const uint8_t *>(gc.src[j])[r];
+                    }
+                }
+            } else {
+                // short segments: time, project and source position written to the sorted slot (the
+                // segment's few KiB stay in L2); k_store_gather moves the other columns afterwards
+                // (the classes without their keys in LDS re-read the segment's cache-resident times
+                // here: t[] is not live past the bucketing - fewer registers, more workgroups per CU)
+#pragma unroll
+                for (int m = 0; m < IPT; ++m)
+                    if (dq[m] >= 0)
+                        out.put(ob + dq[m], KEYS_LDS ? tm_at(m) : time[b + tid + m * BS], p, b + tid + m * BS);
+            }
             __syncthreads();  // LDS is reused by the next segment
             continue;
         }
@@ -705,16 +738,18 @@ struct TableIn {
     GatherCols gc;
     unsigned long long *big;
 };
-static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss, unsigned long long *hist0) {
+static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss, unsigned long long *hist0,
+                               uint32_t *const *spos, const RadixSideMinMax *side) {
     PrefixKeys K;
-    // a prefix that is the project alone (coverage, issues) is sorted straight from the table's
-    // project column with implicit row ids (key_src): no key / row-id copy pass (0.42 ms at config
-    // 3); the builds' (type | project) keys are made by k_keys_prefix_rows
+    // every table is sorted straight from its project column with implicit row ids (key_src): no
+    // key / row-id copy pass (0.42 ms at config 3) - the builds' (type | project) key made from the
+    // two columns in the histogram and the first pass (type_src); k_keys_prefix_rows only for a
+    // table of one row (no pass: its key and row id are the result)
     bool direct[3];
     int64_t total = 0;
     for (int k = 0; k < 3; ++k) {
         const int64_t n = in[k].n > 0 ? in[k].n : 0;
-        direct[k] = in[k].pre.type == nullptr && n > 1 && in[k].prefix_bits > 0;
+        direct[k] = n > 1 && in[k].prefix_bits > 0;
         K.base[k + 1] = K.base[k] + (direct[k] ? 0 : n);
         K.pre[k] = in[k].pre;
         K.keys[k] = n ? c->arena.get<uint32_t>(n) : nullptr;
@@ -740,6 +775,8 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss, 
         r.n = pss[k].n;
         r.bits = r.n > 1 ? t.prefix_bits : 0;
         r.key_src = direct[k] ? t.pre.proj : nullptr;
+        r.type_src = direct[k] ? t.pre.type : nullptr;
+        r.type_shift = t.pre.pbits;
         r.keys = K.keys[k];
         r.vals = K.vals[k];
         r.pl.no_digit_probe = true;
@@ -751,7 +788,7 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss, 
             r.pl.size[1 + j] = t.gc.size[j];
         }
     }
-    radix_sort_tables_payload32(c, rt, 3, hist0);
+    radix_sort_tables_payload32(c, rt, 3, hist0, side);
     PrefixOffs O;
     for (int k = 0; k < 3; ++k) {
         const TableIn &t = in[k];
@@ -768,7 +805,7 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss, 
         ps.S = S;
         ps.offs = c->arena.get<int64_t>(S + 1);
         ps.rows = K.vals[k];
-        ps.out = TimeSortOut{t.otime, t.oproj, c->arena.get<uint32_t>(n)};
+        ps.out = TimeSortOut{t.otime, t.oproj, spos[k]};
         ps.pmask = t.pre.pbits >= 32 ? 0xffffffffu : uint32_t((1ull << t.pre.pbits) - 1ull);
         ps.big = t.big;
         O.keys[k] = K.keys[k];
@@ -798,10 +835,13 @@ static void prefix_sort_tables(fz_ctx *c, const TableIn *in, PrefixSorted *pss, 
 #define FZ_TS_MID 1
 #endif
 constexpr bool kTsMid = FZ_TS_MID;  // the 12,288-row time-sort class
+#ifndef FZ_TS_CLASSES
+#define FZ_TS_CLASSES 0
+#endif
 #ifndef FZ_SPOS_PREFILL
 #define FZ_SPOS_PREFILL 1
 #endif
-static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
+static void time_sort_tables(fz_ctx *c, PrefixSorted *pss, uint8_t *flags) {
     TimeSortTabs T;
     int64_t ntot = 0;
     for (int k = 0; k < 3; ++k) {
@@ -811,7 +851,6 @@ static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
     }
     const int64_t S = T.base[3];
     if (S == 0) return;
-    uint8_t *flags = c->arena.get<uint8_t>(S);
     for (int k = 0; k < 3; ++k) {
         PrefixSorted &ps = pss[k];
         if (ps.S == 0) continue;
@@ -828,14 +867,11 @@ static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
         tb.fused = ps.big + 6;  // big3[6 + k]
         tb.prefilled = FZ_SPOS_PREFILL;
     }
-    // every row's source position starts as kGathered (one fill of all three tables): the bucket
-    // sorts overwrite the rows they sort; a segment they leave to the long-segment pass or the merge
-    // sort keeps the marker without a write of its own (a workgroup marking config 5's 20.8 M-row
-    // giant alone took ~1 ms, the long class's whole launch waiting on it)
-    // (the bigflag arrays cleared in the same launch)
-    const int64_t pf = FZ_SPOS_PREFILL ? 4 : 0;
-    fill_batch(c, {{flags, S, 0}, {pss[0].out.spos, pss[0].n * pf, 0xff}, {pss[1].out.spos, pss[1].n * pf, 0xff},
-                   {pss[2].out.spos, pss[2].n * pf, 0xff}});
+    // every row's source position starts as kGathered and the bigflag arrays as 0 (store_build's
+    // one fill): the bucket sorts overwrite the rows they sort; a segment they leave to the
+    // long-segment pass or the merge sort keeps the marker without a write of its own (a workgroup
+    // marking config 5's 20.8 M-row giant alone took ~1 ms, the long class's whole launch waiting
+    // on it)
     // algorithmic bytes: time 8 read; time 8 + project 4 + source position 4 written; the long
     // class also moves row id 4 + columns in, perm 4 + row 4 + columns out for its rows (added by
     // store_build once their count is read back: fused_gather_bytes)
@@ -849,11 +885,20 @@ static void time_sort_tables(fz_ctx *c, PrefixSorted *pss) {
     const int nh = store_helpers(c);
     if (nh > 0) store_fork(c);
     auto st = [&](int i) { return i > 0 && i <= nh ? c->helpers[i - 1]->stream : c->stream; };
-    k_seg_time_bucket<256, 1024><<<unsigned(S < 16384 ? S : 16384), 256, 0, st(0)>>>(T, 0, false);
-    FZ_LAUNCH_CHECK();
-    k_seg_time_bucket<512, 2048><<<unsigned(S < 4096 ? S : 4096), 512, 0, st(1)>>>(T, 1024, false);
-    FZ_LAUNCH_CHECK();
-    k_seg_time_bucket<1024, 4096><<<unsigned(S < 2048 ? S : 2048), 1024, 0, st(2)>>>(T, 2048, false);
+    // (FZ_TS_CLASSES, experiment builds: 1 - the 512-thread class takes every segment of <= 2048
+    // rows, 2 - the 1024-thread class every segment of <= 4096: fewer launches, fewer rows per
+    // thread idle... or not)
+    if (FZ_TS_CLASSES == 0) {
+        k_seg_time_bucket<256, 1024><<<unsigned(S < 16384 ? S : 16384), 256, 0, st(0)>>>(T, 0, false);
+        FZ_LAUNCH_CHECK();
+    }
+    if (FZ_TS_CLASSES <= 1) {
+        k_seg_time_bucket<512, 2048><<<unsigned(S < 4096 ? S : 4096), 512, 0, st(1)>>>(T, FZ_TS_CLASSES ? 0 : 1024,
+                                                                                        false);
+        FZ_LAUNCH_CHECK();
+    }
+    k_seg_time_bucket<1024, 4096><<<unsigned(S < 2048 ? S : 2048), 1024, 0, st(2)>>>(
+        T, FZ_TS_CLASSES == 2 ? 0 : 2048, false);
     FZ_LAUNCH_CHECK();
     // (a workgroup per CU at most; fewer when the tables are too small to hold many long segments)
     const int64_t g16 = ntot / 16384 < 8 ? 8 : (ntot / 16384 > 256 ? 256 : ntot / 16384);
@@ -1229,7 +1274,7 @@ struct StoreSink {
     }
 };
 
-void store_eligibility(fz_ctx *c);  // fz_rq1.hip
+void store_eligibility(fz_ctx *c, bool zeroed);  // fz_rq1.hip
 
 // Point s.t at the sorted copies of every column (row ids become positions; perm keeps the
 // caller's ids).
@@ -1275,22 +1320,50 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     const int64_t P = s.P;
     const int pbits = bits_for(uint64_t(P > 0 ? P - 1 : 0));
 
-    // the issue-number range (RQ1's ROW_NUMBER dedup key) as per-workgroup partials, read back with
-    // the views' counters below (the build's one host round trip)
+    // ONE fill for the whole build: the eligibility counters, the merge-sort counters and the prefix
+    // sorts' digit totals (big3), the time sort's bigflag arrays (0) and source positions
+    // (kGathered) - sized from the host-known table shapes
+    const int tpbits[3] = {pbits + 2, pbits, pbits};
+    const int64_t tn[3] = {t->n_builds, t->n_cov, t->n_issues};
+    int64_t S_all = 0;
+    for (int k = 0; k < 3; ++k) S_all += tn[k] > 0 ? (int64_t(1) << tpbits[k]) : 0;
+    // big3[k]: rows of table k in segments left to the merge sort, big3[3 + k]: the longest such
+    // segment, big3[6 + k]: rows whose columns the long bucket class gathered (one zeroing for all)
+    unsigned long long *big3 = c->arena.get<unsigned long long>(9 + kRadixTabHistWords);
+    unsigned long long *hist0 = big3 + 9;  // the prefix sorts' digit totals
+    uint8_t *tflags = c->arena.get<uint8_t>(S_all > 0 ? S_all : 1);
+    uint32_t *spos[3];
+    for (int k = 0; k < 3; ++k) spos[k] = tn[k] > 0 ? c->arena.get<uint32_t>(tn[k]) : nullptr;
+    {
+        s.n_elig.ensure<int64_t>(2);
+        const int64_t pf = FZ_SPOS_PREFILL ? 4 : 0;
+        fill_batch(c, {{s.n_elig.ptr, 16, 0},
+                       {big3, (9 + kRadixTabHistWords) * 8, 0},
+                       {tflags, S_all, 0},
+                       {spos[0], tn[0] * pf, 0xff},
+                       {spos[1], tn[1] * pf, 0xff},
+                       {spos[2], tn[2] * pf, 0xff}});
+    }
     // the eligibility histogram reads only the input coverage table: on the third store-build
-    // helper beside the prologue and the prefix sorts (joined with the helpers after them, and
-    // again before the build returns)
+    // helper beside the prefix sorts (joined with the helpers after them, and again before the
+    // build returns)
     bool elig_aside = store_helpers(c) >= 3;
     if (elig_aside) {
         store_fork(c);
-        store_eligibility(c->helpers[2]);
+        store_eligibility(c->helpers[2], true);
     } else {
-        store_eligibility(c);
+        store_eligibility(c, true);
     }
+    // the issue-number range (RQ1's ROW_NUMBER dedup key) as per-workgroup partials, read back with
+    // the views' counters below (the build's one host round trip) - computed by extra workgroups of
+    // the prefix sorts' histogram launch
     const int pblk = int(grid_for(t->n_issues, kBlock * 16, kProBlocks));
     int64_t *ppart = c->arena.get<int64_t>(4 * pblk);
-    k_store_prologue<<<pblk, kBlock, 0, c->stream>>>(t->i_number, t->n_issues, ppart);
-    FZ_LAUNCH_CHECK();
+    RadixSideMinMax side;
+    side.src = t->i_number;
+    side.n = t->n_issues;
+    side.part = ppart;
+    side.blocks = unsigned(pblk);
 
     // the three tables: (prefix = [type|]project) LSD passes, then each segment sorted by time in LDS
     struct Tab {
@@ -1328,11 +1401,6 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         gi.src[0] = t->i_number, gi.dst[0] = s.si_number.ensure<int64_t>(ni), gi.size[0] = 8;
         gi.src[1] = t->i_status, gi.dst[1] = s.si_status.ensure<uint8_t>(ni), gi.size[1] = 1;
     }
-    // big3[k]: rows of table k in segments left to the merge sort, big3[3 + k]: the longest such
-    // segment, big3[6 + k]: rows whose columns the long bucket class gathered (one zeroing for all)
-    unsigned long long *big3 = c->arena.get<unsigned long long>(9 + kRadixTabHistWords);
-    unsigned long long *hist0 = big3 + 9;  // the prefix sorts' digit totals (zeroed with the counters)
-    dev_fill(c, big3, 0, (9 + kRadixTabHistWords) * 8);
     PrefixSorted pss[3];
     TableIn tin[3];
     for (int k = 0; k < 3; ++k) {
@@ -1340,8 +1408,8 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
         tin[k] = TableIn{b.n, b.pre, b.pbits_total, b.time, b.tm->ensure<int64_t>(b.n), b.pr->ensure<uint32_t>(b.n),
                          gcs[k], big3 + k};
     }
-    prefix_sort_tables(c, tin, pss, hist0);
-    time_sort_tables(c, pss);
+    prefix_sort_tables(c, tin, pss, hist0, spos, &side);
+    time_sort_tables(c, pss, tflags);
     // the views (per-project ranges of the sorted tables): their offsets, longest segments and row
     // counts off the prefix offsets - builds' prefix is type << pbits | project (Fuzzing 0, Coverage 1)
     ViewSrc vs;
@@ -1368,8 +1436,9 @@ void store_build(fz_ctx *c, const fz_tables *t, fz_store_stats *stats) {
     FZ_HIP(hipEventRecord(c->ev_readback, c->stream));
     // the gather of the short classes' rows, launched before the host reads the counters (rows of
     // segments left to the long-segment pass / merge sort are marked kGathered: skipped here); the
-    // host's round trip overlaps it
-    gather_tables(c, pss);
+    // host's round trip overlaps it.  (With the direct short classes every bucket-sorted row's
+    // columns are written already: no gather unless the merge sort runs, below.)
+    if (!(kTsDirect && FZ_SPOS_PREFILL)) gather_tables(c, pss);
 #if FZ_SPIN_READBACK
     // spin on the event rather than a blocking wait: the analyses' launches follow this read-back,
     // and a blocking wait's wake-up latency idles the GPU after the gather
