@@ -214,9 +214,11 @@ def main():
                 eng.set_store_helpers(lch[:4])  # (idle while the store builds: the step joins them first)
         rq1_shard = par.GpuRQ1Shard(skids.get("rq1", eng), M)
         rq3_shard = par.GpuRQ3Shard(skids.get("rq3", eng))
-        rq2c_shard = par.GpuRQ2CountShard(skids.get("rq2_count", eng), cont)
+        # (one rank without a cut project: the local kernels group the values by session themselves)
+        smaj = world == 1 and cont < 0
+        rq2c_shard = par.GpuRQ2CountShard(skids.get("rq2_count", eng), cont, session_major=smaj)
         rq4a_shard = par.GpuRQ4aShard(skids.get("rq4a", eng), M)
-        rq4b_shard = par.GpuRQ4bShard(skids.get("rq4b", eng), cont)
+        rq4b_shard = par.GpuRQ4bShard(skids.get("rq4b", eng), cont, session_major=smaj)
         elig_ctl = par.GpuEligibility(eng)
         rq2a_shard = par.GpuRQ2AddShard(skids.get("rq2_add", eng))
         if args.strong:

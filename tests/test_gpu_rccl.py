@@ -23,7 +23,7 @@ ORDER = ("rq3", "rq4b", "rq2_count", "rq1", "rq4a", "rq2_add")
 GROUPS = (("rq3",), ("rq4b",), ("rq2_count",), ("rq1", "rq4a", "rq2_add"))
 
 
-def _worker(rank, port, errfile):
+def _worker(rank, port, errfile, session_major=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
@@ -31,7 +31,7 @@ def _worker(rank, port, errfile):
     try:
         assert dist.get_backend() == "nccl"
         _collectives()
-        _six_drivers()
+        _six_drivers(session_major)
     except BaseException:
         import traceback
         with open(f"{errfile}.{rank}", "w") as f:
@@ -72,7 +72,7 @@ def _collectives():
     assert par.agree_max(17, dev) == 17
 
 
-def _six_drivers():
+def _six_drivers(session_major=False):
     import torch.distributed as dist
     from gpu_common import assert_same
     from test_parallel import rq2_add_result
@@ -100,8 +100,10 @@ def _six_drivers():
     eng.set_store_helpers(lch)
     pg = dist.new_group(backend="nccl")
     shards = {"rq1": par.GpuRQ1Shard(kids["rq1"], M), "rq3": par.GpuRQ3Shard(kids["rq3"]),
-              "rq2_count": par.GpuRQ2CountShard(kids["rq2_count"]), "rq4a": par.GpuRQ4aShard(kids["rq4a"], M),
-              "rq4b": par.GpuRQ4bShard(kids["rq4b"]), "rq2_add": par.GpuRQ2AddShard(kids["rq2_add"])}
+              "rq2_count": par.GpuRQ2CountShard(kids["rq2_count"], session_major=session_major),
+              "rq4a": par.GpuRQ4aShard(kids["rq4a"], M),
+              "rq4b": par.GpuRQ4bShard(kids["rq4b"], session_major=session_major),
+              "rq2_add": par.GpuRQ2AddShard(kids["rq2_add"])}
     graphs = []
 
     def step():
@@ -182,10 +184,13 @@ def _six_drivers():
     eng.close()
 
 
-def test_rccl_world1_six_drivers_on_streams(tmp_path):
+@pytest.mark.parametrize("session_major", [False, True])
+def test_rccl_world1_six_drivers_on_streams(tmp_path, session_major):
+    """session_major: RQ2 count / RQ4b as bench.py runs them on one rank (values grouped by session
+    in the recorded local phase, no run exchange); else the project-major exchange path."""
     errfile = str(tmp_path / "err")
     try:
-        mp.spawn(_worker, args=(_free_port(), errfile), nprocs=1, join=True)
+        mp.spawn(_worker, args=(_free_port(), errfile, session_major), nprocs=1, join=True)
     except Exception:
         msg = open(f"{errfile}.0").read() if os.path.exists(f"{errfile}.0") else ""
         raise AssertionError(msg or "worker failed")

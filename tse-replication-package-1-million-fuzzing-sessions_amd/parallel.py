@@ -456,10 +456,27 @@ def all_gather(x):
     return outs
 
 
+def _small(vals, dtype, device):
+    """A few host numbers as a device tensor without a blocking copy: staged in pinned memory (torch's
+    caching host allocator) and copied asynchronously on the current stream - torch.tensor(...,
+    device=) from pageable memory waits for the stream's earlier work to finish first."""
+    import torch
+    t = torch.tensor(vals, dtype=dtype)
+    if device is None or torch.device(device).type == "cpu":
+        return t
+    return t.pin_memory().to(device, non_blocking=True)
+
+
+def _upload(a: np.ndarray, device):
+    """A host numpy array to the device asynchronously (pinned staging, as _small)."""
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(device, non_blocking=True)
+
+
 def all_gather_v(x):
     """All-gather of a 1-D tensor whose length differs per rank -> list (rank order) of tensors."""
     import torch
-    n = torch.tensor([x.numel()], dtype=torch.int64, device=x.device)
+    n = _small([x.numel()], torch.int64, x.device)
     sizes = [int(v) for v in torch.cat(all_gather(n)).tolist()]
     m = max(max(sizes), 1)
     buf = torch.zeros(m, dtype=x.dtype, device=x.device)
@@ -475,7 +492,7 @@ def all_to_all_v(x, send_counts, recv_counts=None):
     dist = _dist()
     world = dist.get_world_size()
     if recv_counts is None:
-        sc = torch.tensor([int(v) for v in send_counts], dtype=torch.int64, device=x.device)
+        sc = _small([int(v) for v in send_counts], torch.int64, x.device)
         rc = torch.cat(all_gather(sc)).reshape(world, world)[:, dist.get_rank()]
         recv_counts = rc.tolist()
     recv = [int(v) for v in recv_counts]
@@ -925,7 +942,7 @@ def _series_tests_cut(shard, p, holders, piece, base, n, rank, dev):
         m = val.numel()
         ns = min(256, m)
         samp = val[torch.div(torch.arange(ns, device=val.device) * m, ns, rounding_mode="floor")]
-        head = torch.tensor([float(m)], dtype=f64, device=val.device)
+        head = _small([float(m)], f64, val.device)
     else:
         val = torch.zeros(0, dtype=f64, device=dev)
         gidx = torch.zeros(0, dtype=torch.int64, device=dev)
@@ -951,7 +968,7 @@ def _series_tests_cut(shard, p, holders, piece, base, n, rank, dev):
         sd = torch.as_tensor(spl, dtype=f64, device=val.device)
         bnd = torch.searchsorted(val, sd, right=True) if len(spl) else torch.zeros(0, dtype=torch.int64, device=dev)
         bnd = torch.cat([torch.zeros(1, dtype=torch.int64, device=val.device), bnd.to(torch.int64),
-                         torch.tensor([val.numel()], dtype=torch.int64, device=val.device)])
+                         _small([val.numel()], torch.int64, val.device)])
     else:
         bnd = torch.zeros(k + 1, dtype=torch.int64, device=dev)
     allb = host_many(*all_gather(bnd))                 # [world][k + 1]
@@ -1014,7 +1031,7 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     pcnt = part.get("piece_counts")
     if pcnt is None or cont < 0:
         pcnt = torch.zeros(3, dtype=torch.int64, device=dev)
-    info = torch.cat([torch.tensor([cont, lo, hi], dtype=torch.int64, device=dev), pcnt.to(torch.int64), nl])
+    info = torch.cat([_small([cont, lo, hi], torch.int64, dev), pcnt.to(torch.int64), nl])
     if world > 1:
         got = all_gather_cols(pc)
         pc = [torch.cat([got[r][j] for r in range(world)]) for j in range(len(pc))]
@@ -1039,7 +1056,15 @@ def rq2_count_sharded(shard, rank: int, world: int, lo: int, hi: int, gather_val
     own = _owner_cuts(runs.n, world, M)
     a, b = own[rank]
     S = b - a
-    vals, goffs = _exchange_runs(shard, runs, rank, own, vals_a, vals_b)
+    if getattr(shard, "session_major", False):
+        # one rank, no leading piece (a one-GPU run of the sharded step): the local kernels wrote the
+        # values session-major with their offsets (the single-table transpose, in the recorded local
+        # phase) - no runs, no host-built transpose after the read
+        if world != 1 or cont >= 0:
+            raise ValueError("rq2_count_sharded: session-major shard output serves one rank without a cut project")
+        vals, goffs = vals_a[:int(runs.n.sum())], part["session_offsets"][:M + 1]
+    else:
+        vals, goffs = _exchange_runs(shard, runs, rank, own, vals_a, vals_b)
     st = shard.session_stats_grouped(vals, goffs, S, len(proj["eligible"]))
     # sessions with >= 100 values: a prefix, as long as the 100th longest run (:390)
     srt = np.sort(runs.n)[::-1]
@@ -1183,6 +1208,55 @@ def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, f
         if world > 1:
             raise ValueError("rq4b_sharded: the rank's own project range (lo, hi) is needed at world > 1")
         lo, hi = 0, P
+    heads = None
+    if getattr(shard, "session_major", False):
+        # one rank, no leading piece (a one-GPU run of the sharded step): the local kernels grouped
+        # the values by (session, group) already (the single-table transpose, in the recorded local
+        # phase) - no runs, no host-built transpose; one read of the sizes
+        if world != 1 or cont >= 0:
+            raise ValueError("rq4b_sharded: session-major shard output serves one rank without a cut project")
+        head = torch.stack([counts[RQ4B_SESSIONS], counts[RQ4B_VALUES], counts[RQ4B_DELTA_PROJECTS],
+                            counts[RQ4B_INIT_G2], counts[RQ4B_INIT_G1]])
+        m_loc, nv, nd, n2, n1 = (int(v) for v in host_many(head)[0])
+        heads = (nd, n2, n1)
+        M = m_loc
+        a, b = 0, M
+        S = M
+        st = shard.session_stats_grouped(part["trend_values"][:nv], part["trend_offsets"][:2 * M + 1], S, P)
+    else:
+        a = b = S = M = None
+    if heads is None:
+        M, a, b, S, st = _rq4b_exchange_stats(shard, part, rank, world, lo, hi, cont, counts, P, dev)
+    # per-session rows (c2, c1, g2 quartiles, g1 quartiles, p_bm) of every owner, session order
+    cols = [st["c2"][:S], st["c1"][:S]] + [st["g2_q"][:3 * S].reshape(S, 3)[:, j] for j in range(3)] + \
+        [st["g1_q"][:3 * S].reshape(S, 3)[:, j] for j in range(3)] + [st["p_bm"][:S]]
+    own_cols = cols
+    if world > 1:
+        if host_sessions:
+            got = all_gather_cols(cols)
+        else:
+            # the trends read sessions with both groups >= 100 (:849-860): a prefix of length L, the
+            # shorter of the two groups' 100th longest series - each owner's part of it gathered, the
+            # per-session rows stay on their owners
+            runs_n, group = shard._last_runs
+
+            def hundredth(x):
+                x = np.sort(x)[::-1]
+                return int(x[99]) if len(x) >= 100 else 0
+            L = min(hundredth(runs_n[group == 0]), hundredth(runs_n[group == 1]), M)
+            kk = max(0, min(b, L) - a)
+            got = all_gather_cols([x[:kk] for x in cols])
+        cols = [torch.cat([g[j] for g in got]) for j in range(len(cols))]
+    return _rq4b_finish(shard, part, world, counts, cols, own_cols, st, S, M, a, b, heads, finish_later,
+                        host_sessions)
+
+
+def _rq4b_exchange_stats(shard, part, rank, world, lo, hi, cont, counts, P, dev):
+    """rq4b_sharded's project-major exchange: runs from the gathered series lengths, sent to the
+    sessions' owners and transposed by (session, group) there, the owner's session statistics ->
+    (M, a, b, S, stats).  (shard._last_runs: the global run lengths and groups, for the prefix the
+    trends read.)"""
+    import torch
     toffs = part["trend_offsets"][:P + 1]
     # (own ranges gathered into the global axis; one rank keeps its columns over the global axis)
     nloc = (toffs[1:] - toffs[:-1])[lo:hi] if world > 1 else toffs[1:] - toffs[:-1]
@@ -1193,7 +1267,7 @@ def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, f
     pcnt = part.get("piece_counts")
     if pcnt is None or cont < 0:
         pcnt = torch.zeros(3, dtype=torch.int64, device=dev)
-    info = torch.cat([torch.tensor([cont, lo, hi], dtype=torch.int64, device=dev), pcnt.to(torch.int64)])
+    info = torch.cat([_small([cont, lo, hi], torch.int64, dev), pcnt.to(torch.int64)])
     if world > 1:
         got = all_gather_cols([member, nloc])
         member = torch.cat([g[0] for g in got])
@@ -1212,31 +1286,23 @@ def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, f
     own = _owner_cuts(runs.n, world, M) if world > 1 else [(0, M)]
     group = np.where((member_h & 2) != 0, 0, 1)  # G2 -> segment 2s, G1 -> 2s + 1
     vals, goffs = _exchange_runs(shard, runs, rank, own, vals_a, vals_b, group_of=group)
+    shard._last_runs = (runs.n, group)
     a, b = own[rank]
     S = b - a
-    st = shard.session_stats_grouped(vals, goffs, S, P)
-    # per-session rows (c2, c1, g2 quartiles, g1 quartiles, p_bm) of every owner, session order
-    cols = [st["c2"][:S], st["c1"][:S]] + [st["g2_q"][:3 * S].reshape(S, 3)[:, j] for j in range(3)] + \
-        [st["g1_q"][:3 * S].reshape(S, 3)[:, j] for j in range(3)] + [st["p_bm"][:S]]
-    own_cols = cols
-    if world > 1:
-        if host_sessions:
-            got = all_gather_cols(cols)
-        else:
-            # the trends read sessions with both groups >= 100 (:849-860): a prefix of length L, the
-            # shorter of the two groups' 100th longest series - each owner's part of it gathered, the
-            # per-session rows stay on their owners
-            def hundredth(x):
-                x = np.sort(x)[::-1]
-                return int(x[99]) if len(x) >= 100 else 0
-            L = min(hundredth(runs.n[group == 0]), hundredth(runs.n[group == 1]), M)
-            kk = max(0, min(b, L) - a)
-            got = all_gather_cols([x[:kk] for x in cols])
-        cols = [torch.cat([g[j] for g in got]) for j in range(len(cols))]
+    return M, a, b, S, shard.session_stats_grouped(vals, goffs, S, P)
+
+
+def _rq4b_finish(shard, part, world, counts, cols, own_cols, st, S, M, a, b, heads, finish_later, host_sessions):
+    """rq4b_sharded after the per-session statistics: deltas, initial samples, the tail, the one
+    result copy."""
+    import torch
     # coverage deltas: columns of every rank (CSV row, 7 pre, 7 post), put in corpus CSV order below
-    nd, n2, n1 = (int(v) for v in host_many(torch.stack([part["counts"][RQ4B_DELTA_PROJECTS],
-                                                          part["counts"][RQ4B_INIT_G2],
-                                                          part["counts"][RQ4B_INIT_G1]]))[0])
+    if heads is not None:
+        nd, n2, n1 = heads
+    else:
+        nd, n2, n1 = (int(v) for v in host_many(torch.stack([part["counts"][RQ4B_DELTA_PROJECTS],
+                                                              part["counts"][RQ4B_INIT_G2],
+                                                              part["counts"][RQ4B_INIT_G1]]))[0])
     proj = part["delta_order"][:nd]
     pre = part["pre_cov"][:7 * nd].reshape(7, nd)
     post = part["post_cov"][:7 * nd].reshape(7, nd)
@@ -1247,7 +1313,7 @@ def rq4b_sharded(shard, rank: int, world: int, lo: int = None, hi: int = None, f
     # initial coverage: samples in project order, tests once
     x, y = part["init_g2"][:n2], part["init_g1"][:n1]
     if world > 1:  # both samples in one variable gather: [len(x), x, y] per rank
-        nx = torch.tensor([x.numel()], dtype=torch.int64, device=x.device)
+        nx = _small([x.numel()], torch.int64, x.device)
         parts = all_gather_v(torch.cat([nx, x.contiguous().view(torch.int64), y.contiguous().view(torch.int64)]))
         heads = host_many(torch.stack([q[0] for q in parts]))[0]
         xs, ys = [], []
@@ -1448,7 +1514,7 @@ class _GpuExchange:
         table += dst[:, None]
         cuts = np.array([o[0] for o in own] + [own[-1][1]], np.int64)
         h = np.concatenate([desc.reshape(-1), in_off, cuts, table.reshape(-1)])
-        d = torch.from_numpy(h).to(eng.dev, non_blocking=False)
+        d = _upload(h, eng.dev)
         o1 = desc.size
         o2 = o1 + R
         o3 = o2 + W + 1
@@ -1472,8 +1538,8 @@ class _GpuExchange:
             raise ValueError("transpose: runs exceed the values or the session range")
         out = torch.empty(max(n, 1), dtype=torch.float64, device=eng.dev)
         offs = torch.empty(max(S, 1) * G + 1, dtype=torch.int64, device=eng.dev)
-        ro = torch.from_numpy(np.ascontiguousarray(roffs, np.int64)).to(eng.dev)
-        gd = torch.from_numpy(np.ascontiguousarray(grp, np.uint8)).to(eng.dev) if G == 2 and R else None
+        ro = _upload(np.asarray(roffs, np.int64), eng.dev)
+        gd = _upload(np.asarray(grp, np.uint8), eng.dev) if G == 2 and R else None
         vals = vals.contiguous()
         P = lambda t: C.c_void_p(t.data_ptr()) if t is not None and t.numel() else None  # noqa: E731
         E._check(eng.lib, eng.lib.fz_transpose_runs(eng.ctx, P(vals), P(ro), P(gd), R, G, S, n, P(out), P(offs)))
@@ -1508,19 +1574,24 @@ class GpuRQ2CountShard(_GpuExchange):
     leading piece of a cut project, the exchange primitives, fz_rq2_session_stats_grouped,
     fz_rq2_count_tail)."""
 
-    def __init__(self, eng, cont: int = -1):
+    def __init__(self, eng, cont: int = -1, session_major: bool = False):
+        """session_major: (one rank, no cut project) the local kernels write the values session-major
+        (the single-table transpose) and rq2_count_sharded skips the run exchange."""
         import ctypes as C
         from . import engine as E
         from .rq import compute
         self.E, self.C, self.eng, self.cont = E, C, eng, int(cont)
+        if session_major and self.cont >= 0:
+            raise ValueError("GpuRQ2CountShard: a leading piece needs the project-major output")
+        self.session_major = bool(session_major)
         self.bufs = compute.rq2_count_buffers(eng)
 
     pre = False  # launch() already enqueued this step's local kernels (a recorded local phase)
 
     def launch(self):
         E, C, eng, b = self.E, self.C, self.eng, self.bufs
-        E._check(eng.lib, eng.lib.fz_rq2_count_ex(eng.ctx, E.FZ_RQ2C_SKIP_SESSION_STATS | E.FZ_RQ2C_PROJECT_MAJOR,
-                                                  C.byref(b.out)))
+        flags = E.FZ_RQ2C_SKIP_SESSION_STATS | (0 if self.session_major else E.FZ_RQ2C_PROJECT_MAJOR)
+        E._check(eng.lib, eng.lib.fz_rq2_count_ex(eng.ctx, flags, C.byref(b.out)))
         if self.cont >= 0:
             self._piece(E.FZ_PIECE_RQ2)
 
@@ -1532,6 +1603,7 @@ class GpuRQ2CountShard(_GpuExchange):
         out = {k: getattr(b, k) for k in RQ2C_PROJECT_COLS}
         out["null_lines"] = b.counts[E.RQ2C_NULL_LINES:E.RQ2C_NULL_LINES + 1]
         out["values"] = b.session_values
+        out["session_offsets"] = b.session_offsets
         if self.cont >= 0:
             out["piece_values"], out["piece_counts"] = self._pv, self._pc
         return out
@@ -1753,19 +1825,23 @@ class GpuRQ4bShard(_GpuExchange):
     """RQ4b of one rank on its engine (fz_rq4b_ex project-major, fz_piece_values for a leading piece
     of a cut project, the exchange primitives, fz_rq4b_session_stats_grouped, fz_rq4b_tail)."""
 
-    def __init__(self, eng, cont: int = -1):
+    def __init__(self, eng, cont: int = -1, session_major: bool = False):
+        """session_major: as GpuRQ2CountShard (values grouped by (session, group) locally)."""
         import ctypes as C
         from . import engine as E
         from .rq import compute
         self.E, self.C, self.eng, self.cont = E, C, eng, int(cont)
+        if session_major and self.cont >= 0:
+            raise ValueError("GpuRQ4bShard: a leading piece needs the project-major output")
+        self.session_major = bool(session_major)
         self.bufs = compute.rq4b_buffers(eng, shard=True)
 
     pre = False  # launch() already enqueued this step's local kernels (a recorded local phase)
 
     def launch(self):
         E, C, eng, b = self.E, self.C, self.eng, self.bufs
-        E._check(eng.lib, eng.lib.fz_rq4b_ex(eng.ctx, C.byref(eng.groups),
-                                             E.FZ_RQ4B_SKIP_SESSION_STATS | E.FZ_RQ4B_PROJECT_MAJOR, C.byref(b.out)))
+        flags = E.FZ_RQ4B_SKIP_SESSION_STATS | (0 if self.session_major else E.FZ_RQ4B_PROJECT_MAJOR)
+        E._check(eng.lib, eng.lib.fz_rq4b_ex(eng.ctx, C.byref(eng.groups), flags, C.byref(b.out)))
         if self.cont >= 0:
             self._piece(E.FZ_PIECE_RQ4B)
 
