@@ -2477,11 +2477,258 @@ __global__ __launch_bounds__(256) void k_qs_sort_mid(const double *__restrict__ 
     if (tid == 0 && ge100) atomic_add_i64(a.d_ge100, ge100);
 }
 
+// The mid and 1025-2048 lists by ONE WAVE per segment, no workgroup barrier: the segment's keys
+// in registers (32 per lane), a value-bucket histogram in the wave's own LDS slice, the bucket starts
+// by one wave scan, each wanted rank's bucket found by a binary search (one lane per rank) and
+// ranked by the wave - a bucket of more than 64 values is narrowed by re-histogramming its key
+// interval (as k_qs_block).  Eight independent waves per workgroup, up to four workgroups per CU:
+// sessions overlap their latencies instead of queueing behind each other's barriers (k_qs_block
+// held a 256-thread workgroup through ~10 barrier rounds per session).
+constexpr int kQsWaveBlock = 512, kQsWaveNB = 1024;
+// waves per SIMD the register budget allows: 2 (a 4-wave budget of 128 VGPRs spilled 100 / 316 B
+// per lane in the 1024- / 2048-value classes)
+template <int MAXN>
+struct QsWaveWpe {
+    static constexpr int v = 2;
+};
+__device__ __forceinline__ void qs_wave_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+template <int MAXN>
+__global__ __launch_bounds__(kQsWaveBlock) __attribute__((amdgpu_waves_per_eu(QsWaveWpe<MAXN>::v, QsWaveWpe<MAXN>::v))) void k_qs_wave(const double *__restrict__ src,
+                                                          const int64_t *__restrict__ offs,
+                                                          const int32_t *__restrict__ list_a,
+                                                          const int64_t *__restrict__ d_na,
+                                                          const int32_t *__restrict__ list_b,
+                                                          const int64_t *__restrict__ d_nb, QsArgs a) {
+    constexpr int IPT = MAXN / kWave, WPB = kQsWaveBlock / kWave, NBW = kQsWaveNB, BPL = NBW / kWave;
+    static_assert(MAXN % kWave == 0 && NBW % kWave == 0, "qs wave shape");
+    __shared__ uint32_t s_cnt[WPB][NBW + 1];
+    __shared__ uint64_t s_list[WPB][64];
+    __shared__ uint32_t s_fill[WPB];
+    const int w = wave_id(), lane = lane_id();
+    uint32_t *const cnt = s_cnt[w];
+    uint64_t *const lst = s_list[w];
+    const int64_t na = *d_na, ntot = na + (d_nb ? *d_nb : 0);
+    const int nt = 2 + 2 * a.nq;
+    int64_t ge100 = 0;
+    for (int64_t it = int64_t(blockIdx.x) * WPB + w; it < ntot; it += int64_t(gridDim.x) * WPB) {
+        const int64_t s = it < na ? list_a[it] : list_b[it - na];
+        const int64_t b = offs[s];
+        const int n = int(offs[s + 1] - b);
+        uint64_t K[IPT];
+        DD acc{0.0, 0.0};
+        uint64_t lo = ~0ull, hi = 0ull;
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const int i = lane + m * kWave;
+            const double x = i < n ? src[b + i] : 0.0;
+            K[m] = i < n ? f64_key(x) : ~0ull;
+            if (i < n) {
+                acc = dd_add_d(acc, x);
+                lo = K[m] < lo ? K[m] : lo;
+                hi = K[m] > hi ? K[m] : hi;
+            }
+        }
+        lo = wave_min(lo);
+        hi = wave_max(hi);
+        acc = wave_dd_sum(acc);
+        uint64_t mine = lo;  // lane t < nt: the key of target t
+        if (lo != hi) {
+            const int nbk = n < NBW ? n : NBW;
+            const double vlo = f64_from_key(lo), vhi = f64_from_key(hi);
+            const bool vlin = isfinite(vlo) && isfinite(vhi) && isfinite(vhi - vlo) && vhi > vlo;
+            const double vsc = vlin ? double(nbk) / (vhi - vlo) : 0.0;
+            const double ksc = double(nbk) / (double(hi - lo) + 1.0);
+            auto kbucket = [](uint64_t key, uint64_t klo, double sc, int nb) -> uint32_t {
+                const uint32_t q = uint32_t(double(key - klo) * sc);
+                return q < uint32_t(nb) ? q : uint32_t(nb - 1);
+            };
+            // the first level linear in VALUE when the range is finite, else in key (as k_qs_block)
+            auto bucket1 = [&](uint64_t key) -> uint32_t {
+                if (!vlin) return kbucket(key, lo, ksc, nbk);
+                const double q = (f64_from_key(key) - vlo) * vsc;
+                return q < double(nbk - 1) ? uint32_t(q) : uint32_t(nbk - 1);
+            };
+            for (int j = lane; j <= nbk; j += kWave) cnt[j] = 0u;
+            qs_wave_sync();
+#pragma unroll
+            for (int m = 0; m < IPT; ++m)
+                if (lane + m * kWave < n) atomicAdd(&cnt[bucket1(K[m])], 1u);
+            qs_wave_sync();
+            // bucket starts: lane l owns buckets [l * BPL, l * BPL + BPL)
+            auto wave_starts = [&](int nb) {
+                uint32_t cb[BPL], sum = 0;
+#pragma unroll
+                for (int e = 0; e < BPL; ++e) {
+                    const int j = lane * BPL + e;
+                    cb[e] = j < nb ? cnt[j] : 0u;
+                    sum += cb[e];
+                }
+                uint32_t run = wave_incl_scan(sum) - sum;
+                qs_wave_sync();
+#pragma unroll
+                for (int e = 0; e < BPL; ++e) {
+                    const int j = lane * BPL + e;
+                    if (j < nb) cnt[j] = run;
+                    run += cb[e];
+                }
+            };
+            wave_starts(nbk);
+            if (lane == 0) cnt[nbk] = uint32_t(n);
+            qs_wave_sync();
+            int tb = 0;
+            uint32_t toff = 0, tsz = 0;
+            if (lane < nt) {  // target `lane`'s bucket: the last start <= its rank
+                const uint32_t r = uint32_t(qs_rank(n, a, lane));
+                int l0 = 0, h0 = nbk - 1;
+                while (l0 < h0) {
+                    const int mid = (l0 + h0 + 1) >> 1;
+                    if (cnt[mid] <= r) l0 = mid;
+                    else h0 = mid - 1;
+                }
+                tb = l0;
+                toff = r - cnt[l0];
+                tsz = cnt[l0 + 1] - cnt[l0];
+            }
+            // rank `off` among the (<= 64) keys of the list: the wave's answer
+            auto rank_in_list = [&](int sz, uint32_t off) -> uint64_t {
+                const uint64_t e = lane < sz ? lst[lane] : ~0ull;
+                int rk = 0;
+                for (int j = 0; j < sz; ++j) {
+                    const uint64_t o = lst[j];
+                    rk += (o < e) || (o == e && j < lane);
+                }
+                const uint64_t hit = __ballot(lane < sz && rk == int(off));
+                return __shfl(e, hit ? __ffsll((long long)hit) - 1 : 0, 64);
+            };
+            int listed = -1;  // the first-level bucket the list holds
+            for (int t = 0; t < nt; ++t) {
+                const int bt = __shfl(tb, t, 64);
+                const uint32_t off = __shfl(toff, t, 64), sz = __shfl(tsz, t, 64);
+                uint64_t val;
+                if (sz <= 64) {
+                    if (bt != listed) {
+                        if (lane == 0) s_fill[w] = 0u;
+                        qs_wave_sync();
+#pragma unroll
+                        for (int m = 0; m < IPT; ++m)
+                            if (lane + m * kWave < n && bucket1(K[m]) == uint32_t(bt))
+                                lst[atomicAdd(&s_fill[w], 1u)] = K[m];
+                        qs_wave_sync();
+                        listed = bt;
+                    }
+                    val = rank_in_list(int(sz), off);
+                } else {
+                    // narrow the bucket's key interval until it holds <= 64 keys or one key
+                    listed = -1;
+                    uint64_t rlo = ~0ull, rhi = 0ull;
+#pragma unroll
+                    for (int m = 0; m < IPT; ++m)
+                        if (lane + m * kWave < n && bucket1(K[m]) == uint32_t(bt)) {
+                            rlo = K[m] < rlo ? K[m] : rlo;
+                            rhi = K[m] > rhi ? K[m] : rhi;
+                        }
+                    rlo = wave_min(rlo);
+                    rhi = wave_max(rhi);
+                    uint32_t r = off, cntv = sz;
+                    while (rlo != rhi && cntv > 64u) {
+                        const int nb2 = cntv < uint32_t(NBW) ? int(cntv) : NBW;
+                        const double sc2 = double(nb2) / (double(rhi - rlo) + 1.0);
+                        qs_wave_sync();
+                        for (int j = lane; j <= nb2; j += kWave) cnt[j] = 0u;
+                        qs_wave_sync();
+#pragma unroll
+                        for (int m = 0; m < IPT; ++m)
+                            if (lane + m * kWave < n && K[m] >= rlo && K[m] <= rhi)
+                                atomicAdd(&cnt[kbucket(K[m], rlo, sc2, nb2)], 1u);
+                        qs_wave_sync();
+                        // the sub-bucket holding rank r: the lane whose run covers r walks it
+                        uint32_t cb[BPL], sum = 0;
+#pragma unroll
+                        for (int e = 0; e < BPL; ++e) {
+                            const int j = lane * BPL + e;
+                            cb[e] = j < nb2 ? cnt[j] : 0u;
+                            sum += cb[e];
+                        }
+                        const uint32_t run = wave_incl_scan(sum) - sum;
+                        int sb = -1;
+                        uint32_t nr = 0, nc = 0;
+                        if (r >= run && r < run + sum) {
+                            uint32_t before = run;
+#pragma unroll
+                            for (int e = 0; e < BPL; ++e) {
+                                if (sb < 0 && r >= before && r < before + cb[e]) {
+                                    sb = lane * BPL + e;
+                                    nr = r - before;
+                                    nc = cb[e];
+                                }
+                                before += cb[e];
+                            }
+                        }
+                        const uint64_t who = __ballot(sb >= 0);
+                        const int src_lane = __ffsll((long long)who) - 1;
+                        sb = __shfl(sb, src_lane, 64);
+                        r = __shfl(nr, src_lane, 64);
+                        cntv = __shfl(nc, src_lane, 64);
+                        uint64_t nlo = ~0ull, nhi = 0ull;
+#pragma unroll
+                        for (int m = 0; m < IPT; ++m)
+                            if (lane + m * kWave < n && K[m] >= rlo && K[m] <= rhi &&
+                                kbucket(K[m], rlo, sc2, nb2) == uint32_t(sb)) {
+                                nlo = K[m] < nlo ? K[m] : nlo;
+                                nhi = K[m] > nhi ? K[m] : nhi;
+                            }
+                        rlo = wave_min(nlo);
+                        rhi = wave_max(nhi);
+                    }
+                    if (rlo == rhi) {
+                        val = rlo;
+                    } else {  // <= 64 keys in [rlo, rhi]
+                        qs_wave_sync();
+                        if (lane == 0) s_fill[w] = 0u;
+                        qs_wave_sync();
+#pragma unroll
+                        for (int m = 0; m < IPT; ++m)
+                            if (lane + m * kWave < n && K[m] >= rlo && K[m] <= rhi)
+                                lst[atomicAdd(&s_fill[w], 1u)] = K[m];
+                        qs_wave_sync();
+                        val = rank_in_list(int(cntv), r);
+                    }
+                }
+                if (lane == t) mine = val;
+            }
+            qs_wave_sync();  // (the next segment reuses the LDS slice)
+        }
+        // the targets' keys through the wave's list slice (lane t -> slot t), lane 0 writes
+        qs_wave_sync();
+        if (lane < nt) lst[lane] = mine;
+        qs_wave_sync();
+        if (lane == 0) {
+            auto get = [&](int64_t j) {
+                uint64_t r = lst[0];
+                for (int t = 0; t < nt; ++t)
+                    if (qs_rank(n, a, t) == j) r = lst[t];
+                return f64_from_key(r);
+            };
+            qs_write(a, s, n, acc.hi + acc.lo, get);
+            if (n >= 100) ++ge100;
+        }
+        qs_wave_sync();
+    }
+    if (lane == 0 && ge100) atomic_add_i64(a.d_ge100, ge100);
+}
+
 bool seg_qstats_ok(const Segs &sg) { return sg.len_bound() <= kQsMax; }
 #ifndef FZ_QS_BIG_BLOCK
 #define FZ_QS_BIG_BLOCK 512
 #endif
 constexpr int kQsBigBlock = FZ_QS_BIG_BLOCK;  // threads of the 2049 .. kQsMax class
+#ifndef FZ_QS_WAVE
+#define FZ_QS_WAVE 1  // the 65-2048 classes one wave per segment (0: k_qs_sort_mid / k_qs_block<256, 2048>)
+#endif
+constexpr bool kQsWave = FZ_QS_WAVE;
 
 void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_host, int nq, double *mean,
                 double *median, double *pcts, int64_t *d_ge100, double *mean2) {
@@ -2527,11 +2774,22 @@ void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_h
                                                                                       L.d_n + kQsTiny, a);
         FZ_LAUNCH_CHECK();
     }
-    if (lb > kTinySeg) {
+    if (kQsWave && lb > kTinySeg) {
+        // the mid (65-1024) and 1025-2048 lists one wave per segment (16 / 32 keys per lane)
+        constexpr int wpb = kQsWaveBlock / kWave;
+        k_qs_wave<1024><<<grid((caps[1] + wpb - 1) / wpb, 4096), kQsWaveBlock, 0, c->stream>>>(
+            vals, sg.offs, L.ids[1], L.d_n + 1, nullptr, nullptr, a);
+        FZ_LAUNCH_CHECK();
+        if (lb > 1024) {
+            k_qs_wave<2048><<<grid((caps[3] + wpb - 1) / wpb, 4096), kQsWaveBlock, 0, c->stream>>>(
+                vals, sg.offs, L.ids[3], L.d_n + 3, nullptr, nullptr, a);
+            FZ_LAUNCH_CHECK();
+        }
+    } else if (lb > kTinySeg) {
         k_qs_sort_mid<<<grid(caps[1], 8192), 256, 0, c->stream>>>(vals, sg.offs, L.ids[1], L.d_n + 1, a);
         FZ_LAUNCH_CHECK();
     }
-    if (lb > 1024) {
+    if (!kQsWave && lb > 1024) {
         // 1025 - 2048 values (a session of config 3's one-per-project values: 1,250 at an eighth of
         // the table): 256-thread workgroups with 8 values per thread - several per CU in flight, where
         // the 1024-thread class held one workgroup per CU with 15 of its 16 value slots per thread idle
