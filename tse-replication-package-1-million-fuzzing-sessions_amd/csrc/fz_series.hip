@@ -1102,10 +1102,16 @@ __global__ __launch_bounds__(kBlock) void k_bm_wave(const double *__restrict__ s
 // many (config 5's Zipf tail: one session per index of the longest project, ~10^7, nearly all
 // holding a handful of values): size-class lists - sessions of <= 8 values are never tested (both
 // halves need min_n >= 5), <= 64 one wave each, <= 4096 a 256-thread workgroup, longer 1024 threads.
+// (FZ_BM_FEW: up to this many sessions one 1024-thread workgroup each; more take the size classes -
+// a 1024-thread workgroup stages 96 KiB of LDS, one per CU: config 3L's eighth, 10,000 sessions of
+// ~1,000 values, queued 40 rounds deep behind it)
+#ifndef FZ_BM_FEW
+#define FZ_BM_FEW 2048
+#endif
 void bm_halves(fz_ctx *c, const double *sorted, const int64_t *offs2, const int64_t *soffs, int64_t M, int64_t n_cap,
                int64_t min_n, double *pbm) {
     if (M <= 0) return;
-    if (M <= kManySegs) {
+    if (M <= FZ_BM_FEW) {
         k_bm_halves_lds<1024, kBmLdsMax><<<unsigned(M < 4096 ? M : 4096), 1024, 0, c->stream>>>(
             sorted, offs2, M, nullptr, nullptr, min_n, pbm);
         FZ_LAUNCH_CHECK();
