@@ -111,6 +111,8 @@ def parse():
     ap.add_argument("--shard-of", type=int, default=1)
     ap.add_argument("--shard-rank", type=int, default=0)
     ap.add_argument("--cprofile", default="", help="write a cProfile summary of the timed steps (host time) here")
+    ap.add_argument("--project-major", action="store_true",
+                    help="one rank: RQ2 count / RQ4b through the project-major run exchange (as at N > 1)")
     return ap.parse_args()
 
 
@@ -215,7 +217,7 @@ def main():
         rq1_shard = par.GpuRQ1Shard(skids.get("rq1", eng), M)
         rq3_shard = par.GpuRQ3Shard(skids.get("rq3", eng))
         # (one rank without a cut project: the local kernels group the values by session themselves)
-        smaj = world == 1 and cont < 0
+        smaj = world == 1 and cont < 0 and not args.project_major
         rq2c_shard = par.GpuRQ2CountShard(skids.get("rq2_count", eng), cont, session_major=smaj)
         rq4a_shard = par.GpuRQ4aShard(skids.get("rq4a", eng), M)
         rq4b_shard = par.GpuRQ4bShard(skids.get("rq4b", eng), cont, session_major=smaj)

@@ -49,9 +49,13 @@ for s in ${STEPS:-full bench}; do
       C=${CONFIG:-c3L}
       for n in ${NS:-1 8}; do
         for r in $(seq 0 $((n - 1))); do
+          # (REPS runs per shard, each line kept; the summary takes each shard's fastest: one run can
+          # land on a slow moment of the box)
+          for k in $(seq 1 ${REPS:-1}); do
           timeout -k 10 300 python -u bench.py --config $C --steps 10 --warmup 2 --no-cpu-baseline --probe-steps 0 \
             --strong --force-sharded --shard-of $n --shard-rank $r > $O/${T}_sr.json 2> $O/${T}_sr.err || { tail -5 $O/${T}_sr.err; exit 1; }
           python3 -c "import json; d=json.loads([l for l in open('$O/${T}_sr.json') if l.startswith('{')][-1]); print('$C shard $r of $n', d['ms_per_step'], d['config']['rows_per_rank'], flush=True)" | tee -a $O/${T}_strong_$C.txt
+          done
         done
       done ;;
   esac
