@@ -1985,6 +1985,10 @@ struct QsArgs {
     int64_t *d_ge100;              // += segments of >= 100 values
 };
 constexpr int kQsMaxT = 2 * 8 + 2;  // ranks wanted per segment (two per percentile, two for the median)
+#ifndef FZ_QS_KEYS_GLOBAL
+#define FZ_QS_KEYS_GLOBAL 1
+#endif
+constexpr bool kQsKeysGlobal = FZ_QS_KEYS_GLOBAL;
 
 // rank t of the nt = 2 + 2 * nq order statistics a segment of n >= 1 values needs: statistics.median
 // reads ranks 0, 1; np_percentile_sorted(q[j]) reads ranks 2 + 2j, 3 + 2j (its prev / next index)
@@ -2139,7 +2143,11 @@ __global__ __launch_bounds__(kBlock) void k_qs_tiny(const double *__restrict__ s
 
 // The segments of one class list (at most MAXN values each), one workgroup each.
 template <int BS, int MAXN>
-__global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src, const int64_t *__restrict__ offs,
+struct QsBlockWpe {  // (the keys-from-global big class: a register budget for 4 waves per SIMD)
+    static constexpr int v = (MAXN > 2048 && kQsKeysGlobal) ? 3 : 1;
+};
+template <int BS, int MAXN>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(QsBlockWpe<BS, MAXN>::v))) void k_qs_block(const double *__restrict__ src, const int64_t *__restrict__ offs,
                                                  const int32_t *__restrict__ list, const int64_t *__restrict__ d_ln,
                                                  QsArgs a) {
     constexpr int NW = BS / kWave;
@@ -2147,8 +2155,12 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
     constexpr int NB = MAXN < 4096 ? MAXN : 4096;  // buckets
     constexpr int BPT = NB / BS > 0 ? NB / BS : 1;
     // (the 16384 class keeps the keys in LDS: 16 per thread in registers spilled - 31 VGPRs of
-    // scratch per lane, 2.6x the algorithmic bytes in HBM traffic at config 3)
-    constexpr bool KEYS_LDS = MAXN > 2048;
+    // scratch per lane, 2.6x the algorithmic bytes in HBM traffic at config 3; FZ_QS_KEYS_GLOBAL:
+    // it re-reads them from the (L2-resident) session instead - no 128 KiB key array, several
+    // workgroups per CU instead of one)
+    constexpr bool KEYS_GLOBAL = MAXN > 2048 && kQsKeysGlobal;
+    constexpr bool KEYS_LDS = MAXN > 2048 && !KEYS_GLOBAL;
+    constexpr int UF = KEYS_GLOBAL ? 4 : IPT;  // (keys re-read: a few loads in flight per thread, not 32)
     static_assert(MAXN % BS == 0 && NB % BS == 0, "qstats shape");
     __shared__ uint64_t s_keys[KEYS_LDS ? MAXN : 1];
     __shared__ uint32_t s_cnt[NB + 1];
@@ -2169,16 +2181,27 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
         const int64_t s = list[it];
         const int64_t b = offs[s];
         const int64_t n = offs[s + 1] - b;
-        uint64_t kr[KEYS_LDS ? 1 : IPT];
-        auto K = [&](int m) -> uint64_t & { return KEYS_LDS ? s_keys[tid + m * BS] : kr[m]; };
+        uint64_t kr[KEYS_LDS || KEYS_GLOBAL ? 1 : IPT];
+        auto K = [&](int m) -> uint64_t {
+            if constexpr (KEYS_GLOBAL) {
+                const int64_t i = tid + int64_t(m) * BS;
+                return i < n ? f64_key(src[b + i]) : 0ull;
+            } else {
+                return KEYS_LDS ? s_keys[tid + m * BS] : kr[m];
+            }
+        };
+        auto K_set = [&](int m, uint64_t v) {
+            if constexpr (KEYS_LDS) s_keys[tid + m * BS] = v;
+            else if constexpr (!KEYS_GLOBAL) kr[m] = v;
+        };
         uint64_t lo = ~0ull, hi = 0ull;
         DD acc{0.0, 0.0};
-#pragma unroll
+#pragma unroll UF
         for (int m = 0; m < IPT; ++m) {
             const int64_t i = tid + int64_t(m) * BS;
             const double x = i < n ? src[b + i] : 0.0;
             const uint64_t km = i < n ? f64_key(x) : 0ull;
-            K(m) = km;
+            K_set(m, km);
             if (i < n) {
                 acc = dd_add_d(acc, x);
                 lo = km < lo ? km : lo;
@@ -2222,7 +2245,7 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
             return q < double(nb - 1) ? uint32_t(q) : uint32_t(nb - 1);
         };
         if (lo != hi) {
-#pragma unroll
+#pragma unroll UF
             for (int m = 0; m < IPT; ++m)
                 if (tid + int64_t(m) * BS < n) atomicAdd(&s_cnt[bucket1(K(m))], 1u);
             __syncthreads();
@@ -2271,7 +2294,7 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
                 }
             }
             __syncthreads();
-#pragma unroll
+#pragma unroll UF
             for (int m = 0; m < IPT; ++m) {
                 if (tid + int64_t(m) * BS < n) {
                     const uint8_t slot = s_map[bucket1(K(m))];
@@ -2299,7 +2322,7 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
                 // the bucket's key interval [rlo, rhi] (a bucket = the values of one key interval)
                 const uint32_t tb = uint32_t(s_tb[t]);
                 uint64_t rlo = ~0ull, rhi = 0ull;
-#pragma unroll
+#pragma unroll UF
                 for (int m = 0; m < IPT; ++m)
                     if (tid + int64_t(m) * BS < n && bucket1(K(m)) == tb) {
                         rlo = K(m) < rlo ? K(m) : rlo;
@@ -2325,7 +2348,7 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
                     const double sc2 = double(nb2) / (double(rhi - rlo) + 1.0);
                     for (int j = tid; j <= nb2; j += BS) s_cnt[j] = 0u;
                     __syncthreads();
-#pragma unroll
+#pragma unroll UF
                     for (int m = 0; m < IPT; ++m)
                         if (tid + int64_t(m) * BS < n && K(m) >= rlo && K(m) <= rhi)
                             atomicAdd(&s_cnt[bucket(K(m), rlo, sc2, nb2)], 1u);
@@ -2358,7 +2381,7 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
                     __syncthreads();
                     const uint32_t sb = s_cnt[NB];
                     uint64_t nlo = ~0ull, nhi = 0ull;
-#pragma unroll
+#pragma unroll UF
                     for (int m = 0; m < IPT; ++m)
                         if (tid + int64_t(m) * BS < n && K(m) >= rlo && K(m) <= rhi && bucket(K(m), rlo, sc2, nb2) == sb) {
                             nlo = K(m) < nlo ? K(m) : nlo;
@@ -2388,7 +2411,7 @@ __global__ __launch_bounds__(BS) void k_qs_block(const double *__restrict__ src,
                 } else {  // <= 64 values in [rlo, rhi]: list them, one wave ranks them
                     if (tid == 0) s_fill[0] = 0u;
                     __syncthreads();
-#pragma unroll
+#pragma unroll UF
                     for (int m = 0; m < IPT; ++m)
                         if (tid + int64_t(m) * BS < n && K(m) >= rlo && K(m) <= rhi)
                             s_list[0][atomicAdd(&s_fill[0], 1u)] = K(m);
