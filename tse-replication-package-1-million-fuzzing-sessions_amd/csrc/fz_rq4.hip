@@ -552,10 +552,10 @@ void rq4b_session_stats_grouped(fz_ctx *c, const double *values, const int64_t *
     FZ_CHECK(2 * MM < (int64_t(1) << 32), "fz_rq4b_session_stats_grouped: too many sessions");
     int64_t *d_n = c->arena.get<int64_t>(1);
     set_i64(c, d_n, &n, 1);
-    const uint32_t *sid2 = reinterpret_cast<const uint32_t *>(segment_ids(c, Segs{2 * MM, offs2, n}));
     // max_len bounds a whole session (both groups: at most one value per project), so each half too
+    // (segment ids only when the device-wide rank passes need them: rq4b_sessions makes them then)
     const int64_t sess = max_len > 0 && max_len < n ? max_len : n;
-    rq4b_sessions(c, values, sid2, n, d_n, MM, sess, sess, c2, c1, g2q, g1q, pbm, offs2);
+    rq4b_sessions(c, values, nullptr, n, d_n, MM, sess, sess, c2, c1, g2q, g1q, pbm, offs2);
 }
 
 // The last session index with both groups >= 100 (:849-860) -> *last (-1 if none), and Spearman
