@@ -125,6 +125,17 @@ def test_many_segments_lists(engine):
     _spearman(engine, segs[:2000] + segs[-2:])
 
 
+@pytest.mark.parametrize("kinds", [["spread"], ["ties", "dominant", "spread"], ["signed", "powers"]])
+def test_long_segments_radix_path(engine, kinds):
+    """Segments above 2^20 values among short and flagged ones (longer than 16384, or skewed): the
+    long-segment sort (the merge rounds; radix_big_segments in an FZ_BIG_RADIX=1 build) - order
+    statistics and Spearman vs numpy / scipy."""
+    lengths = [1_500_000, 5, 20_000, 16_385, 3000, 0, 1_100_000, 40_000, 64]
+    segs = _segments(31 + len(kinds), lengths, kinds)
+    _session_stats(engine, segs)
+    _spearman(engine, segs)
+
+
 # The per-session statistics by SELECTION (fz_series.hip seg_qstats: no sorted copy) run when no
 # segment exceeds 16384 values (a session holds one value per project); the lists above reach 40000
 # and take the sort path.  Same checks against numpy on lengths up to the selection's bound.

@@ -391,6 +391,9 @@ bool fused_fold_on();
 unsigned *seg_tickets(fz_ctx *c, int64_t S);
 void radix_sort_rows_payload32(fz_ctx *c, const uint32_t *key_src, uint32_t *&keys, uint32_t *&vals, int64_t n,
                                int bits, RadixPayload &pl);
+// radix_sort_pairs_payload32 over the first *d_live of n_cap entries (device count)
+void radix_sort_pairs_payload32_live(fz_ctx *c, uint32_t *&keys, uint32_t *&vals, int64_t n_cap, const int64_t *d_live,
+                                     int bits, RadixPayload &pl);
 // Up to three such sorts (32-bit keys, values, payload columns) in shared launches: one histogram
 // launch for all, then one launch per digit pass over every table that has that digit.  Per table:
 // key_src (optional, as radix_sort_rows_payload32: the first pass reads the keys there and takes the

@@ -1329,6 +1329,11 @@ void radix_sort_pairs_payload32(fz_ctx *c, uint32_t *&keys, uint32_t *&vals, int
     FZ_CHECK(bits <= 32, "radix_sort_pairs_payload32: keys of more than 32 bits");
     radix_payload_impl<uint32_t>(c, keys, vals, n, bits, pl);
 }
+void radix_sort_pairs_payload32_live(fz_ctx *c, uint32_t *&keys, uint32_t *&vals, int64_t n_cap, const int64_t *d_live,
+                                     int bits, RadixPayload &pl) {
+    FZ_CHECK(bits <= 32, "radix_sort_pairs_payload32_live: keys of more than 32 bits");
+    radix_payload_impl<uint32_t>(c, keys, vals, n_cap, bits, pl, d_live);
+}
 void radix_sort_rows_payload32(fz_ctx *c, const uint32_t *key_src, uint32_t *&keys, uint32_t *&vals, int64_t n,
                                int bits, RadixPayload &pl) {
     FZ_CHECK(bits <= 32 && bits > 0 && n > 1, "radix_sort_rows_payload32: bad key width or size");

@@ -611,6 +611,91 @@ __global__ __launch_bounds__(kBlock) void k_f64_from_keys(const uint64_t *__rest
 // buckets average 1/128 of the live values: 6 K at config 2's 0.8 M, against an LDS capacity of
 // 12 K; a longer bucket - a live union of several million - takes the slower in-workgroup merge)
 constexpr int64_t kSampleSortMax = (int64_t(1) << 31) - 1;
+// The segments the bucket sorts flagged (longer than 16,384 values, or skewed) by LSD radix passes
+// instead of the merge rounds: their values copied back to back in position order (64-bit keys,
+// positions), 8 stable passes on the value key over the live rows, then stable passes on the
+// segment index (positions ride as values, the value keys as payload) - the result is each
+// segment's (value, position) order, the merge sort's own order.
+// Measured slower and kept off: config 5L 37.28 vs 36.46 ms with the merge rounds (same box,
+// profiles/r06_big_radix_ab.txt) - a recorded graph runs all eight value passes over ~75 M keys,
+// and the segment passes carry the 8-byte keys; the merge rounds' late rounds touch only the
+// longest segments.
+#ifndef FZ_BIG_RADIX
+#define FZ_BIG_RADIX 0
+#endif
+#ifndef FZ_BIG_RADIX_MIN
+#define FZ_BIG_RADIX_MIN (1 << 20)  // longest flagged segment from which the radix path pays (merge rounds)
+#endif
+constexpr int64_t kBigRadixMin = FZ_BIG_RADIX_MIN;
+__global__ __launch_bounds__(kBlock) void k_big_len(const int64_t *__restrict__ offs, int64_t S,
+                                                    const uint8_t *__restrict__ flag, int64_t *__restrict__ len) {
+    for (int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x; s <= S; s += int64_t(gridDim.x) * kBlock)
+        len[s] = s < S && flag[s] ? offs[s + 1] - offs[s] : 0;
+}
+// tile k of the map: its rows at cofs[s] + (row - offs[s]) of the packed arrays
+__global__ __launch_bounds__(kBlock) void k_big_pack(const double *__restrict__ src, const int64_t *__restrict__ offs,
+                                                     const int64_t *__restrict__ cofs, TileMap tm,
+                                                     uint64_t *__restrict__ key, uint32_t *__restrict__ pos) {
+    const int64_t nt = *tm.d_n;
+    for (int64_t k = blockIdx.x; k < nt; k += gridDim.x) {
+        const int32_t s = tm.seg[k];
+        const int64_t b = tm.begin[k], e = b + kTile < offs[s + 1] ? b + kTile : offs[s + 1];
+        const int64_t base = cofs[s] - offs[s];
+        for (int64_t r = b + threadIdx.x; r < e; r += kBlock) {
+            key[base + r] = f64_key(src[r]);
+            pos[base + r] = uint32_t(r);
+        }
+    }
+}
+// after the value passes: each packed row's segment index (dead rows past the live count: S)
+__global__ __launch_bounds__(kBlock) void k_big_segkey(const int64_t *__restrict__ offs, int64_t S,
+                                                       const uint32_t *__restrict__ pos, const int64_t *__restrict__ d_live,
+                                                       int64_t n_cap, uint32_t *__restrict__ seg) {
+    const int64_t live = *d_live;
+    for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < n_cap; j += int64_t(gridDim.x) * kBlock)
+        seg[j] = j < live ? uint32_t(upper_bound_i64(offs, 0, S + 1, int64_t(pos[j])) - 1) : uint32_t(S);
+}
+__global__ __launch_bounds__(kBlock) void k_big_unpack(const int64_t *__restrict__ offs,
+                                                       const int64_t *__restrict__ cofs, const uint32_t *__restrict__ seg,
+                                                       const uint64_t *__restrict__ key,
+                                                       const uint32_t *__restrict__ pos, const int64_t *__restrict__ d_live,
+                                                       double *__restrict__ out_val, int32_t *__restrict__ out_pos) {
+    const int64_t live = *d_live;
+    for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < live; j += int64_t(gridDim.x) * kBlock) {
+        const uint32_t s = seg[j];
+        const int64_t q = offs[s] + (j - cofs[s]);
+        out_val[q] = f64_from_key(key[j]);
+        out_pos[q] = int32_t(pos[j]);
+    }
+}
+static void radix_big_segments(fz_ctx *c, const int64_t *offs, int64_t S, int64_t n_cap, const uint8_t *flag,
+                               const double *src, double *out_val, int32_t *out_pos) {
+    const TileMap tm = big_tiles(c, offs, S, n_cap, flag);
+    if (tm.cap <= 0) return;
+    int64_t *len = c->arena.get<int64_t>(S + 1);
+    int64_t *cofs = c->arena.get<int64_t>(S + 1);
+    int64_t *d_live = c->arena.get<int64_t>(1);
+    k_big_len<<<grid_for(S + 1), kBlock, 0, c->stream>>>(offs, S, flag, len);
+    FZ_LAUNCH_CHECK();
+    scan_exclusive_i64(c, len, cofs, S + 1, d_live);
+    uint64_t *key = c->arena.get<uint64_t>(n_cap);
+    uint32_t *pos = c->arena.get<uint32_t>(n_cap);
+    k_big_pack<<<unsigned(tm.cap < 4096 ? tm.cap : 4096), kBlock, 0, c->stream>>>(src, offs, cofs, tm, key, pos);
+    FZ_LAUNCH_CHECK();
+    radix_sort_pairs_swap_live(c, key, pos, n_cap, d_live, 64);
+    uint32_t *seg = c->arena.get<uint32_t>(n_cap);
+    k_big_segkey<<<grid_for(n_cap, kBlock, 4096), kBlock, 0, c->stream>>>(offs, S, pos, d_live, n_cap, seg);
+    FZ_LAUNCH_CHECK();
+    RadixPayload pl;
+    pl.n = 1;
+    pl.in[0] = key;
+    pl.size[0] = 8;
+    radix_sort_pairs_payload32_live(c, seg, pos, n_cap, d_live, bits_for(uint64_t(S)), pl);
+    k_big_unpack<<<grid_for(n_cap, kBlock, 4096), kBlock, 0, c->stream>>>(
+        offs, cofs, seg, static_cast<const uint64_t *>(pl.out[0]), pos, d_live, out_val, out_pos);
+    FZ_LAUNCH_CHECK();
+}
+
 SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int32_t *) {
     const int64_t n = sg.n_cap;
     SortedSegs out;
@@ -683,7 +768,10 @@ SortedSegs seg_sort_f64(fz_ctx *c, const double *src, const Segs &sg, const int3
         k_seg_val_bucket<1024, 16384><<<grid(class_cap(kClassBig), 512), 1024, 0, c->stream>>>(
             src, offs, S, kLdsSortMax, out.val, out.pos, class_list(kClassBig), class_n(kClassBig), flag, true);
         FZ_LAUNCH_CHECK();
-        sort_big_segments(c, offs, S, n, lb, flag, F64Key{src}, F64Sink{out.val, out.pos});
+        if (FZ_BIG_RADIX && lb > kBigRadixMin)
+            radix_big_segments(c, offs, S, n, flag, src, out.val, out.pos);
+        else
+            sort_big_segments(c, offs, S, n, lb, flag, F64Key{src}, F64Sink{out.val, out.pos});
     }
     return out;
 }
