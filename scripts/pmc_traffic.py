@@ -21,7 +21,8 @@ import json
 import sys
 
 SCOPES = {
-    "radix_scatter": {"match": ["k_onesweep<"]},
+    # (round 6: the store's three tables share each pass, k_onesweep_tabs)
+    "radix_scatter": {"match": ["k_onesweep<", "k_onesweep_tabs<"]},
     "radix_hist": {"match": ["k_onesweep_hist"]},
     "elig_hist": {"match": ["k_elig_hist"]},
     # (the selective filters - tiles of unselected projects skipped - are probed apart)
@@ -46,7 +47,8 @@ SCOPES = {
     "scan_i64": {"match": ["k_scan_lookback"]},
     # RQ2's per-session order statistics by selection: the small-segment launch opens the scope
     # (the size-class lists and the workgroup classes follow)
-    "seg_qstats": {"open": "k_qs_micro", "match": ["k_qs_micro", "k_qs_tiny", "k_qs_sort_mid", "k_qs_block"], "allow": ["k_fill"]},
+    "seg_qstats": {"open": "k_qs_micro", "match": ["k_qs_micro", "k_qs_tiny", "k_qs_sort_mid", "k_qs_block", "k_qs_wave"],
+                   "allow": ["k_fill"]},
     "describe_select": {"match": ["k_describe_sel"]},
     "spearman_shapiro": {"match": ["k_spearman_index_small"]},
     "ragged_transpose": {"match": ["k_rt_move"]},
