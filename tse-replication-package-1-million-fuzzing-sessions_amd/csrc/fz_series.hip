@@ -2891,19 +2891,17 @@ void seg_qstats(fz_ctx *c, const double *vals, const Segs &sg, const double *q_h
                                                                                       L.d_n + kQsTiny, a);
         FZ_LAUNCH_CHECK();
     }
-    if (kQsWave && lb > kTinySeg) {
-        // the mid (65-1024) and 1025-2048 lists one wave per segment (16 / 32 keys per lane)
-        constexpr int wpb = kQsWaveBlock / kWave;
-        k_qs_wave<1024><<<grid((caps[1] + wpb - 1) / wpb, 4096), kQsWaveBlock, 0, c->stream>>>(
-            vals, sg.offs, L.ids[1], L.d_n + 1, nullptr, nullptr, a);
-        FZ_LAUNCH_CHECK();
-        if (lb > 1024) {
-            k_qs_wave<2048><<<grid((caps[3] + wpb - 1) / wpb, 4096), kQsWaveBlock, 0, c->stream>>>(
-                vals, sg.offs, L.ids[3], L.d_n + 3, nullptr, nullptr, a);
-            FZ_LAUNCH_CHECK();
-        }
-    } else if (lb > kTinySeg) {
+    if (lb > kTinySeg) {
+        // (the mid list stays with the LDS bitonic sort: one wave per session measured 141 vs 67 us
+        // per step at config 2's ~3,000 sessions of <= 1,000 values, serial probe)
         k_qs_sort_mid<<<grid(caps[1], 8192), 256, 0, c->stream>>>(vals, sg.offs, L.ids[1], L.d_n + 1, a);
+        FZ_LAUNCH_CHECK();
+    }
+    if (kQsWave && lb > 1024) {
+        // the 1025-2048 list one wave per segment (32 keys per lane)
+        constexpr int wpb = kQsWaveBlock / kWave;
+        k_qs_wave<2048><<<grid((caps[3] + wpb - 1) / wpb, 4096), kQsWaveBlock, 0, c->stream>>>(
+            vals, sg.offs, L.ids[3], L.d_n + 3, nullptr, nullptr, a);
         FZ_LAUNCH_CHECK();
     }
     if (!kQsWave && lb > 1024) {
