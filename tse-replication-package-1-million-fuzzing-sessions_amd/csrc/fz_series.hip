@@ -568,7 +568,14 @@ uint64_t *sort_small_keys(fz_ctx *c, const double *x, int64_t nmax, const int64_
     return k;
 }
 
+#ifndef FZ_TILE_BUCKETS
+// 1: the merge sort's tile phase tries a bucket sort first (fz_segsort.h) - measured slower and
+// kept off (same box: c5L 35.06 vs 34.82 ms, c4 3.01 vs 2.90; profiles/r06_tile_buckets_ab.txt):
+// tied tiles pay the attempt and the network
+#define FZ_TILE_BUCKETS 0
+#endif
 struct F64Key {
+    static constexpr bool kBuckets = FZ_TILE_BUCKETS;
     const double *src;
     __device__ uint64_t operator()(int64_t i) const { return f64_key(src[i]); }
 };
