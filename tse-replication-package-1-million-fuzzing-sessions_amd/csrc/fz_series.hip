@@ -361,10 +361,20 @@ constexpr int kValSkew = 32;
 #ifndef FZ_VB4_BLOCK
 #define FZ_VB4_BLOCK 1024
 #endif
+#ifndef FZ_VB_C16
+#define FZ_VB_C16 1  // 16-bit counters in the 16,384 class (0: 32-bit, the A/B baseline)
+#endif
+#ifndef FZ_VB_WPE
+#define FZ_VB_WPE 8  // its waves per SIMD: two 1,024-thread workgroups per CU (64 VGPRs)
+#endif
+#ifndef FZ_VB4_WPE
+#define FZ_VB4_WPE 1  // the same for the 4,096 class (1: the compiler's choice)
+#endif
 constexpr int kVb4Block = FZ_VB4_BLOCK;                 // threads per workgroup of the 2049..4096 class
 constexpr int kVb4Grid = 2048 * (1024 / FZ_VB4_BLOCK);  // its persistent grid (same threads in all)
 template <int BS, int MAXN>
-__global__ __launch_bounds__(BS) void k_seg_val_bucket(const double *__restrict__ src, const int64_t *__restrict__ offs,
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(MAXN > kLdsSortMax && FZ_VB_C16 ? FZ_VB_WPE : (MAXN == kLdsSortMax && BS == 1024 ? FZ_VB4_WPE : 1))))
+void k_seg_val_bucket(const double *__restrict__ src, const int64_t *__restrict__ offs,
                                                        int64_t S, int64_t min_len, double *__restrict__ out_val,
                                                        int32_t *__restrict__ out_pos, const int32_t *__restrict__ list,
                                                        const int64_t *__restrict__ d_ln, uint8_t *__restrict__ bigflag,
@@ -372,9 +382,26 @@ __global__ __launch_bounds__(BS) void k_seg_val_bucket(const double *__restrict_
     constexpr int IPT = MAXN / BS;  // values (and buckets in the scan) per thread
     constexpr int NW = BS / kWave;
     constexpr bool KEYS_LDS = MAXN <= kLdsSortMax;
+    // the class without its keys in LDS counts in 16-bit halves of the counter words (counts, starts
+    // and staged positions are < 65,536): 66 KB of LDS instead of 99 KB, two workgroups per CU
+    constexpr bool C16 = !KEYS_LDS && FZ_VB_C16;
+    constexpr int CNT_WORDS = C16 ? (MAXN + 2) / 2 + 1 : MAXN + 1;
     static_assert(MAXN <= 16384 && MAXN % BS == 0 && (MAXN & (MAXN - 1)) == 0, "value bucket sort shape");
-    __shared__ alignas(8) uint32_t s_cnt[MAXN + 1];  // bucket counts, then starts (+ sentinel); staging
-    __shared__ uint16_t s_pos[MAXN];      // positions in bucket order (bitonic fallback: pair positions)
+    static_assert(KEYS_LDS || CNT_WORDS + MAXN / 2 >= MAXN, "value staging: MAXN / 2 u64 slots");
+    // bucket counts, then starts (+ sentinel), then staging; positions in bucket order (u16, bitonic
+    // fallback: pair positions) right after them
+    __shared__ alignas(8) uint32_t s_mem[CNT_WORDS + MAXN / 2];
+    uint32_t *const s_cnt = s_mem;
+    uint16_t *const c16 = reinterpret_cast<uint16_t *>(s_mem);
+    uint16_t *const s_pos = reinterpret_cast<uint16_t *>(s_mem + CNT_WORDS);
+    auto cnt_get = [&](uint32_t q) -> uint32_t {
+        if constexpr (C16) return c16[q];
+        else return s_cnt[q];
+    };
+    auto cnt_set = [&](uint32_t q, uint32_t v) {
+        if constexpr (C16) c16[q] = uint16_t(v);
+        else s_cnt[q] = v;
+    };
     __shared__ uint64_t s_key[KEYS_LDS ? MAXN : 1];
     __shared__ uint64_t s_lo[NW], s_hi[NW];
     __shared__ uint32_t s_tmp[NW], s_max[NW];
@@ -407,7 +434,7 @@ __global__ __launch_bounds__(BS) void k_seg_val_bucket(const double *__restrict_
             s_lo[w] = lo;
             s_hi[w] = hi;
         }
-        for (int j = tid; j < MAXN + 1; j += BS) s_cnt[j] = 0u;
+        for (int j = tid; j < CNT_WORDS; j += BS) s_cnt[j] = 0u;
         __syncthreads();
         lo = ~0ull;
         hi = 0ull;
@@ -423,9 +450,19 @@ __global__ __launch_bounds__(BS) void k_seg_val_bucket(const double *__restrict_
             const int i = tid + m * BS;
             bs[m] = 0u;
             if (i < n) {
-                uint32_t q = uint32_t(double(k[m] - lo) * scale);
+                // (C16: re-read, coalesced, from the cache-resident segment - no key held across
+                // the barrier)
+                const uint64_t km = C16 ? f64_key(src[b + i]) : k[m];
+                uint32_t q = uint32_t(double(km - lo) * scale);
                 q = q < uint32_t(n) ? q : uint32_t(n - 1);
-                bs[m] = (q << 16) | atomicAdd(&s_cnt[q], 1u);
+                uint32_t slot;
+                if constexpr (C16) {  // (a half never exceeds n <= 16,384: no carry into its neighbour)
+                    const uint32_t sh = (q & 1u) << 4;
+                    slot = (atomicAdd(&s_cnt[q >> 1], 1u << sh) >> sh) & 0xffffu;
+                } else {
+                    slot = atomicAdd(&s_cnt[q], 1u);
+                }
+                bs[m] = (q << 16) | slot;
                 if (KEYS_LDS) s_key[i] = k[m];
             }
         }
@@ -434,7 +471,7 @@ __global__ __launch_bounds__(BS) void k_seg_val_bucket(const double *__restrict_
         uint32_t sum = 0, mx = 0;
 #pragma unroll
         for (int e = 0; e < IPT; ++e) {
-            const uint32_t ce = s_cnt[tid * IPT + e];
+            const uint32_t ce = cnt_get(tid * IPT + e);
             sum += ce;
             mx = ce > mx ? ce : mx;
         }
@@ -443,11 +480,11 @@ __global__ __launch_bounds__(BS) void k_seg_val_bucket(const double *__restrict_
         uint32_t run = block_excl_scan<uint32_t, NW>(sum, s_tmp, (uint32_t *)nullptr);
 #pragma unroll
         for (int e = 0; e < IPT; ++e) {  // (block_excl_scan's barriers ordered every read above)
-            const uint32_t ce = s_cnt[tid * IPT + e];
-            s_cnt[tid * IPT + e] = run;
+            const uint32_t ce = cnt_get(tid * IPT + e);
+            cnt_set(tid * IPT + e, run);
             run += ce;
         }
-        if (tid == 0) s_cnt[MAXN] = uint32_t(n);
+        if (tid == 0) cnt_set(MAXN, uint32_t(n));
         __syncthreads();
         uint32_t gmax = 0;
 #pragma unroll
@@ -491,7 +528,7 @@ __global__ __launch_bounds__(BS) void k_seg_val_bucket(const double *__restrict_
 #pragma unroll
         for (int m = 0; m < IPT; ++m) {
             const int i = tid + m * BS;
-            if (i < n) s_pos[s_cnt[bs[m] >> 16] + (bs[m] & 0xffffu)] = uint16_t(i);
+            if (i < n) s_pos[cnt_get(bs[m] >> 16) + (bs[m] & 0xffffu)] = uint16_t(i);
         }
         __syncthreads();
         int32_t dq[IPT];  // sorted position of value i inside the segment
@@ -500,13 +537,18 @@ __global__ __launch_bounds__(BS) void k_seg_val_bucket(const double *__restrict_
             const int i = tid + m * BS;
             dq[m] = -1;
             if (i >= n) continue;
-            const uint32_t st = s_cnt[bs[m] >> 16], en = s_cnt[(bs[m] >> 16) + 1];
+            const uint32_t st = cnt_get(bs[m] >> 16), en = cnt_get((bs[m] >> 16) + 1);
             uint32_t rank = 0;
-            for (uint32_t x = st; en - st > 1 && x < en; ++x) {  // (alone in its bucket: rank 0)
-                const int ox = s_pos[x];
-                if (ox == i) continue;
-                const uint64_t kx = KEYS_LDS ? s_key[ox] : f64_key(src[b + ox]);
-                rank += (kx < k[m]) || (kx == k[m] && ox < i);
+            if (en - st > 1) {  // (alone in its bucket: rank 0)
+                // (C16: the key re-read from the cache-resident segment - k[] is dead past the
+                // bucketing, which keeps the class at 64 registers, two workgroups per CU)
+                const uint64_t km = C16 ? f64_key(src[b + i]) : k[m];
+                for (uint32_t x = st; x < en; ++x) {
+                    const int ox = s_pos[x];
+                    if (ox == i) continue;
+                    const uint64_t kx = KEYS_LDS ? s_key[ox] : f64_key(src[b + ox]);
+                    rank += (kx < km) || (kx == km && ox < i);
+                }
             }
             dq[m] = int32_t(st + rank);
         }
@@ -514,13 +556,25 @@ __global__ __launch_bounds__(BS) void k_seg_val_bucket(const double *__restrict_
         // coalesced output: positions, then values, staged in sorted order (u32 slots for the whole
         // segment in the bucket counts; u64 slots in the key array, or half a segment per round in
         // the bucket counts when the keys are not in LDS)
+        // (C16: the segment-local position, b added on the way out)
 #pragma unroll
         for (int m = 0; m < IPT; ++m)
-            if (dq[m] >= 0) s_cnt[dq[m]] = uint32_t(b + tid + m * BS);
+            if (dq[m] >= 0) cnt_set(dq[m], C16 ? uint32_t(tid + m * BS) : uint32_t(b + tid + m * BS));
         __syncthreads();
-        for (int q = tid; q < n; q += BS) out_pos[b + q] = int32_t(s_cnt[q]);
+        if constexpr (C16) {
+            // the values gathered by the staged positions from the cache-resident segment (the
+            // value is the key's bijective image: the same bits as a staged key)
+            for (int q = tid; q < n; q += BS) {
+                const uint32_t lp = cnt_get(q);
+                out_pos[b + q] = int32_t(uint32_t(b) + lp);
+                out_val[b + q] = src[b + lp];
+            }
+            __syncthreads();  // LDS is reused by the next segment
+            continue;
+        }
+        for (int q = tid; q < n; q += BS) out_pos[b + q] = int32_t(cnt_get(q));
         __syncthreads();
-        uint64_t *stg = KEYS_LDS ? s_key : reinterpret_cast<uint64_t *>(s_cnt);
+        uint64_t *stg = KEYS_LDS ? s_key : reinterpret_cast<uint64_t *>(s_mem);
         constexpr int CAP = KEYS_LDS ? MAXN : MAXN / 2;
         for (int h = 0; h < n; h += CAP) {
 #pragma unroll
