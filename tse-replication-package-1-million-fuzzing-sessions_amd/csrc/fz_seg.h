@@ -101,8 +101,13 @@ __device__ inline bool chunk_arrive(unsigned *tickets, const double *part, doubl
     return true;
 }
 
+#ifndef FZ_CR_WPE
+#define FZ_CR_WPE 4  // k_chunk_reduce's minimum waves per SIMD: the Shapiro-Wilk / rank-test reductions at
+                     // 3 waves (135-175 registers) get 4 (a few spilled): config 2 1.077 -> 1.065 ms, 3L
+                     // unchanged (profiles/r06_occupancy_ab.txt)
+#endif
 template <int NV, typename F>
-__global__ __launch_bounds__(kBlock) void k_chunk_reduce(ChunkMap cm, const int64_t *__restrict__ offs, int64_t cps,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FZ_CR_WPE))) void k_chunk_reduce(ChunkMap cm, const int64_t *__restrict__ offs, int64_t cps,
                                                          int64_t nk_host, F f, double *__restrict__ part,
                                                          double *__restrict__ out, unsigned *tickets = nullptr) {
     __shared__ double s_hi[4][NV], s_lo[4][NV];

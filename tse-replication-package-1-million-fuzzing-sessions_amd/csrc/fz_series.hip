@@ -368,12 +368,14 @@ constexpr int kValSkew = 32;
 #define FZ_VB_WPE 8  // its waves per SIMD: two 1,024-thread workgroups per CU (64 VGPRs)
 #endif
 #ifndef FZ_VB4_WPE
-#define FZ_VB4_WPE 1  // the same for the 4,096 class (1: the compiler's choice)
+#define FZ_VB4_WPE 8  // the same for the 4,096 class: 98 -> 63 registers, two workgroups per CU, the kernel
+                      // 296 -> 191 us and config 3L 19.54 -> 18.72 ms (profiles/r06_occupancy_ab.txt); the
+                      // 256- and 512-thread classes keep the compiler's choice (config 2 a hair slower capped)
 #endif
 constexpr int kVb4Block = FZ_VB4_BLOCK;                 // threads per workgroup of the 2049..4096 class
 constexpr int kVb4Grid = 2048 * (1024 / FZ_VB4_BLOCK);  // its persistent grid (same threads in all)
 template <int BS, int MAXN>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(MAXN > kLdsSortMax && FZ_VB_C16 ? FZ_VB_WPE : (MAXN == kLdsSortMax && BS == 1024 ? FZ_VB4_WPE : 1))))
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(MAXN > kLdsSortMax ? (FZ_VB_C16 ? FZ_VB_WPE : 1) : (BS == 1024 ? FZ_VB4_WPE : 1))))
 void k_seg_val_bucket(const double *__restrict__ src, const int64_t *__restrict__ offs,
                                                        int64_t S, int64_t min_len, double *__restrict__ out_val,
                                                        int32_t *__restrict__ out_pos, const int32_t *__restrict__ list,
