@@ -1153,14 +1153,18 @@ __global__ __launch_bounds__(BS) void k_bm_halves_lds(const double *__restrict__
             const double *own = inx ? X : Y, *oth = inx ? Y : X;
             const int no = inx ? nx : ny, nt = inx ? ny : nx, k = inx ? j : j - nx;
             const double v = own[k];
+            // (each search's predicate holds on a prefix of its range - NaNs sort last and compare
+            // false - so one probe at the range's near end settles the untied case: a value without
+            // ties costs the one search in the other half, not four)
             int la = 0, hi = k;  // first index of v in own (own[k] == v)
+            if (k == 0 || own[k - 1] < v) la = k;
             while (la < hi) {
                 const int md = (la + hi) >> 1;
                 if (own[md] < v) la = md + 1;
                 else hi = md;
             }
             int ua = k + 1;  // one past the last index of v in own
-            hi = no;
+            hi = (ua < no && own[ua] <= v) ? no : ua;
             while (ua < hi) {
                 const int md = (ua + hi) >> 1;
                 if (own[md] <= v) ua = md + 1;
@@ -1174,7 +1178,7 @@ __global__ __launch_bounds__(BS) void k_bm_halves_lds(const double *__restrict__
                 else hi = md;
             }
             int ub = lb;
-            hi = nt;
+            hi = (ub < nt && oth[ub] <= v) ? nt : ub;
             while (ub < hi) {
                 const int md = (ub + hi) >> 1;
                 if (oth[md] <= v) ub = md + 1;
