@@ -2298,8 +2298,12 @@ __global__ __launch_bounds__(kBlock) void k_qs_tiny(const double *__restrict__ s
 
 // The segments of one class list (at most MAXN values each), one workgroup each.
 template <int BS, int MAXN>
-struct QsBlockWpe {  // (the keys-from-global big class: a register budget for 4 waves per SIMD)
-    static constexpr int v = (MAXN > 2048 && kQsKeysGlobal) ? 3 : 1;
+#ifndef FZ_QS_BIG_WPE
+#define FZ_QS_BIG_WPE 6  // the keys-from-global class at 6 waves per SIMD (80 registers, a 60-byte spill): three
+                         // 512-thread workgroups per CU; config 3L 19.13 -> 18.81 ms (profiles/r06_qs_big_wpe_ab.txt)
+#endif
+struct QsBlockWpe {  // (the keys-from-global big class: its waves per SIMD)
+    static constexpr int v = (MAXN > 2048 && kQsKeysGlobal) ? FZ_QS_BIG_WPE : 1;
 };
 template <int BS, int MAXN>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(QsBlockWpe<BS, MAXN>::v))) void k_qs_block(const double *__restrict__ src, const int64_t *__restrict__ offs,
