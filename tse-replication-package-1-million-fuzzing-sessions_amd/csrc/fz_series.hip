@@ -367,6 +367,10 @@ constexpr int kValSkew = 32;
 #ifndef FZ_VB_WPE
 #define FZ_VB_WPE 8  // its waves per SIMD: two 1,024-thread workgroups per CU (64 VGPRs)
 #endif
+#ifndef FZ_VB_SMALL_WPE
+#define FZ_VB_SMALL_WPE 8  // the 256- / 512-thread classes (102 / 104 -> 64 registers): config 5L 34.00 -> 33.84 ms
+                           // (profiles/r06_filter_items_vb_small_ab.txt)
+#endif
 #ifndef FZ_VB4_WPE
 #define FZ_VB4_WPE 8  // the same for the 4,096 class: 98 -> 63 registers, two workgroups per CU, the kernel
                       // 296 -> 191 us and config 3L 19.54 -> 18.72 ms (profiles/r06_occupancy_ab.txt); the
@@ -375,7 +379,7 @@ constexpr int kValSkew = 32;
 constexpr int kVb4Block = FZ_VB4_BLOCK;                 // threads per workgroup of the 2049..4096 class
 constexpr int kVb4Grid = 2048 * (1024 / FZ_VB4_BLOCK);  // its persistent grid (same threads in all)
 template <int BS, int MAXN>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(MAXN > kLdsSortMax ? (FZ_VB_C16 ? FZ_VB_WPE : 1) : (BS == 1024 ? FZ_VB4_WPE : 1))))
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(MAXN > kLdsSortMax ? (FZ_VB_C16 ? FZ_VB_WPE : 1) : (BS == 1024 ? FZ_VB4_WPE : FZ_VB_SMALL_WPE))))
 void k_seg_val_bucket(const double *__restrict__ src, const int64_t *__restrict__ offs,
                                                        int64_t S, int64_t min_len, double *__restrict__ out_val,
                                                        int32_t *__restrict__ out_pos, const int32_t *__restrict__ list,
