@@ -101,7 +101,10 @@ def _np_describe(a):
                 max=float(a.max()), q1=float(np.percentile(a, 25)), q3=float(np.percentile(a, 75)))
 
 
-@pytest.mark.parametrize("n,seed", [(1, 0), (2, 1), (5, 2), (1000, 3), (777_777, 4)])
+@pytest.mark.parametrize("n,seed", [(1, 0), (2, 1), (5, 2), (1000, 3), (777_777, 4),
+                                    # k_describe_sel's network classes: 512 / 1,024 / 2,048 / 4,096 / 8,192 keys
+                                    (64, 5), (511, 6), (512, 7), (513, 8), (1024, 9), (1025, 10), (2048, 11),
+                                    (2049, 12), (4096, 13), (4097, 14), (8192, 15), (8193, 16)])
 def test_describe_matches_numpy(engine, n, seed):
     torch = engine.torch
     rng = np.random.default_rng(seed)

@@ -2594,6 +2594,9 @@ __device__ inline DD block_dd_sum_sel(DD acc, double *s_hi, double *s_lo) {
     return t;
 }
 constexpr int64_t kSelLds = 12288;  // samples of up to this many values are staged in LDS (96 KiB of keys)
+#ifndef FZ_DESC_NET_CLASSES
+#define FZ_DESC_NET_CLASSES 1  // (0: every staged sample through the 4,096- / 8,192-key network; A/B builds)
+#endif
 
 // Sort the staged keys s[0, kSelBlock * E) ascending (entries at >= n read as ~0) by a bitonic
 // network held in registers: E keys per thread, stages of distance < E inside a thread, < 64 E by
@@ -2728,6 +2731,14 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
     }
     __syncthreads();
     if (n <= int64_t(kSelBlock) * 16) {  // (the keys are staged: kSelLds >= 8,192)
+        // the network sized to the sample (kSelBlock * E keys): a 1,000-value sample takes the
+        // 1,024-key network (55 stages of 2 keys a thread), not the 4,096-key one (78 stages of 8)
+#if FZ_DESC_NET_CLASSES
+        if (n <= int64_t(kSelBlock)) wg_bitonic_keys<1>(s_keys, n);
+        else if (n <= int64_t(kSelBlock) * 2) wg_bitonic_keys<2>(s_keys, n);
+        else if (n <= int64_t(kSelBlock) * 4) wg_bitonic_keys<4>(s_keys, n);
+        else
+#endif
         if (n <= int64_t(kSelBlock) * 8) wg_bitonic_keys<8>(s_keys, n);
         else wg_bitonic_keys<16>(s_keys, n);
         if (tid < 7) sh.res[tid] = s_keys[sh.rank[tid]];
