@@ -21,6 +21,10 @@ def samples():
     rng = np.random.default_rng(3)
     yield "ints9022", np.round(rng.normal(0, 60, 9022))
     yield "normal1000", rng.normal(0, 0.6, 1000)
+    yield "normal1500", rng.normal(0, 0.6, 1500)
+    yield "normal2000", rng.normal(0, 0.6, 2000)
+    yield "ints4000", np.round(rng.normal(0, 60, 4000))
+    yield "normal6000", rng.normal(0, 0.6, 6000)
     yield "normal12000", rng.normal(0, 0.6, 12000)
     yield "normal60000", rng.normal(0, 0.6, 60000)
     yield "rates3000", np.round(rng.uniform(0, 100, 3000), 2)

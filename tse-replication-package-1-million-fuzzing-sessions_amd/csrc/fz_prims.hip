@@ -2184,6 +2184,7 @@ struct DescSmallArgs {
     const double *x[kDescBatch];
     const int64_t *d_n[kDescBatch];
     fz_describe *out[kDescBatch];
+    int64_t stage_cap;  // keys staged in the dynamic LDS (its size / 8): samples of up to this many
 };
 // ---- describe by selection (one workgroup per sample, no sorted copy) ------------------------
 // The order statistics a describe needs (median, the quartiles' interpolation neighbours, the
@@ -2594,8 +2595,13 @@ __device__ inline DD block_dd_sum_sel(DD acc, double *s_hi, double *s_lo) {
     return t;
 }
 constexpr int64_t kSelLds = 12288;  // samples of up to this many values are staged in LDS (96 KiB of keys)
-#ifndef FZ_DESC_NET_CLASSES
-#define FZ_DESC_NET_CLASSES 1  // (0: every staged sample through the 4,096- / 8,192-key network; A/B builds)
+#ifndef FZ_DESC_NET_MAX
+#define FZ_DESC_NET_MAX 1024  // samples of up to this many values sorted by a register network (512 .. 8,192)
+#endif
+static_assert(FZ_DESC_NET_MAX >= 512 && FZ_DESC_NET_MAX <= 8192 && (FZ_DESC_NET_MAX & (FZ_DESC_NET_MAX - 1)) == 0,
+              "FZ_DESC_NET_MAX: a network size of 512 .. 8,192 keys");
+#ifndef FZ_DESC_LDS_FIT
+#define FZ_DESC_LDS_FIT 1  // (0: every describe workgroup stages kSelLds keys' worth of LDS; A/B builds)
 #endif
 
 // Sort the staged keys s[0, kSelBlock * E) ascending (entries at >= n read as ~0) by a bitonic
@@ -2660,7 +2666,10 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
     chain_prio();
     constexpr int NW = kSelBlock / kWave;
     __shared__ SelShared sh;
-    __shared__ uint64_t s_keys[kSelLds];
+    // (sized by the launch to the batch's capacity: a 1,000-value sample's workgroup holds 33 KB of
+    // LDS, not 121 KB, and is placed beside the other chains' workgroups instead of waiting for an
+    // idle CU)
+    extern __shared__ uint64_t s_keys[];
     __shared__ double s_hi[NW], s_lo[NW];
     __shared__ unsigned long long s_c[3];
     const int tid = threadIdx.x;
@@ -2678,7 +2687,7 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
     DD acc{0.0, 0.0};
     unsigned long long lt0 = 0, le0 = 0, leinf = 0;
     // (a sample that fits is staged in LDS by this first pass: the later passes read LDS)
-    const bool staged = n <= kSelLds;
+    const bool staged = n <= a.stage_cap;
     auto ld = [=](int64_t i) { return x[i]; };
     sel_for(n, ld, [&](int64_t i, double v) {
         const uint64_t k = f64_key(v);
@@ -2730,17 +2739,24 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
         sh.rank[6] = c_lt0 > 0 ? 0 : (c_le0 < n ? c_le0 : 0);
     }
     __syncthreads();
-    if (n <= int64_t(kSelBlock) * 16) {  // (the keys are staged: kSelLds >= 8,192)
+    if (n <= int64_t(FZ_DESC_NET_MAX)) {  // (the keys are staged: stage_cap >= the network >= n)
         // the network sized to the sample (kSelBlock * E keys): a 1,000-value sample takes the
-        // 1,024-key network (55 stages of 2 keys a thread), not the 4,096-key one (78 stages of 8)
-#if FZ_DESC_NET_CLASSES
+        // 1,024-key network (55 stages of 2 keys a thread).  Only the small networks: unrolled over
+        // 8 / 16 keys a thread the code outgrows the instruction cache (phase stamps: 31 / 88 us for
+        // the 4,096- / 8,192-key networks against 6 us for 1,024 keys and ~15 us for the selection)
         if (n <= int64_t(kSelBlock)) wg_bitonic_keys<1>(s_keys, n);
+#if FZ_DESC_NET_MAX > 512
         else if (n <= int64_t(kSelBlock) * 2) wg_bitonic_keys<2>(s_keys, n);
-        else if (n <= int64_t(kSelBlock) * 4) wg_bitonic_keys<4>(s_keys, n);
-        else
 #endif
-        if (n <= int64_t(kSelBlock) * 8) wg_bitonic_keys<8>(s_keys, n);
+#if FZ_DESC_NET_MAX > 1024
+        else if (n <= int64_t(kSelBlock) * 4) wg_bitonic_keys<4>(s_keys, n);
+#endif
+#if FZ_DESC_NET_MAX > 2048
+        else if (n <= int64_t(kSelBlock) * 8) wg_bitonic_keys<8>(s_keys, n);
+#endif
+#if FZ_DESC_NET_MAX > 4096
         else wg_bitonic_keys<16>(s_keys, n);
+#endif
         if (tid < 7) sh.res[tid] = s_keys[sh.rank[tid]];
         __syncthreads();
     } else if (staged) {
@@ -2814,9 +2830,21 @@ void describe_f64_dn_batch(fz_ctx *c, const DescJob *jobs, int njobs) {
         }
     }
     if (ns > 0) {  // every such job in one launch
+        // the staged keys' LDS: the bitonic network of the largest capacity (every live length fits
+        // it), kSelLds beyond the networks
+        int64_t cap = 1;
+        for (int i = 0; i < njobs; ++i)
+            if (jobs[i].nmax <= kDescSelMax) cap = jobs[i].nmax > cap ? jobs[i].nmax : cap;
+        int64_t net = kSelBlock;
+        while (net < cap && net < FZ_DESC_NET_MAX) net *= 2;
+        a.stage_cap = cap > net || !FZ_DESC_LDS_FIT ? kSelLds : net;
+        const size_t lds = size_t(a.stage_cap) * 8;
+        if (lds > 65536)  // (per device: set on every such launch, never cached)
+            FZ_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_describe_sel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(kSelLds * 8)));
         // (algorithmic bytes: one read of the first job's live values)
         ProbeScope ps(c, "describe_select", 0.0, a.d_n[0], 8.0);
-        k_describe_sel<<<ns, kSelBlock, 0, c->stream>>>(a);
+        k_describe_sel<<<ns, kSelBlock, lds, c->stream>>>(a);
         FZ_LAUNCH_CHECK();
     }
     if (nb > 0) describe_sorted_dn_batch(c, big, nb);
