@@ -2741,9 +2741,10 @@ __global__ __launch_bounds__(kSelBlock) void k_describe_sel(DescSmallArgs a) {
     __syncthreads();
     if (n <= int64_t(FZ_DESC_NET_MAX)) {  // (the keys are staged: stage_cap >= the network >= n)
         // the network sized to the sample (kSelBlock * E keys): a 1,000-value sample takes the
-        // 1,024-key network (55 stages of 2 keys a thread).  Only the small networks: unrolled over
-        // 8 / 16 keys a thread the code outgrows the instruction cache (phase stamps: 31 / 88 us for
-        // the 4,096- / 8,192-key networks against 6 us for 1,024 keys and ~15 us for the selection)
+        // 1,024-key network (55 stages of 2 keys a thread).  Only the small networks: the work of a
+        // network is stages x keys a thread on one CU's four SIMDs (78 x 8 / 91 x 16 at 4,096 /
+        // 8,192 keys: phase stamps 31 / 88 us, against 6 us for 1,024 keys and ~15 us for the
+        // selection's passes)
         if (n <= int64_t(kSelBlock)) wg_bitonic_keys<1>(s_keys, n);
 #if FZ_DESC_NET_MAX > 512
         else if (n <= int64_t(kSelBlock) * 2) wg_bitonic_keys<2>(s_keys, n);
