@@ -1830,21 +1830,17 @@ extern "C" int fz_debug_series_timing(unsigned long long *out) {
     } while (0)
 #endif
 constexpr int kSeriesBlock = 512;  // (1,024 threads spilled 120 VGPRs: the statistics' code)
-constexpr int kSeriesE = int(kSpearmanSmall) / kSeriesBlock;  // elements per thread
-static_assert(kSeriesE == 8, "series network shape");
-__global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__restrict__ x,
-                                                               const int64_t *__restrict__ d_n, double *rho,
-                                                               double *pv, double *w, double *wp) {
-    chain_prio();
-    constexpr int BS = kSeriesBlock, NW = BS / kWave, E = kSeriesE;
-    __shared__ uint64_t sk[kSpearmanSmall];
-    __shared__ int32_t spos[kSpearmanSmall];
-    __shared__ double s_tmp[NW];
-    __shared__ double s_hi[NW][3], s_lo[NW][3];
-    __shared__ double s_m[kSpearmanSmall / 2];
+static_assert(int(kSpearmanSmall) == kSeriesBlock * 8, "series network shape");
+#ifndef FZ_SERIES_NET_CLASSES
+#define FZ_SERIES_NET_CLASSES 1  // (0: every series through the 4,096-pair network; A/B builds)
+#endif
+// The series x[0, n) sorted by (key, position) with a bitonic network of kSeriesBlock * E pairs held
+// in registers (E per thread: stages of distance < E inside a thread, < 64 E by shuffles inside a
+// wave, the rest through LDS with barriers); the sorted values and positions left in sv / spos.
+template <int E>
+__device__ inline void series_net(const double *__restrict__ x, int n, uint64_t *sk, int32_t *spos) {
+    constexpr int BS = kSeriesBlock;
     const int tid = threadIdx.x;
-    SERIES_STAMP(0);
-    const int n = int(*d_n);
     uint64_t k[E];
     int32_t ps[E];
     {  // (all E loads in flight at once: a guarded load per element waited on each in turn)
@@ -1875,7 +1871,7 @@ __global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__r
     // (both loops unrolled: every stage's distance is a constant - the in-thread stages index
     // registers directly instead of through indirect register moves)
 #pragma unroll
-    for (int kk = 2; kk <= int(kSpearmanSmall); kk <<= 1) {
+    for (int kk = 2; kk <= BS * E; kk <<= 1) {
 #pragma unroll
         for (int j = kk >> 1; j > 0; j >>= 1) {
             if (j < E) {
@@ -1921,6 +1917,30 @@ __global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__r
         sv[E * tid + h] = f64_from_key(k[h]);
         spos[E * tid + h] = ps[h];
     }
+}
+__global__ __launch_bounds__(kSeriesBlock) void k_series_small(const double *__restrict__ x,
+                                                               const int64_t *__restrict__ d_n, double *rho,
+                                                               double *pv, double *w, double *wp) {
+    chain_prio();
+    constexpr int BS = kSeriesBlock, NW = BS / kWave;
+    __shared__ uint64_t sk[kSpearmanSmall];
+    __shared__ int32_t spos[kSpearmanSmall];
+    __shared__ double s_tmp[NW];
+    __shared__ double s_hi[NW][3], s_lo[NW][3];
+    __shared__ double s_m[kSpearmanSmall / 2];
+    const int tid = threadIdx.x;
+    SERIES_STAMP(0);
+    const int n = int(*d_n);
+    // the network sized to the series (the work is stages x pairs a thread on one CU: 78 x 8 for
+    // 4,096 pairs, 45 x 1 for 512)
+#if FZ_SERIES_NET_CLASSES
+    if (n <= BS) series_net<1>(x, n, sk, spos);
+    else if (n <= 2 * BS) series_net<2>(x, n, sk, spos);
+    else if (n <= 4 * BS) series_net<4>(x, n, sk, spos);
+    else
+#endif
+        series_net<8>(x, n, sk, spos);
+    double *sv = reinterpret_cast<double *>(sk);
     __syncthreads();
     SERIES_STAMP(1);
     const SpearmanT st = spearman_block<BS>(sv, spos, 0, n, s_tmp, rho, pv, kSeriesDefer);
