@@ -42,6 +42,9 @@ def main():
             eng.lib.fz_debug_series_timing(buf)
             t = [int(v) for v in buf]
             row["phase_us"] = [round((t[i] - t[i - 1]) / 100.0, 2) for i in range(1, 4)]
+            if all(t[4:8]):  # the Shapiro-Wilk pass: normal scores' sum, first sums, second sums, p-value
+                seq = [t[2], t[4], t[5], t[6], t[7]]
+                row["shapiro_us"] = [round((seq[i] - seq[i - 1]) / 100.0, 2) for i in range(1, 5)]
         print(json.dumps(row), flush=True)
     eng.close()
 

@@ -1366,6 +1366,37 @@ __device__ inline void block_dd_sums(const DD (&acc)[NV], double (&s_hi)[NW][NV]
     __syncthreads();
 }
 
+#ifdef FZ_SERIES_TIMING
+// experiment builds only: wall-clock (100 MHz) phase stamps of the last k_series_small launch
+__device__ unsigned long long g_series_t[8];
+#define SERIES_STAMP(ph)                                        \
+    do {                                                        \
+        __syncthreads();                                        \
+        if (threadIdx.x == 0) g_series_t[ph] = wall_clock64(); \
+    } while (0)
+extern "C" int fz_debug_series_timing(unsigned long long *out) {
+    hipDeviceSynchronize();
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_series_t), sizeof(g_series_t));
+    return 0;
+}
+#else
+#define SERIES_STAMP(ph) \
+    do {                 \
+    } while (0)
+#endif
+// (experiment builds: stamps 4-7 inside the one-workgroup Shapiro-Wilk pass of a single-workgroup
+// launch - after the normal scores' sum, the first and second sums, thread 0's p-value)
+#ifdef FZ_SERIES_TIMING
+#define SW_STAMP(ph)                                                                    \
+    do {                                                                                \
+        __syncthreads();                                                                \
+        if (gridDim.x == 1 && threadIdx.x == 0) g_series_t[4 + (ph)] = wall_clock64(); \
+    } while (0)
+#else
+#define SW_STAMP(ph) \
+    do {             \
+    } while (0)
+#endif
 // scipy.stats.shapiro (swilk.c) of one sorted segment v[b, b + n) (src: the same values in input
 // order, for y -= x[N // 2]) by the workgroup, each thread over its run [k0, k1) of <= kSmallPer
 // values: the passes of seg_shapiro (sum of m_i^2, then sx / sa, then ssa / ssx / sax), every sum
@@ -1386,6 +1417,7 @@ __device__ inline void shapiro_block(const double *__restrict__ v, const double 
         }
     double summ2[1];
     block_dd_sums<1, NW>(a0, reinterpret_cast<double(&)[NW][1]>(s_hi), reinterpret_cast<double(&)[NW][1]>(s_lo), summ2);
+    SW_STAMP(0);
     if (n < 3) {
         if (threadIdx.x == 0) {
             *w_out = NAN;
@@ -1418,6 +1450,7 @@ __device__ inline void shapiro_block(const double *__restrict__ v, const double 
     }
     double s1[2];
     block_dd_sums<2, NW>(a1, reinterpret_cast<double(&)[NW][2]>(s_hi), reinterpret_cast<double(&)[NW][2]>(s_lo), s1);
+    SW_STAMP(1);
     const double sx = s1[0] / double(n), sa = s1[1] / double(n);
     DD a2[3] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
 #pragma unroll 4
@@ -1434,6 +1467,7 @@ __device__ inline void shapiro_block(const double *__restrict__ v, const double 
     }
     double s2[3];
     block_dd_sums<3, NW>(a2, s_hi, s_lo, s2);
+    SW_STAMP(2);
     if (threadIdx.x == 0) {
         if (range < stats::kSwSmall) {  // zero range: scipy returns (1.0, 1.0)
             *w_out = 1.0;
@@ -1446,6 +1480,9 @@ __device__ inline void shapiro_block(const double *__restrict__ v, const double 
         const double ww = 1.0 - w1;
         *w_out = ww;
         *p_out = sw_pvalue_once(n, ww, w1);
+#ifdef FZ_SERIES_TIMING
+        if (gridDim.x == 1) g_series_t[7] = wall_clock64();
+#endif
     }
 }
 
@@ -1811,24 +1848,6 @@ void bm_union_sorted(fz_ctx *c, const Segs &one, const double *sorted, const int
 // wave, only the 6 of distance >= 512 through LDS with barriers - the whole network in LDS took
 // 78 barrier stages, ~30 us of RQ2 count's chain), then the Spearman and Shapiro-Wilk passes over
 // the sorted values in LDS.  (Equal keys keep either order: the tie groups are ranked as groups.)
-#ifdef FZ_SERIES_TIMING
-// experiment builds only: wall-clock (100 MHz) phase stamps of the last k_series_small launch
-__device__ unsigned long long g_series_t[8];
-#define SERIES_STAMP(ph)                                        \
-    do {                                                        \
-        __syncthreads();                                        \
-        if (threadIdx.x == 0) g_series_t[ph] = wall_clock64(); \
-    } while (0)
-extern "C" int fz_debug_series_timing(unsigned long long *out) {
-    hipDeviceSynchronize();
-    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_series_t), sizeof(g_series_t));
-    return 0;
-}
-#else
-#define SERIES_STAMP(ph) \
-    do {                 \
-    } while (0)
-#endif
 constexpr int kSeriesBlock = 512;  // (1,024 threads spilled 120 VGPRs: the statistics' code)
 static_assert(int(kSpearmanSmall) == kSeriesBlock * 8, "series network shape");
 #ifndef FZ_SERIES_NET_CLASSES
